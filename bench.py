@@ -1,0 +1,151 @@
+#!/usr/bin/env python3
+"""Headline benchmark: whole-node samples/s of ResNet-50 bf16 training under the MI355X-native
+parameter-server data plane, with gradient-staleness p50 and histogram (BASELINE.json).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]                   (N=1: plain process)
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Config (BASELINE.json configs 2/3): ResNet-50, bf16, NHWC, synthetic ImageNet-shaped data
+(224x224, 1000 classes), random init; every GPU is a worker; PS shards (default 2, BASELINE config
+3; capped at N) colocated on evenly spaced ranks hold the fp32 masters + momentum in HBM and apply
+the fused gfx950 SGD-momentum kernel; push = reduce-scatter / reduce, pull = all-gather /
+broadcast over RCCL, overlapped with backward; async SGD with staleness bound S (default 1: every
+update lands exactly one version late, the pull of step t+1 never waits for the push of step t).
+
+Timing: W untimed warmup steps (include MIOpen tuning and hipGraph capture), then exactly K timed
+steps bracketed by barrier + device synchronize on both sides; the max over ranks is reported.
+Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from parameter_server_distributed_amd import models  # noqa: E402
+from parameter_server_distributed_amd.ops.optim import OptimConfig  # noqa: E402
+from parameter_server_distributed_amd.parallel.collective_ps import CollectivePS  # noqa: E402
+from parameter_server_distributed_amd.parallel.transport import make_transport  # noqa: E402
+from parameter_server_distributed_amd.runtime.trainer import Trainer  # noqa: E402
+
+METRIC = "samples/sec (whole node) ResNet-50 async-SGD"
+
+
+def parse():
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--image-size", type=int, default=224)
+    ap.add_argument("--ps-shards", type=int, default=2)
+    ap.add_argument("--staleness", type=int, default=1)
+    ap.add_argument("--bucket-mb", type=float, default=16.0)
+    ap.add_argument("--lr", type=float, default=0.1)
+    ap.add_argument("--graph", type=int, default=-1, help="hipGraph capture (1/0; -1: on for 1 GPU)")
+    ap.add_argument("--transport", default="auto", choices=["auto", "torch", "rccl"])
+    ap.add_argument("--benchmark-miopen", type=int, default=1, help="torch.backends.cudnn.benchmark")
+    ap.add_argument("--out", default="", help="also write the JSON line to this file")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus and rank == 0:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a GPU (MI355X); CPU plumbing runs live in tests/ and scripts/test_local.sh")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    torch.backends.cudnn.benchmark = bool(a.benchmark_miopen)
+    torch.manual_seed(1234)  # identical init on every rank; the PS init pull makes it exact
+
+    spec = models.build(a.model, dev, torch.bfloat16, image_size=a.image_size)
+    transport = make_transport(a.transport, dev)
+    shards = max(1, min(a.ps_shards, world))
+    ps = CollectivePS(spec.model, OptimConfig("momentum", lr=a.lr, momentum=0.9, weight_decay=5e-5), transport,
+                      num_shards=shards, staleness=a.staleness, bucket_mb=a.bucket_mb, device=dev)
+    batch = spec.make_batch(a.batch, dev, seed=rank)
+    use_graph = (world == 1) if a.graph < 0 else bool(a.graph)
+    tr = Trainer(spec.model, spec.loss, ps, batch, use_graph=use_graph)
+
+    def barrier():
+        if world > 1:
+            dist.barrier(device_ids=[local])
+        torch.cuda.synchronize(dev)
+
+    t_w0 = time.perf_counter()
+    for _ in range(a.warmup):
+        tr.step()
+    barrier()
+    t_w = time.perf_counter() - t_w0
+    mem_peak = torch.cuda.max_memory_allocated(dev)
+
+    barrier()
+    t0 = time.perf_counter()
+    loss = None
+    for _ in range(a.steps):
+        loss = tr.step()
+    torch.cuda.synchronize(dev)
+    barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    ms = el / max(a.steps, 1) * 1e3
+    samples = a.batch * world * a.steps
+    value = samples / el
+    hist = ps.staleness_histogram()
+    if world > 1:
+        h = torch.tensor(hist, device=dev, dtype=torch.int64)
+        dist.all_reduce(h)
+        hist = h.tolist()
+    tot = sum(hist)
+    p50, acc = -1, 0
+    for i, c in enumerate(hist):
+        acc += c
+        if tot and acc * 2 >= tot:
+            p50 = i
+            break
+    while hist and hist[-1] == 0 and len(hist) > 1:
+        hist.pop()
+    final_loss = float(loss.float().item()) if loss is not None else float("nan")
+    if rank == 0:
+        rec = {
+            "metric": METRIC, "value": round(value, 2), "unit": "samples/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random ImageNet-shaped 224x224, random init)",
+            "config": {"model": a.model, "global_batch": a.batch * world, "per_gpu_batch": a.batch, "seq_len": None,
+                       "image_size": a.image_size,
+                       "parallelism": f"ps{shards}-async-s{a.staleness}-dp{world}",
+                       "ps_shards": shards, "ps_owner_ranks": ps.owners, "staleness_bound": a.staleness,
+                       "optimizer": "sgd-momentum(0.9) fused gfx950", "bucket_mb": a.bucket_mb,
+                       "transport": transport.name, "hipgraph": bool(tr.graphs), "graph_error": tr.graph_error},
+            "staleness_p50": p50, "staleness_hist": hist, "final_loss": round(final_loss, 4),
+            "warmup_s": round(t_w, 2), "peak_mem_gb": round(mem_peak / 2**30, 2),
+        }
+        line = json.dumps(rec)
+        print(line, flush=True)
+        if a.out:
+            with open(a.out, "w") as f:
+                f.write(line + "\n")
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

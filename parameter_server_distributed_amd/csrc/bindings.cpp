@@ -1,0 +1,177 @@
+// pybind11 module `parameter_server_distributed_amd._C`.
+#include <torch/extension.h>
+
+#include "checkpoint.h"
+#include "comm.h"
+#include "kernels/launchers.h"
+#include "ops.h"
+#include "ps_core.h"
+#include "registry.h"
+#include "staleness.h"
+
+namespace py = pybind11;
+using namespace psd;
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "MI355X-native parameter-server runtime: gfx950 HIP kernels, RCCL comm, PS/coordinator cores";
+
+  // ---- kernels ----
+  m.def("fused_apply_", &fused_apply_, py::arg("master"), py::arg("grads"), py::arg("state1"), py::arg("state2"),
+        py::arg("shadow"), py::arg("dyn"), py::arg("kind"), py::arg("momentum") = 0.0, py::arg("dampening") = 0.0,
+        py::arg("nesterov") = false, py::arg("weight_decay") = 0.0, py::arg("beta1") = 0.9, py::arg("beta2") = 0.999,
+        py::arg("eps") = 1e-8, py::arg("maximize") = false);
+  m.def("optim_advance_", &optim_advance_, py::arg("dyn"), py::arg("beta1") = 0.9, py::arg("beta2") = 0.999);
+  m.def("multi_reduce_", &multi_reduce_, py::arg("out"), py::arg("srcs"), py::arg("scale") = 1.0);
+  m.def("pack_cast_", &pack_cast_, py::arg("srcs"), py::arg("dsts"));
+  m.def("amax_", &amax_);
+  m.def("quant_fp8_", &quant_fp8_);
+  m.def("dequant_fp8_", &dequant_fp8_);
+  m.attr("OPT_SGD") = (int)OPT_SGD;
+  m.attr("OPT_MOMENTUM") = (int)OPT_MOMENTUM;
+  m.attr("OPT_ADAM") = (int)OPT_ADAM;
+  m.attr("OPT_ADAMW") = (int)OPT_ADAMW;
+
+  // ---- checkpoint ----
+  m.def("save_reference_ckpt", &save_reference_ckpt, py::call_guard<py::gil_scoped_release>());
+  m.def("load_reference_ckpt", &load_reference_ckpt, py::call_guard<py::gil_scoped_release>());
+  m.def("save_native_ckpt", &save_native_ckpt, py::call_guard<py::gil_scoped_release>());
+  m.def("load_native_ckpt", &load_native_ckpt, py::call_guard<py::gil_scoped_release>());
+  m.def("crc32", [](py::bytes b) {
+    std::string s = b;
+    return crc32(s.data(), s.size());
+  });
+
+  // ---- coordinator core ----
+  py::class_<WorkerEntry>(m, "WorkerEntry")
+      .def_readonly("worker_id", &WorkerEntry::worker_id)
+      .def_readonly("address", &WorkerEntry::address)
+      .def_readonly("port", &WorkerEntry::port)
+      .def_readonly("hostname", &WorkerEntry::hostname)
+      .def_readonly("status", &WorkerEntry::status)
+      .def_readonly("last_heartbeat", &WorkerEntry::last_heartbeat)
+      .def_readonly("join_epoch", &WorkerEntry::join_epoch);
+  py::class_<RegisterResult>(m, "RegisterResult")
+      .def_readonly("success", &RegisterResult::success)
+      .def_readonly("message", &RegisterResult::message)
+      .def_readonly("ps_address", &RegisterResult::ps_address)
+      .def_readonly("total_workers", &RegisterResult::total_workers)
+      .def_readonly("membership_epoch", &RegisterResult::membership_epoch);
+  py::class_<ShardInfo>(m, "ShardInfo")
+      .def_readonly("shard_id", &ShardInfo::shard_id)
+      .def_readonly("address", &ShardInfo::address)
+      .def_readonly("rank", &ShardInfo::rank);
+  py::class_<Registry>(m, "Registry")
+      .def(py::init<std::string, int32_t>())
+      .def("register_worker", &Registry::register_worker)
+      .def("heartbeat", &Registry::heartbeat)
+      .def("deregister", &Registry::deregister)
+      .def("list_workers", &Registry::list_workers)
+      .def("live_ids", &Registry::live_ids)
+      .def("ps_address", &Registry::ps_address)
+      .def("set_ps_address", &Registry::set_ps_address)
+      .def("remove_stale", &Registry::remove_stale)
+      .def("membership_epoch", &Registry::membership_epoch)
+      .def("wait_epoch_change", &Registry::wait_epoch_change, py::call_guard<py::gil_scoped_release>())
+      .def("set_shard", &Registry::set_shard)
+      .def("shards", &Registry::shards)
+      .def("kv_set", [](Registry& r, const std::string& k, py::bytes v) { r.kv_set(k, std::string(v)); })
+      .def("kv_get",
+           [](Registry& r, const std::string& k, double timeout) {
+             std::tuple<bool, std::string> res;
+             {
+               py::gil_scoped_release nogil;
+               res = r.kv_get(k, timeout);
+             }
+             return py::make_tuple(std::get<0>(res), py::bytes(std::get<1>(res)));
+           })
+      .def("use_manual_clock", &Registry::use_manual_clock)
+      .def("advance_clock", &Registry::advance_clock)
+      .def("now", &Registry::now);
+
+  // ---- parameter-server core ----
+  py::class_<PSConfig>(m, "PSConfig")
+      .def(py::init<>())
+      .def_readwrite("total_workers", &PSConfig::total_workers)
+      .def_readwrite("async_mode", &PSConfig::async_mode)
+      .def_readwrite("staleness_bound", &PSConfig::staleness_bound)
+      .def_readwrite("window", &PSConfig::window)
+      .def_readwrite("opt_kind", &PSConfig::opt_kind)
+      .def_readwrite("lr", &PSConfig::lr)
+      .def_readwrite("momentum", &PSConfig::momentum)
+      .def_readwrite("dampening", &PSConfig::dampening)
+      .def_readwrite("weight_decay", &PSConfig::weight_decay)
+      .def_readwrite("beta1", &PSConfig::beta1)
+      .def_readwrite("beta2", &PSConfig::beta2)
+      .def_readwrite("eps", &PSConfig::eps)
+      .def_readwrite("nesterov", &PSConfig::nesterov)
+      .def_readwrite("reference_compat", &PSConfig::reference_compat)
+      .def_readwrite("staleness_lr_scaling", &PSConfig::staleness_lr_scaling)
+      .def_readwrite("async_grad_scale", &PSConfig::async_grad_scale)
+      .def_readwrite("pull_timeout_s", &PSConfig::pull_timeout_s);
+  py::class_<PushResult>(m, "PushResult")
+      .def_readonly("success", &PushResult::success)
+      .def_readonly("message", &PushResult::message)
+      .def_readonly("iteration", &PushResult::iteration)
+      .def_readonly("aggregation_complete", &PushResult::aggregation_complete)
+      .def_readonly("workers_received", &PushResult::workers_received)
+      .def_readonly("total_workers", &PushResult::total_workers)
+      .def_readonly("version", &PushResult::version)
+      .def_readonly("staleness", &PushResult::staleness);
+  py::class_<PSCore>(m, "PSCore")
+      .def(py::init<PSConfig, std::string>())
+      .def("initialized", &PSCore::initialized)
+      .def("init_params", &PSCore::init_params, py::call_guard<py::gil_scoped_release>())
+      .def("names", &PSCore::names)
+      .def("shapes", &PSCore::shapes)
+      .def("offsets", &PSCore::offsets)
+      .def("numel", &PSCore::numel)
+      .def("push", &PSCore::push, py::call_guard<py::gil_scoped_release>())
+      .def("pull", &PSCore::pull, py::call_guard<py::gil_scoped_release>())
+      .def("sync_status", &PSCore::sync_status)
+      .def("set_total_workers", &PSCore::set_total_workers)
+      .def("total_workers", &PSCore::total_workers)
+      .def("current_iteration", &PSCore::current_iteration)
+      .def("version", &PSCore::version)
+      .def("staleness_histogram", &PSCore::staleness_histogram)
+      .def("counters", &PSCore::counters)
+      .def("save_reference", &PSCore::save_reference, py::call_guard<py::gil_scoped_release>())
+      .def("load_reference", &PSCore::load_reference, py::call_guard<py::gil_scoped_release>())
+      .def("state_tensors", &PSCore::state_tensors)
+      .def("load_state_tensors", &PSCore::load_state_tensors);
+
+  // ---- staleness / version bookkeeping for the collective data plane ----
+  py::class_<StalenessTracker>(m, "StalenessTracker")
+      .def(py::init<int, int>(), py::arg("num_shards"), py::arg("bins") = 64)
+      .def("on_pull", &StalenessTracker::on_pull)
+      .def("on_apply", &StalenessTracker::on_apply)
+      .def("version", &StalenessTracker::version)
+      .def("histogram", &StalenessTracker::histogram)
+      .def("percentile", &StalenessTracker::percentile)
+      .def("reset", &StalenessTracker::reset);
+
+  // ---- RCCL ----
+  py::class_<RcclComm>(m, "RcclComm")
+      .def_static("unique_id", []() { return py::bytes(RcclComm::unique_id()); })
+      .def_static("version", &RcclComm::version)
+      .def(py::init([](int rank, int world, py::bytes uid, int device) {
+             std::string u = uid;
+             py::gil_scoped_release nogil;
+             return new RcclComm(rank, world, u, device);
+           }),
+           py::arg("rank"), py::arg("world"), py::arg("uid"), py::arg("device"))
+      .def_property_readonly("rank", &RcclComm::rank)
+      .def_property_readonly("world", &RcclComm::world)
+      .def("all_reduce", &RcclComm::all_reduce, py::arg("t"), py::arg("op") = "sum", py::arg("stream") = 0)
+      .def("reduce_scatter", &RcclComm::reduce_scatter, py::arg("inp"), py::arg("out"), py::arg("op") = "sum",
+           py::arg("stream") = 0)
+      .def("all_gather", &RcclComm::all_gather, py::arg("inp"), py::arg("out"), py::arg("stream") = 0)
+      .def("reduce", &RcclComm::reduce, py::arg("inp"), py::arg("out"), py::arg("root"), py::arg("op") = "sum",
+           py::arg("stream") = 0)
+      .def("broadcast", &RcclComm::broadcast, py::arg("t"), py::arg("root"), py::arg("stream") = 0)
+      .def("send", &RcclComm::send, py::arg("t"), py::arg("peer"), py::arg("stream") = 0)
+      .def("recv", &RcclComm::recv, py::arg("t"), py::arg("peer"), py::arg("stream") = 0)
+      .def_static("group_start", &RcclComm::group_start)
+      .def_static("group_end", &RcclComm::group_end)
+      .def("abort", &RcclComm::abort)
+      .def("async_error", &RcclComm::async_error);
+}

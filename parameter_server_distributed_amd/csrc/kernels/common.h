@@ -1,0 +1,60 @@
+// Device helpers shared by the gfx950 kernels (wave64, 16-byte vector memory ops).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace psd {
+
+constexpr int kWave = 64;  // CDNA wavefront: never 32
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+
+// Round-to-nearest-even fp32 -> bf16, NaN preserved (quiet bit forced).
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+// 8 consecutive elements <-> registers, one 16-byte (bf16) or two 16-byte (fp32) loads per lane.
+__device__ __forceinline__ void load8_f32(const float* p, float v[8]) {
+  f32x4 a = *reinterpret_cast<const f32x4*>(p);
+  f32x4 b = *reinterpret_cast<const f32x4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void store8_f32(float* p, const float v[8]) {
+  *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
+  *reinterpret_cast<f32x4*>(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
+}
+__device__ __forceinline__ void load8_bf16(const uint16_t* p, float v[8]) {
+  u32x4 w = *reinterpret_cast<const u32x4*>(p);
+  uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(ws[i] << 16);
+    v[2 * i + 1] = __uint_as_float(ws[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ void store8_bf16(uint16_t* p, const float v[8]) {
+  uint32_t ws[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    ws[i] = (uint32_t)f32_to_bf16(v[2 * i]) | ((uint32_t)f32_to_bf16(v[2 * i + 1]) << 16);
+  *reinterpret_cast<u32x4*>(p) = u32x4{ws[0], ws[1], ws[2], ws[3]};
+}
+
+// Grid size for a grid-stride streaming kernel: enough blocks to fill 256 CUs several times
+// over, capped so that launch + tail cost stays small (guide G11: <= ~2048 blocks).
+inline int stream_grid(int64_t work_items, int block) {
+  int64_t g = (work_items + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > 2048) g = 2048;
+  return (int)g;
+}
+
+}  // namespace psd

@@ -1,0 +1,114 @@
+// FP8 (OCP e4m3fn -- gfx950 is OCP, NOT the MI300 fnuz encoding) quantisation helpers for the
+// fp8-weights path (Wide-ResNet-101 / fp8 GEMMs): per-tensor amax on device, scale = 448/amax,
+// saturating cast, and dequantisation. All stream-shaped: 8 elements per lane, grid-stride.
+#include <hip/hip_fp8.h>
+#include "common.h"
+#include "launchers.h"
+
+namespace psd {
+
+__device__ __forceinline__ float e4m3_to_f32(uint8_t b) {
+  const uint32_t s = b >> 7, e = (b >> 3) & 0xF, m = b & 7;
+  float v;
+  if (e == 0xF && m == 7) return __uint_as_float(0x7fc00000u);  // NaN (e4m3fn has no inf)
+  if (e == 0) v = (float)m * 0.001953125f;                      // m/8 * 2^-6
+  else v = __uint_as_float(((e + 120u) << 23) | (m << 20));     // (1+m/8) * 2^(e-7)
+  return s ? -v : v;
+}
+
+__device__ __forceinline__ uint8_t f32_to_e4m3(float x) {
+  return (uint8_t)__hip_cvt_float_to_fp8(x, __HIP_SATFINITE, __HIP_E4M3);
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void amax_kernel(const void* __restrict__ x, int64_t n, float* amax) {
+  float m = 0.f;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float v = (DT == DT_BF16) ? bf16_to_f32(static_cast<const uint16_t*>(x)[i]) : static_cast<const float*>(x)[i];
+    m = fmaxf(m, fabsf(v));
+  }
+  // wave64 butterfly, then one LDS slot per wave
+  for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, kWave));
+  __shared__ float red[4];
+  const int wid = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  if (lane == 0) red[wid] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float r = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    // non-negative floats order like their bit patterns: integer atomicMax is exact
+    atomicMax(reinterpret_cast<unsigned int*>(amax), __float_as_uint(r));
+  }
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void quant_kernel(const void* __restrict__ x, int64_t n, const float* amax,
+                                                    float fp8_max, uint8_t* __restrict__ out, float* scale_inv) {
+  const float a = fmaxf(*amax, 1e-12f);
+  const float scale = fp8_max / a;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && scale_inv) *scale_inv = a / fp8_max;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t nvec = n >> 3;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    const int64_t i = v << 3;
+    float t[8];
+    if (DT == DT_BF16) load8_bf16(static_cast<const uint16_t*>(x) + i, t);
+    else load8_f32(static_cast<const float*>(x) + i, t);
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) lo |= (uint32_t)f32_to_e4m3(t[e] * scale) << (8 * e);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) hi |= (uint32_t)f32_to_e4m3(t[4 + e] * scale) << (8 * e);
+    *reinterpret_cast<uint2*>(out + i) = make_uint2(lo, hi);
+  }
+  if (blockIdx.x == 0)
+    for (int64_t i = (nvec << 3) + threadIdx.x; i < n; i += blockDim.x) {
+      float v = (DT == DT_BF16) ? bf16_to_f32(static_cast<const uint16_t*>(x)[i]) : static_cast<const float*>(x)[i];
+      out[i] = f32_to_e4m3(v * scale);
+    }
+}
+
+template <int OD>
+__global__ __launch_bounds__(256) void dequant_kernel(const uint8_t* __restrict__ x, int64_t n,
+                                                      const float* scale_inv, void* __restrict__ out) {
+  const float s = *scale_inv;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float v = e4m3_to_f32(x[i]) * s;
+    if (OD == DT_BF16) static_cast<uint16_t*>(out)[i] = f32_to_bf16(v);
+    else static_cast<float*>(out)[i] = v;
+  }
+}
+
+hipError_t launch_amax(const void* x, int32_t dt, int64_t n, float* amax, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int grid = stream_grid(n, 256);
+  if (dt == DT_BF16) hipLaunchKernelGGL(amax_kernel<DT_BF16>, dim3(grid), dim3(256), 0, st, x, n, amax);
+  else if (dt == DT_F32) hipLaunchKernelGGL(amax_kernel<DT_F32>, dim3(grid), dim3(256), 0, st, x, n, amax);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_quant_fp8(const void* x, int32_t dt, int64_t n, const float* amax, float fp8_max, uint8_t* out,
+                            float* scale_inv, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int grid = stream_grid((n >> 3) > 0 ? (n >> 3) : 1, 256);
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(quant_kernel<DT_BF16>, dim3(grid), dim3(256), 0, st, x, n, amax, fp8_max, out, scale_inv);
+  else if (dt == DT_F32)
+    hipLaunchKernelGGL(quant_kernel<DT_F32>, dim3(grid), dim3(256), 0, st, x, n, amax, fp8_max, out, scale_inv);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_dequant_fp8(const uint8_t* x, int64_t n, const float* scale_inv, void* out, int32_t od,
+                              hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int grid = stream_grid(n, 256);
+  if (od == DT_BF16) hipLaunchKernelGGL(dequant_kernel<DT_BF16>, dim3(grid), dim3(256), 0, st, x, n, scale_inv, out);
+  else if (od == DT_F32) hipLaunchKernelGGL(dequant_kernel<DT_F32>, dim3(grid), dim3(256), 0, st, x, n, scale_inv, out);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+}  // namespace psd

@@ -1,0 +1,94 @@
+"""ResNet-50 / ResNet-101 / Wide-ResNet-101-2 (v1.5 bottleneck: stride on the 3x3 conv).
+
+The worker model for the BASELINE.json ResNet configs (the reference itself has no model: its
+"gradient" is the constant 0.01 on a dummy [10,10] tensor, src/worker.cpp:316-329,346-353).
+
+MI355X layout choices: NHWC (``channels_last``) activations and weights so MIOpen picks its
+NHWC implicit-GEMM convolutions on the MFMA units, bf16 compute, and the 1000-way classifier on
+the hand-written MFMA GEMM (``ops.gemm``) when available. Random init, synthetic data.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+def _conv(cin, cout, k, stride=1, groups=1):
+    return nn.Conv2d(cin, cout, k, stride=stride, padding=k // 2, groups=groups, bias=False)
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, cin, planes, stride=1, width_per_group=64, downsample=None):
+        super().__init__()
+        width = int(planes * (width_per_group / 64.0))
+        self.conv1 = _conv(cin, width, 1)
+        self.bn1 = nn.BatchNorm2d(width)
+        self.conv2 = _conv(width, width, 3, stride)
+        self.bn2 = nn.BatchNorm2d(width)
+        self.conv3 = _conv(width, planes * self.expansion, 1)
+        self.bn3 = nn.BatchNorm2d(planes * self.expansion)
+        self.downsample = downsample
+
+    def forward(self, x):
+        idt = x if self.downsample is None else self.downsample(x)
+        out = F.relu(self.bn1(self.conv1(x)), inplace=True)
+        out = F.relu(self.bn2(self.conv2(out)), inplace=True)
+        out = self.bn3(self.conv3(out))
+        return F.relu(out + idt, inplace=True)
+
+
+class ResNet(nn.Module):
+    def __init__(self, layers=(3, 4, 6, 3), num_classes=1000, width_per_group=64, zero_init_residual=True):
+        super().__init__()
+        self.width_per_group = width_per_group
+        self.cin = 64
+        self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.layer1 = self._make(64, layers[0])
+        self.layer2 = self._make(128, layers[1], stride=2)
+        self.layer3 = self._make(256, layers[2], stride=2)
+        self.layer4 = self._make(512, layers[3], stride=2)
+        self.fc = nn.Linear(512 * Bottleneck.expansion, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+        if zero_init_residual:
+            for m in self.modules():
+                if isinstance(m, Bottleneck):
+                    nn.init.zeros_(m.bn3.weight)
+
+    def _make(self, planes, blocks, stride=1):
+        down = None
+        if stride != 1 or self.cin != planes * Bottleneck.expansion:
+            down = nn.Sequential(_conv(self.cin, planes * Bottleneck.expansion, 1, stride),
+                                 nn.BatchNorm2d(planes * Bottleneck.expansion))
+        mods = [Bottleneck(self.cin, planes, stride, self.width_per_group, down)]
+        self.cin = planes * Bottleneck.expansion
+        for _ in range(1, blocks):
+            mods.append(Bottleneck(self.cin, planes, 1, self.width_per_group))
+        return nn.Sequential(*mods)
+
+    def forward(self, x):
+        x = F.relu(self.bn1(self.conv1(x)), inplace=True)
+        x = F.max_pool2d(x, 3, 2, 1)
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
+        return self.fc(x)
+
+
+def resnet50(num_classes=1000):
+    return ResNet((3, 4, 6, 3), num_classes)
+
+
+def resnet101(num_classes=1000):
+    return ResNet((3, 4, 23, 3), num_classes)
+
+
+def wide_resnet101_2(num_classes=1000):
+    return ResNet((3, 4, 23, 3), num_classes, width_per_group=128)

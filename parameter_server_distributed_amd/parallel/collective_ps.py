@@ -1,0 +1,346 @@
+"""Sharded parameter server over RCCL collectives, colocated with the workers (one rank per GPU).
+
+Every rank is a worker; P of the ranks also hold PS shards (P = world by default: every GPU is a
+PS shard). The model's parameters live in ONE flat bf16 working buffer (the model's ``.data`` are
+views into it) and their gradients in one flat bf16 buffer (``.grad`` views), both laid out in
+gradient-ready (reverse registration) order and cut into buckets of ``bucket_mb``. Each bucket is
+split into P equal slices; slice k is owned by PS shard k, which keeps the fp32 master copy and the
+optimizer state for it in HBM.
+
+Per bucket, as soon as backward has accumulated all of its gradients (post-accumulate-grad hook,
+on a dedicated comm stream, overlapped with the rest of backward):
+
+  push   RS(grad bucket) -> owner slices      (reduce per slice when P < world)
+  apply  fused gfx950 kernel: grad/W -> SGD|momentum|Adam(W) on the fp32 master slice -> bf16
+         slice written straight into the working buffer
+  pull   AG(working bucket) in place          (broadcast per slice when P < world)
+
+Staleness: with ``staleness=S`` the apply at step t uses the gradient pushed at step t-S (kept in
+S+1 rotating slots), i.e. every update is applied exactly S versions after the weights it was
+computed on (bounded-staleness / SSP semantics; S=0 is the reference's synchronous barrier,
+src/parameter_server.cpp:37). Versions and the staleness histogram are kept by the native
+``StalenessTracker``.
+
+A bucket's weights are never read again in the same backward once all of its gradients have been
+accumulated (each weight's dgrad and wgrad come from the same autograd node), so updating and
+re-gathering it during backward is race-free. Tied weights (a parameter used by two nodes) would
+break that invariant; such models must pass ``overlap=False``.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import torch
+import torch.nn as nn
+
+from .. import native
+from ..ops.optim import OptimConfig, OptimDyn, advance_, apply_no_advance_
+from .transport import LocalTransport, Transport
+
+ALIGN = 64  # elements: every tensor starts 128-B aligned in the bf16 buffers
+
+
+def _round(x: int, a: int) -> int:
+    return (x + a - 1) // a * a
+
+
+@dataclass
+class Bucket:
+    index: int
+    params: list = field(default_factory=list)  # (name, param, offset_in_flat, numel)
+    offset: int = 0  # element offset in the flat buffers
+    numel: int = 0  # padded: multiple of P * ALIGN
+    slice_numel: int = 0
+    local_offset: int = 0  # offset of this rank's owned slice inside the local shard buffers
+    pending: int = 0
+    launched: bool = False
+
+
+def _flat_view(flat: torch.Tensor, off: int, p: torch.Tensor) -> torch.Tensor:
+    """View of ``flat[off:off+numel]`` with the same shape *and strides* as ``p`` (channels_last
+    conv weights stay channels_last)."""
+    n = p.numel()
+    seg = flat.narrow(0, off, n)
+    if p.dim() == 4 and p.is_contiguous(memory_format=torch.channels_last) and not p.is_contiguous():
+        o, i, kh, kw = p.shape
+        return seg.view(o, kh, kw, i).permute(0, 3, 1, 2)
+    return seg.view(p.shape)
+
+
+class CollectivePS:
+    def __init__(self, model: nn.Module, optim: OptimConfig, transport: Transport | None = None,
+                 num_shards: int | None = None, staleness: int = 0, bucket_mb: float = 16.0,
+                 overlap: bool = True, grad_dtype: torch.dtype = torch.bfloat16,
+                 param_dtype: torch.dtype = torch.bfloat16, device: torch.device | None = None):
+        self.model = model
+        self.cfg = optim
+        self.t = transport or LocalTransport()
+        self.world, self.rank = self.t.world, self.t.rank
+        self.P = num_shards or self.world
+        if not 1 <= self.P <= self.world:
+            raise ValueError(f"num_shards must be in [1, world={self.world}], got {self.P}")
+        # PS shard k lives on rank owners[k]: spread evenly over the node (2 of 8 -> ranks 0 and 4)
+        self.owners = [k * self.world // self.P for k in range(self.P)]
+        self.my_shards = [k for k, r in enumerate(self.owners) if r == self.rank]
+        self.collective_rs = self.P == self.world  # owners == range(world)
+        self.S = int(staleness)
+        self.overlap = overlap
+        self.device = device or next(model.parameters()).device
+        self.is_cuda = self.device.type == "cuda"
+        if grad_dtype != param_dtype:
+            raise ValueError("grad_dtype must equal param_dtype (.grad views must match the parameter dtype)")
+        self.grad_dtype, self.param_dtype = grad_dtype, param_dtype
+        C = native()
+        self.tracker = C.StalenessTracker(self.P, 64)
+        self.step_idx = 0
+
+        params = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
+        params.reverse()  # gradient-ready order ~ reverse of registration
+        elem = torch.finfo(param_dtype).bits // 8
+        cap = max(ALIGN, int(bucket_mb * (1 << 20)) // elem)
+        gran = self.P * ALIGN
+        buckets: list[Bucket] = []
+        cur = Bucket(0)
+        off = 0
+        for name, p in params:
+            n = p.numel()
+            cur.params.append((name, p, off, n))
+            off += _round(n, ALIGN)
+            if off - cur.offset >= cap:
+                cur.numel = _round(off - cur.offset, gran)
+                off = cur.offset + cur.numel
+                buckets.append(cur)
+                cur = Bucket(len(buckets), offset=off)
+        if cur.params:
+            cur.numel = _round(off - cur.offset, gran)
+            off = cur.offset + cur.numel
+            buckets.append(cur)
+        self.buckets = buckets
+        self.total = off
+        lo = 0
+        for b in buckets:
+            b.slice_numel = b.numel // self.P
+            b.local_offset = lo
+            lo += b.slice_numel * len(self.my_shards)
+        self.local_total = lo
+
+        dev = self.device
+        # fp32 staging of the initial values (rank-consistent init is the caller's job: same seed)
+        init = torch.zeros(self.total, dtype=torch.float32, device=dev)
+        for b in buckets:
+            for _, p, o, _n in b.params:
+                _flat_view(init, o, p).copy_(p.detach().float())
+        self.params_flat = init.to(param_dtype)
+        self.grads_flat = torch.zeros(self.total, dtype=grad_dtype, device=dev)
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.master = torch.zeros(max(self.local_total, ALIGN), **f32)
+        self.state1 = torch.zeros_like(self.master) if optim.num_states >= 1 else None
+        self.state2 = torch.zeros_like(self.master) if optim.num_states >= 2 else None
+        for b in buckets:
+            for j, k in enumerate(self.my_shards):
+                src = init.narrow(0, b.offset + k * b.slice_numel, b.slice_numel)
+                self.master.narrow(0, b.local_offset + j * b.slice_numel, b.slice_numel).copy_(src)
+        del init
+        # gradient slots for bounded staleness (slot s holds the reduced owned slices of one step)
+        # (S = 0 reduces in place inside the gradient buffer and needs none)
+        self.slots = [torch.zeros(max(self.local_total, ALIGN), dtype=grad_dtype, device=dev)
+                      for _ in range(self.S + 1)] if self.S > 0 else []
+        self.dyn = OptimDyn(dev, lr=optim.lr, grad_scale=1.0 / self.world)
+
+        # re-point the model at the flat buffers
+        for b in buckets:
+            for _, p, o, _n in b.params:
+                p.data = _flat_view(self.params_flat, o, p)
+                p.grad = _flat_view(self.grads_flat, o, p)
+        self._hooks = []
+        self._p2b = {}
+        for b in buckets:
+            for _, p, _o, _n in b.params:
+                self._p2b[id(p)] = b
+        if overlap:
+            for b in buckets:
+                for _, p, _o, _n in b.params:
+                    self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+        if self.is_cuda:
+            self.comm_stream = torch.cuda.Stream(device=dev)
+            self.ready_events = [torch.cuda.Event() for _ in buckets]
+        self._advanced = False
+        self._next = 0
+        self._sync_init()
+
+    # ------------------------------------------------------------------ setup
+    def _sync_init(self):
+        """Make every rank start from the owners' master values (pull v0)."""
+        if self.world == 1:
+            return
+        for b in self.buckets:
+            self._pull(b)
+        if self.is_cuda:
+            torch.cuda.synchronize(self.device)
+
+    def memory_bytes(self) -> dict:
+        eb = lambda t: 0 if t is None else t.numel() * t.element_size()  # noqa: E731
+        return {"params_bf16": eb(self.params_flat), "grads": eb(self.grads_flat), "master": eb(self.master),
+                "state": eb(self.state1) + eb(self.state2), "slots": sum(eb(s) for s in self.slots)}
+
+    # ------------------------------------------------------------------ per-step protocol
+    def begin_step(self, track: bool = True):
+        """Call before forward: zero the gradient buffer and reset bucket bookkeeping."""
+        if track:
+            self.account_begin()
+        self.grads_flat.zero_()
+        for b in self.buckets:
+            b.pending = len(b.params)
+            b.launched = False
+        self._next = 0
+        self._advanced = False
+
+    def account_begin(self):
+        """Host bookkeeping of a step's pull (runs per step, also under graph replay)."""
+        t = self.step_idx
+        for k in self.my_shards:  # in-flight gradient t is tracked as virtual worker t % (S+1)
+            self.tracker.on_pull(t % (self.S + 1), k)
+
+    def account_finish(self):
+        t = self.step_idx
+        if t >= self.S:
+            for k in self.my_shards:
+                self.tracker.on_apply((t - self.S) % (self.S + 1), k)
+        self.step_idx += 1
+
+    def _on_grad(self, p):
+        b = self._p2b[id(p)]
+        b.pending -= 1
+        # Launch strictly in bucket order so every rank enqueues the same collective sequence
+        # (an out-of-order ready bucket waits for its predecessors).
+        while self._next < len(self.buckets) and self.buckets[self._next].pending <= 0:
+            self._launch(self.buckets[self._next])
+            self._next += 1
+
+    def finish_step(self, track: bool = True):
+        """Call after backward: flush buckets whose hooks did not fire and join the comm stream."""
+        while self._next < len(self.buckets):
+            self._launch(self.buckets[self._next])
+            self._next += 1
+        if self.is_cuda:
+            torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
+        if track:
+            self.account_finish()
+
+    def _launch(self, b: Bucket):
+        b.launched = True
+        if self.is_cuda:
+            ev = self.ready_events[b.index]
+            ev.record(torch.cuda.current_stream(self.device))
+            self.comm_stream.wait_event(ev)
+            with torch.cuda.stream(self.comm_stream):
+                self._push_apply_pull(b)
+        else:
+            self._push_apply_pull(b)
+
+    # ------------------------------------------------------------------ push / apply / pull
+    def _owned_grad_views(self, b: Bucket, slot: int | None):
+        """Where the reduced gradient of my owned slices of bucket b lives."""
+        out = []
+        for j, k in enumerate(self.my_shards):
+            if slot is None:  # in-place in the gradient buffer
+                out.append(self.grads_flat.narrow(0, b.offset + k * b.slice_numel, b.slice_numel))
+            else:
+                out.append(self.slots[slot].narrow(0, b.local_offset + j * b.slice_numel, b.slice_numel))
+        return out
+
+    def _push(self, b: Bucket, slot: int | None):
+        g = self.grads_flat.narrow(0, b.offset, b.numel)
+        if self.world == 1:
+            if slot is not None:
+                self._owned_grad_views(b, slot)[0].copy_(g)
+            return
+        if self.collective_rs:
+            dst = self._owned_grad_views(b, slot)[0] if slot is not None else \
+                g.narrow(0, self.rank * b.slice_numel, b.slice_numel)
+            self.t.reduce_scatter(g, dst)
+        else:
+            for k, owner in enumerate(self.owners):
+                sl = g.narrow(0, k * b.slice_numel, b.slice_numel)
+                self.t.reduce(sl, owner)
+            if slot is not None:
+                for dst, src in zip(self._owned_grad_views(b, slot), self._owned_grad_views(b, None)):
+                    dst.copy_(src)
+
+    def _apply(self, b: Bucket, slot: int | None):
+        if not self._advanced:
+            advance_(self.cfg, self.dyn)
+            self._advanced = True
+        for j, (k, gv) in enumerate(zip(self.my_shards, self._owned_grad_views(b, slot))):
+            lo = b.local_offset + j * b.slice_numel
+            m = self.master.narrow(0, lo, b.slice_numel)
+            s1 = None if self.state1 is None else self.state1.narrow(0, lo, b.slice_numel)
+            s2 = None if self.state2 is None else self.state2.narrow(0, lo, b.slice_numel)
+            shadow = self.params_flat.narrow(0, b.offset + k * b.slice_numel, b.slice_numel)
+            apply_no_advance_(self.cfg, self.dyn, m, gv, s1, s2, shadow)
+
+    def _pull(self, b: Bucket):
+        w = self.params_flat.narrow(0, b.offset, b.numel)
+        if self.world == 1:
+            return
+        if self.collective_rs:
+            self.t.all_gather(w.narrow(0, self.rank * b.slice_numel, b.slice_numel), w)
+        else:
+            for k, owner in enumerate(self.owners):
+                self.t.broadcast(w.narrow(0, k * b.slice_numel, b.slice_numel), owner)
+
+    def _push_apply_pull(self, b: Bucket):
+        t = self.step_idx
+        if self.S == 0:
+            self._push(b, None)
+            self._apply(b, None)
+        else:
+            self._push(b, t % (self.S + 1))
+            if t >= self.S:
+                self._apply(b, (t - self.S) % (self.S + 1))
+        self._pull(b)
+
+    # ------------------------------------------------------------------ reporting / state
+    def staleness_histogram(self):
+        return list(self.tracker.histogram())
+
+    def staleness_p50(self) -> int:
+        return int(self.tracker.percentile(50.0))
+
+    def set_lr(self, lr: float):
+        self.dyn.set(lr=lr)
+
+    def state_dict(self) -> dict:
+        return {"master": self.master.detach().cpu(), "state1": None if self.state1 is None else self.state1.cpu(),
+                "state2": None if self.state2 is None else self.state2.cpu(), "dyn": self.dyn.t.cpu(),
+                "step_idx": self.step_idx, "rank": self.rank, "world": self.world, "P": self.P,
+                "layout": [(b.offset, b.numel, b.local_offset) for b in self.buckets]}
+
+    def load_state_dict(self, sd: dict):
+        self.master.copy_(sd["master"])
+        if self.state1 is not None:
+            self.state1.copy_(sd["state1"])
+        if self.state2 is not None:
+            self.state2.copy_(sd["state2"])
+        self.dyn.t.copy_(sd["dyn"])
+        self.step_idx = int(sd["step_idx"])
+        # re-publish the working copy from the masters
+        for b in self.buckets:
+            for j, k in enumerate(self.my_shards):
+                lo = b.local_offset + j * b.slice_numel
+                self.params_flat.narrow(0, b.offset + k * b.slice_numel, b.slice_numel).copy_(
+                    self.master.narrow(0, lo, b.slice_numel))
+        for b in self.buckets:
+            self._pull(b)
+
+    def full_params_fp32(self) -> dict:
+        """Gather the fp32 masters of every shard (for checkpoints / inspection)."""
+        return {n: p.detach().float().clone() for n, p in self.model.named_parameters()}
+
+    def num_params(self) -> int:
+        return sum(n for b in self.buckets for (_, _, _, n) in b.params)
+
+    def describe(self) -> str:
+        return (f"CollectivePS(world={self.world}, shards={self.P} on ranks {self.owners}, staleness={self.S}, "
+                f"buckets={len(self.buckets)}, params={self.num_params() / 1e6:.2f}M, transport={self.t.name})")

@@ -1,0 +1,114 @@
+"""Worker training step over the collective PS data plane, optionally captured as hipGraphs.
+
+One step = begin (zero grads) -> forward -> backward (per-bucket push/apply/pull launched from
+grad hooks onto the comm stream) -> join. With ``use_graph`` the whole step -- forward, backward,
+every RCCL collective and every fused-apply kernel -- is captured once per staleness phase
+(``t mod (S+1)`` selects the gradient slot, so S+1 graphs) and replayed; the host then only does
+the version / staleness bookkeeping. This replaces a tracing compiler: the step's ~500 kernel
+launches become one graph launch.
+
+Reference parity: ``Worker::run_iteration`` (src/worker.cpp:331-406) is a pull -> compute ->
+push -> poll loop with 500 ms sleeps; here pull/push are collectives inside the step and there is
+no polling.
+"""
+from __future__ import annotations
+
+import time
+
+import torch
+
+from ..parallel.collective_ps import CollectivePS
+
+
+class Trainer:
+    def __init__(self, model, loss_fn, ps: CollectivePS, batch, use_graph: bool = False, graph_warmup: int = 3):
+        self.model = model
+        self.loss_fn = loss_fn
+        self.ps = ps
+        self.x, self.y = batch
+        self.use_graph = use_graph and ps.is_cuda and ps.t.capturable
+        self.graph_warmup = graph_warmup
+        self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
+        self.static_loss = None
+        self.step_count = 0
+        self.graph_error = None
+
+    # eager step ---------------------------------------------------------------
+    def _body(self):
+        self.ps.begin_step()
+        out = self.model(self.x)
+        loss = self.loss_fn(out, self.y)
+        loss.backward()
+        self.ps.finish_step()
+        return loss
+
+    def eager_step(self):
+        loss = self._body()
+        self.step_count += 1
+        return loss
+
+    # graph capture ------------------------------------------------------------
+    def _capture(self, phase: int):
+        ps = self.ps
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(device=ps.device)
+        s.wait_stream(torch.cuda.current_stream(ps.device))
+        saved_idx = ps.step_idx
+        # the captured body must see the slot indices of this phase (and be past the first S
+        # apply-free steps): same residue mod S+1, >= S
+        ps.step_idx = phase + (ps.S + 1)
+        try:
+            with torch.cuda.graph(g, stream=s, pool=self._pool):
+                loss = self._body_captured()
+        finally:
+            ps.step_idx = saved_idx
+        torch.cuda.current_stream(ps.device).wait_stream(s)
+        return g, loss
+
+    def _body_captured(self):
+        # identical device work to _body, but the host bookkeeping (tracker, step counter) is done
+        # per replay by `step()`, not at capture time
+        ps = self.ps
+        ps.begin_step(track=False)
+        out = self.model(self.x)
+        loss = self.loss_fn(out, self.y)
+        loss.backward()
+        ps.finish_step(track=False)
+        return loss
+
+    def step(self):
+        """One training step (eager until the graphs are built, then graph replay)."""
+        ps = self.ps
+        if not self.use_graph:
+            return self.eager_step()
+        phases = ps.S + 1
+        # eager warmup: MIOpen/allocator/autotune must settle before capture; the first S steps
+        # (no apply yet) are also eager
+        if self.step_count < max(self.graph_warmup, ps.S) or self.graph_error is not None:
+            return self.eager_step()
+        key = ps.step_idx % phases
+        if key not in self.graphs:
+            try:
+                if not hasattr(self, "_pool"):
+                    self._pool = torch.cuda.graph_pool_handle()
+                torch.cuda.synchronize(ps.device)
+                g, loss = self._capture(key)
+                self.graphs[key] = (g, loss)
+            except Exception as e:  # capture unsupported by some library kernel: stay eager
+                self.graph_error = repr(e)
+                torch.cuda.synchronize(ps.device)
+                return self.eager_step()
+        g, loss = self.graphs[key]
+        ps.account_begin()
+        g.replay()
+        ps.account_finish()
+        self.step_count += 1
+        return loss
+
+    def run(self, steps: int) -> float:
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            self.step()
+        if self.ps.is_cuda:
+            torch.cuda.synchronize(self.ps.device)
+        return time.perf_counter() - t0

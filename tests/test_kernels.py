@@ -1,0 +1,118 @@
+"""Numerics of the gfx950 kernels (GPU) and their C++ host twins (CPU) against plain PyTorch fp32.
+
+Every kernel test runs twice: on the CPU path (always) and on cuda:0 (``-m gpu``, MI355X).
+"""
+import pytest
+import torch
+
+from parameter_server_distributed_amd.ops import (OptimConfig, OptimDyn, dequantize_fp8, fused_apply_,
+                                                  multi_reduce_, pack_cast_, quantize_fp8)
+
+DEVICES = [pytest.param("cpu", id="cpu"), pytest.param("cuda", id="gpu", marks=pytest.mark.gpu)]
+
+
+def _dev(name):
+    if name == "cuda":
+        if not torch.cuda.is_available():
+            pytest.fail("GPU test selected but no GPU visible")
+        return torch.device("cuda", 0)
+    return torch.device("cpu")
+
+
+def _torch_opt(cfg: OptimConfig, p):
+    if cfg.kind in ("sgd", "momentum"):
+        return torch.optim.SGD([p], lr=cfg.lr, momentum=cfg.momentum if cfg.kind == "momentum" else 0.0,
+                               dampening=cfg.dampening, nesterov=cfg.nesterov, weight_decay=cfg.weight_decay,
+                               maximize=cfg.maximize)
+    cls = torch.optim.Adam if cfg.kind == "adam" else torch.optim.AdamW
+    return cls([p], lr=cfg.lr, betas=(cfg.beta1, cfg.beta2), eps=cfg.eps, weight_decay=cfg.weight_decay,
+               maximize=cfg.maximize, foreach=False)
+
+
+CFGS = [
+    OptimConfig("sgd", lr=1.0, momentum=0.0),  # the reference's p -= g (src/parameter_server.cpp:87)
+    OptimConfig("sgd", lr=0.1, momentum=0.0, weight_decay=1e-2),
+    OptimConfig("momentum", lr=0.05, momentum=0.9),
+    OptimConfig("momentum", lr=0.05, momentum=0.9, nesterov=True, weight_decay=1e-3),
+    OptimConfig("momentum", lr=0.05, momentum=0.8, dampening=0.1),
+    OptimConfig("adam", lr=1e-3, weight_decay=1e-2),
+    OptimConfig("adamw", lr=1e-3, weight_decay=1e-2),
+    OptimConfig("adam", lr=1e-3, maximize=True),
+]
+
+
+@pytest.mark.parametrize("devname", DEVICES)
+@pytest.mark.parametrize("cfg", CFGS, ids=lambda c: f"{c.kind}-wd{c.weight_decay}-n{int(c.nesterov)}")
+@pytest.mark.parametrize("gdtype", [torch.float32, torch.bfloat16], ids=["g32", "g16"])
+@pytest.mark.parametrize("nsrc", [1, 3])
+def test_fused_apply_matches_torch_optim(devname, cfg, gdtype, nsrc):
+    dev = _dev(devname)
+    g = torch.Generator().manual_seed(7)
+    n = 4096 * 3 + 5  # exercises the 8-wide vector body and the scalar tail
+    p0 = torch.randn(n, generator=g)
+    ref = p0.clone().requires_grad_(True)
+    opt = _torch_opt(cfg, ref)
+    master = p0.clone().to(dev)
+    s1 = torch.zeros(n, device=dev) if cfg.num_states >= 1 else None
+    s2 = torch.zeros(n, device=dev) if cfg.num_states >= 2 else None
+    shadow = torch.empty(n, dtype=torch.bfloat16, device=dev)
+    dyn = OptimDyn(dev, lr=cfg.lr, grad_scale=1.0 / nsrc)
+    for step in range(4):
+        srcs = [torch.randn(n, generator=g).to(gdtype) for _ in range(nsrc)]
+        gsum = sum(s.float() for s in srcs) * (1.0 / nsrc)
+        ref.grad = gsum.clone()
+        opt.step()
+        fused_apply_(cfg, dyn, master, [s.to(dev) for s in srcs], s1, s2, shadow)
+    tol = 2e-5 if cfg.kind in ("sgd", "momentum") else 1e-4
+    torch.testing.assert_close(master.cpu(), ref.detach(), rtol=tol, atol=tol)
+    torch.testing.assert_close(shadow.cpu(), master.cpu().to(torch.bfloat16), rtol=0, atol=0)
+    assert dyn.step == 4
+
+
+@pytest.mark.parametrize("devname", DEVICES)
+@pytest.mark.parametrize("sd,od", [(torch.float32, torch.float32), (torch.bfloat16, torch.float32),
+                                   (torch.bfloat16, torch.bfloat16), (torch.float32, torch.bfloat16)])
+@pytest.mark.parametrize("k", [1, 2, 7, 16])
+def test_multi_reduce(devname, sd, od, k):
+    dev = _dev(devname)
+    n = 10_007
+    srcs = [torch.randn(n).to(sd) for _ in range(k)]
+    want = (sum(s.float() for s in srcs) * 0.25).to(od)
+    out = torch.empty(n, dtype=od, device=dev)
+    multi_reduce_(out, [s.to(dev) for s in srcs], 0.25)
+    tol = 1e-6 if od == torch.float32 else 1e-2
+    torch.testing.assert_close(out.cpu().float(), want.float(), rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("devname", DEVICES)
+@pytest.mark.parametrize("sd,dd", [(torch.float32, torch.bfloat16), (torch.bfloat16, torch.float32),
+                                   (torch.float32, torch.float32)])
+def test_pack_cast_many_tensors(devname, sd, dd):
+    dev = _dev(devname)
+    sizes = [1, 7, 8, 100, 8192, 8193, 20000, 3]
+    srcs = [torch.randn(s).to(sd).to(dev) for s in sizes]
+    flat = torch.zeros(sum(sizes) + 64, dtype=dd, device=dev)
+    dsts, off = [], 0
+    for s in sizes:
+        dsts.append(flat.narrow(0, off, s))
+        off += s
+    pack_cast_(srcs, dsts)
+    for s, d in zip(srcs, dsts):
+        torch.testing.assert_close(d.cpu(), s.cpu().to(dd), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("devname", DEVICES)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_fp8_roundtrip(devname, dtype):
+    dev = _dev(devname)
+    x = (torch.randn(4099) * 3).to(dtype).to(dev)
+    q, sinv = quantize_fp8(x)
+    amax = x.float().abs().max()
+    assert abs(sinv.item() - amax.item() / 448.0) < 1e-6 * max(1.0, amax.item())
+    # reference: torch's e4m3fn cast of the scaled input
+    ref_q = (x.float().cpu() * (448.0 / amax.cpu())).clamp(-448, 448).to(torch.float8_e4m3fn)
+    assert torch.equal(q.cpu().view(torch.uint8), ref_q.view(torch.uint8))
+    back = dequantize_fp8(q, sinv, torch.float32)
+    torch.testing.assert_close(back.cpu(), ref_q.float() * sinv.cpu(), rtol=1e-6, atol=1e-6)
+    rel = ((back.cpu() - x.float().cpu()).abs() / (x.float().cpu().abs() + 1e-3)).median()
+    assert rel < 0.05
