@@ -25,6 +25,9 @@ import sys
 import time
 
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+from parameter_server_distributed_amd.utils import miopen as _miopen  # noqa: E402
+
+_miopen.install()  # shipped gfx950 find-db + kernel cache (before torch initialises MIOpen)
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402

@@ -26,6 +26,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("amax_", &amax_);
   m.def("quant_fp8_", &quant_fp8_);
   m.def("dequant_fp8_", &dequant_fp8_);
+  m.def("bn_fwd", &bn_fwd, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("running_mean"),
+        py::arg("running_var"), py::arg("residual"), py::arg("relu"), py::arg("training"), py::arg("momentum"),
+        py::arg("eps"), py::arg("counter"), py::arg("ss_eval"));
+  m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("gamma"), py::arg("save_mean"),
+        py::arg("save_invstd"), py::arg("relu"), py::arg("need_dr"), py::arg("dgamma_out"), py::arg("dbeta_out"));
   m.attr("OPT_SGD") = (int)OPT_SGD;
   m.attr("OPT_MOMENTUM") = (int)OPT_MOMENTUM;
   m.attr("OPT_ADAM") = (int)OPT_ADAM;

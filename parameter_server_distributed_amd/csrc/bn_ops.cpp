@@ -1,0 +1,140 @@
+// Tensor glue for the fused NHWC BatchNorm kernels (kernels/bn.hip).
+#include <ATen/ATen.h>
+#include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPStream.h>
+
+#include <vector>
+
+#include "kernels/launchers_bn.h"
+
+namespace psd {
+
+namespace {
+
+inline hipStream_t stream_of(const at::Tensor& t) { return c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
+
+at::Tensor nhwc(const at::Tensor& t) {
+  if (t.dim() == 4) return t.contiguous(at::MemoryFormat::ChannelsLast);
+  return t.contiguous();
+}
+
+int64_t channels(const at::Tensor& t) { return t.dim() == 4 ? t.size(1) : t.size(-1); }
+
+template <typename T>
+T* opt_ptr(const c10::optional<at::Tensor>& t) {
+  return (t.has_value() && t->defined()) ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
+}
+
+void check_vec(const c10::optional<at::Tensor>& t, int64_t C, at::ScalarType st, const char* name) {
+  if (!t.has_value() || !t->defined()) return;
+  TORCH_CHECK(t->numel() == C && t->scalar_type() == st && t->is_contiguous(), "psd bn: ", name, " must be [C] ",
+              st);
+}
+
+}  // namespace
+
+std::vector<at::Tensor> bn_fwd(const at::Tensor& x_in, c10::optional<at::Tensor> gamma, c10::optional<at::Tensor> beta,
+                               c10::optional<at::Tensor> running_mean, c10::optional<at::Tensor> running_var,
+                               c10::optional<at::Tensor> residual, bool relu, bool training, double momentum, double eps,
+                               c10::optional<at::Tensor> counter, c10::optional<at::Tensor> ss_eval) {
+  TORCH_CHECK(x_in.is_cuda() && x_in.scalar_type() == at::kBFloat16, "psd bn: x must be a bf16 device tensor");
+  const c10::DeviceGuard g(x_in.device());
+  at::Tensor x = nhwc(x_in);
+  const int64_t C = channels(x);
+  TORCH_CHECK(C % 8 == 0, "psd bn: channels must be a multiple of 8, got ", C);
+  const int64_t M = x.numel() / C;
+  check_vec(gamma, C, at::kBFloat16, "gamma");
+  check_vec(beta, C, at::kBFloat16, "beta");
+  check_vec(running_mean, C, at::kFloat, "running_mean");
+  check_vec(running_var, C, at::kFloat, "running_var");
+  at::Tensor res;
+  if (residual.has_value() && residual->defined()) {
+    res = nhwc(*residual);
+    TORCH_CHECK(res.sizes() == x.sizes() && res.scalar_type() == at::kBFloat16, "psd bn: residual shape/dtype");
+  }
+  auto f32 = x.options().dtype(at::kFloat);
+  at::Tensor y = at::empty_like(x);
+  at::Tensor mean = at::empty({C}, f32), invstd = at::empty({C}, f32);
+  at::Tensor ss;
+  at::Tensor part;
+  if (training) {
+    ss = at::empty({2 * C}, f32);
+    part = at::empty({(int64_t)bn_reduce_blocks(M, (int)C) * 2 * C}, f32);
+  } else {
+    TORCH_CHECK(ss_eval.has_value() && ss_eval->numel() == 2 * C, "psd bn: eval mode needs ss_eval [2C]");
+    ss = ss_eval->contiguous();
+  }
+  BnFwdArgs a{};
+  a.x = reinterpret_cast<const uint16_t*>(x.data_ptr());
+  a.res = res.defined() ? reinterpret_cast<const uint16_t*>(res.data_ptr()) : nullptr;
+  a.y = reinterpret_cast<uint16_t*>(y.data_ptr());
+  a.gamma = opt_ptr<const uint16_t>(gamma);
+  a.beta = opt_ptr<const uint16_t>(beta);
+  a.running_mean = training ? opt_ptr<float>(running_mean) : nullptr;
+  a.running_var = training ? opt_ptr<float>(running_var) : nullptr;
+  a.save_mean = mean.data_ptr<float>();
+  a.save_invstd = invstd.data_ptr<float>();
+  a.ss = ss.data_ptr<float>();
+  a.part = part.defined() ? part.data_ptr<float>() : nullptr;
+  a.counter = training ? opt_ptr<int64_t>(counter) : nullptr;
+  a.M = M;
+  a.C = (int32_t)C;
+  a.relu = relu;
+  a.training = training;
+  a.momentum = (float)momentum;
+  a.eps = (float)eps;
+  hipError_t e = launch_bn_fwd(a, stream_of(x));
+  TORCH_CHECK(e == hipSuccess, "psd bn fwd: ", hipGetErrorString(e));
+  return {y, mean, invstd};
+}
+
+std::vector<at::Tensor> bn_bwd(const at::Tensor& dy_in, const at::Tensor& x_in, c10::optional<at::Tensor> y_in,
+                               c10::optional<at::Tensor> gamma, const at::Tensor& save_mean,
+                               const at::Tensor& save_invstd, bool relu, bool need_dr,
+                               c10::optional<at::Tensor> dgamma_out, c10::optional<at::Tensor> dbeta_out) {
+  const c10::DeviceGuard g(x_in.device());
+  at::Tensor x = nhwc(x_in), dy = nhwc(dy_in);
+  const int64_t C = channels(x);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == at::kBFloat16, "psd bn bwd: dy shape/dtype");
+  at::Tensor y;
+  if (relu) {
+    TORCH_CHECK(y_in.has_value() && y_in->defined(), "psd bn bwd: relu needs the forward output");
+    y = nhwc(*y_in);
+  }
+  auto f32 = x.options().dtype(at::kFloat);
+  at::Tensor dx = at::empty_like(x);
+  at::Tensor dr = need_dr ? at::empty_like(x) : at::Tensor();
+  at::Tensor dgamma, dbeta;
+  if (gamma.has_value() && gamma->defined()) {
+    dgamma = (dgamma_out.has_value() && dgamma_out->defined()) ? *dgamma_out : at::empty({C}, x.options());
+    dbeta = (dbeta_out.has_value() && dbeta_out->defined()) ? *dbeta_out : at::empty({C}, x.options());
+    TORCH_CHECK(dgamma.numel() == C && dgamma.scalar_type() == at::kBFloat16 && dgamma.is_contiguous(),
+                "psd bn bwd: dgamma buffer");
+    TORCH_CHECK(dbeta.numel() == C && dbeta.scalar_type() == at::kBFloat16 && dbeta.is_contiguous(),
+                "psd bn bwd: dbeta buffer");
+  }
+  at::Tensor coef = at::empty({3 * C}, f32);
+  at::Tensor part = at::empty({(int64_t)bn_reduce_blocks(M, (int)C) * 2 * C}, f32);
+  BnBwdArgs a{};
+  a.dy = reinterpret_cast<const uint16_t*>(dy.data_ptr());
+  a.y = y.defined() ? reinterpret_cast<const uint16_t*>(y.data_ptr()) : nullptr;
+  a.x = reinterpret_cast<const uint16_t*>(x.data_ptr());
+  a.gamma = opt_ptr<const uint16_t>(gamma);
+  a.save_mean = save_mean.data_ptr<float>();
+  a.save_invstd = save_invstd.data_ptr<float>();
+  a.dx = reinterpret_cast<uint16_t*>(dx.data_ptr());
+  a.dr = dr.defined() ? reinterpret_cast<uint16_t*>(dr.data_ptr()) : nullptr;
+  a.dgamma = dgamma.defined() ? reinterpret_cast<uint16_t*>(dgamma.data_ptr()) : nullptr;
+  a.dbeta = dbeta.defined() ? reinterpret_cast<uint16_t*>(dbeta.data_ptr()) : nullptr;
+  a.coef = coef.data_ptr<float>();
+  a.part = part.data_ptr<float>();
+  a.M = M;
+  a.C = (int32_t)C;
+  a.relu = relu;
+  hipError_t e = launch_bn_bwd(a, stream_of(x));
+  TORCH_CHECK(e == hipSuccess, "psd bn bwd: ", hipGetErrorString(e));
+  return {dx, dr, dgamma, dbeta};
+}
+
+}  // namespace psd

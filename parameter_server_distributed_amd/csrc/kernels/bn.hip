@@ -1,0 +1,353 @@
+// Fused NHWC (channels_last) BatchNorm + residual add + ReLU, forward and backward, for gfx950.
+//
+// Why: rocprofv3 of the ResNet-50 training step (profiles/resnet50_r1_baseline_kernels.md) showed
+// PyTorch's channels_last BN kernels at 66% of the step (collect_statistics 368 us and
+// backward_reduce 400 us per layer on average, 53 layers), plus separate ReLU / ReLU-backward /
+// residual-add kernels. These kernels are pure HBM streaming: the whole BN family of a ResNet-50
+// step moves ~50 GB, i.e. ~9 ms at the measured 6 TB/s roof.
+//
+// Layout: x is [M, C] bf16 row-major (M = N*H*W), C % 8 == 0. One lane owns 8 consecutive channels
+// (a 16-byte load); TPC = C/8 lanes cover a row and a 256-lane block covers RPI = 256/TPC rows
+// per iteration (4 KiB contiguous), so every load instruction is fully coalesced.
+//
+// Forward (training):  reduce (shifted sum/sumsq per block) -> finalize (fp64 combine, running
+//                      stats, scale/shift) -> apply y = act(x*scale + shift [+ r]).
+// Backward:            reduce (sum dy', sum dy'(x-mean); writes dr = dy' for the residual branch)
+//                      -> finalize (dgamma/dbeta straight into the parameter-gradient buffers,
+//                      3 coefficients) -> elementwise dx = A dy' + B x + C.
+// Block partials are combined by a separate finalize launch (no cross-workgroup hand-off inside a
+// launch: correct for any workgroup->XCD placement, cdna_hip_programming.md G16).
+#include "common.h"
+#include "launchers_bn.h"
+
+namespace psd {
+
+namespace {
+
+struct Map {
+  int tpc, rpi, cg, r0;
+  bool active;
+};
+
+__device__ __forceinline__ Map make_map(int C) {
+  Map m;
+  m.tpc = C >> 3;
+  if (m.tpc >= 256) {
+    m.rpi = 1;
+    m.cg = blockIdx.y * 256 + threadIdx.x;
+    m.r0 = 0;
+    m.active = m.cg < m.tpc;
+  } else {
+    m.rpi = 256 / m.tpc;
+    m.cg = threadIdx.x % m.tpc;
+    m.r0 = threadIdx.x / m.tpc;
+    m.active = m.r0 < m.rpi;
+  }
+  return m;
+}
+
+// Sum the per-lane partials (a[8], b[8]) of lanes sharing a channel group and write the block's
+// partials to part[blockIdx.x][0|1][C].
+__device__ __forceinline__ void block_partials(const Map& m, int C, const float a[8], const float b[8], float* part) {
+  float* pa = part + (int64_t)blockIdx.x * 2 * C;
+  float* pb = pa + C;
+  if (m.tpc >= 256) {
+    if (m.active) {
+      store8_f32(pa + m.cg * 8, a);
+      store8_f32(pb + m.cg * 8, b);
+    }
+    return;
+  }
+  __shared__ float red[2][256 * 8];  // [rows][C] flattened: rpi*C <= 256*8
+  if (m.active) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[0][m.r0 * C + m.cg * 8 + j] = a[j];
+      red[1][m.r0 * C + m.cg * 8 + j] = b[j];
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float sa = 0.f, sb = 0.f;
+    for (int r = 0; r < m.rpi; ++r) {
+      sa += red[0][r * C + c];
+      sb += red[1][r * C + c];
+    }
+    pa[c] = sa;
+    pb[c] = sb;
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ forward
+__global__ __launch_bounds__(256) void bn_fwd_reduce_kernel(const uint16_t* __restrict__ x, int64_t M, int C,
+                                                            const float* __restrict__ shift_k, float* __restrict__ part) {
+  const Map m = make_map(C);
+  float a[8], b[8], k[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = b[j] = k[j] = 0.f;
+  if (m.active) {
+    if (shift_k) load8_f32(shift_k + m.cg * 8, k);
+    const int64_t stride = (int64_t)gridDim.x * m.rpi;
+    int64_t r = (int64_t)blockIdx.x * m.rpi + m.r0;
+    for (; r + stride < M; r += 2 * stride) {  // 2 independent 16-B loads in flight per lane
+      float v0[8], v1[8];
+      load8_bf16(x + r * C + m.cg * 8, v0);
+      load8_bf16(x + (r + stride) * C + m.cg * 8, v1);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float d0 = v0[j] - k[j], d1 = v1[j] - k[j];
+        a[j] += d0 + d1;
+        b[j] = fmaf(d0, d0, fmaf(d1, d1, b[j]));
+      }
+    }
+    for (; r < M; r += stride) {
+      float v0[8];
+      load8_bf16(x + r * C + m.cg * 8, v0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float d0 = v0[j] - k[j];
+        a[j] += d0;
+        b[j] = fmaf(d0, d0, b[j]);
+      }
+    }
+  }
+  block_partials(m, C, a, b, part);
+}
+
+__global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const float* __restrict__ part, int nblk, int64_t M, int C,
+                                                              const float* __restrict__ shift_k,
+                                                              const uint16_t* __restrict__ gamma,
+                                                              const uint16_t* __restrict__ beta, float* running_mean,
+                                                              float* running_var, float momentum, float eps,
+                                                              float* __restrict__ save_mean,
+                                                              float* __restrict__ save_invstd, float* __restrict__ ss,
+                                                              int64_t* counter) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0 && counter) *counter += 1;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int b = 0; b < nblk; ++b) {
+    s += part[(int64_t)b * 2 * C + c];
+    q += part[(int64_t)b * 2 * C + C + c];
+  }
+  const double ms = s / (double)M;
+  double var = q / (double)M - ms * ms;
+  if (var < 0) var = 0;
+  const float k = shift_k ? shift_k[c] : 0.f;
+  const float mean = (float)(ms + (double)k);
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  save_mean[c] = mean;
+  save_invstd[c] = invstd;
+  const float g = gamma ? bf16_to_f32(gamma[c]) : 1.f;
+  const float bt = beta ? bf16_to_f32(beta[c]) : 0.f;
+  const float scale = g * invstd;
+  ss[c] = scale;
+  ss[C + c] = bt - mean * scale;
+  if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
+  if (running_var) {
+    const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unbiased;
+  }
+}
+
+template <bool RELU, bool RES>
+__global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
+                                                       const float* __restrict__ ss, uint16_t* __restrict__ y,
+                                                       int64_t nvec, int C) {
+  const int tpc = C >> 3;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;  // host guarantees stride % tpc == 0
+  int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int cg = (int)(v % tpc);
+  float sc[8], sh[8];
+  load8_f32(ss + cg * 8, sc);
+  load8_f32(ss + C + cg * 8, sh);
+  for (; v < nvec; v += stride) {
+    float t[8];
+    load8_bf16(x + v * 8, t);
+    float rr[8];
+    if (RES) load8_bf16(res + v * 8, rr);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float o = fmaf(t[j], sc[j], sh[j]);
+      if (RES) o += rr[j];
+      if (RELU) o = fmaxf(o, 0.f);
+      t[j] = o;
+    }
+    store8_bf16(y + v * 8, t);
+  }
+}
+
+// ------------------------------------------------------------------ backward
+template <bool RELU, bool RES_OUT>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
+                                                            const uint16_t* __restrict__ x, const float* __restrict__ mean,
+                                                            uint16_t* __restrict__ dr, int64_t M, int C,
+                                                            float* __restrict__ part) {
+  const Map m = make_map(C);
+  float a[8], b[8], mu[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = b[j] = 0.f;
+  if (m.active) {
+    load8_f32(mean + m.cg * 8, mu);
+    const int64_t stride = (int64_t)gridDim.x * m.rpi;
+    for (int64_t r = (int64_t)blockIdx.x * m.rpi + m.r0; r < M; r += stride) {
+      const int64_t off = r * C + m.cg * 8;
+      float g[8], xv[8];
+      load8_bf16(dy + off, g);
+      load8_bf16(x + off, xv);
+      if (RELU) {
+        float yv[8];
+        load8_bf16(y + off, yv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
+      }
+      if (RES_OUT) store8_bf16(dr + off, g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        a[j] += g[j];
+        b[j] = fmaf(g[j], xv[j] - mu[j], b[j]);
+      }
+    }
+  }
+  block_partials(m, C, a, b, part);
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, int64_t M, int C,
+                                                              const uint16_t* __restrict__ gamma,
+                                                              const float* __restrict__ mean,
+                                                              const float* __restrict__ invstd,
+                                                              uint16_t* __restrict__ dgamma, uint16_t* __restrict__ dbeta,
+                                                              float* __restrict__ coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s1 = 0.0, s2 = 0.0;
+  for (int b = 0; b < nblk; ++b) {
+    s1 += part[(int64_t)b * 2 * C + c];
+    s2 += part[(int64_t)b * 2 * C + C + c];
+  }
+  const float is = invstd[c];
+  if (dgamma) dgamma[c] = f32_to_bf16((float)(s2 * is));
+  if (dbeta) dbeta[c] = f32_to_bf16((float)s1);
+  const float g = gamma ? bf16_to_f32(gamma[c]) : 1.f;
+  const float k1 = g * is;
+  const float k3 = (float)(s2 * (double)is * (double)is / (double)M);
+  const float k2 = (float)(s1 / (double)M);
+  coef[c] = k1;                                 // A
+  coef[C + c] = -k1 * k3;                       // B
+  coef[2 * C + c] = -k1 * k2 + k1 * k3 * mean[c];  // C
+}
+
+// MODE 0: dy' = dy; MODE 1: dy' = dy * (y > 0); MODE 2: dy' = g (already masked, = dr)
+template <int MODE>
+__global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(const uint16_t* __restrict__ g, const uint16_t* __restrict__ y,
+                                                           const uint16_t* __restrict__ x, const float* __restrict__ coef,
+                                                           uint16_t* __restrict__ dx, int64_t nvec, int C) {
+  const int tpc = C >> 3;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int cg = (int)(v % tpc);
+  float A[8], B[8], Cc[8];
+  load8_f32(coef + cg * 8, A);
+  load8_f32(coef + C + cg * 8, B);
+  load8_f32(coef + 2 * C + cg * 8, Cc);
+  for (; v < nvec; v += stride) {
+    float gv[8], xv[8];
+    load8_bf16(g + v * 8, gv);
+    load8_bf16(x + v * 8, xv);
+    if (MODE == 1) {
+      float yv[8];
+      load8_bf16(y + v * 8, yv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) gv[j] = yv[j] > 0.f ? gv[j] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) gv[j] = fmaf(A[j], gv[j], fmaf(B[j], xv[j], Cc[j]));
+    store8_bf16(dx + v * 8, gv);
+  }
+}
+
+// ------------------------------------------------------------------ host launchers
+static int gcd_i(int a, int b) { return b == 0 ? a : gcd_i(b, a % b); }
+
+static void reduce_grid(int64_t M, int C, int& gx, int& gy) {
+  const int tpc = C >> 3;
+  int rpi;
+  if (tpc >= 256) {
+    gy = (tpc + 255) / 256;
+    rpi = 1;
+  } else {
+    gy = 1;
+    rpi = 256 / tpc;
+  }
+  // ~8+ rows per lane, <= ~2048 blocks in total (256 CUs x 8)
+  int64_t want = (M + (int64_t)rpi * 8 - 1) / ((int64_t)rpi * 8);
+  int64_t cap = 2048 / gy;
+  if (cap < 1) cap = 1;
+  gx = (int)(want < 1 ? 1 : (want > cap ? cap : want));
+}
+
+int bn_reduce_blocks(int64_t M, int C) {
+  int gx, gy;
+  reduce_grid(M, C, gx, gy);
+  return gx;
+}
+
+static int elem_grid(int64_t nvec, int C) {
+  const int tpc = C >> 3;
+  int g = stream_grid(nvec, 256);
+  const int mult = tpc / gcd_i(tpc, 256);  // (g*256) % tpc == 0  <=>  g % mult == 0
+  g = ((g + mult - 1) / mult) * mult;
+  return g;
+}
+
+hipError_t launch_bn_fwd(const BnFwdArgs& a, hipStream_t st) {
+  if (a.M <= 0) return hipSuccess;
+  if (a.C % 8 != 0) return hipErrorInvalidValue;
+  int gx, gy;
+  reduce_grid(a.M, a.C, gx, gy);
+  if (a.training) {
+    hipLaunchKernelGGL(bn_fwd_reduce_kernel, dim3(gx, gy), dim3(256), 0, st, a.x, a.M, a.C, a.running_mean, a.part);
+    hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((a.C + 255) / 256), dim3(256), 0, st, a.part, gx, a.M, a.C,
+                       a.running_mean, a.gamma, a.beta, a.running_mean, a.running_var, a.momentum, a.eps, a.save_mean,
+                       a.save_invstd, a.ss, a.counter);
+  }
+  const int64_t nvec = a.M * (a.C / 8);
+  const int g = elem_grid(nvec, a.C);
+#define PSD_APPLY(R, S) hipLaunchKernelGGL((bn_apply_kernel<R, S>), dim3(g), dim3(256), 0, st, a.x, a.res, a.ss, a.y, nvec, a.C)
+  if (a.relu && a.res) PSD_APPLY(true, true);
+  else if (a.relu) PSD_APPLY(true, false);
+  else if (a.res) PSD_APPLY(false, true);
+  else PSD_APPLY(false, false);
+#undef PSD_APPLY
+  return hipGetLastError();
+}
+
+hipError_t launch_bn_bwd(const BnBwdArgs& a, hipStream_t st) {
+  if (a.M <= 0) return hipSuccess;
+  if (a.C % 8 != 0) return hipErrorInvalidValue;
+  int gx, gy;
+  reduce_grid(a.M, a.C, gx, gy);
+#define PSD_RED(R, O)                                                                                        \
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<R, O>), dim3(gx, gy), dim3(256), 0, st, a.dy, a.y, a.x, a.save_mean, \
+                     a.dr, a.M, a.C, a.part)
+  if (a.relu && a.dr) PSD_RED(true, true);
+  else if (a.relu) PSD_RED(true, false);
+  else if (a.dr) PSD_RED(false, true);
+  else PSD_RED(false, false);
+#undef PSD_RED
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((a.C + 255) / 256), dim3(256), 0, st, a.part, gx, a.M, a.C, a.gamma,
+                     a.save_mean, a.save_invstd, a.dgamma, a.dbeta, a.coef);
+  const int64_t nvec = a.M * (a.C / 8);
+  const int g = elem_grid(nvec, a.C);
+  if (a.dr)
+    hipLaunchKernelGGL(bn_bwd_elemt_kernel<2>, dim3(g), dim3(256), 0, st, a.dr, a.y, a.x, a.coef, a.dx, nvec, a.C);
+  else if (a.relu)
+    hipLaunchKernelGGL(bn_bwd_elemt_kernel<1>, dim3(g), dim3(256), 0, st, a.dy, a.y, a.x, a.coef, a.dx, nvec, a.C);
+  else
+    hipLaunchKernelGGL(bn_bwd_elemt_kernel<0>, dim3(g), dim3(256), 0, st, a.dy, a.y, a.x, a.coef, a.dx, nvec, a.C);
+  return hipGetLastError();
+}
+
+}  // namespace psd

@@ -1,0 +1,51 @@
+// Launch API of the fused NHWC BatchNorm(+residual)(+ReLU) kernels (bn.hip).
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <cstdint>
+
+namespace psd {
+
+struct BnFwdArgs {
+  const uint16_t* x;      // [M, C] bf16
+  const uint16_t* res;    // optional residual [M, C] bf16
+  uint16_t* y;            // [M, C] bf16
+  const uint16_t* gamma;  // [C] bf16 (optional)
+  const uint16_t* beta;   // [C] bf16 (optional)
+  float* running_mean;    // [C] fp32 (optional; also used as the variance shift)
+  float* running_var;     // [C] fp32 (optional)
+  float* save_mean;       // [C]
+  float* save_invstd;     // [C]
+  float* ss;              // [2C] scale, shift (inference: provided; training: produced)
+  float* part;            // [bn_reduce_blocks * 2C] workspace
+  int64_t* counter;       // num_batches_tracked (optional)
+  int64_t M;
+  int32_t C;
+  int32_t relu;
+  int32_t training;
+  float momentum;
+  float eps;
+};
+
+struct BnBwdArgs {
+  const uint16_t* dy;
+  const uint16_t* y;      // forward output (ReLU mask), may be null if !relu
+  const uint16_t* x;      // forward input
+  const uint16_t* gamma;
+  const float* save_mean;
+  const float* save_invstd;
+  uint16_t* dx;
+  uint16_t* dr;           // optional: gradient of the residual input (= masked dy)
+  uint16_t* dgamma;       // optional, bf16 [C]
+  uint16_t* dbeta;        // optional, bf16 [C]
+  float* coef;            // [3C] workspace
+  float* part;            // [bn_reduce_blocks * 2C] workspace
+  int64_t M;
+  int32_t C;
+  int32_t relu;
+};
+
+int bn_reduce_blocks(int64_t M, int C);
+hipError_t launch_bn_fwd(const BnFwdArgs& a, hipStream_t stream);
+hipError_t launch_bn_bwd(const BnBwdArgs& a, hipStream_t stream);
+
+}  // namespace psd

@@ -15,4 +15,13 @@ void amax_(const at::Tensor& x, at::Tensor amax_out);
 void quant_fp8_(const at::Tensor& x, const at::Tensor& amax, double fp8_max, at::Tensor out, at::Tensor scale_inv);
 void dequant_fp8_(const at::Tensor& x, const at::Tensor& scale_inv, at::Tensor out);
 
+std::vector<at::Tensor> bn_fwd(const at::Tensor& x, c10::optional<at::Tensor> gamma, c10::optional<at::Tensor> beta,
+                               c10::optional<at::Tensor> running_mean, c10::optional<at::Tensor> running_var,
+                               c10::optional<at::Tensor> residual, bool relu, bool training, double momentum, double eps,
+                               c10::optional<at::Tensor> counter, c10::optional<at::Tensor> ss_eval);
+std::vector<at::Tensor> bn_bwd(const at::Tensor& dy, const at::Tensor& x, c10::optional<at::Tensor> y,
+                               c10::optional<at::Tensor> gamma, const at::Tensor& save_mean,
+                               const at::Tensor& save_invstd, bool relu, bool need_dr,
+                               c10::optional<at::Tensor> dgamma_out, c10::optional<at::Tensor> dbeta_out);
+
 }  // namespace psd

@@ -55,6 +55,8 @@ def prepare(model: nn.Module, device, dtype=torch.bfloat16, channels_last: bool 
     if channels_last:
         model = model.to(memory_format=torch.channels_last)
     for m in model.modules():
+        if getattr(m, "_psd_fp32_buffers", False):
+            continue
         for k, b in list(m._buffers.items()):
             if b is not None and b.is_floating_point():
                 m._buffers[k] = b.to(dtype)

@@ -13,6 +13,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.bn import FusedBatchNorm2d
+
 
 def _conv(cin, cout, k, stride=1, groups=1):
     return nn.Conv2d(cin, cout, k, stride=stride, padding=k // 2, groups=groups, bias=False)
@@ -24,20 +26,20 @@ class Bottleneck(nn.Module):
     def __init__(self, cin, planes, stride=1, width_per_group=64, downsample=None):
         super().__init__()
         width = int(planes * (width_per_group / 64.0))
+        # BN + ReLU (+ residual) run as one fused NHWC kernel family (ops/bn.py)
         self.conv1 = _conv(cin, width, 1)
-        self.bn1 = nn.BatchNorm2d(width)
+        self.bn1 = FusedBatchNorm2d(width, relu=True)
         self.conv2 = _conv(width, width, 3, stride)
-        self.bn2 = nn.BatchNorm2d(width)
+        self.bn2 = FusedBatchNorm2d(width, relu=True)
         self.conv3 = _conv(width, planes * self.expansion, 1)
-        self.bn3 = nn.BatchNorm2d(planes * self.expansion)
+        self.bn3 = FusedBatchNorm2d(planes * self.expansion, relu=True)  # relu(bn3(conv3) + identity)
         self.downsample = downsample
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
-        out = F.relu(self.bn1(self.conv1(x)), inplace=True)
-        out = F.relu(self.bn2(self.conv2(out)), inplace=True)
-        out = self.bn3(self.conv3(out))
-        return F.relu(out + idt, inplace=True)
+        out = self.bn1(self.conv1(x))
+        out = self.bn2(self.conv2(out))
+        return self.bn3(self.conv3(out), idt)
 
 
 class ResNet(nn.Module):
@@ -46,7 +48,7 @@ class ResNet(nn.Module):
         self.width_per_group = width_per_group
         self.cin = 64
         self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
-        self.bn1 = nn.BatchNorm2d(64)
+        self.bn1 = FusedBatchNorm2d(64, relu=True)
         self.layer1 = self._make(64, layers[0])
         self.layer2 = self._make(128, layers[1], stride=2)
         self.layer3 = self._make(256, layers[2], stride=2)
@@ -55,7 +57,7 @@ class ResNet(nn.Module):
         for m in self.modules():
             if isinstance(m, nn.Conv2d):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
-            elif isinstance(m, nn.BatchNorm2d):
+            elif isinstance(m, nn.BatchNorm2d):  # includes FusedBatchNorm2d
                 nn.init.ones_(m.weight)
                 nn.init.zeros_(m.bias)
         if zero_init_residual:
@@ -67,7 +69,7 @@ class ResNet(nn.Module):
         down = None
         if stride != 1 or self.cin != planes * Bottleneck.expansion:
             down = nn.Sequential(_conv(self.cin, planes * Bottleneck.expansion, 1, stride),
-                                 nn.BatchNorm2d(planes * Bottleneck.expansion))
+                                 FusedBatchNorm2d(planes * Bottleneck.expansion))
         mods = [Bottleneck(self.cin, planes, stride, self.width_per_group, down)]
         self.cin = planes * Bottleneck.expansion
         for _ in range(1, blocks):
@@ -75,7 +77,7 @@ class ResNet(nn.Module):
         return nn.Sequential(*mods)
 
     def forward(self, x):
-        x = F.relu(self.bn1(self.conv1(x)), inplace=True)
+        x = self.bn1(self.conv1(x))
         x = F.max_pool2d(x, 3, 2, 1)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)

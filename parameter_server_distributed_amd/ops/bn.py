@@ -1,0 +1,89 @@
+"""Fused NHWC BatchNorm2d (+ residual add) (+ ReLU) on the gfx950 kernels of ``csrc/kernels/bn.hip``.
+
+``FusedBatchNorm2d`` is a drop-in ``nn.BatchNorm2d`` whose forward also takes an optional residual
+and applies ReLU in the same pass; backward fuses the ReLU mask, the residual-branch gradient and
+the BN input gradient. Running statistics are fp32 (the kernels also use them as the variance
+shift), parameters are whatever dtype the PS data plane gives them (bf16 views).
+
+Grad sink: when the PS data plane owns the parameters it installs ``_psd_grad_sink`` on the
+module; backward then writes dgamma/dbeta straight into the flat gradient buffer (no separate
+accumulate kernel) and returns those views, which autograd's AccumulateGrad adopts.
+
+Device tensors that are not bf16 or whose channel count is not a multiple of 8 -- and every CPU
+tensor -- take the reference composite path (fp32 ``F.batch_norm``), which is also what the tests
+compare the kernels against.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import native
+
+
+def _kernel_ok(x: torch.Tensor) -> bool:
+    return x.is_cuda and x.dtype == torch.bfloat16 and x.dim() in (2, 4) and x.shape[1] % 8 == 0
+
+
+class _FusedBNFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual, mod):
+        C = native()
+        y, mean, invstd = C.bn_fwd(x, weight, bias, mod.running_mean, mod.running_var, residual, mod.relu, True,
+                                   mod.momentum if mod.momentum is not None else 0.1, mod.eps,
+                                   mod.num_batches_tracked, None)
+        ctx.relu = mod.relu
+        ctx.has_res = residual is not None
+        ctx.mod = mod
+        ctx.save_for_backward(x, y if mod.relu else None, weight, mean, invstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, w, mean, invstd = ctx.saved_tensors
+        mod = ctx.mod
+        sink = getattr(mod, "_psd_grad_sink", None)
+        dgo = dbo = None
+        if sink is not None and w is not None:
+            dgo, dbo = sink(mod.weight), sink(mod.bias)
+        dx, dr, dg, db = native().bn_bwd(dy, x, y, w, mean, invstd, ctx.relu, ctx.has_res, dgo, dbo)
+        return dx, (dg if w is not None else None), (db if w is not None else None), (dr if ctx.has_res else None), None
+
+
+class FusedBatchNorm2d(nn.BatchNorm2d):
+    """``nn.BatchNorm2d`` + optional residual + optional ReLU, one fused kernel family on MI355X."""
+
+    _psd_fp32_buffers = True  # models.prepare() keeps our running stats fp32
+
+    def __init__(self, num_features: int, eps: float = 1e-5, momentum: float = 0.1, relu: bool = False):
+        super().__init__(num_features, eps=eps, momentum=momentum)
+        self.relu = relu
+
+    def psd_direct_grad_params(self):
+        return [self.weight, self.bias]
+
+    def forward(self, x, residual=None):
+        if self.training and _kernel_ok(x) and self.running_mean is not None:
+            return _FusedBNFn.apply(x, self.weight, self.bias, residual, self)
+        if not self.training and _kernel_ok(x) and self.running_mean is not None:
+            scale = self.weight.float() * torch.rsqrt(self.running_var + self.eps)
+            shift = self.bias.float() - self.running_mean * scale
+            ss = torch.cat([scale, shift]).contiguous()
+            if torch.is_grad_enabled() and (x.requires_grad or self.weight.requires_grad):
+                return self._reference(x, residual)
+            y, _, _ = native().bn_fwd(x, None, None, None, None, residual, self.relu, False, 0.0, self.eps, None, ss)
+            return y
+        return self._reference(x, residual)
+
+    def _reference(self, x, residual=None):
+        """fp32 composite (CPU / odd shapes / eval-with-grad): numerics reference for the kernels."""
+        y = F.batch_norm(x.float(), self.running_mean, self.running_var,
+                         None if self.weight is None else self.weight.float(),
+                         None if self.bias is None else self.bias.float(),
+                         self.training, self.momentum if self.momentum is not None else 0.1, self.eps)
+        if residual is not None:
+            y = y + residual.float()
+        if self.relu:
+            y = F.relu(y)
+        return y.to(x.dtype)

@@ -148,20 +148,32 @@ class CollectivePS:
                       for _ in range(self.S + 1)] if self.S > 0 else []
         self.dyn = OptimDyn(dev, lr=optim.lr, grad_scale=1.0 / self.world)
 
+        # Modules that can write their parameter gradients straight into our flat buffer (fused BN)
+        # get a grad sink; their params keep .grad = None so autograd adopts the written view
+        # instead of launching an accumulate kernel.
+        self._grad_views = {}
+        self._direct = set()
+        for m in model.modules():
+            if hasattr(m, "psd_direct_grad_params"):
+                for dp in m.psd_direct_grad_params():
+                    if dp is not None and dp.requires_grad:
+                        self._direct.add(id(dp))
+                m._psd_grad_sink = self._sink
         # re-point the model at the flat buffers
         for b in buckets:
             for _, p, o, _n in b.params:
                 p.data = _flat_view(self.params_flat, o, p)
-                p.grad = _flat_view(self.grads_flat, o, p)
+                self._grad_views[id(p)] = _flat_view(self.grads_flat, o, p)
+                p.grad = None if id(p) in self._direct else self._grad_views[id(p)]
+        self._direct_params = [p for b in buckets for (_, p, _o, _n) in b.params if id(p) in self._direct]
         self._hooks = []
         self._p2b = {}
         for b in buckets:
             for _, p, _o, _n in b.params:
                 self._p2b[id(p)] = b
-        if overlap:
-            for b in buckets:
-                for _, p, _o, _n in b.params:
-                    self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+        for b in buckets:
+            for _, p, _o, _n in b.params:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
         if self.is_cuda:
             self.comm_stream = torch.cuda.Stream(device=dev)
             self.ready_events = [torch.cuda.Event() for _ in buckets]
@@ -179,6 +191,10 @@ class CollectivePS:
         if self.is_cuda:
             torch.cuda.synchronize(self.device)
 
+    def _sink(self, p):
+        """Flat-gradient view a fused op may write ``p``'s gradient into (or None)."""
+        return self._grad_views.get(id(p)) if id(p) in self._direct else None
+
     def memory_bytes(self) -> dict:
         eb = lambda t: 0 if t is None else t.numel() * t.element_size()  # noqa: E731
         return {"params_bf16": eb(self.params_flat), "grads": eb(self.grads_flat), "master": eb(self.master),
@@ -190,6 +206,8 @@ class CollectivePS:
         if track:
             self.account_begin()
         self.grads_flat.zero_()
+        for p in self._direct_params:
+            p.grad = None
         for b in self.buckets:
             b.pending = len(b.params)
             b.launched = False
@@ -210,8 +228,14 @@ class CollectivePS:
         self.step_idx += 1
 
     def _on_grad(self, p):
+        if id(p) in self._direct:
+            v = self._grad_views[id(p)]
+            if p.grad is not None and p.grad.data_ptr() != v.data_ptr():
+                v.copy_(p.grad)  # producer did not use the sink (reference / CPU path)
         b = self._p2b[id(p)]
         b.pending -= 1
+        if not self.overlap:
+            return
         # Launch strictly in bucket order so every rank enqueues the same collective sequence
         # (an out-of-order ready bucket waits for its predecessors).
         while self._next < len(self.buckets) and self.buckets[self._next].pending <= 0:

@@ -1,0 +1,34 @@
+"""Ship MIOpen's tuned find-db and compiled-kernel cache with the repo.
+
+A fresh MI355X box starts with an empty MIOpen user database, so the first training step of
+ResNet-50 spends minutes in convolution Find + kernel compilation. ``tuning/miopen`` holds the
+database and kernel cache produced on gfx950 by ``bench.py`` (MIOPEN_USER_DB_PATH /
+MIOPEN_CUSTOM_CACHE_DIR); ``install()`` copies it to a writable scratch directory and points
+MIOpen at it. Must run before the first convolution (ideally before ``import torch``).
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+SRC = os.path.join(ROOT, "tuning", "miopen")
+
+
+def install(force: bool = False) -> str | None:
+    if not force and ("MIOPEN_USER_DB_PATH" in os.environ or os.environ.get("PSD_NO_MIOPEN_DB") == "1"):
+        return os.environ.get("MIOPEN_USER_DB_PATH")
+    if not os.path.isdir(SRC):
+        return None
+    dst = os.path.join(tempfile.gettempdir(), f"psd_miopen_{os.getuid()}_{os.getpid()}")
+    for sub in ("db", "cache"):
+        s = os.path.join(SRC, sub)
+        d = os.path.join(dst, sub)
+        os.makedirs(d, exist_ok=True)
+        if os.path.isdir(s):
+            for f in os.listdir(s):
+                shutil.copy2(os.path.join(s, f), os.path.join(d, f))
+    os.environ["MIOPEN_USER_DB_PATH"] = os.path.join(dst, "db")
+    os.environ["MIOPEN_CUSTOM_CACHE_DIR"] = os.path.join(dst, "cache")
+    return dst

@@ -1,0 +1,87 @@
+"""Fused NHWC BatchNorm(+residual)(+ReLU) gfx950 kernels vs a plain PyTorch fp32 reference."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from parameter_server_distributed_amd.ops.bn import FusedBatchNorm2d
+
+SHAPES = [(4, 64, 8, 8), (2, 256, 7, 7), (2, 2048, 3, 3), (3, 24, 5, 5), (8, 128, 14, 14)]
+
+
+def _ref(x, w, b, rm, rv, res, relu, momentum=0.1, eps=1e-5):
+    y = F.batch_norm(x, rm, rv, w, b, True, momentum, eps)
+    if res is not None:
+        y = y + res
+    return F.relu(y) if relu else y
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(map(str, s)))
+@pytest.mark.parametrize("relu", [False, True])
+@pytest.mark.parametrize("residual", [False, True])
+def test_fused_bn_train_fwd_bwd(gpu, shape, relu, residual):
+    torch.manual_seed(0)
+    N, C, H, W = shape
+    x = (torch.randn(shape) * 2 + 0.5).to(torch.bfloat16)
+    r = torch.randn(shape).to(torch.bfloat16) if residual else None
+    gy = torch.randn(shape).to(torch.bfloat16)
+    m = FusedBatchNorm2d(C, relu=relu).to(gpu)
+    with torch.no_grad():
+        m.weight.copy_(torch.rand(C) + 0.5)
+        m.bias.copy_(torch.randn(C) * 0.1)
+        m.running_mean.copy_(torch.randn(C) * 0.1)
+        m.running_var.copy_(torch.rand(C) + 0.5)
+    m.weight.data = m.weight.data.to(torch.bfloat16)
+    m.bias.data = m.bias.data.to(torch.bfloat16)
+    rm0, rv0 = m.running_mean.cpu().clone(), m.running_var.cpu().clone()
+
+    xd = x.to(gpu).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    rd = r.to(gpu).contiguous(memory_format=torch.channels_last).requires_grad_(True) if residual else None
+    y = m(xd, rd)
+    y.backward(gy.to(gpu).contiguous(memory_format=torch.channels_last))
+
+    # fp32 reference on the same bf16-rounded inputs
+    xr = x.float().requires_grad_(True)
+    rr = r.float().requires_grad_(True) if residual else None
+    wr = m.weight.detach().float().cpu().requires_grad_(True)
+    br = m.bias.detach().float().cpu().requires_grad_(True)
+    rm, rv = rm0.clone(), rv0.clone()
+    yr = _ref(xr, wr, br, rm, rv, rr, relu)
+    yr.backward(gy.float())
+
+    torch.testing.assert_close(y.float().cpu(), yr.detach(), rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(m.running_mean.cpu(), rm, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(m.running_var.cpu(), rv, rtol=1e-3, atol=1e-3)
+    assert int(m.num_batches_tracked.item()) == 1
+    # gradients: bf16 outputs, relative to the gradient scale
+    sc = xr.grad.abs().max().item() + 1e-6
+    torch.testing.assert_close(xd.grad.float().cpu() / sc, xr.grad / sc, rtol=0, atol=2e-2)
+    torch.testing.assert_close(m.weight.grad.float().cpu(), wr.grad, rtol=2e-2, atol=2e-2 * wr.grad.abs().max().item())
+    torch.testing.assert_close(m.bias.grad.float().cpu(), br.grad, rtol=2e-2, atol=2e-2 * br.grad.abs().max().item())
+    if residual:
+        torch.testing.assert_close(rd.grad.float().cpu(), rr.grad, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.gpu
+def test_fused_bn_eval_matches_reference(gpu):
+    torch.manual_seed(1)
+    m = FusedBatchNorm2d(64, relu=True).to(gpu)
+    m.running_mean.normal_()
+    m.running_var.uniform_(0.5, 2.0)
+    m.weight.data = (torch.rand(64, device=gpu) + 0.5).to(torch.bfloat16)
+    m.bias.data = torch.randn(64, device=gpu).to(torch.bfloat16)
+    m.eval()
+    x = torch.randn(2, 64, 9, 9, device=gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        y = m(x)
+        yr = m._reference(x)
+    torch.testing.assert_close(y.float(), yr.float(), rtol=2e-2, atol=2e-2)
+
+
+def test_fused_bn_cpu_reference_path():
+    m = FusedBatchNorm2d(16, relu=True)
+    x = torch.randn(2, 16, 4, 4)
+    r = torch.randn(2, 16, 4, 4)
+    y = m(x, r)
+    ref = F.relu(F.batch_norm(x, None, None, None, None, True) + r)
+    torch.testing.assert_close(y, ref, rtol=1e-5, atol=1e-5)
