@@ -78,6 +78,41 @@ __device__ __forceinline__ void block_partials(const Map& m, int C, const float 
   }
 }
 
+// Finalize launches use one 256-lane block per 8 channels: lane (g, j) = (t >> 3, t & 7) sums the
+// partial rows g, g+32, ... of channel c0+j (independent loads, no serial 2048-deep chain), then
+// the 32 row groups are combined in LDS in fp64. Returns the totals in lanes t < 8.
+constexpr int kFinCh = 8;
+__device__ __forceinline__ bool sum_partials(const float* __restrict__ part, int nblk, int C, int c0, double& s,
+                                             double& q) {
+  const int j = threadIdx.x & 7, g = threadIdx.x >> 3;
+  const int c = c0 + j;
+  double a = 0.0, b = 0.0;
+  if (c < C) {
+    float fa[4] = {0.f, 0.f, 0.f, 0.f}, fb[4] = {0.f, 0.f, 0.f, 0.f};
+    int r = g, k = 0;
+    for (; r < nblk; r += 32, k = (k + 1) & 3) {  // 4 rotating fp32 accumulators, <= 64 rows each
+      fa[k] += part[(int64_t)r * 2 * C + c];
+      fb[k] += part[(int64_t)r * 2 * C + C + c];
+    }
+    a = (double)fa[0] + fa[1] + fa[2] + fa[3];
+    b = (double)fb[0] + fb[1] + fb[2] + fb[3];
+  }
+  __shared__ double red[2][32][kFinCh];
+  red[0][g][j] = a;
+  red[1][g][j] = b;
+  __syncthreads();
+  if (threadIdx.x < kFinCh) {
+    s = 0.0;
+    q = 0.0;
+    for (int k = 0; k < 32; ++k) {
+      s += red[0][k][threadIdx.x];
+      q += red[1][k][threadIdx.x];
+    }
+    return c0 + (int)threadIdx.x < C;
+  }
+  return false;
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ forward
@@ -116,22 +151,19 @@ __global__ __launch_bounds__(256) void bn_fwd_reduce_kernel(const uint16_t* __re
   block_partials(m, C, a, b, part);
 }
 
+// shift_k aliases running_mean (read, then updated by the same lane): no __restrict__ on either.
 __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const float* __restrict__ part, int nblk, int64_t M, int C,
-                                                              const float* __restrict__ shift_k,
+                                                              const float* shift_k,
                                                               const uint16_t* __restrict__ gamma,
                                                               const uint16_t* __restrict__ beta, float* running_mean,
                                                               float* running_var, float momentum, float eps,
                                                               float* __restrict__ save_mean,
                                                               float* __restrict__ save_invstd, float* __restrict__ ss,
                                                               int64_t* counter) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c == 0 && counter) *counter += 1;
-  if (c >= C) return;
-  double s = 0.0, q = 0.0;
-  for (int b = 0; b < nblk; ++b) {
-    s += part[(int64_t)b * 2 * C + c];
-    q += part[(int64_t)b * 2 * C + C + c];
-  }
+  const int c = blockIdx.x * kFinCh + threadIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && counter) *counter += 1;
+  double s, q;
+  if (!sum_partials(part, nblk, C, blockIdx.x * kFinCh, s, q)) return;
   const double ms = s / (double)M;
   double var = q / (double)M - ms * ms;
   if (var < 0) var = 0;
@@ -220,13 +252,9 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
                                                               const float* __restrict__ invstd,
                                                               uint16_t* __restrict__ dgamma, uint16_t* __restrict__ dbeta,
                                                               float* __restrict__ coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s1 = 0.0, s2 = 0.0;
-  for (int b = 0; b < nblk; ++b) {
-    s1 += part[(int64_t)b * 2 * C + c];
-    s2 += part[(int64_t)b * 2 * C + C + c];
-  }
+  const int c = blockIdx.x * kFinCh + threadIdx.x;
+  double s1, s2;
+  if (!sum_partials(part, nblk, C, blockIdx.x * kFinCh, s1, s2)) return;
   const float is = invstd[c];
   if (dgamma) dgamma[c] = f32_to_bf16((float)(s2 * is));
   if (dbeta) dbeta[c] = f32_to_bf16((float)s1);
@@ -309,7 +337,7 @@ hipError_t launch_bn_fwd(const BnFwdArgs& a, hipStream_t st) {
   reduce_grid(a.M, a.C, gx, gy);
   if (a.training) {
     hipLaunchKernelGGL(bn_fwd_reduce_kernel, dim3(gx, gy), dim3(256), 0, st, a.x, a.M, a.C, a.running_mean, a.part);
-    hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((a.C + 255) / 256), dim3(256), 0, st, a.part, gx, a.M, a.C,
+    hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((a.C + kFinCh - 1) / kFinCh), dim3(256), 0, st, a.part, gx, a.M, a.C,
                        a.running_mean, a.gamma, a.beta, a.running_mean, a.running_var, a.momentum, a.eps, a.save_mean,
                        a.save_invstd, a.ss, a.counter);
   }
@@ -337,7 +365,7 @@ hipError_t launch_bn_bwd(const BnBwdArgs& a, hipStream_t st) {
   else if (a.dr) PSD_RED(false, true);
   else PSD_RED(false, false);
 #undef PSD_RED
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((a.C + 255) / 256), dim3(256), 0, st, a.part, gx, a.M, a.C, a.gamma,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((a.C + kFinCh - 1) / kFinCh), dim3(256), 0, st, a.part, gx, a.M, a.C, a.gamma,
                      a.save_mean, a.save_invstd, a.dgamma, a.dbeta, a.coef);
   const int64_t nvec = a.M * (a.C / 8);
   const int g = elem_grid(nvec, a.C);

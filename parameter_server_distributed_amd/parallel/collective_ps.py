@@ -193,7 +193,11 @@ class CollectivePS:
 
     def _sink(self, p):
         """Flat-gradient view a fused op may write ``p``'s gradient into (or None)."""
-        return self._grad_views.get(id(p)) if id(p) in self._direct else None
+        if id(p) not in self._direct:
+            return None
+        v = self._grad_views[id(p)]
+        # a fresh view (refcount 1) so autograd's AccumulateGrad adopts it instead of cloning
+        return v.view(v.shape)
 
     def memory_bytes(self) -> dict:
         eb = lambda t: 0 if t is None else t.numel() * t.element_size()  # noqa: E731
