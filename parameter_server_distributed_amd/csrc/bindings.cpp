@@ -133,7 +133,8 @@ PYBIND11_MODULE(_C, m) {
       .def("push", &PSCore::push, py::call_guard<py::gil_scoped_release>())
       .def("pull", &PSCore::pull, py::call_guard<py::gil_scoped_release>())
       .def("sync_status", &PSCore::sync_status)
-      .def("set_total_workers", &PSCore::set_total_workers)
+      .def("set_total_workers", &PSCore::set_total_workers, py::call_guard<py::gil_scoped_release>())
+      .def("forget_worker", &PSCore::forget_worker)
       .def("total_workers", &PSCore::total_workers)
       .def("current_iteration", &PSCore::current_iteration)
       .def("version", &PSCore::version)

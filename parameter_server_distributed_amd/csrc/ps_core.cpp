@@ -261,20 +261,25 @@ std::tuple<bool, int32_t, int32_t> PSCore::sync_status(int32_t iteration) const 
   return {it->second.aggregated, recv, cfg_.total_workers};
 }
 
-std::tuple<bool, int32_t, int64_t, at::Tensor> PSCore::pull(int32_t wid, int32_t iteration, bool wait) {
+std::tuple<bool, int32_t, int64_t, at::Tensor> PSCore::pull(int32_t wid, int32_t iteration, double wait_s) {
   std::unique_lock<std::mutex> lk(mu_);
+  if (!init_ && wait_s > 0) cv_.wait_for(lk, std::chrono::duration<double>(wait_s), [&] { return init_; });
   if (!init_) return {false, current_iteration_, version_, at::Tensor()};
   bool ready = true;
   if (cfg_.async_mode) {
     if (cfg_.staleness_bound >= 0) {
       auto ok = [&] { return iteration - min_clock_locked() <= cfg_.staleness_bound; };
-      if (wait) cv_.wait_for(lk, std::chrono::duration<double>(cfg_.pull_timeout_s), ok);
+      if (wait_s > 0) cv_.wait_for(lk, std::chrono::duration<double>(wait_s), ok);
       ready = ok();
       if (!ready) ctr_["bound_timeouts"] += 1;
     }
   } else {
-    auto it = iters_.find(iteration);
-    ready = it != iters_.end() && it->second.aggregated;
+    auto agg = [&] {
+      auto it = iters_.find(iteration);
+      return (it != iters_.end() && it->second.aggregated) || iteration < current_iteration_ - cfg_.window;
+    };
+    if (wait_s > 0) cv_.wait_for(lk, std::chrono::duration<double>(wait_s), agg);
+    ready = agg();
   }
   pulled_version_[wid] = version_;
   ctr_["pulls"] += 1;
@@ -286,7 +291,28 @@ void PSCore::set_total_workers(int32_t n) {
   TORCH_CHECK(n >= 1, "psd: total_workers must be >= 1");
   std::lock_guard<std::mutex> g(mu_);
   cfg_.total_workers = n;
-  // drop clocks of workers that no longer exist is handled by the runtime (it knows ids);
+  ctr_["membership_changes"] += 1;
+  // A pending sync iteration that already holds >= n pushes completes now (a worker left).
+  for (auto& kv : iters_) {
+    IterState& st = kv.second;
+    if (!st.aggregated && (int32_t)st.slot_of.size() >= n && !st.slot_of.empty()) {
+      std::vector<at::Tensor> srcs;
+      for (auto& w : st.slot_of) srcs.push_back(slots_[w.second]);
+      apply_locked(srcs, cfg_.reference_compat ? 1.0 : cfg_.lr, 1.0 / (double)st.slot_of.size());
+      for (auto& w : st.slot_of) free_slots_.push_back(w.second);
+      st.slot_of.clear();
+      st.aggregated = true;
+      ++version_;
+      hist_[0] += 1;
+    }
+  }
+  cv_.notify_all();
+}
+
+void PSCore::forget_worker(int32_t wid) {
+  std::lock_guard<std::mutex> g(mu_);
+  clock_.erase(wid);
+  pulled_version_.erase(wid);
   cv_.notify_all();
 }
 

@@ -68,12 +68,15 @@ class PSCore {
 
   PushResult push(int32_t worker_id, int32_t iteration, const std::vector<std::string>& names,
                   const std::vector<at::Tensor>& grads, int64_t pulled_version);
-  // returns (ready, iteration, version, flat fp32 params on CPU; empty if uninitialised)
-  std::tuple<bool, int32_t, int64_t, at::Tensor> pull(int32_t worker_id, int32_t iteration, bool wait);
+  // returns (ready, iteration, version, flat fp32 params on CPU; empty if uninitialised).
+  // wait_s > 0: sync mode blocks until `iteration` is aggregated, async mode until the staleness
+  // bound admits the worker (at most wait_s seconds either way).
+  std::tuple<bool, int32_t, int64_t, at::Tensor> pull(int32_t worker_id, int32_t iteration, double wait_s);
   // returns (ready, workers_received, total_workers)
   std::tuple<bool, int32_t, int32_t> sync_status(int32_t iteration) const;
 
   void set_total_workers(int32_t n);
+  void forget_worker(int32_t worker_id);  // elastic leave: drop its SSP clock
   int32_t total_workers() const;
   int32_t current_iteration() const;
   int64_t version() const;

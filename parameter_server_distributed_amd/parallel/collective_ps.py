@@ -306,7 +306,11 @@ class CollectivePS:
             s1 = None if self.state1 is None else self.state1.narrow(0, lo, b.slice_numel)
             s2 = None if self.state2 is None else self.state2.narrow(0, lo, b.slice_numel)
             shadow = self.params_flat.narrow(0, b.offset + k * b.slice_numel, b.slice_numel)
-            apply_no_advance_(self.cfg, self.dyn, m, gv, s1, s2, shadow)
+            if self.param_dtype == torch.bfloat16:  # the kernel writes the bf16 working copy itself
+                apply_no_advance_(self.cfg, self.dyn, m, gv, s1, s2, shadow)
+            else:  # fp32 working copy (CPU / fp32 runs): publish the master slice
+                apply_no_advance_(self.cfg, self.dyn, m, gv, s1, s2, None)
+                shadow.copy_(m)
 
     def _pull(self, b: Bucket):
         w = self.params_flat.narrow(0, b.offset, b.numel)
