@@ -38,7 +38,14 @@ from parameter_server_distributed_amd.parallel.collective_ps import CollectivePS
 from parameter_server_distributed_amd.parallel.transport import make_transport  # noqa: E402
 from parameter_server_distributed_amd.runtime.trainer import Trainer  # noqa: E402
 
-METRIC = "samples/sec (whole node) ResNet-50 async-SGD"
+METRICS = {
+    "resnet50": ("samples/sec (whole node) ResNet-50 async-SGD", "samples/s"),
+    "bert_base": ("sequences/sec (whole node) BERT-base Adam", "sequences/s"),
+    "wide_resnet101_2": ("samples/sec (whole node) Wide-ResNet-101-2 fp8-weights", "samples/s"),
+    "resnet101": ("samples/sec (whole node) ResNet-101", "samples/s"),
+    "mlp": ("samples/sec (whole node) 2-layer MLP", "samples/s"),
+}
+DEFAULT_BATCH = {"resnet50": 256, "bert_base": 64, "wide_resnet101_2": 128, "resnet101": 256, "mlp": 4096}
 
 
 def parse():
@@ -47,12 +54,16 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--model", default="resnet50")
-    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (0: model default)")
     ap.add_argument("--image-size", type=int, default=224)
+    ap.add_argument("--seq-len", type=int, default=128)
     ap.add_argument("--ps-shards", type=int, default=2)
+    ap.add_argument("--placement", default="colocated", choices=["colocated", "disjoint"],
+                    help="disjoint: first half of the ranks are workers, second half PS shards")
     ap.add_argument("--staleness", type=int, default=1)
     ap.add_argument("--bucket-mb", type=float, default=16.0)
-    ap.add_argument("--lr", type=float, default=0.1)
+    ap.add_argument("--optimizer", default="", help="momentum|adam|adamw (default: momentum; adamw for BERT)")
+    ap.add_argument("--lr", type=float, default=0.0)
     ap.add_argument("--graph", type=int, default=-1, help="hipGraph capture (1/0; -1: on for 1 GPU)")
     ap.add_argument("--transport", default="auto", choices=["auto", "torch", "rccl"])
     ap.add_argument("--benchmark-miopen", type=int, default=1, help="torch.backends.cudnn.benchmark")
@@ -76,11 +87,22 @@ def main():
     torch.backends.cudnn.benchmark = bool(a.benchmark_miopen)
     torch.manual_seed(1234)  # identical init on every rank; the PS init pull makes it exact
 
-    spec = models.build(a.model, dev, torch.bfloat16, image_size=a.image_size)
+    a.model = a.model.lower().replace("-", "_")
+    a.batch = a.batch or DEFAULT_BATCH.get(a.model, 64)
+    spec = models.build(a.model, dev, torch.bfloat16, image_size=a.image_size, seq_len=a.seq_len)
     transport = make_transport(a.transport, dev)
-    shards = max(1, min(a.ps_shards, world))
-    ps = CollectivePS(spec.model, OptimConfig("momentum", lr=a.lr, momentum=0.9, weight_decay=5e-5), transport,
-                      num_shards=shards, staleness=a.staleness, bucket_mb=a.bucket_mb, device=dev)
+    opt_kind = a.optimizer or ("adamw" if a.model.startswith("bert") else "momentum")
+    lr = a.lr or (1e-4 if opt_kind.startswith("adam") else 0.1)
+    optim = OptimConfig(opt_kind, lr=lr, momentum=0.9, weight_decay=0.01 if opt_kind == "adamw" else 5e-5)
+    kw = {}
+    if a.placement == "disjoint" and world >= 2:
+        kw = dict(worker_ranks=list(range(world // 2)), ps_ranks=list(range(world // 2, world)))
+        shards = world - world // 2
+    else:
+        shards = max(1, min(a.ps_shards, world))
+    ps = CollectivePS(spec.model, optim, transport, num_shards=shards, staleness=a.staleness, bucket_mb=a.bucket_mb,
+                      device=dev, overlap=not spec.tied_weights, **kw)
+    n_workers = len(ps.worker_ranks)
     batch = spec.make_batch(a.batch, dev, seed=rank)
     use_graph = (world == 1) if a.graph < 0 else bool(a.graph)
     tr = Trainer(spec.model, spec.loss, ps, batch, use_graph=use_graph)
@@ -110,7 +132,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     ms = el / max(a.steps, 1) * 1e3
-    samples = a.batch * world * a.steps
+    samples = a.batch * n_workers * a.steps
     value = samples / el
     hist = ps.staleness_histogram()
     if world > 1:
@@ -128,15 +150,20 @@ def main():
         hist.pop()
     final_loss = float(loss.float().item()) if loss is not None else float("nan")
     if rank == 0:
+        metric, unit = METRICS.get(a.model, (f"samples/sec (whole node) {a.model}", "samples/s"))
+        data = ("synthetic (random token ids, 15% MLM labels, random init)" if a.model.startswith("bert") else
+                "synthetic (random ImageNet-shaped 224x224, random init)")
         rec = {
-            "metric": METRIC, "value": round(value, 2), "unit": "samples/s", "n_gpus": world, "steps": a.steps,
+            "metric": metric, "value": round(value, 2), "unit": unit, "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random ImageNet-shaped 224x224, random init)",
-            "config": {"model": a.model, "global_batch": a.batch * world, "per_gpu_batch": a.batch, "seq_len": None,
-                       "image_size": a.image_size,
-                       "parallelism": f"ps{shards}-async-s{a.staleness}-dp{world}",
-                       "ps_shards": shards, "ps_owner_ranks": ps.owners, "staleness_bound": a.staleness,
-                       "optimizer": "sgd-momentum(0.9) fused gfx950", "bucket_mb": a.bucket_mb,
+            "vs_baseline": None, "dtype": "bf16", "data": data,
+            "config": {"model": a.model, "global_batch": a.batch * n_workers, "per_gpu_batch": a.batch,
+                       "seq_len": a.seq_len if a.model.startswith("bert") else None,
+                       "image_size": None if a.model.startswith("bert") else a.image_size,
+                       "parallelism": f"ps{shards}-{'async' if a.staleness else 'sync'}-s{a.staleness}-dp{n_workers}"
+                                      + ("-disjoint" if kw else ""),
+                       "ps_shards": shards, "ps_owner_ranks": ps.owners, "worker_ranks": ps.worker_ranks,
+                       "staleness_bound": a.staleness, "optimizer": f"{opt_kind} fused gfx950", "bucket_mb": a.bucket_mb,
                        "transport": transport.name, "hipgraph": bool(tr.graphs), "graph_error": tr.graph_error},
             "staleness_p50": p50, "staleness_hist": hist, "final_loss": round(final_loss, 4),
             "warmup_s": round(t_w, 2), "peak_mem_gb": round(mem_peak / 2**30, 2),

@@ -1,0 +1,103 @@
+// Tensor glue for the MFMA GEMM (kernels/gemm.hip).
+#include <ATen/ATen.h>
+#include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPStream.h>
+
+#include "kernels/launchers_gemm.h"
+
+namespace psd {
+
+namespace {
+inline hipStream_t stream_of(const at::Tensor& t) { return c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
+void chk2d(const at::Tensor& t, const char* n) {
+  TORCH_CHECK(t.is_cuda() && t.dim() == 2 && t.scalar_type() == at::kBFloat16 && t.stride(1) == 1 &&
+                  t.stride(0) % 8 == 0 && (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0,
+              "psd gemm: ", n, " must be a 2-D bf16 device tensor, unit inner stride, 16-B aligned rows");
+}
+}  // namespace
+
+// out[M,N] = A op B (+bias)(act). A: a_kmajor ? [M,K] : [K,M]; B: b_kmajor ? [N,K] : [K,N].
+void gemm_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool b_kmajor, at::Tensor out,
+           c10::optional<at::Tensor> bias, int64_t act, c10::optional<at::Tensor> aux) {
+  chk2d(A, "A");
+  chk2d(B, "B");
+  const int64_t M = a_kmajor ? A.size(0) : A.size(1), K = a_kmajor ? A.size(1) : A.size(0);
+  const int64_t N = b_kmajor ? B.size(0) : B.size(1), K2 = b_kmajor ? B.size(1) : B.size(0);
+  TORCH_CHECK(K == K2, "psd gemm: K mismatch ", K, " vs ", K2);
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == M && out.size(1) == N && out.stride(1) == 1, "psd gemm: out shape");
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat, "psd gemm: out dtype");
+  TORCH_CHECK(K % 8 == 0 || !(a_kmajor && b_kmajor), "psd gemm: K must be a multiple of 8 for K-major operands");
+  TORCH_CHECK(a_kmajor || M % 8 == 0, "psd gemm: M must be a multiple of 8 for an M-major A");
+  TORCH_CHECK(b_kmajor || N % 8 == 0, "psd gemm: N must be a multiple of 8 for an N-major B");
+  TORCH_CHECK(!(a_kmajor ^ b_kmajor) || K % 8 == 0, "psd gemm: K must be a multiple of 8");
+  const c10::DeviceGuard g(A.device());
+  GemmArgs a{};
+  a.A = A.data_ptr();
+  a.B = B.data_ptr();
+  a.C = out.data_ptr();
+  a.bias = (bias.has_value() && bias->defined()) ? bias->data_ptr() : nullptr;
+  if (a.bias) TORCH_CHECK(bias->numel() == N && bias->scalar_type() == at::kBFloat16, "psd gemm: bias [N] bf16");
+  a.aux = (aux.has_value() && aux->defined()) ? aux->data_ptr() : nullptr;
+  a.M = (int)M;
+  a.N = (int)N;
+  a.K = (int)K;
+  a.lda = (int)A.stride(0);
+  a.ldb = (int)B.stride(0);
+  a.ldc = (int)out.stride(0);
+  a.a_kmajor = a_kmajor;
+  a.b_kmajor = b_kmajor;
+  a.act = (int)act;
+  a.c_f32 = out.scalar_type() == at::kFloat;
+  hipError_t e = launch_gemm(a, stream_of(A));
+  TORCH_CHECK(e == hipSuccess, "psd gemm: ", hipGetErrorString(e));
+}
+
+// out[M,N] (+)= scale * (A op B) via split-K fp32 slabs (weight gradients: K = tokens).
+void gemm_splitk_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool b_kmajor, at::Tensor out,
+                  bool accumulate, double scale, int64_t splits) {
+  chk2d(A, "A");
+  chk2d(B, "B");
+  const int64_t M = a_kmajor ? A.size(0) : A.size(1), K = a_kmajor ? A.size(1) : A.size(0);
+  const int64_t N = b_kmajor ? B.size(0) : B.size(1), K2 = b_kmajor ? B.size(1) : B.size(0);
+  TORCH_CHECK(K == K2, "psd gemm_splitk: K mismatch");
+  TORCH_CHECK(out.is_contiguous() && out.numel() == M * N, "psd gemm_splitk: out must be contiguous [M,N]");
+  TORCH_CHECK(a_kmajor || M % 8 == 0, "psd gemm_splitk: M % 8");
+  TORCH_CHECK(b_kmajor || N % 8 == 0, "psd gemm_splitk: N % 8");
+  const c10::DeviceGuard g(A.device());
+  const int s = splits > 0 ? (int)splits : gemm_splits((int)M, (int)N, (int)K);
+  at::Tensor slab = at::empty({(int64_t)s * M * N}, A.options().dtype(at::kFloat));
+  GemmArgs a{};
+  a.A = A.data_ptr();
+  a.B = B.data_ptr();
+  a.M = (int)M;
+  a.N = (int)N;
+  a.K = (int)K;
+  a.lda = (int)A.stride(0);
+  a.ldb = (int)B.stride(0);
+  a.ldc = (int)N;
+  a.a_kmajor = a_kmajor;
+  a.b_kmajor = b_kmajor;
+  hipError_t e = launch_gemm_splitk(a, slab.data_ptr<float>(), s, out.data_ptr(), out.scalar_type() == at::kBFloat16,
+                                    accumulate, (float)scale, stream_of(A));
+  TORCH_CHECK(e == hipSuccess, "psd gemm_splitk: ", hipGetErrorString(e));
+}
+
+// out[N] (+)= column sums of x[M,N] (bias gradient)
+void colsum_(const at::Tensor& x, at::Tensor out, bool accumulate) {
+  chk2d(x, "x");
+  const int64_t M = x.size(0), N = x.size(1);
+  TORCH_CHECK(N % 8 == 0 && x.is_contiguous(), "psd colsum: N % 8 and contiguous");
+  TORCH_CHECK(out.numel() == N && out.is_contiguous(), "psd colsum: out [N]");
+  const c10::DeviceGuard g(x.device());
+  at::Tensor part = at::zeros({N}, x.options().dtype(at::kFloat));
+  const bool bf = out.scalar_type() == at::kBFloat16;
+  hipError_t e = launch_colsum(reinterpret_cast<const uint16_t*>(x.data_ptr()), M, (int)N, part.data_ptr<float>(),
+                               out.data_ptr(), bf, accumulate, stream_of(x));
+  TORCH_CHECK(e == hipSuccess, "psd colsum: ", hipGetErrorString(e));
+  if (!bf) {
+    if (accumulate) out.add_(part);
+    else out.copy_(part);
+  }
+}
+
+}  // namespace psd

@@ -1,0 +1,31 @@
+// Launch API of the MFMA bf16 GEMM (gemm.hip).
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <cstdint>
+
+namespace psd {
+
+struct GemmArgs {
+  const void* A;     // bf16; a_kmajor ? [M][lda] : [K][lda]
+  const void* B;     // bf16; b_kmajor ? [N][ldb] : [K][ldb]
+  void* C;           // [M][ldc] bf16 (or fp32 if c_f32); split-K: fp32 slabs
+  const void* bias;  // bf16 [N] or null
+  void* aux;         // GELU pre-activation out [M][ldc] bf16 or null
+  int M, N, K;
+  int lda, ldb, ldc;
+  int a_kmajor, b_kmajor;
+  int act;           // 0 none, 1 relu, 2 gelu(tanh)
+  int c_f32;
+  int k_per_split;
+};
+
+hipError_t launch_gemm(const GemmArgs& g, hipStream_t stream);
+int gemm_splits(int M, int N, int K);
+// split-K GEMM into fp32 slabs [splits][M][N], then out = (acc ? out : 0) + scale * sum(slabs)
+hipError_t launch_gemm_splitk(const GemmArgs& g, float* slab, int splits, void* out, int out_bf16, int accumulate,
+                              float scale, hipStream_t stream);
+// out[n] (+)= sum_m x[m][n]; part_zeroed is an fp32 [N] scratch (zeroed by the caller)
+hipError_t launch_colsum(const uint16_t* x, int64_t M, int N, float* part_zeroed, void* out, int out_bf16,
+                         int accumulate, hipStream_t stream);
+
+}  // namespace psd

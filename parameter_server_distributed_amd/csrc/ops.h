@@ -24,4 +24,10 @@ std::vector<at::Tensor> bn_bwd(const at::Tensor& dy, const at::Tensor& x, c10::o
                                const at::Tensor& save_invstd, bool relu, bool need_dr,
                                c10::optional<at::Tensor> dgamma_out, c10::optional<at::Tensor> dbeta_out);
 
+void gemm_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool b_kmajor, at::Tensor out,
+           c10::optional<at::Tensor> bias, int64_t act, c10::optional<at::Tensor> aux);
+void gemm_splitk_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool b_kmajor, at::Tensor out,
+                  bool accumulate, double scale, int64_t splits);
+void colsum_(const at::Tensor& x, at::Tensor out, bool accumulate);
+
 }  // namespace psd

@@ -1,0 +1,87 @@
+"""BERT-base (12 layers, hidden 768, 12 heads, FFN 3072) with the masked-LM head, for BASELINE.json
+config 4 (BERT-base with the Adam update kernel). Random init, synthetic token batches.
+
+Every Linear is an ``MfmaLinear`` (hand-written gfx950 MFMA GEMM forward + both backward GEMMs,
+bias/GELU fused); attention is ``F.scaled_dot_product_attention`` (ROCm flash attention).
+Deviations from the original BERT, both standard in large-scale training and stated here: the
+vocabulary is padded to 30528 (a multiple of 64, for the GEMM tiles) and the MLM decoder weight is
+untied from the word embedding (the PS data plane overlaps each bucket's update with the rest of
+backward, which requires every weight to be consumed by exactly one autograd node).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops.linear import MfmaLinear
+
+VOCAB = 30528
+
+
+class BertLayer(nn.Module):
+    def __init__(self, hidden=768, heads=12, ffn=3072, dropout=0.1):
+        super().__init__()
+        self.heads = heads
+        self.qkv = MfmaLinear(hidden, 3 * hidden)
+        self.proj = MfmaLinear(hidden, hidden)
+        self.ln1 = nn.LayerNorm(hidden, eps=1e-12)
+        self.ffn1 = MfmaLinear(hidden, ffn, act="gelu")
+        self.ffn2 = MfmaLinear(ffn, hidden)
+        self.ln2 = nn.LayerNorm(hidden, eps=1e-12)
+        self.p = dropout
+
+    def forward(self, x):
+        B, S, H = x.shape
+        q, k, v = self.qkv(x).view(B, S, 3, self.heads, H // self.heads).permute(2, 0, 3, 1, 4).unbind(0)
+        a = F.scaled_dot_product_attention(q, k, v, dropout_p=self.p if self.training else 0.0)
+        a = a.transpose(1, 2).reshape(B, S, H)
+        x = self.ln1(x + F.dropout(self.proj(a), self.p, self.training))
+        return self.ln2(x + F.dropout(self.ffn2(self.ffn1(x)), self.p, self.training))
+
+
+class BertForMLM(nn.Module):
+    def __init__(self, layers=12, hidden=768, heads=12, vocab=VOCAB, max_pos=512, dropout=0.1):
+        super().__init__()
+        self.vocab = vocab
+        self.word = nn.Embedding(vocab, hidden)
+        self.pos = nn.Embedding(max_pos, hidden)
+        self.tok_type = nn.Embedding(2, hidden)
+        self.ln = nn.LayerNorm(hidden, eps=1e-12)
+        self.layers = nn.ModuleList([BertLayer(hidden, heads, 4 * hidden, dropout) for _ in range(layers)])
+        self.head = MfmaLinear(hidden, hidden, act="gelu")
+        self.head_ln = nn.LayerNorm(hidden, eps=1e-12)
+        self.decoder = MfmaLinear(hidden, vocab)
+        self.p = dropout
+        for m in self.modules():
+            if isinstance(m, nn.Linear):
+                nn.init.normal_(m.weight, std=0.02)
+                nn.init.zeros_(m.bias)
+            elif isinstance(m, nn.Embedding):
+                nn.init.normal_(m.weight, std=0.02)
+
+    def forward(self, batch):
+        ids, types = batch
+        S = ids.shape[1]
+        pos = torch.arange(S, device=ids.device)
+        x = self.word(ids) + self.pos(pos)[None] + self.tok_type(types)
+        x = F.dropout(self.ln(x), self.p, self.training)
+        for layer in self.layers:
+            x = layer(x)
+        return self.decoder(self.head_ln(self.head(x)))
+
+    @staticmethod
+    def loss(logits, labels):
+        return F.cross_entropy(logits.float().view(-1, logits.shape[-1]), labels.view(-1), ignore_index=-100)
+
+
+def bert_batch(batch: int, seq: int, vocab: int, device, seed: int = 0, mask_prob: float = 0.15):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    ids = torch.randint(0, vocab, (batch, seq), generator=g)
+    types = (torch.arange(seq)[None, :] >= seq // 2).long().expand(batch, seq).contiguous()
+    labels = torch.full((batch, seq), -100, dtype=torch.long)
+    m = torch.rand(batch, seq, generator=g) < mask_prob
+    labels[m] = ids[m]
+    return (ids.to(device), types.to(device)), labels.to(device)

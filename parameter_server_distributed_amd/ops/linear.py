@@ -1,0 +1,94 @@
+"""Linear layer on the hand-written MFMA GEMM (csrc/kernels/gemm.hip).
+
+forward   y  = act(x W^T + b)     NT GEMM, bias + ReLU/GELU fused in the epilogue (GELU keeps the
+                                  pre-activation for backward)
+backward  dx = dy' W              NN GEMM (W read N-major through ds_read_b64_tr_b16: no transpose)
+          dW = dy'^T x            TN split-K GEMM, reduced straight into the PS flat-gradient
+                                  buffer when the data plane installed a grad sink
+          db = colsum(dy')        column-sum kernel (also into the sink)
+
+CPU tensors (and non-bf16 / unaligned shapes) use ``F.linear`` -- the reference the tests compare
+against.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import native
+
+ACTS = {None: 0, "none": 0, "relu": 1, "gelu": 2}
+
+
+def _ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    return (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.shape[0] % 8 == 0
+            and w.shape[1] % 8 == 0)
+
+
+class _LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, mod):
+        C = native()
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1]).contiguous()
+        M, N = x2.shape[0], weight.shape[0]
+        y = torch.empty(M, N, dtype=x.dtype, device=x.device)
+        act = ACTS[mod.act]
+        aux = torch.empty_like(y) if act == 2 else None
+        C.gemm_(x2, weight, True, True, y, bias, act, aux)
+        ctx.act = act
+        ctx.mod = mod
+        ctx.has_bias = bias is not None
+        ctx.in_shape = shp
+        ctx.save_for_backward(x2, weight, y if act == 1 else aux)
+        return y.view(*shp[:-1], N)
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = native()
+        x2, w, keep = ctx.saved_tensors
+        dy2 = dy.reshape(-1, w.shape[0]).contiguous()
+        if ctx.act == 1:
+            dy2 = dy2 * (keep > 0)
+        elif ctx.act == 2:
+            dy2 = torch.ops.aten.gelu_backward(dy2, keep, approximate="tanh")
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(x2.shape, dtype=dy2.dtype, device=dy2.device)
+            C.gemm_(dy2, w, True, False, dx)
+            dx = dx.view(ctx.in_shape)
+        sink = getattr(ctx.mod, "_psd_grad_sink", None)
+        dw = db = None
+        if ctx.needs_input_grad[1]:
+            dw = sink(ctx.mod.weight) if sink is not None else None
+            if dw is None:
+                dw = torch.empty(w.shape, dtype=w.dtype, device=w.device)
+            C.gemm_splitk_(dy2, x2, False, False, dw, False, 1.0, 0)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = sink(ctx.mod.bias) if sink is not None else None
+            if db is None:
+                db = torch.empty(w.shape[0], dtype=w.dtype, device=w.device)
+            C.colsum_(dy2, db, False)
+        return dx, dw, db, None
+
+
+class MfmaLinear(nn.Linear):
+    """``nn.Linear`` (+ fused activation) running on the gfx950 MFMA GEMM for bf16 device tensors."""
+
+    def __init__(self, in_features, out_features, bias=True, act=None, device=None, dtype=None):
+        super().__init__(in_features, out_features, bias=bias, device=device, dtype=dtype)
+        self.act = act
+
+    def psd_direct_grad_params(self):
+        return [p for p in (self.weight, self.bias) if p is not None]
+
+    def forward(self, x):
+        if _ok(x, self.weight):
+            return _LinearFn.apply(x, self.weight, self.bias, self)
+        y = F.linear(x, self.weight.to(x.dtype), None if self.bias is None else self.bias.to(x.dtype))
+        if self.act == "relu":
+            y = F.relu(y)
+        elif self.act == "gelu":
+            y = F.gelu(y, approximate="tanh")
+        return y

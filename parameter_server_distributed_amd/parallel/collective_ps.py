@@ -72,18 +72,30 @@ class CollectivePS:
     def __init__(self, model: nn.Module, optim: OptimConfig, transport: Transport | None = None,
                  num_shards: int | None = None, staleness: int = 0, bucket_mb: float = 16.0,
                  overlap: bool = True, grad_dtype: torch.dtype = torch.bfloat16,
-                 param_dtype: torch.dtype = torch.bfloat16, device: torch.device | None = None):
+                 param_dtype: torch.dtype = torch.bfloat16, device: torch.device | None = None,
+                 ps_ranks: list[int] | None = None, worker_ranks: list[int] | None = None):
         self.model = model
         self.cfg = optim
         self.t = transport or LocalTransport()
         self.world, self.rank = self.t.world, self.t.rank
-        self.P = num_shards or self.world
-        if not 1 <= self.P <= self.world:
-            raise ValueError(f"num_shards must be in [1, world={self.world}], got {self.P}")
-        # PS shard k lives on rank owners[k]: spread evenly over the node (2 of 8 -> ranks 0 and 4)
-        self.owners = [k * self.world // self.P for k in range(self.P)]
+        # placement: by default every rank is a worker and the P shards are spread evenly over the
+        # node (2 of 8 -> ranks 0 and 4); ps_ranks / worker_ranks give disjoint placements
+        # (e.g. 4 PS GPUs + 4 worker GPUs). Non-worker ranks run idle_step(): they take part in the
+        # collectives with zero gradients and apply/publish their shards.
+        self.worker_ranks = list(worker_ranks) if worker_ranks is not None else list(range(self.world))
+        self.is_worker = self.rank in self.worker_ranks
+        if ps_ranks is not None:
+            self.owners = list(ps_ranks)
+            self.P = len(self.owners)
+        else:
+            self.P = num_shards or self.world
+            if not 1 <= self.P <= self.world:
+                raise ValueError(f"num_shards must be in [1, world={self.world}], got {self.P}")
+            self.owners = [k * self.world // self.P for k in range(self.P)]
+        if not self.owners or any(not 0 <= r < self.world for r in self.owners) or len(set(self.owners)) != self.P:
+            raise ValueError(f"invalid PS ranks {self.owners} for world {self.world}")
         self.my_shards = [k for k, r in enumerate(self.owners) if r == self.rank]
-        self.collective_rs = self.P == self.world  # owners == range(world)
+        self.collective_rs = self.owners == list(range(self.world))  # every rank owns its slice
         self.S = int(staleness)
         self.overlap = overlap
         self.device = device or next(model.parameters()).device
@@ -146,7 +158,7 @@ class CollectivePS:
         # (S = 0 reduces in place inside the gradient buffer and needs none)
         self.slots = [torch.zeros(max(self.local_total, ALIGN), dtype=grad_dtype, device=dev)
                       for _ in range(self.S + 1)] if self.S > 0 else []
-        self.dyn = OptimDyn(dev, lr=optim.lr, grad_scale=1.0 / self.world)
+        self.dyn = OptimDyn(dev, lr=optim.lr, grad_scale=1.0 / len(self.worker_ranks))
 
         # Modules that can write their parameter gradients straight into our flat buffer (fused BN)
         # get a grad sink; their params keep .grad = None so autograd adopts the written view
@@ -230,6 +242,11 @@ class CollectivePS:
             for k in self.my_shards:
                 self.tracker.on_apply((t - self.S) % (self.S + 1), k)
         self.step_idx += 1
+
+    def idle_step(self):
+        """A PS-only rank's step: zero contribution to the push, apply + publish its shards."""
+        self.begin_step()
+        self.finish_step()
 
     def _on_grad(self, p):
         if id(p) in self._direct:

@@ -35,6 +35,10 @@ class Trainer:
 
     # eager step ---------------------------------------------------------------
     def _body(self):
+        if not self.ps.is_worker:  # disjoint placement: PS-only rank
+            self.ps.begin_step()
+            self.ps.finish_step()
+            return torch.zeros((), device=self.ps.device)
         self.ps.begin_step()
         out = self.model(self.x)
         loss = self.loss_fn(out, self.y)
@@ -69,6 +73,10 @@ class Trainer:
         # identical device work to _body, but the host bookkeeping (tracker, step counter) is done
         # per replay by `step()`, not at capture time
         ps = self.ps
+        if not ps.is_worker:
+            ps.begin_step(track=False)
+            ps.finish_step(track=False)
+            return torch.zeros((), device=ps.device)
         ps.begin_step(track=False)
         out = self.model(self.x)
         loss = self.loss_fn(out, self.y)

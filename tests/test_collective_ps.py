@@ -25,13 +25,16 @@ def _port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, shards, stale, out):
+def _worker(rank, world, port, shards, stale, out, disjoint=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.manual_seed(0)
     spec = models.build("mlp", torch.device("cpu"), torch.float32, hidden=64)
+    kw = {}
+    if disjoint:  # first half workers, second half PS shards
+        kw = dict(worker_ranks=list(range(world // 2)), ps_ranks=list(range(world // 2, world)))
     ps = CollectivePS(spec.model, OptimConfig(**CFG), TorchDistTransport(), num_shards=shards, staleness=stale,
-                      bucket_mb=0.0005, grad_dtype=torch.float32, param_dtype=torch.float32)
+                      bucket_mb=0.0005, grad_dtype=torch.float32, param_dtype=torch.float32, **kw)
     assert len(ps.buckets) > 1
     tr = Trainer(spec.model, spec.loss, ps, spec.make_batch(16, torch.device("cpu"), seed=rank))
     for _ in range(STEPS):
@@ -83,6 +86,18 @@ def test_gloo_world2_matches_reference(tmp_path, shards, stale):
         assert sum(hist) == applied
         if stale and applied > stale:
             assert hist[stale] >= 1
+
+
+@pytest.mark.slow
+def test_gloo_disjoint_placement_2_workers_2_ps(tmp_path):
+    """BASELINE config 4 layout in miniature: PS shards on ranks that do no compute."""
+    out = str(tmp_path / "r0.pt")
+    mp.spawn(_worker, args=(4, _port(), 2, 0, out, True), nprocs=4, join=True)
+    got = torch.load(out, weights_only=True)
+    want = _reference(2, 0)
+    for n in want:
+        torch.testing.assert_close(got["params"][n], want[n], rtol=1e-5, atol=1e-6, msg=n)
+    assert sum(got["hist"]) == 0  # rank 0 is a pure worker: it owns no shard
 
 
 def test_world1_local_matches_reference():
