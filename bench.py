@@ -62,11 +62,12 @@ def parse():
                     help="disjoint: first half of the ranks are workers, second half PS shards")
     ap.add_argument("--staleness", type=int, default=1)
     ap.add_argument("--bucket-mb", type=float, default=16.0)
+    ap.add_argument("--pull-dtype", default="", help="bf16|fp8 published-weight dtype (default: fp8 for WRN-101)")
     ap.add_argument("--optimizer", default="", help="momentum|adam|adamw (default: momentum; adamw for BERT)")
     ap.add_argument("--lr", type=float, default=0.0)
     ap.add_argument("--graph", type=int, default=-1, help="hipGraph capture (1/0; -1: on for 1 GPU)")
     ap.add_argument("--transport", default="auto", choices=["auto", "torch", "rccl"])
-    ap.add_argument("--benchmark-miopen", type=int, default=1, help="torch.backends.cudnn.benchmark")
+    ap.add_argument("--benchmark-miopen", type=int, default=0, help="torch.backends.cudnn.benchmark")
     ap.add_argument("--out", default="", help="also write the JSON line to this file")
     return ap.parse_args()
 
@@ -100,8 +101,9 @@ def main():
         shards = world - world // 2
     else:
         shards = max(1, min(a.ps_shards, world))
+    pull_dtype = a.pull_dtype or ("fp8" if a.model.startswith("wide") else "bf16")
     ps = CollectivePS(spec.model, optim, transport, num_shards=shards, staleness=a.staleness, bucket_mb=a.bucket_mb,
-                      device=dev, overlap=not spec.tied_weights, **kw)
+                      device=dev, overlap=not spec.tied_weights, pull_dtype=pull_dtype, **kw)
     n_workers = len(ps.worker_ranks)
     batch = spec.make_batch(a.batch, dev, seed=rank)
     use_graph = (world == 1) if a.graph < 0 else bool(a.graph)
@@ -164,6 +166,7 @@ def main():
                                       + ("-disjoint" if kw else ""),
                        "ps_shards": shards, "ps_owner_ranks": ps.owners, "worker_ranks": ps.worker_ranks,
                        "staleness_bound": a.staleness, "optimizer": f"{opt_kind} fused gfx950", "bucket_mb": a.bucket_mb,
+                       "pull_dtype": pull_dtype,
                        "transport": transport.name, "hipgraph": bool(tr.graphs), "graph_error": tr.graph_error},
             "staleness_p50": p50, "staleness_hist": hist, "final_loss": round(final_loss, 4),
             "warmup_s": round(t_w, 2), "peak_mem_gb": round(mem_peak / 2**30, 2),

@@ -6,6 +6,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import signal
 import sys
 import time
 
@@ -31,6 +32,13 @@ def main(argv=None):
     w = Worker(a.coordinator, a.worker_id, a.worker_addr, a.worker_port, model=a.model, batch=a.batch,
                device=a.device, heartbeat_s=a.heartbeat_s, bf16_wire=a.bf16_wire, mode=a.mode)
     w.initialize()
+
+    def _leave(signum, frame):  # scale_workers.sh down: deregister so the barrier shrinks at once
+        print(f"worker {a.worker_id} leaving (signal {signum})", flush=True)
+        w.shutdown(deregister=True)
+        sys.exit(0)
+
+    signal.signal(signal.SIGTERM, _leave)
     start = w.start_iteration
     if a.checkpoint_path:
         epoch, it = w.load_checkpoint_from_server(a.checkpoint_path)

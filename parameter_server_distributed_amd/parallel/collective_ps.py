@@ -73,7 +73,8 @@ class CollectivePS:
                  num_shards: int | None = None, staleness: int = 0, bucket_mb: float = 16.0,
                  overlap: bool = True, grad_dtype: torch.dtype = torch.bfloat16,
                  param_dtype: torch.dtype = torch.bfloat16, device: torch.device | None = None,
-                 ps_ranks: list[int] | None = None, worker_ranks: list[int] | None = None):
+                 ps_ranks: list[int] | None = None, worker_ranks: list[int] | None = None,
+                 pull_dtype: str = "bf16"):
         self.model = model
         self.cfg = optim
         self.t = transport or LocalTransport()
@@ -159,6 +160,16 @@ class CollectivePS:
         self.slots = [torch.zeros(max(self.local_total, ALIGN), dtype=grad_dtype, device=dev)
                       for _ in range(self.S + 1)] if self.S > 0 else []
         self.dyn = OptimDyn(dev, lr=optim.lr, grad_scale=1.0 / len(self.worker_ranks))
+        # fp8 pull (Wide-ResNet fp8-weights config): owners quantise their fp32 master slices to OCP
+        # e4m3fn with a per-(bucket, shard) amax scale; the all-gather moves 1 byte/param (half of
+        # bf16) and every rank dequantises into its bf16 working buffer.
+        if pull_dtype not in ("bf16", "fp8"):
+            raise ValueError(f"pull_dtype must be bf16 or fp8, got {pull_dtype}")
+        self.pull_fp8 = pull_dtype == "fp8" and param_dtype == torch.bfloat16
+        if self.pull_fp8:
+            self.p8 = torch.zeros(self.total, dtype=torch.float8_e4m3fn, device=dev)
+            self.p8_scale = torch.ones(len(buckets) * self.P, dtype=torch.float32, device=dev)
+            self.p8_amax = torch.zeros(len(buckets) * self.P, dtype=torch.float32, device=dev)
 
         # Modules that can write their parameter gradients straight into our flat buffer (fused BN)
         # get a grad sink; their params keep .grad = None so autograd adopts the written view
@@ -196,6 +207,13 @@ class CollectivePS:
     # ------------------------------------------------------------------ setup
     def _sync_init(self):
         """Make every rank start from the owners' master values (pull v0)."""
+        if self.pull_fp8:
+            for b in self.buckets:
+                for j, k in enumerate(self.my_shards):
+                    self._quant_slice(b, k, self.master.narrow(0, b.local_offset + j * b.slice_numel, b.slice_numel))
+            for b in self.buckets:
+                self._pull(b)
+            return
         if self.world == 1:
             return
         for b in self.buckets:
@@ -323,13 +341,44 @@ class CollectivePS:
             s1 = None if self.state1 is None else self.state1.narrow(0, lo, b.slice_numel)
             s2 = None if self.state2 is None else self.state2.narrow(0, lo, b.slice_numel)
             shadow = self.params_flat.narrow(0, b.offset + k * b.slice_numel, b.slice_numel)
-            if self.param_dtype == torch.bfloat16:  # the kernel writes the bf16 working copy itself
+            if self.pull_fp8:
+                apply_no_advance_(self.cfg, self.dyn, m, gv, s1, s2, None)
+                self._quant_slice(b, k, m)
+            elif self.param_dtype == torch.bfloat16:  # the kernel writes the bf16 working copy itself
                 apply_no_advance_(self.cfg, self.dyn, m, gv, s1, s2, shadow)
             else:  # fp32 working copy (CPU / fp32 runs): publish the master slice
                 apply_no_advance_(self.cfg, self.dyn, m, gv, s1, s2, None)
                 shadow.copy_(m)
 
+    def _quant_slice(self, b: Bucket, k: int, src: torch.Tensor):
+        C = native()
+        i = b.index * self.P + k
+        amax = self.p8_amax.narrow(0, i, 1)
+        amax.zero_()
+        C.amax_(src, amax)
+        C.quant_fp8_(src, amax, 448.0, self.p8.narrow(0, b.offset + k * b.slice_numel, b.slice_numel),
+                     self.p8_scale.narrow(0, i, 1))
+
+    def _pull_fp8(self, b: Bucket):
+        C = native()
+        q = self.p8.narrow(0, b.offset, b.numel).view(torch.uint8)
+        sc = self.p8_scale.narrow(0, b.index * self.P, self.P)
+        if self.world > 1:
+            if self.collective_rs:
+                self.t.all_gather(q.narrow(0, self.rank * b.slice_numel, b.slice_numel), q)
+                self.t.all_gather(sc.narrow(0, self.rank, 1), sc)
+            else:
+                for k, owner in enumerate(self.owners):
+                    self.t.broadcast(q.narrow(0, k * b.slice_numel, b.slice_numel), owner)
+                    self.t.broadcast(sc.narrow(0, k, 1), owner)
+        for k in range(self.P):
+            lo = b.offset + k * b.slice_numel
+            C.dequant_fp8_(self.p8.narrow(0, lo, b.slice_numel), sc.narrow(0, k, 1),
+                           self.params_flat.narrow(0, lo, b.slice_numel))
+
     def _pull(self, b: Bucket):
+        if self.pull_fp8:
+            return self._pull_fp8(b)
         w = self.params_flat.narrow(0, b.offset, b.numel)
         if self.world == 1:
             return

@@ -111,3 +111,19 @@ def test_world1_local_matches_reference():
     want = _reference(1, 0)
     for n, p in spec.model.named_parameters():
         torch.testing.assert_close(p.detach(), want[n], rtol=1e-5, atol=1e-6)
+
+
+def test_fp8_pull_publishes_fp8_representable_weights():
+    torch.manual_seed(0)
+    spec = models.build("mlp", torch.device("cpu"), torch.bfloat16, hidden=64)
+    ps = CollectivePS(spec.model, OptimConfig(**CFG), staleness=0, bucket_mb=0.0005, pull_dtype="fp8")
+    tr = Trainer(spec.model, spec.loss, ps, spec.make_batch(16, torch.device("cpu"), seed=0))
+    for _ in range(2):
+        tr.step()
+    for b in ps.buckets:
+        m = ps.master.narrow(0, b.local_offset, b.slice_numel)
+        scale = m.abs().max().clamp_min(1e-12) / 448.0
+        q = (m / scale).clamp(-448, 448).to(torch.float8_e4m3fn)
+        want = (q.float() * scale).to(torch.bfloat16)
+        got = ps.params_flat.narrow(0, b.offset, b.slice_numel)
+        torch.testing.assert_close(got.float(), want.float(), rtol=1e-2, atol=1e-6)
