@@ -36,6 +36,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_splitk_", &gemm_splitk_, py::arg("A"), py::arg("B"), py::arg("a_kmajor"), py::arg("b_kmajor"),
         py::arg("out"), py::arg("accumulate") = false, py::arg("scale") = 1.0, py::arg("splits") = 0);
   m.def("colsum_", &colsum_, py::arg("x"), py::arg("out"), py::arg("accumulate") = false);
+  m.def("maxpool3s2_fwd", &maxpool3s2_fwd);
+  m.def("maxpool3s2_bwd", &maxpool3s2_bwd);
   m.attr("OPT_SGD") = (int)OPT_SGD;
   m.attr("OPT_MOMENTUM") = (int)OPT_MOMENTUM;
   m.attr("OPT_ADAM") = (int)OPT_ADAM;

@@ -138,3 +138,31 @@ std::vector<at::Tensor> bn_bwd(const at::Tensor& dy_in, const at::Tensor& x_in, 
 }
 
 }  // namespace psd
+
+// ---- NHWC 3x3/s2/p1 max-pool (kernels/pool.hip)
+#include "kernels/launchers_pool.h"
+namespace psd {
+std::vector<at::Tensor> maxpool3s2_fwd(const at::Tensor& x_in) {
+  TORCH_CHECK(x_in.is_cuda() && x_in.scalar_type() == at::kBFloat16 && x_in.dim() == 4, "psd maxpool: bf16 NCHW-shaped");
+  const c10::DeviceGuard g(x_in.device());
+  at::Tensor x = x_in.contiguous(at::MemoryFormat::ChannelsLast);
+  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
+  at::Tensor y = at::empty({N, C, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  at::Tensor arg = at::empty({N, C, Ho, Wo}, x.options().dtype(at::kByte).memory_format(at::MemoryFormat::ChannelsLast));
+  hipError_t e = launch_maxpool_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<uint16_t*>(y.data_ptr()),
+                                    arg.data_ptr<uint8_t>(), N, H, W, C, Ho, Wo, stream_of(x));
+  TORCH_CHECK(e == hipSuccess, "psd maxpool fwd: ", hipGetErrorString(e));
+  return {y, arg};
+}
+at::Tensor maxpool3s2_bwd(const at::Tensor& dy_in, const at::Tensor& arg, int64_t H, int64_t W) {
+  const c10::DeviceGuard g(dy_in.device());
+  at::Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
+  const int N = dy.size(0), C = dy.size(1), Ho = dy.size(2), Wo = dy.size(3);
+  at::Tensor dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  hipError_t e = launch_maxpool_bwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()), arg.data_ptr<uint8_t>(),
+                                    reinterpret_cast<uint16_t*>(dx.data_ptr()), N, (int)H, (int)W, C, Ho, Wo, stream_of(dy));
+  TORCH_CHECK(e == hipSuccess, "psd maxpool bwd: ", hipGetErrorString(e));
+  return dx;
+}
+}  // namespace psd

@@ -126,16 +126,18 @@ __global__ __launch_bounds__(256) void bn_fwd_reduce_kernel(const uint16_t* __re
     if (shift_k) load8_f32(shift_k + m.cg * 8, k);
     const int64_t stride = (int64_t)gridDim.x * m.rpi;
     int64_t r = (int64_t)blockIdx.x * m.rpi + m.r0;
-    for (; r + stride < M; r += 2 * stride) {  // 2 independent 16-B loads in flight per lane
-      float v0[8], v1[8];
-      load8_bf16(x + r * C + m.cg * 8, v0);
-      load8_bf16(x + (r + stride) * C + m.cg * 8, v1);
+    for (; r + 3 * stride < M; r += 4 * stride) {  // 4 independent 16-B loads in flight per lane
+      float v[4][8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float d0 = v0[j] - k[j], d1 = v1[j] - k[j];
-        a[j] += d0 + d1;
-        b[j] = fmaf(d0, d0, fmaf(d1, d1, b[j]));
-      }
+      for (int u = 0; u < 4; ++u) load8_bf16(x + (r + u * stride) * C + m.cg * 8, v[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = v[u][j] - k[j];
+          a[j] += d;
+          b[j] = fmaf(d, d, b[j]);
+        }
     }
     for (; r < M; r += stride) {
       float v0[8];
@@ -224,23 +226,39 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
   if (m.active) {
     load8_f32(mean + m.cg * 8, mu);
     const int64_t stride = (int64_t)gridDim.x * m.rpi;
-    for (int64_t r = (int64_t)blockIdx.x * m.rpi + m.r0; r < M; r += stride) {
-      const int64_t off = r * C + m.cg * 8;
-      float g[8], xv[8];
-      load8_bf16(dy + off, g);
-      load8_bf16(x + off, xv);
-      if (RELU) {
-        float yv[8];
-        load8_bf16(y + off, yv);
+    auto body = [&](int64_t off, const float* g0, const float* xv, const float* yv) {
+      float g[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
-      }
+      for (int j = 0; j < 8; ++j) g[j] = RELU ? (yv[j] > 0.f ? g0[j] : 0.f) : g0[j];
       if (RES_OUT) store8_bf16(dr + off, g);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         a[j] += g[j];
         b[j] = fmaf(g[j], xv[j] - mu[j], b[j]);
       }
+    };
+    int64_t r = (int64_t)blockIdx.x * m.rpi + m.r0;
+    for (; r + stride < M; r += 2 * stride) {  // two rows (6 loads) in flight per lane
+      const int64_t o0 = r * C + m.cg * 8, o1 = (r + stride) * C + m.cg * 8;
+      float g0[8], g1[8], x0[8], x1[8], y0[8], y1[8];
+      load8_bf16(dy + o0, g0);
+      load8_bf16(dy + o1, g1);
+      load8_bf16(x + o0, x0);
+      load8_bf16(x + o1, x1);
+      if (RELU) {
+        load8_bf16(y + o0, y0);
+        load8_bf16(y + o1, y1);
+      }
+      body(o0, g0, x0, y0);
+      body(o1, g1, x1, y1);
+    }
+    for (; r < M; r += stride) {
+      const int64_t o0 = r * C + m.cg * 8;
+      float g0[8], x0[8], y0[8];
+      load8_bf16(dy + o0, g0);
+      load8_bf16(x + o0, x0);
+      if (RELU) load8_bf16(y + o0, y0);
+      body(o0, g0, x0, y0);
     }
   }
   block_partials(m, C, a, b, part);
@@ -309,9 +327,10 @@ static void reduce_grid(int64_t M, int C, int& gx, int& gy) {
     gy = 1;
     rpi = 256 / tpc;
   }
-  // ~8+ rows per lane, <= ~2048 blocks in total (256 CUs x 8)
-  int64_t want = (M + (int64_t)rpi * 8 - 1) / ((int64_t)rpi * 8);
-  int64_t cap = 2048 / gy;
+  // >= 16 rows per lane (4 loads in flight each), <= 512 partial rows: the finalize kernel then
+  // sums at most 16 partials per lane instead of a 2048-deep dependent chain
+  int64_t want = (M + (int64_t)rpi * 16 - 1) / ((int64_t)rpi * 16);
+  int64_t cap = 512 / gy;
   if (cap < 1) cap = 1;
   gx = (int)(want < 1 ? 1 : (want > cap ? cap : want));
 }

@@ -479,25 +479,65 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
-// column sums of a [M][N] bf16 matrix (bias gradient): out[n] = sum_m x[m][n] (fp32 partials per
-// block-row, then a tiny second pass). Lane = 8 columns; 256 lanes cover 256/(N/8) rows.
+// column sums of a [M][N] bf16 matrix (bias gradient), deterministic two-pass: block partials
+// (lane = 8 columns, 4 rows in flight) -> one finalize lane per column summing <= 64 partial rows.
+constexpr int kColsumMaxBlocks = 64;
 __global__ __launch_bounds__(256) void colsum_partial_kernel(const uint16_t* __restrict__ x, int64_t M, int N,
                                                              float* __restrict__ part) {
   const int tpc = N >> 3;
   const int rpi = tpc >= 256 ? 1 : 256 / tpc;
   const int cg = tpc >= 256 ? blockIdx.y * 256 + threadIdx.x : threadIdx.x % tpc;
   const int r0 = tpc >= 256 ? 0 : threadIdx.x / tpc;
+  const bool active = cg < tpc && r0 < rpi;
   float a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (cg < tpc && r0 < rpi)
-    for (int64_t r = (int64_t)blockIdx.x * rpi + r0; r < M; r += (int64_t)gridDim.x * rpi) {
+  if (active) {
+    const int64_t stride = (int64_t)gridDim.x * rpi;
+    int64_t r = (int64_t)blockIdx.x * rpi + r0;
+    for (; r + 3 * stride < M; r += 4 * stride) {
+      float t[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) load8_bf16(x + (r + u * stride) * N + cg * 8, t[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a[e] += t[u][e];
+    }
+    for (; r < M; r += stride) {
       float t[8];
       load8_bf16(x + r * N + cg * 8, t);
 #pragma unroll
       for (int e = 0; e < 8; ++e) a[e] += t[e];
     }
-  if (cg < tpc && r0 < rpi)
+  }
+  __shared__ float red[256 * 8];
+  if (tpc >= 256) {
+    if (active) store8_f32(part + (int64_t)blockIdx.x * N + cg * 8, a);
+    return;
+  }
+  if (active)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) atomicAdd(part + cg * 8 + e, a[e]);
+    for (int e = 0; e < 8; ++e) red[r0 * N + cg * 8 + e] = a[e];
+  __syncthreads();
+  for (int c = threadIdx.x; c < N; c += 256) {
+    float sum = 0.f;
+    for (int rr = 0; rr < rpi; ++rr) sum += red[rr * N + c];
+    part[(int64_t)blockIdx.x * N + c] = sum;
+  }
+}
+
+__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ part, int nblk, int N, void* out,
+                                                           int out_bf16, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= N) return;
+  float s = 0.f;
+  for (int b = 0; b < nblk; ++b) s += part[(int64_t)b * N + c];
+  if (out_bf16) {
+    uint16_t* o = reinterpret_cast<uint16_t*>(out);
+    o[c] = f32_to_bf16(s + (accumulate ? bf16_to_f32(o[c]) : 0.f));
+  } else {
+    float* o = reinterpret_cast<float*>(out);
+    o[c] = s + (accumulate ? o[c] : 0.f);
+  }
 }
 
 __global__ void f32_to_bf16_kernel(const float* in, uint16_t* out, int n, int accumulate) {
@@ -533,7 +573,9 @@ static bool big_ok(const GemmArgs& g, int kseg) {
   // enough 256x256 tiles to fill the chip, no K tail inside a stage, MN-major operands 8-aligned
   const int64_t tiles = (int64_t)((g.M + 255) / 256) * ((g.N + 255) / 256);
   if (getenv("PSD_GEMM_SMALL_ONLY")) return false;
-  return g.M >= 256 && g.N >= 256 && kseg % 64 == 0 && tiles >= 64 && g.K >= 256;
+  // split-K (MODE 1) passes tiles * splits via k_per_split < K
+  const int64_t waves = g.k_per_split > 0 ? tiles * ((g.K + g.k_per_split - 1) / g.k_per_split) : tiles;
+  return g.M >= 256 && g.N >= 256 && kseg % 64 == 0 && waves >= 64 && g.K >= 256;
 }
 
 template <bool AK, bool BKM, int MODE>
@@ -556,6 +598,14 @@ hipError_t launch_gemm(const GemmArgs& g, hipStream_t st) {
 }
 
 int gemm_splits(int M, int N, int K) {
+  if (M >= 256 && N >= 256 && K % 64 == 0 && K >= 4096) {  // 256x256 tiles, one workgroup per CU
+    const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+    int s = (256 + tiles - 1) / tiles;
+    const int kmax = K / 512;
+    if (s > kmax) s = kmax;
+    if (s > 64) s = 64;
+    return s < 1 ? 1 : s;
+  }
   const int BM = M <= 64 ? 64 : 128, BN = N <= 64 ? 64 : 128;
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   int s = (512 + tiles - 1) / tiles;      // ~2 workgroups per CU
@@ -589,19 +639,18 @@ hipError_t launch_gemm_splitk(const GemmArgs& g0, float* slab, int splits, void*
   return hipGetLastError();
 }
 
-hipError_t launch_colsum(const uint16_t* x, int64_t M, int N, float* part_zeroed, void* out, int out_bf16,
+hipError_t launch_colsum(const uint16_t* x, int64_t M, int N, float* part, void* out, int out_bf16,
                          int accumulate, hipStream_t st) {
   if (N % 8 != 0) return hipErrorInvalidValue;
   const int tpc = N / 8;
   const int gy = tpc >= 256 ? (tpc + 255) / 256 : 1;
   const int rpi = tpc >= 256 ? 1 : 256 / tpc;
   int64_t gx = (M + (int64_t)rpi * 16 - 1) / ((int64_t)rpi * 16);
-  if (gx > 1024 / gy) gx = 1024 / gy;
+  if (gx > kColsumMaxBlocks) gx = kColsumMaxBlocks;
   if (gx < 1) gx = 1;
-  hipLaunchKernelGGL(colsum_partial_kernel, dim3((unsigned)gx, gy), dim3(256), 0, st, x, M, N, part_zeroed);
-  if (out_bf16)
-    hipLaunchKernelGGL(f32_to_bf16_kernel, dim3((N + 255) / 256), dim3(256), 0, st, part_zeroed,
-                       reinterpret_cast<uint16_t*>(out), N, accumulate);
+  hipLaunchKernelGGL(colsum_partial_kernel, dim3((unsigned)gx, gy), dim3(256), 0, st, x, M, N, part);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((N + 255) / 256), dim3(256), 0, st, part, (int)gx, N, out, out_bf16,
+                     accumulate);
   return hipGetLastError();
 }
 

@@ -29,5 +29,7 @@ void gemm_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool b_kmajo
 void gemm_splitk_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool b_kmajor, at::Tensor out,
                   bool accumulate, double scale, int64_t splits);
 void colsum_(const at::Tensor& x, at::Tensor out, bool accumulate);
+std::vector<at::Tensor> maxpool3s2_fwd(const at::Tensor& x);
+at::Tensor maxpool3s2_bwd(const at::Tensor& dy, const at::Tensor& arg, int64_t H, int64_t W);
 
 }  // namespace psd

@@ -63,25 +63,31 @@ class BertForMLM(nn.Module):
                 nn.init.normal_(m.weight, std=0.02)
 
     def forward(self, batch):
-        ids, types = batch
+        ids, types, mlm_pos = batch
         S = ids.shape[1]
         pos = torch.arange(S, device=ids.device)
         x = self.word(ids) + self.pos(pos)[None] + self.tok_type(types)
         x = F.dropout(self.ln(x), self.p, self.training)
         for layer in self.layers:
             x = layer(x)
+        # MLM head only on the masked positions (max_predictions_per_seq per sequence, as in the
+        # original BERT pre-training): 6-7x less head/decoder/softmax work than all tokens
+        x = x.reshape(-1, x.shape[-1]).index_select(0, mlm_pos)
         return self.decoder(self.head_ln(self.head(x)))
 
     @staticmethod
     def loss(logits, labels):
-        return F.cross_entropy(logits.float().view(-1, logits.shape[-1]), labels.view(-1), ignore_index=-100)
+        return F.cross_entropy(logits.float(), labels)
 
 
 def bert_batch(batch: int, seq: int, vocab: int, device, seed: int = 0, mask_prob: float = 0.15):
+    """Synthetic pre-training batch: random ids, sentence-B types for the second half, and
+    round(mask_prob * seq) masked positions per sequence (flat indices) with their labels."""
     g = torch.Generator(device="cpu").manual_seed(seed)
     ids = torch.randint(0, vocab, (batch, seq), generator=g)
     types = (torch.arange(seq)[None, :] >= seq // 2).long().expand(batch, seq).contiguous()
-    labels = torch.full((batch, seq), -100, dtype=torch.long)
-    m = torch.rand(batch, seq, generator=g) < mask_prob
-    labels[m] = ids[m]
-    return (ids.to(device), types.to(device)), labels.to(device)
+    npred = max(1, round(mask_prob * seq))
+    cols = torch.stack([torch.randperm(seq, generator=g)[:npred].sort().values for _ in range(batch)])
+    flat = (cols + torch.arange(batch)[:, None] * seq).reshape(-1)
+    labels = ids.reshape(-1)[flat]
+    return (ids.to(device), types.to(device), flat.to(device)), labels.to(device)

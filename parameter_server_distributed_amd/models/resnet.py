@@ -14,6 +14,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.bn import FusedBatchNorm2d
+from ..ops.pool import max_pool_3x3s2
 
 
 def _conv(cin, cout, k, stride=1, groups=1):
@@ -78,7 +79,7 @@ class ResNet(nn.Module):
 
     def forward(self, x):
         x = self.bn1(self.conv1(x))
-        x = F.max_pool2d(x, 3, 2, 1)
+        x = max_pool_3x3s2(x)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
         return self.fc(x)

@@ -8,6 +8,7 @@ MIOpen at it. Must run before the first convolution (ideally before ``import tor
 """
 from __future__ import annotations
 
+import atexit
 import os
 import shutil
 import tempfile
@@ -31,4 +32,7 @@ def install(force: bool = False) -> str | None:
                 shutil.copy2(os.path.join(s, f), os.path.join(d, f))
     os.environ["MIOPEN_USER_DB_PATH"] = os.path.join(dst, "db")
     os.environ["MIOPEN_CUSTOM_CACHE_DIR"] = os.path.join(dst, "cache")
+    out = os.environ.get("PSD_MIOPEN_DB_OUT")
+    if out:  # tuning run: export the grown database for tuning/miopen
+        atexit.register(lambda: shutil.copytree(dst, out, dirs_exist_ok=True))
     return dst

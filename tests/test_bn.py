@@ -85,3 +85,21 @@ def test_fused_bn_cpu_reference_path():
     y = m(x, r)
     ref = F.relu(F.batch_norm(x, None, None, None, None, True) + r)
     torch.testing.assert_close(y, ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(2, 64, 112, 112), (3, 16, 9, 7), (1, 8, 2, 2)], ids=str)
+def test_maxpool3s2_matches_torch(gpu, shape):
+    from parameter_server_distributed_amd.ops.pool import max_pool_3x3s2
+
+    torch.manual_seed(0)
+    x = torch.randn(shape).to(torch.bfloat16)
+    xd = x.to(gpu).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    y = max_pool_3x3s2(xd)
+    g = torch.randn(y.shape).to(torch.bfloat16)
+    y.backward(g.to(gpu).contiguous(memory_format=torch.channels_last))
+    xr = x.float().requires_grad_(True)
+    yr = F.max_pool2d(xr, 3, 2, 1)
+    yr.backward(g.float())
+    torch.testing.assert_close(y.float().cpu(), yr.detach(), rtol=0, atol=0)
+    torch.testing.assert_close(xd.grad.float().cpu(), xr.grad, rtol=1e-2, atol=1e-2)
