@@ -45,7 +45,7 @@ METRICS = {
     "resnet101": ("samples/sec (whole node) ResNet-101", "samples/s"),
     "mlp": ("samples/sec (whole node) 2-layer MLP", "samples/s"),
 }
-DEFAULT_BATCH = {"resnet50": 256, "bert_base": 64, "wide_resnet101_2": 128, "resnet101": 256, "mlp": 4096}
+DEFAULT_BATCH = {"resnet50": 512, "bert_base": 64, "wide_resnet101_2": 128, "resnet101": 256, "mlp": 4096}
 
 
 def parse():
@@ -67,8 +67,9 @@ def parse():
     ap.add_argument("--lr", type=float, default=0.0)
     ap.add_argument("--graph", type=int, default=-1, help="hipGraph capture (1/0; -1: on for 1 GPU)")
     ap.add_argument("--transport", default="auto", choices=["auto", "torch", "rccl"])
-    ap.add_argument("--benchmark-miopen", type=int, default=0, help="torch.backends.cudnn.benchmark")
+    ap.add_argument("--benchmark-miopen", type=int, default=1, help="torch.backends.cudnn.benchmark")
     ap.add_argument("--out", default="", help="also write the JSON line to this file")
+    ap.add_argument("--trace", default="", help="per-step phase trace (JSON lines, one file per rank); eager")
     return ap.parse_args()
 
 
@@ -107,7 +108,12 @@ def main():
     n_workers = len(ps.worker_ranks)
     batch = spec.make_batch(a.batch, dev, seed=rank)
     use_graph = (world == 1) if a.graph < 0 else bool(a.graph)
-    tr = Trainer(spec.model, spec.loss, ps, batch, use_graph=use_graph)
+    tracer = None
+    if a.trace:
+        from parameter_server_distributed_amd.utils.trace import StepTracer, rank_path
+
+        tracer = StepTracer(rank_path(a.trace, rank), rank, dev)
+    tr = Trainer(spec.model, spec.loss, ps, batch, use_graph=use_graph, tracer=tracer)
 
     def barrier():
         if world > 1:
@@ -176,6 +182,8 @@ def main():
         if a.out:
             with open(a.out, "w") as f:
                 f.write(line + "\n")
+    if tracer is not None:
+        tracer.close()
     if world > 1:
         dist.destroy_process_group()
 

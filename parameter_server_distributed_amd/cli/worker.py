@@ -27,10 +27,13 @@ def main(argv=None):
     ap.add_argument("--mode", default="sync", choices=["sync", "async"])
     ap.add_argument("--heartbeat-s", type=float, default=5.0)
     ap.add_argument("--bf16-wire", action="store_true", help="push gradients as bf16 bytes")
+    ap.add_argument("--reference-wire", action="store_true",
+                    help="encode tensors as the reference did (repeated float), not bulk bytes")
     ap.add_argument("--stats-json", default="", help="write final PS stats + losses to this file")
     a = ap.parse_intermixed_args(argv)
     w = Worker(a.coordinator, a.worker_id, a.worker_addr, a.worker_port, model=a.model, batch=a.batch,
-               device=a.device, heartbeat_s=a.heartbeat_s, bf16_wire=a.bf16_wire, mode=a.mode)
+               device=a.device, heartbeat_s=a.heartbeat_s, bf16_wire=a.bf16_wire, mode=a.mode,
+               raw_wire=not a.reference_wire)
     w.initialize()
 
     def _leave(signum, frame):  # scale_workers.sh down: deregister so the barrier shrinks at once
@@ -44,11 +47,13 @@ def main(argv=None):
         epoch, it = w.load_checkpoint_from_server(a.checkpoint_path)
         start = it + 1 if it > 0 else 0
         print(f"worker {a.worker_id} loaded checkpoint epoch {epoch}, resuming at iteration {start}", flush=True)
-    losses = []
+    losses, iter_s = [], []
     t0 = time.time()
     ok_all = True
     for it in range(start, start + a.iterations):
+        ti = time.time()
         done, loss, r = w.run_iteration(it)
+        iter_s.append(time.time() - ti)
         losses.append(loss)
         ok_all &= done
         print(f"worker {a.worker_id} iter {it} done={'true' if done else 'false'} loss={loss:.4f} "
@@ -59,7 +64,8 @@ def main(argv=None):
     if a.stats_json:
         st = w.stats()
         with open(a.stats_json, "w") as f:
-            json.dump({"losses": losses, "version": st.version, "hist": list(st.staleness_histogram),
+            json.dump({"losses": losses, "iter_seconds": iter_s, "version": st.version,
+                       "hist": list(st.staleness_histogram),
                        "counters": json.loads(st.counters_json or "{}"), "seconds": dt}, f)
     w.shutdown()
     return 0 if ok_all else 1

@@ -11,8 +11,10 @@ import torch.nn.functional as F
 
 
 class MLP(nn.Module):
-    def __init__(self, in_features: int = 784, hidden: int = 512, num_classes: int = 10, linear_cls=nn.Linear):
+    def __init__(self, in_features: int = 784, hidden: int = 512, num_classes: int = 10, linear_cls=None):
         super().__init__()
+        if linear_cls is None:
+            from ..ops.linear import MfmaLinear as linear_cls
         self.fc1 = linear_cls(in_features, hidden)
         self.fc2 = linear_cls(hidden, num_classes)
 

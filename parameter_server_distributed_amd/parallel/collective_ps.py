@@ -202,6 +202,7 @@ class CollectivePS:
             self.ready_events = [torch.cuda.Event() for _ in buckets]
         self._advanced = False
         self._next = 0
+        self.tracer = None  # utils.trace.StepTracer (set by the Trainer)
         self._sync_init()
 
     # ------------------------------------------------------------------ setup
@@ -298,6 +299,13 @@ class CollectivePS:
             ev.record(torch.cuda.current_stream(self.device))
             self.comm_stream.wait_event(ev)
             with torch.cuda.stream(self.comm_stream):
+                if self.tracer is not None:
+                    with self.tracer.comm_span(self.comm_stream):
+                        self._push_apply_pull(b)
+                else:
+                    self._push_apply_pull(b)
+        elif self.tracer is not None:
+            with self.tracer.comm_span():
                 self._push_apply_pull(b)
         else:
             self._push_apply_pull(b)

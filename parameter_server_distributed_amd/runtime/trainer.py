@@ -21,7 +21,8 @@ from ..parallel.collective_ps import CollectivePS
 
 
 class Trainer:
-    def __init__(self, model, loss_fn, ps: CollectivePS, batch, use_graph: bool = False, graph_warmup: int = 3):
+    def __init__(self, model, loss_fn, ps: CollectivePS, batch, use_graph: bool = False, graph_warmup: int = 3,
+                 tracer=None):
         self.model = model
         self.loss_fn = loss_fn
         self.ps = ps
@@ -32,6 +33,10 @@ class Trainer:
         self.static_loss = None
         self.step_count = 0
         self.graph_error = None
+        self.tracer = tracer
+        if tracer is not None:
+            self.use_graph = False  # per-phase timing needs eager steps
+            ps.tracer = tracer
 
     # eager step ---------------------------------------------------------------
     def _body(self):
@@ -39,11 +44,24 @@ class Trainer:
             self.ps.begin_step()
             self.ps.finish_step()
             return torch.zeros((), device=self.ps.device)
-        self.ps.begin_step()
-        out = self.model(self.x)
-        loss = self.loss_fn(out, self.y)
-        loss.backward()
-        self.ps.finish_step()
+        tr = self.tracer
+        if tr is None:
+            self.ps.begin_step()
+            out = self.model(self.x)
+            loss = self.loss_fn(out, self.y)
+            loss.backward()
+            self.ps.finish_step()
+            return loss
+        with tr.phase("begin"):
+            self.ps.begin_step()
+        with tr.phase("forward"):
+            out = self.model(self.x)
+            loss = self.loss_fn(out, self.y)
+        with tr.phase("backward"):
+            loss.backward()
+        with tr.phase("finish"):
+            self.ps.finish_step()
+        tr.end_step(self.step_count, version=self.ps.step_idx)
         return loss
 
     def eager_step(self):

@@ -127,3 +127,23 @@ def test_fp8_pull_publishes_fp8_representable_weights():
         want = (q.float() * scale).to(torch.bfloat16)
         got = ps.params_flat.narrow(0, b.offset, b.slice_numel)
         torch.testing.assert_close(got.float(), want.float(), rtol=1e-2, atol=1e-6)
+
+
+def test_tracer_records_phases(tmp_path):
+    from parameter_server_distributed_amd.utils.trace import StepTracer
+
+    torch.manual_seed(0)
+    spec = models.build("mlp", torch.device("cpu"), torch.float32, hidden=64)
+    ps = CollectivePS(spec.model, OptimConfig(**CFG), staleness=0, bucket_mb=0.0005, grad_dtype=torch.float32,
+                      param_dtype=torch.float32)
+    p = str(tmp_path / "trace.jsonl")
+    tr = Trainer(spec.model, spec.loss, ps, spec.make_batch(16, torch.device("cpu")), tracer=StepTracer(p))
+    for _ in range(3):
+        tr.step()
+    tr.tracer.close()
+    import json
+
+    recs = [json.loads(ln) for ln in open(p)]
+    assert [r["step"] for r in recs] == [0, 1, 2]
+    for k in ("forward_ms", "backward_ms", "finish_ms", "comm_ms"):
+        assert k in recs[-1] and recs[-1][k] >= 0
