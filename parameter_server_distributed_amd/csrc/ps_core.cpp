@@ -9,6 +9,14 @@
 
 namespace psd {
 
+// Timed waits use a system_clock deadline: libstdc++ then waits with pthread_cond_timedwait, which
+// ThreadSanitizer intercepts (its steady_clock path, pthread_cond_clockwait, is invisible to the
+// GCC 11 TSAN runtime and yields false "double lock" reports in tests/test_sanitizers.py).
+static inline std::chrono::system_clock::time_point deadline(double seconds) {
+  return std::chrono::system_clock::now() +
+         std::chrono::duration_cast<std::chrono::system_clock::duration>(std::chrono::duration<double>(seconds));
+}
+
 namespace {
 constexpr int64_t kAlign = 8;  // elements: keeps every tensor 16-B aligned inside the flat buffers
 constexpr int kHistBins = 64;
@@ -263,13 +271,13 @@ std::tuple<bool, int32_t, int32_t> PSCore::sync_status(int32_t iteration) const 
 
 std::tuple<bool, int32_t, int64_t, at::Tensor> PSCore::pull(int32_t wid, int32_t iteration, double wait_s) {
   std::unique_lock<std::mutex> lk(mu_);
-  if (!init_ && wait_s > 0) cv_.wait_for(lk, std::chrono::duration<double>(wait_s), [&] { return init_; });
+  if (!init_ && wait_s > 0) cv_.wait_until(lk, deadline(wait_s), [&] { return init_; });
   if (!init_) return {false, current_iteration_, version_, at::Tensor()};
   bool ready = true;
   if (cfg_.async_mode) {
     if (cfg_.staleness_bound >= 0) {
       auto ok = [&] { return iteration - min_clock_locked() <= cfg_.staleness_bound; };
-      if (wait_s > 0) cv_.wait_for(lk, std::chrono::duration<double>(wait_s), ok);
+      if (wait_s > 0) cv_.wait_until(lk, deadline(wait_s), ok);
       ready = ok();
       if (!ready) ctr_["bound_timeouts"] += 1;
     }
@@ -278,7 +286,7 @@ std::tuple<bool, int32_t, int64_t, at::Tensor> PSCore::pull(int32_t wid, int32_t
       auto it = iters_.find(iteration);
       return (it != iters_.end() && it->second.aggregated) || iteration < current_iteration_ - cfg_.window;
     };
-    if (wait_s > 0) cv_.wait_for(lk, std::chrono::duration<double>(wait_s), agg);
+    if (wait_s > 0) cv_.wait_until(lk, deadline(wait_s), agg);
     ready = agg();
   }
   pulled_version_[wid] = version_;

@@ -5,6 +5,14 @@
 
 namespace psd {
 
+// Timed waits use a system_clock deadline: libstdc++ then waits with pthread_cond_timedwait, which
+// ThreadSanitizer intercepts (its steady_clock path, pthread_cond_clockwait, is invisible to the
+// GCC 11 TSAN runtime and yields false "double lock" reports in tests/test_sanitizers.py).
+static inline std::chrono::system_clock::time_point deadline(double seconds) {
+  return std::chrono::system_clock::now() +
+         std::chrono::duration_cast<std::chrono::system_clock::duration>(std::chrono::duration<double>(seconds));
+}
+
 static double mono_seconds() {
   using namespace std::chrono;
   return duration_cast<duration<double>>(steady_clock::now().time_since_epoch()).count();
@@ -135,7 +143,7 @@ int64_t Registry::membership_epoch() const {
 
 int64_t Registry::wait_epoch_change(int64_t known, double timeout_s) {
   std::unique_lock<std::mutex> lk(mu_);
-  cv_.wait_for(lk, std::chrono::duration<double>(timeout_s), [&] { return epoch_ != known; });
+  cv_.wait_until(lk, deadline(timeout_s), [&] { return epoch_ != known; });
   return epoch_;
 }
 
@@ -161,7 +169,7 @@ void Registry::kv_set(const std::string& key, const std::string& value) {
 
 std::tuple<bool, std::string> Registry::kv_get(const std::string& key, double timeout_s) {
   std::unique_lock<std::mutex> lk(mu_);
-  cv_.wait_for(lk, std::chrono::duration<double>(timeout_s), [&] { return kv_.count(key) > 0; });
+  cv_.wait_until(lk, deadline(timeout_s), [&] { return kv_.count(key) > 0; });
   auto it = kv_.find(key);
   if (it == kv_.end()) return {false, std::string()};
   return {true, it->second};
