@@ -91,9 +91,15 @@ std::vector<at::Tensor> bn_fwd(const at::Tensor& x_in, c10::optional<at::Tensor>
 std::vector<at::Tensor> bn_bwd(const at::Tensor& dy_in, const at::Tensor& x_in, c10::optional<at::Tensor> y_in,
                                c10::optional<at::Tensor> gamma, const at::Tensor& save_mean,
                                const at::Tensor& save_invstd, bool relu, bool need_dr,
-                               c10::optional<at::Tensor> dgamma_out, c10::optional<at::Tensor> dbeta_out) {
+                               c10::optional<at::Tensor> dgamma_out, c10::optional<at::Tensor> dbeta_out,
+                               c10::optional<at::Tensor> dy2_in) {
   const c10::DeviceGuard g(x_in.device());
   at::Tensor x = nhwc(x_in), dy = nhwc(dy_in);
+  at::Tensor dy2;
+  if (dy2_in.has_value() && dy2_in->defined()) {
+    dy2 = nhwc(*dy2_in);
+    TORCH_CHECK(dy2.sizes() == x.sizes() && dy2.scalar_type() == at::kBFloat16, "psd bn bwd: dy2 shape/dtype");
+  }
   const int64_t C = channels(x);
   const int64_t M = x.numel() / C;
   TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == at::kBFloat16, "psd bn bwd: dy shape/dtype");
@@ -118,6 +124,7 @@ std::vector<at::Tensor> bn_bwd(const at::Tensor& dy_in, const at::Tensor& x_in, 
   at::Tensor part = at::empty({(int64_t)bn_reduce_blocks(M, (int)C) * 2 * C}, f32);
   BnBwdArgs a{};
   a.dy = reinterpret_cast<const uint16_t*>(dy.data_ptr());
+  a.dy2 = dy2.defined() ? reinterpret_cast<const uint16_t*>(dy2.data_ptr()) : nullptr;
   a.y = y.defined() ? reinterpret_cast<const uint16_t*>(y.data_ptr()) : nullptr;
   a.x = reinterpret_cast<const uint16_t*>(x.data_ptr());
   a.gamma = opt_ptr<const uint16_t>(gamma);

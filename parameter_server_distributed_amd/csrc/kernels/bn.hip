@@ -215,7 +215,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
 
 // ------------------------------------------------------------------ backward
 template <bool RELU, bool RES_OUT>
-__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ dy2,
+                                                            const uint16_t* __restrict__ y,
                                                             const uint16_t* __restrict__ x, const float* __restrict__ mean,
                                                             uint16_t* __restrict__ dr, int64_t M, int C,
                                                             float* __restrict__ part) {
@@ -245,6 +246,16 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
       load8_bf16(dy + o1, g1);
       load8_bf16(x + o0, x0);
       load8_bf16(x + o1, x1);
+      if (dy2) {  // residual-branch gradient folded in (replaces an autograd add kernel)
+        float h0[8], h1[8];
+        load8_bf16(dy2 + o0, h0);
+        load8_bf16(dy2 + o1, h1);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          g0[j] += h0[j];
+          g1[j] += h1[j];
+        }
+      }
       if (RELU) {
         load8_bf16(y + o0, y0);
         load8_bf16(y + o1, y1);
@@ -257,6 +268,12 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
       float g0[8], x0[8], y0[8];
       load8_bf16(dy + o0, g0);
       load8_bf16(x + o0, x0);
+      if (dy2) {
+        float h0[8];
+        load8_bf16(dy2 + o0, h0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g0[j] += h0[j];
+      }
       if (RELU) load8_bf16(y + o0, y0);
       body(o0, g0, x0, y0);
     }
@@ -287,7 +304,8 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
 
 // MODE 0: dy' = dy; MODE 1: dy' = dy * (y > 0); MODE 2: dy' = g (already masked, = dr)
 template <int MODE>
-__global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(const uint16_t* __restrict__ g, const uint16_t* __restrict__ y,
+__global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(const uint16_t* __restrict__ g, const uint16_t* __restrict__ g2,
+                                                           const uint16_t* __restrict__ y,
                                                            const uint16_t* __restrict__ x, const float* __restrict__ coef,
                                                            uint16_t* __restrict__ dx, int64_t nvec, int C) {
   const int tpc = C >> 3;
@@ -302,6 +320,12 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(const uint16_t* __res
     float gv[8], xv[8];
     load8_bf16(g + v * 8, gv);
     load8_bf16(x + v * 8, xv);
+    if (MODE != 2 && g2) {
+      float h[8];
+      load8_bf16(g2 + v * 8, h);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) gv[j] += h[j];
+    }
     if (MODE == 1) {
       float yv[8];
       load8_bf16(y + v * 8, yv);
@@ -377,7 +401,7 @@ hipError_t launch_bn_bwd(const BnBwdArgs& a, hipStream_t st) {
   int gx, gy;
   reduce_grid(a.M, a.C, gx, gy);
 #define PSD_RED(R, O)                                                                                        \
-  hipLaunchKernelGGL((bn_bwd_reduce_kernel<R, O>), dim3(gx, gy), dim3(256), 0, st, a.dy, a.y, a.x, a.save_mean, \
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<R, O>), dim3(gx, gy), dim3(256), 0, st, a.dy, a.dy2, a.y, a.x, a.save_mean, \
                      a.dr, a.M, a.C, a.part)
   if (a.relu && a.dr) PSD_RED(true, true);
   else if (a.relu) PSD_RED(true, false);
@@ -389,11 +413,11 @@ hipError_t launch_bn_bwd(const BnBwdArgs& a, hipStream_t st) {
   const int64_t nvec = a.M * (a.C / 8);
   const int g = elem_grid(nvec, a.C);
   if (a.dr)
-    hipLaunchKernelGGL(bn_bwd_elemt_kernel<2>, dim3(g), dim3(256), 0, st, a.dr, a.y, a.x, a.coef, a.dx, nvec, a.C);
+    hipLaunchKernelGGL(bn_bwd_elemt_kernel<2>, dim3(g), dim3(256), 0, st, a.dr, nullptr, a.y, a.x, a.coef, a.dx, nvec, a.C);
   else if (a.relu)
-    hipLaunchKernelGGL(bn_bwd_elemt_kernel<1>, dim3(g), dim3(256), 0, st, a.dy, a.y, a.x, a.coef, a.dx, nvec, a.C);
+    hipLaunchKernelGGL(bn_bwd_elemt_kernel<1>, dim3(g), dim3(256), 0, st, a.dy, a.dy2, a.y, a.x, a.coef, a.dx, nvec, a.C);
   else
-    hipLaunchKernelGGL(bn_bwd_elemt_kernel<0>, dim3(g), dim3(256), 0, st, a.dy, a.y, a.x, a.coef, a.dx, nvec, a.C);
+    hipLaunchKernelGGL(bn_bwd_elemt_kernel<0>, dim3(g), dim3(256), 0, st, a.dy, a.dy2, a.y, a.x, a.coef, a.dx, nvec, a.C);
   return hipGetLastError();
 }
 

@@ -35,12 +35,16 @@ class Bottleneck(nn.Module):
         self.conv3 = _conv(width, planes * self.expansion, 1)
         self.bn3 = FusedBatchNorm2d(planes * self.expansion, relu=True)  # relu(bn3(conv3) + identity)
         self.downsample = downsample
+        self.fuse_residual_grad = True
 
-    def forward(self, x):
+    def forward(self, x, prev_bn=None):
+        """``prev_bn``: the fused BN that produced ``x`` (the previous block's bn3). For identity
+        blocks the residual gradient is then handed to it inside the BN kernels (no autograd add)."""
         idt = x if self.downsample is None else self.downsample(x)
         out = self.bn1(self.conv1(x))
         out = self.bn2(self.conv2(out))
-        return self.bn3(self.conv3(out), idt)
+        fuse = prev_bn if (self.downsample is None and self.fuse_residual_grad) else None
+        return self.bn3(self.conv3(out), idt, resid_grad_to=fuse)
 
 
 class ResNet(nn.Module):
@@ -80,7 +84,11 @@ class ResNet(nn.Module):
     def forward(self, x):
         x = self.bn1(self.conv1(x))
         x = max_pool_3x3s2(x)
-        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        prev = None
+        for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
+            for blk in layer:
+                x = blk(x, prev)
+                prev = blk.bn3
         x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
         return self.fc(x)
 

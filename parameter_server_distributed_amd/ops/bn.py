@@ -28,7 +28,7 @@ def _kernel_ok(x: torch.Tensor) -> bool:
 
 class _FusedBNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, mod):
+    def forward(ctx, x, weight, bias, residual, mod, resid_to=None):
         C = native()
         y, mean, invstd = C.bn_fwd(x, weight, bias, mod.running_mean, mod.running_var, residual, mod.relu, True,
                                    mod.momentum if mod.momentum is not None else 0.1, mod.eps,
@@ -36,6 +36,7 @@ class _FusedBNFn(torch.autograd.Function):
         ctx.relu = mod.relu
         ctx.has_res = residual is not None
         ctx.mod = mod
+        ctx.resid_to = resid_to
         ctx.save_for_backward(x, y if mod.relu else None, weight, mean, invstd)
         return y
 
@@ -47,8 +48,17 @@ class _FusedBNFn(torch.autograd.Function):
         dgo = dbo = None
         if sink is not None and w is not None:
             dgo, dbo = sink(mod.weight), sink(mod.bias)
-        dx, dr, dg, db = native().bn_bwd(dy, x, y, w, mean, invstd, ctx.relu, ctx.has_res, dgo, dbo)
-        return dx, (dg if w is not None else None), (db if w is not None else None), (dr if ctx.has_res else None), None
+        # residual-branch fusion: the identity-path gradient of this BN's output was stashed by the
+        # next block's bn3 backward; fold it in here instead of an autograd add kernel
+        dy2 = mod._psd_pending_dr.pop() if getattr(mod, "_psd_pending_dr", None) else None
+        dx, dr, dg, db = native().bn_bwd(dy, x, y, w, mean, invstd, ctx.relu, ctx.has_res, dgo, dbo, dy2)
+        res_grad = None
+        if ctx.has_res:
+            if ctx.resid_to is not None:
+                ctx.resid_to._psd_pending_dr.append(dr)
+            else:
+                res_grad = dr
+        return dx, (dg if w is not None else None), (db if w is not None else None), res_grad, None, None
 
 
 class FusedBatchNorm2d(nn.BatchNorm2d):
@@ -59,12 +69,20 @@ class FusedBatchNorm2d(nn.BatchNorm2d):
     def __init__(self, num_features: int, eps: float = 1e-5, momentum: float = 0.1, relu: bool = False):
         super().__init__(num_features, eps=eps, momentum=momentum)
         self.relu = relu
+        self._psd_pending_dr: list = []
 
     def psd_direct_grad_params(self):
         return [self.weight, self.bias]
 
-    def forward(self, x, residual=None):
+    def forward(self, x, residual=None, resid_grad_to: "FusedBatchNorm2d | None" = None):
+        """``resid_grad_to``: the FusedBatchNorm2d that produced ``residual``. Its gradient is then
+        handed to that module's backward directly (fused into its kernels) and ``residual`` is used
+        detached -- the caller guarantees the residual has no other consumer needing autograd."""
         if self.training and _kernel_ok(x) and self.running_mean is not None:
+            if resid_grad_to is not None and residual is not None and torch.is_grad_enabled() \
+                    and isinstance(resid_grad_to, FusedBatchNorm2d) and resid_grad_to.training \
+                    and _kernel_ok(residual) and residual.requires_grad:
+                return _FusedBNFn.apply(x, self.weight, self.bias, residual.detach(), self, resid_grad_to)
             return _FusedBNFn.apply(x, self.weight, self.bias, residual, self)
         if not self.training and _kernel_ok(x) and self.running_mean is not None:
             scale = self.weight.float() * torch.rsqrt(self.running_var + self.eps)

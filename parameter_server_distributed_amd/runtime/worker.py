@@ -55,8 +55,9 @@ class Worker:
         dtype = torch.float32 if self.device.type == "cpu" else torch.bfloat16
         self.spec = models.build(model, self.device, dtype)
         self.model = self.spec.model
-        if dtype != torch.float32:
-            self.model.to(dtype)
+        if dtype != torch.float32:  # parameters only: fused-BN running stats stay fp32
+            for prm in self.model.parameters():
+                prm.data = prm.data.to(dtype)
         self.batch = self.spec.make_batch(batch, self.device, seed=1000 + self.worker_id)
         self.status = cpb.IDLE
         self._status_lock = threading.Lock()

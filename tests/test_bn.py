@@ -103,3 +103,27 @@ def test_maxpool3s2_matches_torch(gpu, shape):
     yr.backward(g.float())
     torch.testing.assert_close(y.float().cpu(), yr.detach(), rtol=0, atol=0)
     torch.testing.assert_close(xd.grad.float().cpu(), xr.grad, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.gpu
+def test_resnet_residual_grad_fusion_matches_unfused(gpu):
+    """Identity-block residual gradients handed BN-to-BN inside the kernels == autograd's add."""
+    from parameter_server_distributed_amd import models
+
+    torch.manual_seed(0)
+    grads = []
+    for fuse in (True, False):
+        torch.manual_seed(0)
+        spec = models.build("resnet50", gpu, torch.bfloat16, image_size=64, num_classes=10)
+        m = spec.model
+        for p in m.parameters():
+            p.data = p.data.to(torch.bfloat16)
+        for mod in m.modules():
+            if hasattr(mod, "fuse_residual_grad"):
+                mod.fuse_residual_grad = fuse
+        x, y = spec.make_batch(4, gpu, seed=3)
+        spec.loss(m(x), y).backward()
+        grads.append({n: p.grad.float().clone() for n, p in m.named_parameters()})
+    for n in grads[0]:
+        a, b = grads[0][n], grads[1][n]
+        torch.testing.assert_close(a, b, rtol=3e-2, atol=3e-2 * (b.abs().max().item() + 1e-3), msg=n)
