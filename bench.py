@@ -70,6 +70,12 @@ def parse():
     ap.add_argument("--benchmark-miopen", type=int, default=1, help="torch.backends.cudnn.benchmark")
     ap.add_argument("--out", default="", help="also write the JSON line to this file")
     ap.add_argument("--trace", default="", help="per-step phase trace (JSON lines, one file per rank); eager")
+    ap.add_argument("--ckpt-prefix", default="", help="sharded PS checkpoint path prefix")
+    ap.add_argument("--ckpt-every", type=int, default=0, help="checkpoint every N steps (async, off the step)")
+    ap.add_argument("--resume", default="", help="load PS shards from this checkpoint prefix before training")
+    from parameter_server_distributed_amd.utils.config import apply_config
+
+    apply_config(ap)
     return ap.parse_args()
 
 
@@ -113,7 +119,10 @@ def main():
         from parameter_server_distributed_amd.utils.trace import StepTracer, rank_path
 
         tracer = StepTracer(rank_path(a.trace, rank), rank, dev)
-    tr = Trainer(spec.model, spec.loss, ps, batch, use_graph=use_graph, tracer=tracer)
+    if a.resume:
+        ps.load(a.resume)
+    tr = Trainer(spec.model, spec.loss, ps, batch, use_graph=use_graph, tracer=tracer,
+                 checkpoint_prefix=a.ckpt_prefix or None, checkpoint_every=a.ckpt_every)
 
     def barrier():
         if world > 1:

@@ -14,6 +14,9 @@ def main(argv=None):
     ap.add_argument("--expiry-s", type=float, default=30.0, help="drop workers silent for longer (reference: 30)")
     ap.add_argument("--sweep-s", type=float, default=10.0, help="expiry sweep period (reference: 10)")
     ap.add_argument("--shards", default="", help="comma-separated PS shard addresses (default: the PS address)")
+    from ..utils.config import apply_config
+
+    apply_config(ap, argv)
     a = ap.parse_intermixed_args(argv)
     shards = [s for s in a.shards.split(",") if s]
     serve(a.listen, a.ps_address, a.expiry_s, a.sweep_s, shards)

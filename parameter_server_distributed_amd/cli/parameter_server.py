@@ -25,6 +25,9 @@ def main(argv=None):
                     help="reference semantics: first aggregate becomes the params, p -= g (lr 1)")
     ap.add_argument("--coordinator", default="", help="follow live membership from this coordinator")
     ap.add_argument("--ckpt-dir", default=".")
+    from ..utils.config import apply_config
+
+    apply_config(ap, argv)
     a = ap.parse_intermixed_args(argv)
     opt = OptimConfig(a.optimizer, lr=a.lr, momentum=a.momentum if a.optimizer == "momentum" else 0.0,
                       weight_decay=a.weight_decay)

@@ -30,6 +30,9 @@ def main(argv=None):
     ap.add_argument("--reference-wire", action="store_true",
                     help="encode tensors as the reference did (repeated float), not bulk bytes")
     ap.add_argument("--stats-json", default="", help="write final PS stats + losses to this file")
+    from ..utils.config import apply_config
+
+    apply_config(ap, argv)
     a = ap.parse_intermixed_args(argv)
     w = Worker(a.coordinator, a.worker_id, a.worker_addr, a.worker_port, model=a.model, batch=a.batch,
                device=a.device, heartbeat_s=a.heartbeat_s, bf16_wire=a.bf16_wire, mode=a.mode,

@@ -28,7 +28,7 @@ break that invariant; such models must pass ``overlap=False``.
 """
 from __future__ import annotations
 
-import math
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -420,6 +420,7 @@ class CollectivePS:
     def state_dict(self) -> dict:
         return {"master": self.master.detach().cpu(), "state1": None if self.state1 is None else self.state1.cpu(),
                 "state2": None if self.state2 is None else self.state2.cpu(), "dyn": self.dyn.t.cpu(),
+                "slots": [sl.cpu() for sl in self.slots],
                 "step_idx": self.step_idx, "rank": self.rank, "world": self.world, "P": self.P,
                 "layout": [(b.offset, b.numel, b.local_offset) for b in self.buckets]}
 
@@ -430,6 +431,9 @@ class CollectivePS:
         if self.state2 is not None:
             self.state2.copy_(sd["state2"])
         self.dyn.t.copy_(sd["dyn"])
+        # in-flight (reduced, not yet applied) gradients of the last S steps
+        for dst, src in zip(self.slots, sd.get("slots") or []):
+            dst.copy_(src)
         self.step_idx = int(sd["step_idx"])
         # re-publish the working copy from the masters
         for b in self.buckets:
@@ -439,6 +443,106 @@ class CollectivePS:
                     self.master.narrow(0, lo, b.slice_numel))
         for b in self.buckets:
             self._pull(b)
+
+    # ------------------------------------------------------------------ sharded checkpoint
+    def _manifest(self) -> dict:
+        return {"format": "psd-collective-v1", "world": self.world, "P": self.P, "owners": self.owners,
+                "worker_ranks": self.worker_ranks, "staleness": self.S, "step_idx": self.step_idx,
+                "optimizer": self.cfg.to_dict(), "total": self.total,
+                "buckets": [{"offset": b.offset, "numel": b.numel, "slice": b.slice_numel,
+                             "params": [(n, list(p.shape), o, k) for (n, p, o, k) in b.params]}
+                            for b in self.buckets]}
+
+    def save(self, prefix: str, blocking: bool = True):
+        """Write this rank's PS shards (fp32 masters, optimizer state, step scalars) to
+        ``{prefix}.rank{r}.psd`` (atomic, CRC-checked; csrc/checkpoint.cpp) plus rank 0's JSON
+        manifest. The device->host copies run on a side stream into pinned memory and, with
+        ``blocking=False``, the file write happens on a host thread while training continues.
+        Returns the writer thread (or None)."""
+        import json
+        import threading
+
+        C = native()
+        tensors = [self.master, self.dyn.t] + [t for t in (self.state1, self.state2) if t is not None] \
+            + list(self.slots)
+        if self.is_cuda:
+            side = torch.cuda.Stream(device=self.device)
+            side.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(side):
+                host = [torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for t in tensors]
+                for h, t in zip(host, tensors):
+                    h.copy_(t, non_blocking=True)
+            done = torch.cuda.Event()
+            done.record(side)
+        else:
+            host = [t.detach().clone() for t in tensors]
+            done = None
+        man = self._manifest()
+        man["rank"] = self.rank
+        man["my_shards"] = self.my_shards
+        man_s = json.dumps(man)
+        path = f"{prefix}.rank{self.rank}.psd"
+
+        def write():
+            if done is not None:
+                done.synchronize()
+            C.save_native_ckpt(path, man_s, host)
+            if self.rank == 0:
+                with open(f"{prefix}.manifest.json.tmp", "w") as f:
+                    f.write(man_s)
+                os.replace(f"{prefix}.manifest.json.tmp", f"{prefix}.manifest.json")
+
+        if blocking:
+            write()
+            return None
+        th = threading.Thread(target=write, name="psd-ckpt", daemon=True)
+        th.start()
+        return th
+
+    def load(self, prefix: str):
+        """Restore this rank's shards from ``save(prefix)`` (same world / shard layout) and
+        re-publish the working parameters."""
+        import json
+
+        man, ts = native().load_native_ckpt(f"{prefix}.rank{self.rank}.psd")
+        m = json.loads(man)
+        if m["world"] != self.world or m["owners"] != self.owners or m["total"] != self.total:
+            raise ValueError(f"checkpoint layout (world {m['world']}, owners {m['owners']}) does not match this "
+                             f"run (world {self.world}, owners {self.owners})")
+        sd = {"master": ts[0], "dyn": ts[1], "step_idx": m["step_idx"]}
+        k = 2
+        if self.state1 is not None:
+            sd["state1"] = ts[k]
+            k += 1
+        if self.state2 is not None:
+            sd["state2"] = ts[k]
+            k += 1
+        sd["slots"] = ts[k:]
+        self.load_state_dict(sd)
+        if self.is_cuda:
+            torch.cuda.synchronize(self.device)
+
+    def export_reference(self, path: str, epoch: int, iteration: int = 0):
+        """Gather the fp32 masters and write the reference's binary checkpoint layout on rank 0
+        (collective: every rank must call)."""
+        full = torch.zeros(self.total, dtype=torch.float32, device=self.device)
+        for b in self.buckets:
+            for j, k in enumerate(self.my_shards):
+                full.narrow(0, b.offset + k * b.slice_numel, b.slice_numel).copy_(
+                    self.master.narrow(0, b.local_offset + j * b.slice_numel, b.slice_numel))
+        if self.world > 1:
+            for b in self.buckets:
+                for k, owner in enumerate(self.owners):
+                    self.t.broadcast(full.narrow(0, b.offset + k * b.slice_numel, b.slice_numel), owner)
+        if self.rank != 0:
+            return
+        names, shapes, tensors = [], [], []
+        for b in self.buckets:
+            for (n, p, o, k) in b.params:
+                names.append(n)
+                shapes.append(list(p.shape))
+                tensors.append(full.narrow(0, o, k).cpu())
+        native().save_reference_ckpt(path, epoch, iteration, names, shapes, tensors)
 
     def full_params_fp32(self) -> dict:
         """Gather the fp32 masters of every shard (for checkpoints / inspection)."""

@@ -22,7 +22,7 @@ from ..parallel.collective_ps import CollectivePS
 
 class Trainer:
     def __init__(self, model, loss_fn, ps: CollectivePS, batch, use_graph: bool = False, graph_warmup: int = 3,
-                 tracer=None):
+                 tracer=None, checkpoint_prefix: str | None = None, checkpoint_every: int = 0):
         self.model = model
         self.loss_fn = loss_fn
         self.ps = ps
@@ -34,6 +34,11 @@ class Trainer:
         self.step_count = 0
         self.graph_error = None
         self.tracer = tracer
+        # periodic sharded PS checkpoint (reference: checkpoint thread every ckpt_interval,
+        # src/parameter_main.cpp): device->host on a side stream, file write on a host thread
+        self.checkpoint_prefix = checkpoint_prefix
+        self.checkpoint_every = int(checkpoint_every)
+        self._ckpt_thread = None
         if tracer is not None:
             self.use_graph = False  # per-phase timing needs eager steps
             ps.tracer = tracer
@@ -104,6 +109,23 @@ class Trainer:
 
     def step(self):
         """One training step (eager until the graphs are built, then graph replay)."""
+        loss = self._step()
+        if self.checkpoint_every > 0 and self.checkpoint_prefix and self.step_count % self.checkpoint_every == 0:
+            self.checkpoint()
+        return loss
+
+    def checkpoint(self, blocking: bool = False):
+        """Snapshot the PS shards to ``checkpoint_prefix`` (waits for the previous write first)."""
+        if self._ckpt_thread is not None:
+            self._ckpt_thread.join()
+        self._ckpt_thread = self.ps.save(self.checkpoint_prefix, blocking=blocking)
+
+    def wait_checkpoint(self):
+        if self._ckpt_thread is not None:
+            self._ckpt_thread.join()
+            self._ckpt_thread = None
+
+    def _step(self):
         ps = self.ps
         if not self.use_graph:
             return self.eager_step()
@@ -135,6 +157,7 @@ class Trainer:
         t0 = time.perf_counter()
         for _ in range(steps):
             self.step()
+        self.wait_checkpoint()
         if self.ps.is_cuda:
             torch.cuda.synchronize(self.ps.device)
         return time.perf_counter() - t0

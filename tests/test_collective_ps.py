@@ -147,3 +147,40 @@ def test_tracer_records_phases(tmp_path):
     assert [r["step"] for r in recs] == [0, 1, 2]
     for k in ("forward_ms", "backward_ms", "finish_ms", "comm_ms"):
         assert k in recs[-1] and recs[-1][k] >= 0
+
+
+def _ckpt_worker(rank, world, port, prefix, phase, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    spec = models.build("mlp", torch.device("cpu"), torch.float32, hidden=64)
+    ps = CollectivePS(spec.model, OptimConfig(**CFG), TorchDistTransport(), staleness=1, bucket_mb=0.0005,
+                      grad_dtype=torch.float32, param_dtype=torch.float32)
+    tr = Trainer(spec.model, spec.loss, ps, spec.make_batch(16, torch.device("cpu"), seed=rank))
+    if phase == "save":
+        for _ in range(2):
+            tr.step()
+        th = ps.save(prefix, blocking=False)
+        th.join()
+        ps.export_reference(prefix + ".ref.ckpt", epoch=1, iteration=2)
+    else:
+        ps.load(prefix)
+    for _ in range(2):
+        tr.step()
+    if rank == 0:
+        torch.save({n: p.detach().clone() for n, p in spec.model.named_parameters()}, out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.slow
+def test_sharded_checkpoint_resume_is_exact(tmp_path, C):
+    prefix = str(tmp_path / "ck")
+    mp.spawn(_ckpt_worker, args=(2, _port(), prefix, "save", str(tmp_path / "a.pt")), nprocs=2, join=True)
+    mp.spawn(_ckpt_worker, args=(2, _port(), prefix, "load", str(tmp_path / "b.pt")), nprocs=2, join=True)
+    a = torch.load(str(tmp_path / "a.pt"), weights_only=True)
+    b = torch.load(str(tmp_path / "b.pt"), weights_only=True)
+    for n in a:
+        torch.testing.assert_close(a[n], b[n], rtol=0, atol=0, msg=n)
+    epoch, it, names, shapes, _, data = C.load_reference_ckpt(prefix + ".ref.ckpt")
+    assert (epoch, it) == (1, 2) and "fc1.weight" in names

@@ -257,3 +257,35 @@ def test_native_checkpoint_crc_and_atomicity(C, tmp_path):
     open(p, "wb").write(bytes(raw))
     with pytest.raises(RuntimeError, match="checksum"):
         C.load_native_ckpt(p)
+
+
+def test_run_config_yaml_and_json(tmp_path):
+    import argparse
+
+    from parameter_server_distributed_amd.utils.config import apply_config
+
+    y = tmp_path / "r.yaml"
+    y.write_text("ps-shards: 4\nstaleness: 2\n")
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ps-shards", type=int, default=2)
+    ap.add_argument("--staleness", type=int, default=1)
+    apply_config(ap, ["--config", str(y), "--staleness", "3"])
+    a = ap.parse_args(["--config", str(y), "--staleness", "3"])
+    assert (a.ps_shards, a.staleness) == (4, 3)  # file sets defaults, flags win
+    j = tmp_path / "r.json"
+    j.write_text('{"bogus": 1}')
+    ap2 = argparse.ArgumentParser()
+    with pytest.raises(SystemExit):
+        apply_config(ap2, ["--config", str(j)])
+
+
+def test_shipped_configs_parse():
+    import glob
+    import os
+
+    from parameter_server_distributed_amd.utils.config import load_config
+
+    files = glob.glob(os.path.join(os.path.dirname(__file__), "..", "configs", "*.yaml"))
+    assert files
+    for f in files:
+        assert "model" in load_config(f)
