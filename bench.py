@@ -70,6 +70,8 @@ def parse():
     ap.add_argument("--benchmark-miopen", type=int, default=1, help="torch.backends.cudnn.benchmark")
     ap.add_argument("--out", default="", help="also write the JSON line to this file")
     ap.add_argument("--trace", default="", help="per-step phase trace (JSON lines, one file per rank); eager")
+    ap.add_argument("--push-mode", default="p2p", choices=["auto", "reduce", "p2p"],
+                    help="push/pull when PS shards < ranks: grouped send/recv (p2p) or RCCL reduce/broadcast")
     ap.add_argument("--ckpt-prefix", default="", help="sharded PS checkpoint path prefix")
     ap.add_argument("--ckpt-every", type=int, default=0, help="checkpoint every N steps (async, off the step)")
     ap.add_argument("--resume", default="", help="load PS shards from this checkpoint prefix before training")
@@ -110,7 +112,8 @@ def main():
         shards = max(1, min(a.ps_shards, world))
     pull_dtype = a.pull_dtype or ("fp8" if a.model.startswith("wide") else "bf16")
     ps = CollectivePS(spec.model, optim, transport, num_shards=shards, staleness=a.staleness, bucket_mb=a.bucket_mb,
-                      device=dev, overlap=not spec.tied_weights, pull_dtype=pull_dtype, **kw)
+                      device=dev, overlap=not spec.tied_weights, pull_dtype=pull_dtype,
+                      push_mode=a.push_mode, **kw)
     n_workers = len(ps.worker_ranks)
     batch = spec.make_batch(a.batch, dev, seed=rank)
     use_graph = (world == 1) if a.graph < 0 else bool(a.graph)

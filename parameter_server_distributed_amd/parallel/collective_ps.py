@@ -35,6 +35,7 @@ import torch
 import torch.nn as nn
 
 from .. import native
+from ..ops import multi_reduce_
 from ..ops.optim import OptimConfig, OptimDyn, advance_, apply_no_advance_
 from .transport import LocalTransport, Transport
 
@@ -74,7 +75,7 @@ class CollectivePS:
                  overlap: bool = True, grad_dtype: torch.dtype = torch.bfloat16,
                  param_dtype: torch.dtype = torch.bfloat16, device: torch.device | None = None,
                  ps_ranks: list[int] | None = None, worker_ranks: list[int] | None = None,
-                 pull_dtype: str = "bf16"):
+                 pull_dtype: str = "bf16", push_mode: str = "auto"):
         self.model = model
         self.cfg = optim
         self.t = transport or LocalTransport()
@@ -97,6 +98,16 @@ class CollectivePS:
             raise ValueError(f"invalid PS ranks {self.owners} for world {self.world}")
         self.my_shards = [k for k, r in enumerate(self.owners) if r == self.rank]
         self.collective_rs = self.owners == list(range(self.world))  # every rank owns its slice
+        # push when not every rank owns a slice: "reduce" = one RCCL reduce per slice onto its owner
+        # (a ring through every rank); "p2p" = grouped send of slice k from each worker straight to
+        # owner k into a per-worker inbox, summed by the fused apply's multi-source reduce (the
+        # SURVEY 5.8 plan for PS shards that are fewer than / disjoint from the workers).
+        if push_mode not in ("auto", "reduce", "p2p"):
+            raise ValueError(f"push_mode must be auto|reduce|p2p, got {push_mode}")
+        self.push_p2p = (not self.collective_rs) and self.world > 1 and push_mode == "p2p"
+        self.remote_workers = [w for w in self.worker_ranks if w != self.rank]
+        if self.push_p2p and len(self.worker_ranks) > 16:
+            raise ValueError("p2p push sums at most 16 worker sources per shard")
         self.S = int(staleness)
         self.overlap = overlap
         self.device = device or next(model.parameters()).device
@@ -160,6 +171,9 @@ class CollectivePS:
         self.slots = [torch.zeros(max(self.local_total, ALIGN), dtype=grad_dtype, device=dev)
                       for _ in range(self.S + 1)] if self.S > 0 else []
         self.dyn = OptimDyn(dev, lr=optim.lr, grad_scale=1.0 / len(self.worker_ranks))
+        # p2p inbox: one slice per (owned shard, remote worker)
+        self.inbox = torch.zeros(max(self.local_total * len(self.remote_workers), ALIGN), dtype=grad_dtype,
+                                 device=dev) if self.push_p2p and self.my_shards else None
         # fp8 pull (Wide-ResNet fp8-weights config): owners quantise their fp32 master slices to OCP
         # e4m3fn with a per-(bucket, shard) amax scale; the all-gather moves 1 byte/param (half of
         # bf16) and every rank dequantises into its bf16 working buffer.
@@ -321,8 +335,36 @@ class CollectivePS:
                 out.append(self.slots[slot].narrow(0, b.local_offset + j * b.slice_numel, b.slice_numel))
         return out
 
+    def _inbox_views(self, b: Bucket, j: int):
+        n = b.slice_numel
+        base = (b.local_offset + j * n) * len(self.remote_workers)
+        return [self.inbox.narrow(0, base + i * n, n) for i in range(len(self.remote_workers))]
+
+    def _push_p2p(self, b: Bucket, slot: int | None):
+        """Workers send slice k to owner k; owners receive one slice per remote worker."""
+        g = self.grads_flat.narrow(0, b.offset, b.numel)
+        sends, recvs = [], []
+        if self.is_worker:
+            for k, owner in enumerate(self.owners):
+                if owner != self.rank:
+                    sends.append((g.narrow(0, k * b.slice_numel, b.slice_numel), owner))
+        for j, k in enumerate(self.my_shards):
+            recvs += list(zip(self._inbox_views(b, j), self.remote_workers))
+        self.t.exchange(sends, recvs)
+        self._p2p_sources = {}
+        for j, k in enumerate(self.my_shards):
+            srcs = self._inbox_views(b, j)
+            if self.is_worker:
+                srcs.append(g.narrow(0, k * b.slice_numel, b.slice_numel))
+            if slot is None:
+                self._p2p_sources[j] = srcs  # S = 0: summed inside the fused apply
+            else:
+                multi_reduce_(self.slots[slot].narrow(0, b.local_offset + j * b.slice_numel, b.slice_numel), srcs)
+
     def _push(self, b: Bucket, slot: int | None):
         g = self.grads_flat.narrow(0, b.offset, b.numel)
+        if self.push_p2p:
+            return self._push_p2p(b, slot)
         if self.world == 1:
             if slot is not None:
                 self._owned_grad_views(b, slot)[0].copy_(g)
@@ -344,6 +386,8 @@ class CollectivePS:
             advance_(self.cfg, self.dyn)
             self._advanced = True
         for j, (k, gv) in enumerate(zip(self.my_shards, self._owned_grad_views(b, slot))):
+            if self.push_p2p and slot is None:
+                gv = self._p2p_sources[j]
             lo = b.local_offset + j * b.slice_numel
             m = self.master.narrow(0, lo, b.slice_numel)
             s1 = None if self.state1 is None else self.state1.narrow(0, lo, b.slice_numel)
@@ -392,6 +436,16 @@ class CollectivePS:
             return
         if self.collective_rs:
             self.t.all_gather(w.narrow(0, self.rank * b.slice_numel, b.slice_numel), w)
+        elif self.push_p2p:
+            # each owner sends its slice to every other rank directly (one xGMI link per peer)
+            sends, recvs = [], []
+            for k, owner in enumerate(self.owners):
+                sl = w.narrow(0, k * b.slice_numel, b.slice_numel)
+                if owner == self.rank:
+                    sends += [(sl, r) for r in range(self.world) if r != self.rank]
+                else:
+                    recvs.append((sl, owner))
+            self.t.exchange(sends, recvs)
         else:
             for k, owner in enumerate(self.owners):
                 self.t.broadcast(w.narrow(0, k * b.slice_numel, b.slice_numel), owner)

@@ -46,6 +46,14 @@ class Transport:
     def recv(self, t: torch.Tensor, peer: int) -> None:
         raise NotImplementedError
 
+    def exchange(self, sends, recvs) -> None:
+        """Grouped point-to-point: every (tensor, peer) in ``sends`` / ``recvs`` in one batch."""
+        with self.group():
+            for t, p in sends:
+                self.send(t, p)
+            for t, p in recvs:
+                self.recv(t, p)
+
     def group(self):
         return _NullCtx()
 
@@ -131,6 +139,13 @@ class TorchDistTransport(Transport):
 
     def recv(self, t, peer):
         dist.recv(t, src=self._g(peer), group=self.group_)
+
+    def exchange(self, sends, recvs):
+        ops = [dist.P2POp(dist.isend, t, self._g(p), self.group_) for t, p in sends] + \
+              [dist.P2POp(dist.irecv, t, self._g(p), self.group_) for t, p in recvs]
+        if ops:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
 
 
 class RcclTransport(Transport):

@@ -25,7 +25,7 @@ def _port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, shards, stale, out, disjoint=False):
+def _worker(rank, world, port, shards, stale, out, disjoint=False, push_mode="auto"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.manual_seed(0)
@@ -34,7 +34,7 @@ def _worker(rank, world, port, shards, stale, out, disjoint=False):
     if disjoint:  # first half workers, second half PS shards
         kw = dict(worker_ranks=list(range(world // 2)), ps_ranks=list(range(world // 2, world)))
     ps = CollectivePS(spec.model, OptimConfig(**CFG), TorchDistTransport(), num_shards=shards, staleness=stale,
-                      bucket_mb=0.0005, grad_dtype=torch.float32, param_dtype=torch.float32, **kw)
+                      bucket_mb=0.0005, grad_dtype=torch.float32, param_dtype=torch.float32, push_mode=push_mode, **kw)
     assert len(ps.buckets) > 1
     tr = Trainer(spec.model, spec.loss, ps, spec.make_batch(16, torch.device("cpu"), seed=rank))
     for _ in range(STEPS):
@@ -98,6 +98,18 @@ def test_gloo_disjoint_placement_2_workers_2_ps(tmp_path):
     for n in want:
         torch.testing.assert_close(got["params"][n], want[n], rtol=1e-5, atol=1e-6, msg=n)
     assert sum(got["hist"]) == 0  # rank 0 is a pure worker: it owns no shard
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("disjoint,shards,stale", [(True, 2, 0), (True, 2, 1), (False, 1, 0), (False, 2, 2)])
+def test_gloo_p2p_push_matches_reference(tmp_path, disjoint, shards, stale):
+    """Grouped send/recv push into per-worker inboxes + multi-source fused apply."""
+    out = str(tmp_path / "r0.pt")
+    mp.spawn(_worker, args=(4, _port(), shards, stale, out, disjoint, "p2p"), nprocs=4, join=True)
+    got = torch.load(out, weights_only=True)
+    want = _reference(2 if disjoint else 4, stale)
+    for n in want:
+        torch.testing.assert_close(got["params"][n], want[n], rtol=1e-5, atol=1e-6, msg=n)
 
 
 def test_world1_local_matches_reference():
