@@ -45,6 +45,11 @@ METRICS = {
     "resnet101": ("samples/sec (whole node) ResNet-101", "samples/s"),
     "mlp": ("samples/sec (whole node) 2-layer MLP", "samples/s"),
 }
+# Reference-semantics baseline (tools/reference_baseline.py, measured on 1x MI355X: the same worker
+# model on the GPU, gRPC `repeated float` fp32 tensors, one host-memory PS, sync barrier, p -= g),
+# samples/s per worker GPU. vs_baseline divides by this x n_workers, i.e. it credits the reference
+# with perfect scaling (its single PS would in fact serialize N workers).
+REF_BASELINE = {"resnet50": 285.119}
 DEFAULT_BATCH = {"resnet50": 512, "bert_base": 64, "wide_resnet101_2": 128, "resnet101": 256, "mlp": 4096}
 
 
@@ -176,7 +181,8 @@ def main():
         rec = {
             "metric": metric, "value": round(value, 2), "unit": unit, "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "bf16", "data": data,
+            "vs_baseline": (round(value / (REF_BASELINE[a.model] * n_workers), 2)
+                            if a.model in REF_BASELINE else None), "dtype": "bf16", "data": data,
             "config": {"model": a.model, "global_batch": a.batch * n_workers, "per_gpu_batch": a.batch,
                        "seq_len": a.seq_len if a.model.startswith("bert") else None,
                        "image_size": None if a.model.startswith("bert") else a.image_size,

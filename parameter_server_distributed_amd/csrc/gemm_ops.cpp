@@ -90,7 +90,7 @@ void colsum_(const at::Tensor& x, at::Tensor out, bool accumulate) {
   TORCH_CHECK(out.numel() == N && out.is_contiguous(), "psd colsum: out [N]");
   const c10::DeviceGuard g(x.device());
   TORCH_CHECK(out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat, "psd colsum: out dtype");
-  at::Tensor part = at::empty({64 * N}, x.options().dtype(at::kFloat));
+  at::Tensor part = at::empty({512 * N}, x.options().dtype(at::kFloat));
   hipError_t e = launch_colsum(reinterpret_cast<const uint16_t*>(x.data_ptr()), M, (int)N, part.data_ptr<float>(),
                                out.data_ptr(), out.scalar_type() == at::kBFloat16, accumulate, stream_of(x));
   TORCH_CHECK(e == hipSuccess, "psd colsum: ", hipGetErrorString(e));

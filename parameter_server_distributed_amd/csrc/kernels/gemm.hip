@@ -307,6 +307,69 @@ __device__ __forceinline__ void glds_stage(const uint16_t* __restrict__ src, int
 }
 }  // namespace
 
+// Epilogue of the 256x256 kernels: fp32 slab / fp32 C direct stores, or bf16 C (+bias, +act)
+// staged through LDS and written as 16-byte row chunks.
+template <int MODE>
+__device__ __forceinline__ void big_epilogue(const GemmArgs& g, f32x16 (&acc)[4][2], int m0, int n0, int wm, int wn,
+                                             int lane, uint8_t* smem) {
+  const int hl = lane >> 5, cl = lane & 31;
+  if (MODE == 1 || g.c_f32) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wn * 64 + j * 32 + cl;
+      if (n >= g.N) continue;
+      const float bias = (MODE == 0 && g.bias) ? bf16_to_f32(reinterpret_cast<const uint16_t*>(g.bias)[n]) : 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+          if (m >= g.M) continue;
+          if (MODE == 1) {
+            reinterpret_cast<float*>(g.C)[(int64_t)blockIdx.z * g.M * g.N + (int64_t)m * g.N + n] = acc[i][j][r];
+          } else {
+            float v = acc[i][j][r] + bias;
+            if (g.act == 1) v = fmaxf(v, 0.f);
+            else if (g.act == 2) v = gelu_tanh(v);
+            reinterpret_cast<float*>(g.C)[(int64_t)m * g.ldc + n] = v;
+          }
+        }
+    }
+    return;
+  }
+  uint16_t* cs = reinterpret_cast<uint16_t*>(smem);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int nl = wn * 64 + j * 32 + cl;
+    const int n = n0 + nl;
+    const float bias = (g.bias && n < g.N) ? bf16_to_f32(reinterpret_cast<const uint16_t*>(g.bias)[n]) : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ml = wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+        float v = acc[i][j][r] + bias;
+        if (g.act == 2 && g.aux && n < g.N && m0 + ml < g.M)
+          reinterpret_cast<uint16_t*>(g.aux)[(int64_t)(m0 + ml) * g.ldc + n] = f32_to_bf16(v);
+        if (g.act == 1) v = fmaxf(v, 0.f);
+        else if (g.act == 2) v = gelu_tanh(v);
+        cs[ml * kBigLdc + nl] = f32_to_bf16(v);
+      }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < kBig * (kBig / 8); c += 512) {
+    const int ml = c >> 5, nl = (c & 31) * 8;
+    const int m = m0 + ml, n = n0 + nl;
+    if (m >= g.M || n >= g.N) continue;
+    uint16_t* o = reinterpret_cast<uint16_t*>(g.C) + (int64_t)m * g.ldc + n;
+    const uint16_t* src = cs + ml * kBigLdc + nl;
+    if (n + 8 <= g.N && ((reinterpret_cast<uintptr_t>(o) & 15) == 0))
+      *reinterpret_cast<u32x4*>(o) = *reinterpret_cast<const u32x4*>(src);
+    else
+      for (int e = 0; e < 8 && n + e < g.N; ++e) o[e] = src[e];
+  }
+}
+
 template <bool AK, bool BKM, int MODE>
 __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -368,62 +431,127 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g) {
     __builtin_amdgcn_s_barrier();  // every wave done reading `cur` before it is re-filled
   }
 
-  const int hl = lane >> 5, cl = lane & 31;
-  if (MODE == 1 || g.c_f32) {
+  big_epilogue<MODE>(g, acc, m0, n0, wm, wn, lane, smem);
+}
+
+// ---------------------------------------------------------------------------------------------
+// 256x256 tile, ring-pipelined: the K loop runs over half-stages of 32 k (A 16 KiB + B 16 KiB),
+// kept in a 4-slot LDS ring (128 KiB). Three half-stages are in flight ahead of the one being
+// multiplied; one raw s_barrier per half-stage both publishes slot h (after this wave's counted
+// vmcnt) and releases slot h-1 for the DMA of half-stage h+3. Per half-stage each wave issues 12
+// (K-major) fragment reads and 16 v_mfma_f32_32x32x16_bf16, the MFMA cluster fenced with
+// s_setprio (cdna_hip_programming.md T5). K-major half-stage image: [256 rows][32 k] (64-B rows,
+// 16-B chunk XOR (row>>2)&3: conflict-free for the ds_read_b128 lane groups); M/N-major:
+// [32 k][256] read with ds_read_b64_tr_b16 (same image as the 2-stage kernel, 32 k-rows).
+namespace {
+constexpr int kHalfK = 32;
+constexpr int kHalfOp = kBig * kHalfK * 2;  // 16 KiB per operand per half-stage
+constexpr int kHalfSlot = 2 * kHalfOp;      // A + B
+
+__device__ __forceinline__ int kmaj32_off(int row, int c) { return row * 64 + ((c ^ ((row >> 2) & 3)) << 4); }
+
+template <bool KMAJ>
+__device__ __forceinline__ void glds_half(const uint16_t* __restrict__ src, int ld, int nrows, int r0, int k0,
+                                          uint8_t* lds, int wid, int lane) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = n0 + wn * 64 + j * 32 + cl;
-      if (n >= g.N) continue;
-      const float bias = (MODE == 0 && g.bias) ? bf16_to_f32(reinterpret_cast<const uint16_t*>(g.bias)[n]) : 0.f;
+  for (int i = 0; i < 2; ++i) {
+    const int piece = i * 8 + wid;  // 16 x 1 KiB pieces per operand half-stage
+    const uint16_t* gp;
+    if (KMAJ) {  // a piece is 16 rows x 64 B
+      const int row = piece * 16 + (lane >> 2);
+      const int c = (lane & 3) ^ ((row >> 2) & 3);
+      const int gr = min(r0 + row, nrows - 1);
+      gp = src + (int64_t)gr * ld + k0 + c * 8;
+    } else {  // a piece is 2 k-rows x 512 B
+      const int k = piece * 2 + (lane >> 5);
+      const int col = ((lane & 31) * 8) ^ ((k & 3) << 5);
+      const int gc = min(r0 + col, nrows - 8);
+      gp = src + (int64_t)(k0 + k) * ld + gc;
+    }
+    __builtin_amdgcn_global_load_lds((const void*)gp, (__attribute__((address_space(3))) void*)(lds + piece * 1024), 16,
+                                     0, 0);
+  }
+}
+
+template <bool KMAJ>
+__device__ __forceinline__ bf16x8 frag_half(const uint8_t* lds, int r0, int ks, int lane) {
+  if (KMAJ) {
+    const int row = r0 + (lane & 31);
+    const u32x4 w = *reinterpret_cast<const u32x4*>(lds + kmaj32_off(row, ks * 2 + (lane >> 5)));
+    return __builtin_bit_cast(bf16x8, w);
+  } else {
+    return frag<kBig, false>(lds, r0, ks);
+  }
+}
+}  // namespace
+
+template <bool AK, bool BKM, int MODE>
+__global__ __launch_bounds__(512) void gemm256r_kernel(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int tiles_n = (g.N + kBig - 1) / kBig;
+  const int tiles_m = (g.M + kBig - 1) / kBig;
+  const int wg = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int m0 = (wg / tiles_n) * kBig, n0 = (wg % tiles_n) * kBig;
+  int kbeg = 0, kend = g.K;
+  if (MODE == 1) {
+    kbeg = blockIdx.z * g.k_per_split;
+    kend = min(g.K, kbeg + g.k_per_split);
+  }
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid >> 2, wn = wid & 3;
+  const uint16_t* A = reinterpret_cast<const uint16_t*>(g.A);
+  const uint16_t* B = reinterpret_cast<const uint16_t*>(g.B);
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nh = (kend - kbeg) / kHalfK;
+  auto stage = [&](int h) {
+    uint8_t* slot = smem + (h & 3) * kHalfSlot;
+    glds_half<AK>(A, g.lda, g.M, m0, kbeg + h * kHalfK, slot, wid, lane);
+    glds_half<BKM>(B, g.ldb, g.N, n0, kbeg + h * kHalfK, slot + kHalfOp, wid, lane);
+  };
+#pragma unroll
+  for (int p = 0; p < 3; ++p)
+    if (p < nh) stage(p);
+  for (int h = 0; h < nh; ++h) {
+    // half-stage h landed (this wave's DMA): leave min(2, nh-1-h) half-stages (4 DMA each) in flight
+    const int ahead = nh - 1 - h;
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave: slot h published, slot h-1 no longer read
+    __builtin_amdgcn_sched_barrier(0);
+    if (h + 3 < nh) stage(h + 3);
+    const uint8_t* As = smem + (h & 3) * kHalfSlot;
+    const uint8_t* Bs = As + kHalfOp;
+    bf16x8 af[2][4], bfr[2][2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bfr[ks][j] = frag_half<BKM>(Bs, wn * 64 + j * 32, ks, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[ks][i] = frag_half<AK>(As, wm * 128 + i * 32, ks, lane);
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = m0 + wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-          if (m >= g.M) continue;
-          if (MODE == 1) {
-            reinterpret_cast<float*>(g.C)[(int64_t)blockIdx.z * g.M * g.N + (int64_t)m * g.N + n] = acc[i][j][r];
-          } else {
-            float v = acc[i][j][r] + bias;
-            if (g.act == 1) v = fmaxf(v, 0.f);
-            else if (g.act == 2) v = gelu_tanh(v);
-            reinterpret_cast<float*>(g.C)[(int64_t)m * g.ldc + n] = v;
-          }
-        }
-    }
-    return;
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ks][i], bfr[ks][j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
   }
-  uint16_t* cs = reinterpret_cast<uint16_t*>(smem);
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int nl = wn * 64 + j * 32 + cl;
-    const int n = n0 + nl;
-    const float bias = (g.bias && n < g.N) ? bf16_to_f32(reinterpret_cast<const uint16_t*>(g.bias)[n]) : 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int ml = wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-        float v = acc[i][j][r] + bias;
-        if (g.act == 2 && g.aux && n < g.N && m0 + ml < g.M)
-          reinterpret_cast<uint16_t*>(g.aux)[(int64_t)(m0 + ml) * g.ldc + n] = f32_to_bf16(v);
-        if (g.act == 1) v = fmaxf(v, 0.f);
-        else if (g.act == 2) v = gelu_tanh(v);
-        cs[ml * kBigLdc + nl] = f32_to_bf16(v);
-      }
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < kBig * (kBig / 8); c += 512) {
-    const int ml = c >> 5, nl = (c & 31) * 8;
-    const int m = m0 + ml, n = n0 + nl;
-    if (m >= g.M || n >= g.N) continue;
-    uint16_t* o = reinterpret_cast<uint16_t*>(g.C) + (int64_t)m * g.ldc + n;
-    const uint16_t* src = cs + ml * kBigLdc + nl;
-    if (n + 8 <= g.N && ((reinterpret_cast<uintptr_t>(o) & 15) == 0))
-      *reinterpret_cast<u32x4*>(o) = *reinterpret_cast<const u32x4*>(src);
-    else
-      for (int e = 0; e < 8 && n + e < g.N; ++e) o[e] = src[e];
-  }
+  __builtin_amdgcn_s_barrier();  // the epilogue reuses the ring
+  big_epilogue<MODE>(g, acc, m0, n0, wm, wn, lane, smem);
 }
 
 // out = (accumulate ? out : 0) + sum_s slab[s]   (M*N elements, 8 per lane)
@@ -481,7 +609,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 
 // column sums of a [M][N] bf16 matrix (bias gradient), deterministic two-pass: block partials
 // (lane = 8 columns, 4 rows in flight) -> one finalize lane per column summing <= 64 partial rows.
-constexpr int kColsumMaxBlocks = 64;
+constexpr int kColsumMaxBlocks = 512;  // partial rows (the caller's workspace is [512 * N] fp32)
 __global__ __launch_bounds__(256) void colsum_partial_kernel(const uint16_t* __restrict__ x, int64_t M, int N,
                                                              float* __restrict__ part) {
   const int tpc = N >> 3;
@@ -525,12 +653,20 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const uint16_t* __r
   }
 }
 
+// Deterministic second pass: block = 32 columns x 8 partial-row lanes; fixed summation order.
 __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ part, int nblk, int N, void* out,
                                                            int out_bf16, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= N) return;
+  const int cl = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
   float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += part[(int64_t)b * N + c];
+  if (c < N)
+    for (int b = rl; b < nblk; b += 8) s += part[(int64_t)b * N + c];
+  __shared__ float red[8][33];
+  red[rl][cl] = s;
+  __syncthreads();
+  if (rl != 0 || c >= N) return;
+#pragma unroll
+  for (int r = 1; r < 8; ++r) s += red[r][cl];
   if (out_bf16) {
     uint16_t* o = reinterpret_cast<uint16_t*>(out);
     o[c] = f32_to_bf16(s + (accumulate ? bf16_to_f32(o[c]) : 0.f));
@@ -555,17 +691,29 @@ static hipError_t launch_t(const GemmArgs& g, int splits, hipStream_t st) {
   return hipGetLastError();
 }
 
+static bool use_ring() {
+  static const int v = [] {
+    const char* e = getenv("PSD_GEMM_RING");
+    return e ? atoi(e) : 1;
+  }();
+  return v != 0;
+}
+
 template <bool AK, bool BKM, int MODE>
 static hipError_t launch_big(const GemmArgs& g, int splits, hipStream_t st) {
-  static bool attr_set = false;  // one instantiation per template: set the >64 KiB LDS limit once
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm256_kernel<AK, BKM, MODE>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, kBigLds);
+  const bool ring = use_ring();
+  const void* fn = ring ? (const void*)gemm256r_kernel<AK, BKM, MODE> : (const void*)gemm256_kernel<AK, BKM, MODE>;
+  static bool attr_set[2] = {false, false};  // per instantiation: set the >64 KiB LDS limit once
+  if (!attr_set[ring]) {
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kBigLds);
     if (e != hipSuccess) return e;
-    attr_set = true;
+    attr_set[ring] = true;
   }
   const int nwg = ((g.M + kBig - 1) / kBig) * ((g.N + kBig - 1) / kBig);
-  hipLaunchKernelGGL((gemm256_kernel<AK, BKM, MODE>), dim3(nwg, 1, splits), dim3(512), kBigLds, st, g);
+  if (ring)
+    hipLaunchKernelGGL((gemm256r_kernel<AK, BKM, MODE>), dim3(nwg, 1, splits), dim3(512), kBigLds, st, g);
+  else
+    hipLaunchKernelGGL((gemm256_kernel<AK, BKM, MODE>), dim3(nwg, 1, splits), dim3(512), kBigLds, st, g);
   return hipGetLastError();
 }
 
@@ -645,11 +793,15 @@ hipError_t launch_colsum(const uint16_t* x, int64_t M, int N, float* part, void*
   const int tpc = N / 8;
   const int gy = tpc >= 256 ? (tpc + 255) / 256 : 1;
   const int rpi = tpc >= 256 ? 1 : 256 / tpc;
-  int64_t gx = (M + (int64_t)rpi * 16 - 1) / ((int64_t)rpi * 16);
+  // enough row-chunks to fill the chip (~1024 resident blocks over all column groups), each
+  // thread summing >= 8 rows
+  int64_t gx = (M + (int64_t)rpi * 8 - 1) / ((int64_t)rpi * 8);
+  const int64_t want = (1024 + gy - 1) / gy;
+  if (gx > want) gx = want;
   if (gx > kColsumMaxBlocks) gx = kColsumMaxBlocks;
   if (gx < 1) gx = 1;
   hipLaunchKernelGGL(colsum_partial_kernel, dim3((unsigned)gx, gy), dim3(256), 0, st, x, M, N, part);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3((N + 255) / 256), dim3(256), 0, st, part, (int)gx, N, out, out_bf16,
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((N + 31) / 32), dim3(256), 0, st, part, (int)gx, N, out, out_bf16,
                      accumulate);
   return hipGetLastError();
 }

@@ -24,7 +24,7 @@ int gemm_splits(int M, int N, int K);
 // split-K GEMM into fp32 slabs [splits][M][N], then out = (acc ? out : 0) + scale * sum(slabs)
 hipError_t launch_gemm_splitk(const GemmArgs& g, float* slab, int splits, void* out, int out_bf16, int accumulate,
                               float scale, hipStream_t stream);
-// out[n] (+)= sum_m x[m][n]; part is an fp32 [64 * N] scratch
+// out[n] (+)= sum_m x[m][n]; part is an fp32 [512 * N] scratch
 hipError_t launch_colsum(const uint16_t* x, int64_t M, int N, float* part, void* out, int out_bf16,
                          int accumulate, hipStream_t stream);
 

@@ -78,6 +78,18 @@ def test_colsum(gpu):
     torch.testing.assert_close(o32.cpu(), x.float().sum(0), rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("shape", [(8192, 768), (8192, 3072), (8192, 4096), (37, 2056), (100000, 64)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_colsum_shapes_deterministic(gpu, shape):
+    x = torch.randn(*shape, device=gpu).to(torch.bfloat16)
+    o1 = torch.zeros(shape[1], device=gpu)
+    o2 = torch.zeros(shape[1], device=gpu)
+    native().colsum_(x, o1, False)
+    native().colsum_(x, o2, False)
+    assert torch.equal(o1, o2)
+    torch.testing.assert_close(o1.cpu(), x.float().sum(0).cpu(), rtol=1e-4, atol=2e-3)
+
+
 @pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, False), (False, True)],
                          ids=["NT", "NN", "TN", "TT"])
 @pytest.mark.parametrize("shape", [(2048, 2048, 256), (2000, 2120, 320), (2304, 4096, 768)],
