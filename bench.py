@@ -75,8 +75,9 @@ def parse():
     ap.add_argument("--benchmark-miopen", type=int, default=1, help="torch.backends.cudnn.benchmark")
     ap.add_argument("--out", default="", help="also write the JSON line to this file")
     ap.add_argument("--trace", default="", help="per-step phase trace (JSON lines, one file per rank); eager")
-    ap.add_argument("--push-mode", default="p2p", choices=["auto", "reduce", "p2p"],
-                    help="push/pull when PS shards < ranks: grouped send/recv (p2p) or RCCL reduce/broadcast")
+    ap.add_argument("--push-mode", default="reduce", choices=["auto", "reduce", "p2p"],
+                    help="push/pull when PS shards < ranks: RCCL reduce/broadcast per slice (default) or "
+                         "grouped send/recv into per-worker inboxes (p2p)")
     ap.add_argument("--ckpt-prefix", default="", help="sharded PS checkpoint path prefix")
     ap.add_argument("--ckpt-every", type=int, default=0, help="checkpoint every N steps (async, off the step)")
     ap.add_argument("--resume", default="", help="load PS shards from this checkpoint prefix before training")

@@ -36,6 +36,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("aux") = py::none());
   m.def("gemm_splitk_", &gemm_splitk_, py::arg("A"), py::arg("B"), py::arg("a_kmajor"), py::arg("b_kmajor"),
         py::arg("out"), py::arg("accumulate") = false, py::arg("scale") = 1.0, py::arg("splits") = 0);
+  m.def("gemm_fp8_", &gemm_fp8_, py::arg("A"), py::arg("B"), py::arg("a_scale"), py::arg("b_scale"), py::arg("out"),
+        py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("aux") = py::none());
   m.def("colsum_", &colsum_, py::arg("x"), py::arg("out"), py::arg("accumulate") = false);
   m.def("maxpool3s2_fwd", &maxpool3s2_fwd);
   m.def("maxpool3s2_bwd", &maxpool3s2_bwd);

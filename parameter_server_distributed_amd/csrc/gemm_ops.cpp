@@ -82,6 +82,44 @@ void gemm_splitk_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool 
   TORCH_CHECK(e == hipSuccess, "psd gemm_splitk: ", hipGetErrorString(e));
 }
 
+// out[M,N] = (A_q . B_q^T) * a_scale * b_scale (+bias)(act): A [M,K], B [N,K] OCP e4m3fn, K % 128 == 0
+void gemm_fp8_(const at::Tensor& A, const at::Tensor& B, const at::Tensor& a_scale, const at::Tensor& b_scale,
+               at::Tensor out, c10::optional<at::Tensor> bias, int64_t act, c10::optional<at::Tensor> aux) {
+  for (const at::Tensor* t : {&A, &B})
+    TORCH_CHECK(t->is_cuda() && t->dim() == 2 && t->scalar_type() == at::kFloat8_e4m3fn && t->stride(1) == 1 &&
+                    t->stride(0) % 16 == 0 && (reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0,
+                "psd gemm_fp8: operands must be 2-D e4m3fn device tensors, unit inner stride, 16-B aligned rows");
+  const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
+  TORCH_CHECK(B.size(1) == K, "psd gemm_fp8: K mismatch");
+  TORCH_CHECK(K % 128 == 0, "psd gemm_fp8: K must be a multiple of 128");
+  TORCH_CHECK(a_scale.scalar_type() == at::kFloat && b_scale.scalar_type() == at::kFloat && a_scale.numel() >= 1 &&
+                  b_scale.numel() >= 1 && a_scale.is_cuda() && b_scale.is_cuda(),
+              "psd gemm_fp8: scales must be fp32 device scalars");
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == M && out.size(1) == N && out.stride(1) == 1, "psd gemm_fp8: out shape");
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat, "psd gemm_fp8: out dtype");
+  const c10::DeviceGuard g(A.device());
+  GemmArgs a{};
+  a.A = A.data_ptr();
+  a.B = B.data_ptr();
+  a.C = out.data_ptr();
+  a.bias = (bias.has_value() && bias->defined()) ? bias->data_ptr() : nullptr;
+  if (a.bias) TORCH_CHECK(bias->numel() == N && bias->scalar_type() == at::kBFloat16, "psd gemm_fp8: bias [N] bf16");
+  a.aux = (aux.has_value() && aux->defined()) ? aux->data_ptr() : nullptr;
+  a.M = (int)M;
+  a.N = (int)N;
+  a.K = (int)K;
+  a.lda = (int)A.stride(0);
+  a.ldb = (int)B.stride(0);
+  a.ldc = (int)out.stride(0);
+  a.a_kmajor = a.b_kmajor = 1;
+  a.act = (int)act;
+  a.c_f32 = out.scalar_type() == at::kFloat;
+  a.a_scale = a_scale.data_ptr<float>();
+  a.b_scale = b_scale.data_ptr<float>();
+  hipError_t e = launch_gemm_fp8(a, stream_of(A));
+  TORCH_CHECK(e == hipSuccess, "psd gemm_fp8: ", hipGetErrorString(e));
+}
+
 // out[N] (+)= column sums of x[M,N] (bias gradient)
 void colsum_(const at::Tensor& x, at::Tensor out, bool accumulate) {
   chk2d(x, "x");

@@ -554,6 +554,355 @@ __global__ __launch_bounds__(512) void gemm256r_kernel(GemmArgs g) {
   big_epilogue<MODE>(g, acc, m0, n0, wm, wn, lane, smem);
 }
 
+// ---------------------------------------------------------------------------------------------
+// 256x256 tile, 8-phase ping-pong schedule (cdna_hip_programming.md §5 "256² 8-phase template",
+// T2-T5), v_mfma_f32_16x16x32_bf16. 8 waves = 2 wave rows (wr) x 4 wave cols (wc); each wave owns
+// 128x64 of C as four 64x32 quadrants (qm, qn). A K-tile (64 k) is four phases, one quadrant each:
+//   phase 0: q(0,0)  reads B(qn0) then A(qm0)      stages A-half1 of tile t+1
+//   phase 1: q(0,1)  reads B(qn1)                   stages B-half0 of tile t+2
+//   phase 2: q(1,0)  reads A(qm1)  (B(qn0) kept)    stages A-half0 of tile t+2
+//   phase 3: q(1,1)  no reads                       stages B-half1 of tile t+2, vmcnt(6)
+// The LDS holds two K-tiles, each as four 16 KiB half-tiles: A-half h = the rows of quadrant row h
+// of both wave rows, B-half h = the cols of quadrant col h of all four wave cols, so a half-tile is
+// dead for the whole block as soon as its quadrant has been read. Every phase is
+// {ds_reads, 2 LDS-DMA} -> s_barrier -> 16 MFMA (s_setprio 1) -> s_barrier, and wave row 1 runs one
+// barrier behind wave row 0: the two waves sharing a SIMD alternate between reading and MFMA.
+// RAW: a tile's last half is retired by the counted vmcnt(6) of the phase before its first read.
+// WAR: a half is restaged >= 2 phases after its last read, or 1 phase after when an lgkmcnt before
+// the reading phase's first barrier retired it (phase 0's lgkmcnt(8) retires the B(qn0) reads).
+// Tiles past the end are staged from the last valid K offset (same count of DMA per phase, data
+// never read), so the vmcnt bookkeeping is uniform.
+namespace {
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int mn8_off(int k, int col) {  // M/N-major half image [64 k][128], 256-B rows
+  const int f = (k & 3) | ((k >> 1) & 4);  // the 8 k-rows of one tr-read half-wave hit 8 distinct 32-B slots
+  return k * 256 + ((col ^ (f << 4)) << 1);
+}
+
+// half-tile local row/col -> tile row/col (SEG = quadrant extent: 64 rows of A, 32 cols of B)
+template <int SEG>
+__device__ __forceinline__ int half_to_tile(int r, int h) {
+  return (r / SEG) * (2 * SEG) + h * SEG + (r % SEG);
+}
+
+template <bool KMAJ, int SEG, int ESZ = 2, int PW = 2>
+__device__ __forceinline__ void stage8(const void* __restrict__ srcv, int ld, int nrows, int r0, int k0, int h,
+                                       uint8_t* lds, int wid, int lane) {
+  const uint8_t* src = reinterpret_cast<const uint8_t*>(srcv);  // ld, k0 in elements of ESZ bytes
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    const int piece = i * 8 + wid;  // PW * 8 pieces of 1 KiB per half-tile
+    const uint8_t* gp;
+    if (KMAJ) {  // [128 rows][128 B of k]: a piece is 8 rows x 128 B
+      const int row = piece * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      const int gr = min(r0 + half_to_tile<SEG>(row, h), nrows - 1);
+      gp = src + ((int64_t)gr * ld + k0) * ESZ + c * 16;
+    } else {  // [64 k][128 cols] bf16: a piece is 4 k-rows x 256 B
+      const int k = piece * 4 + (lane >> 4);
+      const int f = (k & 3) | ((k >> 1) & 4);
+      const int col = ((lane & 15) * 8) ^ (f << 4);
+      const int gc = min(r0 + half_to_tile<SEG>(col, h), nrows - 8);
+      gp = src + ((int64_t)(k0 + k) * ld + gc) * ESZ;
+    }
+    __builtin_amdgcn_global_load_lds((const void*)gp, (__attribute__((address_space(3))) void*)(lds + piece * 1024), 16,
+                                     0, 0);
+  }
+}
+
+// 16x16x32 fragment: lane holds row/col (rb*16 + lane&15), k = ks*32 + 8*(lane>>4) + 0..7
+template <bool KMAJ>
+__device__ __forceinline__ bf16x8 frag8(const uint8_t* lds, int rb, int ks, int lane) {
+  if (KMAJ) {
+    const int row = rb * 16 + (lane & 15);
+    const u32x4 w = *reinterpret_cast<const u32x4*>(lds + kmaj_off(row, ks * 4 + (lane >> 4)));
+    return __builtin_bit_cast(bf16x8, w);
+  } else {
+    const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
+    const int k = ks * 32 + 8 * g + q;
+    const int col = rb * 16 + 4 * p;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + mn8_off(k, col)));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + mn8_off(k + 4, col)));
+    s16x4 both[2] = {lo, hi};
+    return __builtin_bit_cast(bf16x8, both);
+  }
+}
+
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+// fp8 (e4m3) 16x16x128 fragment: 32 bytes of one 128-B row = 16-B chunks (lane>>4) and 4+(lane>>4);
+// A and B use the same k order, which is all the dot product needs
+__device__ __forceinline__ i32x8 frag8_f8(const uint8_t* lds, int rb, int lane) {
+  const int row = rb * 16 + (lane & 15);
+  const u32x4 lo = *reinterpret_cast<const u32x4*>(lds + kmaj_off(row, lane >> 4));
+  const u32x4 hi = *reinterpret_cast<const u32x4*>(lds + kmaj_off(row, 4 + (lane >> 4)));
+  return i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  else static_assert(N == 6 || N == 5, "vmcnt");
+}
+template <int N>
+__device__ __forceinline__ void wait_lgkm() {
+  if constexpr (N >= 15) asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
+  else static_assert(N == 8 || N == 4, "lgkmcnt");
+}
+
+// grouped tile order inside one XCD's contiguous range: 4 tile-rows share each B panel
+__device__ __forceinline__ void tile_of(int wg, int tiles_m, int tiles_n, int& tm, int& tn) {
+  constexpr int G = 4;
+  const int per = G * tiles_n;
+  const int grp = wg / per;
+  const int first = grp * G;
+  const int gsz = min(G, tiles_m - first);
+  const int r = wg - grp * per;
+  tm = first + r % gsz;
+  tn = r / gsz;
+}
+}  // namespace
+
+#define PSD_SYNC_OPEN()                              \
+  __builtin_amdgcn_s_barrier();                      \
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
+  __builtin_amdgcn_sched_barrier(0);                 \
+  __builtin_amdgcn_s_setprio(1);
+#define PSD_SYNC_CLOSE()               \
+  __builtin_amdgcn_s_setprio(0);       \
+  __builtin_amdgcn_sched_barrier(0);   \
+  __builtin_amdgcn_s_barrier();        \
+  __builtin_amdgcn_sched_barrier(0);
+
+// BM: 256 (8 waves x 128x64 of C) or 128 (8 waves x 64x64: twice the tiles for narrow problems).
+// F8: A [M][K] and B [N][K] OCP e4m3 (K-major only), K-tile = 128, MX-scaled
+// v_mfma_scale_f32_16x16x128_f8f6f4 with unit block scales (2x the bf16 MFMA rate); the per-tensor
+// dequant factors *a_scale * *b_scale are applied in the epilogue.
+template <int BM>
+struct P8 {
+  static constexpr int IM = BM / 64;         // 16-row blocks per quadrant
+  static constexpr int QA = BM / 4;          // quadrant rows
+  static constexpr int HA = BM / 2 * 128;    // A half-tile bytes
+  static constexpr int HB = 128 * 128;       // B half-tile bytes
+  static constexpr int PWA = HA / 8192;      // A DMA pieces per wave per half-tile
+  static constexpr int VM = 4 + PWA;         // DMA in flight after phase 3 (three half-tiles)
+  static constexpr int BUF = 2 * HA + 2 * HB;
+  static constexpr int LDS = (2 * BUF > BM * kBigLdc * 2) ? 2 * BUF : BM * kBigLdc * 2;
+};
+
+template <int BM, bool AK, bool BKM, int MODE, bool F8 = false>
+__global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
+  static_assert(!F8 || (AK && BKM), "fp8 GEMM takes K-major operands");
+  using P = P8<BM>;
+  constexpr int IM = P::IM;
+  constexpr int KT = F8 ? 128 : BK;  // k per K-tile (128-B LDS rows either way)
+  constexpr int ESZ = F8 ? 1 : 2;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int tiles_n = (g.N + kBig - 1) / kBig;
+  const int tiles_m = (g.M + BM - 1) / BM;
+  const int wg = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  int tm, tn;
+  tile_of(wg, tiles_m, tiles_n, tm, tn);
+  const int m0 = tm * BM, n0 = tn * kBig;
+  int kbeg = 0, kend = g.K;
+  if (MODE == 1) {
+    kbeg = blockIdx.z * g.k_per_split;
+    kend = min(g.K, kbeg + g.k_per_split);
+  }
+  const int nt = (kend - kbeg) / KT;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+
+  f32x4 acc[8 * IM];
+#pragma unroll
+  for (int i = 0; i < 8 * IM; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto half = [&](int t, int idx) {  // idx: 0/1 A-half, 2/3 B-half
+    return smem + (t & 1) * P::BUF + (idx < 2 ? idx * P::HA : 2 * P::HA + (idx - 2) * P::HB);
+  };
+  auto kofs = [&](int t) { return kbeg + min(t, nt - 1) * KT; };
+  auto stA = [&](int t, int h) {
+    stage8<AK, P::QA, ESZ, P::PWA>(g.A, g.lda, g.M, m0, kofs(t), h, half(t, h), wid, lane);
+  };
+  auto stB = [&](int t, int h) { stage8<BKM, 32, ESZ, 2>(g.B, g.ldb, g.N, n0, kofs(t), h, half(t, 2 + h), wid, lane); };
+
+  if (nt > 0) {
+    stB(0, 0);
+    stA(0, 0);
+    stB(0, 1);
+    stA(0, 1);
+    stB(1, 0);
+    stA(1, 0);
+    stB(1, 1);
+    wait_vm<P::VM>();  // tile 0 landed (this wave's DMA)
+  }
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();  // wave row 1 runs one barrier behind
+  __builtin_amdgcn_sched_barrier(0);
+
+  // register subtiles: bf16 [row block][k-step] x 8 elements, or fp8 [row block] x 32 bytes
+  bf16x8 a0[IM][2], a1[IM][2], b0[2][2], b1[2][2];
+  i32x8 fa0[IM], fa1[IM], fb0[2], fb1[2];
+  auto readA = [&](const uint8_t* h, bf16x8 (&a)[IM][2], i32x8 (&fa)[IM]) {
+    if constexpr (F8) {
+#pragma unroll
+      for (int i = 0; i < IM; ++i) fa[i] = frag8_f8(h, wr * IM + i, lane);
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < IM; ++i) a[i][ks] = frag8<AK>(h, wr * IM + i, ks, lane);
+    }
+  };
+  auto readB = [&](const uint8_t* h, bf16x8 (&b)[2][2], i32x8 (&fb)[2]) {
+    if constexpr (F8) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fb[j] = frag8_f8(h, wc * 2 + j, lane);
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) b[j][ks] = frag8<BKM>(h, wc * 2 + j, ks, lane);
+    }
+  };
+  // one C quadrant x one K-tile: 8*IM bf16 MFMA (k-step outer: independent accumulators between
+  // dependent issues) or 4*IM fp8 MX MFMA
+  auto quad = [&](int q, bf16x8 (&a)[IM][2], bf16x8 (&b)[2][2], i32x8 (&fa)[IM], i32x8 (&fb)[2]) {
+    if constexpr (F8) {
+#pragma unroll
+      for (int i = 0; i < IM; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[(q * IM + i) * 2 + j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+              fa[i], fb[j], acc[(q * IM + i) * 2 + j], 0, 0, 0, 127, 0, 127);
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < IM; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[(q * IM + i) * 2 + j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][ks], b[j][ks], acc[(q * IM + i) * 2 + j], 0, 0, 0);
+    }
+  };
+  // A reads of phase 0 (issued after the B reads): what may stay in flight at its lgkmcnt
+  constexpr int kAReads = (AK ? 2 : 4) * IM;
+
+  for (int t = 0; t < nt; ++t) {
+    // ---- phase 0: q(0,0)
+    readB(half(t, 2), b0, fb0);
+    __builtin_amdgcn_sched_barrier(0);
+    readA(half(t, 0), a0, fa0);
+    stA(t + 1, 1);
+    wait_lgkm<kAReads>();  // retires every B(qn0) read (lgkmcnt saturates at 15)
+    __builtin_amdgcn_sched_barrier(0);
+    PSD_SYNC_OPEN()
+    quad(0, a0, b0, fa0, fb0);
+    PSD_SYNC_CLOSE()
+    // ---- phase 1: q(0,1)
+    readB(half(t, 3), b1, fb1);
+    stB(t + 2, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    PSD_SYNC_OPEN()
+    quad(1, a0, b1, fa0, fb1);
+    PSD_SYNC_CLOSE()
+    // ---- phase 2: q(1,0)
+    readA(half(t, 1), a1, fa1);
+    stA(t + 2, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    PSD_SYNC_OPEN()
+    quad(2, a1, b0, fa1, fb0);
+    PSD_SYNC_CLOSE()
+    // ---- phase 3: q(1,1)
+    stB(t + 2, 1);
+    wait_vm<P::VM>();  // tile t+1 complete (its A-half1 was staged in phase 0)
+    __builtin_amdgcn_sched_barrier(0);
+    PSD_SYNC_OPEN()
+    quad(3, a1, b1, fa1, fb1);
+    PSD_SYNC_CLOSE()
+  }
+  if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the two wave rows
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // all DMA landed and all reads done: the epilogue reuses the LDS
+
+  // epilogue: 16x16 C layout, col = lane&15, row = 4*(lane>>4) + r
+  if constexpr (F8) {
+    const float mul = *g.a_scale * *g.b_scale;
+#pragma unroll
+    for (int i = 0; i < 8 * IM; ++i) acc[i] *= mul;
+  }
+  const int cl = lane & 15, rq = (lane >> 4) * 4;
+  auto mrow = [&](int qm, int i, int r) { return wr * (BM / 2) + qm * P::QA + i * 16 + rq + r; };
+  auto ncol = [&](int qn, int j) { return wc * 64 + qn * 32 + j * 16 + cl; };
+  if (MODE == 1 || g.c_f32) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = n0 + ncol(q & 1, j);
+        if (n >= g.N) continue;
+        const float bias = (MODE == 0 && g.bias) ? bf16_to_f32(reinterpret_cast<const uint16_t*>(g.bias)[n]) : 0.f;
+#pragma unroll
+        for (int i = 0; i < IM; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = m0 + mrow(q >> 1, i, r);
+            if (m >= g.M) continue;
+            const float v0 = acc[(q * IM + i) * 2 + j][r];
+            if (MODE == 1) {
+              reinterpret_cast<float*>(g.C)[(int64_t)blockIdx.z * g.M * g.N + (int64_t)m * g.N + n] = v0;
+            } else {
+              float v = v0 + bias;
+              if (g.act == 1) v = fmaxf(v, 0.f);
+              else if (g.act == 2) v = gelu_tanh(v);
+              reinterpret_cast<float*>(g.C)[(int64_t)m * g.ldc + n] = v;
+            }
+          }
+      }
+    return;
+  }
+  uint16_t* cs = reinterpret_cast<uint16_t*>(smem);
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int nl = ncol(q & 1, j);
+      const int n = n0 + nl;
+      const float bias = (g.bias && n < g.N) ? bf16_to_f32(reinterpret_cast<const uint16_t*>(g.bias)[n]) : 0.f;
+#pragma unroll
+      for (int i = 0; i < IM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ml = mrow(q >> 1, i, r);
+          float v = acc[(q * IM + i) * 2 + j][r] + bias;
+          if (g.act == 2 && g.aux && n < g.N && m0 + ml < g.M)
+            reinterpret_cast<uint16_t*>(g.aux)[(int64_t)(m0 + ml) * g.ldc + n] = f32_to_bf16(v);
+          if (g.act == 1) v = fmaxf(v, 0.f);
+          else if (g.act == 2) v = gelu_tanh(v);
+          cs[ml * kBigLdc + nl] = f32_to_bf16(v);
+        }
+    }
+  __syncthreads();
+  for (int c = threadIdx.x; c < BM * (kBig / 8); c += 512) {
+    const int ml = c >> 5, nl = (c & 31) * 8;
+    const int m = m0 + ml, n = n0 + nl;
+    if (m >= g.M || n >= g.N) continue;
+    uint16_t* o = reinterpret_cast<uint16_t*>(g.C) + (int64_t)m * g.ldc + n;
+    const uint16_t* src = cs + ml * kBigLdc + nl;
+    if (n + 8 <= g.N && ((reinterpret_cast<uintptr_t>(o) & 15) == 0))
+      *reinterpret_cast<u32x4*>(o) = *reinterpret_cast<const u32x4*>(src);
+    else
+      for (int e = 0; e < 8 && n + e < g.N; ++e) o[e] = src[e];
+  }
+}
+#undef PSD_SYNC_OPEN
+#undef PSD_SYNC_CLOSE
+
 // out = (accumulate ? out : 0) + sum_s slab[s]   (M*N elements, 8 per lane)
 template <bool OUT_BF16>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ slab, int splits, int64_t mn,
@@ -691,26 +1040,57 @@ static hipError_t launch_t(const GemmArgs& g, int splits, hipStream_t st) {
   return hipGetLastError();
 }
 
-static bool use_ring() {
+// 256x256 kernel variant: 0 = 2-stage, 1 = half-stage ring, 2 = 8-phase ping-pong (default)
+static int big_variant() {
   static const int v = [] {
-    const char* e = getenv("PSD_GEMM_RING");
-    return e ? atoi(e) : 1;
+    const char* e = getenv("PSD_GEMM_BIG");
+    return e ? atoi(e) : 2;
   }();
-  return v != 0;
+  return v;
+}
+
+template <int BM, bool AK, bool BKM, int MODE, bool F8 = false>
+static hipError_t launch_8p(const GemmArgs& g, int splits, hipStream_t st) {
+  constexpr int lds = P8<BM>::LDS;
+  static bool attr_set = false;  // per instantiation: set the >64 KiB LDS limit once
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)gemm8p_kernel<BM, AK, BKM, MODE, F8>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int nwg = ((g.M + BM - 1) / BM) * ((g.N + kBig - 1) / kBig);
+  hipLaunchKernelGGL((gemm8p_kernel<BM, AK, BKM, MODE, F8>), dim3(nwg, 1, splits), dim3(512), lds, st, g);
+  return hipGetLastError();
+}
+
+// 8-phase tile height: a 128x256 tile costs ~0.55 of a 256x256 one, so narrow problems (few
+// 256-tiles: wave quantisation over 256 CUs) take BM = 128 when that finishes in fewer rounds.
+static int pick_bm(int M, int N, int splits) {
+  const int64_t tn = (N + 255) / 256;
+  const int64_t t256 = (int64_t)((M + 255) / 256) * tn * splits;
+  const int64_t t128 = (int64_t)((M + 127) / 128) * tn * splits;
+  const double c256 = (double)((t256 + 255) / 256);
+  const double c128 = 0.55 * (double)((t128 + 255) / 256);
+  return (M >= 128 && c128 < c256) ? 128 : 256;
 }
 
 template <bool AK, bool BKM, int MODE>
 static hipError_t launch_big(const GemmArgs& g, int splits, hipStream_t st) {
-  const bool ring = use_ring();
-  const void* fn = ring ? (const void*)gemm256r_kernel<AK, BKM, MODE> : (const void*)gemm256_kernel<AK, BKM, MODE>;
-  static bool attr_set[2] = {false, false};  // per instantiation: set the >64 KiB LDS limit once
-  if (!attr_set[ring]) {
+  const int var = big_variant();
+  if (var == 2) {
+    return pick_bm(g.M, g.N, splits) == 128 ? launch_8p<128, AK, BKM, MODE>(g, splits, st)
+                                            : launch_8p<256, AK, BKM, MODE>(g, splits, st);
+  }
+  const void* fn = var == 1 ? (const void*)gemm256r_kernel<AK, BKM, MODE> : (const void*)gemm256_kernel<AK, BKM, MODE>;
+  static bool attr_set[2] = {false, false};
+  if (!attr_set[var == 1]) {
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kBigLds);
     if (e != hipSuccess) return e;
-    attr_set[ring] = true;
+    attr_set[var == 1] = true;
   }
   const int nwg = ((g.M + kBig - 1) / kBig) * ((g.N + kBig - 1) / kBig);
-  if (ring)
+  if (var == 1)
     hipLaunchKernelGGL((gemm256r_kernel<AK, BKM, MODE>), dim3(nwg, 1, splits), dim3(512), kBigLds, st, g);
   else
     hipLaunchKernelGGL((gemm256_kernel<AK, BKM, MODE>), dim3(nwg, 1, splits), dim3(512), kBigLds, st, g);
@@ -718,12 +1098,16 @@ static hipError_t launch_big(const GemmArgs& g, int splits, hipStream_t st) {
 }
 
 static bool big_ok(const GemmArgs& g, int kseg) {
-  // enough 256x256 tiles to fill the chip, no K tail inside a stage, MN-major operands 8-aligned
-  const int64_t tiles = (int64_t)((g.M + 255) / 256) * ((g.N + 255) / 256);
+  // enough big tiles to fill the chip, no K tail inside a stage, MN-major operands 8-aligned
   if (getenv("PSD_GEMM_SMALL_ONLY")) return false;
-  // split-K (MODE 1) passes tiles * splits via k_per_split < K
-  const int64_t waves = g.k_per_split > 0 ? tiles * ((g.K + g.k_per_split - 1) / g.k_per_split) : tiles;
-  return g.M >= 256 && g.N >= 256 && kseg % 64 == 0 && waves >= 64 && g.K >= 256;
+  const int splits = g.k_per_split > 0 ? (g.K + g.k_per_split - 1) / g.k_per_split : 1;
+  if (big_variant() == 2) {  // 8-phase: BM 128 or 256, BN 256
+    const int bm = pick_bm(g.M, g.N, splits);
+    const int64_t tiles = (int64_t)((g.M + bm - 1) / bm) * ((g.N + 255) / 256) * splits;
+    return g.M >= 128 && g.N >= 256 && kseg % 64 == 0 && tiles >= 64 && g.K >= 256;
+  }
+  const int64_t tiles = (int64_t)((g.M + 255) / 256) * ((g.N + 255) / 256) * splits;
+  return g.M >= 256 && g.N >= 256 && kseg % 64 == 0 && tiles >= 64 && g.K >= 256;
 }
 
 template <bool AK, bool BKM, int MODE>
@@ -743,6 +1127,13 @@ hipError_t launch_gemm(const GemmArgs& g, hipStream_t st) {
   if (g.a_kmajor && !g.b_kmajor) return launch_layout<true, false, 0>(g, 1, st);
   if (!g.a_kmajor && !g.b_kmajor) return launch_layout<false, false, 0>(g, 1, st);
   return launch_layout<false, true, 0>(g, 1, st);
+}
+
+hipError_t launch_gemm_fp8(const GemmArgs& g, hipStream_t st) {
+  if (g.M <= 0 || g.N <= 0) return hipSuccess;
+  if (g.K % 128 != 0 || !g.a_kmajor || !g.b_kmajor || !g.a_scale || !g.b_scale) return hipErrorInvalidValue;
+  return pick_bm(g.M, g.N, 1) == 128 ? launch_8p<128, true, true, 0, true>(g, 1, st)
+                                     : launch_8p<256, true, true, 0, true>(g, 1, st);
 }
 
 int gemm_splits(int M, int N, int K) {

@@ -17,9 +17,13 @@ struct GemmArgs {
   int act;           // 0 none, 1 relu, 2 gelu(tanh)
   int c_f32;
   int k_per_split;
+  const float* a_scale;  // fp8 GEMM: dequant factors (device scalars), else unused
+  const float* b_scale;
 };
 
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t stream);
+// C = (A_e4m3 . B_e4m3^T) * a_scale * b_scale (+bias)(act); A [M][K], B [N][K] fp8, K % 128 == 0
+hipError_t launch_gemm_fp8(const GemmArgs& g, hipStream_t stream);
 int gemm_splits(int M, int N, int K);
 // split-K GEMM into fp32 slabs [splits][M][N], then out = (acc ? out : 0) + scale * sum(slabs)
 hipError_t launch_gemm_splitk(const GemmArgs& g, float* slab, int splits, void* out, int out_bf16, int accumulate,

@@ -7,6 +7,11 @@ backward  dx = dy' W              NN GEMM (W read N-major through ds_read_b64_tr
                                   buffer when the data plane installed a grad sink
           db = colsum(dy')        column-sum kernel (also into the sink)
 
+fp8 (``MfmaLinear(..., fp8=True)``): the forward GEMM runs on OCP e4m3 operands with per-tensor
+amax scaling (x and W quantised each step by the amax/quant kernels) on the MX-scaled
+v_mfma_scale_f32_16x16x128_f8f6f4 (2x the bf16 MFMA rate); the backward GEMMs stay bf16 on the
+saved bf16 x and W (fp8 forward / bf16 backward recipe). Needs in_features % 128 == 0.
+
 CPU tensors (and non-bf16 / unaligned shapes) use ``F.linear`` -- the reference the tests compare
 against.
 """
@@ -36,7 +41,14 @@ class _LinearFn(torch.autograd.Function):
         y = torch.empty(M, N, dtype=x.dtype, device=x.device)
         act = ACTS[mod.act]
         aux = torch.empty_like(y) if act == 2 else None
-        C.gemm_(x2, weight, True, True, y, bias, act, aux)
+        if mod.fp8 and x2.shape[1] % 128 == 0:
+            from . import quantize_fp8
+
+            xq, sx = quantize_fp8(x2)
+            wq, sw = quantize_fp8(weight)
+            C.gemm_fp8_(xq, wq, sx, sw, y, bias, act, aux)
+        else:
+            C.gemm_(x2, weight, True, True, y, bias, act, aux)
         ctx.act = act
         ctx.mod = mod
         ctx.has_bias = bias is not None
@@ -76,9 +88,10 @@ class _LinearFn(torch.autograd.Function):
 class MfmaLinear(nn.Linear):
     """``nn.Linear`` (+ fused activation) running on the gfx950 MFMA GEMM for bf16 device tensors."""
 
-    def __init__(self, in_features, out_features, bias=True, act=None, device=None, dtype=None):
+    def __init__(self, in_features, out_features, bias=True, act=None, device=None, dtype=None, fp8=False):
         super().__init__(in_features, out_features, bias=bias, device=device, dtype=dtype)
         self.act = act
+        self.fp8 = fp8
 
     def psd_direct_grad_params(self):
         return [p for p in (self.weight, self.bias) if p is not None]

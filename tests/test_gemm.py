@@ -54,8 +54,9 @@ def test_gemm_splitk_exact(gpu, a_k, b_k, shape):
 
 
 @pytest.mark.parametrize("act", [0, 1, 2], ids=["none", "relu", "gelu"])
-def test_gemm_bias_act_epilogue(gpu, act):
-    M, N, K = 200, 136, 96
+@pytest.mark.parametrize("shape", [(200, 136, 96), (2048, 2056, 512)], ids=["small", "big"])
+def test_gemm_bias_act_epilogue(gpu, act, shape):
+    M, N, K = shape
     A, B, ref = _ops(M, N, K, True, True, gpu, ints=False, seed=5)
     bias = torch.randn(N).to(torch.bfloat16)
     z = ref + bias.float()
@@ -92,15 +93,27 @@ def test_colsum_shapes_deterministic(gpu, shape):
 
 @pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, False), (False, True)],
                          ids=["NT", "NN", "TN", "TT"])
-@pytest.mark.parametrize("shape", [(2048, 2048, 256), (2000, 2120, 320), (2304, 4096, 768)],
+@pytest.mark.parametrize("shape", [(2048, 2048, 256), (2000, 2120, 320), (2304, 4096, 768), (8192, 768, 768),
+                                   (3000, 1000, 512)],
                          ids=lambda s: "x".join(map(str, s)))
 def test_gemm_256_tile_path_exact(gpu, a_k, b_k, shape):
-    """Shapes large enough for the 256x256 global_load_lds kernel (incl. ragged M/N edges)."""
+    """Shapes large enough for the 8-phase kernel, 256x256 and 128x256 tiles (incl. ragged M/N)."""
     M, N, K = shape
     A, B, ref = _ops(M, N, K, a_k, b_k, gpu, seed=11)
     out = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
     native().gemm_(A, B, a_k, b_k, out)
     torch.testing.assert_close(out.float().cpu(), ref.bfloat16().float(), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("c_f32", [False, True], ids=["bf16", "f32"])
+def test_gemm_256_long_k_exact(gpu, c_f32):
+    """Many K-tiles through the 256x256 pipeline (staging wraps the LDS buffers many times)."""
+    M, N, K = 2304, 2048, 4160
+    A, B, ref = _ops(M, N, K, True, True, gpu, seed=13)
+    out = torch.empty(M, N, dtype=torch.float32 if c_f32 else torch.bfloat16, device=gpu)
+    native().gemm_(A, B, True, True, out)
+    want = ref if c_f32 else ref.bfloat16().float()
+    torch.testing.assert_close(out.float().cpu(), want, rtol=0, atol=0)
 
 
 def test_gemm_256_splitk_exact(gpu):
@@ -109,3 +122,62 @@ def test_gemm_256_splitk_exact(gpu):
     out = torch.zeros(M, N, dtype=torch.float32, device=gpu)
     native().gemm_splitk_(A, B, False, False, out, False, 1.0, 0)
     torch.testing.assert_close(out.cpu(), ref, rtol=0, atol=0)
+
+
+# ---------------------------------------------------------------- fp8 (OCP e4m3fn) forward GEMM
+@pytest.mark.parametrize("shape", [(2048, 2048, 512), (300, 520, 256), (4096, 768, 3072)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_gemm_fp8_exact_small_ints(gpu, shape):
+    """Small integers are exact in e4m3: the MX-scaled fp8 MFMA must reproduce the fp32 product."""
+    M, N, K = shape
+    g = torch.Generator().manual_seed(21)
+    a = torch.randint(-3, 4, (M, K), generator=g).float()
+    b = torch.randint(-3, 4, (N, K), generator=g).float()
+    aq, bq = a.to(torch.float8_e4m3fn).to(gpu), b.to(torch.float8_e4m3fn).to(gpu)
+    sa = torch.tensor([0.5], device=gpu)
+    sb = torch.tensor([2.0], device=gpu)
+    out = torch.empty(M, N, dtype=torch.float32, device=gpu)
+    native().gemm_fp8_(aq, bq, sa, sb, out)
+    torch.testing.assert_close(out.cpu(), a @ b.t(), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("act", [0, 2], ids=["none", "gelu"])
+def test_gemm_fp8_quantized_matches_dequant_reference(gpu, act):
+    from parameter_server_distributed_amd.ops import quantize_fp8
+
+    M, N, K = 1024, 1536, 768
+    x = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=gpu) * 0.05).to(torch.bfloat16)
+    bias = torch.randn(N, device=gpu).to(torch.bfloat16)
+    xq, sx = quantize_fp8(x)
+    wq, sw = quantize_fp8(w)
+    ref = (xq.float() * sx) @ (wq.float() * sw).t() + bias.float()
+    if act == 2:
+        ref = torch.nn.functional.gelu(ref, approximate="tanh")
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
+    native().gemm_fp8_(xq, wq, sx, sw, out, bias, act)
+    torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=1e-2)
+
+
+def test_mfma_linear_fp8_forward_backward(gpu):
+    from parameter_server_distributed_amd.ops.linear import MfmaLinear
+
+    torch.manual_seed(0)
+    lin = MfmaLinear(512, 384, act="gelu", fp8=True).to(gpu, torch.bfloat16)
+    ref = torch.nn.Linear(512, 384).to(gpu)
+    with torch.no_grad():
+        ref.weight.copy_(lin.weight.float())
+        ref.bias.copy_(lin.bias.float())
+    x = torch.randn(256, 512, device=gpu)
+    xb = x.to(torch.bfloat16).requires_grad_(True)
+    xr = x.clone().requires_grad_(True)
+    y = lin(xb)
+    yr = torch.nn.functional.gelu(ref(xr), approximate="tanh")
+    rel = (y.float() - yr).norm() / yr.norm()
+    assert rel < 0.06, rel  # e4m3 forward
+    g = torch.randn_like(yr)
+    y.backward(g.to(torch.bfloat16))
+    yr.backward(g)
+    relx = (xb.grad.float() - xr.grad).norm() / xr.grad.norm()
+    relw = (lin.weight.grad.float() - ref.weight.grad).norm() / ref.weight.grad.norm()
+    assert relx < 0.08 and relw < 0.08, (relx, relw)

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B of the MFMA GEMM kernels on square and BERT-base shapes (uniform random operands): prints
 one markdown row per (shape, layout) with us and TFLOP/s, plus the max error against an fp32
-torch reference. Select the 256x256 kernel variant with PSD_GEMM_RING=0/1 (one per process)."""
+torch reference. Select the 256x256 kernel variant with PSD_GEMM_BIG=0/1/2 (one per process)."""
 import argparse
 import os
 import sys
@@ -31,7 +31,7 @@ def t_us(fn, it=20):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--label", default=os.environ.get("PSD_GEMM_RING", "1"))
+    ap.add_argument("--label", default=os.environ.get("PSD_GEMM_BIG", "2"))
     a = ap.parse_args()
     C = native()
     dev = torch.device("cuda")
@@ -49,6 +49,13 @@ def main():
                 ("wgrad TN", lambda: C.gemm_splitk_(dY, X, False, False, dW, False, 1.0, 0),
                  lambda: dY.float().t() @ X.float(), dW),
                 ("blas fwd", lambda: torch.mm(X, W.t()), None, None)]
+        if K % 128 == 0:
+            from parameter_server_distributed_amd.ops import quantize_fp8
+
+            Xq, sx = quantize_fp8(X)
+            Wq, sw = quantize_fp8(W)
+            runs.append(("fp8 fwd NT", lambda: C.gemm_fp8_(Xq, Wq, sx, sw, Y),
+                         lambda: (Xq.float() * sx) @ (Wq.float() * sw).t(), Y))
         for lay, fn, ref, out in runs:
             us = t_us(fn)
             err = ""
