@@ -653,6 +653,28 @@ __device__ __forceinline__ void wait_lgkm() {
   else static_assert(N == 8 || N == 4, "lgkmcnt");
 }
 
+template <int CTRL>
+__device__ __forceinline__ float dpp_q(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+// 4x4 transpose inside a lane quad: in v[r] = C[row r][col L]; out w[c] = C[row L][col c]
+__device__ __forceinline__ void quad_t4(const f32x4 v, int L, float (&w)[4]) {
+  const bool o1 = L & 1, o2 = (L >> 1) & 1;
+  const float r0 = dpp_q<0xB1>(o1 ? v[0] : v[1]);  // quad_perm [1,0,3,2]: partner L^1
+  const float r1 = dpp_q<0xB1>(o1 ? v[2] : v[3]);
+  const float a0 = o1 ? r0 : v[0], a1 = o1 ? v[1] : r0;  // row L&1,     cols (L&~1, L|1)
+  const float b0 = o1 ? r1 : v[2], b1 = o1 ? v[3] : r1;  // row (L&1)+2, same cols
+  const float q0 = dpp_q<0x4E>(o2 ? a0 : b0);            // quad_perm [2,3,0,1]: partner L^2
+  const float q1 = dpp_q<0x4E>(o2 ? a1 : b1);
+  w[0] = o2 ? q0 : a0;
+  w[1] = o2 ? q1 : a1;
+  w[2] = o2 ? b0 : q0;
+  w[3] = o2 ? b1 : q1;
+}
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+}
+
 // grouped tile order inside one XCD's contiguous range: 4 tile-rows share each B panel
 __device__ __forceinline__ void tile_of(int wg, int tiles_m, int tiles_n, int& tm, int& tn) {
   constexpr int G = 4;
@@ -696,6 +718,7 @@ struct P8 {
 template <int BM, bool AK, bool BKM, int MODE, bool F8 = false>
 __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
   static_assert(!F8 || (AK && BKM), "fp8 GEMM takes K-major operands");
+  static_assert(BM == 256 || AK, "BM = 128 takes a K-major A");
   using P = P8<BM>;
   constexpr int IM = P::IM;
   constexpr int KT = F8 ? 128 : BK;  // k per K-tile (128-B LDS rows either way)
@@ -837,32 +860,41 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
     for (int i = 0; i < 8 * IM; ++i) acc[i] *= mul;
   }
   const int cl = lane & 15, rq = (lane >> 4) * 4;
-  auto mrow = [&](int qm, int i, int r) { return wr * (BM / 2) + qm * P::QA + i * 16 + rq + r; };
-  auto ncol = [&](int qn, int j) { return wc * 64 + qn * 32 + j * 16 + cl; };
+  // Each quad of lanes (4 consecutive columns x the same 4 rows) is transposed in registers with
+  // two DPP exchanges, so every lane owns 4 consecutive columns of one row: 16-B fp32 / 8-B bf16
+  // stores instead of 4-B / 2-B scatters.
+  const int L = cl & 3;
+  auto mrow = [&](int qm, int i) { return wr * (BM / 2) + qm * P::QA + i * 16 + rq + L; };
+  auto ncol = [&](int qn, int j) { return wc * 64 + qn * 32 + j * 16 + (cl & ~3); };
+  auto bias_of = [&](int n) {
+    return (MODE == 0 && g.bias && n < g.N) ? bf16_to_f32(reinterpret_cast<const uint16_t*>(g.bias)[n]) : 0.f;
+  };
   if (MODE == 1 || g.c_f32) {
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int n = n0 + ncol(q & 1, j);
-        if (n >= g.N) continue;
-        const float bias = (MODE == 0 && g.bias) ? bf16_to_f32(reinterpret_cast<const uint16_t*>(g.bias)[n]) : 0.f;
+        const float bias = bias_of(n0 + wc * 64 + (q & 1) * 32 + j * 16 + cl);
 #pragma unroll
-        for (int i = 0; i < IM; ++i)
+        for (int i = 0; i < IM; ++i) {
+          float w[4];
+          quad_t4(acc[(q * IM + i) * 2 + j] + bias, L, w);
+          const int m = m0 + mrow(q >> 1, i);
+          if (m >= g.M || n >= g.N) continue;
+          float* o;
+          if (MODE == 1) {
+            o = reinterpret_cast<float*>(g.C) + (int64_t)blockIdx.z * g.M * g.N + (int64_t)m * g.N + n;
+          } else {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int m = m0 + mrow(q >> 1, i, r);
-            if (m >= g.M) continue;
-            const float v0 = acc[(q * IM + i) * 2 + j][r];
-            if (MODE == 1) {
-              reinterpret_cast<float*>(g.C)[(int64_t)blockIdx.z * g.M * g.N + (int64_t)m * g.N + n] = v0;
-            } else {
-              float v = v0 + bias;
-              if (g.act == 1) v = fmaxf(v, 0.f);
-              else if (g.act == 2) v = gelu_tanh(v);
-              reinterpret_cast<float*>(g.C)[(int64_t)m * g.ldc + n] = v;
-            }
+            for (int e = 0; e < 4; ++e) w[e] = g.act == 1 ? fmaxf(w[e], 0.f) : (g.act == 2 ? gelu_tanh(w[e]) : w[e]);
+            o = reinterpret_cast<float*>(g.C) + (int64_t)m * g.ldc + n;
           }
+          if (n + 4 <= g.N && (reinterpret_cast<uintptr_t>(o) & 15) == 0)
+            *reinterpret_cast<f32x4*>(o) = f32x4{w[0], w[1], w[2], w[3]};
+          else
+            for (int e = 0; e < 4 && n + e < g.N; ++e) o[e] = w[e];
+        }
       }
     return;
   }
@@ -873,19 +905,23 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
     for (int j = 0; j < 2; ++j) {
       const int nl = ncol(q & 1, j);
       const int n = n0 + nl;
-      const float bias = (g.bias && n < g.N) ? bf16_to_f32(reinterpret_cast<const uint16_t*>(g.bias)[n]) : 0.f;
+      const float bias = bias_of(n0 + wc * 64 + (q & 1) * 32 + j * 16 + cl);
 #pragma unroll
-      for (int i = 0; i < IM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int ml = mrow(q >> 1, i, r);
-          float v = acc[(q * IM + i) * 2 + j][r] + bias;
-          if (g.act == 2 && g.aux && n < g.N && m0 + ml < g.M)
-            reinterpret_cast<uint16_t*>(g.aux)[(int64_t)(m0 + ml) * g.ldc + n] = f32_to_bf16(v);
-          if (g.act == 1) v = fmaxf(v, 0.f);
-          else if (g.act == 2) v = gelu_tanh(v);
-          cs[ml * kBigLdc + nl] = f32_to_bf16(v);
+      for (int i = 0; i < IM; ++i) {
+        float w[4];
+        quad_t4(acc[(q * IM + i) * 2 + j] + bias, L, w);
+        const int ml = mrow(q >> 1, i);
+        if (g.act == 2 && g.aux && m0 + ml < g.M && n < g.N) {  // pre-activation for the GELU backward
+          uint16_t* ax = reinterpret_cast<uint16_t*>(g.aux) + (int64_t)(m0 + ml) * g.ldc + n;
+          if (n + 4 <= g.N && (reinterpret_cast<uintptr_t>(ax) & 7) == 0)
+            *reinterpret_cast<uint2*>(ax) = uint2{pack_bf16x2(w[0], w[1]), pack_bf16x2(w[2], w[3])};
+          else
+            for (int e = 0; e < 4 && n + e < g.N; ++e) ax[e] = f32_to_bf16(w[e]);
         }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = g.act == 1 ? fmaxf(w[e], 0.f) : (g.act == 2 ? gelu_tanh(w[e]) : w[e]);
+        *reinterpret_cast<uint2*>(cs + ml * kBigLdc + nl) = uint2{pack_bf16x2(w[0], w[1]), pack_bf16x2(w[2], w[3])};
+      }
     }
   __syncthreads();
   for (int c = threadIdx.x; c < BM * (kBig / 8); c += 512) {
@@ -1066,7 +1102,9 @@ static hipError_t launch_8p(const GemmArgs& g, int splits, hipStream_t st) {
 
 // 8-phase tile height: a 128x256 tile costs ~0.55 of a 256x256 one, so narrow problems (few
 // 256-tiles: wave quantisation over 256 CUs) take BM = 128 when that finishes in fewer rounds.
-static int pick_bm(int M, int N, int splits) {
+// (BM = 128 needs a K-major A: its M-major half image would be 64 columns wide)
+static int pick_bm(int M, int N, int splits, bool a_kmajor = true) {
+  if (!a_kmajor) return 256;
   const int64_t tn = (N + 255) / 256;
   const int64_t t256 = (int64_t)((M + 255) / 256) * tn * splits;
   const int64_t t128 = (int64_t)((M + 127) / 128) * tn * splits;
@@ -1079,8 +1117,10 @@ template <bool AK, bool BKM, int MODE>
 static hipError_t launch_big(const GemmArgs& g, int splits, hipStream_t st) {
   const int var = big_variant();
   if (var == 2) {
-    return pick_bm(g.M, g.N, splits) == 128 ? launch_8p<128, AK, BKM, MODE>(g, splits, st)
-                                            : launch_8p<256, AK, BKM, MODE>(g, splits, st);
+    if constexpr (AK) {
+      if (pick_bm(g.M, g.N, splits) == 128) return launch_8p<128, AK, BKM, MODE>(g, splits, st);
+    }
+    return launch_8p<256, AK, BKM, MODE>(g, splits, st);
   }
   const void* fn = var == 1 ? (const void*)gemm256r_kernel<AK, BKM, MODE> : (const void*)gemm256_kernel<AK, BKM, MODE>;
   static bool attr_set[2] = {false, false};
@@ -1102,7 +1142,7 @@ static bool big_ok(const GemmArgs& g, int kseg) {
   if (getenv("PSD_GEMM_SMALL_ONLY")) return false;
   const int splits = g.k_per_split > 0 ? (g.K + g.k_per_split - 1) / g.k_per_split : 1;
   if (big_variant() == 2) {  // 8-phase: BM 128 or 256, BN 256
-    const int bm = pick_bm(g.M, g.N, splits);
+    const int bm = pick_bm(g.M, g.N, splits, g.a_kmajor);
     const int64_t tiles = (int64_t)((g.M + bm - 1) / bm) * ((g.N + 255) / 256) * splits;
     return g.M >= 128 && g.N >= 256 && kseg % 64 == 0 && tiles >= 64 && g.K >= 256;
   }
