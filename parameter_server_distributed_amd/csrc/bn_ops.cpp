@@ -85,14 +85,14 @@ std::vector<at::Tensor> bn_fwd(const at::Tensor& x_in, c10::optional<at::Tensor>
   a.eps = (float)eps;
   hipError_t e = launch_bn_fwd(a, stream_of(x));
   TORCH_CHECK(e == hipSuccess, "psd bn fwd: ", hipGetErrorString(e));
-  return {y, mean, invstd};
+  return {y, mean, invstd, ss};
 }
 
 std::vector<at::Tensor> bn_bwd(const at::Tensor& dy_in, const at::Tensor& x_in, c10::optional<at::Tensor> y_in,
                                c10::optional<at::Tensor> gamma, const at::Tensor& save_mean,
                                const at::Tensor& save_invstd, bool relu, bool need_dr,
                                c10::optional<at::Tensor> dgamma_out, c10::optional<at::Tensor> dbeta_out,
-                               c10::optional<at::Tensor> dy2_in) {
+                               c10::optional<at::Tensor> dy2_in, c10::optional<at::Tensor> ss_in) {
   const c10::DeviceGuard g(x_in.device());
   at::Tensor x = nhwc(x_in), dy = nhwc(dy_in);
   at::Tensor dy2;
@@ -103,10 +103,17 @@ std::vector<at::Tensor> bn_bwd(const at::Tensor& dy_in, const at::Tensor& x_in, 
   const int64_t C = channels(x);
   const int64_t M = x.numel() / C;
   TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == at::kBFloat16, "psd bn bwd: dy shape/dtype");
-  at::Tensor y;
+  at::Tensor y, ss;
   if (relu) {
-    TORCH_CHECK(y_in.has_value() && y_in->defined(), "psd bn bwd: relu needs the forward output");
-    y = nhwc(*y_in);
+    // ReLU mask source: the forward output y, or (no residual) x with the forward scale/shift
+    if (y_in.has_value() && y_in->defined()) {
+      y = nhwc(*y_in);
+    } else {
+      TORCH_CHECK(ss_in.has_value() && ss_in->defined(), "psd bn bwd: relu needs the forward output or scale/shift");
+      TORCH_CHECK(!need_dr, "psd bn bwd: a residual ReLU mask needs the forward output");
+      ss = ss_in->contiguous();
+      TORCH_CHECK(ss.numel() == 2 * C && ss.scalar_type() == at::kFloat, "psd bn bwd: ss must be fp32 [2C]");
+    }
   }
   auto f32 = x.options().dtype(at::kFloat);
   at::Tensor dx = at::empty_like(x);
@@ -126,7 +133,8 @@ std::vector<at::Tensor> bn_bwd(const at::Tensor& dy_in, const at::Tensor& x_in, 
   a.dy = reinterpret_cast<const uint16_t*>(dy.data_ptr());
   a.dy2 = dy2.defined() ? reinterpret_cast<const uint16_t*>(dy2.data_ptr()) : nullptr;
   a.y = y.defined() ? reinterpret_cast<const uint16_t*>(y.data_ptr()) : nullptr;
-  a.x = reinterpret_cast<const uint16_t*>(x.data_ptr());
+  a.ss = ss.defined() ? ss.data_ptr<float>() : nullptr;
+  a.x =reinterpret_cast<const uint16_t*>(x.data_ptr());
   a.gamma = opt_ptr<const uint16_t>(gamma);
   a.save_mean = save_mean.data_ptr<float>();
   a.save_invstd = save_invstd.data_ptr<float>();

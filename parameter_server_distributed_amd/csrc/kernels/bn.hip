@@ -214,23 +214,37 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
 }
 
 // ------------------------------------------------------------------ backward
-template <bool RELU, bool RES_OUT>
+// ReLU mask source. kMaskY: y > 0 from the saved forward output (needed when a residual was added
+// before the ReLU). kMaskX: x*scale + shift > 0 recomputed from the forward's fp32 scale/shift --
+// the same fmaf the apply kernel rounded to y, so the mask is identical -- which saves one full
+// [M, C] read in both backward passes (and keeps y out of the autograd context).
+enum MaskSrc : int { kMaskNone = 0, kMaskY = 1, kMaskX = 2 };
+
+template <int MASK, bool RES_OUT>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ dy2,
-                                                            const uint16_t* __restrict__ y,
+                                                            const uint16_t* __restrict__ y, const float* __restrict__ ssf,
                                                             const uint16_t* __restrict__ x, const float* __restrict__ mean,
                                                             uint16_t* __restrict__ dr, int64_t M, int C,
                                                             float* __restrict__ part) {
   const Map m = make_map(C);
-  float a[8], b[8], mu[8];
+  float a[8], b[8], mu[8], sc[8], sh[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) a[j] = b[j] = 0.f;
   if (m.active) {
     load8_f32(mean + m.cg * 8, mu);
+    if (MASK == kMaskX) {
+      load8_f32(ssf + m.cg * 8, sc);
+      load8_f32(ssf + C + m.cg * 8, sh);
+    }
     const int64_t stride = (int64_t)gridDim.x * m.rpi;
     auto body = [&](int64_t off, const float* g0, const float* xv, const float* yv) {
       float g[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) g[j] = RELU ? (yv[j] > 0.f ? g0[j] : 0.f) : g0[j];
+      for (int j = 0; j < 8; ++j) {
+        if (MASK == kMaskY) g[j] = yv[j] > 0.f ? g0[j] : 0.f;
+        else if (MASK == kMaskX) g[j] = fmaf(xv[j], sc[j], sh[j]) > 0.f ? g0[j] : 0.f;
+        else g[j] = g0[j];
+      }
       if (RES_OUT) store8_bf16(dr + off, g);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -256,7 +270,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
           g1[j] += h1[j];
         }
       }
-      if (RELU) {
+      if (MASK == kMaskY) {
         load8_bf16(y + o0, y0);
         load8_bf16(y + o1, y1);
       }
@@ -274,7 +288,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
 #pragma unroll
         for (int j = 0; j < 8; ++j) g0[j] += h0[j];
       }
-      if (RELU) load8_bf16(y + o0, y0);
+      if (MASK == kMaskY) load8_bf16(y + o0, y0);
       body(o0, g0, x0, y0);
     }
   }
@@ -302,20 +316,25 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
   coef[2 * C + c] = -k1 * k2 + k1 * k3 * mean[c];  // C
 }
 
-// MODE 0: dy' = dy; MODE 1: dy' = dy * (y > 0); MODE 2: dy' = g (already masked, = dr)
+// MODE 0: dy' = dy; MODE 1: dy' = dy * (y > 0); MODE 2: dy' = g (already masked, = dr);
+// MODE 3: dy' = dy * (x*scale + shift > 0) (mask recomputed, kMaskX)
 template <int MODE>
 __global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(const uint16_t* __restrict__ g, const uint16_t* __restrict__ g2,
-                                                           const uint16_t* __restrict__ y,
+                                                           const uint16_t* __restrict__ y, const float* __restrict__ ssf,
                                                            const uint16_t* __restrict__ x, const float* __restrict__ coef,
                                                            uint16_t* __restrict__ dx, int64_t nvec, int C) {
   const int tpc = C >> 3;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int cg = (int)(v % tpc);
-  float A[8], B[8], Cc[8];
+  float A[8], B[8], Cc[8], sc[8], sh[8];
   load8_f32(coef + cg * 8, A);
   load8_f32(coef + C + cg * 8, B);
   load8_f32(coef + 2 * C + cg * 8, Cc);
+  if (MODE == 3) {
+    load8_f32(ssf + cg * 8, sc);
+    load8_f32(ssf + C + cg * 8, sh);
+  }
   for (; v < nvec; v += stride) {
     float gv[8], xv[8];
     load8_bf16(g + v * 8, gv);
@@ -331,6 +350,10 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(const uint16_t* __res
       load8_bf16(y + v * 8, yv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) gv[j] = yv[j] > 0.f ? gv[j] : 0.f;
+    }
+    if (MODE == 3) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) gv[j] = fmaf(xv[j], sc[j], sh[j]) > 0.f ? gv[j] : 0.f;
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) gv[j] = fmaf(A[j], gv[j], fmaf(B[j], xv[j], Cc[j]));
@@ -400,24 +423,30 @@ hipError_t launch_bn_bwd(const BnBwdArgs& a, hipStream_t st) {
   if (a.C % 8 != 0) return hipErrorInvalidValue;
   int gx, gy;
   reduce_grid(a.M, a.C, gx, gy);
-#define PSD_RED(R, O)                                                                                        \
-  hipLaunchKernelGGL((bn_bwd_reduce_kernel<R, O>), dim3(gx, gy), dim3(256), 0, st, a.dy, a.dy2, a.y, a.x, a.save_mean, \
-                     a.dr, a.M, a.C, a.part)
-  if (a.relu && a.dr) PSD_RED(true, true);
-  else if (a.relu) PSD_RED(true, false);
-  else if (a.dr) PSD_RED(false, true);
-  else PSD_RED(false, false);
+  // ReLU mask: from y when given, else recomputed from x and the forward scale/shift
+  const int mask = !a.relu ? kMaskNone : (a.y ? kMaskY : kMaskX);
+  if (mask == kMaskX && !a.ss) return hipErrorInvalidValue;
+#define PSD_RED(K, O)                                                                                              \
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<K, O>), dim3(gx, gy), dim3(256), 0, st, a.dy, a.dy2, a.y, a.ss, a.x,     \
+                     a.save_mean, a.dr, a.M, a.C, a.part)
+  if (mask == kMaskY && a.dr) PSD_RED(kMaskY, true);
+  else if (mask == kMaskY) PSD_RED(kMaskY, false);
+  else if (mask == kMaskX && a.dr) PSD_RED(kMaskX, true);
+  else if (mask == kMaskX) PSD_RED(kMaskX, false);
+  else if (a.dr) PSD_RED(kMaskNone, true);
+  else PSD_RED(kMaskNone, false);
 #undef PSD_RED
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((a.C + kFinCh - 1) / kFinCh), dim3(256), 0, st, a.part, gx, a.M, a.C, a.gamma,
                      a.save_mean, a.save_invstd, a.dgamma, a.dbeta, a.coef);
   const int64_t nvec = a.M * (a.C / 8);
   const int g = elem_grid(nvec, a.C);
-  if (a.dr)
-    hipLaunchKernelGGL(bn_bwd_elemt_kernel<2>, dim3(g), dim3(256), 0, st, a.dr, nullptr, a.y, a.x, a.coef, a.dx, nvec, a.C);
-  else if (a.relu)
-    hipLaunchKernelGGL(bn_bwd_elemt_kernel<1>, dim3(g), dim3(256), 0, st, a.dy, a.dy2, a.y, a.x, a.coef, a.dx, nvec, a.C);
-  else
-    hipLaunchKernelGGL(bn_bwd_elemt_kernel<0>, dim3(g), dim3(256), 0, st, a.dy, a.dy2, a.y, a.x, a.coef, a.dx, nvec, a.C);
+#define PSD_EL(MODE, G, G2) \
+  hipLaunchKernelGGL(bn_bwd_elemt_kernel<MODE>, dim3(g), dim3(256), 0, st, G, G2, a.y, a.ss, a.x, a.coef, a.dx, nvec, a.C)
+  if (a.dr) PSD_EL(2, a.dr, nullptr);
+  else if (mask == kMaskY) PSD_EL(1, a.dy, a.dy2);
+  else if (mask == kMaskX) PSD_EL(3, a.dy, a.dy2);
+  else PSD_EL(0, a.dy, a.dy2);
+#undef PSD_EL
   return hipGetLastError();
 }
 

@@ -29,7 +29,8 @@ struct BnFwdArgs {
 struct BnBwdArgs {
   const uint16_t* dy;
   const uint16_t* dy2;    // optional second upstream gradient (residual-branch fusion): dy + dy2
-  const uint16_t* y;      // forward output (ReLU mask), may be null if !relu
+  const uint16_t* y;      // forward output (ReLU mask); null: mask recomputed from x and ss
+  const float* ss;        // [2C] forward scale/shift (needed when relu && !y)
   const uint16_t* x;      // forward input
   const uint16_t* gamma;
   const float* save_mean;

@@ -23,7 +23,7 @@ std::vector<at::Tensor> bn_bwd(const at::Tensor& dy, const at::Tensor& x, c10::o
                                c10::optional<at::Tensor> gamma, const at::Tensor& save_mean,
                                const at::Tensor& save_invstd, bool relu, bool need_dr,
                                c10::optional<at::Tensor> dgamma_out, c10::optional<at::Tensor> dbeta_out,
-                               c10::optional<at::Tensor> dy2);
+                               c10::optional<at::Tensor> dy2, c10::optional<at::Tensor> ss);
 
 void gemm_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool b_kmajor, at::Tensor out,
            c10::optional<at::Tensor> bias, int64_t act, c10::optional<at::Tensor> aux);

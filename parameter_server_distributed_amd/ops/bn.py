@@ -30,19 +30,23 @@ class _FusedBNFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, mod, resid_to=None):
         C = native()
-        y, mean, invstd = C.bn_fwd(x, weight, bias, mod.running_mean, mod.running_var, residual, mod.relu, True,
-                                   mod.momentum if mod.momentum is not None else 0.1, mod.eps,
-                                   mod.num_batches_tracked, None)
+        y, mean, invstd, ss = C.bn_fwd(x, weight, bias, mod.running_mean, mod.running_var, residual, mod.relu, True,
+                                       mod.momentum if mod.momentum is not None else 0.1, mod.eps,
+                                       mod.num_batches_tracked, None)
         ctx.relu = mod.relu
         ctx.has_res = residual is not None
         ctx.mod = mod
         ctx.resid_to = resid_to
-        ctx.save_for_backward(x, y if mod.relu else None, weight, mean, invstd)
+        # ReLU mask for backward: without a residual it is recomputed from x and the fp32
+        # scale/shift (one [M, C] read less per backward pass); with one, y itself is kept
+        keep_y = mod.relu and ctx.has_res
+        ctx.save_for_backward(x, y if keep_y else None, weight, mean, invstd,
+                              ss if (mod.relu and not keep_y) else None)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, w, mean, invstd = ctx.saved_tensors
+        x, y, w, mean, invstd, ss = ctx.saved_tensors
         mod = ctx.mod
         sink = getattr(mod, "_psd_grad_sink", None)
         dgo = dbo = None
@@ -51,7 +55,7 @@ class _FusedBNFn(torch.autograd.Function):
         # residual-branch fusion: the identity-path gradient of this BN's output was stashed by the
         # next block's bn3 backward; fold it in here instead of an autograd add kernel
         dy2 = mod._psd_pending_dr.pop() if getattr(mod, "_psd_pending_dr", None) else None
-        dx, dr, dg, db = native().bn_bwd(dy, x, y, w, mean, invstd, ctx.relu, ctx.has_res, dgo, dbo, dy2)
+        dx, dr, dg, db = native().bn_bwd(dy, x, y, w, mean, invstd, ctx.relu, ctx.has_res, dgo, dbo, dy2, ss)
         res_grad = None
         if ctx.has_res:
             if ctx.resid_to is not None:
@@ -90,7 +94,7 @@ class FusedBatchNorm2d(nn.BatchNorm2d):
             ss = torch.cat([scale, shift]).contiguous()
             if torch.is_grad_enabled() and (x.requires_grad or self.weight.requires_grad):
                 return self._reference(x, residual)
-            y, _, _ = native().bn_fwd(x, None, None, None, None, residual, self.relu, False, 0.0, self.eps, None, ss)
+            y, _, _, _ = native().bn_fwd(x, None, None, None, None, residual, self.relu, False, 0.0, self.eps, None, ss)
             return y
         return self._reference(x, residual)
 
