@@ -14,12 +14,15 @@ def main(argv=None):
     ap.add_argument("--expiry-s", type=float, default=30.0, help="drop workers silent for longer (reference: 30)")
     ap.add_argument("--sweep-s", type=float, default=10.0, help="expiry sweep period (reference: 10)")
     ap.add_argument("--shards", default="", help="comma-separated PS shard addresses (default: the PS address)")
+    ap.add_argument("--store-port", type=int, default=0,
+                    help="rendezvous store port for elastic collective workers (0: any free port, -1: none)")
     from ..utils.config import apply_config
 
     apply_config(ap, argv)
     a = ap.parse_intermixed_args(argv)
     shards = [s for s in a.shards.split(",") if s]
-    serve(a.listen, a.ps_address, a.expiry_s, a.sweep_s, shards)
+    serve(a.listen, a.ps_address, a.expiry_s, a.sweep_s, shards,
+          store_port=None if a.store_port < 0 else a.store_port)
 
 
 if __name__ == "__main__":

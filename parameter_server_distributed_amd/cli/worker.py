@@ -30,10 +30,23 @@ def main(argv=None):
     ap.add_argument("--reference-wire", action="store_true",
                     help="encode tensors as the reference did (repeated float), not bulk bytes")
     ap.add_argument("--stats-json", default="", help="write final PS stats + losses to this file")
+    # elastic collective data plane (runtime/elastic.py): RCCL/gloo world rebuilt on join/leave
+    ap.add_argument("--elastic", action="store_true",
+                    help="train on the collective PS data plane; join/leave mid-run via the coordinator")
+    ap.add_argument("--ps-shards", type=int, default=0, help="elastic: PS shards (0: one per rank)")
+    ap.add_argument("--staleness", type=int, default=0, help="elastic: staleness bound S")
+    ap.add_argument("--optimizer", default="momentum")
+    ap.add_argument("--lr", type=float, default=0.05)
+    ap.add_argument("--bucket-mb", type=float, default=16.0)
+    ap.add_argument("--pull-dtype", default="bf16")
+    ap.add_argument("--check-every", type=int, default=5, help="elastic: membership check period (steps)")
+    ap.add_argument("--min-workers", type=int, default=1, help="elastic: workers to wait for at start")
     from ..utils.config import apply_config
 
     apply_config(ap, argv)
     a = ap.parse_intermixed_args(argv)
+    if a.elastic:
+        return elastic_main(a)
     w = Worker(a.coordinator, a.worker_id, a.worker_addr, a.worker_port, model=a.model, batch=a.batch,
                device=a.device, heartbeat_s=a.heartbeat_s, bf16_wire=a.bf16_wire, mode=a.mode,
                raw_wire=not a.reference_wire)
@@ -72,6 +85,64 @@ def main(argv=None):
                        "counters": json.loads(st.counters_json or "{}"), "seconds": dt}, f)
     w.shutdown()
     return 0 if ok_all else 1
+
+
+def elastic_main(a) -> int:
+    """Elastic worker on the collective data plane: prints the reference's per-iteration lines
+    (``worker <id> iter <it> done=true``) with the generation / world it ran in."""
+    import torch
+
+    from .. import models
+    from ..ops.optim import OptimConfig
+    from ..parallel.collective_ps import CollectivePS
+    from ..runtime.elastic import ElasticAgent, ElasticTrainer
+    from ..runtime.trainer import Trainer
+
+    dev = torch.device("cuda", 0) if a.device == "cuda" else torch.device("cpu")
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+    torch.manual_seed(0)
+    dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
+    spec = models.build(a.model, dev, dtype)
+    batch = spec.make_batch(a.batch, dev, seed=1000 + a.worker_id)
+    optim = OptimConfig(a.optimizer, lr=a.lr, momentum=0.9)
+    agent = ElasticAgent(a.coordinator, a.worker_id, heartbeat_s=min(a.heartbeat_s, 1.0))
+
+    def make_ps(model, transport):
+        shards = a.ps_shards if 0 < a.ps_shards <= transport.world else transport.world
+        return CollectivePS(model, optim, transport, num_shards=shards, staleness=a.staleness,
+                            bucket_mb=a.bucket_mb, device=dev, overlap=not spec.tied_weights,
+                            grad_dtype=dtype, param_dtype=dtype, pull_dtype=a.pull_dtype)
+
+    def make_trainer(ps):
+        return Trainer(spec.model, spec.loss, ps, batch, use_graph=False)
+
+    def on_step(step, loss, plan):
+        print(f"worker {a.worker_id} iter {step - 1} done=true loss={float(loss.detach()):.4f} gen={plan.gen} "
+              f"world={len(plan.members)}", flush=True)
+
+    et = ElasticTrainer(agent, spec.model, make_ps, make_trainer, a.iterations, dev, check_every=a.check_every,
+                        min_workers=a.min_workers, on_step=on_step)
+    et.install_signal_handler()
+    t0 = time.time()
+    res = et.run()
+    dt = time.time() - t0
+    if "left_at" in res:
+        print(f"worker {a.worker_id} left at iteration {res['left_at']} (handed its shards over)", flush=True)
+    else:
+        print(f"worker {a.worker_id} finished {a.iterations} iterations ({len(res['losses'])} here) in {dt:.2f} s "
+              f"after {res['resizes']} membership changes", flush=True)
+        csum = float(sum(p.double().sum() for p in res["params"].values()))
+        print(f"worker {a.worker_id} param checksum {csum:.10e}", flush=True)
+    if a.stats_json:
+        out = {"history": res["history"], "losses": res["losses"], "seconds": dt,
+               "left_at": res.get("left_at"), "finished_at": res.get("finished_at"),
+               "staleness_hist": res.get("staleness_hist")}
+        if res.get("params") is not None:
+            out["param_checksum"] = float(sum(p.double().sum() for p in res["params"].values()))
+        with open(a.stats_json, "w") as f:
+            json.dump(out, f)
+    return 0
 
 
 if __name__ == "__main__":

@@ -28,6 +28,7 @@ break that invariant; such models must pass ``overlap=False``.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 from dataclasses import dataclass, field
 
@@ -597,6 +598,111 @@ class CollectivePS:
                 shapes.append(list(p.shape))
                 tensors.append(full.narrow(0, o, k).cpu())
         native().save_reference_ckpt(path, epoch, iteration, names, shapes, tensors)
+
+    # ------------------------------------------------------------------ elastic resize
+    def close(self):
+        """Detach from the model (grad hooks, grad sinks) so a new CollectivePS over a different
+        world can take it over; the model keeps its current parameter values."""
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+        for m in self.model.modules():
+            if getattr(m, "_psd_grad_sink", None) == self._sink:
+                del m._psd_grad_sink
+        for p in self.model.parameters():
+            p.grad = None
+            p.data = p.data.clone()
+
+    def drain(self):
+        """Apply the up-to-S reduced gradients still in flight (steps t-S .. t-1) and publish the
+        result, so the shard state is complete at a membership change (no update is dropped).
+        Collective: every rank of the current world calls it at the same step boundary."""
+        t = self.step_idx
+        stream = self.comm_stream if self.is_cuda else None
+        if stream is not None:
+            stream.wait_stream(torch.cuda.current_stream(self.device))
+        ctx = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+        with ctx:
+            for j in range(max(0, t - self.S), t):  # pending: the gradient of step j is in slot j % (S+1)
+                self._advanced = False
+                for b in self.buckets:
+                    self._apply(b, j % (self.S + 1))
+                    self._pull(b)
+                for k in self.my_shards:
+                    self.tracker.on_apply(j % (self.S + 1), k)
+            for s in self.slots:
+                s.zero_()
+        if stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(stream)
+
+    def _canon_index(self):
+        """(flat offset, canonical offset, numel) per parameter, canonical = model.named_parameters
+        order without padding -- a layout independent of world size, shard count and buckets."""
+        where = {id(p): (o, n) for b in self.buckets for (_, p, o, n) in b.params}
+        out, c = [], 0
+        for _, p in self.model.named_parameters():
+            if id(p) in where:
+                o, n = where[id(p)]
+                out.append((o, c, n))
+                c += n
+        return out, c
+
+    def canonical_state(self, root: int) -> dict:
+        """Gather the fp32 masters + optimizer state of every shard onto rank ``root`` in the
+        canonical layout (collective). Returns the tensors on ``root``, None elsewhere."""
+        idx, n = self._canon_index()
+        out = {}
+        for key, src in (("master", self.master), ("state1", self.state1), ("state2", self.state2)):
+            if src is None:
+                continue
+            full = torch.zeros(self.total, dtype=torch.float32, device=self.device)
+            for b in self.buckets:
+                for j, k in enumerate(self.my_shards):
+                    full.narrow(0, b.offset + k * b.slice_numel, b.slice_numel).copy_(
+                        src.narrow(0, b.local_offset + j * b.slice_numel, b.slice_numel))
+            if self.world > 1:
+                self.t.reduce(full, root)  # owners hold disjoint slices: the sum is the gather
+            if self.rank == root:
+                canon = torch.empty(n, dtype=torch.float32, device=self.device)
+                for o, c, k in idx:
+                    canon.narrow(0, c, k).copy_(full.narrow(0, o, k))
+                out[key] = canon
+        if self.rank != root:
+            return None
+        out["dyn"] = self.dyn.t.detach().clone()
+        return out
+
+    def load_canonical_state(self, sd: dict):
+        """Inverse of ``canonical_state`` for this (possibly different) world: every rank passes the
+        full canonical tensors; owners keep their slices and every rank publishes the weights."""
+        idx, n = self._canon_index()
+        for key, dst in (("master", self.master), ("state1", self.state1), ("state2", self.state2)):
+            if dst is None or key not in sd:
+                continue
+            canon = sd[key].to(self.device)
+            if canon.numel() != n:
+                raise ValueError(f"canonical {key} has {canon.numel()} elements, model has {n}")
+            full = torch.zeros(self.total, dtype=torch.float32, device=self.device)
+            for o, c, k in idx:
+                full.narrow(0, o, k).copy_(canon.narrow(0, c, k))
+            for b in self.buckets:
+                for j, k in enumerate(self.my_shards):
+                    dst.narrow(0, b.local_offset + j * b.slice_numel, b.slice_numel).copy_(
+                        full.narrow(0, b.offset + k * b.slice_numel, b.slice_numel))
+            if key == "master":
+                if self.pull_fp8:
+                    for b in self.buckets:
+                        for j, k in enumerate(self.my_shards):
+                            self._quant_slice(b, k, self.master.narrow(0, b.local_offset + j * b.slice_numel,
+                                                                       b.slice_numel))
+                        self._pull(b)
+                else:
+                    self.params_flat.copy_(full)
+        if "dyn" in sd:
+            self.dyn.t.copy_(sd["dyn"].to(self.dyn.t.device))
+        for s in self.slots:
+            s.zero_()
+        self.step_idx = 0
 
     def full_params_fp32(self) -> dict:
         """Gather the fp32 masters of every shard (for checkpoints / inspection)."""

@@ -111,10 +111,26 @@ class CoordinatorService:
         self._stop.set()
 
 
+STORE_KEY = "psd/store_port"
+
+
+def host_store(svc: CoordinatorService, port: int = 0):
+    """Host the rendezvous TCPStore of the elastic collective data plane (runtime/elastic.py) in
+    the coordinator process, so it outlives any worker, and advertise its port in the kv."""
+    import torch.distributed as dist
+
+    store = dist.TCPStore("0.0.0.0", port, is_master=True, wait_for_workers=False)
+    svc.reg.kv_set(STORE_KEY, str(store.port).encode())
+    log.info("rendezvous store on port %d", store.port)
+    return store
+
+
 def serve(listen: str, ps_address: str, expiry_s: float = 30.0, sweep_s: float = 10.0,
-          shard_addresses: list[str] | None = None, block: bool = True):
+          shard_addresses: list[str] | None = None, block: bool = True, store_port: int | None = 0):
+    """``store_port``: port of the elastic rendezvous store (0: any free port; None: no store)."""
     host, port = split_host_port(ps_address, 50051)
     svc = CoordinatorService(host, port, expiry_s, sweep_s, shard_addresses)
+    svc.store = host_store(svc, store_port) if store_port is not None else None
     server = service.make_server()
     service.add_service(server, pb, svc)
     bound = server.add_insecure_port(listen)

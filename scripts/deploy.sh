@@ -5,6 +5,8 @@
 #   HOSTFILE unset  -> everything on localhost, worker i pinned to GPU (i % NUM_GPUS) when GPUs exist
 #   HOSTFILE=path   -> lines "host [gpu_count]"; the first host runs coordinator + PS, workers are
 #                      spread round-robin over the hosts with ssh (REMOTE_DIR must hold this repo)
+#   MODE=collective -> no PS process: workers run with --elastic, the PS shards live in their GPUs
+#                      (RCCL data plane) and scale_workers.sh up|down resizes the world mid-run
 # Env: WORKER_COUNT (3) ITERATIONS (100) COORDINATOR_PORT (50052) PS_PORT (50051)
 #      CHECKPOINT_INTERVAL (10) PS_FLAGS WORKER_FLAGS CLUSTER_DIR (/tmp/psd_cluster) SSH_USER KEY_FILE
 set -e
@@ -36,11 +38,17 @@ echo "coordinator: $COORD_HOST:$COORDINATOR_PORT  parameter server: $COORD_HOST:
 run_on "$HEAD" "COORDINATOR_PORT=$COORDINATOR_PORT PS_ADDRESS=$COORD_HOST:$PS_PORT LOG_FILE=$CLUSTER_DIR/coordinator.log \
   PID_FILE=$CLUSTER_DIR/coordinator.pid bash scripts/start_coordinator.sh"
 sleep 2
+if [ "$MODE" = "collective" ]; then
+  WORKER_FLAGS="--elastic --min-workers $WORKER_COUNT $WORKER_FLAGS"
+  echo "$WORKER_FLAGS" > "$CLUSTER_DIR/worker_flags"
+else
+rm -f "$CLUSTER_DIR/worker_flags"
 run_on "$HEAD" "PS_PORT=$PS_PORT TOTAL_WORKERS=$WORKER_COUNT CHECKPOINT_INTERVAL=$CHECKPOINT_INTERVAL \
   PS_FLAGS='--coordinator $COORD_HOST:$COORDINATOR_PORT --ckpt-dir $CLUSTER_DIR $PS_FLAGS' \
   LOG_FILE=$CLUSTER_DIR/parameter_server.log PID_FILE=$CLUSTER_DIR/parameter_server.pid \
   bash scripts/start_parameter_server.sh"
 sleep 2
+fi
 for ((i = 0; i < WORKER_COUNT; i++)); do
   H=${HOSTS[$((i % ${#HOSTS[@]}))]}
   GPU=""

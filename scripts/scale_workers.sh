@@ -20,6 +20,9 @@ if [ -z "$CMD" ] || [ -z "$N" ]; then
 fi
 CUR=$(cat "$CLUSTER_DIR/worker_count" 2>/dev/null || echo 0)
 COORD=$(cat "$CLUSTER_DIR/coordinator_address")
+# collective (MODE=collective deploy): joiners run with the deploy's elastic flags; the running world
+# absorbs them at its next membership check, and leavers hand their PS shards over before exiting
+[ -f "$CLUSTER_DIR/worker_flags" ] && WORKER_FLAGS="$(cat "$CLUSTER_DIR/worker_flags" | sed 's/--min-workers [0-9]*//') $WORKER_FLAGS"
 NUM_GPUS=${NUM_GPUS:-$(python3 -c "import torch;print(torch.cuda.device_count())" 2>/dev/null || echo 0)}
 case "$CMD" in
   up)

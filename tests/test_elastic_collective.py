@@ -1,0 +1,177 @@
+"""Elastic join/leave on the collective data plane (runtime/elastic.py): layout-independent PS
+state hand-over (canonical_state / load_canonical_state), draining of in-flight bounded-staleness
+gradients, and a multi-process run through deploy.sh MODE=collective + scale_workers.sh up/down
+(gloo ranks on CPU; the same code builds RCCL worlds on GPUs)."""
+import os
+import re
+import socket
+import subprocess
+import time
+
+import pytest
+import torch
+
+from parameter_server_distributed_amd import models
+from parameter_server_distributed_amd.ops.optim import OptimConfig
+from parameter_server_distributed_amd.parallel.collective_ps import CollectivePS
+from parameter_server_distributed_amd.runtime.trainer import Trainer
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CPU = torch.device("cpu")
+
+
+def _mlp(seed=0):
+    torch.manual_seed(seed)
+    return models.build("mlp", CPU, torch.float32)
+
+
+def _ps(spec, S, bucket_mb, opt="adam"):
+    return CollectivePS(spec.model, OptimConfig(opt, lr=1e-3), staleness=S, bucket_mb=bucket_mb,
+                        grad_dtype=torch.float32, param_dtype=torch.float32)
+
+
+@pytest.mark.parametrize("opt", ["momentum", "adam"])
+def test_canonical_state_roundtrip_across_layouts(opt):
+    spec = _mlp()
+    ps = _ps(spec, 1, 0.05, opt)
+    tr = Trainer(spec.model, spec.loss, ps, spec.make_batch(16, CPU))
+    for _ in range(4):
+        tr.step()
+    ps.drain()
+    sd = ps.canonical_state(root=0)
+    ref = {n: p.detach().clone() for n, p in spec.model.named_parameters()}
+    ps.close()
+    for n, p in spec.model.named_parameters():  # close() keeps the values, detached from the buffers
+        torch.testing.assert_close(p.detach(), ref[n], rtol=0, atol=0)
+    with torch.no_grad():
+        for p in spec.model.parameters():
+            p.zero_()
+    ps2 = _ps(spec, 2, 1.0, opt)  # different bucketing and staleness
+    ps2.load_canonical_state(sd)
+    for n, p in spec.model.named_parameters():
+        torch.testing.assert_close(p.detach(), ref[n], rtol=0, atol=0)
+    sd2 = ps2.canonical_state(root=0)
+    for k in sd:
+        torch.testing.assert_close(sd2[k], sd[k], rtol=0, atol=0)
+    assert ps2.step_idx == 0 and all(float(s.abs().sum()) == 0 for s in ps2.slots)
+
+
+def test_drain_applies_each_pending_gradient_once():
+    """S=2: after 5 steps only 3 updates were applied; drain applies the 2 in flight."""
+    spec = _mlp()
+    ps = _ps(spec, 2, 0.05, "momentum")
+    tr = Trainer(spec.model, spec.loss, ps, spec.make_batch(16, CPU))
+    for _ in range(5):
+        tr.step()
+    assert ps.dyn.step == 3
+    ps.drain()
+    assert ps.dyn.step == 5
+    assert sum(ps.staleness_histogram()) == 5
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _read(p):
+    try:
+        with open(p) as f:
+            return f.read()
+    except FileNotFoundError:
+        return ""
+
+
+def _iters(txt):
+    return [int(m) for m in re.findall(r"iter (\d+) done=true", txt)]
+
+
+def _wait_exit(pids, timeout):
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        alive = 0
+        for p in pids:
+            try:
+                os.kill(p, 0)
+                alive += 1
+            except ProcessLookupError:
+                pass
+        if not alive:
+            return True
+        time.sleep(0.3)
+    return False
+
+
+@pytest.mark.slow
+def test_collective_deploy_scale_up_down(tmp_path):
+    """deploy 2 elastic workers, scale up to 3 mid-run (the joiner starts at the step the world
+    grew), scale down to 2 (the leaver hands its shards over); survivors run every global step
+    exactly once across three generations and end with identical weights."""
+    cd = str(tmp_path / "cluster")
+    it = 500
+    env = dict(os.environ, CLUSTER_DIR=cd, MODE="collective", WORKER_COUNT="2", ITERATIONS=str(it), NUM_GPUS="0",
+               COORDINATOR_PORT=str(_port()), PS_PORT=str(_port()),
+               WORKER_FLAGS="--batch 32 --lr 0.01 --staleness 1 --check-every 5", PYTHONPATH=ROOT)
+    try:
+        subprocess.run(["bash", f"{ROOT}/scripts/deploy.sh"], env=env, check=True, timeout=60, capture_output=True)
+        t0 = time.time()
+        while max(_iters(_read(f"{cd}/worker_0.log")) or [0]) < 40 and time.time() - t0 < 90:
+            time.sleep(0.2)
+        r = subprocess.run(["bash", f"{ROOT}/scripts/scale_workers.sh", "up", "3"], env=env, capture_output=True,
+                           text=True, timeout=60)
+        assert r.returncode == 0, r.stdout + r.stderr
+        t0 = time.time()
+        while "world=3" not in _read(f"{cd}/worker_2.log") and time.time() - t0 < 90:
+            time.sleep(0.2)
+        assert "world=3" in _read(f"{cd}/worker_2.log"), _read(f"{cd}/worker_2.log")[-3000:]
+        r = subprocess.run(["bash", f"{ROOT}/scripts/scale_workers.sh", "down", "2"], env=env, capture_output=True,
+                           text=True, timeout=60)
+        assert r.returncode == 0, r.stdout + r.stderr
+        pids = [int(_read(f"{cd}/worker_{i}.pid")) for i in range(3)]
+        assert _wait_exit(pids, 180)
+        logs = [_read(f"{cd}/worker_{i}.log") for i in range(3)]
+        assert f"worker 0 finished {it} iterations" in logs[0], logs[0][-3000:]
+        assert f"worker 1 finished {it} iterations" in logs[1], logs[1][-3000:]
+        assert "worker 2 left at iteration" in logs[2], logs[2][-3000:]
+        for i in (0, 1):
+            assert _iters(logs[i]) == list(range(it)), i
+            assert "world=2" in logs[i] and "world=3" in logs[i]
+        j = _iters(logs[2])
+        assert j and j[0] > 0 and j == list(range(j[0], j[-1] + 1))
+        sums = [re.findall(r"param checksum ([-0-9.e+]+)", lg) for lg in logs[:2]]
+        assert sums[0] and sums[0] == sums[1], sums
+    finally:
+        for name in ("worker_0", "worker_1", "worker_2", "coordinator"):
+            p = _read(f"{cd}/{name}.pid").strip()
+            if p:
+                try:
+                    os.kill(int(p), 9)
+                except (ProcessLookupError, ValueError):
+                    pass
+
+
+@pytest.mark.gpu
+def test_handover_roundtrip_gpu_bf16(gpu):
+    """The hand-over path on the GPU data plane (bf16 working copy, fp32 masters in HBM, fused
+    apply): drain + canonical_state on one layout, load_canonical_state on another."""
+    torch.manual_seed(0)
+    spec = models.build("resnet50", gpu, torch.bfloat16, image_size=32, num_classes=10)
+    ps = CollectivePS(spec.model, OptimConfig("momentum", lr=0.01), staleness=1, bucket_mb=4, device=gpu)
+    tr = Trainer(spec.model, spec.loss, ps, spec.make_batch(4, gpu))
+    for _ in range(3):
+        tr.step()
+    ps.drain()
+    sd = ps.canonical_state(root=0)
+    ref = {n: p.detach().clone() for n, p in spec.model.named_parameters()}
+    ps.close()
+    ps2 = CollectivePS(spec.model, OptimConfig("momentum", lr=0.01), staleness=0, bucket_mb=16, device=gpu)
+    ps2.load_canonical_state(sd)
+    torch.cuda.synchronize()
+    for n, p in spec.model.named_parameters():
+        torch.testing.assert_close(p.detach(), ref[n], rtol=0, atol=0, msg=n)
+    sd2 = ps2.canonical_state(root=0)
+    for k in sd:
+        torch.testing.assert_close(sd2[k], sd[k], rtol=0, atol=0)
+    tr2 = Trainer(spec.model, spec.loss, ps2, spec.make_batch(4, gpu))
+    assert torch.isfinite(tr2.step()).item()

@@ -50,9 +50,39 @@ def main():
     print(f"# {a.title}\n")
     print(f"- window: last {S} steps, wall {(t1 - t0) / 1e6 / S:.2f} ms/step, kernel-busy {busy / 1e6 / S:.2f} ms/step, "
           f"{len(win) / S:.0f} kernels/step\n")
+    cats = collections.defaultdict(lambda: [0, 0])
+    for n, (d, c) in agg.items():
+        cats[category(n)][0] += d
+        cats[category(n)][1] += c
+    print("| category | share | calls/step | ms/step |\n|---|---:|---:|---:|")
+    for n, (d, c) in sorted(cats.items(), key=lambda kv: -kv[1][0]):
+        print(f"| {n} | {d / busy * 100:.1f}% | {c / S:.1f} | {d / 1e6 / S:.3f} |")
+    print()
     print("| share | calls/step | avg us | ms/step | kernel |\n|---:|---:|---:|---:|---|")
     for n, (d, c) in sorted(agg.items(), key=lambda kv: -kv[1][0])[: a.top]:
         print(f"| {d / busy * 100:.1f}% | {c / S:.1f} | {d / c / 1e3:.1f} | {d / 1e6 / S:.3f} | `{n}` |")
+
+
+CATEGORIES = [
+    ("psd: batchnorm", r"psd::bn_"),
+    ("psd: gemm", r"psd::.*(gemm|colsum|splitk)"),
+    ("psd: optimizer / PS apply", r"psd::.*(fused_apply|optim|multi_reduce|pack_cast|quant|amax|f32_to_bf16)"),
+    ("psd: other (pool, ...)", r"psd::"),
+    ("MIOpen/CK conv fwd", r"conv_fwd|igemm_fwd|fwd_gtc"),
+    ("MIOpen/CK conv bwd-data", r"bwd_data|igemm_bwd|bwd_gtc"),
+    ("MIOpen/CK conv bwd-weight", r"wrw|bwd_weight"),
+    ("CK batched GEMM (1x1 conv)", r"batched_gemm|gemm_xdl"),
+    ("MIOpen tensor ops / fills", r"SubTensorOp|fillBuffer|Transpose|transpose"),
+    ("torch elementwise / reduce", r"at::native"),
+    ("RCCL", r"nccl|rccl"),
+]
+
+
+def category(name: str) -> str:
+    for cat, pat in CATEGORIES:
+        if re.search(pat, name):
+            return cat
+    return "other"
 
 
 if __name__ == "__main__":
