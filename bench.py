@@ -139,8 +139,11 @@ def main():
         torch.cuda.synchronize(dev)
 
     t_w0 = time.perf_counter()
-    for _ in range(a.warmup):
+    for i in range(a.warmup):
         tr.step()
+        if rank == 0:  # progress (MIOpen tuning of unseen shapes can take minutes)
+            torch.cuda.synchronize(dev)
+            print(f"warmup step {i + 1}/{a.warmup}: {time.perf_counter() - t_w0:.1f} s", file=sys.stderr, flush=True)
     barrier()
     t_w = time.perf_counter() - t_w0
     mem_peak = torch.cuda.max_memory_allocated(dev)

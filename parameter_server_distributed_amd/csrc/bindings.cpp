@@ -28,10 +28,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("dequant_fp8_", &dequant_fp8_);
   m.def("bn_fwd", &bn_fwd, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("running_mean"),
         py::arg("running_var"), py::arg("residual"), py::arg("relu"), py::arg("training"), py::arg("momentum"),
-        py::arg("eps"), py::arg("counter"), py::arg("ss_eval"));
+        py::arg("eps"), py::arg("counter"), py::arg("ss_eval"), py::arg("mask_out") = false);
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("gamma"), py::arg("save_mean"),
         py::arg("save_invstd"), py::arg("relu"), py::arg("need_dr"), py::arg("dgamma_out"), py::arg("dbeta_out"),
-        py::arg("dy2") = py::none(), py::arg("ss") = py::none());
+        py::arg("dy2") = py::none(), py::arg("ss") = py::none(), py::arg("mbits") = py::none());
   m.def("gemm_", &gemm_, py::arg("A"), py::arg("B"), py::arg("a_kmajor"), py::arg("b_kmajor"), py::arg("out"),
         py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("aux") = py::none());
   m.def("gemm_splitk_", &gemm_splitk_, py::arg("A"), py::arg("B"), py::arg("a_kmajor"), py::arg("b_kmajor"),

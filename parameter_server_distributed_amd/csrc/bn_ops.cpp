@@ -36,7 +36,7 @@ void check_vec(const c10::optional<at::Tensor>& t, int64_t C, at::ScalarType st,
 std::vector<at::Tensor> bn_fwd(const at::Tensor& x_in, c10::optional<at::Tensor> gamma, c10::optional<at::Tensor> beta,
                                c10::optional<at::Tensor> running_mean, c10::optional<at::Tensor> running_var,
                                c10::optional<at::Tensor> residual, bool relu, bool training, double momentum, double eps,
-                               c10::optional<at::Tensor> counter, c10::optional<at::Tensor> ss_eval) {
+                               c10::optional<at::Tensor> counter, c10::optional<at::Tensor> ss_eval, bool mask_out) {
   TORCH_CHECK(x_in.is_cuda() && x_in.scalar_type() == at::kBFloat16, "psd bn: x must be a bf16 device tensor");
   const c10::DeviceGuard g(x_in.device());
   at::Tensor x = nhwc(x_in);
@@ -54,6 +54,8 @@ std::vector<at::Tensor> bn_fwd(const at::Tensor& x_in, c10::optional<at::Tensor>
   }
   auto f32 = x.options().dtype(at::kFloat);
   at::Tensor y = at::empty_like(x);
+  at::Tensor mbits;
+  if (relu && mask_out) mbits = at::empty({M * C / 8}, x.options().dtype(at::kByte));
   at::Tensor mean = at::empty({C}, f32), invstd = at::empty({C}, f32);
   at::Tensor ss;
   at::Tensor part;
@@ -68,6 +70,7 @@ std::vector<at::Tensor> bn_fwd(const at::Tensor& x_in, c10::optional<at::Tensor>
   a.x = reinterpret_cast<const uint16_t*>(x.data_ptr());
   a.res = res.defined() ? reinterpret_cast<const uint16_t*>(res.data_ptr()) : nullptr;
   a.y = reinterpret_cast<uint16_t*>(y.data_ptr());
+  a.mbits = mbits.defined() ? mbits.data_ptr<uint8_t>() : nullptr;
   a.gamma = opt_ptr<const uint16_t>(gamma);
   a.beta = opt_ptr<const uint16_t>(beta);
   a.running_mean = training ? opt_ptr<float>(running_mean) : nullptr;
@@ -85,14 +88,15 @@ std::vector<at::Tensor> bn_fwd(const at::Tensor& x_in, c10::optional<at::Tensor>
   a.eps = (float)eps;
   hipError_t e = launch_bn_fwd(a, stream_of(x));
   TORCH_CHECK(e == hipSuccess, "psd bn fwd: ", hipGetErrorString(e));
-  return {y, mean, invstd, ss};
+  return {y, mean, invstd, ss, mbits};
 }
 
 std::vector<at::Tensor> bn_bwd(const at::Tensor& dy_in, const at::Tensor& x_in, c10::optional<at::Tensor> y_in,
                                c10::optional<at::Tensor> gamma, const at::Tensor& save_mean,
                                const at::Tensor& save_invstd, bool relu, bool need_dr,
                                c10::optional<at::Tensor> dgamma_out, c10::optional<at::Tensor> dbeta_out,
-                               c10::optional<at::Tensor> dy2_in, c10::optional<at::Tensor> ss_in) {
+                               c10::optional<at::Tensor> dy2_in, c10::optional<at::Tensor> ss_in,
+                               c10::optional<at::Tensor> mbits_in) {
   const c10::DeviceGuard g(x_in.device());
   at::Tensor x = nhwc(x_in), dy = nhwc(dy_in);
   at::Tensor dy2;
@@ -103,10 +107,16 @@ std::vector<at::Tensor> bn_bwd(const at::Tensor& dy_in, const at::Tensor& x_in, 
   const int64_t C = channels(x);
   const int64_t M = x.numel() / C;
   TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == at::kBFloat16, "psd bn bwd: dy shape/dtype");
-  at::Tensor y, ss;
+  at::Tensor y, ss, mbits;
   if (relu) {
-    // ReLU mask source: the forward output y, or (no residual) x with the forward scale/shift
-    if (y_in.has_value() && y_in->defined()) {
+    // ReLU mask source: the forward bit-mask, the forward output y, or (no residual) x with the
+    // forward scale/shift
+    if (mbits_in.has_value() && mbits_in->defined()) {
+      mbits = *mbits_in;
+      TORCH_CHECK(need_dr, "psd bn bwd: the bit-mask path is for residual BNs");
+      TORCH_CHECK(mbits.scalar_type() == at::kByte && mbits.is_contiguous() && mbits.numel() == M * C / 8,
+                  "psd bn bwd: mbits must be uint8 [M*C/8]");
+    } else if (y_in.has_value() && y_in->defined()) {
       y = nhwc(*y_in);
     } else {
       TORCH_CHECK(ss_in.has_value() && ss_in->defined(), "psd bn bwd: relu needs the forward output or scale/shift");
@@ -134,7 +144,8 @@ std::vector<at::Tensor> bn_bwd(const at::Tensor& dy_in, const at::Tensor& x_in, 
   a.dy2 = dy2.defined() ? reinterpret_cast<const uint16_t*>(dy2.data_ptr()) : nullptr;
   a.y = y.defined() ? reinterpret_cast<const uint16_t*>(y.data_ptr()) : nullptr;
   a.ss = ss.defined() ? ss.data_ptr<float>() : nullptr;
-  a.x =reinterpret_cast<const uint16_t*>(x.data_ptr());
+  a.mbits = mbits.defined() ? mbits.data_ptr<uint8_t>() : nullptr;
+  a.x = reinterpret_cast<const uint16_t*>(x.data_ptr());
   a.gamma = opt_ptr<const uint16_t>(gamma);
   a.save_mean = save_mean.data_ptr<float>();
   a.save_invstd = save_invstd.data_ptr<float>();

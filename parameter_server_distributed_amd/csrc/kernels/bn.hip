@@ -186,10 +186,12 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const float* __res
   }
 }
 
-template <bool RELU, bool RES>
+// MASK_OUT: also write the ReLU mask as one bit per element (one byte per 8-channel vector, so a
+// wave stores 64 consecutive bytes): backward then reads 1/16 of the bytes y would cost.
+template <bool RELU, bool RES, bool MASK_OUT>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
                                                        const float* __restrict__ ss, uint16_t* __restrict__ y,
-                                                       int64_t nvec, int C) {
+                                                       uint8_t* __restrict__ mbits, int64_t nvec, int C) {
   const int tpc = C >> 3;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;  // host guarantees stride % tpc == 0
   int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -210,6 +212,12 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
       t[j] = o;
     }
     store8_bf16(y + v * 8, t);
+    if (MASK_OUT) {
+      uint32_t bits = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bits |= (t[j] > 0.f ? 1u : 0u) << j;
+      mbits[v] = (uint8_t)bits;
+    }
   }
 }
 
@@ -218,11 +226,13 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
 // before the ReLU). kMaskX: x*scale + shift > 0 recomputed from the forward's fp32 scale/shift --
 // the same fmaf the apply kernel rounded to y, so the mask is identical -- which saves one full
 // [M, C] read in both backward passes (and keeps y out of the autograd context).
-enum MaskSrc : int { kMaskNone = 0, kMaskY = 1, kMaskX = 2 };
+// kMaskBits: the 1-bit-per-element mask the forward apply wrote (residual BNs: 1/16 of y's bytes).
+enum MaskSrc : int { kMaskNone = 0, kMaskY = 1, kMaskX = 2, kMaskBits = 3 };
 
 template <int MASK, bool RES_OUT>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ dy2,
-                                                            const uint16_t* __restrict__ y, const float* __restrict__ ssf,
+                                                            const uint16_t* __restrict__ y, const uint8_t* __restrict__ mbits,
+                                                            const float* __restrict__ ssf,
                                                             const uint16_t* __restrict__ x, const float* __restrict__ mean,
                                                             uint16_t* __restrict__ dr, int64_t M, int C,
                                                             float* __restrict__ part) {
@@ -237,12 +247,13 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
       load8_f32(ssf + C + m.cg * 8, sh);
     }
     const int64_t stride = (int64_t)gridDim.x * m.rpi;
-    auto body = [&](int64_t off, const float* g0, const float* xv, const float* yv) {
+    auto body = [&](int64_t off, const float* g0, const float* xv, const float* yv, uint32_t bits) {
       float g[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         if (MASK == kMaskY) g[j] = yv[j] > 0.f ? g0[j] : 0.f;
         else if (MASK == kMaskX) g[j] = fmaf(xv[j], sc[j], sh[j]) > 0.f ? g0[j] : 0.f;
+        else if (MASK == kMaskBits) g[j] = ((bits >> j) & 1u) ? g0[j] : 0.f;
         else g[j] = g0[j];
       }
       if (RES_OUT) store8_bf16(dr + off, g);
@@ -274,8 +285,13 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
         load8_bf16(y + o0, y0);
         load8_bf16(y + o1, y1);
       }
-      body(o0, g0, x0, y0);
-      body(o1, g1, x1, y1);
+      uint32_t b0 = 0, b1 = 0;
+      if (MASK == kMaskBits) {  // one byte per 8-channel vector
+        b0 = mbits[o0 >> 3];
+        b1 = mbits[o1 >> 3];
+      }
+      body(o0, g0, x0, y0, b0);
+      body(o1, g1, x1, y1, b1);
     }
     for (; r < M; r += stride) {
       const int64_t o0 = r * C + m.cg * 8;
@@ -289,7 +305,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
         for (int j = 0; j < 8; ++j) g0[j] += h0[j];
       }
       if (MASK == kMaskY) load8_bf16(y + o0, y0);
-      body(o0, g0, x0, y0);
+      const uint32_t b0 = MASK == kMaskBits ? (uint32_t)mbits[o0 >> 3] : 0u;
+      body(o0, g0, x0, y0, b0);
     }
   }
   block_partials(m, C, a, b, part);
@@ -409,11 +426,14 @@ hipError_t launch_bn_fwd(const BnFwdArgs& a, hipStream_t st) {
   }
   const int64_t nvec = a.M * (a.C / 8);
   const int g = elem_grid(nvec, a.C);
-#define PSD_APPLY(R, S) hipLaunchKernelGGL((bn_apply_kernel<R, S>), dim3(g), dim3(256), 0, st, a.x, a.res, a.ss, a.y, nvec, a.C)
-  if (a.relu && a.res) PSD_APPLY(true, true);
-  else if (a.relu) PSD_APPLY(true, false);
-  else if (a.res) PSD_APPLY(false, true);
-  else PSD_APPLY(false, false);
+#define PSD_APPLY(R, S, B) \
+  hipLaunchKernelGGL((bn_apply_kernel<R, S, B>), dim3(g), dim3(256), 0, st, a.x, a.res, a.ss, a.y, a.mbits, nvec, a.C)
+  if (a.relu && a.res && a.mbits) PSD_APPLY(true, true, true);
+  else if (a.relu && a.mbits) PSD_APPLY(true, false, true);
+  else if (a.relu && a.res) PSD_APPLY(true, true, false);
+  else if (a.relu) PSD_APPLY(true, false, false);
+  else if (a.res) PSD_APPLY(false, true, false);
+  else PSD_APPLY(false, false, false);
 #undef PSD_APPLY
   return hipGetLastError();
 }
@@ -423,13 +443,15 @@ hipError_t launch_bn_bwd(const BnBwdArgs& a, hipStream_t st) {
   if (a.C % 8 != 0) return hipErrorInvalidValue;
   int gx, gy;
   reduce_grid(a.M, a.C, gx, gy);
-  // ReLU mask: from y when given, else recomputed from x and the forward scale/shift
-  const int mask = !a.relu ? kMaskNone : (a.y ? kMaskY : kMaskX);
+  // ReLU mask: forward bit-mask, else y, else recomputed from x and the forward scale/shift
+  const int mask = !a.relu ? kMaskNone : (a.mbits ? kMaskBits : (a.y ? kMaskY : kMaskX));
   if (mask == kMaskX && !a.ss) return hipErrorInvalidValue;
+  if (mask == kMaskBits && !a.dr) return hipErrorInvalidValue;  // bits are kept for residual BNs only
 #define PSD_RED(K, O)                                                                                              \
-  hipLaunchKernelGGL((bn_bwd_reduce_kernel<K, O>), dim3(gx, gy), dim3(256), 0, st, a.dy, a.dy2, a.y, a.ss, a.x,     \
-                     a.save_mean, a.dr, a.M, a.C, a.part)
-  if (mask == kMaskY && a.dr) PSD_RED(kMaskY, true);
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<K, O>), dim3(gx, gy), dim3(256), 0, st, a.dy, a.dy2, a.y, a.mbits, a.ss, \
+                     a.x, a.save_mean, a.dr, a.M, a.C, a.part)
+  if (mask == kMaskBits) PSD_RED(kMaskBits, true);
+  else if (mask == kMaskY && a.dr) PSD_RED(kMaskY, true);
   else if (mask == kMaskY) PSD_RED(kMaskY, false);
   else if (mask == kMaskX && a.dr) PSD_RED(kMaskX, true);
   else if (mask == kMaskX) PSD_RED(kMaskX, false);

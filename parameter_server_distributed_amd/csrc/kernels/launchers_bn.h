@@ -9,6 +9,7 @@ struct BnFwdArgs {
   const uint16_t* x;      // [M, C] bf16
   const uint16_t* res;    // optional residual [M, C] bf16
   uint16_t* y;            // [M, C] bf16
+  uint8_t* mbits;         // optional: ReLU mask out, 1 bit per element ([M * C / 8] bytes)
   const uint16_t* gamma;  // [C] bf16 (optional)
   const uint16_t* beta;   // [C] bf16 (optional)
   float* running_mean;    // [C] fp32 (optional; also used as the variance shift)
@@ -30,7 +31,8 @@ struct BnBwdArgs {
   const uint16_t* dy;
   const uint16_t* dy2;    // optional second upstream gradient (residual-branch fusion): dy + dy2
   const uint16_t* y;      // forward output (ReLU mask); null: mask recomputed from x and ss
-  const float* ss;        // [2C] forward scale/shift (needed when relu && !y)
+  const float* ss;        // [2C] forward scale/shift (needed when relu && !y && !mbits)
+  const uint8_t* mbits;   // forward ReLU bit-mask (residual BNs; requires dr)
   const uint16_t* x;      // forward input
   const uint16_t* gamma;
   const float* save_mean;

@@ -18,12 +18,14 @@ void dequant_fp8_(const at::Tensor& x, const at::Tensor& scale_inv, at::Tensor o
 std::vector<at::Tensor> bn_fwd(const at::Tensor& x, c10::optional<at::Tensor> gamma, c10::optional<at::Tensor> beta,
                                c10::optional<at::Tensor> running_mean, c10::optional<at::Tensor> running_var,
                                c10::optional<at::Tensor> residual, bool relu, bool training, double momentum, double eps,
-                               c10::optional<at::Tensor> counter, c10::optional<at::Tensor> ss_eval);
+                               c10::optional<at::Tensor> counter, c10::optional<at::Tensor> ss_eval,
+                               bool mask_out);
 std::vector<at::Tensor> bn_bwd(const at::Tensor& dy, const at::Tensor& x, c10::optional<at::Tensor> y,
                                c10::optional<at::Tensor> gamma, const at::Tensor& save_mean,
                                const at::Tensor& save_invstd, bool relu, bool need_dr,
                                c10::optional<at::Tensor> dgamma_out, c10::optional<at::Tensor> dbeta_out,
-                               c10::optional<at::Tensor> dy2, c10::optional<at::Tensor> ss);
+                               c10::optional<at::Tensor> dy2, c10::optional<at::Tensor> ss,
+                               c10::optional<at::Tensor> mbits);
 
 void gemm_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool b_kmajor, at::Tensor out,
            c10::optional<at::Tensor> bias, int64_t act, c10::optional<at::Tensor> aux);

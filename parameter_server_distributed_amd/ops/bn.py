@@ -30,23 +30,24 @@ class _FusedBNFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, mod, resid_to=None):
         C = native()
-        y, mean, invstd, ss = C.bn_fwd(x, weight, bias, mod.running_mean, mod.running_var, residual, mod.relu, True,
-                                       mod.momentum if mod.momentum is not None else 0.1, mod.eps,
-                                       mod.num_batches_tracked, None)
+        has_res = residual is not None
+        y, mean, invstd, ss, mbits = C.bn_fwd(x, weight, bias, mod.running_mean, mod.running_var, residual, mod.relu,
+                                              True, mod.momentum if mod.momentum is not None else 0.1, mod.eps,
+                                              mod.num_batches_tracked, None, mask_out=mod.relu and has_res)
         ctx.relu = mod.relu
         ctx.has_res = residual is not None
         ctx.mod = mod
         ctx.resid_to = resid_to
         # ReLU mask for backward: without a residual it is recomputed from x and the fp32
-        # scale/shift (one [M, C] read less per backward pass); with one, y itself is kept
-        keep_y = mod.relu and ctx.has_res
-        ctx.save_for_backward(x, y if keep_y else None, weight, mean, invstd,
-                              ss if (mod.relu and not keep_y) else None)
+        # scale/shift (one [M, C] read less per backward pass); with one, the forward kernel wrote
+        # it as a bit-mask (1/16 of y's bytes)
+        ctx.save_for_backward(x, mbits if mod.relu and has_res else None, weight, mean, invstd,
+                              ss if (mod.relu and not has_res) else None)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, w, mean, invstd, ss = ctx.saved_tensors
+        x, mbits, w, mean, invstd, ss = ctx.saved_tensors
         mod = ctx.mod
         sink = getattr(mod, "_psd_grad_sink", None)
         dgo = dbo = None
@@ -55,7 +56,8 @@ class _FusedBNFn(torch.autograd.Function):
         # residual-branch fusion: the identity-path gradient of this BN's output was stashed by the
         # next block's bn3 backward; fold it in here instead of an autograd add kernel
         dy2 = mod._psd_pending_dr.pop() if getattr(mod, "_psd_pending_dr", None) else None
-        dx, dr, dg, db = native().bn_bwd(dy, x, y, w, mean, invstd, ctx.relu, ctx.has_res, dgo, dbo, dy2, ss)
+        dx, dr, dg, db = native().bn_bwd(dy, x, None, w, mean, invstd, ctx.relu, ctx.has_res, dgo, dbo, dy2, ss,
+                                         mbits)
         res_grad = None
         if ctx.has_res:
             if ctx.resid_to is not None:
@@ -94,8 +96,7 @@ class FusedBatchNorm2d(nn.BatchNorm2d):
             ss = torch.cat([scale, shift]).contiguous()
             if torch.is_grad_enabled() and (x.requires_grad or self.weight.requires_grad):
                 return self._reference(x, residual)
-            y, _, _, _ = native().bn_fwd(x, None, None, None, None, residual, self.relu, False, 0.0, self.eps, None, ss)
-            return y
+            return native().bn_fwd(x, None, None, None, None, residual, self.relu, False, 0.0, self.eps, None, ss)[0]
         return self._reference(x, residual)
 
     def _reference(self, x, residual=None):
