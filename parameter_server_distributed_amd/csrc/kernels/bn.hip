@@ -191,7 +191,7 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const float* __res
 template <bool RELU, bool RES, bool MASK_OUT>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
                                                        const float* __restrict__ ss, uint16_t* __restrict__ y,
-                                                       uint8_t* __restrict__ mbits, int64_t nvec, int C) {
+                                                       uint8_t* __restrict__ mbits, int pack4, int64_t nvec, int C) {
   const int tpc = C >> 3;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;  // host guarantees stride % tpc == 0
   int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -216,7 +216,13 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
       uint32_t bits = 0;
 #pragma unroll
       for (int j = 0; j < 8; ++j) bits |= (t[j] > 0.f ? 1u : 0u) << j;
-      mbits[v] = (uint8_t)bits;
+      if (pack4) {  // 4 lanes -> one dword store (host: nvec % 4 == 0, so a lane quad is all active)
+        const uint32_t b1 = __shfl_down(bits, 1), b2 = __shfl_down(bits, 2), b3 = __shfl_down(bits, 3);
+        if ((threadIdx.x & 3) == 0)
+          *reinterpret_cast<uint32_t*>(mbits + v) = bits | (b1 << 8) | (b2 << 16) | (b3 << 24);
+      } else {
+        mbits[v] = (uint8_t)bits;
+      }
     }
   }
 }
@@ -427,7 +433,8 @@ hipError_t launch_bn_fwd(const BnFwdArgs& a, hipStream_t st) {
   const int64_t nvec = a.M * (a.C / 8);
   const int g = elem_grid(nvec, a.C);
 #define PSD_APPLY(R, S, B) \
-  hipLaunchKernelGGL((bn_apply_kernel<R, S, B>), dim3(g), dim3(256), 0, st, a.x, a.res, a.ss, a.y, a.mbits, nvec, a.C)
+  hipLaunchKernelGGL((bn_apply_kernel<R, S, B>), dim3(g), dim3(256), 0, st, a.x, a.res, a.ss, a.y, a.mbits, \
+                     (int)(nvec % 4 == 0), nvec, a.C)
   if (a.relu && a.res && a.mbits) PSD_APPLY(true, true, true);
   else if (a.relu && a.mbits) PSD_APPLY(true, false, true);
   else if (a.relu && a.res) PSD_APPLY(true, true, false);

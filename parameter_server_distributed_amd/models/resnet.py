@@ -17,6 +17,26 @@ from ..ops.bn import FusedBatchNorm2d
 from ..ops.pool import max_pool_3x3s2
 
 
+class _Fork(torch.autograd.Function):
+    """Two aliases of a block input for its two consumers (conv1 and the downsample conv). Autograd
+    hands their gradients to backward separately; the downsample-branch one is passed to the fused
+    BN that produced the input (added inside its backward kernels) instead of an autograd add kernel
+    over the whole activation. Ordering is by construction: this node's backward runs before the
+    producer BN's, which consumes the gradient it returns."""
+
+    @staticmethod
+    def forward(ctx, x, bn):
+        ctx.bn = bn
+        return x.view_as(x), x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g_main, g_ds):
+        if g_main is None or g_ds is None:
+            return (g_ds if g_main is None else g_main), None
+        ctx.bn._psd_pending_dr.append(g_ds)
+        return g_main, None
+
+
 def _conv(cin, cout, k, stride=1, groups=1):
     return nn.Conv2d(cin, cout, k, stride=stride, padding=k // 2, groups=groups, bias=False)
 
@@ -38,10 +58,15 @@ class Bottleneck(nn.Module):
         self.fuse_residual_grad = True
 
     def forward(self, x, prev_bn=None):
-        """``prev_bn``: the fused BN that produced ``x`` (the previous block's bn3). For identity
-        blocks the residual gradient is then handed to it inside the BN kernels (no autograd add)."""
-        idt = x if self.downsample is None else self.downsample(x)
-        out = self.bn1(self.conv1(x))
+        """``prev_bn``: the fused BN that produced ``x`` (the previous block's bn3). The second
+        gradient of ``x`` -- the identity residual's, or the downsample conv's -- is then handed to
+        it inside the BN kernels (no autograd add over the activation)."""
+        xm = xd = x
+        if (self.downsample is not None and prev_bn is not None and self.fuse_residual_grad
+                and torch.is_grad_enabled() and x.requires_grad and prev_bn.training and x.is_cuda):
+            xm, xd = _Fork.apply(x, prev_bn)  # downsample-branch gradient -> prev_bn's kernels
+        idt = x if self.downsample is None else self.downsample(xd)
+        out = self.bn1(self.conv1(xm))
         out = self.bn2(self.conv2(out))
         fuse = prev_bn if (self.downsample is None and self.fuse_residual_grad) else None
         return self.bn3(self.conv3(out), idt, resid_grad_to=fuse)
