@@ -40,7 +40,10 @@ PYBIND11_MODULE(_C, m) {
         py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("aux") = py::none());
   m.def("colsum_", &colsum_, py::arg("x"), py::arg("out"), py::arg("accumulate") = false);
   m.def("maxpool3s2_fwd", &maxpool3s2_fwd);
-  m.def("maxpool3s2_bwd", &maxpool3s2_bwd);
+  m.def("maxpool3s2_bwd", &maxpool3s2_bwd, py::arg("dy"), py::arg("arg"), py::arg("H"), py::arg("W"),
+        py::arg("dy2") = py::none());
+  m.def("gap_fwd", &gap_fwd);
+  m.def("gap_bwd", &gap_bwd);
   m.attr("OPT_SGD") = (int)OPT_SGD;
   m.attr("OPT_MOMENTUM") = (int)OPT_MOMENTUM;
   m.attr("OPT_ADAM") = (int)OPT_ADAM;

@@ -181,14 +181,51 @@ std::vector<at::Tensor> maxpool3s2_fwd(const at::Tensor& x_in) {
   TORCH_CHECK(e == hipSuccess, "psd maxpool fwd: ", hipGetErrorString(e));
   return {y, arg};
 }
-at::Tensor maxpool3s2_bwd(const at::Tensor& dy_in, const at::Tensor& arg, int64_t H, int64_t W) {
+at::Tensor maxpool3s2_bwd(const at::Tensor& dy_in, const at::Tensor& arg, int64_t H, int64_t W,
+                          const c10::optional<at::Tensor>& dy2_in) {
   const c10::DeviceGuard g(dy_in.device());
   at::Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
   const int N = dy.size(0), C = dy.size(1), Ho = dy.size(2), Wo = dy.size(3);
+  TORCH_CHECK(arg.is_contiguous(at::MemoryFormat::ChannelsLast) && arg.sizes() == dy.sizes(), "psd maxpool bwd: argmax shape");
+  at::Tensor dy2;
+  if (dy2_in.has_value() && dy2_in->defined()) {
+    dy2 = dy2_in->contiguous(at::MemoryFormat::ChannelsLast);
+    TORCH_CHECK(dy2.sizes() == dy.sizes() && dy2.scalar_type() == at::kBFloat16, "psd maxpool bwd: dy2 shape/dtype");
+  }
   at::Tensor dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
-  hipError_t e = launch_maxpool_bwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()), arg.data_ptr<uint8_t>(),
+  hipError_t e = launch_maxpool_bwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
+                                    dy2.defined() ? reinterpret_cast<const uint16_t*>(dy2.data_ptr()) : nullptr,
+                                    arg.data_ptr<uint8_t>(),
                                     reinterpret_cast<uint16_t*>(dx.data_ptr()), N, (int)H, (int)W, C, Ho, Wo, stream_of(dy));
   TORCH_CHECK(e == hipSuccess, "psd maxpool bwd: ", hipGetErrorString(e));
+  return dx;
+}
+}  // namespace psd
+
+// ---- NHWC global average pool (kernels/pool.hip)
+namespace psd {
+at::Tensor gap_fwd(const at::Tensor& x_in) {
+  TORCH_CHECK(x_in.is_cuda() && x_in.scalar_type() == at::kBFloat16 && x_in.dim() == 4 && x_in.size(1) % 8 == 0,
+              "psd gap: bf16 NCHW-shaped, C % 8 == 0");
+  const c10::DeviceGuard g(x_in.device());
+  at::Tensor x = x_in.contiguous(at::MemoryFormat::ChannelsLast);
+  const int N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
+  at::Tensor y = at::empty({N, C}, x.options());
+  hipError_t e = launch_gap_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<uint16_t*>(y.data_ptr()),
+                                N, HW, C, stream_of(x));
+  TORCH_CHECK(e == hipSuccess, "psd gap fwd: ", hipGetErrorString(e));
+  return y;
+}
+at::Tensor gap_bwd(const at::Tensor& dy_in, int64_t H, int64_t W) {
+  TORCH_CHECK(dy_in.is_cuda() && dy_in.scalar_type() == at::kBFloat16 && dy_in.dim() == 2 && dy_in.size(1) % 8 == 0,
+              "psd gap bwd: bf16 [N, C], C % 8 == 0");
+  const c10::DeviceGuard g(dy_in.device());
+  at::Tensor dy = dy_in.contiguous();
+  const int N = dy.size(0), C = dy.size(1);
+  at::Tensor dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  hipError_t e = launch_gap_bwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<uint16_t*>(dx.data_ptr()),
+                                N, (int)(H * W), C, stream_of(dy));
+  TORCH_CHECK(e == hipSuccess, "psd gap bwd: ", hipGetErrorString(e));
   return dx;
 }
 }  // namespace psd

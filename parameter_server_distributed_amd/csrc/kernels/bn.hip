@@ -20,6 +20,8 @@
 #include "common.h"
 #include "launchers_bn.h"
 
+#include <cstdlib>
+
 namespace psd {
 
 namespace {
@@ -45,6 +47,12 @@ __device__ __forceinline__ Map make_map(int C) {
   }
   return m;
 }
+
+// Row visited at logical position r. With rev = 1 the reduce passes walk the rows back to front,
+// meant to hit the tail the producing convolution wrote last in the 256 MB Infinity Cache (MALL)
+// and leave the head cached for the front-to-back apply pass. Measured neutral at b1024 (the
+// passes are HBM-bound at 5.4-6 TB/s either way), kept as an A/B switch.
+__device__ __forceinline__ int64_t row_of(int64_t r, int64_t M, int rev) { return rev ? M - 1 - r : r; }
 
 // Sum the per-lane partials (a[8], b[8]) of lanes sharing a channel group and write the block's
 // partials to part[blockIdx.x][0|1][C].
@@ -117,7 +125,8 @@ __device__ __forceinline__ bool sum_partials(const float* __restrict__ part, int
 
 // ------------------------------------------------------------------ forward
 __global__ __launch_bounds__(256) void bn_fwd_reduce_kernel(const uint16_t* __restrict__ x, int64_t M, int C,
-                                                            const float* __restrict__ shift_k, float* __restrict__ part) {
+                                                            const float* __restrict__ shift_k, float* __restrict__ part,
+                                                            int rev) {
   const Map m = make_map(C);
   float a[8], b[8], k[8];
 #pragma unroll
@@ -129,7 +138,7 @@ __global__ __launch_bounds__(256) void bn_fwd_reduce_kernel(const uint16_t* __re
     for (; r + 3 * stride < M; r += 4 * stride) {  // 4 independent 16-B loads in flight per lane
       float v[4][8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) load8_bf16(x + (r + u * stride) * C + m.cg * 8, v[u]);
+      for (int u = 0; u < 4; ++u) load8_bf16(x + row_of(r + u * stride, M, rev) * C + m.cg * 8, v[u]);
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
@@ -141,7 +150,7 @@ __global__ __launch_bounds__(256) void bn_fwd_reduce_kernel(const uint16_t* __re
     }
     for (; r < M; r += stride) {
       float v0[8];
-      load8_bf16(x + r * C + m.cg * 8, v0);
+      load8_bf16(x + row_of(r, M, rev) * C + m.cg * 8, v0);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float d0 = v0[j] - k[j];
@@ -241,7 +250,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
                                                             const float* __restrict__ ssf,
                                                             const uint16_t* __restrict__ x, const float* __restrict__ mean,
                                                             uint16_t* __restrict__ dr, int64_t M, int C,
-                                                            float* __restrict__ part) {
+                                                            float* __restrict__ part, int rev) {
   const Map m = make_map(C);
   float a[8], b[8], mu[8], sc[8], sh[8];
 #pragma unroll
@@ -271,7 +280,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
     };
     int64_t r = (int64_t)blockIdx.x * m.rpi + m.r0;
     for (; r + stride < M; r += 2 * stride) {  // two rows (6 loads) in flight per lane
-      const int64_t o0 = r * C + m.cg * 8, o1 = (r + stride) * C + m.cg * 8;
+      const int64_t o0 = row_of(r, M, rev) * C + m.cg * 8, o1 = row_of(r + stride, M, rev) * C + m.cg * 8;
       float g0[8], g1[8], x0[8], x1[8], y0[8], y1[8];
       load8_bf16(dy + o0, g0);
       load8_bf16(dy + o1, g1);
@@ -300,7 +309,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
       body(o1, g1, x1, y1, b1);
     }
     for (; r < M; r += stride) {
-      const int64_t o0 = r * C + m.cg * 8;
+      const int64_t o0 = row_of(r, M, rev) * C + m.cg * 8;
       float g0[8], x0[8], y0[8];
       load8_bf16(dy + o0, g0);
       load8_bf16(x + o0, x0);
@@ -385,6 +394,16 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(const uint16_t* __res
 }
 
 // ------------------------------------------------------------------ host launchers
+// PSD_BN_REVERSE=1 walks the reduce passes back to front (A/B switch; measured neutral on a
+// b1024 ResNet-50 step, so off by default).
+static int bn_reverse() {
+  static const int v = [] {
+    const char* e = getenv("PSD_BN_REVERSE");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 static int gcd_i(int a, int b) { return b == 0 ? a : gcd_i(b, a % b); }
 
 static void reduce_grid(int64_t M, int C, int& gx, int& gy) {
@@ -425,7 +444,8 @@ hipError_t launch_bn_fwd(const BnFwdArgs& a, hipStream_t st) {
   int gx, gy;
   reduce_grid(a.M, a.C, gx, gy);
   if (a.training) {
-    hipLaunchKernelGGL(bn_fwd_reduce_kernel, dim3(gx, gy), dim3(256), 0, st, a.x, a.M, a.C, a.running_mean, a.part);
+    hipLaunchKernelGGL(bn_fwd_reduce_kernel, dim3(gx, gy), dim3(256), 0, st, a.x, a.M, a.C, a.running_mean, a.part,
+                       bn_reverse());
     hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((a.C + kFinCh - 1) / kFinCh), dim3(256), 0, st, a.part, gx, a.M, a.C,
                        a.running_mean, a.gamma, a.beta, a.running_mean, a.running_var, a.momentum, a.eps, a.save_mean,
                        a.save_invstd, a.ss, a.counter);
@@ -456,7 +476,8 @@ hipError_t launch_bn_bwd(const BnBwdArgs& a, hipStream_t st) {
   if (mask == kMaskBits && !a.dr) return hipErrorInvalidValue;  // bits are kept for residual BNs only
 #define PSD_RED(K, O)                                                                                              \
   hipLaunchKernelGGL((bn_bwd_reduce_kernel<K, O>), dim3(gx, gy), dim3(256), 0, st, a.dy, a.dy2, a.y, a.mbits, a.ss, \
-                     a.x, a.save_mean, a.dr, a.M, a.C, a.part)
+                     a.x, a.save_mean, a.dr, a.M, a.C, a.part, \
+                     bn_reverse())
   if (mask == kMaskBits) PSD_RED(kMaskBits, true);
   else if (mask == kMaskY && a.dr) PSD_RED(kMaskY, true);
   else if (mask == kMaskY) PSD_RED(kMaskY, false);

@@ -52,7 +52,10 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint16_t* __rest
   }
 }
 
-__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const uint16_t* __restrict__ dy, const uint8_t* __restrict__ arg,
+// dy2 (optional, same shape as dy): a second consumer's gradient of the pool output (the
+// downsample branch of the first bottleneck), summed here instead of by an autograd add kernel.
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ dy2,
+                                                          const uint8_t* __restrict__ arg,
                                                           uint16_t* __restrict__ dx, int N, int H, int W, int C, int Ho,
                                                           int Wo) {
   const int c8n = C >> 3;
@@ -80,6 +83,12 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const uint16_t* __rest
         const uint2 ai = *reinterpret_cast<const uint2*>(arg + o);
         float g[8];
         load8_bf16(dy + o, g);
+        if (dy2) {
+          float g2[8];
+          load8_bf16(dy2 + o, g2);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) g[e] += g2[e];
+        }
         const uint8_t want = (uint8_t)(dh * 3 + dw);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -100,11 +109,76 @@ hipError_t launch_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int 
   return hipGetLastError();
 }
 
-hipError_t launch_maxpool_bwd(const uint16_t* dy, const uint8_t* arg, uint16_t* dx, int N, int H, int W, int C, int Ho,
+hipError_t launch_maxpool_bwd(const uint16_t* dy, const uint16_t* dy2, const uint8_t* arg, uint16_t* dx, int N, int H, int W, int C, int Ho,
                               int Wo, hipStream_t st) {
   if (C % 8) return hipErrorInvalidValue;
   const int64_t total = (int64_t)N * H * W * (C / 8);
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(stream_grid(total, 256)), dim3(256), 0, st, dy, arg, dx, N, H, W, C, Ho, Wo);
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(stream_grid(total, 256)), dim3(256), 0, st, dy, dy2, arg, dx, N, H, W, C, Ho, Wo);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ global average pool
+// NHWC [N, HW, C] -> [N, C] (the ResNet head). One lane per (n, 8 channels): HW 16-byte loads
+// with stride C, fp32 sum. Backward writes dx[n, hw, :] = dy[n, :] / HW with 16-byte stores
+// (PyTorch's channels_last expand kernel took ~400 us per b1024 step for the same 205 MB).
+__global__ __launch_bounds__(256) void gap_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, int N,
+                                                      int HW, int C, float inv) {
+  const int c8n = C >> 3;
+  const int64_t total = (int64_t)N * c8n;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t n = t / c8n;
+    const int c8 = (int)(t % c8n);
+    const uint16_t* p = x + n * HW * C + c8 * 8;
+    float a[8] = {0, 0, 0, 0, 0, 0, 0, 0}, b[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int i = 0;
+    for (; i + 1 < HW; i += 2) {
+      float v0[8], v1[8];
+      load8_bf16(p + (int64_t)i * C, v0);
+      load8_bf16(p + (int64_t)(i + 1) * C, v1);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        a[e] += v0[e];
+        b[e] += v1[e];
+      }
+    }
+    if (i < HW) {
+      float v0[8];
+      load8_bf16(p + (int64_t)i * C, v0);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] += v0[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] = (a[e] + b[e]) * inv;
+    store8_bf16(y + t * 8, a);
+  }
+}
+
+__global__ __launch_bounds__(256) void gap_bwd_kernel(const uint16_t* __restrict__ dy, uint16_t* __restrict__ dx, int N,
+                                                      int HW, int C, float inv) {
+  const int c8n = C >> 3;
+  const int64_t total = (int64_t)N * HW * c8n;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int c8 = (int)(t % c8n);
+    const int64_t n = t / ((int64_t)HW * c8n);
+    float g[8];
+    load8_bf16(dy + (n * c8n + c8) * 8, g);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] *= inv;
+    store8_bf16(dx + t * 8, g);
+  }
+}
+
+hipError_t launch_gap_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t st) {
+  if (C % 8 || HW <= 0) return hipErrorInvalidValue;
+  const int64_t total = (int64_t)N * (C / 8);
+  hipLaunchKernelGGL(gap_fwd_kernel, dim3(stream_grid(total, 256)), dim3(256), 0, st, x, y, N, HW, C, 1.f / HW);
+  return hipGetLastError();
+}
+
+hipError_t launch_gap_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipStream_t st) {
+  if (C % 8 || HW <= 0) return hipErrorInvalidValue;
+  const int64_t total = (int64_t)N * HW * (C / 8);
+  hipLaunchKernelGGL(gap_bwd_kernel, dim3(stream_grid(total, 256)), dim3(256), 0, st, dy, dx, N, HW, C, 1.f / HW);
   return hipGetLastError();
 }
 

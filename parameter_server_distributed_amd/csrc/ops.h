@@ -35,6 +35,9 @@ void colsum_(const at::Tensor& x, at::Tensor out, bool accumulate);
 void gemm_fp8_(const at::Tensor& A, const at::Tensor& B, const at::Tensor& a_scale, const at::Tensor& b_scale,
                at::Tensor out, c10::optional<at::Tensor> bias, int64_t act, c10::optional<at::Tensor> aux);
 std::vector<at::Tensor> maxpool3s2_fwd(const at::Tensor& x);
-at::Tensor maxpool3s2_bwd(const at::Tensor& dy, const at::Tensor& arg, int64_t H, int64_t W);
+at::Tensor maxpool3s2_bwd(const at::Tensor& dy, const at::Tensor& arg, int64_t H, int64_t W,
+                          const c10::optional<at::Tensor>& dy2);
+at::Tensor gap_fwd(const at::Tensor& x);
+at::Tensor gap_bwd(const at::Tensor& dy, int64_t H, int64_t W);
 
 }  // namespace psd

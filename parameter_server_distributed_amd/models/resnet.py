@@ -11,18 +11,18 @@ from __future__ import annotations
 
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
 from ..ops.bn import FusedBatchNorm2d
-from ..ops.pool import max_pool_3x3s2
+from ..ops.conv import Conv1x1
+from ..ops.pool import MaxPool3x3s2, global_avg_pool
 
 
 class _Fork(torch.autograd.Function):
     """Two aliases of a block input for its two consumers (conv1 and the downsample conv). Autograd
     hands their gradients to backward separately; the downsample-branch one is passed to the fused
-    BN that produced the input (added inside its backward kernels) instead of an autograd add kernel
-    over the whole activation. Ordering is by construction: this node's backward runs before the
-    producer BN's, which consumes the gradient it returns."""
+    BN (or the stem max-pool) that produced the input and added inside its backward kernels,
+    instead of by an autograd add kernel over the whole activation. Ordering is by construction:
+    this node's backward runs before the producer's, which consumes the gradient it returns."""
 
     @staticmethod
     def forward(ctx, x, bn):
@@ -38,6 +38,8 @@ class _Fork(torch.autograd.Function):
 
 
 def _conv(cin, cout, k, stride=1, groups=1):
+    if k == 1 and stride == 1 and groups == 1:
+        return Conv1x1(cin, cout)  # per-shape MIOpen / hipBLASLt (ops/conv.py)
     return nn.Conv2d(cin, cout, k, stride=stride, padding=k // 2, groups=groups, bias=False)
 
 
@@ -79,6 +81,7 @@ class ResNet(nn.Module):
         self.cin = 64
         self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
         self.bn1 = FusedBatchNorm2d(64, relu=True)
+        self.maxpool = MaxPool3x3s2()
         self.layer1 = self._make(64, layers[0])
         self.layer2 = self._make(128, layers[1], stride=2)
         self.layer3 = self._make(256, layers[2], stride=2)
@@ -108,14 +111,14 @@ class ResNet(nn.Module):
 
     def forward(self, x):
         x = self.bn1(self.conv1(x))
-        x = max_pool_3x3s2(x)
-        prev = None
+        x = self.maxpool(x)
+        # the first bottleneck's downsample-branch gradient goes to the max-pool's backward kernel
+        prev = self.maxpool if self.maxpool.native_last else None
         for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
             for blk in layer:
                 x = blk(x, prev)
                 prev = blk.bn3
-        x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
-        return self.fc(x)
+        return self.fc(global_avg_pool(x))
 
 
 def resnet50(num_classes=1000):

@@ -1,0 +1,138 @@
+"""1x1 / stride-1 convolutions of the NHWC ResNets as GEMMs where that is faster than MIOpen.
+
+On NHWC bf16 a 1x1 stride-1 convolution *is* a GEMM over the [N*H*W, C] view of the activation:
+
+  forward  Y[M, cout] = X[M, cin] . W[cout, cin]^T
+  dgrad    dX[M, cin] = dY[M, cout] . W[cout, cin]
+  wgrad    dW[cout, cin] = dY^T . X            (a K = N*H*W reduction)
+
+rocprofv3 of the b1024 ResNet-50 step (profiles/resnet50_b1024_r1_kernels.md) showed MIOpen
+running every 1x1 bwd-data as a CK kernel that needs its output zero-filled first (a 50-240 us
+``fillBufferAligned`` per layer) and, including that fill, 1.2-1.9x slower than hipBLASLt on the
+same GEMM (tools/gemm_bench.py, profiles/gemm_vs_hipblaslt_miopen_r1.md). Forward is a toss-up per
+shape, wgrad is MIOpen's (hipBLASLt is 4-9x slower on the K = N*H*W reduction).
+
+So each shape is autotuned once, in the first eager step (the same role as MIOpen's own Find):
+forward picks MIOpen or hipBLASLt, bwd-data picks MIOpen or hipBLASLt, by timing both with HIP
+events; bwd-weight always stays on MIOpen. Decisions are cached per (M, cin, cout); inside a
+hipGraph capture no timing happens (an undecided shape takes MIOpen). ``PSD_CONV1X1=0`` turns the
+GEMM routes off (A/B switch).
+
+Reference parity: none -- the reference has no model (its gradient is the constant 0.01,
+src/worker.cpp:316-329). This is worker-side compute for the BASELINE.json ResNet configs.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+_DECISIONS: dict[tuple, str] = {}
+
+
+def _enabled() -> bool:
+    return os.environ.get("PSD_CONV1X1", "1") != "0"
+
+
+def _time_ms(fn, reps: int = 3) -> float:
+    fn()  # warm (library heuristics / kernel load)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def _choose(key: tuple, candidates: dict) -> str:
+    """Fastest candidate for ``key`` (timed once, cached); MIOpen while a graph is being captured."""
+    got = _DECISIONS.get(key)
+    if got is not None:
+        return got
+    if torch.cuda.is_current_stream_capturing():
+        return "miopen"
+    times = {name: _time_ms(fn) for name, fn in candidates.items()}
+    best = min(times, key=times.get)
+    _DECISIONS[key] = best
+    return best
+
+
+def decisions() -> dict:
+    """The cached per-shape choices (for logs / tests)."""
+    return dict(_DECISIONS)
+
+
+def _as_2d(t: torch.Tensor) -> torch.Tensor:
+    """[N, C, H, W] channels_last -> the [N*H*W, C] row-major view."""
+    n, c, h, w = t.shape
+    return t.permute(0, 2, 3, 1).reshape(n * h * w, c)
+
+
+def _from_2d(t2: torch.Tensor, n: int, h: int, w: int) -> torch.Tensor:
+    return t2.view(n, h, w, t2.shape[1]).permute(0, 3, 1, 2)
+
+
+class _Conv1x1Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight):
+        n, cin, h, w = x.shape
+        cout = weight.shape[0]
+        w2 = weight.reshape(cout, cin)
+        x2 = _as_2d(x)
+        key = ("fwd", n * h * w, cin, cout)
+
+        def gemm():
+            return _from_2d(torch.mm(x2, w2.t()), n, h, w)
+
+        def miopen():
+            return F.conv2d(x, weight)
+
+        how = _choose(key, {"gemm": gemm, "miopen": miopen})
+        y = gemm() if how == "gemm" else miopen()
+        ctx.save_for_backward(x, weight)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        n, cin, h, w = x.shape
+        cout = weight.shape[0]
+        if not dy.is_contiguous(memory_format=torch.channels_last):
+            dy = dy.contiguous(memory_format=torch.channels_last)
+        need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        dx = dw = None
+        conv_bwd = torch.ops.aten.convolution_backward
+        args = (None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1)
+        if need_x:
+            w2 = weight.reshape(cout, cin)
+            dy2 = _as_2d(dy)
+            key = ("dgrad", n * h * w, cin, cout)
+
+            def gemm():
+                return _from_2d(torch.mm(dy2, w2), n, h, w)
+
+            def miopen():
+                return conv_bwd(dy, x, weight, *args, [True, False, False])[0]
+
+            dx = gemm() if _choose(key, {"gemm": gemm, "miopen": miopen}) == "gemm" else miopen()
+        if need_w:
+            dw = conv_bwd(dy, x, weight, *args, [False, True, False])[1]
+        return dx, dw
+
+
+class Conv1x1(nn.Conv2d):
+    """``nn.Conv2d(cin, cout, 1, bias=False)`` whose NHWC bf16 training path runs the per-shape
+    fastest of MIOpen / hipBLASLt for forward and bwd-data (see module docstring)."""
+
+    def __init__(self, cin: int, cout: int):
+        super().__init__(cin, cout, 1, stride=1, padding=0, bias=False)
+
+    def forward(self, x):
+        if (_enabled() and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
+                and self.weight.dtype == torch.bfloat16 and torch.is_grad_enabled()
+                and x.is_contiguous(memory_format=torch.channels_last)):
+            return _Conv1x1Fn.apply(x, self.weight)
+        return F.conv2d(x, self.weight)

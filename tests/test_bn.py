@@ -127,3 +127,80 @@ def test_resnet_residual_grad_fusion_matches_unfused(gpu):
     for n in grads[0]:
         a, b = grads[0][n], grads[1][n]
         torch.testing.assert_close(a, b, rtol=3e-2, atol=3e-2 * (b.abs().max().item() + 1e-3), msg=n)
+
+
+@pytest.mark.gpu
+def test_maxpool3s2_second_gradient_is_summed(gpu):
+    """dy2 (the first bottleneck's downsample-branch gradient) is added inside the gather kernel."""
+    from parameter_server_distributed_amd import native
+
+    torch.manual_seed(0)
+    x = torch.randn(2, 16, 12, 10).to(torch.bfloat16).to(gpu).contiguous(memory_format=torch.channels_last)
+    y, arg = native().maxpool3s2_fwd(x)
+    g1 = torch.randn(y.shape).to(torch.bfloat16).to(gpu).contiguous(memory_format=torch.channels_last)
+    g2 = torch.randn(y.shape).to(torch.bfloat16).to(gpu).contiguous(memory_format=torch.channels_last)
+    both = native().maxpool3s2_bwd(g1, arg, 12, 10, g2)
+    xr = x.float().cpu().requires_grad_(True)
+    F.max_pool2d(xr, 3, 2, 1).backward(g1.float().cpu() + g2.float().cpu())
+    torch.testing.assert_close(both.float().cpu(), xr.grad, rtol=1e-2, atol=2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(4, 2048, 7, 7), (3, 64, 5, 3), (2, 8, 1, 1)], ids=str)
+def test_global_avg_pool_matches_torch(gpu, shape):
+    from parameter_server_distributed_amd.ops.pool import global_avg_pool
+
+    torch.manual_seed(0)
+    x = torch.randn(shape).to(torch.bfloat16)
+    xd = x.to(gpu).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    y = global_avg_pool(xd)
+    assert y.shape == (shape[0], shape[1])
+    g = torch.randn(y.shape).to(torch.bfloat16)
+    y.backward(g.to(gpu))
+    xr = x.float().requires_grad_(True)
+    yr = torch.flatten(F.adaptive_avg_pool2d(xr, 1), 1)
+    yr.backward(g.float())
+    torch.testing.assert_close(y.float().cpu(), yr.detach(), rtol=1e-2, atol=1e-2)
+    assert xd.grad.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(xd.grad.float().cpu(), xr.grad, rtol=1e-2, atol=1e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("route", ["gemm", "miopen"])
+def test_conv1x1_routes_match_fp32(gpu, route):
+    """Both routes of the 1x1 conv (hipBLASLt GEMM / MIOpen) against an fp32 conv, fwd + both grads."""
+    from parameter_server_distributed_amd.ops import conv as cv
+
+    torch.manual_seed(0)
+    m = cv.Conv1x1(64, 96).to(gpu).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    x = torch.randn(3, 64, 10, 12).to(torch.bfloat16).to(gpu).contiguous(memory_format=torch.channels_last)
+    xd = x.clone().requires_grad_(True)
+    M = 3 * 10 * 12
+    for kind in ("fwd", "dgrad"):
+        cv._DECISIONS[(kind, M, 64, 96)] = route
+    try:
+        y = m(xd)
+        g = torch.randn(y.shape).to(torch.bfloat16).to(gpu).contiguous(memory_format=torch.channels_last)
+        y.backward(g)
+    finally:
+        for kind in ("fwd", "dgrad"):
+            cv._DECISIONS.pop((kind, M, 64, 96), None)
+    xr = x.float().cpu().requires_grad_(True)
+    wr = m.weight.detach().float().cpu().requires_grad_(True)
+    yr = F.conv2d(xr, wr)
+    yr.backward(g.float().cpu())
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(y.float().cpu(), yr.detach(), rtol=2e-2, atol=5e-2)
+    torch.testing.assert_close(xd.grad.float().cpu(), xr.grad, rtol=2e-2, atol=5e-2)
+    torch.testing.assert_close(m.weight.grad.float().cpu(), wr.grad, rtol=2e-2, atol=2e-1)
+
+
+@pytest.mark.gpu
+def test_conv1x1_autotune_records_a_choice(gpu):
+    from parameter_server_distributed_amd.ops import conv as cv
+
+    m = cv.Conv1x1(32, 64).to(gpu).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    x = torch.randn(2, 32, 8, 8, device=gpu, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    m(x.requires_grad_(True)).sum().backward()
+    d = cv.decisions()
+    assert d[("fwd", 128, 32, 64)] in ("gemm", "miopen") and d[("dgrad", 128, 32, 64)] in ("gemm", "miopen")
