@@ -163,6 +163,108 @@ std::vector<at::Tensor> bn_bwd(const at::Tensor& dy_in, const at::Tensor& x_in, 
   return {dx, dr, dgamma, dbeta};
 }
 
+
+// Stem BN + ReLU + 3x3/s2 max-pool (training forward): returns {y_pool, argmax, mean, invstd, ss}.
+std::vector<at::Tensor> bn_pool_fwd(const at::Tensor& x_in, const at::Tensor& gamma, const at::Tensor& beta,
+                                    const at::Tensor& running_mean, const at::Tensor& running_var, double momentum,
+                                    double eps, c10::optional<at::Tensor> counter) {
+  TORCH_CHECK(x_in.is_cuda() && x_in.scalar_type() == at::kBFloat16 && x_in.dim() == 4, "psd bn_pool: bf16 NCHW-shaped x");
+  const c10::DeviceGuard g(x_in.device());
+  at::Tensor x = nhwc(x_in);
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(bn_pool_supported((int)H, (int)W, (int)C), "psd bn_pool: unsupported shape ", x.sizes());
+  const int64_t M = N * H * W;
+  check_vec(gamma, C, at::kBFloat16, "gamma");
+  check_vec(beta, C, at::kBFloat16, "beta");
+  check_vec(running_mean, C, at::kFloat, "running_mean");
+  check_vec(running_var, C, at::kFloat, "running_var");
+  auto f32 = x.options().dtype(at::kFloat);
+  const auto cl = x.options().memory_format(at::MemoryFormat::ChannelsLast);
+  at::Tensor y = at::empty({N, C, H / 2, W / 2}, cl);
+  at::Tensor arg = at::empty({N, C, H / 2, W / 2}, cl.dtype(at::kByte));
+  at::Tensor mean = at::empty({C}, f32), invstd = at::empty({C}, f32), ss = at::empty({2 * C}, f32);
+  at::Tensor part = at::empty({(int64_t)bn_reduce_blocks(M, (int)C) * 2 * C}, f32);
+  BnFwdArgs a{};
+  a.x = reinterpret_cast<const uint16_t*>(x.data_ptr());
+  a.y = reinterpret_cast<uint16_t*>(y.data_ptr());
+  a.gamma = reinterpret_cast<const uint16_t*>(gamma.data_ptr());
+  a.beta = reinterpret_cast<const uint16_t*>(beta.data_ptr());
+  a.running_mean = running_mean.data_ptr<float>();
+  a.running_var = running_var.data_ptr<float>();
+  a.save_mean = mean.data_ptr<float>();
+  a.save_invstd = invstd.data_ptr<float>();
+  a.ss = ss.data_ptr<float>();
+  a.part = part.data_ptr<float>();
+  a.counter = opt_ptr<int64_t>(counter);
+  a.pool_arg = arg.data_ptr<uint8_t>();
+  a.N = (int32_t)N;
+  a.H = (int32_t)H;
+  a.W = (int32_t)W;
+  a.M = M;
+  a.C = (int32_t)C;
+  a.relu = 1;
+  a.training = 1;
+  a.momentum = (float)momentum;
+  a.eps = (float)eps;
+  hipError_t e = launch_bn_fwd(a, stream_of(x));
+  TORCH_CHECK(e == hipSuccess, "psd bn_pool fwd: ", hipGetErrorString(e));
+  return {y, arg, mean, invstd, ss};
+}
+
+// Backward of bn_pool_fwd: gpool (+ gpool2, a second consumer's gradient of the pooled output)
+// -> {dx, dgamma, dbeta}; the pool gradient is recomputed inside the BN passes.
+std::vector<at::Tensor> bn_pool_bwd(const at::Tensor& gpool_in, c10::optional<at::Tensor> gpool2_in, const at::Tensor& arg,
+                                    const at::Tensor& x_in, const at::Tensor& gamma, const at::Tensor& save_mean,
+                                    const at::Tensor& save_invstd, const at::Tensor& ss,
+                                    c10::optional<at::Tensor> dgamma_out, c10::optional<at::Tensor> dbeta_out) {
+  const c10::DeviceGuard g(x_in.device());
+  at::Tensor x = nhwc(x_in), gp = nhwc(gpool_in);
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(bn_pool_supported((int)H, (int)W, (int)C), "psd bn_pool bwd: unsupported shape ", x.sizes());
+  const std::vector<int64_t> ps{N, C, H / 2, W / 2};
+  TORCH_CHECK(gp.sizes() == ps && gp.scalar_type() == at::kBFloat16, "psd bn_pool bwd: gpool shape/dtype");
+  TORCH_CHECK(arg.sizes() == ps && arg.scalar_type() == at::kByte && arg.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "psd bn_pool bwd: argmax shape");
+  TORCH_CHECK(ss.numel() == 2 * C && ss.scalar_type() == at::kFloat && ss.is_contiguous(), "psd bn_pool bwd: ss");
+  at::Tensor gp2;
+  if (gpool2_in.has_value() && gpool2_in->defined()) {
+    gp2 = nhwc(*gpool2_in);
+    TORCH_CHECK(gp2.sizes() == ps && gp2.scalar_type() == at::kBFloat16, "psd bn_pool bwd: gpool2 shape/dtype");
+  }
+  const int64_t M = N * H * W;
+  auto f32 = x.options().dtype(at::kFloat);
+  at::Tensor dx = at::empty_like(x);
+  at::Tensor dgamma = (dgamma_out.has_value() && dgamma_out->defined()) ? *dgamma_out : at::empty({C}, x.options());
+  at::Tensor dbeta = (dbeta_out.has_value() && dbeta_out->defined()) ? *dbeta_out : at::empty({C}, x.options());
+  TORCH_CHECK(dgamma.numel() == C && dgamma.scalar_type() == at::kBFloat16 && dgamma.is_contiguous(), "psd bn_pool: dgamma");
+  TORCH_CHECK(dbeta.numel() == C && dbeta.scalar_type() == at::kBFloat16 && dbeta.is_contiguous(), "psd bn_pool: dbeta");
+  at::Tensor coef = at::empty({3 * C}, f32);
+  at::Tensor part = at::empty({(int64_t)bn_pool_reduce_blocks((int)N, (int)H, (int)W, (int)C) * 2 * C}, f32);
+  BnBwdArgs a{};
+  a.gpool = reinterpret_cast<const uint16_t*>(gp.data_ptr());
+  a.gpool2 = gp2.defined() ? reinterpret_cast<const uint16_t*>(gp2.data_ptr()) : nullptr;
+  a.pool_arg = arg.data_ptr<uint8_t>();
+  a.ss = ss.data_ptr<float>();
+  a.x = reinterpret_cast<const uint16_t*>(x.data_ptr());
+  a.gamma = reinterpret_cast<const uint16_t*>(gamma.data_ptr());
+  a.save_mean = save_mean.data_ptr<float>();
+  a.save_invstd = save_invstd.data_ptr<float>();
+  a.dx = reinterpret_cast<uint16_t*>(dx.data_ptr());
+  a.dgamma = reinterpret_cast<uint16_t*>(dgamma.data_ptr());
+  a.dbeta = reinterpret_cast<uint16_t*>(dbeta.data_ptr());
+  a.coef = coef.data_ptr<float>();
+  a.part = part.data_ptr<float>();
+  a.N = (int32_t)N;
+  a.H = (int32_t)H;
+  a.W = (int32_t)W;
+  a.M = M;
+  a.C = (int32_t)C;
+  a.relu = 1;
+  hipError_t e = launch_bn_bwd(a, stream_of(x));
+  TORCH_CHECK(e == hipSuccess, "psd bn_pool bwd: ", hipGetErrorString(e));
+  return {dx, dgamma, dbeta};
+}
+
 }  // namespace psd
 
 // ---- NHWC 3x3/s2/p1 max-pool (kernels/pool.hip)

@@ -19,6 +19,7 @@
 // launch: correct for any workgroup->XCD placement, cdna_hip_programming.md G16).
 #include "common.h"
 #include "launchers_bn.h"
+#include "pool_gather.h"
 
 #include <cstdlib>
 
@@ -393,6 +394,173 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(const uint16_t* __res
   }
 }
 
+// ------------------------------------------------------------------ stem: BN + ReLU + 3x3/s2 max-pool
+// The stem BN's output feeds only the max-pool, so it is never materialised: the forward applies
+// scale/shift + ReLU inside the pool window (rounded to bf16 first: bitwise the unfused result),
+// and the backward recomputes the pool gradient from the pooled gradients + 1-byte argmax inside
+// both BN backward passes. Per b1024 step this drops the 1.64 GB y write + read and the 1.64 GB
+// pool-gradient write + two reads.
+//
+// Backward work item = one 2x2 input block (2k..2k+1, 2j..2j+1) x 8 channels: its gradient comes
+// from the 4 pooled outputs (k..k+1, j..j+1) only (even rows / cols sit in one window, odd ones in
+// two), so each pooled gradient is loaded once per block instead of once per covered input.
+__global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(const uint16_t* __restrict__ x, const float* __restrict__ ss,
+                                                              uint16_t* __restrict__ y, uint8_t* __restrict__ arg, int N,
+                                                              int H, int W, int C, int Ho, int Wo) {
+  const int c8n = C >> 3;
+  const int64_t total = (int64_t)N * Ho * Wo * c8n;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int c8 = (int)(t % c8n);
+    int64_t r = t / c8n;
+    const int wo = (int)(r % Wo);
+    r /= Wo;
+    const int ho = (int)(r % Ho);
+    const int n = (int)(r / Ho);
+    float sc[8], sh[8];
+    load8_f32(ss + c8 * 8, sc);
+    load8_f32(ss + C + c8 * 8, sh);
+    float best[8];
+    uint8_t bi[8];
+    maxpool3s2_max8(
+        x, n, ho, wo, c8, H, W, C,
+        [&](float v, int e) { return bf16_to_f32(f32_to_bf16(fmaxf(fmaf(v, sc[e], sh[e]), 0.f))); }, best, bi);
+    store8_bf16(y + t * 8, best);
+    store_argmax8(arg + t * 8, bi);
+  }
+}
+
+// Pool gradient of the 2x2 input block (2k.., 2j..) for 8 channels: g[q][8], q = 2*(row parity) + col parity.
+__device__ __forceinline__ void pool_grad_block(const uint16_t* __restrict__ gp, const uint16_t* __restrict__ gp2,
+                                                const uint8_t* __restrict__ arg, int n, int k, int j, int c8, int C,
+                                                int Ho, int Wo, float g[4][8]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[q][e] = 0.f;
+  // output (k + a, j + b) -> input (2k + pr, 2j + pc) through window offset (dh, dw) = (pr + 1 - 2a, pc + 1 - 2b)
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int ho = k + a, wo = j + b;
+      if (ho >= Ho || wo >= Wo) continue;
+      const int64_t o = (((int64_t)n * Ho + ho) * Wo + wo) * C + c8 * 8;
+      const uint2 ai = *reinterpret_cast<const uint2*>(arg + o);
+      float v[8];
+      load8_bf16(gp + o, v);
+      if (gp2) {
+        float v2[8];
+        load8_bf16(gp2 + o, v2);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += v2[e];
+      }
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        const int dh = pr + 1 - 2 * a;
+        if (dh < 0) continue;
+#pragma unroll
+        for (int pc = 0; pc < 2; ++pc) {
+          const int dw = pc + 1 - 2 * b;
+          if (dw < 0) continue;
+          const uint8_t want = (uint8_t)(dh * 3 + dw);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const uint8_t ae = (uint8_t)(((e < 4 ? ai.x : ai.y) >> (8 * (e & 3))) & 0xff);
+            if (ae == want) g[2 * pr + pc][e] += v[e];
+          }
+        }
+      }
+    }
+  }
+}
+
+// Blocks of the pool-fused backward: lane = (block item r0, channel group cg), rpi = 256 / (C/8)
+// items per block iteration; items are (n, k, j) 2x2 input blocks.
+__global__ __launch_bounds__(256) void bn_bwd_reduce_pool_kernel(const uint16_t* __restrict__ gp,
+                                                                 const uint16_t* __restrict__ gp2,
+                                                                 const uint8_t* __restrict__ arg,
+                                                                 const float* __restrict__ ssf,
+                                                                 const uint16_t* __restrict__ x,
+                                                                 const float* __restrict__ mean, int N, int H, int W,
+                                                                 int C, float* __restrict__ part) {
+  const Map m = make_map(C);
+  const int Ho = H / 2, Wo = W / 2;
+  float a[8], b[8], mu[8], sc[8], sh[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) a[e] = b[e] = 0.f;
+  if (m.active) {
+    load8_f32(mean + m.cg * 8, mu);
+    load8_f32(ssf + m.cg * 8, sc);
+    load8_f32(ssf + C + m.cg * 8, sh);
+    const int64_t items = (int64_t)N * Ho * Wo;
+    const int64_t stride = (int64_t)gridDim.x * m.rpi;
+    for (int64_t it = (int64_t)blockIdx.x * m.rpi + m.r0; it < items; it += stride) {
+      const int j = (int)(it % Wo);
+      const int64_t q = it / Wo;
+      const int k = (int)(q % Ho);
+      const int n = (int)(q / Ho);
+      float g[4][8];
+      pool_grad_block(gp, gp2, arg, n, k, j, m.cg, C, Ho, Wo, g);
+#pragma unroll
+      for (int pq = 0; pq < 4; ++pq) {
+        const int h = 2 * k + (pq >> 1), w = 2 * j + (pq & 1);
+        float xv[8];
+        load8_bf16(x + (((int64_t)n * H + h) * W + w) * C + m.cg * 8, xv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float gm = fmaf(xv[e], sc[e], sh[e]) > 0.f ? g[pq][e] : 0.f;
+          a[e] += gm;
+          b[e] = fmaf(gm, xv[e] - mu[e], b[e]);
+        }
+      }
+    }
+  }
+  block_partials(m, C, a, b, part);
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_elemt_pool_kernel(const uint16_t* __restrict__ gp,
+                                                                const uint16_t* __restrict__ gp2,
+                                                                const uint8_t* __restrict__ arg,
+                                                                const float* __restrict__ ssf,
+                                                                const uint16_t* __restrict__ x,
+                                                                const float* __restrict__ coef,
+                                                                uint16_t* __restrict__ dx, int N, int H, int W, int C) {
+  const int c8n = C >> 3;
+  const int Ho = H / 2, Wo = W / 2;
+  const int64_t total = (int64_t)N * Ho * Wo * c8n;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;  // host: stride % c8n == 0
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c8 = (int)(t % c8n);
+  float A[8], B[8], Cc[8], sc[8], sh[8];
+  load8_f32(coef + c8 * 8, A);
+  load8_f32(coef + C + c8 * 8, B);
+  load8_f32(coef + 2 * C + c8 * 8, Cc);
+  load8_f32(ssf + c8 * 8, sc);
+  load8_f32(ssf + C + c8 * 8, sh);
+  for (; t < total; t += stride) {
+    const int64_t it = t / c8n;
+    const int j = (int)(it % Wo);
+    const int64_t q = it / Wo;
+    const int k = (int)(q % Ho);
+    const int n = (int)(q / Ho);
+    float g[4][8];
+    pool_grad_block(gp, gp2, arg, n, k, j, c8, C, Ho, Wo, g);
+#pragma unroll
+    for (int pq = 0; pq < 4; ++pq) {
+      const int h = 2 * k + (pq >> 1), w = 2 * j + (pq & 1);
+      const int64_t off = (((int64_t)n * H + h) * W + w) * C + c8 * 8;
+      float xv[8];
+      load8_bf16(x + off, xv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float gm = fmaf(xv[e], sc[e], sh[e]) > 0.f ? g[pq][e] : 0.f;
+        g[pq][e] = fmaf(A[e], gm, fmaf(B[e], xv[e], Cc[e]));
+      }
+      store8_bf16(dx + off, g[pq]);
+    }
+  }
+}
+
 // ------------------------------------------------------------------ host launchers
 // PSD_BN_REVERSE=1 walks the reduce passes back to front (A/B switch; measured neutral on a
 // b1024 ResNet-50 step, so off by default).
@@ -450,6 +618,15 @@ hipError_t launch_bn_fwd(const BnFwdArgs& a, hipStream_t st) {
                        a.running_mean, a.gamma, a.beta, a.running_mean, a.running_var, a.momentum, a.eps, a.save_mean,
                        a.save_invstd, a.ss, a.counter);
   }
+  if (a.pool_arg) {  // stem: y is the pooled output, the BN output is never written
+    if (!a.relu || a.res || a.mbits || !bn_pool_supported(a.H, a.W, a.C) || (int64_t)a.N * a.H * a.W != a.M)
+      return hipErrorInvalidValue;
+    const int Ho = a.H / 2, Wo = a.W / 2;
+    const int64_t total = (int64_t)a.N * Ho * Wo * (a.C / 8);
+    hipLaunchKernelGGL(bn_relu_maxpool_kernel, dim3(stream_grid(total, 256)), dim3(256), 0, st, a.x, a.ss, a.y,
+                       a.pool_arg, a.N, a.H, a.W, a.C, Ho, Wo);
+    return hipGetLastError();
+  }
   const int64_t nvec = a.M * (a.C / 8);
   const int g = elem_grid(nvec, a.C);
 #define PSD_APPLY(R, S, B) \
@@ -465,9 +642,39 @@ hipError_t launch_bn_fwd(const BnFwdArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+bool bn_pool_supported(int H, int W, int C) {
+  // 2x2 blocks of an even input; a block's lanes (C/8 channel groups) tile 256 lanes exactly
+  return H > 0 && W > 0 && H % 2 == 0 && W % 2 == 0 && C % 8 == 0 && C / 8 <= 256 && 256 % (C / 8) == 0;
+}
+
+// More blocks than the plain reduce (<= 2048, not 512): a work item gathers 4 pooled gradients and
+// 4 inputs, and at 512 blocks the pass ran at half the streaming bandwidth (latency-bound).
+int bn_pool_reduce_blocks(int N, int H, int W, int C) {
+  const int64_t items = (int64_t)N * (H / 2) * (W / 2);
+  const int rpi = 256 / (C / 8);
+  int64_t g = (items + (int64_t)rpi * 4 - 1) / ((int64_t)rpi * 4);
+  return (int)(g < 1 ? 1 : (g > 2048 ? 2048 : g));
+}
+
+static hipError_t launch_bn_bwd_pool(const BnBwdArgs& a, hipStream_t st) {
+  if (!a.relu || !a.ss || a.dr || a.dy2 || !bn_pool_supported(a.H, a.W, a.C) || (int64_t)a.N * a.H * a.W != a.M)
+    return hipErrorInvalidValue;
+  const int gx = bn_pool_reduce_blocks(a.N, a.H, a.W, a.C), gy = 1;  // the caller sized part for this
+  hipLaunchKernelGGL(bn_bwd_reduce_pool_kernel, dim3(gx, gy), dim3(256), 0, st, a.gpool, a.gpool2, a.pool_arg, a.ss, a.x,
+                     a.save_mean, a.N, a.H, a.W, a.C, a.part);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((a.C + kFinCh - 1) / kFinCh), dim3(256), 0, st, a.part, gx, a.M, a.C,
+                     a.gamma, a.save_mean, a.save_invstd, a.dgamma, a.dbeta, a.coef);
+  const int64_t total = (int64_t)a.N * (a.H / 2) * (a.W / 2) * (a.C / 8);
+  const int g = elem_grid(total, a.C);
+  hipLaunchKernelGGL(bn_bwd_elemt_pool_kernel, dim3(g), dim3(256), 0, st, a.gpool, a.gpool2, a.pool_arg, a.ss, a.x,
+                     a.coef, a.dx, a.N, a.H, a.W, a.C);
+  return hipGetLastError();
+}
+
 hipError_t launch_bn_bwd(const BnBwdArgs& a, hipStream_t st) {
   if (a.M <= 0) return hipSuccess;
   if (a.C % 8 != 0) return hipErrorInvalidValue;
+  if (a.gpool) return launch_bn_bwd_pool(a, st);
   int gx, gy;
   reduce_grid(a.M, a.C, gx, gy);
   // ReLU mask: forward bit-mask, else y, else recomputed from x and the forward scale/shift

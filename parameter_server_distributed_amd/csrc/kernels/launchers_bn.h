@@ -19,6 +19,8 @@ struct BnFwdArgs {
   float* ss;              // [2C] scale, shift (inference: provided; training: produced)
   float* part;            // [bn_reduce_blocks * 2C] workspace
   int64_t* counter;       // num_batches_tracked (optional)
+  uint8_t* pool_arg;      // stem fusion: y = maxpool3x3s2(relu(bn(x))) [N, H/2, W/2, C] + argmax (optional)
+  int32_t N, H, W;        // x as [N, H, W, C] (pool fusion only)
   int64_t M;
   int32_t C;
   int32_t relu;
@@ -43,11 +45,20 @@ struct BnBwdArgs {
   uint16_t* dbeta;        // optional, bf16 [C]
   float* coef;            // [3C] workspace
   float* part;            // [bn_reduce_blocks * 2C] workspace
+  // stem fusion: dy = maxpool3x3s2 backward of gpool (+ gpool2) through pool_arg, computed on the
+  // fly (never materialised); x is [N, H, W, C], H and W even; ReLU mask from x and ss
+  const uint16_t* gpool;
+  const uint16_t* gpool2;
+  const uint8_t* pool_arg;
+  int32_t N, H, W;
   int64_t M;
   int32_t C;
   int32_t relu;
 };
 
+// true when the fused stem BN+ReLU+max-pool kernels support this shape
+bool bn_pool_supported(int H, int W, int C);
+int bn_pool_reduce_blocks(int N, int H, int W, int C);  // partial rows of the pool-fused backward
 int bn_reduce_blocks(int64_t M, int C);
 hipError_t launch_bn_fwd(const BnFwdArgs& a, hipStream_t stream);
 hipError_t launch_bn_bwd(const BnBwdArgs& a, hipStream_t stream);

@@ -4,6 +4,7 @@
 // (260 us fwd + 610 us bwd per ResNet-50 b256 step in profiles/resnet50_r1_fusedbn_kernels.md).
 #include "common.h"
 #include "launchers_pool.h"
+#include "pool_gather.h"
 
 namespace psd {
 
@@ -21,34 +22,9 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint16_t* __rest
     const int n = (int)(r / Ho);
     float best[8];
     uint8_t bi[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      best[e] = -INFINITY;
-      bi[e] = 0;
-    }
-#pragma unroll
-    for (int dh = 0; dh < 3; ++dh) {
-      const int h = 2 * ho - 1 + dh;
-      if (h < 0 || h >= H) continue;
-#pragma unroll
-      for (int dw = 0; dw < 3; ++dw) {
-        const int w = 2 * wo - 1 + dw;
-        if (w < 0 || w >= W) continue;
-        float v[8];
-        load8_bf16(x + (((int64_t)n * H + h) * W + w) * C + c8 * 8, v);
-#pragma unroll
-        for (int e = 0; e < 8; ++e)
-          if (v[e] > best[e] || (v[e] != v[e])) {  // NaN propagates like torch
-            best[e] = v[e];
-            bi[e] = (uint8_t)(dh * 3 + dw);
-          }
-      }
-    }
-    const int64_t o = t * 8;
-    store8_bf16(y + o, best);
-    uint32_t lo = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
-    uint32_t hi = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
-    *reinterpret_cast<uint2*>(arg + o) = make_uint2(lo, hi);
+    maxpool3s2_max8(x, n, ho, wo, c8, H, W, C, [](float v, int) { return v; }, best, bi);
+    store8_bf16(y + t * 8, best);
+    store_argmax8(arg + t * 8, bi);
   }
 }
 
@@ -67,36 +43,8 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const uint16_t* __rest
     r /= W;
     const int h = (int)(r % H);
     const int n = (int)(r / H);
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const int ho0 = h / 2, wo0 = w / 2;  // candidate outputs: ho in {ho0, ho0+1} with window rows 2ho-1..2ho+1
-#pragma unroll
-    for (int a = 0; a < 2; ++a) {
-      const int ho = ho0 + a;
-      const int dh = h - (2 * ho - 1);
-      if (ho >= Ho || dh < 0 || dh > 2) continue;
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const int wo = wo0 + b;
-        const int dw = w - (2 * wo - 1);
-        if (wo >= Wo || dw < 0 || dw > 2) continue;
-        const int64_t o = (((int64_t)n * Ho + ho) * Wo + wo) * C + c8 * 8;
-        const uint2 ai = *reinterpret_cast<const uint2*>(arg + o);
-        float g[8];
-        load8_bf16(dy + o, g);
-        if (dy2) {
-          float g2[8];
-          load8_bf16(dy2 + o, g2);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) g[e] += g2[e];
-        }
-        const uint8_t want = (uint8_t)(dh * 3 + dw);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const uint8_t ae = (uint8_t)(((e < 4 ? ai.x : ai.y) >> (8 * (e & 3))) & 0xff);
-          if (ae == want) acc[e] += g[e];
-        }
-      }
-    }
+    float acc[8];
+    maxpool3s2_grad8(dy, dy2, arg, n, h, w, c8, C, Ho, Wo, acc);
     store8_bf16(dx + t * 8, acc);
   }
 }

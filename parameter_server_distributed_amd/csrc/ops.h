@@ -38,6 +38,13 @@ std::vector<at::Tensor> maxpool3s2_fwd(const at::Tensor& x);
 at::Tensor maxpool3s2_bwd(const at::Tensor& dy, const at::Tensor& arg, int64_t H, int64_t W,
                           const c10::optional<at::Tensor>& dy2);
 at::Tensor gap_fwd(const at::Tensor& x);
+std::vector<at::Tensor> bn_pool_fwd(const at::Tensor& x, const at::Tensor& gamma, const at::Tensor& beta,
+                                    const at::Tensor& running_mean, const at::Tensor& running_var, double momentum,
+                                    double eps, c10::optional<at::Tensor> counter);
+std::vector<at::Tensor> bn_pool_bwd(const at::Tensor& gpool, c10::optional<at::Tensor> gpool2, const at::Tensor& arg,
+                                    const at::Tensor& x, const at::Tensor& gamma, const at::Tensor& save_mean,
+                                    const at::Tensor& save_invstd, const at::Tensor& ss,
+                                    c10::optional<at::Tensor> dgamma_out, c10::optional<at::Tensor> dbeta_out);
 at::Tensor gap_bwd(const at::Tensor& dy, int64_t H, int64_t W);
 
 }  // namespace psd

@@ -67,6 +67,43 @@ class _FusedBNFn(torch.autograd.Function):
         return dx, (dg if w is not None else None), (db if w is not None else None), res_grad, None, None
 
 
+class _BNReluPoolFn(torch.autograd.Function):
+    """Stem: maxpool3x3s2(relu(bn(x))) without materialising the BN output (kernels/bn.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, mod, pool):
+        y, arg, mean, invstd, ss = native().bn_pool_fwd(x, weight, bias, mod.running_mean, mod.running_var,
+                                                        mod.momentum if mod.momentum is not None else 0.1, mod.eps,
+                                                        mod.num_batches_tracked)
+        ctx.mod, ctx.pool = mod, pool
+        ctx.save_for_backward(x, arg, weight, mean, invstd, ss)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, arg, w, mean, invstd, ss = ctx.saved_tensors
+        sink = getattr(ctx.mod, "_psd_grad_sink", None)
+        dgo = dbo = None
+        if sink is not None:
+            dgo, dbo = sink(ctx.mod.weight), sink(ctx.mod.bias)
+        pend = getattr(ctx.pool, "_psd_pending_dr", None)
+        gy2 = pend.pop() if pend else None  # the first bottleneck's downsample-branch gradient
+        dx, dg, db = native().bn_pool_bwd(gy, gy2, arg, x, w, mean, invstd, ss, dgo, dbo)
+        return dx, dg, db, None, None
+
+
+def bn_relu_maxpool(bn: "FusedBatchNorm2d", pool, x: torch.Tensor) -> torch.Tensor:
+    """``pool(bn(x))`` for the ResNet stem (``bn`` with ReLU, ``pool`` a 3x3/s2/p1 max-pool module
+    that can take a second output gradient through ``_psd_pending_dr``). Training on gfx950 runs
+    the fused kernels; everything else composes the two modules."""
+    if (bn.training and bn.relu and _kernel_ok(x) and x.dim() == 4 and bn.running_mean is not None
+            and bn.weight is not None and bn.weight.dtype == torch.bfloat16
+            and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0 and 256 % (x.shape[1] // 8) == 0):
+        pool.native_last = True
+        return _BNReluPoolFn.apply(x, bn.weight, bn.bias, bn, pool)
+    return pool(bn(x))
+
+
 class FusedBatchNorm2d(nn.BatchNorm2d):
     """``nn.BatchNorm2d`` + optional residual + optional ReLU, one fused kernel family on MI355X."""
 

@@ -204,3 +204,55 @@ def test_conv1x1_autotune_records_a_choice(gpu):
     m(x.requires_grad_(True)).sum().backward()
     d = cv.decisions()
     assert d[("fwd", 128, 32, 64)] in ("gemm", "miopen") and d[("dgrad", 128, 32, 64)] in ("gemm", "miopen")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,second", [((4, 64, 16, 12), False), ((2, 64, 112, 112), True), ((3, 16, 6, 10), True),
+                                          ((1, 256, 8, 40), True)],
+                         ids=str)
+def test_stem_bn_relu_maxpool_fused_matches_composite(gpu, shape, second):
+    """Fused stem (BN + ReLU + max-pool, pool gradient recomputed inside the BN backward) against
+    the unfused gfx950 kernels (BN kernel, then pool kernel: same bf16 ties in the pool windows)
+    for the output, running stats and every gradient, and the forward against fp32."""
+    from parameter_server_distributed_amd.ops.bn import FusedBatchNorm2d, bn_relu_maxpool
+    from parameter_server_distributed_amd.ops.pool import MaxPool3x3s2
+
+    torch.manual_seed(0)
+    C = shape[1]
+    x = (torch.randn(shape) * 2 + 0.3).to(torch.bfloat16)
+    g = torch.randn((shape[0], C, shape[2] // 2, shape[3] // 2)).to(torch.bfloat16)
+    g2 = torch.randn(g.shape).to(torch.bfloat16) if second else None
+    cl = dict(memory_format=torch.channels_last)
+    res = []
+    for fused in (True, False):
+        torch.manual_seed(1)
+        bn = FusedBatchNorm2d(C, relu=True).to(gpu)
+        with torch.no_grad():
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.uniform_(-0.5, 0.5)
+        bn.weight.data = bn.weight.data.to(torch.bfloat16)
+        bn.bias.data = bn.bias.data.to(torch.bfloat16)
+        pool = MaxPool3x3s2()
+        xd = x.to(gpu).contiguous(**cl).requires_grad_(True)
+        if fused:
+            y = bn_relu_maxpool(bn, pool, xd)
+            if second:
+                pool._psd_pending_dr.append(g2.to(gpu).contiguous(**cl))
+            y.backward(g.to(gpu).contiguous(**cl))
+            assert not pool._psd_pending_dr
+        else:
+            y = pool(bn(xd))
+            y.backward((g + g2 if second else g).to(gpu).contiguous(**cl))
+        res.append((y.float().cpu(), xd.grad.float().cpu(), bn.weight.grad.float().cpu(), bn.bias.grad.float().cpu(),
+                    bn.running_mean.cpu(), bn.running_var.cpu(), bn.weight.detach().float().cpu(),
+                    bn.bias.detach().float().cpu()))
+    (y, dx, dw, db, rm, rv, w, b), (y0, dx0, dw0, db0, rm0, rv0, _, _) = res
+    torch.testing.assert_close(y, y0, rtol=0, atol=0)
+    torch.testing.assert_close(rm, rm0, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(rv, rv0, rtol=1e-6, atol=1e-6)
+    # unfused rounds the pool gradient (and g + g2) to bf16 before the BN backward; fused keeps fp32
+    torch.testing.assert_close(dx, dx0, rtol=2e-2, atol=2e-2 * dx0.abs().max().item())
+    torch.testing.assert_close(dw, dw0, rtol=2e-2, atol=2e-2 * dw0.abs().max().item())
+    torch.testing.assert_close(db, db0, rtol=2e-2, atol=2e-2 * db0.abs().max().item())
+    yr = F.max_pool2d(F.relu(F.batch_norm(x.float(), None, None, w, b, True, 0.1, 1e-5)), 3, 2, 1)
+    torch.testing.assert_close(y, yr, rtol=2e-2, atol=3e-2)

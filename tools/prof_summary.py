@@ -72,6 +72,7 @@ CATEGORIES = [
     ("MIOpen/CK conv bwd-data", r"bwd_data|igemm_bwd|bwd_gtc"),
     ("MIOpen/CK conv bwd-weight", r"wrw|bwd_weight"),
     ("CK batched GEMM (1x1 conv)", r"batched_gemm|gemm_xdl"),
+    ("hipBLASLt GEMM (1x1 conv fwd/dgrad, fc)", r"^Cijk_"),
     ("MIOpen tensor ops / fills", r"SubTensorOp|fillBuffer|Transpose|transpose"),
     ("torch elementwise / reduce", r"at::native"),
     ("RCCL", r"nccl|rccl"),
