@@ -6,6 +6,7 @@
 #include <vector>
 
 #include "kernels/launchers_bn.h"
+#include "kernels/launchers_stem.h"
 
 namespace psd {
 
@@ -209,6 +210,69 @@ std::vector<at::Tensor> bn_pool_fwd(const at::Tensor& x_in, const at::Tensor& ga
   hipError_t e = launch_bn_fwd(a, stream_of(x));
   TORCH_CHECK(e == hipSuccess, "psd bn_pool fwd: ", hipGetErrorString(e));
   return {y, arg, mean, invstd, ss};
+}
+
+// ResNet stem forward: conv 7x7/s2/p3 (3 -> 64, kernels/stem.hip, BN statistics reduced in its
+// epilogue) -> BN finalize -> fused BN + ReLU + max-pool. Returns {y_pool, argmax, mean, invstd, ss,
+// conv_out}; conv_out (the BN input) is kept for the backward.
+std::vector<at::Tensor> stem_fwd(const at::Tensor& x_in, const at::Tensor& w, const at::Tensor& gamma,
+                                 const at::Tensor& beta, const at::Tensor& running_mean, const at::Tensor& running_var,
+                                 double momentum, double eps, c10::optional<at::Tensor> counter) {
+  TORCH_CHECK(x_in.is_cuda() && x_in.scalar_type() == at::kBFloat16 && x_in.dim() == 4 && x_in.size(1) == 3,
+              "psd stem: bf16 [N, 3, H, W] input");
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.sizes() == at::IntArrayRef({64, 3, 7, 7}), "psd stem: weight [64,3,7,7]");
+  const c10::DeviceGuard g(x_in.device());
+  at::Tensor x = x_in.contiguous(at::MemoryFormat::ChannelsLast);
+  const int64_t N = x.size(0), H = x.size(2), W = x.size(3), Ho = H / 2, Wo = W / 2;
+  TORCH_CHECK(stem_conv_supported((int)H, (int)W, (int)Ho, (int)Wo) && bn_pool_supported((int)Ho, (int)Wo, 64),
+              "psd stem: unsupported input ", x.sizes());
+  check_vec(gamma, 64, at::kBFloat16, "gamma");
+  check_vec(beta, 64, at::kBFloat16, "beta");
+  check_vec(running_mean, 64, at::kFloat, "running_mean");
+  check_vec(running_var, 64, at::kFloat, "running_var");
+  // [co][ci][kh][kw] -> [co][kh*24 + kw*3 + ci], zero for kw*3+ci >= 21 and the 8th kh block
+  at::Tensor wk = at::constant_pad_nd(w.permute({0, 2, 3, 1}).reshape({64, 7, 21}), {0, 3, 0, 1}).reshape({64, 192})
+                      .contiguous();
+  const auto cl = x.options().memory_format(at::MemoryFormat::ChannelsLast);
+  auto f32 = x.options().dtype(at::kFloat);
+  at::Tensor conv = at::empty({N, 64, Ho, Wo}, cl);
+  const int nblk = stem_conv_blocks((int)N, (int)Ho);
+  at::Tensor part = at::empty({(int64_t)nblk * 128}, f32);
+  hipStream_t st = stream_of(x);
+  hipError_t e = launch_stem_conv(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                  reinterpret_cast<const uint16_t*>(wk.data_ptr()),
+                                  reinterpret_cast<uint16_t*>(conv.data_ptr()), running_mean.data_ptr<float>(),
+                                  part.data_ptr<float>(), (int)N, (int)H, (int)W, (int)Ho, (int)Wo, st);
+  TORCH_CHECK(e == hipSuccess, "psd stem conv: ", hipGetErrorString(e));
+  at::Tensor y = at::empty({N, 64, Ho / 2, Wo / 2}, cl);
+  at::Tensor arg = at::empty({N, 64, Ho / 2, Wo / 2}, cl.dtype(at::kByte));
+  at::Tensor mean = at::empty({64}, f32), invstd = at::empty({64}, f32), ss = at::empty({128}, f32);
+  BnFwdArgs a{};
+  a.x = reinterpret_cast<const uint16_t*>(conv.data_ptr());
+  a.y = reinterpret_cast<uint16_t*>(y.data_ptr());
+  a.gamma = reinterpret_cast<const uint16_t*>(gamma.data_ptr());
+  a.beta = reinterpret_cast<const uint16_t*>(beta.data_ptr());
+  a.running_mean = running_mean.data_ptr<float>();
+  a.running_var = running_var.data_ptr<float>();
+  a.save_mean = mean.data_ptr<float>();
+  a.save_invstd = invstd.data_ptr<float>();
+  a.ss = ss.data_ptr<float>();
+  a.part = part.data_ptr<float>();
+  a.part_ready = nblk;
+  a.counter = opt_ptr<int64_t>(counter);
+  a.pool_arg = arg.data_ptr<uint8_t>();
+  a.N = (int32_t)N;
+  a.H = (int32_t)Ho;
+  a.W = (int32_t)Wo;
+  a.M = N * Ho * Wo;
+  a.C = 64;
+  a.relu = 1;
+  a.training = 1;
+  a.momentum = (float)momentum;
+  a.eps = (float)eps;
+  e = launch_bn_fwd(a, st);
+  TORCH_CHECK(e == hipSuccess, "psd stem bn_pool: ", hipGetErrorString(e));
+  return {y, arg, mean, invstd, ss, conv};
 }
 
 // Backward of bn_pool_fwd: gpool (+ gpool2, a second consumer's gradient of the pooled output)

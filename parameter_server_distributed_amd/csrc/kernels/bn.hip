@@ -612,8 +612,11 @@ hipError_t launch_bn_fwd(const BnFwdArgs& a, hipStream_t st) {
   int gx, gy;
   reduce_grid(a.M, a.C, gx, gy);
   if (a.training) {
-    hipLaunchKernelGGL(bn_fwd_reduce_kernel, dim3(gx, gy), dim3(256), 0, st, a.x, a.M, a.C, a.running_mean, a.part,
-                       bn_reverse());
+    if (a.part_ready > 0)  // statistics already reduced by the producing kernel (stem conv epilogue)
+      gx = a.part_ready;
+    else
+      hipLaunchKernelGGL(bn_fwd_reduce_kernel, dim3(gx, gy), dim3(256), 0, st, a.x, a.M, a.C, a.running_mean, a.part,
+                         bn_reverse());
     hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((a.C + kFinCh - 1) / kFinCh), dim3(256), 0, st, a.part, gx, a.M, a.C,
                        a.running_mean, a.gamma, a.beta, a.running_mean, a.running_var, a.momentum, a.eps, a.save_mean,
                        a.save_invstd, a.ss, a.counter);

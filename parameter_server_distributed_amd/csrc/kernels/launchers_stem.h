@@ -1,0 +1,13 @@
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <cstdint>
+
+namespace psd {
+// 7x7/s2/p3 3->64 NHWC bf16 stem convolution (kernels/stem.hip). wk = weights repacked as
+// [64][192] (k = kh*24 + kw*3 + ci, zero elsewhere); part receives stem_conv_blocks() rows of
+// [2][64] shifted BN partial sums (shift = running mean, may be null).
+bool stem_conv_supported(int H, int W, int Ho, int Wo);
+int stem_conv_blocks(int N, int Ho);
+hipError_t launch_stem_conv(const uint16_t* x, const uint16_t* wk, uint16_t* y, const float* shift, float* part, int N,
+                            int H, int W, int Ho, int Wo, hipStream_t stream);
+}  // namespace psd

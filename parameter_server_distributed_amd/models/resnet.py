@@ -12,8 +12,8 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from ..ops.bn import FusedBatchNorm2d, bn_relu_maxpool
-from ..ops.conv import Conv1x1
+from ..ops.bn import FusedBatchNorm2d
+from ..ops.conv import Conv1x1, stem_forward
 from ..ops.pool import MaxPool3x3s2, global_avg_pool
 
 
@@ -110,7 +110,7 @@ class ResNet(nn.Module):
         return nn.Sequential(*mods)
 
     def forward(self, x):
-        x = bn_relu_maxpool(self.bn1, self.maxpool, self.conv1(x))  # one fused kernel family on gfx950
+        x = stem_forward(self.conv1, self.bn1, self.maxpool, x)  # conv + BN + ReLU + pool, fused on gfx950
         # the first bottleneck's downsample-branch gradient goes to the max-pool's backward kernel
         prev = self.maxpool if self.maxpool.native_last else None
         for layer in (self.layer1, self.layer2, self.layer3, self.layer4):

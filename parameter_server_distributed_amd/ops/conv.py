@@ -1,4 +1,5 @@
-"""1x1 / stride-1 convolutions of the NHWC ResNets as GEMMs where that is faster than MIOpen.
+"""Convolution routing for the NHWC ResNets: 1x1 / stride-1 convolutions as GEMMs where that is
+faster than MIOpen, and the stem convolution on its own gfx950 kernel (bottom of this file).
 
 On NHWC bf16 a 1x1 stride-1 convolution *is* a GEMM over the [N*H*W, C] view of the activation:
 
@@ -136,3 +137,59 @@ class Conv1x1(nn.Conv2d):
                 and x.is_contiguous(memory_format=torch.channels_last)):
             return _Conv1x1Fn.apply(x, self.weight)
         return F.conv2d(x, self.weight)
+
+
+# ---------------------------------------------------------------------------------------------
+# ResNet stem: conv 7x7/s2/p3 (3 -> 64) + BN + ReLU + 3x3/s2 max-pool
+
+
+class _StemFn(torch.autograd.Function):
+    """Forward: the gfx950 stem convolution (kernels/stem.hip, BN statistics in its epilogue) and
+    the fused BN + ReLU + max-pool; nothing between the image and the pooled map is written except
+    the conv output the BN backward needs. Backward: the pool-fused BN backward, then the weight
+    gradient on MIOpen (the image needs no gradient)."""
+
+    @staticmethod
+    def forward(ctx, x, w, bn_w, bn_b, bn, pool):
+        from .. import native
+
+        y, arg, mean, invstd, ss, conv_out = native().stem_fwd(
+            x, w, bn_w, bn_b, bn.running_mean, bn.running_var, bn.momentum if bn.momentum is not None else 0.1, bn.eps,
+            bn.num_batches_tracked)
+        ctx.bn, ctx.pool = bn, pool
+        ctx.save_for_backward(x, w, conv_out, arg, bn_w, mean, invstd, ss)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        from .. import native
+
+        x, w, conv_out, arg, bn_w, mean, invstd, ss = ctx.saved_tensors
+        sink = getattr(ctx.bn, "_psd_grad_sink", None)
+        dgo = dbo = None
+        if sink is not None:
+            dgo, dbo = sink(ctx.bn.weight), sink(ctx.bn.bias)
+        pend = getattr(ctx.pool, "_psd_pending_dr", None)
+        gy2 = pend.pop() if pend else None
+        dconv, dg, db = native().bn_pool_bwd(gy, gy2, arg, conv_out, bn_w, mean, invstd, ss, dgo, dbo)
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dw = torch.ops.aten.convolution_backward(dconv, x, w, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1,
+                                                     [False, True, False])[1]
+        return None, dw, dg, db, None, None
+
+
+def stem_forward(conv: nn.Conv2d, bn, pool, x: torch.Tensor) -> torch.Tensor:
+    """``pool(relu(bn(conv(x))))`` for the ResNet stem: the fused gfx950 path when training on a
+    supported shape, else the composition (``ops.bn.bn_relu_maxpool`` after ``conv``)."""
+    from .bn import bn_relu_maxpool
+
+    w = conv.weight
+    if (_enabled() and bn.training and bn.relu and torch.is_grad_enabled() and x.is_cuda and x.dim() == 4
+            and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and tuple(w.shape) == (64, 3, 7, 7)
+            and conv.stride == (2, 2) and conv.padding == (3, 3) and conv.bias is None and not x.requires_grad
+            and bn.weight is not None and bn.weight.dtype == torch.bfloat16 and bn.running_mean is not None
+            and x.shape[2] % 8 == 0 and x.shape[3] % 32 == 0):
+        pool.native_last = True
+        return _StemFn.apply(x, w, bn.weight, bn.bias, bn, pool)
+    return bn_relu_maxpool(bn, pool, conv(x))

