@@ -275,6 +275,27 @@ std::vector<at::Tensor> stem_fwd(const at::Tensor& x_in, const at::Tensor& w, co
   return {y, arg, mean, invstd, ss, conv};
 }
 
+// Weight gradient of the stem conv (kernels/stem.hip): x [N, 3, H, W], dy [N, 64, H/2, W/2] (both
+// channels_last bf16) -> dW [64, 3, 7, 7] bf16 channels_last.
+at::Tensor stem_wgrad(const at::Tensor& x_in, const at::Tensor& dy_in) {
+  TORCH_CHECK(x_in.is_cuda() && x_in.scalar_type() == at::kBFloat16 && x_in.dim() == 4 && x_in.size(1) == 3,
+              "psd stem wgrad: bf16 [N, 3, H, W] input");
+  const c10::DeviceGuard g(x_in.device());
+  at::Tensor x = x_in.contiguous(at::MemoryFormat::ChannelsLast), dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
+  const int64_t N = x.size(0), H = x.size(2), W = x.size(3), Ho = H / 2, Wo = W / 2;
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && dy.sizes() == at::IntArrayRef({N, 64, Ho, Wo}), "psd stem wgrad: dy shape");
+  TORCH_CHECK(stem_wgrad_supported((int)H, (int)W, (int)Ho, (int)Wo), "psd stem wgrad: unsupported input ", x.sizes());
+  const int nblk = stem_wgrad_blocks((int)N, (int)Ho);
+  at::Tensor part = at::empty({(int64_t)nblk * 192 * 64}, x.options().dtype(at::kFloat));
+  at::Tensor dw = at::empty({64, 3, 7, 7}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  hipError_t e = launch_stem_wgrad(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                   reinterpret_cast<const uint16_t*>(dy.data_ptr()), part.data_ptr<float>(),
+                                   reinterpret_cast<uint16_t*>(dw.data_ptr()), (int)N, (int)H, (int)W, (int)Ho, (int)Wo,
+                                   stream_of(x));
+  TORCH_CHECK(e == hipSuccess, "psd stem wgrad: ", hipGetErrorString(e));
+  return dw;
+}
+
 // Backward of bn_pool_fwd: gpool (+ gpool2, a second consumer's gradient of the pooled output)
 // -> {dx, dgamma, dbeta}; the pool gradient is recomputed inside the BN passes.
 std::vector<at::Tensor> bn_pool_bwd(const at::Tensor& gpool_in, c10::optional<at::Tensor> gpool2_in, const at::Tensor& arg,

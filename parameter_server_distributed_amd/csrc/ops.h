@@ -44,6 +44,7 @@ std::vector<at::Tensor> bn_pool_fwd(const at::Tensor& x, const at::Tensor& gamma
 std::vector<at::Tensor> stem_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& gamma, const at::Tensor& beta,
                                  const at::Tensor& running_mean, const at::Tensor& running_var, double momentum,
                                  double eps, c10::optional<at::Tensor> counter);
+at::Tensor stem_wgrad(const at::Tensor& x, const at::Tensor& dy);
 std::vector<at::Tensor> bn_pool_bwd(const at::Tensor& gpool, c10::optional<at::Tensor> gpool2, const at::Tensor& arg,
                                     const at::Tensor& x, const at::Tensor& gamma, const at::Tensor& save_mean,
                                     const at::Tensor& save_invstd, const at::Tensor& ss,

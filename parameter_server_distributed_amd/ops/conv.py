@@ -147,7 +147,7 @@ class _StemFn(torch.autograd.Function):
     """Forward: the gfx950 stem convolution (kernels/stem.hip, BN statistics in its epilogue) and
     the fused BN + ReLU + max-pool; nothing between the image and the pooled map is written except
     the conv output the BN backward needs. Backward: the pool-fused BN backward, then the weight
-    gradient on MIOpen (the image needs no gradient)."""
+    gradient on the gfx950 stem wgrad kernel (the image needs no gradient)."""
 
     @staticmethod
     def forward(ctx, x, w, bn_w, bn_b, bn, pool):
@@ -172,10 +172,7 @@ class _StemFn(torch.autograd.Function):
         pend = getattr(ctx.pool, "_psd_pending_dr", None)
         gy2 = pend.pop() if pend else None
         dconv, dg, db = native().bn_pool_bwd(gy, gy2, arg, conv_out, bn_w, mean, invstd, ss, dgo, dbo)
-        dw = None
-        if ctx.needs_input_grad[1]:
-            dw = torch.ops.aten.convolution_backward(dconv, x, w, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1,
-                                                     [False, True, False])[1]
+        dw = native().stem_wgrad(x, dconv) if ctx.needs_input_grad[1] else None
         return None, dw, dg, db, None, None
 
 
@@ -189,7 +186,7 @@ def stem_forward(conv: nn.Conv2d, bn, pool, x: torch.Tensor) -> torch.Tensor:
             and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and tuple(w.shape) == (64, 3, 7, 7)
             and conv.stride == (2, 2) and conv.padding == (3, 3) and conv.bias is None and not x.requires_grad
             and bn.weight is not None and bn.weight.dtype == torch.bfloat16 and bn.running_mean is not None
-            and x.shape[2] % 8 == 0 and x.shape[3] % 32 == 0):
+            and x.shape[2] % 8 == 0 and x.shape[3] % 32 == 0 and x.shape[3] <= 352):
         pool.native_last = True
         return _StemFn.apply(x, w, bn.weight, bn.bias, bn, pool)
     return bn_relu_maxpool(bn, pool, conv(x))

@@ -320,3 +320,21 @@ def test_stem_conv_fused_matches_unfused(gpu, shape):
     for a, b in ((conv.weight.grad, dw0), (bn.weight.grad, bn0.weight.grad), (bn.bias.grad, bn0.bias.grad)):
         a, b = a.float(), b.float()
         assert ((a - b).norm() / b.norm()).item() < 2e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(2, 3, 64, 64), (4, 3, 224, 224), (3, 3, 32, 96)], ids=str)
+def test_stem_wgrad_matches_fp32(gpu, shape):
+    """gfx950 stem weight gradient (MFMA reduction over all output pixels) against an fp32 conv."""
+    from parameter_server_distributed_amd import native
+
+    torch.manual_seed(0)
+    cl = dict(memory_format=torch.channels_last)
+    x = torch.randn(shape).to(torch.bfloat16)
+    dy = torch.randn(shape[0], 64, shape[2] // 2, shape[3] // 2).to(torch.bfloat16)
+    dw = native().stem_wgrad(x.to(gpu).contiguous(**cl), dy.to(gpu).contiguous(**cl))
+    assert dw.shape == (64, 3, 7, 7) and dw.is_contiguous(memory_format=torch.channels_last)
+    w = torch.zeros(64, 3, 7, 7, requires_grad=True)
+    torch.nn.functional.conv2d(x.float(), w, stride=2, padding=3).backward(dy.float())
+    ref = w.grad
+    torch.testing.assert_close(dw.float().cpu(), ref, rtol=2e-2, atol=1e-2 * ref.abs().max().item())
