@@ -76,6 +76,9 @@ def parse():
     # per-shape Find (warmup ~1 s instead of ~2-4 min per rank; measured 1-2 % slower steps)
     ap.add_argument("--benchmark-miopen", type=int, default=0, help="torch.backends.cudnn.benchmark (MIOpen Find)")
     ap.add_argument("--out", default="", help="also write the JSON line to this file")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend for N > 1: nccl (= RCCL, the data plane) or gloo (rehearsal of the "
+                         "multi-rank flow with several ranks sharing one GPU; not a performance path)")
     ap.add_argument("--trace", default="", help="per-step phase trace (JSON lines, one file per rank); eager")
     ap.add_argument("--push-mode", default="reduce", choices=["auto", "reduce", "p2p"],
                     help="push/pull when PS shards < ranks: RCCL reduce/broadcast per slice (default) or "
@@ -98,10 +101,16 @@ def main():
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU (MI355X); CPU plumbing runs live in tests/ and scripts/test_local.sh")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    if a.backend == "nccl" and world > 1 and local >= ndev:
+        raise SystemExit(f"LOCAL_RANK {local} but only {ndev} visible GPU(s): RCCL needs one GPU per rank")
+    dev = torch.device("cuda", local % ndev)  # gloo rehearsal: ranks may share a GPU
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
     torch.backends.cudnn.benchmark = bool(a.benchmark_miopen)
     torch.manual_seed(1234)  # identical init on every rank; the PS init pull makes it exact
 
@@ -137,7 +146,10 @@ def main():
 
     def barrier():
         if world > 1:
-            dist.barrier(device_ids=[local])
+            if a.backend == "nccl":
+                dist.barrier(device_ids=[dev.index])
+            else:
+                dist.barrier()
         torch.cuda.synchronize(dev)
 
     t_w0 = time.perf_counter()

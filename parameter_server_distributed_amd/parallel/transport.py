@@ -129,6 +129,11 @@ class TorchDistTransport(Transport):
             dist.all_gather_into_tensor(out, inp, group=self.group_)
 
     def reduce(self, t, root):
+        if self.backend == "gloo" and t.is_cuda:
+            # gloo has no device reduce: all-reduce (only the root's copy is consumed). Rehearsal
+            # path for several ranks sharing one GPU (bench.py --backend gloo), not a data plane.
+            dist.all_reduce(t, group=self.group_)
+            return
         dist.reduce(t, dst=self._g(root), group=self.group_)
 
     def broadcast(self, t, root):
