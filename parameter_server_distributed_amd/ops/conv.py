@@ -24,46 +24,29 @@ src/worker.cpp:316-329). This is worker-side compute for the BASELINE.json ResNe
 """
 from __future__ import annotations
 
-import os
-
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-_DECISIONS: dict[tuple, str] = {}
+from . import autotune as _at
 
 
 def _enabled() -> bool:
-    return os.environ.get("PSD_CONV1X1", "1") != "0"
-
-
-def _time_ms(fn, reps: int = 3) -> float:
-    fn()  # warm (library heuristics / kernel load)
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(reps):
-        fn()
-    e.record()
-    e.synchronize()
-    return s.elapsed_time(e) / reps
+    return _at.enabled("PSD_CONV1X1")
 
 
 def _choose(key: tuple, candidates: dict) -> str:
-    """Fastest candidate for ``key`` (timed once, cached); MIOpen while a graph is being captured."""
-    got = _DECISIONS.get(key)
-    if got is not None:
-        return got
-    if torch.cuda.is_current_stream_capturing():
-        return "miopen"
-    times = {name: _time_ms(fn) for name, fn in candidates.items()}
-    best = min(times, key=times.get)
-    _DECISIONS[key] = best
-    return best
+    """Fastest candidate for ``key`` (ops/autotune.py); MIOpen while a graph is being captured."""
+    return _at.choose(("conv1x1",) + key, candidates, "miopen")
 
 
 def decisions() -> dict:
-    """The cached per-shape choices (for logs / tests)."""
-    return dict(_DECISIONS)
+    """The cached per-shape 1x1-conv choices, keyed (kind, M, cin, cout) (for logs / tests)."""
+    return {k[1:]: v for k, v in _at.decisions().items() if k[0] == "conv1x1"}
+
+
+def set_decision(key: tuple, name: str | None) -> None:
+    _at.set_decision(("conv1x1",) + key, name)
 
 
 def _as_2d(t: torch.Tensor) -> torch.Tensor:

@@ -12,6 +12,12 @@ amax scaling (x and W quantised each step by the amax/quant kernels) on the MX-s
 v_mfma_scale_f32_16x16x128_f8f6f4 (2x the bf16 MFMA rate); the backward GEMMs stay bf16 on the
 saved bf16 x and W (fp8 forward / bf16 backward recipe). Needs in_features % 128 == 0.
 
+Per-shape routing (ops/autotune.py): for bf16 the forward, dgrad and wgrad GEMMs are each timed
+once against hipBLASLt (torch.addmm / mm; bias + activation then run as separate passes) and the
+faster path is kept. Measured on BERT-base (M = 8192 tokens) hipBLASLt wins most forward / dgrad
+shapes, the split-K MFMA wgrad writing straight into the PS gradient buffer stays competitive.
+``PSD_LINEAR_TUNE=0`` pins everything to the MFMA kernels.
+
 CPU tensors (and non-bf16 / unaligned shapes) use ``F.linear`` -- the reference the tests compare
 against.
 """
@@ -22,6 +28,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import native
+from . import autotune as _at
 
 ACTS = {None: 0, "none": 0, "relu": 1, "gelu": 2}
 
@@ -29,6 +36,13 @@ ACTS = {None: 0, "none": 0, "relu": 1, "gelu": 2}
 def _ok(x: torch.Tensor, w: torch.Tensor) -> bool:
     return (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.shape[0] % 8 == 0
             and w.shape[1] % 8 == 0)
+
+
+def _route(key: tuple, mfma, blas):
+    """The faster of the MFMA kernel and hipBLASLt for this GEMM shape (ops/autotune.py)."""
+    if not _at.enabled("PSD_LINEAR_TUNE"):
+        return mfma
+    return mfma if _at.choose(("linear",) + key, {"mfma": mfma, "blas": blas}, "mfma") == "mfma" else blas
 
 
 class _LinearFn(torch.autograd.Function):
@@ -48,7 +62,21 @@ class _LinearFn(torch.autograd.Function):
             wq, sw = quantize_fp8(weight)
             C.gemm_fp8_(xq, wq, sx, sw, y, bias, act, aux)
         else:
-            C.gemm_(x2, weight, True, True, y, bias, act, aux)
+            def mfma():
+                C.gemm_(x2, weight, True, True, y, bias, act, aux)
+
+            def blas():
+                pre = aux if act == 2 else y
+                if bias is not None:
+                    torch.addmm(bias, x2, weight.t(), out=pre)
+                else:
+                    torch.mm(x2, weight.t(), out=pre)
+                if act == 1:
+                    torch.relu_(y)
+                elif act == 2:
+                    torch.ops.aten.gelu.out(aux, approximate="tanh", out=y)
+
+            _route(("fwd", M, x2.shape[1], N, act, bias is not None), mfma, blas)()
         ctx.act = act
         ctx.mod = mod
         ctx.has_bias = bias is not None
@@ -65,10 +93,12 @@ class _LinearFn(torch.autograd.Function):
             dy2 = dy2 * (keep > 0)
         elif ctx.act == 2:
             dy2 = torch.ops.aten.gelu_backward(dy2, keep, approximate="tanh")
+        M, K, N = x2.shape[0], x2.shape[1], w.shape[0]
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(x2.shape, dtype=dy2.dtype, device=dy2.device)
-            C.gemm_(dy2, w, True, False, dx)
+            _route(("dgrad", M, K, N), lambda: C.gemm_(dy2, w, True, False, dx),
+                   lambda: torch.mm(dy2, w, out=dx))()
             dx = dx.view(ctx.in_shape)
         sink = getattr(ctx.mod, "_psd_grad_sink", None)
         dw = db = None
@@ -76,7 +106,8 @@ class _LinearFn(torch.autograd.Function):
             dw = sink(ctx.mod.weight) if sink is not None else None
             if dw is None:
                 dw = torch.empty(w.shape, dtype=w.dtype, device=w.device)
-            C.gemm_splitk_(dy2, x2, False, False, dw, False, 1.0, 0)
+            _route(("wgrad", M, K, N), lambda: C.gemm_splitk_(dy2, x2, False, False, dw, False, 1.0, 0),
+                   lambda: torch.mm(dy2.t(), x2, out=dw))()
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = sink(ctx.mod.bias) if sink is not None else None
             if db is None:

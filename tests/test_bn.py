@@ -183,14 +183,14 @@ def test_conv1x1_routes_match_fp32(gpu, route):
     xd = x.clone().requires_grad_(True)
     M = 3 * 10 * 12
     for kind in ("fwd", "dgrad"):
-        cv._DECISIONS[(kind, M, 64, 96)] = route
+        cv.set_decision((kind, M, 64, 96), route)
     try:
         y = m(xd)
         g = torch.randn(y.shape).to(torch.bfloat16).to(gpu).contiguous(memory_format=torch.channels_last)
         y.backward(g)
     finally:
         for kind in ("fwd", "dgrad"):
-            cv._DECISIONS.pop((kind, M, 64, 96), None)
+            cv.set_decision((kind, M, 64, 96), None)
     xr = x.float().cpu().requires_grad_(True)
     wr = m.weight.detach().float().cpu().requires_grad_(True)
     yr = F.conv2d(xr, wr)

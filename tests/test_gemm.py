@@ -181,3 +181,42 @@ def test_mfma_linear_fp8_forward_backward(gpu):
     relx = (xb.grad.float() - xr.grad).norm() / xr.grad.norm()
     relw = (lin.weight.grad.float() - ref.weight.grad).norm() / ref.weight.grad.norm()
     assert relx < 0.08 and relw < 0.08, (relx, relw)
+
+
+@pytest.mark.parametrize("route", ["mfma", "blas"])
+@pytest.mark.parametrize("act", [None, "relu", "gelu"])
+def test_mfma_linear_routes_match_fp32(gpu, route, act):
+    """Both per-shape routes of MfmaLinear (MFMA kernels / hipBLASLt + separate epilogue) against an
+    fp32 nn.Linear: forward, dx, dW, db."""
+    from parameter_server_distributed_amd.ops import autotune as at
+    from parameter_server_distributed_amd.ops.linear import ACTS, MfmaLinear
+
+    torch.manual_seed(0)
+    M, K, N = 384, 256, 320
+    lin = MfmaLinear(K, N, act=act).to(gpu, torch.bfloat16)
+    ref = torch.nn.Linear(K, N).to(gpu)
+    with torch.no_grad():
+        ref.weight.copy_(lin.weight.float())
+        ref.bias.copy_(lin.bias.float())
+    keys = [("linear", "fwd", M, K, N, ACTS[act], True), ("linear", "dgrad", M, K, N), ("linear", "wgrad", M, K, N)]
+    for k in keys:
+        at.set_decision(k, route)
+    try:
+        x = torch.randn(M, K, device=gpu)
+        xb = x.to(torch.bfloat16).requires_grad_(True)
+        xr = x.to(torch.bfloat16).float().requires_grad_(True)
+        y = lin(xb)
+        yr = ref(xr)
+        if act == "relu":
+            yr = torch.relu(yr)
+        elif act == "gelu":
+            yr = torch.nn.functional.gelu(yr, approximate="tanh")
+        g = torch.randn_like(yr)
+        y.backward(g.to(torch.bfloat16))
+        yr.backward(g.to(torch.bfloat16).float())
+    finally:
+        for k in keys:
+            at.set_decision(k, None)
+    for a, b in ((y, yr), (xb.grad, xr.grad), (lin.weight.grad, ref.weight.grad), (lin.bias.grad, ref.bias.grad)):
+        rel = ((a.float() - b).norm() / b.norm()).item()
+        assert rel < 2e-2, rel
