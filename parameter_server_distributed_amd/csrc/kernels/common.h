@@ -12,12 +12,16 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
 
-// Round-to-nearest-even fp32 -> bf16, NaN preserved (quiet bit forced).
-__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
+// Round-to-nearest-even fp32 -> bf16, NaN preserved. A plain cast is one v_cvt_pk_bf16_f32 on
+// gfx950 (two values per instruction when paired, pack_bf16x2_rne); the integer-arithmetic rounding
+// this replaced cost ~5 VALU per value, which made the BN apply and stem pool passes issue-bound
+// (SQ_WAIT_INST_ANY ~45 % of wave cycles in profiles/pmc_r1.md).
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
+
+typedef __bf16 psd_bf16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pack_bf16x2_rne(float lo, float hi) {
+  const psd_bf16x2 v = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(uint32_t, v);
 }
 
 // 8 consecutive elements <-> registers, one 16-byte (bf16) or two 16-byte (fp32) loads per lane.
@@ -43,8 +47,7 @@ __device__ __forceinline__ void load8_bf16(const uint16_t* p, float v[8]) {
 __device__ __forceinline__ void store8_bf16(uint16_t* p, const float v[8]) {
   uint32_t ws[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-    ws[i] = (uint32_t)f32_to_bf16(v[2 * i]) | ((uint32_t)f32_to_bf16(v[2 * i + 1]) << 16);
+  for (int i = 0; i < 4; ++i) ws[i] = pack_bf16x2_rne(v[2 * i], v[2 * i + 1]);
   *reinterpret_cast<u32x4*>(p) = u32x4{ws[0], ws[1], ws[2], ws[3]};
 }
 
