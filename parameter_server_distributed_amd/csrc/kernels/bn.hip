@@ -227,7 +227,11 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
 #pragma unroll
       for (int j = 0; j < 8; ++j) bits |= (t[j] > 0.f ? 1u : 0u) << j;
       if (pack4) {  // 4 lanes -> one dword store (host: nvec % 4 == 0, so a lane quad is all active)
-        const uint32_t b1 = __shfl_down(bits, 1), b2 = __shfl_down(bits, 2), b3 = __shfl_down(bits, 3);
+        // lanes 1..3 of the quad via DPP quad_perm broadcasts (VALU; __shfl_down was an LDS
+        // ds_bpermute per value)
+        const uint32_t b1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0x55, 0xF, 0xF, false);
+        const uint32_t b2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0xAA, 0xF, 0xF, false);
+        const uint32_t b3 = (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0xFF, 0xF, 0xF, false);
         if ((threadIdx.x & 3) == 0)
           *reinterpret_cast<uint32_t*>(mbits + v) = bits | (b1 << 8) | (b2 << 16) | (b3 << 24);
       } else {
