@@ -1224,10 +1224,11 @@ hipError_t launch_colsum(const uint16_t* x, int64_t M, int N, float* part, void*
   const int tpc = N / 8;
   const int gy = tpc >= 256 ? (tpc + 255) / 256 : 1;
   const int rpi = tpc >= 256 ? 1 : 256 / tpc;
-  // enough row-chunks to fill the chip (~1024 resident blocks over all column groups), each
-  // thread summing >= 8 rows
-  int64_t gx = (M + (int64_t)rpi * 8 - 1) / ((int64_t)rpi * 8);
-  const int64_t want = (1024 + gy - 1) / gy;
+  // each thread sums >= 32 rows and there are <= ~256 partial rows: the finalize (one lane group
+  // per 32 columns, latency-bound) then sums <= 32 partials per lane. At >= 8 rows per thread and
+  // 512 partial rows the finalize alone took 20 us per BERT bias (profiles/bert_base_b64_r1_tuned_kernels.md).
+  int64_t gx = (M + (int64_t)rpi * 32 - 1) / ((int64_t)rpi * 32);
+  const int64_t want = (256 + gy - 1) / gy;
   if (gx > want) gx = want;
   if (gx > kColsumMaxBlocks) gx = kColsumMaxBlocks;
   if (gx < 1) gx = 1;
