@@ -48,6 +48,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("stem_fwd", &stem_fwd, py::arg("x"), py::arg("w"), py::arg("gamma"), py::arg("beta"), py::arg("running_mean"),
         py::arg("running_var"), py::arg("momentum"), py::arg("eps"), py::arg("counter") = py::none());
   m.def("stem_wgrad", &stem_wgrad);
+  m.def("ln_fwd", &ln_fwd, py::arg("x"), py::arg("h"), py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("p"),
+        py::arg("seed"), py::arg("step") = py::none());
+  m.def("ln_bwd", &ln_bwd, py::arg("dy"), py::arg("s"), py::arg("mean"), py::arg("rstd"), py::arg("gamma"), py::arg("p"),
+        py::arg("seed"), py::arg("step") = py::none(), py::arg("dgamma_out") = py::none(),
+        py::arg("dbeta_out") = py::none());
   m.def("bn_pool_bwd", &bn_pool_bwd, py::arg("gpool"), py::arg("gpool2"), py::arg("arg"), py::arg("x"), py::arg("gamma"),
         py::arg("save_mean"), py::arg("save_invstd"), py::arg("ss"), py::arg("dgamma_out") = py::none(),
         py::arg("dbeta_out") = py::none());

@@ -1,0 +1,33 @@
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <cstdint>
+
+namespace psd {
+// y = LayerNorm(x + dropout_p(h)) over rows of H (kernels/layernorm.hip) and its backward.
+struct LnArgs {
+  const uint16_t* x;      // fwd: residual input [rows, H] bf16
+  const uint16_t* h;      // fwd: branch output (dropout applied) [rows, H] bf16
+  const uint16_t* gamma;  // [H] bf16
+  const uint16_t* beta;   // [H] bf16
+  uint16_t* y;            // fwd out [rows, H]
+  uint16_t* s;            // fwd out / bwd in: x + dropout(h), the LN input, bf16
+  float* mean;            // [rows]
+  float* rstd;            // [rows]
+  const uint16_t* dy;     // bwd in
+  uint16_t* dx;           // bwd out: gradient of x (= of s)
+  uint16_t* dh;           // bwd out: gradient of h (dropout mask applied)
+  uint16_t* dgamma;       // bwd out [H] bf16 (may be the PS gradient sink)
+  uint16_t* dbeta;        // bwd out [H] bf16
+  float* part;            // bwd workspace [ln_bwd_blocks(rows)][2][H] fp32
+  const int64_t* step;    // device step counter mixed into the dropout hash (may be null)
+  int64_t rows;
+  int32_t H;
+  float eps;
+  float p;                // dropout probability (0: identity)
+  uint32_t seed;          // per call site
+};
+bool ln_supported(int H);
+int ln_bwd_blocks(int64_t rows);
+hipError_t launch_ln_fwd(const LnArgs& a, hipStream_t stream);
+hipError_t launch_ln_bwd(const LnArgs& a, hipStream_t stream);
+}  // namespace psd

@@ -1,0 +1,242 @@
+// Fused transformer residual block tail for gfx950: y = LayerNorm(x + dropout(h)) forward and the
+// matching backward (LN backward + dropout backward + the residual branch's gradient), bf16 in/out,
+// fp32 statistics.
+//
+// Why: BERT-base's 24 post-attention / post-FFN sites ran this as 3 PyTorch kernels forward
+// (dropout, add, layer_norm) and 4 backward (layer_norm_grad_input, two gamma/beta partial passes,
+// masked_scale) -- ~2.9 ms of an 18 ms step (profiles/bert_base_b64_r1_tuned_kernels.md), each
+// re-reading the [tokens, 768] activations. Here forward reads x and h once and writes y plus the
+// bf16 sum s (the LN input backward needs); backward reads dy and s once and writes the residual
+// gradient dx and the pre-dropout gradient dh.
+//
+// Layout: one wave (64 lanes) per row of H = 64*E elements, lane l owning columns [l*E, l*E + E)
+// (8-byte loads/stores; E % 4 == 0: H = 768 -> E = 12). Row statistics by wave butterfly reductions.
+// Dropout keeps element i with probability 1-p from a counter-based hash of (seed, step, i); the
+// step is read from device memory (a counter the model bumps on the device every forward), so a
+// replayed hipGraph draws new masks every step, and the backward regenerates the same mask.
+// gamma/beta gradients: per-lane column partials across the rows a wave visits -> block partials
+// [blk][2][H] -> deterministic finalize (fixed order).
+#include "common.h"
+#include "launchers_ln.h"
+
+namespace psd {
+
+namespace {
+
+__device__ __forceinline__ uint32_t mix32(uint32_t h) {  // murmur3 finalizer
+  h ^= h >> 16;
+  h *= 0x85ebca6bu;
+  h ^= h >> 13;
+  h *= 0xc2b2ae35u;
+  h ^= h >> 16;
+  return h;
+}
+
+__device__ __forceinline__ bool keep_elem(uint32_t key, uint64_t idx, uint32_t thresh) {
+  const uint32_t a = mix32(key ^ (uint32_t)idx * 0x9e3779b9u);
+  return mix32(a ^ (uint32_t)(idx >> 32) ^ 0x7f4a7c15u) >= thresh;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+template <int E>
+__device__ __forceinline__ void load_e(const uint16_t* p, float v[E]) {
+#pragma unroll
+  for (int i = 0; i < E / 4; ++i) {
+    const uint2 w = *reinterpret_cast<const uint2*>(p + 4 * i);
+    v[4 * i + 0] = __uint_as_float(w.x << 16);
+    v[4 * i + 1] = __uint_as_float(w.x & 0xffff0000u);
+    v[4 * i + 2] = __uint_as_float(w.y << 16);
+    v[4 * i + 3] = __uint_as_float(w.y & 0xffff0000u);
+  }
+}
+
+template <int E>
+__device__ __forceinline__ void store_e(uint16_t* p, const float v[E]) {
+#pragma unroll
+  for (int i = 0; i < E / 4; ++i)
+    *reinterpret_cast<uint2*>(p + 4 * i) = make_uint2(pack_bf16x2_rne(v[4 * i], v[4 * i + 1]),
+                                                      pack_bf16x2_rne(v[4 * i + 2], v[4 * i + 3]));
+}
+
+__device__ __forceinline__ uint32_t dropout_key(uint32_t seed, const int64_t* step) {
+  return mix32(seed * 0x27d4eb2fu ^ (uint32_t)(step ? *step : 0) * 0x165667b1u);
+}
+
+}  // namespace
+
+template <int E>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ h,
+                                                     const uint16_t* __restrict__ gamma,
+                                                     const uint16_t* __restrict__ beta, uint16_t* __restrict__ y,
+                                                     uint16_t* __restrict__ s_out, float* __restrict__ mean_out,
+                                                     float* __restrict__ rstd_out, int64_t rows, float eps,
+                                                     uint32_t seed, const int64_t* __restrict__ step, uint32_t thresh,
+                                                     float scale) {
+  constexpr int H = 64 * E;
+  const int lane = threadIdx.x & 63;
+  const int c0 = lane * E;
+  float g[E], b[E];
+  load_e<E>(gamma + c0, g);
+  load_e<E>(beta + c0, b);
+  const uint32_t key = dropout_key(seed, step);
+  const int64_t wstride = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < rows; r += wstride) {
+    const int64_t off = r * H + c0;
+    float xv[E], hv[E];
+    load_e<E>(x + off, xv);
+    load_e<E>(h + off, hv);
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      const float d = (thresh == 0u || keep_elem(key, (uint64_t)(off + i), thresh)) ? hv[i] * scale : 0.f;
+      xv[i] = bf16_to_f32(f32_to_bf16(xv[i] + d));  // s, rounded as stored (the LN input)
+      sum += xv[i];
+    }
+    const float mean = wave_sum(sum) * (1.f / H);
+    float sq = 0.f;
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      const float d = xv[i] - mean;
+      sq = fmaf(d, d, sq);
+    }
+    const float rstd = rsqrtf(wave_sum(sq) * (1.f / H) + eps);
+    store_e<E>(s_out + off, xv);
+#pragma unroll
+    for (int i = 0; i < E; ++i) hv[i] = fmaf((xv[i] - mean) * rstd, g[i], b[i]);
+    store_e<E>(y + off, hv);
+    if (lane == 0) {
+      mean_out[r] = mean;
+      rstd_out[r] = rstd;
+    }
+  }
+}
+
+template <int E>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ s,
+                                                     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+                                                     const uint16_t* __restrict__ gamma, uint16_t* __restrict__ dx,
+                                                     uint16_t* __restrict__ dh, float* __restrict__ part, int64_t rows,
+                                                     uint32_t seed, const int64_t* __restrict__ step, uint32_t thresh,
+                                                     float scale) {
+  constexpr int H = 64 * E;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c0 = lane * E;
+  float g[E], pg[E], pb[E];
+  load_e<E>(gamma + c0, g);
+#pragma unroll
+  for (int i = 0; i < E; ++i) pg[i] = pb[i] = 0.f;
+  const uint32_t key = dropout_key(seed, step);
+  const int64_t wstride = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv; r < rows; r += wstride) {
+    const int64_t off = r * H + c0;
+    float dv[E], sv[E];
+    load_e<E>(dy + off, dv);
+    load_e<E>(s + off, sv);
+    const float mean = mean_in[r], rstd = rstd_in[r];
+    float a = 0.f, bsum = 0.f;
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      sv[i] = (sv[i] - mean) * rstd;  // xhat
+      pg[i] = fmaf(dv[i], sv[i], pg[i]);
+      pb[i] += dv[i];
+      dv[i] *= g[i];  // dxhat
+      a += dv[i];
+      bsum = fmaf(dv[i], sv[i], bsum);
+    }
+    a = wave_sum(a) * (1.f / H);
+    bsum = wave_sum(bsum) * (1.f / H);
+#pragma unroll
+    for (int i = 0; i < E; ++i) dv[i] = rstd * (dv[i] - a - sv[i] * bsum);  // d s
+    store_e<E>(dx + off, dv);
+#pragma unroll
+    for (int i = 0; i < E; ++i)
+      dv[i] = (thresh == 0u || keep_elem(key, (uint64_t)(off + i), thresh)) ? dv[i] * scale : 0.f;
+    store_e<E>(dh + off, dv);
+  }
+  // block partials of dgamma / dbeta: [blk][2][H], waves summed in a fixed order
+  __shared__ float red[4][2][H];
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    red[wv][0][c0 + i] = pg[i];
+    red[wv][1][c0 + i] = pb[i];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < 2 * H; c += blockDim.x) {
+    const int which = c / H, col = c - which * H;
+    part[((int64_t)blockIdx.x * 2 + which) * H + col] =
+        (red[0][which][col] + red[1][which][col]) + (red[2][which][col] + red[3][which][col]);
+  }
+}
+
+// dgamma/dbeta[c] = sum over blocks of part[blk][which][c] -> bf16 (into the PS sink). Block =
+// 32 outputs x 8 partial-row lanes, combined in a fixed order (deterministic); one lane per output
+// walking all 256 partials was latency-bound at ~43 us.
+__global__ __launch_bounds__(256) void ln_param_grad_kernel(const float* __restrict__ part, int nblk, int H,
+                                                            uint16_t* __restrict__ dgamma, uint16_t* __restrict__ dbeta) {
+  const int cl = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const int t = blockIdx.x * 32 + cl;  // t = which * H + col
+  float s0 = 0.f;
+  if (t < 2 * H) {
+    const int which = t / H, col = t - which * H;
+    for (int b = rl; b < nblk; b += 8) s0 += part[((int64_t)b * 2 + which) * H + col];
+  }
+  __shared__ float red[8][33];
+  red[rl][cl] = s0;
+  __syncthreads();
+  if (rl != 0 || t >= 2 * H) return;
+#pragma unroll
+  for (int r = 1; r < 8; ++r) s0 += red[r][cl];
+  const int which = t / H, col = t - which * H;
+  (which ? dbeta : dgamma)[col] = f32_to_bf16(s0);
+}
+
+int ln_bwd_blocks(int64_t rows) {
+  const int64_t want = (rows + 4 * 8 - 1) / (4 * 8);  // >= 8 rows per wave
+  return (int)(want < 1 ? 1 : (want > 256 ? 256 : want));
+}
+
+bool ln_supported(int H) { return H == 768 || H == 1024; }
+
+static uint32_t keep_thresh(float p) {
+  if (p <= 0.f) return 0u;
+  const double t = (double)p * 4294967296.0;
+  return t >= 4294967295.0 ? 4294967295u : (uint32_t)t;
+}
+
+hipError_t launch_ln_fwd(const LnArgs& a, hipStream_t st) {
+  if (!ln_supported(a.H)) return hipErrorInvalidValue;
+  const int64_t blocks64 = (a.rows + 3) / 4;
+  const int blocks = (int)(blocks64 > 2048 ? 2048 : (blocks64 < 1 ? 1 : blocks64));
+  const uint32_t th = keep_thresh(a.p);
+  const float sc = a.p > 0.f ? 1.f / (1.f - a.p) : 1.f;
+#define PSD_LNF(E)                                                                                                  \
+  hipLaunchKernelGGL(ln_fwd_kernel<E>, dim3(blocks), dim3(256), 0, st, a.x, a.h, a.gamma, a.beta, a.y, a.s, a.mean, \
+                     a.rstd, a.rows, a.eps, a.seed, a.step, th, sc)
+  if (a.H == 768) PSD_LNF(12);
+  else PSD_LNF(16);
+#undef PSD_LNF
+  return hipGetLastError();
+}
+
+hipError_t launch_ln_bwd(const LnArgs& a, hipStream_t st) {
+  if (!ln_supported(a.H)) return hipErrorInvalidValue;
+  const int blocks = ln_bwd_blocks(a.rows);
+  const uint32_t th = keep_thresh(a.p);
+  const float sc = a.p > 0.f ? 1.f / (1.f - a.p) : 1.f;
+#define PSD_LNB(E)                                                                                                  \
+  hipLaunchKernelGGL(ln_bwd_kernel<E>, dim3(blocks), dim3(256), 0, st, a.dy, a.s, a.mean, a.rstd, a.gamma, a.dx, \
+                     a.dh, a.part, a.rows, a.seed, a.step, th, sc)
+  if (a.H == 768) PSD_LNB(12);
+  else PSD_LNB(16);
+#undef PSD_LNB
+  hipLaunchKernelGGL(ln_param_grad_kernel, dim3((2 * a.H + 31) / 32), dim3(256), 0, st, a.part, blocks, a.H,
+                     a.dgamma, a.dbeta);
+  return hipGetLastError();
+}
+
+}  // namespace psd

@@ -16,21 +16,23 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.layernorm import FusedAddLayerNorm, bump_step
 from ..ops.linear import MfmaLinear
 
 VOCAB = 30528
 
 
 class BertLayer(nn.Module):
-    def __init__(self, hidden=768, heads=12, ffn=3072, dropout=0.1):
+    def __init__(self, hidden=768, heads=12, ffn=3072, dropout=0.1, index=0):
         super().__init__()
         self.heads = heads
         self.qkv = MfmaLinear(hidden, 3 * hidden)
         self.proj = MfmaLinear(hidden, hidden)
-        self.ln1 = nn.LayerNorm(hidden, eps=1e-12)
+        # LayerNorm(x + dropout(branch)) as one fused kernel family (ops/layernorm.py)
+        self.ln1 = FusedAddLayerNorm(hidden, eps=1e-12, p=dropout, seed=2 * index + 1)
         self.ffn1 = MfmaLinear(hidden, ffn, act="gelu")
         self.ffn2 = MfmaLinear(ffn, hidden)
-        self.ln2 = nn.LayerNorm(hidden, eps=1e-12)
+        self.ln2 = FusedAddLayerNorm(hidden, eps=1e-12, p=dropout, seed=2 * index + 2)
         self.p = dropout
 
     def forward(self, x):
@@ -38,8 +40,8 @@ class BertLayer(nn.Module):
         q, k, v = self.qkv(x).view(B, S, 3, self.heads, H // self.heads).permute(2, 0, 3, 1, 4).unbind(0)
         a = F.scaled_dot_product_attention(q, k, v, dropout_p=self.p if self.training else 0.0)
         a = a.transpose(1, 2).reshape(B, S, H)
-        x = self.ln1(x + F.dropout(self.proj(a), self.p, self.training))
-        return self.ln2(x + F.dropout(self.ffn2(self.ffn1(x)), self.p, self.training))
+        x = self.ln1(x, self.proj(a))
+        return self.ln2(x, self.ffn2(self.ffn1(x)))
 
 
 class BertForMLM(nn.Module):
@@ -50,11 +52,13 @@ class BertForMLM(nn.Module):
         self.pos = nn.Embedding(max_pos, hidden)
         self.tok_type = nn.Embedding(2, hidden)
         self.ln = nn.LayerNorm(hidden, eps=1e-12)
-        self.layers = nn.ModuleList([BertLayer(hidden, heads, 4 * hidden, dropout) for _ in range(layers)])
+        self.layers = nn.ModuleList([BertLayer(hidden, heads, 4 * hidden, dropout, i) for i in range(layers)])
         self.head = MfmaLinear(hidden, hidden, act="gelu")
         self.head_ln = nn.LayerNorm(hidden, eps=1e-12)
         self.decoder = MfmaLinear(hidden, vocab)
         self.p = dropout
+        # device step counter for the fused LayerNorms' dropout masks (ops/layernorm.py)
+        self.register_buffer("_psd_rng_step", torch.zeros(1, dtype=torch.int64), persistent=False)
         for m in self.modules():
             if isinstance(m, nn.Linear):
                 nn.init.normal_(m.weight, std=0.02)
@@ -64,6 +68,7 @@ class BertForMLM(nn.Module):
 
     def forward(self, batch):
         ids, types, mlm_pos = batch
+        bump_step(self)
         S = ids.shape[1]
         pos = torch.arange(S, device=ids.device)
         x = self.word(ids) + self.pos(pos)[None] + self.tok_type(types)

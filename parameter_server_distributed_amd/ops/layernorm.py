@@ -1,0 +1,79 @@
+"""``LayerNorm(x + dropout(h))`` -- the transformer residual tail -- on the fused gfx950 kernels of
+``csrc/kernels/layernorm.hip`` (one pass forward, one pass backward + a tiny gamma/beta finalize).
+
+Dropout masks come from a counter-based hash of (per-site seed, device step counter, element), so
+they are regenerated in backward instead of stored, and a replayed hipGraph draws fresh masks each
+step: the owning model bumps the shared counter on the device at the start of every forward
+(``bump_step``). gamma/beta gradients go straight into the PS flat-gradient buffer when the data
+plane installed a grad sink (as the fused BN does).
+
+CPU tensors, other dtypes or hidden sizes use the composite ``F.layer_norm(x + F.dropout(h))`` --
+the reference the tests compare against.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import native
+
+
+class _AddLNFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, h, weight, bias, mod, p):
+        C = native()
+        shp = x.shape
+        y, s, mean, rstd = C.ln_fwd(x.contiguous(), h.contiguous(), weight, bias, mod.eps, p, mod.seed, mod.step)
+        ctx.mod, ctx.p = mod, p
+        ctx.save_for_backward(s, mean, rstd, weight)
+        return y.view(shp)
+
+    @staticmethod
+    def backward(ctx, dy):
+        s, mean, rstd, w = ctx.saved_tensors
+        mod = ctx.mod
+        sink = getattr(mod, "_psd_grad_sink", None)
+        dgo = dbo = None
+        if sink is not None:
+            dgo, dbo = sink(mod.weight), sink(mod.bias)
+        dx, dh, dg, db = native().ln_bwd(dy, s, mean, rstd, w, ctx.p, mod.seed, mod.step, dgo, dbo)
+        return dx.view(dy.shape), dh.view(dy.shape), dg, db, None, None
+
+
+class FusedAddLayerNorm(nn.LayerNorm):
+    """``nn.LayerNorm`` applied to ``x + dropout(h)`` in one fused kernel family on MI355X."""
+
+    def __init__(self, hidden: int, eps: float = 1e-12, p: float = 0.1, seed: int = 0):
+        super().__init__(hidden, eps=eps)
+        self.p = p
+        self.seed = int(seed) & 0x7FFFFFFF
+        self.step = None  # device int64 counter, set by the owning model (dropout masks per step)
+
+    def psd_direct_grad_params(self):
+        return [self.weight, self.bias]
+
+    def _kernel_ok(self, x, h) -> bool:
+        return (x.is_cuda and x.dtype == torch.bfloat16 and h.dtype == torch.bfloat16 and x.shape == h.shape
+                and x.shape[-1] in (768, 1024) and self.weight is not None and self.weight.dtype == torch.bfloat16)
+
+    def forward(self, x, h):
+        p = self.p if self.training else 0.0
+        if self._kernel_ok(x, h):
+            return _AddLNFn.apply(x, h, self.weight, self.bias, self, p)
+        return F.layer_norm(x + F.dropout(h, p, self.training), self.normalized_shape,
+                            None if self.weight is None else self.weight.to(x.dtype),
+                            None if self.bias is None else self.bias.to(x.dtype), self.eps)
+
+
+def bump_step(model: nn.Module) -> None:
+    """Advance the model's dropout step counter (a non-persistent int64 buffer ``_psd_rng_step``,
+    moved with the model) and point every FusedAddLayerNorm at it. Called at the start of each
+    training forward; the increment runs on the device, so a captured hipGraph replays it."""
+    step = getattr(model, "_psd_rng_step", None)
+    if step is None or not model.training:
+        return
+    for m in model.modules():
+        if isinstance(m, FusedAddLayerNorm):
+            m.step = step
+    step.add_(1)
