@@ -1,0 +1,327 @@
+// Fused multi-head self-attention for short sequences (BERT pre-training, S <= 128, head dim 64) on
+// gfx950, forward and backward, reading the packed QKV projection output [B, S, 3, H, 64] in place and
+// writing O as [B, S, H, 64] (the output projection's input, no transpose) and dQKV in the packed
+// layout (the QKV projection's dgrad input, no stack/cat).
+//
+// One workgroup per (batch, head), S/32 waves; the whole head (Q, K, V, dO: S x 64 bf16 each) lives
+// in LDS and every product is a v_mfma_f32_32x32x16_bf16:
+//   forward   S^T = K Q^T (keys x queries: the softmax reduction runs over a lane's own registers
+//             plus one lane^32 exchange), P = softmax, dropout, then O = P V with P staged through
+//             LDS; the row log-sum-exp is saved for backward.
+//   backward  wave w owns key block w: S^T and dP^T = V dO^T recomputed, dS = P (dP - rowsum(dO.O)),
+//             dV = Pd^T dO and dK = dS^T Q from transposed LDS reads (ds_read_b64_tr_b16); then
+//             wave w owns query block w: dQ = dS K.
+// Dropout keeps (b, h, q, key) from the same counter hash as the fused LayerNorm (seed, device step
+// counter), so the mask is regenerated in backward and a replayed hipGraph draws fresh masks.
+//
+// Replaces what the reference's stub gradient (src/worker.cpp:316-329) stands in for: the model's
+// real forward/backward; the attention is BERT's (BASELINE config 4).
+#include "common.h"
+#include "launchers_attn.h"
+
+namespace psd {
+
+namespace {
+
+typedef __bf16 abf16x8 __attribute__((ext_vector_type(8)));
+typedef short as16x4 __attribute__((ext_vector_type(4)));
+typedef float af32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) as16x4 alds_s16x4;
+
+constexpr int D = 64;                 // head dim
+constexpr int LDT = D + 8;            // Q/K/V/dO tile row stride (elements): 144 B
+
+__device__ __forceinline__ uint32_t amix32(uint32_t h) {  // murmur3 finalizer (as layernorm.hip)
+  h ^= h >> 16;
+  h *= 0x85ebca6bu;
+  h ^= h >> 13;
+  h *= 0xc2b2ae35u;
+  h ^= h >> 16;
+  return h;
+}
+__device__ __forceinline__ bool akeep(uint32_t key, uint64_t idx, uint32_t thresh) {
+  const uint32_t a = amix32(key ^ (uint32_t)idx * 0x9e3779b9u);
+  return amix32(a ^ (uint32_t)(idx >> 32) ^ 0x7f4a7c15u) >= thresh;
+}
+__device__ __forceinline__ uint32_t attn_key(uint32_t seed, const int64_t* step) {
+  return amix32(seed * 0x27d4eb2fu ^ (uint32_t)(step ? *step : 0) * 0x165667b1u);
+}
+
+// A/B fragment whose 8 k-values are contiguous in LDS: lane -> row r0 + lane%32, k = k0 + 8*(lane/32) + e
+__device__ __forceinline__ abf16x8 rowfrag(const uint8_t* base, int stride_b, int r0, int k0) {
+  const int lane = threadIdx.x & 63;
+  const u32x4 w = *reinterpret_cast<const u32x4*>(base + (r0 + (lane & 31)) * stride_b + (k0 + 8 * (lane >> 5)) * 2);
+  return __builtin_bit_cast(abf16x8, w);
+}
+// Same fragment from a [k][col] tile (col contiguous): ds_read_b64_tr_b16 transposes within 16 lanes.
+// lane -> col c0 + lane%32, k = k0 + 8*(lane/32) + e
+__device__ __forceinline__ abf16x8 trfrag(const uint8_t* base, int stride_b, int k0, int c0) {
+  const int lane = threadIdx.x & 63;
+  const int G = lane >> 4, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
+  const int k = k0 + 8 * (G >> 1) + q;
+  const int col = c0 + 16 * (G & 1) + 4 * p;
+  const as16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((alds_s16x4*)(base + k * stride_b + col * 2));
+  const as16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((alds_s16x4*)(base + (k + 4) * stride_b + col * 2));
+  as16x4 both[2] = {lo, hi};
+  return __builtin_bit_cast(abf16x8, both);
+}
+
+__device__ __forceinline__ af32x16 mfma(abf16x8 a, abf16x8 b, af32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ af32x16 zero16() {
+  af32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+// accumulator element i of a 32x32 tile: row (i&3) + 8*(i>>2) + 4*(lane/32), col lane%32
+__device__ __forceinline__ int acc_row(int i, int hh) { return (i & 3) + 8 * (i >> 2) + 4 * hh; }
+
+// rows [0, S) of a [.., S, 3, H, 64] (or [.., S, H, 64]) tensor -> LDS tile [S][LDT]
+__device__ __forceinline__ void stage_rows(uint8_t* lds, const uint16_t* src, int64_t row_stride, int S) {
+  for (int c = threadIdx.x; c < S * 8; c += blockDim.x) {
+    const int r = c >> 3, ch = c & 7;
+    *reinterpret_cast<u32x4*>(lds + r * LDT * 2 + ch * 16) =
+        *reinterpret_cast<const u32x4*>(src + (int64_t)r * row_stride + ch * 8);
+  }
+}
+
+}  // namespace
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnArgs a) {
+  constexpr int S = 32 * NW, LDP = S + 8;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* Ks = smem;
+  uint8_t* Vs = Ks + S * LDT * 2;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5;
+  uint8_t* Ps = Vs + S * LDT * 2 + w * 32 * LDP * 2;  // this wave's 32 query rows of P
+
+  const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;
+  const int HD = a.H * D;
+  const int64_t qkv_rs = 3 * (int64_t)HD;
+  const uint16_t* base = a.qkv + (int64_t)b * S * qkv_rs + h * D;
+  stage_rows(Ks, base + HD, qkv_rs, S);
+  stage_rows(Vs, base + 2 * HD, qkv_rs, S);
+  const int q0 = 32 * w, q = q0 + (lane & 31);
+  abf16x8 qf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+    qf[ks] = __builtin_bit_cast(abf16x8, *reinterpret_cast<const u32x4*>(base + (int64_t)q * qkv_rs + 16 * ks + 8 * hh));
+  __syncthreads();
+
+  af32x16 sc[NW];  // S^T tiles: lane owns query q, keys 32j + acc_row(i)
+#pragma unroll
+  for (int j = 0; j < NW; ++j) {
+    sc[j] = zero16();
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) sc[j] = mfma(rowfrag(Ks, LDT * 2, 32 * j, 16 * ks), qf[ks], sc[j]);
+  }
+  float m = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < NW; ++j)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m = fmaxf(m, sc[j][i]);
+  m = fmaxf(m, __shfl_xor(m, 32));
+  const float sl = a.scale * 1.4426950408889634f;
+  float l = 0.f;
+#pragma unroll
+  for (int j = 0; j < NW; ++j)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      sc[j][i] = exp2f((sc[j][i] - m) * sl);
+      l += sc[j][i];
+    }
+  l += __shfl_xor(l, 32);
+  if (hh == 0) a.lse[(int64_t)bh * S + q] = m * a.scale + logf(l);
+  const float inv = 1.f / l;
+  const uint32_t key = attn_key(a.seed, a.step);
+  const bool drop = a.thresh != 0u;
+  const uint64_t rowidx = ((uint64_t)bh * S + q) * S;
+#pragma unroll
+  for (int j = 0; j < NW; ++j)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int kk = 32 * j + 8 * g + 4 * hh + e;
+        v[e] = sc[j][4 * g + e] * inv;
+        if (drop) v[e] = akeep(key, rowidx + kk, a.thresh) ? v[e] * a.rescale : 0.f;
+      }
+      *reinterpret_cast<uint2*>(Ps + (lane & 31) * LDP * 2 + (32 * j + 8 * g + 4 * hh) * 2) =
+          make_uint2(pack_bf16x2_rne(v[0], v[1]), pack_bf16x2_rne(v[2], v[3]));
+    }
+  __syncthreads();
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt) {
+    af32x16 o = zero16();
+#pragma unroll
+    for (int ks = 0; ks < S / 16; ++ks) o = mfma(rowfrag(Ps, LDP * 2, 0, 16 * ks), trfrag(Vs, LDT * 2, 16 * ks, 32 * dt), o);
+    uint16_t* out = a.o + ((int64_t)b * S) * HD + h * D + 32 * dt + (lane & 31);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) out[(int64_t)(q0 + acc_row(i, hh)) * HD] = f32_to_bf16(o[i]);
+  }
+}
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a) {
+  constexpr int S = 32 * NW, LDP = S + 8;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* Qs = smem;
+  uint8_t* Ks = Qs + S * LDT * 2;
+  uint8_t* Vs = Ks + S * LDT * 2;
+  uint8_t* dOs = Vs + S * LDT * 2;
+  uint8_t* Pd = dOs + S * LDT * 2;  // dropped, rescaled probabilities [q][key]
+  uint8_t* dS = Pd + S * LDP * 2;   // dS = P (dP - D) [q][key]
+  float* lse_s = reinterpret_cast<float*>(dS + S * LDP * 2);
+  float* D_s = lse_s + S;
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5;
+  const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;
+  const int HD = a.H * D;
+  const int64_t qkv_rs = 3 * (int64_t)HD;
+  const uint16_t* base = a.qkv + (int64_t)b * S * qkv_rs + h * D;
+  const int64_t ob = (int64_t)b * S * HD + h * D;
+  stage_rows(Qs, base, qkv_rs, S);
+  stage_rows(Ks, base + HD, qkv_rs, S);
+  stage_rows(Vs, base + 2 * HD, qkv_rs, S);
+  stage_rows(dOs, a.dout + ob, HD, S);
+  for (int r = threadIdx.x; r < S; r += blockDim.x) lse_s[r] = a.lse[(int64_t)bh * S + r];
+  // D[q] = sum_d dO[q, d] O[q, d]: 8 lanes per row, 8 elements each
+  for (int c = threadIdx.x; c < S * 8; c += blockDim.x) {
+    const int r = c >> 3, ch = c & 7;
+    float x[8], y[8];
+    load8_bf16(a.dout + ob + (int64_t)r * HD + ch * 8, x);
+    load8_bf16(a.o + ob + (int64_t)r * HD + ch * 8, y);
+    float s = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += x[e] * y[e];
+    s += __shfl_xor(s, 1);
+    s += __shfl_xor(s, 2);
+    s += __shfl_xor(s, 4);
+    if (ch == 0) D_s[r] = s;
+  }
+  __syncthreads();
+
+  // phase 1: wave w owns keys k0..k0+31; recompute S^T and dP^T against every query block
+  const int k0 = 32 * w;
+  abf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    kf[ks] = rowfrag(Ks, LDT * 2, k0, 16 * ks);
+    vf[ks] = rowfrag(Vs, LDT * 2, k0, 16 * ks);
+  }
+  const uint32_t key = attn_key(a.seed, a.step);
+  const bool drop = a.thresh != 0u;
+  const float sl = a.scale * 1.4426950408889634f;
+#pragma unroll
+  for (int t = 0; t < NW; ++t) {
+    af32x16 st = zero16(), dpt = zero16();
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      st = mfma(kf[ks], rowfrag(Qs, LDT * 2, 32 * t, 16 * ks), st);
+      dpt = mfma(vf[ks], rowfrag(dOs, LDT * 2, 32 * t, 16 * ks), dpt);
+    }
+    const int q = 32 * t + (lane & 31);
+    const float lse2 = lse_s[q] * 1.4426950408889634f, Dq = D_s[q];
+    const uint64_t rowidx = ((uint64_t)bh * S + q) * S;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      float pv[4], dv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int i = 4 * g + e;
+        const float p = exp2f(st[i] * sl - lse2);
+        float pd = p, dp = dpt[i];
+        if (drop) {
+          const bool kp = akeep(key, rowidx + k0 + 8 * g + 4 * hh + e, a.thresh);
+          pd = kp ? p * a.rescale : 0.f;
+          dp = kp ? dp * a.rescale : 0.f;
+        }
+        pv[e] = pd;
+        dv[e] = p * (dp - Dq);
+      }
+      const int off = q * LDP * 2 + (k0 + 8 * g + 4 * hh) * 2;
+      *reinterpret_cast<uint2*>(Pd + off) = make_uint2(pack_bf16x2_rne(pv[0], pv[1]), pack_bf16x2_rne(pv[2], pv[3]));
+      *reinterpret_cast<uint2*>(dS + off) = make_uint2(pack_bf16x2_rne(dv[0], dv[1]), pack_bf16x2_rne(dv[2], dv[3]));
+    }
+  }
+  __syncthreads();
+
+  // phase 2: dV[key, d] = sum_q Pd[q, key] dO[q, d];  dK = scale * sum_q dS[q, key] Q[q, d]
+  uint16_t* dq_base = a.dqkv + (int64_t)b * S * qkv_rs + h * D;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt) {
+    af32x16 dv = zero16(), dk = zero16();
+#pragma unroll
+    for (int ks = 0; ks < S / 16; ++ks) {
+      dv = mfma(trfrag(Pd, LDP * 2, 16 * ks, k0), trfrag(dOs, LDT * 2, 16 * ks, 32 * dt), dv);
+      dk = mfma(trfrag(dS, LDP * 2, 16 * ks, k0), trfrag(Qs, LDT * 2, 16 * ks, 32 * dt), dk);
+    }
+    const int d = 32 * dt + (lane & 31);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int64_t r = (int64_t)(k0 + acc_row(i, hh)) * qkv_rs + d;
+      dq_base[r + HD] = f32_to_bf16(dk[i] * a.scale);
+      dq_base[r + 2 * HD] = f32_to_bf16(dv[i]);
+    }
+  }
+  // phase 3: wave w owns queries q0..q0+31: dQ = scale * dS K
+  const int q0 = 32 * w;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt) {
+    af32x16 dq = zero16();
+#pragma unroll
+    for (int ks = 0; ks < S / 16; ++ks) dq = mfma(rowfrag(dS, LDP * 2, q0, 16 * ks), trfrag(Ks, LDT * 2, 16 * ks, 32 * dt), dq);
+    const int d = 32 * dt + (lane & 31);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dq_base[(int64_t)(q0 + acc_row(i, hh)) * qkv_rs + d] = f32_to_bf16(dq[i] * a.scale);
+  }
+}
+
+bool attn_supported(int S, int head_dim) { return head_dim == D && S >= 32 && S <= 128 && S % 32 == 0; }
+
+static int fwd_lds(int S) { return 2 * S * LDT * 2 + S * (S + 8) * 2; }
+static int bwd_lds(int S) { return 4 * S * LDT * 2 + 2 * S * (S + 8) * 2 + 2 * S * 4; }
+
+template <int NW>
+static hipError_t launch_fwd_t(const AttnArgs& a, hipStream_t st) {
+  const int lds = fwd_lds(32 * NW);
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_fwd_kernel<NW>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(attn_fwd_kernel<NW>, dim3(a.B * a.H), dim3(64 * NW), lds, st, a);
+  return hipGetLastError();
+}
+template <int NW>
+static hipError_t launch_bwd_t(const AttnArgs& a, hipStream_t st) {
+  const int lds = bwd_lds(32 * NW);
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd_kernel<NW>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(attn_bwd_kernel<NW>, dim3(a.B * a.H), dim3(64 * NW), lds, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_attn_fwd(const AttnArgs& a, hipStream_t st) {
+  if (!attn_supported(a.S, D)) return hipErrorInvalidValue;
+  switch (a.S / 32) {
+    case 1: return launch_fwd_t<1>(a, st);
+    case 2: return launch_fwd_t<2>(a, st);
+    case 3: return launch_fwd_t<3>(a, st);
+    default: return launch_fwd_t<4>(a, st);
+  }
+}
+hipError_t launch_attn_bwd(const AttnArgs& a, hipStream_t st) {
+  if (!attn_supported(a.S, D)) return hipErrorInvalidValue;
+  switch (a.S / 32) {
+    case 1: return launch_bwd_t<1>(a, st);
+    case 2: return launch_bwd_t<2>(a, st);
+    case 3: return launch_bwd_t<3>(a, st);
+    default: return launch_bwd_t<4>(a, st);
+  }
+}
+
+}  // namespace psd

@@ -2,7 +2,7 @@
 config 4 (BERT-base with the Adam update kernel). Random init, synthetic token batches.
 
 Every Linear is an ``MfmaLinear`` (hand-written gfx950 MFMA GEMM forward + both backward GEMMs,
-bias/GELU fused); attention is ``F.scaled_dot_product_attention`` (ROCm flash attention).
+bias/GELU fused); attention is the fused gfx950 kernel of ``ops/attention.py`` (SDPA off-GPU).
 Deviations from the original BERT, both standard in large-scale training and stated here: the
 vocabulary is padded to 30528 (a multiple of 64, for the GEMM tiles) and the MLM decoder weight is
 untied from the word embedding (the PS data plane overlaps each bucket's update with the rest of
@@ -16,6 +16,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.attention import FusedSelfAttention
 from ..ops.layernorm import FusedAddLayerNorm, bump_step
 from ..ops.linear import MfmaLinear
 
@@ -27,6 +28,8 @@ class BertLayer(nn.Module):
         super().__init__()
         self.heads = heads
         self.qkv = MfmaLinear(hidden, 3 * hidden)
+        # packed QKV in, [B, S, hidden] out: one fused kernel per direction (ops/attention.py)
+        self.attn = FusedSelfAttention(heads, p=dropout, seed=1000 + index)
         self.proj = MfmaLinear(hidden, hidden)
         # LayerNorm(x + dropout(branch)) as one fused kernel family (ops/layernorm.py)
         self.ln1 = FusedAddLayerNorm(hidden, eps=1e-12, p=dropout, seed=2 * index + 1)
@@ -36,11 +39,7 @@ class BertLayer(nn.Module):
         self.p = dropout
 
     def forward(self, x):
-        B, S, H = x.shape
-        q, k, v = self.qkv(x).view(B, S, 3, self.heads, H // self.heads).permute(2, 0, 3, 1, 4).unbind(0)
-        a = F.scaled_dot_product_attention(q, k, v, dropout_p=self.p if self.training else 0.0)
-        a = a.transpose(1, 2).reshape(B, S, H)
-        x = self.ln1(x, self.proj(a))
+        x = self.ln1(x, self.proj(self.attn(self.qkv(x))))
         return self.ln2(x, self.ffn2(self.ffn1(x)))
 
 
