@@ -27,6 +27,8 @@ import time
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 from parameter_server_distributed_amd.utils import miopen as _miopen  # noqa: E402
 
+from parameter_server_distributed_amd.utils import tunableop as _tunableop  # noqa: E402
+
 _miopen.install()  # shipped gfx950 find-db + kernel cache (before torch initialises MIOpen)
 
 import torch  # noqa: E402
@@ -75,6 +77,10 @@ def parse():
     # MIOpen immediate mode by default: solutions come from the shipped find-db / heuristics with no
     # per-shape Find (warmup ~1 s instead of ~2-4 min per rank; measured 1-2 % slower steps)
     ap.add_argument("--benchmark-miopen", type=int, default=0, help="torch.backends.cudnn.benchmark (MIOpen Find)")
+    ap.add_argument("--tunableop", default="auto", choices=["auto", "off", "tune"],
+                    help="library GEMM solution choice: shipped TunableOp results (auto), heuristic (off), "
+                         "or time every hipBLASLt/rocBLAS solution per shape (tune; see --tunableop-out)")
+    ap.add_argument("--tunableop-out", default="", help="tune mode: write the TunableOp results here")
     ap.add_argument("--out", default="", help="also write the JSON line to this file")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N > 1: nccl (= RCCL, the data plane) or gloo (rehearsal of the "
@@ -112,6 +118,7 @@ def main():
         else:
             dist.init_process_group("gloo")
     torch.backends.cudnn.benchmark = bool(a.benchmark_miopen)
+    tunable_mode = _tunableop.install(a.tunableop)
     torch.manual_seed(1234)  # identical init on every rank; the PS init pull makes it exact
 
     a.model = a.model.lower().replace("-", "_")
@@ -208,7 +215,7 @@ def main():
                                       + ("-disjoint" if kw else ""),
                        "ps_shards": shards, "ps_owner_ranks": ps.owners, "worker_ranks": ps.worker_ranks,
                        "staleness_bound": a.staleness, "optimizer": f"{opt_kind} fused gfx950", "bucket_mb": a.bucket_mb,
-                       "pull_dtype": pull_dtype,
+                       "pull_dtype": pull_dtype, "tunableop": tunable_mode,
                        "transport": transport.name, "hipgraph": bool(tr.graphs), "graph_error": tr.graph_error},
             "staleness_p50": p50, "staleness_hist": hist, "final_loss": round(final_loss, 4),
             "warmup_s": round(t_w, 2), "peak_mem_gb": round(mem_peak / 2**30, 2),
@@ -218,6 +225,8 @@ def main():
         if a.out:
             with open(a.out, "w") as f:
                 f.write(line + "\n")
+    if tunable_mode == "tune" and a.tunableop_out:
+        _tunableop.dump(a.tunableop_out if world == 1 else f"{a.tunableop_out}.{rank}")
     if tracer is not None:
         tracer.close()
     if world > 1:
