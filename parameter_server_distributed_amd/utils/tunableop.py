@@ -36,7 +36,13 @@ def install(mode: str = "auto", path: str | None = None) -> str:
         return "tune"
     tn.tuning_enable(False)
     tn.record_untuned_enable(False)
-    tn.read_file(path or SHIPPED)
+    try:
+        ok = tn.read_file(path or SHIPPED)
+    except Exception:  # unreadable / other library versions: keep the library heuristic
+        ok = False
+    if ok is False:
+        tn.enable(False)
+        return "off"
     return "use"
 
 
