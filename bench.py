@@ -52,7 +52,7 @@ METRICS = {
 # samples/s per worker GPU. vs_baseline divides by this x n_workers, i.e. it credits the reference
 # with perfect scaling (its single PS would in fact serialize N workers).
 REF_BASELINE = {"resnet50": 285.119}
-DEFAULT_BATCH = {"resnet50": 1024, "bert_base": 64, "wide_resnet101_2": 128, "resnet101": 256, "mlp": 4096}
+DEFAULT_BATCH = {"resnet50": 1024, "bert_base": 256, "wide_resnet101_2": 512, "resnet101": 256, "mlp": 4096}
 
 
 def parse():
