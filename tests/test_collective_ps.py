@@ -89,6 +89,20 @@ def test_gloo_world2_matches_reference(tmp_path, shards, stale):
 
 
 @pytest.mark.slow
+@pytest.mark.parametrize("world", [4, 8])
+def test_gloo_bench_layout_2_shards_async(tmp_path, world):
+    """The driver's scaling layout (bench.py defaults at N = 4 / 8): 2 PS shards colocated on
+    ranks 0 and N/2, every rank a worker, staleness bound 1, reduce/broadcast push/pull."""
+    out = str(tmp_path / "r0.pt")
+    mp.spawn(_worker, args=(world, _port(), 2, 1, out, False, "reduce"), nprocs=world, join=True)
+    got = torch.load(out, weights_only=True)
+    want = _reference(world, 1)
+    for n in want:
+        torch.testing.assert_close(got["params"][n], want[n], rtol=1e-5, atol=1e-6, msg=n)
+    assert sum(got["hist"]) == STEPS - 1 and got["hist"][1] >= 1
+
+
+@pytest.mark.slow
 def test_gloo_disjoint_placement_2_workers_2_ps(tmp_path):
     """BASELINE config 4 layout in miniature: PS shards on ranks that do no compute."""
     out = str(tmp_path / "r0.pt")
