@@ -199,6 +199,15 @@ def main():
     while hist and hist[-1] == 0 and len(hist) > 1:
         hist.pop()
     final_loss = float(loss.float().item()) if loss is not None else float("nan")
+    # health of the run: a silent NaN in the weights invalidates a throughput number (round-1 lesson:
+    # a bad library GEMM produced NaN weights that a ReLU hid behind a finite loss)
+    finite = torch.tensor([float(bool(torch.isfinite(ps.params_flat).all())) and float(final_loss == final_loss)],
+                          device=dev)
+    if world > 1:
+        dist.all_reduce(finite, op=dist.ReduceOp.MIN)
+    params_finite = bool(finite.item() > 0)
+    if not params_finite and rank == 0:
+        print("WARNING: non-finite weights or loss at the end of the timed steps", file=sys.stderr, flush=True)
     if rank == 0:
         metric, unit = METRICS.get(a.model, (f"samples/sec (whole node) {a.model}", "samples/s"))
         data = ("synthetic (random token ids, 15% MLM labels, random init)" if a.model.startswith("bert") else
@@ -218,6 +227,7 @@ def main():
                        "pull_dtype": pull_dtype, "tunableop": tunable_mode,
                        "transport": transport.name, "hipgraph": bool(tr.graphs), "graph_error": tr.graph_error},
             "staleness_p50": p50, "staleness_hist": hist, "final_loss": round(final_loss, 4),
+            "params_finite": params_finite,
             "warmup_s": round(t_w, 2), "peak_mem_gb": round(mem_peak / 2**30, 2),
         }
         line = json.dumps(rec)

@@ -218,7 +218,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
     for (int j = 0; j < 8; ++j) {
       float o = fmaf(t[j], sc[j], sh[j]);
       if (RES) o += rr[j];
-      if (RELU) o = fmaxf(o, 0.f);
+      if (RELU) o = relu_nan(o);
       t[j] = o;
     }
     store8_bf16(y + v * 8, t);
@@ -427,7 +427,7 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(const uint16_t* __
     uint8_t bi[8];
     maxpool3s2_max8(
         x, n, ho, wo, c8, H, W, C,
-        [&](float v, int e) { return bf16_to_f32(f32_to_bf16(fmaxf(fmaf(v, sc[e], sh[e]), 0.f))); }, best, bi);
+        [&](float v, int e) { return bf16_to_f32(f32_to_bf16(relu_nan(fmaf(v, sc[e], sh[e])))); }, best, bi);
     store8_bf16(y + t * 8, best);
     store_argmax8(arg + t * 8, bi);
   }

@@ -24,6 +24,11 @@ __device__ __forceinline__ uint32_t pack_bf16x2_rne(float lo, float hi) {
   return __builtin_bit_cast(uint32_t, v);
 }
 
+// ReLU with torch semantics: NaN propagates (relu(NaN) = NaN). fmaxf(x, 0) would return 0 for a
+// NaN input and silently hide an upstream fault (a bad library GEMM once fed NaN into a BN whose
+// fmaxf ReLU turned it into zeros: the step "trained" with NaN weights and a finite loss).
+__device__ __forceinline__ float relu_nan(float x) { return x < 0.f ? 0.f : x; }
+
 // 8 consecutive elements <-> registers, one 16-byte (bf16) or two 16-byte (fp32) loads per lane.
 __device__ __forceinline__ void load8_f32(const float* p, float v[8]) {
   f32x4 a = *reinterpret_cast<const f32x4*>(p);

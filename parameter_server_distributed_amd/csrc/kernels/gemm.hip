@@ -222,7 +222,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
           const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
           if (m >= g.M) continue;
           float v = acc[i][j][r] + bias;
-          if (g.act == 1) v = fmaxf(v, 0.f);
+          if (g.act == 1) v = relu_nan(v);
           else if (g.act == 2) v = gelu_tanh(v);
           reinterpret_cast<float*>(g.C)[(int64_t)m * g.ldc + n] = v;
         }
@@ -247,7 +247,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
         float v = acc[i][j][r] + bias;
         if (g.act == 2 && g.aux && n < g.N && m0 + ml < g.M)
           reinterpret_cast<uint16_t*>(g.aux)[(int64_t)(m0 + ml) * g.ldc + n] = f32_to_bf16(v);
-        if (g.act == 1) v = fmaxf(v, 0.f);
+        if (g.act == 1) v = relu_nan(v);
         else if (g.act == 2) v = gelu_tanh(v);
         cs[ml * LDC + nl] = f32_to_bf16(v);
       }
@@ -329,7 +329,7 @@ __device__ __forceinline__ void big_epilogue(const GemmArgs& g, f32x16 (&acc)[4]
             reinterpret_cast<float*>(g.C)[(int64_t)blockIdx.z * g.M * g.N + (int64_t)m * g.N + n] = acc[i][j][r];
           } else {
             float v = acc[i][j][r] + bias;
-            if (g.act == 1) v = fmaxf(v, 0.f);
+            if (g.act == 1) v = relu_nan(v);
             else if (g.act == 2) v = gelu_tanh(v);
             reinterpret_cast<float*>(g.C)[(int64_t)m * g.ldc + n] = v;
           }
@@ -351,7 +351,7 @@ __device__ __forceinline__ void big_epilogue(const GemmArgs& g, f32x16 (&acc)[4]
         float v = acc[i][j][r] + bias;
         if (g.act == 2 && g.aux && n < g.N && m0 + ml < g.M)
           reinterpret_cast<uint16_t*>(g.aux)[(int64_t)(m0 + ml) * g.ldc + n] = f32_to_bf16(v);
-        if (g.act == 1) v = fmaxf(v, 0.f);
+        if (g.act == 1) v = relu_nan(v);
         else if (g.act == 2) v = gelu_tanh(v);
         cs[ml * kBigLdc + nl] = f32_to_bf16(v);
       }
@@ -887,7 +887,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
             o = reinterpret_cast<float*>(g.C) + (int64_t)blockIdx.z * g.M * g.N + (int64_t)m * g.N + n;
           } else {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) w[e] = g.act == 1 ? fmaxf(w[e], 0.f) : (g.act == 2 ? gelu_tanh(w[e]) : w[e]);
+            for (int e = 0; e < 4; ++e) w[e] = g.act == 1 ? relu_nan(w[e]) : (g.act == 2 ? gelu_tanh(w[e]) : w[e]);
             o = reinterpret_cast<float*>(g.C) + (int64_t)m * g.ldc + n;
           }
           if (n + 4 <= g.N && (reinterpret_cast<uintptr_t>(o) & 15) == 0)
@@ -919,7 +919,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
             for (int e = 0; e < 4 && n + e < g.N; ++e) ax[e] = f32_to_bf16(w[e]);
         }
 #pragma unroll
-        for (int e = 0; e < 4; ++e) w[e] = g.act == 1 ? fmaxf(w[e], 0.f) : (g.act == 2 ? gelu_tanh(w[e]) : w[e]);
+        for (int e = 0; e < 4; ++e) w[e] = g.act == 1 ? relu_nan(w[e]) : (g.act == 2 ? gelu_tanh(w[e]) : w[e]);
         *reinterpret_cast<uint2*>(cs + ml * kBigLdc + nl) = uint2{pack_bf16x2(w[0], w[1]), pack_bf16x2(w[2], w[3])};
       }
     }

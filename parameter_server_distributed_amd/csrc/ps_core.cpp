@@ -186,6 +186,17 @@ PushResult PSCore::push(int32_t wid, int32_t iteration, const std::vector<std::s
   }
 
   if (cfg_.async_mode) {
+    // apply-on-arrival is not idempotent: a client retry of a push the server already applied
+    // (its deadline expired after the apply) must not apply the gradient twice
+    auto ck = clock_.find(wid);
+    if (ck != clock_.end() && iteration < ck->second) {
+      ctr_["duplicates"] += 1;
+      r.success = true;
+      r.aggregation_complete = true;
+      r.version = version_;
+      r.message = "duplicate push ignored: iteration already applied";
+      return r;
+    }
     const int32_t s = take_slot_locked();
     fill_slot_locked(slots_[s], names, grads);
     int64_t base = pulled_version >= 0 ? pulled_version

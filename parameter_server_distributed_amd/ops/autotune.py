@@ -5,6 +5,14 @@ hand-written gfx950 kernel and a library path (hipBLASLt / MIOpen) for the same 
 eager call of a shape times every candidate (one warm call + 3 timed), caches the fastest and
 uses it from then on. Inside a hipGraph capture nothing is timed: an undecided shape takes the
 ``default`` candidate (the Trainer always runs eager warmup steps before it captures).
+
+Like MIOpen's Find, a candidate must also be *correct* to be chosen: the outputs of its warm call
+and of its last timed call are compared with the default candidate's (finite wherever the default
+is finite, max |diff| <= 5 % of max |ref|). A library solution that returns garbage is dropped.
+This is not hypothetical: the hipBLASLt solution TunableOp had recorded for ResNet-50's
+layer1 conv3 forward (``tn_256_3211264_64``, b1024) returned NaN/garbage rows, the timing-based
+choice picked it on some runs, and the BN ReLU turned the NaN into zeros so the step kept a
+finite loss on broken weights (tools/rank_check.py, tools/gemm_nan_probe.py; README).
 """
 from __future__ import annotations
 
@@ -19,19 +27,53 @@ def enabled(var: str) -> bool:
     return os.environ.get(var, "1") != "0"
 
 
-def _time_ms(fn, reps: int = 3) -> float:
-    fn()  # warm (library heuristics / kernel load)
+_REJECTED: dict[tuple, list] = {}
+
+
+def _snap(out, probe):
+    if out is None and probe is not None:
+        out = probe()
+    return out.detach().float().clone() if isinstance(out, torch.Tensor) else None
+
+
+def _time_ms(fn, reps: int = 3, probe=None):
+    """(ms per call, [output of the warm call, output of the last timed call])."""
+    outs = [_snap(fn(), probe)]  # warm (library heuristics / kernel load)
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
+    last = None
     for _ in range(reps):
-        fn()
+        last = fn()
     e.record()
     e.synchronize()
-    return s.elapsed_time(e) / reps
+    outs.append(_snap(last, probe))
+    return s.elapsed_time(e) / reps, outs
 
 
-def choose(key: tuple, candidates: dict, default: str) -> str:
-    """Name of the fastest candidate for ``key`` (timed once, cached)."""
+def _agrees(outs: list, ref: list) -> bool:
+    for o, r in zip(outs, ref):
+        if o is None or r is None:
+            continue
+        if o.shape != r.shape:
+            return False
+        fin = torch.isfinite(r)
+        if not bool(torch.isfinite(o)[fin].all()):
+            return False
+        d = (o[fin] - r[fin]).abs().max() if bool(fin.any()) else torch.zeros(())
+        if float(d) > 0.05 * float(r[fin].abs().max() if bool(fin.any()) else 0.0) + 1e-2:
+            return False
+    return True
+
+
+def rejected() -> dict:
+    """Candidates dropped for wrong output, per key (for logs / tests)."""
+    return dict(_REJECTED)
+
+
+def choose(key: tuple, candidates: dict, default: str, probe=None) -> str:
+    """Name of the fastest *correct* candidate for ``key`` (timed and validated once, cached).
+    ``probe``: returns the output tensor of a candidate that writes into a preallocated buffer
+    instead of returning its result."""
     got = _DECISIONS.get(key)
     if got is not None:
         return got
@@ -41,8 +83,19 @@ def choose(key: tuple, candidates: dict, default: str) -> str:
         return forced
     if torch.cuda.is_current_stream_capturing():
         return default
-    times = {name: _time_ms(fn) for name, fn in candidates.items()}
-    best = min(times, key=times.get)
+    runs = {name: _time_ms(fn, probe=probe) for name, fn in candidates.items()}
+    ref_name = default if default in runs else next(iter(runs))
+    ref = runs[ref_name][1]
+    if any(o is not None and not bool(torch.isfinite(o).all()) for o in ref):
+        # the default itself misbehaves: judge against any candidate with a finite output
+        ref_name = next((n for n, r in runs.items() if all(o is None or bool(torch.isfinite(o).all())
+                                                           for o in r[1])), ref_name)
+        ref = runs[ref_name][1]
+    ok = {n: r[0] for n, r in runs.items() if n == ref_name or _agrees(r[1], ref)}
+    bad = [n for n in runs if n not in ok]
+    if bad:
+        _REJECTED[key] = bad
+    best = min(ok, key=ok.get)
     _DECISIONS[key] = best
     return best
 

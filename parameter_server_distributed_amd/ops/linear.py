@@ -38,11 +38,13 @@ def _ok(x: torch.Tensor, w: torch.Tensor) -> bool:
             and w.shape[1] % 8 == 0)
 
 
-def _route(key: tuple, mfma, blas):
-    """The faster of the MFMA kernel and hipBLASLt for this GEMM shape (ops/autotune.py)."""
+def _route(key: tuple, mfma, blas, out: torch.Tensor | None = None):
+    """The faster of the MFMA kernel and hipBLASLt for this GEMM shape (ops/autotune.py); ``out``
+    is the buffer both candidates write (validated against each other on the first call)."""
     if not _at.enabled("PSD_LINEAR_TUNE"):
         return mfma
-    return mfma if _at.choose(("linear",) + key, {"mfma": mfma, "blas": blas}, "mfma") == "mfma" else blas
+    probe = (lambda: out) if out is not None else None
+    return mfma if _at.choose(("linear",) + key, {"mfma": mfma, "blas": blas}, "mfma", probe) == "mfma" else blas
 
 
 class _LinearFn(torch.autograd.Function):
@@ -76,7 +78,7 @@ class _LinearFn(torch.autograd.Function):
                 elif act == 2:
                     torch.ops.aten.gelu.out(aux, approximate="tanh", out=y)
 
-            _route(("fwd", M, x2.shape[1], N, act, bias is not None), mfma, blas)()
+            _route(("fwd", M, x2.shape[1], N, act, bias is not None), mfma, blas, y)()
         ctx.act = act
         ctx.mod = mod
         ctx.has_bias = bias is not None
@@ -98,7 +100,7 @@ class _LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.empty(x2.shape, dtype=dy2.dtype, device=dy2.device)
             _route(("dgrad", M, K, N), lambda: C.gemm_(dy2, w, True, False, dx),
-                   lambda: torch.mm(dy2, w, out=dx))()
+                   lambda: torch.mm(dy2, w, out=dx), dx)()
             dx = dx.view(ctx.in_shape)
         sink = getattr(ctx.mod, "_psd_grad_sink", None)
         dw = db = None
@@ -107,7 +109,7 @@ class _LinearFn(torch.autograd.Function):
             if dw is None:
                 dw = torch.empty(w.shape, dtype=w.dtype, device=w.device)
             _route(("wgrad", M, K, N), lambda: C.gemm_splitk_(dy2, x2, False, False, dw, False, 1.0, 0),
-                   lambda: torch.mm(dy2.t(), x2, out=dw))()
+                   lambda: torch.mm(dy2.t(), x2, out=dw), dw)()
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = sink(ctx.mod.bias) if sink is not None else None
             if db is None:

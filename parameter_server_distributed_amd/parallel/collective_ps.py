@@ -490,12 +490,16 @@ class CollectivePS:
         for dst, src in zip(self.slots, sd.get("slots") or []):
             dst.copy_(src)
         self.step_idx = int(sd["step_idx"])
-        # re-publish the working copy from the masters
+        # re-publish the working copy from the masters (fp8 pull: re-quantise the owned slices,
+        # the published fp8 buffers still hold the pre-load weights)
         for b in self.buckets:
             for j, k in enumerate(self.my_shards):
                 lo = b.local_offset + j * b.slice_numel
-                self.params_flat.narrow(0, b.offset + k * b.slice_numel, b.slice_numel).copy_(
-                    self.master.narrow(0, lo, b.slice_numel))
+                m = self.master.narrow(0, lo, b.slice_numel)
+                if self.pull_fp8:
+                    self._quant_slice(b, k, m)
+                else:
+                    self.params_flat.narrow(0, b.offset + k * b.slice_numel, b.slice_numel).copy_(m)
         for b in self.buckets:
             self._pull(b)
 
@@ -521,14 +525,26 @@ class CollectivePS:
         tensors = [self.master, self.dyn.t] + [t for t in (self.state1, self.state2) if t is not None] \
             + list(self.slots)
         if self.is_cuda:
+            # Snapshot on the current stream first (HBM->HBM, ~50 us for ResNet-50's state): the
+            # next step's fused apply (comm stream, or the replayed graph on this stream) is
+            # ordered after it, so the file holds exactly this step. The slow device->host copy
+            # then reads the snapshot on a side stream while training continues.
+            cur = torch.cuda.current_stream(self.device)
+            if getattr(self, "_ckpt_done", None) is not None:
+                cur.wait_event(self._ckpt_done)  # the previous D2H still reads the snapshot
+            if getattr(self, "_ckpt_snap", None) is None or len(self._ckpt_snap) != len(tensors):
+                self._ckpt_snap = [torch.empty_like(t) for t in tensors]
+            for s, t in zip(self._ckpt_snap, tensors):
+                s.copy_(t)
             side = torch.cuda.Stream(device=self.device)
-            side.wait_stream(torch.cuda.current_stream(self.device))
+            side.wait_stream(cur)
             with torch.cuda.stream(side):
                 host = [torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for t in tensors]
-                for h, t in zip(host, tensors):
-                    h.copy_(t, non_blocking=True)
+                for h, s in zip(host, self._ckpt_snap):
+                    h.copy_(s, non_blocking=True)
             done = torch.cuda.Event()
             done.record(side)
+            self._ckpt_done = done
         else:
             host = [t.detach().clone() for t in tensors]
             done = None

@@ -210,3 +210,52 @@ def test_sharded_checkpoint_resume_is_exact(tmp_path, C):
         torch.testing.assert_close(a[n], b[n], rtol=0, atol=0, msg=n)
     epoch, it, names, shapes, _, data = C.load_reference_ckpt(prefix + ".ref.ckpt")
     assert (epoch, it) == (1, 2) and "fc1.weight" in names
+
+
+def _fp8_run(prefix, phase):
+    torch.manual_seed(0)
+    spec = models.build("mlp", torch.device("cpu"), torch.bfloat16, hidden=64)
+    ps = CollectivePS(spec.model, OptimConfig(**CFG), staleness=1, bucket_mb=0.0005, pull_dtype="fp8")
+    tr = Trainer(spec.model, spec.loss, ps, spec.make_batch(16, torch.device("cpu"), seed=0))
+    if phase == "save":
+        for _ in range(3):
+            tr.step()
+        ps.save(prefix)
+    else:
+        ps.load(prefix)
+    for _ in range(2):
+        tr.step()
+    return {n: p.detach().clone() for n, p in spec.model.named_parameters()}
+
+
+def test_fp8_pull_resume_is_exact(tmp_path):
+    """Resume of an fp8-published run re-quantises the restored masters: the first
+    gradients after load must be computed on the checkpointed weights, not the initial ones."""
+    prefix = str(tmp_path / "ck8")
+    a = _fp8_run(prefix, "save")
+    b = _fp8_run(prefix, "load")
+    for n in a:
+        torch.testing.assert_close(a[n], b[n], rtol=0, atol=0, msg=n)
+
+
+@pytest.mark.gpu
+def test_async_save_is_a_consistent_snapshot_gpu(tmp_path, gpu, C):
+    """save(blocking=False) followed at once by more training steps must write exactly the state of
+    the step it was called at (the snapshot is ordered before the next fused apply)."""
+    torch.manual_seed(0)
+    spec = models.build("resnet50", gpu, torch.bfloat16, image_size=32, num_classes=10)
+    ps = CollectivePS(spec.model, OptimConfig("momentum", lr=0.05), staleness=1, bucket_mb=4, device=gpu)
+    tr = Trainer(spec.model, spec.loss, ps, spec.make_batch(8, gpu))
+    for _ in range(3):
+        tr.step()
+    ref, live = str(tmp_path / "ref"), str(tmp_path / "live")
+    ps.save(ref, blocking=True)
+    th = ps.save(live, blocking=False)
+    for _ in range(3):
+        tr.step()
+    th.join()
+    _, a = C.load_native_ckpt(ref + ".rank0.psd")
+    _, b = C.load_native_ckpt(live + ".rank0.psd")
+    assert len(a) == len(b)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
