@@ -5,12 +5,16 @@ parameter-server data plane, with gradient-staleness p50 and histogram (BASELINE
   python bench.py [--gpus N] [--steps K] [--warmup W]                   (N=1: plain process)
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
-Config (BASELINE.json configs 2/3): ResNet-50, bf16, NHWC, synthetic ImageNet-shaped data
-(224x224, 1000 classes), random init; every GPU is a worker; PS shards (default 2, BASELINE config
-3; capped at N) colocated on evenly spaced ranks hold the fp32 masters + momentum in HBM and apply
-the fused gfx950 SGD-momentum kernel; push = reduce-scatter / reduce, pull = all-gather /
-broadcast over RCCL, overlapped with backward; async SGD with staleness bound S (default 1: every
-update lands exactly one version late, the pull of step t+1 never waits for the push of step t).
+Config (BASELINE.json config 3): ResNet-50, bf16, NHWC, synthetic ImageNet-shaped data (224x224,
+1000 classes), random init; every GPU is a worker; PS shards (default 2, capped at N) colocated on
+evenly spaced ranks hold the fp32 masters + momentum in HBM. Default ``--ps-mode async``: each
+worker DMA-copies its gradient buckets over xGMI into its inbox on the owning GPUs while backward
+runs; the owner applies every push on arrival with the fused gfx950 SGD-momentum kernel and
+publishes a new bf16 snapshot; a worker pulls the latest snapshots at the start of a step and
+blocks only if it would lead the slowest worker by more than S steps (SSP, default S = 1). The
+staleness histogram counts, per apply, the updates the shard took between the snapshot the
+gradient was computed on and the apply. ``--ps-mode collective`` is the lock-step RCCL
+reduce-scatter / all-gather plane (fixed S-step gradient delay; hipGraph replay at N = 1).
 
 Timing: W untimed warmup steps (include MIOpen tuning and hipGraph capture), then exactly K timed
 steps bracketed by barrier + device synchronize on both sides; the max over ranks is reported.
@@ -68,6 +72,10 @@ def parse():
     ap.add_argument("--placement", default="colocated", choices=["colocated", "disjoint"],
                     help="disjoint: first half of the ranks are workers, second half PS shards")
     ap.add_argument("--staleness", type=int, default=1)
+    ap.add_argument("--ps-mode", default="async", choices=["async", "collective"],
+                    help="async: apply-on-arrival PS shards over xGMI peer memory with an SSP bound "
+                         "(parallel/async_ps.py); collective: lock-step RCCL reduce-scatter/all-gather with a "
+                         "fixed S-step gradient delay (parallel/collective_ps.py)")
     ap.add_argument("--bucket-mb", type=float, default=16.0)
     ap.add_argument("--pull-dtype", default="", help="bf16|fp8 published-weight dtype (default: fp8 for WRN-101)")
     ap.add_argument("--optimizer", default="", help="momentum|adam|adamw (default: momentum; adamw for BERT)")
@@ -124,7 +132,6 @@ def main():
     a.model = a.model.lower().replace("-", "_")
     a.batch = a.batch or DEFAULT_BATCH.get(a.model, 64)
     spec = models.build(a.model, dev, torch.bfloat16, image_size=a.image_size, seq_len=a.seq_len)
-    transport = make_transport(a.transport, dev)
     opt_kind = a.optimizer or ("adamw" if a.model.startswith("bert") else "momentum")
     lr = a.lr or (1e-4 if opt_kind.startswith("adam") else 0.1)
     optim = OptimConfig(opt_kind, lr=lr, momentum=0.9, weight_decay=0.01 if opt_kind == "adamw" else 5e-5)
@@ -135,9 +142,17 @@ def main():
     else:
         shards = max(1, min(a.ps_shards, world))
     pull_dtype = a.pull_dtype or ("fp8" if a.model.startswith("wide") else "bf16")
-    ps = CollectivePS(spec.model, optim, transport, num_shards=shards, staleness=a.staleness, bucket_mb=a.bucket_mb,
-                      device=dev, overlap=not spec.tied_weights, pull_dtype=pull_dtype,
-                      push_mode=a.push_mode, **kw)
+    mode = a.ps_mode if pull_dtype == "bf16" else "collective"  # fp8-published weights: collective plane
+    if mode == "async":
+        from parameter_server_distributed_amd.parallel.async_ps import AsyncPS
+
+        ps = AsyncPS(spec.model, optim, num_shards=shards, staleness=a.staleness, bucket_mb=a.bucket_mb, device=dev,
+                     overlap=not spec.tied_weights, **kw)
+    else:
+        transport = make_transport(a.transport, dev)
+        ps = CollectivePS(spec.model, optim, transport, num_shards=shards, staleness=a.staleness,
+                          bucket_mb=a.bucket_mb, device=dev, overlap=not spec.tied_weights, pull_dtype=pull_dtype,
+                          push_mode=a.push_mode, **kw)
     n_workers = len(ps.worker_ranks)
     batch = spec.make_batch(a.batch, dev, seed=rank)
     use_graph = (world == 1) if a.graph < 0 else bool(a.graph)
@@ -182,6 +197,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     ms = el / max(a.steps, 1) * 1e3
+    if mode == "async":
+        ps.drain()  # outside the timed region: every push of the run applied before reporting
     samples = a.batch * n_workers * a.steps
     value = samples / el
     hist = ps.staleness_histogram()
@@ -220,12 +237,14 @@ def main():
             "config": {"model": a.model, "global_batch": a.batch * n_workers, "per_gpu_batch": a.batch,
                        "seq_len": a.seq_len if a.model.startswith("bert") else None,
                        "image_size": None if a.model.startswith("bert") else a.image_size,
-                       "parallelism": f"ps{shards}-{'async' if a.staleness else 'sync'}-s{a.staleness}-dp{n_workers}"
+                       "parallelism": (f"ps{shards}-async-ssp{a.staleness}-dp{n_workers}" if mode == "async" else
+                                       f"ps{shards}-{'delayed' if a.staleness else 'sync'}-s{a.staleness}-dp{n_workers}")
                                       + ("-disjoint" if kw else ""),
+                       "ps_mode": mode,
                        "ps_shards": shards, "ps_owner_ranks": ps.owners, "worker_ranks": ps.worker_ranks,
                        "staleness_bound": a.staleness, "optimizer": f"{opt_kind} fused gfx950", "bucket_mb": a.bucket_mb,
                        "pull_dtype": pull_dtype, "tunableop": tunable_mode,
-                       "transport": transport.name, "hipgraph": bool(tr.graphs), "graph_error": tr.graph_error},
+                       "transport": ps.t.name, "hipgraph": bool(tr.graphs), "graph_error": tr.graph_error},
             "staleness_p50": p50, "staleness_hist": hist, "final_loss": round(final_loss, 4),
             "params_finite": params_finite,
             "warmup_s": round(t_w, 2), "peak_mem_gb": round(mem_peak / 2**30, 2),
@@ -239,6 +258,8 @@ def main():
         _tunableop.dump(a.tunableop_out if world == 1 else f"{a.tunableop_out}.{rank}")
     if tracer is not None:
         tracer.close()
+    if mode == "async":
+        ps.close()
     if world > 1:
         dist.destroy_process_group()
 

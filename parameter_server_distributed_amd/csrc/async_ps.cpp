@@ -1,0 +1,623 @@
+#include "async_ps.h"
+
+#include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <fcntl.h>
+#include <hip/hip_runtime_api.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstring>
+#include <sstream>
+
+#include "ops.h"
+
+namespace psd {
+
+namespace {
+
+constexpr uint64_t kMagic = 0x5053444153594e43ull;  // "PSDASYNC"
+constexpr int kMaxShards = 64, kMaxWorkers = 64, kRing = 16, kMaxBuf = 8, kBins = 64;
+constexpr int64_t kAlignBytes = 256;
+
+struct Msg {
+  int64_t step;
+  int64_t pulled;  // shard version the gradient was computed on
+};
+
+struct alignas(64) Mailbox {  // single producer (worker wi) -> single consumer (owner of shard k)
+  std::atomic<int64_t> head;
+  char pad0[56];
+  std::atomic<int64_t> tail;
+  char pad1[56];
+  Msg ring[kRing];
+};
+
+struct alignas(64) ShardCtl {
+  std::atomic<int64_t> version;  // applies completed
+  std::atomic<int32_t> latest;   // publish buffer holding `version`
+  int32_t pad;
+  std::atomic<int64_t> buf_version[kMaxBuf];
+  std::atomic<int32_t> readers[kMaxBuf];
+  std::atomic<int64_t> clock[kMaxWorkers];  // pushes of worker wi applied at this shard
+};
+
+static_assert(std::atomic<int64_t>::is_always_lock_free, "cross-process atomics need lock-free int64");
+
+}  // namespace
+
+struct AsyncCtl {
+  std::atomic<uint64_t> magic;
+  std::atomic<int32_t> error;
+  int32_t pad;
+  char msg[512];
+  ShardCtl shard[kMaxShards];
+  Mailbox mb[kMaxShards][kMaxWorkers];
+};
+
+namespace {
+
+inline void hip_ok(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, "psd async: ", what, " failed: ", hipGetErrorString(e));
+}
+
+int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+void backoff(int& spins) {
+  if (++spins < 64) {
+    std::this_thread::yield();
+  } else {
+    std::this_thread::sleep_for(std::chrono::microseconds(spins < 1024 ? 20 : 200));
+  }
+}
+
+void* map_shm(const std::string& name, size_t bytes, bool create) {
+  int fd = shm_open(name.c_str(), create ? (O_CREAT | O_EXCL | O_RDWR) : O_RDWR, 0600);
+  TORCH_CHECK(fd >= 0, "psd async: shm_open(", name, ") failed: ", std::strerror(errno));
+  if (create) TORCH_CHECK(ftruncate(fd, (off_t)bytes) == 0, "psd async: ftruncate failed: ", std::strerror(errno));
+  void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  TORCH_CHECK(p != MAP_FAILED, "psd async: mmap(", name, ") failed: ", std::strerror(errno));
+  return p;
+}
+
+}  // namespace
+
+AsyncEngine::AsyncEngine(int rank, int world, std::vector<int> owners, std::vector<int> workers,
+                         std::vector<int64_t> shard_off, std::vector<int64_t> shard_len, int staleness, int nbuf,
+                         std::string shm_name, bool create, int device, double timeout_s, int elem_bytes)
+    : rank_(rank),
+      world_(world),
+      S_(staleness),
+      nbuf_(nbuf),
+      device_(device),
+      timeout_s_(timeout_s),
+      esz_(elem_bytes),
+      owners_(std::move(owners)),
+      workers_(std::move(workers)),
+      shard_off_(std::move(shard_off)),
+      shard_len_(std::move(shard_len)),
+      shm_name_(std::move(shm_name)),
+      hist_(kBins, 0) {
+  const int P = (int)owners_.size(), W = (int)workers_.size();
+  TORCH_CHECK(P >= 1 && P <= kMaxShards, "psd async: 1..", kMaxShards, " shards");
+  TORCH_CHECK(W >= 1 && W <= kMaxWorkers, "psd async: 1..", kMaxWorkers, " workers");
+  TORCH_CHECK(S_ >= 0 && S_ + 1 <= kRing, "psd async: staleness bound must be in [0, ", kRing - 1, "]");
+  TORCH_CHECK(nbuf_ >= 2 && nbuf_ <= kMaxBuf, "psd async: 2..", kMaxBuf, " publish buffers");
+  TORCH_CHECK(esz_ == 2 || esz_ == 4, "psd async: bf16 (2) or fp32 (4) elements");
+  TORCH_CHECK((int)shard_off_.size() == P && (int)shard_len_.size() == P, "psd async: shard ranges per owner");
+  for (int k = 0; k < P; ++k) {
+    TORCH_CHECK(owners_[k] >= 0 && owners_[k] < world_, "psd async: bad owner rank");
+    if (owners_[k] == rank_) my_shards_.push_back(k);
+  }
+  my_wi_ = worker_index(rank_);
+
+  // control block
+  ctl_bytes_ = sizeof(AsyncCtl);
+  if (create) {
+    shm_unlink(shm_name_.c_str());
+    ctl_ = static_cast<AsyncCtl*>(map_shm(shm_name_, ctl_bytes_, true));
+    std::memset(static_cast<void*>(ctl_), 0, ctl_bytes_);
+    ctl_->magic.store(kMagic);
+    created_ = true;
+  } else {
+    ctl_ = static_cast<AsyncCtl*>(map_shm(shm_name_, ctl_bytes_, false));
+    TORCH_CHECK(ctl_->magic.load() == kMagic, "psd async: control block ", shm_name_, " not initialised");
+  }
+
+  // this rank's inbox + publish memory
+  local_bytes_ = region_bytes_for(rank_);
+  peer_base_.assign(world_, nullptr);
+  peer_ipc_.assign(world_, false);
+  peer_bytes_.assign(world_, 0);
+  if (local_bytes_ > 0) {
+    if (device_ >= 0) {
+      const c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device_));
+      // uncached fine-grained: peers' DMA writes / reads are coherent without cache maintenance
+      hipError_t e = hipExtMallocWithFlags(&local_mem_, (size_t)local_bytes_, hipDeviceMallocUncached);
+      mem_kind_ = "uncached";
+      if (e != hipSuccess) {
+        (void)hipGetLastError();
+        e = hipExtMallocWithFlags(&local_mem_, (size_t)local_bytes_, hipDeviceMallocFinegrained);
+        mem_kind_ = "finegrained";
+      }
+      hip_ok(e, "hipExtMallocWithFlags(inbox/publish)");
+      hip_ok(hipMemset(local_mem_, 0, (size_t)local_bytes_), "hipMemset");
+    } else {
+      std::ostringstream nm;
+      nm << shm_name_ << "_m" << rank_;
+      local_shm_ = nm.str();
+      shm_unlink(local_shm_.c_str());
+      local_mem_ = map_shm(local_shm_, (size_t)local_bytes_, true);
+      std::memset(local_mem_, 0, (size_t)local_bytes_);
+      mem_kind_ = "host-shm";
+    }
+    peer_base_[rank_] = static_cast<char*>(local_mem_);
+    peer_bytes_[rank_] = local_bytes_;
+  }
+
+  shards_.resize(P);
+  const auto opt = at::TensorOptions()
+                       .dtype(esz_ == 2 ? at::kBFloat16 : at::kFloat)
+                       .device(device_ >= 0 ? c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device_)
+                                            : c10::Device(c10::kCPU));
+  for (int k : my_shards_) {
+    ShardState& st = shards_[k];
+    for (int wi = 0; wi < W; ++wi)
+      for (int s = 0; s <= S_; ++s) st.inbox.push_back(at::from_blob(inbox_ptr(k, wi, s), {shard_len_[k]}, opt));
+    for (int b = 0; b < nbuf_; ++b) st.publish.push_back(at::from_blob(publish_ptr(k, b), {shard_len_[k]}, opt));
+    st.busy.assign(nbuf_, false);
+  }
+  if (device_ >= 0) {
+    ps_stream_ = c10::hip::getStreamFromPool(/*isHighPriority=*/true, (c10::DeviceIndex)device_).stream();
+  }
+}
+
+AsyncEngine::~AsyncEngine() {
+  try {
+    stop();
+  } catch (...) {
+  }
+  for (int r = 0; r < world_; ++r) {
+    if (r == rank_ || !peer_base_[r]) continue;
+    if (peer_ipc_[r]) (void)hipIpcCloseMemHandle(peer_base_[r]);
+    else munmap(peer_base_[r], (size_t)peer_bytes_[r]);
+  }
+  if (local_mem_) {
+    if (device_ >= 0) (void)hipFree(local_mem_);
+    else {
+      munmap(local_mem_, (size_t)local_bytes_);
+      shm_unlink(local_shm_.c_str());
+    }
+  }
+  std::lock_guard<std::mutex> g(act_mu_);
+  for (auto& a : actions_)
+    if (a.event) (void)hipEventDestroy(static_cast<hipEvent_t>(a.event));
+  if (ctl_) {
+    munmap(static_cast<void*>(ctl_), ctl_bytes_);
+    if (created_) shm_unlink(shm_name_.c_str());
+  }
+}
+
+// ------------------------------------------------------------------ layout
+int AsyncEngine::worker_index(int rank) const {
+  for (size_t i = 0; i < workers_.size(); ++i)
+    if (workers_[i] == rank) return (int)i;
+  return -1;
+}
+
+int64_t AsyncEngine::region_bytes_for(int rank) const {
+  int64_t b = 0;
+  for (size_t k = 0; k < owners_.size(); ++k)
+    if (owners_[k] == rank)
+      b += ((int64_t)workers_.size() * (S_ + 1) + nbuf_) * round_up(shard_len_[k] * esz_, kAlignBytes);
+  return b;
+}
+
+int64_t AsyncEngine::shard_base(int rank, int shard) const {
+  int64_t b = 0;
+  for (int k = 0; k < shard; ++k)
+    if (owners_[k] == rank) b += ((int64_t)workers_.size() * (S_ + 1) + nbuf_) * round_up(shard_len_[k] * esz_, kAlignBytes);
+  return b;
+}
+
+char* AsyncEngine::inbox_ptr(int shard, int wi, int slot) const {
+  const int o = owners_[shard];
+  TORCH_CHECK(peer_base_[o], "psd async: rank ", o, " memory not attached");
+  const int64_t sb = round_up(shard_len_[shard] * esz_, kAlignBytes);
+  return peer_base_[o] + shard_base(o, shard) + ((int64_t)wi * (S_ + 1) + slot) * sb;
+}
+
+char* AsyncEngine::publish_ptr(int shard, int buf) const {
+  const int o = owners_[shard];
+  TORCH_CHECK(peer_base_[o], "psd async: rank ", o, " memory not attached");
+  const int64_t sb = round_up(shard_len_[shard] * esz_, kAlignBytes);
+  return peer_base_[o] + shard_base(o, shard) + ((int64_t)workers_.size() * (S_ + 1) + buf) * sb;
+}
+
+// ------------------------------------------------------------------ memory exchange
+std::string AsyncEngine::local_desc() const {
+  if (!local_mem_) return "N";
+  if (device_ < 0) return "C" + local_shm_;
+  hipIpcMemHandle_t h;
+  hip_ok(hipIpcGetMemHandle(&h, local_mem_), "hipIpcGetMemHandle");
+  std::string s = "G";
+  s.append(reinterpret_cast<const char*>(&h), sizeof(h));
+  return s;
+}
+
+void AsyncEngine::attach_peer(int rank, const std::string& desc) {
+  TORCH_CHECK(rank >= 0 && rank < world_, "psd async: bad peer rank");
+  if (rank == rank_ || desc.empty() || desc[0] == 'N') return;
+  const int64_t bytes = region_bytes_for(rank);
+  if (desc[0] == 'C') {
+    peer_base_[rank] = static_cast<char*>(map_shm(desc.substr(1), (size_t)bytes, false));
+  } else {
+    TORCH_CHECK(desc[0] == 'G' && desc.size() == 1 + sizeof(hipIpcMemHandle_t), "psd async: bad descriptor");
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, desc.data() + 1, sizeof(h));
+    const c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device_));
+    void* p = nullptr;
+    hip_ok(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+    peer_base_[rank] = static_cast<char*>(p);
+    peer_ipc_[rank] = true;
+  }
+  peer_bytes_[rank] = bytes;
+}
+
+// ------------------------------------------------------------------ owner side
+void AsyncEngine::set_shard_state(int shard, at::Tensor master, c10::optional<at::Tensor> state1,
+                                  c10::optional<at::Tensor> state2, at::Tensor dyn, int64_t kind, double momentum,
+                                  double dampening, bool nesterov, double weight_decay, double beta1, double beta2,
+                                  double eps) {
+  TORCH_CHECK(shard >= 0 && shard < (int)owners_.size() && owners_[shard] == rank_, "psd async: shard ", shard,
+              " is not owned by rank ", rank_);
+  TORCH_CHECK(master.numel() == shard_len_[shard] && master.scalar_type() == at::kFloat && master.is_contiguous(),
+              "psd async: master must be contiguous fp32 of the shard length");
+  ShardState& st = shards_[shard];
+  st.master = master;
+  st.s1 = state1.has_value() ? *state1 : at::Tensor();
+  st.s2 = state2.has_value() ? *state2 : at::Tensor();
+  st.dyn = dyn;
+  st.hyper.kind = (int32_t)kind;
+  st.hyper.momentum = (float)momentum;
+  st.hyper.dampening = (float)dampening;
+  st.hyper.nesterov = nesterov;
+  st.hyper.weight_decay = (float)weight_decay;
+  st.hyper.beta1 = (float)beta1;
+  st.hyper.beta2 = (float)beta2;
+  st.hyper.eps = (float)eps;
+}
+
+void AsyncEngine::publish_initial(int shard) {
+  ShardState& st = shards_[shard];
+  TORCH_CHECK(st.master.defined(), "psd async: set_shard_state first");
+  st.publish[0].copy_(st.master);
+  if (device_ >= 0) hip_ok(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  ShardCtl& s = ctl_->shard[shard];
+  s.buf_version[0].store(0);
+  s.latest.store(0);
+  s.version.store(0);
+  st.enq = 0;
+}
+
+void AsyncEngine::start() {
+  if (running_) return;
+  stop_.store(false);
+  running_ = true;
+  thr_ = std::thread([this] { run(); });
+}
+
+void AsyncEngine::stop() {
+  if (!running_) return;
+  stop_.store(true);
+  thr_.join();
+  running_ = false;
+  // finish what is in flight (unpins / posts / applies) so the shared state is final and no
+  // kernel or copy still touches the inbox / publish memory when it is freed
+  for (int guard = 0; guard < 1000; ++guard) {
+    if (device_ >= 0) {
+      (void)hipStreamSynchronize(static_cast<hipStream_t>(ps_stream_));
+      std::lock_guard<std::mutex> g(act_mu_);
+      for (auto& a : actions_)
+        if (a.event) (void)hipEventSynchronize(static_cast<hipEvent_t>(a.event));
+    }
+    if (!poll_once() && pending_.empty()) break;
+  }
+}
+
+void AsyncEngine::run() {
+  try {
+    if (device_ >= 0) hip_ok(hipSetDevice(device_), "hipSetDevice");
+    int spins = 0;
+    while (!stop_.load()) {
+      if (ctl_->error.load()) break;
+      if (poll_once()) spins = 0;
+      else backoff(spins);
+    }
+  } catch (const std::exception& e) {
+    fail(std::string("engine thread (rank ") + std::to_string(rank_) + "): " + e.what());
+  }
+}
+
+bool AsyncEngine::poll_once() {
+  bool progress = false;
+  // 1. worker-side deferred actions (unpin after a pull copy, post after push copies)
+  for (;;) {
+    Action a;
+    {
+      std::lock_guard<std::mutex> g(act_mu_);
+      if (actions_.empty()) break;
+      Action& f = actions_.front();
+      if (!done(f.event)) break;
+      a = std::move(f);
+      actions_.pop_front();
+    }
+    a.fn();
+    if (a.event) (void)hipEventDestroy(static_cast<hipEvent_t>(a.event));
+    progress = true;
+  }
+  // 2. apply completions (one stream: in order)
+  while (!pending_.empty()) {
+    Pending& p = pending_.front();
+    if (!done(p.event)) break;
+    ShardCtl& s = ctl_->shard[p.shard];
+    const int64_t v = s.version.load() + 1;
+    s.buf_version[p.buf].store(v);
+    s.latest.store(p.buf);
+    s.version.store(v);
+    s.clock[p.wi].fetch_add(1);
+    shards_[p.shard].busy[p.buf] = false;
+    {
+      std::lock_guard<std::mutex> g(hist_mu_);
+      hist_[std::min<int64_t>(std::max<int64_t>(p.staleness, 0), kBins - 1)] += 1;
+    }
+    n_applies_.fetch_add(1);
+    if (log_on_) {
+      std::lock_guard<std::mutex> g(hist_mu_);
+      log_.push_back({p.shard, workers_[p.wi], p.step, p.staleness, v});
+    }
+    if (p.event) (void)hipEventDestroy(static_cast<hipEvent_t>(p.event));
+    pending_.pop_front();
+    progress = true;
+  }
+  // 3. new pushes -> apply on arrival
+  const int W = (int)workers_.size();
+  for (int k : my_shards_) {
+    ShardState& st = shards_[k];
+    ShardCtl& s = ctl_->shard[k];
+    for (int wi = 0; wi < W; ++wi) {
+      Mailbox& mb = ctl_->mb[k][wi];
+      const int64_t t = mb.tail.load();
+      if (t >= mb.head.load()) continue;
+      int buf = -1;
+      const int latest = s.latest.load();
+      for (int b = 0; b < nbuf_; ++b)
+        if (b != latest && !st.busy[b] && s.readers[b].load() == 0) {
+          buf = b;
+          break;
+        }
+      if (buf < 0) break;  // every snapshot is pinned or in flight: retry after completions
+      const Msg m = mb.ring[t % kRing];
+      mb.tail.store(t + 1);
+      const int slot = (int)(m.step % (S_ + 1));
+      at::Tensor g = st.inbox[(size_t)wi * (S_ + 1) + slot];
+      const int64_t stale = st.enq - m.pulled;
+      st.enq += 1;
+      st.busy[buf] = true;
+      hipEvent_t ev = nullptr;
+      if (device_ >= 0) {
+        c10::hip::HIPStreamGuard sg(c10::hip::getStreamFromExternal(static_cast<hipStream_t>(ps_stream_),
+                                                                    (c10::DeviceIndex)device_));
+        apply_into(st, g, buf);
+        hip_ok(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+        hip_ok(hipEventRecord(ev, static_cast<hipStream_t>(ps_stream_)), "hipEventRecord");
+      } else {
+        apply_into(st, g, buf);
+      }
+      pending_.push_back(Pending{k, wi, buf, m.step, stale, ev});
+      progress = true;
+    }
+  }
+  return progress;
+}
+
+// One update: optimizer step counter, fused apply of the inbox slot onto the fp32 master, and the
+// new snapshot written into publish buffer `buf` (bf16: by the apply kernel itself).
+void AsyncEngine::apply_into(ShardState& st, const at::Tensor& g, int buf) {
+  optim_advance_(st.dyn, st.hyper.beta1, st.hyper.beta2);
+  const bool bf16 = esz_ == 2;
+  fused_apply_(st.master, {g}, st.s1.defined() ? c10::optional<at::Tensor>(st.s1) : c10::nullopt,
+               st.s2.defined() ? c10::optional<at::Tensor>(st.s2) : c10::nullopt,
+               bf16 ? c10::optional<at::Tensor>(st.publish[buf]) : c10::nullopt, st.dyn, st.hyper.kind,
+               st.hyper.momentum, st.hyper.dampening, st.hyper.nesterov, st.hyper.weight_decay, st.hyper.beta1,
+               st.hyper.beta2, st.hyper.eps, false);
+  if (!bf16) st.publish[buf].copy_(st.master);
+}
+
+bool AsyncEngine::done(void* event) {
+  if (!event) return true;
+  const hipError_t e = hipEventQuery(static_cast<hipEvent_t>(event));
+  if (e == hipErrorNotReady) return false;
+  hip_ok(e, "hipEventQuery");
+  return true;
+}
+
+// ------------------------------------------------------------------ worker side
+void AsyncEngine::copy(void* dst, const void* src, int64_t bytes, void* stream) {
+  if (bytes <= 0) return;
+  if (device_ >= 0) {
+    hip_ok(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDefault, static_cast<hipStream_t>(stream)),
+           "hipMemcpyAsync");
+  } else {
+    std::memcpy(dst, src, (size_t)bytes);
+  }
+}
+
+void AsyncEngine::defer(void* stream, std::function<void()> fn) {
+  if (device_ < 0 || !running_) {
+    if (device_ >= 0) hip_ok(hipStreamSynchronize(static_cast<hipStream_t>(stream)), "hipStreamSynchronize");
+    fn();
+    return;
+  }
+  hipEvent_t ev = nullptr;
+  hip_ok(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+  hip_ok(hipEventRecord(ev, static_cast<hipStream_t>(stream)), "hipEventRecord");
+  std::lock_guard<std::mutex> g(act_mu_);
+  actions_.push_back(Action{ev, std::move(fn)});
+}
+
+void AsyncEngine::post(int shard, int wi, int64_t step, int64_t pulled) {
+  Mailbox& mb = ctl_->mb[shard][wi];
+  const int64_t h = mb.head.load();
+  if (h - mb.tail.load() >= kRing) {
+    fail("mailbox overflow (shard " + std::to_string(shard) + ", worker " + std::to_string(wi) + ")");
+    return;
+  }
+  mb.ring[h % kRing] = Msg{step, pulled};
+  mb.head.store(h + 1);
+  n_posts_.fetch_add(1);
+}
+
+void AsyncEngine::check_error() const {
+  if (ctl_->error.load()) TORCH_CHECK(false, "psd async: ", std::string(ctl_->msg));
+}
+
+void AsyncEngine::fail(const std::string& msg) {
+  int32_t z = 0;
+  if (ctl_->error.compare_exchange_strong(z, 1)) {
+    std::strncpy(ctl_->msg, msg.c_str(), sizeof(ctl_->msg) - 1);
+  }
+}
+
+std::vector<int64_t> AsyncEngine::pull(int64_t step, at::Tensor params_flat, int64_t stream) {
+  TORCH_CHECK(my_wi_ >= 0, "psd async: rank ", rank_, " is not a worker");
+  TORCH_CHECK(params_flat.is_contiguous() && params_flat.element_size() == esz_, "psd async: working buffer dtype");
+  const double t0 = now_s();
+  const int64_t need = step - S_;
+  const int P = (int)owners_.size(), W = (int)workers_.size();
+  if (need > 0) {
+    for (int k = 0; k < P; ++k) {
+      for (int wi = 0; wi < W; ++wi) {
+        int spins = 0;
+        while (ctl_->shard[k].clock[wi].load() < need) {
+          check_error();
+          if (now_s() - t0 > timeout_s_) {
+            const std::string m = "pull of step " + std::to_string(step) + " on rank " + std::to_string(rank_) +
+                                  " waited " + std::to_string(timeout_s_) + " s for worker " +
+                                  std::to_string(workers_[wi]) + " at shard " + std::to_string(k) + " (clock " +
+                                  std::to_string(ctl_->shard[k].clock[wi].load()) + " < " + std::to_string(need) + ")";
+            fail(m);
+            TORCH_CHECK(false, "psd async: ", m);
+          }
+          backoff(spins);
+        }
+      }
+    }
+  }
+  wait_us_.fetch_add((int64_t)((now_s() - t0) * 1e6));
+  std::vector<int64_t> pulled(P);
+  char* dst = static_cast<char*>(params_flat.data_ptr());
+  for (int k = 0; k < P; ++k) {
+    ShardCtl& s = ctl_->shard[k];
+    int b;
+    for (;;) {  // pin the latest snapshot (re-check: the owner never writes the latest or a pinned one)
+      b = s.latest.load();
+      s.readers[b].fetch_add(1);
+      if (s.latest.load() == b) break;
+      s.readers[b].fetch_sub(1);
+    }
+    pulled[k] = s.buf_version[b].load();
+    copy(dst + shard_off_[k] * esz_, publish_ptr(k, b), shard_len_[k] * esz_, reinterpret_cast<void*>(stream));
+    std::atomic<int32_t>* rd = &s.readers[b];
+    defer(reinterpret_cast<void*>(stream), [rd] { rd->fetch_sub(1); });
+  }
+  n_pulls_.fetch_add(1);
+  return pulled;
+}
+
+void AsyncEngine::push(int64_t step, const at::Tensor& grads_flat, int64_t lo, int64_t hi, int64_t stream) {
+  TORCH_CHECK(my_wi_ >= 0, "psd async: rank ", rank_, " is not a worker");
+  TORCH_CHECK(grads_flat.is_contiguous() && grads_flat.element_size() == esz_, "psd async: gradient buffer dtype");
+  check_error();
+  const char* src = static_cast<const char*>(grads_flat.data_ptr());
+  const int slot = (int)(step % (S_ + 1));
+  for (size_t k = 0; k < owners_.size(); ++k) {
+    const int64_t a = std::max(lo, shard_off_[k]), b = std::min(hi, shard_off_[k] + shard_len_[k]);
+    if (a >= b) continue;
+    copy(inbox_ptr((int)k, my_wi_, slot) + (a - shard_off_[k]) * esz_, src + a * esz_, (b - a) * esz_,
+         reinterpret_cast<void*>(stream));
+  }
+}
+
+void AsyncEngine::commit(int64_t step, std::vector<int64_t> pulled, int64_t stream) {
+  TORCH_CHECK(my_wi_ >= 0, "psd async: rank ", rank_, " is not a worker");
+  TORCH_CHECK(pulled.size() == owners_.size(), "psd async: one pulled version per shard");
+  const int wi = my_wi_;
+  const int P = (int)owners_.size();
+  defer(reinterpret_cast<void*>(stream), [this, wi, P, step, pulled] {
+    for (int k = 0; k < P; ++k) post(k, wi, step, pulled[k]);
+  });
+}
+
+void AsyncEngine::wait_applied(int64_t nsteps) {
+  TORCH_CHECK(my_wi_ >= 0, "psd async: rank ", rank_, " is not a worker");
+  const double t0 = now_s();
+  for (size_t k = 0; k < owners_.size(); ++k) {
+    int spins = 0;
+    while (ctl_->shard[k].clock[my_wi_].load() < nsteps) {
+      check_error();
+      TORCH_CHECK(now_s() - t0 <= timeout_s_, "psd async: rank ", rank_, " waited ", timeout_s_,
+                  " s for its pushes to be applied at shard ", k);
+      backoff(spins);
+    }
+  }
+}
+
+void AsyncEngine::wait_all_applied(int64_t nsteps) {
+  const double t0 = now_s();
+  for (size_t k = 0; k < owners_.size(); ++k) {
+    for (size_t wi = 0; wi < workers_.size(); ++wi) {
+      int spins = 0;
+      while (ctl_->shard[k].clock[wi].load() < nsteps) {
+        check_error();
+        TORCH_CHECK(now_s() - t0 <= timeout_s_, "psd async: rank ", rank_, " waited ", timeout_s_,
+                    " s for worker ", workers_[wi], " at shard ", k);
+        backoff(spins);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ introspection
+std::vector<int64_t> AsyncEngine::histogram() const {
+  std::lock_guard<std::mutex> g(hist_mu_);
+  return hist_;
+}
+
+int64_t AsyncEngine::version(int shard) const { return ctl_->shard[shard].version.load(); }
+
+std::vector<int64_t> AsyncEngine::clocks(int shard) const {
+  std::vector<int64_t> c(workers_.size());
+  for (size_t wi = 0; wi < workers_.size(); ++wi) c[wi] = ctl_->shard[shard].clock[wi].load();
+  return c;
+}
+
+std::vector<std::vector<int64_t>> AsyncEngine::apply_log() const {
+  std::lock_guard<std::mutex> g(hist_mu_);
+  return log_;
+}
+
+std::string AsyncEngine::error() const { return ctl_->error.load() ? std::string(ctl_->msg) : std::string(); }
+
+std::vector<int64_t> AsyncEngine::counters() const {
+  return {n_applies_.load(), n_posts_.load(), n_pulls_.load(), wait_us_.load()};
+}
+
+}  // namespace psd

@@ -1,0 +1,158 @@
+// Asynchronous parameter-server data plane: apply-on-arrival with bounded staleness (SSP) over
+// xGMI peer memory, no collectives.
+//
+// The reference PS handles each worker's push as it arrives (src/parameter_server.cpp:18-75) but
+// then waits for all `total_workers` before applying (:37) -- it has no asynchronous mode. Here
+// every PS shard applies each worker's gradient the moment it lands, and a worker only waits when
+// it would lead the slowest worker by more than S steps (stale-synchronous parallel).
+//
+// MI355X design (one process per GPU, one node, 7 xGMI links per GPU):
+//   * Each shard owner allocates, in its own HBM, a gradient *inbox* (one slot ring of S+1 slices
+//     per worker) and NB *publish* buffers (bf16 snapshots of its shard). Both are uncached
+//     fine-grained memory exported with hipIpcGetMemHandle and mapped by every peer
+//     (hipIpcOpenMemHandle + lazy peer access), so a peer's DMA write or read is coherent without
+//     any cache maintenance on the owner.
+//   * push: a worker DMA-copies its gradient slice straight into its inbox slot on the owner's GPU
+//     (hipMemcpyAsync over the direct xGMI link to that peer), then posts a message to a
+//     single-producer ring in a shared-memory control block once the copy has completed.
+//   * apply: the owner's engine thread (C++, no GIL) polls the rings and, per message, launches
+//     the fused gfx950 optimizer kernel on its PS stream: inbox slot -> fp32 master / state ->
+//     bf16 written into a free publish buffer. When the kernel completes the buffer becomes the
+//     shard's latest snapshot, the shard version and the worker's clock advance, and the staleness
+//     (updates applied since the snapshot the gradient was computed on) is recorded exactly.
+//   * pull: a worker waits until every worker's clock at every shard is >= step - S (SSP), pins
+//     the latest publish buffer (reader count), DMA-copies it into its working weights and
+//     unpins when the copy completes.
+// No GPU kernel ever waits on another process (no spinning collective kernels that could
+// interlock through shared hardware queues); every host wait has a deadline and reports an
+// error instead of hanging. With device = -1 the same protocol runs on host memory in POSIX
+// shared memory (CPU CI, gloo plumbing config).
+#pragma once
+#include <torch/extension.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "kernels/launchers.h"
+
+namespace psd {
+
+struct AsyncCtl;  // shared-memory control block (async_ps.cpp)
+
+class AsyncEngine {
+ public:
+  AsyncEngine(int rank, int world, std::vector<int> owners, std::vector<int> workers, std::vector<int64_t> shard_off,
+              std::vector<int64_t> shard_len, int staleness, int nbuf, std::string shm_name, bool create, int device,
+              double timeout_s, int elem_bytes = 2);
+  ~AsyncEngine();
+
+  // -- memory exchange (collective through the caller's store) --
+  std::string local_desc() const;                  // how peers map this rank's inbox/publish memory
+  void attach_peer(int rank, const std::string& desc);
+
+  // -- owner side --
+  void set_shard_state(int shard, at::Tensor master, c10::optional<at::Tensor> state1, c10::optional<at::Tensor> state2,
+                       at::Tensor dyn, int64_t kind, double momentum, double dampening, bool nesterov,
+                       double weight_decay, double beta1, double beta2, double eps);
+  void publish_initial(int shard);  // bf16(master) -> publish buffer 0, version 0 (blocking)
+  void start();
+  void stop();
+
+  // -- worker side --
+  std::vector<int64_t> pull(int64_t step, at::Tensor params_flat, int64_t stream);
+  void push(int64_t step, const at::Tensor& grads_flat, int64_t lo, int64_t hi, int64_t stream);
+  void commit(int64_t step, std::vector<int64_t> pulled, int64_t stream);
+  void wait_applied(int64_t nsteps);  // this worker's pushes 0..nsteps-1 applied at every shard
+  void wait_all_applied(int64_t nsteps);  // every worker's pushes 0..nsteps-1 applied at every shard
+
+  // -- introspection --
+  std::vector<int64_t> histogram() const;  // staleness of the applies this process performed
+  int64_t version(int shard) const;
+  std::vector<int64_t> clocks(int shard) const;
+  std::vector<int> my_shards() const { return my_shards_; }
+  std::string memory_kind() const { return mem_kind_; }
+  std::string error() const;
+  std::vector<int64_t> counters() const;  // applies, pushes posted, pulls, pull waits (us)
+  // completed applies in order: (shard, worker rank, step, staleness, version after) -- for tests
+  // and replay; recorded only after enable_log()
+  void enable_log(bool on) { log_on_ = on; }
+  std::vector<std::vector<int64_t>> apply_log() const;
+
+ private:
+  struct Pending {
+    int shard, wi, buf;
+    int64_t step, staleness;
+    void* event;  // hipEvent_t (GPU)
+  };
+  struct Action {
+    void* event;  // completion of the copies this action waits for (GPU), null = immediate
+    std::function<void()> fn;
+  };
+  struct ShardState {
+    at::Tensor master, s1, s2, dyn;
+    OptimHyper hyper{};
+    std::vector<at::Tensor> inbox;    // [workers * (S+1)] bf16 views
+    std::vector<at::Tensor> publish;  // [nbuf] bf16 views
+    std::vector<bool> busy;           // publish buffer is the target of an enqueued apply
+    int64_t enq = 0;                  // applies enqueued (the version the next apply starts from)
+  };
+
+  int64_t slot_elems(int shard) const { return shard_len_[shard]; }
+  int64_t region_bytes_for(int rank) const;
+  int64_t shard_base(int rank, int shard) const;  // byte offset of shard's region in rank's allocation
+  char* inbox_ptr(int shard, int wi, int slot) const;
+  char* publish_ptr(int shard, int buf) const;
+  void apply_into(ShardState& st, const at::Tensor& g, int buf);
+  static bool done(void* event);
+  void run();
+  bool poll_once();
+  void check_error() const;
+  void fail(const std::string& msg);
+  void copy(void* dst, const void* src, int64_t bytes, void* stream);
+  void defer(void* stream, std::function<void()> fn);
+  void post(int shard, int wi, int64_t step, int64_t pulled);
+  int worker_index(int rank) const;
+
+  int rank_, world_, S_, nbuf_, device_;
+  double timeout_s_;
+  int esz_;
+  std::vector<int> owners_, workers_, my_shards_;
+  std::vector<int64_t> shard_off_, shard_len_;
+  int my_wi_ = -1;
+  std::string shm_name_;
+  bool created_ = false;
+  AsyncCtl* ctl_ = nullptr;
+  size_t ctl_bytes_ = 0;
+  std::string mem_kind_;
+
+  // this rank's inbox/publish memory and the peers' mappings
+  void* local_mem_ = nullptr;
+  int64_t local_bytes_ = 0;
+  std::string local_shm_;
+  std::vector<char*> peer_base_;      // per rank: base pointer of its allocation in this process
+  std::vector<bool> peer_ipc_;        // mapped through hipIpcOpenMemHandle (must be closed)
+  std::vector<int64_t> peer_bytes_;
+
+  std::vector<ShardState> shards_;  // indexed by shard id (only owned ones are populated)
+  void* ps_stream_ = nullptr;       // hipStream_t of the apply kernels
+
+  std::thread thr_;
+  std::atomic<bool> stop_{false};
+  bool running_ = false;
+  std::deque<Pending> pending_;
+  std::mutex act_mu_;
+  std::deque<Action> actions_;
+  std::vector<int64_t> hist_;
+  bool log_on_ = false;
+  std::vector<std::vector<int64_t>> log_;
+  mutable std::mutex hist_mu_;
+  std::atomic<int64_t> n_applies_{0}, n_posts_{0}, n_pulls_{0}, wait_us_{0};
+};
+
+}  // namespace psd

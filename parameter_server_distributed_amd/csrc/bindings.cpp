@@ -1,6 +1,7 @@
 // pybind11 module `parameter_server_distributed_amd._C`.
 #include <torch/extension.h>
 
+#include "async_ps.h"
 #include "checkpoint.h"
 #include "comm.h"
 #include "kernels/launchers.h"
@@ -184,6 +185,34 @@ PYBIND11_MODULE(_C, m) {
       .def("histogram", &StalenessTracker::histogram)
       .def("percentile", &StalenessTracker::percentile)
       .def("reset", &StalenessTracker::reset);
+
+  // ---- asynchronous apply-on-arrival PS over peer memory ----
+  py::class_<AsyncEngine>(m, "AsyncEngine")
+      .def(py::init<int, int, std::vector<int>, std::vector<int>, std::vector<int64_t>, std::vector<int64_t>, int, int,
+                    std::string, bool, int, double, int>(),
+           py::arg("rank"), py::arg("world"), py::arg("owners"), py::arg("workers"), py::arg("shard_off"),
+           py::arg("shard_len"), py::arg("staleness"), py::arg("nbuf"), py::arg("shm_name"), py::arg("create"),
+           py::arg("device"), py::arg("timeout_s"), py::arg("elem_bytes") = 2)
+      .def("local_desc", [](const AsyncEngine& e) { return py::bytes(e.local_desc()); })
+      .def("attach_peer", [](AsyncEngine& e, int r, py::bytes d) { e.attach_peer(r, std::string(d)); })
+      .def("set_shard_state", &AsyncEngine::set_shard_state)
+      .def("publish_initial", &AsyncEngine::publish_initial)
+      .def("start", &AsyncEngine::start)
+      .def("stop", &AsyncEngine::stop, py::call_guard<py::gil_scoped_release>())
+      .def("pull", &AsyncEngine::pull, py::call_guard<py::gil_scoped_release>())
+      .def("push", &AsyncEngine::push, py::call_guard<py::gil_scoped_release>())
+      .def("commit", &AsyncEngine::commit, py::call_guard<py::gil_scoped_release>())
+      .def("wait_applied", &AsyncEngine::wait_applied, py::call_guard<py::gil_scoped_release>())
+      .def("wait_all_applied", &AsyncEngine::wait_all_applied, py::call_guard<py::gil_scoped_release>())
+      .def("histogram", &AsyncEngine::histogram)
+      .def("version", &AsyncEngine::version)
+      .def("clocks", &AsyncEngine::clocks)
+      .def("my_shards", &AsyncEngine::my_shards)
+      .def("memory_kind", &AsyncEngine::memory_kind)
+      .def("error", &AsyncEngine::error)
+      .def("counters", &AsyncEngine::counters)
+      .def("enable_log", &AsyncEngine::enable_log)
+      .def("apply_log", &AsyncEngine::apply_log);
 
   // ---- RCCL ----
   py::class_<RcclComm>(m, "RcclComm")

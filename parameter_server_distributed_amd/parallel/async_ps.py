@@ -1,0 +1,359 @@
+"""Asynchronous parameter server: apply-on-arrival with a stale-synchronous bound, over peer memory.
+
+The collective data plane (``collective_ps.CollectivePS``) moves every rank in lock-step: its
+"asynchrony" is a fixed S-step gradient delay. This one is the real thing (BASELINE.json config 3,
+SURVEY 7.5.2): each PS shard applies each worker's push the moment it lands, versions advance per
+push, and a worker blocks only when it would lead the slowest worker by more than S steps.
+
+Per step of a worker (``begin_step`` / grad hooks / ``finish_step``):
+
+  pull    SSP wait (every worker's clock at every shard >= step - S), then DMA-copy each shard's
+          latest published snapshot into the working weights (pinned while the copy runs)
+  fwd/bwd on the current stream; as each gradient bucket completes (post-accumulate-grad hook) its
+          slices are DMA-copied over xGMI straight into this worker's inbox slot on the owning GPU
+          (comm stream, overlapped with the rest of backward)
+  commit  once the copies have landed, a message (step, pulled versions) is posted to each shard's
+          single-producer ring in the shared control block
+
+The owner's native engine thread (``csrc/async_ps.cpp``) applies each message with the fused gfx950
+optimizer kernel (grad scale 1/W, so W pushes make one averaged step), writes the bf16 snapshot
+into a free publish buffer and advances the shard version, the worker's clock and the staleness
+histogram (staleness = shard version at apply - version the gradient was computed on).
+
+Layout: the parameters live in one flat working buffer (``.data`` views, reverse registration
+order, 64-element aligned) split into P contiguous shards; gradients alternate between two flat
+buffers so the next step never waits for the previous step's push copies. One node, one process
+per GPU (the control block is POSIX shared memory); ``device=cpu`` runs the identical protocol on
+host shared memory (CPU CI / gloo plumbing).
+
+Reference parity: ``ParameterServerCore::receive_gradients`` (src/parameter_server.cpp:18-75)
+buffers every push and applies only at the all-worker barrier (:37); there is no async mode and no
+version, so none of this has a counterpart beyond the push/pull/apply roles.
+"""
+from __future__ import annotations
+
+import os
+import uuid
+from dataclasses import dataclass, field
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from .. import native
+from ..ops.optim import OptimConfig, OptimDyn
+from .collective_ps import ALIGN, _flat_view, _round
+
+_INSTANCE = [0]
+
+
+class _NoTransport:
+    name = "ipc"
+    capturable = False
+
+
+@dataclass
+class _Bucket:
+    index: int
+    params: list = field(default_factory=list)  # (name, param, offset, numel)
+    lo: int = 0
+    hi: int = 0
+    pending: int = 0
+
+
+def _store_and_group():
+    if dist.is_available() and dist.is_initialized():
+        return dist.distributed_c10d._get_default_store(), dist.get_rank(), dist.get_world_size()
+    return dist.HashStore(), 0, 1
+
+
+class AsyncPS:
+    def __init__(self, model: nn.Module, optim: OptimConfig, num_shards: int | None = None, staleness: int = 1,
+                 bucket_mb: float = 16.0, device: torch.device | None = None, ps_ranks: list[int] | None = None,
+                 worker_ranks: list[int] | None = None, param_dtype: torch.dtype = torch.bfloat16, nbuf: int = 4,
+                 timeout_s: float | None = None, overlap: bool = True, store=None, log: bool = False):
+        self.model = model
+        self.cfg = optim
+        st, self.rank, self.world = _store_and_group()
+        self.store = store or st
+        self.t = _NoTransport()
+        self.worker_ranks = list(worker_ranks) if worker_ranks is not None else list(range(self.world))
+        self.is_worker = self.rank in self.worker_ranks
+        self.W = len(self.worker_ranks)
+        if ps_ranks is not None:
+            self.owners = list(ps_ranks)
+        else:
+            P = num_shards or self.world
+            if not 1 <= P <= self.world:
+                raise ValueError(f"num_shards must be in [1, world={self.world}], got {P}")
+            self.owners = [k * self.world // P for k in range(P)]
+        self.P = len(self.owners)
+        self.my_shards = [k for k, r in enumerate(self.owners) if r == self.rank]
+        self.S = int(staleness)
+        self.overlap = overlap
+        self.device = device or next(model.parameters()).device
+        self.is_cuda = self.device.type == "cuda"
+        if param_dtype not in (torch.bfloat16, torch.float32):
+            raise ValueError("AsyncPS publishes bf16 or fp32 weights")
+        self.param_dtype = param_dtype
+        self.step_idx = 0
+        self.pulled = [0] * self.P
+        timeout_s = float(os.environ.get("PSD_ASYNC_TIMEOUT", timeout_s or 600.0))
+
+        # ---- flat layout (same conventions as CollectivePS: reverse registration, 64-aligned)
+        params = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
+        params.reverse()
+        off = 0
+        layout = []
+        for n, p in params:
+            layout.append((n, p, off, p.numel()))
+            off += _round(p.numel(), ALIGN)
+        total = _round(max(off, ALIGN), self.P * ALIGN)
+        self.total = total
+        # P contiguous shards, 64-element aligned, balanced by size
+        bounds = [_round(total * k // self.P, ALIGN) for k in range(self.P)] + [total]
+        self.shard_off = bounds[:-1]
+        self.shard_len = [bounds[k + 1] - bounds[k] for k in range(self.P)]
+        # push buckets: consecutive parameter ranges of ~bucket_mb
+        elem = torch.finfo(param_dtype).bits // 8
+        cap = max(ALIGN, int(bucket_mb * (1 << 20)) // elem)
+        self.buckets: list[_Bucket] = []
+        cur = _Bucket(0, lo=0)
+        for n, p, o, k in layout:
+            cur.params.append((n, p, o, k))
+            cur.hi = o + _round(k, ALIGN)
+            if cur.hi - cur.lo >= cap:
+                self.buckets.append(cur)
+                cur = _Bucket(len(self.buckets), lo=cur.hi)
+        if cur.params:
+            self.buckets.append(cur)
+        self.buckets[-1].hi = total  # the tail padding travels with the last bucket
+
+        dev = self.device
+        init = torch.zeros(total, dtype=torch.float32, device=dev)
+        for n, p, o, k in layout:
+            _flat_view(init, o, p).copy_(p.detach().float())
+        self.params_flat = init.to(param_dtype)
+        self.grads = [torch.zeros(total, dtype=param_dtype, device=dev) for _ in range(2)]
+        self.gb = 0
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.master, self.state1, self.state2, self.dyn = {}, {}, {}, {}
+        for k in self.my_shards:
+            self.master[k] = init.narrow(0, self.shard_off[k], self.shard_len[k]).clone()
+            if optim.num_states >= 1:
+                self.state1[k] = torch.zeros(self.shard_len[k], **f32)
+            if optim.num_states >= 2:
+                self.state2[k] = torch.zeros(self.shard_len[k], **f32)
+            self.dyn[k] = OptimDyn(dev, lr=optim.lr, grad_scale=1.0 / self.W)
+        del init
+
+        # grad sinks (fused BN / MFMA linear write their parameter gradients straight into the buffer)
+        self._direct = set()
+        for m in model.modules():
+            if hasattr(m, "psd_direct_grad_params"):
+                for dp in m.psd_direct_grad_params():
+                    if dp is not None and dp.requires_grad:
+                        self._direct.add(id(dp))
+                m._psd_grad_sink = self._sink
+        self._layout = layout
+        self._p2b = {}
+        for b in self.buckets:
+            for _, p, _o, _n in b.params:
+                self._p2b[id(p)] = b
+        for n, p, o, k in layout:
+            p.data = _flat_view(self.params_flat, o, p)
+        self._set_grad_views()
+        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for _, p, _o, _n in layout]
+        self._next = 0
+        if self.is_cuda:
+            self.comm_stream = torch.cuda.Stream(device=dev)
+            self.push_done = [None, None]
+
+        # ---- native engine: control block (rank 0 creates), memory exchange, initial publish
+        _INSTANCE[0] += 1
+        key = f"psd/async/{_INSTANCE[0]}"
+        if self.rank == 0:
+            self.store.set(f"{key}/shm", f"/psd_{os.getpid()}_{uuid.uuid4().hex[:12]}")
+        shm = self.store.get(f"{key}/shm").decode()
+        C = native()
+        devidx = dev.index if (self.is_cuda and dev.index is not None) else (torch.cuda.current_device()
+                                                                            if self.is_cuda else -1)
+        if self.rank != 0:
+            self.store.wait([f"{key}/ctl"])
+        self.engine = C.AsyncEngine(self.rank, self.world, self.owners, self.worker_ranks, self.shard_off,
+                                    self.shard_len, self.S, nbuf, shm, self.rank == 0, devidx, timeout_s,
+                                    torch.finfo(param_dtype).bits // 8)
+        if self.rank == 0:
+            self.store.set(f"{key}/ctl", b"1")
+        self.store.set(f"{key}/desc/{self.rank}", self.engine.local_desc())
+        for r in range(self.world):
+            self.engine.attach_peer(r, self.store.get(f"{key}/desc/{r}"))
+        for k in self.my_shards:
+            self.engine.set_shard_state(k, self.master[k], self.state1.get(k), self.state2.get(k), self.dyn[k].t,
+                                        optim.code, optim.momentum, optim.dampening, optim.nesterov,
+                                        optim.weight_decay, optim.beta1, optim.beta2, optim.eps)
+            self.engine.publish_initial(k)
+        if log:
+            self.engine.enable_log(True)
+        self._key = key
+        self._barrier("init")
+        self.engine.start()
+        self.tracer = None
+        self.closed = False
+
+    # ------------------------------------------------------------------ helpers
+    def _barrier(self, tag: str):
+        if self.world == 1:
+            return
+        k = f"{self._key}/bar/{tag}"
+        self.store.add(k, 1)
+        import time
+
+        t0 = time.time()
+        while int(self.store.add(k, 0)) < self.world:
+            if time.time() - t0 > 600:
+                raise RuntimeError(f"AsyncPS barrier {tag} timed out")
+            time.sleep(0.001)
+
+    def _stream_ptr(self, s=None) -> int:
+        if not self.is_cuda:
+            return 0
+        s = s or torch.cuda.current_stream(self.device)
+        return s.cuda_stream
+
+    def _set_grad_views(self):
+        g = self.grads[self.gb]
+        self._grad_views = {}
+        for n, p, o, k in self._layout:
+            v = _flat_view(g, o, p)
+            self._grad_views[id(p)] = v
+            p.grad = None if id(p) in self._direct else v
+
+    def _sink(self, p):
+        if id(p) not in self._direct:
+            return None
+        v = self._grad_views[id(p)]
+        return v.view(v.shape)
+
+    def memory_bytes(self) -> dict:
+        eb = lambda t: t.numel() * t.element_size()  # noqa: E731
+        return {"params": eb(self.params_flat), "grads": 2 * eb(self.grads[0]),
+                "master": sum(eb(t) for t in self.master.values()),
+                "state": sum(eb(t) for t in list(self.state1.values()) + list(self.state2.values()))}
+
+    # ------------------------------------------------------------------ per-step protocol
+    def begin_step(self, track: bool = True):
+        if not self.is_worker:
+            return
+        self.gb = self.step_idx % 2
+        if self.is_cuda and self.push_done[self.gb] is not None:
+            # the push copies of step t-2 read this gradient buffer
+            torch.cuda.current_stream(self.device).wait_event(self.push_done[self.gb])
+        self.grads[self.gb].zero_()
+        self._set_grad_views()
+        for b in self.buckets:
+            b.pending = len(b.params)
+        self._next = 0
+        self.pulled = list(self.engine.pull(self.step_idx, self.params_flat, self._stream_ptr()))
+
+    def _on_grad(self, p):
+        if id(p) in self._direct:
+            v = self._grad_views[id(p)]
+            if p.grad is not None and p.grad.data_ptr() != v.data_ptr():
+                v.copy_(p.grad)
+        b = self._p2b[id(p)]
+        b.pending -= 1
+        if not self.overlap:
+            return
+        while self._next < len(self.buckets) and self.buckets[self._next].pending <= 0:
+            self._push(self.buckets[self._next])
+            self._next += 1
+
+    def _push(self, b: _Bucket):
+        g = self.grads[self.gb]
+        if self.is_cuda:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+            self.comm_stream.wait_event(ev)
+            self.engine.push(self.step_idx, g, b.lo, b.hi, self.comm_stream.cuda_stream)
+        else:
+            self.engine.push(self.step_idx, g, b.lo, b.hi, 0)
+
+    def finish_step(self, track: bool = True):
+        if not self.is_worker:
+            return
+        while self._next < len(self.buckets):
+            self._push(self.buckets[self._next])
+            self._next += 1
+        if self.is_cuda:
+            self.engine.commit(self.step_idx, self.pulled, self.comm_stream.cuda_stream)
+            ev = torch.cuda.Event()
+            ev.record(self.comm_stream)
+            self.push_done[self.gb] = ev
+        else:
+            self.engine.commit(self.step_idx, self.pulled, 0)
+        self.step_idx += 1
+
+    def idle_step(self):
+        pass
+
+    # ------------------------------------------------------------------ end of run / reporting
+    def drain(self):
+        """Block until every worker's pushes so far are applied everywhere (collective: all ranks)."""
+        steps = torch.tensor([self.step_idx if self.is_worker else 0], dtype=torch.int64)
+        if self.world > 1 and dist.is_initialized():
+            steps = steps.to(self.device) if dist.get_backend() == "nccl" else steps
+            dist.all_reduce(steps, op=dist.ReduceOp.MAX)
+        self.engine.wait_all_applied(int(steps.item()))
+        if self.is_cuda:
+            torch.cuda.synchronize(self.device)
+
+    def close(self):
+        if self.closed:
+            return
+        self.engine.stop()
+        self._barrier("close")
+        for h in self._hooks:
+            h.remove()
+        for m in self.model.modules():
+            if getattr(m, "_psd_grad_sink", None) == self._sink:
+                del m._psd_grad_sink
+        self.closed = True
+
+    def staleness_histogram(self):
+        return list(self.engine.histogram())
+
+    def staleness_p50(self) -> int:
+        h = self.staleness_histogram()
+        tot, acc = sum(h), 0
+        for i, c in enumerate(h):
+            acc += c
+            if tot and acc * 2 >= tot:
+                return i
+        return -1
+
+    def versions(self) -> list[int]:
+        return [int(self.engine.version(k)) for k in range(self.P)]
+
+    def apply_log(self):
+        return [tuple(x) for x in self.engine.apply_log()]
+
+    def set_lr(self, lr: float):
+        for d in self.dyn.values():
+            d.set(lr=lr)
+
+    def num_params(self) -> int:
+        return sum(k for (_, _, _, k) in self._layout)
+
+    def state_dict(self) -> dict:
+        """This rank's shard state (call after ``drain``)."""
+        return {"master": {k: v.detach().cpu() for k, v in self.master.items()},
+                "state1": {k: v.cpu() for k, v in self.state1.items()},
+                "state2": {k: v.cpu() for k, v in self.state2.items()},
+                "dyn": {k: d.t.cpu() for k, d in self.dyn.items()}, "versions": self.versions(),
+                "step_idx": self.step_idx}
+
+    def describe(self) -> str:
+        return (f"AsyncPS(world={self.world}, shards={self.P} on ranks {self.owners}, workers={self.worker_ranks}, "
+                f"SSP bound={self.S}, buckets={len(self.buckets)}, params={self.num_params() / 1e6:.2f}M, "
+                f"memory={self.engine.memory_kind()})")

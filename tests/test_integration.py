@@ -115,7 +115,7 @@ def test_checkpoint_and_resume(cluster_factory):
     assert w.wait(timeout=90) == 0, c.log("worker0.log")
     deadline = time.time() + 15
     ck = os.path.join(c.tmp, "checkpoint_epoch_2.ckpt")
-    while not os.path.exists(ck) and time.time() < deadline:
+    while not (os.path.exists(ck) and os.path.exists(ck + ".state")) and time.time() < deadline:
         time.sleep(0.2)
     assert os.path.exists(ck) and os.path.exists(ck + ".state"), os.listdir(c.tmp)
     first = _done_lines(c.log("worker0.log"))
