@@ -99,9 +99,11 @@ def _replay_and_check(out_dir, world, stale, bf16=False):
         for w in workers:
             for t, e in recs[w].items():
                 want = snaps[e["pulled"][k]]
-                if bf16:  # published snapshots are bf16(master)
+                tol = dict(rtol=1e-5, atol=1e-6)
+                if bf16:  # published snapshots are bf16(master): one ulp where the replay sits on a tie
                     want = want.to(torch.bfloat16).float()
-                torch.testing.assert_close(e["weights"].narrow(0, off[k], ln[k]), want, rtol=1e-5, atol=1e-6)
+                    tol = dict(rtol=2 ** -7, atol=1e-6)
+                torch.testing.assert_close(e["weights"].narrow(0, off[k], ln[k]), want, **tol)
                 assert min(e["clock_min"]) >= t - stale, (w, t, e["clock_min"])
     return hist_total
 
