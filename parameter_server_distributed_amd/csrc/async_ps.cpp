@@ -184,24 +184,41 @@ AsyncEngine::~AsyncEngine() {
     stop();
   } catch (...) {
   }
+  close_peers();
+  free_local();
+}
+
+void AsyncEngine::close_peers() {
   for (int r = 0; r < world_; ++r) {
     if (r == rank_ || !peer_base_[r]) continue;
     if (peer_ipc_[r]) (void)hipIpcCloseMemHandle(peer_base_[r]);
     else munmap(peer_base_[r], (size_t)peer_bytes_[r]);
+    peer_base_[r] = nullptr;
   }
+}
+
+void AsyncEngine::free_local() {
+  // callers: stop() first, and every peer has closed its mapping (Python barrier in between)
+  shards_.clear();
   if (local_mem_) {
     if (device_ >= 0) (void)hipFree(local_mem_);
     else {
       munmap(local_mem_, (size_t)local_bytes_);
       shm_unlink(local_shm_.c_str());
     }
+    local_mem_ = nullptr;
+    if (rank_ < (int)peer_base_.size()) peer_base_[rank_] = nullptr;
   }
-  std::lock_guard<std::mutex> g(act_mu_);
-  for (auto& a : actions_)
-    if (a.event) (void)hipEventDestroy(static_cast<hipEvent_t>(a.event));
+  {
+    std::lock_guard<std::mutex> g(act_mu_);
+    for (auto& a : actions_)
+      if (a.event) (void)hipEventDestroy(static_cast<hipEvent_t>(a.event));
+    actions_.clear();
+  }
   if (ctl_) {
     munmap(static_cast<void*>(ctl_), ctl_bytes_);
     if (created_) shm_unlink(shm_name_.c_str());
+    ctl_ = nullptr;
   }
 }
 

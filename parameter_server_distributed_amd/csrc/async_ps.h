@@ -63,6 +63,10 @@ class AsyncEngine {
   void publish_initial(int shard);  // bf16(master) -> publish buffer 0, version 0 (blocking)
   void start();
   void stop();
+  // teardown in two collective phases (barrier between): unmap the peers' memory, then free our
+  // own -- explicitly, before interpreter exit tears the HIP runtime down
+  void close_peers();
+  void free_local();
 
   // -- worker side --
   std::vector<int64_t> pull(int64_t step, at::Tensor params_flat, int64_t stream);

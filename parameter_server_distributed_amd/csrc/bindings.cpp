@@ -199,6 +199,8 @@ PYBIND11_MODULE(_C, m) {
       .def("publish_initial", &AsyncEngine::publish_initial)
       .def("start", &AsyncEngine::start)
       .def("stop", &AsyncEngine::stop, py::call_guard<py::gil_scoped_release>())
+      .def("close_peers", &AsyncEngine::close_peers)
+      .def("free_local", &AsyncEngine::free_local)
       .def("pull", &AsyncEngine::pull, py::call_guard<py::gil_scoped_release>())
       .def("push", &AsyncEngine::push, py::call_guard<py::gil_scoped_release>())
       .def("commit", &AsyncEngine::commit, py::call_guard<py::gil_scoped_release>())

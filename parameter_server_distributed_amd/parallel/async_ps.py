@@ -309,10 +309,17 @@ class AsyncPS:
             torch.cuda.synchronize(self.device)
 
     def close(self):
+        """Collective: stop the engine, unmap the peers' memory, free this rank's (all ranks call)."""
         if self.closed:
             return
         self.engine.stop()
-        self._barrier("close")
+        self._barrier("stop")
+        self.engine.close_peers()
+        self._barrier("unmapped")
+        hist, vers, log = self.staleness_histogram(), self.versions(), self.apply_log()
+        self._final = (hist, vers, log)
+        self.engine.free_local()
+        self.engine = None
         for h in self._hooks:
             h.remove()
         for m in self.model.modules():
@@ -321,6 +328,8 @@ class AsyncPS:
         self.closed = True
 
     def staleness_histogram(self):
+        if self.engine is None:
+            return list(self._final[0])
         return list(self.engine.histogram())
 
     def staleness_p50(self) -> int:
@@ -333,9 +342,13 @@ class AsyncPS:
         return -1
 
     def versions(self) -> list[int]:
+        if self.engine is None:
+            return list(self._final[1])
         return [int(self.engine.version(k)) for k in range(self.P)]
 
     def apply_log(self):
+        if self.engine is None:
+            return list(self._final[2])
         return [tuple(x) for x in self.engine.apply_log()]
 
     def set_lr(self, lr: float):
