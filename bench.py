@@ -80,7 +80,9 @@ def parse():
     ap.add_argument("--pull-dtype", default="", help="bf16|fp8 published-weight dtype (default: fp8 for WRN-101)")
     ap.add_argument("--optimizer", default="", help="momentum|adam|adamw (default: momentum; adamw for BERT)")
     ap.add_argument("--lr", type=float, default=0.0)
-    ap.add_argument("--graph", type=int, default=-1, help="hipGraph capture (1/0; -1: on for 1 GPU)")
+    ap.add_argument("--graph", type=int, default=-1,
+                    help="hipGraph capture of the whole step (1/0; -1: whenever the data plane is capturable: "
+                         "the collective plane on the native RCCL transport or at N = 1; never the async engine)")
     ap.add_argument("--transport", default="auto", choices=["auto", "torch", "rccl"])
     # MIOpen immediate mode by default: solutions come from the shipped find-db / heuristics with no
     # per-shape Find (warmup ~1 s instead of ~2-4 min per rank; measured 1-2 % slower steps)
@@ -155,7 +157,7 @@ def main():
                           push_mode=a.push_mode, **kw)
     n_workers = len(ps.worker_ranks)
     batch = spec.make_batch(a.batch, dev, seed=rank)
-    use_graph = (world == 1) if a.graph < 0 else bool(a.graph)
+    use_graph = a.graph != 0  # the Trainer keeps eager steps unless ps.t is capturable
     tracer = None
     if a.trace:
         from parameter_server_distributed_amd.utils.trace import StepTracer, rank_path

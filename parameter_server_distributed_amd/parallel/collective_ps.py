@@ -81,6 +81,9 @@ class CollectivePS:
         self.cfg = optim
         self.t = transport or LocalTransport()
         self.world, self.rank = self.t.world, self.t.rank
+        # world 1 with the local transport: push / pull are identities and are skipped; any other
+        # transport (RCCL at world 1 in tests) runs the real collectives
+        self._trivial = self.world == 1 and isinstance(self.t, LocalTransport)
         # placement: by default every rank is a worker and the P shards are spread evenly over the
         # node (2 of 8 -> ranks 0 and 4); ps_ranks / worker_ranks give disjoint placements
         # (e.g. 4 PS GPUs + 4 worker GPUs). Non-worker ranks run idle_step(): they take part in the
@@ -230,7 +233,7 @@ class CollectivePS:
             for b in self.buckets:
                 self._pull(b)
             return
-        if self.world == 1:
+        if self._trivial:
             return
         for b in self.buckets:
             self._pull(b)
@@ -366,7 +369,7 @@ class CollectivePS:
         g = self.grads_flat.narrow(0, b.offset, b.numel)
         if self.push_p2p:
             return self._push_p2p(b, slot)
-        if self.world == 1:
+        if self._trivial:
             if slot is not None:
                 self._owned_grad_views(b, slot)[0].copy_(g)
             return
@@ -416,7 +419,7 @@ class CollectivePS:
         C = native()
         q = self.p8.narrow(0, b.offset, b.numel).view(torch.uint8)
         sc = self.p8_scale.narrow(0, b.index * self.P, self.P)
-        if self.world > 1:
+        if not self._trivial:
             if self.collective_rs:
                 self.t.all_gather(q.narrow(0, self.rank * b.slice_numel, b.slice_numel), q)
                 self.t.all_gather(sc.narrow(0, self.rank, 1), sc)
@@ -433,7 +436,7 @@ class CollectivePS:
         if self.pull_fp8:
             return self._pull_fp8(b)
         w = self.params_flat.narrow(0, b.offset, b.numel)
-        if self.world == 1:
+        if self._trivial:
             return
         if self.collective_rs:
             self.t.all_gather(w.narrow(0, self.rank * b.slice_numel, b.slice_numel), w)

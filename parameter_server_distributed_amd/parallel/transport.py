@@ -5,7 +5,8 @@
   stream), never block the host and are legal inside hipGraph capture. The 128-byte RCCL unique
   id is bootstrapped through the rendezvous store (torch TCPStore or the coordinator's kv).
 * ``TorchDistTransport`` -- ``torch.distributed`` process group: ``gloo`` for the CPU plumbing
-  config / CI (BASELINE config 1), or the ``nccl`` (= RCCL) backend.
+  config / CI (BASELINE config 1) and the several-ranks-on-one-GPU rehearsal. Device tensors over
+  an nccl process group always go through ``RcclTransport`` (one RCCL path, no torch-PG detour).
 * ``LocalTransport`` -- world size 1: push/pull are identities (the colocated shard *is* the
   worker's buffer), so no copy is issued.
 
@@ -210,18 +211,37 @@ class RcclTransport(Transport):
         self.comm.abort()
 
 
-def make_transport(kind: str = "auto", device: torch.device | None = None) -> Transport:
-    """Pick the transport for the current process group / device.
-
-    ``auto``: world 1 -> local; CPU tensors -> torch (gloo); GPU -> torch PG (RCCL) unless
-    ``PSD_TRANSPORT=rccl`` selects the native communicator.
-    """
+def transport_kind(world: int, backend: str | None, kind: str = "auto", device_type: str = "cuda") -> str:
+    """Which transport a process uses (pure policy, unit-tested): world 1 -> ``local``; device
+    tensors over an nccl (= RCCL) process group -> the native ``rccl`` communicator on the PS comm
+    stream (graph-capturable); gloo / CPU tensors -> ``torch``. ``kind`` (or ``PSD_TRANSPORT``)
+    overrides the automatic choice."""
     kind = os.environ.get("PSD_TRANSPORT", kind)
-    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size() == 1:
-        return LocalTransport()
+    if world <= 1:
+        if kind not in ("auto", "local"):
+            return kind  # tests: drive RCCL / torch collectives even at world size 1
+        return "local"
     if kind == "local":
         raise ValueError("local transport requires world size 1")
-    if kind == "rccl":
+    if kind != "auto":
+        return kind
+    if backend == "nccl" and device_type == "cuda":
+        return "rccl"
+    return "torch"
+
+
+def make_transport(kind: str = "auto", device: torch.device | None = None) -> Transport:
+    """The transport for the current process group and device (see ``transport_kind``)."""
+    init = dist.is_available() and dist.is_initialized()
+    world = dist.get_world_size() if init else 1
+    backend = dist.get_backend() if init else None
+    dtype_ = device.type if device is not None else ("cuda" if torch.cuda.is_available() else "cpu")
+    k = transport_kind(world, backend, kind, dtype_)
+    if k == "local":
+        return LocalTransport()
+    if k == "rccl":
         dev = device.index if device is not None and device.index is not None else torch.cuda.current_device()
-        return RcclTransport(dist.get_rank(), dist.get_world_size(), dev)
+        if not init:
+            return RcclTransport(0, 1, dev, store=dist.HashStore())
+        return RcclTransport(dist.get_rank(), world, dev)
     return TorchDistTransport()

@@ -259,3 +259,19 @@ def test_async_save_is_a_consistent_snapshot_gpu(tmp_path, gpu, C):
     assert len(a) == len(b)
     for x, y in zip(a, b):
         assert torch.equal(x, y)
+
+
+def test_transport_policy_native_rccl_at_n_gt_1(monkeypatch):
+    """N > 1 over an nccl process group always selects the native RCCL communicator (no torch-PG
+    detour for device tensors); gloo / CPU select torch; world 1 is local."""
+    from parameter_server_distributed_amd.parallel.transport import transport_kind
+
+    monkeypatch.delenv("PSD_TRANSPORT", raising=False)
+    assert transport_kind(8, "nccl") == "rccl"
+    assert transport_kind(2, "nccl") == "rccl"
+    assert transport_kind(2, "gloo") == "torch"
+    assert transport_kind(2, "nccl", device_type="cpu") == "torch"
+    assert transport_kind(1, "nccl") == "local"
+    assert transport_kind(1, None, "rccl") == "rccl"
+    with pytest.raises(ValueError):
+        transport_kind(2, "nccl", "local")

@@ -54,3 +54,29 @@ def test_rccl_transport_drives_collective_ps(gpu):
     losses = [float(tr.step()) for _ in range(6)]
     assert losses[-1] < losses[0]
     assert ps.staleness_p50() == 1
+
+
+def test_rccl_transport_graph_capture_matches_local(gpu, monkeypatch):
+    """A whole collective-PS step (fwd, bwd, RCCL reduce-scatter / all-gather, fused apply) captured
+    in a hipGraph on the native transport and replayed: same weights as the local-transport graph."""
+    import torch.distributed as dist
+
+    from parameter_server_distributed_amd import models
+    from parameter_server_distributed_amd.ops.optim import OptimConfig
+    from parameter_server_distributed_amd.parallel.collective_ps import CollectivePS
+    from parameter_server_distributed_amd.parallel.transport import LocalTransport, RcclTransport
+    from parameter_server_distributed_amd.runtime.trainer import Trainer
+
+    monkeypatch.setenv("PSD_LINEAR_TUNE", "0")  # same GEMM kernels in both runs
+    out = []
+    for t in (LocalTransport(), RcclTransport(0, 1, gpu.index or 0, store=dist.HashStore())):
+        torch.manual_seed(0)
+        spec = models.build("mlp", gpu, torch.bfloat16)
+        ps = CollectivePS(spec.model, OptimConfig("momentum", lr=0.05), t, staleness=1, bucket_mb=0.1, device=gpu)
+        tr = Trainer(spec.model, spec.loss, ps, spec.make_batch(256, gpu), use_graph=True)
+        for _ in range(8):
+            tr.step()
+        torch.cuda.synchronize()
+        assert tr.graphs and tr.graph_error is None, tr.graph_error
+        out.append(ps.params_flat.clone())
+    assert torch.equal(out[0], out[1])
