@@ -145,12 +145,22 @@ def main():
         shards = max(1, min(a.ps_shards, world))
     pull_dtype = a.pull_dtype or ("fp8" if a.model.startswith("wide") else "bf16")
     mode = a.ps_mode if pull_dtype == "bf16" else "collective"  # fp8-published weights: collective plane
+    fallback = None
     if mode == "async":
         from parameter_server_distributed_amd.parallel.async_ps import AsyncPS
 
-        ps = AsyncPS(spec.model, optim, num_shards=shards, staleness=a.staleness, bucket_mb=a.bucket_mb, device=dev,
-                     overlap=not spec.tied_weights, **kw)
-    else:
+        try:
+            ps = AsyncPS(spec.model, optim, num_shards=shards, staleness=a.staleness, bucket_mb=a.bucket_mb,
+                         device=dev, overlap=not spec.tied_weights, **kw)
+        except RuntimeError as e:  # collective on every rank (AsyncPS._agree): fall back together
+            fallback = str(e)[:300]
+            mode = "collective"
+            if rank == 0:
+                print(f"WARNING: async peer-memory plane unavailable ({fallback}); using the collective plane",
+                      file=sys.stderr, flush=True)
+            torch.manual_seed(1234)
+            spec = models.build(a.model, dev, torch.bfloat16, image_size=a.image_size, seq_len=a.seq_len)
+    if mode == "collective":
         transport = make_transport(a.transport, dev)
         ps = CollectivePS(spec.model, optim, transport, num_shards=shards, staleness=a.staleness,
                           bucket_mb=a.bucket_mb, device=dev, overlap=not spec.tied_weights, pull_dtype=pull_dtype,
@@ -242,7 +252,7 @@ def main():
                        "parallelism": (f"ps{shards}-async-ssp{a.staleness}-dp{n_workers}" if mode == "async" else
                                        f"ps{shards}-{'delayed' if a.staleness else 'sync'}-s{a.staleness}-dp{n_workers}")
                                       + ("-disjoint" if kw else ""),
-                       "ps_mode": mode,
+                       "ps_mode": mode, "async_fallback": fallback,
                        "ps_shards": shards, "ps_owner_ranks": ps.owners, "worker_ranks": ps.worker_ranks,
                        "staleness_bound": a.staleness, "optimizer": f"{opt_kind} fused gfx950", "bucket_mb": a.bucket_mb,
                        "pull_dtype": pull_dtype, "tunableop": tunable_mode,

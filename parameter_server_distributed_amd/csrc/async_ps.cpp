@@ -612,6 +612,12 @@ void AsyncEngine::wait_all_applied(int64_t nsteps) {
   }
 }
 
+at::Tensor AsyncEngine::inbox_view(int shard, int wi, int slot) const {
+  TORCH_CHECK(shard >= 0 && shard < (int)owners_.size() && owners_[shard] == rank_, "psd async: not my shard");
+  TORCH_CHECK(wi >= 0 && wi < (int)workers_.size() && slot >= 0 && slot <= S_, "psd async: bad inbox index");
+  return shards_[shard].inbox[(size_t)wi * (S_ + 1) + slot];
+}
+
 // ------------------------------------------------------------------ introspection
 std::vector<int64_t> AsyncEngine::histogram() const {
   std::lock_guard<std::mutex> g(hist_mu_);

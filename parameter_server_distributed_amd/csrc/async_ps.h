@@ -75,6 +75,9 @@ class AsyncEngine {
   void wait_applied(int64_t nsteps);  // this worker's pushes 0..nsteps-1 applied at every shard
   void wait_all_applied(int64_t nsteps);  // every worker's pushes 0..nsteps-1 applied at every shard
 
+  // this rank's inbox slot of worker index wi at shard (owner side; start-up self-test)
+  at::Tensor inbox_view(int shard, int wi, int slot) const;
+
   // -- introspection --
   std::vector<int64_t> histogram() const;  // staleness of the applies this process performed
   int64_t version(int shard) const;

@@ -206,6 +206,7 @@ PYBIND11_MODULE(_C, m) {
       .def("commit", &AsyncEngine::commit, py::call_guard<py::gil_scoped_release>())
       .def("wait_applied", &AsyncEngine::wait_applied, py::call_guard<py::gil_scoped_release>())
       .def("wait_all_applied", &AsyncEngine::wait_all_applied, py::call_guard<py::gil_scoped_release>())
+      .def("inbox_view", &AsyncEngine::inbox_view)
       .def("histogram", &AsyncEngine::histogram)
       .def("version", &AsyncEngine::version)
       .def("clocks", &AsyncEngine::clocks)

@@ -185,9 +185,29 @@ class AsyncPS:
                                     torch.finfo(param_dtype).bits // 8)
         if self.rank == 0:
             self.store.set(f"{key}/ctl", b"1")
+        try:
+            self._connect(key, optim, log)
+        except Exception:
+            # release this rank's shared memory / IPC mappings before the (collective) error escapes
+            self.engine.stop()
+            self.engine.close_peers()
+            self.engine.free_local()
+            self.engine = None
+            raise
+        self.tracer = None
+        self.closed = False
+
+    def _connect(self, key, optim, log):
+        """Exchange memory descriptors, map the peers, publish version 0, self-test, start."""
+        self._key = key
         self.store.set(f"{key}/desc/{self.rank}", self.engine.local_desc())
-        for r in range(self.world):
-            self.engine.attach_peer(r, self.store.get(f"{key}/desc/{r}"))
+        err = ""
+        try:
+            for r in range(self.world):
+                self.engine.attach_peer(r, self.store.get(f"{key}/desc/{r}"))
+        except Exception as e:  # noqa: BLE001 -- reported collectively below
+            err = f"rank {self.rank}: {e}"
+        self._agree("attach", err)
         for k in self.my_shards:
             self.engine.set_shard_state(k, self.master[k], self.state1.get(k), self.state2.get(k), self.dyn[k].t,
                                         optim.code, optim.momentum, optim.dampening, optim.nesterov,
@@ -195,11 +215,54 @@ class AsyncPS:
             self.engine.publish_initial(k)
         if log:
             self.engine.enable_log(True)
-        self._key = key
         self._barrier("init")
+        self.selftest()
         self.engine.start()
-        self.tracer = None
-        self.closed = False
+
+    def selftest(self):
+        """Collective start-up check of the peer-memory paths on this node (before any training):
+        every worker DMA-writes a known pattern into its inbox on every shard owner, and every
+        owner verifies what landed; every worker pulls the version-0 snapshots and compares them
+        with its own initial weights. Raises on any mismatch on any rank (so a caller can fall
+        back to the collective plane instead of training on a broken path)."""
+        dev = self.device
+        ok, why = True, ""
+        if self.is_worker:
+            pat = (torch.arange(self.total, device=dev) % 251 + (self.rank + 1)).to(self.param_dtype)
+            self.engine.push(0, pat, 0, self.total, self._stream_ptr())
+            got = torch.empty_like(self.params_flat)
+            self.engine.pull(0, got, self._stream_ptr())
+            if self.is_cuda:
+                torch.cuda.synchronize(dev)
+            if not torch.equal(got, self.params_flat):
+                ok, why = False, f"rank {self.rank}: pulled snapshot != initial weights"
+        if os.environ.get("PSD_ASYNC_SELFTEST_FAIL_RANK") == str(self.rank):  # fault injection (tests)
+            ok, why = False, f"rank {self.rank}: injected self-test failure"
+        self._barrier("selftest-push")
+        for k in self.my_shards:
+            for wi, w in enumerate(self.worker_ranks):
+                v = self.engine.inbox_view(k, wi, 0)
+                want = (torch.arange(self.shard_off[k], self.shard_off[k] + self.shard_len[k], device=dev) % 251
+                        + (w + 1)).to(self.param_dtype)
+                if not torch.equal(v, want):
+                    ok, why = False, f"rank {self.rank}: shard {k} inbox of worker {w} holds wrong data"
+                v.zero_()
+        if self.is_cuda:
+            torch.cuda.synchronize(dev)
+        self._agree("selftest", "" if ok else why)
+        self.selftest_ok = True
+
+    def _agree(self, tag: str, err: str):
+        """Collective status exchange through the store: every rank raises if any rank failed."""
+        self.store.set(f"{self._key}/{tag}/{self.rank}", err or "ok")
+        errs = []
+        for r in range(self.world):
+            self.store.wait([f"{self._key}/{tag}/{r}"])
+            v = self.store.get(f"{self._key}/{tag}/{r}").decode()
+            if v != "ok":
+                errs.append(v)
+        if errs:
+            raise RuntimeError(f"AsyncPS {tag} failed: " + "; ".join(errs))
 
     # ------------------------------------------------------------------ helpers
     def _barrier(self, tag: str):

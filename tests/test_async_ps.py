@@ -167,3 +167,29 @@ def test_async_gpu_ipc_matches_replay(tmp_path, gpu, world, stale):
     _replay_and_check(str(tmp_path), world, stale, bf16=True)
     mem = torch.load(os.path.join(str(tmp_path), "r0.pt"), weights_only=False)["mem"]
     assert mem in ("uncached", "finegrained"), mem
+
+
+def _selftest_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PSD_ASYNC_SELFTEST_FAIL_RANK="1")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    spec = models.build("mlp", torch.device("cpu"), torch.float32, hidden=64)
+    try:
+        AsyncPS(spec.model, OptimConfig(**CFG), num_shards=2, staleness=1, param_dtype=torch.float32)
+        res = "no error"
+    except RuntimeError as e:
+        res = str(e)
+    with open(os.path.join(out_dir, f"st{rank}.txt"), "w") as f:
+        f.write(res)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.slow
+def test_async_selftest_failure_is_collective(tmp_path):
+    """A peer-memory self-test failure on one rank raises on every rank (bench.py then falls back to
+    the collective plane on all of them together instead of hanging)."""
+    mp.spawn(_selftest_worker, args=(2, _port(), str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        txt = open(os.path.join(str(tmp_path), f"st{r}.txt")).read()
+        assert "selftest failed" in txt and "injected" in txt, txt
