@@ -28,7 +28,7 @@
 // error instead of hanging. With device = -1 the same protocol runs on host memory in POSIX
 // shared memory (CPU CI, gloo plumbing config).
 #pragma once
-#include <torch/extension.h>
+#include <ATen/ATen.h>
 
 #include <atomic>
 #include <condition_variable>

@@ -75,6 +75,70 @@ def test_emit_proto(tmp_path):
     assert "repeated float data = 3;" in txt
 
 
+REF_PROTO = os.environ.get("PSD_REFERENCE_PROTO_DIR", "/root/reference/proto")
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_PROTO), reason="reference .proto files not present")
+@pytest.mark.parametrize("pkg,fname", [("coordinator", "coordinator.proto"),
+                                       ("parameter_server", "parameter_server.proto")])
+def test_schema_is_a_wire_superset_of_the_reference_proto(pkg, fname):
+    """Parse the reference's own .proto (read-only) and require every message, field name, field
+    number, scalar/enum/message type, label (repeated or not), enum value and rpc signature to be
+    identical in our proto/psd_*.proto -- names, numbers *and* types (the old test
+    checked hand-copied numbers only)."""
+    from parameter_server_distributed_amd.rpc import protoparse
+
+    ref = protoparse.describe(protoparse.parse_file(os.path.join(REF_PROTO, fname)))
+    ours = protoparse.describe(schema.FILES[pkg])
+    diff = {k: (v, ours.get(k)) for k, v in ref.items() if ours.get(k) != v}
+    assert not diff, diff
+    ref_fd = protoparse.parse_file(os.path.join(REF_PROTO, fname))
+    assert ref_fd.package == schema.FILES[pkg].package
+    # additions are additive: our extra fields never reuse a number the reference message has
+    for m in schema.FILES[pkg].message_type:
+        rm = next((x for x in ref_fd.message_type if x.name == m.name), None)
+        if rm is None:
+            continue
+        ref_nums = {f.number: f.name for f in rm.field}
+        for f in m.field:
+            assert ref_nums.get(f.number, f.name) == f.name, (m.name, f.name, f.number)
+
+
+def test_wire_types_of_reference_fields():
+    """Types the reference relies on, pinned without the reference tree (e.g. timestamp int64,
+    shape repeated int32, data repeated float)."""
+    from google.protobuf.descriptor import FieldDescriptor as FD
+
+    hb = schema.coordinator.HeartbeatResponse.DESCRIPTOR.fields_by_name["timestamp"]
+    assert hb.type == FD.TYPE_INT64
+    t = schema.parameter_server.Tensor.DESCRIPTOR.fields_by_name
+    assert t["shape"].type == FD.TYPE_INT32 and t["shape"].is_repeated
+    assert t["data"].type == FD.TYPE_FLOAT and t["data"].is_repeated
+    assert schema.coordinator.HeartbeatRequest.DESCRIPTOR.fields_by_name["status"].enum_type.name == "WorkerStatus"
+    g = schema.parameter_server.GradientUpdate.DESCRIPTOR.fields_by_name["gradients"]
+    assert g.message_type.name == "Tensor" and g.is_repeated
+
+
+def test_proto_parser_grammar_and_errors():
+    from parameter_server_distributed_amd.rpc import protoparse
+
+    fd = protoparse.parse('''
+        syntax = "proto3";  /* block
+        comment */ package demo;
+        option cc_enable_arenas = true;
+        enum E { A = 0; B = 1; }
+        message M { repeated int64 xs = 1 [packed = true]; E e = 2; N n = 3; reserved 9; }
+        message N {}
+        service S { rpc Do(M) returns (N); rpc Opt(N) returns (M) {} }
+    ''', "demo.proto")
+    d = protoparse.describe(fd)
+    assert d["M.xs"][0] == 1 and d["M.e"][3] == "E" and d["M.n"][3] == "N" and d["rpc S.Opt"] == ("N", "M")
+    with pytest.raises(protoparse.ProtoSyntaxError):
+        protoparse.parse('syntax = "proto3"; package p; message M { Unknown u = 1; }', "bad.proto")
+    with pytest.raises(protoparse.ProtoSyntaxError):
+        protoparse.parse('syntax = "proto3"; package p; extend M {}', "bad.proto")
+
+
 def test_split_host_port():
     assert split_host_port("localhost:50051", 1) == ("localhost", 50051)
     assert split_host_port("10.0.0.5", 50051) == ("10.0.0.5", 50051)
