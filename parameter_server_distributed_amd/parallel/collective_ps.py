@@ -719,6 +719,8 @@ class CollectivePS:
                     self.params_flat.copy_(full)
         if "dyn" in sd:
             self.dyn.t.copy_(sd["dyn"].to(self.dyn.t.device))
+            # step count / bias corrections / lr carry over; the 1/W averaging is this world's
+            self.dyn.set(grad_scale=1.0 / len(self.worker_ranks))
         for s in self.slots:
             s.zero_()
         self.step_idx = 0

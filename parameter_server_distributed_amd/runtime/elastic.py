@@ -26,11 +26,27 @@ Here every worker process is one rank of a collective world built per *generatio
 A joiner registers with the coordinator (which bumps the epoch) and waits for the first plan that
 lists it. A graceful leaver (SIGTERM from ``scale_workers.sh down``) keeps training until the next
 check, hands its shards over and exits 0.
+
+Crash recovery (a rank dies without handing over -- SIGKILL, OOM, a lost node): its PS shards are
+gone, so the job restarts from the last *canonical checkpoint* (every ``checkpoint_every`` steps
+rank 0 writes the drained, layout-independent fp32 masters + optimizer state with the global step,
+atomically, CRC-checked: csrc/checkpoint.cpp). Survivors notice the failure in one of two ways:
+the collective they are blocked in fails (gloo sees the peer's socket close; the per-generation
+process-group timeout bounds any other wait), or the watchdog thread sees the coordinator expire a
+member of the current plan (missed heartbeats) and aborts the RCCL communicator so the blocked
+collective returns. They then tear the group down, one survivor (store election) waits until the
+coordinator's live set no longer lists the dead member and publishes the next plan (survivors +
+joiners, step = checkpoint step, ``restore``), and everyone rebuilds the world, reloads the
+checkpoint re-sharded for the new world and continues. Steps after the checkpoint are recomputed;
+the parameter state is exactly the checkpoint's (reference: the coordinator's expiry,
+src/coordinator.cpp:52-67, and the ops-level PS restart, scripts/scale_workers.sh:137-144, which
+lost all in-memory state).
 """
 from __future__ import annotations
 
 import datetime
 import json
+import os
 import signal
 import socket
 import threading
@@ -55,6 +71,7 @@ class Plan:
     step: int  # global step the generation starts at
     epoch: int  # coordinator membership epoch the plan was made from
     done: bool = False
+    restore: bool = False  # start from the canonical checkpoint (crash recovery)
 
     def dumps(self) -> str:
         return json.dumps(self.__dict__)
@@ -155,6 +172,52 @@ def _init_group(agent: ElasticAgent, plan: Plan, backend: str, device) -> None:
                             timeout=agent.timeout, **kw)
 
 
+def _destroy_group():
+    try:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+    except Exception:  # noqa: BLE001 -- the group of a failed generation may be half torn down
+        pass
+
+
+class _Watchdog:
+    """Per-generation failure detector: when the coordinator expires a member of the current plan
+    (missed heartbeats), abort the native RCCL communicator so a collective blocked on the dead
+    peer returns, and flag the generation as failed."""
+
+    def __init__(self, agent: ElasticAgent, plan: Plan, ps, period_s: float = 0.5):
+        self.agent, self.plan, self.ps = agent, plan, ps
+        self.fired = False
+        self.dead: list[int] = []
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, args=(period_s,), name="elastic-watchdog", daemon=True)
+        self._t.start()
+
+    def _run(self, period_s):
+        seen = self.agent.epoch
+        while not self._stop.wait(period_s):
+            if self.agent.epoch == seen:
+                continue
+            seen = self.agent.epoch
+            try:
+                _, live = self.agent.live()
+            except Exception:  # noqa: BLE001
+                continue
+            dead = sorted(set(self.plan.members) - set(live))
+            if dead:
+                self.dead, self.fired = dead, True
+                abort = getattr(getattr(self.ps, "t", None), "abort", None)
+                if abort is not None:
+                    try:
+                        abort()
+                    except Exception:  # noqa: BLE001
+                        pass
+                return
+
+    def stop(self):
+        self._stop.set()
+
+
 class ElasticTrainer:
     """Runs ``steps`` global training steps across membership changes.
 
@@ -164,7 +227,8 @@ class ElasticTrainer:
     """
 
     def __init__(self, agent: ElasticAgent, model, make_ps, make_trainer, steps: int, device,
-                 check_every: int = 10, min_workers: int = 1, backend: str | None = None, on_step=None):
+                 check_every: int = 10, min_workers: int = 1, backend: str | None = None, on_step=None,
+                 checkpoint_dir: str | None = None, checkpoint_every: int = 0, collective_timeout_s: float = 0.0):
         self.agent = agent
         self.model = model
         self.make_ps, self.make_trainer = make_ps, make_trainer
@@ -177,7 +241,13 @@ class ElasticTrainer:
         self.leaving = False
         self.history = []  # (gen, members, start step)
         self.resizes = 0
+        self.recoveries = 0
         self.log = agent.log
+        self.checkpoint_dir = checkpoint_dir
+        self.checkpoint_every = int(checkpoint_every) if checkpoint_dir else 0
+        # bounds every collective of a generation (a dead peer must not block survivors forever)
+        if collective_timeout_s > 0:
+            self.agent.timeout = datetime.timedelta(seconds=collective_timeout_s)
 
     def request_leave(self, *_):
         """SIGTERM handler (scale_workers.sh down): hand over at the next check, then exit."""
@@ -199,23 +269,53 @@ class ElasticTrainer:
             _init_group(self.agent, plan, self.backend, self.device)
             rank, world = dist.get_rank(), dist.get_world_size()
             self.history.append((plan.gen, list(plan.members), plan.step))
-            self.log.info("generation %d: rank %d of %d (members %s) from step %d", plan.gen, rank, world,
-                          plan.members, plan.step)
+            self.log.info("generation %d: rank %d of %d (members %s) from step %d%s", plan.gen, rank, world,
+                          plan.members, plan.step, " (restored from checkpoint)" if plan.restore else "")
             ps = self.make_ps(self.model, make_transport("auto", self.device))
-            if plan.gen > 0:  # state handed over by the previous generation's leader (new rank 0)
+            if plan.restore:
+                ps.load_canonical_state(self._load_checkpoint(ps))
+                step = plan.step
+            elif plan.gen > 0:  # state handed over by the previous generation's leader (new rank 0)
                 ps.load_canonical_state(self._broadcast_state(ps, state))
-                state = None
+            state = None
             tr = self.make_trainer(ps)
             self.agent.status = cpb.TRAINING
             leavers = None
-            while step < self.steps and leavers is None:
-                loss = tr.step()
-                step += 1
-                losses.append(loss.detach().clone())
-                if self.on_step is not None:
-                    self.on_step(step, loss, plan)
-                if step % self.check_every == 0 and step < self.steps:
-                    leavers = self._check(plan, world, rank)
+            watchdog = _Watchdog(self.agent, plan, ps)
+            try:
+                while step < self.steps and leavers is None:
+                    loss = tr.step()
+                    step += 1
+                    losses.append(loss.detach().clone())
+                    if self.on_step is not None:
+                        self.on_step(step, loss, plan)
+                    if self.checkpoint_every and step % self.checkpoint_every == 0 and step < self.steps:
+                        self._save_checkpoint(ps, step)
+                    if step % self.check_every == 0 and step < self.steps:
+                        leavers = self._check(plan, world, rank)
+                    if watchdog.fired:
+                        raise RuntimeError(f"member(s) {watchdog.dead} of generation {plan.gen} died")
+            except Exception as e:  # noqa: BLE001 -- a peer died mid-collective: recover
+                watchdog.stop()
+                if not self.checkpoint_every:
+                    raise
+                self.log.warning("generation %d failed at step %d (%s): recovering from the last checkpoint",
+                                 plan.gen, step, str(e).splitlines()[0][:200])
+                try:
+                    ps.close()
+                except Exception:  # noqa: BLE001
+                    pass
+                del tr, ps
+                _destroy_group()
+                plan = self._recover(plan)
+                self.recoveries += 1
+                result["recovered_at"] = result.get("recovered_at", []) + [step]
+                if self.agent.worker_id not in plan.members:
+                    result["losses"] = [float(x) for x in losses]
+                    self.agent.leave()
+                    return result
+                continue
+            watchdog.stop()
             if hasattr(tr, "wait_checkpoint"):
                 tr.wait_checkpoint()
             if leavers is None:  # all steps done
@@ -251,9 +351,57 @@ class ElasticTrainer:
                 return result
         result["finished_at"] = step
         result["resizes"] = self.resizes
+        result["recoveries"] = self.recoveries
         result["losses"] = [float(x) for x in losses]
         self.agent.leave()
         return result
+
+    # ------------------------------------------------------------------ crash recovery
+    def _ckpt_path(self) -> str:
+        return os.path.join(self.checkpoint_dir, "elastic_canonical.psd")
+
+    def _save_checkpoint(self, ps, step: int):
+        """Collective: drain, gather the canonical state to rank 0, write it atomically."""
+        from .. import native
+
+        ps.drain()
+        sd = ps.canonical_state(root=0)
+        if dist.get_rank() == 0:
+            keys = [k for k in ("master", "state1", "state2", "dyn") if k in sd]
+            man = json.dumps({"step": step, "keys": keys, "format": "psd-elastic-canonical-v1"})
+            os.makedirs(self.checkpoint_dir, exist_ok=True)
+            native().save_native_ckpt(self._ckpt_path(), man, [sd[k].detach().cpu() for k in keys])
+        self.last_checkpoint = step
+
+    def _load_checkpoint(self, ps) -> dict:
+        from .. import native
+
+        man, ts = native().load_native_ckpt(self._ckpt_path())
+        m = json.loads(man)
+        return {k: t for k, t in zip(m["keys"], ts)}
+
+    def _checkpoint_step(self) -> int:
+        from .. import native
+
+        if not self.checkpoint_dir or not os.path.exists(self._ckpt_path()):
+            raise RuntimeError("a member died and no canonical checkpoint exists to recover from")
+        man, _ = native().load_native_ckpt(self._ckpt_path())
+        return int(json.loads(man)["step"])
+
+    def _recover(self, plan: Plan) -> Plan:
+        """After a failed generation: one survivor (store election) waits for the coordinator to
+        drop the dead member(s), then publishes the restore plan; everyone reads it."""
+        if self.agent.store.add(f"{PREFIX}/recover/{plan.gen}", 1) == 1:
+            t0 = time.time()
+            while True:
+                ep, live = self.agent.live()
+                if set(plan.members) - set(live) or time.time() - t0 > self.agent.timeout.total_seconds():
+                    break
+                time.sleep(0.2)
+            members = sorted(set(live))
+            self.agent.publish(Plan(plan.gen + 1, members, self._checkpoint_step(), ep, done=not members,
+                                    restore=True))
+        return self.agent.next_plan(plan.gen)
 
     def _check(self, plan: Plan, world: int, rank: int):
         """Collective (same step on every rank): the set of ranks leaving if the membership changes,

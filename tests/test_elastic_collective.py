@@ -6,6 +6,7 @@ import os
 import re
 import socket
 import subprocess
+import sys
 import time
 
 import pytest
@@ -175,3 +176,89 @@ def test_handover_roundtrip_gpu_bf16(gpu):
         torch.testing.assert_close(sd2[k], sd[k], rtol=0, atol=0)
     tr2 = Trainer(spec.model, spec.loss, ps2, spec.make_batch(4, gpu))
     assert torch.isfinite(tr2.step()).item()
+
+
+@pytest.mark.slow
+def test_crash_recovery_from_canonical_checkpoint(tmp_path):
+    """SIGKILL one of 3 ranks mid-run (no hand-over, no deregistration). The
+    survivors' blocked collective fails, the coordinator expires the dead worker, one survivor
+    publishes a restore plan and both rebuild a 2-rank world from the last canonical checkpoint
+    (step 10; the crash is at step 12) and finish all 30 steps. Their final parameters equal an
+    fp32 replay of steps 10..29 with 2 workers starting from that checkpoint."""
+    from parameter_server_distributed_amd import native
+
+    cport = _port()
+    coord = subprocess.Popen([os.path.join(ROOT, "bin", "coordinator"), f"127.0.0.1:{cport}", "127.0.0.1:1",
+                              "--expiry-s", "2", "--sweep-s", "0.3", "--store-port", "0"],
+                             stdout=open(tmp_path / "coord.log", "w"), stderr=subprocess.STDOUT,
+                             env=dict(os.environ, PYTHONPATH=ROOT))
+    procs = []
+    try:
+        ck = str(tmp_path / "ck")
+        steps, kill_at = 30, 12
+        for w in range(3):
+            procs.append(subprocess.Popen(
+                [sys.executable, os.path.join(ROOT, "tests", "elastic_crash_worker.py"), f"127.0.0.1:{cport}", str(w),
+                 str(steps), ck, str(tmp_path / f"w{w}.json"), str(kill_at if w == 2 else -1)],
+                stdout=open(tmp_path / f"w{w}.log", "w"), stderr=subprocess.STDOUT, env=dict(os.environ, PYTHONPATH=ROOT)))
+        rcs = [p.wait(timeout=240) for p in procs]
+        logs = [open(tmp_path / f"w{w}.log").read() for w in range(3)]
+        assert rcs[2] == -9 and rcs[0] == 0 and rcs[1] == 0, (rcs, logs[0][-3000:], logs[1][-3000:])
+        import json
+
+        res = [json.load(open(tmp_path / f"w{w}.json")) for w in (0, 1)]
+        for r in res:
+            assert r["finished_at"] == steps and r["recovered_at"], r
+            assert r["history"][-1][1] == [0, 1] and r["history"][-1][2] == 10, r["history"]
+        got = [torch.load(str(tmp_path / f"w{w}.json.pt"), weights_only=True) for w in (0, 1)]
+        for n in got[0]:
+            assert torch.equal(got[0][n], got[1][n]), n
+        # replay from the checkpoint the survivors restored
+        man, ts = native().load_native_ckpt(os.path.join(ck, "elastic_canonical.psd"))
+        m = json.loads(man)
+        sd = dict(zip(m["keys"], ts))
+        assert m["step"] >= 10
+        torch.manual_seed(0)
+        spec = models.build("mlp", CPU, torch.float32, hidden=64)
+        params = list(spec.model.parameters())
+        off = 0
+        for p in params:
+            p.data.copy_(sd["master"][off:off + p.numel()].view_as(p))
+            off += p.numel()
+        opt = torch.optim.SGD(params, lr=0.05, momentum=0.9, weight_decay=1e-3)
+        off = 0
+        for p in params:
+            opt.state[p]["momentum_buffer"] = sd["state1"][off:off + p.numel()].view_as(p).clone()
+            off += p.numel()
+        batches = [spec.make_batch(16, CPU, seed=1000 + w) for w in (0, 1)]
+        for _ in range(m["step"], steps):
+            grads = [torch.zeros_like(p) for p in params]
+            for x, y in batches:
+                spec.model.zero_grad()
+                spec.loss(spec.model(x), y).backward()
+                for g, p in zip(grads, params):
+                    g += p.grad / 2
+            for p, g in zip(params, grads):
+                p.grad = g
+            opt.step()
+        for n, p in spec.model.named_parameters():
+            torch.testing.assert_close(got[0][n], p.detach(), rtol=1e-5, atol=1e-6, msg=n)
+    finally:
+        for p in procs + [coord]:
+            if p.poll() is None:
+                p.kill()
+
+
+def test_reshard_resets_grad_scale_to_the_new_world():
+    """A canonical state from a W-worker world loaded into another world keeps lr / step / bias
+    corrections but averages over the *new* worker count (a W=3 scale in a 2-worker world made every
+    update 2/3 too small until the crash-recovery replay test caught it)."""
+    spec = _mlp()
+    ps = _ps(spec, 0, 0.05, "momentum")
+    sd = ps.canonical_state(root=0)
+    f = sd["dyn"].view(torch.float32)
+    f[1] = 1.0 / 3.0
+    sd["dyn"][4] = 7
+    ps.load_canonical_state(sd)
+    assert float(ps.dyn.t.view(torch.float32)[1]) == 1.0 / len(ps.worker_ranks)
+    assert int(ps.dyn.t[4]) == 7
