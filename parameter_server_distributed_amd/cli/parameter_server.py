@@ -25,6 +25,8 @@ def main(argv=None):
                     help="reference semantics: first aggregate becomes the params, p -= g (lr 1)")
     ap.add_argument("--coordinator", default="", help="follow live membership from this coordinator")
     ap.add_argument("--ckpt-dir", default=".")
+    ap.add_argument("--resume-latest", action="store_true",
+                    help="load the newest checkpoint_epoch_<N>.ckpt in --ckpt-dir at start (supervised restarts)")
     from ..utils.config import apply_config
 
     apply_config(ap, argv)
@@ -33,7 +35,8 @@ def main(argv=None):
                       weight_decay=a.weight_decay)
     serve(a.listen, a.total_workers, a.checkpoint_interval, device=a.device, optim=opt, mode=a.mode,
           staleness=a.staleness, reference_compat=a.reference_compat, ckpt_dir=a.ckpt_dir,
-          coordinator=a.coordinator or None, staleness_lr_scaling=a.staleness_lr_scaling)
+          coordinator=a.coordinator or None, staleness_lr_scaling=a.staleness_lr_scaling,
+          resume_latest=a.resume_latest)
 
 
 if __name__ == "__main__":

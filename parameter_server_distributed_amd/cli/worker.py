@@ -41,6 +41,11 @@ def main(argv=None):
     ap.add_argument("--pull-dtype", default="bf16")
     ap.add_argument("--check-every", type=int, default=5, help="elastic: membership check period (steps)")
     ap.add_argument("--min-workers", type=int, default=1, help="elastic: workers to wait for at start")
+    ap.add_argument("--elastic-ckpt-dir", default="",
+                    help="elastic: shared directory for canonical checkpoints (crash recovery)")
+    ap.add_argument("--elastic-ckpt-every", type=int, default=0, help="elastic: checkpoint period (steps)")
+    ap.add_argument("--collective-timeout-s", type=float, default=0.0,
+                    help="elastic: bound on any collective of a generation (0: the agent timeout)")
     from ..utils.config import apply_config
 
     apply_config(ap, argv)
@@ -122,7 +127,8 @@ def elastic_main(a) -> int:
               f"world={len(plan.members)}", flush=True)
 
     et = ElasticTrainer(agent, spec.model, make_ps, make_trainer, a.iterations, dev, check_every=a.check_every,
-                        min_workers=a.min_workers, on_step=on_step)
+                        min_workers=a.min_workers, on_step=on_step, checkpoint_dir=a.elastic_ckpt_dir or None,
+                        checkpoint_every=a.elastic_ckpt_every, collective_timeout_s=a.collective_timeout_s)
     et.install_signal_handler()
     t0 = time.time()
     res = et.run()

@@ -218,12 +218,35 @@ class ParameterServerService:
         if m.get("names") == self.core.names():
             self.core.load_state_tensors(ts, int(m["iteration"]), int(m["version"]))
 
+    def resume_latest(self) -> str | None:
+        """Load the newest ``checkpoint_epoch_<N>.ckpt`` (+ its optimizer-state sidecar) found in
+        ``ckpt_dir`` -- a supervised restart (scripts/supervise.sh) comes back with its parameters,
+        where the reference's restart lost them (scripts/scale_workers.sh:137-144)."""
+        import re
+
+        best, path = -1, None
+        for f in os.listdir(self.ckpt_dir) if os.path.isdir(self.ckpt_dir) else []:
+            m = re.fullmatch(r"checkpoint_epoch_(\d+)\.ckpt", f)
+            if m and int(m.group(1)) > best:
+                best, path = int(m.group(1)), os.path.join(self.ckpt_dir, f)
+        if path is None:
+            log.info("resume: no checkpoint in %s, starting fresh", self.ckpt_dir)
+            return None
+        ok, epoch = self.core.load_reference(path)
+        self._load_native_sidecar(path)
+        self._last_epoch = epoch
+        log.info("resumed from %s (epoch %d, iteration %d)", path, epoch, self.core.current_iteration())
+        return path
+
     def stop(self):
         self._stop.set()
 
 
-def serve(listen: str, total_workers: int = 2, checkpoint_interval: int = 10, block: bool = True, **kw):
+def serve(listen: str, total_workers: int = 2, checkpoint_interval: int = 10, block: bool = True,
+          resume_latest: bool = False, **kw):
     svc = ParameterServerService(total_workers, checkpoint_interval, **kw)
+    if resume_latest:
+        svc.resume_latest()
     server = service.make_server(max_workers=max(32, 4 * total_workers + 8))
     service.add_service(server, pb, svc)
     bound = server.add_insecure_port(listen)

@@ -9,6 +9,10 @@ BINARY_PATH=${BINARY_PATH:-$HERE/bin/coordinator}
 LOG_FILE=${LOG_FILE:-/tmp/coordinator.log}
 PID_FILE=${PID_FILE:-/tmp/coordinator.pid}
 echo "starting coordinator on port $COORDINATOR_PORT (parameter server $PS_ADDRESS)" | tee -a "$LOG_FILE"
-nohup "$BINARY_PATH" "0.0.0.0:$COORDINATOR_PORT" "$PS_ADDRESS" $COORDINATOR_FLAGS >> "$LOG_FILE" 2>&1 &
+if [ "${SUPERVISE:-0}" = "1" ]; then  # restart on crash (the reference's systemd Restart=always)
+  nohup "$HERE/scripts/supervise.sh" "$PID_FILE.child" "$BINARY_PATH" "0.0.0.0:$COORDINATOR_PORT" "$PS_ADDRESS" $COORDINATOR_FLAGS >> "$LOG_FILE" 2>&1 &
+else
+  nohup "$BINARY_PATH" "0.0.0.0:$COORDINATOR_PORT" "$PS_ADDRESS" $COORDINATOR_FLAGS >> "$LOG_FILE" 2>&1 &
+fi
 echo $! > "$PID_FILE"
 echo "coordinator started with PID $(cat "$PID_FILE")"

@@ -11,7 +11,12 @@ BINARY_PATH=${BINARY_PATH:-$HERE/bin/parameter_server}
 LOG_FILE=${LOG_FILE:-/tmp/parameter_server.log}
 PID_FILE=${PID_FILE:-/tmp/parameter_server.pid}
 echo "starting parameter server on port $PS_PORT with $TOTAL_WORKERS workers" | tee -a "$LOG_FILE"
-nohup "$BINARY_PATH" "0.0.0.0:$PS_PORT" "$TOTAL_WORKERS" "$CHECKPOINT_INTERVAL" --device "$PS_DEVICE" $PS_FLAGS \
+if [ "${SUPERVISE:-0}" = "1" ]; then  # restart on crash (the reference's systemd Restart=always)
+  nohup "$HERE/scripts/supervise.sh" "$PID_FILE.child" "$BINARY_PATH" "0.0.0.0:$PS_PORT" "$TOTAL_WORKERS" "$CHECKPOINT_INTERVAL" --device "$PS_DEVICE" $PS_FLAGS \
+  --resume-latest >> "$LOG_FILE" 2>&1 &
+else
+  nohup "$BINARY_PATH" "0.0.0.0:$PS_PORT" "$TOTAL_WORKERS" "$CHECKPOINT_INTERVAL" --device "$PS_DEVICE" $PS_FLAGS \
   >> "$LOG_FILE" 2>&1 &
+fi
 echo $! > "$PID_FILE"
 echo "parameter server started with PID $(cat "$PID_FILE")"

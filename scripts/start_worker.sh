@@ -23,6 +23,10 @@ fi
 echo "starting worker $WORKER_ID connecting to coordinator $COORDINATOR_ADDR" | tee -a "$LOG_FILE"
 ARGS=("$COORDINATOR_ADDR" "$WORKER_ID" "$ITERATIONS" "$WORKER_ADDR" "$WORKER_PORT")
 [ -n "$CHECKPOINT_PATH" ] && ARGS+=("$CHECKPOINT_PATH")
-nohup "$BINARY_PATH" "${ARGS[@]}" $WORKER_FLAGS >> "$LOG_FILE" 2>&1 &
+if [ "${SUPERVISE:-0}" = "1" ]; then  # restart on crash (the reference's systemd Restart=always)
+  nohup "$HERE/scripts/supervise.sh" "$PID_FILE.child" "$BINARY_PATH" "${ARGS[@]}" $WORKER_FLAGS >> "$LOG_FILE" 2>&1 &
+else
+  nohup "$BINARY_PATH" "${ARGS[@]}" $WORKER_FLAGS >> "$LOG_FILE" 2>&1 &
+fi
 echo $! > "$PID_FILE"
 echo "worker $WORKER_ID started with PID $(cat "$PID_FILE")"
