@@ -133,7 +133,13 @@ class AsyncPS:
         init = torch.zeros(total, dtype=torch.float32, device=dev)
         for n, p, o, k in layout:
             _flat_view(init, o, p).copy_(p.detach().float())
-        self.params_flat = init.to(param_dtype)
+        # working weights: with S >= 1 two buffers alternate per step, so the pull of step t+1 (DMA
+        # from the owners' publish buffers) runs on a side stream while step t computes
+        self.prefetch = self.S >= 1
+        self.pbufs = [init.to(param_dtype)]
+        if self.prefetch:
+            self.pbufs.append(self.pbufs[0].clone())
+        self.cb = 0
         self.grads = [torch.zeros(total, dtype=param_dtype, device=dev) for _ in range(2)]
         self.gb = 0
         f32 = dict(dtype=torch.float32, device=dev)
@@ -160,14 +166,19 @@ class AsyncPS:
         for b in self.buckets:
             for _, p, _o, _n in b.params:
                 self._p2b[id(p)] = b
-        for n, p, o, k in layout:
-            p.data = _flat_view(self.params_flat, o, p)
+        self._pviews = [[_flat_view(b, o, p) for (_n, p, o, _k) in layout] for b in self.pbufs]
+        for (n, p, o, k), v in zip(layout, self._pviews[0]):
+            p.data = v
         self._set_grad_views()
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for _, p, _o, _n in layout]
         self._next = 0
         if self.is_cuda:
             self.comm_stream = torch.cuda.Stream(device=dev)
+            self.pull_stream = torch.cuda.Stream(device=dev)
             self.push_done = [None, None]
+            self.step_done = [None, None]  # end of a step's work on the compute stream, per buffer
+            self.pull_done = [None, None]
+        self._prefetched = None  # (step, pulled versions) of the pull issued ahead
 
         # ---- native engine: control block (rank 0 creates), memory exchange, initial publish
         _INSTANCE[0] += 1
@@ -265,6 +276,11 @@ class AsyncPS:
             raise RuntimeError(f"AsyncPS {tag} failed: " + "; ".join(errs))
 
     # ------------------------------------------------------------------ helpers
+    @property
+    def params_flat(self) -> torch.Tensor:
+        """The working weights of the current step."""
+        return self.pbufs[self.cb]
+
     def _barrier(self, tag: str):
         if self.world == 1:
             return
@@ -300,7 +316,7 @@ class AsyncPS:
 
     def memory_bytes(self) -> dict:
         eb = lambda t: t.numel() * t.element_size()  # noqa: E731
-        return {"params": eb(self.params_flat), "grads": 2 * eb(self.grads[0]),
+        return {"params": sum(eb(b) for b in self.pbufs), "grads": 2 * eb(self.grads[0]),
                 "master": sum(eb(t) for t in self.master.values()),
                 "state": sum(eb(t) for t in list(self.state1.values()) + list(self.state2.values()))}
 
@@ -308,7 +324,8 @@ class AsyncPS:
     def begin_step(self, track: bool = True):
         if not self.is_worker:
             return
-        self.gb = self.step_idx % 2
+        t = self.step_idx
+        self.gb = t % 2
         if self.is_cuda and self.push_done[self.gb] is not None:
             # the push copies of step t-2 read this gradient buffer
             torch.cuda.current_stream(self.device).wait_event(self.push_done[self.gb])
@@ -317,7 +334,31 @@ class AsyncPS:
         for b in self.buckets:
             b.pending = len(b.params)
         self._next = 0
-        self.pulled = list(self.engine.pull(self.step_idx, self.params_flat, self._stream_ptr()))
+        if self.prefetch:
+            self.cb = t % 2
+            for (_n, p, _o, _k), v in zip(self._layout, self._pviews[self.cb]):
+                p.data = v
+            if self._prefetched is not None and self._prefetched[0] == t:
+                self.pulled = self._prefetched[1]
+                if self.is_cuda:
+                    torch.cuda.current_stream(self.device).wait_event(self.pull_done[self.cb])
+                return
+        self.pulled = list(self.engine.pull(t, self.params_flat, self._stream_ptr()))
+
+    def _prefetch_pull(self, t: int):
+        """Issue the pull of step t (the next one) now: the SSP wait happens on the host here, the
+        DMA on the pull stream, after the step that last used that buffer (t-2) is done with it."""
+        nb = t % 2
+        if self.is_cuda:
+            if self.step_done[nb] is not None:
+                self.pull_stream.wait_event(self.step_done[nb])
+            pulled = self.engine.pull(t, self.pbufs[nb], self.pull_stream.cuda_stream)
+            ev = torch.cuda.Event()
+            ev.record(self.pull_stream)
+            self.pull_done[nb] = ev
+        else:
+            pulled = self.engine.pull(t, self.pbufs[nb], 0)
+        self._prefetched = (t, list(pulled))
 
     def _on_grad(self, p):
         if id(p) in self._direct:
@@ -353,9 +394,14 @@ class AsyncPS:
             ev = torch.cuda.Event()
             ev.record(self.comm_stream)
             self.push_done[self.gb] = ev
+            done = torch.cuda.Event()
+            done.record(torch.cuda.current_stream(self.device))
+            self.step_done[self.cb] = done
         else:
             self.engine.commit(self.step_idx, self.pulled, 0)
         self.step_idx += 1
+        if self.prefetch:
+            self._prefetch_pull(self.step_idx)
 
     def idle_step(self):
         pass
