@@ -102,10 +102,44 @@ def parse():
     ap.add_argument("--ckpt-prefix", default="", help="sharded PS checkpoint path prefix")
     ap.add_argument("--ckpt-every", type=int, default=0, help="checkpoint every N steps (async, off the step)")
     ap.add_argument("--resume", default="", help="load PS shards from this checkpoint prefix before training")
+    ap.add_argument("--comm-probe", type=int, default=1,
+                    help="N > 1 with RCCL: after the timed steps, measure all-reduce / reduce-scatter / all-gather "
+                         "bus bandwidth vs bucket size over xGMI and report it (comm_probe in the JSON)")
     from parameter_server_distributed_amd.utils.config import apply_config
 
     apply_config(ap)
     return ap.parse_args()
+
+
+def comm_probe(dev, world: int, sizes_mb=(1, 4, 16, 64, 256), iters: int = 5) -> dict:
+    """RCCL bus bandwidth (GB/s, NCCL-tests convention) per collective and bucket size on this node
+    -- the measurement behind the bucket-size choice for 7 xGMI links per GPU.
+    Runs outside the timed region, on the already-initialised process group."""
+    out = {}
+    for mb in sizes_mb:
+        n = (mb << 20) // 2 // world * world  # bf16 elements, divisible by the world size
+        x = torch.ones(n, dtype=torch.bfloat16, device=dev)
+        part = torch.empty(n // world, dtype=torch.bfloat16, device=dev)
+        res = {}
+        for name, fn, factor in (
+                ("all_reduce", lambda: dist.all_reduce(x), 2.0 * (world - 1) / world),
+                ("reduce_scatter", lambda: dist.reduce_scatter_tensor(part, x), (world - 1) / world),
+                ("all_gather", lambda: dist.all_gather_into_tensor(x, part), (world - 1) / world)):
+            for _ in range(2):
+                fn()
+            torch.cuda.synchronize(dev)
+            dist.barrier(device_ids=[dev.index])
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                fn()
+            torch.cuda.synchronize(dev)
+            el = (time.perf_counter() - t0) / iters
+            t = torch.tensor([el], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            res[name] = round(n * 2 * factor / float(t.item()) / 1e9, 1)
+        out[f"{mb}MB"] = res
+        del x, part
+    return out
 
 
 def main():
@@ -227,6 +261,12 @@ def main():
             break
     while hist and hist[-1] == 0 and len(hist) > 1:
         hist.pop()
+    probe = None
+    if world > 1 and a.backend == "nccl" and a.comm_probe:
+        try:
+            probe = comm_probe(dev, world)
+        except Exception as e:  # noqa: BLE001 -- a diagnostic must not cost the measurement
+            probe = {"error": str(e)[:200]}
     final_loss = float(loss.float().item()) if loss is not None else float("nan")
     # health of the run: a silent NaN in the weights invalidates a throughput number (round-1 lesson:
     # a bad library GEMM produced NaN weights that a ReLU hid behind a finite loss)
@@ -258,7 +298,7 @@ def main():
                        "pull_dtype": pull_dtype, "tunableop": tunable_mode,
                        "transport": ps.t.name, "hipgraph": bool(tr.graphs), "graph_error": tr.graph_error},
             "staleness_p50": p50, "staleness_hist": hist, "final_loss": round(final_loss, 4),
-            "params_finite": params_finite,
+            "params_finite": params_finite, "comm_probe_busbw_GBps": probe,
             "warmup_s": round(t_w, 2), "peak_mem_gb": round(mem_peak / 2**30, 2),
         }
         line = json.dumps(rec)
