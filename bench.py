@@ -262,6 +262,12 @@ def main():
     while hist and hist[-1] == 0 and len(hist) > 1:
         hist.pop()
     probe = None
+    async_bw = None
+    if mode == "async" and a.comm_probe:
+        try:
+            async_bw = ps.probe_bandwidth()
+        except Exception as e:  # noqa: BLE001
+            async_bw = {"error": str(e)[:200]}
     if world > 1 and a.backend == "nccl" and a.comm_probe:
         try:
             probe = comm_probe(dev, world)
@@ -298,7 +304,7 @@ def main():
                        "pull_dtype": pull_dtype, "tunableop": tunable_mode,
                        "transport": ps.t.name, "hipgraph": bool(tr.graphs), "graph_error": tr.graph_error},
             "staleness_p50": p50, "staleness_hist": hist, "final_loss": round(final_loss, 4),
-            "params_finite": params_finite, "comm_probe_busbw_GBps": probe,
+            "params_finite": params_finite, "comm_probe_busbw_GBps": probe, "async_plane_bw": async_bw,
             "warmup_s": round(t_w, 2), "peak_mem_gb": round(mem_peak / 2**30, 2),
         }
         line = json.dumps(rec)

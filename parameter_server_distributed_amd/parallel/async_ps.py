@@ -417,6 +417,30 @@ class AsyncPS:
         if self.is_cuda:
             torch.cuda.synchronize(self.device)
 
+    def probe_bandwidth(self, reps: int = 3) -> dict:
+        """After ``drain``: time this worker's full push (DMA of the whole gradient into its inbox slot
+        on every owner, no commit) and a full pull (latest snapshots into a scratch buffer) -- the
+        peer-memory data plane's achieved bandwidth on this node (xGMI links at N > 1)."""
+        if not (self.is_worker and self.is_cuda):
+            return {}
+        g = self.grads[0]
+        tmp = torch.empty_like(self.params_flat)
+        st = torch.cuda.current_stream(self.device)
+        out = {}
+        for name, fn in (("push", lambda: self.engine.push(self.step_idx, g, 0, self.total, st.cuda_stream)),
+                         ("pull", lambda: self.engine.pull(0, tmp, st.cuda_stream))):
+            fn()
+            torch.cuda.synchronize(self.device)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(reps):
+                fn()
+            e.record()
+            e.synchronize()
+            ms = s.elapsed_time(e) / reps
+            out[f"{name}_GBps"] = round(self.total * g.element_size() / (ms * 1e-3) / 1e9, 1)
+        return out
+
     def close(self):
         """Collective: stop the engine, unmap the peers' memory, free this rank's (all ranks call)."""
         if self.closed:
