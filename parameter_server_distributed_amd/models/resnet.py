@@ -4,8 +4,11 @@ The worker model for the BASELINE.json ResNet configs (the reference itself has 
 "gradient" is the constant 0.01 on a dummy [10,10] tensor, src/worker.cpp:316-329,346-353).
 
 MI355X layout choices: NHWC (``channels_last``) activations and weights so MIOpen picks its
-NHWC implicit-GEMM convolutions on the MFMA units, bf16 compute, and the 1000-way classifier on
-the hand-written MFMA GEMM (``ops.gemm``) when available. Random init, synthetic data.
+NHWC implicit-GEMM convolutions on the MFMA units, bf16 compute, the stem on our own gfx950
+kernels (ops/conv.py), every BatchNorm (+ residual + ReLU) on the fused NHWC kernels (ops/bn.py),
+1x1 convolutions routed per shape between MIOpen and hipBLASLt (ops/conv.py). The 1000-way
+classifier is a plain ``nn.Linear`` (hipBLASLt; 0.02 ms of an 89 ms step). Random init, synthetic
+data.
 """
 from __future__ import annotations
 

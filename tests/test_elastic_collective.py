@@ -178,8 +178,7 @@ def test_handover_roundtrip_gpu_bf16(gpu):
     assert torch.isfinite(tr2.step()).item()
 
 
-@pytest.mark.slow
-def test_crash_recovery_from_canonical_checkpoint(tmp_path):
+def _crash_recovery(tmp_path, device):
     """SIGKILL one of 3 ranks mid-run (no hand-over, no deregistration). The
     survivors' blocked collective fails, the coordinator expires the dead worker, one survivor
     publishes a restore plan and both rebuild a 2-rank world from the last canonical checkpoint
@@ -199,7 +198,7 @@ def test_crash_recovery_from_canonical_checkpoint(tmp_path):
         for w in range(3):
             procs.append(subprocess.Popen(
                 [sys.executable, os.path.join(ROOT, "tests", "elastic_crash_worker.py"), f"127.0.0.1:{cport}", str(w),
-                 str(steps), ck, str(tmp_path / f"w{w}.json"), str(kill_at if w == 2 else -1)],
+                 str(steps), ck, str(tmp_path / f"w{w}.json"), str(kill_at if w == 2 else -1), device],
                 stdout=open(tmp_path / f"w{w}.log", "w"), stderr=subprocess.STDOUT, env=dict(os.environ, PYTHONPATH=ROOT)))
         rcs = [p.wait(timeout=240) for p in procs]
         logs = [open(tmp_path / f"w{w}.log").read() for w in range(3)]
@@ -241,12 +240,26 @@ def test_crash_recovery_from_canonical_checkpoint(tmp_path):
             for p, g in zip(params, grads):
                 p.grad = g
             opt.step()
+        tol = dict(rtol=1e-5, atol=1e-6) if device == "cpu" else dict(rtol=1e-4, atol=1e-5)
         for n, p in spec.model.named_parameters():
-            torch.testing.assert_close(got[0][n], p.detach(), rtol=1e-5, atol=1e-6, msg=n)
+            torch.testing.assert_close(got[0][n], p.detach(), msg=n, **tol)
     finally:
         for p in procs + [coord]:
             if p.poll() is None:
                 p.kill()
+
+
+@pytest.mark.slow
+def test_crash_recovery_from_canonical_checkpoint(tmp_path):
+    _crash_recovery(tmp_path, "cpu")
+
+
+@pytest.mark.gpu
+def test_crash_recovery_gpu_ranks(tmp_path, gpu):
+    """the multi-rank elastic path on device tensors -- 3 ranks on the one GPU
+    (gloo group over cuda tensors, fused apply kernel on the HBM shards), one SIGKILLed mid-run,
+    survivors restore from the canonical checkpoint and match the fp32 replay."""
+    _crash_recovery(tmp_path, "cuda:0")
 
 
 def test_reshard_resets_grad_scale_to_the_new_world():
