@@ -24,6 +24,7 @@
 #include "common.h"
 #include "launchers_gemm.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace psd {
@@ -46,9 +47,12 @@ __device__ __forceinline__ int mnmaj_off(int k, int col) {  // byte offset in a 
   return (k * ROWS + (col ^ ((k & mask) << 5))) * 2;
 }
 
+// GELU(tanh) = x * sigmoid(2u), u = sqrt(2/pi) (x + 0.044715 x^3): one v_exp_f32 + one v_rcp_f32
+// (x -> -inf: exp -> inf, rcp -> 0, result -0 as the tanh form)
 __device__ __forceinline__ float gelu_tanh(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
+  const float k0 = 2.f * 0.7978845608028654f, k1 = 2.f * 0.7978845608028654f * 0.044715f;
+  const float e = __expf(-x * (k0 + k1 * x * x));
+  return x * __builtin_amdgcn_rcpf(1.f + e);
 }
 
 // Stage loader: each lane moves ROWS*8/256 16-byte chunks global -> registers.
@@ -586,29 +590,45 @@ __device__ __forceinline__ int half_to_tile(int r, int h) {
   return (r / SEG) * (2 * SEG) + h * SEG + (r % SEG);
 }
 
-template <bool KMAJ, int SEG, int ESZ = 2, int PW = 2>
-__device__ __forceinline__ void stage8(const void* __restrict__ srcv, int ld, int nrows, int r0, int k0, int h,
-                                       uint8_t* lds, int wid, int lane) {
-  const uint8_t* src = reinterpret_cast<const uint8_t*>(srcv);  // ld, k0 in elements of ESZ bytes
+// Buffer-descriptor LDS-DMA staging: per piece the lane's byte offset = (scalar tile/k origin) +
+// (per-lane part, loop-invariant); rows past the operand's end fall outside the descriptor's range
+// and load zeros (only garbage rows/cols of C, never stored, depend on them), so no per-lane clamp.
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+// per-lane byte offsets of one operand's pieces (piece i of half h), loop-invariant
+template <bool KMAJ, int SEG, int ESZ, int PW>
+__device__ __forceinline__ void stage8_offsets(int ld, int wid, int lane, uint32_t (*vo)[PW]) {
 #pragma unroll
-  for (int i = 0; i < PW; ++i) {
-    const int piece = i * 8 + wid;  // PW * 8 pieces of 1 KiB per half-tile
-    const uint8_t* gp;
-    if (KMAJ) {  // [128 rows][128 B of k]: a piece is 8 rows x 128 B
-      const int row = piece * 8 + (lane >> 3);
-      const int c = (lane & 7) ^ ((row >> 1) & 7);
-      const int gr = min(r0 + half_to_tile<SEG>(row, h), nrows - 1);
-      gp = src + ((int64_t)gr * ld + k0) * ESZ + c * 16;
-    } else {  // [64 k][128 cols] bf16: a piece is 4 k-rows x 256 B
-      const int k = piece * 4 + (lane >> 4);
-      const int f = (k & 3) | ((k >> 1) & 4);
-      const int col = ((lane & 15) * 8) ^ (f << 4);
-      const int gc = min(r0 + half_to_tile<SEG>(col, h), nrows - 8);
-      gp = src + ((int64_t)(k0 + k) * ld + gc) * ESZ;
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const int piece = i * 8 + wid;  // PW * 8 pieces of 1 KiB per half-tile
+      if (KMAJ) {  // [128 rows][128 B of k]: a piece is 8 rows x 128 B
+        const int row = piece * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ ((row >> 1) & 7);
+        vo[h][i] = (uint32_t)half_to_tile<SEG>(row, h) * (uint32_t)ld * ESZ + c * 16;
+      } else {  // [64 k][128 cols] bf16: a piece is 4 k-rows x 256 B
+        const int k = piece * 4 + (lane >> 4);
+        const int f = (k & 3) | ((k >> 1) & 4);
+        const int col = ((lane & 15) * 8) ^ (f << 4);
+        vo[h][i] = ((uint32_t)k * (uint32_t)ld + half_to_tile<SEG>(col, h)) * ESZ;
+      }
     }
-    __builtin_amdgcn_global_load_lds((const void*)gp, (__attribute__((address_space(3))) void*)(lds + piece * 1024), 16,
-                                     0, 0);
-  }
+}
+template <bool KMAJ, int ESZ, int PW>
+__device__ __forceinline__ void stage8(const void* base, uint32_t bytes, const uint32_t* vo, int ld, int r0, int k0,
+                                       uint8_t* lds, int wid) {
+  // scalar origin of the piece grid (bytes): K-major [rows][ld] at (r0, k0); M/N-major [k][ld] at (k0, r0);
+  // readfirstlane keeps it a separate scalar term (not folded into a per-lane multiply)
+  const uint32_t so = __builtin_amdgcn_readfirstlane(KMAJ ? ((uint32_t)r0 * (uint32_t)ld + (uint32_t)k0) * ESZ
+                                                          : ((uint32_t)k0 * (uint32_t)ld + (uint32_t)r0) * ESZ);
+  const rsrc_t src = make_rsrc(base, bytes);  // wave-uniform (kernel arguments)
+#pragma unroll
+  for (int i = 0; i < PW; ++i)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(src, (__attribute__((address_space(3))) void*)(lds + (i * 8 + wid) * 1024),
+                                             16, vo[i] + so, 0, 0, 0);
 }
 
 // 16x16x32 fragment: lane holds row/col (rb*16 + lane&15), k = ks*32 + 8*(lane>>4) + 0..7
@@ -641,9 +661,8 @@ __device__ __forceinline__ i32x8 frag8_f8(const uint8_t* lds, int rb, int lane) 
 
 template <int N>
 __device__ __forceinline__ void wait_vm() {
-  if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-  else static_assert(N == 6 || N == 5, "vmcnt");
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 template <int N>
 __device__ __forceinline__ void wait_lgkm() {
@@ -703,6 +722,16 @@ __device__ __forceinline__ void tile_of(int wg, int tiles_m, int tiles_n, int& t
 // F8: A [M][K] and B [N][K] OCP e4m3 (K-major only), K-tile = 128, MX-scaled
 // v_mfma_scale_f32_16x16x128_f8f6f4 with unit block scales (2x the bf16 MFMA rate); the per-tensor
 // dequant factors *a_scale * *b_scale are applied in the epilogue.
+//
+// Persistent: a grid of G <= tiles workgroups (one per CU, LDS-limited), workgroup b owns the tiles
+// v = b, b + G, b + 2G, ... (xcd_remap keeps v % 8 = the XCD, so each XCD walks a contiguous tile
+// range). The K-tiles of consecutive output tiles form ONE stream: the two stages the 8-phase loop
+// issues past the end of a tile are the next tile's first two K-tiles, so the LDS pipeline never
+// drains between tiles. The epilogue therefore cannot stage C through the pipeline LDS (both buffers
+// hold the next tile): each quad of lanes transposes its 4x4 C block in registers (quad_t4); fp32
+// goes out as 16-byte row segments, bf16 through a per-wave 4 KiB LDS slot (whole 128-byte rows
+// per store); the stores drain while the next tile's first phases run (retired by the first
+// phase-3 vmcnt, in issue order).
 template <int BM>
 struct P8 {
   static constexpr int IM = BM / 64;         // 16-row blocks per quadrant
@@ -712,10 +741,21 @@ struct P8 {
   static constexpr int PWA = HA / 8192;      // A DMA pieces per wave per half-tile
   static constexpr int VM = 4 + PWA;         // DMA in flight after phase 3 (three half-tiles)
   static constexpr int BUF = 2 * HA + 2 * HB;
-  static constexpr int LDS = (2 * BUF > BM * kBigLdc * 2) ? 2 * BUF : BM * kBigLdc * 2;
+  static constexpr int STG = 4096;           // per-wave epilogue staging (16 rows x 64 cols, C + aux)
+  static constexpr int LDS = 2 * BUF + 8 * STG;
 };
 
-template <int BM, bool AK, bool BKM, int MODE, bool F8 = false>
+template <int ACT>
+__device__ __forceinline__ float act_apply(float x) {
+  if constexpr (ACT == 1) return relu_nan(x);
+  else if constexpr (ACT == 2) return gelu_tanh(x);
+  else return x;
+}
+
+// ACT: the epilogue activation as a template parameter (g.act must match): per-element branches made
+// the unrolled epilogue several times larger, and at one output tile per ~10 K-tiles its instruction
+// fetch, not its arithmetic, was the cost.
+template <int BM, bool AK, bool BKM, int MODE, bool F8 = false, int ACT = 0>
 __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
   static_assert(!F8 || (AK && BKM), "fp8 GEMM takes K-major operands");
   static_assert(BM == 256 || AK, "BM = 128 takes a K-major A");
@@ -726,16 +766,21 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int tiles_n = (g.N + kBig - 1) / kBig;
   const int tiles_m = (g.M + BM - 1) / BM;
-  const int wg = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  int tm, tn;
-  tile_of(wg, tiles_m, tiles_n, tm, tn);
-  const int m0 = tm * BM, n0 = tn * kBig;
+  const int ntiles = tiles_m * tiles_n;
+  const int G = gridDim.x;
+  const int ntl = (ntiles - (int)blockIdx.x + G - 1) / G;  // this workgroup's tiles (>= 1: G <= ntiles)
+  auto origin = [&](int j, int& m0, int& n0) {
+    int tm, tn;
+    tile_of(xcd_remap(blockIdx.x + j * G, ntiles), tiles_m, tiles_n, tm, tn);
+    m0 = tm * BM;
+    n0 = tn * kBig;
+  };
   int kbeg = 0, kend = g.K;
   if (MODE == 1) {
     kbeg = blockIdx.z * g.k_per_split;
     kend = min(g.K, kbeg + g.k_per_split);
   }
-  const int nt = (kend - kbeg) / KT;
+  const int nt = (kend - kbeg) / KT;  // >= 2 whenever G < ntiles (host contract)
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wid >> 2, wc = wid & 3;
@@ -744,23 +789,32 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
 #pragma unroll
   for (int i = 0; i < 8 * IM; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto half = [&](int t, int idx) {  // idx: 0/1 A-half, 2/3 B-half
-    return smem + (t & 1) * P::BUF + (idx < 2 ? idx * P::HA : 2 * P::HA + (idx - 2) * P::HB);
+  int jt = 0, base = 0;  // current tile (local index) and its first K-tile in the stream
+  int cm0, cn0, xm0, xn0;
+  origin(0, cm0, cn0);
+  xm0 = cm0;
+  xn0 = cn0;
+  if (ntl > 1) origin(1, xm0, xn0);
+  auto half = [&](int u, int idx) {  // idx: 0/1 A-half, 2/3 B-half; u = K-tile index in the stream
+    return smem + (u & 1) * P::BUF + (idx < 2 ? idx * P::HA : 2 * P::HA + (idx - 2) * P::HB);
   };
-  auto kofs = [&](int t) { return kbeg + min(t, nt - 1) * KT; };
-  auto stA = [&](int t, int h) {
-    stage8<AK, P::QA, ESZ, P::PWA>(g.A, g.lda, g.M, m0, kofs(t), h, half(t, h), wid, lane);
-  };
-  auto stB = [&](int t, int h) { stage8<BKM, 32, ESZ, 2>(g.B, g.ldb, g.N, n0, kofs(t), h, half(t, 2 + h), wid, lane); };
-
+  // operand extents in bytes (host contract: < 2^32): K-major [rows][ld], M/N-major [K][ld]
+  const uint32_t bytesA = AK ? ((uint32_t)(g.M - 1) * g.lda + g.K) * ESZ : ((uint32_t)(g.K - 1) * g.lda + g.M) * ESZ;
+  const uint32_t bytesB = BKM ? ((uint32_t)(g.N - 1) * g.ldb + g.K) * ESZ : ((uint32_t)(g.K - 1) * g.ldb + g.N) * ESZ;
+  uint32_t voA[2][P::PWA], voB[2][2];  // [half][piece]
+  stage8_offsets<AK, P::QA, ESZ, P::PWA>(g.lda, wid, lane, voA);
+  stage8_offsets<BKM, 32, ESZ, 2>(g.ldb, wid, lane, voB);
+  auto stA = [&](int u, int m0, int k, int h) { stage8<AK, ESZ, P::PWA>(g.A, bytesA, voA[h], g.lda, m0, k, half(u, h), wid); };
+  auto stB = [&](int u, int n0, int k, int h) { stage8<BKM, ESZ, 2>(g.B, bytesB, voB[h], g.ldb, n0, k, half(u, 2 + h), wid); };
   if (nt > 0) {
-    stB(0, 0);
-    stA(0, 0);
-    stB(0, 1);
-    stA(0, 1);
-    stB(1, 0);
-    stA(1, 0);
-    stB(1, 1);
+    const int k1 = kbeg + min(1, nt - 1) * KT;  // nt = 1: a split of one K-tile re-stages it
+    stB(0, cn0, kbeg, 0);
+    stA(0, cm0, kbeg, 0);
+    stB(0, cn0, kbeg, 1);
+    stA(0, cm0, kbeg, 1);
+    stB(1, cn0, k1, 0);
+    stA(1, cm0, k1, 0);
+    stB(1, cn0, k1, 1);
     wait_vm<P::VM>();  // tile 0 landed (this wave's DMA)
   }
   __builtin_amdgcn_s_barrier();
@@ -815,126 +869,191 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
   };
   // A reads of phase 0 (issued after the B reads): what may stay in flight at its lgkmcnt
   constexpr int kAReads = (AK ? 2 : 4) * IM;
+  // epilogue geometry: 16x16 C layout, col = lane&15, row = 4*(lane>>4) + r; after quad_t4 every
+  // lane owns 4 consecutive columns of one row
+  const int cl = lane & 15, rq = (lane >> 4) * 4;
+  const int L = cl & 3;
+  auto mrow = [&](int qm, int i) { return wr * (BM / 2) + qm * P::QA + i * 16 + rq + L; };
+  auto ncol = [&](int qn, int j) { return wc * 64 + qn * 32 + j * 16 + (cl & ~3); };
 
-  for (int t = 0; t < nt; ++t) {
+  // VMEM stores of one tile's epilogue, per lane, in both output paths (exact: every store is
+  // issued unconditionally, out-of-range rows/cols go to an offset outside the buffer descriptor)
+  constexpr int kEpiStores = 8 * IM;
+  // One K-tile of the 8-phase schedule at stream index u (= base + t); (am1, ak1) is the A source
+  // of K-tile u+1, (am2, bn2, ak2) the A/B sources of K-tile u+2. first: the K-tile right after an
+  // epilogue, whose phase-0 DMA was issued before the epilogue's stores; its phase-3 wait leaves
+  // those stores in flight (they are older than K-tile u+2's DMA only)
+  auto kstep = [&](int u, int am1, int ak1, int am2, int bn2, int ak2, bool first) {
     // ---- phase 0: q(0,0)
-    readB(half(t, 2), b0, fb0);
+    readB(half(u, 2), b0, fb0);
     __builtin_amdgcn_sched_barrier(0);
-    readA(half(t, 0), a0, fa0);
-    stA(t + 1, 1);
+    readA(half(u, 0), a0, fa0);
+    if (!first) stA(u + 1, am1, ak1, 1);
     wait_lgkm<kAReads>();  // retires every B(qn0) read (lgkmcnt saturates at 15)
     __builtin_amdgcn_sched_barrier(0);
     PSD_SYNC_OPEN()
     quad(0, a0, b0, fa0, fb0);
     PSD_SYNC_CLOSE()
     // ---- phase 1: q(0,1)
-    readB(half(t, 3), b1, fb1);
-    stB(t + 2, 0);
+    readB(half(u, 3), b1, fb1);
+    stB(u + 2, bn2, ak2, 0);
     __builtin_amdgcn_sched_barrier(0);
     PSD_SYNC_OPEN()
     quad(1, a0, b1, fa0, fb1);
     PSD_SYNC_CLOSE()
     // ---- phase 2: q(1,0)
-    readA(half(t, 1), a1, fa1);
-    stA(t + 2, 0);
+    readA(half(u, 1), a1, fa1);
+    stA(u + 2, am2, ak2, 0);
     __builtin_amdgcn_sched_barrier(0);
     PSD_SYNC_OPEN()
     quad(2, a1, b0, fa1, fb0);
     PSD_SYNC_CLOSE()
     // ---- phase 3: q(1,1)
-    stB(t + 2, 1);
-    wait_vm<P::VM>();  // tile t+1 complete (its A-half1 was staged in phase 0)
+    stB(u + 2, bn2, ak2, 1);
+    if (first)
+      wait_vm<P::VM + kEpiStores>();  // K-tile u+1 complete; the epilogue stores may still drain
+    else
+      wait_vm<P::VM>();  // K-tile u+1 complete (its A-half1 was staged in phase 0)
     __builtin_amdgcn_sched_barrier(0);
     PSD_SYNC_OPEN()
     quad(3, a1, b1, fa1, fb1);
     PSD_SYNC_CLOSE()
+  };
+
+  // output descriptors (host contract: extents < 2^32 bytes, N % 8 == 0, ldc % 8 == 0)
+  constexpr uint32_t kOOB = 0xFFFFFFF0u;  // an offset past every descriptor's range: store dropped
+  const bool f32out = MODE == 1 || g.c_f32;
+  uint8_t* cbase = reinterpret_cast<uint8_t*>(g.C) + (MODE == 1 ? (int64_t)blockIdx.z * g.M * g.N * 4 : 0);
+  const int ldo = MODE == 1 ? g.N : g.ldc;
+  const uint32_t cbytes = (g.dbg & 1) ? 0u : ((uint32_t)(g.M - 1) * ldo + g.N) * (f32out ? 4 : 2);
+  const bool want_aux = MODE == 0 && ACT == 2 && g.aux;
+  uint8_t* stg = smem + 2 * P::BUF + wid * P::STG;  // this wave's epilogue staging slot
+  float fmul = 1.f;
+  if constexpr (F8) {
+    fmul = *g.a_scale * *g.b_scale;
+    asm volatile("" ::"v"(fmul));  // materialise now (a load left to the epilogue would drain the DMA there)
+  }
+
+  for (; jt < ntl; ++jt) {
+    // bias of the wave's 64 columns -> the head of its (idle) staging slot by LDS-DMA, 4 B per lane
+    // (columns past N load zeros); retired by the K loop's own counted waits (older than its DMA,
+    // nt >= 2) and read back at the epilogue. A register load would make the compiler wait for it,
+    // and with it every older store and DMA, right here.
+    if (MODE == 0 && g.bias)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(make_rsrc(g.bias, (uint32_t)g.N * 2),
+                                               (__attribute__((address_space(3))) void*)stg, 4,
+                                               (uint32_t)(cn0 + wc * 64 + 2 * lane) * 2, 0, 0, 0);
+    // K-tiles nt, nt+1 of this tile's stream = the next tile's first two K-tiles (past the
+    // workgroup's last tile: the last valid K-tile again, same DMA count, never read)
+    const bool more = jt + 1 < ntl;
+    const int sm0 = more ? xm0 : cm0, sn0 = more ? xn0 : cn0;
+    const int sk0 = more ? kbeg : kbeg + max(nt - 1, 0) * KT;
+    const int sk1 = more ? kbeg + min(1, nt - 1) * KT : sk0;
+    for (int t = 0; t < nt; ++t) {  // uniform scalar selects, no branches in the K loop
+      const int d1 = t + 1 - nt, d2 = t + 2 - nt;
+      const int am1 = d1 >= 0 ? sm0 : cm0;
+      const int ak1 = d1 >= 0 ? sk0 : kbeg + (t + 1) * KT;
+      const int am2 = d2 >= 0 ? sm0 : cm0, bn2 = d2 >= 0 ? sn0 : cn0;
+      const int ak2 = d2 > 0 ? sk1 : (d2 == 0 ? sk0 : kbeg + (t + 2) * KT);
+      kstep(base + t, am1, ak1, am2, bn2, ak2, jt > 0 && t == 0);
+    }
+    // the next tile's first K-tile issues its phase-0 DMA (A-half1 of its K-tile 1) here, BEFORE
+    // the stores below, so that its phase-3 wait can leave the stores in flight (nt >= 2 whenever
+    // a workgroup has more than one tile)
+    if (more) stA(base + nt + 1, xm0, kbeg + KT, 1);
+
+    // ---- epilogue of tile jt (no barrier: the pipeline LDS already holds the next tile)
+    float bv[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+    if (MODE == 0 && g.bias) {
+#pragma unroll
+      for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bv[qn][j] = bf16_to_f32(reinterpret_cast<const uint16_t*>(stg)[qn * 32 + j * 16 + cl]);
+    }
+    if constexpr (F8) {
+#pragma unroll
+      for (int i = 0; i < 8 * IM; ++i) acc[i] *= fmul;
+    }
+    const rsrc_t rc = make_rsrc(cbase, cbytes);
+    if (g.dbg & 2) {
+    } else if (f32out) {  // fp32: 16-byte row segments straight from registers
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int n = cn0 + ncol(q & 1, j);
+#pragma unroll
+          for (int i = 0; i < IM; ++i) {
+            float w[4];
+            quad_t4(acc[(q * IM + i) * 2 + j] + bv[q & 1][j], L, w);
+            const int m = cm0 + mrow(q >> 1, i);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) w[e] = act_apply<ACT>(w[e]);
+            const uint32_t off = (m < g.M && n < g.N) ? ((uint32_t)m * ldo + n) * 4 : kOOB;
+            __builtin_amdgcn_raw_buffer_store_b128(
+                u32x4{__float_as_uint(w[0]), __float_as_uint(w[1]), __float_as_uint(w[2]), __float_as_uint(w[3])},
+                rc, off, 0, 0);
+          }
+        }
+    } else {
+      // bf16: each wave stages its 128x64 (BM 256) / 64x64 C block 16 rows at a time through its
+      // own 4 KiB of LDS (no barrier: one wave's LDS ops complete in order), so the global stores
+      // are 16-byte lanes covering whole 128-byte row segments. Staging image: [16 rows][128 B],
+      // 8-byte column group g stored at g ^ 2*(row & 7) (conflict-spreading; keeps 16-byte pairs).
+      // The GELU pre-activation (aux) goes through the second 2 KiB; without aux its stores are
+      // issued against an empty descriptor (dropped) to keep the store count exact.
+      const rsrc_t ra = make_rsrc(want_aux ? g.aux : g.C, want_aux ? cbytes : 0u);
+      const int rrow = lane >> 3, c16 = lane & 7;  // read side: 8 rows x 8 16-byte chunks per pass
+#pragma unroll
+      for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+        for (int i = 0; i < IM; ++i) {
+          const int r = rq + L;  // this lane's row within the 16-row block (after quad_t4)
+#pragma unroll
+          for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              float w[4];
+              quad_t4(acc[((qm * 2 + qn) * IM + i) * 2 + j] + bv[qn][j], L, w);
+              const int gcol = (qn * 32 + j * 16 + (cl & ~3)) >> 2;  // 8-byte group 0..15
+              const int off = r * 128 + ((gcol ^ ((r & 7) << 1)) << 3);
+              // inline-asm LDS writes: a plain store would make the compiler wait for every
+              // LDS-DMA in flight (it cannot tell this slot from the pipeline buffers)
+              const uint32_t la = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)(stg + off);
+              if (want_aux) {
+                const uint64_t pa = (uint64_t)pack_bf16x2(w[0], w[1]) | ((uint64_t)pack_bf16x2(w[2], w[3]) << 32);
+                asm volatile("ds_write_b64 %0, %1 offset:2048" ::"v"(la), "v"(pa) : "memory");
+              }
+#pragma unroll
+              for (int e = 0; e < 4; ++e) w[e] = act_apply<ACT>(w[e]);
+              const uint64_t pc = (uint64_t)pack_bf16x2(w[0], w[1]) | ((uint64_t)pack_bf16x2(w[2], w[3]) << 32);
+              asm volatile("ds_write_b64 %0, %1" ::"v"(la), "v"(pc) : "memory");
+            }
+          const int mb = cm0 + wr * (BM / 2) + qm * P::QA + i * 16;
+          const int n = cn0 + wc * 64 + c16 * 8;
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            const int rr = k * 8 + rrow;
+            const int off = rr * 128 + (((2 * c16) ^ ((rr & 7) << 1)) << 3);
+            const int m = mb + rr;
+            const u32x4 v = *reinterpret_cast<const u32x4*>(stg + off);
+            const u32x4 va = *reinterpret_cast<const u32x4*>(stg + 2048 + off);
+            const uint32_t go = (m < g.M && n < g.N) ? ((uint32_t)m * ldo + n) * 2 : kOOB;
+            __builtin_amdgcn_raw_buffer_store_b128(v, rc, go, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(va, ra, go, 0, 0);
+          }
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staging reads retired: clean lgkm count
+#pragma unroll
+    for (int i = 0; i < 8 * IM; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    base += nt;
+    cm0 = xm0;
+    cn0 = xn0;
+    if (jt + 2 < ntl) origin(jt + 2, xm0, xn0);
   }
   if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the two wave rows
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();  // all DMA landed and all reads done: the epilogue reuses the LDS
-
-  // epilogue: 16x16 C layout, col = lane&15, row = 4*(lane>>4) + r
-  if constexpr (F8) {
-    const float mul = *g.a_scale * *g.b_scale;
-#pragma unroll
-    for (int i = 0; i < 8 * IM; ++i) acc[i] *= mul;
-  }
-  const int cl = lane & 15, rq = (lane >> 4) * 4;
-  // Each quad of lanes (4 consecutive columns x the same 4 rows) is transposed in registers with
-  // two DPP exchanges, so every lane owns 4 consecutive columns of one row: 16-B fp32 / 8-B bf16
-  // stores instead of 4-B / 2-B scatters.
-  const int L = cl & 3;
-  auto mrow = [&](int qm, int i) { return wr * (BM / 2) + qm * P::QA + i * 16 + rq + L; };
-  auto ncol = [&](int qn, int j) { return wc * 64 + qn * 32 + j * 16 + (cl & ~3); };
-  auto bias_of = [&](int n) {
-    return (MODE == 0 && g.bias && n < g.N) ? bf16_to_f32(reinterpret_cast<const uint16_t*>(g.bias)[n]) : 0.f;
-  };
-  if (MODE == 1 || g.c_f32) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int n = n0 + ncol(q & 1, j);
-        const float bias = bias_of(n0 + wc * 64 + (q & 1) * 32 + j * 16 + cl);
-#pragma unroll
-        for (int i = 0; i < IM; ++i) {
-          float w[4];
-          quad_t4(acc[(q * IM + i) * 2 + j] + bias, L, w);
-          const int m = m0 + mrow(q >> 1, i);
-          if (m >= g.M || n >= g.N) continue;
-          float* o;
-          if (MODE == 1) {
-            o = reinterpret_cast<float*>(g.C) + (int64_t)blockIdx.z * g.M * g.N + (int64_t)m * g.N + n;
-          } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) w[e] = g.act == 1 ? relu_nan(w[e]) : (g.act == 2 ? gelu_tanh(w[e]) : w[e]);
-            o = reinterpret_cast<float*>(g.C) + (int64_t)m * g.ldc + n;
-          }
-          if (n + 4 <= g.N && (reinterpret_cast<uintptr_t>(o) & 15) == 0)
-            *reinterpret_cast<f32x4*>(o) = f32x4{w[0], w[1], w[2], w[3]};
-          else
-            for (int e = 0; e < 4 && n + e < g.N; ++e) o[e] = w[e];
-        }
-      }
-    return;
-  }
-  uint16_t* cs = reinterpret_cast<uint16_t*>(smem);
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int nl = ncol(q & 1, j);
-      const int n = n0 + nl;
-      const float bias = bias_of(n0 + wc * 64 + (q & 1) * 32 + j * 16 + cl);
-#pragma unroll
-      for (int i = 0; i < IM; ++i) {
-        float w[4];
-        quad_t4(acc[(q * IM + i) * 2 + j] + bias, L, w);
-        const int ml = mrow(q >> 1, i);
-        if (g.act == 2 && g.aux && m0 + ml < g.M && n < g.N) {  // pre-activation for the GELU backward
-          uint16_t* ax = reinterpret_cast<uint16_t*>(g.aux) + (int64_t)(m0 + ml) * g.ldc + n;
-          if (n + 4 <= g.N && (reinterpret_cast<uintptr_t>(ax) & 7) == 0)
-            *reinterpret_cast<uint2*>(ax) = uint2{pack_bf16x2(w[0], w[1]), pack_bf16x2(w[2], w[3])};
-          else
-            for (int e = 0; e < 4 && n + e < g.N; ++e) ax[e] = f32_to_bf16(w[e]);
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) w[e] = g.act == 1 ? relu_nan(w[e]) : (g.act == 2 ? gelu_tanh(w[e]) : w[e]);
-        *reinterpret_cast<uint2*>(cs + ml * kBigLdc + nl) = uint2{pack_bf16x2(w[0], w[1]), pack_bf16x2(w[2], w[3])};
-      }
-    }
-  __syncthreads();
-  for (int c = threadIdx.x; c < BM * (kBig / 8); c += 512) {
-    const int ml = c >> 5, nl = (c & 31) * 8;
-    const int m = m0 + ml, n = n0 + nl;
-    if (m >= g.M || n >= g.N) continue;
-    uint16_t* o = reinterpret_cast<uint16_t*>(g.C) + (int64_t)m * g.ldc + n;
-    const uint16_t* src = cs + ml * kBigLdc + nl;
-    if (n + 8 <= g.N && ((reinterpret_cast<uintptr_t>(o) & 15) == 0))
-      *reinterpret_cast<u32x4*>(o) = *reinterpret_cast<const u32x4*>(src);
-    else
-      for (int e = 0; e < 8 && n + e < g.N; ++e) o[e] = src[e];
-  }
 }
 #undef PSD_SYNC_OPEN
 #undef PSD_SYNC_CLOSE
@@ -1085,19 +1204,54 @@ static int big_variant() {
   return v;
 }
 
-template <int BM, bool AK, bool BKM, int MODE, bool F8 = false>
-static hipError_t launch_8p(const GemmArgs& g, int splits, hipStream_t st) {
+// workgroups of the persistent 8-phase grid: one per CU (the kernel's LDS allows no second);
+// PSD_GEMM_PERSIST=0 launches one workgroup per tile instead
+static int persistent_grid() {
+  static const int n = [] {
+    const char* e = getenv("PSD_GEMM_PERSIST");
+    if (e && atoi(e) == 0) return 1 << 30;
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      return 1 << 30;
+    return cus;
+  }();
+  return n;
+}
+
+template <int BM, bool AK, bool BKM, int MODE, bool F8, int ACT>
+static hipError_t launch_8p_act(const GemmArgs& g, int splits, hipStream_t st) {
   constexpr int lds = P8<BM>::LDS;
   static bool attr_set = false;  // per instantiation: set the >64 KiB LDS limit once
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm8p_kernel<BM, AK, BKM, MODE, F8>,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
   const int nwg = ((g.M + BM - 1) / BM) * ((g.N + kBig - 1) / kBig);
-  hipLaunchKernelGGL((gemm8p_kernel<BM, AK, BKM, MODE, F8>), dim3(nwg, 1, splits), dim3(512), lds, st, g);
+  // persistent grid (one workgroup per CU) for the single-split GEMMs; the kernel needs >= 2
+  // K-tiles per tile to run tiles back to back (big_ok guarantees K >= 256)
+  constexpr int KT = F8 ? 128 : BK;
+  int grid = nwg;
+  if (MODE == 0 && splits == 1 && g.K / KT >= 2) grid = std::min(nwg, persistent_grid());
+  static const int dbg = [] {
+    const char* e = getenv("PSD_GEMM_DBG");
+    return e ? atoi(e) : 0;
+  }();
+  GemmArgs ga = g;
+  ga.dbg = dbg;
+  hipLaunchKernelGGL((gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT>), dim3(grid, 1, splits), dim3(512), lds, st, ga);
   return hipGetLastError();
+}
+
+template <int BM, bool AK, bool BKM, int MODE, bool F8 = false>
+static hipError_t launch_8p(const GemmArgs& g, int splits, hipStream_t st) {
+  if constexpr (MODE == 0) {
+    if (g.act == 1) return launch_8p_act<BM, AK, BKM, MODE, F8, 1>(g, splits, st);
+    if (g.act == 2) return launch_8p_act<BM, AK, BKM, MODE, F8, 2>(g, splits, st);
+  }
+  return launch_8p_act<BM, AK, BKM, MODE, F8, 0>(g, splits, st);
 }
 
 // 8-phase tile height: a 128x256 tile costs ~0.55 of a 256x256 one, so narrow problems (few
@@ -1137,9 +1291,21 @@ static hipError_t launch_big(const GemmArgs& g, int splits, hipStream_t st) {
   return hipGetLastError();
 }
 
+// the 8-phase kernel addresses each operand through a buffer descriptor with 32-bit byte offsets
+static bool fits_rsrc(const GemmArgs& g, int esz) {
+  const int64_t a = g.a_kmajor ? (int64_t)(g.M - 1) * g.lda + g.K : (int64_t)(g.K - 1) * g.lda + g.M;
+  const int64_t b = g.b_kmajor ? (int64_t)(g.N - 1) * g.ldb + g.K : (int64_t)(g.K - 1) * g.ldb + g.N;
+  const int64_t c = (int64_t)(g.M - 1) * (g.k_per_split > 0 ? g.N : g.ldc) + g.N;  // C / one split-K slab
+  return a * esz < (int64_t)1 << 32 && b * esz < (int64_t)1 << 32 && c * 4 < (int64_t)1 << 32;
+}
+
 static bool big_ok(const GemmArgs& g, int kseg) {
   // enough big tiles to fill the chip, no K tail inside a stage, MN-major operands 8-aligned
   if (getenv("PSD_GEMM_SMALL_ONLY")) return false;
+  if (big_variant() == 2 && !fits_rsrc(g, 2)) return false;
+  // 8-phase epilogue: 16-byte stores of 8 bf16 / 4 fp32 columns, whole or dropped
+  if (big_variant() == 2 && (g.N % 8 != 0 || (g.k_per_split == 0 && g.ldc % 8 != 0))) return false;
+  if (big_variant() == 2 && (reinterpret_cast<uintptr_t>(g.bias) & 3)) return false;  // bias: dword LDS-DMA
   const int splits = g.k_per_split > 0 ? (g.K + g.k_per_split - 1) / g.k_per_split : 1;
   if (big_variant() == 2) {  // 8-phase: BM 128 or 256, BN 256
     const int bm = pick_bm(g.M, g.N, splits, g.a_kmajor);
@@ -1171,7 +1337,9 @@ hipError_t launch_gemm(const GemmArgs& g, hipStream_t st) {
 
 hipError_t launch_gemm_fp8(const GemmArgs& g, hipStream_t st) {
   if (g.M <= 0 || g.N <= 0) return hipSuccess;
-  if (g.K % 128 != 0 || !g.a_kmajor || !g.b_kmajor || !g.a_scale || !g.b_scale) return hipErrorInvalidValue;
+  if (g.K % 128 != 0 || !g.a_kmajor || !g.b_kmajor || !g.a_scale || !g.b_scale || !fits_rsrc(g, 1) ||
+      g.N % 8 != 0 || g.ldc % 8 != 0 || (reinterpret_cast<uintptr_t>(g.bias) & 3))
+    return hipErrorInvalidValue;
   return pick_bm(g.M, g.N, 1) == 128 ? launch_8p<128, true, true, 0, true>(g, 1, st)
                                      : launch_8p<256, true, true, 0, true>(g, 1, st);
 }

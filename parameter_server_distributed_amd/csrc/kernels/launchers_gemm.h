@@ -19,6 +19,7 @@ struct GemmArgs {
   int k_per_split;
   const float* a_scale;  // fp8 GEMM: dequant factors (device scalars), else unused
   const float* b_scale;
+  int dbg;  // timing experiments (PSD_GEMM_DBG): 1 drop the C stores, 2 skip the epilogue; 0 in production
 };
 
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t stream);

@@ -124,8 +124,39 @@ def test_gemm_256_splitk_exact(gpu):
     torch.testing.assert_close(out.cpu(), ref, rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, False), (False, True)],
+                         ids=["NT", "NN", "TN", "TT"])
+@pytest.mark.parametrize("shape", [(8264, 2104, 320), (16384, 4096, 256), (4160, 8448, 576)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_gemm_persistent_multi_tile_exact(gpu, a_k, b_k, shape):
+    """More tiles than CUs: each persistent workgroup runs several tiles back to back, the next tile's
+    first K-tiles staged during the previous one (odd K-tile counts flip the LDS buffer parity at
+    the seam; ragged M/N clamp rows of the NEXT tile's stages)."""
+    M, N, K = shape
+    A, B, ref = _ops(M, N, K, a_k, b_k, gpu, seed=17)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
+    native().gemm_(A, B, a_k, b_k, out)
+    torch.testing.assert_close(out.float().cpu(), ref.bfloat16().float(), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("act", [0, 1, 2], ids=["none", "relu", "gelu"])
+def test_gemm_persistent_bias_act_epilogue(gpu, act):
+    M, N, K = 8192, 3072, 256  # 384 tiles of 256x256: > 1 tile per workgroup
+    A, B, ref = _ops(M, N, K, True, True, gpu, ints=False, seed=19)
+    bias = torch.randn(N).to(torch.bfloat16)
+    z = ref + bias.float()
+    want = {0: z, 1: torch.relu(z), 2: torch.nn.functional.gelu(z, approximate="tanh")}[act]
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
+    aux = torch.empty(M, N, dtype=torch.bfloat16, device=gpu) if act == 2 else None
+    native().gemm_(A, B, True, True, out, bias.to(gpu), act, aux)
+    torch.testing.assert_close(out.float().cpu(), want, rtol=2e-2, atol=2e-2)
+    if aux is not None:
+        torch.testing.assert_close(aux.float().cpu(), z, rtol=2e-2, atol=2e-2)
+
+
 # ---------------------------------------------------------------- fp8 (OCP e4m3fn) forward GEMM
-@pytest.mark.parametrize("shape", [(2048, 2048, 512), (300, 520, 256), (4096, 768, 3072)],
+@pytest.mark.parametrize("shape", [(2048, 2048, 512), (300, 520, 256), (4096, 768, 3072), (8192, 8192, 256),
+                                   (8320, 4352, 384)],
                          ids=lambda s: "x".join(map(str, s)))
 def test_gemm_fp8_exact_small_ints(gpu, shape):
     """Small integers are exact in e4m3: the MX-scaled fp8 MFMA must reproduce the fp32 product."""

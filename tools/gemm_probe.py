@@ -62,19 +62,24 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default="all", choices=["bert", "square", "all"])
     ap.add_argument("--it", type=int, default=20)
+    ap.add_argument("--ksweep", default="", help="LAYOUTxMxN: time K = 256..4096 (per-tile fixed cost = intercept)")
     ap.add_argument("--pmc", default="", help="LAYOUTxMxNxK: launch ours 5x only (for rocprofv3 --pmc)")
+    ap.add_argument("--lib", action="store_true", help="with --pmc: launch hipBLASLt instead of ours")
     a = ap.parse_args()
     import torch.cuda.tunable as tn
 
     tn.enable(False)
     if a.pmc:
         lay, M, N, K = a.pmc.split("x")
-        ours, _, _, _ = make(lay, int(M), int(N), int(K))
+        ours, lib, _, _ = make(lay, int(M), int(N), int(K))
         for _ in range(5):
-            ours()
+            (lib if a.lib else ours)()
         torch.cuda.synchronize()
         return
     shapes = {"bert": BERT, "square": SQUARE, "all": SQUARE + BERT}[a.shapes]
+    if a.ksweep:
+        lay, M, N = a.ksweep.split("x")
+        shapes = [(lay, int(M), int(N), k) for k in (256, 512, 768, 1024, 1536, 2048, 3072, 4096)]
     print("| layout | M | N | K | ours us | TF/s | hipBLASLt us | TF/s | ours/lib | max rel err |")
     print("|---|---:|---:|---:|---:|---:|---:|---:|---:|---:|")
     for lay, M, N, K in shapes:
