@@ -1204,17 +1204,23 @@ static int big_variant() {
   return v;
 }
 
+static int cu_count() {
+  static const int n = [] {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      return 256;
+    return cus;
+  }();
+  return n;
+}
+
 // workgroups of the persistent 8-phase grid: one per CU (the kernel's LDS allows no second);
 // PSD_GEMM_PERSIST=0 launches one workgroup per tile instead
 static int persistent_grid() {
   static const int n = [] {
     const char* e = getenv("PSD_GEMM_PERSIST");
-    if (e && atoi(e) == 0) return 1 << 30;
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-      return 1 << 30;
-    return cus;
+    return (e && atoi(e) == 0) ? (1 << 30) : cu_count();
   }();
   return n;
 }
@@ -1346,8 +1352,10 @@ hipError_t launch_gemm_fp8(const GemmArgs& g, hipStream_t st) {
 
 int gemm_splits(int M, int N, int K) {
   if (M >= 256 && N >= 256 && K % 64 == 0 && K >= 4096) {  // 256x256 tiles, one workgroup per CU
+    // as many splits as fit ONE round of workgroups: rounding up (e.g. 36 tiles x 8 = 288 > 256
+    // CUs) ran a second, almost empty round and doubled the BERT wgrad time
     const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
-    int s = (256 + tiles - 1) / tiles;
+    int s = std::max(1, cu_count() / tiles);
     const int kmax = K / 512;
     if (s > kmax) s = kmax;
     if (s > 64) s = 64;
