@@ -120,6 +120,53 @@ void gemm_fp8_(const at::Tensor& A, const at::Tensor& B, const at::Tensor& a_sca
   TORCH_CHECK(e == hipSuccess, "psd gemm_fp8: ", hipGetErrorString(e));
 }
 
+// Implicit-GEMM NHWC convolution forward on the persistent 8-phase MFMA kernel (no bias/activation):
+// x [Nb, C, H, W] channels_last bf16, w2 [Cout, R*S*C] bf16 ((r, s, ci) order, i.e. an OHWI
+// weight viewed 2-D), out [Nb*Ho*Wo, Cout] (an NHWC output's 2-D view). Returns false (nothing
+// launched) when the shape is outside the kernel's contract -- the caller falls back.
+bool conv_fwd_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride,
+               int64_t pad) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.scalar_type() == at::kBFloat16 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "psd conv_fwd: x must be a channels_last bf16 device tensor");
+  chk2d(w2, "w2");
+  TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.scalar_type() == at::kBFloat16, "psd conv_fwd: out");
+  const int64_t Nb = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
+  const int64_t M = Nb * Ho * Wo, Cout = w2.size(0), K = R * S * C;
+  TORCH_CHECK(w2.size(1) == K, "psd conv_fwd: w2 must be [Cout, R*S*C]");
+  TORCH_CHECK(out.size(0) == M && out.size(1) == Cout, "psd conv_fwd: out must be [Nb*Ho*Wo, Cout]");
+  const int64_t xbytes = x.numel() * 2;
+  if ((C & (C - 1)) != 0 || C < 64 || xbytes >= ((int64_t)1 << 32) || M >= ((int64_t)1 << 31)) return false;
+  int logc = 0;
+  while ((1 << logc) < C) ++logc;
+  const c10::DeviceGuard g(x.device());
+  GemmArgs a{};
+  a.A = x.data_ptr();
+  a.B = w2.data_ptr();
+  a.C = out.data_ptr();
+  a.M = (int)M;
+  a.N = (int)Cout;
+  a.K = (int)K;
+  a.lda = (int)K;
+  a.ldb = (int)w2.stride(0);
+  a.ldc = (int)out.stride(0);
+  a.a_kmajor = a.b_kmajor = 1;
+  a.cv_H = (int)H;
+  a.cv_W = (int)W;
+  a.cv_logC = logc;
+  a.cv_Ho = (int)Ho;
+  a.cv_Wo = (int)Wo;
+  a.cv_S = (int)S;
+  a.cv_stride = (int)stride;
+  a.cv_pad = (int)pad;
+  a.cv_abytes = (uint32_t)xbytes;
+  hipError_t e = launch_conv_fwd(a, stream_of(x));
+  if (e == hipErrorNotSupported) return false;
+  TORCH_CHECK(e == hipSuccess, "psd conv_fwd: ", hipGetErrorString(e));
+  return true;
+}
+
 // out[N] (+)= column sums of x[M,N] (bias gradient)
 void colsum_(const at::Tensor& x, at::Tensor out, bool accumulate) {
   chk2d(x, "x");

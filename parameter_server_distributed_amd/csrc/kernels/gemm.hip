@@ -755,9 +755,13 @@ __device__ __forceinline__ float act_apply(float x) {
 // ACT: the epilogue activation as a template parameter (g.act must match): per-element branches made
 // the unrolled epilogue several times larger, and at one output tile per ~10 K-tiles its instruction
 // fetch, not its arithmetic, was the cost.
-template <int BM, bool AK, bool BKM, int MODE, bool F8 = false, int ACT = 0>
+// GA: A is gathered as an implicit-GEMM convolution input (GemmArgs cv_*): each lane's A rows are
+// output pixels whose (r, s)-shifted input pixel is computed per K-tile (one (r, s) per K-tile:
+// C % 64 == 0); pixels outside the image get an offset past the descriptor, i.e. the zero padding.
+template <int BM, bool AK, bool BKM, int MODE, bool F8 = false, int ACT = 0, bool GA = false>
 __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
   static_assert(!F8 || (AK && BKM), "fp8 GEMM takes K-major operands");
+  static_assert(!GA || (AK && MODE == 0), "implicit-GEMM convolution: K-major A, single split");
   static_assert(BM == 256 || AK, "BM = 128 takes a K-major A");
   using P = P8<BM>;
   constexpr int IM = P::IM;
@@ -804,7 +808,50 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
   uint32_t voA[2][P::PWA], voB[2][2];  // [half][piece]
   stage8_offsets<AK, P::QA, ESZ, P::PWA>(g.lda, wid, lane, voA);
   stage8_offsets<BKM, 32, ESZ, 2>(g.ldb, wid, lane, voB);
-  auto stA = [&](int u, int m0, int k, int h) { stage8<AK, ESZ, P::PWA>(g.A, bytesA, voA[h], g.lda, m0, k, half(u, h), wid); };
+  // GA: per (tile, half, piece) the window origin of the lane's output pixel: p0 = its top-left input
+  // pixel index, hw = (h0 << 16) | (w0 & 0xffff) (h0 = -32768 for rows past M)
+  int cp0[2][P::PWA], chw[2][P::PWA], np0[2][P::PWA], nhw[2][P::PWA];
+  auto conv_rows = [&](int m0, int (&p0)[2][P::PWA], int (&hw)[2][P::PWA]) {
+    const int howo = g.cv_Ho * g.cv_Wo;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < P::PWA; ++i) {
+        const int row = (i * 8 + wid) * 8 + (lane >> 3);
+        const int m = m0 + half_to_tile<P::QA>(row, h);
+        const int n = m / howo, rem = m - n * howo;
+        const int ho = rem / g.cv_Wo, wo = rem - ho * g.cv_Wo;
+        const int h0 = ho * g.cv_stride - g.cv_pad, w0 = wo * g.cv_stride - g.cv_pad;
+        p0[h][i] = (n * g.cv_H + h0) * g.cv_W + w0;
+        hw[h][i] = m < g.M ? (int)(((uint32_t)h0 << 16) | ((uint32_t)w0 & 0xffffu)) : (int)0x80000000u;
+      }
+  };
+  if constexpr (GA) {
+    conv_rows(cm0, cp0, chw);
+    conv_rows(xm0, np0, nhw);
+  }
+  auto stA = [&](int u, int m0, int k, int h) {
+    if constexpr (GA) {
+      const bool cur = m0 == cm0;  // tiles with equal m0 share their A rows
+      const int rs = k >> g.cv_logC, ci0 = k & ((1 << g.cv_logC) - 1);
+      const int r = rs / g.cv_S, s = rs - r * g.cv_S;
+      const rsrc_t src = make_rsrc(g.A, g.cv_abytes);
+      uint8_t* lds = half(u, h);
+#pragma unroll
+      for (int i = 0; i < P::PWA; ++i) {
+        const int row = (i * 8 + wid) * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ ((row >> 1) & 7);
+        const int p0 = cur ? cp0[h][i] : np0[h][i], hw = cur ? chw[h][i] : nhw[h][i];
+        const int hh = (hw >> 16) + r, ww = ((int)((uint32_t)hw << 16) >> 16) + s;
+        const bool ok = (unsigned)hh < (unsigned)g.cv_H && (unsigned)ww < (unsigned)g.cv_W;
+        const uint32_t off = ok ? ((uint32_t)((p0 + r * g.cv_W + s) << g.cv_logC) + ci0) * 2 + c * 16 : 0xFFFFFFF0u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(src, (__attribute__((address_space(3))) void*)(lds + (i * 8 + wid) * 1024),
+                                                 16, off, 0, 0, 0);
+      }
+    } else {
+      stage8<AK, ESZ, P::PWA>(g.A, bytesA, voA[h], g.lda, m0, k, half(u, h), wid);
+    }
+  };
   auto stB = [&](int u, int n0, int k, int h) { stage8<BKM, ESZ, 2>(g.B, bytesB, voB[h], g.ldb, n0, k, half(u, 2 + h), wid); };
   if (nt > 0) {
     const int k1 = kbeg + min(1, nt - 1) * KT;  // nt = 1: a split of one K-tile re-stages it
@@ -1051,6 +1098,13 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
     cm0 = xm0;
     cn0 = xn0;
     if (jt + 2 < ntl) origin(jt + 2, xm0, xn0);
+    if constexpr (GA) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < P::PWA; ++i) cp0[h][i] = np0[h][i], chw[h][i] = nhw[h][i];
+      if (jt + 2 < ntl) conv_rows(xm0, np0, nhw);
+    }
   }
   if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the two wave rows
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1225,12 +1279,12 @@ static int persistent_grid() {
   return n;
 }
 
-template <int BM, bool AK, bool BKM, int MODE, bool F8, int ACT>
+template <int BM, bool AK, bool BKM, int MODE, bool F8, int ACT, bool GA = false>
 static hipError_t launch_8p_act(const GemmArgs& g, int splits, hipStream_t st) {
   constexpr int lds = P8<BM>::LDS;
   static bool attr_set = false;  // per instantiation: set the >64 KiB LDS limit once
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT>,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT, GA>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     attr_set = true;
@@ -1247,7 +1301,7 @@ static hipError_t launch_8p_act(const GemmArgs& g, int splits, hipStream_t st) {
   }();
   GemmArgs ga = g;
   ga.dbg = dbg;
-  hipLaunchKernelGGL((gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT>), dim3(grid, 1, splits), dim3(512), lds, st, ga);
+  hipLaunchKernelGGL((gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT, GA>), dim3(grid, 1, splits), dim3(512), lds, st, ga);
   return hipGetLastError();
 }
 
@@ -1339,6 +1393,20 @@ hipError_t launch_gemm(const GemmArgs& g, hipStream_t st) {
   if (g.a_kmajor && !g.b_kmajor) return launch_layout<true, false, 0>(g, 1, st);
   if (!g.a_kmajor && !g.b_kmajor) return launch_layout<false, false, 0>(g, 1, st);
   return launch_layout<false, true, 0>(g, 1, st);
+}
+
+hipError_t launch_conv_fwd(const GemmArgs& g, hipStream_t st) {
+  if (g.M <= 0 || g.N <= 0) return hipSuccess;
+  const int C = 1 << g.cv_logC;
+  const int64_t xbytes = (int64_t)g.cv_abytes;
+  const bool ok = g.a_kmajor && g.b_kmajor && g.cv_logC >= 6 && g.K % C == 0 && g.K % 64 == 0 &&
+                  g.M >= 128 && g.N >= 256 && g.N % 8 == 0 && g.ldc % 8 == 0 && !g.bias && g.act == 0 &&
+                  (int64_t)(g.N - 1) * g.ldb + g.K < ((int64_t)1 << 31) && xbytes > 0 &&
+                  (int64_t)(g.M - 1) * g.ldc + g.N < ((int64_t)1 << 31) && g.cv_S > 0 && g.cv_W < 32768 &&
+                  g.cv_H < 32768 && big_variant() == 2;
+  if (!ok) return hipErrorNotSupported;
+  return pick_bm(g.M, g.N, 1) == 128 ? launch_8p_act<128, true, true, 0, false, 0, true>(g, 1, st)
+                                     : launch_8p_act<256, true, true, 0, false, 0, true>(g, 1, st);
 }
 
 hipError_t launch_gemm_fp8(const GemmArgs& g, hipStream_t st) {

@@ -20,12 +20,19 @@ struct GemmArgs {
   const float* a_scale;  // fp8 GEMM: dequant factors (device scalars), else unused
   const float* b_scale;
   int dbg;  // timing experiments (PSD_GEMM_DBG): 1 drop the C stores, 2 skip the epilogue; 0 in production
+  // implicit-GEMM convolution (launch_conv_fwd): A = NHWC input [Nb][H][W][C], M = Nb*Ho*Wo output
+  // pixels, K = R*S*C ordered (r, s, ci), C a power of two >= 64; B = weights [Cout][R][S][C]
+  int cv_H, cv_W, cv_logC, cv_Ho, cv_Wo, cv_S, cv_stride, cv_pad;
+  uint32_t cv_abytes;  // input tensor bytes
 };
 
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t stream);
 // C = (A_e4m3 . B_e4m3^T) * a_scale * b_scale (+bias)(act); A [M][K], B [N][K] fp8, K % 128 == 0
 hipError_t launch_gemm_fp8(const GemmArgs& g, hipStream_t stream);
 int gemm_splits(int M, int N, int K);
+// out[M][Cout] = conv(x, w) (NHWC, no bias / activation), on the persistent 8-phase kernel with A
+// gathered from the input; hipErrorNotSupported when the shape is outside that kernel's contract
+hipError_t launch_conv_fwd(const GemmArgs& g, hipStream_t stream);
 // split-K GEMM into fp32 slabs [splits][M][N], then out = (acc ? out : 0) + scale * sum(slabs)
 hipError_t launch_gemm_splitk(const GemmArgs& g, float* slab, int splits, void* out, int out_bf16, int accumulate,
                               float scale, hipStream_t stream);
