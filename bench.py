@@ -142,6 +142,22 @@ def comm_probe(dev, world: int, sizes_mb=(1, 4, 16, 64, 256), iters: int = 5) ->
     return out
 
 
+def autotune_summary() -> dict:
+    """{op/kind: {choice: count}} of the per-shape kernel choices (ops/autotune.py) and the
+    candidates rejected for wrong output."""
+    from parameter_server_distributed_amd.ops import autotune
+
+    out: dict = {}
+    for key, how in autotune.decisions().items():
+        k = f"{key[0]}/{key[1]}" if len(key) > 1 else str(key[0])
+        out.setdefault(k, {}).setdefault(how, 0)
+        out[k][how] += 1
+    rej = autotune.rejected()
+    if rej:
+        out["rejected"] = {"/".join(map(str, k[:2])): v for k, v in rej.items()}
+    return out
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -306,6 +322,7 @@ def main():
             "staleness_p50": p50, "staleness_hist": hist, "final_loss": round(final_loss, 4),
             "params_finite": params_finite, "comm_probe_busbw_GBps": probe, "async_plane_bw": async_bw,
             "warmup_s": round(t_w, 2), "peak_mem_gb": round(mem_peak / 2**30, 2),
+            "autotune": autotune_summary(),
         }
         line = json.dumps(rec)
         print(line, flush=True)

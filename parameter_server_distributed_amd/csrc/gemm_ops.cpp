@@ -181,4 +181,25 @@ void colsum_(const at::Tensor& x, at::Tensor out, bool accumulate) {
   TORCH_CHECK(e == hipSuccess, "psd colsum: ", hipGetErrorString(e));
 }
 
+// GELU(tanh) backward fused with the bias gradient: dx = bf16(dy * gelu'(pre)) and out[N] (+)= colsum(dx)
+void gelu_bwd_colsum_(const at::Tensor& dy, const at::Tensor& pre, at::Tensor dx, at::Tensor out, bool accumulate) {
+  chk2d(dy, "dy");
+  chk2d(pre, "pre");
+  chk2d(dx, "dx");
+  const int64_t M = dy.size(0), N = dy.size(1);
+  TORCH_CHECK(N % 8 == 0 && dy.is_contiguous() && pre.is_contiguous() && dx.is_contiguous() && pre.sizes() == dy.sizes() &&
+                  dx.sizes() == dy.sizes(),
+              "psd gelu_bwd_colsum: contiguous [M, N] tensors, N % 8");
+  TORCH_CHECK(out.numel() == N && out.is_contiguous() &&
+                  (out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat),
+              "psd gelu_bwd_colsum: out [N] bf16/fp32");
+  const c10::DeviceGuard g(dy.device());
+  at::Tensor part = at::empty({512 * N}, dy.options().dtype(at::kFloat));
+  hipError_t e = launch_colsum(reinterpret_cast<const uint16_t*>(dy.data_ptr()), M, (int)N, part.data_ptr<float>(),
+                               out.data_ptr(), out.scalar_type() == at::kBFloat16, accumulate, stream_of(dy),
+                               reinterpret_cast<const uint16_t*>(pre.data_ptr()),
+                               reinterpret_cast<uint16_t*>(dx.data_ptr()));
+  TORCH_CHECK(e == hipSuccess, "psd gelu_bwd_colsum: ", hipGetErrorString(e));
+}
+
 }  // namespace psd

@@ -1168,8 +1168,22 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 // column sums of a [M][N] bf16 matrix (bias gradient), deterministic two-pass: block partials
 // (lane = 8 columns, 4 rows in flight) -> one finalize lane per column summing <= 64 partial rows.
 constexpr int kColsumMaxBlocks = 512;  // partial rows (the caller's workspace is [512 * N] fp32)
+// GELU(tanh) derivative: s = sigmoid(2u), d/dx [x s] = s + 2 x s (1 - s) u'(x)
+__device__ __forceinline__ float gelu_tanh_grad(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float u = k0 * (x + k1 * x * x * x);
+  const float sg = __builtin_amdgcn_rcpf(1.f + __expf(-2.f * u));
+  return sg + 2.f * x * sg * (1.f - sg) * k0 * (1.f + 3.f * k1 * x * x);
+}
+
+// Column partial sums of x[M, N] (bias gradients). GELU: x = bf16(dy * gelu'(pre)) is computed on
+// the fly from dy and the saved pre-activation, written to xo, and summed as written (the GELU
+// backward and the bias gradient of a GELU Linear in one pass over dy / pre).
+template <bool GELU>
 __global__ __launch_bounds__(256) void colsum_partial_kernel(const uint16_t* __restrict__ x, int64_t M, int N,
-                                                             float* __restrict__ part) {
+                                                             float* __restrict__ part,
+                                                             const uint16_t* __restrict__ pre = nullptr,
+                                                             uint16_t* __restrict__ xo = nullptr) {
   const int tpc = N >> 3;
   const int rpi = tpc >= 256 ? 1 : 256 / tpc;
   const int cg = tpc >= 256 ? blockIdx.y * 256 + threadIdx.x : threadIdx.x % tpc;
@@ -1179,10 +1193,20 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const uint16_t* __r
   if (active) {
     const int64_t stride = (int64_t)gridDim.x * rpi;
     int64_t r = (int64_t)blockIdx.x * rpi + r0;
+    auto get = [&](int64_t row, float (&t)[8]) {
+      load8_bf16(x + row * N + cg * 8, t);
+      if constexpr (GELU) {
+        float p[8];
+        load8_bf16(pre + row * N + cg * 8, p);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) t[e] = bf16_to_f32(f32_to_bf16(t[e] * gelu_tanh_grad(p[e])));
+        store8_bf16(xo + row * N + cg * 8, t);
+      }
+    };
     for (; r + 3 * stride < M; r += 4 * stride) {
       float t[4][8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) load8_bf16(x + (r + u * stride) * N + cg * 8, t[u]);
+      for (int u = 0; u < 4; ++u) get(r + u * stride, t[u]);
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
@@ -1190,7 +1214,7 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const uint16_t* __r
     }
     for (; r < M; r += stride) {
       float t[8];
-      load8_bf16(x + r * N + cg * 8, t);
+      get(r, t);
 #pragma unroll
       for (int e = 0; e < 8; ++e) a[e] += t[e];
     }
@@ -1463,7 +1487,7 @@ hipError_t launch_gemm_splitk(const GemmArgs& g0, float* slab, int splits, void*
 }
 
 hipError_t launch_colsum(const uint16_t* x, int64_t M, int N, float* part, void* out, int out_bf16,
-                         int accumulate, hipStream_t st) {
+                         int accumulate, hipStream_t st, const uint16_t* pre, uint16_t* xo) {
   if (N % 8 != 0) return hipErrorInvalidValue;
   const int tpc = N / 8;
   const int gy = tpc >= 256 ? (tpc + 255) / 256 : 1;
@@ -1476,7 +1500,11 @@ hipError_t launch_colsum(const uint16_t* x, int64_t M, int N, float* part, void*
   if (gx > want) gx = want;
   if (gx > kColsumMaxBlocks) gx = kColsumMaxBlocks;
   if (gx < 1) gx = 1;
-  hipLaunchKernelGGL(colsum_partial_kernel, dim3((unsigned)gx, gy), dim3(256), 0, st, x, M, N, part);
+  if (pre)
+    hipLaunchKernelGGL(colsum_partial_kernel<true>, dim3((unsigned)gx, gy), dim3(256), 0, st, x, M, N, part, pre, xo);
+  else
+    hipLaunchKernelGGL(colsum_partial_kernel<false>, dim3((unsigned)gx, gy), dim3(256), 0, st, x, M, N, part,
+                       nullptr, nullptr);
   hipLaunchKernelGGL(colsum_final_kernel, dim3((N + 31) / 32), dim3(256), 0, st, part, (int)gx, N, out, out_bf16,
                      accumulate);
   return hipGetLastError();

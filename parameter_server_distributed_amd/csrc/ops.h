@@ -32,6 +32,7 @@ void gemm_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool b_kmajo
 void gemm_splitk_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool b_kmajor, at::Tensor out,
                   bool accumulate, double scale, int64_t splits);
 void colsum_(const at::Tensor& x, at::Tensor out, bool accumulate);
+void gelu_bwd_colsum_(const at::Tensor& dy, const at::Tensor& pre, at::Tensor dx, at::Tensor out, bool accumulate);
 bool conv_fwd_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride,
                int64_t pad);
 void gemm_fp8_(const at::Tensor& A, const at::Tensor& B, const at::Tensor& a_scale, const at::Tensor& b_scale,

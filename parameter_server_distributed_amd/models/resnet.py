@@ -3,10 +3,10 @@
 The worker model for the BASELINE.json ResNet configs (the reference itself has no model: its
 "gradient" is the constant 0.01 on a dummy [10,10] tensor, src/worker.cpp:316-329,346-353).
 
-MI355X layout choices: NHWC (``channels_last``) activations and weights so MIOpen picks its
-NHWC implicit-GEMM convolutions on the MFMA units, bf16 compute, the stem on our own gfx950
-kernels (ops/conv.py), every BatchNorm (+ residual + ReLU) on the fused NHWC kernels (ops/bn.py),
-1x1 convolutions routed per shape between MIOpen and hipBLASLt (ops/conv.py). The 1000-way
+MI355X layout choices: NHWC (``channels_last``) activations and weights, bf16 compute, the stem
+on our own gfx950 kernels (ops/conv.py), every BatchNorm (+ residual + ReLU) on the fused NHWC
+kernels (ops/bn.py), 1x1 convolutions routed per shape between MIOpen and hipBLASLt, the 3x3 and
+strided convolutions between MIOpen and our implicit-GEMM MFMA kernel (ops/conv.py). The 1000-way
 classifier is a plain ``nn.Linear`` (hipBLASLt; 0.02 ms of an 89 ms step). Random init, synthetic
 data.
 """
@@ -16,7 +16,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.bn import FusedBatchNorm2d
-from ..ops.conv import Conv1x1, stem_forward
+from ..ops.conv import Conv1x1, ConvNHWC, stem_forward
 from ..ops.pool import MaxPool3x3s2, global_avg_pool
 
 
@@ -43,6 +43,8 @@ class _Fork(torch.autograd.Function):
 def _conv(cin, cout, k, stride=1, groups=1):
     if k == 1 and stride == 1 and groups == 1:
         return Conv1x1(cin, cout)  # per-shape MIOpen / hipBLASLt (ops/conv.py)
+    if groups == 1:
+        return ConvNHWC(cin, cout, k, stride)  # per-shape MIOpen / implicit-GEMM MFMA kernel (ops/conv.py)
     return nn.Conv2d(cin, cout, k, stride=stride, padding=k // 2, groups=groups, bias=False)
 
 

@@ -28,6 +28,7 @@ def enabled(var: str) -> bool:
 
 
 _REJECTED: dict[tuple, list] = {}
+_TIMES: dict[tuple, dict] = {}
 
 
 def _snap(out, probe):
@@ -97,7 +98,15 @@ def choose(key: tuple, candidates: dict, default: str, probe=None) -> str:
         _REJECTED[key] = bad
     best = min(ok, key=ok.get)
     _DECISIONS[key] = best
+    _TIMES[key] = {n: round(r[0], 4) for n, r in runs.items()}
+    if os.environ.get("PSD_AUTOTUNE_LOG"):
+        print(f"[autotune] {key}: {_TIMES[key]} -> {best}" + (f" (rejected {bad})" if bad else ""), flush=True)
     return best
+
+
+def times() -> dict:
+    """ms per call of every timed candidate, per key (for logs / bench JSON)."""
+    return dict(_TIMES)
 
 
 def decisions() -> dict:

@@ -14,10 +14,16 @@ same GEMM (tools/gemm_bench.py, profiles/gemm_vs_hipblaslt_miopen_r1.md). Forwar
 shape, wgrad is MIOpen's (hipBLASLt is 4-9x slower on the K = N*H*W reduction).
 
 So each shape is autotuned once, in the first eager step (the same role as MIOpen's own Find):
-forward picks MIOpen or hipBLASLt, bwd-data picks MIOpen or hipBLASLt, by timing both with HIP
-events; bwd-weight always stays on MIOpen. Decisions are cached per (M, cin, cout); inside a
+forward and bwd-data pick MIOpen, hipBLASLt or our MFMA GEMM (kernels/gemm.hip), bwd-weight MIOpen
+or our split-K MFMA GEMM, by timing the candidates with HIP events (and validating their outputs). Decisions are cached per (M, cin, cout); inside a
 hipGraph capture no timing happens (an undecided shape takes MIOpen). ``PSD_CONV1X1=0`` turns the
 GEMM routes off (A/B switch).
+
+Every other convolution (3x3 at any stride, strided 1x1 downsample) is a ``ConvNHWC``: forward
+picks MIOpen or the implicit-GEMM kernel (the persistent 8-phase MFMA GEMM of kernels/gemm.hip
+with its A operand gathered from the NHWC input, ``conv_fwd_``; 1.2-1.6x MIOpen on the ResNet-50 /
+WRN-101-2 b1024 shapes, profiles/conv_igemm_vs_miopen_r2.md), and a stride-1 bwd-data is the same
+kernel run on dY with the flipped, transposed weights. The weight gradient stays on MIOpen.
 
 Reference parity: none -- the reference has no model (its gradient is the constant 0.01,
 src/worker.cpp:316-329). This is worker-side compute for the BASELINE.json ResNet configs.
@@ -49,6 +55,17 @@ def set_decision(key: tuple, name: str | None) -> None:
     _at.set_decision(("conv1x1",) + key, name)
 
 
+def _native():
+    from .. import native
+
+    return native()
+
+
+def _psd_ok(k: int, n: int) -> bool:
+    """Shapes the MFMA GEMM takes as a 1x1 convolution (bf16 rows of 16-B multiples)."""
+    return k % 8 == 0 and n % 8 == 0 and _at.enabled("PSD_CONV1X1_PSD")
+
+
 def _as_2d(t: torch.Tensor) -> torch.Tensor:
     """[N, C, H, W] channels_last -> the [N*H*W, C] row-major view."""
     n, c, h, w = t.shape
@@ -74,8 +91,15 @@ class _Conv1x1Fn(torch.autograd.Function):
         def miopen():
             return F.conv2d(x, weight)
 
-        how = _choose(key, {"gemm": gemm, "miopen": miopen})
-        y = gemm() if how == "gemm" else miopen()
+        def psd():  # the persistent 8-phase MFMA GEMM (kernels/gemm.hip)
+            out = torch.empty(n * h * w, cout, device=x.device, dtype=x.dtype)
+            _native().gemm_(x2, w2, True, True, out)
+            return _from_2d(out, n, h, w)
+
+        cands = {"gemm": gemm, "miopen": miopen}
+        if _psd_ok(cin, cout):
+            cands["psd"] = psd
+        y = cands[_choose(key, cands)]()
         ctx.save_for_backward(x, weight)
         return y
 
@@ -101,9 +125,31 @@ class _Conv1x1Fn(torch.autograd.Function):
             def miopen():
                 return conv_bwd(dy, x, weight, *args, [True, False, False])[0]
 
-            dx = gemm() if _choose(key, {"gemm": gemm, "miopen": miopen}) == "gemm" else miopen()
+            def psd():
+                out = torch.empty(n * h * w, cin, device=dy.device, dtype=dy.dtype)
+                _native().gemm_(dy2, w2, True, False, out)
+                return _from_2d(out, n, h, w)
+
+            cands = {"gemm": gemm, "miopen": miopen}
+            if _psd_ok(cout, cin):
+                cands["psd"] = psd
+            dx = cands[_choose(key, cands)]()
         if need_w:
-            dw = conv_bwd(dy, x, weight, *args, [False, True, False])[1]
+            def miopen_w():
+                return conv_bwd(dy, x, weight, *args, [False, True, False])[1]
+
+            def psd_w():  # dW = dY^T X: split-K MFMA GEMM over the N*H*W reduction
+                out = torch.empty(cout, cin, device=dy.device, dtype=dy.dtype)
+                _native().gemm_splitk_(_as_2d(dy), _as_2d(x), False, False, out)
+                return out.view(cout, cin, 1, 1)
+
+            cands = {"miopen": miopen_w}
+            if _psd_ok(cout, cin) and cout % 8 == 0:
+                cands["psd"] = psd_w
+            how = _choose(("wgrad", n * h * w, cin, cout), cands)
+            dw = cands[how]()
+            if how == "psd" and weight.is_contiguous(memory_format=torch.channels_last):
+                dw = dw.contiguous(memory_format=torch.channels_last)
         return dx, dw
 
 
@@ -120,6 +166,108 @@ class Conv1x1(nn.Conv2d):
                 and x.is_contiguous(memory_format=torch.channels_last)):
             return _Conv1x1Fn.apply(x, self.weight)
         return F.conv2d(x, self.weight)
+
+
+# ---------------------------------------------------------------------------------------------
+# general NHWC convolution: implicit-GEMM forward / stride-1 bwd-data, MIOpen otherwise
+
+
+def _pow2_ge64(c: int) -> bool:
+    return c >= 64 and (c & (c - 1)) == 0
+
+
+def _igemm_ok(cin: int, cout: int) -> bool:
+    """conv_fwd_'s contract (kernels/gemm.hip launch_conv_fwd): C a power of two >= 64 (one (r, s)
+    per 64-wide K-tile), Cout >= 256 (one 256-wide N tile) and a multiple of 8."""
+    return _pow2_ge64(cin) and cout >= 256 and cout % 8 == 0
+
+
+def _igemm(x: torch.Tensor, w2: torch.Tensor, k: int, stride: int, pad: int):
+    """conv(x, w) on the implicit-GEMM kernel, as a channels_last [N, Cout, Ho, Wo] tensor, or None
+    when the kernel declines the shape."""
+    from .. import native
+
+    n, _, h, w = x.shape
+    ho, wo = (h + 2 * pad - k) // stride + 1, (w + 2 * pad - k) // stride + 1
+    out = torch.empty(n * ho * wo, w2.shape[0], device=x.device, dtype=x.dtype)
+    if not native().conv_fwd_(x, w2, out, k, k, stride, pad):
+        return None
+    return _from_2d(out, n, ho, wo)
+
+
+class _ConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, stride, pad):
+        cout, cin, k, _ = weight.shape
+        n, _, h, w = x.shape
+        ctx.stride, ctx.pad = stride, pad
+        ctx.save_for_backward(x, weight)
+
+        def miopen():
+            return F.conv2d(x, weight, stride=stride, padding=pad)
+
+        if not _igemm_ok(cin, cout):
+            return miopen()
+        w2 = weight.permute(0, 2, 3, 1).reshape(cout, k * k * cin)
+        if not w2.is_contiguous():
+            w2 = w2.contiguous()
+
+        def igemm():
+            y = _igemm(x, w2, k, stride, pad)
+            return miopen() if y is None else y
+
+        key = ("fwd", n, cin, h, w, cout, k, stride)
+        return igemm() if _at.choose(("conv",) + key, {"igemm": igemm, "miopen": miopen}, "miopen") == "igemm" \
+            else miopen()
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        stride, pad = ctx.stride, ctx.pad
+        cout, cin, k, _ = weight.shape
+        n, _, h, w = x.shape
+        if not dy.is_contiguous(memory_format=torch.channels_last):
+            dy = dy.contiguous(memory_format=torch.channels_last)
+        conv_bwd = torch.ops.aten.convolution_backward
+        args = (None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            def miopen():
+                return conv_bwd(dy, x, weight, *args, [True, False, False])[0]
+
+            if stride == 1 and _igemm_ok(cout, cin) and 2 * pad == k - 1:
+                # dX = conv(dY, W'), W'[ci, r, s, co] = W[co, ci, k-1-r, k-1-s]: same kernel, same padding
+                wf = weight.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, k * k * cout).contiguous()
+
+                def igemm():
+                    y = _igemm(dy, wf, k, 1, pad)
+                    return miopen() if y is None else y
+
+                key = ("dgrad", n, cin, h, w, cout, k, stride)
+                dx = igemm() if _at.choose(("conv",) + key, {"igemm": igemm, "miopen": miopen},
+                                           "miopen") == "igemm" else miopen()
+            else:
+                dx = miopen()
+        if ctx.needs_input_grad[1]:
+            dw = conv_bwd(dy, x, weight, *args, [False, True, False])[1]
+        return dx, dw, None, None
+
+
+class ConvNHWC(nn.Conv2d):
+    """``nn.Conv2d(cin, cout, k, stride, padding=k//2, bias=False)`` whose NHWC bf16 training path
+    runs forward (and a stride-1 bwd-data) on the implicit-GEMM kernel where that is faster than
+    MIOpen (per shape, validated; see module docstring)."""
+
+    def __init__(self, cin: int, cout: int, k: int, stride: int = 1):
+        super().__init__(cin, cout, k, stride=stride, padding=k // 2, bias=False)
+
+    def forward(self, x):
+        if (_enabled() and _at.enabled("PSD_CONV_IGEMM") and x.is_cuda and x.dtype == torch.bfloat16
+                and x.dim() == 4 and self.weight.dtype == torch.bfloat16 and self.groups == 1
+                and self.dilation == (1, 1) and x.is_contiguous(memory_format=torch.channels_last)
+                and self.weight.is_contiguous(memory_format=torch.channels_last)):
+            return _ConvFn.apply(x, self.weight, self.stride[0], self.padding[0])
+        return F.conv2d(x, self.weight, stride=self.stride, padding=self.padding)
 
 
 # ---------------------------------------------------------------------------------------------

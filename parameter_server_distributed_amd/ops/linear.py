@@ -5,7 +5,8 @@ forward   y  = act(x W^T + b)     NT GEMM, bias + ReLU/GELU fused in the epilogu
 backward  dx = dy' W              NN GEMM (W read N-major through ds_read_b64_tr_b16: no transpose)
           dW = dy'^T x            TN split-K GEMM, reduced straight into the PS flat-gradient
                                   buffer when the data plane installed a grad sink
-          db = colsum(dy')        column-sum kernel (also into the sink)
+          db = colsum(dy')        column-sum kernel (also into the sink); for GELU the activation
+                                  backward and this column sum are one pass (gelu_bwd_colsum_)
 
 fp8 (``MfmaLinear(..., fp8=True)``): the forward GEMM runs on OCP e4m3 operands with per-tensor
 amax scaling (x and W quantised each step by the amax/quant kernels) on the MX-scaled
@@ -91,8 +92,18 @@ class _LinearFn(torch.autograd.Function):
         C = native()
         x2, w, keep = ctx.saved_tensors
         dy2 = dy.reshape(-1, w.shape[0]).contiguous()
+        sink = getattr(ctx.mod, "_psd_grad_sink", None)
+        db = None
         if ctx.act == 1:
             dy2 = dy2 * (keep > 0)
+        elif ctx.act == 2 and ctx.has_bias and ctx.needs_input_grad[2] and dy2.shape[1] % 8 == 0:
+            # GELU backward and the bias gradient in one pass over dy / pre (kernels/gemm.hip)
+            db = sink(ctx.mod.bias) if sink is not None else None
+            if db is None:
+                db = torch.empty(w.shape[0], dtype=w.dtype, device=w.device)
+            g = torch.empty_like(dy2)
+            C.gelu_bwd_colsum_(dy2, keep, g, db, False)
+            dy2 = g
         elif ctx.act == 2:
             dy2 = torch.ops.aten.gelu_backward(dy2, keep, approximate="tanh")
         M, K, N = x2.shape[0], x2.shape[1], w.shape[0]
@@ -102,15 +113,14 @@ class _LinearFn(torch.autograd.Function):
             _route(("dgrad", M, K, N), lambda: C.gemm_(dy2, w, True, False, dx),
                    lambda: torch.mm(dy2, w, out=dx), dx)()
             dx = dx.view(ctx.in_shape)
-        sink = getattr(ctx.mod, "_psd_grad_sink", None)
-        dw = db = None
+        dw = None
         if ctx.needs_input_grad[1]:
             dw = sink(ctx.mod.weight) if sink is not None else None
             if dw is None:
                 dw = torch.empty(w.shape, dtype=w.dtype, device=w.device)
             _route(("wgrad", M, K, N), lambda: C.gemm_splitk_(dy2, x2, False, False, dw, False, 1.0, 0),
                    lambda: torch.mm(dy2.t(), x2, out=dw), dw)()
-        if ctx.has_bias and ctx.needs_input_grad[2]:
+        if ctx.has_bias and ctx.needs_input_grad[2] and db is None:
             db = sink(ctx.mod.bias) if sink is not None else None
             if db is None:
                 db = torch.empty(w.shape[0], dtype=w.dtype, device=w.device)

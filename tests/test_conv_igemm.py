@@ -43,3 +43,51 @@ def test_conv_fwd_declines_unsupported(gpu):
     w2 = torch.zeros(256, 9 * 96, device=gpu, dtype=torch.bfloat16)
     out = torch.empty(2 * 64, 256, device=gpu, dtype=torch.bfloat16)
     assert native().conv_fwd_(x, w2, out, 3, 3, 1, 1) is False  # C not a power of two
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_convnhwc_module_matches_fp32(gpu, monkeypatch, stride):
+    """ConvNHWC forward (implicit GEMM) and backward (stride 1: bwd-data on the same kernel with the
+    flipped weights) vs an fp32 nn.Conv2d on the same bf16-rounded operands."""
+    from parameter_server_distributed_amd.ops.conv import ConvNHWC
+
+    monkeypatch.setenv("PSD_AUTOTUNE_FORCE", "igemm")
+    torch.manual_seed(3)
+    conv = ConvNHWC(256, 256, 3, stride).to(gpu, torch.bfloat16).to(memory_format=torch.channels_last)
+    ref = torch.nn.Conv2d(256, 256, 3, stride=stride, padding=1, bias=False).to(gpu)
+    ref.weight.data.copy_(conv.weight.float())
+    x = torch.randn(8, 256, 14, 14, device=gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    xr = x.float().clone().requires_grad_(True)
+    x.requires_grad_(True)
+    y = conv(x)
+    yr = ref(xr)
+    torch.testing.assert_close(y.float(), yr.detach(), rtol=2e-2, atol=2e-2 * float(yr.abs().max()))
+    gy = torch.randn_like(yr)
+    y.backward(gy.to(torch.bfloat16))
+    yr.backward(gy)
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=2e-2, atol=2e-2 * float(xr.grad.abs().max()))
+    torch.testing.assert_close(conv.weight.grad.float(), ref.weight.grad, rtol=2e-2,
+                               atol=2e-2 * float(ref.weight.grad.abs().max()))
+
+
+def test_conv1x1_psd_route_matches_fp32(gpu, monkeypatch):
+    """Conv1x1 with every route forced to the MFMA GEMM (fwd NT, dgrad NN, split-K wgrad TN)."""
+    from parameter_server_distributed_amd.ops.conv import Conv1x1
+
+    monkeypatch.setenv("PSD_AUTOTUNE_FORCE", "psd")
+    torch.manual_seed(4)
+    conv = Conv1x1(256, 512).to(gpu, torch.bfloat16).to(memory_format=torch.channels_last)
+    ref = torch.nn.Conv2d(256, 512, 1, bias=False).to(gpu)
+    ref.weight.data.copy_(conv.weight.float())
+    x = torch.randn(16, 256, 14, 14, device=gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    xr = x.float().clone().requires_grad_(True)
+    x.requires_grad_(True)
+    y = conv(x)
+    yr = ref(xr)
+    torch.testing.assert_close(y.float(), yr.detach(), rtol=2e-2, atol=2e-2 * float(yr.abs().max()))
+    gy = torch.randn_like(yr)
+    y.backward(gy.to(torch.bfloat16))
+    yr.backward(gy)
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=2e-2, atol=2e-2 * float(xr.grad.abs().max()))
+    torch.testing.assert_close(conv.weight.grad.float(), ref.weight.grad, rtol=2e-2,
+                               atol=2e-2 * float(ref.weight.grad.abs().max()))

@@ -251,3 +251,15 @@ def test_mfma_linear_routes_match_fp32(gpu, route, act):
     for a, b in ((y, yr), (xb.grad, xr.grad), (lin.weight.grad, ref.weight.grad), (lin.bias.grad, ref.bias.grad)):
         rel = ((a.float() - b).norm() / b.norm()).item()
         assert rel < 2e-2, rel
+
+
+def test_gelu_bwd_colsum_matches_torch(gpu):
+    M, N = 3000, 776
+    dy = torch.randn(M, N, device=gpu).to(torch.bfloat16)
+    pre = (torch.randn(M, N, device=gpu) * 3).to(torch.bfloat16)
+    dx = torch.empty_like(dy)
+    db = torch.zeros(N, device=gpu)
+    native().gelu_bwd_colsum_(dy, pre, dx, db, False)
+    want = torch.ops.aten.gelu_backward(dy.float(), pre.float(), approximate="tanh")
+    torch.testing.assert_close(dx.float(), want, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(db, dx.float().sum(0), rtol=1e-4, atol=1e-2)
