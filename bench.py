@@ -77,6 +77,9 @@ def parse():
                          "(parallel/async_ps.py); collective: lock-step RCCL reduce-scatter/all-gather with a "
                          "fixed S-step gradient delay (parallel/collective_ps.py)")
     ap.add_argument("--bucket-mb", type=float, default=16.0)
+    ap.add_argument("--fp8-compute", type=int, default=-1,
+                    help="fp8 (e4m3 MFMA) forward of the bottleneck convolutions, bf16 backward "
+                         "(1/0; -1: on for Wide-ResNet-101-2, the BASELINE 'CDNA4 fp8 MFMA' config)")
     ap.add_argument("--pull-dtype", default="", help="bf16|fp8 published-weight dtype (default: fp8 for WRN-101)")
     ap.add_argument("--optimizer", default="", help="momentum|adam|adamw (default: momentum; adamw for BERT)")
     ap.add_argument("--lr", type=float, default=0.0)
@@ -183,7 +186,8 @@ def main():
 
     a.model = a.model.lower().replace("-", "_")
     a.batch = a.batch or DEFAULT_BATCH.get(a.model, 64)
-    spec = models.build(a.model, dev, torch.bfloat16, image_size=a.image_size, seq_len=a.seq_len)
+    fp8_compute = a.fp8_compute == 1 or (a.fp8_compute < 0 and a.model.startswith("wide"))
+    spec = models.build(a.model, dev, torch.bfloat16, image_size=a.image_size, seq_len=a.seq_len, fp8=fp8_compute)
     opt_kind = a.optimizer or ("adamw" if a.model.startswith("bert") else "momentum")
     lr = a.lr or (1e-4 if opt_kind.startswith("adam") else 0.1)
     optim = OptimConfig(opt_kind, lr=lr, momentum=0.9, weight_decay=0.01 if opt_kind == "adamw" else 5e-5)
@@ -209,7 +213,8 @@ def main():
                 print(f"WARNING: async peer-memory plane unavailable ({fallback}); using the collective plane",
                       file=sys.stderr, flush=True)
             torch.manual_seed(1234)
-            spec = models.build(a.model, dev, torch.bfloat16, image_size=a.image_size, seq_len=a.seq_len)
+            spec = models.build(a.model, dev, torch.bfloat16, image_size=a.image_size, seq_len=a.seq_len,
+                                fp8=fp8_compute)
     if mode == "collective":
         transport = make_transport(a.transport, dev)
         ps = CollectivePS(spec.model, optim, transport, num_shards=shards, staleness=a.staleness,
@@ -307,7 +312,8 @@ def main():
             "metric": metric, "value": round(value, 2), "unit": unit, "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": (round(value / (REF_BASELINE[a.model] * n_workers), 2)
-                            if a.model in REF_BASELINE else None), "dtype": "bf16", "data": data,
+                            if a.model in REF_BASELINE else None),
+            "dtype": "fp8-e4m3 fwd convs / bf16" if fp8_compute else "bf16", "data": data,
             "config": {"model": a.model, "global_batch": a.batch * n_workers, "per_gpu_batch": a.batch,
                        "seq_len": a.seq_len if a.model.startswith("bert") else None,
                        "image_size": None if a.model.startswith("bert") else a.image_size,
@@ -317,7 +323,7 @@ def main():
                        "ps_mode": mode, "async_fallback": fallback,
                        "ps_shards": shards, "ps_owner_ranks": ps.owners, "worker_ranks": ps.worker_ranks,
                        "staleness_bound": a.staleness, "optimizer": f"{opt_kind} fused gfx950", "bucket_mb": a.bucket_mb,
-                       "pull_dtype": pull_dtype, "tunableop": tunable_mode,
+                       "pull_dtype": pull_dtype, "fp8_compute": fp8_compute, "tunableop": tunable_mode,
                        "transport": ps.t.name, "hipgraph": bool(tr.graphs), "graph_error": tr.graph_error},
             "staleness_p50": p50, "staleness_hist": hist, "final_loss": round(final_loss, 4),
             "params_finite": params_finite, "comm_probe_busbw_GBps": probe, "async_plane_bw": async_bw,

@@ -121,23 +121,33 @@ void gemm_fp8_(const at::Tensor& A, const at::Tensor& B, const at::Tensor& a_sca
 }
 
 // Implicit-GEMM NHWC convolution forward on the persistent 8-phase MFMA kernel (no bias/activation):
-// x [Nb, C, H, W] channels_last bf16, w2 [Cout, R*S*C] bf16 ((r, s, ci) order, i.e. an OHWI
-// weight viewed 2-D), out [Nb*Ho*Wo, Cout] (an NHWC output's 2-D view). Returns false (nothing
-// launched) when the shape is outside the kernel's contract -- the caller falls back.
-bool conv_fwd_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride,
-               int64_t pad) {
-  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.scalar_type() == at::kBFloat16 &&
-                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
-              "psd conv_fwd: x must be a channels_last bf16 device tensor");
-  chk2d(w2, "w2");
+// x [Nb, C, H, W] channels_last, w2 [Cout, R*S*C] ((r, s, ci) order, i.e. an OHWI weight viewed
+// 2-D), out [Nb*Ho*Wo, Cout] bf16 (an NHWC output's 2-D view). bf16 operands, or OCP e4m3 ones with
+// per-tensor dequant scales (xs, ws: fp32 device scalars). Returns false (nothing launched) when the
+// shape is outside the kernel's contract -- the caller falls back.
+static bool conv_fwd_impl(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S,
+                          int64_t stride, int64_t pad, const at::Tensor* xs, const at::Tensor* ws) {
+  const bool f8 = xs != nullptr;
+  const auto dt = f8 ? at::kFloat8_e4m3fn : at::kBFloat16;
+  const int esz = f8 ? 1 : 2;
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.scalar_type() == dt && x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "psd conv_fwd: x must be a channels_last ", f8 ? "e4m3fn" : "bf16", " device tensor");
+  TORCH_CHECK(w2.is_cuda() && w2.dim() == 2 && w2.scalar_type() == dt && w2.stride(1) == 1 &&
+                  (w2.stride(0) * esz) % 16 == 0 && (reinterpret_cast<uintptr_t>(w2.data_ptr()) & 15) == 0,
+              "psd conv_fwd: w2 must be a 2-D device tensor like x, unit inner stride, 16-B aligned rows");
   TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.scalar_type() == at::kBFloat16, "psd conv_fwd: out");
+  if (f8)
+    TORCH_CHECK(xs->scalar_type() == at::kFloat && ws->scalar_type() == at::kFloat && xs->is_cuda() && ws->is_cuda() &&
+                    xs->numel() >= 1 && ws->numel() >= 1,
+                "psd conv_fwd_fp8: scales must be fp32 device scalars");
   const int64_t Nb = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
   const int64_t Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
   const int64_t M = Nb * Ho * Wo, Cout = w2.size(0), K = R * S * C;
   TORCH_CHECK(w2.size(1) == K, "psd conv_fwd: w2 must be [Cout, R*S*C]");
   TORCH_CHECK(out.size(0) == M && out.size(1) == Cout, "psd conv_fwd: out must be [Nb*Ho*Wo, Cout]");
-  const int64_t xbytes = x.numel() * 2;
-  if ((C & (C - 1)) != 0 || C < 64 || xbytes >= ((int64_t)1 << 32) || M >= ((int64_t)1 << 31)) return false;
+  const int64_t xbytes = x.numel() * esz;
+  if ((C & (C - 1)) != 0 || C < (f8 ? 128 : 64) || xbytes >= ((int64_t)1 << 32) || M >= ((int64_t)1 << 31))
+    return false;
   int logc = 0;
   while ((1 << logc) < C) ++logc;
   const c10::DeviceGuard g(x.device());
@@ -161,10 +171,24 @@ bool conv_fwd_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_
   a.cv_stride = (int)stride;
   a.cv_pad = (int)pad;
   a.cv_abytes = (uint32_t)xbytes;
-  hipError_t e = launch_conv_fwd(a, stream_of(x));
+  if (f8) {
+    a.a_scale = xs->data_ptr<float>();
+    a.b_scale = ws->data_ptr<float>();
+  }
+  hipError_t e = f8 ? launch_conv_fwd_fp8(a, stream_of(x)) : launch_conv_fwd(a, stream_of(x));
   if (e == hipErrorNotSupported) return false;
   TORCH_CHECK(e == hipSuccess, "psd conv_fwd: ", hipGetErrorString(e));
   return true;
+}
+
+bool conv_fwd_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride,
+               int64_t pad) {
+  return conv_fwd_impl(x, w2, out, R, S, stride, pad, nullptr, nullptr);
+}
+
+bool conv_fwd_fp8_(const at::Tensor& x, const at::Tensor& w2, const at::Tensor& x_scale, const at::Tensor& w_scale,
+                   at::Tensor out, int64_t R, int64_t S, int64_t stride, int64_t pad) {
+  return conv_fwd_impl(x, w2, out, R, S, stride, pad, &x_scale, &w_scale);
 }
 
 // out[N] (+)= column sums of x[M,N] (bias gradient)

@@ -844,7 +844,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
         const int p0 = cur ? cp0[h][i] : np0[h][i], hw = cur ? chw[h][i] : nhw[h][i];
         const int hh = (hw >> 16) + r, ww = ((int)((uint32_t)hw << 16) >> 16) + s;
         const bool ok = (unsigned)hh < (unsigned)g.cv_H && (unsigned)ww < (unsigned)g.cv_W;
-        const uint32_t off = ok ? ((uint32_t)((p0 + r * g.cv_W + s) << g.cv_logC) + ci0) * 2 + c * 16 : 0xFFFFFFF0u;
+        const uint32_t off = ok ? ((uint32_t)((p0 + r * g.cv_W + s) << g.cv_logC) + ci0) * ESZ + c * 16 : 0xFFFFFFF0u;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(src, (__attribute__((address_space(3))) void*)(lds + (i * 8 + wid) * 1024),
                                                  16, off, 0, 0, 0);
       }
@@ -1431,6 +1431,21 @@ hipError_t launch_conv_fwd(const GemmArgs& g, hipStream_t st) {
   if (!ok) return hipErrorNotSupported;
   return pick_bm(g.M, g.N, 1) == 128 ? launch_8p_act<128, true, true, 0, false, 0, true>(g, 1, st)
                                      : launch_8p_act<256, true, true, 0, false, 0, true>(g, 1, st);
+}
+
+// fp8 implicit-GEMM forward: x and w OCP e4m3 (C % 128 == 0: one (r, s) per 128-wide K-tile),
+// dequantised by *a_scale * *b_scale in the epilogue (bf16 out)
+hipError_t launch_conv_fwd_fp8(const GemmArgs& g, hipStream_t st) {
+  if (g.M <= 0 || g.N <= 0) return hipSuccess;
+  const int C = 1 << g.cv_logC;
+  const bool ok = g.a_kmajor && g.b_kmajor && g.cv_logC >= 7 && g.K % C == 0 && g.K % 128 == 0 && g.K >= 256 &&
+                  g.M >= 128 && g.N >= 256 && g.N % 8 == 0 && g.ldc % 8 == 0 && !g.bias && g.act == 0 && !g.c_f32 &&
+                  g.a_scale && g.b_scale && (int64_t)(g.N - 1) * g.ldb + g.K < ((int64_t)1 << 31) &&
+                  g.cv_abytes > 0 && (int64_t)(g.M - 1) * g.ldc + g.N < ((int64_t)1 << 31) && g.cv_S > 0 &&
+                  g.cv_W < 32768 && g.cv_H < 32768;
+  if (!ok) return hipErrorNotSupported;
+  return pick_bm(g.M, g.N, 1) == 128 ? launch_8p_act<128, true, true, 0, true, 0, true>(g, 1, st)
+                                     : launch_8p_act<256, true, true, 0, true, 0, true>(g, 1, st);
 }
 
 hipError_t launch_gemm_fp8(const GemmArgs& g, hipStream_t st) {

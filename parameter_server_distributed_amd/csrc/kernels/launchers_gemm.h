@@ -33,6 +33,8 @@ int gemm_splits(int M, int N, int K);
 // out[M][Cout] = conv(x, w) (NHWC, no bias / activation), on the persistent 8-phase kernel with A
 // gathered from the input; hipErrorNotSupported when the shape is outside that kernel's contract
 hipError_t launch_conv_fwd(const GemmArgs& g, hipStream_t stream);
+// the same with x and w OCP e4m3 (C % 128 == 0), dequantised by *a_scale * *b_scale (bf16 out)
+hipError_t launch_conv_fwd_fp8(const GemmArgs& g, hipStream_t stream);
 // split-K GEMM into fp32 slabs [splits][M][N], then out = (acc ? out : 0) + scale * sum(slabs)
 hipError_t launch_gemm_splitk(const GemmArgs& g, float* slab, int splits, void* out, int out_bf16, int accumulate,
                               float scale, hipStream_t stream);

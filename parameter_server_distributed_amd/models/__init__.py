@@ -71,7 +71,7 @@ def build(name: str, device, dtype=torch.bfloat16, num_classes: int | None = Non
         cls = num_classes or 1000
         size = kw.get("image_size", 224)
         cl = device.type == "cuda" if isinstance(device, torch.device) else str(device).startswith("cuda")
-        m = prepare(ctor(cls), device, dtype, channels_last=cl)
+        m = prepare(ctor(cls, fp8=bool(kw.get("fp8", False))), device, dtype, channels_last=cl)
         return ModelSpec(name, m, _image_batch(size, cls, dtype, cl), _ce, "images", channels_last=cl)
     if name == "mlp":
         m = prepare(MLP(hidden=kw.get("hidden", 512)), device, dtype)

@@ -6,7 +6,9 @@ The worker model for the BASELINE.json ResNet configs (the reference itself has 
 MI355X layout choices: NHWC (``channels_last``) activations and weights, bf16 compute, the stem
 on our own gfx950 kernels (ops/conv.py), every BatchNorm (+ residual + ReLU) on the fused NHWC
 kernels (ops/bn.py), 1x1 convolutions routed per shape between MIOpen and hipBLASLt, the 3x3 and
-strided convolutions between MIOpen and our implicit-GEMM MFMA kernel (ops/conv.py). The 1000-way
+strided convolutions between MIOpen and our implicit-GEMM MFMA kernel (ops/conv.py); with
+``fp8=True`` (the Wide-ResNet-101-2 config, "CDNA4 fp8 MFMA") the bottleneck convolutions' forward
+runs on e4m3 operands through the fp8 GEMM / implicit-GEMM kernels. The 1000-way
 classifier is a plain ``nn.Linear`` (hipBLASLt; 0.02 ms of an 89 ms step). Random init, synthetic
 data.
 """
@@ -40,26 +42,26 @@ class _Fork(torch.autograd.Function):
         return g_main, None
 
 
-def _conv(cin, cout, k, stride=1, groups=1):
+def _conv(cin, cout, k, stride=1, groups=1, fp8=False):
     if k == 1 and stride == 1 and groups == 1:
-        return Conv1x1(cin, cout)  # per-shape MIOpen / hipBLASLt (ops/conv.py)
+        return Conv1x1(cin, cout, fp8=fp8)  # per-shape MIOpen / hipBLASLt / MFMA GEMM (ops/conv.py)
     if groups == 1:
-        return ConvNHWC(cin, cout, k, stride)  # per-shape MIOpen / implicit-GEMM MFMA kernel (ops/conv.py)
+        return ConvNHWC(cin, cout, k, stride, fp8=fp8)  # per-shape MIOpen / implicit-GEMM MFMA kernel (ops/conv.py)
     return nn.Conv2d(cin, cout, k, stride=stride, padding=k // 2, groups=groups, bias=False)
 
 
 class Bottleneck(nn.Module):
     expansion = 4
 
-    def __init__(self, cin, planes, stride=1, width_per_group=64, downsample=None):
+    def __init__(self, cin, planes, stride=1, width_per_group=64, downsample=None, fp8=False):
         super().__init__()
         width = int(planes * (width_per_group / 64.0))
         # BN + ReLU (+ residual) run as one fused NHWC kernel family (ops/bn.py)
-        self.conv1 = _conv(cin, width, 1)
+        self.conv1 = _conv(cin, width, 1, fp8=fp8)
         self.bn1 = FusedBatchNorm2d(width, relu=True)
-        self.conv2 = _conv(width, width, 3, stride)
+        self.conv2 = _conv(width, width, 3, stride, fp8=fp8)
         self.bn2 = FusedBatchNorm2d(width, relu=True)
-        self.conv3 = _conv(width, planes * self.expansion, 1)
+        self.conv3 = _conv(width, planes * self.expansion, 1, fp8=fp8)
         self.bn3 = FusedBatchNorm2d(planes * self.expansion, relu=True)  # relu(bn3(conv3) + identity)
         self.downsample = downsample
         self.fuse_residual_grad = True
@@ -80,8 +82,13 @@ class Bottleneck(nn.Module):
 
 
 class ResNet(nn.Module):
-    def __init__(self, layers=(3, 4, 6, 3), num_classes=1000, width_per_group=64, zero_init_residual=True):
+    def __init__(self, layers=(3, 4, 6, 3), num_classes=1000, width_per_group=64, zero_init_residual=True,
+                 fp8=False):
+        """``fp8``: bottleneck convolutions run their forward on e4m3 operands (fp8 MFMA GEMM /
+        implicit GEMM, per-tensor scales) and their backward in bf16, where the shape allows
+        (ops/conv.py); the stem and the classifier stay bf16."""
         super().__init__()
+        self.fp8 = fp8
         self.width_per_group = width_per_group
         self.cin = 64
         self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
@@ -106,12 +113,12 @@ class ResNet(nn.Module):
     def _make(self, planes, blocks, stride=1):
         down = None
         if stride != 1 or self.cin != planes * Bottleneck.expansion:
-            down = nn.Sequential(_conv(self.cin, planes * Bottleneck.expansion, 1, stride),
+            down = nn.Sequential(_conv(self.cin, planes * Bottleneck.expansion, 1, stride, fp8=self.fp8),
                                  FusedBatchNorm2d(planes * Bottleneck.expansion))
-        mods = [Bottleneck(self.cin, planes, stride, self.width_per_group, down)]
+        mods = [Bottleneck(self.cin, planes, stride, self.width_per_group, down, fp8=self.fp8)]
         self.cin = planes * Bottleneck.expansion
         for _ in range(1, blocks):
-            mods.append(Bottleneck(self.cin, planes, 1, self.width_per_group))
+            mods.append(Bottleneck(self.cin, planes, 1, self.width_per_group, fp8=self.fp8))
         return nn.Sequential(*mods)
 
     def forward(self, x):
@@ -125,13 +132,13 @@ class ResNet(nn.Module):
         return self.fc(global_avg_pool(x))
 
 
-def resnet50(num_classes=1000):
-    return ResNet((3, 4, 6, 3), num_classes)
+def resnet50(num_classes=1000, fp8=False):
+    return ResNet((3, 4, 6, 3), num_classes, fp8=fp8)
 
 
-def resnet101(num_classes=1000):
-    return ResNet((3, 4, 23, 3), num_classes)
+def resnet101(num_classes=1000, fp8=False):
+    return ResNet((3, 4, 23, 3), num_classes, fp8=fp8)
 
 
-def wide_resnet101_2(num_classes=1000):
-    return ResNet((3, 4, 23, 3), num_classes, width_per_group=128)
+def wide_resnet101_2(num_classes=1000, fp8=False):
+    return ResNet((3, 4, 23, 3), num_classes, width_per_group=128, fp8=fp8)

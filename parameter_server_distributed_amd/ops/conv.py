@@ -76,13 +76,34 @@ def _from_2d(t2: torch.Tensor, n: int, h: int, w: int) -> torch.Tensor:
     return t2.view(n, h, w, t2.shape[1]).permute(0, 3, 1, 2)
 
 
+def _fp8_ok(k: int, n: int) -> bool:
+    """Shapes the fp8 MFMA GEMM / implicit-GEMM kernel takes (K a multiple of 128, >= 256 columns)."""
+    return k % 128 == 0 and k >= 256 and n >= 256 and n % 8 == 0 and _at.enabled("PSD_FP8_COMPUTE")
+
+
+def _q8(t2: torch.Tensor):
+    """Per-tensor OCP e4m3 quantisation of a contiguous tensor (just-in-time amax): (q, scale_inv)."""
+    from . import quantize_fp8
+
+    return quantize_fp8(t2)
+
+
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight):
+    def forward(ctx, x, weight, fp8=False):
         n, cin, h, w = x.shape
         cout = weight.shape[0]
         w2 = weight.reshape(cout, cin)
         x2 = _as_2d(x)
+        ctx.save_for_backward(x, weight)
+        if fp8 and _fp8_ok(cin, cout):
+            # fp8 forward / bf16 backward: e4m3 operands on the MX-scaled MFMA (2x the bf16 rate),
+            # dequantised in the epilogue; backward runs on the saved bf16 x and W
+            xq, sx = _q8(x2)
+            wq, sw = _q8(w2)
+            out = torch.empty(n * h * w, cout, device=x.device, dtype=x.dtype)
+            _native().gemm_fp8_(xq, wq, sx, sw, out)
+            return _from_2d(out, n, h, w)
         key = ("fwd", n * h * w, cin, cout)
 
         def gemm():
@@ -99,9 +120,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         cands = {"gemm": gemm, "miopen": miopen}
         if _psd_ok(cin, cout):
             cands["psd"] = psd
-        y = cands[_choose(key, cands)]()
-        ctx.save_for_backward(x, weight)
-        return y
+        return cands[_choose(key, cands)]()
 
     @staticmethod
     def backward(ctx, dy):
@@ -150,21 +169,22 @@ class _Conv1x1Fn(torch.autograd.Function):
             dw = cands[how]()
             if how == "psd" and weight.is_contiguous(memory_format=torch.channels_last):
                 dw = dw.contiguous(memory_format=torch.channels_last)
-        return dx, dw
+        return dx, dw, None
 
 
 class Conv1x1(nn.Conv2d):
     """``nn.Conv2d(cin, cout, 1, bias=False)`` whose NHWC bf16 training path runs the per-shape
     fastest of MIOpen / hipBLASLt for forward and bwd-data (see module docstring)."""
 
-    def __init__(self, cin: int, cout: int):
+    def __init__(self, cin: int, cout: int, fp8: bool = False):
         super().__init__(cin, cout, 1, stride=1, padding=0, bias=False)
+        self.fp8 = fp8  # fp8 forward (e4m3 MFMA) / bf16 backward where the shape allows
 
     def forward(self, x):
         if (_enabled() and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
                 and self.weight.dtype == torch.bfloat16 and torch.is_grad_enabled()
                 and x.is_contiguous(memory_format=torch.channels_last)):
-            return _Conv1x1Fn.apply(x, self.weight)
+            return _Conv1x1Fn.apply(x, self.weight, self.fp8)
         return F.conv2d(x, self.weight)
 
 
@@ -195,9 +215,24 @@ def _igemm(x: torch.Tensor, w2: torch.Tensor, k: int, stride: int, pad: int):
     return _from_2d(out, n, ho, wo)
 
 
+def _igemm_fp8(x: torch.Tensor, w2: torch.Tensor, k: int, stride: int, pad: int):
+    """conv(x, w) with e4m3 operands on the implicit-GEMM kernel (per-tensor just-in-time scales),
+    bf16 channels_last out, or None when the kernel declines the shape."""
+    from .. import native
+
+    n, c, h, w = x.shape
+    ho, wo = (h + 2 * pad - k) // stride + 1, (w + 2 * pad - k) // stride + 1
+    xq, sx = _q8(x.permute(0, 2, 3, 1))  # the NHWC storage, quantised in place order
+    wq, sw = _q8(w2)
+    out = torch.empty(n * ho * wo, w2.shape[0], device=x.device, dtype=x.dtype)
+    if not native().conv_fwd_fp8_(xq.permute(0, 3, 1, 2), wq, sx, sw, out, k, k, stride, pad):
+        return None
+    return _from_2d(out, n, ho, wo)
+
+
 class _ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, stride, pad):
+    def forward(ctx, x, weight, stride, pad, fp8=False):
         cout, cin, k, _ = weight.shape
         n, _, h, w = x.shape
         ctx.stride, ctx.pad = stride, pad
@@ -205,6 +240,12 @@ class _ConvFn(torch.autograd.Function):
 
         def miopen():
             return F.conv2d(x, weight, stride=stride, padding=pad)
+
+        if fp8 and cin % 128 == 0 and _fp8_ok(k * k * cin, cout):
+            w2 = weight.permute(0, 2, 3, 1).reshape(cout, k * k * cin)
+            y = _igemm_fp8(x, w2 if w2.is_contiguous() else w2.contiguous(), k, stride, pad)
+            if y is not None:
+                return y
 
         if not _igemm_ok(cin, cout):
             return miopen()
@@ -250,7 +291,7 @@ class _ConvFn(torch.autograd.Function):
                 dx = miopen()
         if ctx.needs_input_grad[1]:
             dw = conv_bwd(dy, x, weight, *args, [False, True, False])[1]
-        return dx, dw, None, None
+        return dx, dw, None, None, None
 
 
 class ConvNHWC(nn.Conv2d):
@@ -258,15 +299,16 @@ class ConvNHWC(nn.Conv2d):
     runs forward (and a stride-1 bwd-data) on the implicit-GEMM kernel where that is faster than
     MIOpen (per shape, validated; see module docstring)."""
 
-    def __init__(self, cin: int, cout: int, k: int, stride: int = 1):
+    def __init__(self, cin: int, cout: int, k: int, stride: int = 1, fp8: bool = False):
         super().__init__(cin, cout, k, stride=stride, padding=k // 2, bias=False)
+        self.fp8 = fp8  # fp8 forward (e4m3 implicit GEMM) / bf16 backward where the shape allows
 
     def forward(self, x):
         if (_enabled() and _at.enabled("PSD_CONV_IGEMM") and x.is_cuda and x.dtype == torch.bfloat16
                 and x.dim() == 4 and self.weight.dtype == torch.bfloat16 and self.groups == 1
                 and self.dilation == (1, 1) and x.is_contiguous(memory_format=torch.channels_last)
                 and self.weight.is_contiguous(memory_format=torch.channels_last)):
-            return _ConvFn.apply(x, self.weight, self.stride[0], self.padding[0])
+            return _ConvFn.apply(x, self.weight, self.stride[0], self.padding[0], self.fp8)
         return F.conv2d(x, self.weight, stride=self.stride, padding=self.padding)
 
 

@@ -91,3 +91,70 @@ def test_conv1x1_psd_route_matches_fp32(gpu, monkeypatch):
     torch.testing.assert_close(x.grad.float(), xr.grad, rtol=2e-2, atol=2e-2 * float(xr.grad.abs().max()))
     torch.testing.assert_close(conv.weight.grad.float(), ref.weight.grad, rtol=2e-2,
                                atol=2e-2 * float(ref.weight.grad.abs().max()))
+
+
+# ---------------------------------------------------------------- fp8 (e4m3) implicit GEMM
+F8_CASES = [  # Nb, C, H, W, Cout, R, stride, pad
+    (4, 128, 14, 14, 256, 3, 1, 1),
+    (8, 256, 28, 28, 512, 1, 2, 0),
+    (64, 256, 14, 14, 256, 3, 1, 1),   # several tiles per persistent workgroup
+    (3, 512, 7, 7, 264, 3, 2, 1),      # ragged M and N
+]
+
+
+@pytest.mark.parametrize("case", F8_CASES, ids=lambda c: "x".join(map(str, c)))
+def test_conv_fwd_fp8_exact(gpu, case):
+    """e4m3 operands holding small integers (exact in e4m3, products exact in the fp32 MFMA
+    accumulator) and power-of-two dequant scales: the kernel must equal the fp32 convolution."""
+    Nb, C, H, W, Cout, R, stride, pad = case
+    g = torch.Generator().manual_seed(11)
+    x = torch.randint(-3, 4, (Nb, C, H, W), generator=g).float()
+    w = torch.randint(-3, 4, (Cout, C, R, R), generator=g).float()
+    ref = F.conv2d(x, w, stride=stride, padding=pad) * 0.25
+    Ho, Wo = ref.shape[2], ref.shape[3]
+    xq = x.to(gpu).contiguous(memory_format=torch.channels_last).to(torch.float8_e4m3fn)
+    wq = _w2(w.to(gpu)).to(torch.float8_e4m3fn)
+    sx = torch.tensor([0.5], device=gpu)
+    sw = torch.tensor([0.5], device=gpu)
+    out = torch.empty(Nb * Ho * Wo, Cout, device=gpu, dtype=torch.bfloat16)
+    assert xq.is_contiguous(memory_format=torch.channels_last)
+    assert native().conv_fwd_fp8_(xq, wq, sx, sw, out, R, R, stride, pad)
+    want = ref.permute(0, 2, 3, 1).reshape(-1, Cout).bfloat16().float()
+    torch.testing.assert_close(out.float().cpu(), want, rtol=0, atol=0)
+
+
+def test_conv_fwd_fp8_declines_small_c(gpu):
+    xq = torch.zeros(2, 64, 8, 8, device=gpu).contiguous(memory_format=torch.channels_last).to(torch.float8_e4m3fn)
+    wq = torch.zeros(256, 9 * 64, device=gpu).to(torch.float8_e4m3fn)
+    one = torch.ones(1, device=gpu)
+    out = torch.empty(2 * 64, 256, device=gpu, dtype=torch.bfloat16)
+    assert native().conv_fwd_fp8_(xq, wq, one, one, out, 3, 3, 1, 1) is False  # C < 128
+
+
+@pytest.mark.parametrize("kind", ["3x3", "3x3s2", "1x1"])
+def test_fp8_conv_modules_match_fp32(gpu, kind):
+    """fp8-forward / bf16-backward modules vs fp32 nn.Conv2d: forward within e4m3 error (per-tensor
+    scales), gradients as tight as the bf16 path (they never see fp8)."""
+    from parameter_server_distributed_amd.ops.conv import Conv1x1, ConvNHWC
+
+    torch.manual_seed(5)
+    k, stride = (1, 1) if kind == "1x1" else (3, 2 if kind.endswith("s2") else 1)
+    conv = (Conv1x1(256, 512, fp8=True) if kind == "1x1" else ConvNHWC(256, 256, 3, stride, fp8=True))
+    conv = conv.to(gpu, torch.bfloat16).to(memory_format=torch.channels_last)
+    ref = torch.nn.Conv2d(256, conv.out_channels, k, stride=stride, padding=k // 2, bias=False).to(gpu)
+    ref.weight.data.copy_(conv.weight.float())
+    x = torch.randn(8, 256, 14, 14, device=gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    xr = x.float().clone().requires_grad_(True)
+    x.requires_grad_(True)
+    y = conv(x)
+    yr = ref(xr)
+    err = (y.float() - yr.detach()).abs()
+    scale = float(yr.abs().max())
+    assert float(err.max()) < 0.08 * scale, (float(err.max()), scale)
+    assert float(err.mean()) < 0.01 * scale
+    gy = torch.randn_like(yr)
+    y.backward(gy.to(torch.bfloat16))
+    yr.backward(gy)
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=2e-2, atol=2e-2 * float(xr.grad.abs().max()))
+    torch.testing.assert_close(conv.weight.grad.float(), ref.weight.grad, rtol=2e-2,
+                               atol=2e-2 * float(ref.weight.grad.abs().max()))
