@@ -199,7 +199,7 @@ void colsum_(const at::Tensor& x, at::Tensor out, bool accumulate) {
   TORCH_CHECK(out.numel() == N && out.is_contiguous(), "psd colsum: out [N]");
   const c10::DeviceGuard g(x.device());
   TORCH_CHECK(out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat, "psd colsum: out dtype");
-  at::Tensor part = at::empty({512 * N}, x.options().dtype(at::kFloat));
+  at::Tensor part = at::empty({(int64_t)kColsumPartRows * N}, x.options().dtype(at::kFloat));
   hipError_t e = launch_colsum(reinterpret_cast<const uint16_t*>(x.data_ptr()), M, (int)N, part.data_ptr<float>(),
                                out.data_ptr(), out.scalar_type() == at::kBFloat16, accumulate, stream_of(x));
   TORCH_CHECK(e == hipSuccess, "psd colsum: ", hipGetErrorString(e));
@@ -218,7 +218,7 @@ void gelu_bwd_colsum_(const at::Tensor& dy, const at::Tensor& pre, at::Tensor dx
                   (out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat),
               "psd gelu_bwd_colsum: out [N] bf16/fp32");
   const c10::DeviceGuard g(dy.device());
-  at::Tensor part = at::empty({512 * N}, dy.options().dtype(at::kFloat));
+  at::Tensor part = at::empty({(int64_t)kColsumPartRows * N}, dy.options().dtype(at::kFloat));
   hipError_t e = launch_colsum(reinterpret_cast<const uint16_t*>(dy.data_ptr()), M, (int)N, part.data_ptr<float>(),
                                out.data_ptr(), out.scalar_type() == at::kBFloat16, accumulate, stream_of(dy),
                                reinterpret_cast<const uint16_t*>(pre.data_ptr()),

@@ -1167,7 +1167,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 
 // column sums of a [M][N] bf16 matrix (bias gradient), deterministic two-pass: block partials
 // (lane = 8 columns, 4 rows in flight) -> one finalize lane per column summing <= 64 partial rows.
-constexpr int kColsumMaxBlocks = 512;  // partial rows (the caller's workspace is [512 * N] fp32)
+constexpr int kColsumMaxBlocks = kColsumPartRows;  // partial rows (the caller's workspace: [kColsumPartRows * N] fp32)
 // GELU(tanh) derivative: s = sigmoid(2u), d/dx [x s] = s + 2 x s (1 - s) u'(x)
 __device__ __forceinline__ float gelu_tanh_grad(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
@@ -1235,26 +1235,42 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const uint16_t* __r
   }
 }
 
-// Deterministic second pass: block = 32 columns x 8 partial-row lanes; fixed summation order.
-__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ part, int nblk, int N, void* out,
-                                                           int out_bf16, int accumulate) {
-  const int cl = threadIdx.x & 31, rl = threadIdx.x >> 5;
-  const int c = blockIdx.x * 32 + cl;
-  float s = 0.f;
-  if (c < N)
-    for (int b = rl; b < nblk; b += 8) s += part[(int64_t)b * N + c];
-  __shared__ float red[8][33];
-  red[rl][cl] = s;
+// Deterministic second pass: block = 8 columns x 128 partial-row lanes (1024 lanes), 4 independent
+// accumulators per lane (a lane's loads are independent: ~nblk/512 round trips instead of a
+// nblk/8-deep dependent chain), then the 128 lanes of a column are combined in LDS in a fixed order.
+__global__ __launch_bounds__(1024) void colsum_final_kernel(const float* __restrict__ part, int nblk, int N, void* out,
+                                                            int out_bf16, int accumulate) {
+  const int cl = threadIdx.x & 7, rl = threadIdx.x >> 3;
+  const int c = blockIdx.x * 8 + cl;
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c < N) {
+    int b = rl;
+    for (; b + 384 < nblk; b += 512)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s[u] += part[(int64_t)(b + 128 * u) * N + c];
+    for (; b < nblk; b += 128) s[0] += part[(int64_t)b * N + c];
+  }
+  __shared__ float red[128][9];
+  __shared__ float red2[8][9];
+  red[rl][cl] = (s[0] + s[1]) + (s[2] + s[3]);
+  __syncthreads();
+  if (rl < 8) {  // 8 x 8 lanes: each sums 16 of the 128 row lanes of one column
+    float t = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t += red[rl * 16 + r][cl];
+    red2[rl][cl] = t;
+  }
   __syncthreads();
   if (rl != 0 || c >= N) return;
+  float t = red2[0][cl];
 #pragma unroll
-  for (int r = 1; r < 8; ++r) s += red[r][cl];
+  for (int r = 1; r < 8; ++r) t += red2[r][cl];
   if (out_bf16) {
     uint16_t* o = reinterpret_cast<uint16_t*>(out);
-    o[c] = f32_to_bf16(s + (accumulate ? bf16_to_f32(o[c]) : 0.f));
+    o[c] = f32_to_bf16(t + (accumulate ? bf16_to_f32(o[c]) : 0.f));
   } else {
     float* o = reinterpret_cast<float*>(out);
-    o[c] = s + (accumulate ? o[c] : 0.f);
+    o[c] = t + (accumulate ? o[c] : 0.f);
   }
 }
 
@@ -1507,11 +1523,13 @@ hipError_t launch_colsum(const uint16_t* x, int64_t M, int N, float* part, void*
   const int tpc = N / 8;
   const int gy = tpc >= 256 ? (tpc + 255) / 256 : 1;
   const int rpi = tpc >= 256 ? 1 : 256 / tpc;
-  // each thread sums >= 32 rows and there are <= ~256 partial rows: the finalize (one lane group
-  // per 32 columns, latency-bound) then sums <= 32 partials per lane. At >= 8 rows per thread and
-  // 512 partial rows the finalize alone took 20 us per BERT bias (profiles/bert_base_b64_r1_tuned_kernels.md).
-  int64_t gx = (M + (int64_t)rpi * 32 - 1) / ((int64_t)rpi * 32);
-  const int64_t want = (256 + gy - 1) / gy;
+  // A pure streaming pass: its bandwidth is set by the bytes in flight. At one 256-lane block per CU
+  // (256 partial rows) the fused GELU-backward variant ran at half the HBM roof (260 us for a BERT
+  // [32768, 3072] pass, rocprofv3 profiles/bert_base_b256_r2_kernels.md), so aim for ~8 blocks per CU
+  // (each lane still sums >= 8 rows, 4 loads in flight); the finalize reads the partials with 32
+  // independent lanes per column.
+  const int64_t want = (int64_t)(8 * 256 + gy - 1) / gy;
+  int64_t gx = (M + (int64_t)rpi * 8 - 1) / ((int64_t)rpi * 8);
   if (gx > want) gx = want;
   if (gx > kColsumMaxBlocks) gx = kColsumMaxBlocks;
   if (gx < 1) gx = 1;
@@ -1520,7 +1538,7 @@ hipError_t launch_colsum(const uint16_t* x, int64_t M, int N, float* part, void*
   else
     hipLaunchKernelGGL(colsum_partial_kernel<false>, dim3((unsigned)gx, gy), dim3(256), 0, st, x, M, N, part,
                        nullptr, nullptr);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3((N + 31) / 32), dim3(256), 0, st, part, (int)gx, N, out, out_bf16,
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((N + 7) / 8), dim3(1024), 0, st, part, (int)gx, N, out, out_bf16,
                      accumulate);
   return hipGetLastError();
 }

@@ -38,7 +38,8 @@ hipError_t launch_conv_fwd_fp8(const GemmArgs& g, hipStream_t stream);
 // split-K GEMM into fp32 slabs [splits][M][N], then out = (acc ? out : 0) + scale * sum(slabs)
 hipError_t launch_gemm_splitk(const GemmArgs& g, float* slab, int splits, void* out, int out_bf16, int accumulate,
                               float scale, hipStream_t stream);
-// out[n] (+)= sum_m x[m][n]; part is an fp32 [512 * N] scratch
+// out[n] (+)= sum_m x[m][n]; part is an fp32 [kColsumPartRows * N] scratch
+constexpr int kColsumPartRows = 2048;
 // pre/xo (optional): x is dy of a GELU(tanh) output; xo = bf16(dy * gelu'(pre)) is written and summed
 hipError_t launch_colsum(const uint16_t* x, int64_t M, int N, float* part, void* out, int out_bf16,
                          int accumulate, hipStream_t stream, const uint16_t* pre = nullptr, uint16_t* xo = nullptr);

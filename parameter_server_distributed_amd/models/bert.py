@@ -39,8 +39,10 @@ class BertLayer(nn.Module):
         self.p = dropout
 
     def forward(self, x):
-        x = self.ln1(x, self.proj(self.attn(self.qkv(x))))
-        return self.ln2(x, self.ffn2(self.ffn1(x)))
+        # each residual LayerNorm hands the gradient of its x input to the Linear that also reads x
+        # (folded into that Linear's bwd-data GEMM, ops/layernorm.py)
+        x = self.ln1(x, self.proj(self.attn(self.qkv(x))), x_grad_to=self.qkv)
+        return self.ln2(x, self.ffn2(self.ffn1(x)), x_grad_to=self.ffn1)
 
 
 class BertForMLM(nn.Module):

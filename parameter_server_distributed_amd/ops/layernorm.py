@@ -21,11 +21,11 @@ from .. import native
 
 class _AddLNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, h, weight, bias, mod, p):
+    def forward(ctx, x, h, weight, bias, mod, p, x_grad_to=None):
         C = native()
         shp = x.shape
         y, s, mean, rstd = C.ln_fwd(x.contiguous(), h.contiguous(), weight, bias, mod.eps, p, mod.seed, mod.step)
-        ctx.mod, ctx.p = mod, p
+        ctx.mod, ctx.p, ctx.x_grad_to = mod, p, x_grad_to
         ctx.save_for_backward(s, mean, rstd, weight)
         return y.view(shp)
 
@@ -38,7 +38,12 @@ class _AddLNFn(torch.autograd.Function):
         if sink is not None:
             dgo, dbo = sink(mod.weight), sink(mod.bias)
         dx, dh, dg, db = native().ln_bwd(dy, s, mean, rstd, w, ctx.p, mod.seed, mod.step, dgo, dbo)
-        return dx.view(dy.shape), dh.view(dy.shape), dg, db, None, None
+        if ctx.x_grad_to is not None:
+            # residual-branch gradient handed to the Linear that also consumes x: its dgrad GEMM
+            # accumulates onto it (beta = 1) instead of autograd adding the two [M, H] gradients
+            ctx.x_grad_to._psd_pending_dx.append(dx)
+            return None, dh.view(dy.shape), dg, db, None, None, None
+        return dx.view(dy.shape), dh.view(dy.shape), dg, db, None, None, None
 
 
 class FusedAddLayerNorm(nn.LayerNorm):
@@ -57,9 +62,16 @@ class FusedAddLayerNorm(nn.LayerNorm):
         return (x.is_cuda and x.dtype == torch.bfloat16 and h.dtype == torch.bfloat16 and x.shape == h.shape
                 and x.shape[-1] in (768, 1024) and self.weight is not None and self.weight.dtype == torch.bfloat16)
 
-    def forward(self, x, h):
+    def forward(self, x, h, x_grad_to=None):
+        """``x_grad_to``: the ``MfmaLinear`` that consumed ``x`` earlier in the forward (the block's
+        first projection). The gradient of ``x`` through this LayerNorm is then handed to that
+        Linear's backward, which folds it into its bwd-data GEMM (beta = 1): the residual-stream
+        gradient add is gone. The caller guarantees ``x`` has no other consumer."""
         p = self.p if self.training else 0.0
         if self._kernel_ok(x, h):
+            if (x_grad_to is not None and torch.is_grad_enabled() and x.requires_grad
+                    and getattr(x_grad_to, "psd_takes_pending_dx", lambda _x: False)(x)):
+                return _AddLNFn.apply(x.detach(), h, self.weight, self.bias, self, p, x_grad_to)
             return _AddLNFn.apply(x, h, self.weight, self.bias, self, p)
         return F.layer_norm(x + F.dropout(h, p, self.training), self.normalized_shape,
                             None if self.weight is None else self.weight.to(x.dtype),

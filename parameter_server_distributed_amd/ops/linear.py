@@ -108,7 +108,13 @@ class _LinearFn(torch.autograd.Function):
             dy2 = torch.ops.aten.gelu_backward(dy2, keep, approximate="tanh")
         M, K, N = x2.shape[0], x2.shape[1], w.shape[0]
         dx = None
-        if ctx.needs_input_grad[0]:
+        pend = ctx.mod._psd_pending_dx
+        if ctx.needs_input_grad[0] and pend:
+            # x's other gradient (a residual LayerNorm's, ops/layernorm.py): accumulated by the GEMM
+            dx = pend.pop().view(M, K)
+            dx.addmm_(dy2, w)
+            dx = dx.view(ctx.in_shape)
+        elif ctx.needs_input_grad[0]:
             dx = torch.empty(x2.shape, dtype=dy2.dtype, device=dy2.device)
             _route(("dgrad", M, K, N), lambda: C.gemm_(dy2, w, True, False, dx),
                    lambda: torch.mm(dy2, w, out=dx), dx)()
@@ -135,6 +141,12 @@ class MfmaLinear(nn.Linear):
         super().__init__(in_features, out_features, bias=bias, device=device, dtype=dtype)
         self.act = act
         self.fp8 = fp8
+        self._psd_pending_dx: list = []  # gradients of the input handed over by a residual LayerNorm
+
+    def psd_takes_pending_dx(self, x) -> bool:
+        """True when this module's forward on ``x`` ran the autograd Function whose backward folds a
+        handed-over input gradient into its bwd-data GEMM."""
+        return _ok(x, self.weight) and x.shape[-1] == self.in_features
 
     def psd_direct_grad_params(self):
         return [p for p in (self.weight, self.bias) if p is not None]

@@ -42,7 +42,7 @@ import torch.nn as nn
 
 from .. import native
 from ..ops.optim import OptimConfig, OptimDyn
-from .collective_ps import ALIGN, _flat_view, _round
+from .collective_ps import ALIGN, _flat_view, _round, zero_grads_, zero_plan
 
 _INSTANCE = [0]
 
@@ -162,6 +162,8 @@ class AsyncPS:
                         self._direct.add(id(dp))
                 m._psd_grad_sink = self._sink
         self._layout = layout
+        self._zero_plan = zero_plan([(o, p.numel()) for (_n, p, o, _k) in layout if id(p) not in self._direct], total)
+        self._arrived: set = set()
         self._p2b = {}
         for b in self.buckets:
             for _, p, _o, _n in b.params:
@@ -329,7 +331,8 @@ class AsyncPS:
         if self.is_cuda and self.push_done[self.gb] is not None:
             # the push copies of step t-2 read this gradient buffer
             torch.cuda.current_stream(self.device).wait_event(self.push_done[self.gb])
-        self.grads[self.gb].zero_()
+        zero_grads_(self.grads[self.gb], self._zero_plan)
+        self._arrived = set()
         self._set_grad_views()
         for b in self.buckets:
             b.pending = len(b.params)
@@ -361,6 +364,7 @@ class AsyncPS:
         self._prefetched = (t, list(pulled))
 
     def _on_grad(self, p):
+        self._arrived.add(id(p))
         if id(p) in self._direct:
             v = self._grad_views[id(p)]
             if p.grad is not None and p.grad.data_ptr() != v.data_ptr():
@@ -375,6 +379,10 @@ class AsyncPS:
 
     def _push(self, b: _Bucket):
         g = self.grads[self.gb]
+        if b.pending > 0 and self._zero_plan is not None:  # flushed with gradients missing
+            for _n, p, _o, _k in b.params:
+                if id(p) in self._direct and id(p) not in self._arrived:
+                    self._grad_views[id(p)].zero_()
         if self.is_cuda:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.device))

@@ -59,6 +59,31 @@ class Bucket:
     launched: bool = False
 
 
+def zero_plan(spans, total: int, max_ranges: int = 8):
+    """Ranges of a flat gradient buffer to zero before a step: the merged ``(offset, numel)`` spans of
+    the parameters whose gradients are *accumulated* into their views (everything but the grad-sink
+    params, whose kernels overwrite their views). ``None`` (zero the whole buffer in one launch)
+    when that is most of the buffer or would take more than ``max_ranges`` launches. BERT-base:
+    the embeddings only, 24M of 110M elements."""
+    merged = []
+    for off, n in sorted(spans):
+        if merged and off <= merged[-1][0] + merged[-1][1]:
+            merged[-1][1] = max(merged[-1][1], off + n - merged[-1][0])
+        else:
+            merged.append([off, n])
+    if len(merged) > max_ranges or sum(n for _, n in merged) > total // 2:
+        return None
+    return [tuple(r) for r in merged]
+
+
+def zero_grads_(flat: torch.Tensor, plan) -> None:
+    if plan is None:
+        flat.zero_()
+        return
+    for off, n in plan:
+        flat.narrow(0, off, n).zero_()
+
+
 def _flat_view(flat: torch.Tensor, off: int, p: torch.Tensor) -> torch.Tensor:
     """View of ``flat[off:off+numel]`` with the same shape *and strides* as ``p`` (channels_last
     conv weights stay channels_last)."""
@@ -207,6 +232,11 @@ class CollectivePS:
                 self._grad_views[id(p)] = _flat_view(self.grads_flat, o, p)
                 p.grad = None if id(p) in self._direct else self._grad_views[id(p)]
         self._direct_params = [p for b in buckets for (_, p, _o, _n) in b.params if id(p) in self._direct]
+        # grad-sink views are overwritten every step: only the accumulated ones need zeroing (a sink
+        # param that gets no gradient in a step is zeroed when its bucket is flushed)
+        self._zero_plan = zero_plan([(o, p.numel()) for b in buckets for (_, p, o, _n) in b.params
+                                     if id(p) not in self._direct], self.grads_flat.numel())
+        self._arrived: set = set()
         self._hooks = []
         self._p2b = {}
         for b in buckets:
@@ -258,7 +288,8 @@ class CollectivePS:
         """Call before forward: zero the gradient buffer and reset bucket bookkeeping."""
         if track:
             self.account_begin()
-        self.grads_flat.zero_()
+        zero_grads_(self.grads_flat, self._zero_plan)
+        self._arrived = set()
         for p in self._direct_params:
             p.grad = None
         for b in self.buckets:
@@ -286,6 +317,7 @@ class CollectivePS:
         self.finish_step()
 
     def _on_grad(self, p):
+        self._arrived.add(id(p))
         if id(p) in self._direct:
             v = self._grad_views[id(p)]
             if p.grad is not None and p.grad.data_ptr() != v.data_ptr():
@@ -312,6 +344,10 @@ class CollectivePS:
 
     def _launch(self, b: Bucket):
         b.launched = True
+        if b.pending > 0 and self._zero_plan is not None:  # flushed with gradients missing
+            for _, p, _o, _n in b.params:
+                if id(p) in self._direct and id(p) not in self._arrived:
+                    self._grad_views[id(p)].zero_()
         if self.is_cuda:
             ev = self.ready_events[b.index]
             ev.record(torch.cuda.current_stream(self.device))

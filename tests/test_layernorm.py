@@ -70,3 +70,34 @@ def test_dropout_mask_changes_with_device_step(gpu):
     m3 = _mask(C, shape, 0.1, 6, s1, gpu)
     assert torch.equal(m1, m1b)  # regenerable (backward reuses it)
     assert not torch.equal(m1, m2) and not torch.equal(m1, m3)
+
+
+def test_residual_grad_handoff_matches_autograd_add(gpu, monkeypatch):
+    """BertLayer with each residual LayerNorm handing x's gradient to the Linear that also reads x
+    (accumulated by its bwd-data GEMM) vs the same layer with autograd adding the two gradients."""
+    from parameter_server_distributed_amd.models.bert import BertLayer
+    from parameter_server_distributed_amd.ops import layernorm as lnmod
+
+    torch.manual_seed(1)
+    layer = BertLayer(768, 12, 3072, dropout=0.0).to(gpu).to(torch.bfloat16)
+    step = torch.tensor([1], device=gpu, dtype=torch.int64)
+    for m in layer.modules():
+        if hasattr(m, "step"):
+            m.step = step
+    x0 = torch.randn(4, 128, 768, device=gpu).to(torch.bfloat16)
+
+    def run():
+        layer.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        y = layer(x)
+        y.float().pow(2).mean().backward()
+        return x.grad.float(), {n: p.grad.float().clone() for n, p in layer.named_parameters()}
+
+    gx, gp = run()
+    assert not layer.qkv._psd_pending_dx and not layer.ffn1._psd_pending_dx
+    orig = lnmod.FusedAddLayerNorm.forward
+    monkeypatch.setattr(lnmod.FusedAddLayerNorm, "forward", lambda self, x, h, x_grad_to=None: orig(self, x, h))
+    rx, rp = run()
+    torch.testing.assert_close(gx, rx, rtol=2e-2, atol=2e-2 * float(rx.abs().max()))
+    for n in rp:
+        torch.testing.assert_close(gp[n], rp[n], rtol=2e-2, atol=2e-2 * float(rp[n].abs().max()) + 1e-6, msg=n)
