@@ -86,9 +86,12 @@ void gemm_splitk_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool 
 void gemm_fp8_(const at::Tensor& A, const at::Tensor& B, const at::Tensor& a_scale, const at::Tensor& b_scale,
                at::Tensor out, c10::optional<at::Tensor> bias, int64_t act, c10::optional<at::Tensor> aux) {
   for (const at::Tensor* t : {&A, &B})
-    TORCH_CHECK(t->is_cuda() && t->dim() == 2 && t->scalar_type() == at::kFloat8_e4m3fn && t->stride(1) == 1 &&
-                    t->stride(0) % 16 == 0 && (reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0,
-                "psd gemm_fp8: operands must be 2-D e4m3fn device tensors, unit inner stride, 16-B aligned rows");
+    TORCH_CHECK(t->is_cuda() && t->dim() == 2 && t->stride(1) == 1 && t->stride(0) % 16 == 0 &&
+                    (reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0,
+                "psd gemm_fp8: operands must be 2-D fp8 device tensors, unit inner stride, 16-B aligned rows");
+  TORCH_CHECK((A.scalar_type() == at::kFloat8_e4m3fn || A.scalar_type() == at::kFloat8_e5m2) &&
+                  B.scalar_type() == at::kFloat8_e4m3fn,
+              "psd gemm_fp8: A e4m3fn or e5m2, B e4m3fn");
   const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
   TORCH_CHECK(B.size(1) == K, "psd gemm_fp8: K mismatch");
   TORCH_CHECK(K % 128 == 0, "psd gemm_fp8: K must be a multiple of 128");
@@ -116,6 +119,7 @@ void gemm_fp8_(const at::Tensor& A, const at::Tensor& B, const at::Tensor& a_sca
   a.c_f32 = out.scalar_type() == at::kFloat;
   a.a_scale = a_scale.data_ptr<float>();
   a.b_scale = b_scale.data_ptr<float>();
+  a.f8a = A.scalar_type() == at::kFloat8_e5m2 ? 1 : 0;
   hipError_t e = launch_gemm_fp8(a, stream_of(A));
   TORCH_CHECK(e == hipSuccess, "psd gemm_fp8: ", hipGetErrorString(e));
 }
@@ -129,9 +133,11 @@ static bool conv_fwd_impl(const at::Tensor& x, const at::Tensor& w2, at::Tensor 
                           int64_t stride, int64_t pad, const at::Tensor* xs, const at::Tensor* ws) {
   const bool f8 = xs != nullptr;
   const auto dt = f8 ? at::kFloat8_e4m3fn : at::kBFloat16;
+  const bool x_e5 = f8 && x.scalar_type() == at::kFloat8_e5m2;  // bwd-data: e5m2 dY
   const int esz = f8 ? 1 : 2;
-  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.scalar_type() == dt && x.is_contiguous(at::MemoryFormat::ChannelsLast),
-              "psd conv_fwd: x must be a channels_last ", f8 ? "e4m3fn" : "bf16", " device tensor");
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && (x.scalar_type() == dt || x_e5) &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "psd conv_fwd: x must be a channels_last ", f8 ? "e4m3fn / e5m2" : "bf16", " device tensor");
   TORCH_CHECK(w2.is_cuda() && w2.dim() == 2 && w2.scalar_type() == dt && w2.stride(1) == 1 &&
                   (w2.stride(0) * esz) % 16 == 0 && (reinterpret_cast<uintptr_t>(w2.data_ptr()) & 15) == 0,
               "psd conv_fwd: w2 must be a 2-D device tensor like x, unit inner stride, 16-B aligned rows");
@@ -174,6 +180,7 @@ static bool conv_fwd_impl(const at::Tensor& x, const at::Tensor& w2, at::Tensor 
   if (f8) {
     a.a_scale = xs->data_ptr<float>();
     a.b_scale = ws->data_ptr<float>();
+    a.f8a = x_e5 ? 1 : 0;
   }
   hipError_t e = f8 ? launch_conv_fwd_fp8(a, stream_of(x)) : launch_conv_fwd(a, stream_of(x));
   if (e == hipErrorNotSupported) return false;

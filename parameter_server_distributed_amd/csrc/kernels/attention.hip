@@ -165,8 +165,12 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnArgs a) {
   }
 }
 
+// 2*NW waves: the LDS image (Q, K, V, dO, Pd, dS: ~144 KiB at S = 128) allows one workgroup per
+// CU, so a 32-row block is split between two waves (query blocks / head-dim halves) to keep two
+// waves per SIMD: at one wave per SIMD (the first version) nothing hid the LDS and MFMA latencies
+// and the kernel ran at 3.5x its HBM time (profiles/bert_base_b256_r2_kernels.md).
 template <int NW>
-__global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a) {
+__global__ __launch_bounds__(128 * NW) void attn_bwd_kernel(AttnArgs a) {
   constexpr int S = 32 * NW, LDP = S + 8;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* Qs = smem;
@@ -178,7 +182,8 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a) {
   float* lse_s = reinterpret_cast<float*>(dS + S * LDP * 2);
   float* D_s = lse_s + S;
 
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5;
+  const int lane = threadIdx.x & 63, hh = lane >> 5;
+  const int w = threadIdx.x >> 7, sub = (threadIdx.x >> 6) & 1;  // 32-row block, half of its work
   const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;
   const int HD = a.H * D;
   const int64_t qkv_rs = 3 * (int64_t)HD;
@@ -205,7 +210,8 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a) {
   }
   __syncthreads();
 
-  // phase 1: wave w owns keys k0..k0+31; recompute S^T and dP^T against every query block
+  // phase 1: waves (w, sub) own keys k0..k0+31; recompute S^T and dP^T against the query blocks
+  // t = sub, sub + 2, ...
   const int k0 = 32 * w;
   abf16x8 kf[4], vf[4];
 #pragma unroll
@@ -217,7 +223,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a) {
   const bool drop = a.thresh != 0u;
   const float sl = a.scale * 1.4426950408889634f;
 #pragma unroll
-  for (int t = 0; t < NW; ++t) {
+  for (int t = sub; t < NW; t += 2) {
     af32x16 st = zero16(), dpt = zero16();
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
@@ -251,9 +257,10 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a) {
   __syncthreads();
 
   // phase 2: dV[key, d] = sum_q Pd[q, key] dO[q, d];  dK = scale * sum_q dS[q, key] Q[q, d]
+  // (wave (w, sub): keys of block w, head dims 32*sub..)
   uint16_t* dq_base = a.dqkv + (int64_t)b * S * qkv_rs + h * D;
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt) {
+  {
+    const int dt = sub;
     af32x16 dv = zero16(), dk = zero16();
 #pragma unroll
     for (int ks = 0; ks < S / 16; ++ks) {
@@ -268,10 +275,10 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a) {
       dq_base[r + 2 * HD] = f32_to_bf16(dv[i]);
     }
   }
-  // phase 3: wave w owns queries q0..q0+31: dQ = scale * dS K
+  // phase 3: waves (w, sub) own queries q0..q0+31, head dims 32*sub..: dQ = scale * dS K
   const int q0 = 32 * w;
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt) {
+  {
+    const int dt = sub;
     af32x16 dq = zero16();
 #pragma unroll
     for (int ks = 0; ks < S / 16; ++ks) dq = mfma(rowfrag(dS, LDP * 2, q0, 16 * ks), trfrag(Ks, LDT * 2, 16 * ks, 32 * dt), dq);
@@ -301,7 +308,7 @@ static hipError_t launch_bwd_t(const AttnArgs& a, hipStream_t st) {
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd_kernel<NW>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(attn_bwd_kernel<NW>, dim3(a.B * a.H), dim3(64 * NW), lds, st, a);
+  hipLaunchKernelGGL(attn_bwd_kernel<NW>, dim3(a.B * a.H), dim3(128 * NW), lds, st, a);
   return hipGetLastError();
 }
 

@@ -19,15 +19,32 @@ __device__ __forceinline__ float e4m3_to_f32(uint8_t b) {
 __device__ __forceinline__ uint8_t f32_to_e4m3(float x) {
   return (uint8_t)__hip_cvt_float_to_fp8(x, __HIP_SATFINITE, __HIP_E4M3);
 }
+__device__ __forceinline__ uint8_t f32_to_e5m2(float x) {
+  return (uint8_t)__hip_cvt_float_to_fp8(x, __HIP_SATFINITE, __HIP_E5M2);
+}
+template <bool E5>
+__device__ __forceinline__ uint8_t f32_to_f8(float x) {
+  if constexpr (E5) return f32_to_e5m2(x);
+  else return f32_to_e4m3(x);
+}
 
 template <int DT>
 __global__ __launch_bounds__(256) void amax_kernel(const void* __restrict__ x, int64_t n, float* amax) {
   float m = 0.f;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    float v = (DT == DT_BF16) ? bf16_to_f32(static_cast<const uint16_t*>(x)[i]) : static_cast<const float*>(x)[i];
-    m = fmaxf(m, fabsf(v));
+  const int64_t nvec = n >> 3;  // 16-byte loads (bf16) / two 16-byte loads (fp32) per lane
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    float t[8];
+    if (DT == DT_BF16) load8_bf16(static_cast<const uint16_t*>(x) + (v << 3), t);
+    else load8_f32(static_cast<const float*>(x) + (v << 3), t);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(t[e]));
   }
+  if (blockIdx.x == 0)
+    for (int64_t i = (nvec << 3) + threadIdx.x; i < n; i += blockDim.x) {
+      const float v = (DT == DT_BF16) ? bf16_to_f32(static_cast<const uint16_t*>(x)[i]) : static_cast<const float*>(x)[i];
+      m = fmaxf(m, fabsf(v));
+    }
   // wave64 butterfly, then one LDS slot per wave
   for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, kWave));
   __shared__ float red[4];
@@ -41,7 +58,116 @@ __global__ __launch_bounds__(256) void amax_kernel(const void* __restrict__ x, i
   }
 }
 
+// ---- just-in-time per-tensor quantisation in two launches, no atomics and no zero-fill:
+// amax_partial writes one max per block (16-byte loads, 4 in flight per lane); the quant kernel's
+// blocks each reduce those <= kAmaxBlocks partials (4 KiB, L2-resident) before quantising. The first
+// version (one 2-byte load per lane per iteration, a per-call atomic into a zeroed scalar) took
+// 47 us per call and 11 % of the Wide-ResNet-101-2 fp8 step (profiles/wrn101_2_fp8_b512_r2_kernels.md).
+constexpr int kAmaxBlocks = 1024;
+
+__device__ __forceinline__ float block_max(float m) {
+  for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, kWave));
+  __shared__ float red[4];
+  const int wid = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  if (lane == 0) red[wid] = m;
+  __syncthreads();
+  return fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+template <bool E5>
+__device__ __forceinline__ uint8_t f32_to_f8_(float x) {
+  return (uint8_t)__hip_cvt_float_to_fp8(x, __HIP_SATFINITE, E5 ? __HIP_E5M2 : __HIP_E4M3);
+}
+
 template <int DT>
+__global__ __launch_bounds__(256) void amax_partial_kernel(const void* __restrict__ x, int64_t n, float* __restrict__ part) {
+  float m = 0.f;
+  const int64_t nvec = n >> 3;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  auto ld = [&](int64_t vi, float (&t)[8]) {
+    if (DT == DT_BF16) load8_bf16(static_cast<const uint16_t*>(x) + (vi << 3), t);
+    else load8_f32(static_cast<const float*>(x) + (vi << 3), t);
+  };
+  for (; v + 3 * stride < nvec; v += 4 * stride) {
+    float t[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) ld(v + u * stride, t[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(t[u][e]));
+  }
+  for (; v < nvec; v += stride) {
+    float t[8];
+    ld(v, t);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(t[e]));
+  }
+  if (blockIdx.x == 0)
+    for (int64_t i = (nvec << 3) + threadIdx.x; i < n; i += blockDim.x) {
+      const float f = (DT == DT_BF16) ? bf16_to_f32(static_cast<const uint16_t*>(x)[i]) : static_cast<const float*>(x)[i];
+      m = fmaxf(m, fabsf(f));
+    }
+  m = block_max(m);
+  if (threadIdx.x == 0) part[blockIdx.x] = m;
+}
+
+template <int DT, bool E5>
+__global__ __launch_bounds__(256) void quant_part_kernel(const void* __restrict__ x, int64_t n,
+                                                         const float* __restrict__ part, int nparts, float fp8_max,
+                                                         uint8_t* __restrict__ out, float* scale_inv) {
+  float pm = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) pm = fmaxf(pm, part[i]);
+  const float a = fmaxf(block_max(pm), 1e-12f);
+  const float scale = fp8_max / a;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && scale_inv) *scale_inv = a / fp8_max;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t nvec = n >> 3;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    const int64_t i = v << 3;
+    float t[8];
+    if (DT == DT_BF16) load8_bf16(static_cast<const uint16_t*>(x) + i, t);
+    else load8_f32(static_cast<const float*>(x) + i, t);
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) lo |= (uint32_t)f32_to_f8_<E5>(t[e] * scale) << (8 * e);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) hi |= (uint32_t)f32_to_f8_<E5>(t[4 + e] * scale) << (8 * e);
+    *reinterpret_cast<uint2*>(out + i) = make_uint2(lo, hi);
+  }
+  if (blockIdx.x == 0)
+    for (int64_t i = (nvec << 3) + threadIdx.x; i < n; i += blockDim.x) {
+      const float f = (DT == DT_BF16) ? bf16_to_f32(static_cast<const uint16_t*>(x)[i]) : static_cast<const float*>(x)[i];
+      out[i] = f32_to_f8_<E5>(f * scale);
+    }
+}
+
+template <int DT>
+static void launch_jit_t(const void* x, int64_t n, float* part, int nb, int gq, float fp8_max, uint8_t* out,
+                         float* scale_inv, hipStream_t st, int e5m2) {
+  hipLaunchKernelGGL(amax_partial_kernel<DT>, dim3((unsigned)nb), dim3(256), 0, st, x, n, part);
+  if (e5m2)
+    hipLaunchKernelGGL((quant_part_kernel<DT, true>), dim3(gq), dim3(256), 0, st, x, n, part, nb, fp8_max, out, scale_inv);
+  else
+    hipLaunchKernelGGL((quant_part_kernel<DT, false>), dim3(gq), dim3(256), 0, st, x, n, part, nb, fp8_max, out, scale_inv);
+}
+
+hipError_t launch_quant_fp8_jit(const void* x, int32_t dt, int64_t n, float* part, float fp8_max, uint8_t* out,
+                                float* scale_inv, hipStream_t st, int e5m2) {
+  if (n <= 0) return hipSuccess;
+  if (dt != DT_BF16 && dt != DT_F32) return hipErrorInvalidValue;
+  int64_t nb = ((n >> 3) + 256 * 8 - 1) / (256 * 8);  // >= 8 vectors per lane
+  if (nb < 1) nb = 1;
+  if (nb > kAmaxBlocks) nb = kAmaxBlocks;
+  const int gq = stream_grid((n >> 3) > 0 ? (n >> 3) : 1, 256);
+  if (dt == DT_BF16) launch_jit_t<DT_BF16>(x, n, part, (int)nb, gq, fp8_max, out, scale_inv, st, e5m2);
+  else launch_jit_t<DT_F32>(x, n, part, (int)nb, gq, fp8_max, out, scale_inv, st, e5m2);
+  return hipGetLastError();
+}
+
+// E5: OCP e5m2 output (gradients), else e4m3
+template <int DT, bool E5>
 __global__ __launch_bounds__(256) void quant_kernel(const void* __restrict__ x, int64_t n, const float* amax,
                                                     float fp8_max, uint8_t* __restrict__ out, float* scale_inv) {
   const float a = fmaxf(*amax, 1e-12f);
@@ -56,15 +182,15 @@ __global__ __launch_bounds__(256) void quant_kernel(const void* __restrict__ x, 
     else load8_f32(static_cast<const float*>(x) + i, t);
     uint32_t lo = 0, hi = 0;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) lo |= (uint32_t)f32_to_e4m3(t[e] * scale) << (8 * e);
+    for (int e = 0; e < 4; ++e) lo |= (uint32_t)f32_to_f8<E5>(t[e] * scale) << (8 * e);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) hi |= (uint32_t)f32_to_e4m3(t[4 + e] * scale) << (8 * e);
+    for (int e = 0; e < 4; ++e) hi |= (uint32_t)f32_to_f8<E5>(t[4 + e] * scale) << (8 * e);
     *reinterpret_cast<uint2*>(out + i) = make_uint2(lo, hi);
   }
   if (blockIdx.x == 0)
     for (int64_t i = (nvec << 3) + threadIdx.x; i < n; i += blockDim.x) {
       float v = (DT == DT_BF16) ? bf16_to_f32(static_cast<const uint16_t*>(x)[i]) : static_cast<const float*>(x)[i];
-      out[i] = f32_to_e4m3(v * scale);
+      out[i] = f32_to_f8<E5>(v * scale);
     }
 }
 
@@ -82,7 +208,7 @@ __global__ __launch_bounds__(256) void dequant_kernel(const uint8_t* __restrict_
 
 hipError_t launch_amax(const void* x, int32_t dt, int64_t n, float* amax, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  const int grid = stream_grid(n, 256);
+  const int grid = stream_grid((n >> 3) > 0 ? (n >> 3) : 1, 256);
   if (dt == DT_BF16) hipLaunchKernelGGL(amax_kernel<DT_BF16>, dim3(grid), dim3(256), 0, st, x, n, amax);
   else if (dt == DT_F32) hipLaunchKernelGGL(amax_kernel<DT_F32>, dim3(grid), dim3(256), 0, st, x, n, amax);
   else return hipErrorInvalidValue;
@@ -90,13 +216,17 @@ hipError_t launch_amax(const void* x, int32_t dt, int64_t n, float* amax, hipStr
 }
 
 hipError_t launch_quant_fp8(const void* x, int32_t dt, int64_t n, const float* amax, float fp8_max, uint8_t* out,
-                            float* scale_inv, hipStream_t st) {
+                            float* scale_inv, hipStream_t st, int e5m2) {
   if (n <= 0) return hipSuccess;
   const int grid = stream_grid((n >> 3) > 0 ? (n >> 3) : 1, 256);
-  if (dt == DT_BF16)
-    hipLaunchKernelGGL(quant_kernel<DT_BF16>, dim3(grid), dim3(256), 0, st, x, n, amax, fp8_max, out, scale_inv);
+  if (dt == DT_BF16 && e5m2)
+    hipLaunchKernelGGL((quant_kernel<DT_BF16, true>), dim3(grid), dim3(256), 0, st, x, n, amax, fp8_max, out, scale_inv);
+  else if (dt == DT_BF16)
+    hipLaunchKernelGGL((quant_kernel<DT_BF16, false>), dim3(grid), dim3(256), 0, st, x, n, amax, fp8_max, out, scale_inv);
+  else if (dt == DT_F32 && e5m2)
+    hipLaunchKernelGGL((quant_kernel<DT_F32, true>), dim3(grid), dim3(256), 0, st, x, n, amax, fp8_max, out, scale_inv);
   else if (dt == DT_F32)
-    hipLaunchKernelGGL(quant_kernel<DT_F32>, dim3(grid), dim3(256), 0, st, x, n, amax, fp8_max, out, scale_inv);
+    hipLaunchKernelGGL((quant_kernel<DT_F32, false>), dim3(grid), dim3(256), 0, st, x, n, amax, fp8_max, out, scale_inv);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }

@@ -758,7 +758,8 @@ __device__ __forceinline__ float act_apply(float x) {
 // GA: A is gathered as an implicit-GEMM convolution input (GemmArgs cv_*): each lane's A rows are
 // output pixels whose (r, s)-shifted input pixel is computed per K-tile (one (r, s) per K-tile:
 // C % 64 == 0); pixels outside the image get an offset past the descriptor, i.e. the zero padding.
-template <int BM, bool AK, bool BKM, int MODE, bool F8 = false, int ACT = 0, bool GA = false>
+// F8A: the A operand's fp8 format (0 e4m3, 1 e5m2: bwd-data of the fp8 convolutions takes e5m2 dY)
+template <int BM, bool AK, bool BKM, int MODE, bool F8 = false, int ACT = 0, bool GA = false, int F8A = 0>
 __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
   static_assert(!F8 || (AK && BKM), "fp8 GEMM takes K-major operands");
   static_assert(!GA || (AK && MODE == 0), "implicit-GEMM convolution: K-major A, single split");
@@ -902,7 +903,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[(q * IM + i) * 2 + j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
-              fa[i], fb[j], acc[(q * IM + i) * 2 + j], 0, 0, 0, 127, 0, 127);
+              fa[i], fb[j], acc[(q * IM + i) * 2 + j], F8A, 0, 0, 127, 0, 127);
     } else {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
@@ -1319,12 +1320,12 @@ static int persistent_grid() {
   return n;
 }
 
-template <int BM, bool AK, bool BKM, int MODE, bool F8, int ACT, bool GA = false>
+template <int BM, bool AK, bool BKM, int MODE, bool F8, int ACT, bool GA = false, int F8A = 0>
 static hipError_t launch_8p_act(const GemmArgs& g, int splits, hipStream_t st) {
   constexpr int lds = P8<BM>::LDS;
   static bool attr_set = false;  // per instantiation: set the >64 KiB LDS limit once
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT, GA>,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT, GA, F8A>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     attr_set = true;
@@ -1341,7 +1342,7 @@ static hipError_t launch_8p_act(const GemmArgs& g, int splits, hipStream_t st) {
   }();
   GemmArgs ga = g;
   ga.dbg = dbg;
-  hipLaunchKernelGGL((gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT, GA>), dim3(grid, 1, splits), dim3(512), lds, st, ga);
+  hipLaunchKernelGGL((gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT, GA, F8A>), dim3(grid, 1, splits), dim3(512), lds, st, ga);
   return hipGetLastError();
 }
 
@@ -1460,8 +1461,12 @@ hipError_t launch_conv_fwd_fp8(const GemmArgs& g, hipStream_t st) {
                   g.cv_abytes > 0 && (int64_t)(g.M - 1) * g.ldc + g.N < ((int64_t)1 << 31) && g.cv_S > 0 &&
                   g.cv_W < 32768 && g.cv_H < 32768;
   if (!ok) return hipErrorNotSupported;
-  return pick_bm(g.M, g.N, 1) == 128 ? launch_8p_act<128, true, true, 0, true, 0, true>(g, 1, st)
-                                     : launch_8p_act<256, true, true, 0, true, 0, true>(g, 1, st);
+  const bool b128 = pick_bm(g.M, g.N, 1) == 128;
+  if (g.f8a == 1)
+    return b128 ? launch_8p_act<128, true, true, 0, true, 0, true, 1>(g, 1, st)
+                : launch_8p_act<256, true, true, 0, true, 0, true, 1>(g, 1, st);
+  return b128 ? launch_8p_act<128, true, true, 0, true, 0, true>(g, 1, st)
+              : launch_8p_act<256, true, true, 0, true, 0, true>(g, 1, st);
 }
 
 hipError_t launch_gemm_fp8(const GemmArgs& g, hipStream_t st) {
@@ -1469,6 +1474,11 @@ hipError_t launch_gemm_fp8(const GemmArgs& g, hipStream_t st) {
   if (g.K % 128 != 0 || !g.a_kmajor || !g.b_kmajor || !g.a_scale || !g.b_scale || !fits_rsrc(g, 1) ||
       g.N % 8 != 0 || g.ldc % 8 != 0 || (reinterpret_cast<uintptr_t>(g.bias) & 3))
     return hipErrorInvalidValue;
+  if (g.f8a == 1) {  // e5m2 A (fp8 bwd-data): no bias / activation
+    if (g.bias || g.act) return hipErrorInvalidValue;
+    return pick_bm(g.M, g.N, 1) == 128 ? launch_8p_act<128, true, true, 0, true, 0, false, 1>(g, 1, st)
+                                       : launch_8p_act<256, true, true, 0, true, 0, false, 1>(g, 1, st);
+  }
   return pick_bm(g.M, g.N, 1) == 128 ? launch_8p<128, true, true, 0, true>(g, 1, st)
                                      : launch_8p<256, true, true, 0, true>(g, 1, st);
 }

@@ -89,7 +89,10 @@ hipError_t launch_pack_cast(const PackSeg* segs, const int32_t* chunk_seg, const
 // fp32/bf16 -> fp8 e4m3fn (OCP) with a per-tensor scale; amax is reduced on device.
 hipError_t launch_amax(const void* x, int32_t dtype, int64_t n, float* amax_out, hipStream_t stream);
 hipError_t launch_quant_fp8(const void* x, int32_t dtype, int64_t n, const float* amax,
-                            float fp8_max, uint8_t* out, float* scale_inv_out, hipStream_t stream);
+                            float fp8_max, uint8_t* out, float* scale_inv_out, hipStream_t stream, int e5m2 = 0);
+// just-in-time per-tensor quantisation (amax partials + quantise, two launches); part: >= 1024 floats
+hipError_t launch_quant_fp8_jit(const void* x, int32_t dtype, int64_t n, float* part, float fp8_max, uint8_t* out,
+                                float* scale_inv, hipStream_t stream, int e5m2);
 hipError_t launch_dequant_fp8(const uint8_t* x, int64_t n, const float* scale_inv, void* out,
                               int32_t out_dtype, hipStream_t stream);
 

@@ -24,6 +24,7 @@ struct GemmArgs {
   // pixels, K = R*S*C ordered (r, s, ci), C a power of two >= 64; B = weights [Cout][R][S][C]
   int cv_H, cv_W, cv_logC, cv_Ho, cv_Wo, cv_S, cv_stride, cv_pad;
   uint32_t cv_abytes;  // input tensor bytes
+  int f8a;             // fp8 GEMMs: format of A (0 OCP e4m3, 1 OCP e5m2); B is always e4m3
 };
 
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t stream);

@@ -280,6 +280,7 @@ void amax_(const at::Tensor& x, at::Tensor amax_out) {
   TORCH_CHECK(x.is_contiguous(), "psd: amax input must be contiguous");
   if (x.is_cuda()) {
     const c10::DeviceGuard g(x.device());
+    if (x.numel() >= 8) check_aligned(x, "x");  // 16-byte vector loads
     hip_check(launch_amax(x.data_ptr(), dt_of(x), x.numel(), amax_out.data_ptr<float>(), cur_stream(x)), "amax");
     return;
   }
@@ -291,8 +292,9 @@ void amax_(const at::Tensor& x, at::Tensor amax_out) {
 }
 
 void quant_fp8_(const at::Tensor& x, const at::Tensor& amax, double fp8_max, at::Tensor out, at::Tensor scale_inv) {
-  TORCH_CHECK(out.scalar_type() == at::kFloat8_e4m3fn && out.numel() == x.numel() && out.is_contiguous(),
-              "psd: quant_fp8 out must be float8_e4m3fn like x");
+  const bool e5 = out.scalar_type() == at::kFloat8_e5m2;
+  TORCH_CHECK((out.scalar_type() == at::kFloat8_e4m3fn || e5) && out.numel() == x.numel() && out.is_contiguous(),
+              "psd: quant_fp8 out must be float8_e4m3fn or float8_e5m2 like x");
   TORCH_CHECK(x.is_contiguous(), "psd: quant_fp8 input must be contiguous");
   if (x.is_cuda()) {
     const c10::DeviceGuard g(x.device());
@@ -301,14 +303,35 @@ void quant_fp8_(const at::Tensor& x, const at::Tensor& amax, double fp8_max, at:
       TORCH_CHECK((reinterpret_cast<uintptr_t>(out.data_ptr()) & 7u) == 0, "psd: fp8 out must be 8-byte aligned");
     }
     hip_check(launch_quant_fp8(x.data_ptr(), dt_of(x), x.numel(), amax.data_ptr<float>(), (float)fp8_max,
-                               reinterpret_cast<uint8_t*>(out.data_ptr()), scale_inv.data_ptr<float>(), cur_stream(x)),
+                               reinterpret_cast<uint8_t*>(out.data_ptr()), scale_inv.data_ptr<float>(), cur_stream(x),
+                               e5 ? 1 : 0),
               "quant_fp8");
     return;
   }
   const float a = std::max(amax.data_ptr<float>()[0], 1e-12f);
   const float scale = (float)fp8_max / a;
   scale_inv.data_ptr<float>()[0] = a / (float)fp8_max;
-  out.copy_((x.to(at::kFloat) * scale).clamp(-fp8_max, fp8_max).to(at::kFloat8_e4m3fn));
+  out.copy_((x.to(at::kFloat) * scale).clamp(-fp8_max, fp8_max).to(out.scalar_type()));
+}
+
+// out = fp8(x * fp8_max / amax(x)), scale_inv = amax / fp8_max: amax found on the device in the same
+// call (out e4m3fn or e5m2; fp8_max follows the format)
+void quant_fp8_jit_(const at::Tensor& x, at::Tensor out, at::Tensor scale_inv) {
+  const bool e5 = out.scalar_type() == at::kFloat8_e5m2;
+  TORCH_CHECK((out.scalar_type() == at::kFloat8_e4m3fn || e5) && out.numel() == x.numel() && out.is_contiguous(),
+              "psd: quant_fp8_jit out must be float8_e4m3fn or float8_e5m2 like x");
+  TORCH_CHECK(x.is_contiguous() && x.is_cuda(), "psd: quant_fp8_jit input must be a contiguous device tensor");
+  TORCH_CHECK(scale_inv.scalar_type() == at::kFloat && scale_inv.numel() >= 1, "psd: scale_inv fp32[>=1]");
+  const c10::DeviceGuard g(x.device());
+  if (x.numel() >= 8) {
+    check_aligned(x, "x");
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(out.data_ptr()) & 7u) == 0, "psd: fp8 out must be 8-byte aligned");
+  }
+  at::Tensor part = at::empty({1024}, x.options().dtype(at::kFloat));
+  hip_check(launch_quant_fp8_jit(x.data_ptr(), dt_of(x), x.numel(), part.data_ptr<float>(), e5 ? 57344.f : 448.f,
+                                 reinterpret_cast<uint8_t*>(out.data_ptr()), scale_inv.data_ptr<float>(), cur_stream(x),
+                                 e5 ? 1 : 0),
+            "quant_fp8_jit");
 }
 
 void dequant_fp8_(const at::Tensor& x, const at::Tensor& scale_inv, at::Tensor out) {

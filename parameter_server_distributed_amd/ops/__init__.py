@@ -12,6 +12,7 @@ from .. import native
 from .optim import OptimConfig, OptimDyn, advance_, apply_no_advance_, fused_apply_  # noqa: F401
 
 FP8_E4M3_MAX = 448.0
+FP8_E5M2_MAX = 57344.0
 
 
 def multi_reduce_(out: torch.Tensor, srcs, scale: float = 1.0) -> torch.Tensor:
@@ -25,16 +26,20 @@ def pack_cast_(srcs, dsts) -> None:
     native().pack_cast_(list(srcs), list(dsts))
 
 
-def quantize_fp8(x: torch.Tensor, amax: torch.Tensor | None = None):
-    """Per-tensor OCP e4m3fn quantisation; returns ``(q, scale_inv)`` with ``x ~= q * scale_inv``."""
+def quantize_fp8(x: torch.Tensor, amax: torch.Tensor | None = None, e5m2: bool = False):
+    """Per-tensor OCP fp8 quantisation (e4m3fn, or e5m2 for gradients); returns ``(q, scale_inv)``
+    with ``x ~= q * scale_inv``."""
     C = native()
     x = x.contiguous()
+    q = torch.empty(x.shape, dtype=torch.float8_e5m2 if e5m2 else torch.float8_e4m3fn, device=x.device)
+    sinv = torch.empty(1, dtype=torch.float32, device=x.device)
+    if amax is None and x.is_cuda:  # amax + quantise in two launches, no atomics / zero-fill
+        C.quant_fp8_jit_(x, q, sinv)
+        return q, sinv
     if amax is None:
         amax = torch.zeros(1, dtype=torch.float32, device=x.device)
         C.amax_(x, amax)
-    q = torch.empty(x.shape, dtype=torch.float8_e4m3fn, device=x.device)
-    sinv = torch.empty(1, dtype=torch.float32, device=x.device)
-    C.quant_fp8_(x, amax, FP8_E4M3_MAX, q, sinv)
+    C.quant_fp8_(x, amax, FP8_E5M2_MAX if e5m2 else FP8_E4M3_MAX, q, sinv)
     return q, sinv
 
 

@@ -81,11 +81,12 @@ def _fp8_ok(k: int, n: int) -> bool:
     return k % 128 == 0 and k >= 256 and n >= 256 and n % 8 == 0 and _at.enabled("PSD_FP8_COMPUTE")
 
 
-def _q8(t2: torch.Tensor):
-    """Per-tensor OCP e4m3 quantisation of a contiguous tensor (just-in-time amax): (q, scale_inv)."""
+def _q8(t2: torch.Tensor, e5m2: bool = False):
+    """Per-tensor OCP fp8 quantisation of a contiguous tensor (just-in-time amax): (q, scale_inv).
+    e4m3 for activations and weights, e5m2 (wider range) for output gradients."""
     from . import quantize_fp8
 
-    return quantize_fp8(t2)
+    return quantize_fp8(t2, e5m2=e5m2)
 
 
 class _Conv1x1Fn(torch.autograd.Function):
@@ -96,6 +97,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         w2 = weight.reshape(cout, cin)
         x2 = _as_2d(x)
         ctx.save_for_backward(x, weight)
+        ctx.fp8 = fp8
         if fp8 and _fp8_ok(cin, cout):
             # fp8 forward / bf16 backward: e4m3 operands on the MX-scaled MFMA (2x the bf16 rate),
             # dequantised in the epilogue; backward runs on the saved bf16 x and W
@@ -133,6 +135,14 @@ class _Conv1x1Fn(torch.autograd.Function):
         dx = dw = None
         conv_bwd = torch.ops.aten.convolution_backward
         args = (None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1)
+        if need_x and ctx.fp8 and _fp8_ok(cout, cin):
+            # fp8 bwd-data: e5m2 dY (K-major [M, cout]) x e4m3 W^T ([cin, cout], K-major)
+            dyq, sdy = _q8(_as_2d(dy), e5m2=True)
+            wtq, swt = _q8(weight.reshape(cout, cin).t().contiguous())
+            out = torch.empty(n * h * w, cin, device=dy.device, dtype=dy.dtype)
+            _native().gemm_fp8_(dyq, wtq, sdy, swt, out)
+            dx = _from_2d(out, n, h, w)
+            need_x = False
         if need_x:
             w2 = weight.reshape(cout, cin)
             dy2 = _as_2d(dy)
@@ -215,14 +225,15 @@ def _igemm(x: torch.Tensor, w2: torch.Tensor, k: int, stride: int, pad: int):
     return _from_2d(out, n, ho, wo)
 
 
-def _igemm_fp8(x: torch.Tensor, w2: torch.Tensor, k: int, stride: int, pad: int):
-    """conv(x, w) with e4m3 operands on the implicit-GEMM kernel (per-tensor just-in-time scales),
-    bf16 channels_last out, or None when the kernel declines the shape."""
+def _igemm_fp8(x: torch.Tensor, w2: torch.Tensor, k: int, stride: int, pad: int, e5m2: bool = False):
+    """conv(x, w) with fp8 operands on the implicit-GEMM kernel (per-tensor just-in-time scales; x
+    e4m3, or e5m2 when it is an output gradient), bf16 channels_last out, or None when the kernel
+    declines the shape."""
     from .. import native
 
     n, c, h, w = x.shape
     ho, wo = (h + 2 * pad - k) // stride + 1, (w + 2 * pad - k) // stride + 1
-    xq, sx = _q8(x.permute(0, 2, 3, 1))  # the NHWC storage, quantised in place order
+    xq, sx = _q8(x.permute(0, 2, 3, 1), e5m2=e5m2)  # the NHWC storage, quantised in place order
     wq, sw = _q8(w2)
     out = torch.empty(n * ho * wo, w2.shape[0], device=x.device, dtype=x.dtype)
     if not native().conv_fwd_fp8_(xq.permute(0, 3, 1, 2), wq, sx, sw, out, k, k, stride, pad):
@@ -235,7 +246,7 @@ class _ConvFn(torch.autograd.Function):
     def forward(ctx, x, weight, stride, pad, fp8=False):
         cout, cin, k, _ = weight.shape
         n, _, h, w = x.shape
-        ctx.stride, ctx.pad = stride, pad
+        ctx.stride, ctx.pad, ctx.fp8 = stride, pad, fp8
         ctx.save_for_backward(x, weight)
 
         def miopen():
@@ -276,7 +287,14 @@ class _ConvFn(torch.autograd.Function):
             def miopen():
                 return conv_bwd(dy, x, weight, *args, [True, False, False])[0]
 
-            if stride == 1 and _igemm_ok(cout, cin) and 2 * pad == k - 1:
+            if stride == 1 and _igemm_ok(cout, cin) and 2 * pad == k - 1 and ctx.fp8 and cout % 128 == 0 \
+                    and _fp8_ok(k * k * cout, cin):
+                # fp8 bwd-data: e5m2 dY gathered by the implicit GEMM, e4m3 flipped weights
+                wf = weight.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, k * k * cout).contiguous()
+                dx = _igemm_fp8(dy, wf, k, 1, pad, e5m2=True)
+                if dx is None:
+                    dx = miopen()
+            elif stride == 1 and _igemm_ok(cout, cin) and 2 * pad == k - 1:
                 # dX = conv(dY, W'), W'[ci, r, s, co] = W[co, ci, k-1-r, k-1-s]: same kernel, same padding
                 wf = weight.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, k * k * cout).contiguous()
 
