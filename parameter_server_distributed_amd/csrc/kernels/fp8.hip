@@ -166,6 +166,66 @@ hipError_t launch_quant_fp8_jit(const void* x, int32_t dt, int64_t n, float* par
   return hipGetLastError();
 }
 
+// ---- delayed scaling (one read of x): quantise with the scale of the amax recorded by the previous
+// call of the same tensor role (hist[0] * margin) and record this call's amax into hist[1] (integer
+// atomicMax: non-negative floats order like their bit patterns); the roll kernel then moves
+// hist[1] -> hist[0] and clears hist[1] for the next call. Values above the previous amax saturate.
+template <int DT, bool E5>
+__global__ __launch_bounds__(256) void quant_delayed_kernel(const void* __restrict__ x, int64_t n, float* hist,
+                                                            float fp8_max, float margin, uint8_t* __restrict__ out,
+                                                            float* __restrict__ scale_inv) {
+  const float a = fmaxf(hist[0] * margin, 1e-12f);
+  const float scale = fp8_max / a;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *scale_inv = a / fp8_max;
+  float m = 0.f;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t nvec = n >> 3;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    const int64_t i = v << 3;
+    float t[8];
+    if (DT == DT_BF16) load8_bf16(static_cast<const uint16_t*>(x) + i, t);
+    else load8_f32(static_cast<const float*>(x) + i, t);
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(t[e]));
+#pragma unroll
+    for (int e = 0; e < 4; ++e) lo |= (uint32_t)f32_to_f8_<E5>(t[e] * scale) << (8 * e);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) hi |= (uint32_t)f32_to_f8_<E5>(t[4 + e] * scale) << (8 * e);
+    *reinterpret_cast<uint2*>(out + i) = make_uint2(lo, hi);
+  }
+  if (blockIdx.x == 0)
+    for (int64_t i = (nvec << 3) + threadIdx.x; i < n; i += blockDim.x) {
+      const float f = (DT == DT_BF16) ? bf16_to_f32(static_cast<const uint16_t*>(x)[i]) : static_cast<const float*>(x)[i];
+      m = fmaxf(m, fabsf(f));
+      out[i] = f32_to_f8_<E5>(f * scale);
+    }
+  m = block_max(m);
+  if (threadIdx.x == 0) atomicMax(reinterpret_cast<unsigned int*>(hist + 1), __float_as_uint(m));
+}
+
+__global__ void amax_roll_kernel(float* hist) {
+  hist[0] = hist[1];
+  hist[1] = 0.f;
+}
+
+hipError_t launch_quant_fp8_delayed(const void* x, int32_t dt, int64_t n, float* hist, float fp8_max, float margin,
+                                    uint8_t* out, float* scale_inv, hipStream_t st, int e5m2) {
+  if (n <= 0) return hipSuccess;
+  const int gq = stream_grid((n >> 3) > 0 ? (n >> 3) : 1, 256);
+  if (dt == DT_BF16 && e5m2)
+    hipLaunchKernelGGL((quant_delayed_kernel<DT_BF16, true>), dim3(gq), dim3(256), 0, st, x, n, hist, fp8_max, margin, out, scale_inv);
+  else if (dt == DT_BF16)
+    hipLaunchKernelGGL((quant_delayed_kernel<DT_BF16, false>), dim3(gq), dim3(256), 0, st, x, n, hist, fp8_max, margin, out, scale_inv);
+  else if (dt == DT_F32 && e5m2)
+    hipLaunchKernelGGL((quant_delayed_kernel<DT_F32, true>), dim3(gq), dim3(256), 0, st, x, n, hist, fp8_max, margin, out, scale_inv);
+  else if (dt == DT_F32)
+    hipLaunchKernelGGL((quant_delayed_kernel<DT_F32, false>), dim3(gq), dim3(256), 0, st, x, n, hist, fp8_max, margin, out, scale_inv);
+  else return hipErrorInvalidValue;
+  hipLaunchKernelGGL(amax_roll_kernel, dim3(1), dim3(1), 0, st, hist);
+  return hipGetLastError();
+}
+
 // E5: OCP e5m2 output (gradients), else e4m3
 template <int DT, bool E5>
 __global__ __launch_bounds__(256) void quant_kernel(const void* __restrict__ x, int64_t n, const float* amax,

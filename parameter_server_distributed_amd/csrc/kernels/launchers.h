@@ -93,6 +93,10 @@ hipError_t launch_quant_fp8(const void* x, int32_t dtype, int64_t n, const float
 // just-in-time per-tensor quantisation (amax partials + quantise, two launches); part: >= 1024 floats
 hipError_t launch_quant_fp8_jit(const void* x, int32_t dtype, int64_t n, float* part, float fp8_max, uint8_t* out,
                                 float* scale_inv, hipStream_t stream, int e5m2);
+// delayed-scaling quantisation: scale from hist[0] * margin (the previous call's amax), this call's
+// amax recorded and rolled into hist[0] (hist: 2 device floats, hist[1] == 0 between calls)
+hipError_t launch_quant_fp8_delayed(const void* x, int32_t dtype, int64_t n, float* hist, float fp8_max, float margin,
+                                    uint8_t* out, float* scale_inv, hipStream_t stream, int e5m2);
 hipError_t launch_dequant_fp8(const uint8_t* x, int64_t n, const float* scale_inv, void* out,
                               int32_t out_dtype, hipStream_t stream);
 

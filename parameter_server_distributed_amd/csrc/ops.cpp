@@ -334,6 +334,26 @@ void quant_fp8_jit_(const at::Tensor& x, at::Tensor out, at::Tensor scale_inv) {
             "quant_fp8_jit");
 }
 
+// delayed scaling: out = fp8(x * fp8_max / (hist[0] * margin)); this call's amax -> hist[0] afterwards
+void quant_fp8_delayed_(const at::Tensor& x, at::Tensor out, at::Tensor scale_inv, at::Tensor hist, double margin) {
+  const bool e5 = out.scalar_type() == at::kFloat8_e5m2;
+  TORCH_CHECK((out.scalar_type() == at::kFloat8_e4m3fn || e5) && out.numel() == x.numel() && out.is_contiguous(),
+              "psd: quant_fp8_delayed out must be float8_e4m3fn or float8_e5m2 like x");
+  TORCH_CHECK(x.is_contiguous() && x.is_cuda(), "psd: quant_fp8_delayed input must be a contiguous device tensor");
+  TORCH_CHECK(scale_inv.scalar_type() == at::kFloat && scale_inv.numel() >= 1 && hist.scalar_type() == at::kFloat &&
+                  hist.numel() >= 2 && hist.is_cuda() && hist.is_contiguous(),
+              "psd: scale_inv fp32[>=1], hist fp32[2] device tensors");
+  const c10::DeviceGuard g(x.device());
+  if (x.numel() >= 8) {
+    check_aligned(x, "x");
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(out.data_ptr()) & 7u) == 0, "psd: fp8 out must be 8-byte aligned");
+  }
+  hip_check(launch_quant_fp8_delayed(x.data_ptr(), dt_of(x), x.numel(), hist.data_ptr<float>(), e5 ? 57344.f : 448.f,
+                                     (float)margin, reinterpret_cast<uint8_t*>(out.data_ptr()),
+                                     scale_inv.data_ptr<float>(), cur_stream(x), e5 ? 1 : 0),
+            "quant_fp8_delayed");
+}
+
 void dequant_fp8_(const at::Tensor& x, const at::Tensor& scale_inv, at::Tensor out) {
   TORCH_CHECK(x.scalar_type() == at::kFloat8_e4m3fn && out.numel() == x.numel(), "psd: dequant_fp8 shape/dtype");
   if (x.is_cuda()) {

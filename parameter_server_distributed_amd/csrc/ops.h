@@ -14,6 +14,7 @@ void pack_cast_(const std::vector<at::Tensor>& srcs, const std::vector<at::Tenso
 void amax_(const at::Tensor& x, at::Tensor amax_out);
 void quant_fp8_(const at::Tensor& x, const at::Tensor& amax, double fp8_max, at::Tensor out, at::Tensor scale_inv);
 void quant_fp8_jit_(const at::Tensor& x, at::Tensor out, at::Tensor scale_inv);
+void quant_fp8_delayed_(const at::Tensor& x, at::Tensor out, at::Tensor scale_inv, at::Tensor hist, double margin);
 void dequant_fp8_(const at::Tensor& x, const at::Tensor& scale_inv, at::Tensor out);
 
 std::vector<at::Tensor> bn_fwd(const at::Tensor& x, c10::optional<at::Tensor> gamma, c10::optional<at::Tensor> beta,

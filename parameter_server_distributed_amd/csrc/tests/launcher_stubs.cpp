@@ -16,7 +16,14 @@ hipError_t launch_pack_cast(const PackSeg*, const int32_t*, const int64_t*, int6
   return hipErrorNotSupported;
 }
 hipError_t launch_amax(const void*, int32_t, int64_t, float*, hipStream_t) { return hipErrorNotSupported; }
-hipError_t launch_quant_fp8(const void*, int32_t, int64_t, const float*, float, uint8_t*, float*, hipStream_t) {
+hipError_t launch_quant_fp8(const void*, int32_t, int64_t, const float*, float, uint8_t*, float*, hipStream_t, int) {
+  return hipErrorNotSupported;
+}
+hipError_t launch_quant_fp8_jit(const void*, int32_t, int64_t, float*, float, uint8_t*, float*, hipStream_t, int) {
+  return hipErrorNotSupported;
+}
+hipError_t launch_quant_fp8_delayed(const void*, int32_t, int64_t, float*, float, float, uint8_t*, float*, hipStream_t,
+                                    int) {
   return hipErrorNotSupported;
 }
 hipError_t launch_dequant_fp8(const uint8_t*, int64_t, const float*, void*, int32_t, hipStream_t) {

@@ -81,27 +81,61 @@ def _fp8_ok(k: int, n: int) -> bool:
     return k % 128 == 0 and k >= 256 and n >= 256 and n % 8 == 0 and _at.enabled("PSD_FP8_COMPUTE")
 
 
-def _q8(t2: torch.Tensor, e5m2: bool = False):
-    """Per-tensor OCP fp8 quantisation of a contiguous tensor (just-in-time amax): (q, scale_inv).
-    e4m3 for activations and weights, e5m2 (wider range) for output gradients."""
+def _q8(t2: torch.Tensor, e5m2: bool = False, scaler: "DelayedScale | None" = None):
+    """Per-tensor OCP fp8 quantisation of a contiguous tensor: (q, scale_inv). e4m3 for activations
+    and weights, e5m2 (wider range) for output gradients. Weights: just-in-time amax (two launches);
+    activations / gradients with a ``scaler``: delayed scaling (one pass, see DelayedScale)."""
     from . import quantize_fp8
 
+    if scaler is not None:
+        return scaler.quantize(t2, e5m2)
     return quantize_fp8(t2, e5m2=e5m2)
+
+
+class DelayedScale:
+    """Delayed fp8 scaling for one tensor role of one layer (its input activations, or its output
+    gradient): each call quantises with the amax the previous call recorded (times ``margin``) and
+    records its own in the same pass (kernels/fp8.hip quant_delayed_kernel), so the tensor is read
+    once instead of twice (amax pass + quantise pass). The first call scales just-in-time and seeds
+    the history. Values above the previous step's amax saturate at the fp8 maximum. The history is a
+    device tensor, so a captured hipGraph keeps updating it. ``PSD_FP8_DELAYED=0``: always
+    just-in-time."""
+
+    def __init__(self, margin: float = 1.0):
+        self.margin = float(margin)
+        self.hist = None
+
+    def quantize(self, x: torch.Tensor, e5m2: bool):
+        from . import FP8_E4M3_MAX, FP8_E5M2_MAX, quantize_fp8
+
+        x = x.contiguous()
+        if self.hist is None or self.hist.device != x.device or not _at.enabled("PSD_FP8_DELAYED"):
+            q, sinv = quantize_fp8(x, e5m2=e5m2)
+            if _at.enabled("PSD_FP8_DELAYED"):
+                self.hist = torch.zeros(2, dtype=torch.float32, device=x.device)
+                self.hist[:1].copy_(sinv * (FP8_E5M2_MAX if e5m2 else FP8_E4M3_MAX) / self.margin)
+            return q, sinv
+        q = torch.empty(x.shape, dtype=torch.float8_e5m2 if e5m2 else torch.float8_e4m3fn, device=x.device)
+        sinv = torch.empty(1, dtype=torch.float32, device=x.device)
+        _native().quant_fp8_delayed_(x, q, sinv, self.hist, self.margin)
+        return q, sinv
 
 
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, fp8=False):
+    def forward(ctx, x, weight, f8=None):
+        """``f8``: (activation scaler, gradient scaler) of an fp8 module, else None."""
+        fp8 = f8 is not None
         n, cin, h, w = x.shape
         cout = weight.shape[0]
         w2 = weight.reshape(cout, cin)
         x2 = _as_2d(x)
         ctx.save_for_backward(x, weight)
-        ctx.fp8 = fp8
+        ctx.fp8, ctx.f8 = fp8, f8
         if fp8 and _fp8_ok(cin, cout):
-            # fp8 forward / bf16 backward: e4m3 operands on the MX-scaled MFMA (2x the bf16 rate),
-            # dequantised in the epilogue; backward runs on the saved bf16 x and W
-            xq, sx = _q8(x2)
+            # fp8 forward: e4m3 operands on the MX-scaled MFMA (2x the bf16 rate), dequantised in the
+            # epilogue; the weight gradient runs on the saved bf16 x and W
+            xq, sx = _q8(x2, scaler=f8[0])
             wq, sw = _q8(w2)
             out = torch.empty(n * h * w, cout, device=x.device, dtype=x.dtype)
             _native().gemm_fp8_(xq, wq, sx, sw, out)
@@ -137,7 +171,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         args = (None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1)
         if need_x and ctx.fp8 and _fp8_ok(cout, cin):
             # fp8 bwd-data: e5m2 dY (K-major [M, cout]) x e4m3 W^T ([cin, cout], K-major)
-            dyq, sdy = _q8(_as_2d(dy), e5m2=True)
+            dyq, sdy = _q8(_as_2d(dy), e5m2=True, scaler=ctx.f8[1])
             wtq, swt = _q8(weight.reshape(cout, cin).t().contiguous())
             out = torch.empty(n * h * w, cin, device=dy.device, dtype=dy.dtype)
             _native().gemm_fp8_(dyq, wtq, sdy, swt, out)
@@ -188,13 +222,14 @@ class Conv1x1(nn.Conv2d):
 
     def __init__(self, cin: int, cout: int, fp8: bool = False):
         super().__init__(cin, cout, 1, stride=1, padding=0, bias=False)
-        self.fp8 = fp8  # fp8 forward (e4m3 MFMA) / bf16 backward where the shape allows
+        self.fp8 = fp8  # fp8 forward (e4m3) and bwd-data (e5m2 dY) where the shape allows
+        self._f8 = (DelayedScale(1.0), DelayedScale(2.0))  # input activations, output gradient
 
     def forward(self, x):
         if (_enabled() and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
                 and self.weight.dtype == torch.bfloat16 and torch.is_grad_enabled()
                 and x.is_contiguous(memory_format=torch.channels_last)):
-            return _Conv1x1Fn.apply(x, self.weight, self.fp8)
+            return _Conv1x1Fn.apply(x, self.weight, self._f8 if self.fp8 else None)
         return F.conv2d(x, self.weight)
 
 
@@ -225,7 +260,8 @@ def _igemm(x: torch.Tensor, w2: torch.Tensor, k: int, stride: int, pad: int):
     return _from_2d(out, n, ho, wo)
 
 
-def _igemm_fp8(x: torch.Tensor, w2: torch.Tensor, k: int, stride: int, pad: int, e5m2: bool = False):
+def _igemm_fp8(x: torch.Tensor, w2: torch.Tensor, k: int, stride: int, pad: int, e5m2: bool = False,
+               scaler: "DelayedScale | None" = None):
     """conv(x, w) with fp8 operands on the implicit-GEMM kernel (per-tensor just-in-time scales; x
     e4m3, or e5m2 when it is an output gradient), bf16 channels_last out, or None when the kernel
     declines the shape."""
@@ -233,7 +269,7 @@ def _igemm_fp8(x: torch.Tensor, w2: torch.Tensor, k: int, stride: int, pad: int,
 
     n, c, h, w = x.shape
     ho, wo = (h + 2 * pad - k) // stride + 1, (w + 2 * pad - k) // stride + 1
-    xq, sx = _q8(x.permute(0, 2, 3, 1), e5m2=e5m2)  # the NHWC storage, quantised in place order
+    xq, sx = _q8(x.permute(0, 2, 3, 1), e5m2=e5m2, scaler=scaler)  # the NHWC storage, in place order
     wq, sw = _q8(w2)
     out = torch.empty(n * ho * wo, w2.shape[0], device=x.device, dtype=x.dtype)
     if not native().conv_fwd_fp8_(xq.permute(0, 3, 1, 2), wq, sx, sw, out, k, k, stride, pad):
@@ -243,10 +279,12 @@ def _igemm_fp8(x: torch.Tensor, w2: torch.Tensor, k: int, stride: int, pad: int,
 
 class _ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, stride, pad, fp8=False):
+    def forward(ctx, x, weight, stride, pad, f8=None):
+        """``f8``: (activation scaler, gradient scaler) of an fp8 module, else None."""
+        fp8 = f8 is not None
         cout, cin, k, _ = weight.shape
         n, _, h, w = x.shape
-        ctx.stride, ctx.pad, ctx.fp8 = stride, pad, fp8
+        ctx.stride, ctx.pad, ctx.fp8, ctx.f8 = stride, pad, fp8, f8
         ctx.save_for_backward(x, weight)
 
         def miopen():
@@ -254,7 +292,7 @@ class _ConvFn(torch.autograd.Function):
 
         if fp8 and cin % 128 == 0 and _fp8_ok(k * k * cin, cout):
             w2 = weight.permute(0, 2, 3, 1).reshape(cout, k * k * cin)
-            y = _igemm_fp8(x, w2 if w2.is_contiguous() else w2.contiguous(), k, stride, pad)
+            y = _igemm_fp8(x, w2 if w2.is_contiguous() else w2.contiguous(), k, stride, pad, scaler=f8[0])
             if y is not None:
                 return y
 
@@ -291,7 +329,7 @@ class _ConvFn(torch.autograd.Function):
                     and _fp8_ok(k * k * cout, cin):
                 # fp8 bwd-data: e5m2 dY gathered by the implicit GEMM, e4m3 flipped weights
                 wf = weight.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, k * k * cout).contiguous()
-                dx = _igemm_fp8(dy, wf, k, 1, pad, e5m2=True)
+                dx = _igemm_fp8(dy, wf, k, 1, pad, e5m2=True, scaler=ctx.f8[1])
                 if dx is None:
                     dx = miopen()
             elif stride == 1 and _igemm_ok(cout, cin) and 2 * pad == k - 1:
@@ -319,14 +357,15 @@ class ConvNHWC(nn.Conv2d):
 
     def __init__(self, cin: int, cout: int, k: int, stride: int = 1, fp8: bool = False):
         super().__init__(cin, cout, k, stride=stride, padding=k // 2, bias=False)
-        self.fp8 = fp8  # fp8 forward (e4m3 implicit GEMM) / bf16 backward where the shape allows
+        self.fp8 = fp8  # fp8 forward (e4m3 implicit GEMM) and stride-1 bwd-data (e5m2 dY) where allowed
+        self._f8 = (DelayedScale(1.0), DelayedScale(2.0))  # input activations, output gradient
 
     def forward(self, x):
         if (_enabled() and _at.enabled("PSD_CONV_IGEMM") and x.is_cuda and x.dtype == torch.bfloat16
                 and x.dim() == 4 and self.weight.dtype == torch.bfloat16 and self.groups == 1
                 and self.dilation == (1, 1) and x.is_contiguous(memory_format=torch.channels_last)
                 and self.weight.is_contiguous(memory_format=torch.channels_last)):
-            return _ConvFn.apply(x, self.weight, self.stride[0], self.padding[0], self.fp8)
+            return _ConvFn.apply(x, self.weight, self.stride[0], self.padding[0], self._f8 if self.fp8 else None)
         return F.conv2d(x, self.weight, stride=self.stride, padding=self.padding)
 
 

@@ -103,16 +103,54 @@ def test_pack_cast_many_tensors(devname, sd, dd):
 
 @pytest.mark.parametrize("devname", DEVICES)
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_fp8_roundtrip(devname, dtype):
+@pytest.mark.parametrize("n,e5m2", [(4099, False), (3_000_017, False), (4099, True), (2_500_003, True)])
+def test_fp8_roundtrip(devname, dtype, n, e5m2):
+    """Per-tensor quantisation (on the GPU: amax partials + quantise) bit-equal to torch's cast of
+    the scaled input, e4m3fn and e5m2, with odd tails and several amax blocks."""
     dev = _dev(devname)
-    x = (torch.randn(4099) * 3).to(dtype).to(dev)
-    q, sinv = quantize_fp8(x)
+    x = (torch.randn(n, generator=torch.Generator().manual_seed(n)) * 3).to(dtype)
+    x[n // 3] = -17.5  # the amax sits in one block, negative
+    x = x.to(dev)
+    q, sinv = quantize_fp8(x, e5m2=e5m2)
+    fmax, fdt = (57344.0, torch.float8_e5m2) if e5m2 else (448.0, torch.float8_e4m3fn)
     amax = x.float().abs().max()
-    assert abs(sinv.item() - amax.item() / 448.0) < 1e-6 * max(1.0, amax.item())
-    # reference: torch's e4m3fn cast of the scaled input
-    ref_q = (x.float().cpu() * (448.0 / amax.cpu())).clamp(-448, 448).to(torch.float8_e4m3fn)
+    assert abs(sinv.item() - amax.item() / fmax) < 1e-6 * max(1.0, amax.item() / fmax * 448.0)
+    # reference: torch's fp8 cast of the scaled input
+    ref_q = (x.float().cpu() * (fmax / amax.cpu())).clamp(-fmax, fmax).to(fdt)
+    assert q.dtype == fdt
     assert torch.equal(q.cpu().view(torch.uint8), ref_q.view(torch.uint8))
+    if e5m2:
+        return
     back = dequantize_fp8(q, sinv, torch.float32)
     torch.testing.assert_close(back.cpu(), ref_q.float() * sinv.cpu(), rtol=1e-6, atol=1e-6)
     rel = ((back.cpu() - x.float().cpu()).abs() / (x.float().cpu().abs() + 1e-3)).median()
     assert rel < 0.05
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("e5m2", [False, True])
+def test_fp8_delayed_scaling(e5m2):
+    """DelayedScale: the first call scales just-in-time; later calls quantise with the amax the
+    previous call recorded (in the same pass), so quantising the same tensor again is bit-equal to
+    the just-in-time result, and a tensor with a larger amax saturates instead of rescaling."""
+    from parameter_server_distributed_amd.ops.conv import DelayedScale
+
+    dev = _dev("cuda")
+    x = (torch.randn(1_000_003, generator=torch.Generator().manual_seed(3)) * 2).to(torch.bfloat16).to(dev)
+    ds = DelayedScale(1.0)
+    q0, s0 = ds.quantize(x, e5m2)
+    qj, sj = quantize_fp8(x, e5m2=e5m2)
+    assert torch.equal(q0.view(torch.uint8), qj.view(torch.uint8)) and torch.equal(s0, sj)
+    q1, s1 = ds.quantize(x, e5m2)  # delayed: previous amax == this amax
+    torch.cuda.synchronize()
+    assert torch.equal(q1.view(torch.uint8), qj.view(torch.uint8))
+    torch.testing.assert_close(s1, sj, rtol=1e-6, atol=0)
+    amax = float(x.float().abs().max())
+    assert abs(float(ds.hist[0]) - amax) <= 1e-6 * amax and float(ds.hist[1]) == 0.0
+    y = x * 4  # amax grows 4x: quantised with the old scale (saturating), history follows
+    q2, s2 = ds.quantize(y, e5m2)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(s2, sj, rtol=1e-6, atol=0)
+    fmax = 57344.0 if e5m2 else 448.0
+    assert float(q2.float().abs().max()) == fmax
+    assert abs(float(ds.hist[0]) - 4 * amax) <= 1e-5 * amax
