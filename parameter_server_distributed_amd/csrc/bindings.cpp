@@ -32,7 +32,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("hist"), py::arg("margin") = 1.0);
   m.def("bn_fwd", &bn_fwd, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("running_mean"),
         py::arg("running_var"), py::arg("residual"), py::arg("relu"), py::arg("training"), py::arg("momentum"),
-        py::arg("eps"), py::arg("counter"), py::arg("ss_eval"), py::arg("mask_out") = false);
+        py::arg("eps"), py::arg("counter"), py::arg("ss_eval"), py::arg("mask_out") = false,
+        py::arg("residual_ss") = py::none(), py::arg("stats_only") = false);
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("gamma"), py::arg("save_mean"),
         py::arg("save_invstd"), py::arg("relu"), py::arg("need_dr"), py::arg("dgamma_out"), py::arg("dbeta_out"),
         py::arg("dy2") = py::none(), py::arg("ss") = py::none(), py::arg("mbits") = py::none());

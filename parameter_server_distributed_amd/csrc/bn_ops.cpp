@@ -37,7 +37,8 @@ void check_vec(const c10::optional<at::Tensor>& t, int64_t C, at::ScalarType st,
 std::vector<at::Tensor> bn_fwd(const at::Tensor& x_in, c10::optional<at::Tensor> gamma, c10::optional<at::Tensor> beta,
                                c10::optional<at::Tensor> running_mean, c10::optional<at::Tensor> running_var,
                                c10::optional<at::Tensor> residual, bool relu, bool training, double momentum, double eps,
-                               c10::optional<at::Tensor> counter, c10::optional<at::Tensor> ss_eval, bool mask_out) {
+                               c10::optional<at::Tensor> counter, c10::optional<at::Tensor> ss_eval, bool mask_out,
+                               c10::optional<at::Tensor> residual_ss, bool stats_only) {
   TORCH_CHECK(x_in.is_cuda() && x_in.scalar_type() == at::kBFloat16, "psd bn: x must be a bf16 device tensor");
   const c10::DeviceGuard g(x_in.device());
   at::Tensor x = nhwc(x_in);
@@ -54,9 +55,15 @@ std::vector<at::Tensor> bn_fwd(const at::Tensor& x_in, c10::optional<at::Tensor>
     TORCH_CHECK(res.sizes() == x.sizes() && res.scalar_type() == at::kBFloat16, "psd bn: residual shape/dtype");
   }
   auto f32 = x.options().dtype(at::kFloat);
-  at::Tensor y = at::empty_like(x);
+  TORCH_CHECK(!stats_only || training, "psd bn: stats_only needs training mode");
+  const bool rss = residual_ss.has_value() && residual_ss->defined();
+  if (rss)
+    TORCH_CHECK(res.defined() && relu && residual_ss->numel() == 2 * C && residual_ss->scalar_type() == at::kFloat &&
+                    residual_ss->is_contiguous(),
+                "psd bn: residual_ss [2C] fp32 needs a residual and ReLU");
+  at::Tensor y = stats_only ? at::empty({0}, x.options()) : at::empty_like(x);
   at::Tensor mbits;
-  if (relu && mask_out) mbits = at::empty({M * C / 8}, x.options().dtype(at::kByte));
+  if (relu && mask_out && !stats_only) mbits = at::empty({M * C / 8}, x.options().dtype(at::kByte));
   at::Tensor mean = at::empty({C}, f32), invstd = at::empty({C}, f32);
   at::Tensor ss;
   at::Tensor part;
@@ -87,6 +94,8 @@ std::vector<at::Tensor> bn_fwd(const at::Tensor& x_in, c10::optional<at::Tensor>
   a.training = training;
   a.momentum = (float)momentum;
   a.eps = (float)eps;
+  a.res_ss = rss ? residual_ss->data_ptr<float>() : nullptr;
+  a.stats_only = stats_only;
   hipError_t e = launch_bn_fwd(a, stream_of(x));
   TORCH_CHECK(e == hipSuccess, "psd bn fwd: ", hipGetErrorString(e));
   return {y, mean, invstd, ss, mbits};

@@ -198,17 +198,25 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const float* __res
 
 // MASK_OUT: also write the ReLU mask as one bit per element (one byte per 8-channel vector, so a
 // wave stores 64 consecutive bytes): backward then reads 1/16 of the bytes y would cost.
-template <bool RELU, bool RES, bool MASK_OUT>
+// RSS: the residual is itself a raw BN input (the downsample branch's convolution output) whose
+// scale/shift rss is applied here, so that BN's own apply pass (a full write + read of the
+// residual) never runs.
+template <bool RELU, bool RES, bool MASK_OUT, bool RSS = false>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
                                                        const float* __restrict__ ss, uint16_t* __restrict__ y,
-                                                       uint8_t* __restrict__ mbits, int pack4, int64_t nvec, int C) {
+                                                       uint8_t* __restrict__ mbits, int pack4, int64_t nvec, int C,
+                                                       const float* __restrict__ rss = nullptr) {
   const int tpc = C >> 3;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;  // host guarantees stride % tpc == 0
   int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int cg = (int)(v % tpc);
-  float sc[8], sh[8];
+  float sc[8], sh[8], rsc[8], rsh[8];
   load8_f32(ss + cg * 8, sc);
   load8_f32(ss + C + cg * 8, sh);
+  if (RSS) {
+    load8_f32(rss + cg * 8, rsc);
+    load8_f32(rss + C + cg * 8, rsh);
+  }
   for (; v < nvec; v += stride) {
     float t[8];
     load8_bf16(x + v * 8, t);
@@ -217,7 +225,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float o = fmaf(t[j], sc[j], sh[j]);
-      if (RES) o += rr[j];
+      if (RSS) o += fmaf(rr[j], rsc[j], rsh[j]);
+      else if (RES) o += rr[j];
       if (RELU) o = relu_nan(o);
       t[j] = o;
     }
@@ -624,6 +633,7 @@ hipError_t launch_bn_fwd(const BnFwdArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((a.C + kFinCh - 1) / kFinCh), dim3(256), 0, st, a.part, gx, a.M, a.C,
                        a.running_mean, a.gamma, a.beta, a.running_mean, a.running_var, a.momentum, a.eps, a.save_mean,
                        a.save_invstd, a.ss, a.counter);
+    if (a.stats_only) return hipGetLastError();
   }
   if (a.pool_arg) {  // stem: y is the pooled output, the BN output is never written
     if (!a.relu || a.res || a.mbits || !bn_pool_supported(a.H, a.W, a.C) || (int64_t)a.N * a.H * a.W != a.M)
@@ -638,7 +648,17 @@ hipError_t launch_bn_fwd(const BnFwdArgs& a, hipStream_t st) {
   const int g = elem_grid(nvec, a.C);
 #define PSD_APPLY(R, S, B) \
   hipLaunchKernelGGL((bn_apply_kernel<R, S, B>), dim3(g), dim3(256), 0, st, a.x, a.res, a.ss, a.y, a.mbits, \
-                     (int)(nvec % 4 == 0), nvec, a.C)
+                     (int)(nvec % 4 == 0), nvec, a.C, nullptr)
+  if (a.res_ss) {  // residual = bn(res) applied on the fly (ReLU blocks only)
+    if (!a.res || !a.relu) return hipErrorInvalidValue;
+    if (a.mbits)
+      hipLaunchKernelGGL((bn_apply_kernel<true, true, true, true>), dim3(g), dim3(256), 0, st, a.x, a.res, a.ss, a.y,
+                         a.mbits, (int)(nvec % 4 == 0), nvec, a.C, a.res_ss);
+    else
+      hipLaunchKernelGGL((bn_apply_kernel<true, true, false, true>), dim3(g), dim3(256), 0, st, a.x, a.res, a.ss, a.y,
+                         a.mbits, (int)(nvec % 4 == 0), nvec, a.C, a.res_ss);
+    return hipGetLastError();
+  }
   if (a.relu && a.res && a.mbits) PSD_APPLY(true, true, true);
   else if (a.relu && a.mbits) PSD_APPLY(true, false, true);
   else if (a.relu && a.res) PSD_APPLY(true, true, false);

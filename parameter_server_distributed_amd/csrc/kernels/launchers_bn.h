@@ -20,6 +20,8 @@ struct BnFwdArgs {
   float* part;            // [bn_reduce_blocks * 2C] workspace
   int64_t* counter;       // num_batches_tracked (optional)
   int32_t part_ready;     // > 0: part already holds this many rows of partial sums (producer epilogue)
+  const float* res_ss;    // optional [2C]: res is a raw BN input, added as res*res_ss[c] + res_ss[C+c]
+  int32_t stats_only;     // training: statistics / running stats / scale-shift only, no apply pass
   uint8_t* pool_arg;      // stem fusion: y = maxpool3x3s2(relu(bn(x))) [N, H/2, W/2, C] + argmax (optional)
   int32_t N, H, W;        // x as [N, H, W, C] (pool fusion only)
   int64_t M;

@@ -21,7 +21,7 @@ std::vector<at::Tensor> bn_fwd(const at::Tensor& x, c10::optional<at::Tensor> ga
                                c10::optional<at::Tensor> running_mean, c10::optional<at::Tensor> running_var,
                                c10::optional<at::Tensor> residual, bool relu, bool training, double momentum, double eps,
                                c10::optional<at::Tensor> counter, c10::optional<at::Tensor> ss_eval,
-                               bool mask_out);
+                               bool mask_out, c10::optional<at::Tensor> residual_ss, bool stats_only);
 std::vector<at::Tensor> bn_bwd(const at::Tensor& dy, const at::Tensor& x, c10::optional<at::Tensor> y,
                                c10::optional<at::Tensor> gamma, const at::Tensor& save_mean,
                                const at::Tensor& save_invstd, bool relu, bool need_dr,

@@ -17,7 +17,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from ..ops.bn import FusedBatchNorm2d
+from ..ops.bn import FusedBatchNorm2d, bn_add_bn_relu
 from ..ops.conv import Conv1x1, ConvNHWC, stem_forward
 from ..ops.pool import MaxPool3x3s2, global_avg_pool
 
@@ -74,6 +74,11 @@ class Bottleneck(nn.Module):
         if (self.downsample is not None and prev_bn is not None and self.fuse_residual_grad
                 and torch.is_grad_enabled() and x.requires_grad and prev_bn.training and x.is_cuda):
             xm, xd = _Fork.apply(x, prev_bn)  # downsample-branch gradient -> prev_bn's kernels
+        if self.downsample is not None and self.fuse_residual_grad and len(self.downsample) == 2:
+            # relu(bn3(conv3) + bn_ds(conv_ds)): the downsample BN is applied inside bn3's apply pass
+            r = self.downsample[0](xd)
+            out = self.bn2(self.conv2(self.bn1(self.conv1(xm))))
+            return bn_add_bn_relu(self.bn3, self.conv3(out), self.downsample[1], r)
         idt = x if self.downsample is None else self.downsample(xd)
         out = self.bn1(self.conv1(xm))
         out = self.bn2(self.conv2(out))

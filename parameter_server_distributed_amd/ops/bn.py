@@ -67,6 +67,54 @@ class _FusedBNFn(torch.autograd.Function):
         return dx, (dg if w is not None else None), (db if w is not None else None), res_grad, None, None
 
 
+class _BNAddBNReluFn(torch.autograd.Function):
+    """``relu(bn3(x) + bnd(r))`` -- a bottleneck's tail when the residual is the downsample branch
+    (conv -> BN). The downsample BN only reduces its statistics; its scale/shift is applied to r
+    inside bn3's apply kernel, so the downsample BN output (a full [M, C] write and read) never
+    exists. Backward: bn3's backward (ReLU mask, residual gradient dr), then the downsample BN's
+    backward on dr."""
+
+    @staticmethod
+    def forward(ctx, x, w3, b3, r, wd, bd, bn3, bnd):
+        C = native()
+        mom = lambda m: m.momentum if m.momentum is not None else 0.1  # noqa: E731
+        _, mean_d, invstd_d, ss_d, _ = C.bn_fwd(r, wd, bd, bnd.running_mean, bnd.running_var, None, False, True,
+                                                mom(bnd), bnd.eps, bnd.num_batches_tracked, None, stats_only=True)
+        y, mean, invstd, _, mbits = C.bn_fwd(x, w3, b3, bn3.running_mean, bn3.running_var, r, True, True, mom(bn3),
+                                             bn3.eps, bn3.num_batches_tracked, None, mask_out=True, residual_ss=ss_d)
+        ctx.bn3, ctx.bnd = bn3, bnd
+        ctx.save_for_backward(x, mbits, w3, mean, invstd, r, wd, mean_d, invstd_d)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, mbits, w3, mean, invstd, r, wd, mean_d, invstd_d = ctx.saved_tensors
+        bn3, bnd = ctx.bn3, ctx.bnd
+        C = native()
+
+        def sinks(m):
+            sink = getattr(m, "_psd_grad_sink", None)
+            return (sink(m.weight), sink(m.bias)) if sink is not None else (None, None)
+
+        dg3o, db3o = sinks(bn3)
+        dy2 = bn3._psd_pending_dr.pop() if getattr(bn3, "_psd_pending_dr", None) else None
+        dx, dr, dg3, db3 = C.bn_bwd(dy, x, None, w3, mean, invstd, True, True, dg3o, db3o, dy2, None, mbits)
+        dgdo, dbdo = sinks(bnd)
+        drr, _, dgd, dbd = C.bn_bwd(dr, r, None, wd, mean_d, invstd_d, False, False, dgdo, dbdo, None, None, None)
+        return dx, dg3, db3, drr, dgd, dbd, None, None
+
+
+def bn_add_bn_relu(bn3: "FusedBatchNorm2d", x: torch.Tensor, bnd: "FusedBatchNorm2d", r: torch.Tensor):
+    """``relu(bn3(x) + bnd(r))`` with the downsample BN applied inside bn3's apply pass (training,
+    bf16 NHWC on gfx950); anything else composes the two modules."""
+    if (bn3.training and bnd.training and bn3.relu and not bnd.relu and _kernel_ok(x) and _kernel_ok(r)
+            and x.shape == r.shape and x.dim() == 4 and bn3.running_mean is not None and bnd.running_mean is not None
+            and bn3.weight is not None and bnd.weight is not None and bn3.weight.dtype == torch.bfloat16
+            and bnd.weight.dtype == torch.bfloat16 and torch.is_grad_enabled()):
+        return _BNAddBNReluFn.apply(x, bn3.weight, bn3.bias, r, bnd.weight, bnd.bias, bn3, bnd)
+    return bn3(x, bnd(r))
+
+
 class _BNReluPoolFn(torch.autograd.Function):
     """Stem: maxpool3x3s2(relu(bn(x))) without materialising the BN output (kernels/bn.hip)."""
 

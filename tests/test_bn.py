@@ -338,3 +338,44 @@ def test_stem_wgrad_matches_fp32(gpu, shape):
     torch.nn.functional.conv2d(x.float(), w, stride=2, padding=3).backward(dy.float())
     ref = w.grad
     torch.testing.assert_close(dw.float().cpu(), ref, rtol=2e-2, atol=1e-2 * ref.abs().max().item())
+
+
+@pytest.mark.gpu
+def test_downsample_bn_applied_inside_bn3_matches_unfused(gpu):
+    """Bottleneck with a downsample branch: relu(bn3(conv3) + bn_ds(conv_ds)) with the downsample BN
+    applied inside bn3's apply pass (ops/bn.py bn_add_bn_relu) vs the unfused modules: output,
+    every gradient and both BNs' running statistics."""
+    import copy
+
+    import torch.nn as nn
+
+    from parameter_server_distributed_amd.models.resnet import Bottleneck, _conv
+    from parameter_server_distributed_amd.ops.bn import FusedBatchNorm2d
+
+    torch.manual_seed(0)
+    down = nn.Sequential(_conv(64, 256, 1, 2), FusedBatchNorm2d(256))
+    blk = Bottleneck(64, 64, 2, 64, down).to(gpu).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    for m in blk.modules():
+        if isinstance(m, FusedBatchNorm2d):
+            m.running_mean.data = m.running_mean.data.float()
+            m.running_var.data = m.running_var.data.float()
+            with torch.no_grad():
+                m.weight.uniform_(0.5, 1.5)
+                m.bias.uniform_(-0.2, 0.2)
+    ref = copy.deepcopy(blk)
+    ref.fuse_residual_grad = False
+    x0 = torch.randn(8, 64, 28, 28, device=gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    outs = []
+    for m in (blk, ref):
+        x = x0.clone().requires_grad_(True)
+        y = m(x)
+        y.float().pow(2).mean().backward()
+        outs.append((y.float(), x.grad.float(), {n: p.grad.float() for n, p in m.named_parameters()},
+                     {n: b.float() for n, b in m.named_buffers() if b.is_floating_point()}))
+    (y, gx, gp, bufs), (yr, gxr, gpr, bufsr) = outs
+    torch.testing.assert_close(y, yr, rtol=2e-2, atol=2e-2 * float(yr.abs().max()))
+    torch.testing.assert_close(gx, gxr, rtol=2e-2, atol=2e-2 * float(gxr.abs().max()))
+    for n in gpr:
+        torch.testing.assert_close(gp[n], gpr[n], rtol=3e-2, atol=3e-2 * float(gpr[n].abs().max()) + 1e-6, msg=n)
+    for n in bufsr:
+        torch.testing.assert_close(bufs[n], bufsr[n], rtol=1e-3, atol=1e-3, msg=n)
