@@ -121,11 +121,20 @@ class DelayedScale:
         return q, sinv
 
 
+def _sink_view(mod, weight):
+    """The PS data plane's gradient view for ``weight`` (written instead of returning a fresh dW that
+    autograd would then add into the flat gradient buffer), or None."""
+    sink = getattr(mod, "_psd_grad_sink", None) if mod is not None else None
+    return sink(weight) if sink is not None else None
+
+
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, f8=None):
-        """``f8``: (activation scaler, gradient scaler) of an fp8 module, else None."""
+    def forward(ctx, x, weight, f8=None, mod=None):
+        """``f8``: (activation scaler, gradient scaler) of an fp8 module, else None. ``mod``: the
+        module, whose ``_psd_grad_sink`` (installed by the PS data plane) receives dW directly."""
         fp8 = f8 is not None
+        ctx.mod = mod
         n, cin, h, w = x.shape
         cout = weight.shape[0]
         w2 = weight.reshape(cout, cin)
@@ -210,10 +219,17 @@ class _Conv1x1Fn(torch.autograd.Function):
             if _psd_ok(cout, cin) and cout % 8 == 0:
                 cands["psd"] = psd_w
             how = _choose(("wgrad", n * h * w, cin, cout), cands)
-            dw = cands[how]()
-            if how == "psd" and weight.is_contiguous(memory_format=torch.channels_last):
-                dw = dw.contiguous(memory_format=torch.channels_last)
-        return dx, dw, None
+            sv = _sink_view(ctx.mod, weight)
+            if sv is not None and how == "psd":  # split-K result reduced straight into the PS buffer
+                _native().gemm_splitk_(_as_2d(dy), _as_2d(x), False, False, sv.view(cout, cin))
+                dw = sv
+            else:
+                dw = cands[how]()
+                if sv is not None:
+                    dw = sv.copy_(dw)
+                elif how == "psd" and weight.is_contiguous(memory_format=torch.channels_last):
+                    dw = dw.contiguous(memory_format=torch.channels_last)
+        return dx, dw, None, None
 
 
 class Conv1x1(nn.Conv2d):
@@ -225,11 +241,14 @@ class Conv1x1(nn.Conv2d):
         self.fp8 = fp8  # fp8 forward (e4m3) and bwd-data (e5m2 dY) where the shape allows
         self._f8 = (DelayedScale(1.0), DelayedScale(2.0))  # input activations, output gradient
 
+    def psd_direct_grad_params(self):
+        return [self.weight]
+
     def forward(self, x):
         if (_enabled() and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
                 and self.weight.dtype == torch.bfloat16 and torch.is_grad_enabled()
                 and x.is_contiguous(memory_format=torch.channels_last)):
-            return _Conv1x1Fn.apply(x, self.weight, self._f8 if self.fp8 else None)
+            return _Conv1x1Fn.apply(x, self.weight, self._f8 if self.fp8 else None, self)
         return F.conv2d(x, self.weight)
 
 
@@ -279,9 +298,11 @@ def _igemm_fp8(x: torch.Tensor, w2: torch.Tensor, k: int, stride: int, pad: int,
 
 class _ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, stride, pad, f8=None):
-        """``f8``: (activation scaler, gradient scaler) of an fp8 module, else None."""
+    def forward(ctx, x, weight, stride, pad, f8=None, mod=None):
+        """``f8``: (activation scaler, gradient scaler) of an fp8 module, else None; ``mod`` as for
+        _Conv1x1Fn (dW straight into the PS gradient buffer)."""
         fp8 = f8 is not None
+        ctx.mod = mod
         cout, cin, k, _ = weight.shape
         n, _, h, w = x.shape
         ctx.stride, ctx.pad, ctx.fp8, ctx.f8 = stride, pad, fp8, f8
@@ -347,7 +368,10 @@ class _ConvFn(torch.autograd.Function):
                 dx = miopen()
         if ctx.needs_input_grad[1]:
             dw = conv_bwd(dy, x, weight, *args, [False, True, False])[1]
-        return dx, dw, None, None, None
+            sv = _sink_view(ctx.mod, weight)
+            if sv is not None:
+                dw = sv.copy_(dw)
+        return dx, dw, None, None, None, None
 
 
 class ConvNHWC(nn.Conv2d):
@@ -360,12 +384,16 @@ class ConvNHWC(nn.Conv2d):
         self.fp8 = fp8  # fp8 forward (e4m3 implicit GEMM) and stride-1 bwd-data (e5m2 dY) where allowed
         self._f8 = (DelayedScale(1.0), DelayedScale(2.0))  # input activations, output gradient
 
+    def psd_direct_grad_params(self):
+        return [self.weight]
+
     def forward(self, x):
         if (_enabled() and _at.enabled("PSD_CONV_IGEMM") and x.is_cuda and x.dtype == torch.bfloat16
                 and x.dim() == 4 and self.weight.dtype == torch.bfloat16 and self.groups == 1
                 and self.dilation == (1, 1) and x.is_contiguous(memory_format=torch.channels_last)
                 and self.weight.is_contiguous(memory_format=torch.channels_last)):
-            return _ConvFn.apply(x, self.weight, self.stride[0], self.padding[0], self._f8 if self.fp8 else None)
+            return _ConvFn.apply(x, self.weight, self.stride[0], self.padding[0], self._f8 if self.fp8 else None,
+                                 self)
         return F.conv2d(x, self.weight, stride=self.stride, padding=self.padding)
 
 
