@@ -34,6 +34,10 @@ PYBIND11_MODULE(_C, m) {
         py::arg("running_var"), py::arg("residual"), py::arg("relu"), py::arg("training"), py::arg("momentum"),
         py::arg("eps"), py::arg("counter"), py::arg("ss_eval"), py::arg("mask_out") = false,
         py::arg("residual_ss") = py::none(), py::arg("stats_only") = false);
+  m.def("bn_bwd_dual", &bn_bwd_dual, py::arg("dy"), py::arg("x"), py::arg("gamma"), py::arg("save_mean"),
+        py::arg("save_invstd"), py::arg("mbits"), py::arg("dy2"), py::arg("xd"), py::arg("gamma_d"), py::arg("mean_d"),
+        py::arg("invstd_d"), py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none(),
+        py::arg("dgamma_d_out") = py::none(), py::arg("dbeta_d_out") = py::none());
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("gamma"), py::arg("save_mean"),
         py::arg("save_invstd"), py::arg("relu"), py::arg("need_dr"), py::arg("dgamma_out"), py::arg("dbeta_out"),
         py::arg("dy2") = py::none(), py::arg("ss") = py::none(), py::arg("mbits") = py::none());

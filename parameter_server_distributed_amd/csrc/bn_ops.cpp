@@ -174,6 +174,74 @@ std::vector<at::Tensor> bn_bwd(const at::Tensor& dy_in, const at::Tensor& x_in, 
 }
 
 
+// relu(bn3(x) + bnd(xd)) backward (ops/bn.py _BNAddBNReluFn): bn3 through its forward bit-mask, and
+// the downsample BN fed by the residual gradient dr, in one reduce and one elementwise pass.
+// Returns {dx, dxd, dgamma, dbeta, dgamma_d, dbeta_d}.
+std::vector<at::Tensor> bn_bwd_dual(const at::Tensor& dy_in, const at::Tensor& x_in, const at::Tensor& gamma,
+                                    const at::Tensor& save_mean, const at::Tensor& save_invstd, const at::Tensor& mbits,
+                                    c10::optional<at::Tensor> dy2_in, const at::Tensor& xd_in, const at::Tensor& gamma_d,
+                                    const at::Tensor& mean_d, const at::Tensor& invstd_d,
+                                    c10::optional<at::Tensor> dgamma_out, c10::optional<at::Tensor> dbeta_out,
+                                    c10::optional<at::Tensor> dgamma_d_out, c10::optional<at::Tensor> dbeta_d_out) {
+  const c10::DeviceGuard g(x_in.device());
+  at::Tensor x = nhwc(x_in), dy = nhwc(dy_in), xd = nhwc(xd_in);
+  const int64_t C = channels(x);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0 && dy.sizes() == x.sizes() && xd.sizes() == x.sizes() &&
+                  dy.scalar_type() == at::kBFloat16 && xd.scalar_type() == at::kBFloat16,
+              "psd bn bwd_dual: dy / xd like x (bf16)");
+  at::Tensor dy2;
+  if (dy2_in.has_value() && dy2_in->defined()) {
+    dy2 = nhwc(*dy2_in);
+    TORCH_CHECK(dy2.sizes() == x.sizes() && dy2.scalar_type() == at::kBFloat16, "psd bn bwd_dual: dy2 shape/dtype");
+  }
+  TORCH_CHECK(mbits.scalar_type() == at::kByte && mbits.is_contiguous() && mbits.numel() == M * C / 8,
+              "psd bn bwd_dual: mbits must be uint8 [M*C/8]");
+  for (const at::Tensor* t : {&save_mean, &save_invstd, &mean_d, &invstd_d})
+    TORCH_CHECK(t->numel() == C && t->scalar_type() == at::kFloat && t->is_contiguous(), "psd bn bwd_dual: stats [C]");
+  auto grad_buf = [&](const c10::optional<at::Tensor>& o) {
+    at::Tensor t = (o.has_value() && o->defined()) ? *o : at::empty({C}, x.options());
+    TORCH_CHECK(t.numel() == C && t.scalar_type() == at::kBFloat16 && t.is_contiguous(), "psd bn bwd_dual: grad buffer");
+    return t;
+  };
+  at::Tensor dgamma = grad_buf(dgamma_out), dbeta = grad_buf(dbeta_out);
+  at::Tensor dgamma_d = grad_buf(dgamma_d_out), dbeta_d = grad_buf(dbeta_d_out);
+  auto f32 = x.options().dtype(at::kFloat);
+  at::Tensor dx = at::empty_like(x), dxd = at::empty_like(x), dr = at::empty_like(x);
+  at::Tensor coef = at::empty({3 * C}, f32), coef_d = at::empty({3 * C}, f32);
+  const int64_t np = (int64_t)bn_reduce_blocks(M, (int)C) * 2 * C;
+  at::Tensor part = at::empty({np}, f32), part_d = at::empty({np}, f32);
+  BnBwdArgs a{};
+  a.dy = reinterpret_cast<const uint16_t*>(dy.data_ptr());
+  a.dy2 = dy2.defined() ? reinterpret_cast<const uint16_t*>(dy2.data_ptr()) : nullptr;
+  a.mbits = mbits.data_ptr<uint8_t>();
+  a.x = reinterpret_cast<const uint16_t*>(x.data_ptr());
+  a.gamma = reinterpret_cast<const uint16_t*>(gamma.data_ptr());
+  a.save_mean = save_mean.data_ptr<float>();
+  a.save_invstd = save_invstd.data_ptr<float>();
+  a.dx = reinterpret_cast<uint16_t*>(dx.data_ptr());
+  a.dr = reinterpret_cast<uint16_t*>(dr.data_ptr());
+  a.dgamma = reinterpret_cast<uint16_t*>(dgamma.data_ptr());
+  a.dbeta = reinterpret_cast<uint16_t*>(dbeta.data_ptr());
+  a.coef = coef.data_ptr<float>();
+  a.part = part.data_ptr<float>();
+  a.M = M;
+  a.C = (int32_t)C;
+  a.relu = 1;
+  a.xd = reinterpret_cast<const uint16_t*>(xd.data_ptr());
+  a.gamma_d = reinterpret_cast<const uint16_t*>(gamma_d.data_ptr());
+  a.mean_d = mean_d.data_ptr<float>();
+  a.invstd_d = invstd_d.data_ptr<float>();
+  a.dxd = reinterpret_cast<uint16_t*>(dxd.data_ptr());
+  a.dgamma_d = reinterpret_cast<uint16_t*>(dgamma_d.data_ptr());
+  a.dbeta_d = reinterpret_cast<uint16_t*>(dbeta_d.data_ptr());
+  a.coef_d = coef_d.data_ptr<float>();
+  a.part_d = part_d.data_ptr<float>();
+  hipError_t e = launch_bn_bwd(a, stream_of(x));
+  TORCH_CHECK(e == hipSuccess, "psd bn bwd_dual: ", hipGetErrorString(e));
+  return {dx, dxd, dgamma, dbeta, dgamma_d, dbeta_d};
+}
+
 // Stem BN + ReLU + 3x3/s2 max-pool (training forward): returns {y_pool, argmax, mean, invstd, ss}.
 std::vector<at::Tensor> bn_pool_fwd(const at::Tensor& x_in, const at::Tensor& gamma, const at::Tensor& beta,
                                     const at::Tensor& running_mean, const at::Tensor& running_var, double momentum,

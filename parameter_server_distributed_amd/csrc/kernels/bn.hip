@@ -258,25 +258,32 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
 // kMaskBits: the 1-bit-per-element mask the forward apply wrote (residual BNs: 1/16 of y's bytes).
 enum MaskSrc : int { kMaskNone = 0, kMaskY = 1, kMaskX = 2, kMaskBits = 3 };
 
-template <int MASK, bool RES_OUT>
+// DUAL: also the reduction of a second BN that shares dy' (the downsample BN whose output was the
+// residual: its upstream gradient is exactly dr): sum dy'(xd - mean_d) into part_d (sum dy' is common).
+template <int MASK, bool RES_OUT, bool DUAL = false>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ dy2,
                                                             const uint16_t* __restrict__ y, const uint8_t* __restrict__ mbits,
                                                             const float* __restrict__ ssf,
                                                             const uint16_t* __restrict__ x, const float* __restrict__ mean,
                                                             uint16_t* __restrict__ dr, int64_t M, int C,
-                                                            float* __restrict__ part, int rev) {
+                                                            float* __restrict__ part, int rev,
+                                                            const uint16_t* __restrict__ xd = nullptr,
+                                                            const float* __restrict__ mean_d = nullptr,
+                                                            float* __restrict__ part_d = nullptr) {
   const Map m = make_map(C);
-  float a[8], b[8], mu[8], sc[8], sh[8];
+  float a[8], b[8], bd[8], mu[8], mud[8], sc[8], sh[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) a[j] = b[j] = 0.f;
+  for (int j = 0; j < 8; ++j) a[j] = b[j] = bd[j] = 0.f;
   if (m.active) {
     load8_f32(mean + m.cg * 8, mu);
+    if (DUAL) load8_f32(mean_d + m.cg * 8, mud);
     if (MASK == kMaskX) {
       load8_f32(ssf + m.cg * 8, sc);
       load8_f32(ssf + C + m.cg * 8, sh);
     }
     const int64_t stride = (int64_t)gridDim.x * m.rpi;
-    auto body = [&](int64_t off, const float* g0, const float* xv, const float* yv, uint32_t bits) {
+    auto body = [&](int64_t off, const float* g0, const float* xv, const float* yv, uint32_t bits,
+                    const float* xdv) {
       float g[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -290,6 +297,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
       for (int j = 0; j < 8; ++j) {
         a[j] += g[j];
         b[j] = fmaf(g[j], xv[j] - mu[j], b[j]);
+        if (DUAL) bd[j] = fmaf(g[j], xdv[j] - mud[j], bd[j]);
       }
     };
     int64_t r = (int64_t)blockIdx.x * m.rpi + m.r0;
@@ -319,8 +327,13 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
         b0 = mbits[o0 >> 3];
         b1 = mbits[o1 >> 3];
       }
-      body(o0, g0, x0, y0, b0);
-      body(o1, g1, x1, y1, b1);
+      float d0[8], d1[8];
+      if (DUAL) {
+        load8_bf16(xd + o0, d0);
+        load8_bf16(xd + o1, d1);
+      }
+      body(o0, g0, x0, y0, b0, d0);
+      body(o1, g1, x1, y1, b1, d1);
     }
     for (; r < M; r += stride) {
       const int64_t o0 = row_of(r, M, rev) * C + m.cg * 8;
@@ -335,10 +348,16 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
       }
       if (MASK == kMaskY) load8_bf16(y + o0, y0);
       const uint32_t b0 = MASK == kMaskBits ? (uint32_t)mbits[o0 >> 3] : 0u;
-      body(o0, g0, x0, y0, b0);
+      float d0[8];
+      if (DUAL) load8_bf16(xd + o0, d0);
+      body(o0, g0, x0, y0, b0, d0);
     }
   }
   block_partials(m, C, a, b, part);
+  if (DUAL) {
+    __syncthreads();  // block_partials' LDS staging is reused
+    block_partials(m, C, a, bd, part_d);
+  }
 }
 
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, int64_t M, int C,
@@ -404,6 +423,37 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(const uint16_t* __res
 #pragma unroll
     for (int j = 0; j < 8; ++j) gv[j] = fmaf(A[j], gv[j], fmaf(B[j], xv[j], Cc[j]));
     store8_bf16(dx + v * 8, gv);
+  }
+}
+
+// dual elementwise pass: dx = A g + B x + C and dxd = Ad g + Bd xd + Cd from one read of g (= dr)
+__global__ __launch_bounds__(256) void bn_bwd_elemt_dual_kernel(const uint16_t* __restrict__ g, const uint16_t* __restrict__ x,
+                                                                const float* __restrict__ coef, uint16_t* __restrict__ dx,
+                                                                const uint16_t* __restrict__ xd,
+                                                                const float* __restrict__ coef_d,
+                                                                uint16_t* __restrict__ dxd, int64_t nvec, int C) {
+  const int tpc = C >> 3;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int cg = (int)(v % tpc);
+  float A[8], B[8], Cc[8], Ad[8], Bd[8], Cd[8];
+  load8_f32(coef + cg * 8, A);
+  load8_f32(coef + C + cg * 8, B);
+  load8_f32(coef + 2 * C + cg * 8, Cc);
+  load8_f32(coef_d + cg * 8, Ad);
+  load8_f32(coef_d + C + cg * 8, Bd);
+  load8_f32(coef_d + 2 * C + cg * 8, Cd);
+  for (; v < nvec; v += stride) {
+    float gv[8], xv[8], dv[8], o[8];
+    load8_bf16(g + v * 8, gv);
+    load8_bf16(x + v * 8, xv);
+    load8_bf16(xd + v * 8, dv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = fmaf(A[j], gv[j], fmaf(B[j], xv[j], Cc[j]));
+    store8_bf16(dx + v * 8, o);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = fmaf(Ad[j], gv[j], fmaf(Bd[j], dv[j], Cd[j]));
+    store8_bf16(dxd + v * 8, o);
   }
 }
 
@@ -708,6 +758,21 @@ hipError_t launch_bn_bwd(const BnBwdArgs& a, hipStream_t st) {
   const int mask = !a.relu ? kMaskNone : (a.mbits ? kMaskBits : (a.y ? kMaskY : kMaskX));
   if (mask == kMaskX && !a.ss) return hipErrorInvalidValue;
   if (mask == kMaskBits && !a.dr) return hipErrorInvalidValue;  // bits are kept for residual BNs only
+  if (a.xd) {  // dual: this BN (bit-mask, dr out) + the downsample BN fed by dr
+    if (mask != kMaskBits || !a.dxd || !a.coef_d || !a.part_d || !a.mean_d || !a.invstd_d)
+      return hipErrorInvalidValue;
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<kMaskBits, true, true>), dim3(gx, gy), dim3(256), 0, st, a.dy, a.dy2, a.y,
+                       a.mbits, a.ss, a.x, a.save_mean, a.dr, a.M, a.C, a.part, bn_reverse(), a.xd, a.mean_d, a.part_d);
+    const dim3 fg((a.C + kFinCh - 1) / kFinCh);
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, fg, dim3(256), 0, st, a.part, gx, a.M, a.C, a.gamma, a.save_mean,
+                       a.save_invstd, a.dgamma, a.dbeta, a.coef);
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, fg, dim3(256), 0, st, a.part_d, gx, a.M, a.C, a.gamma_d, a.mean_d,
+                       a.invstd_d, a.dgamma_d, a.dbeta_d, a.coef_d);
+    const int64_t nvec = a.M * (a.C / 8);
+    hipLaunchKernelGGL(bn_bwd_elemt_dual_kernel, dim3(elem_grid(nvec, a.C)), dim3(256), 0, st, a.dr, a.x, a.coef, a.dx,
+                       a.xd, a.coef_d, a.dxd, nvec, a.C);
+    return hipGetLastError();
+  }
 #define PSD_RED(K, O)                                                                                              \
   hipLaunchKernelGGL((bn_bwd_reduce_kernel<K, O>), dim3(gx, gy), dim3(256), 0, st, a.dy, a.dy2, a.y, a.mbits, a.ss, \
                      a.x, a.save_mean, a.dr, a.M, a.C, a.part, \

@@ -57,6 +57,18 @@ struct BnBwdArgs {
   int64_t M;
   int32_t C;
   int32_t relu;
+  // dual (downsample blocks, ops/bn.py _BNAddBNReluFn): a second BN whose output was the residual,
+  // input xd; its reduction rides on this one's reduce pass (same dr) and its dx on the same elemt
+  // pass. Needs the bit-mask path with dr.
+  const uint16_t* xd;
+  const uint16_t* gamma_d;
+  const float* mean_d;
+  const float* invstd_d;
+  uint16_t* dxd;
+  uint16_t* dgamma_d;
+  uint16_t* dbeta_d;
+  float* coef_d;  // [3C]
+  float* part_d;  // like part
 };
 
 // true when the fused stem BN+ReLU+max-pool kernels support this shape

@@ -22,6 +22,12 @@ std::vector<at::Tensor> bn_fwd(const at::Tensor& x, c10::optional<at::Tensor> ga
                                c10::optional<at::Tensor> residual, bool relu, bool training, double momentum, double eps,
                                c10::optional<at::Tensor> counter, c10::optional<at::Tensor> ss_eval,
                                bool mask_out, c10::optional<at::Tensor> residual_ss, bool stats_only);
+std::vector<at::Tensor> bn_bwd_dual(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& gamma,
+                                    const at::Tensor& save_mean, const at::Tensor& save_invstd, const at::Tensor& mbits,
+                                    c10::optional<at::Tensor> dy2, const at::Tensor& xd, const at::Tensor& gamma_d,
+                                    const at::Tensor& mean_d, const at::Tensor& invstd_d,
+                                    c10::optional<at::Tensor> dgamma_out, c10::optional<at::Tensor> dbeta_out,
+                                    c10::optional<at::Tensor> dgamma_d_out, c10::optional<at::Tensor> dbeta_d_out);
 std::vector<at::Tensor> bn_bwd(const at::Tensor& dy, const at::Tensor& x, c10::optional<at::Tensor> y,
                                c10::optional<at::Tensor> gamma, const at::Tensor& save_mean,
                                const at::Tensor& save_invstd, bool relu, bool need_dr,

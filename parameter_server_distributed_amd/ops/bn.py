@@ -71,8 +71,8 @@ class _BNAddBNReluFn(torch.autograd.Function):
     """``relu(bn3(x) + bnd(r))`` -- a bottleneck's tail when the residual is the downsample branch
     (conv -> BN). The downsample BN only reduces its statistics; its scale/shift is applied to r
     inside bn3's apply kernel, so the downsample BN output (a full [M, C] write and read) never
-    exists. Backward: bn3's backward (ReLU mask, residual gradient dr), then the downsample BN's
-    backward on dr."""
+    exists. Backward: both BNs in one reduce pass and one elementwise pass (the downsample BN's
+    upstream gradient is bn3's residual gradient dr)."""
 
     @staticmethod
     def forward(ctx, x, w3, b3, r, wd, bd, bn3, bnd):
@@ -97,10 +97,12 @@ class _BNAddBNReluFn(torch.autograd.Function):
             return (sink(m.weight), sink(m.bias)) if sink is not None else (None, None)
 
         dg3o, db3o = sinks(bn3)
-        dy2 = bn3._psd_pending_dr.pop() if getattr(bn3, "_psd_pending_dr", None) else None
-        dx, dr, dg3, db3 = C.bn_bwd(dy, x, None, w3, mean, invstd, True, True, dg3o, db3o, dy2, None, mbits)
         dgdo, dbdo = sinks(bnd)
-        drr, _, dgd, dbd = C.bn_bwd(dr, r, None, wd, mean_d, invstd_d, False, False, dgdo, dbdo, None, None, None)
+        dy2 = bn3._psd_pending_dr.pop() if getattr(bn3, "_psd_pending_dr", None) else None
+        # one reduce pass for both BNs (the downsample BN's upstream gradient is bn3's dr) and one
+        # elementwise pass writing both input gradients (kernels/bn.hip, dual mode)
+        dx, drr, dg3, db3, dgd, dbd = C.bn_bwd_dual(dy, x, w3, mean, invstd, mbits, dy2, r, wd, mean_d, invstd_d,
+                                                    dg3o, db3o, dgdo, dbdo)
         return dx, dg3, db3, drr, dgd, dbd, None, None
 
 
