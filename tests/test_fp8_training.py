@@ -1,0 +1,64 @@
+"""fp8 compute (e4m3 forward / e5m2-dY bwd-data convolutions with delayed scaling, BASELINE config 5)
+against the same model trained in bf16: over several SGD steps from the same initial weights on the
+same batches, the loss trajectories and the final weights stay within fp8 error of each other, and
+the fp8 kernels really ran (their delayed-scaling histories were seeded)."""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _train(model, batches, steps, lr=0.05):
+    opt = torch.optim.SGD([p for p in model.parameters() if p.requires_grad], lr=lr, momentum=0.9)
+    losses = []
+    for t in range(steps):
+        x, y = batches[t % len(batches)]
+        loss = F.cross_entropy(model(x).float(), y)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+        losses.append(float(loss))
+    return losses
+
+
+def test_fp8_wide_resnet_tracks_bf16(gpu):
+    from parameter_server_distributed_amd.models import prepare
+    from parameter_server_distributed_amd.models.resnet import ResNet
+    from parameter_server_distributed_amd.ops.conv import Conv1x1, ConvNHWC
+
+    torch.manual_seed(0)
+    # a short Wide-ResNet (width_per_group 128, one block per stage): stages 2-4 have fp8 shapes
+    base = ResNet((1, 1, 1, 1), num_classes=100, width_per_group=128, zero_init_residual=False)
+    m8 = copy.deepcopy(base)
+    for mod in m8.modules():
+        if isinstance(mod, (Conv1x1, ConvNHWC)):
+            mod.fp8 = True
+    mb = prepare(base, gpu, torch.bfloat16, channels_last=True)
+    m8 = prepare(m8, gpu, torch.bfloat16, channels_last=True)
+    for m in (mb, m8):  # bf16 weights (the PS data plane's working copy)
+        for p in m.parameters():
+            p.data = p.data.to(torch.bfloat16)
+        m.train()
+    g = torch.Generator().manual_seed(1)
+    batches = [(torch.randn(16, 3, 64, 64, generator=g).to(gpu, torch.bfloat16).contiguous(memory_format=torch.channels_last),
+                torch.randint(0, 100, (16,), generator=g).to(gpu)) for _ in range(2)]
+    steps = 6
+    init = [p.detach().float().clone() for p in mb.parameters()]
+    lb = _train(mb, batches, steps)
+    l8 = _train(m8, batches, steps)
+    used = [mod for mod in m8.modules() if isinstance(mod, (Conv1x1, ConvNHWC)) and mod._f8[0].hist is not None]
+    assert len(used) >= 6, "fp8 forward kernels did not run"
+    assert any(mod._f8[1].hist is not None for mod in used), "fp8 bwd-data kernels did not run"
+    for a, b in zip(lb, l8):
+        assert abs(a - b) <= 0.05 * abs(a) + 0.05, (lb, l8)
+    assert l8[-1] < l8[0], l8  # it trains
+    # the weight *updates* of the two runs agree to within fp8 error
+    num = den = 0.0
+    for p0, pb, p8 in zip(init, mb.parameters(), m8.parameters()):
+        db, d8 = pb.float() - p0, p8.float() - p0
+        num += float((db - d8).pow(2).sum())
+        den += float(db.pow(2).sum())
+    assert (num / den) ** 0.5 < 0.25, (num / den) ** 0.5
