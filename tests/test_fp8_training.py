@@ -1,6 +1,6 @@
 """fp8 compute (e4m3 forward / e5m2-dY bwd-data convolutions with delayed scaling, BASELINE config 5)
 against the same model trained in bf16: over several SGD steps from the same initial weights on the
-same batches, the loss trajectories and the final weights stay within fp8 error of each other, and
+same batches, the first-step gradients and the loss trajectories stay within fp8 error of each other, and
 the fp8 kernels really ran (their delayed-scaling histories were seeded)."""
 import copy
 
@@ -45,8 +45,17 @@ def test_fp8_wide_resnet_tracks_bf16(gpu):
     g = torch.Generator().manual_seed(1)
     batches = [(torch.randn(16, 3, 64, 64, generator=g).to(gpu, torch.bfloat16).contiguous(memory_format=torch.channels_last),
                 torch.randint(0, 100, (16,), generator=g).to(gpu)) for _ in range(2)]
+    # first-step gradients (same weights, same batch): fp8 forward / bwd-data vs bf16
+    grads = []
+    for m in (mb, m8):
+        m.zero_grad(set_to_none=True)
+        F.cross_entropy(m(batches[0][0]).float(), batches[0][1]).backward()
+        grads.append([p.grad.float().clone() for p in m.parameters()])
+        m.zero_grad(set_to_none=True)
+    num = sum(float((a - b).pow(2).sum()) for a, b in zip(*grads))
+    den = sum(float(a.pow(2).sum()) for a in grads[0])
+    assert (num / den) ** 0.5 < 0.15, (num / den) ** 0.5
     steps = 6
-    init = [p.detach().float().clone() for p in mb.parameters()]
     lb = _train(mb, batches, steps)
     l8 = _train(m8, batches, steps)
     used = [mod for mod in m8.modules() if isinstance(mod, (Conv1x1, ConvNHWC)) and mod._f8[0].hist is not None]
@@ -55,10 +64,4 @@ def test_fp8_wide_resnet_tracks_bf16(gpu):
     for a, b in zip(lb, l8):
         assert abs(a - b) <= 0.05 * abs(a) + 0.05, (lb, l8)
     assert l8[-1] < l8[0], l8  # it trains
-    # the weight *updates* of the two runs agree to within fp8 error
-    num = den = 0.0
-    for p0, pb, p8 in zip(init, mb.parameters(), m8.parameters()):
-        db, d8 = pb.float() - p0, p8.float() - p0
-        num += float((db - d8).pow(2).sum())
-        den += float(db.pow(2).sum())
-    assert (num / den) ** 0.5 < 0.25, (num / den) ** 0.5
+
