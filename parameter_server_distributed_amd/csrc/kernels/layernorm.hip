@@ -132,12 +132,32 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
   for (int i = 0; i < E; ++i) pg[i] = pb[i] = 0.f;
   const uint32_t key = dropout_key(seed, step);
   const int64_t wstride = (int64_t)gridDim.x * (blockDim.x >> 6);
-  for (int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv; r < rows; r += wstride) {
+  // software-pipelined: the next row's dy / s / stats loads are issued before this row's two wave
+  // reductions (one row per wave per iteration otherwise left the loads latency-bound, 2.9 TB/s)
+  int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+  float ndv[E], nsv[E], nmean = 0.f, nrstd = 0.f;
+  if (r < rows) {
+    load_e<E>(dy + r * H + c0, ndv);
+    load_e<E>(s + r * H + c0, nsv);
+    nmean = mean_in[r];
+    nrstd = rstd_in[r];
+  }
+  for (; r < rows; r += wstride) {
     const int64_t off = r * H + c0;
     float dv[E], sv[E];
-    load_e<E>(dy + off, dv);
-    load_e<E>(s + off, sv);
-    const float mean = mean_in[r], rstd = rstd_in[r];
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      dv[i] = ndv[i];
+      sv[i] = nsv[i];
+    }
+    const float mean = nmean, rstd = nrstd;
+    const int64_t rn = r + wstride;
+    if (rn < rows) {
+      load_e<E>(dy + rn * H + c0, ndv);
+      load_e<E>(s + rn * H + c0, nsv);
+      nmean = mean_in[rn];
+      nrstd = rstd_in[rn];
+    }
     float a = 0.f, bsum = 0.f;
 #pragma unroll
     for (int i = 0; i < E; ++i) {
@@ -183,7 +203,13 @@ __global__ __launch_bounds__(256) void ln_param_grad_kernel(const float* __restr
   float s0 = 0.f;
   if (t < 2 * H) {
     const int which = t / H, col = t - which * H;
-    for (int b = rl; b < nblk; b += 8) s0 += part[((int64_t)b * 2 + which) * H + col];
+    float s4[4] = {0.f, 0.f, 0.f, 0.f};  // independent loads: nblk/32 round trips, not nblk/8
+    int b = rl;
+    for (; b + 24 < nblk; b += 32)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s4[u] += part[((int64_t)(b + 8 * u) * 2 + which) * H + col];
+    for (; b < nblk; b += 8) s4[0] += part[((int64_t)b * 2 + which) * H + col];
+    s0 = (s4[0] + s4[1]) + (s4[2] + s4[3]);
   }
   __shared__ float red[8][33];
   red[rl][cl] = s0;
@@ -196,8 +222,8 @@ __global__ __launch_bounds__(256) void ln_param_grad_kernel(const float* __restr
 }
 
 int ln_bwd_blocks(int64_t rows) {
-  const int64_t want = (rows + 4 * 8 - 1) / (4 * 8);  // >= 8 rows per wave
-  return (int)(want < 1 ? 1 : (want > 256 ? 256 : want));
+  const int64_t want = (rows + 4 * 8 - 1) / (4 * 8);  // >= 8 rows per wave, <= 2 blocks per CU
+  return (int)(want < 1 ? 1 : (want > 512 ? 512 : want));
 }
 
 bool ln_supported(int H) { return H == 768 || H == 1024; }
