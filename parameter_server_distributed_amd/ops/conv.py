@@ -178,7 +178,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         dx = dw = None
         conv_bwd = torch.ops.aten.convolution_backward
         args = (None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1)
-        if need_x and ctx.fp8 and _fp8_ok(cout, cin):
+        if need_x and ctx.fp8 and _fp8_ok(cout, cin) and _at.enabled("PSD_FP8_DGRAD"):
             # fp8 bwd-data: e5m2 dY (K-major [M, cout]) x e4m3 W^T ([cin, cout], K-major)
             dyq, sdy = _q8(_as_2d(dy), e5m2=True, scaler=ctx.f8[1])
             wtq, swt = _q8(weight.reshape(cout, cin).t().contiguous())
@@ -347,7 +347,7 @@ class _ConvFn(torch.autograd.Function):
                 return conv_bwd(dy, x, weight, *args, [True, False, False])[0]
 
             if stride == 1 and _igemm_ok(cout, cin) and 2 * pad == k - 1 and ctx.fp8 and cout % 128 == 0 \
-                    and _fp8_ok(k * k * cout, cin):
+                    and _fp8_ok(k * k * cout, cin) and _at.enabled("PSD_FP8_DGRAD"):
                 # fp8 bwd-data: e5m2 dY gathered by the implicit GEMM, e4m3 flipped weights
                 wf = weight.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, k * k * cout).contiguous()
                 dx = _igemm_fp8(dy, wf, k, 1, pad, e5m2=True, scaler=ctx.f8[1])
