@@ -30,7 +30,9 @@ class ModelSpec:
 
 
 def _ce(out, y):
-    return F.cross_entropy(out.float(), y)
+    from ..ops.loss import cross_entropy  # fused bf16 kernels on the GPU, fp32 F.cross_entropy elsewhere
+
+    return cross_entropy(out, y)
 
 
 def _image_batch(size: int, classes: int, dtype, channels_last: bool):

@@ -19,6 +19,7 @@ import torch.nn.functional as F
 from ..ops.attention import FusedSelfAttention
 from ..ops.layernorm import FusedAddLayerNorm, bump_step
 from ..ops.linear import MfmaLinear
+from ..ops.loss import cross_entropy
 
 VOCAB = 30528
 
@@ -83,7 +84,7 @@ class BertForMLM(nn.Module):
 
     @staticmethod
     def loss(logits, labels):
-        return F.cross_entropy(logits.float(), labels)
+        return cross_entropy(logits, labels)  # fused bf16 softmax-CE kernels (ops/loss.py)
 
 
 def bert_batch(batch: int, seq: int, vocab: int, device, seed: int = 0, mask_prob: float = 0.15):

@@ -6,7 +6,7 @@ R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 OUT=$R/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd "$R"
-timeout -k 10 400 python -u -m pytest tests/test_layernorm.py tests/test_attention.py tests/test_gemm.py tests/test_fp8_training.py -m gpu -q --timeout 200 --timeout-method thread > "$OUT/gpu_tests.txt" 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_layernorm.py tests/test_attention.py tests/test_gemm.py tests/test_fp8_training.py tests/test_kernels.py -m gpu -q --timeout 200 --timeout-method thread > "$OUT/gpu_tests.txt" 2>&1
 echo "tests rc=$?" >> "$OUT/gpu_tests.txt"
 tail -3 "$OUT/gpu_tests.txt"
 timeout -k 10 300 python3 bench.py --model bert_base --steps 20 --warmup 5 --out "$OUT/bench_bert.json" > "$OUT/bench_bert.log" 2>&1 || exit $?

@@ -154,3 +154,27 @@ def test_fp8_delayed_scaling(e5m2):
     fmax = 57344.0 if e5m2 else 448.0
     assert float(q2.float().abs().max()) == fmax
     assert abs(float(ds.hist[0]) - 4 * amax) <= 1e-5 * amax
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows,V", [(4864, 30528), (1024, 1000), (37, 264), (8, 30522 + 6)])
+def test_fused_cross_entropy_matches_fp32(rows, V):
+    """Fused bf16 softmax cross-entropy (kernels/xent.hip) vs F.cross_entropy on the same values in
+    fp32: loss, and the gradient (bf16-rounded), including ignored (-100) rows."""
+    from parameter_server_distributed_amd.ops.loss import cross_entropy
+
+    dev = _dev("cuda")
+    g = torch.Generator().manual_seed(rows)
+    x = (torch.randn(rows, V, generator=g) * 3).to(torch.bfloat16).to(dev)
+    y = torch.randint(0, V, (rows,), generator=g)
+    y[::7] = -100
+    y = y.to(dev)
+    xr = x.float().clone().requires_grad_(True)
+    ref = torch.nn.functional.cross_entropy(xr, y)
+    ref.backward()
+    xk = x.clone().requires_grad_(True)
+    loss = cross_entropy(xk, y)
+    loss.backward()
+    torch.testing.assert_close(loss.float(), ref.detach(), rtol=1e-5, atol=1e-5)
+    assert xk.grad.dtype == torch.bfloat16
+    torch.testing.assert_close(xk.grad.float(), xr.grad, rtol=1e-2, atol=1e-2 * float(xr.grad.abs().max()))
