@@ -51,6 +51,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("aux") = py::none());
   m.def("conv_fwd_", &conv_fwd_, py::arg("x"), py::arg("w2"), py::arg("out"), py::arg("R"), py::arg("S"),
         py::arg("stride"), py::arg("pad"));
+  m.def("conv_wgrad_", &conv_wgrad_, py::arg("dy"), py::arg("x"), py::arg("out"), py::arg("R"), py::arg("S"),
+        py::arg("stride"), py::arg("pad"), py::arg("splits") = 0);
   m.def("conv_fwd_fp8_", &conv_fwd_fp8_, py::arg("x"), py::arg("w2"), py::arg("x_scale"), py::arg("w_scale"),
         py::arg("out"), py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"));
   m.def("gelu_bwd_colsum_", &gelu_bwd_colsum_, py::arg("dy"), py::arg("pre"), py::arg("dx"), py::arg("out"),

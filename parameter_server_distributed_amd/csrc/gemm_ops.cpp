@@ -198,6 +198,59 @@ bool conv_fwd_fp8_(const at::Tensor& x, const at::Tensor& w2, const at::Tensor& 
   return conv_fwd_impl(x, w2, out, R, S, stride, pad, &x_scale, &w_scale);
 }
 
+// Implicit-GEMM convolution weight gradient: out [Cout, R*S*C] (an OHWI weight viewed 2-D, bf16) =
+// dY^T . im2col(x), dY [Nb, Cout, Ho, Wo] and x [Nb, C, H, W] channels_last bf16; split-K over the
+// output pixels (splits <= 0: about one round of workgroups). False (nothing launched) outside the
+// kernel's contract.
+bool conv_wgrad_(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64_t R, int64_t S, int64_t stride,
+                 int64_t pad, int64_t splits) {
+  TORCH_CHECK(dy.is_cuda() && x.is_cuda() && dy.dim() == 4 && x.dim() == 4 && dy.scalar_type() == at::kBFloat16 &&
+                  x.scalar_type() == at::kBFloat16 && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "psd conv_wgrad: dy and x must be channels_last bf16 device tensors");
+  const int64_t Nb = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t Cout = dy.size(1), Ho = dy.size(2), Wo = dy.size(3);
+  TORCH_CHECK(dy.size(0) == Nb && Ho == (H + 2 * pad - R) / stride + 1 && Wo == (W + 2 * pad - S) / stride + 1,
+              "psd conv_wgrad: dy shape does not match the convolution");
+  const int64_t N = R * S * C, K = Nb * Ho * Wo;
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == Cout && out.size(1) == N && out.is_contiguous() &&
+                  out.scalar_type() == at::kBFloat16,
+              "psd conv_wgrad: out must be a contiguous bf16 [Cout, R*S*C]");
+  const int64_t xbytes = x.numel() * 2;
+  if ((C & (C - 1)) != 0 || C < 8 || xbytes >= ((int64_t)1 << 32) || K >= ((int64_t)1 << 31) || K % 64 != 0)
+    return false;
+  int logc = 0;
+  while ((1 << logc) < C) ++logc;
+  const c10::DeviceGuard g(x.device());
+  const int64_t tiles = ((Cout + 255) / 256) * ((N + 255) / 256);
+  int64_t s = splits > 0 ? splits : std::max<int64_t>(1, 256 / tiles);
+  s = std::min<int64_t>(s, std::max<int64_t>(1, K / 128));  // >= 2 K-tiles per split
+  at::Tensor slab = at::empty({s * Cout * N}, x.options().dtype(at::kFloat));
+  GemmArgs a{};
+  a.A = dy.data_ptr();
+  a.B = x.data_ptr();
+  a.M = (int)Cout;
+  a.N = (int)N;
+  a.K = (int)K;
+  a.lda = (int)Cout;
+  a.ldb = (int)N;
+  a.ldc = (int)N;
+  a.a_kmajor = a.b_kmajor = 0;
+  a.cv_H = (int)H;
+  a.cv_W = (int)W;
+  a.cv_logC = logc;
+  a.cv_Ho = (int)Ho;
+  a.cv_Wo = (int)Wo;
+  a.cv_S = (int)S;
+  a.cv_stride = (int)stride;
+  a.cv_pad = (int)pad;
+  a.cv_abytes = (uint32_t)xbytes;
+  hipError_t e = launch_conv_wgrad(a, slab.data_ptr<float>(), (int)s, out.data_ptr(), stream_of(x));
+  if (e == hipErrorNotSupported) return false;
+  TORCH_CHECK(e == hipSuccess, "psd conv_wgrad: ", hipGetErrorString(e));
+  return true;
+}
+
 // out[N] (+)= column sums of x[M,N] (bias gradient)
 void colsum_(const at::Tensor& x, at::Tensor out, bool accumulate) {
   chk2d(x, "x");

@@ -759,8 +759,14 @@ __device__ __forceinline__ float act_apply(float x) {
 // output pixels whose (r, s)-shifted input pixel is computed per K-tile (one (r, s) per K-tile:
 // C % 64 == 0); pixels outside the image get an offset past the descriptor, i.e. the zero padding.
 // F8A: the A operand's fp8 format (0 e4m3, 1 e5m2: bwd-data of the fp8 convolutions takes e5m2 dY)
-template <int BM, bool AK, bool BKM, int MODE, bool F8 = false, int ACT = 0, bool GA = false, int F8A = 0>
+// GB: B is gathered as the im2col image of a convolution input for the weight gradient (MODE 1):
+// dW[cout][(r, s, ci)] = sum over output pixels p of dY[p][cout] * x[pixel(p) + (r, s)][ci], A = dY
+// M-major ([pixels][cout]), B = the gathered [pixels][R*S*C] N-major image (each lane's 16 bytes are
+// 8 channels of one shifted input pixel; pixels outside the image load zeros).
+template <int BM, bool AK, bool BKM, int MODE, bool F8 = false, int ACT = 0, bool GA = false, int F8A = 0,
+          bool GB = false>
 __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
+  static_assert(!GB || (!AK && !BKM && MODE == 1 && !F8 && !GA), "implicit-GEMM wgrad: M-major dY, split-K");
   static_assert(!F8 || (AK && BKM), "fp8 GEMM takes K-major operands");
   static_assert(!GA || (AK && MODE == 0), "implicit-GEMM convolution: K-major A, single split");
   static_assert(BM == 256 || AK, "BM = 128 takes a K-major A");
@@ -853,7 +859,32 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
       stage8<AK, ESZ, P::PWA>(g.A, bytesA, voA[h], g.lda, m0, k, half(u, h), wid);
     }
   };
-  auto stB = [&](int u, int n0, int k, int h) { stage8<BKM, ESZ, 2>(g.B, bytesB, voB[h], g.ldb, n0, k, half(u, 2 + h), wid); };
+  auto stB = [&](int u, int n0, int k, int h) {
+    if constexpr (GB) {
+      const rsrc_t src = make_rsrc(g.B, g.cv_abytes);
+      uint8_t* lds = half(u, 2 + h);
+      const int howo = g.cv_Ho * g.cv_Wo;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int kk = (i * 8 + wid) * 4 + (lane >> 4);  // this lane's k-row (pixel) of the K-tile
+        const int f = (kk & 3) | ((kk >> 1) & 4);
+        const int col = ((lane & 15) * 8) ^ (f << 4);
+        const int n = n0 + half_to_tile<32>(col, h);      // (r, s, ci) column of dW
+        const int rs = n >> g.cv_logC, ci = n & ((1 << g.cv_logC) - 1);
+        const int r = rs / g.cv_S, sx = rs - r * g.cv_S;
+        const int pix = k + kk;                           // output pixel
+        const int img = pix / howo, rem = pix - img * howo;
+        const int ho = rem / g.cv_Wo, wo = rem - ho * g.cv_Wo;
+        const int hi = ho * g.cv_stride - g.cv_pad + r, wi = wo * g.cv_stride - g.cv_pad + sx;
+        const bool ok = n < g.N && pix < g.K && (unsigned)hi < (unsigned)g.cv_H && (unsigned)wi < (unsigned)g.cv_W;
+        const uint32_t off = ok ? ((uint32_t)(((img * g.cv_H + hi) * g.cv_W + wi) << g.cv_logC) + ci) * 2 : 0xFFFFFFF0u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(src, (__attribute__((address_space(3))) void*)(lds + (i * 8 + wid) * 1024),
+                                                 16, off, 0, 0, 0);
+      }
+    } else {
+      stage8<BKM, ESZ, 2>(g.B, bytesB, voB[h], g.ldb, n0, k, half(u, 2 + h), wid);
+    }
+  };
   if (nt > 0) {
     const int k1 = kbeg + min(1, nt - 1) * KT;  // nt = 1: a split of one K-tile re-stages it
     stB(0, cn0, kbeg, 0);
@@ -1320,12 +1351,12 @@ static int persistent_grid() {
   return n;
 }
 
-template <int BM, bool AK, bool BKM, int MODE, bool F8, int ACT, bool GA = false, int F8A = 0>
+template <int BM, bool AK, bool BKM, int MODE, bool F8, int ACT, bool GA = false, int F8A = 0, bool GB = false>
 static hipError_t launch_8p_act(const GemmArgs& g, int splits, hipStream_t st) {
   constexpr int lds = P8<BM>::LDS;
   static bool attr_set = false;  // per instantiation: set the >64 KiB LDS limit once
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT, GA, F8A>,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT, GA, F8A, GB>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     attr_set = true;
@@ -1342,7 +1373,7 @@ static hipError_t launch_8p_act(const GemmArgs& g, int splits, hipStream_t st) {
   }();
   GemmArgs ga = g;
   ga.dbg = dbg;
-  hipLaunchKernelGGL((gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT, GA, F8A>), dim3(grid, 1, splits), dim3(512), lds, st, ga);
+  hipLaunchKernelGGL((gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT, GA, F8A, GB>), dim3(grid, 1, splits), dim3(512), lds, st, ga);
   return hipGetLastError();
 }
 
@@ -1481,6 +1512,30 @@ hipError_t launch_gemm_fp8(const GemmArgs& g, hipStream_t st) {
   }
   return pick_bm(g.M, g.N, 1) == 128 ? launch_8p<128, true, true, 0, true>(g, 1, st)
                                      : launch_8p<256, true, true, 0, true>(g, 1, st);
+}
+
+// Implicit-GEMM convolution weight gradient: out[Cout][R*S*C] (bf16) = dY^T . im2col(x), split-K over
+// the output pixels into fp32 slabs, then the deterministic slab reduce. g: A = dY [pixels][Cout]
+// (lda = Cout), B = x (NHWC), M = Cout, N = R*S*C, K = pixels, cv_* the convolution geometry.
+hipError_t launch_conv_wgrad(const GemmArgs& g0, float* slab, int splits, void* out, hipStream_t st) {
+  if (g0.M <= 0 || g0.N <= 0) return hipSuccess;
+  const bool ok = !g0.a_kmajor && !g0.b_kmajor && g0.cv_logC >= 3 && g0.N % (1 << g0.cv_logC) == 0 &&
+                  g0.M >= 256 && g0.M % 8 == 0 && g0.N >= 256 && g0.N % 8 == 0 && g0.K % 64 == 0 && g0.K >= 128 &&
+                  g0.cv_abytes > 0 && g0.cv_S > 0 && g0.cv_W < 32768 && g0.cv_H < 32768 && splits >= 1 &&
+                  (int64_t)(g0.K - 1) * g0.lda + g0.M < ((int64_t)1 << 31) && big_variant() == 2;
+  if (!ok) return hipErrorNotSupported;
+  GemmArgs g = g0;
+  g.C = slab;
+  int kps = (g.K + splits - 1) / splits;
+  kps = (kps + 2 * BK - 1) / (2 * BK) * (2 * BK);  // >= 2 K-tiles per split, whole K-tiles
+  g.k_per_split = kps;
+  const int eff = (g.K + kps - 1) / kps;
+  hipError_t e = launch_8p_act<256, false, false, 1, false, 0, false, 0, true>(g, eff, st);
+  if (e != hipSuccess) return e;
+  const int64_t mn = (int64_t)g.M * g.N;
+  hipLaunchKernelGGL(splitk_reduce_kernel<true>, dim3(stream_grid((mn >> 3) > 0 ? (mn >> 3) : 1, 256)), dim3(256), 0, st,
+                     slab, eff, mn, out, 0, 1.f);
+  return hipGetLastError();
 }
 
 int gemm_splits(int M, int N, int K) {

@@ -36,6 +36,10 @@ int gemm_splits(int M, int N, int K);
 hipError_t launch_conv_fwd(const GemmArgs& g, hipStream_t stream);
 // the same with x and w OCP e4m3 (C % 128 == 0), dequantised by *a_scale * *b_scale (bf16 out)
 hipError_t launch_conv_fwd_fp8(const GemmArgs& g, hipStream_t stream);
+// implicit-GEMM weight gradient: out [Cout][R*S*C] bf16 = dY^T . im2col(x) (A = dY [pixels][Cout],
+// B = x NHWC, K = pixels % 64 == 0), split-K into slab [splits][Cout][R*S*C] fp32 + reduce;
+// hipErrorNotSupported outside the kernel's contract
+hipError_t launch_conv_wgrad(const GemmArgs& g, float* slab, int splits, void* out, hipStream_t stream);
 // split-K GEMM into fp32 slabs [splits][M][N], then out = (acc ? out : 0) + scale * sum(slabs)
 hipError_t launch_gemm_splitk(const GemmArgs& g, float* slab, int splits, void* out, int out_bf16, int accumulate,
                               float scale, hipStream_t stream);

@@ -23,7 +23,9 @@ Every other convolution (3x3 at any stride, strided 1x1 downsample) is a ``ConvN
 picks MIOpen or the implicit-GEMM kernel (the persistent 8-phase MFMA GEMM of kernels/gemm.hip
 with its A operand gathered from the NHWC input, ``conv_fwd_``; 1.2-1.6x MIOpen on the ResNet-50 /
 WRN-101-2 b1024 shapes, profiles/conv_igemm_vs_miopen_r2.md), and a stride-1 bwd-data is the same
-kernel run on dY with the flipped, transposed weights. The weight gradient stays on MIOpen.
+kernel run on dY with the flipped, transposed weights. The weight gradient picks MIOpen or the
+implicit-GEMM weight-gradient mode of the same kernel (dY^T . im2col(x), the im2col image gathered
+per K-tile; split-K over the output pixels).
 
 Reference parity: none -- the reference has no model (its gradient is the constant 0.01,
 src/worker.cpp:316-329). This is worker-side compute for the BASELINE.json ResNet configs.
@@ -266,6 +268,14 @@ def _igemm_ok(cin: int, cout: int) -> bool:
     return _pow2_ge64(cin) and cout >= 256 and cout % 8 == 0
 
 
+def _wgrad_ok(cin: int, cout: int, k: int, dy: torch.Tensor) -> bool:
+    """conv_wgrad_'s contract (kernels/gemm.hip launch_conv_wgrad): C a power of two >= 8, Cout >= 256
+    (one 256-row tile) and a multiple of 8, R*S*C >= 256, output pixels a multiple of 64."""
+    n, _, ho, wo = dy.shape
+    return (cin >= 8 and (cin & (cin - 1)) == 0 and cout >= 256 and cout % 8 == 0 and k * k * cin >= 256
+            and (n * ho * wo) % 64 == 0)
+
+
 def _igemm(x: torch.Tensor, w2: torch.Tensor, k: int, stride: int, pad: int):
     """conv(x, w) on the implicit-GEMM kernel, as a channels_last [N, Cout, Ho, Wo] tensor, or None
     when the kernel declines the shape."""
@@ -367,10 +377,34 @@ class _ConvFn(torch.autograd.Function):
             else:
                 dx = miopen()
         if ctx.needs_input_grad[1]:
-            dw = conv_bwd(dy, x, weight, *args, [False, True, False])[1]
             sv = _sink_view(ctx.mod, weight)
-            if sv is not None:
-                dw = sv.copy_(dw)
+
+            def miopen_w():
+                return conv_bwd(dy, x, weight, *args, [False, True, False])[1]
+
+            def igemm_w(into=None):  # dW = dY^T . im2col(x): split-K implicit GEMM (kernels/gemm.hip)
+                o = into if into is not None else torch.empty(cout, k, k, cin, device=dy.device, dtype=dy.dtype)
+                if not _native().conv_wgrad_(dy, x, o.view(cout, k * k * cin), k, k, stride, pad):
+                    return None
+                return o.permute(0, 3, 1, 2)  # OHWI storage = the channels_last [Cout, Cin, k, k] weight
+
+            def igemm_c():
+                y = igemm_w()
+                return miopen_w() if y is None else y
+
+            cands = {"miopen": miopen_w}
+            if (_at.enabled("PSD_CONV_WGRAD") and _wgrad_ok(cin, cout, k, dy)
+                    and weight.is_contiguous(memory_format=torch.channels_last)):
+                cands["igemm"] = igemm_c
+            key = ("wgrad", n, cin, h, w, cout, k, stride)
+            how = _at.choose(("conv",) + key, cands, "miopen") if len(cands) > 1 else "miopen"
+            dw = None
+            if how == "igemm":
+                dw = igemm_w(sv.permute(0, 2, 3, 1) if sv is not None else None)
+            if dw is None:
+                dw = miopen_w()
+                if sv is not None:
+                    dw = sv.copy_(dw)
         return dx, dw, None, None, None, None
 
 

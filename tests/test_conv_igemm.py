@@ -171,3 +171,53 @@ def test_fp8_conv_modules_match_fp32(gpu, kind):
     assert float(gerr.mean()) < 0.015 * gscale
     torch.testing.assert_close(conv.weight.grad.float(), ref.weight.grad, rtol=2e-2,
                                atol=2e-2 * float(ref.weight.grad.abs().max()))
+
+
+# ---------------------------------------------------------------- implicit-GEMM weight gradient
+WG_CASES = [  # Nb, C, H, W, Cout, R, stride, pad
+    (4, 64, 16, 16, 256, 3, 1, 1),
+    (8, 128, 14, 14, 256, 3, 2, 1),
+    (16, 256, 8, 8, 512, 1, 2, 0),
+    (32, 256, 14, 14, 256, 3, 1, 1),   # long pixel reduction: several K-tiles per split
+    (2, 128, 12, 12, 264, 3, 1, 1),    # ragged Cout
+]
+
+
+@pytest.mark.parametrize("case", WG_CASES, ids=lambda c: "x".join(map(str, c)))
+def test_conv_wgrad_exact(gpu, case):
+    """dW = dY^T . im2col(x) on the gathered-B split-K kernel vs the fp32 weight gradient, small
+    integers (exact products, exact fp32 sums below 2^24)."""
+    Nb, C, H, W, Cout, R, stride, pad = case
+    g = torch.Generator().manual_seed(13)
+    x = torch.randint(-2, 3, (Nb, C, H, W), generator=g).float()
+    wt = torch.zeros(Cout, C, R, R, requires_grad=True)
+    y = F.conv2d(x, wt, stride=stride, padding=pad)
+    dy = torch.randint(-2, 3, y.shape, generator=g).float()
+    y.backward(dy)
+    ref = wt.grad.permute(0, 2, 3, 1).reshape(Cout, -1)  # OHWI
+    out = torch.empty(Cout, R * R * C, device=gpu, dtype=torch.bfloat16)
+    xd = x.to(gpu, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dyd = dy.to(gpu, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    assert native().conv_wgrad_(dyd, xd, out, R, R, stride, pad)
+    torch.testing.assert_close(out.float().cpu(), ref.bfloat16().float(), rtol=0, atol=0)
+
+
+def test_convnhwc_wgrad_route_matches_fp32(gpu, monkeypatch):
+    """ConvNHWC with every route forced to the implicit-GEMM kernels, weight gradient included."""
+    from parameter_server_distributed_amd.ops.conv import ConvNHWC
+
+    monkeypatch.setenv("PSD_AUTOTUNE_FORCE", "igemm")
+    torch.manual_seed(6)
+    conv = ConvNHWC(128, 256, 3, 1).to(gpu, torch.bfloat16).to(memory_format=torch.channels_last)
+    ref = torch.nn.Conv2d(128, 256, 3, padding=1, bias=False).to(gpu)
+    ref.weight.data.copy_(conv.weight.float())
+    x = torch.randn(8, 128, 14, 14, device=gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    xr = x.float().clone().requires_grad_(True)
+    y = conv(x.requires_grad_(True))
+    yr = ref(xr)
+    gy = torch.randn_like(yr)
+    y.backward(gy.to(torch.bfloat16))
+    yr.backward(gy)
+    assert conv.weight.grad.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(conv.weight.grad.float(), ref.weight.grad, rtol=2e-2,
+                               atol=2e-2 * float(ref.weight.grad.abs().max()))
