@@ -217,8 +217,7 @@ bool conv_wgrad_(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int6
                   out.scalar_type() == at::kBFloat16,
               "psd conv_wgrad: out must be a contiguous bf16 [Cout, R*S*C]");
   const int64_t xbytes = x.numel() * 2;
-  if ((C & (C - 1)) != 0 || C < 8 || xbytes >= ((int64_t)1 << 32) || K >= ((int64_t)1 << 31) || K % 64 != 0)
-    return false;
+  if ((C & (C - 1)) != 0 || C < 8 || xbytes >= ((int64_t)1 << 32) || K >= ((int64_t)1 << 31) || K < 128) return false;
   int logc = 0;
   while ((1 << logc) < C) ++logc;
   const c10::DeviceGuard g(x.device());

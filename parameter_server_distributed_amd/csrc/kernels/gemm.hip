@@ -791,7 +791,9 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
     kbeg = blockIdx.z * g.k_per_split;
     kend = min(g.K, kbeg + g.k_per_split);
   }
-  const int nt = (kend - kbeg) / KT;  // >= 2 whenever G < ntiles (host contract)
+  // >= 2 whenever G < ntiles (host contract); GB: a partial last K-tile reads zeros past K (both
+  // operands are range-checked), so K needs no multiple of 64
+  const int nt = GB ? (kend - kbeg + KT - 1) / KT : (kend - kbeg) / KT;
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wid >> 2, wc = wid & 3;
@@ -1520,7 +1522,7 @@ hipError_t launch_gemm_fp8(const GemmArgs& g, hipStream_t st) {
 hipError_t launch_conv_wgrad(const GemmArgs& g0, float* slab, int splits, void* out, hipStream_t st) {
   if (g0.M <= 0 || g0.N <= 0) return hipSuccess;
   const bool ok = !g0.a_kmajor && !g0.b_kmajor && g0.cv_logC >= 3 && g0.N % (1 << g0.cv_logC) == 0 &&
-                  g0.M >= 256 && g0.M % 8 == 0 && g0.N >= 256 && g0.N % 8 == 0 && g0.K % 64 == 0 && g0.K >= 128 &&
+                  g0.M >= 256 && g0.M % 8 == 0 && g0.N >= 256 && g0.N % 8 == 0 && g0.K >= 128 &&
                   g0.cv_abytes > 0 && g0.cv_S > 0 && g0.cv_W < 32768 && g0.cv_H < 32768 && splits >= 1 &&
                   (int64_t)(g0.K - 1) * g0.lda + g0.M < ((int64_t)1 << 31) && big_variant() == 2;
   if (!ok) return hipErrorNotSupported;

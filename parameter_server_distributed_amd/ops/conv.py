@@ -270,10 +270,10 @@ def _igemm_ok(cin: int, cout: int) -> bool:
 
 def _wgrad_ok(cin: int, cout: int, k: int, dy: torch.Tensor) -> bool:
     """conv_wgrad_'s contract (kernels/gemm.hip launch_conv_wgrad): C a power of two >= 8, Cout >= 256
-    (one 256-row tile) and a multiple of 8, R*S*C >= 256, output pixels a multiple of 64."""
+    (one 256-row tile) and a multiple of 8, R*S*C >= 256, >= 128 output pixels."""
     n, _, ho, wo = dy.shape
     return (cin >= 8 and (cin & (cin - 1)) == 0 and cout >= 256 and cout % 8 == 0 and k * k * cin >= 256
-            and (n * ho * wo) % 64 == 0)
+            and n * ho * wo >= 128)
 
 
 def _igemm(x: torch.Tensor, w2: torch.Tensor, k: int, stride: int, pad: int):
