@@ -35,7 +35,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_fwd", &bn_fwd, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("running_mean"),
         py::arg("running_var"), py::arg("residual"), py::arg("relu"), py::arg("training"), py::arg("momentum"),
         py::arg("eps"), py::arg("counter"), py::arg("ss_eval"), py::arg("mask_out") = false,
-        py::arg("residual_ss") = py::none(), py::arg("stats_only") = false);
+        py::arg("residual_ss") = py::none(), py::arg("stats_only") = false, py::arg("q8_out") = py::none(),
+        py::arg("q8_hist") = py::none(), py::arg("q8_sinv") = py::none(), py::arg("q8_margin") = 1.0);
   m.def("bn_bwd_dual", &bn_bwd_dual, py::arg("dy"), py::arg("x"), py::arg("gamma"), py::arg("save_mean"),
         py::arg("save_invstd"), py::arg("mbits"), py::arg("dy2"), py::arg("xd"), py::arg("gamma_d"), py::arg("mean_d"),
         py::arg("invstd_d"), py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none(),

@@ -38,7 +38,9 @@ std::vector<at::Tensor> bn_fwd(const at::Tensor& x_in, c10::optional<at::Tensor>
                                c10::optional<at::Tensor> running_mean, c10::optional<at::Tensor> running_var,
                                c10::optional<at::Tensor> residual, bool relu, bool training, double momentum, double eps,
                                c10::optional<at::Tensor> counter, c10::optional<at::Tensor> ss_eval, bool mask_out,
-                               c10::optional<at::Tensor> residual_ss, bool stats_only) {
+                               c10::optional<at::Tensor> residual_ss, bool stats_only,
+                               c10::optional<at::Tensor> q8_out, c10::optional<at::Tensor> q8_hist,
+                               c10::optional<at::Tensor> q8_sinv, double q8_margin) {
   TORCH_CHECK(x_in.is_cuda() && x_in.scalar_type() == at::kBFloat16, "psd bn: x must be a bf16 device tensor");
   const c10::DeviceGuard g(x_in.device());
   at::Tensor x = nhwc(x_in);
@@ -96,6 +98,20 @@ std::vector<at::Tensor> bn_fwd(const at::Tensor& x_in, c10::optional<at::Tensor>
   a.eps = (float)eps;
   a.res_ss = rss ? residual_ss->data_ptr<float>() : nullptr;
   a.stats_only = stats_only;
+  if (q8_out.has_value() && q8_out->defined()) {
+    const at::Tensor& q = *q8_out;
+    const bool laid = q.dim() == 4 ? q.is_contiguous(at::MemoryFormat::ChannelsLast) : q.is_contiguous();
+    TORCH_CHECK(!stats_only && relu && q.scalar_type() == at::kFloat8_e4m3fn && q.sizes() == x.sizes() && laid &&
+                    (reinterpret_cast<uintptr_t>(q.data_ptr()) & 7) == 0,
+                "psd bn: q8_out must be an e4m3fn tensor laid out like x (ReLU BNs)");
+    TORCH_CHECK(q8_hist.has_value() && q8_hist->numel() >= 2 && q8_hist->scalar_type() == at::kFloat &&
+                    q8_sinv.has_value() && q8_sinv->numel() >= 1 && q8_sinv->scalar_type() == at::kFloat,
+                "psd bn: q8_out needs q8_hist fp32[2] and q8_sinv fp32[1]");
+    a.q8 = reinterpret_cast<uint8_t*>(q.data_ptr());
+    a.q8hist = q8_hist->data_ptr<float>();
+    a.q8sinv = q8_sinv->data_ptr<float>();
+    a.q8margin = (float)q8_margin;
+  }
   hipError_t e = launch_bn_fwd(a, stream_of(x));
   TORCH_CHECK(e == hipSuccess, "psd bn fwd: ", hipGetErrorString(e));
   return {y, mean, invstd, ss, mbits};

@@ -17,6 +17,7 @@
 //                      3 coefficients) -> elementwise dx = A dy' + B x + C.
 // Block partials are combined by a separate finalize launch (no cross-workgroup hand-off inside a
 // launch: correct for any workgroup->XCD placement, cdna_hip_programming.md G16).
+#include <hip/hip_fp8.h>
 #include "common.h"
 #include "launchers_bn.h"
 #include "pool_gather.h"
@@ -201,11 +202,23 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const float* __res
 // RSS: the residual is itself a raw BN input (the downsample branch's convolution output) whose
 // scale/shift rss is applied here, so that BN's own apply pass (a full write + read of the
 // residual) never runs.
-template <bool RELU, bool RES, bool MASK_OUT, bool RSS = false>
+// Q8: also write y as OCP e4m3 for an fp8 consumer convolution (delayed scaling: scale from the
+// consumer's amax history q8hist[0] * margin, this pass's amax max-reduced into q8hist[1]; the
+// roll kernel after the launch moves it to q8hist[0]) -- the consumer's own quantise pass (a full
+// read of y) never runs.
+template <bool RELU, bool RES, bool MASK_OUT, bool RSS = false, bool Q8 = false>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
                                                        const float* __restrict__ ss, uint16_t* __restrict__ y,
                                                        uint8_t* __restrict__ mbits, int pack4, int64_t nvec, int C,
-                                                       const float* __restrict__ rss = nullptr) {
+                                                       const float* __restrict__ rss = nullptr,
+                                                       uint8_t* __restrict__ q8 = nullptr, float* q8hist = nullptr,
+                                                       float q8margin = 1.f, float* __restrict__ q8sinv = nullptr) {
+  float q8scale = 0.f, q8max = 0.f;
+  if (Q8) {
+    const float a = fmaxf(q8hist[0] * q8margin, 1e-12f);
+    q8scale = 448.f / a;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *q8sinv = a / 448.f;
+  }
   const int tpc = C >> 3;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;  // host guarantees stride % tpc == 0
   int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -231,6 +244,18 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
       t[j] = o;
     }
     store8_bf16(y + v * 8, t);
+    if (Q8) {  // quantise the stored (bf16-rounded) values
+      uint32_t lo = 0, hi = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float r = bf16_to_f32(f32_to_bf16(t[j]));
+        q8max = fmaxf(q8max, fabsf(r));
+        const uint32_t b = (uint32_t)__hip_cvt_float_to_fp8(r * q8scale, __HIP_SATFINITE, __HIP_E4M3);
+        if (j < 4) lo |= b << (8 * j);
+        else hi |= b << (8 * (j - 4));
+      }
+      *reinterpret_cast<uint2*>(q8 + v * 8) = make_uint2(lo, hi);
+    }
     if (MASK_OUT) {
       uint32_t bits = 0;
 #pragma unroll
@@ -248,6 +273,16 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
       }
     }
   }
+  if (Q8) {
+    for (int off = 32; off > 0; off >>= 1) q8max = fmaxf(q8max, __shfl_xor(q8max, off, kWave));
+    if ((threadIdx.x & (kWave - 1)) == 0)
+      atomicMax(reinterpret_cast<unsigned int*>(q8hist + 1), __float_as_uint(q8max));  // one per wave
+  }
+}
+
+__global__ void bn_q8_roll_kernel(float* hist) {
+  hist[0] = hist[1];
+  hist[1] = 0.f;
 }
 
 // ------------------------------------------------------------------ backward
@@ -699,6 +734,20 @@ hipError_t launch_bn_fwd(const BnFwdArgs& a, hipStream_t st) {
 #define PSD_APPLY(R, S, B) \
   hipLaunchKernelGGL((bn_apply_kernel<R, S, B>), dim3(g), dim3(256), 0, st, a.x, a.res, a.ss, a.y, a.mbits, \
                      (int)(nvec % 4 == 0), nvec, a.C, nullptr)
+  if (a.q8) {  // fp8 side output for the consumer convolution (ReLU BNs: bn1 / bn2 / residual bn3)
+    if (!a.relu || !a.q8hist || !a.q8sinv) return hipErrorInvalidValue;
+    const int p4 = (int)(nvec % 4 == 0);
+#define PSD_APQ(S, B, RS)                                                                                      \
+  hipLaunchKernelGGL((bn_apply_kernel<true, S, B, RS, true>), dim3(g), dim3(256), 0, st, a.x, a.res, a.ss, a.y, \
+                     a.mbits, p4, nvec, a.C, a.res_ss, a.q8, a.q8hist, a.q8margin, a.q8sinv)
+    if (a.res_ss && a.res && a.mbits) PSD_APQ(true, true, true);
+    else if (a.res && a.mbits && !a.res_ss) PSD_APQ(true, true, false);
+    else if (!a.res && !a.mbits && !a.res_ss) PSD_APQ(false, false, false);
+    else return hipErrorInvalidValue;
+#undef PSD_APQ
+    hipLaunchKernelGGL(bn_q8_roll_kernel, dim3(1), dim3(1), 0, st, a.q8hist);
+    return hipGetLastError();
+  }
   if (a.res_ss) {  // residual = bn(res) applied on the fly (ReLU blocks only)
     if (!a.res || !a.relu) return hipErrorInvalidValue;
     if (a.mbits)

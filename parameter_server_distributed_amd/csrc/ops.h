@@ -21,7 +21,9 @@ std::vector<at::Tensor> bn_fwd(const at::Tensor& x, c10::optional<at::Tensor> ga
                                c10::optional<at::Tensor> running_mean, c10::optional<at::Tensor> running_var,
                                c10::optional<at::Tensor> residual, bool relu, bool training, double momentum, double eps,
                                c10::optional<at::Tensor> counter, c10::optional<at::Tensor> ss_eval,
-                               bool mask_out, c10::optional<at::Tensor> residual_ss, bool stats_only);
+                               bool mask_out, c10::optional<at::Tensor> residual_ss, bool stats_only,
+                               c10::optional<at::Tensor> q8_out, c10::optional<at::Tensor> q8_hist,
+                               c10::optional<at::Tensor> q8_sinv, double q8_margin);
 std::vector<at::Tensor> bn_bwd_dual(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& gamma,
                                     const at::Tensor& save_mean, const at::Tensor& save_invstd, const at::Tensor& mbits,
                                     c10::optional<at::Tensor> dy2, const at::Tensor& xd, const at::Tensor& gamma_d,

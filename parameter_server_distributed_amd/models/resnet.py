@@ -65,6 +65,10 @@ class Bottleneck(nn.Module):
         self.bn3 = FusedBatchNorm2d(planes * self.expansion, relu=True)  # relu(bn3(conv3) + identity)
         self.downsample = downsample
         self.fuse_residual_grad = True
+        if fp8:  # bn1 / bn2 quantise their outputs for the fp8 conv2 / conv3 in their apply pass
+            # (plain attributes: object.__setattr__ keeps the consumer from becoming a submodule)
+            object.__setattr__(self.bn1, "_psd_q8_consumer", self.conv2)
+            object.__setattr__(self.bn2, "_psd_q8_consumer", self.conv3)
 
     def forward(self, x, prev_bn=None):
         """``prev_bn``: the fused BN that produced ``x`` (the previous block's bn3). The second
@@ -114,6 +118,10 @@ class ResNet(nn.Module):
             for m in self.modules():
                 if isinstance(m, Bottleneck):
                     nn.init.zeros_(m.bn3.weight)
+        if fp8:  # each block's bn3 quantises the block output for the next block's fp8 conv1
+            blocks = [b for layer in (self.layer1, self.layer2, self.layer3, self.layer4) for b in layer]
+            for prev, nxt in zip(blocks, blocks[1:]):
+                object.__setattr__(prev.bn3, "_psd_q8_consumer", nxt.conv1)
 
     def _make(self, planes, blocks, stride=1):
         down = None

@@ -26,14 +26,36 @@ def _kernel_ok(x: torch.Tensor) -> bool:
     return x.is_cuda and x.dtype == torch.bfloat16 and x.dim() in (2, 4) and x.shape[1] % 8 == 0
 
 
+def _q8_args(mod, x: torch.Tensor) -> dict:
+    """If ``mod``'s output feeds an fp8 convolution (``_psd_q8_consumer``, wired by the model) whose
+    activation scaler already has an amax history, the apply pass also writes the e4m3 copy the
+    consumer would otherwise quantise in a pass of its own (ops/conv.py DelayedScale)."""
+    cons = getattr(mod, "_psd_q8_consumer", None)
+    if cons is None or not mod.relu or x.dim() != 4 or not cons.psd_fp8_consumes(x.shape[1]):
+        return {}
+    sc = cons._f8[0]
+    if sc.hist is None or sc.hist.device != x.device:
+        return {}
+    q = torch.empty_like(x, dtype=torch.float8_e4m3fn, memory_format=torch.channels_last)
+    return {"q8_out": q, "q8_hist": sc.hist, "q8_sinv": torch.empty(1, dtype=torch.float32, device=x.device),
+            "q8_margin": sc.margin}
+
+
+def _q8_hand_over(mod, y: torch.Tensor, kw: dict) -> None:
+    if kw:
+        mod._psd_q8_consumer._psd_q8_pending = (y, kw["q8_out"], kw["q8_sinv"])
+
+
 class _FusedBNFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, mod, resid_to=None):
         C = native()
         has_res = residual is not None
+        q8 = _q8_args(mod, x)
         y, mean, invstd, ss, mbits = C.bn_fwd(x, weight, bias, mod.running_mean, mod.running_var, residual, mod.relu,
                                               True, mod.momentum if mod.momentum is not None else 0.1, mod.eps,
-                                              mod.num_batches_tracked, None, mask_out=mod.relu and has_res)
+                                              mod.num_batches_tracked, None, mask_out=mod.relu and has_res, **q8)
+        _q8_hand_over(mod, y, q8)
         ctx.relu = mod.relu
         ctx.has_res = residual is not None
         ctx.mod = mod
@@ -80,8 +102,11 @@ class _BNAddBNReluFn(torch.autograd.Function):
         mom = lambda m: m.momentum if m.momentum is not None else 0.1  # noqa: E731
         _, mean_d, invstd_d, ss_d, _ = C.bn_fwd(r, wd, bd, bnd.running_mean, bnd.running_var, None, False, True,
                                                 mom(bnd), bnd.eps, bnd.num_batches_tracked, None, stats_only=True)
+        q8 = _q8_args(bn3, x)
         y, mean, invstd, _, mbits = C.bn_fwd(x, w3, b3, bn3.running_mean, bn3.running_var, r, True, True, mom(bn3),
-                                             bn3.eps, bn3.num_batches_tracked, None, mask_out=True, residual_ss=ss_d)
+                                             bn3.eps, bn3.num_batches_tracked, None, mask_out=True, residual_ss=ss_d,
+                                             **q8)
+        _q8_hand_over(bn3, y, q8)
         ctx.bn3, ctx.bnd = bn3, bnd
         ctx.save_for_backward(x, mbits, w3, mean, invstd, r, wd, mean_d, invstd_d)
         return y

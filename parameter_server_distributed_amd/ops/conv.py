@@ -94,6 +94,20 @@ def _q8(t2: torch.Tensor, e5m2: bool = False, scaler: "DelayedScale | None" = No
     return quantize_fp8(t2, e5m2=e5m2)
 
 
+def _take_q8(mod, x: torch.Tensor):
+    """The e4m3 copy of ``x`` that the producing BN's apply pass wrote for this module (ops/bn.py,
+    delayed scaling with this module's activation scaler), as (q [N, C, H, W] channels_last,
+    scale_inv), or None. Consumed once."""
+    pend = getattr(mod, "_psd_q8_pending", None) if mod is not None else None
+    if pend is None:
+        return None
+    mod._psd_q8_pending = None
+    y, q, sinv = pend
+    if y.data_ptr() != x.data_ptr() or y.shape != x.shape or y.stride() != x.stride():
+        return None
+    return q, sinv
+
+
 class DelayedScale:
     """Delayed fp8 scaling for one tensor role of one layer (its input activations, or its output
     gradient): each call quantises with the amax the previous call recorded (times ``margin``) and
@@ -146,7 +160,11 @@ class _Conv1x1Fn(torch.autograd.Function):
         if fp8 and _fp8_ok(cin, cout):
             # fp8 forward: e4m3 operands on the MX-scaled MFMA (2x the bf16 rate), dequantised in the
             # epilogue; the weight gradient runs on the saved bf16 x and W
-            xq, sx = _q8(x2, scaler=f8[0])
+            got = _take_q8(mod, x)
+            if got is not None:  # quantised by the producing BN's apply pass
+                xq, sx = got[0].permute(0, 2, 3, 1).reshape(n * h * w, cin), got[1]
+            else:
+                xq, sx = _q8(x2, scaler=f8[0])
             wq, sw = _q8(w2)
             out = torch.empty(n * h * w, cout, device=x.device, dtype=x.dtype)
             _native().gemm_fp8_(xq, wq, sx, sw, out)
@@ -246,6 +264,10 @@ class Conv1x1(nn.Conv2d):
     def psd_direct_grad_params(self):
         return [self.weight]
 
+    def psd_fp8_consumes(self, cin: int) -> bool:
+        """True when this module's forward quantises its input (so a producer may do it instead)."""
+        return self.fp8 and _fp8_ok(cin, self.out_channels) and _enabled()
+
     def forward(self, x):
         if (_enabled() and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
                 and self.weight.dtype == torch.bfloat16 and torch.is_grad_enabled()
@@ -290,7 +312,7 @@ def _igemm(x: torch.Tensor, w2: torch.Tensor, k: int, stride: int, pad: int):
 
 
 def _igemm_fp8(x: torch.Tensor, w2: torch.Tensor, k: int, stride: int, pad: int, e5m2: bool = False,
-               scaler: "DelayedScale | None" = None):
+               scaler: "DelayedScale | None" = None, pre=None):
     """conv(x, w) with fp8 operands on the implicit-GEMM kernel (per-tensor just-in-time scales; x
     e4m3, or e5m2 when it is an output gradient), bf16 channels_last out, or None when the kernel
     declines the shape."""
@@ -298,7 +320,10 @@ def _igemm_fp8(x: torch.Tensor, w2: torch.Tensor, k: int, stride: int, pad: int,
 
     n, c, h, w = x.shape
     ho, wo = (h + 2 * pad - k) // stride + 1, (w + 2 * pad - k) // stride + 1
-    xq, sx = _q8(x.permute(0, 2, 3, 1), e5m2=e5m2, scaler=scaler)  # the NHWC storage, in place order
+    if pre is not None:  # (q channels_last [N, C, H, W], scale_inv) from the producing BN
+        xq, sx = pre[0].permute(0, 2, 3, 1), pre[1]
+    else:
+        xq, sx = _q8(x.permute(0, 2, 3, 1), e5m2=e5m2, scaler=scaler)  # the NHWC storage, in place order
     wq, sw = _q8(w2)
     out = torch.empty(n * ho * wo, w2.shape[0], device=x.device, dtype=x.dtype)
     if not native().conv_fwd_fp8_(xq.permute(0, 3, 1, 2), wq, sx, sw, out, k, k, stride, pad):
@@ -323,7 +348,8 @@ class _ConvFn(torch.autograd.Function):
 
         if fp8 and cin % 128 == 0 and _fp8_ok(k * k * cin, cout):
             w2 = weight.permute(0, 2, 3, 1).reshape(cout, k * k * cin)
-            y = _igemm_fp8(x, w2 if w2.is_contiguous() else w2.contiguous(), k, stride, pad, scaler=f8[0])
+            y = _igemm_fp8(x, w2 if w2.is_contiguous() else w2.contiguous(), k, stride, pad, scaler=f8[0],
+                           pre=_take_q8(mod, x))
             if y is not None:
                 return y
 
@@ -420,6 +446,11 @@ class ConvNHWC(nn.Conv2d):
 
     def psd_direct_grad_params(self):
         return [self.weight]
+
+    def psd_fp8_consumes(self, cin: int) -> bool:
+        k = self.kernel_size[0]
+        return (self.fp8 and cin % 128 == 0 and _fp8_ok(k * k * cin, self.out_channels) and _enabled()
+                and _at.enabled("PSD_CONV_IGEMM"))
 
     def forward(self, x):
         if (_enabled() and _at.enabled("PSD_CONV_IGEMM") and x.is_cuda and x.dtype == torch.bfloat16

@@ -2,8 +2,6 @@
 against the same model trained in bf16: over several SGD steps from the same initial weights on the
 same batches, the first-step gradients and the loss trajectories stay within fp8 error of each other, and
 the fp8 kernels really ran (their delayed-scaling histories were seeded)."""
-import copy
-
 import pytest
 import torch
 import torch.nn.functional as F
@@ -29,13 +27,12 @@ def test_fp8_wide_resnet_tracks_bf16(gpu):
     from parameter_server_distributed_amd.models.resnet import ResNet
     from parameter_server_distributed_amd.ops.conv import Conv1x1, ConvNHWC
 
+    # a short Wide-ResNet (width_per_group 128, two blocks per stage): stages 2-4 have fp8 shapes;
+    # the same seed gives both models the same initial weights
     torch.manual_seed(0)
-    # a short Wide-ResNet (width_per_group 128, one block per stage): stages 2-4 have fp8 shapes
-    base = ResNet((1, 1, 1, 1), num_classes=100, width_per_group=128)
-    m8 = copy.deepcopy(base)
-    for mod in m8.modules():
-        if isinstance(mod, (Conv1x1, ConvNHWC)):
-            mod.fp8 = True
+    base = ResNet((2, 2, 2, 2), num_classes=100, width_per_group=128)
+    torch.manual_seed(0)
+    m8 = ResNet((2, 2, 2, 2), num_classes=100, width_per_group=128, fp8=True)
     mb = prepare(base, gpu, torch.bfloat16, channels_last=True)
     m8 = prepare(m8, gpu, torch.bfloat16, channels_last=True)
     for m in (mb, m8):  # bf16 weights (the PS data plane's working copy)
@@ -70,3 +67,33 @@ def test_fp8_wide_resnet_tracks_bf16(gpu):
         assert abs(a - b) <= 0.05 * abs(a) + 0.05, (lb, l8)
     assert l8[-1] < l8[0], l8  # it trains
 
+
+
+def test_bn_apply_writes_the_consumers_fp8_input(gpu):
+    """A ReLU BN feeding an fp8 convolution writes the e4m3 copy of its output in the apply pass
+    with the consumer's delayed scale: bit-equal to the consumer quantising the output itself with
+    the same amax history, and the history then holds the output's amax."""
+    from parameter_server_distributed_amd.ops.bn import FusedBatchNorm2d
+    from parameter_server_distributed_amd.ops.conv import Conv1x1, DelayedScale
+
+    torch.manual_seed(2)
+    bn = FusedBatchNorm2d(256, relu=True).to(gpu)
+    bn.weight.data = bn.weight.data.to(torch.bfloat16)
+    bn.bias.data = bn.bias.data.to(torch.bfloat16)
+    conv = Conv1x1(256, 512, fp8=True).to(gpu, torch.bfloat16)
+    object.__setattr__(bn, "_psd_q8_consumer", conv)
+    conv._f8[0].hist = torch.tensor([3.0, 0.0], device=gpu)
+    x = torch.randn(4, 256, 14, 14, device=gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y = bn(x.requires_grad_(True))
+    yb, q, sinv = conv._psd_q8_pending
+    assert yb is y
+    ref = DelayedScale(1.0)
+    ref.hist = torch.tensor([3.0, 0.0], device=gpu)
+    qr, sr = ref.quantize(y.detach().permute(0, 2, 3, 1), False)
+    torch.cuda.synchronize()
+    assert torch.equal(q.permute(0, 2, 3, 1).contiguous().view(torch.uint8), qr.view(torch.uint8))
+    assert torch.equal(sinv, sr)
+    amax = float(y.detach().float().abs().max())
+    assert float(conv._f8[0].hist[0]) == amax and float(conv._f8[0].hist[1]) == 0.0
+    out = conv(y)  # consumes the hand-over
+    assert conv._psd_q8_pending is None and out.shape == (4, 512, 14, 14)
