@@ -15,6 +15,8 @@ compare the kernels against.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -32,6 +34,8 @@ def _q8_args(mod, x: torch.Tensor) -> dict:
     consumer would otherwise quantise in a pass of its own (ops/conv.py DelayedScale)."""
     cons = getattr(mod, "_psd_q8_consumer", None)
     if cons is None or not mod.relu or x.dim() != 4 or not cons.psd_fp8_consumes(x.shape[1]):
+        return {}
+    if os.environ.get("PSD_FP8_HANDOVER", "1") == "0":  # A/B switch
         return {}
     sc = cons._f8[0]
     if sc.hist is None or sc.hist.device != x.device:
