@@ -35,7 +35,10 @@ def _q8_args(mod, x: torch.Tensor) -> dict:
     cons = getattr(mod, "_psd_q8_consumer", None)
     if cons is None or not mod.relu or x.dim() != 4 or not cons.psd_fp8_consumes(x.shape[1]):
         return {}
-    if os.environ.get("PSD_FP8_HANDOVER", "1") == "0":  # A/B switch
+    # measured on Wide-ResNet-101-2 b512: 3,589 / 3,584 img/s with the hand-over vs 3,606 without
+    # (same box, one call): the extra fp8 convert in the apply pass costs what the saved read of y
+    # gains, so it is opt-in (PSD_FP8_HANDOVER=1)
+    if os.environ.get("PSD_FP8_HANDOVER", "0") != "1":
         return {}
     sc = cons._f8[0]
     if sc.hist is None or sc.hist.device != x.device:

@@ -69,13 +69,14 @@ def test_fp8_wide_resnet_tracks_bf16(gpu):
 
 
 
-def test_bn_apply_writes_the_consumers_fp8_input(gpu):
+def test_bn_apply_writes_the_consumers_fp8_input(gpu, monkeypatch):
     """A ReLU BN feeding an fp8 convolution writes the e4m3 copy of its output in the apply pass
     with the consumer's delayed scale: bit-equal to the consumer quantising the output itself with
     the same amax history, and the history then holds the output's amax."""
     from parameter_server_distributed_amd.ops.bn import FusedBatchNorm2d
     from parameter_server_distributed_amd.ops.conv import Conv1x1, DelayedScale
 
+    monkeypatch.setenv("PSD_FP8_HANDOVER", "1")
     torch.manual_seed(2)
     bn = FusedBatchNorm2d(256, relu=True).to(gpu)
     bn.weight.data = bn.weight.data.to(torch.bfloat16)
