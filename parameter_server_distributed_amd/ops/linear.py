@@ -48,6 +48,27 @@ def _route(key: tuple, mfma, blas, out: torch.Tensor | None = None):
     return mfma if _at.choose(("linear",) + key, {"mfma": mfma, "blas": blas}, "mfma", probe) == "mfma" else blas
 
 
+def _dgrad_route(key: tuple, dy2: torch.Tensor, w: torch.Tensor, dx: torch.Tensor):
+    """dX = dY . W on the fastest of: the MFMA GEMM with W read N-major (NN), the MFMA GEMM on a
+    transposed copy of W (NT: both operands K-major, the kernel's fastest layout; the copy is
+    |W| bytes), or hipBLASLt -- timed and validated once per shape (ops/autotune.py)."""
+    C = native()
+
+    def nn_():
+        C.gemm_(dy2, w, True, False, dx)
+
+    def nt_():
+        C.gemm_(dy2, w.t().contiguous(), True, True, dx)
+
+    def blas():
+        torch.mm(dy2, w, out=dx)
+
+    if not _at.enabled("PSD_LINEAR_TUNE"):
+        return nn_
+    cands = {"mfma": nn_, "mfma_t": nt_, "blas": blas}
+    return cands[_at.choose(("linear",) + key, cands, "mfma", lambda: dx)]
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, mod):
@@ -116,8 +137,7 @@ class _LinearFn(torch.autograd.Function):
             dx = dx.view(ctx.in_shape)
         elif ctx.needs_input_grad[0]:
             dx = torch.empty(x2.shape, dtype=dy2.dtype, device=dy2.device)
-            _route(("dgrad", M, K, N), lambda: C.gemm_(dy2, w, True, False, dx),
-                   lambda: torch.mm(dy2, w, out=dx), dx)()
+            _dgrad_route(("dgrad", M, K, N), dy2, w, dx)()
             dx = dx.view(ctx.in_shape)
         dw = None
         if ctx.needs_input_grad[1]:
