@@ -275,3 +275,38 @@ def test_transport_policy_native_rccl_at_n_gt_1(monkeypatch):
     assert transport_kind(1, None, "rccl") == "rccl"
     with pytest.raises(ValueError):
         transport_kind(2, "nccl", "local")
+
+
+def test_zero_plan_merges_accumulated_ranges():
+    """The PS zeroes only the gradient ranges that are accumulated into (not the grad-sink ones):
+    adjacent / overlapping spans merge; too many ranges or most of the buffer -> one full zero."""
+    from parameter_server_distributed_amd.parallel.collective_ps import zero_grads_, zero_plan
+
+    assert zero_plan([(64, 64), (0, 64), (256, 10)], 4096) == [(0, 128), (256, 10)]
+    assert zero_plan([(0, 3000)], 4096) is None  # most of the buffer
+    assert zero_plan([(i * 100, 10) for i in range(20)], 4096) is None  # too many launches
+    assert zero_plan([], 4096) == []
+    g = torch.ones(512)
+    zero_grads_(g, [(0, 128), (256, 10)])
+    assert float(g[:128].sum()) == 0 and float(g[128:256].sum()) == 128 and float(g[256:266].sum()) == 0
+    zero_grads_(g, None)
+    assert float(g.sum()) == 0
+
+
+def test_bert_sink_params_skip_the_zero_fill():
+    """With MfmaLinear / LayerNorm grad sinks, only the embeddings (and the plain LayerNorms) are
+    accumulated: the PS zero plan covers a small part of BERT's gradient buffer."""
+    from parameter_server_distributed_amd.parallel.collective_ps import zero_plan
+
+    spec = models.build("bert_base", torch.device("cpu"), torch.float32, layers=2)
+    direct = set()
+    for m in spec.model.modules():
+        if hasattr(m, "psd_direct_grad_params"):
+            direct.update(id(p) for p in m.psd_direct_grad_params() if p is not None)
+    off, spans = 0, []
+    for p in spec.model.parameters():
+        if id(p) not in direct:
+            spans.append((off, p.numel()))
+        off += p.numel()
+    plan = zero_plan(spans, off)
+    assert plan is not None and sum(n for _, n in plan) < off // 2
