@@ -1388,6 +1388,15 @@ static hipError_t launch_8p(const GemmArgs& g, int splits, hipStream_t st) {
   return launch_8p_act<BM, AK, BKM, MODE, F8, 0>(g, splits, st);
 }
 
+// A/B override of the fp8 tile height (PSD_GEMM_F8_BM=128|256; 0: the pick_bm heuristic)
+static int f8_bm_override() {
+  static const int v = [] {
+    const char* e = getenv("PSD_GEMM_F8_BM");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 // 8-phase tile height: a 128x256 tile costs ~0.55 of a 256x256 one, so narrow problems (few
 // 256-tiles: wave quantisation over 256 CUs) take BM = 128 when that finishes in fewer rounds.
 // (BM = 128 needs a K-major A: its M-major half image would be 64 columns wide)
@@ -1494,7 +1503,7 @@ hipError_t launch_conv_fwd_fp8(const GemmArgs& g, hipStream_t st) {
                   g.cv_abytes > 0 && (int64_t)(g.M - 1) * g.ldc + g.N < ((int64_t)1 << 31) && g.cv_S > 0 &&
                   g.cv_W < 32768 && g.cv_H < 32768;
   if (!ok) return hipErrorNotSupported;
-  const bool b128 = pick_bm(g.M, g.N, 1) == 128;
+  const bool b128 = f8_bm_override() ? f8_bm_override() == 128 : pick_bm(g.M, g.N, 1) == 128;
   if (g.f8a == 1)
     return b128 ? launch_8p_act<128, true, true, 0, true, 0, true, 1>(g, 1, st)
                 : launch_8p_act<256, true, true, 0, true, 0, true, 1>(g, 1, st);
