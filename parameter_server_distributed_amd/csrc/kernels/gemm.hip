@@ -1503,7 +1503,10 @@ hipError_t launch_conv_fwd_fp8(const GemmArgs& g, hipStream_t st) {
                   g.cv_abytes > 0 && (int64_t)(g.M - 1) * g.ldc + g.N < ((int64_t)1 << 31) && g.cv_S > 0 &&
                   g.cv_W < 32768 && g.cv_H < 32768;
   if (!ok) return hipErrorNotSupported;
-  const bool b128 = f8_bm_override() ? f8_bm_override() == 128 : pick_bm(g.M, g.N, 1) == 128;
+  // 128-row tiles always: WRN-101-2 b512 A/B on two boxes, 3,443 vs 3,313 and 3,806 / 3,779 vs
+  // 3,749 img/s against the bf16-calibrated pick_bm (the fp8 tile is LDS/DMA-bound, so the taller
+  // tile's extra reuse buys less than its wave quantisation costs)
+  const bool b128 = f8_bm_override() ? f8_bm_override() == 128 : true;
   if (g.f8a == 1)
     return b128 ? launch_8p_act<128, true, true, 0, true, 0, true, 1>(g, 1, st)
                 : launch_8p_act<256, true, true, 0, true, 0, true, 1>(g, 1, st);
