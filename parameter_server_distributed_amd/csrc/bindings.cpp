@@ -1,6 +1,7 @@
 // pybind11 module `parameter_server_distributed_amd._C`.
 #include <torch/extension.h>
 
+#include "async_hyper.h"
 #include "async_ps.h"
 #include "checkpoint.h"
 #include "comm.h"
@@ -21,6 +22,21 @@ PYBIND11_MODULE(_C, m) {
         py::arg("shadow"), py::arg("dyn"), py::arg("kind"), py::arg("momentum") = 0.0, py::arg("dampening") = 0.0,
         py::arg("nesterov") = false, py::arg("weight_decay") = 0.0, py::arg("beta1") = 0.9, py::arg("beta2") = 0.999,
         py::arg("eps") = 1e-8, py::arg("maximize") = false);
+  m.def(
+      "async_hyper",
+      [](int kind, int workers, double momentum, double beta1, double beta2, double weight_decay) {
+        const AsyncHyper h = async_hyper(kind, workers, momentum, beta1, beta2, weight_decay);
+        py::dict d;
+        d["lr_factor"] = h.lr_factor;
+        d["grad_scale"] = h.grad_scale;
+        d["momentum"] = h.momentum;
+        d["beta1"] = h.beta1;
+        d["beta2"] = h.beta2;
+        d["weight_decay"] = h.weight_decay;
+        return d;
+      },
+      py::arg("kind"), py::arg("workers"), py::arg("momentum"), py::arg("beta1"), py::arg("beta2"),
+      py::arg("weight_decay"), "per-push optimizer hyperparameters of an apply-on-arrival PS (async_hyper.h)");
   m.def("optim_advance_", &optim_advance_, py::arg("dyn"), py::arg("beta1") = 0.9, py::arg("beta2") = 0.999);
   m.def("multi_reduce_", &multi_reduce_, py::arg("out"), py::arg("srcs"), py::arg("scale") = 1.0);
   m.def("pack_cast_", &pack_cast_, py::arg("srcs"), py::arg("dsts"));
@@ -36,7 +52,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("running_var"), py::arg("residual"), py::arg("relu"), py::arg("training"), py::arg("momentum"),
         py::arg("eps"), py::arg("counter"), py::arg("ss_eval"), py::arg("mask_out") = false,
         py::arg("residual_ss") = py::none(), py::arg("stats_only") = false, py::arg("q8_out") = py::none(),
-        py::arg("q8_hist") = py::none(), py::arg("q8_sinv") = py::none(), py::arg("q8_margin") = 1.0);
+        py::arg("q8_hist") = py::none(), py::arg("q8_sinv") = py::none(), py::arg("q8_margin") = 1.0,
+        py::arg("part_in") = py::none(), py::arg("part_rows") = 0);
+  m.def("bn_reduce_", &bn_reduce_, py::arg("x"), py::arg("shift"));
   m.def("bn_bwd_dual", &bn_bwd_dual, py::arg("dy"), py::arg("x"), py::arg("gamma"), py::arg("save_mean"),
         py::arg("save_invstd"), py::arg("mbits"), py::arg("dy2"), py::arg("xd"), py::arg("gamma_d"), py::arg("mean_d"),
         py::arg("invstd_d"), py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none(),
@@ -50,6 +68,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("out"), py::arg("accumulate") = false, py::arg("scale") = 1.0, py::arg("splits") = 0);
   m.def("gemm_fp8_", &gemm_fp8_, py::arg("A"), py::arg("B"), py::arg("a_scale"), py::arg("b_scale"), py::arg("out"),
         py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("aux") = py::none());
+  m.def("convn_", &convn_, py::arg("x"), py::arg("w2"), py::arg("out"), py::arg("R"), py::arg("S"), py::arg("stride"),
+        py::arg("pad"), py::arg("part") = py::none(), py::arg("shift") = py::none());
+  m.def("convn_stats_rows", &convn_stats_rows_, py::arg("M"));
   m.def("conv_fwd_", &conv_fwd_, py::arg("x"), py::arg("w2"), py::arg("out"), py::arg("R"), py::arg("S"),
         py::arg("stride"), py::arg("pad"));
   m.def("conv_wgrad_", &conv_wgrad_, py::arg("dy"), py::arg("x"), py::arg("out"), py::arg("R"), py::arg("S"),

@@ -40,7 +40,8 @@ std::vector<at::Tensor> bn_fwd(const at::Tensor& x_in, c10::optional<at::Tensor>
                                c10::optional<at::Tensor> counter, c10::optional<at::Tensor> ss_eval, bool mask_out,
                                c10::optional<at::Tensor> residual_ss, bool stats_only,
                                c10::optional<at::Tensor> q8_out, c10::optional<at::Tensor> q8_hist,
-                               c10::optional<at::Tensor> q8_sinv, double q8_margin) {
+                               c10::optional<at::Tensor> q8_sinv, double q8_margin, c10::optional<at::Tensor> part_in,
+                               int64_t part_rows) {
   TORCH_CHECK(x_in.is_cuda() && x_in.scalar_type() == at::kBFloat16, "psd bn: x must be a bf16 device tensor");
   const c10::DeviceGuard g(x_in.device());
   at::Tensor x = nhwc(x_in);
@@ -68,10 +69,19 @@ std::vector<at::Tensor> bn_fwd(const at::Tensor& x_in, c10::optional<at::Tensor>
   if (relu && mask_out && !stats_only) mbits = at::empty({M * C / 8}, x.options().dtype(at::kByte));
   at::Tensor mean = at::empty({C}, f32), invstd = at::empty({C}, f32);
   at::Tensor ss;
-  at::Tensor part;
+  at::Tensor part, fold;
+  const bool have_part = part_in.has_value() && part_in->defined();
   if (training) {
     ss = at::empty({2 * C}, f32);
-    part = at::empty({(int64_t)bn_reduce_blocks(M, (int)C) * 2 * C}, f32);
+    if (have_part) {  // statistics partials from the producing convolution's epilogue (kernels/convn.hip)
+      TORCH_CHECK(part_rows > 0 && part_in->scalar_type() == at::kFloat && part_in->is_contiguous() &&
+                      part_in->numel() >= part_rows * 2 * C && part_in->device() == x.device(),
+                  "psd bn: part_in must be fp32 [part_rows, 2, C] on x's device");
+      part = *part_in;
+      if (part_rows > kFoldRows) fold = at::empty({(int64_t)kFoldRows * 2 * C}, f32);
+    } else {
+      part = at::empty({(int64_t)bn_reduce_blocks(M, (int)C) * 2 * C}, f32);
+    }
   } else {
     TORCH_CHECK(ss_eval.has_value() && ss_eval->numel() == 2 * C, "psd bn: eval mode needs ss_eval [2C]");
     ss = ss_eval->contiguous();
@@ -89,6 +99,10 @@ std::vector<at::Tensor> bn_fwd(const at::Tensor& x_in, c10::optional<at::Tensor>
   a.save_invstd = invstd.data_ptr<float>();
   a.ss = ss.data_ptr<float>();
   a.part = part.defined() ? part.data_ptr<float>() : nullptr;
+  if (training && have_part) {
+    a.part_ready = (int32_t)part_rows;
+    a.fold_ws = fold.defined() ? fold.data_ptr<float>() : nullptr;
+  }
   a.counter = training ? opt_ptr<int64_t>(counter) : nullptr;
   a.M = M;
   a.C = (int32_t)C;
@@ -115,6 +129,20 @@ std::vector<at::Tensor> bn_fwd(const at::Tensor& x_in, c10::optional<at::Tensor>
   hipError_t e = launch_bn_fwd(a, stream_of(x));
   TORCH_CHECK(e == hipSuccess, "psd bn fwd: ", hipGetErrorString(e));
   return {y, mean, invstd, ss, mbits};
+}
+
+at::Tensor bn_reduce_(const at::Tensor& x_in, const at::Tensor& shift) {
+  TORCH_CHECK(x_in.is_cuda() && x_in.scalar_type() == at::kBFloat16, "psd bn_reduce: x must be a bf16 device tensor");
+  const c10::DeviceGuard g(x_in.device());
+  at::Tensor x = nhwc(x_in);
+  const int64_t C = channels(x), M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0 && shift.numel() == C && shift.scalar_type() == at::kFloat && shift.is_contiguous(),
+              "psd bn_reduce: C % 8 == 0 and an fp32 [C] shift");
+  at::Tensor part = at::empty({(int64_t)bn_reduce_blocks(M, (int)C), 2, C}, x.options().dtype(at::kFloat));
+  const hipError_t e = launch_bn_reduce(reinterpret_cast<const uint16_t*>(x.data_ptr()), M, (int)C,
+                                        shift.data_ptr<float>(), part.data_ptr<float>(), stream_of(x));
+  TORCH_CHECK(e == hipSuccess, "psd bn_reduce: ", hipGetErrorString(e));
+  return part;
 }
 
 std::vector<at::Tensor> bn_bwd(const at::Tensor& dy_in, const at::Tensor& x_in, c10::optional<at::Tensor> y_in,

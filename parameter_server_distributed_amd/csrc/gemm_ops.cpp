@@ -3,6 +3,7 @@
 #include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
 
+#include "kernels/launchers_convn.h"
 #include "kernels/launchers_gemm.h"
 
 namespace psd {
@@ -185,6 +186,66 @@ static bool conv_fwd_impl(const at::Tensor& x, const at::Tensor& w2, at::Tensor 
   hipError_t e = f8 ? launch_conv_fwd_fp8(a, stream_of(x)) : launch_conv_fwd(a, stream_of(x));
   if (e == hipErrorNotSupported) return false;
   TORCH_CHECK(e == hipSuccess, "psd conv_fwd: ", hipGetErrorString(e));
+  return true;
+}
+
+int64_t convn_stats_rows_(int64_t M) { return convn_stats_rows((int)M); }
+
+bool convn_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride, int64_t pad,
+            c10::optional<at::Tensor> part, c10::optional<at::Tensor> shift) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.scalar_type() == at::kBFloat16 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "psd convn: x must be a channels_last bf16 device tensor");
+  TORCH_CHECK(w2.is_cuda() && w2.dim() == 2 && w2.scalar_type() == at::kBFloat16 && w2.is_contiguous(),
+              "psd convn: w2 must be a contiguous bf16 [Cout, R*S*C] device tensor");
+  TORCH_CHECK(out.is_cuda() && out.dim() == 2 && out.stride(1) == 1 && out.scalar_type() == at::kBFloat16 &&
+                  (reinterpret_cast<uintptr_t>(out.data_ptr()) & 15) == 0,
+              "psd convn: out must be a bf16 [M, Cout] device tensor, 16-B aligned");
+  const int64_t Nb = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
+  const int64_t M = Nb * Ho * Wo, Cout = w2.size(0), K = R * S * C;
+  TORCH_CHECK(w2.size(1) == K, "psd convn: w2 must be [Cout, R*S*C]");
+  TORCH_CHECK(out.size(0) == M && out.size(1) == Cout, "psd convn: out must be [Nb*Ho*Wo, Cout]");
+  const bool stats = part.has_value() && part->defined();
+  if (stats) {
+    TORCH_CHECK(shift.has_value() && shift->defined() && shift->numel() == Cout && shift->scalar_type() == at::kFloat &&
+                    shift->is_contiguous() && shift->device() == x.device(),
+                "psd convn: statistics need an fp32 [Cout] shift on x's device");
+    TORCH_CHECK(part->scalar_type() == at::kFloat && part->is_contiguous() && part->device() == x.device() &&
+                    part->numel() >= (int64_t)convn_stats_rows((int)M) * 2 * Cout,
+                "psd convn: part must be fp32 [convn_stats_rows(M), 2, Cout]");
+  }
+  const int64_t xbytes = x.numel() * 2, wbytes = w2.numel() * 2;
+  if ((C & (C - 1)) != 0 || C < 64 || xbytes > 0xFFFFFF00ll || wbytes >= ((int64_t)1 << 32) ||
+      M >= ((int64_t)1 << 31) - 256 || convn_tile_n((int)Cout) == 0 || out.stride(0) % 8 != 0 || Ho <= 0 || Wo <= 0)
+    return false;
+  int logc = 0;
+  while ((1 << logc) < C) ++logc;
+  const c10::DeviceGuard g(x.device());
+  ConvnArgs a{};
+  a.x = x.data_ptr();
+  a.w = w2.data_ptr();
+  a.y = out.data_ptr();
+  a.part = stats ? part->data_ptr<float>() : nullptr;
+  a.shift = stats ? shift->data_ptr<float>() : nullptr;
+  a.xbytes = (uint32_t)xbytes;
+  a.wbytes = (uint32_t)wbytes;
+  a.M = (int)M;
+  a.N = (int)Cout;
+  a.K = (int)K;
+  a.H = (int)H;
+  a.W = (int)W;
+  a.logC = logc;
+  a.Ho = (int)Ho;
+  a.Wo = (int)Wo;
+  a.R = (int)R;
+  a.S = (int)S;
+  a.stride = (int)stride;
+  a.pad = (int)pad;
+  a.ldc = (int)out.stride(0);
+  const hipError_t e = launch_convn(a, c10::hip::getCurrentHIPStream(x.device().index()).stream());
+  if (e == hipErrorNotSupported) return false;
+  TORCH_CHECK(e == hipSuccess, "psd convn: ", hipGetErrorString(e));
   return true;
 }
 

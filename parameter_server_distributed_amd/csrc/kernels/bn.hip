@@ -164,6 +164,28 @@ __global__ __launch_bounds__(256) void bn_fwd_reduce_kernel(const uint16_t* __re
   block_partials(m, C, a, b, part);
 }
 
+// Fold many partial rows (a producer epilogue writes one per output tile: ~50k rows for a b1024
+// layer1 convolution) into F rows before the finalize, which would otherwise sum them with 8
+// blocks: out[f][c] = sum of the rows r = f (mod F). Block = 8 row groups x 32 column quads,
+// independent 16-byte loads, rows combined in LDS in a fixed order (deterministic).
+__global__ __launch_bounds__(256) void bn_part_fold_kernel(const float* __restrict__ in, int nblk, int C2,
+                                                           float* __restrict__ out, int F) {
+  const int cq = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int c = (blockIdx.y * 32 + cq) * 4;
+  const int f = blockIdx.x;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  if (c < C2)
+    for (int r = f + F * rg; r < nblk; r += F * 8) s += *reinterpret_cast<const f32x4*>(in + (int64_t)r * C2 + c);
+  __shared__ f32x4 red[8][32];
+  red[rg][cq] = s;
+  __syncthreads();
+  if (rg == 0 && c < C2) {
+#pragma unroll
+    for (int k = 1; k < 8; ++k) s += red[k][cq];
+    *reinterpret_cast<f32x4*>(out + (int64_t)f * C2 + c) = s;
+  }
+}
+
 // shift_k aliases running_mean (read, then updated by the same lane): no __restrict__ on either.
 __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const float* __restrict__ part, int nblk, int64_t M, int C,
                                                               const float* shift_k,
@@ -690,6 +712,14 @@ static void reduce_grid(int64_t M, int C, int& gx, int& gy) {
   gx = (int)(want < 1 ? 1 : (want > cap ? cap : want));
 }
 
+hipError_t launch_bn_reduce(const uint16_t* x, int64_t M, int C, const float* shift, float* part, hipStream_t st) {
+  if (M <= 0 || C % 8 != 0) return hipErrorInvalidValue;
+  int gx, gy;
+  reduce_grid(M, C, gx, gy);
+  hipLaunchKernelGGL(bn_fwd_reduce_kernel, dim3(gx, gy), dim3(256), 0, st, x, M, C, shift, part, bn_reverse());
+  return hipGetLastError();
+}
+
 int bn_reduce_blocks(int64_t M, int C) {
   int gx, gy;
   reduce_grid(M, C, gx, gy);
@@ -710,12 +740,20 @@ hipError_t launch_bn_fwd(const BnFwdArgs& a, hipStream_t st) {
   int gx, gy;
   reduce_grid(a.M, a.C, gx, gy);
   if (a.training) {
-    if (a.part_ready > 0)  // statistics already reduced by the producing kernel (stem conv epilogue)
+    const float* part = a.part;
+    if (a.part_ready > kFoldRows) {  // many producer partial rows (convolution epilogue): fold first
+      if (!a.fold_ws) return hipErrorInvalidValue;
+      hipLaunchKernelGGL(bn_part_fold_kernel, dim3(kFoldRows, (2 * a.C + 127) / 128), dim3(256), 0, st, a.part,
+                         a.part_ready, 2 * a.C, a.fold_ws, kFoldRows);
+      part = a.fold_ws;
+      gx = kFoldRows;
+    } else if (a.part_ready > 0) {  // statistics already reduced by the producing kernel (stem conv epilogue)
       gx = a.part_ready;
-    else
+    } else {
       hipLaunchKernelGGL(bn_fwd_reduce_kernel, dim3(gx, gy), dim3(256), 0, st, a.x, a.M, a.C, a.running_mean, a.part,
                          bn_reverse());
-    hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((a.C + kFinCh - 1) / kFinCh), dim3(256), 0, st, a.part, gx, a.M, a.C,
+    }
+    hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((a.C + kFinCh - 1) / kFinCh), dim3(256), 0, st, part, gx, a.M, a.C,
                        a.running_mean, a.gamma, a.beta, a.running_mean, a.running_var, a.momentum, a.eps, a.save_mean,
                        a.save_invstd, a.ss, a.counter);
     if (a.stats_only) return hipGetLastError();

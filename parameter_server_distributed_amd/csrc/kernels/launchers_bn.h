@@ -20,6 +20,7 @@ struct BnFwdArgs {
   float* part;            // [bn_reduce_blocks * 2C] workspace
   int64_t* counter;       // num_batches_tracked (optional)
   int32_t part_ready;     // > 0: part already holds this many rows of partial sums (producer epilogue)
+  float* fold_ws;         // [kFoldRows * 2C] workspace, needed when part_ready > kFoldRows
   const float* res_ss;    // optional [2C]: res is a raw BN input, added as res*res_ss[c] + res_ss[C+c]
   int32_t stats_only;     // training: statistics / running stats / scale-shift only, no apply pass
   uint8_t* q8;            // optional [M, C] e4m3 copy of y for an fp8 consumer (delayed scaling)
@@ -79,6 +80,10 @@ struct BnBwdArgs {
 bool bn_pool_supported(int H, int W, int C);
 int bn_pool_reduce_blocks(int N, int H, int W, int C);  // partial rows of the pool-fused backward
 int bn_reduce_blocks(int64_t M, int C);
+// rows the finalize sums directly; more producer partial rows are folded into this many first
+constexpr int kFoldRows = 512;
+// the statistics pass alone (shifted sums into part [bn_reduce_blocks * 2C]): autotune timing
+hipError_t launch_bn_reduce(const uint16_t* x, int64_t M, int C, const float* shift, float* part, hipStream_t st);
 hipError_t launch_bn_fwd(const BnFwdArgs& a, hipStream_t stream);
 hipError_t launch_bn_bwd(const BnBwdArgs& a, hipStream_t stream);
 

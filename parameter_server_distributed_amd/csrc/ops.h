@@ -23,7 +23,10 @@ std::vector<at::Tensor> bn_fwd(const at::Tensor& x, c10::optional<at::Tensor> ga
                                c10::optional<at::Tensor> counter, c10::optional<at::Tensor> ss_eval,
                                bool mask_out, c10::optional<at::Tensor> residual_ss, bool stats_only,
                                c10::optional<at::Tensor> q8_out, c10::optional<at::Tensor> q8_hist,
-                               c10::optional<at::Tensor> q8_sinv, double q8_margin);
+                               c10::optional<at::Tensor> q8_sinv, double q8_margin, c10::optional<at::Tensor> part_in,
+                               int64_t part_rows);
+// statistics pass of the BN forward alone: shifted sums of x [M, C] into a fresh [rows, 2, C] fp32
+at::Tensor bn_reduce_(const at::Tensor& x, const at::Tensor& shift);
 std::vector<at::Tensor> bn_bwd_dual(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& gamma,
                                     const at::Tensor& save_mean, const at::Tensor& save_invstd, const at::Tensor& mbits,
                                     c10::optional<at::Tensor> dy2, const at::Tensor& xd, const at::Tensor& gamma_d,
@@ -43,6 +46,12 @@ void gemm_splitk_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool 
                   bool accumulate, double scale, int64_t splits);
 void colsum_(const at::Tensor& x, at::Tensor out, bool accumulate);
 void gelu_bwd_colsum_(const at::Tensor& dy, const at::Tensor& pre, at::Tensor dx, at::Tensor out, bool accumulate);
+// narrow-output implicit-GEMM convolution (kernels/convn.hip): out [Nb*Ho*Wo, Cout] = conv(x, w2),
+// w2 [Cout, R*S*C]; with part/shift also the consumer BN's shifted statistics partials
+// [convn_stats_rows, 2, Cout]. False (nothing launched) outside the kernel's contract.
+bool convn_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride, int64_t pad,
+            c10::optional<at::Tensor> part, c10::optional<at::Tensor> shift);
+int64_t convn_stats_rows_(int64_t M);
 bool conv_fwd_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride,
                int64_t pad);
 bool conv_wgrad_(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64_t R, int64_t S, int64_t stride,

@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <chrono>
 
+#include "async_hyper.h"
 #include "checkpoint.h"
 #include "kernels/launchers.h"
 #include "ops.h"
@@ -107,7 +108,7 @@ void PSCore::fill_slot_locked(at::Tensor& slot, const std::vector<std::string>& 
   }
 }
 
-void PSCore::apply_locked(const std::vector<at::Tensor>& sources, double lr, double grad_scale) {
+void PSCore::apply_locked(const std::vector<at::Tensor>& sources, double lr, double grad_scale, const AsyncHyper* ah) {
   std::vector<at::Tensor> srcs = sources;
   if (srcs.size() > (size_t)kMaxSources) {  // pre-reduce in groups of 16 (exact fp32 sums)
     at::Tensor acc = at::empty_like(srcs[0]);
@@ -128,11 +129,13 @@ void PSCore::apply_locked(const std::vector<at::Tensor>& sources, double lr, dou
   hf[0] = (float)lr;
   hf[1] = (float)grad_scale;
   dyn_.copy_(host);
-  optim_advance_(dyn_, cfg_.beta1, cfg_.beta2);
+  // async pushes run with the per-push hyperparameters of async_hyper.h (one push = 1/W round)
+  const double mom = ah ? ah->momentum : cfg_.momentum, wd = ah ? ah->weight_decay : cfg_.weight_decay;
+  const double b1 = ah ? ah->beta1 : cfg_.beta1, b2 = ah ? ah->beta2 : cfg_.beta2;
+  optim_advance_(dyn_, b1, b2);
   fused_apply_(master_, srcs, s1_.defined() ? c10::optional<at::Tensor>(s1_) : c10::nullopt,
                s2_.defined() ? c10::optional<at::Tensor>(s2_) : c10::nullopt, c10::nullopt, dyn_, cfg_.opt_kind,
-               cfg_.momentum, cfg_.dampening, cfg_.nesterov, cfg_.weight_decay, cfg_.beta1, cfg_.beta2, cfg_.eps,
-               false);
+               mom, cfg_.dampening, cfg_.nesterov, wd, b1, b2, cfg_.eps, false);
   ctr_["applies"] += 1;
 }
 
@@ -202,9 +205,12 @@ PushResult PSCore::push(int32_t wid, int32_t iteration, const std::vector<std::s
     int64_t base = pulled_version >= 0 ? pulled_version
                                        : (pulled_version_.count(wid) ? pulled_version_[wid] : version_);
     const int64_t stale = std::max<int64_t>(0, version_ - base);
-    const double lr = cfg_.staleness_lr_scaling ? cfg_.lr / (1.0 + (double)stale) : cfg_.lr;
-    const double scale = cfg_.async_grad_scale > 0 ? cfg_.async_grad_scale : 1.0 / cfg_.total_workers;
-    apply_locked({slots_[s]}, lr, scale);
+    const AsyncHyper ah = async_hyper(cfg_.opt_kind, cfg_.total_workers, cfg_.momentum, cfg_.beta1, cfg_.beta2,
+                                      cfg_.weight_decay);
+    const double lr0 = cfg_.lr * ah.lr_factor;
+    const double lr = cfg_.staleness_lr_scaling ? lr0 / (1.0 + (double)stale) : lr0;
+    const double scale = cfg_.async_grad_scale > 0 ? cfg_.async_grad_scale : ah.grad_scale;
+    apply_locked({slots_[s]}, lr, scale, &ah);
     free_slots_.push_back(s);
     ++version_;
     hist_[std::min<int64_t>(stale, kHistBins - 1)] += 1;

@@ -27,6 +27,8 @@
 
 namespace psd {
 
+struct AsyncHyper;  // async_hyper.h
+
 struct PSConfig {
   int32_t total_workers = 1;
   int32_t async_mode = 0;        // 0 = sync barrier (reference), 1 = async apply-on-arrival
@@ -122,7 +124,8 @@ class PSCore {
   void alloc_state_locked();
   int32_t take_slot_locked();
   void fill_slot_locked(at::Tensor& slot, const std::vector<std::string>& names, const std::vector<at::Tensor>& grads);
-  void apply_locked(const std::vector<at::Tensor>& sources, double lr, double grad_scale);
+  void apply_locked(const std::vector<at::Tensor>& sources, double lr, double grad_scale,
+                    const AsyncHyper* ah = nullptr);
   void trim_locked();
   int32_t min_clock_locked() const;
 };

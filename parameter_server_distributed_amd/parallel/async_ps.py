@@ -16,9 +16,15 @@ Per step of a worker (``begin_step`` / grad hooks / ``finish_step``):
           single-producer ring in the shared control block
 
 The owner's native engine thread (``csrc/async_ps.cpp``) applies each message with the fused gfx950
-optimizer kernel (grad scale 1/W, so W pushes make one averaged step), writes the bf16 snapshot
+optimizer kernel, writes the bf16 snapshot
 into a free publish buffer and advances the shard version, the worker's clock and the staleness
 histogram (staleness = shard version at apply - version the gradient was computed on).
+
+Optimizer semantics: one round (every worker pushing once) is W applies. Each push runs with the
+per-push hyperparameters of ``csrc/async_hyper.h`` (SGD: grad x 1/W; momentum: beta^(1/W) and a
+rescaled lr; Adam/AdamW: beta1^(1/W), beta2^(1/W), lr/W), which keep the synchronous optimizer's
+per-round EMA horizons, displacement and bias-correction schedule, and are the synchronous ones at
+W = 1 (pinned against the sync trajectory by tests/test_async_ps.py).
 
 Layout: the parameters live in one flat working buffer (``.data`` views, reverse registration
 order, 64-element aligned) split into P contiguous shards; gradients alternate between two flat
@@ -71,7 +77,12 @@ class AsyncPS:
     def __init__(self, model: nn.Module, optim: OptimConfig, num_shards: int | None = None, staleness: int = 1,
                  bucket_mb: float = 16.0, device: torch.device | None = None, ps_ranks: list[int] | None = None,
                  worker_ranks: list[int] | None = None, param_dtype: torch.dtype = torch.bfloat16, nbuf: int = 4,
-                 timeout_s: float | None = None, overlap: bool = True, store=None, log: bool = False):
+                 timeout_s: float | None = None, overlap: bool = True, store=None, log: bool = False,
+                 semantics: str = "round"):
+        """``semantics``: "round" (default) runs each push with the per-push hyperparameters of
+        csrc/async_hyper.h (W pushes behave like one synchronous step); "push" is the naive rule,
+        every push a full optimizer step on grad / W with the synchronous hyperparameters (kept as
+        an A/B baseline: its momentum horizon is W x shorter and Adam takes W x the lr)."""
         self.model = model
         self.cfg = optim
         st, self.rank, self.world = _store_and_group()
@@ -143,6 +154,16 @@ class AsyncPS:
         self.grads = [torch.zeros(total, dtype=param_dtype, device=dev) for _ in range(2)]
         self.gb = 0
         f32 = dict(dtype=torch.float32, device=dev)
+        # per-push hyperparameters (module docstring)
+        if semantics not in ("round", "push"):
+            raise ValueError(f"semantics must be 'round' or 'push', got {semantics!r}")
+        self.semantics = semantics
+        if semantics == "round":
+            self.hyper = native().async_hyper(optim.code, self.W, optim.momentum, optim.beta1, optim.beta2,
+                                              optim.weight_decay)
+        else:
+            self.hyper = dict(lr_factor=1.0, grad_scale=1.0 / self.W, momentum=optim.momentum, beta1=optim.beta1,
+                              beta2=optim.beta2, weight_decay=optim.weight_decay)
         self.master, self.state1, self.state2, self.dyn = {}, {}, {}, {}
         for k in self.my_shards:
             self.master[k] = init.narrow(0, self.shard_off[k], self.shard_len[k]).clone()
@@ -150,7 +171,7 @@ class AsyncPS:
                 self.state1[k] = torch.zeros(self.shard_len[k], **f32)
             if optim.num_states >= 2:
                 self.state2[k] = torch.zeros(self.shard_len[k], **f32)
-            self.dyn[k] = OptimDyn(dev, lr=optim.lr, grad_scale=1.0 / self.W)
+            self.dyn[k] = OptimDyn(dev, lr=optim.lr * self.hyper["lr_factor"], grad_scale=self.hyper["grad_scale"])
         del init
 
         # grad sinks (fused BN / MFMA linear write their parameter gradients straight into the buffer)
@@ -222,9 +243,10 @@ class AsyncPS:
             err = f"rank {self.rank}: {e}"
         self._agree("attach", err)
         for k in self.my_shards:
+            h = self.hyper
             self.engine.set_shard_state(k, self.master[k], self.state1.get(k), self.state2.get(k), self.dyn[k].t,
-                                        optim.code, optim.momentum, optim.dampening, optim.nesterov,
-                                        optim.weight_decay, optim.beta1, optim.beta2, optim.eps)
+                                        optim.code, h["momentum"], optim.dampening, optim.nesterov,
+                                        h["weight_decay"], h["beta1"], h["beta2"], optim.eps)
             self.engine.publish_initial(k)
         if log:
             self.engine.enable_log(True)
@@ -493,8 +515,9 @@ class AsyncPS:
         return [tuple(x) for x in self.engine.apply_log()]
 
     def set_lr(self, lr: float):
+        """``lr``: the synchronous (per-round) learning rate; each push runs with its async share."""
         for d in self.dyn.values():
-            d.set(lr=lr)
+            d.set(lr=lr * self.hyper["lr_factor"])
 
     def num_params(self) -> int:
         return sum(k for (_, _, _, k) in self._layout)

@@ -77,6 +77,9 @@ def _replay_and_check(out_dir, world, stale, bf16=False):
     workers, owners = R[0]["workers"], R[0]["owners"]
     off, ln = R[0]["shard_off"], R[0]["shard_len"]
     W = len(workers)
+    from parameter_server_distributed_amd import native
+
+    h = native().async_hyper(1, W, CFG["momentum"], 0.9, 0.999, CFG["weight_decay"])
     recs = {R[r]["rank"]: {e["step"]: e for e in R[r]["rec"]} for r in range(world)}
     hist_total = [0] * 64
     for k, o in enumerate(owners):
@@ -88,10 +91,10 @@ def _replay_and_check(out_dir, world, stale, bf16=False):
             assert v == i + 1
             e = recs[w][t]
             assert st == i - e["pulled"][k], (k, w, t, st, i, e["pulled"][k])
-            g = e["grad"].narrow(0, off[k], ln[k]) * (1.0 / W)
-            g = g + CFG["weight_decay"] * p
-            buf = g.clone() if buf is None else CFG["momentum"] * buf + g
-            p = p - CFG["lr"] * buf
+            g = e["grad"].narrow(0, off[k], ln[k]) * h["grad_scale"]
+            g = g + h["weight_decay"] * p
+            buf = g.clone() if buf is None else h["momentum"] * buf + g
+            p = p - CFG["lr"] * h["lr_factor"] * buf
             snaps[v] = p.clone()
             hist_total[min(st, 63)] += 1
         assert len(log) == W * len(recs[workers[0]]), "every push applied exactly once"
@@ -167,6 +170,104 @@ def test_async_gpu_ipc_matches_replay(tmp_path, gpu, world, stale):
     _replay_and_check(str(tmp_path), world, stale, bf16=True)
     mem = torch.load(os.path.join(str(tmp_path), "r0.pt"), weights_only=False)["mem"]
     assert mem in ("uncached", "finegrained"), mem
+
+
+# ---------------------------------------------------------------------------------------------
+# optimizer semantics at W > 1: the async trajectory against the synchronous one
+
+
+SEM_STEPS = 30
+SEM_CFGS = {"momentum": dict(kind="momentum", lr=0.05, momentum=0.9),
+            "adamw": dict(kind="adamw", lr=2e-3, weight_decay=0.01)}
+
+
+def _sem_batches(W):
+    spec = models.build("mlp", torch.device("cpu"), torch.float32, hidden=64)
+    return [spec.make_batch(64, torch.device("cpu"), seed=100 + w) for w in range(W)]
+
+
+def _sem_loss(spec, batches):
+    with torch.no_grad():
+        return sum(float(spec.loss(spec.model(x), y)) for x, y in batches) / len(batches)
+
+
+def _sem_sync(kind):
+    """The synchronous reference: torch.optim on the average of the W workers' gradients."""
+    torch.manual_seed(0)
+    spec = models.build("mlp", torch.device("cpu"), torch.float32, hidden=64)
+    c = SEM_CFGS[kind]
+    if kind == "momentum":
+        opt = torch.optim.SGD(spec.model.parameters(), lr=c["lr"], momentum=c["momentum"])
+    else:
+        opt = torch.optim.AdamW(spec.model.parameters(), lr=c["lr"], weight_decay=c["weight_decay"])
+    batches = _sem_batches(4)
+    losses = []
+    for _ in range(SEM_STEPS):
+        opt.zero_grad()
+        sum(spec.loss(spec.model(x), y) for x, y in batches).div(len(batches)).backward()
+        opt.step()
+        losses.append(_sem_loss(spec, batches))
+    return losses
+
+
+def _sem_worker(rank, world, port, kind, semantics, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    spec = models.build("mlp", torch.device("cpu"), torch.float32, hidden=64)
+    ps = AsyncPS(spec.model, OptimConfig(**SEM_CFGS[kind]), num_shards=2, staleness=1, bucket_mb=0.0005,
+                 param_dtype=torch.float32, semantics=semantics)
+    batches = _sem_batches(world)
+    x, y = batches[rank]
+    for _ in range(SEM_STEPS):
+        ps.begin_step()
+        spec.loss(spec.model(x), y).backward()
+        ps.finish_step()
+    ps.drain()
+    ps.begin_step()  # pull the final version
+    if rank == 0:
+        with open(os.path.join(out_dir, "loss.txt"), "w") as f:
+            f.write(repr(_sem_loss(spec, batches)))
+    ps.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("kind", ["momentum", "adamw"])
+def test_async_w4_tracks_sync_trajectory(tmp_path, kind):
+    """W = 4 workers, SSP bound 1, apply-on-arrival: the final loss is within 10 % of the
+    synchronous S = 0 reference (torch.optim on the averaged gradient) after the same number of
+    rounds; the naive per-push rule (every push a full step, hyperparameters unchanged) is not."""
+    sync = _sem_sync(kind)
+    res = {}
+    for sem in ("round", "push"):
+        d = tmp_path / sem
+        d.mkdir()
+        mp.spawn(_sem_worker, args=(4, _port(), kind, sem, str(d)), nprocs=4, join=True)
+        res[sem] = float(open(d / "loss.txt").read())
+    start = _sem_loss_init()
+    dev = {s: abs(v - sync[-1]) / sync[-1] for s, v in res.items()}
+    assert sync[-1] < 0.8 * start, (start, sync[-1])  # the reference is actually training
+    assert dev["round"] < 0.10, (kind, sync[-1], res)
+    assert dev["push"] > 2 * dev["round"], (kind, sync[-1], res)
+
+
+def _sem_loss_init():
+    torch.manual_seed(0)
+    spec = models.build("mlp", torch.device("cpu"), torch.float32, hidden=64)
+    return _sem_loss(spec, _sem_batches(4))
+
+
+def test_async_hyper_reduces_to_sync_at_w1(C):
+    for kind in range(4):
+        h = C.async_hyper(kind, 1, 0.9, 0.9, 0.999, 1e-3)
+        assert h == dict(lr_factor=1.0, grad_scale=1.0, momentum=0.9, beta1=0.9, beta2=0.999, weight_decay=1e-3)
+    h = C.async_hyper(1, 8, 0.9, 0.9, 0.999, 1e-3)
+    assert abs(h["momentum"] ** 8 - 0.9) < 1e-12 and abs(h["grad_scale"] - 0.125) < 1e-12
+    assert abs(h["lr_factor"] - (1 - 0.9 ** 0.125) / 0.1) < 1e-12
+    h = C.async_hyper(3, 8, 0.9, 0.9, 0.999, 1e-2)
+    assert abs(h["beta2"] ** 8 - 0.999) < 1e-12 and h["lr_factor"] == 0.125 and h["grad_scale"] == 1.0
 
 
 def _selftest_worker(rank, world, port, out_dir):

@@ -1,0 +1,113 @@
+"""Narrow-output implicit-GEMM convolution (kernels/convn.hip) vs PyTorch fp32 ``F.conv2d``, and
+the BatchNorm statistics it reduces in its epilogue vs the fp32 reference statistics of the
+stored output.
+
+Operands are small integers (exact in bf16 and in the fp32 accumulator), so a wrong gathered pixel,
+a missed zero pad, a swapped (r, s) or a misplaced output column is a hard mismatch."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from parameter_server_distributed_amd import native
+
+pytestmark = pytest.mark.gpu
+
+CASES = [  # Nb, C, H, W, Cout, R, stride, pad
+    (4, 64, 14, 14, 64, 3, 1, 1),      # layer1 conv2 shape family (BN = 64)
+    (3, 128, 14, 14, 128, 3, 1, 1),    # layer2 conv2 (BN = 128), ragged M (588 rows)
+    (4, 128, 28, 28, 128, 3, 2, 1),    # strided 3x3
+    (2, 256, 15, 17, 64, 1, 1, 0),     # 1x1 256 -> 64, odd image, ragged M
+    (2, 64, 14, 14, 256, 1, 1, 0),     # 1x1 K = 64 -> 256 (layer1 conv3: one K-tile)
+    (2, 128, 7, 9, 512, 1, 1, 0),      # 1x1 -> 512: two 256-wide column tiles
+    (2, 256, 14, 14, 512, 1, 2, 0),    # strided 1x1 (downsample)
+    (1, 64, 5, 5, 64, 3, 1, 1),        # M = 25 < one tile
+]
+
+
+def _w2(w):
+    return w.permute(0, 2, 3, 1).reshape(w.shape[0], -1).contiguous()
+
+
+def _case(case, gpu, seed=7):
+    Nb, C, H, W, Cout, R, stride, pad = case
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randint(-2, 3, (Nb, C, H, W), generator=g).float()
+    w = torch.randint(-2, 3, (Cout, C, R, R), generator=g).float()
+    ref = F.conv2d(x, w, stride=stride, padding=pad)
+    xd = x.to(gpu, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    return x, w, ref, xd
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(map(str, c)))
+def test_convn_exact(gpu, case):
+    Nb, C, H, W, Cout, R, stride, pad = case
+    x, w, ref, xd = _case(case, gpu)
+    Ho, Wo = ref.shape[2], ref.shape[3]
+    out = torch.full((Nb * Ho * Wo, Cout), 7.0, device=gpu, dtype=torch.bfloat16)
+    assert native().convn_(xd, _w2(w.to(gpu, torch.bfloat16)), out, R, R, stride, pad)
+    want = ref.permute(0, 2, 3, 1).reshape(-1, Cout).bfloat16().float()
+    torch.testing.assert_close(out.float().cpu(), want, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("case", CASES[:5], ids=lambda c: "x".join(map(str, c)))
+def test_convn_stats_partials(gpu, case):
+    """Summed over the partial rows, the epilogue's shifted sums equal the fp32 sums of the stored
+    bf16 output (exact-integer data: every partial is an exact fp32 integer sum)."""
+    Nb, C, H, W, Cout, R, stride, pad = case
+    x, w, ref, xd = _case(case, gpu, seed=11)
+    M = ref.numel() // Cout
+    rows = native().convn_stats_rows(M)
+    part = torch.full((rows, 2, Cout), float("nan"), device=gpu)
+    shift = torch.randint(-3, 4, (Cout,)).float().to(gpu)
+    out = torch.empty(M, Cout, device=gpu, dtype=torch.bfloat16)
+    assert native().convn_(xd, _w2(w.to(gpu, torch.bfloat16)), out, R, R, stride, pad, part=part, shift=shift)
+    y = out.double().cpu()
+    d = y - shift.double().cpu()
+    got = part.double().cpu().sum(0)
+    assert torch.isfinite(got).all()
+    torch.testing.assert_close(got[0], d.sum(0), rtol=1e-6, atol=1e-3)
+    torch.testing.assert_close(got[1], (d * d).sum(0), rtol=1e-6, atol=1e-3)
+
+
+def test_convn_declines_unsupported(gpu):
+    x = torch.zeros(2, 96, 8, 8, device=gpu, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    out = torch.empty(2 * 64, 64, device=gpu, dtype=torch.bfloat16)
+    assert native().convn_(x, torch.zeros(64, 9 * 96, device=gpu, dtype=torch.bfloat16), out, 3, 3, 1, 1) is False
+    x = torch.zeros(2, 64, 8, 8, device=gpu, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    out = torch.empty(2 * 64, 96, device=gpu, dtype=torch.bfloat16)  # 96 output channels: no tile
+    assert native().convn_(x, torch.zeros(96, 9 * 64, device=gpu, dtype=torch.bfloat16), out, 3, 3, 1, 1) is False
+
+
+@pytest.mark.parametrize("relu", [False, True])
+def test_bn_fwd_from_conv_partials_matches_fp32(gpu, relu):
+    """BN forward fed with the convolution's statistics partials (fold + finalize, no reduce pass)
+    vs fp32 F.batch_norm on the same bf16 conv output: output, batch statistics, running stats."""
+    torch.manual_seed(5)
+    Nb, C, H, W, Cout = 8, 64, 28, 28, 64  # M = 6272 -> 98 partial rows
+    x = torch.randn(Nb, C, H, W, device=gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Cout, C, 3, 3, device=gpu) * 0.05).to(torch.bfloat16)
+    M = Nb * H * W
+    rm = torch.randn(Cout, device=gpu) * 0.1
+    rv = torch.rand(Cout, device=gpu) + 0.5
+    gamma = (torch.rand(Cout, device=gpu) + 0.5).to(torch.bfloat16)
+    beta = (torch.randn(Cout, device=gpu) * 0.1).to(torch.bfloat16)
+    rows = native().convn_stats_rows(M)
+    part = torch.empty(rows, 2, Cout, device=gpu)
+    out = torch.empty(M, Cout, device=gpu, dtype=torch.bfloat16)
+    assert native().convn_(x, _w2(w), out, 3, 3, 1, 1, part=part, shift=rm)
+    y4 = out.view(Nb, H, W, Cout).permute(0, 3, 1, 2)
+    rm1, rv1 = rm.clone(), rv.clone()
+    cnt = torch.zeros((), dtype=torch.int64, device=gpu)
+    yb, mean, invstd, _, _ = native().bn_fwd(y4, gamma, beta, rm1, rv1, None, relu, True, 0.1, 1e-5, cnt, None,
+                                             part_in=part, part_rows=rows)
+    rm2, rv2 = rm.clone(), rv.clone()
+    ref = F.batch_norm(y4.float(), rm2, rv2, gamma.float(), beta.float(), True, 0.1, 1e-5)
+    if relu:
+        ref = F.relu(ref)
+    yf = y4.float()
+    torch.testing.assert_close(mean, yf.mean((0, 2, 3)), rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(invstd, torch.rsqrt(yf.var((0, 2, 3), unbiased=False) + 1e-5), rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(rm1, rm2, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(rv1, rv2, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(yb.float(), ref, rtol=1e-2, atol=2e-2)
+    assert int(cnt) == 1
