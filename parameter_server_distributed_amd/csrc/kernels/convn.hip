@@ -92,7 +92,7 @@ struct Geo {
 }  // namespace
 
 template <int BN, int WNT, bool STATS>
-__global__ __launch_bounds__((Geo<BN, WNT>::NT)) void convn_kernel(ConvnArgs a) {
+__global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
   using G = Geo<BN, WNT>;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int tiles_m = gridDim.x;
@@ -118,13 +118,6 @@ __global__ __launch_bounds__((Geo<BN, WNT>::NT)) void convn_kernel(ConvnArgs a) 
       hw[i] = m < a.M ? (int)(((uint32_t)h0 << 16) | ((uint32_t)w0 & 0xffffu)) : (int)0x80000000u;
     }
   }
-  uint32_t bo[G::BPW];  // per-lane byte offset of this lane's weight chunk, K-tile 0
-#pragma unroll
-  for (int i = 0; i < G::BPW; ++i) {
-    const int row = (i * G::NW + wid) * 8 + (lane >> 3);
-    const int kc = (lane & 7) ^ ((row >> 1) & 7);
-    bo[i] = ((uint32_t)(n0 + row) * (uint32_t)a.K + kc * 8) * 2;
-  }
   const rsrc_t xr = make_rsrc(a.x, a.xbytes);
   const rsrc_t wrs = make_rsrc(a.w, a.wbytes);
   const int cmask = (1 << a.logC) - 1;
@@ -145,12 +138,17 @@ __global__ __launch_bounds__((Geo<BN, WNT>::NT)) void convn_kernel(ConvnArgs a) 
       __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(slot + piece * 1024), 16,
                                                off, 0, 0, 0);
     }
+    // (the weight offsets are recomputed per K-tile: a per-lane offset array captured by this lambda
+    // made hipcc's host pass silently drop the kernel's instantiation -- an undefined stub symbol)
 #pragma unroll
     for (int i = 0; i < G::BPW; ++i) {
       const int piece = i * G::NW + wid;
+      const int row = piece * 8 + (lane >> 3);
+      const int kc = (lane & 7) ^ ((row >> 1) & 7);
+      const uint32_t off = ((uint32_t)(n0 + row) * (uint32_t)a.K + (uint32_t)(k0 + kc * 8)) * 2u;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs,
                                                (__attribute__((address_space(3))) void*)(slot + G::AB + piece * 1024),
-                                               16, bo[i] + (uint32_t)k0 * 2u, 0, 0, 0);
+                                               16, off, 0, 0, 0);
     }
   };
 
