@@ -312,16 +312,37 @@ void AsyncEngine::set_shard_state(int shard, at::Tensor master, c10::optional<at
   st.hyper.eps = (float)eps;
 }
 
-void AsyncEngine::publish_initial(int shard) {
+void AsyncEngine::publish_initial(int shard, int64_t version, std::vector<int64_t> clocks) {
   ShardState& st = shards_[shard];
   TORCH_CHECK(st.master.defined(), "psd async: set_shard_state first");
+  TORCH_CHECK(!running_, "psd async: publish_initial while the engine runs");
+  TORCH_CHECK(version >= 0 && (clocks.empty() || clocks.size() == workers_.size()),
+              "psd async: publish_initial takes a version >= 0 and one clock per worker");
   st.publish[0].copy_(st.master);
   if (device_ >= 0) hip_ok(hipDeviceSynchronize(), "hipDeviceSynchronize");
   ShardCtl& s = ctl_->shard[shard];
-  s.buf_version[0].store(0);
+  s.buf_version[0].store(version);
   s.latest.store(0);
-  s.version.store(0);
-  st.enq = 0;
+  s.version.store(version);
+  for (size_t wi = 0; wi < clocks.size(); ++wi) s.clock[wi].store(clocks[wi]);
+  st.enq = version;
+  st.round.clear();
+}
+
+void AsyncEngine::set_round(int k) {
+  TORCH_CHECK(!running_, "psd async: set_round while the engine runs");
+  TORCH_CHECK(k >= 1 && k <= (int)workers_.size() && k <= kMaxSources, "psd async: round size must be in [1, min(W, ",
+              kMaxSources, ")], got ", k);
+  round_ = k;
+}
+
+int AsyncEngine::free_buf(int shard) const {
+  const ShardState& st = shards_[shard];
+  const ShardCtl& s = ctl_->shard[shard];
+  const int latest = s.latest.load();
+  for (int b = 0; b < nbuf_; ++b)
+    if (b != latest && !st.busy[b] && s.readers[b].load() == 0) return b;
+  return -1;
 }
 
 void AsyncEngine::start() {
@@ -389,43 +410,45 @@ bool AsyncEngine::poll_once() {
     s.buf_version[p.buf].store(v);
     s.latest.store(p.buf);
     s.version.store(v);
-    s.clock[p.wi].fetch_add(1);
+    for (const RoundItem& it : p.items) s.clock[it.wi].fetch_add(1);
     shards_[p.shard].busy[p.buf] = false;
     {
       std::lock_guard<std::mutex> g(hist_mu_);
-      hist_[std::min<int64_t>(std::max<int64_t>(p.staleness, 0), kBins - 1)] += 1;
+      for (const RoundItem& it : p.items) {
+        hist_[std::min<int64_t>(std::max<int64_t>(it.staleness, 0), kBins - 1)] += 1;
+        if (log_on_) log_.push_back({p.shard, workers_[it.wi], it.step, it.staleness, v});
+      }
     }
     n_applies_.fetch_add(1);
-    if (log_on_) {
-      std::lock_guard<std::mutex> g(hist_mu_);
-      log_.push_back({p.shard, workers_[p.wi], p.step, p.staleness, v});
-    }
     if (p.event) (void)hipEventDestroy(static_cast<hipEvent_t>(p.event));
     pending_.pop_front();
     progress = true;
   }
-  // 3. new pushes -> apply on arrival
+  // 3. new pushes -> the shard's current round (one message per worker per pass: arrival order,
+  //    no worker starved); a complete round is applied at once
   const int W = (int)workers_.size();
   for (int k : my_shards_) {
     ShardState& st = shards_[k];
-    ShardCtl& s = ctl_->shard[k];
     for (int wi = 0; wi < W; ++wi) {
       Mailbox& mb = ctl_->mb[k][wi];
       const int64_t t = mb.tail.load();
       if (t >= mb.head.load()) continue;
+      const bool completes = (int)st.round.size() + 1 >= round_;
       int buf = -1;
-      const int latest = s.latest.load();
-      for (int b = 0; b < nbuf_; ++b)
-        if (b != latest && !st.busy[b] && s.readers[b].load() == 0) {
-          buf = b;
-          break;
-        }
-      if (buf < 0) break;  // every snapshot is pinned or in flight: retry after completions
+      if (completes) {
+        buf = free_buf(k);
+        if (buf < 0) break;  // every snapshot is pinned or in flight: retry after completions
+      }
       const Msg m = mb.ring[t % kRing];
       mb.tail.store(t + 1);
-      const int slot = (int)(m.step % (S_ + 1));
-      at::Tensor g = st.inbox[(size_t)wi * (S_ + 1) + slot];
-      const int64_t stale = st.enq - m.pulled;
+      st.round.push_back(RoundItem{wi, (int)(m.step % (S_ + 1)), m.step, m.pulled, 0});
+      progress = true;
+      if (!completes) continue;
+      std::vector<at::Tensor> g;
+      for (RoundItem& it : st.round) {
+        it.staleness = st.enq - it.pulled;
+        g.push_back(st.inbox[(size_t)it.wi * (S_ + 1) + it.slot]);
+      }
       st.enq += 1;
       st.busy[buf] = true;
       hipEvent_t ev = nullptr;
@@ -438,19 +461,20 @@ bool AsyncEngine::poll_once() {
       } else {
         apply_into(st, g, buf);
       }
-      pending_.push_back(Pending{k, wi, buf, m.step, stale, ev});
-      progress = true;
+      pending_.push_back(Pending{k, buf, std::move(st.round), ev});
+      st.round.clear();
     }
   }
   return progress;
 }
 
-// One update: optimizer step counter, fused apply of the inbox slot onto the fp32 master, and the
-// new snapshot written into publish buffer `buf` (bf16: by the apply kernel itself).
-void AsyncEngine::apply_into(ShardState& st, const at::Tensor& g, int buf) {
+// One update: optimizer step counter, fused apply of the round's inbox slots (summed in registers,
+// scaled by the dyn grad_scale = 1/K) onto the fp32 master, and the new snapshot written into
+// publish buffer `buf` (bf16: by the apply kernel itself).
+void AsyncEngine::apply_into(ShardState& st, const std::vector<at::Tensor>& g, int buf) {
   optim_advance_(st.dyn, st.hyper.beta1, st.hyper.beta2);
   const bool bf16 = esz_ == 2;
-  fused_apply_(st.master, {g}, st.s1.defined() ? c10::optional<at::Tensor>(st.s1) : c10::nullopt,
+  fused_apply_(st.master, g, st.s1.defined() ? c10::optional<at::Tensor>(st.s1) : c10::nullopt,
                st.s2.defined() ? c10::optional<at::Tensor>(st.s2) : c10::nullopt,
                bf16 ? c10::optional<at::Tensor>(st.publish[buf]) : c10::nullopt, st.dyn, st.hyper.kind,
                st.hyper.momentum, st.hyper.dampening, st.hyper.nesterov, st.hyper.weight_decay, st.hyper.beta1,

@@ -15,11 +15,15 @@
 //   * push: a worker DMA-copies its gradient slice straight into its inbox slot on the owner's GPU
 //     (hipMemcpyAsync over the direct xGMI link to that peer), then posts a message to a
 //     single-producer ring in a shared-memory control block once the copy has completed.
-//   * apply: the owner's engine thread (C++, no GIL) polls the rings and, per message, launches
-//     the fused gfx950 optimizer kernel on its PS stream: inbox slot -> fp32 master / state ->
-//     bf16 written into a free publish buffer. When the kernel completes the buffer becomes the
-//     shard's latest snapshot, the shard version and the worker's clock advance, and the staleness
-//     (updates applied since the snapshot the gradient was computed on) is recorded exactly.
+//   * apply: the owner's engine thread (C++, no GIL) polls the rings and gathers the arriving pushes
+//     into rounds of K (any workers, in arrival order; set_round). A complete round launches the
+//     fused gfx950 optimizer kernel on its PS stream: the K inbox slots summed in registers, scaled
+//     by 1/K -> fp32 master / state -> bf16 written into a free publish buffer. When the kernel
+//     completes the buffer becomes the shard's latest snapshot, the shard version advances by one,
+//     the clock of every worker in the round advances, and each push's staleness (versions applied
+//     since the snapshot its gradient was computed on) is recorded exactly. K = W is K-batch-async
+//     SGD ("round" semantics: at SSP bound 0 the rounds are exactly the synchronous steps); K = 1
+//     applies every push on arrival ("push" semantics).
 //   * pull: a worker waits until every worker's clock at every shard is >= step - S (SSP), pins
 //     the latest publish buffer (reader count), DMA-copies it into its working weights and
 //     unpins when the copy completes.
@@ -60,7 +64,10 @@ class AsyncEngine {
   void set_shard_state(int shard, at::Tensor master, c10::optional<at::Tensor> state1, c10::optional<at::Tensor> state2,
                        at::Tensor dyn, int64_t kind, double momentum, double dampening, bool nesterov,
                        double weight_decay, double beta1, double beta2, double eps);
-  void publish_initial(int shard);  // bf16(master) -> publish buffer 0, version 0 (blocking)
+  // bf16(master) -> publish buffer 0 as the shard's snapshot `version` (blocking); with `clocks`
+  // (one per worker) the SSP clocks are restored too (checkpoint resume)
+  void publish_initial(int shard, int64_t version = 0, std::vector<int64_t> clocks = {});
+  void set_round(int k);            // pushes per optimizer step (1..min(W, 16)); before start()
   void start();
   void stop();
   // teardown in two collective phases (barrier between): unmap the peers' memory, then free our
@@ -92,9 +99,13 @@ class AsyncEngine {
   std::vector<std::vector<int64_t>> apply_log() const;
 
  private:
+  struct RoundItem {
+    int wi, slot;
+    int64_t step, pulled, staleness;
+  };
   struct Pending {
-    int shard, wi, buf;
-    int64_t step, staleness;
+    int shard, buf;
+    std::vector<RoundItem> items;
     void* event;  // hipEvent_t (GPU)
   };
   struct Action {
@@ -108,6 +119,7 @@ class AsyncEngine {
     std::vector<at::Tensor> publish;  // [nbuf] bf16 views
     std::vector<bool> busy;           // publish buffer is the target of an enqueued apply
     int64_t enq = 0;                  // applies enqueued (the version the next apply starts from)
+    std::vector<RoundItem> round;     // pushes taken from the mailboxes, not yet applied
   };
 
   int64_t slot_elems(int shard) const { return shard_len_[shard]; }
@@ -115,7 +127,8 @@ class AsyncEngine {
   int64_t shard_base(int rank, int shard) const;  // byte offset of shard's region in rank's allocation
   char* inbox_ptr(int shard, int wi, int slot) const;
   char* publish_ptr(int shard, int buf) const;
-  void apply_into(ShardState& st, const at::Tensor& g, int buf);
+  void apply_into(ShardState& st, const std::vector<at::Tensor>& g, int buf);
+  int free_buf(int shard) const;
   static bool done(void* event);
   void run();
   bool poll_once();
@@ -127,6 +140,7 @@ class AsyncEngine {
   int worker_index(int rank) const;
 
   int rank_, world_, S_, nbuf_, device_;
+  int round_ = 1;
   double timeout_s_;
   int esz_;
   std::vector<int> owners_, workers_, my_shards_;

@@ -69,8 +69,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_fp8_", &gemm_fp8_, py::arg("A"), py::arg("B"), py::arg("a_scale"), py::arg("b_scale"), py::arg("out"),
         py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("aux") = py::none());
   m.def("convn_", &convn_, py::arg("x"), py::arg("w2"), py::arg("out"), py::arg("R"), py::arg("S"), py::arg("stride"),
-        py::arg("pad"), py::arg("part") = py::none(), py::arg("shift") = py::none());
+        py::arg("pad"), py::arg("part") = py::none(), py::arg("shift") = py::none(), py::arg("variant") = -1);
   m.def("convn_stats_rows", &convn_stats_rows_, py::arg("M"));
+  m.def("convn_variants", &convn_variants_, py::arg("N"));
   m.def("conv_fwd_", &conv_fwd_, py::arg("x"), py::arg("w2"), py::arg("out"), py::arg("R"), py::arg("S"),
         py::arg("stride"), py::arg("pad"));
   m.def("conv_wgrad_", &conv_wgrad_, py::arg("dy"), py::arg("x"), py::arg("out"), py::arg("R"), py::arg("S"),
@@ -236,7 +237,9 @@ PYBIND11_MODULE(_C, m) {
       .def("local_desc", [](const AsyncEngine& e) { return py::bytes(e.local_desc()); })
       .def("attach_peer", [](AsyncEngine& e, int r, py::bytes d) { e.attach_peer(r, std::string(d)); })
       .def("set_shard_state", &AsyncEngine::set_shard_state)
-      .def("publish_initial", &AsyncEngine::publish_initial)
+      .def("publish_initial", &AsyncEngine::publish_initial, py::arg("shard"), py::arg("version") = 0,
+           py::arg("clocks") = std::vector<int64_t>{})
+      .def("set_round", &AsyncEngine::set_round)
       .def("start", &AsyncEngine::start)
       .def("stop", &AsyncEngine::stop, py::call_guard<py::gil_scoped_release>())
       .def("close_peers", &AsyncEngine::close_peers)

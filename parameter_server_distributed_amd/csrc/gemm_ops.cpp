@@ -190,9 +190,10 @@ static bool conv_fwd_impl(const at::Tensor& x, const at::Tensor& w2, at::Tensor 
 }
 
 int64_t convn_stats_rows_(int64_t M) { return convn_stats_rows((int)M); }
+int64_t convn_variants_(int64_t N) { return convn_variants((int)N); }
 
-bool convn_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride, int64_t pad,
-            c10::optional<at::Tensor> part, c10::optional<at::Tensor> shift) {
+int64_t convn_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride,
+               int64_t pad, c10::optional<at::Tensor> part, c10::optional<at::Tensor> shift, int64_t variant) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.scalar_type() == at::kBFloat16 &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast),
               "psd convn: x must be a channels_last bf16 device tensor");
@@ -217,8 +218,9 @@ bool convn_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_t R
   }
   const int64_t xbytes = x.numel() * 2, wbytes = w2.numel() * 2;
   if ((C & (C - 1)) != 0 || C < 64 || xbytes > 0xFFFFFF00ll || wbytes >= ((int64_t)1 << 32) ||
-      M >= ((int64_t)1 << 31) - 256 || convn_tile_n((int)Cout) == 0 || out.stride(0) % 8 != 0 || Ho <= 0 || Wo <= 0)
-    return false;
+      M >= ((int64_t)1 << 31) - 256 || convn_tile_n((int)Cout) == 0 || out.stride(0) % 8 != 0 || Ho <= 0 || Wo <= 0 ||
+      variant >= convn_variants((int)Cout))
+    return 0;
   int logc = 0;
   while ((1 << logc) < C) ++logc;
   const c10::DeviceGuard g(x.device());
@@ -243,10 +245,11 @@ bool convn_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_t R
   a.stride = (int)stride;
   a.pad = (int)pad;
   a.ldc = (int)out.stride(0);
+  a.variant = (int)variant;
   const hipError_t e = launch_convn(a, c10::hip::getCurrentHIPStream(x.device().index()).stream());
-  if (e == hipErrorNotSupported) return false;
+  if (e == hipErrorNotSupported) return 0;
   TORCH_CHECK(e == hipSuccess, "psd convn: ", hipGetErrorString(e));
-  return true;
+  return stats ? convn_part_rows((int)M, (int)Cout, (int)variant) : 1;
 }
 
 bool conv_fwd_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride,

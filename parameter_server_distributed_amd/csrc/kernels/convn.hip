@@ -11,24 +11,30 @@
 // needs a separate BN statistics pass over the whole activation (bn_fwd_reduce: 4 ms of the step).
 //
 // Shape of the kernel (one output tile per workgroup, many workgroups per launch):
-//   * tile = 128 output pixels x BN output channels (BN = 64, 128 or 256 = the whole layer
-//     width for the narrow layers: the gathered input rows are staged once per pixel tile);
-//   * 2 x (BN / WNT) waves, each owning 64 x WNT of C on v_mfma_f32_16x16x32_bf16;
+//   * tile = BM (128 / 256) output pixels x BN output channels (BN = 64, 128 or 256 = the whole
+//     layer width for the narrow layers: the gathered input rows are staged once per pixel tile);
+//   * (BM / 64) x (BN / WNT) waves, each owning 64 pixels x WNT channels of C on
+//     v_mfma_f32_16x16x32_bf16;
 //   * K-tile = 64 channels of one (r, s) (C % 64 == 0); A rows gathered straight into LDS by
 //     buffer_load ... lds (16 B per lane, 8 channels of one shifted input pixel; pixels outside the
 //     image fall outside the buffer range and load zeros = the padding), B = the weight rows;
 //     K-major [rows][64] images, 16-B chunks XOR-swizzled by (row >> 1) & 7 on the SOURCE address
 //     (the LDS-DMA image is lane-linear), read with ds_read_b128;
-//   * 3-slot LDS ring, two K-tiles in flight, one raw s_barrier per K-tile: iteration t waits for
-//     its own DMA of tile t with a counted vmcnt (tile t+1 stays in flight), the barrier publishes
-//     tile t and retires every wave's reads of tile t-1, whose slot then receives tile t+2;
+//   * NSLOT-deep LDS ring, NSLOT-1 K-tiles in flight, one raw s_barrier per K-tile: iteration t
+//     waits for its own DMA of tile t with a counted vmcnt (the later tiles stay in flight), the
+//     barrier publishes tile t and retires every wave's reads of tile t-1, whose slot then
+//     receives tile t+NSLOT-1 (the ring is sized to min(NSLOT, K-tiles) at launch: a one-K-tile
+//     1x1 convolution keeps several workgroups per CU);
 //   * XCD-aware tile order (consecutive pixel tiles -- which share input rows through the 3x3
 //     halo -- land on one XCD's L2);
-//   * epilogue: bf16 C through LDS to 16-byte row stores; with STATS, per output channel the shifted
-//     sums sum(y - k) and sum((y - k)^2) over the tile's valid rows (y rounded to bf16 first: the
-//     statistics of the tensor that is stored), one partial row per (pixel tile, wave row) in the
-//     layout of bn_fwd_reduce_kernel (bn.hip), so the BN forward skips its reduce pass and goes
-//     straight to the finalize.
+//   * epilogue per wave, no block barrier: each 16-row block of the wave's C is transposed in
+//     registers (quad_t4: 4 consecutive columns per lane), packed to bf16 and staged through the
+//     wave's own 2 KiB of LDS, then stored as 16-byte lanes covering whole row segments; with
+//     STATS, per output channel the shifted sums sum(y - k) and sum((y - k)^2) over the wave's
+//     valid rows (y rounded to bf16 first: the statistics of the tensor that is stored), one
+//     partial row per 64-pixel wave row in the layout of bn_fwd_reduce_kernel (bn.hip), so the BN
+//     forward skips its reduce pass and goes straight to the finalize (kernel-start loads of the
+//     shift: a load issued in the epilogue of a one-K-tile convolution is pure exposed latency).
 // The same kernel runs a stride-1 bwd-data (conv of dY with the flipped, transposed weights) and
 // a 1x1 bwd-data (dY . W as a 1x1 conv of dY with W^T).
 #include "common.h"
@@ -71,36 +77,68 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
 }
 
-template <int BN, int WNT>
+// 4x4 transpose inside a lane quad: in v[r] = C[row r][col L]; out w[c] = C[row L][col c]
+template <int CTRL>
+__device__ __forceinline__ float dpp_q(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ void quad_t4(const f32x4 v, int L, float (&w)[4]) {
+  const bool o1 = L & 1, o2 = (L >> 1) & 1;
+  const float r0 = dpp_q<0xB1>(o1 ? v[0] : v[1]);  // quad_perm [1,0,3,2]: partner L^1
+  const float r1 = dpp_q<0xB1>(o1 ? v[2] : v[3]);
+  const float a0 = o1 ? r0 : v[0], a1 = o1 ? v[1] : r0;
+  const float b0 = o1 ? r1 : v[2], b1 = o1 ? v[3] : r1;
+  const float q0 = dpp_q<0x4E>(o2 ? a0 : b0);  // quad_perm [2,3,0,1]: partner L^2
+  const float q1 = dpp_q<0x4E>(o2 ? a1 : b1);
+  w[0] = o2 ? q0 : a0;
+  w[1] = o2 ? q1 : a1;
+  w[2] = o2 ? b0 : q0;
+  w[3] = o2 ? b1 : q1;
+}
+
+template <int BM, int BN, int WNT, int NSLOT>
 struct Geo {
+  static constexpr int WM = BM / 64;         // wave rows (64 output pixels each)
   static constexpr int NWC = BN / WNT;       // wave columns
-  static constexpr int NW = 2 * NWC;         // waves (2 wave rows of 64 pixels)
+  static constexpr int NW = WM * NWC;        // waves
   static constexpr int NT = 64 * NW;
   static constexpr int JN = WNT / 16;        // 16-column MFMA blocks per wave
-  static constexpr int APW = 16 / NW;        // A DMA pieces (1 KiB = 8 rows) per wave per K-tile
+  static constexpr int APW = (BM / 8) / NW;  // A DMA pieces (1 KiB = 8 rows) per wave per K-tile
   static constexpr int BPW = (BN / 8) / NW;  // B DMA pieces per wave per K-tile
   static constexpr int DPS = APW + BPW;      // DMA per wave per K-tile (the counted vmcnt)
-  static constexpr int AB = kBM * 128;       // A bytes per K-tile
+  static constexpr int AB = BM * 128;        // A bytes per K-tile
   static constexpr int SLOT = AB + BN * 128;
-  static constexpr int LDC = BN + 8;         // epilogue staging row (bf16 elements, +16 B)
-  static constexpr int RING = 3 * SLOT;
-  static constexpr int LDS = RING > kBM * LDC * 2 ? RING : kBM * LDC * 2;
-  static_assert(16 % NW == 0 && (BN / 8) % NW == 0, "DMA pieces must divide over the waves");
-  static_assert(LDS <= 160 * 1024, "LDS");
+  static constexpr int STG = 2048;           // per-wave epilogue staging (16 rows x <= 128 B)
+  static constexpr int LDS_MAX = NSLOT * SLOT + NW * STG;
+  static_assert((BM / 8) % NW == 0 && (BN / 8) % NW == 0 && APW >= 1 && BPW >= 1, "DMA pieces per wave");
+  static_assert(DPS * (NSLOT - 2) < 64, "vmcnt is 6 bits");
+  static_assert(LDS_MAX <= 160 * 1024, "LDS");
+  static_assert(WNT == 32 || WNT == 64, "wave tile width");
 };
 
 }  // namespace
 
-template <int BN, int WNT, bool STATS>
+template <int BM, int BN, int WNT, int NSLOT, bool STATS>
 __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
-  using G = Geo<BN, WNT>;
+  using G = Geo<BM, BN, WNT, NSLOT>;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int tiles_m = gridDim.x;
   const int tm = xcd_remap(blockIdx.x, tiles_m);
-  const int m0 = tm * kBM, n0 = blockIdx.y * BN;
+  const int m0 = tm * BM, n0 = blockIdx.y * BN;
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wid / G::NWC, wc = wid % G::NWC;
+  const int cl = lane & 15, rq = (lane >> 4) * 4;
+
+  // statistics shift of this lane's columns, loaded before any DMA is issued (its latency hides
+  // behind the whole K loop)
+  float kshift[G::JN];
+#pragma unroll
+  for (int j = 0; j < G::JN; ++j) kshift[j] = 0.f;
+  if constexpr (STATS) {
+#pragma unroll
+    for (int j = 0; j < G::JN; ++j) kshift[j] = a.shift[n0 + wc * WNT + j * 16 + cl];
+  }
 
   // this lane's A rows (one per DMA piece): window origin p0 = top-left input pixel index,
   // hw = (h0 << 16) | (w0 & 0xffff); rows past M get h0 = -32768 (never in the image)
@@ -121,9 +159,10 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
   const rsrc_t xr = make_rsrc(a.x, a.xbytes);
   const rsrc_t wrs = make_rsrc(a.w, a.wbytes);
   const int cmask = (1 << a.logC) - 1;
+  const int nslot = a.nslot;  // ring depth of this launch: min(NSLOT, K-tiles)
 
   auto stage = [&](int t) {
-    uint8_t* slot = smem + (t % 3) * G::SLOT;
+    uint8_t* slot = smem + (t % nslot) * G::SLOT;
     const int k0 = t * kBK;
     const int rs = k0 >> a.logC, ci0 = k0 & cmask;
     const int r = rs / a.S, s = rs - r * a.S;
@@ -159,15 +198,23 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
     for (int j = 0; j < G::JN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nt = a.K / kBK;
-  stage(0);
-  if (nt > 1) stage(1);
+  const int D = nslot - 1 > 0 ? nslot - 1 : 1;  // K-tiles issued ahead
+  for (int p = 0; p < D && p < nt; ++p) stage(p);
   for (int t = 0; t < nt; ++t) {
-    if (t + 1 < nt) wait_vm<G::DPS>();  // K-tile t landed (this wave's DMA), t+1 in flight
-    else wait_vm<0>();
+    // K-tile t landed (this wave's DMA): leave the (up to D-1) later K-tiles in flight
+    const int ahead = min(nt - 1 - t, D - 1);
+    if constexpr (NSLOT >= 4) {
+      if (ahead >= 2) wait_vm<2 * G::DPS>();
+      else if (ahead == 1) wait_vm<G::DPS>();
+      else wait_vm<0>();
+    } else {
+      if (ahead >= 1) wait_vm<G::DPS>();
+      else wait_vm<0>();
+    }
     __builtin_amdgcn_s_barrier();  // every wave: tile t published, tile t-1 no longer read
     __builtin_amdgcn_sched_barrier(0);
-    if (t + 2 < nt) stage(t + 2);
-    const uint8_t* As = smem + (t % 3) * G::SLOT;
+    if (t + D < nt) stage(t + D);
+    const uint8_t* As = smem + (t % nslot) * G::SLOT;
     const uint8_t* Bs = As + G::AB;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -184,79 +231,88 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
     __builtin_amdgcn_sched_barrier(0);
   }
 
-  // ---- epilogue: C layout col = lane & 15, row = 4 * (lane >> 4) + r
-  __syncthreads();  // the ring is free (every DMA retired by the last vmcnt(0))
-  uint16_t* cs = reinterpret_cast<uint16_t*>(smem);
-  const int cl = lane & 15, rq = (lane >> 4) * 4;
+  // ---- epilogue (per wave, no barrier: the staging slot is this wave's own): C layout of a
+  // 16x16 block col = lane & 15, row = 4 * (lane >> 4) + r
+  if constexpr (STATS) {
 #pragma unroll
-  for (int j = 0; j < G::JN; ++j) {
-    const int col = wc * WNT + j * 16 + cl;
-    float s1 = 0.f, s2 = 0.f;
-    float k = 0.f;
-    if constexpr (STATS) k = a.shift[n0 + col];
+    for (int j = 0; j < G::JN; ++j) {
+      float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wr * 64 + i * 16 + rq + r;
-        const uint16_t hv = f32_to_bf16(acc[i][j][r]);
-        cs[row * G::LDC + col] = hv;
-        if constexpr (STATS) {
-          if (m0 + row < a.M) {
-            const float d = bf16_to_f32(hv) - k;
-            s1 += d;
-            s2 = fmaf(d, d, s2);
-          }
+        for (int r = 0; r < 4; ++r) {
+          const float d = bf16_to_f32(f32_to_bf16(acc[i][j][r])) - kshift[j];
+          const bool ok = m0 + wr * 64 + i * 16 + rq + r < a.M;
+          s1 += ok ? d : 0.f;
+          s2 = ok ? fmaf(d, d, s2) : s2;
         }
-      }
-    if constexpr (STATS) {
       s1 += __shfl_xor(s1, 16);
       s2 += __shfl_xor(s2, 16);
       s1 += __shfl_xor(s1, 32);
       s2 += __shfl_xor(s2, 32);
       if (lane < 16) {
-        float* pr = a.part + ((int64_t)tm * 2 + wr) * 2 * a.N;
-        pr[n0 + col] = s1;
-        pr[a.N + n0 + col] = s2;
+        float* pr = a.part + ((int64_t)tm * G::WM + wr) * 2 * a.N;
+        const int col = n0 + wc * WNT + j * 16 + cl;
+        pr[col] = s1;
+        pr[a.N + col] = s2;
       }
     }
   }
-  __syncthreads();
-  constexpr int CPR = BN / 8;  // 16-byte chunks per tile row
+  uint8_t* stg = smem + a.nslot * G::SLOT + wid * G::STG;
+  const int L = cl & 3;
+  constexpr int RB = WNT * 2;       // staged row bytes (one 16-row block)
+  constexpr int CPR = RB / 16;      // 16-byte chunks per staged row
+  constexpr int PASSES = 16 * CPR / 64;
   uint16_t* y = reinterpret_cast<uint16_t*>(a.y);
-#pragma unroll 4
-  for (int c = threadIdx.x; c < kBM * CPR; c += G::NT) {
-    const int row = c / CPR, cc = (c % CPR) * 8;
-    const int m = m0 + row;
-    if (m < a.M)
-      *reinterpret_cast<u32x4*>(y + (int64_t)m * a.ldc + n0 + cc) = *reinterpret_cast<const u32x4*>(cs + row * G::LDC + cc);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = rq + L;  // this lane's row within the 16-row block after quad_t4
+#pragma unroll
+    for (int j = 0; j < G::JN; ++j) {
+      float w[4];
+      quad_t4(acc[i][j], L, w);
+      const int c8 = (j * 16 + (cl & ~3)) >> 2;  // 8-byte column group within the staged row
+      const int off = r * RB + ((c8 ^ ((r & 7) << 1)) & (RB / 8 - 1)) * 8;
+      const uint32_t lo = pack_bf16x2_rne(w[0], w[1]), hi = pack_bf16x2_rne(w[2], w[3]);
+      *reinterpret_cast<uint64_t*>(stg + off) = (uint64_t)lo | ((uint64_t)hi << 32);
+    }
+    // one wave's LDS ops complete in order: the reads below see the writes above
+#pragma unroll
+    for (int ps = 0; ps < PASSES; ++ps) {
+      const int c = ps * 64 + lane;
+      const int rr = c / CPR, c16 = c % CPR;
+      const int off = rr * RB + (((2 * c16) ^ ((rr & 7) << 1)) & (RB / 8 - 1)) * 8;
+      const u32x4 v = *reinterpret_cast<const u32x4*>(stg + off);
+      const int m = m0 + wr * 64 + i * 16 + rr;
+      if (m < a.M) *reinterpret_cast<u32x4*>(y + (int64_t)m * a.ldc + n0 + wc * WNT + c16 * 8) = v;
+    }
   }
 }
 
 // ------------------------------------------------------------------ host side
-namespace {
-
-template <int BN, int WNT, bool STATS>
-hipError_t launch_t(const ConvnArgs& a, hipStream_t st) {
-  using G = Geo<BN, WNT>;
+template <int BM, int BN, int WNT, int NSLOT, bool STATS>
+static hipError_t convn_launch_t(const ConvnArgs& a0, hipStream_t st) {
+  using G = Geo<BM, BN, WNT, NSLOT>;
   static bool attr = false;
   if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)convn_kernel<BN, WNT, STATS>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
+    const hipError_t e = hipFuncSetAttribute((const void*)convn_kernel<BM, BN, WNT, NSLOT, STATS>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_MAX);
     if (e != hipSuccess) return e;
     attr = true;
   }
-  const int tiles_m = (a.M + kBM - 1) / kBM;
-  hipLaunchKernelGGL((convn_kernel<BN, WNT, STATS>), dim3(tiles_m, a.N / BN), dim3(G::NT), G::LDS, st, a);
+  ConvnArgs a = a0;
+  const int nt = a.K / kBK;
+  a.nslot = nt < NSLOT ? (nt < 2 ? 1 : nt) : NSLOT;
+  const int lds = a.nslot * G::SLOT + G::NW * G::STG;
+  const int tiles_m = (a.M + BM - 1) / BM;
+  hipLaunchKernelGGL((convn_kernel<BM, BN, WNT, NSLOT, STATS>), dim3(tiles_m, a.N / BN), dim3(G::NT), lds, st, a);
   return hipGetLastError();
 }
 
-template <int BN, int WNT>
-hipError_t launch_s(const ConvnArgs& a, hipStream_t st) {
-  return a.part ? launch_t<BN, WNT, true>(a, st) : launch_t<BN, WNT, false>(a, st);
+template <int BM, int BN, int WNT, int NSLOT>
+static hipError_t convn_launch_s(const ConvnArgs& a, hipStream_t st) {
+  return a.part ? convn_launch_t<BM, BN, WNT, NSLOT, true>(a, st) : convn_launch_t<BM, BN, WNT, NSLOT, false>(a, st);
 }
-
-}  // namespace
 
 int convn_tile_n(int N) {
   if (N == 64) return 64;
@@ -265,7 +321,34 @@ int convn_tile_n(int N) {
   return 0;
 }
 
-int convn_stats_rows(int M) { return 2 * ((M + kBM - 1) / kBM); }
+// variants (tile geometry) per output width; a.variant < 0 picks the default
+static int convn_variant_count(int bn) { return bn == 256 ? 2 : 4; }
+
+int convn_variants(int N) {
+  const int bn = convn_tile_n(N);
+  return bn ? convn_variant_count(bn) : 0;
+}
+
+static int default_variant(const ConvnArgs& a, int bn) {
+  (void)a;
+  (void)bn;
+  return 0;
+}
+
+static int stats_bm(int bn, int v) {
+  if (bn == 64) return (v == 2 || v == 3) ? 256 : 128;
+  if (bn == 128) return (v == 2 || v == 3) ? 256 : 128;
+  return 128;
+}
+
+int convn_stats_rows(int M) { return 4 * ((M + 255) / 256) + 4; }  // >= (BM/64) * tiles for every variant
+
+int convn_part_rows(int M, int N, int variant) {
+  const int bn = convn_tile_n(N);
+  if (!bn) return 0;
+  const int bm = stats_bm(bn, variant);
+  return (bm / 64) * ((M + bm - 1) / bm);
+}
 
 hipError_t launch_convn(const ConvnArgs& a, hipStream_t st) {
   if (a.M <= 0) return hipSuccess;
@@ -273,12 +356,23 @@ hipError_t launch_convn(const ConvnArgs& a, hipStream_t st) {
   const int C = 1 << a.logC;
   const bool ok = bn > 0 && a.logC >= 6 && a.K % kBK == 0 && a.K == a.R * a.S * C && a.ldc % 8 == 0 &&
                   a.ldc >= a.N && a.H < 32768 && a.W < 32768 && a.xbytes > 0 && a.xbytes <= 0xFFFFFF00u &&
-                  a.wbytes > 0 && (!a.part || a.shift);
+                  a.wbytes > 0 && (!a.part || a.shift) && a.variant < convn_variant_count(bn);
   if (!ok) return hipErrorNotSupported;
+  const int v = a.variant >= 0 ? a.variant : default_variant(a, bn);
   switch (bn) {
-    case 64: return launch_s<64, 32>(a, st);
-    case 128: return launch_s<128, 32>(a, st);
-    default: return launch_s<256, 64>(a, st);
+    case 64:  // 4 waves of 64x32 | 2 waves of 64x64 | 4 waves of 64x64 (BM 256) | 8 waves of 64x32 (BM 256)
+      if (v == 0) return convn_launch_s<128, 64, 32, 3>(a, st);
+      if (v == 1) return convn_launch_s<128, 64, 64, 4>(a, st);
+      if (v == 2) return convn_launch_s<256, 64, 64, 3>(a, st);
+      return convn_launch_s<256, 64, 32, 3>(a, st);
+    case 128:  // 8 waves of 64x32 | 4 waves of 64x64 | 8 waves of 64x64 (BM 256) | 4 waves 64x64, 4 slots
+      if (v == 0) return convn_launch_s<128, 128, 32, 3>(a, st);
+      if (v == 1) return convn_launch_s<128, 128, 64, 3>(a, st);
+      if (v == 2) return convn_launch_s<256, 128, 64, 2>(a, st);
+      return convn_launch_s<128, 128, 64, 4>(a, st);
+    default:  // 8 waves of 64x64, 3 or 2 slots
+      if (v == 0) return convn_launch_s<128, 256, 64, 3>(a, st);
+      return convn_launch_s<128, 256, 64, 2>(a, st);
   }
 }
 

@@ -16,12 +16,17 @@ struct ConvnArgs {
   int M, N, K;
   int H, W, logC, Ho, Wo, R, S, stride, pad;
   int ldc;
+  int variant;  // tile geometry (convn_variants(N) of them); -1: the default
+  int nslot;    // set by the launcher
 };
 
 // output-channel tile of the kernel for N output channels (64, 128, 256 for N % 256 == 0), 0: unsupported
 int convn_tile_n(int N);
-// rows of the statistics partials for M output pixels (one per 64-pixel wave row)
+// rows to allocate for the statistics partials of M output pixels (any variant)
 int convn_stats_rows(int M);
+// rows a launch with this variant writes (one per 64-pixel wave row of every tile)
+int convn_part_rows(int M, int N, int variant);
+int convn_variants(int N);
 // hipErrorNotSupported outside the kernel's contract (nothing launched)
 hipError_t launch_convn(const ConvnArgs& a, hipStream_t stream);
 

@@ -47,11 +47,13 @@ void gemm_splitk_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool 
 void colsum_(const at::Tensor& x, at::Tensor out, bool accumulate);
 void gelu_bwd_colsum_(const at::Tensor& dy, const at::Tensor& pre, at::Tensor dx, at::Tensor out, bool accumulate);
 // narrow-output implicit-GEMM convolution (kernels/convn.hip): out [Nb*Ho*Wo, Cout] = conv(x, w2),
-// w2 [Cout, R*S*C]; with part/shift also the consumer BN's shifted statistics partials
-// [convn_stats_rows, 2, Cout]. False (nothing launched) outside the kernel's contract.
-bool convn_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride, int64_t pad,
-            c10::optional<at::Tensor> part, c10::optional<at::Tensor> shift);
+// w2 [Cout, R*S*C]; with part/shift also the consumer BN's shifted statistics partials (a buffer of
+// convn_stats_rows(M) x 2 x Cout). Returns 0 (nothing launched) outside the kernel's contract, else
+// the partial rows written (1 without statistics).
+int64_t convn_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride,
+               int64_t pad, c10::optional<at::Tensor> part, c10::optional<at::Tensor> shift, int64_t variant);
 int64_t convn_stats_rows_(int64_t M);
+int64_t convn_variants_(int64_t N);
 bool conv_fwd_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride,
                int64_t pad);
 bool conv_wgrad_(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64_t R, int64_t S, int64_t stride,

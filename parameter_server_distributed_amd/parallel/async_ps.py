@@ -20,11 +20,20 @@ optimizer kernel, writes the bf16 snapshot
 into a free publish buffer and advances the shard version, the worker's clock and the staleness
 histogram (staleness = shard version at apply - version the gradient was computed on).
 
-Optimizer semantics: one round (every worker pushing once) is W applies. Each push runs with the
-per-push hyperparameters of ``csrc/async_hyper.h`` (SGD: grad x 1/W; momentum: beta^(1/W) and a
-rescaled lr; Adam/AdamW: beta1^(1/W), beta2^(1/W), lr/W), which keep the synchronous optimizer's
-per-round EMA horizons, displacement and bias-correction schedule, and are the synchronous ones at
-W = 1 (pinned against the sync trajectory by tests/test_async_ps.py).
+Optimizer semantics (``semantics``):
+
+  "round" (default): K-batch asynchronous SGD with K = W (min(W, 16)). Each shard takes the pushes
+          in arrival order, from whichever workers, and every K of them make ONE optimizer step on
+          their average with the synchronous hyperparameters (the K inbox slots are summed inside
+          the fused apply kernel). A worker's clock advances when the round holding its push has
+          been applied. At SSP bound 0 the rounds are exactly the synchronous steps (a worker
+          cannot push step t+1 before every step-t push is applied), so the trajectory equals the
+          synchronous one; at S >= 1 a round may mix steps (stale gradients, bounded by S).
+  "push": every push is applied on arrival as its own step, with the per-push hyperparameters of
+          ``csrc/async_hyper.h`` (SGD grad x 1/W; momentum beta^(1/W) and a rescaled lr; Adam/AdamW
+          beta^(1/W), lr/W), which keep the synchronous per-round EMA horizons and steady-state
+          displacement -- lower latency, approximate. Both are pinned against the synchronous
+          trajectory in tests/test_async_ps.py.
 
 Layout: the parameters live in one flat working buffer (``.data`` views, reverse registration
 order, 64-element aligned) split into P contiguous shards; gradients alternate between two flat
@@ -79,10 +88,8 @@ class AsyncPS:
                  worker_ranks: list[int] | None = None, param_dtype: torch.dtype = torch.bfloat16, nbuf: int = 4,
                  timeout_s: float | None = None, overlap: bool = True, store=None, log: bool = False,
                  semantics: str = "round"):
-        """``semantics``: "round" (default) runs each push with the per-push hyperparameters of
-        csrc/async_hyper.h (W pushes behave like one synchronous step); "push" is the naive rule,
-        every push a full optimizer step on grad / W with the synchronous hyperparameters (kept as
-        an A/B baseline: its momentum horizon is W x shorter and Adam takes W x the lr)."""
+        """``semantics``: "round" (K-batch async, default) or "push" (apply-on-arrival with the
+        per-push hyperparameters of csrc/async_hyper.h); see the module docstring."""
         self.model = model
         self.cfg = optim
         st, self.rank, self.world = _store_and_group()
@@ -158,11 +165,12 @@ class AsyncPS:
         if semantics not in ("round", "push"):
             raise ValueError(f"semantics must be 'round' or 'push', got {semantics!r}")
         self.semantics = semantics
-        if semantics == "round":
+        self.round = min(self.W, 16) if semantics == "round" else 1
+        if semantics == "push":
             self.hyper = native().async_hyper(optim.code, self.W, optim.momentum, optim.beta1, optim.beta2,
                                               optim.weight_decay)
         else:
-            self.hyper = dict(lr_factor=1.0, grad_scale=1.0 / self.W, momentum=optim.momentum, beta1=optim.beta1,
+            self.hyper = dict(lr_factor=1.0, grad_scale=1.0 / self.round, momentum=optim.momentum, beta1=optim.beta1,
                               beta2=optim.beta2, weight_decay=optim.weight_decay)
         self.master, self.state1, self.state2, self.dyn = {}, {}, {}, {}
         for k in self.my_shards:
@@ -248,6 +256,7 @@ class AsyncPS:
                                         optim.code, h["momentum"], optim.dampening, optim.nesterov,
                                         h["weight_decay"], h["beta1"], h["beta2"], optim.eps)
             self.engine.publish_initial(k)
+        self.engine.set_round(self.round)
         if log:
             self.engine.enable_log(True)
         self._barrier("init")

@@ -40,13 +40,18 @@ def _case(case, gpu, seed=7):
 
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(map(str, c)))
 def test_convn_exact(gpu, case):
+    """Every tile variant of the output width, exact against fp32 F.conv2d."""
     Nb, C, H, W, Cout, R, stride, pad = case
     x, w, ref, xd = _case(case, gpu)
     Ho, Wo = ref.shape[2], ref.shape[3]
-    out = torch.full((Nb * Ho * Wo, Cout), 7.0, device=gpu, dtype=torch.bfloat16)
-    assert native().convn_(xd, _w2(w.to(gpu, torch.bfloat16)), out, R, R, stride, pad)
     want = ref.permute(0, 2, 3, 1).reshape(-1, Cout).bfloat16().float()
-    torch.testing.assert_close(out.float().cpu(), want, rtol=0, atol=0)
+    w2 = _w2(w.to(gpu, torch.bfloat16))
+    nv = native().convn_variants(Cout)
+    assert nv >= 2
+    for v in range(nv):
+        out = torch.full((Nb * Ho * Wo, Cout), 7.0, device=gpu, dtype=torch.bfloat16)
+        assert native().convn_(xd, w2, out, R, R, stride, pad, variant=v) == 1
+        torch.testing.assert_close(out.float().cpu(), want, rtol=0, atol=0, msg=lambda m: f"variant {v}: {m}")
 
 
 @pytest.mark.parametrize("case", CASES[:5], ids=lambda c: "x".join(map(str, c)))
@@ -56,26 +61,28 @@ def test_convn_stats_partials(gpu, case):
     Nb, C, H, W, Cout, R, stride, pad = case
     x, w, ref, xd = _case(case, gpu, seed=11)
     M = ref.numel() // Cout
-    rows = native().convn_stats_rows(M)
-    part = torch.full((rows, 2, Cout), float("nan"), device=gpu)
     shift = torch.randint(-3, 4, (Cout,)).float().to(gpu)
-    out = torch.empty(M, Cout, device=gpu, dtype=torch.bfloat16)
-    assert native().convn_(xd, _w2(w.to(gpu, torch.bfloat16)), out, R, R, stride, pad, part=part, shift=shift)
-    y = out.double().cpu()
-    d = y - shift.double().cpu()
-    got = part.double().cpu().sum(0)
-    assert torch.isfinite(got).all()
-    torch.testing.assert_close(got[0], d.sum(0), rtol=1e-6, atol=1e-3)
-    torch.testing.assert_close(got[1], (d * d).sum(0), rtol=1e-6, atol=1e-3)
+    for v in range(native().convn_variants(Cout)):
+        part = torch.full((native().convn_stats_rows(M), 2, Cout), float("nan"), device=gpu)
+        out = torch.empty(M, Cout, device=gpu, dtype=torch.bfloat16)
+        rows = native().convn_(xd, _w2(w.to(gpu, torch.bfloat16)), out, R, R, stride, pad, part=part, shift=shift,
+                               variant=v)
+        assert 1 <= rows <= part.shape[0]
+        y = out.double().cpu()
+        d = y - shift.double().cpu()
+        got = part[:rows].double().cpu().sum(0)
+        assert torch.isfinite(got).all(), v
+        torch.testing.assert_close(got[0], d.sum(0), rtol=1e-6, atol=1e-3)
+        torch.testing.assert_close(got[1], (d * d).sum(0), rtol=1e-6, atol=1e-3)
 
 
 def test_convn_declines_unsupported(gpu):
     x = torch.zeros(2, 96, 8, 8, device=gpu, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
     out = torch.empty(2 * 64, 64, device=gpu, dtype=torch.bfloat16)
-    assert native().convn_(x, torch.zeros(64, 9 * 96, device=gpu, dtype=torch.bfloat16), out, 3, 3, 1, 1) is False
+    assert native().convn_(x, torch.zeros(64, 9 * 96, device=gpu, dtype=torch.bfloat16), out, 3, 3, 1, 1) == 0
     x = torch.zeros(2, 64, 8, 8, device=gpu, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
     out = torch.empty(2 * 64, 96, device=gpu, dtype=torch.bfloat16)  # 96 output channels: no tile
-    assert native().convn_(x, torch.zeros(96, 9 * 64, device=gpu, dtype=torch.bfloat16), out, 3, 3, 1, 1) is False
+    assert native().convn_(x, torch.zeros(96, 9 * 64, device=gpu, dtype=torch.bfloat16), out, 3, 3, 1, 1) == 0
 
 
 @pytest.mark.parametrize("relu", [False, True])
@@ -91,10 +98,10 @@ def test_bn_fwd_from_conv_partials_matches_fp32(gpu, relu):
     rv = torch.rand(Cout, device=gpu) + 0.5
     gamma = (torch.rand(Cout, device=gpu) + 0.5).to(torch.bfloat16)
     beta = (torch.randn(Cout, device=gpu) * 0.1).to(torch.bfloat16)
-    rows = native().convn_stats_rows(M)
-    part = torch.empty(rows, 2, Cout, device=gpu)
+    part = torch.empty(native().convn_stats_rows(M), 2, Cout, device=gpu)
     out = torch.empty(M, Cout, device=gpu, dtype=torch.bfloat16)
-    assert native().convn_(x, _w2(w), out, 3, 3, 1, 1, part=part, shift=rm)
+    rows = native().convn_(x, _w2(w), out, 3, 3, 1, 1, part=part, shift=rm)
+    assert rows > 0
     y4 = out.view(Nb, H, W, Cout).permute(0, 3, 1, 2)
     rm1, rv1 = rm.clone(), rv.clone()
     cnt = torch.zeros((), dtype=torch.int64, device=gpu)

@@ -15,6 +15,9 @@ import torch.nn.functional as F
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from parameter_server_distributed_amd import native  # noqa: E402
+from parameter_server_distributed_amd.utils import miopen as _miopen  # noqa: E402
+
+_miopen.install()  # the bench's MIOpen setup: shipped find-db, immediate mode
 
 SHAPES = [  # name, C, H, Cout, R, stride
     ("l1.conv1 1x1 64->64", 64, 56, 64, 1, 1),
@@ -53,8 +56,8 @@ def main():
     torch.backends.cudnn.benchmark = False
     C_ = native()
     print(f"batch {a.batch}; times in us (HBM bytes = x + y once)\n")
-    print("| shape | M | GFLOP | MB | miopen fwd | convn fwd | convn+stats | MIOpen+bn_reduce | TF/s convn | GB/s convn |")
-    print("|---|---:|---:|---:|---:|---:|---:|---:|---:|---:|")
+    print("| shape | M | GFLOP | MB | miopen fwd | convn fwd per variant | best | convn+stats (best) | MIOpen+bn_reduce | TF/s | GB/s |")
+    print("|---|---:|---:|---:|---:|---|---:|---:|---:|---:|---:|")
     for name, C, H, Cout, R, stride in SHAPES:
         pad = R // 2
         x = torch.randn(a.batch, C, H, H, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
@@ -69,18 +72,24 @@ def main():
         shift = torch.zeros(Cout, device=dev)
         t_mi = timeit(lambda: F.conv2d(x, w, stride=stride, padding=pad), a.reps)
         ok = C_.convn_(x, w2, out, R, R, stride, pad)
-        t_cn = timeit(lambda: C_.convn_(x, w2, out, R, R, stride, pad), a.reps) if ok else float("nan")
-        t_cs = timeit(lambda: C_.convn_(x, w2, out, R, R, stride, pad, part=part, shift=shift), a.reps) \
-            if ok else float("nan")
+        tv = {}
+        for v in range(C_.convn_variants(Cout) if ok else 0):
+            tv[v] = timeit(lambda: C_.convn_(x, w2, out, R, R, stride, pad, variant=v), a.reps)
+        best = min(tv, key=tv.get) if tv else 0
+        t_cn = tv[best] if tv else float("nan")
+        t_cs = timeit(lambda: C_.convn_(x, w2, out, R, R, stride, pad, part=part, shift=shift, variant=best),
+                      a.reps) if ok else float("nan")
         y = F.conv2d(x, w, stride=stride, padding=pad)
         t_red = timeit(lambda: C_.bn_reduce_(y, shift), a.reps)
         if ok:
+            C_.convn_(x, w2, out, R, R, stride, pad, variant=best)
             ref = y.permute(0, 2, 3, 1).reshape(M, Cout).float()
             err = float((out.float() - ref).abs().max()) / max(float(ref.abs().max()), 1e-6)
             assert err < 2e-2, (name, err)
         gf = 2.0 * M * Cout * R * R * C / 1e9
         mb = (x.numel() + M * Cout) * 2 / 1e6
-        print(f"| {name} | {M} | {gf:.0f} | {mb:.0f} | {t_mi:.0f} | {t_cn:.0f} | {t_cs:.0f} | {t_mi + t_red:.0f} | "
+        vs = " / ".join(f"{t:.0f}" for t in tv.values())
+        print(f"| {name} | {M} | {gf:.0f} | {mb:.0f} | {t_mi:.0f} | {vs} | v{best} {t_cn:.0f} | {t_cs:.0f} | {t_mi + t_red:.0f} | "
               f"{gf / t_cn * 1e3:.0f} | {mb / t_cn * 1e3:.0f} |", flush=True)
         del x, w, w2, out, y, part
 
