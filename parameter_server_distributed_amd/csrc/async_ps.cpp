@@ -8,7 +8,9 @@
 #include <sys/mman.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <sstream>
 
@@ -19,7 +21,8 @@ namespace psd {
 namespace {
 
 constexpr uint64_t kMagic = 0x5053444153594e43ull;  // "PSDASYNC"
-constexpr int kMaxShards = 64, kMaxWorkers = 64, kRing = 16, kMaxBuf = 8, kBins = 64;
+constexpr int kMaxShards = 64, kMaxWorkers = 64, kRing = 16, kMaxBuf = 8, kBins = 64, kMaxRanks = 128;
+constexpr int64_t kHbLeft = -1;  // heartbeat slot of a rank whose engine stopped on purpose
 constexpr int64_t kAlignBytes = 256;
 
 struct Msg {
@@ -53,6 +56,9 @@ struct AsyncCtl {
   std::atomic<int32_t> error;
   int32_t pad;
   char msg[512];
+  // liveness: each rank's engine thread stamps its slot (steady-clock us, one clock for every
+  // process of the node) every few ms; a peer silent for dead_after_s is presumed dead
+  std::atomic<int64_t> hb_us[kMaxRanks];
   ShardCtl shard[kMaxShards];
   Mailbox mb[kMaxShards][kMaxWorkers];
 };
@@ -67,6 +73,11 @@ int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 
 double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int64_t now_us() {
+  return std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
 }
 
 void backoff(int& spins) {
@@ -111,6 +122,8 @@ AsyncEngine::AsyncEngine(int rank, int world, std::vector<int> owners, std::vect
   TORCH_CHECK(S_ >= 0 && S_ + 1 <= kRing, "psd async: staleness bound must be in [0, ", kRing - 1, "]");
   TORCH_CHECK(nbuf_ >= 2 && nbuf_ <= kMaxBuf, "psd async: 2..", kMaxBuf, " publish buffers");
   TORCH_CHECK(esz_ == 2 || esz_ == 4, "psd async: bf16 (2) or fp32 (4) elements");
+  TORCH_CHECK(world_ >= 1 && world_ <= kMaxRanks, "psd async: 1..", kMaxRanks, " ranks");
+  if (const char* e = getenv("PSD_ASYNC_DEAD_S")) dead_after_s_ = atof(e);
   TORCH_CHECK((int)shard_off_.size() == P && (int)shard_len_.size() == P, "psd async: shard ranges per owner");
   for (int k = 0; k < P; ++k) {
     TORCH_CHECK(owners_[k] >= 0 && owners_[k] < world_, "psd async: bad owner rank");
@@ -357,6 +370,7 @@ void AsyncEngine::stop() {
   stop_.store(true);
   thr_.join();
   running_ = false;
+  if (ctl_) ctl_->hb_us[rank_].store(kHbLeft);  // stopped on purpose: not a dead peer
   // finish what is in flight (unpins / posts / applies) so the shared state is final and no
   // kernel or copy still touches the inbox / publish memory when it is freed
   for (int guard = 0; guard < 1000; ++guard) {
@@ -374,7 +388,14 @@ void AsyncEngine::run() {
   try {
     if (device_ >= 0) hip_ok(hipSetDevice(device_), "hipSetDevice");
     int spins = 0;
+    int64_t last_check = now_us();
     while (!stop_.load()) {
+      const int64_t t = now_us();
+      ctl_->hb_us[rank_].store(t);
+      if (dead_after_s_ > 0 && t - last_check > 100000) {  // peers' liveness, every 100 ms
+        last_check = t;
+        check_peers(t);
+      }
       if (ctl_->error.load()) break;
       if (poll_once()) spins = 0;
       else backoff(spins);
@@ -444,6 +465,10 @@ bool AsyncEngine::poll_once() {
       st.round.push_back(RoundItem{wi, (int)(m.step % (S_ + 1)), m.step, m.pulled, 0});
       progress = true;
       if (!completes) continue;
+      // sources in worker order: the fp32 sum inside the apply kernel is then independent of the
+      // arrival order (bitwise-reproducible rounds at SSP bound 0)
+      std::sort(st.round.begin(), st.round.end(),
+                [](const RoundItem& x, const RoundItem& y) { return x.wi != y.wi ? x.wi < y.wi : x.step < y.step; });
       std::vector<at::Tensor> g;
       for (RoundItem& it : st.round) {
         it.staleness = st.enq - it.pulled;
@@ -525,6 +550,22 @@ void AsyncEngine::post(int shard, int wi, int64_t step, int64_t pulled) {
   mb.head.store(h + 1);
   n_posts_.fetch_add(1);
 }
+
+void AsyncEngine::check_peers(int64_t t) {
+  for (int r = 0; r < world_; ++r) {
+    if (r == rank_) continue;
+    const int64_t h = ctl_->hb_us[r].load();
+    if (h <= 0) continue;  // not started yet, or stopped on purpose
+    const double silent = (double)(t - h) * 1e-6;
+    if (silent > dead_after_s_) {
+      fail("rank " + std::to_string(r) + " presumed dead: its async engine has been silent for " +
+           std::to_string((int)silent) + " s (PSD_ASYNC_DEAD_S=" + std::to_string((int)dead_after_s_) + ")");
+      return;
+    }
+  }
+}
+
+void AsyncEngine::inject_error(const std::string& msg) { fail(msg); }
 
 void AsyncEngine::check_error() const {
   if (ctl_->error.load()) TORCH_CHECK(false, "psd async: ", std::string(ctl_->msg));

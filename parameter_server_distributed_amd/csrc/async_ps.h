@@ -29,7 +29,9 @@
 //     unpins when the copy completes.
 // No GPU kernel ever waits on another process (no spinning collective kernels that could
 // interlock through shared hardware queues); every host wait has a deadline and reports an
-// error instead of hanging. With device = -1 the same protocol runs on host memory in POSIX
+// error instead of hanging. Liveness: every engine thread stamps a heartbeat in the control block;
+// a peer silent for PSD_ASYNC_DEAD_S (10 s) -- a killed or hung process -- sets the shared error,
+// so every rank's SSP wait fails within seconds instead of at the 600 s deadline. With device = -1 the same protocol runs on host memory in POSIX
 // shared memory (CPU CI, gloo plumbing config).
 #pragma once
 #include <ATen/ATen.h>
@@ -92,6 +94,8 @@ class AsyncEngine {
   std::vector<int> my_shards() const { return my_shards_; }
   std::string memory_kind() const { return mem_kind_; }
   std::string error() const;
+  // fail every rank's waits now (an external failure detector, e.g. the coordinator expired a peer)
+  void inject_error(const std::string& msg);
   std::vector<int64_t> counters() const;  // applies, pushes posted, pulls, pull waits (us)
   // completed applies in order: (shard, worker rank, step, staleness, version after) -- for tests
   // and replay; recorded only after enable_log()
@@ -133,6 +137,7 @@ class AsyncEngine {
   void run();
   bool poll_once();
   void check_error() const;
+  void check_peers(int64_t now_us);
   void fail(const std::string& msg);
   void copy(void* dst, const void* src, int64_t bytes, void* stream);
   void defer(void* stream, std::function<void()> fn);
@@ -142,6 +147,7 @@ class AsyncEngine {
   int rank_, world_, S_, nbuf_, device_;
   int round_ = 1;
   double timeout_s_;
+  double dead_after_s_ = 10.0;  // a peer's engine silent this long is presumed dead (PSD_ASYNC_DEAD_S)
   int esz_;
   std::vector<int> owners_, workers_, my_shards_;
   std::vector<int64_t> shard_off_, shard_len_;

@@ -256,6 +256,7 @@ PYBIND11_MODULE(_C, m) {
       .def("my_shards", &AsyncEngine::my_shards)
       .def("memory_kind", &AsyncEngine::memory_kind)
       .def("error", &AsyncEngine::error)
+      .def("inject_error", &AsyncEngine::inject_error)
       .def("counters", &AsyncEngine::counters)
       .def("enable_log", &AsyncEngine::enable_log)
       .def("apply_log", &AsyncEngine::apply_log);

@@ -335,9 +335,10 @@ static int default_variant(const ConvnArgs& a, int bn) {
   return 0;
 }
 
+// BM of each variant (must match the dispatch in launch_convn)
 static int stats_bm(int bn, int v) {
   if (bn == 64) return (v == 2 || v == 3) ? 256 : 128;
-  if (bn == 128) return (v == 2 || v == 3) ? 256 : 128;
+  if (bn == 128) return v == 2 ? 256 : 128;
   return 128;
 }
 

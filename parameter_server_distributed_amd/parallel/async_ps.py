@@ -59,12 +59,22 @@ from .. import native
 from ..ops.optim import OptimConfig, OptimDyn
 from .collective_ps import ALIGN, _flat_view, _round, zero_grads_, zero_plan
 
-_INSTANCE = [0]
+_INSTANCE: dict = {}  # AsyncPS instances per rendezvous store (a new elastic generation starts at 0)
 
 
 class _NoTransport:
+    """The async plane moves tensors by peer-memory DMA, not through a Transport; ``abort`` is the
+    hook a failure detector (runtime/elastic.py _Watchdog) calls to fail every blocked wait."""
+
     name = "ipc"
     capturable = False
+
+    def __init__(self, ps=None):
+        self.ps = ps
+
+    def abort(self):
+        if self.ps is not None and self.ps.engine is not None:
+            self.ps.engine.inject_error("aborted by a failure detector (a peer was declared dead)")
 
 
 @dataclass
@@ -94,7 +104,7 @@ class AsyncPS:
         self.cfg = optim
         st, self.rank, self.world = _store_and_group()
         self.store = store or st
-        self.t = _NoTransport()
+        self.t = _NoTransport(self)
         self.worker_ranks = list(worker_ranks) if worker_ranks is not None else list(range(self.world))
         self.is_worker = self.rank in self.worker_ranks
         self.W = len(self.worker_ranks)
@@ -212,8 +222,9 @@ class AsyncPS:
         self._prefetched = None  # (step, pulled versions) of the pull issued ahead
 
         # ---- native engine: control block (rank 0 creates), memory exchange, initial publish
-        _INSTANCE[0] += 1
-        key = f"psd/async/{_INSTANCE[0]}"
+        n = _INSTANCE.get(id(self.store), 0) + 1
+        _INSTANCE[id(self.store)] = n
+        key = f"psd/async/{n}"
         if self.rank == 0:
             self.store.set(f"{key}/shm", f"/psd_{os.getpid()}_{uuid.uuid4().hex[:12]}")
         shm = self.store.get(f"{key}/shm").decode()
@@ -238,6 +249,7 @@ class AsyncPS:
             raise
         self.tracer = None
         self.closed = False
+        self._ckpt_seq = 0
 
     def _connect(self, key, optim, log):
         """Exchange memory descriptors, map the peers, publish version 0, self-test, start."""
@@ -456,6 +468,14 @@ class AsyncPS:
         if self.is_cuda:
             torch.cuda.synchronize(self.device)
 
+    def refresh_weights(self):
+        """After ``drain``: the working weights (the model's parameter views) = the latest applied
+        snapshot. Workers otherwise hold the weights of their last pull, one round behind."""
+        if self.is_worker and self.engine is not None:
+            self.pulled = list(self.engine.pull(0, self.params_flat, self._stream_ptr()))
+            if self.is_cuda:
+                torch.cuda.synchronize(self.device)
+
     def probe_bandwidth(self, reps: int = 3) -> dict:
         """After ``drain``: time this worker's full push (DMA of the whole gradient into its inbox slot
         on every owner, no commit) and a full pull (latest snapshots into a scratch buffer) -- the
@@ -480,9 +500,40 @@ class AsyncPS:
             out[f"{name}_GBps"] = round(self.total * g.element_size() / (ms * 1e-3) / 1e9, 1)
         return out
 
+    def abort(self):
+        """Non-collective teardown after a failure (a dead peer would never reach close()'s
+        barriers): raise the shared error so every peer's waits fail, stop the engine, unmap the
+        peers' memory and free this rank's. Pushes not yet applied are lost; recovery restarts from
+        a checkpoint (runtime/elastic.py)."""
+        if self.closed or self.engine is None:
+            return
+        try:
+            self.engine.inject_error(f"rank {self.rank} aborted")
+        except Exception:  # noqa: BLE001
+            pass
+        self.engine.stop()
+        hist, vers, log = self.staleness_histogram(), self.versions(), self.apply_log()
+        self._final = (hist, vers, log)
+        self.engine.close_peers()
+        self.engine.free_local()
+        self.engine = None
+        self._release_model()
+        self.closed = True
+
+    def _release_model(self):
+        for h in self._hooks:
+            h.remove()
+        for m in self.model.modules():
+            if getattr(m, "_psd_grad_sink", None) == self._sink:
+                del m._psd_grad_sink
+
     def close(self):
-        """Collective: stop the engine, unmap the peers' memory, free this rank's (all ranks call)."""
+        """Collective: stop the engine, unmap the peers' memory, free this rank's (all ranks call).
+        After a failure (the shared error is set) this is ``abort``: no barriers with dead peers."""
         if self.closed:
+            return
+        if self.engine.error():
+            self.abort()
             return
         self.engine.stop()
         self._barrier("stop")
@@ -492,11 +543,7 @@ class AsyncPS:
         self._final = (hist, vers, log)
         self.engine.free_local()
         self.engine = None
-        for h in self._hooks:
-            h.remove()
-        for m in self.model.modules():
-            if getattr(m, "_psd_grad_sink", None) == self._sink:
-                del m._psd_grad_sink
+        self._release_model()
         self.closed = True
 
     def staleness_histogram(self):
@@ -538,6 +585,209 @@ class AsyncPS:
                 "state2": {k: v.cpu() for k, v in self.state2.items()},
                 "dyn": {k: d.t.cpu() for k, d in self.dyn.items()}, "versions": self.versions(),
                 "step_idx": self.step_idx}
+
+    # ------------------------------------------------------------------ checkpoint / resume
+    def _quiesce(self):
+        """Collective: every push so far applied at every shard, so the masters, optimizer state,
+        versions and clocks form one consistent cut."""
+        self.drain()
+
+    def _layout_meta(self) -> dict:
+        return {"world": self.world, "owners": self.owners, "workers": self.worker_ranks, "P": self.P,
+                "shard_off": self.shard_off, "shard_len": self.shard_len, "total": self.total,
+                "staleness": self.S, "semantics": self.semantics, "round": self.round,
+                "optimizer": self.cfg.to_dict(), "params": [(n, list(p.shape), o, k) for (n, p, o, k) in self._layout]}
+
+    def save(self, prefix: str, blocking: bool = True):
+        """Sharded checkpoint (collective: every rank calls at the same step). After a drain, each
+        shard owner writes ``{prefix}.rank{r}.psd`` (atomic, CRC-checked: csrc/checkpoint.cpp) with
+        its fp32 masters, optimizer state and step scalars, plus the shard versions and every
+        worker's SSP clock; rank 0 writes ``{prefix}.manifest.json``. The device state is
+        snapshotted (HBM->HBM) before any rank returns, so the engines' next applies cannot race
+        the copy; with ``blocking=False`` the device->host copy and the file write run on a host
+        thread while training continues. Returns that thread (or None).
+
+        Reference: the periodic checkpoint thread (src/parameter_server_service.cpp:150-169) and
+        ParameterServerCore::save_checkpoint (src/parameter_server.cpp:112-144), which kept no
+        optimizer state, versions or worker iteration."""
+        import json
+        import threading
+
+        self._quiesce()
+        C = native()
+        snap = []
+        meta = {"step_idx": self.step_idx if self.is_worker else None, "shards": {}}
+        for k in self.my_shards:
+            ts = [self.master[k], self.dyn[k].t] + [d[k] for d in (self.state1, self.state2) if k in d]
+            snap.extend(t.detach().clone() for t in ts)
+            meta["shards"][str(k)] = {"version": int(self.engine.version(k)), "clocks": list(self.engine.clocks(k)),
+                                      "n": len(ts)}
+        # the workers' step (the owners that are not workers learn it from the store)
+        steps = torch.tensor([self.step_idx if self.is_worker else 0], dtype=torch.int64)
+        if self.world > 1 and dist.is_initialized():
+            steps = steps.to(self.device) if dist.get_backend() == "nccl" else steps
+            dist.all_reduce(steps, op=dist.ReduceOp.MAX)
+        meta["step_idx"] = int(steps.item())
+        if self.is_cuda:
+            torch.cuda.synchronize(self.device)
+        self._barrier(f"ckpt-snap-{self._ckpt_seq}")  # every owner's snapshot taken before anyone pushes
+        self._ckpt_seq += 1
+        man = {"format": "psd-async-v1", **self._layout_meta(), **meta, "rank": self.rank}
+        man_s = json.dumps(man)
+        path = f"{prefix}.rank{self.rank}.psd"
+
+        def write():
+            host = [t.cpu() for t in snap]
+            C.save_native_ckpt(path, man_s, host)
+            if self.rank == 0:
+                m0 = {k: v for k, v in man.items() if k not in ("shards", "rank")}
+                with open(f"{prefix}.manifest.json.tmp", "w") as f:
+                    f.write(json.dumps(m0))
+                os.replace(f"{prefix}.manifest.json.tmp", f"{prefix}.manifest.json")
+
+        if blocking:
+            write()
+            return None
+        th = threading.Thread(target=write, name="psd-async-ckpt", daemon=True)
+        th.start()
+        return th
+
+    def load(self, prefix: str):
+        """Resume from ``save(prefix)`` with the same layout (collective, before the first step):
+        every owner restores its shards' masters, optimizer state and step scalars and re-publishes
+        them as the saved shard versions with the saved SSP clocks; every worker continues at the
+        saved step (its first pull waits on the restored clocks)."""
+        import json
+
+        man, ts = native().load_native_ckpt(f"{prefix}.rank{self.rank}.psd")
+        m = json.loads(man)
+        mine = self._layout_meta()
+        for key in ("world", "owners", "workers", "shard_off", "shard_len", "total", "round"):
+            if m[key] != mine[key]:
+                raise ValueError(f"checkpoint {prefix}: {key} {m[key]} does not match this run's {mine[key]}")
+        if m["optimizer"]["kind"] != self.cfg.kind:
+            raise ValueError(f"checkpoint optimizer {m['optimizer']['kind']} != {self.cfg.kind}")
+        self.engine.stop()
+        i = 0
+        for k in self.my_shards:
+            sh = m["shards"][str(k)]
+            self.master[k].copy_(ts[i])
+            self.dyn[k].t.copy_(ts[i + 1])
+            j = i + 2
+            for d in (self.state1, self.state2):
+                if k in d:
+                    d[k].copy_(ts[j])
+                    j += 1
+            i += sh["n"]
+            self.engine.publish_initial(k, sh["version"], sh["clocks"])
+        self.step_idx = int(m["step_idx"])
+        self._prefetched = None
+        self.engine.start()
+        if self.is_cuda:
+            torch.cuda.synchronize(self.device)
+        self._barrier(f"ckpt-load-{self._ckpt_seq}")
+        self._ckpt_seq += 1
+        if self.is_worker:  # working weights = the restored snapshot (forward hooks, eval before a step)
+            self.pulled = list(self.engine.pull(0, self.params_flat, self._stream_ptr()))
+            if self.is_cuda:
+                torch.cuda.synchronize(self.device)
+
+    def _canon_index(self):
+        """(flat offset, canonical offset, numel) per parameter, canonical = model.named_parameters
+        order without padding (the layout CollectivePS.canonical_state uses too)."""
+        where = {id(p): (o, k) for (_n, p, o, k) in self._layout}
+        out, c = [], 0
+        for _, p in self.model.named_parameters():
+            if id(p) in where:
+                o, k = where[id(p)]
+                out.append((o, c, k))
+                c += k
+        return out, c
+
+    def canonical_state(self, root: int) -> dict | None:
+        """Collective: drain, then gather every shard's fp32 master + optimizer state onto rank
+        ``root`` in the layout-independent canonical order (owners hold disjoint ranges: a sum
+        reduce is the gather). Returns the tensors on ``root``, None elsewhere."""
+        self._quiesce()
+        idx, n = self._canon_index()
+        out = {}
+        for key, src in (("master", self.master), ("state1", self.state1), ("state2", self.state2)):
+            if (key == "state1" and self.cfg.num_states < 1) or (key == "state2" and self.cfg.num_states < 2):
+                continue
+            full = torch.zeros(self.total, dtype=torch.float32, device=self.device)
+            for k, t in src.items():
+                full.narrow(0, self.shard_off[k], self.shard_len[k]).copy_(t)
+            if self.world > 1 and dist.is_initialized():
+                dist.reduce(full, root)
+            if self.rank == root:
+                canon = torch.empty(n, dtype=torch.float32, device=self.device)
+                for o, c, k in idx:
+                    canon.narrow(0, c, k).copy_(full.narrow(0, o, k))
+                out[key] = canon
+        # step scalars: every shard advanced in lock-step (one apply per round), take shard 0's
+        d = self.dyn[0].t.detach().clone() if 0 in self.dyn else torch.zeros(8, dtype=torch.int32, device=self.device)
+        if self.world > 1 and dist.is_initialized():
+            if self.owners[0] != root:
+                if self.rank == self.owners[0]:
+                    dist.send(d, root)
+                elif self.rank == root:
+                    dist.recv(d, self.owners[0])
+        if self.rank != root:
+            return None
+        out["dyn"] = d
+        return out
+
+    def load_canonical_state(self, sd: dict):
+        """Inverse of ``canonical_state`` for this (possibly different) world and shard layout:
+        every rank passes the full canonical tensors; owners keep their ranges and re-publish them
+        (version 0 of this plane), workers take the weights."""
+        idx, n = self._canon_index()
+        full = {}
+        for key in ("master", "state1", "state2"):
+            if key not in sd:
+                continue
+            canon = sd[key].to(self.device)
+            if canon.numel() != n:
+                raise ValueError(f"canonical {key} has {canon.numel()} elements, model has {n}")
+            f = torch.zeros(self.total, dtype=torch.float32, device=self.device)
+            for o, c, k in idx:
+                f.narrow(0, o, k).copy_(canon.narrow(0, c, k))
+            full[key] = f
+        self.engine.stop()
+        for k in self.my_shards:
+            for key, dst in (("master", self.master), ("state1", self.state1), ("state2", self.state2)):
+                if key in full and k in dst:
+                    dst[k].copy_(full[key].narrow(0, self.shard_off[k], self.shard_len[k]))
+            if "dyn" in sd:
+                self.dyn[k].t.copy_(sd["dyn"].to(self.dyn[k].t.device))
+                # lr / grad scale of THIS plane's semantics and worker count
+                self.dyn[k].set(lr=self.cfg.lr * self.hyper["lr_factor"], grad_scale=self.hyper["grad_scale"])
+            self.engine.publish_initial(k)
+        self.engine.start()
+        self.params_flat.copy_(full["master"].to(self.param_dtype))
+        for b in self.pbufs[1:]:
+            b.copy_(self.params_flat)
+        self.step_idx = 0
+        self._prefetched = None
+        if self.is_cuda:
+            torch.cuda.synchronize(self.device)
+        self._barrier(f"canon-load-{self._ckpt_seq}")
+        self._ckpt_seq += 1
+
+    def export_reference(self, path: str, epoch: int, iteration: int = 0):
+        """The reference's binary checkpoint layout (src/parameter_server.cpp:112-144: fp32 params by
+        name) on rank 0, from the drained fp32 masters (collective)."""
+        sd = self.canonical_state(root=0)
+        if self.rank != 0:
+            return
+        names, shapes, vals = [], [], []
+        idx, _ = self._canon_index()
+        params = [(n, p) for n, p in self.model.named_parameters() if p.requires_grad]
+        for (n, p), (_o, c, k) in zip(params, idx):
+            names.append(n)
+            shapes.append(list(p.shape))
+            vals.append(sd["master"].narrow(0, c, k).view(p.shape).cpu())
+        native().save_reference_ckpt(path, epoch, iteration, names, shapes, vals)
 
     def describe(self) -> str:
         return (f"AsyncPS(world={self.world}, shards={self.P} on ranks {self.owners}, workers={self.worker_ranks}, "

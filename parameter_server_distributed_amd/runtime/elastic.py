@@ -321,6 +321,9 @@ class ElasticTrainer:
             if leavers is None:  # all steps done
                 if rank == 0:
                     self.agent.publish(Plan(plan.gen + 1, [], step, self.agent.epoch, done=True))
+                if hasattr(ps, "refresh_weights"):  # async plane: workers hold their last pull
+                    ps.drain()
+                    ps.refresh_weights()
                 result["params"] = {n: p.detach().float().cpu() for n, p in self.model.named_parameters()}
                 result["staleness_hist"] = ps.staleness_histogram()
                 ps.close()

@@ -1,6 +1,7 @@
-"""One elastic collective worker for tests/test_elastic_collective.py::test_crash_recovery (run as a
+"""One elastic worker for tests/test_elastic_collective.py::test_crash_recovery (run as a
 subprocess so that it can be SIGKILLed). argv: coordinator worker_id steps ckpt_dir out_json kill_at
-[device] (cpu, or cuda:0 -- every rank on the one GPU, gloo process group over cuda tensors)"""
+[device] [plane] (device cpu, or cuda:0 -- every rank on the one GPU, gloo process group over cuda
+tensors; plane collective (CollectivePS) or async (AsyncPS, K-batch rounds at SSP bound 0))"""
 import json
 import os
 import signal
@@ -13,6 +14,7 @@ sys.path.insert(0, ROOT)
 
 from parameter_server_distributed_amd import models  # noqa: E402
 from parameter_server_distributed_amd.ops.optim import OptimConfig  # noqa: E402
+from parameter_server_distributed_amd.parallel.async_ps import AsyncPS  # noqa: E402
 from parameter_server_distributed_amd.parallel.collective_ps import CollectivePS  # noqa: E402
 from parameter_server_distributed_amd.runtime.elastic import ElasticAgent, ElasticTrainer  # noqa: E402
 from parameter_server_distributed_amd.runtime.trainer import Trainer  # noqa: E402
@@ -24,6 +26,7 @@ def main():
     coord, wid, steps, ckpt_dir, out, kill_at = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4], \
         sys.argv[5], int(sys.argv[6])
     dev = torch.device(sys.argv[7] if len(sys.argv) > 7 else "cpu")
+    plane = sys.argv[8] if len(sys.argv) > 8 else "collective"
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
     torch.manual_seed(0)
@@ -33,6 +36,9 @@ def main():
     trace = []
 
     def make_ps(model, transport):
+        if plane == "async":
+            return AsyncPS(model, OptimConfig(**CFG), num_shards=transport.world, staleness=0, bucket_mb=0.0005,
+                           param_dtype=torch.float32, device=dev, timeout_s=60.0)
         return CollectivePS(model, OptimConfig(**CFG), transport, num_shards=transport.world, staleness=0,
                             bucket_mb=0.0005, grad_dtype=torch.float32, param_dtype=torch.float32, device=dev)
 

@@ -300,6 +300,73 @@ def test_async_hyper_reduces_to_sync_at_w1(C):
     assert abs(h["beta2"] ** 8 - 0.999) < 1e-12 and h["lr_factor"] == 0.125 and h["grad_scale"] == 1.0
 
 
+# ---------------------------------------------------------------------------------------------
+# checkpoint / resume on the async plane
+
+
+def _ckpt_worker(rank, world, port, mode, prefix, out_dir, steps, stale, kind):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    spec = models.build("mlp", torch.device("cpu"), torch.float32, hidden=64)
+    cfg = dict(CFG) if kind == "momentum" else dict(kind="adamw", lr=2e-3, weight_decay=0.01)
+    ps = AsyncPS(spec.model, OptimConfig(**cfg), num_shards=2, staleness=stale, bucket_mb=0.0005,
+                 param_dtype=torch.float32)
+    from parameter_server_distributed_amd.runtime.trainer import Trainer
+
+    tr = Trainer(spec.model, spec.loss, ps, spec.make_batch(16, torch.device("cpu"), seed=rank),
+                 checkpoint_prefix=prefix if mode == "save" else None, checkpoint_every=3 if mode == "save" else 0)
+    if mode == "resume":
+        ps.load(prefix)
+        assert ps.step_idx == 3
+    for _ in range(steps):
+        tr.step()
+    tr.wait_checkpoint()
+    ps.drain()
+    ps.refresh_weights()
+    torch.save({"master": {k: v.clone() for k, v in ps.master.items()}, "versions": ps.versions(),
+                "params": ps.params_flat.clone(), "step": ps.step_idx},
+               os.path.join(out_dir, f"{mode}{rank}.pt"))
+    ps.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("kind", ["momentum", "adamw"])
+def test_async_save_resume_exact(tmp_path, kind):
+    """a 3-rank async run (2 PS shards, SSP bound 0) checkpointed by the Trainer
+    every 3 steps (non-blocking writer thread) and resumed from the step-3 checkpoint in new
+    processes ends bitwise equal to the uninterrupted 6-step run: masters, optimizer state and
+    step scalars, shard versions and SSP clocks are restored (round sums are in worker order, so
+    bound-0 runs are reproducible bit for bit)."""
+    prefix = str(tmp_path / "ck")
+    mp.spawn(_ckpt_worker, args=(3, _port(), "full", prefix, str(tmp_path), 6, 0, kind), nprocs=3, join=True)
+    mp.spawn(_ckpt_worker, args=(3, _port(), "save", prefix, str(tmp_path), 3, 0, kind), nprocs=3, join=True)
+    assert os.path.exists(prefix + ".manifest.json")
+    mp.spawn(_ckpt_worker, args=(3, _port(), "resume", prefix, str(tmp_path), 3, 0, kind), nprocs=3, join=True)
+    for r in range(3):
+        full = torch.load(os.path.join(str(tmp_path), f"full{r}.pt"), weights_only=True)
+        res = torch.load(os.path.join(str(tmp_path), f"resume{r}.pt"), weights_only=True)
+        assert res["versions"] == full["versions"] == [6, 6]
+        assert res["step"] == full["step"] == 6
+        for k in full["master"]:
+            assert torch.equal(full["master"][k], res["master"][k]), (r, k)
+        assert torch.equal(full["params"], res["params"]), r
+
+
+@pytest.mark.slow
+def test_async_resume_rejects_other_layout(tmp_path):
+    prefix = str(tmp_path / "ck")
+    mp.spawn(_ckpt_worker, args=(3, _port(), "save", prefix, str(tmp_path), 3, 0, "momentum"), nprocs=3, join=True)
+    torch.manual_seed(0)
+    spec = models.build("mlp", torch.device("cpu"), torch.float32, hidden=64)
+    ps = AsyncPS(spec.model, OptimConfig(**CFG), staleness=0, bucket_mb=0.0005, param_dtype=torch.float32)
+    with pytest.raises((ValueError, RuntimeError)):
+        ps.load(prefix)
+    ps.close()
+
+
 def _selftest_worker(rank, world, port, out_dir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PSD_ASYNC_SELFTEST_FAIL_RANK="1")
     dist.init_process_group("gloo", rank=rank, world_size=world)

@@ -178,7 +178,7 @@ def test_handover_roundtrip_gpu_bf16(gpu):
     assert torch.isfinite(tr2.step()).item()
 
 
-def _crash_recovery(tmp_path, device):
+def _crash_recovery(tmp_path, device, plane="collective"):
     """SIGKILL one of 3 ranks mid-run (no hand-over, no deregistration). The
     survivors' blocked collective fails, the coordinator expires the dead worker, one survivor
     publishes a restore plan and both rebuild a 2-rank world from the last canonical checkpoint
@@ -198,8 +198,9 @@ def _crash_recovery(tmp_path, device):
         for w in range(3):
             procs.append(subprocess.Popen(
                 [sys.executable, os.path.join(ROOT, "tests", "elastic_crash_worker.py"), f"127.0.0.1:{cport}", str(w),
-                 str(steps), ck, str(tmp_path / f"w{w}.json"), str(kill_at if w == 2 else -1), device],
-                stdout=open(tmp_path / f"w{w}.log", "w"), stderr=subprocess.STDOUT, env=dict(os.environ, PYTHONPATH=ROOT)))
+                 str(steps), ck, str(tmp_path / f"w{w}.json"), str(kill_at if w == 2 else -1), device, plane],
+                stdout=open(tmp_path / f"w{w}.log", "w"), stderr=subprocess.STDOUT,
+                env=dict(os.environ, PYTHONPATH=ROOT, PSD_ASYNC_DEAD_S="3")))
         rcs = [p.wait(timeout=240) for p in procs]
         logs = [open(tmp_path / f"w{w}.log").read() for w in range(3)]
         assert rcs[2] == -9 and rcs[0] == 0 and rcs[1] == 0, (rcs, logs[0][-3000:], logs[1][-3000:])
@@ -252,6 +253,16 @@ def _crash_recovery(tmp_path, device):
 @pytest.mark.slow
 def test_crash_recovery_from_canonical_checkpoint(tmp_path):
     _crash_recovery(tmp_path, "cpu")
+
+
+@pytest.mark.slow
+def test_async_plane_crash_recovery(tmp_path):
+    """the same SIGKILL scenario on the asynchronous peer-memory plane. The
+    dead rank's engine heartbeat stops; within PSD_ASYNC_DEAD_S (3 s here, not the 600 s SSP
+    deadline) every survivor's SSP wait fails, the survivors abort their engines (no barrier with
+    the dead peer), rebuild a 2-rank AsyncPS from the canonical checkpoint and finish; K-batch rounds
+    at bound 0 are the synchronous steps, so they match the same fp32 replay."""
+    _crash_recovery(tmp_path, "cpu", plane="async")
 
 
 @pytest.mark.gpu
