@@ -325,6 +325,14 @@ def main():
                        "staleness_bound": a.staleness, "optimizer": f"{opt_kind} fused gfx950", "bucket_mb": a.bucket_mb,
                        "pull_dtype": pull_dtype, "fp8_compute": fp8_compute, "tunableop": tunable_mode,
                        "transport": ps.t.name, "hipgraph": bool(tr.graphs), "graph_error": tr.graph_error},
+            "ps_semantics": (f"K-batch async SGD, K={ps.round} pushes per step (staleness bound {a.staleness}: "
+                             f"gradients may be up to {a.staleness + 1} steps stale; at bound 0 exactly synchronous)"
+                             if mode == "async" else
+                             (f"synchronous, fixed {a.staleness}-step gradient delay" if a.staleness else "synchronous")),
+            "vs_baseline_note": ("vs the reference-semantics baseline (sync barrier, gRPC fp32 tensors, one host PS, "
+                                 "285.1 img/s x workers, tools/reference_baseline.py); this run's weights may be "
+                                 f"up to {a.staleness + 1} steps stale (SSP bound {a.staleness})"
+                                 if a.model in REF_BASELINE else None),
             "staleness_p50": p50, "staleness_hist": hist, "final_loss": round(final_loss, 4),
             "params_finite": params_finite, "comm_probe_busbw_GBps": probe, "async_plane_bw": async_bw,
             "warmup_s": round(t_w, 2), "peak_mem_gb": round(mem_peak / 2**30, 2),

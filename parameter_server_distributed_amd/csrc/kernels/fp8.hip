@@ -204,6 +204,26 @@ __global__ __launch_bounds__(256) void quant_delayed_kernel(const void* __restri
   if (threadIdx.x == 0) atomicMax(reinterpret_cast<unsigned int*>(hist + 1), __float_as_uint(m));
 }
 
+// Guard of the delayed path: when the recorded amax it scaled with was 0 or not finite (a tensor
+// role that was all zeros on the previous step -- e.g. the dY of a zero-initialised bn3 -- or
+// whose previous amax overflowed), every element would have saturated; re-quantise with this
+// pass's own amax (hist[1], complete: same stream) instead. A valid history returns at once.
+template <int DT, bool E5>
+__global__ __launch_bounds__(256) void requant_unscaled_kernel(const void* __restrict__ x, int64_t n,
+                                                               const float* hist, float fp8_max,
+                                                               uint8_t* __restrict__ out, float* __restrict__ scale_inv) {
+  const float h0 = hist[0];
+  if (h0 > 0.f && h0 <= 3.0e38f) return;  // NaN fails the first test
+  const float a = fmaxf(hist[1], 1e-12f);
+  const float scale = fp8_max / a;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *scale_inv = a / fp8_max;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float f = (DT == DT_BF16) ? bf16_to_f32(static_cast<const uint16_t*>(x)[i]) : static_cast<const float*>(x)[i];
+    out[i] = f32_to_f8_<E5>(f * scale);
+  }
+}
+
 __global__ void amax_roll_kernel(float* hist) {
   hist[0] = hist[1];
   hist[1] = 0.f;
@@ -222,6 +242,15 @@ hipError_t launch_quant_fp8_delayed(const void* x, int32_t dt, int64_t n, float*
   else if (dt == DT_F32)
     hipLaunchKernelGGL((quant_delayed_kernel<DT_F32, false>), dim3(gq), dim3(256), 0, st, x, n, hist, fp8_max, margin, out, scale_inv);
   else return hipErrorInvalidValue;
+  const int gr = stream_grid(n, 256) < 256 ? stream_grid(n, 256) : 256;
+  if (dt == DT_BF16 && e5m2)
+    hipLaunchKernelGGL((requant_unscaled_kernel<DT_BF16, true>), dim3(gr), dim3(256), 0, st, x, n, hist, fp8_max, out, scale_inv);
+  else if (dt == DT_BF16)
+    hipLaunchKernelGGL((requant_unscaled_kernel<DT_BF16, false>), dim3(gr), dim3(256), 0, st, x, n, hist, fp8_max, out, scale_inv);
+  else if (e5m2)
+    hipLaunchKernelGGL((requant_unscaled_kernel<DT_F32, true>), dim3(gr), dim3(256), 0, st, x, n, hist, fp8_max, out, scale_inv);
+  else
+    hipLaunchKernelGGL((requant_unscaled_kernel<DT_F32, false>), dim3(gr), dim3(256), 0, st, x, n, hist, fp8_max, out, scale_inv);
   hipLaunchKernelGGL(amax_roll_kernel, dim3(1), dim3(1), 0, st, hist);
   return hipGetLastError();
 }

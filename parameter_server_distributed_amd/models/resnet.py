@@ -65,6 +65,12 @@ class Bottleneck(nn.Module):
         self.bn3 = FusedBatchNorm2d(planes * self.expansion, relu=True)  # relu(bn3(conv3) + identity)
         self.downsample = downsample
         self.fuse_residual_grad = True
+        # each convolution's consumer BN: the conv epilogue can reduce its batch statistics
+        # (ops/conv.py, kernels/convn.hip); plain attributes, not submodules
+        for conv, bn in ((self.conv1, self.bn1), (self.conv2, self.bn2), (self.conv3, self.bn3)):
+            object.__setattr__(conv, "_psd_bn", bn)
+        if downsample is not None and len(downsample) == 2:
+            object.__setattr__(downsample[0], "_psd_bn", downsample[1])
         if fp8:  # bn1 / bn2 quantise their outputs for the fp8 conv2 / conv3 in their apply pass
             # (plain attributes: object.__setattr__ keeps the consumer from becoming a submodule)
             object.__setattr__(self.bn1, "_psd_q8_consumer", self.conv2)

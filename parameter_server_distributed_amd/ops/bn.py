@@ -48,6 +48,19 @@ def _q8_args(mod, x: torch.Tensor) -> dict:
             "q8_margin": sc.margin}
 
 
+def _stats_args(mod, x: torch.Tensor) -> dict:
+    """The batch-statistics partials the producing convolution reduced in its epilogue for exactly
+    this tensor (ops/conv.py, kernels/convn.hip), as bn_fwd arguments; consumed once."""
+    pend = getattr(mod, "_psd_stats_pending", None)
+    if pend is None:
+        return {}
+    mod._psd_stats_pending = None
+    y, part, rows = pend
+    if y.data_ptr() != x.data_ptr() or y.shape != x.shape or y.stride() != x.stride():
+        return {}
+    return {"part_in": part, "part_rows": rows}
+
+
 def _q8_hand_over(mod, y: torch.Tensor, kw: dict) -> None:
     if kw:
         mod._psd_q8_consumer._psd_q8_pending = (y, kw["q8_out"], kw["q8_sinv"])
@@ -61,7 +74,8 @@ class _FusedBNFn(torch.autograd.Function):
         q8 = _q8_args(mod, x)
         y, mean, invstd, ss, mbits = C.bn_fwd(x, weight, bias, mod.running_mean, mod.running_var, residual, mod.relu,
                                               True, mod.momentum if mod.momentum is not None else 0.1, mod.eps,
-                                              mod.num_batches_tracked, None, mask_out=mod.relu and has_res, **q8)
+                                              mod.num_batches_tracked, None, mask_out=mod.relu and has_res, **q8,
+                                              **_stats_args(mod, x))
         _q8_hand_over(mod, y, q8)
         ctx.relu = mod.relu
         ctx.has_res = residual is not None
@@ -108,11 +122,12 @@ class _BNAddBNReluFn(torch.autograd.Function):
         C = native()
         mom = lambda m: m.momentum if m.momentum is not None else 0.1  # noqa: E731
         _, mean_d, invstd_d, ss_d, _ = C.bn_fwd(r, wd, bd, bnd.running_mean, bnd.running_var, None, False, True,
-                                                mom(bnd), bnd.eps, bnd.num_batches_tracked, None, stats_only=True)
+                                                mom(bnd), bnd.eps, bnd.num_batches_tracked, None, stats_only=True,
+                                                **_stats_args(bnd, r))
         q8 = _q8_args(bn3, x)
         y, mean, invstd, _, mbits = C.bn_fwd(x, w3, b3, bn3.running_mean, bn3.running_var, r, True, True, mom(bn3),
                                              bn3.eps, bn3.num_batches_tracked, None, mask_out=True, residual_ss=ss_d,
-                                             **q8)
+                                             **q8, **_stats_args(bn3, x))
         _q8_hand_over(bn3, y, q8)
         ctx.bn3, ctx.bnd = bn3, bnd
         ctx.save_for_backward(x, mbits, w3, mean, invstd, r, wd, mean_d, invstd_d)
@@ -195,6 +210,7 @@ class FusedBatchNorm2d(nn.BatchNorm2d):
         super().__init__(num_features, eps=eps, momentum=momentum)
         self.relu = relu
         self._psd_pending_dr: list = []
+        self._psd_stats_pending = None  # (conv output, statistics partials, rows) from the producing conv
 
     def psd_direct_grad_params(self):
         return [self.weight, self.bias]

@@ -108,6 +108,74 @@ def _take_q8(mod, x: torch.Tensor):
     return q, sinv
 
 
+# ---------------------------------------------------------------------------------------------
+# narrow-output implicit-GEMM kernel (kernels/convn.hip) + the consumer BN's statistics
+
+
+def _psdn_ok(cin: int, cout: int) -> bool:
+    """convn_'s contract: C a power of two >= 64, Cout 64 / 128 / a multiple of 256."""
+    return cin >= 64 and (cin & (cin - 1)) == 0 and (cout in (64, 128) or cout % 256 == 0) and \
+        _at.enabled("PSD_CONVN")
+
+
+def _bn_consumer(mod):
+    """The training-mode FusedBatchNorm2d that consumes ``mod``'s output (wired by the model as
+    ``_psd_bn``), whose batch statistics the convolution epilogue can reduce, or None."""
+    bn = getattr(mod, "_psd_bn", None) if mod is not None else None
+    if (bn is None or not bn.training or bn.running_mean is None or not torch.is_grad_enabled()
+            or not _at.enabled("PSD_CONVN_STATS")):
+        return None
+    return bn
+
+
+def _convn_variants(x, w2, k: int, stride: int, pad: int, bn=None) -> dict:
+    """{"psdn<v>": fn} over the kernel's tile variants; fn() -> the channels_last conv output. With a
+    consumer ``bn`` every call also reduces the BN's statistics partials in its epilogue and hands
+    them to the BN (``_psd_stats_pending``: its forward then skips the statistics pass)."""
+    C = _native()
+    n, _, h, w = x.shape
+    cout = w2.shape[0]
+    ho, wo = (h + 2 * pad - k) // stride + 1, (w + 2 * pad - k) // stride + 1
+    M = n * ho * wo
+
+    def make(v):
+        def fn():
+            out = torch.empty(M, cout, device=x.device, dtype=x.dtype)
+            part = None
+            if bn is not None:
+                part = torch.empty(C.convn_stats_rows(M), 2, cout, device=x.device, dtype=torch.float32)
+            rows = C.convn_(x, w2, out, k, k, stride, pad, part=part,
+                            shift=bn.running_mean if bn is not None else None, variant=v)
+            if rows == 0:
+                raise RuntimeError("convn_ declined a shape _psdn_ok accepted")
+            y = _from_2d(out, n, ho, wo)
+            if bn is not None:
+                bn._psd_stats_pending = (y, part, rows)
+            return y
+        return fn
+
+    return {f"psdn{v}": make(v) for v in range(C.convn_variants(cout))}
+
+
+def _with_bn_reduce(fn, bn):
+    """Timing twin of a library candidate: its output plus the BN statistics pass it leaves to the
+    BN (so the autotuner compares the fused kernel against library conv + reduce)."""
+    def g():
+        y = fn()
+        _native().bn_reduce_(y, bn.running_mean)
+        return y
+    return g
+
+
+def _route(key: tuple, cands: dict, default: str, bn=None) -> str:
+    """Autotuned choice among ``cands``; with a consumer BN the library candidates are timed with
+    the statistics pass they leave behind (the psdn ones reduce it in their epilogue)."""
+    if bn is None:
+        return _at.choose(key, cands, default)
+    timed = {name: (fn if name.startswith("psdn") else _with_bn_reduce(fn, bn)) for name, fn in cands.items()}
+    return _at.choose(key + ("bnstats",), timed, default)
+
+
 class DelayedScale:
     """Delayed fp8 scaling for one tensor role of one layer (its input activations, or its output
     gradient): each call quantises with the amax the previous call recorded (times ``margin``) and
@@ -185,7 +253,11 @@ class _Conv1x1Fn(torch.autograd.Function):
         cands = {"gemm": gemm, "miopen": miopen}
         if _psd_ok(cin, cout):
             cands["psd"] = psd
-        return cands[_choose(key, cands)]()
+        bn = None
+        if _psdn_ok(cin, cout):
+            bn = _bn_consumer(mod)
+            cands.update(_convn_variants(x, w2 if w2.is_contiguous() else w2.contiguous(), 1, 1, 0, bn))
+        return cands[_route(("conv1x1",) + key, cands, "miopen", bn)]()
 
     @staticmethod
     def backward(ctx, dy):
@@ -225,6 +297,8 @@ class _Conv1x1Fn(torch.autograd.Function):
             cands = {"gemm": gemm, "miopen": miopen}
             if _psd_ok(cout, cin):
                 cands["psd"] = psd
+            if _psdn_ok(cout, cin):  # dX = dY . W as a 1x1 convolution of dY with W^T [cin, cout]
+                cands.update(_convn_variants(dy, w2.t().contiguous(), 1, 1, 0))
             dx = cands[_choose(key, cands)]()
         if need_w:
             def miopen_w():
@@ -353,7 +427,7 @@ class _ConvFn(torch.autograd.Function):
             if y is not None:
                 return y
 
-        if not _igemm_ok(cin, cout):
+        if not _igemm_ok(cin, cout) and not _psdn_ok(cin, cout):
             return miopen()
         w2 = weight.permute(0, 2, 3, 1).reshape(cout, k * k * cin)
         if not w2.is_contiguous():
@@ -363,9 +437,15 @@ class _ConvFn(torch.autograd.Function):
             y = _igemm(x, w2, k, stride, pad)
             return miopen() if y is None else y
 
+        cands = {"miopen": miopen}
+        if _igemm_ok(cin, cout):
+            cands["igemm"] = igemm
+        bn = None
+        if _psdn_ok(cin, cout):
+            bn = _bn_consumer(mod)
+            cands.update(_convn_variants(x, w2, k, stride, pad, bn))
         key = ("fwd", n, cin, h, w, cout, k, stride)
-        return igemm() if _at.choose(("conv",) + key, {"igemm": igemm, "miopen": miopen}, "miopen") == "igemm" \
-            else miopen()
+        return cands[_route(("conv",) + key, cands, "miopen", bn)]()
 
     @staticmethod
     def backward(ctx, dy):
@@ -389,7 +469,7 @@ class _ConvFn(torch.autograd.Function):
                 dx = _igemm_fp8(dy, wf, k, 1, pad, e5m2=True, scaler=ctx.f8[1])
                 if dx is None:
                     dx = miopen()
-            elif stride == 1 and _igemm_ok(cout, cin) and 2 * pad == k - 1:
+            elif stride == 1 and (_igemm_ok(cout, cin) or _psdn_ok(cout, cin)) and 2 * pad == k - 1:
                 # dX = conv(dY, W'), W'[ci, r, s, co] = W[co, ci, k-1-r, k-1-s]: same kernel, same padding
                 wf = weight.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, k * k * cout).contiguous()
 
@@ -397,9 +477,13 @@ class _ConvFn(torch.autograd.Function):
                     y = _igemm(dy, wf, k, 1, pad)
                     return miopen() if y is None else y
 
+                cands = {"miopen": miopen}
+                if _igemm_ok(cout, cin):
+                    cands["igemm"] = igemm
+                if _psdn_ok(cout, cin):
+                    cands.update(_convn_variants(dy, wf, k, 1, pad))
                 key = ("dgrad", n, cin, h, w, cout, k, stride)
-                dx = igemm() if _at.choose(("conv",) + key, {"igemm": igemm, "miopen": miopen},
-                                           "miopen") == "igemm" else miopen()
+                dx = cands[_at.choose(("conv",) + key, cands, "miopen")]()
             else:
                 dx = miopen()
         if ctx.needs_input_grad[1]:

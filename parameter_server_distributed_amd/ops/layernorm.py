@@ -26,6 +26,7 @@ class _AddLNFn(torch.autograd.Function):
         shp = x.shape
         y, s, mean, rstd = C.ln_fwd(x.contiguous(), h.contiguous(), weight, bias, mod.eps, p, mod.seed, mod.step)
         ctx.mod, ctx.p, ctx.x_grad_to = mod, p, x_grad_to
+        ctx.tok = getattr(x_grad_to, "_psd_tok", None) if x_grad_to is not None else None
         ctx.save_for_backward(s, mean, rstd, weight)
         return y.view(shp)
 
@@ -41,7 +42,7 @@ class _AddLNFn(torch.autograd.Function):
         if ctx.x_grad_to is not None:
             # residual-branch gradient handed to the Linear that also consumes x: its dgrad GEMM
             # accumulates onto it (beta = 1) instead of autograd adding the two [M, H] gradients
-            ctx.x_grad_to._psd_pending_dx.append(dx)
+            ctx.x_grad_to._psd_pending_dx.append((ctx.tok, dx))
             return None, dh.view(dy.shape), dg, db, None, None, None
         return dx.view(dy.shape), dh.view(dy.shape), dg, db, None, None, None
 

@@ -103,6 +103,11 @@ class _LinearFn(torch.autograd.Function):
             _route(("fwd", M, x2.shape[1], N, act, bias is not None), mfma, blas, y)()
         ctx.act = act
         ctx.mod = mod
+        # per-forward token: a residual LayerNorm that hands this forward's input gradient over
+        # records it, and backward only takes a hand-over carrying its own token (a backward that
+        # stopped between the two -- an exception, autograd.grad on a partial graph -- can never
+        # leave a stale gradient for the next step)
+        ctx.tok = mod._psd_tok = getattr(mod, "_psd_tok", 0) + 1
         ctx.has_bias = bias is not None
         ctx.in_shape = shp
         ctx.save_for_backward(x2, weight, y if act == 1 else aux)
@@ -130,9 +135,16 @@ class _LinearFn(torch.autograd.Function):
         M, K, N = x2.shape[0], x2.shape[1], w.shape[0]
         dx = None
         pend = ctx.mod._psd_pending_dx
-        if ctx.needs_input_grad[0] and pend:
+        got = None
+        while pend:  # older hand-overs (of an aborted backward) are dropped
+            tok, g = pend.pop()
+            if tok == ctx.tok:
+                got = g
+                break
+        pend.clear()
+        if ctx.needs_input_grad[0] and got is not None:
             # x's other gradient (a residual LayerNorm's, ops/layernorm.py): accumulated by the GEMM
-            dx = pend.pop().view(M, K)
+            dx = got.view(M, K)
             dx.addmm_(dy2, w)
             dx = dx.view(ctx.in_shape)
         elif ctx.needs_input_grad[0]:

@@ -275,6 +275,8 @@ class ElasticTrainer:
             if plan.restore:
                 ps.load_canonical_state(self._load_checkpoint(ps))
                 step = plan.step
+                # the steps after the checkpoint are recomputed: their first losses are void
+                losses = [(s_, l_) for (s_, l_) in losses if s_ <= step]
             elif plan.gen > 0:  # state handed over by the previous generation's leader (new rank 0)
                 ps.load_canonical_state(self._broadcast_state(ps, state))
             state = None
@@ -286,7 +288,7 @@ class ElasticTrainer:
                 while step < self.steps and leavers is None:
                     loss = tr.step()
                     step += 1
-                    losses.append(loss.detach().clone())
+                    losses.append((step, loss.detach().clone()))
                     if self.on_step is not None:
                         self.on_step(step, loss, plan)
                     if self.checkpoint_every and step % self.checkpoint_every == 0 and step < self.steps:
@@ -311,7 +313,7 @@ class ElasticTrainer:
                 self.recoveries += 1
                 result["recovered_at"] = result.get("recovered_at", []) + [step]
                 if self.agent.worker_id not in plan.members:
-                    result["losses"] = [float(x) for x in losses]
+                    result["losses"] = [float(x) for _, x in losses]
                     self.agent.leave()
                     return result
                 continue
@@ -349,13 +351,14 @@ class ElasticTrainer:
             if self.agent.worker_id not in plan.members:
                 self.log.info("left the job at step %d (handed over to %s)", step, plan.members)
                 result["left_at"] = step
-                result["losses"] = [float(x) for x in losses]
+                result["losses"] = [float(x) for _, x in losses]
                 self.agent.leave()
                 return result
         result["finished_at"] = step
         result["resizes"] = self.resizes
         result["recoveries"] = self.recoveries
-        result["losses"] = [float(x) for x in losses]
+        result["losses"] = [float(x) for _, x in losses]
+        result["loss_steps"] = [s_ for s_, _ in losses]
         self.agent.leave()
         return result
 

@@ -118,3 +118,43 @@ def test_bn_fwd_from_conv_partials_matches_fp32(gpu, relu):
     torch.testing.assert_close(rv1, rv2, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(yb.float(), ref, rtol=1e-2, atol=2e-2)
     assert int(cnt) == 1
+
+
+@pytest.mark.parametrize("k,cin,cout,stride", [(3, 64, 64, 1), (1, 256, 64, 1), (1, 64, 256, 1), (3, 128, 128, 2)])
+def test_conv_bn_module_psdn_route_matches_fp32(gpu, monkeypatch, k, cin, cout, stride):
+    """The model-level route: ConvNHWC / Conv1x1 forced onto the narrow kernel (forward, stride-1
+    bwd-data) with the consumer FusedBatchNorm2d's statistics reduced in the conv epilogue, vs an
+    fp32 nn.Conv2d + F.batch_norm (+ ReLU) on the same bf16 operands: output, running stats and the
+    input / weight / BN gradients."""
+    from parameter_server_distributed_amd.ops.bn import FusedBatchNorm2d
+    from parameter_server_distributed_amd.ops.conv import Conv1x1, ConvNHWC
+
+    monkeypatch.setenv("PSD_AUTOTUNE_FORCE", "psdn0")
+    torch.manual_seed(3)
+    conv = (Conv1x1(cin, cout) if k == 1 and stride == 1 else ConvNHWC(cin, cout, k, stride))
+    conv = conv.to(gpu, torch.bfloat16).to(memory_format=torch.channels_last)
+    bn = FusedBatchNorm2d(cout, relu=True).to(gpu)
+    bn.weight.data = bn.weight.data.to(torch.bfloat16)
+    bn.bias.data = bn.bias.data.to(torch.bfloat16)
+    object.__setattr__(conv, "_psd_bn", bn)
+    ref = torch.nn.Conv2d(cin, cout, k, stride=stride, padding=k // 2, bias=False).to(gpu)
+    ref.weight.data.copy_(conv.weight.float())
+    x = torch.randn(8, cin, 16, 16, device=gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    xr = x.detach().float().clone().requires_grad_(True)
+    rm, rv = bn.running_mean.clone(), bn.running_var.clone()
+    gw = bn.weight.detach().float().clone().requires_grad_(True)
+    gb = bn.bias.detach().float().clone().requires_grad_(True)
+    y = bn(conv(x))
+    assert bn._psd_stats_pending is None  # handed over and consumed
+    yr = F.relu(F.batch_norm(ref(xr), rm, rv, gw, gb, True, 0.1, 1e-5))
+    torch.testing.assert_close(y.float(), yr.detach(), rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(bn.running_mean, rm, rtol=1e-2, atol=1e-3)
+    torch.testing.assert_close(bn.running_var, rv, rtol=1e-2, atol=1e-3)
+    g = torch.randn_like(yr)
+    y.backward(g.to(torch.bfloat16))
+    yr.backward(g)
+    for got, want in ((x.grad, xr.grad), (conv.weight.grad, ref.weight.grad), (bn.weight.grad, gw.grad),
+                      (bn.bias.grad, gb.grad)):
+        err = float((got.float() - want).abs().max())
+        assert err < 0.05 * float(want.abs().max()) + 1e-3, (err, float(want.abs().max()))

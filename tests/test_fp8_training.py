@@ -98,3 +98,25 @@ def test_bn_apply_writes_the_consumers_fp8_input(gpu, monkeypatch):
     assert float(conv._f8[0].hist[0]) == amax and float(conv._f8[0].hist[1]) == 0.0
     out = conv(y)  # consumes the hand-over
     assert conv._psd_q8_pending is None and out.shape == (4, 512, 14, 14)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("e5m2", [False, True])
+def test_delayed_scale_recovers_from_zero_history(gpu, e5m2):
+    """a tensor role that was all zeros on the previous step (the dY of a zero-initialised
+    bn3 at step 0) recorded amax 0; the next call must not scale by fp8_max / 1e-12 (every element
+    saturated, the dequantised gradient ~1e-12) but fall back to its own amax."""
+    from parameter_server_distributed_amd.ops.conv import DelayedScale
+
+    sc = DelayedScale(2.0)
+    z = torch.zeros(4096, device=gpu, dtype=torch.bfloat16)
+    sc.quantize(z, e5m2)
+    sc.quantize(z, e5m2)  # history now holds amax 0
+    assert float(sc.hist[0]) == 0.0
+    x = (torch.randn(4096, device=gpu) * 3e-3).to(torch.bfloat16)
+    q, sinv = sc.quantize(x, e5m2)
+    deq = q.float() * sinv
+    rel = float((deq - x.float()).norm() / x.float().norm())
+    assert rel < (0.15 if e5m2 else 0.08), rel
+    q2, sinv2 = sc.quantize(x, e5m2)  # now a valid delayed history: the same scale as just-in-time
+    assert float((q2.float() * sinv2 - x.float()).norm() / x.float().norm()) < (0.15 if e5m2 else 0.08)
