@@ -76,7 +76,9 @@ def parse():
                     help="async: apply-on-arrival PS shards over xGMI peer memory with an SSP bound "
                          "(parallel/async_ps.py); collective: lock-step RCCL reduce-scatter/all-gather with a "
                          "fixed S-step gradient delay (parallel/collective_ps.py)")
-    ap.add_argument("--bucket-mb", type=float, default=16.0)
+    ap.add_argument("--bucket-mb", type=float, default=0.0,
+                    help="push bucket size; 0 (default): at N > 1 probe the per-link p2p bandwidth vs size over "
+                         "RCCL before building the PS and take the knee (parallel/bucketing.py), 16 MB at N = 1")
     ap.add_argument("--fp8-compute", type=int, default=-1,
                     help="fp8 (e4m3 MFMA) forward of the bottleneck convolutions, bf16 backward "
                          "(1/0; -1: on for Wide-ResNet-101-2, the BASELINE 'CDNA4 fp8 MFMA' config)")
@@ -197,6 +199,18 @@ def main():
         shards = world - world // 2
     else:
         shards = max(1, min(a.ps_shards, world))
+    bucket_probe = None
+    if a.bucket_mb <= 0:
+        a.bucket_mb = 16.0
+        if world > 1 and a.backend == "nccl":
+            from parameter_server_distributed_amd.parallel import bucketing
+
+            try:
+                bucket_probe = bucketing.probe_p2p(dev)
+                model_mb = sum(p.numel() for p in spec.model.parameters()) * 2 / 2**20
+                a.bucket_mb = bucketing.choose_bucket_mb(bucket_probe, model_mb)
+            except Exception as e:  # noqa: BLE001 -- a diagnostic must not cost the run
+                bucket_probe = {"error": str(e)[:200]}
     pull_dtype = a.pull_dtype or ("fp8" if a.model.startswith("wide") else "bf16")
     mode = a.ps_mode if pull_dtype == "bf16" else "collective"  # fp8-published weights: collective plane
     fallback = None
@@ -333,6 +347,7 @@ def main():
                                  "285.1 img/s x workers, tools/reference_baseline.py); this run's weights may be "
                                  f"up to {a.staleness + 1} steps stale (SSP bound {a.staleness})"
                                  if a.model in REF_BASELINE else None),
+            "bucket_mb_chosen": a.bucket_mb, "bucket_probe_GBps": bucket_probe,
             "staleness_p50": p50, "staleness_hist": hist, "final_loss": round(final_loss, 4),
             "params_finite": params_finite, "comm_probe_busbw_GBps": probe, "async_plane_bw": async_bw,
             "warmup_s": round(t_w, 2), "peak_mem_gb": round(mem_peak / 2**30, 2),
