@@ -46,6 +46,13 @@ def main(argv=None):
     ap.add_argument("--elastic-ckpt-every", type=int, default=0, help="elastic: checkpoint period (steps)")
     ap.add_argument("--collective-timeout-s", type=float, default=0.0,
                     help="elastic: bound on any collective of a generation (0: the agent timeout)")
+    ap.add_argument("--ps-plane", default="collective", choices=["collective", "async"],
+                    help="elastic: lock-step RCCL plane, or the asynchronous peer-memory plane (K-batch rounds, SSP "
+                         "bound --staleness; one node)")
+    ap.add_argument("--fp8-compute", action="store_true",
+                    help="fp8 (e4m3 MFMA) forward / e5m2 bwd-data of the ResNet bottleneck convolutions "
+                         "(BASELINE config 5: Wide-ResNet-101-2 fp8)")
+    ap.add_argument("--image-size", type=int, default=224, help="ResNet models: synthetic image size")
     from ..utils.config import apply_config
 
     apply_config(ap, argv)
@@ -92,13 +99,23 @@ def main(argv=None):
     return 0 if ok_all else 1
 
 
+def build_model(a, dev, dtype):
+    """The worker's model from the CLI flags (``--fp8-compute``: fp8 bottleneck convolutions)."""
+    from .. import models
+
+    kw = {}
+    if a.model.lower().replace("-", "_") in ("resnet50", "resnet101", "wide_resnet101_2", "wrn101"):
+        kw = dict(fp8=bool(a.fp8_compute), image_size=a.image_size)
+    return models.build(a.model, dev, dtype, **kw)
+
+
 def elastic_main(a) -> int:
     """Elastic worker on the collective data plane: prints the reference's per-iteration lines
     (``worker <id> iter <it> done=true``) with the generation / world it ran in."""
     import torch
 
-    from .. import models
     from ..ops.optim import OptimConfig
+    from ..parallel.async_ps import AsyncPS
     from ..parallel.collective_ps import CollectivePS
     from ..runtime.elastic import ElasticAgent, ElasticTrainer
     from ..runtime.trainer import Trainer
@@ -108,13 +125,16 @@ def elastic_main(a) -> int:
         torch.cuda.set_device(dev)
     torch.manual_seed(0)
     dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
-    spec = models.build(a.model, dev, dtype)
+    spec = build_model(a, dev, dtype)
     batch = spec.make_batch(a.batch, dev, seed=1000 + a.worker_id)
     optim = OptimConfig(a.optimizer, lr=a.lr, momentum=0.9)
     agent = ElasticAgent(a.coordinator, a.worker_id, heartbeat_s=min(a.heartbeat_s, 1.0))
 
     def make_ps(model, transport):
         shards = a.ps_shards if 0 < a.ps_shards <= transport.world else transport.world
+        if a.ps_plane == "async":
+            return AsyncPS(model, optim, num_shards=shards, staleness=a.staleness, bucket_mb=a.bucket_mb, device=dev,
+                           overlap=not spec.tied_weights, param_dtype=dtype)
         return CollectivePS(model, optim, transport, num_shards=shards, staleness=a.staleness,
                             bucket_mb=a.bucket_mb, device=dev, overlap=not spec.tied_weights,
                             grad_dtype=dtype, param_dtype=dtype, pull_dtype=a.pull_dtype)

@@ -87,8 +87,6 @@ def build(name: str, device, dtype=torch.bfloat16, num_classes: int | None = Non
 
         m = prepare(BertForMLM(**{k: v for k, v in kw.items() if k in ("layers", "hidden", "heads", "vocab")}),
                     device, dtype)
-        if dtype == torch.bfloat16:  # LayerNorm / embedding buffers follow the compute dtype
-            pass
         seq = kw.get("seq_len", 128)
 
         def make(batch, device, seed=0):

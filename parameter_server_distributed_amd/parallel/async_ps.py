@@ -278,11 +278,15 @@ class AsyncPS:
     def selftest(self):
         """Collective start-up check of the peer-memory paths on this node (before any training):
         every worker DMA-writes a known pattern into its inbox on every shard owner, and every
-        owner verifies what landed; every worker pulls the version-0 snapshots and compares them
-        with its own initial weights. Raises on any mismatch on any rank (so a caller can fall
-        back to the collective plane instead of training on a broken path)."""
+        owner verifies what landed; every worker pulls the version-0 snapshots and compares each
+        shard with its owner's published checksum (the ranks' weights need not agree yet: an elastic
+        joiner's are replaced by load_canonical_state next). Raises on any mismatch on any rank (so a
+        caller can fall back to the collective plane instead of training on a broken path)."""
         dev = self.device
         ok, why = True, ""
+        for k in self.my_shards:  # the snapshot each owner published: bf16/fp32(master)
+            v = self.master[k].to(self.param_dtype).double()
+            self.store.set(f"{self._key}/ck/{k}", f"{float(v.sum())!r} {float(v.abs().sum())!r}")
         if self.is_worker:
             pat = (torch.arange(self.total, device=dev) % 251 + (self.rank + 1)).to(self.param_dtype)
             self.engine.push(0, pat, 0, self.total, self._stream_ptr())
@@ -290,8 +294,13 @@ class AsyncPS:
             self.engine.pull(0, got, self._stream_ptr())
             if self.is_cuda:
                 torch.cuda.synchronize(dev)
-            if not torch.equal(got, self.params_flat):
-                ok, why = False, f"rank {self.rank}: pulled snapshot != initial weights"
+            for k in range(self.P):
+                self.store.wait([f"{self._key}/ck/{k}"])
+                want_s, want_a = (float(x) for x in self.store.get(f"{self._key}/ck/{k}").decode().split())
+                sl = got.narrow(0, self.shard_off[k], self.shard_len[k]).double()
+                if abs(float(sl.sum()) - want_s) > 1e-6 * max(want_a, 1.0) or \
+                        abs(float(sl.abs().sum()) - want_a) > 1e-6 * max(want_a, 1.0):
+                    ok, why = False, f"rank {self.rank}: pulled shard {k} != its owner's snapshot"
         if os.environ.get("PSD_ASYNC_SELFTEST_FAIL_RANK") == str(self.rank):  # fault injection (tests)
             ok, why = False, f"rank {self.rank}: injected self-test failure"
         self._barrier("selftest-push")
@@ -703,6 +712,13 @@ class AsyncPS:
                 out.append((o, c, k))
                 c += k
         return out, c
+
+    def canonical_keys(self) -> list:
+        return ["master", "state1", "state2"][: 1 + self.cfg.num_states]
+
+    def dyn_template(self) -> torch.Tensor:
+        """A tensor shaped like the step-scalar block (the receive buffer of a broadcast)."""
+        return torch.zeros(8, dtype=torch.int32, device=self.device)
 
     def canonical_state(self, root: int) -> dict | None:
         """Collective: drain, then gather every shard's fp32 master + optimizer state onto rank

@@ -431,14 +431,18 @@ class ElasticTrainer:
     def _broadcast_state(self, ps, state):
         """New rank 0 holds the canonical state; give every rank a copy."""
         idx, n = ps._canon_index()
-        keys = ["master"] + [k for k, t in (("state1", ps.state1), ("state2", ps.state2)) if t is not None]
+        if hasattr(ps, "canonical_keys"):  # AsyncPS: optimizer states from its config
+            keys = ps.canonical_keys()
+        else:
+            keys = ["master"] + [k for k, t in (("state1", ps.state1), ("state2", ps.state2)) if t is not None]
         out = {}
         for k in keys:
             t = state[k].to(self.device) if dist.get_rank() == 0 else torch.empty(n, dtype=torch.float32,
                                                                                   device=self.device)
             dist.broadcast(t, 0)
             out[k] = t
-        d = state["dyn"].to(ps.dyn.t.device) if dist.get_rank() == 0 else torch.empty_like(ps.dyn.t)
+        dyn = ps.dyn_template() if hasattr(ps, "dyn_template") else ps.dyn.t
+        d = state["dyn"].to(dyn.device) if dist.get_rank() == 0 else torch.empty_like(dyn)
         dist.broadcast(d, 0)
         out["dyn"] = d
         return out

@@ -105,15 +105,18 @@ def _wait_exit(pids, timeout):
 
 
 @pytest.mark.slow
-def test_collective_deploy_scale_up_down(tmp_path):
+@pytest.mark.parametrize("plane", ["collective", "async"])
+def test_collective_deploy_scale_up_down(tmp_path, plane):
     """deploy 2 elastic workers, scale up to 3 mid-run (the joiner starts at the step the world
     grew), scale down to 2 (the leaver hands its shards over); survivors run every global step
-    exactly once across three generations and end with identical weights."""
+    exactly once across three generations and end with identical weights. ``async``: the same on
+    the asynchronous peer-memory plane (AsyncPS canonical-state hand-over between generations)."""
     cd = str(tmp_path / "cluster")
     it = 500
     env = dict(os.environ, CLUSTER_DIR=cd, MODE="collective", WORKER_COUNT="2", ITERATIONS=str(it), NUM_GPUS="0",
                COORDINATOR_PORT=str(_port()), PS_PORT=str(_port()),
-               WORKER_FLAGS="--batch 32 --lr 0.01 --staleness 1 --check-every 5", PYTHONPATH=ROOT)
+               WORKER_FLAGS=f"--batch 32 --lr 0.01 --staleness 1 --check-every 5 --ps-plane {plane}",
+               PYTHONPATH=ROOT)
     try:
         subprocess.run(["bash", f"{ROOT}/scripts/deploy.sh"], env=env, check=True, timeout=60, capture_output=True)
         t0 = time.time()
@@ -286,3 +289,20 @@ def test_reshard_resets_grad_scale_to_the_new_world():
     ps.load_canonical_state(sd)
     assert float(ps.dyn.t.view(torch.float32)[1]) == 1.0 / len(ps.worker_ranks)
     assert int(ps.dyn.t[4]) == 7
+
+
+def test_elastic_worker_fp8_compute_flag():
+    """the elastic worker builds BASELINE config 5's model with fp8 compute
+    (``--fp8-compute``): every bottleneck convolution is an fp8-capable module with fp8 on."""
+    from parameter_server_distributed_amd.cli.worker import build_model
+    from parameter_server_distributed_amd.ops.conv import Conv1x1, ConvNHWC
+
+    class A:
+        model, fp8_compute, image_size = "resnet50", True, 32
+
+    spec = build_model(A, CPU, torch.float32)
+    convs = [m for m in spec.model.modules() if isinstance(m, (Conv1x1, ConvNHWC))]
+    assert len(convs) >= 48 and all(m.fp8 for m in convs)
+    A.fp8_compute = False
+    assert not any(m.fp8 for m in build_model(A, CPU, torch.float32).model.modules()
+                   if isinstance(m, (Conv1x1, ConvNHWC)))
