@@ -158,8 +158,9 @@ def elastic_main(a) -> int:
     else:
         print(f"worker {a.worker_id} finished {a.iterations} iterations ({len(res['losses'])} here) in {dt:.2f} s "
               f"after {res['resizes']} membership changes", flush=True)
-        csum = float(sum(p.double().sum() for p in res["params"].values()))
-        print(f"worker {a.worker_id} param checksum {csum:.10e}", flush=True)
+        if res.get("params") is not None:  # (a joiner that arrived after the last step has none)
+            csum = float(sum(p.double().sum() for p in res["params"].values()))
+            print(f"worker {a.worker_id} param checksum {csum:.10e}", flush=True)
     if a.stats_json:
         out = {"history": res["history"], "losses": res["losses"], "seconds": dt,
                "left_at": res.get("left_at"), "finished_at": res.get("finished_at"),
