@@ -65,8 +65,10 @@ def main():
 
 CATEGORIES = [
     ("psd: batchnorm", r"psd::bn_"),
+    ("psd: narrow conv (convn)", r"psd::convn_kernel"),
     ("psd: gemm", r"psd::.*(gemm|colsum|splitk)"),
-    ("psd: optimizer / PS apply", r"psd::.*(fused_apply|optim|multi_reduce|pack_cast|quant|amax|f32_to_bf16)"),
+    ("psd: fp8 quantise / amax", r"psd::.*(quant|amax|requant)"),
+    ("psd: optimizer / PS apply", r"psd::.*(fused_apply|optim|multi_reduce|pack_cast|f32_to_bf16)"),
     ("psd: other (pool, ...)", r"psd::"),
     ("MIOpen/CK conv fwd", r"conv_fwd|igemm_fwd|fwd_gtc"),
     ("MIOpen/CK conv bwd-data", r"bwd_data|igemm_bwd|bwd_gtc"),
