@@ -96,6 +96,17 @@ __device__ __forceinline__ void quad_t4(const f32x4 v, int L, float (&w)[4]) {
   w[3] = o2 ? b1 : q1;
 }
 
+// x[lane ^ 16] / x[lane ^ 32] through the gfx950 half-row / half-wave swaps (VALU, no LDS round
+// trip: the statistics reduction of a one-K-tile convolution is on its critical path)
+__device__ __forceinline__ float xor16(float x, int lane) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float((lane & 16) ? r[0] : r[1]);
+}
+__device__ __forceinline__ float xor32(float x, int lane) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float((lane & 32) ? r[0] : r[1]);
+}
+
 template <int BM, int BN, int WNT, int NSLOT>
 struct Geo {
   static constexpr int WM = BM / 64;         // wave rows (64 output pixels each)
@@ -246,10 +257,10 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
           s1 += ok ? d : 0.f;
           s2 = ok ? fmaf(d, d, s2) : s2;
         }
-      s1 += __shfl_xor(s1, 16);
-      s2 += __shfl_xor(s2, 16);
-      s1 += __shfl_xor(s1, 32);
-      s2 += __shfl_xor(s2, 32);
+      s1 += xor16(s1, lane);
+      s2 += xor16(s2, lane);
+      s1 += xor32(s1, lane);
+      s2 += xor32(s2, lane);
       if (lane < 16) {
         float* pr = a.part + ((int64_t)tm * G::WM + wr) * 2 * a.N;
         const int col = n0 + wc * WNT + j * 16 + cl;
@@ -361,16 +372,16 @@ hipError_t launch_convn(const ConvnArgs& a, hipStream_t st) {
   if (!ok) return hipErrorNotSupported;
   const int v = a.variant >= 0 ? a.variant : default_variant(a, bn);
   switch (bn) {
-    case 64:  // 4 waves of 64x32 | 2 waves of 64x64 | 4 waves of 64x64 (BM 256) | 8 waves of 64x32 (BM 256)
+    case 64:  // 4 waves of 64x32 (3 / 2 slots) | 4 waves of 64x64 (BM 256) | 8 waves of 64x32 (BM 256)
       if (v == 0) return convn_launch_s<128, 64, 32, 3>(a, st);
-      if (v == 1) return convn_launch_s<128, 64, 64, 4>(a, st);
+      if (v == 1) return convn_launch_s<128, 64, 32, 2>(a, st);
       if (v == 2) return convn_launch_s<256, 64, 64, 3>(a, st);
       return convn_launch_s<256, 64, 32, 3>(a, st);
-    case 128:  // 8 waves of 64x32 | 4 waves of 64x64 | 8 waves of 64x64 (BM 256) | 4 waves 64x64, 4 slots
+    case 128:  // 8 waves of 64x32 (3 / 2 slots) | 4 waves of 64x64 | 8 waves of 64x64 (BM 256)
       if (v == 0) return convn_launch_s<128, 128, 32, 3>(a, st);
       if (v == 1) return convn_launch_s<128, 128, 64, 3>(a, st);
       if (v == 2) return convn_launch_s<256, 128, 64, 2>(a, st);
-      return convn_launch_s<128, 128, 64, 4>(a, st);
+      return convn_launch_s<128, 128, 32, 2>(a, st);
     default:  // 8 waves of 64x64, 3 or 2 slots
       if (v == 0) return convn_launch_s<128, 256, 64, 3>(a, st);
       return convn_launch_s<128, 256, 64, 2>(a, st);
