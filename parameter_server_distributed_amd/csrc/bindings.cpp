@@ -71,6 +71,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("convn_", &convn_, py::arg("x"), py::arg("w2"), py::arg("out"), py::arg("R"), py::arg("S"), py::arg("stride"),
         py::arg("pad"), py::arg("part") = py::none(), py::arg("shift") = py::none(), py::arg("variant") = -1);
   m.def("convn_stats_rows", &convn_stats_rows_, py::arg("M"));
+  m.def("convn_bwd_", &convn_bwd_, py::arg("dy"), py::arg("w2"), py::arg("out"), py::arg("R"), py::arg("S"),
+        py::arg("stride"), py::arg("pad"), py::arg("part"), py::arg("variant"), py::arg("mode"), py::arg("bx"),
+        py::arg("bmean"), py::arg("bss") = py::none(), py::arg("bdr") = py::none(), py::arg("bmbits") = py::none());
+  m.def("bn_bwd_pre", &bn_bwd_pre, py::arg("g"), py::arg("x"), py::arg("gamma"), py::arg("save_mean"),
+        py::arg("save_invstd"), py::arg("part"), py::arg("rows"), py::arg("dgamma_out") = py::none(),
+        py::arg("dbeta_out") = py::none());
   m.def("convn_variants", &convn_variants_, py::arg("N"));
   m.def("conv_fwd_", &conv_fwd_, py::arg("x"), py::arg("w2"), py::arg("out"), py::arg("R"), py::arg("S"),
         py::arg("stride"), py::arg("pad"));

@@ -218,6 +218,40 @@ std::vector<at::Tensor> bn_bwd(const at::Tensor& dy_in, const at::Tensor& x_in, 
 }
 
 
+// BN backward whose reduction the producing convolution's bwd-data epilogue already ran
+// (kernels/convn.hip bwd modes): g = the masked gradient (for a residual BN also the residual-branch
+// gradient), part = [rows, 2, C] partials. Returns {dx, dgamma, dbeta}.
+std::vector<at::Tensor> bn_bwd_pre(const at::Tensor& g_in, const at::Tensor& x_in, c10::optional<at::Tensor> gamma,
+                                   const at::Tensor& save_mean, const at::Tensor& save_invstd, const at::Tensor& part,
+                                   int64_t rows, c10::optional<at::Tensor> dgamma_out,
+                                   c10::optional<at::Tensor> dbeta_out) {
+  const c10::DeviceGuard dg(x_in.device());
+  at::Tensor x = nhwc(x_in), g = nhwc(g_in);
+  const int64_t C = channels(x), M = x.numel() / C;
+  TORCH_CHECK(g.sizes() == x.sizes() && g.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16,
+              "psd bn_bwd_pre: g like x (bf16)");
+  TORCH_CHECK(part.scalar_type() == at::kFloat && part.is_contiguous() && rows > 0 && part.numel() >= rows * 2 * C,
+              "psd bn_bwd_pre: part must be fp32 [rows, 2, C]");
+  auto f32 = x.options().dtype(at::kFloat);
+  at::Tensor dx = at::empty_like(x);
+  at::Tensor dgamma, dbeta;
+  if (gamma.has_value() && gamma->defined()) {
+    dgamma = (dgamma_out.has_value() && dgamma_out->defined()) ? *dgamma_out : at::empty({C}, x.options());
+    dbeta = (dbeta_out.has_value() && dbeta_out->defined()) ? *dbeta_out : at::empty({C}, x.options());
+  }
+  at::Tensor coef = at::empty({3 * C}, f32);
+  at::Tensor fold = rows > kFoldRows ? at::empty({(int64_t)kFoldRows * 2 * C}, f32) : at::Tensor();
+  const hipError_t e = launch_bn_bwd_pre(
+      reinterpret_cast<const uint16_t*>(g.data_ptr()), reinterpret_cast<const uint16_t*>(x.data_ptr()),
+      opt_ptr<const uint16_t>(gamma), save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(),
+      part.data_ptr<float>(), (int)rows, fold.defined() ? fold.data_ptr<float>() : nullptr,
+      dgamma.defined() ? reinterpret_cast<uint16_t*>(dgamma.data_ptr()) : nullptr,
+      dbeta.defined() ? reinterpret_cast<uint16_t*>(dbeta.data_ptr()) : nullptr, coef.data_ptr<float>(),
+      reinterpret_cast<uint16_t*>(dx.data_ptr()), M, (int)C, stream_of(x));
+  TORCH_CHECK(e == hipSuccess, "psd bn_bwd_pre: ", hipGetErrorString(e));
+  return {dx, dgamma, dbeta};
+}
+
 // relu(bn3(x) + bnd(xd)) backward (ops/bn.py _BNAddBNReluFn): bn3 through its forward bit-mask, and
 // the downsample BN fed by the residual gradient dr, in one reduce and one elementwise pass.
 // Returns {dx, dxd, dgamma, dbeta, dgamma_d, dbeta_d}.

@@ -252,6 +252,87 @@ int64_t convn_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_
   return stats ? convn_part_rows((int)M, (int)Cout, (int)variant) : 1;
 }
 
+// bwd-data on the narrow kernel with the producing BN's backward reduction in the epilogue
+// (kernels/convn.hip bwd modes): out = g = mask (conv(dy, w2) [+ dr]); part gets the partials.
+// Returns the partial rows written, 0 when the kernel declines (nothing launched).
+int64_t convn_bwd_(const at::Tensor& dy, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride,
+                   int64_t pad, at::Tensor part, int64_t variant, int64_t mode, const at::Tensor& bx,
+                   const at::Tensor& bmean, c10::optional<at::Tensor> bss, c10::optional<at::Tensor> bdr,
+                   c10::optional<at::Tensor> bmbits) {
+  TORCH_CHECK(dy.is_cuda() && dy.dim() == 4 && dy.scalar_type() == at::kBFloat16 &&
+                  dy.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "psd convn_bwd: dy must be a channels_last bf16 device tensor");
+  TORCH_CHECK(w2.is_cuda() && w2.dim() == 2 && w2.scalar_type() == at::kBFloat16 && w2.is_contiguous(),
+              "psd convn_bwd: w2 must be a contiguous bf16 [N, R*S*C] tensor");
+  TORCH_CHECK(out.dim() == 2 && out.is_contiguous() && out.scalar_type() == at::kBFloat16, "psd convn_bwd: out");
+  TORCH_CHECK(mode == 1 || mode == 2, "psd convn_bwd: mode 1 (mask from x, ss) or 2 (bit-mask + dr)");
+  const int64_t Nb = dy.size(0), C = dy.size(1), H = dy.size(2), W = dy.size(3);
+  const int64_t Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
+  const int64_t M = Nb * Ho * Wo, N = w2.size(0), K = R * S * C;
+  TORCH_CHECK(w2.size(1) == K && out.size(0) == M && out.size(1) == N, "psd convn_bwd: shapes");
+  auto like_out = [&](const at::Tensor& t, const char* what) {
+    const at::Tensor u = t.dim() == 4 ? t.permute({0, 2, 3, 1}) : t;
+    TORCH_CHECK(t.scalar_type() == at::kBFloat16 && t.numel() == M * N && t.device() == dy.device() &&
+                    (t.dim() == 4 ? t.is_contiguous(at::MemoryFormat::ChannelsLast) : t.is_contiguous()),
+                "psd convn_bwd: ", what, " must be a contiguous bf16 [M, N] (or channels_last) tensor");
+    (void)u;
+  };
+  like_out(bx, "bx");
+  TORCH_CHECK(bmean.scalar_type() == at::kFloat && bmean.numel() == N && bmean.is_contiguous(), "psd convn_bwd: bmean");
+  TORCH_CHECK(part.scalar_type() == at::kFloat && part.is_contiguous() &&
+                  part.numel() >= (int64_t)convn_stats_rows((int)M) * 2 * N,
+              "psd convn_bwd: part must be fp32 [convn_stats_rows(M), 2, N]");
+  if (mode == 1) {
+    TORCH_CHECK(bss.has_value() && bss->defined() && bss->numel() == 2 * N && bss->scalar_type() == at::kFloat &&
+                    bss->is_contiguous(),
+                "psd convn_bwd: mode 1 needs ss fp32 [2N]");
+  } else {
+    TORCH_CHECK(bdr.has_value() && bdr->defined(), "psd convn_bwd: mode 2 needs dr");
+    like_out(*bdr, "dr");
+    TORCH_CHECK(bmbits.has_value() && bmbits->defined() && bmbits->scalar_type() == at::kByte &&
+                    bmbits->numel() == M * N / 8 && bmbits->is_contiguous(),
+                "psd convn_bwd: mode 2 needs the uint8 [M*N/8] bit-mask");
+  }
+  const int64_t xbytes = dy.numel() * 2, wbytes = w2.numel() * 2;
+  if ((C & (C - 1)) != 0 || C < 64 || xbytes > 0xFFFFFF00ll || wbytes >= ((int64_t)1 << 32) ||
+      M >= ((int64_t)1 << 31) - 256 || convn_tile_n((int)N) == 0 || variant >= convn_variants((int)N) || N % 8 != 0)
+    return 0;
+  int logc = 0;
+  while ((1 << logc) < C) ++logc;
+  const c10::DeviceGuard g(dy.device());
+  ConvnArgs a{};
+  a.x = dy.data_ptr();
+  a.w = w2.data_ptr();
+  a.y = out.data_ptr();
+  a.part = part.data_ptr<float>();
+  a.xbytes = (uint32_t)xbytes;
+  a.wbytes = (uint32_t)wbytes;
+  a.M = (int)M;
+  a.N = (int)N;
+  a.K = (int)K;
+  a.H = (int)H;
+  a.W = (int)W;
+  a.logC = logc;
+  a.Ho = (int)Ho;
+  a.Wo = (int)Wo;
+  a.R = (int)R;
+  a.S = (int)S;
+  a.stride = (int)stride;
+  a.pad = (int)pad;
+  a.ldc = (int)N;
+  a.variant = (int)variant;
+  a.bwd = (int)mode;
+  a.bx = reinterpret_cast<const uint16_t*>(bx.data_ptr());
+  a.bmean = bmean.data_ptr<float>();
+  a.bss = mode == 1 ? bss->data_ptr<float>() : nullptr;
+  a.bdr = mode == 2 ? reinterpret_cast<const uint16_t*>(bdr->data_ptr()) : nullptr;
+  a.bmbits = mode == 2 ? bmbits->data_ptr<uint8_t>() : nullptr;
+  const hipError_t e = launch_convn(a, c10::hip::getCurrentHIPStream(dy.device().index()).stream());
+  if (e == hipErrorNotSupported) return 0;
+  TORCH_CHECK(e == hipSuccess, "psd convn_bwd: ", hipGetErrorString(e));
+  return convn_part_rows((int)M, (int)N, (int)variant);
+}
+
 bool conv_fwd_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride,
                int64_t pad) {
   return conv_fwd_impl(x, w2, out, R, S, stride, pad, nullptr, nullptr);

@@ -835,6 +835,30 @@ static hipError_t launch_bn_bwd_pool(const BnBwdArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+// BN backward from a producer-reduced gradient (kernels/convn.hip bwd modes): g is already masked
+// (and holds the residual-branch gradient), part holds `rows` rows of (sum g, sum g (x - mean)).
+hipError_t launch_bn_bwd_pre(const uint16_t* g, const uint16_t* x, const uint16_t* gamma, const float* mean,
+                             const float* invstd, const float* part, int rows, float* fold_ws, uint16_t* dgamma,
+                             uint16_t* dbeta, float* coef, uint16_t* dx, int64_t M, int C, hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  if (C % 8 != 0 || rows <= 0) return hipErrorInvalidValue;
+  const float* p = part;
+  int nblk = rows;
+  if (rows > kFoldRows) {
+    if (!fold_ws) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(bn_part_fold_kernel, dim3(kFoldRows, (2 * C + 127) / 128), dim3(256), 0, st, part, rows, 2 * C,
+                       fold_ws, kFoldRows);
+    p = fold_ws;
+    nblk = kFoldRows;
+  }
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(256), 0, st, p, nblk, M, C, gamma,
+                     mean, invstd, dgamma, dbeta, coef);
+  const int64_t nvec = M * (C / 8);
+  hipLaunchKernelGGL(bn_bwd_elemt_kernel<2>, dim3(elem_grid(nvec, C)), dim3(256), 0, st, g, nullptr, nullptr, nullptr, x,
+                     coef, dx, nvec, C);
+  return hipGetLastError();
+}
+
 hipError_t launch_bn_bwd(const BnBwdArgs& a, hipStream_t st) {
   if (a.M <= 0) return hipSuccess;
   if (a.C % 8 != 0) return hipErrorInvalidValue;

@@ -107,6 +107,11 @@ __device__ __forceinline__ float xor32(float x, int lane) {
   return __uint_as_float((lane & 32) ? r[0] : r[1]);
 }
 
+template <int N>
+__device__ __forceinline__ float ror_row(float x) {  // x of lane (l + N) mod 16 within its 16-lane row
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x120 + N, 0xF, 0xF, true));
+}
+
 template <int BM, int BN, int WNT, int NSLOT>
 struct Geo {
   static constexpr int WM = BM / 64;         // wave rows (64 output pixels each)
@@ -129,7 +134,14 @@ struct Geo {
 
 }  // namespace
 
-template <int BM, int BN, int WNT, int NSLOT, bool STATS>
+// BWD (bwd-data of a convolution whose input came out of a BatchNorm + ReLU): the epilogue also runs
+// that BN's backward reduction. 1: ReLU mask recomputed from the BN input x and the forward
+// scale/shift (bn1 / bn2 of a bottleneck); 2: the output plus the handed-over residual-branch
+// gradient dr, masked by the forward bit-mask (the previous block's bn3, whose output fed this
+// convolution and the identity residual). The stored output is then g = mask (dX [+ dr]) -- the
+// masked gradient the BN's elementwise pass consumes and, for 2, the residual gradient handed on --
+// and the partials are sum g and sum g (x - mean) per channel (the layout of bn_bwd_reduce_kernel).
+template <int BM, int BN, int WNT, int NSLOT, bool STATS, int BWD = 0>
 __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
   using G = Geo<BM, BN, WNT, NSLOT>;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -275,6 +287,19 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
   constexpr int CPR = RB / 16;      // 16-byte chunks per staged row
   constexpr int PASSES = 16 * CPR / 64;
   uint16_t* y = reinterpret_cast<uint16_t*>(a.y);
+  // BWD: this lane's 8 output channels are fixed (64 % CPR == 0): per-channel constants once
+  const int my_c16 = lane % CPR;
+  const int my_col = n0 + wc * WNT + my_c16 * 8;
+  float bmu[8], bsc[8], bsh[8], ga[8], gb[8];
+  if constexpr (BWD != 0) {
+    load8_f32(a.bmean + my_col, bmu);
+    if constexpr (BWD == 1) {
+      load8_f32(a.bss + my_col, bsc);
+      load8_f32(a.bss + a.N + my_col, bsh);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ga[e] = gb[e] = 0.f;
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int r = rq + L;  // this lane's row within the 16-row block after quad_t4
@@ -293,20 +318,70 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
       const int c = ps * 64 + lane;
       const int rr = c / CPR, c16 = c % CPR;
       const int off = rr * RB + (((2 * c16) ^ ((rr & 7) << 1)) & (RB / 8 - 1)) * 8;
-      const u32x4 v = *reinterpret_cast<const u32x4*>(stg + off);
+      u32x4 v = *reinterpret_cast<const u32x4*>(stg + off);
       const int m = m0 + wr * 64 + i * 16 + rr;
-      if (m < a.M) *reinterpret_cast<u32x4*>(y + (int64_t)m * a.ldc + n0 + wc * WNT + c16 * 8) = v;
+      if (m < a.M) {
+        const int64_t go = (int64_t)m * a.ldc + n0 + wc * WNT + c16 * 8;
+        if constexpr (BWD != 0) {
+          float d[8], xv[8];
+          load8_bf16(reinterpret_cast<const uint16_t*>(&v), d);
+          load8_bf16(a.bx + (int64_t)m * a.N + my_col, xv);
+          if constexpr (BWD == 2) {
+            float rv[8];
+            load8_bf16(a.bdr + (int64_t)m * a.N + my_col, rv);
+            const uint32_t bits = a.bmbits[((int64_t)m * a.N + my_col) >> 3];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) d[e] = ((bits >> e) & 1u) ? d[e] + rv[e] : 0.f;
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) d[e] = fmaf(xv[e], bsc[e], bsh[e]) > 0.f ? d[e] : 0.f;
+          }
+          uint32_t pk[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) pk[e] = pack_bf16x2_rne(d[2 * e], d[2 * e + 1]);
+          v = u32x4{pk[0], pk[1], pk[2], pk[3]};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float gq = bf16_to_f32(f32_to_bf16(d[e]));  // the stored g
+            ga[e] += gq;
+            gb[e] = fmaf(gq, xv[e] - bmu[e], gb[e]);
+          }
+        }
+        *reinterpret_cast<u32x4*>(y + go) = v;
+      }
+    }
+  }
+  if constexpr (BWD != 0) {
+    // lanes sharing this lane's channels: lane % CPR equal -> rotate-sum within the 16-lane row,
+    // then across rows
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if constexpr (CPR == 4) {
+        ga[e] += ror_row<4>(ga[e]);
+        gb[e] += ror_row<4>(gb[e]);
+      }
+      ga[e] += ror_row<8>(ga[e]);
+      gb[e] += ror_row<8>(gb[e]);
+      ga[e] += xor16(ga[e], lane);
+      gb[e] += xor16(gb[e], lane);
+      ga[e] += xor32(ga[e], lane);
+      gb[e] += xor32(gb[e], lane);
+    }
+    if (lane < CPR) {
+      float* pr = a.part + ((int64_t)tm * G::WM + wr) * 2 * a.N;
+      store8_f32(pr + my_col, ga);
+      store8_f32(pr + a.N + my_col, gb);
     }
   }
 }
 
 // ------------------------------------------------------------------ host side
-template <int BM, int BN, int WNT, int NSLOT, bool STATS>
+template <int BM, int BN, int WNT, int NSLOT, bool STATS, int BWD>
 static hipError_t convn_launch_t(const ConvnArgs& a0, hipStream_t st) {
   using G = Geo<BM, BN, WNT, NSLOT>;
   static bool attr = false;
   if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)convn_kernel<BM, BN, WNT, NSLOT, STATS>,
+    const hipError_t e = hipFuncSetAttribute((const void*)convn_kernel<BM, BN, WNT, NSLOT, STATS, BWD>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_MAX);
     if (e != hipSuccess) return e;
     attr = true;
@@ -316,13 +391,16 @@ static hipError_t convn_launch_t(const ConvnArgs& a0, hipStream_t st) {
   a.nslot = nt < NSLOT ? (nt < 2 ? 1 : nt) : NSLOT;
   const int lds = a.nslot * G::SLOT + G::NW * G::STG;
   const int tiles_m = (a.M + BM - 1) / BM;
-  hipLaunchKernelGGL((convn_kernel<BM, BN, WNT, NSLOT, STATS>), dim3(tiles_m, a.N / BN), dim3(G::NT), lds, st, a);
+  hipLaunchKernelGGL((convn_kernel<BM, BN, WNT, NSLOT, STATS, BWD>), dim3(tiles_m, a.N / BN), dim3(G::NT), lds, st, a);
   return hipGetLastError();
 }
 
 template <int BM, int BN, int WNT, int NSLOT>
 static hipError_t convn_launch_s(const ConvnArgs& a, hipStream_t st) {
-  return a.part ? convn_launch_t<BM, BN, WNT, NSLOT, true>(a, st) : convn_launch_t<BM, BN, WNT, NSLOT, false>(a, st);
+  if (a.bwd == 1) return convn_launch_t<BM, BN, WNT, NSLOT, false, 1>(a, st);
+  if (a.bwd == 2) return convn_launch_t<BM, BN, WNT, NSLOT, false, 2>(a, st);
+  return a.part ? convn_launch_t<BM, BN, WNT, NSLOT, true, 0>(a, st)
+                : convn_launch_t<BM, BN, WNT, NSLOT, false, 0>(a, st);
 }
 
 int convn_tile_n(int N) {
@@ -368,7 +446,10 @@ hipError_t launch_convn(const ConvnArgs& a, hipStream_t st) {
   const int C = 1 << a.logC;
   const bool ok = bn > 0 && a.logC >= 6 && a.K % kBK == 0 && a.K == a.R * a.S * C && a.ldc % 8 == 0 &&
                   a.ldc >= a.N && a.H < 32768 && a.W < 32768 && a.xbytes > 0 && a.xbytes <= 0xFFFFFF00u &&
-                  a.wbytes > 0 && (!a.part || a.shift) && a.variant < convn_variant_count(bn);
+                  a.wbytes > 0 && a.variant < convn_variant_count(bn) &&
+                  (a.bwd == 0 ? (!a.part || a.shift)
+                              : (a.part && a.bx && a.bmean && a.ldc == a.N &&
+                                 (a.bwd == 1 ? a.bss != nullptr : (a.bwd == 2 && a.bdr && a.bmbits))));
   if (!ok) return hipErrorNotSupported;
   const int v = a.variant >= 0 ? a.variant : default_variant(a, bn);
   switch (bn) {

@@ -86,5 +86,10 @@ constexpr int kFoldRows = 512;
 hipError_t launch_bn_reduce(const uint16_t* x, int64_t M, int C, const float* shift, float* part, hipStream_t st);
 hipError_t launch_bn_fwd(const BnFwdArgs& a, hipStream_t stream);
 hipError_t launch_bn_bwd(const BnBwdArgs& a, hipStream_t stream);
+// backward from a producer-reduced, already-masked gradient g (convolution bwd-data epilogue):
+// fold (> kFoldRows partial rows: fold_ws [kFoldRows * 2C]) + finalize + dx = A g + B x + C
+hipError_t launch_bn_bwd_pre(const uint16_t* g, const uint16_t* x, const uint16_t* gamma, const float* mean,
+                             const float* invstd, const float* part, int rows, float* fold_ws, uint16_t* dgamma,
+                             uint16_t* dbeta, float* coef, uint16_t* dx, int64_t M, int C, hipStream_t stream);
 
 }  // namespace psd

@@ -18,6 +18,14 @@ struct ConvnArgs {
   int ldc;
   int variant;  // tile geometry (convn_variants(N) of them); -1: the default
   int nslot;    // set by the launcher
+  // bwd-data with the producing BN's backward reduction in the epilogue (bwd 1 / 2, convn.hip);
+  // part then receives sum g and sum g (x - mean) per channel
+  int bwd;
+  const uint16_t* bx;     // [M][N] the BN's input (its forward x)
+  const float* bmean;     // [N] its saved mean
+  const float* bss;       // bwd 1: [2N] its forward scale / shift (ReLU mask)
+  const uint16_t* bdr;    // bwd 2: [M][N] the residual-branch gradient to add
+  const uint8_t* bmbits;  // bwd 2: [M*N/8] the forward ReLU bit-mask
 };
 
 // output-channel tile of the kernel for N output channels (64, 128, 256 for N % 256 == 0), 0: unsupported

@@ -53,6 +53,14 @@ void gelu_bwd_colsum_(const at::Tensor& dy, const at::Tensor& pre, at::Tensor dx
 int64_t convn_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride,
                int64_t pad, c10::optional<at::Tensor> part, c10::optional<at::Tensor> shift, int64_t variant);
 int64_t convn_stats_rows_(int64_t M);
+int64_t convn_bwd_(const at::Tensor& dy, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride,
+                   int64_t pad, at::Tensor part, int64_t variant, int64_t mode, const at::Tensor& bx,
+                   const at::Tensor& bmean, c10::optional<at::Tensor> bss, c10::optional<at::Tensor> bdr,
+                   c10::optional<at::Tensor> bmbits);
+std::vector<at::Tensor> bn_bwd_pre(const at::Tensor& g, const at::Tensor& x, c10::optional<at::Tensor> gamma,
+                                   const at::Tensor& save_mean, const at::Tensor& save_invstd, const at::Tensor& part,
+                                   int64_t rows, c10::optional<at::Tensor> dgamma_out,
+                                   c10::optional<at::Tensor> dbeta_out);
 int64_t convn_variants_(int64_t N);
 bool conv_fwd_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride,
                int64_t pad);

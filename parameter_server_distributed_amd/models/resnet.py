@@ -71,6 +71,11 @@ class Bottleneck(nn.Module):
             object.__setattr__(conv, "_psd_bn", bn)
         if downsample is not None and len(downsample) == 2:
             object.__setattr__(downsample[0], "_psd_bn", downsample[1])
+        # the BN whose output each convolution consumes (its backward reduction can run in the
+        # convolution's bwd-data epilogue); conv1's is set per forward (identity blocks only)
+        object.__setattr__(self.conv2, "_psd_bn_in", self.bn1)
+        object.__setattr__(self.conv3, "_psd_bn_in", self.bn2)
+        object.__setattr__(self.conv1, "_psd_bn_in", None)
         if fp8:  # bn1 / bn2 quantise their outputs for the fp8 conv2 / conv3 in their apply pass
             # (plain attributes: object.__setattr__ keeps the consumer from becoming a submodule)
             object.__setattr__(self.bn1, "_psd_q8_consumer", self.conv2)
@@ -90,6 +95,10 @@ class Bottleneck(nn.Module):
             out = self.bn2(self.conv2(self.bn1(self.conv1(xm))))
             return bn_add_bn_relu(self.bn3, self.conv3(out), self.downsample[1], r)
         idt = x if self.downsample is None else self.downsample(xd)
+        # identity block: x (prev_bn's output) feeds conv1 and the residual, whose gradient is handed
+        # to prev_bn -- conv1's bwd-data can run prev_bn's backward reduction
+        object.__setattr__(self.conv1, "_psd_bn_in",
+                           prev_bn if (self.fuse_residual_grad and isinstance(prev_bn, FusedBatchNorm2d)) else None)
         out = self.bn1(self.conv1(xm))
         out = self.bn2(self.conv2(out))
         fuse = prev_bn if (self.downsample is None and self.fuse_residual_grad) else None

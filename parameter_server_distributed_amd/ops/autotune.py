@@ -76,12 +76,14 @@ def choose(key: tuple, candidates: dict, default: str, probe=None) -> str:
     ``probe``: returns the output tensor of a candidate that writes into a preallocated buffer
     instead of returning its result."""
     got = _DECISIONS.get(key)
-    if got is not None:
+    if got is not None and got in candidates:
         return got
-    forced = os.environ.get("PSD_AUTOTUNE_FORCE")  # e.g. "mfma" / "blas" / "miopen" / "gemm": A/B runs
-    if forced and forced in candidates:
-        _DECISIONS[key] = forced
-        return forced
+    # A/B runs: e.g. "mfma" / "blas" / "miopen" / "gemm", or a priority list "psdnb0,psdn0" (the
+    # first name this op offers wins)
+    for forced in os.environ.get("PSD_AUTOTUNE_FORCE", "").split(","):
+        if forced and forced in candidates:
+            _DECISIONS[key] = forced
+            return forced
     if torch.cuda.is_current_stream_capturing():
         return default
     runs = {name: _time_ms(fn, probe=probe) for name, fn in candidates.items()}

@@ -77,6 +77,8 @@ class _FusedBNFn(torch.autograd.Function):
                                               mod.num_batches_tracked, None, mask_out=mod.relu and has_res, **q8,
                                               **_stats_args(mod, x))
         _q8_hand_over(mod, y, q8)
+        # for the consumer convolution's bwd-data epilogue (ops/conv.py _bn_bwd_fusion): ReLU BNs
+        mod._psd_fwd = (y, x, mean, ss, mbits if has_res else None) if mod.relu else None
         ctx.relu = mod.relu
         ctx.has_res = residual is not None
         ctx.mod = mod
@@ -92,10 +94,26 @@ class _FusedBNFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, mbits, w, mean, invstd, ss = ctx.saved_tensors
         mod = ctx.mod
+        mod._psd_fwd = None
         sink = getattr(mod, "_psd_grad_sink", None)
         dgo = dbo = None
         if sink is not None and w is not None:
             dgo, dbo = sink(mod.weight), sink(mod.bias)
+        pre = getattr(mod, "_psd_bwd_pre", None)
+        mod._psd_bwd_pre = None
+        if pre is not None and pre[0].data_ptr() == dy.data_ptr() and pre[0].shape == dy.shape:
+            # the consumer convolution's bwd-data epilogue reduced this BN's backward and wrote the
+            # masked gradient g (= the residual-branch gradient for a residual BN): finalize + one
+            # elementwise pass here
+            g, part, rows = pre
+            dx, dg, db = native().bn_bwd_pre(g, x, w, mean, invstd, part, rows, dgo, dbo)
+            res_grad = None
+            if ctx.has_res:
+                if ctx.resid_to is not None:
+                    ctx.resid_to._psd_pending_dr.append(g)
+                else:
+                    res_grad = g
+            return dx, (dg if w is not None else None), (db if w is not None else None), res_grad, None, None
         # residual-branch fusion: the identity-path gradient of this BN's output was stashed by the
         # next block's bn3 backward; fold it in here instead of an autograd add kernel
         dy2 = mod._psd_pending_dr.pop() if getattr(mod, "_psd_pending_dr", None) else None
@@ -211,6 +229,8 @@ class FusedBatchNorm2d(nn.BatchNorm2d):
         self.relu = relu
         self._psd_pending_dr: list = []
         self._psd_stats_pending = None  # (conv output, statistics partials, rows) from the producing conv
+        self._psd_fwd = None  # (output, input, mean, scale/shift, ReLU bits) for the consumer conv's bwd fusion
+        self._psd_bwd_pre = None  # (masked gradient, partials, rows) from the consumer conv's bwd-data
 
     def psd_direct_grad_params(self):
         return [self.weight, self.bias]

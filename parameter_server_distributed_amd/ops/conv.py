@@ -157,6 +157,67 @@ def _convn_variants(x, w2, k: int, stride: int, pad: int, bn=None) -> dict:
     return {f"psdn{v}": make(v) for v in range(C.convn_variants(cout))}
 
 
+def _bn_bwd_fusion(mod, x: torch.Tensor):
+    """When ``mod``'s input ``x`` is exactly the output of a FusedBatchNorm2d + ReLU (wired by the
+    model as ``_psd_bn_in``) whose only autograd consumer is ``mod``, the bwd-data epilogue can run
+    that BN's backward reduction (kernels/convn.hip bwd modes): mode 1 (no residual: ReLU mask from
+    its x and scale/shift) or mode 2 (a residual BN: bit-mask, plus the residual-branch gradient
+    handed over by the next block). Returns the arguments, or None."""
+    bn = getattr(mod, "_psd_bn_in", None) if mod is not None else None
+    st = getattr(bn, "_psd_fwd", None) if bn is not None else None
+    if st is None or not _at.enabled("PSD_CONVN_BWD"):
+        return None
+    y, bx, mean, ss, mbits = st
+    if y.data_ptr() != x.data_ptr() or y.shape != x.shape or y.stride() != x.stride():
+        return None
+    if mbits is not None:
+        if not bn._psd_pending_dr:
+            return None
+        return dict(mode=2, bn=bn, bx=bx, mean=mean, mbits=mbits)
+    return dict(mode=1, bn=bn, bx=bx, mean=mean, ss=ss)
+
+
+def _convn_bwd_variants(dy, w2, k: int, pad: int, fu: dict, dr) -> dict:
+    """{"psdnb<v>": fn}: stride-1 bwd-data on the narrow kernel whose epilogue runs the producing
+    BN's backward reduction; fn() -> g (the masked gradient the BN's elementwise pass takes), with
+    the partials handed to the BN (``_psd_bwd_pre``)."""
+    C = _native()
+    n, _, h, w = dy.shape
+    cout = w2.shape[0]
+    M = n * h * w
+
+    def make(v):
+        def fn():
+            out = torch.empty(M, cout, device=dy.device, dtype=dy.dtype)
+            part = torch.empty(C.convn_stats_rows(M), 2, cout, device=dy.device, dtype=torch.float32)
+            rows = C.convn_bwd_(dy, w2, out, k, k, 1, pad, part, v, fu["mode"], fu["bx"], fu["mean"],
+                                bss=fu.get("ss"), bdr=dr, bmbits=fu.get("mbits"))
+            if rows == 0:
+                raise RuntimeError("convn_bwd_ declined a shape _psdn_ok accepted")
+            g = _from_2d(out, n, h, w)
+            fu["bn"]._psd_bwd_pre = (g, part, rows)
+            return g
+        return fn
+
+    return {f"psdnb{v}": make(v) for v in range(C.convn_variants(cout))}
+
+
+def _dgrad_route(key: tuple, cands: dict, default: str, fu, dy_like) -> torch.Tensor:
+    """bwd-data: the fastest candidate; with a BN backward fusion available the library and
+    unfused candidates are timed with the reduction pass they leave to the BN. A non-fused choice
+    returns the handed-over residual gradient to the BN's queue."""
+    if fu is None:
+        return cands[_at.choose(key, cands, default)]()
+    timed = {name: (fn if name.startswith("psdnb") else _with_bn_reduce(fn, fu["bn"])) for name, fn in cands.items()}
+    how = _at.choose(key + ("bnbwd",), timed, default)
+    out = cands[how]()
+    if not how.startswith("psdnb"):
+        fu["bn"]._psd_bwd_pre = None
+        if fu.get("dr") is not None:
+            fu["bn"]._psd_pending_dr.append(fu["dr"])
+    return out
+
+
 def _with_bn_reduce(fn, bn):
     """Timing twin of a library candidate: its output plus the BN statistics pass it leaves to the
     BN (so the autotuner compares the fused kernel against library conv + reduce)."""
@@ -297,9 +358,15 @@ class _Conv1x1Fn(torch.autograd.Function):
             cands = {"gemm": gemm, "miopen": miopen}
             if _psd_ok(cout, cin):
                 cands["psd"] = psd
+            fu = None
             if _psdn_ok(cout, cin):  # dX = dY . W as a 1x1 convolution of dY with W^T [cin, cout]
-                cands.update(_convn_variants(dy, w2.t().contiguous(), 1, 1, 0))
-            dx = cands[_choose(key, cands)]()
+                wt = w2.t().contiguous()
+                cands.update(_convn_variants(dy, wt, 1, 1, 0))
+                fu = _bn_bwd_fusion(ctx.mod, x)
+                if fu is not None:
+                    fu["dr"] = fu["bn"]._psd_pending_dr.pop() if fu["mode"] == 2 else None
+                    cands.update(_convn_bwd_variants(dy, wt, 1, 0, fu, fu["dr"]))
+            dx = _dgrad_route(("conv1x1",) + key, cands, "miopen", fu, x)
         if need_w:
             def miopen_w():
                 return conv_bwd(dy, x, weight, *args, [False, True, False])[1]
@@ -480,10 +547,15 @@ class _ConvFn(torch.autograd.Function):
                 cands = {"miopen": miopen}
                 if _igemm_ok(cout, cin):
                     cands["igemm"] = igemm
+                fu = None
                 if _psdn_ok(cout, cin):
                     cands.update(_convn_variants(dy, wf, k, 1, pad))
+                    fu = _bn_bwd_fusion(ctx.mod, x)
+                    if fu is not None:
+                        fu["dr"] = fu["bn"]._psd_pending_dr.pop() if fu["mode"] == 2 else None
+                        cands.update(_convn_bwd_variants(dy, wf, k, pad, fu, fu["dr"]))
                 key = ("dgrad", n, cin, h, w, cout, k, stride)
-                dx = cands[_at.choose(("conv",) + key, cands, "miopen")]()
+                dx = _dgrad_route(("conv",) + key, cands, "miopen", fu, x)
             else:
                 dx = miopen()
         if ctx.needs_input_grad[1]:

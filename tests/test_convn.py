@@ -158,3 +158,41 @@ def test_conv_bn_module_psdn_route_matches_fp32(gpu, monkeypatch, k, cin, cout, 
                       (bn.bias.grad, gb.grad)):
         err = float((got.float() - want).abs().max())
         assert err < 0.05 * float(want.abs().max()) + 1e-3, (err, float(want.abs().max()))
+
+
+def test_resnet_convn_fusions_match_library_path(gpu, monkeypatch):
+    """ResNet-50 end to end with the narrow kernel forced wherever it applies -- forward with the
+    consumer BN's statistics in the epilogue, bwd-data with the producing BN's backward reduction
+    in the epilogue (bn1 / bn2 from x and scale/shift; identity-block bn3 with the residual
+    gradient added under the bit-mask) -- vs the same model with the kernel off (library
+    convolutions, separate BN passes): loss and every parameter gradient."""
+    from parameter_server_distributed_amd import models
+    from parameter_server_distributed_amd.ops import autotune
+
+    res = []
+    for on in (True, False):
+        monkeypatch.setenv("PSD_CONVN", "1" if on else "0")
+        monkeypatch.setenv("PSD_AUTOTUNE_FORCE", "psdnb0,psdn0" if on else "miopen")
+        autotune._DECISIONS.clear()
+        torch.manual_seed(0)
+        spec = models.build("resnet50", gpu, torch.bfloat16, image_size=64, num_classes=10)
+        m = spec.model
+        x, y = spec.make_batch(8, gpu, seed=3)
+        loss = spec.loss(m(x), y)
+        loss.backward()
+        res.append((float(loss), {n: p.grad.float().clone() for n, p in m.named_parameters()},
+                    {n: b.clone() for n, b in m.named_buffers() if "running" in n}))
+        if on:  # the fused paths actually ran
+            picks = autotune.decisions()
+            assert any(v == "psdnb0" for v in picks.values()), picks
+            assert any(v == "psdn0" for k, v in picks.items() if "bnstats" in k), picks
+    autotune._DECISIONS.clear()
+    assert abs(res[0][0] - res[1][0]) < 0.02 * abs(res[1][0]) + 1e-3, (res[0][0], res[1][0])
+    for n in res[1][1]:
+        a, b = res[0][1][n], res[1][1][n]
+        if b.norm() == 0:
+            assert a.norm() < 1e-3, n
+            continue
+        assert ((a - b).norm() / b.norm()).item() < 0.1, n
+    for n in res[1][2]:
+        torch.testing.assert_close(res[0][2][n], res[1][2][n], rtol=2e-2, atol=2e-3, msg=n)
