@@ -177,6 +177,8 @@ def test_resnet_convn_fusions_match_library_path(gpu, monkeypatch):
         torch.manual_seed(0)
         spec = models.build("resnet50", gpu, torch.bfloat16, image_size=64, num_classes=10)
         m = spec.model
+        for p in m.parameters():  # bf16 parameters (the PS data plane's working copy)
+            p.data = p.data.to(torch.bfloat16)
         x, y = spec.make_batch(8, gpu, seed=3)
         loss = spec.loss(m(x), y)
         loss.backward()
