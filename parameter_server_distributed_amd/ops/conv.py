@@ -122,8 +122,9 @@ def _bn_consumer(mod):
     """The training-mode FusedBatchNorm2d that consumes ``mod``'s output (wired by the model as
     ``_psd_bn``), whose batch statistics the convolution epilogue can reduce, or None."""
     bn = getattr(mod, "_psd_bn", None) if mod is not None else None
-    if (bn is None or not bn.training or bn.running_mean is None or not torch.is_grad_enabled()
-            or not _at.enabled("PSD_CONVN_STATS")):
+    # (no grad-mode test: this runs inside the autograd Function's forward, where grad mode is off;
+    # the module's forward only takes the Function path with grad enabled)
+    if bn is None or not bn.training or bn.running_mean is None or not _at.enabled("PSD_CONVN_STATS"):
         return None
     return bn
 
