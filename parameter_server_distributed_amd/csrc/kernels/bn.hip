@@ -741,8 +741,7 @@ hipError_t launch_bn_fwd(const BnFwdArgs& a, hipStream_t st) {
   reduce_grid(a.M, a.C, gx, gy);
   if (a.training) {
     const float* part = a.part;
-    if (a.part_ready > kFoldRows) {  // many producer partial rows (convolution epilogue): fold first
-      if (!a.fold_ws) return hipErrorInvalidValue;
+    if (a.part_ready > kFoldRows && a.fold_ws) {  // many producer partial rows (convolution epilogue): fold first
       hipLaunchKernelGGL(bn_part_fold_kernel, dim3(kFoldRows, (2 * a.C + 127) / 128), dim3(256), 0, st, a.part,
                          a.part_ready, 2 * a.C, a.fold_ws, kFoldRows);
       part = a.fold_ws;
