@@ -55,6 +55,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("q8_hist") = py::none(), py::arg("q8_sinv") = py::none(), py::arg("q8_margin") = 1.0,
         py::arg("part_in") = py::none(), py::arg("part_rows") = 0);
   m.def("bn_reduce_", &bn_reduce_, py::arg("x"), py::arg("shift"));
+  m.def("bn_bwd_reduce_", &bn_bwd_reduce_, py::arg("dy"), py::arg("x"), py::arg("save_mean"),
+        py::arg("ss") = py::none(), py::arg("dy2") = py::none(), py::arg("mbits") = py::none());
   m.def("bn_bwd_dual", &bn_bwd_dual, py::arg("dy"), py::arg("x"), py::arg("gamma"), py::arg("save_mean"),
         py::arg("save_invstd"), py::arg("mbits"), py::arg("dy2"), py::arg("xd"), py::arg("gamma_d"), py::arg("mean_d"),
         py::arg("invstd_d"), py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none(),

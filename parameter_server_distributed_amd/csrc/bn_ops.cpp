@@ -217,6 +217,53 @@ std::vector<at::Tensor> bn_bwd(const at::Tensor& dy_in, const at::Tensor& x_in, 
   return {dx, dr, dgamma, dbeta};
 }
 
+// The BN backward's reduction pass alone, as the BN would run it after a bwd-data convolution that
+// does not fuse it: ReLU mask from x and ss (mbits absent), or the residual BN's bit-mask with the
+// residual-branch gradient dy2 folded in and dr written. Autotune timing twin (ops/conv.py).
+// Returns the partials.
+at::Tensor bn_bwd_reduce_(const at::Tensor& dy_in, const at::Tensor& x_in, const at::Tensor& save_mean,
+                          c10::optional<at::Tensor> ss_in, c10::optional<at::Tensor> dy2_in,
+                          c10::optional<at::Tensor> mbits_in) {
+  const c10::DeviceGuard g(x_in.device());
+  at::Tensor x = nhwc(x_in), dy = nhwc(dy_in);
+  const int64_t C = channels(x), M = x.numel() / C;
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16 &&
+                  C % 8 == 0 && save_mean.numel() == C,
+              "psd bn_bwd_reduce: dy like x (bf16, C % 8 == 0), mean [C]");
+  const bool bits = mbits_in.has_value() && mbits_in->defined();
+  at::Tensor dy2, ss, mbits, dr;
+  if (bits) {
+    mbits = *mbits_in;
+    TORCH_CHECK(mbits.scalar_type() == at::kByte && mbits.is_contiguous() && mbits.numel() == M * C / 8,
+                "psd bn_bwd_reduce: mbits must be uint8 [M*C/8]");
+    dr = at::empty_like(x);
+  } else {
+    TORCH_CHECK(ss_in.has_value() && ss_in->defined() && ss_in->numel() == 2 * C, "psd bn_bwd_reduce: ss [2C]");
+    ss = ss_in->contiguous();
+  }
+  if (dy2_in.has_value() && dy2_in->defined()) {
+    dy2 = nhwc(*dy2_in);
+    TORCH_CHECK(dy2.sizes() == x.sizes() && dy2.scalar_type() == at::kBFloat16, "psd bn_bwd_reduce: dy2 like x");
+  }
+  at::Tensor part = at::empty({(int64_t)bn_reduce_blocks(M, (int)C), 2, C}, x.options().dtype(at::kFloat));
+  BnBwdArgs a{};
+  a.dy = reinterpret_cast<const uint16_t*>(dy.data_ptr());
+  a.dy2 = dy2.defined() ? reinterpret_cast<const uint16_t*>(dy2.data_ptr()) : nullptr;
+  a.ss = ss.defined() ? ss.data_ptr<float>() : nullptr;
+  a.mbits = bits ? mbits.data_ptr<uint8_t>() : nullptr;
+  a.x = reinterpret_cast<const uint16_t*>(x.data_ptr());
+  a.save_mean = save_mean.data_ptr<float>();
+  a.dr = dr.defined() ? reinterpret_cast<uint16_t*>(dr.data_ptr()) : nullptr;
+  a.part = part.data_ptr<float>();
+  a.M = M;
+  a.C = (int32_t)C;
+  a.relu = 1;
+  a.reduce_only = 1;
+  const hipError_t e = launch_bn_bwd(a, stream_of(x));
+  TORCH_CHECK(e == hipSuccess, "psd bn_bwd_reduce: ", hipGetErrorString(e));
+  return part;
+}
+
 
 // BN backward whose reduction the producing convolution's bwd-data epilogue already ran
 // (kernels/convn.hip bwd modes): g = the masked gradient (for a residual BN also the residual-branch

@@ -895,6 +895,7 @@ hipError_t launch_bn_bwd(const BnBwdArgs& a, hipStream_t st) {
   else if (a.dr) PSD_RED(kMaskNone, true);
   else PSD_RED(kMaskNone, false);
 #undef PSD_RED
+  if (a.reduce_only) return hipGetLastError();
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((a.C + kFinCh - 1) / kFinCh), dim3(256), 0, st, a.part, gx, a.M, a.C, a.gamma,
                      a.save_mean, a.save_invstd, a.dgamma, a.dbeta, a.coef);
   const int64_t nvec = a.M * (a.C / 8);

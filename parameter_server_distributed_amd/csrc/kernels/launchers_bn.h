@@ -74,6 +74,9 @@ struct BnBwdArgs {
   uint16_t* dbeta_d;
   float* coef_d;  // [3C]
   float* part_d;  // like part
+  // the reduction pass alone (partials into part, dr when given): what a bwd-data convolution that
+  // does not fuse it leaves to the BN (autotune timing twin, ops/conv.py _with_bn_bwd_reduce)
+  int32_t reduce_only;
 };
 
 // true when the fused stem BN+ReLU+max-pool kernels support this shape

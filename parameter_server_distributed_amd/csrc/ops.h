@@ -27,6 +27,9 @@ std::vector<at::Tensor> bn_fwd(const at::Tensor& x, c10::optional<at::Tensor> ga
                                int64_t part_rows);
 // statistics pass of the BN forward alone: shifted sums of x [M, C] into a fresh [rows, 2, C] fp32
 at::Tensor bn_reduce_(const at::Tensor& x, const at::Tensor& shift);
+at::Tensor bn_bwd_reduce_(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& save_mean,
+                          c10::optional<at::Tensor> ss, c10::optional<at::Tensor> dy2,
+                          c10::optional<at::Tensor> mbits);
 std::vector<at::Tensor> bn_bwd_dual(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& gamma,
                                     const at::Tensor& save_mean, const at::Tensor& save_invstd, const at::Tensor& mbits,
                                     c10::optional<at::Tensor> dy2, const at::Tensor& xd, const at::Tensor& gamma_d,

@@ -209,7 +209,7 @@ def _dgrad_route(key: tuple, cands: dict, default: str, fu, dy_like) -> torch.Te
     returns the handed-over residual gradient to the BN's queue."""
     if fu is None:
         return cands[_at.choose(key, cands, default)]()
-    timed = {name: (fn if name.startswith("psdnb") else _with_bn_reduce(fn, fu["bn"])) for name, fn in cands.items()}
+    timed = {name: (fn if name.startswith("psdnb") else _with_bn_bwd_reduce(fn, fu)) for name, fn in cands.items()}
     how = _at.choose(key + ("bnbwd",), timed, default)
     out = cands[how]()
     if not how.startswith("psdnb"):
@@ -226,6 +226,18 @@ def _with_bn_reduce(fn, bn):
         y = fn()
         _native().bn_reduce_(y, bn.running_mean)
         return y
+    return g
+
+
+def _with_bn_bwd_reduce(fn, fu):
+    """Timing twin of an unfused bwd-data candidate: its output plus the BN backward reduction it
+    leaves to the BN -- the same pass the BN then runs (mask from x and scale/shift, or the residual
+    BN's bit-mask with the handed-over residual gradient folded in and dr written)."""
+    def g():
+        dx = fn()
+        _native().bn_bwd_reduce_(dx, fu["bx"], fu["mean"], ss=fu.get("ss"), dy2=fu.get("dr"),
+                                 mbits=fu.get("mbits"))
+        return dx
     return g
 
 
