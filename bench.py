@@ -26,6 +26,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
@@ -256,11 +257,20 @@ def main():
         torch.cuda.synchronize(dev)
 
     t_w0 = time.perf_counter()
+    warm_done = threading.Event()
+
+    def heartbeat():  # a first step that autotunes many unseen shapes can run for minutes
+        while not warm_done.wait(30.0):
+            print(f"  ... warmup running, {time.perf_counter() - t_w0:.0f} s", file=sys.stderr, flush=True)
+
+    if rank == 0:
+        threading.Thread(target=heartbeat, daemon=True).start()
     for i in range(a.warmup):
         tr.step()
         if rank == 0:  # progress (MIOpen tuning of unseen shapes can take minutes)
             torch.cuda.synchronize(dev)
             print(f"warmup step {i + 1}/{a.warmup}: {time.perf_counter() - t_w0:.1f} s", file=sys.stderr, flush=True)
+    warm_done.set()
     barrier()
     t_w = time.perf_counter() - t_w0
     mem_peak = torch.cuda.max_memory_allocated(dev)
