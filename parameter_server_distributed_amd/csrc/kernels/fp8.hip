@@ -330,4 +330,102 @@ hipError_t launch_dequant_fp8(const uint8_t* x, int64_t n, const float* scale_in
   return hipGetLastError();
 }
 
+// ---- MX (OCP microscaling) fp8: one E8M0 scale per 32 consecutive elements ---------------------
+// The format the block-scaled MFMA (v_mfma_scale_f32_16x16x128_f8f6f4) consumes: a lane's 32 K-values
+// and the E8M0 byte 2^(s - 127) they share. Purely local -- no amax pass, no history, no device
+// scalar -- so a PS owner quantises its slice of the flat weight buffer on its own (K-major weight
+// rows of a multiple of 32 elements keep every block inside one GEMM row: tools/probes/mx_probe.hip
+// pins the lane map), and an activation is quantised in the pass that produces it.
+// Scale choice: the smallest power of two with amax * 2^-e <= fp8 max (no saturation in the block).
+__device__ __forceinline__ int mx_exp_byte(float amax, float fmax) {
+  if (!(amax > 0.f) || !(amax < 3.0e38f)) return 127;  // zero / non-finite block: unit scale
+  int p;
+  const float m = frexpf(amax / fmax, &p);  // amax / fmax = m 2^p, m in [0.5, 1)
+  int e = (m == 0.5f) ? p - 1 : p;
+  e = e < -127 ? -127 : (e > 127 ? 127 : e);
+  return e + 127;
+}
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+
+// 8 elements per lane, 4 lanes per 32-element block (n % 32 == 0; the grid stride is a multiple
+// of 4 lanes, so a block's lanes are active together)
+template <int DT, bool E5>
+__global__ __launch_bounds__(256) void quant_mx_kernel(const void* __restrict__ x, int64_t n, uint8_t* __restrict__ q,
+                                                       uint8_t* __restrict__ sc) {
+  const float fmax = E5 ? 57344.f : 448.f;
+  const int64_t nvec = n >> 3;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    float t[8];
+    if (DT == DT_BF16) load8_bf16(static_cast<const uint16_t*>(x) + (v << 3), t);
+    else load8_f32(static_cast<const float*>(x) + (v << 3), t);
+    float m = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(t[e]));
+    m = fmaxf(m, dpp_f<0xB1>(m));  // quad_perm [1,0,3,2]
+    m = fmaxf(m, dpp_f<0x4E>(m));  // quad_perm [2,3,0,1]: the block's 4 lanes agree
+    const int eb = mx_exp_byte(m, fmax);
+    const float inv = __uint_as_float((uint32_t)(254 - eb) << 23);  // 2^(127 - eb)
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      lo |= (uint32_t)f32_to_f8<E5>(t[e] * inv) << (8 * e);
+      hi |= (uint32_t)f32_to_f8<E5>(t[e + 4] * inv) << (8 * e);
+    }
+    *reinterpret_cast<uint2*>(q + (v << 3)) = make_uint2(lo, hi);
+    if ((v & 3) == 0) sc[v >> 2] = (uint8_t)eb;
+  }
+}
+
+template <int OD>
+__global__ __launch_bounds__(256) void dequant_mx_kernel(const uint8_t* __restrict__ q, const uint8_t* __restrict__ sc,
+                                                         int64_t n, void* __restrict__ out) {
+  const int64_t nvec = n >> 3;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    const uint2 b = *reinterpret_cast<const uint2*>(q + (v << 3));
+    const float s = __uint_as_float((uint32_t)sc[v >> 2] << 23);  // 2^(eb - 127) (eb 0: 0, exact enough)
+    float t[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      t[e] = e4m3_to_f32((uint8_t)(b.x >> (8 * e))) * s;
+      t[e + 4] = e4m3_to_f32((uint8_t)(b.y >> (8 * e))) * s;
+    }
+    if (OD == DT_BF16) store8_bf16(static_cast<uint16_t*>(out) + (v << 3), t);
+    else store8_f32(static_cast<float*>(out) + (v << 3), t);
+  }
+}
+
+hipError_t launch_quant_mx(const void* x, int32_t dt, int64_t n, int e5m2, uint8_t* q, uint8_t* scales, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (n % 32 != 0) return hipErrorInvalidValue;
+  const int grid = stream_grid(n >> 3, 256);
+#define PSD_QMX(D, E) hipLaunchKernelGGL((quant_mx_kernel<D, E>), dim3(grid), dim3(256), 0, st, x, n, q, scales)
+  if (dt == DT_BF16) {
+    if (e5m2) PSD_QMX(DT_BF16, true);
+    else PSD_QMX(DT_BF16, false);
+  } else if (dt == DT_F32) {
+    if (e5m2) PSD_QMX(DT_F32, true);
+    else PSD_QMX(DT_F32, false);
+  } else {
+    return hipErrorInvalidValue;
+  }
+#undef PSD_QMX
+  return hipGetLastError();
+}
+
+hipError_t launch_dequant_mx(const uint8_t* q, const uint8_t* scales, int64_t n, void* out, int32_t od, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (n % 32 != 0) return hipErrorInvalidValue;
+  const int grid = stream_grid(n >> 3, 256);
+  if (od == DT_BF16) hipLaunchKernelGGL(dequant_mx_kernel<DT_BF16>, dim3(grid), dim3(256), 0, st, q, scales, n, out);
+  else if (od == DT_F32) hipLaunchKernelGGL(dequant_mx_kernel<DT_F32>, dim3(grid), dim3(256), 0, st, q, scales, n, out);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
 }  // namespace psd

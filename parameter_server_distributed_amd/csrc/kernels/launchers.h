@@ -99,5 +99,11 @@ hipError_t launch_quant_fp8_delayed(const void* x, int32_t dtype, int64_t n, flo
                                     uint8_t* out, float* scale_inv, hipStream_t stream, int e5m2);
 hipError_t launch_dequant_fp8(const uint8_t* x, int64_t n, const float* scale_inv, void* out,
                               int32_t out_dtype, hipStream_t stream);
+// MX fp8 (OCP microscaling): e4m3 / e5m2 payload + one E8M0 scale byte per 32 consecutive elements
+// (n % 32 == 0; scales: n / 32 bytes)
+hipError_t launch_quant_mx(const void* x, int32_t dtype, int64_t n, int e5m2, uint8_t* q, uint8_t* scales,
+                           hipStream_t stream);
+hipError_t launch_dequant_mx(const uint8_t* q, const uint8_t* scales, int64_t n, void* out, int32_t out_dtype,
+                             hipStream_t stream);
 
 }  // namespace psd
