@@ -43,6 +43,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("amax_", &amax_);
   m.def("quant_fp8_", &quant_fp8_);
   m.def("dequant_fp8_", &dequant_fp8_);
+  m.def("quant_mx_", &quant_mx_, py::arg("x"), py::arg("out"), py::arg("scales"));
+  m.def("dequant_mx_", &dequant_mx_, py::arg("q"), py::arg("scales"), py::arg("out"));
   m.def("quant_fp8_jit_", &quant_fp8_jit_, py::arg("x"), py::arg("out"), py::arg("scale_inv"));
   m.def("quant_fp8_delayed_", &quant_fp8_delayed_, py::arg("x"), py::arg("out"), py::arg("scale_inv"),
         py::arg("hist"), py::arg("margin") = 1.0);

@@ -96,9 +96,18 @@ void gemm_fp8_(const at::Tensor& A, const at::Tensor& B, const at::Tensor& a_sca
   const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
   TORCH_CHECK(B.size(1) == K, "psd gemm_fp8: K mismatch");
   TORCH_CHECK(K % 128 == 0, "psd gemm_fp8: K must be a multiple of 128");
-  TORCH_CHECK(a_scale.scalar_type() == at::kFloat && b_scale.scalar_type() == at::kFloat && a_scale.numel() >= 1 &&
-                  b_scale.numel() >= 1 && a_scale.is_cuda() && b_scale.is_cuda(),
-              "psd gemm_fp8: scales must be fp32 device scalars");
+  // per-tensor (fp32 device scalars) or MX (uint8 E8M0 per 32 contiguous K: A [M, K/32], B [N, K/32])
+  const bool mx = a_scale.scalar_type() == at::kByte;
+  if (mx) {
+    TORCH_CHECK(b_scale.scalar_type() == at::kByte && a_scale.is_cuda() && b_scale.is_cuda() &&
+                    a_scale.is_contiguous() && b_scale.is_contiguous() && a_scale.numel() == M * (K / 32) &&
+                    b_scale.numel() == N * (K / 32) && A.stride(0) == K && B.stride(0) == K,
+                "psd gemm_fp8: MX scales must be uint8 [M, K/32] / [N, K/32] (contiguous operands)");
+  } else {
+    TORCH_CHECK(a_scale.scalar_type() == at::kFloat && b_scale.scalar_type() == at::kFloat && a_scale.numel() >= 1 &&
+                    b_scale.numel() >= 1 && a_scale.is_cuda() && b_scale.is_cuda(),
+                "psd gemm_fp8: scales must be fp32 device scalars (or MX uint8 block scales)");
+  }
   TORCH_CHECK(out.dim() == 2 && out.size(0) == M && out.size(1) == N && out.stride(1) == 1, "psd gemm_fp8: out shape");
   TORCH_CHECK(out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat, "psd gemm_fp8: out dtype");
   const c10::DeviceGuard g(A.device());
@@ -118,8 +127,13 @@ void gemm_fp8_(const at::Tensor& A, const at::Tensor& B, const at::Tensor& a_sca
   a.a_kmajor = a.b_kmajor = 1;
   a.act = (int)act;
   a.c_f32 = out.scalar_type() == at::kFloat;
-  a.a_scale = a_scale.data_ptr<float>();
-  a.b_scale = b_scale.data_ptr<float>();
+  if (mx) {
+    a.a_mx = a_scale.data_ptr<uint8_t>();
+    a.b_mx = b_scale.data_ptr<uint8_t>();
+  } else {
+    a.a_scale = a_scale.data_ptr<float>();
+    a.b_scale = b_scale.data_ptr<float>();
+  }
   a.f8a = A.scalar_type() == at::kFloat8_e5m2 ? 1 : 0;
   hipError_t e = launch_gemm_fp8(a, stream_of(A));
   TORCH_CHECK(e == hipSuccess, "psd gemm_fp8: ", hipGetErrorString(e));
@@ -143,10 +157,17 @@ static bool conv_fwd_impl(const at::Tensor& x, const at::Tensor& w2, at::Tensor 
                   (w2.stride(0) * esz) % 16 == 0 && (reinterpret_cast<uintptr_t>(w2.data_ptr()) & 15) == 0,
               "psd conv_fwd: w2 must be a 2-D device tensor like x, unit inner stride, 16-B aligned rows");
   TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.scalar_type() == at::kBFloat16, "psd conv_fwd: out");
-  if (f8)
+  const bool mx = f8 && xs->scalar_type() == at::kByte;  // MX: E8M0 per 32 channels of x, per 32 K of w2
+  if (mx) {
+    TORCH_CHECK(ws->scalar_type() == at::kByte && xs->is_cuda() && ws->is_cuda() && xs->is_contiguous() &&
+                    ws->is_contiguous() && xs->numel() == x.numel() / 32 && ws->numel() == w2.numel() / 32 &&
+                    w2.stride(0) == w2.size(1),
+                "psd conv_fwd_fp8: MX scales must be uint8 [pixels, C/32] / [Cout, K/32] (contiguous w2)");
+  } else if (f8) {
     TORCH_CHECK(xs->scalar_type() == at::kFloat && ws->scalar_type() == at::kFloat && xs->is_cuda() && ws->is_cuda() &&
                     xs->numel() >= 1 && ws->numel() >= 1,
-                "psd conv_fwd_fp8: scales must be fp32 device scalars");
+                "psd conv_fwd_fp8: scales must be fp32 device scalars (or MX uint8 block scales)");
+  }
   const int64_t Nb = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
   const int64_t Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
   const int64_t M = Nb * Ho * Wo, Cout = w2.size(0), K = R * S * C;
@@ -178,7 +199,11 @@ static bool conv_fwd_impl(const at::Tensor& x, const at::Tensor& w2, at::Tensor 
   a.cv_stride = (int)stride;
   a.cv_pad = (int)pad;
   a.cv_abytes = (uint32_t)xbytes;
-  if (f8) {
+  if (mx) {
+    a.a_mx = xs->data_ptr<uint8_t>();
+    a.b_mx = ws->data_ptr<uint8_t>();
+    a.f8a = x_e5 ? 1 : 0;
+  } else if (f8) {
     a.a_scale = xs->data_ptr<float>();
     a.b_scale = ws->data_ptr<float>();
     a.f8a = x_e5 ? 1 : 0;

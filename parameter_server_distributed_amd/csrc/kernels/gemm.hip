@@ -732,15 +732,19 @@ __device__ __forceinline__ void tile_of(int wg, int tiles_m, int tiles_n, int& t
 // goes out as 16-byte row segments, bf16 through a per-wave 4 KiB LDS slot (whole 128-byte rows
 // per store); the stores drain while the next tile's first phases run (retired by the first
 // phase-3 vmcnt, in issue order).
-template <int BM>
+// MX: the block-scaled fp8 form (per-32-K E8M0 scales of A rows and B columns): each K-tile's
+// scales (BM x 4 B of A, 256 x 4 B of B) ride in SC bytes at the end of its buffer, staged by one
+// extra 4-byte LDS-DMA per wave with the A-half0 pieces (so it is counted in VM like them).
+template <int BM, bool MX = false>
 struct P8 {
   static constexpr int IM = BM / 64;         // 16-row blocks per quadrant
   static constexpr int QA = BM / 4;          // quadrant rows
   static constexpr int HA = BM / 2 * 128;    // A half-tile bytes
   static constexpr int HB = 128 * 128;       // B half-tile bytes
   static constexpr int PWA = HA / 8192;      // A DMA pieces per wave per half-tile
-  static constexpr int VM = 4 + PWA;         // DMA in flight after phase 3 (three half-tiles)
-  static constexpr int BUF = 2 * HA + 2 * HB;
+  static constexpr int VM = 4 + PWA + (MX ? 1 : 0);  // DMA in flight after phase 3 (three half-tiles)
+  static constexpr int SC = MX ? 2048 : 0;   // scale bytes per buffer: A [BM][4] at 0, B [256][4] at 512
+  static constexpr int BUF = 2 * HA + 2 * HB + SC;
   static constexpr int STG = 4096;           // per-wave epilogue staging (16 rows x 64 cols, C + aux)
   static constexpr int LDS = 2 * BUF + 8 * STG;
 };
@@ -764,13 +768,14 @@ __device__ __forceinline__ float act_apply(float x) {
 // M-major ([pixels][cout]), B = the gathered [pixels][R*S*C] N-major image (each lane's 16 bytes are
 // 8 channels of one shifted input pixel; pixels outside the image load zeros).
 template <int BM, bool AK, bool BKM, int MODE, bool F8 = false, int ACT = 0, bool GA = false, int F8A = 0,
-          bool GB = false>
+          bool GB = false, bool MX = false>
 __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
+  static_assert(!MX || (F8 && BM == 128 && MODE == 0), "MX: fp8, 128-row tiles (LDS), single split");
   static_assert(!GB || (!AK && !BKM && MODE == 1 && !F8 && !GA), "implicit-GEMM wgrad: M-major dY, split-K");
   static_assert(!F8 || (AK && BKM), "fp8 GEMM takes K-major operands");
   static_assert(!GA || (AK && MODE == 0), "implicit-GEMM convolution: K-major A, single split");
   static_assert(BM == 256 || AK, "BM = 128 takes a K-major A");
-  using P = P8<BM>;
+  using P = P8<BM, MX>;
   constexpr int IM = P::IM;
   constexpr int KT = F8 ? 128 : BK;  // k per K-tile (128-B LDS rows either way)
   constexpr int ESZ = F8 ? 1 : 2;
@@ -839,7 +844,39 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
     conv_rows(cm0, cp0, chw);
     conv_rows(xm0, np0, nhw);
   }
-  auto stA = [&](int u, int m0, int k, int h) {
+  auto stA = [&](int u, int m0, int k, int h, int n0s) {
+    if constexpr (MX) {
+      if (h == 0) {  // this K-tile's scales: waves 0-1 A rows, 2-5 B columns, 6-7 a dummy (zeros)
+        uint8_t* sc = smem + (u & 1) * P::BUF + 2 * P::HA + 2 * P::HB;
+        const uint32_t kblk = (uint32_t)g.K >> 5, kb = (uint32_t)k >> 5;
+        const bool isA = wid < 2, isB = wid >= 2 && wid < 6;
+        const uint32_t abytes = GA ? (g.cv_abytes >> 5) : (uint32_t)g.M * kblk;
+        const rsrc_t src = isB ? make_rsrc(g.b_mx, (uint32_t)g.N * kblk) : make_rsrc(g.a_mx, abytes);
+        uint32_t off = 0xFFFFFFF0u;  // past every range: zeros
+        if (isA) {
+          const int row = m0 + wid * 64 + lane;
+          if constexpr (GA) {  // the row's gathered input pixel for this K-tile's (r, s): [pixels][C/32] scales
+            if (row < g.M) {
+              const int howo = g.cv_Ho * g.cv_Wo;
+              const int n = row / howo, rem = row - n * howo;
+              const int ho = rem / g.cv_Wo, wo = rem - ho * g.cv_Wo;
+              const int rs = k >> g.cv_logC, ci0 = k & ((1 << g.cv_logC) - 1);
+              const int r = rs / g.cv_S, s = rs - r * g.cv_S;
+              const int hh = ho * g.cv_stride - g.cv_pad + r, ww = wo * g.cv_stride - g.cv_pad + s;
+              if ((unsigned)hh < (unsigned)g.cv_H && (unsigned)ww < (unsigned)g.cv_W)
+                off = ((uint32_t)((n * g.cv_H + hh) * g.cv_W + ww) << (g.cv_logC - 5)) + ((uint32_t)ci0 >> 5);
+            }
+          } else {
+            if (row < g.M) off = (uint32_t)row * kblk + kb;
+          }
+        } else if (isB) {
+          const int col = n0s + (wid - 2) * 64 + lane;
+          if (col < g.N) off = (uint32_t)col * kblk + kb;
+        }
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(src, (__attribute__((address_space(3))) void*)(sc + wid * 256), 4, off,
+                                                 0, 0, 0);
+      }
+    }
     if constexpr (GA) {
       const bool cur = m0 == cm0;  // tiles with equal m0 share their A rows
       const int rs = k >> g.cv_logC, ci0 = k & ((1 << g.cv_logC) - 1);
@@ -890,11 +927,11 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
   if (nt > 0) {
     const int k1 = kbeg + min(1, nt - 1) * KT;  // nt = 1: a split of one K-tile re-stages it
     stB(0, cn0, kbeg, 0);
-    stA(0, cm0, kbeg, 0);
+    stA(0, cm0, kbeg, 0, cn0);
     stB(0, cn0, kbeg, 1);
-    stA(0, cm0, kbeg, 1);
+    stA(0, cm0, kbeg, 1, cn0);
     stB(1, cn0, k1, 0);
-    stA(1, cm0, k1, 0);
+    stA(1, cm0, k1, 0, cn0);
     stB(1, cn0, k1, 1);
     wait_vm<P::VM>();  // tile 0 landed (this wave's DMA)
   }
@@ -929,6 +966,29 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
   };
   // one C quadrant x one K-tile: 8*IM bf16 MFMA (k-step outer: independent accumulators between
   // dependent issues) or 4*IM fp8 MX MFMA
+  // MX: this lane's E8M0 scales of the current K-tile -- A [half][row block], B [half][col block];
+  // lane (16 b + r) supplies block b (K bytes [32b, 32b+32)) of row / column r of its fragment
+  // (tools/probes/mx_probe.hip)
+  int sa[2][IM], sb[2][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int i = 0; i < IM; ++i) sa[h][i] = 127;
+    sb[h][0] = sb[h][1] = 127;
+  }
+  auto readS = [&](int u) {
+    if constexpr (MX) {
+      const uint8_t* sc = smem + (u & 1) * P::BUF + 2 * P::HA + 2 * P::HB;
+      const int b = lane >> 4, r = lane & 15;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int i = 0; i < IM; ++i) sa[h][i] = sc[half_to_tile<P::QA>((wr * IM + i) * 16 + r, h) * 4 + b];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) sb[h][j] = sc[512 + half_to_tile<32>((wc * 2 + j) * 16 + r, h) * 4 + b];
+      }
+    }
+  };
   auto quad = [&](int q, bf16x8 (&a)[IM][2], bf16x8 (&b)[2][2], i32x8 (&fa)[IM], i32x8 (&fb)[2]) {
     if constexpr (F8) {
 #pragma unroll
@@ -936,7 +996,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[(q * IM + i) * 2 + j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
-              fa[i], fb[j], acc[(q * IM + i) * 2 + j], F8A, 0, 0, 127, 0, 127);
+              fa[i], fb[j], acc[(q * IM + i) * 2 + j], F8A, 0, 0, sa[q >> 1][i], 0, sb[q & 1][j]);
     } else {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
@@ -966,10 +1026,11 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
   // those stores in flight (they are older than K-tile u+2's DMA only)
   auto kstep = [&](int u, int am1, int ak1, int am2, int bn2, int ak2, bool first) {
     // ---- phase 0: q(0,0)
+    readS(u);  // (before the B reads: retired by the same lgkmcnt wait)
     readB(half(u, 2), b0, fb0);
     __builtin_amdgcn_sched_barrier(0);
     readA(half(u, 0), a0, fa0);
-    if (!first) stA(u + 1, am1, ak1, 1);
+    if (!first) stA(u + 1, am1, ak1, 1, 0);
     wait_lgkm<kAReads>();  // retires every B(qn0) read (lgkmcnt saturates at 15)
     __builtin_amdgcn_sched_barrier(0);
     PSD_SYNC_OPEN()
@@ -984,7 +1045,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
     PSD_SYNC_CLOSE()
     // ---- phase 2: q(1,0)
     readA(half(u, 1), a1, fa1);
-    stA(u + 2, am2, ak2, 0);
+    stA(u + 2, am2, ak2, 0, bn2);
     __builtin_amdgcn_sched_barrier(0);
     PSD_SYNC_OPEN()
     quad(2, a1, b0, fa1, fb0);
@@ -1010,7 +1071,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
   const bool want_aux = MODE == 0 && ACT == 2 && g.aux;
   uint8_t* stg = smem + 2 * P::BUF + wid * P::STG;  // this wave's epilogue staging slot
   float fmul = 1.f;
-  if constexpr (F8) {
+  if constexpr (F8 && !MX) {
     fmul = *g.a_scale * *g.b_scale;
     asm volatile("" ::"v"(fmul));  // materialise now (a load left to the epilogue would drain the DMA there)
   }
@@ -1041,7 +1102,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
     // the next tile's first K-tile issues its phase-0 DMA (A-half1 of its K-tile 1) here, BEFORE
     // the stores below, so that its phase-3 wait can leave the stores in flight (nt >= 2 whenever
     // a workgroup has more than one tile)
-    if (more) stA(base + nt + 1, xm0, kbeg + KT, 1);
+    if (more) stA(base + nt + 1, xm0, kbeg + KT, 1, 0);
 
     // ---- epilogue of tile jt (no barrier: the pipeline LDS already holds the next tile)
     float bv[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
@@ -1051,7 +1112,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) bv[qn][j] = bf16_to_f32(reinterpret_cast<const uint16_t*>(stg)[qn * 32 + j * 16 + cl]);
     }
-    if constexpr (F8) {
+    if constexpr (F8 && !MX) {
 #pragma unroll
       for (int i = 0; i < 8 * IM; ++i) acc[i] *= fmul;
     }
@@ -1353,12 +1414,13 @@ static int persistent_grid() {
   return n;
 }
 
-template <int BM, bool AK, bool BKM, int MODE, bool F8, int ACT, bool GA = false, int F8A = 0, bool GB = false>
+template <int BM, bool AK, bool BKM, int MODE, bool F8, int ACT, bool GA = false, int F8A = 0, bool GB = false,
+          bool MX = false>
 static hipError_t launch_8p_act(const GemmArgs& g, int splits, hipStream_t st) {
-  constexpr int lds = P8<BM>::LDS;
+  constexpr int lds = P8<BM, MX>::LDS;
   static bool attr_set = false;  // per instantiation: set the >64 KiB LDS limit once
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT, GA, F8A, GB>,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT, GA, F8A, GB, MX>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     attr_set = true;
@@ -1375,7 +1437,8 @@ static hipError_t launch_8p_act(const GemmArgs& g, int splits, hipStream_t st) {
   }();
   GemmArgs ga = g;
   ga.dbg = dbg;
-  hipLaunchKernelGGL((gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT, GA, F8A, GB>), dim3(grid, 1, splits), dim3(512), lds, st, ga);
+  hipLaunchKernelGGL((gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT, GA, F8A, GB, MX>), dim3(grid, 1, splits), dim3(512), lds,
+                     st, ga);
   return hipGetLastError();
 }
 
@@ -1497,15 +1560,20 @@ hipError_t launch_conv_fwd(const GemmArgs& g, hipStream_t st) {
 hipError_t launch_conv_fwd_fp8(const GemmArgs& g, hipStream_t st) {
   if (g.M <= 0 || g.N <= 0) return hipSuccess;
   const int C = 1 << g.cv_logC;
+  const bool mx = g.a_mx && g.b_mx;
   const bool ok = g.a_kmajor && g.b_kmajor && g.cv_logC >= 7 && g.K % C == 0 && g.K % 128 == 0 && g.K >= 256 &&
                   g.M >= 128 && g.N >= 256 && g.N % 8 == 0 && g.ldc % 8 == 0 && !g.bias && g.act == 0 && !g.c_f32 &&
-                  g.a_scale && g.b_scale && (int64_t)(g.N - 1) * g.ldb + g.K < ((int64_t)1 << 31) &&
+                  ((g.a_scale && g.b_scale) || (mx && g.ldb == g.K)) &&
+                  (int64_t)(g.N - 1) * g.ldb + g.K < ((int64_t)1 << 31) &&
                   g.cv_abytes > 0 && (int64_t)(g.M - 1) * g.ldc + g.N < ((int64_t)1 << 31) && g.cv_S > 0 &&
                   g.cv_W < 32768 && g.cv_H < 32768;
   if (!ok) return hipErrorNotSupported;
   // 128-row tiles always: WRN-101-2 b512 A/B on two boxes, 3,443 vs 3,313 and 3,806 / 3,779 vs
   // 3,749 img/s against the bf16-calibrated pick_bm (the fp8 tile is LDS/DMA-bound, so the taller
   // tile's extra reuse buys less than its wave quantisation costs)
+  if (mx)  // block-scaled: 128-row tiles (the scale staging needs the LDS a 256-row tile leaves no room for)
+    return g.f8a == 1 ? launch_8p_act<128, true, true, 0, true, 0, true, 1, false, true>(g, 1, st)
+                      : launch_8p_act<128, true, true, 0, true, 0, true, 0, false, true>(g, 1, st);
   const bool b128 = f8_bm_override() ? f8_bm_override() == 128 : true;
   if (g.f8a == 1)
     return b128 ? launch_8p_act<128, true, true, 0, true, 0, true, 1>(g, 1, st)
@@ -1516,6 +1584,18 @@ hipError_t launch_conv_fwd_fp8(const GemmArgs& g, hipStream_t st) {
 
 hipError_t launch_gemm_fp8(const GemmArgs& g, hipStream_t st) {
   if (g.M <= 0 || g.N <= 0) return hipSuccess;
+  if (g.a_mx || g.b_mx) {  // block-scaled (MX): 128-row tiles
+    if (!g.a_mx || !g.b_mx || g.K % 128 != 0 || !g.a_kmajor || !g.b_kmajor || g.lda != g.K || g.ldb != g.K ||
+        !fits_rsrc(g, 1) || g.N % 8 != 0 || g.ldc % 8 != 0 || (reinterpret_cast<uintptr_t>(g.bias) & 3))
+      return hipErrorInvalidValue;
+    if (g.f8a == 1) {
+      if (g.bias || g.act) return hipErrorInvalidValue;
+      return launch_8p_act<128, true, true, 0, true, 0, false, 1, false, true>(g, 1, st);
+    }
+    if (g.act == 1) return launch_8p_act<128, true, true, 0, true, 1, false, 0, false, true>(g, 1, st);
+    if (g.act == 2) return launch_8p_act<128, true, true, 0, true, 2, false, 0, false, true>(g, 1, st);
+    return launch_8p_act<128, true, true, 0, true, 0, false, 0, false, true>(g, 1, st);
+  }
   if (g.K % 128 != 0 || !g.a_kmajor || !g.b_kmajor || !g.a_scale || !g.b_scale || !fits_rsrc(g, 1) ||
       g.N % 8 != 0 || g.ldc % 8 != 0 || (reinterpret_cast<uintptr_t>(g.bias) & 3))
     return hipErrorInvalidValue;

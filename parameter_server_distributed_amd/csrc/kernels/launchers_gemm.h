@@ -25,6 +25,10 @@ struct GemmArgs {
   int cv_H, cv_W, cv_logC, cv_Ho, cv_Wo, cv_S, cv_stride, cv_pad;
   uint32_t cv_abytes;  // input tensor bytes
   int f8a;             // fp8 GEMMs: format of A (0 OCP e4m3, 1 OCP e5m2); B is always e4m3
+  // MX fp8 (both set: block-scaled instead of a_scale / b_scale): E8M0 scale bytes per 32 contiguous
+  // K-elements, A [M][K/32] (implicit-GEMM conv: of the input, [pixels][C/32]), B [N][K/32]
+  const uint8_t* a_mx;
+  const uint8_t* b_mx;
 };
 
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t stream);

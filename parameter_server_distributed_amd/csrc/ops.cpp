@@ -366,4 +366,37 @@ void dequant_fp8_(const at::Tensor& x, const at::Tensor& scale_inv, at::Tensor o
   out.copy_(x.to(at::kFloat) * scale_inv.data_ptr<float>()[0]);
 }
 
+// MX fp8: out = fp8(x / 2^(s - 127)) with one E8M0 byte s per 32 consecutive elements (scales)
+void quant_mx_(const at::Tensor& x, at::Tensor out, at::Tensor scales) {
+  const bool e5 = out.scalar_type() == at::kFloat8_e5m2;
+  TORCH_CHECK((out.scalar_type() == at::kFloat8_e4m3fn || e5) && out.numel() == x.numel() && out.is_contiguous(),
+              "psd: quant_mx out must be float8_e4m3fn or float8_e5m2 like x");
+  TORCH_CHECK(x.is_contiguous() && x.is_cuda() && x.numel() % 32 == 0,
+              "psd: quant_mx input must be a contiguous device tensor of a multiple of 32 elements");
+  TORCH_CHECK(scales.scalar_type() == at::kByte && scales.is_contiguous() && scales.numel() == x.numel() / 32,
+              "psd: quant_mx scales must be uint8 [numel / 32]");
+  const c10::DeviceGuard g(x.device());
+  if (x.numel() == 0) return;
+  check_aligned(x, "x");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(out.data_ptr()) & 7u) == 0, "psd: fp8 out must be 8-byte aligned");
+  hip_check(launch_quant_mx(x.data_ptr(), dt_of(x), x.numel(), e5 ? 1 : 0, reinterpret_cast<uint8_t*>(out.data_ptr()),
+                            scales.data_ptr<uint8_t>(), cur_stream(x)),
+            "quant_mx");
+}
+
+void dequant_mx_(const at::Tensor& q, const at::Tensor& scales, at::Tensor out) {
+  TORCH_CHECK(q.scalar_type() == at::kFloat8_e4m3fn && q.is_contiguous() && q.is_cuda() && out.numel() == q.numel() &&
+                  out.is_contiguous() && q.numel() % 32 == 0,
+              "psd: dequant_mx q must be a contiguous e4m3fn device tensor (numel % 32 == 0), out like q");
+  TORCH_CHECK(scales.scalar_type() == at::kByte && scales.is_contiguous() && scales.numel() == q.numel() / 32,
+              "psd: dequant_mx scales must be uint8 [numel / 32]");
+  const c10::DeviceGuard g(q.device());
+  if (q.numel() == 0) return;
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(q.data_ptr()) & 7u) == 0, "psd: fp8 q must be 8-byte aligned");
+  check_aligned(out, "out");
+  hip_check(launch_dequant_mx(reinterpret_cast<const uint8_t*>(q.data_ptr()), scales.data_ptr<uint8_t>(), q.numel(),
+                              out.data_ptr(), dt_of(out), cur_stream(q)),
+            "dequant_mx");
+}
+
 }  // namespace psd

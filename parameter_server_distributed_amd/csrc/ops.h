@@ -16,6 +16,8 @@ void quant_fp8_(const at::Tensor& x, const at::Tensor& amax, double fp8_max, at:
 void quant_fp8_jit_(const at::Tensor& x, at::Tensor out, at::Tensor scale_inv);
 void quant_fp8_delayed_(const at::Tensor& x, at::Tensor out, at::Tensor scale_inv, at::Tensor hist, double margin);
 void dequant_fp8_(const at::Tensor& x, const at::Tensor& scale_inv, at::Tensor out);
+void quant_mx_(const at::Tensor& x, at::Tensor out, at::Tensor scales);
+void dequant_mx_(const at::Tensor& q, const at::Tensor& scales, at::Tensor out);
 
 std::vector<at::Tensor> bn_fwd(const at::Tensor& x, c10::optional<at::Tensor> gamma, c10::optional<at::Tensor> beta,
                                c10::optional<at::Tensor> running_mean, c10::optional<at::Tensor> running_var,

@@ -47,3 +47,37 @@ def dequantize_fp8(q: torch.Tensor, scale_inv: torch.Tensor, dtype=torch.bfloat1
     out = torch.empty(q.shape, dtype=dtype, device=q.device)
     native().dequant_fp8_(q.contiguous(), scale_inv, out)
     return out
+
+
+def quantize_mx(x: torch.Tensor, e5m2: bool = False):
+    """MX (OCP microscaling) fp8: ``(q, scales)`` with one E8M0 byte per 32 consecutive elements of
+    the contiguous ``x`` (numel % 32 == 0), ``x ~= q * 2^(scale - 127)`` blockwise -- the operand
+    format of the block-scaled MFMA (``gemm_fp8_`` / ``conv_fwd_fp8_`` with uint8 scales). Device
+    tensors run kernels/fp8.hip quant_mx_kernel; host tensors the reference below (same rounding)."""
+    x = x.contiguous()
+    if not x.is_cuda:
+        return quantize_mx_ref(x, e5m2)
+    q = torch.empty(x.shape, dtype=torch.float8_e5m2 if e5m2 else torch.float8_e4m3fn, device=x.device)
+    s = torch.empty(x.numel() // 32, dtype=torch.uint8, device=x.device)
+    native().quant_mx_(x, q, s)
+    return q, s
+
+
+def quantize_mx_ref(x: torch.Tensor, e5m2: bool = False):
+    """PyTorch reference of quant_mx_kernel: per 32-block the smallest power of two 2^e with
+    amax * 2^-e <= fp8 max (E8M0 byte e + 127; 127 for an all-zero block), round-to-nearest-even."""
+    fmax = FP8_E5M2_MAX if e5m2 else FP8_E4M3_MAX
+    xf = x.float().reshape(-1, 32)
+    amax = xf.abs().amax(1)
+    m, p = torch.frexp(amax / fmax)
+    e = torch.where(m == 0.5, p - 1, p).clamp(-127, 127)
+    e = torch.where((amax > 0) & torch.isfinite(amax), e, torch.zeros_like(e))
+    q = (xf * torch.exp2(-e.float()).unsqueeze(1)).clamp(-fmax, fmax)
+    q = q.to(torch.float8_e5m2 if e5m2 else torch.float8_e4m3fn).reshape(x.shape)
+    return q, (e + 127).to(torch.uint8)
+
+
+def dequantize_mx_ref(q: torch.Tensor, scales: torch.Tensor) -> torch.Tensor:
+    """fp32 ``q * 2^(scale - 127)`` blockwise (reference / host path of dequant_mx_)."""
+    v = q.float().reshape(-1, 32) * torch.exp2(scales.float() - 127.0).unsqueeze(1)
+    return v.reshape(q.shape)
