@@ -62,7 +62,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_bwd_dual", &bn_bwd_dual, py::arg("dy"), py::arg("x"), py::arg("gamma"), py::arg("save_mean"),
         py::arg("save_invstd"), py::arg("mbits"), py::arg("dy2"), py::arg("xd"), py::arg("gamma_d"), py::arg("mean_d"),
         py::arg("invstd_d"), py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none(),
-        py::arg("dgamma_d_out") = py::none(), py::arg("dbeta_d_out") = py::none());
+        py::arg("dgamma_d_out") = py::none(), py::arg("dbeta_d_out") = py::none(), py::arg("fold") = false);
+  m.def("bn_bwd_coef", &bn_bwd_coef, py::arg("dy"), py::arg("x"), py::arg("gamma"), py::arg("save_mean"),
+        py::arg("save_invstd"), py::arg("mbits") = py::none(), py::arg("dy2") = py::none(), py::arg("part") = py::none(),
+        py::arg("rows") = 0, py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none());
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("gamma"), py::arg("save_mean"),
         py::arg("save_invstd"), py::arg("relu"), py::arg("need_dr"), py::arg("dgamma_out"), py::arg("dbeta_out"),
         py::arg("dy2") = py::none(), py::arg("ss") = py::none(), py::arg("mbits") = py::none());
@@ -73,11 +76,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_fp8_", &gemm_fp8_, py::arg("A"), py::arg("B"), py::arg("a_scale"), py::arg("b_scale"), py::arg("out"),
         py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("aux") = py::none());
   m.def("convn_", &convn_, py::arg("x"), py::arg("w2"), py::arg("out"), py::arg("R"), py::arg("S"), py::arg("stride"),
-        py::arg("pad"), py::arg("part") = py::none(), py::arg("shift") = py::none(), py::arg("variant") = -1);
+        py::arg("pad"), py::arg("part") = py::none(), py::arg("shift") = py::none(), py::arg("variant") = -1,
+        py::arg("x2") = py::none(), py::arg("bias") = py::none());
   m.def("convn_stats_rows", &convn_stats_rows_, py::arg("M"));
   m.def("convn_bwd_", &convn_bwd_, py::arg("dy"), py::arg("w2"), py::arg("out"), py::arg("R"), py::arg("S"),
         py::arg("stride"), py::arg("pad"), py::arg("part"), py::arg("variant"), py::arg("mode"), py::arg("bx"),
-        py::arg("bmean"), py::arg("bss") = py::none(), py::arg("bdr") = py::none(), py::arg("bmbits") = py::none());
+        py::arg("bmean"), py::arg("bss") = py::none(), py::arg("bdr") = py::none(), py::arg("bmbits") = py::none(),
+        py::arg("x2") = py::none(), py::arg("bias") = py::none());
   m.def("bn_bwd_pre", &bn_bwd_pre, py::arg("g"), py::arg("x"), py::arg("gamma"), py::arg("save_mean"),
         py::arg("save_invstd"), py::arg("part"), py::arg("rows"), py::arg("dgamma_out") = py::none(),
         py::arg("dbeta_out") = py::none());
@@ -86,6 +91,14 @@ PYBIND11_MODULE(_C, m) {
         py::arg("stride"), py::arg("pad"));
   m.def("conv_wgrad_", &conv_wgrad_, py::arg("dy"), py::arg("x"), py::arg("out"), py::arg("R"), py::arg("S"),
         py::arg("stride"), py::arg("pad"), py::arg("splits") = 0);
+  m.def("convw_", &convw_, py::arg("dy"), py::arg("x"), py::arg("out"), py::arg("R"), py::arg("S"), py::arg("stride"),
+        py::arg("pad"), py::arg("variant") = -1, py::arg("accumulate") = false, py::arg("fold") = false);
+  m.def("bn_elemt_coef", &bn_elemt_coef, py::arg("g"), py::arg("x"), py::arg("coef"));
+  m.def("convw_fold_rows", &convw_fold_rows, py::arg("Cout"), py::arg("Cin"));
+  m.def("bnfold_dgrad_weights", &bnfold_dgrad_weights, py::arg("w"), py::arg("coef"));
+  m.def("bnfold_combine", &bnfold_combine, py::arg("P"), py::arg("w"), py::arg("coef"), py::arg("out"),
+        py::arg("accumulate") = false);
+  m.def("convw_variants", &convw_variants_, py::arg("Cout"), py::arg("KK"));
   m.def("conv_fwd_fp8_", &conv_fwd_fp8_, py::arg("x"), py::arg("w2"), py::arg("x_scale"), py::arg("w_scale"),
         py::arg("out"), py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"));
   m.def("gelu_bwd_colsum_", &gelu_bwd_colsum_, py::arg("dy"), py::arg("pre"), py::arg("dx"), py::arg("out"),

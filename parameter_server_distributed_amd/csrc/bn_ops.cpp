@@ -6,6 +6,7 @@
 #include <vector>
 
 #include "kernels/launchers_bn.h"
+#include "ops.h"
 #include "kernels/launchers_stem.h"
 
 namespace psd {
@@ -307,7 +308,8 @@ std::vector<at::Tensor> bn_bwd_dual(const at::Tensor& dy_in, const at::Tensor& x
                                     c10::optional<at::Tensor> dy2_in, const at::Tensor& xd_in, const at::Tensor& gamma_d,
                                     const at::Tensor& mean_d, const at::Tensor& invstd_d,
                                     c10::optional<at::Tensor> dgamma_out, c10::optional<at::Tensor> dbeta_out,
-                                    c10::optional<at::Tensor> dgamma_d_out, c10::optional<at::Tensor> dbeta_d_out) {
+                                    c10::optional<at::Tensor> dgamma_d_out, c10::optional<at::Tensor> dbeta_d_out,
+                                    bool fold) {
   const c10::DeviceGuard g(x_in.device());
   at::Tensor x = nhwc(x_in), dy = nhwc(dy_in), xd = nhwc(xd_in);
   const int64_t C = channels(x);
@@ -332,7 +334,8 @@ std::vector<at::Tensor> bn_bwd_dual(const at::Tensor& dy_in, const at::Tensor& x
   at::Tensor dgamma = grad_buf(dgamma_out), dbeta = grad_buf(dbeta_out);
   at::Tensor dgamma_d = grad_buf(dgamma_d_out), dbeta_d = grad_buf(dbeta_d_out);
   auto f32 = x.options().dtype(at::kFloat);
-  at::Tensor dx = at::empty_like(x), dxd = at::empty_like(x), dr = at::empty_like(x);
+  // fold: no dx (the consumer convolution folds it); its coefficients and dr (= g) are returned
+  at::Tensor dx = fold ? at::Tensor() : at::empty_like(x), dxd = at::empty_like(x), dr = at::empty_like(x);
   at::Tensor coef = at::empty({3 * C}, f32), coef_d = at::empty({3 * C}, f32);
   const int64_t np = (int64_t)bn_reduce_blocks(M, (int)C) * 2 * C;
   at::Tensor part = at::empty({np}, f32), part_d = at::empty({np}, f32);
@@ -344,7 +347,7 @@ std::vector<at::Tensor> bn_bwd_dual(const at::Tensor& dy_in, const at::Tensor& x
   a.gamma = reinterpret_cast<const uint16_t*>(gamma.data_ptr());
   a.save_mean = save_mean.data_ptr<float>();
   a.save_invstd = save_invstd.data_ptr<float>();
-  a.dx = reinterpret_cast<uint16_t*>(dx.data_ptr());
+  a.dx = fold ? nullptr : reinterpret_cast<uint16_t*>(dx.data_ptr());
   a.dr = reinterpret_cast<uint16_t*>(dr.data_ptr());
   a.dgamma = reinterpret_cast<uint16_t*>(dgamma.data_ptr());
   a.dbeta = reinterpret_cast<uint16_t*>(dbeta.data_ptr());
@@ -364,7 +367,79 @@ std::vector<at::Tensor> bn_bwd_dual(const at::Tensor& dy_in, const at::Tensor& x
   a.part_d = part_d.data_ptr<float>();
   hipError_t e = launch_bn_bwd(a, stream_of(x));
   TORCH_CHECK(e == hipSuccess, "psd bn bwd_dual: ", hipGetErrorString(e));
+  if (fold) return {dx, dxd, dgamma, dbeta, dgamma_d, dbeta_d, coef, dr};
   return {dx, dxd, dgamma, dbeta, dgamma_d, dbeta_d};
+}
+
+// BN backward without the elementwise pass (the BN-backward fold: the consumer convolution's dgrad /
+// wgrad take g and these coefficients, kernels/bnfold.hip): returns {g, coef [3C] = (A, B, C) of
+// dx = A g + B x + C, dgamma, dbeta}. With `part` the producer-reduced partials of an already masked
+// g = dy (kernels/convn.hip bwd mode 2); else one reduction pass over dy (+ dy2) under the forward
+// bit-mask that also writes g (the residual-branch gradient).
+std::vector<at::Tensor> bn_bwd_coef(const at::Tensor& dy_in, const at::Tensor& x_in, const at::Tensor& gamma,
+                                    const at::Tensor& save_mean, const at::Tensor& save_invstd,
+                                    c10::optional<at::Tensor> mbits_in, c10::optional<at::Tensor> dy2_in,
+                                    c10::optional<at::Tensor> part, int64_t rows, c10::optional<at::Tensor> dgamma_out,
+                                    c10::optional<at::Tensor> dbeta_out) {
+  const c10::DeviceGuard dg(x_in.device());
+  at::Tensor x = nhwc(x_in), dy = nhwc(dy_in);
+  const int64_t C = channels(x), M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0 && dy.sizes() == x.sizes() && dy.scalar_type() == at::kBFloat16 &&
+                  x.scalar_type() == at::kBFloat16,
+              "psd bn_bwd_coef: dy like x (bf16)");
+  for (const at::Tensor* t : {&save_mean, &save_invstd})
+    TORCH_CHECK(t->numel() == C && t->scalar_type() == at::kFloat && t->is_contiguous(), "psd bn_bwd_coef: stats [C]");
+  auto f32 = x.options().dtype(at::kFloat);
+  auto grad_buf = [&](const c10::optional<at::Tensor>& o) {
+    at::Tensor t = (o.has_value() && o->defined()) ? *o : at::empty({C}, x.options());
+    TORCH_CHECK(t.numel() == C && t.scalar_type() == at::kBFloat16 && t.is_contiguous(), "psd bn_bwd_coef: grad buffer");
+    return t;
+  };
+  at::Tensor dgamma = grad_buf(dgamma_out), dbeta = grad_buf(dbeta_out);
+  at::Tensor coef = at::empty({3 * C}, f32);
+  const uint16_t* gam = reinterpret_cast<const uint16_t*>(gamma.data_ptr());
+  if (part.has_value() && part->defined()) {
+    TORCH_CHECK(part->scalar_type() == at::kFloat && part->is_contiguous() && rows > 0 && part->numel() >= rows * 2 * C,
+                "psd bn_bwd_coef: part must be fp32 [rows, 2, C]");
+    at::Tensor fold = rows > kFoldRows ? at::empty({(int64_t)kFoldRows * 2 * C}, f32) : at::Tensor();
+    const hipError_t e = launch_bn_bwd_pre(
+        reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(x.data_ptr()), gam,
+        save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(), part->data_ptr<float>(), (int)rows,
+        fold.defined() ? fold.data_ptr<float>() : nullptr, reinterpret_cast<uint16_t*>(dgamma.data_ptr()),
+        reinterpret_cast<uint16_t*>(dbeta.data_ptr()), coef.data_ptr<float>(), nullptr, M, (int)C, stream_of(x));
+    TORCH_CHECK(e == hipSuccess, "psd bn_bwd_coef: ", hipGetErrorString(e));
+    return {dy, coef, dgamma, dbeta};
+  }
+  TORCH_CHECK(mbits_in.has_value() && mbits_in->defined() && mbits_in->scalar_type() == at::kByte &&
+                  mbits_in->is_contiguous() && mbits_in->numel() == M * C / 8,
+              "psd bn_bwd_coef: without partials the forward bit-mask (uint8 [M*C/8]) is required");
+  at::Tensor dy2;
+  if (dy2_in.has_value() && dy2_in->defined()) {
+    dy2 = nhwc(*dy2_in);
+    TORCH_CHECK(dy2.sizes() == x.sizes() && dy2.scalar_type() == at::kBFloat16, "psd bn_bwd_coef: dy2 shape/dtype");
+  }
+  at::Tensor g = at::empty_like(x);
+  at::Tensor pt = at::empty({(int64_t)bn_reduce_blocks(M, (int)C) * 2 * C}, f32);
+  BnBwdArgs a{};
+  a.dy = reinterpret_cast<const uint16_t*>(dy.data_ptr());
+  a.dy2 = dy2.defined() ? reinterpret_cast<const uint16_t*>(dy2.data_ptr()) : nullptr;
+  a.mbits = mbits_in->data_ptr<uint8_t>();
+  a.x = reinterpret_cast<const uint16_t*>(x.data_ptr());
+  a.gamma = gam;
+  a.save_mean = save_mean.data_ptr<float>();
+  a.save_invstd = save_invstd.data_ptr<float>();
+  a.dr = reinterpret_cast<uint16_t*>(g.data_ptr());
+  a.dgamma = reinterpret_cast<uint16_t*>(dgamma.data_ptr());
+  a.dbeta = reinterpret_cast<uint16_t*>(dbeta.data_ptr());
+  a.coef = coef.data_ptr<float>();
+  a.part = pt.data_ptr<float>();
+  a.M = M;
+  a.C = (int32_t)C;
+  a.relu = 1;
+  a.coef_only = 1;
+  const hipError_t e = launch_bn_bwd(a, stream_of(x));
+  TORCH_CHECK(e == hipSuccess, "psd bn_bwd_coef: ", hipGetErrorString(e));
+  return {g, coef, dgamma, dbeta};
 }
 
 // Stem BN + ReLU + 3x3/s2 max-pool (training forward): returns {y_pool, argmax, mean, invstd, ss}.
@@ -617,4 +692,72 @@ at::Tensor gap_bwd(const at::Tensor& dy_in, int64_t H, int64_t W) {
   TORCH_CHECK(e == hipSuccess, "psd gap bwd: ", hipGetErrorString(e));
   return dx;
 }
+// ---- BN-backward fold of a 1x1 conv -> BN pair (kernels/bnfold.hip)
+
+namespace {
+at::Tensor fold_w2d(const at::Tensor& w) {
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && (w.dim() == 2 || (w.dim() == 4 && w.size(2) == 1 &&
+                                                                                   w.size(3) == 1)),
+              "psd bnfold: w must be the bf16 [Cout, Cin(, 1, 1)] weight of a 1x1 convolution");
+  return w.reshape({w.size(0), w.size(1)}).contiguous();
+}
+}  // namespace
+
+// The folded dgrad operands: w2 [Cin, Cout + Cin] bf16 = [(A o W)^T | W^T (B o W)] and the bias
+// bvec [Cin] fp32 = C^T W, so dgrad = [g | x] . w2^T + bvec (kernels/convn.hip with x2 = x).
+std::vector<at::Tensor> bnfold_dgrad_weights(const at::Tensor& w_in, const at::Tensor& coef) {
+  const c10::DeviceGuard dg(w_in.device());
+  const at::Tensor w = fold_w2d(w_in);
+  const int64_t Cout = w.size(0), Cin = w.size(1);
+  TORCH_CHECK(coef.scalar_type() == at::kFloat && coef.is_contiguous() && coef.numel() == 3 * Cout &&
+                  coef.device() == w.device(),
+              "psd bnfold: coef must be fp32 [3 * Cout]");
+  at::Tensor w2 = at::empty({Cin, Cout + Cin}, w.options());
+  at::Tensor bw = at::empty({Cout, Cin}, w.options());
+  at::Tensor bvec = at::empty({Cin}, w.options().dtype(at::kFloat));
+  hipError_t e = launch_bnfold_prep(reinterpret_cast<const uint16_t*>(w.data_ptr()), coef.data_ptr<float>(), (int)Cout,
+                                    (int)Cin, reinterpret_cast<uint16_t*>(w2.data_ptr()), (int)(Cout + Cin),
+                                    reinterpret_cast<uint16_t*>(bw.data_ptr()), bvec.data_ptr<float>(), stream_of(w));
+  TORCH_CHECK(e == hipSuccess, "psd bnfold prep: ", hipGetErrorString(e));
+  // M = (B o W)^T W (Cin x Cin, symmetric) into the right block of w2 (the MFMA GEMM, TN layout)
+  gemm_(bw, w, false, false, w2.narrow(1, Cout, Cin), c10::nullopt, 0, c10::nullopt);
+  return {w2, bvec};
+}
+
+// dW = A o P[:Cout] + B o (W P[Cout:Cout+Cin]) + C P[Cout+Cin] (P = kernels/convw.hip fold output)
+// into out (bf16 [Cout, Cin] view, += with accumulate)
+void bnfold_combine(const at::Tensor& P, const at::Tensor& w_in, const at::Tensor& coef, at::Tensor out,
+                    bool accumulate) {
+  const c10::DeviceGuard dg(w_in.device());
+  const at::Tensor w = fold_w2d(w_in);
+  const int64_t Cout = w.size(0), Cin = w.size(1);
+  TORCH_CHECK(P.scalar_type() == at::kFloat && P.is_contiguous() && P.dim() == 2 && P.size(1) == Cin &&
+                  P.size(0) > Cout + Cin && P.device() == w.device(),
+              "psd bnfold combine: P must be the fp32 convw fold result [rows, Cin]");
+  TORCH_CHECK(coef.scalar_type() == at::kFloat && coef.is_contiguous() && coef.numel() == 3 * Cout,
+              "psd bnfold combine: coef must be fp32 [3 * Cout]");
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 && out.is_contiguous() && out.numel() == Cout * Cin &&
+                  out.device() == w.device(),
+              "psd bnfold combine: out must be a contiguous bf16 [Cout, Cin]");
+  hipError_t e = launch_bnfold_combine(P.data_ptr<float>(), reinterpret_cast<const uint16_t*>(w.data_ptr()),
+                                       coef.data_ptr<float>(), (int)Cout, (int)Cin,
+                                       reinterpret_cast<uint16_t*>(out.data_ptr()), accumulate ? 1 : 0, stream_of(w));
+  TORCH_CHECK(e == hipSuccess, "psd bnfold combine: ", hipGetErrorString(e));
+}
+
+at::Tensor bn_elemt_coef(const at::Tensor& g_in, const at::Tensor& x_in, const at::Tensor& coef) {
+  const c10::DeviceGuard dg(x_in.device());
+  at::Tensor x = nhwc(x_in), g = nhwc(g_in);
+  const int64_t C = channels(x), M = x.numel() / C;
+  TORCH_CHECK(g.sizes() == x.sizes() && g.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16 &&
+                  coef.scalar_type() == at::kFloat && coef.numel() == 3 * C && coef.is_contiguous(),
+              "psd bn_elemt_coef: g like x (bf16), coef fp32 [3C]");
+  at::Tensor dx = at::empty_like(x);
+  const hipError_t e = launch_bn_elemt_coef(reinterpret_cast<const uint16_t*>(g.data_ptr()),
+                                            reinterpret_cast<const uint16_t*>(x.data_ptr()), coef.data_ptr<float>(),
+                                            reinterpret_cast<uint16_t*>(dx.data_ptr()), M, (int)C, stream_of(x));
+  TORCH_CHECK(e == hipSuccess, "psd bn_elemt_coef: ", hipGetErrorString(e));
+  return dx;  // empty_like keeps the channels_last layout
+}
+
 }  // namespace psd

@@ -4,6 +4,7 @@
 #include <c10/hip/HIPStream.h>
 
 #include "kernels/launchers_convn.h"
+#include "kernels/launchers_convw.h"
 #include "kernels/launchers_gemm.h"
 
 namespace psd {
@@ -217,8 +218,36 @@ static bool conv_fwd_impl(const at::Tensor& x, const at::Tensor& w2, at::Tensor 
 int64_t convn_stats_rows_(int64_t M) { return convn_stats_rows((int)M); }
 int64_t convn_variants_(int64_t N) { return convn_variants((int)N); }
 
+namespace {
+// K-concatenated second operand + epilogue bias of a convn launch (the BN-backward fold); returns the
+// extra K (C2) or -1 when x2 is unusable. x2: channels_last bf16 [Nb, C2, H, W] like the input.
+int64_t convn_x2(ConvnArgs& a, const at::Tensor& x, c10::optional<at::Tensor> x2, c10::optional<at::Tensor> bias,
+                 int64_t N) {
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() == N && bias->is_contiguous() &&
+                    bias->device() == x.device(),
+                "psd convn: bias must be fp32 [N] on the input's device");
+    a.bias = bias->data_ptr<float>();
+  }
+  if (!(x2.has_value() && x2->defined())) return 0;
+  TORCH_CHECK(x2->is_cuda() && x2->dim() == 4 && x2->scalar_type() == at::kBFloat16 &&
+                  x2->is_contiguous(at::MemoryFormat::ChannelsLast) && x2->device() == x.device() &&
+                  x2->size(0) == x.size(0) && x2->size(2) == x.size(2) && x2->size(3) == x.size(3),
+              "psd convn: x2 must be a channels_last bf16 tensor with the input's N, H, W");
+  const int64_t C2 = x2->size(1), bytes = x2->numel() * 2;
+  if (C2 < 64 || (C2 & (C2 - 1)) != 0 || bytes > 0xFFFFFF00ll) return -1;
+  int l = 0;
+  while ((1 << l) < C2) ++l;
+  a.x2 = x2->data_ptr();
+  a.x2bytes = (uint32_t)bytes;
+  a.logC2 = l;
+  return C2;
+}
+}  // namespace
+
 int64_t convn_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride,
-               int64_t pad, c10::optional<at::Tensor> part, c10::optional<at::Tensor> shift, int64_t variant) {
+               int64_t pad, c10::optional<at::Tensor> part, c10::optional<at::Tensor> shift, int64_t variant,
+               c10::optional<at::Tensor> x2, c10::optional<at::Tensor> bias) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.scalar_type() == at::kBFloat16 &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast),
               "psd convn: x must be a channels_last bf16 device tensor");
@@ -229,8 +258,12 @@ int64_t convn_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_
               "psd convn: out must be a bf16 [M, Cout] device tensor, 16-B aligned");
   const int64_t Nb = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
   const int64_t Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
-  const int64_t M = Nb * Ho * Wo, Cout = w2.size(0), K = R * S * C;
-  TORCH_CHECK(w2.size(1) == K, "psd convn: w2 must be [Cout, R*S*C]");
+  const int64_t M = Nb * Ho * Wo, Cout = w2.size(0), K1 = R * S * C;
+  ConvnArgs a{};
+  const int64_t C2 = convn_x2(a, x, x2, bias, Cout);
+  if (C2 < 0) return 0;
+  const int64_t K = K1 + C2;
+  TORCH_CHECK(w2.size(1) == K, "psd convn: w2 must be [Cout, R*S*C (+ C2)]");
   TORCH_CHECK(out.size(0) == M && out.size(1) == Cout, "psd convn: out must be [Nb*Ho*Wo, Cout]");
   const bool stats = part.has_value() && part->defined();
   if (stats) {
@@ -249,7 +282,7 @@ int64_t convn_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_
   int logc = 0;
   while ((1 << logc) < C) ++logc;
   const c10::DeviceGuard g(x.device());
-  ConvnArgs a{};
+  a.K1 = (int)K1;
   a.x = x.data_ptr();
   a.w = w2.data_ptr();
   a.y = out.data_ptr();
@@ -283,7 +316,7 @@ int64_t convn_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_
 int64_t convn_bwd_(const at::Tensor& dy, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride,
                    int64_t pad, at::Tensor part, int64_t variant, int64_t mode, const at::Tensor& bx,
                    const at::Tensor& bmean, c10::optional<at::Tensor> bss, c10::optional<at::Tensor> bdr,
-                   c10::optional<at::Tensor> bmbits) {
+                   c10::optional<at::Tensor> bmbits, c10::optional<at::Tensor> x2, c10::optional<at::Tensor> bias) {
   TORCH_CHECK(dy.is_cuda() && dy.dim() == 4 && dy.scalar_type() == at::kBFloat16 &&
                   dy.is_contiguous(at::MemoryFormat::ChannelsLast),
               "psd convn_bwd: dy must be a channels_last bf16 device tensor");
@@ -293,7 +326,11 @@ int64_t convn_bwd_(const at::Tensor& dy, const at::Tensor& w2, at::Tensor out, i
   TORCH_CHECK(mode == 1 || mode == 2, "psd convn_bwd: mode 1 (mask from x, ss) or 2 (bit-mask + dr)");
   const int64_t Nb = dy.size(0), C = dy.size(1), H = dy.size(2), W = dy.size(3);
   const int64_t Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
-  const int64_t M = Nb * Ho * Wo, N = w2.size(0), K = R * S * C;
+  const int64_t M = Nb * Ho * Wo, N = w2.size(0), K1 = R * S * C;
+  ConvnArgs a{};
+  const int64_t C2 = convn_x2(a, dy, x2, bias, N);
+  if (C2 < 0) return 0;
+  const int64_t K = K1 + C2;
   TORCH_CHECK(w2.size(1) == K && out.size(0) == M && out.size(1) == N, "psd convn_bwd: shapes");
   auto like_out = [&](const at::Tensor& t, const char* what) {
     const at::Tensor u = t.dim() == 4 ? t.permute({0, 2, 3, 1}) : t;
@@ -325,7 +362,7 @@ int64_t convn_bwd_(const at::Tensor& dy, const at::Tensor& w2, at::Tensor out, i
   int logc = 0;
   while ((1 << logc) < C) ++logc;
   const c10::DeviceGuard g(dy.device());
-  ConvnArgs a{};
+  a.K1 = (int)K1;
   a.x = dy.data_ptr();
   a.w = w2.data_ptr();
   a.y = out.data_ptr();
@@ -453,6 +490,75 @@ void gelu_bwd_colsum_(const at::Tensor& dy, const at::Tensor& pre, at::Tensor dx
                                reinterpret_cast<const uint16_t*>(pre.data_ptr()),
                                reinterpret_cast<uint16_t*>(dx.data_ptr()));
   TORCH_CHECK(e == hipSuccess, "psd gelu_bwd_colsum: ", hipGetErrorString(e));
+}
+
+// Narrow implicit-GEMM weight gradient (kernels/convw.hip): out[Cout][R*S*C] (bf16, the OHWI weight
+// layout) = dY^T . im2col(x), or out += that with accumulate. Returns false when the kernel declines
+// the shape (nothing launched).
+int64_t convw_variants_(int64_t Cout, int64_t KK) { return convw_variants((int)Cout, (int)KK); }
+
+// rows of a fold launch's fp32 result: [g^T x (Cout) | x^T x (Cin) | column sums of x (+ padding)]
+// 0 when the fold launch is not supported for this shape
+int64_t convw_fold_rows(int64_t Cout, int64_t Cin) {
+  const int64_t rows = (Cout + Cin + 16 + 127) / 128 * 128;
+  return convw_fold_ok((int)Cout, (int)Cin, (int)rows) ? rows : 0;
+}
+
+bool convw_(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64_t R, int64_t S, int64_t stride,
+            int64_t pad, int64_t variant, bool accumulate, bool fold) {
+  TORCH_CHECK(dy.is_cuda() && x.is_cuda() && dy.dim() == 4 && x.dim() == 4 && dy.scalar_type() == at::kBFloat16 &&
+                  x.scalar_type() == at::kBFloat16 && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast) && dy.device() == x.device(),
+              "psd convw: dy and x must be channels_last bf16 tensors on one device");
+  const int64_t Nb = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t Cout = dy.size(1), Ho = dy.size(2), Wo = dy.size(3);
+  TORCH_CHECK(dy.size(0) == Nb && Ho == (H + 2 * pad - R) / stride + 1 && Wo == (W + 2 * pad - S) / stride + 1,
+              "psd convw: dy shape does not match the convolution");
+  const int64_t KK = R * S * C, M = Nb * Ho * Wo;
+  const int64_t rows = fold ? convw_fold_rows(Cout, KK) : Cout;
+  TORCH_CHECK(out.is_cuda() && out.device() == x.device() && out.dim() == 2 && out.size(0) == rows &&
+                  out.size(1) == KK && out.is_contiguous() &&
+                  out.scalar_type() == (fold ? at::kFloat : at::kBFloat16) &&
+                  (reinterpret_cast<uintptr_t>(out.data_ptr()) & 15) == 0,
+              "psd convw: out must be a contiguous [Cout, R*S*C] bf16 tensor (fold: fp32 [convw_fold_rows, C]) "
+              "on x's device");
+  if (fold && (R != 1 || S != 1 || stride != 1 || pad != 0 || accumulate)) return false;
+  const int64_t xbytes = x.numel() * 2, dybytes = dy.numel() * 2;
+  if ((C & (C - 1)) != 0 || C < 64 || xbytes > 0xFFFFFF00ll || dybytes > 0xFFFFFF00ll || M >= ((int64_t)1 << 31) ||
+      (!fold && variant >= convw_variants((int)Cout, (int)KK)) || H >= 32768 || W >= 32768)
+    return false;
+  int logc = 0;
+  while ((1 << logc) < C) ++logc;
+  const c10::DeviceGuard g(x.device());
+  ConvwArgs a{};
+  a.dy = dy.data_ptr();
+  a.x = x.data_ptr();
+  a.out = out.data_ptr();
+  a.dybytes = (uint32_t)dybytes;
+  a.xbytes = (uint32_t)xbytes;
+  a.M = (int)M;
+  a.Cout = (int)Cout;
+  a.KK = (int)KK;
+  a.H = (int)H;
+  a.W = (int)W;
+  a.logC = logc;
+  a.Ho = (int)Ho;
+  a.Wo = (int)Wo;
+  a.S = (int)S;
+  a.stride = (int)stride;
+  a.pad = (int)pad;
+  a.variant = (int)variant;
+  a.accumulate = accumulate ? 1 : 0;
+  a.fold = fold ? 1 : 0;
+  a.Arows = (int)rows;
+  const ConvwPlan p = convw_plan(a);
+  if (p.splits <= 0) return false;
+  at::Tensor slab = at::empty({p.slab_floats}, x.options().dtype(at::kFloat));
+  a.slab = slab.data_ptr<float>();
+  const hipError_t e = launch_convw(a, stream_of(x));
+  if (e == hipErrorNotSupported) return false;
+  TORCH_CHECK(e == hipSuccess, "psd convw: ", hipGetErrorString(e));
+  return true;
 }
 
 }  // namespace psd

@@ -484,6 +484,9 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(const uint16_t* __res
 }
 
 // dual elementwise pass: dx = A g + B x + C and dxd = Ad g + Bd xd + Cd from one read of g (= dr)
+// WDX false (the BN-backward fold of this BN's consumer convolution, ops/bn.py): only the downsample
+// BN's input gradient is written; this BN's own is folded into its producer's backward GEMMs
+template <bool WDX>
 __global__ __launch_bounds__(256) void bn_bwd_elemt_dual_kernel(const uint16_t* __restrict__ g, const uint16_t* __restrict__ x,
                                                                 const float* __restrict__ coef, uint16_t* __restrict__ dx,
                                                                 const uint16_t* __restrict__ xd,
@@ -501,13 +504,16 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_dual_kernel(const uint16_t* 
   load8_f32(coef_d + C + cg * 8, Bd);
   load8_f32(coef_d + 2 * C + cg * 8, Cd);
   for (; v < nvec; v += stride) {
-    float gv[8], xv[8], dv[8], o[8];
+    float gv[8], dv[8], o[8];
     load8_bf16(g + v * 8, gv);
-    load8_bf16(x + v * 8, xv);
     load8_bf16(xd + v * 8, dv);
+    if constexpr (WDX) {
+      float xv[8];
+      load8_bf16(x + v * 8, xv);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = fmaf(A[j], gv[j], fmaf(B[j], xv[j], Cc[j]));
-    store8_bf16(dx + v * 8, o);
+      for (int j = 0; j < 8; ++j) o[j] = fmaf(A[j], gv[j], fmaf(B[j], xv[j], Cc[j]));
+      store8_bf16(dx + v * 8, o);
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = fmaf(Ad[j], gv[j], fmaf(Bd[j], dv[j], Cd[j]));
     store8_bf16(dxd + v * 8, o);
@@ -852,6 +858,19 @@ hipError_t launch_bn_bwd_pre(const uint16_t* g, const uint16_t* x, const uint16_
   }
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(256), 0, st, p, nblk, M, C, gamma,
                      mean, invstd, dgamma, dbeta, coef);
+  if (!dx) return hipGetLastError();  // coefficients only (BN-backward fold)
+  const int64_t nvec = M * (C / 8);
+  hipLaunchKernelGGL(bn_bwd_elemt_kernel<2>, dim3(elem_grid(nvec, C)), dim3(256), 0, st, g, nullptr, nullptr, nullptr, x,
+                     coef, dx, nvec, C);
+  return hipGetLastError();
+}
+
+// dx = A g + B x + C per channel from finalized coefficients (the unfolded twin of the BN-backward
+// fold: what the BN's own elementwise pass writes)
+hipError_t launch_bn_elemt_coef(const uint16_t* g, const uint16_t* x, const float* coef, uint16_t* dx, int64_t M, int C,
+                                hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  if (C % 8 != 0) return hipErrorInvalidValue;
   const int64_t nvec = M * (C / 8);
   hipLaunchKernelGGL(bn_bwd_elemt_kernel<2>, dim3(elem_grid(nvec, C)), dim3(256), 0, st, g, nullptr, nullptr, nullptr, x,
                      coef, dx, nvec, C);
@@ -879,8 +898,12 @@ hipError_t launch_bn_bwd(const BnBwdArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, fg, dim3(256), 0, st, a.part_d, gx, a.M, a.C, a.gamma_d, a.mean_d,
                        a.invstd_d, a.dgamma_d, a.dbeta_d, a.coef_d);
     const int64_t nvec = a.M * (a.C / 8);
-    hipLaunchKernelGGL(bn_bwd_elemt_dual_kernel, dim3(elem_grid(nvec, a.C)), dim3(256), 0, st, a.dr, a.x, a.coef, a.dx,
-                       a.xd, a.coef_d, a.dxd, nvec, a.C);
+    if (a.dx)
+      hipLaunchKernelGGL(bn_bwd_elemt_dual_kernel<true>, dim3(elem_grid(nvec, a.C)), dim3(256), 0, st, a.dr, a.x, a.coef,
+                         a.dx, a.xd, a.coef_d, a.dxd, nvec, a.C);
+    else
+      hipLaunchKernelGGL(bn_bwd_elemt_dual_kernel<false>, dim3(elem_grid(nvec, a.C)), dim3(256), 0, st, a.dr, a.x,
+                         a.coef, a.dx, a.xd, a.coef_d, a.dxd, nvec, a.C);
     return hipGetLastError();
   }
 #define PSD_RED(K, O)                                                                                              \
@@ -898,6 +921,7 @@ hipError_t launch_bn_bwd(const BnBwdArgs& a, hipStream_t st) {
   if (a.reduce_only) return hipGetLastError();
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((a.C + kFinCh - 1) / kFinCh), dim3(256), 0, st, a.part, gx, a.M, a.C, a.gamma,
                      a.save_mean, a.save_invstd, a.dgamma, a.dbeta, a.coef);
+  if (a.coef_only) return hipGetLastError();  // coefficients for the consumer's BN-backward fold
   const int64_t nvec = a.M * (a.C / 8);
   const int g = elem_grid(nvec, a.C);
 #define PSD_EL(MODE, G, G2) \

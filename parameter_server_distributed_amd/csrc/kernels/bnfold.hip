@@ -1,0 +1,93 @@
+// BN-backward fold for a 1x1 convolution followed by a BatchNorm (ResNet's conv3 -> bn3): the BN's
+// input gradient  dy = A g + B y + C  (per channel c; g the masked upstream gradient, y = x W^T the
+// conv output, kernels/bn.hip bn_bwd_finalize_kernel) is never materialised. Its two consumers are
+// rewritten onto g and the conv input x, which the GEMMs read anyway:
+//
+//   dgrad  dx = dy W = [g | x] . [ (A o W)^T | W^T (B o W) ]^T + (C^T W)     (K = Cout + Cin)
+//   wgrad  dW = dy^T x = A o (g^T x) + B o (W (x^T x)) + C (1^T x)
+//
+// kernels/convn.hip runs the dgrad with the K-concatenated operand and the bias, kernels/convw.hip the
+// wgrad products g^T x, x^T x and 1^T x in one pass. This file holds the small per-step kernels
+// around them: the folded dgrad weight and bias (prep) and the wgrad combination (combine). What the
+// fold removes per bottleneck: the BN elementwise pass (read g and y, write dy: three full
+// activations) -- ~1 ms per layer1 block at b1024 (profiles/resnet50_b1024_r3s3_kernels.md).
+#include "common.h"
+#include "launchers_bn.h"
+
+namespace psd {
+
+// one block per input channel j: w2[j][c] = A_c W[c][j] (c < Cout, row stride ldw), bw[c][j] = B_c W[c][j],
+// bvec[j] = sum_c C_c W[c][j]
+__global__ __launch_bounds__(256) void bnfold_prep_kernel(const uint16_t* __restrict__ W, const float* __restrict__ coef,
+                                                          int Cout, int Wd, uint16_t* __restrict__ w2, int ldw,
+                                                          uint16_t* __restrict__ bw, float* __restrict__ bvec) {
+  __shared__ float red[256];
+  const int j = blockIdx.x;
+  float acc = 0.f;
+  for (int c = threadIdx.x; c < Cout; c += blockDim.x) {
+    const float w = bf16_to_f32(W[(int64_t)c * Wd + j]);
+    w2[(int64_t)j * ldw + c] = f32_to_bf16(coef[c] * w);
+    bw[(int64_t)c * Wd + j] = f32_to_bf16(coef[Cout + c] * w);
+    acc = fmaf(coef[2 * Cout + c], w, acc);
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) bvec[j] = red[0];
+}
+
+// 8 output rows per block: dW[c][i] = A_c P[c][i] + B_c sum_k W[c][k] P[Cout + k][i] + C_c P[Cout + Wd][i]
+constexpr int kCombRows = 8;
+__global__ __launch_bounds__(256) void bnfold_combine_kernel(const float* __restrict__ P, const uint16_t* __restrict__ W,
+                                                             const float* __restrict__ coef, int Cout, int Wd,
+                                                             uint16_t* __restrict__ out, int accumulate) {
+  extern __shared__ float wrow[];  // [kCombRows][Wd]
+  const int c0 = blockIdx.x * kCombRows;
+  for (int e = threadIdx.x; e < kCombRows * Wd; e += blockDim.x) {
+    const int r = e / Wd, k = e - r * Wd;
+    wrow[e] = c0 + r < Cout ? bf16_to_f32(W[(int64_t)(c0 + r) * Wd + k]) : 0.f;
+  }
+  __syncthreads();
+  const float* G = P + (int64_t)Cout * Wd;
+  const float* s = G + (int64_t)Wd * Wd;
+  for (int i = threadIdx.x; i < Wd; i += blockDim.x) {
+    float t[kCombRows];
+#pragma unroll
+    for (int r = 0; r < kCombRows; ++r) t[r] = 0.f;
+    for (int k = 0; k < Wd; ++k) {
+      const float gk = G[(int64_t)k * Wd + i];
+#pragma unroll
+      for (int r = 0; r < kCombRows; ++r) t[r] = fmaf(wrow[r * Wd + k], gk, t[r]);
+    }
+    const float si = s[i];
+#pragma unroll
+    for (int r = 0; r < kCombRows; ++r) {
+      const int c = c0 + r;
+      if (c >= Cout) break;
+      float v = coef[c] * P[(int64_t)c * Wd + i] + coef[Cout + c] * t[r] + coef[2 * Cout + c] * si;
+      uint16_t* o = out + (int64_t)c * Wd + i;
+      if (accumulate) v += bf16_to_f32(*o);
+      *o = f32_to_bf16(v);
+    }
+  }
+}
+
+hipError_t launch_bnfold_prep(const uint16_t* W, const float* coef, int Cout, int Wd, uint16_t* w2, int ldw,
+                              uint16_t* bw, float* bvec, hipStream_t st) {
+  if (Cout <= 0 || Wd <= 0 || ldw < Cout) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bnfold_prep_kernel, dim3(Wd), dim3(256), 0, st, W, coef, Cout, Wd, w2, ldw, bw, bvec);
+  return hipGetLastError();
+}
+
+hipError_t launch_bnfold_combine(const float* P, const uint16_t* W, const float* coef, int Cout, int Wd,
+                                 uint16_t* out, int accumulate, hipStream_t st) {
+  if (Cout <= 0 || Wd <= 0 || Wd > 4096) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bnfold_combine_kernel, dim3((Cout + kCombRows - 1) / kCombRows), dim3(256),
+                     kCombRows * Wd * sizeof(float), st, P, W, coef, Cout, Wd, out, accumulate);
+  return hipGetLastError();
+}
+
+}  // namespace psd

@@ -180,6 +180,7 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
     }
   }
   const rsrc_t xr = make_rsrc(a.x, a.xbytes);
+  const rsrc_t x2r = make_rsrc(a.x2 ? a.x2 : a.x, a.x2 ? a.x2bytes : 0u);
   const rsrc_t wrs = make_rsrc(a.w, a.wbytes);
   const int cmask = (1 << a.logC) - 1;
   const int nslot = a.nslot;  // ring depth of this launch: min(NSLOT, K-tiles)
@@ -187,6 +188,19 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
   auto stage = [&](int t) {
     uint8_t* slot = smem + (t % nslot) * G::SLOT;
     const int k0 = t * kBK;
+    if (k0 >= a.K1) {  // K-concatenated second operand (1x1: the row is the output pixel itself)
+      const int c0 = k0 - a.K1;
+#pragma unroll
+      for (int i = 0; i < G::APW; ++i) {
+        const int piece = i * G::NW + wid;
+        const int row = piece * 8 + (lane >> 3);
+        const int kc = (lane & 7) ^ ((row >> 1) & 7);
+        const bool ok = hw[i] != (int)0x80000000u;
+        const uint32_t off = ok ? ((((uint32_t)p0[i]) << a.logC2) + (uint32_t)(c0 + kc * 8)) * 2u : kOOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(x2r, (__attribute__((address_space(3))) void*)(slot + piece * 1024),
+                                                 16, off, 0, 0, 0);
+      }
+    } else {
     const int rs = k0 >> a.logC, ci0 = k0 & cmask;
     const int r = rs / a.S, s = rs - r * a.S;
 #pragma unroll
@@ -199,6 +213,7 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
       const uint32_t off = ok ? ((((uint32_t)(p0[i] + r * a.W + s)) << a.logC) + (uint32_t)(ci0 + kc * 8)) * 2u : kOOB;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(slot + piece * 1024), 16,
                                                off, 0, 0, 0);
+    }
     }
     // (the weight offsets are recomputed per K-tile: a per-lane offset array captured by this lambda
     // made hipcc's host pass silently drop the kernel's instantiation -- an undefined stub symbol)
@@ -256,6 +271,14 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
 
   // ---- epilogue (per wave, no barrier: the staging slot is this wave's own): C layout of a
   // 16x16 block col = lane & 15, row = 4 * (lane >> 4) + r
+  if (a.bias) {  // per-output-channel bias (the BN-backward fold's constant term)
+#pragma unroll
+    for (int j = 0; j < G::JN; ++j) {
+      const float bv = a.bias[n0 + wc * WNT + j * 16 + cl];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i][j] += f32x4{bv, bv, bv, bv};
+    }
+  }
   if constexpr (STATS) {
 #pragma unroll
     for (int j = 0; j < G::JN; ++j) {
@@ -440,11 +463,17 @@ int convn_part_rows(int M, int N, int variant) {
   return (bm / 64) * ((M + bm - 1) / bm);
 }
 
-hipError_t launch_convn(const ConvnArgs& a, hipStream_t st) {
-  if (a.M <= 0) return hipSuccess;
+hipError_t launch_convn(const ConvnArgs& a_in, hipStream_t st) {
+  if (a_in.M <= 0) return hipSuccess;
+  ConvnArgs a = a_in;
+  if (!a.x2) a.K1 = a.K;  // every K-tile from x
   const int bn = convn_tile_n(a.N);
   const int C = 1 << a.logC;
-  const bool ok = bn > 0 && a.logC >= 6 && a.K % kBK == 0 && a.K == a.R * a.S * C && a.ldc % 8 == 0 &&
+  const bool two = a.x2 != nullptr;
+  const int K1 = two ? a.K1 : a.K;
+  const bool ok = bn > 0 && a.logC >= 6 && a.K % kBK == 0 && K1 == a.R * a.S * C && a.ldc % 8 == 0 &&
+                  (!two || (a.R == 1 && a.S == 1 && a.stride == 1 && a.pad == 0 && a.logC2 >= 6 && K1 % kBK == 0 &&
+                            a.K == K1 + (1 << a.logC2) && a.x2bytes > 0 && a.x2bytes <= 0xFFFFFF00u)) &&
                   a.ldc >= a.N && a.H < 32768 && a.W < 32768 && a.xbytes > 0 && a.xbytes <= 0xFFFFFF00u &&
                   a.wbytes > 0 && a.variant < convn_variant_count(bn) &&
                   (a.bwd == 0 ? (!a.part || a.shift)

@@ -1,0 +1,429 @@
+// Narrow implicit-GEMM convolution weight gradient for gfx950 (NHWC bf16), split over the output
+// pixels.
+//
+//   dW[co][kk] = sum_m dY[m][co] * A(m, kk)      m = output pixel (Nb*Ho*Wo), kk = (r, s, ci),
+//                                                A(m, kk) = x[pixel(m) * stride - pad + (r, s)][ci]
+//
+// Why its own kernel: the weight gradients of ResNet's 64/128-channel layers are pure HBM streams
+// (layer1's 1x1 256->64: 2 GB of dY + x read for 0.1 TFLOP) that MIOpen's assembly kernels ran at
+// about the copy roofline while the 256x256-tile split-K GEMM (gemm.hip) wasted 3/4 of its tile on
+// a 64-row output (2-4x slower: profiles/resnet50_b1024_r3_bnbwd_twin_autotune.txt). Here the tile
+// is the narrow output itself, so every dY and x element is read from HBM once:
+//   * workgroup = 8 waves, output tile TCO (64 / 128 / 256 output channels) x TKK (64..256 columns
+//     = 1..4 K-blocks of 64 channels of one (r, s)); a wave owns I x J 16x16 blocks of it on
+//     v_mfma_f32_16x16x32_bf16 (the MFMA k = 32 output pixels);
+//   * a stage = 64 output pixels: the dY rows [64 px][TCO] and, per K-block, the gathered input
+//     rows [64 px][64 ch] are DMA'd straight into LDS (buffer_load ... lds, 16 B per lane; a pixel
+//     outside the image or past M falls outside the buffer range and loads zeros = the padding) as
+//     [64 px][64 ch] sub-images whose 16-B chunks are XOR-swizzled by row bits 1 and 3 on the SOURCE
+//     address (the DMA image is lane-linear);
+//   * both operands are pixel-major, so every MFMA fragment is read with the CDNA4 transpose read
+//     ds_read_b64_tr_b16 (8 consecutive pixels of one channel per lane); with the swizzle the 8 rows
+//     of a 32-lane half cover all 64 banks (conflict-free);
+//   * NSLOT-deep stage ring, one raw s_barrier per stage and a counted vmcnt (the later stages stay
+//     in flight), like convn.hip; every lane of a wave moves the same pixel row in all its pieces,
+//     so the pixel -> (n, ho, wo) division runs once per lane per stage;
+//   * grid = pixel splits x output tiles (XCD-aware order: the tiles of one split -- which share
+//     their dY stage -- land on one XCD's L2), sized to one round of workgroups; each split writes
+//     its fp32 partial tile to a slab, the deterministic slab reduce (gemm.hip) writes bf16 dW.
+#include <algorithm>
+
+#include "common.h"
+#include "launchers_convw.h"
+#include "launchers_gemm.h"
+
+namespace psd {
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+constexpr int kBP = 64;                  // output pixels per stage (two 32-deep MFMA k-steps)
+constexpr int kSub = 64 * 128;           // one [64 px][64 ch] bf16 sub-image
+constexpr uint32_t kOOB = 0xFFFFFFF0u;   // past every descriptor's range: the load returns zeros
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+
+// 16-B chunk c of sub-image row r is stored at chunk c ^ swz(r). A ds_read_b64_tr_b16 fragment read
+// touches, per 32-lane half, rows {q, q + 8} (q = 0..3, plus a multiple of 16) with one 32-B segment
+// each; (r & 1, swz) is distinct on those 8 rows, so they cover the 8 segments of a 256-B bank row.
+__device__ __forceinline__ int swz(int r) { return (((r >> 1) & 1) | (((r >> 3) & 1) << 1)) << 1; }
+
+// v_mfma_f32_16x16x32_bf16 operand from a [64 px][64 ch] sub-image: lane -> channel cb*16 + (lane & 15),
+// pixels ks*32 + 8*(lane >> 4) + 0..7 (the MFMA k). Transpose read: lane 4q+p of a 16-lane group
+// addresses row q, channels 4p..4p+3; lane i receives channel i of the 4 rows.
+__device__ __forceinline__ bf16x8 trfrag(const uint8_t* sub, int ks, int cb, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int r0 = ks * 32 + 8 * g + q, r1 = r0 + 4;
+  const int c = 2 * cb + (p >> 1), b = (p & 1) * 8;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(sub + r0 * 128 + ((c ^ swz(r0)) << 4) + b));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(sub + r1 * 128 + ((c ^ swz(r1)) << 4) + b));
+  const s16x4 both[2] = {lo, hi};
+  return __builtin_bit_cast(bf16x8, both);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  // bijective: blocks with equal bid % 8 (one XCD under round-robin dispatch) get a contiguous range
+  const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+}
+
+// 4x4 transpose inside a lane quad: in v[r] = C[row r][col L]; out w[c] = C[row L][col c]
+template <int CTRL>
+__device__ __forceinline__ float dpp_q(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ void quad_t4(const f32x4 v, int L, float (&w)[4]) {
+  const bool o1 = L & 1, o2 = (L >> 1) & 1;
+  const float r0 = dpp_q<0xB1>(o1 ? v[0] : v[1]);
+  const float r1 = dpp_q<0xB1>(o1 ? v[2] : v[3]);
+  const float a0 = o1 ? r0 : v[0], a1 = o1 ? v[1] : r0;
+  const float b0 = o1 ? r1 : v[2], b1 = o1 ? v[3] : r1;
+  const float q0 = dpp_q<0x4E>(o2 ? a0 : b0);
+  const float q1 = dpp_q<0x4E>(o2 ? a1 : b1);
+  w[0] = o2 ? q0 : a0;
+  w[1] = o2 ? q1 : a1;
+  w[2] = o2 ? b0 : q0;
+  w[3] = o2 ? b1 : q1;
+}
+
+template <int TCO, int TKK, int WR, int NSLOT, int NAR = -1>
+struct WGeo {
+  static constexpr int NW = 8;                // waves (one DMA piece = 8 pixel rows each)
+  static constexpr int NT = 64 * NW;
+  static constexpr int WC = NW / WR;          // wave columns
+  static constexpr int I = TCO / 16 / WR;     // 16-row blocks per wave
+  static constexpr int J = TKK / 16 / WC;     // 16-column blocks per wave
+  // dY sub-images per stage: every row of the tile, or (NAR >= 0: a single-tile fold launch) only
+  // the first NAR * 64 rows -- the rest are x rows (read from the B sub-images) and ones
+  static constexpr int NA = NAR >= 0 ? NAR : TCO / 64;
+  static constexpr int NB = TKK / 64;         // x sub-images (K-blocks) per stage
+  static constexpr int DPS = NA + NB;         // DMA per wave per stage: one 1 KiB piece of each sub-image
+  static constexpr int SLOT = DPS * kSub;
+  static constexpr int LDS = NSLOT * SLOT;
+  static_assert(I >= 1 && J >= 1 && I * 16 * WR == TCO && J * 16 * WC == TKK, "wave tiling");
+  static_assert(I * J <= 16, "accumulators");
+  static_assert(DPS * (NSLOT - 2) < 64 && NSLOT <= 5, "vmcnt is 6 bits");
+  static_assert(LDS <= 160 * 1024, "LDS");
+};
+
+}  // namespace
+
+template <int TCO, int TKK, int WR, int NSLOT, int NAR = -1>
+__global__ __launch_bounds__(512) void convw_kernel(ConvwArgs a) {
+  using G = WGeo<TCO, TKK, WR, NSLOT, NAR>;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int tiles_co = a.Arows / TCO;
+  const int ntile = tiles_co * (a.KK / TKK);
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid / ntile, tile = bid - split * ntile;
+  const int co0 = (tile % tiles_co) * TCO, kk0 = (tile / tiles_co) * TKK;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid / G::WC, wc = wid % G::WC;
+  const int prow = wid * 8 + (lane >> 3);       // this lane's pixel row in every piece it moves
+  const int kc = (lane & 7) ^ swz(prow);        // the global 16-B chunk it moves into LDS chunk lane & 7
+  const int howo = a.Ho * a.Wo;
+  const int cmask = (1 << a.logC) - 1;
+  const rsrc_t dyr = make_rsrc(a.dy, a.dybytes);
+  const rsrc_t xr = make_rsrc(a.x, a.xbytes);
+
+  const int total = (a.M + kBP - 1) / kBP;
+  const int st0 = split * a.stages_per_split;
+  const int nst = max(0, min(a.stages_per_split, total - st0));
+
+  auto stage = [&](int t) {
+    uint8_t* slot = smem + (t % NSLOT) * G::SLOT + wid * 1024;
+    const int m = (st0 + t) * kBP + prow;
+    const bool mv = m < a.M;
+#pragma unroll
+    for (int j = 0; j < G::NA; ++j) {
+      // fold rows past dY are read from the x sub-images / constants: their DMA loads nothing (out of
+      // range) but keeps every wave's per-stage count equal to DPS (the counted vmcnt)
+      const bool dyrow = co0 + j * 64 < a.Cout;
+      const uint32_t off = (mv && dyrow) ? ((uint32_t)m * (uint32_t)a.Cout + (uint32_t)(co0 + j * 64 + kc * 8)) * 2u : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(dyr, (__attribute__((address_space(3))) void*)(slot + j * kSub), 16,
+                                               off, 0, 0, 0);
+    }
+    const int n = m / howo, rem = m - n * howo;
+    const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
+    const int hb = ho * a.stride - a.pad, wb = wo * a.stride - a.pad;
+#pragma unroll
+    for (int b = 0; b < G::NB; ++b) {
+      const int k0 = kk0 + b * 64;
+      const int rs = k0 >> a.logC, ci0 = k0 & cmask;
+      const int r = rs / a.S, s = rs - r * a.S;
+      const int hh = hb + r, ww = wb + s;
+      const bool ok = mv && (unsigned)hh < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
+      const uint32_t off =
+          ok ? ((((uint32_t)((n * a.H + hh) * a.W + ww)) << a.logC) + (uint32_t)(ci0 + kc * 8)) * 2u : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(slot + (G::NA + b) * kSub),
+                                               16, off, 0, 0, 0);
+    }
+  };
+
+  f32x4 acc[G::I][G::J];
+#pragma unroll
+  for (int i = 0; i < G::I; ++i)
+#pragma unroll
+    for (int j = 0; j < G::J; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  constexpr int D = NSLOT - 1;  // stages issued ahead
+  for (int p = 0; p < D && p < nst; ++p) stage(p);
+  for (int t = 0; t < nst; ++t) {
+    // stage t landed (this wave's DMA): leave the (up to D-1) later stages in flight
+    const int ahead = min(nst - 1 - t, D - 1);
+    if constexpr (D >= 4) {
+      if (ahead >= 3) wait_vm<3 * G::DPS>();
+      else if (ahead == 2) wait_vm<2 * G::DPS>();
+      else if (ahead == 1) wait_vm<G::DPS>();
+      else wait_vm<0>();
+    } else if constexpr (D == 3) {
+      if (ahead >= 2) wait_vm<2 * G::DPS>();
+      else if (ahead == 1) wait_vm<G::DPS>();
+      else wait_vm<0>();
+    } else if constexpr (D == 2) {
+      if (ahead >= 1) wait_vm<G::DPS>();
+      else wait_vm<0>();
+    } else {
+      wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();  // every wave: stage t published, stage t-1 no longer read
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + D < nst) stage(t + D);
+    const uint8_t* sl = smem + (t % NSLOT) * G::SLOT;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[G::I], bf[G::J];
+#pragma unroll
+      for (int j = 0; j < G::J; ++j) {
+        const int cbk = wc * G::J + j;  // 16-column block of the tile
+        bf[j] = trfrag(sl + (G::NA + (cbk >> 2)) * kSub, ks, cbk & 3, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < G::I; ++i) {
+        const int rb = wr * G::I + i;  // 16-row block of the tile
+        const int gr = co0 + rb * 16;  // its first output row (wave-uniform source choice)
+        if (gr < a.Cout) {
+          af[i] = trfrag(sl + (rb >> 2) * kSub, ks, rb & 3, lane);
+        } else if (gr < a.Cout + a.KK) {  // fold: x rows = the B sub-images of this (whole-KK) tile
+          const int xb = (gr - a.Cout) >> 4;
+          af[i] = trfrag(sl + (G::NA + (xb >> 2)) * kSub, ks, xb & 3, lane);
+        } else {  // fold: ones rows -> column sums of x
+          af[i] = bf16x8{(__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f,
+                         (__bf16)1.f};
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < G::I; ++i)
+#pragma unroll
+        for (int j = 0; j < G::J; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+
+  // epilogue: this split's fp32 partial tile; a lane quad transposes each 16x16 block so a lane
+  // stores 4 consecutive columns of one row (16 B)
+  float* sl = a.slab + (int64_t)split * a.Arows * a.KK;
+  const int L = lane & 3, rq = (lane >> 4) * 4, cq = (lane & 15) & ~3;
+#pragma unroll
+  for (int i = 0; i < G::I; ++i)
+#pragma unroll
+    for (int j = 0; j < G::J; ++j) {
+      float w[4];
+      quad_t4(acc[i][j], L, w);
+      const int row = co0 + (wr * G::I + i) * 16 + rq + L;
+      const int col = kk0 + (wc * G::J + j) * 16 + cq;
+      *reinterpret_cast<f32x4*>(sl + (int64_t)row * a.KK + col) = f32x4{w[0], w[1], w[2], w[3]};
+    }
+}
+
+// ------------------------------------------------------------------ host side
+namespace {
+
+struct Cfg {
+  int tco, tkk, lds;
+};
+
+// tile variants per output-tile height (TCO): (TKK, WR, NSLOT) instantiated below
+constexpr int kTkk64[] = {256, 192, 128, 64};
+constexpr int kTkk128[] = {256, 192, 128, 64};
+constexpr int kTkk256[] = {128, 64};
+
+int tile_co(int Cout, bool fold = false) {
+  if (Cout % 256 == 0) return 256;
+  if (Cout == 128 || (fold && Cout % 128 == 0)) return 128;
+  if (Cout == 64 || (fold && Cout % 64 == 0)) return 64;
+  return 0;
+}
+
+// the v-th TKK that divides KK for this TCO (0 when there is none)
+int pick_tkk(int tco, int KK, int v) {
+  const int* list = tco == 64 ? kTkk64 : tco == 128 ? kTkk128 : kTkk256;
+  const int n = tco == 256 ? 2 : 4;
+  int k = 0;
+  for (int i = 0; i < n; ++i)
+    if (KK % list[i] == 0) {
+      if (k == v) return list[i];
+      ++k;
+    }
+  return 0;
+}
+
+// ring depth: as many stages as fit the 160 KiB LDS (<= 5; 4 for the 2-workgroup 64x64 tile) -- the
+// kernel streams HBM, so its bandwidth is set by the stages in flight (3 -> 4 slots: +5-10 %)
+constexpr int nslot_of(int tco, int tkk) {
+  return (tco + tkk) <= 128 ? 4 : std::min(5, (160 * 1024) / ((tco + tkk) / 64 * kSub));
+}
+int lds_of(int tco, int tkk) {
+  if (tco == 384) return 4 * (256 + 64) / 64 * kSub;  // the single-tile fold: 4 dY + 1 x sub-images, 4 slots
+  return nslot_of(tco, tkk) * (tco + tkk) / 64 * kSub;
+}
+
+int cu_count() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+template <int TCO, int TKK, int WR, int NSLOT, int NAR = -1>
+hipError_t launch_t(const ConvwArgs& a, int grid, hipStream_t st) {
+  using G = WGeo<TCO, TKK, WR, NSLOT, NAR>;
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)convw_kernel<TCO, TKK, WR, NSLOT, NAR>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL((convw_kernel<TCO, TKK, WR, NSLOT, NAR>), dim3(grid), dim3(G::NT), G::LDS, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+int convw_variants(int Cout, int KK) {
+  const int tco = tile_co(Cout);  // plain launches (fold launches have one fixed tile)
+  if (!tco || KK <= 0 || KK % 64 != 0) return 0;
+  int n = 0;
+  while (pick_tkk(tco, KK, n)) ++n;
+  return n;
+}
+
+// (tco, tkk) of a launch, 0 when unsupported; fold launches take the whole KK in one tile
+static void tile_of(const ConvwArgs& a, int& tco, int& tkk) {
+  const int rows = a.fold ? a.Arows : a.Cout;
+  tco = tile_co(rows, a.fold != 0);
+  tkk = 0;
+  if (!tco) return;
+  if (a.fold) {
+    if (a.Cout == 256 && a.KK == 64 && a.Arows == 384) {  // one tile holds every row: dY read once
+      tco = 384;
+      tkk = 64;
+      return;
+    }
+    for (int v = 0; pick_tkk(tco, a.KK, v); ++v)
+      if (pick_tkk(tco, a.KK, v) == a.KK) tkk = a.KK;
+    if (!tkk && tco > 64 && a.KK <= 256) {  // a narrower row tile admits a wider TKK
+      tco = 64;
+      for (int v = 0; pick_tkk(tco, a.KK, v); ++v)
+        if (pick_tkk(tco, a.KK, v) == a.KK) tkk = a.KK;
+    }
+    return;
+  }
+  tkk = pick_tkk(tco, a.KK, a.variant < 0 ? 0 : a.variant);
+}
+
+bool convw_fold_ok(int Cout, int KK, int Arows) {
+  ConvwArgs a{};
+  a.Cout = Cout;
+  a.KK = KK;
+  a.Arows = Arows;
+  a.fold = 1;
+  int tco, tkk;
+  tile_of(a, tco, tkk);
+  return tkk == KK && tco > 0 && Arows % tco == 0 && Cout % 64 == 0 && KK >= 64 && (KK & (KK - 1)) == 0;
+}
+
+ConvwPlan convw_plan(const ConvwArgs& a) {
+  ConvwPlan p{0, 0};
+  int tco, tkk;
+  tile_of(a, tco, tkk);
+  if (!tkk || a.M <= 0) return p;
+  const int arows = a.fold ? a.Arows : a.Cout;
+  const int ntile = (arows / tco) * (a.KK / tkk);
+  const int occ = std::max(1, std::min(2, (160 * 1024) / lds_of(tco, tkk)));
+  const int total = (a.M + kBP - 1) / kBP;
+  // one round of workgroups over the chip, >= 4 stages per split
+  int splits = std::max(1, (cu_count() * occ) / ntile);
+  splits = std::min(splits, std::max(1, total / 4));
+  const int sps = (total + splits - 1) / splits;
+  p.splits = (total + sps - 1) / sps;
+  const int64_t mn = (int64_t)arows * a.KK;
+  p.slab_floats = (int64_t)p.splits * mn + splitk_tree_floats(p.splits, mn);  // slabs + the reduce tree
+  return p;
+}
+
+hipError_t launch_convw(const ConvwArgs& a_in, hipStream_t st) {
+  if (a_in.M <= 0) return hipSuccess;
+  ConvwArgs a0 = a_in;
+  if (!a0.fold) a0.Arows = a0.Cout;
+  int tco, tkk;
+  tile_of(a0, tco, tkk);
+  const int C = 1 << a0.logC;
+  const bool ok = tkk > 0 && a0.logC >= 6 &&
+                  (!a0.fold || (a0.S == 1 && a0.KK == C && a0.stride == 1 && a0.pad == 0 && a0.Cout % 64 == 0 &&
+                                a0.Arows > a0.Cout + a0.KK && a0.Arows % tco == 0 && tkk == a0.KK)) &&
+                  a0.Cout % 64 == 0 && a0.KK % C == 0 && a0.KK / C == (a0.KK / C / a0.S) * a0.S && a0.S > 0 &&
+                  a0.H < 32768 && a0.W < 32768 && a0.Ho > 0 && a0.Wo > 0 && a0.dybytes > 0 &&
+                  a0.dybytes <= 0xFFFFFF00u && a0.xbytes > 0 && a0.xbytes <= 0xFFFFFF00u && a0.slab && a0.out &&
+                  (int64_t)a0.M * a0.Cout * 2 <= (int64_t)a0.dybytes;
+  if (!ok) return hipErrorNotSupported;
+  ConvwArgs a = a0;
+  const ConvwPlan p = convw_plan(a);
+  const int total = (a.M + kBP - 1) / kBP;
+  a.splits = p.splits;
+  a.stages_per_split = (total + p.splits - 1) / p.splits;
+  const int grid = p.splits * (a.Arows / tco) * (a.KK / tkk);
+  hipError_t e = hipErrorNotSupported;
+#define PSD_CONVW(TCO_, TKK_, WR_) launch_t<TCO_, TKK_, WR_, nslot_of(TCO_, TKK_)>(a, grid, st)
+  if (tco == 384) {
+    e = launch_t<384, 64, 8, 4, 4>(a, grid, st);
+  } else if (tco == 64) {
+    if (tkk == 256) e = PSD_CONVW(64, 256, 2);
+    else if (tkk == 192) e = PSD_CONVW(64, 192, 2);
+    else if (tkk == 128) e = PSD_CONVW(64, 128, 2);
+    else e = PSD_CONVW(64, 64, 4);
+  } else if (tco == 128) {
+    if (tkk == 256) e = PSD_CONVW(128, 256, 2);
+    else if (tkk == 192) e = PSD_CONVW(128, 192, 2);
+    else if (tkk == 128) e = PSD_CONVW(128, 128, 2);
+    else e = PSD_CONVW(128, 64, 4);
+  } else {
+    if (tkk == 128) e = PSD_CONVW(256, 128, 4);
+    else e = PSD_CONVW(256, 64, 4);
+  }
+#undef PSD_CONVW
+  if (e != hipSuccess) return e;
+  const int64_t mn = (int64_t)a.Arows * a.KK;
+  return launch_splitk_reduce(a.slab, a.splits, mn, a.out, a.fold ? 0 : 1, a.accumulate, 1.f, st,
+                              a.slab + (int64_t)a.splits * mn);
+}
+
+}  // namespace psd

@@ -1676,6 +1676,62 @@ hipError_t launch_gemm_splitk(const GemmArgs& g0, float* slab, int splits, void*
   return hipGetLastError();
 }
 
+// One level of a split-sum tree: out[c] = sum of in[s] for s in [G c, min(G c + G, splits)), mn
+// (a multiple of 8) elements per slab, 8 per lane, the G loads of a lane independent. A serial loop
+// over hundreds of splits in one lane (splitk_reduce_kernel) runs at the latency of dependent
+// round trips when mn is small (a 64x64 weight gradient over 512 pixel splits: ~150 us); levels of
+// G = 8 keep every lane's loads in flight together.
+template <int G>
+__global__ __launch_bounds__(256) void split_tree_kernel(const float* __restrict__ in, int splits, int64_t mn,
+                                                         float* __restrict__ out) {
+  const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= (mn >> 3)) return;
+  const int c = blockIdx.y, s0 = c * G;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < G; ++k) {
+    if (s0 + k < splits) {
+      float t[8];
+      load8_f32(in + (int64_t)(s0 + k) * mn + v * 8, t);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += t[e];
+    }
+  }
+  store8_f32(out + (int64_t)c * mn + v * 8, acc);
+}
+
+int64_t splitk_tree_floats(int splits, int64_t mn) { return ((int64_t)(splits + 7) / 8 + 1) * mn; }
+
+// out (bf16 or fp32, [mn]) = (accumulate ? out : 0) + scale * sum over `splits` fp32 slabs of mn
+// elements (the deterministic reduce of every split-K / split-pixel launch, e.g. convw.hip). With a
+// tree workspace (splitk_tree_floats) and more than 8 splits, levels of 8 run first, ping-ponging
+// between the workspace and the (consumed) slab.
+hipError_t launch_splitk_reduce(float* slab, int splits, int64_t mn, void* out, int out_bf16, int accumulate,
+                                float scale, hipStream_t st, float* tree) {
+  if (mn <= 0) return hipSuccess;
+  if (tree && mn % 8 == 0) {
+    float* src = slab;
+    float* dst = tree;
+    while (splits > 8) {
+      const int chunks = (splits + 7) / 8;
+      const dim3 grid((unsigned)(((mn >> 3) + 255) / 256), (unsigned)chunks);
+      hipLaunchKernelGGL(split_tree_kernel<8>, grid, dim3(256), 0, st, src, splits, mn, dst);
+      splits = chunks;
+      float* t = src;
+      src = dst;
+      dst = t;
+    }
+    slab = src;
+  }
+  const int grid = stream_grid((mn >> 3) > 0 ? (mn >> 3) : 1, 256);
+  if (out_bf16)
+    hipLaunchKernelGGL(splitk_reduce_kernel<true>, dim3(grid), dim3(256), 0, st, slab, splits, mn, out, accumulate, scale);
+  else
+    hipLaunchKernelGGL(splitk_reduce_kernel<false>, dim3(grid), dim3(256), 0, st, slab, splits, mn, out, accumulate,
+                       scale);
+  return hipGetLastError();
+}
+
 hipError_t launch_colsum(const uint16_t* x, int64_t M, int N, float* part, void* out, int out_bf16,
                          int accumulate, hipStream_t st, const uint16_t* pre, uint16_t* xo) {
   if (N % 8 != 0) return hipErrorInvalidValue;

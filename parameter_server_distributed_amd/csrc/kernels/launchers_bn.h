@@ -77,6 +77,9 @@ struct BnBwdArgs {
   // the reduction pass alone (partials into part, dr when given): what a bwd-data convolution that
   // does not fuse it leaves to the BN (autotune timing twin, ops/conv.py _with_bn_bwd_reduce)
   int32_t reduce_only;
+  // reduction + finalize only (coef, dgamma, dbeta; dr when given): the consumer convolution folds
+  // the elementwise pass into its backward GEMMs (ops/bn.py, kernels/bnfold.hip)
+  int32_t coef_only;
 };
 
 // true when the fused stem BN+ReLU+max-pool kernels support this shape
@@ -94,5 +97,13 @@ hipError_t launch_bn_bwd(const BnBwdArgs& a, hipStream_t stream);
 hipError_t launch_bn_bwd_pre(const uint16_t* g, const uint16_t* x, const uint16_t* gamma, const float* mean,
                              const float* invstd, const float* part, int rows, float* fold_ws, uint16_t* dgamma,
                              uint16_t* dbeta, float* coef, uint16_t* dx, int64_t M, int C, hipStream_t stream);
+
+// BN-backward fold (bnfold.hip); bn_elemt_coef (bn.hip): dx = A g + B x + C from finalized coefficients
+hipError_t launch_bn_elemt_coef(const uint16_t* g, const uint16_t* x, const float* coef, uint16_t* dx, int64_t M, int C,
+                                hipStream_t stream);
+hipError_t launch_bnfold_prep(const uint16_t* W, const float* coef, int Cout, int Wd, uint16_t* w2, int ldw,
+                              uint16_t* bw, float* bvec, hipStream_t stream);
+hipError_t launch_bnfold_combine(const float* P, const uint16_t* W, const float* coef, int Cout, int Wd,
+                                 uint16_t* out, int accumulate, hipStream_t stream);
 
 }  // namespace psd

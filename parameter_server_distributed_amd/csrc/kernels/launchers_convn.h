@@ -26,6 +26,13 @@ struct ConvnArgs {
   const float* bss;       // bwd 1: [2N] its forward scale / shift (ReLU mask)
   const uint16_t* bdr;    // bwd 2: [M][N] the residual-branch gradient to add
   const uint8_t* bmbits;  // bwd 2: [M*N/8] the forward ReLU bit-mask
+  // K-concatenated second operand (1x1 only): A(m, k) = x2[m][k - K1] for k >= K1, so
+  // y = [x | x2] . w^T with w [N][K1 + C2] (the BN-backward fold of ops/bn.py: dgrad of a 1x1 conv
+  // whose BN input gradient is never materialised)
+  const void* x2;         // bf16 [M][C2], C2 = 1 << logC2 >= 64
+  uint32_t x2bytes;
+  int K1, logC2;
+  const float* bias;      // optional fp32 [N] added to the output in the epilogue (before bwd / stats)
 };
 
 // output-channel tile of the kernel for N output channels (64, 128, 256 for N % 256 == 0), 0: unsupported

@@ -44,6 +44,12 @@ hipError_t launch_conv_fwd_fp8(const GemmArgs& g, hipStream_t stream);
 // B = x NHWC, K = pixels % 64 == 0), split-K into slab [splits][Cout][R*S*C] fp32 + reduce;
 // hipErrorNotSupported outside the kernel's contract
 hipError_t launch_conv_wgrad(const GemmArgs& g, float* slab, int splits, void* out, hipStream_t stream);
+// out = (accumulate ? out : 0) + scale * sum_s slab[s] over mn elements (bf16 or fp32 out). With
+// `tree` (splitk_tree_floats(splits, mn) fp32 of workspace) many splits are summed in levels of 8
+// first; the slab is then overwritten.
+int64_t splitk_tree_floats(int splits, int64_t mn);
+hipError_t launch_splitk_reduce(float* slab, int splits, int64_t mn, void* out, int out_bf16, int accumulate,
+                                float scale, hipStream_t stream, float* tree = nullptr);
 // split-K GEMM into fp32 slabs [splits][M][N], then out = (acc ? out : 0) + scale * sum(slabs)
 hipError_t launch_gemm_splitk(const GemmArgs& g, float* slab, int splits, void* out, int out_bf16, int accumulate,
                               float scale, hipStream_t stream);

@@ -37,7 +37,15 @@ std::vector<at::Tensor> bn_bwd_dual(const at::Tensor& dy, const at::Tensor& x, c
                                     c10::optional<at::Tensor> dy2, const at::Tensor& xd, const at::Tensor& gamma_d,
                                     const at::Tensor& mean_d, const at::Tensor& invstd_d,
                                     c10::optional<at::Tensor> dgamma_out, c10::optional<at::Tensor> dbeta_out,
-                                    c10::optional<at::Tensor> dgamma_d_out, c10::optional<at::Tensor> dbeta_d_out);
+                                    c10::optional<at::Tensor> dgamma_d_out, c10::optional<at::Tensor> dbeta_d_out, bool fold);
+at::Tensor bn_elemt_coef(const at::Tensor& g, const at::Tensor& x, const at::Tensor& coef);
+std::vector<at::Tensor> bnfold_dgrad_weights(const at::Tensor& w, const at::Tensor& coef);
+void bnfold_combine(const at::Tensor& P, const at::Tensor& w, const at::Tensor& coef, at::Tensor out, bool accumulate);
+std::vector<at::Tensor> bn_bwd_coef(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& gamma,
+                                    const at::Tensor& save_mean, const at::Tensor& save_invstd,
+                                    c10::optional<at::Tensor> mbits, c10::optional<at::Tensor> dy2,
+                                    c10::optional<at::Tensor> part, int64_t rows, c10::optional<at::Tensor> dgamma_out,
+                                    c10::optional<at::Tensor> dbeta_out);
 std::vector<at::Tensor> bn_bwd(const at::Tensor& dy, const at::Tensor& x, c10::optional<at::Tensor> y,
                                c10::optional<at::Tensor> gamma, const at::Tensor& save_mean,
                                const at::Tensor& save_invstd, bool relu, bool need_dr,
@@ -56,12 +64,14 @@ void gelu_bwd_colsum_(const at::Tensor& dy, const at::Tensor& pre, at::Tensor dx
 // convn_stats_rows(M) x 2 x Cout). Returns 0 (nothing launched) outside the kernel's contract, else
 // the partial rows written (1 without statistics).
 int64_t convn_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride,
-               int64_t pad, c10::optional<at::Tensor> part, c10::optional<at::Tensor> shift, int64_t variant);
+               int64_t pad, c10::optional<at::Tensor> part, c10::optional<at::Tensor> shift, int64_t variant,
+               c10::optional<at::Tensor> x2, c10::optional<at::Tensor> bias);
 int64_t convn_stats_rows_(int64_t M);
 int64_t convn_bwd_(const at::Tensor& dy, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride,
                    int64_t pad, at::Tensor part, int64_t variant, int64_t mode, const at::Tensor& bx,
                    const at::Tensor& bmean, c10::optional<at::Tensor> bss, c10::optional<at::Tensor> bdr,
-                   c10::optional<at::Tensor> bmbits);
+                   c10::optional<at::Tensor> bmbits, c10::optional<at::Tensor> x2,
+                   c10::optional<at::Tensor> bias);
 std::vector<at::Tensor> bn_bwd_pre(const at::Tensor& g, const at::Tensor& x, c10::optional<at::Tensor> gamma,
                                    const at::Tensor& save_mean, const at::Tensor& save_invstd, const at::Tensor& part,
                                    int64_t rows, c10::optional<at::Tensor> dgamma_out,
@@ -71,6 +81,10 @@ bool conv_fwd_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_
                int64_t pad);
 bool conv_wgrad_(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64_t R, int64_t S, int64_t stride,
                  int64_t pad, int64_t splits);
+bool convw_(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64_t R, int64_t S, int64_t stride,
+            int64_t pad, int64_t variant, bool accumulate, bool fold);
+int64_t convw_fold_rows(int64_t Cout, int64_t Cin);
+int64_t convw_variants_(int64_t Cout, int64_t KK);
 bool conv_fwd_fp8_(const at::Tensor& x, const at::Tensor& w2, const at::Tensor& x_scale, const at::Tensor& w_scale,
                    at::Tensor out, int64_t R, int64_t S, int64_t stride, int64_t pad);
 void gemm_fp8_(const at::Tensor& A, const at::Tensor& B, const at::Tensor& a_scale, const at::Tensor& b_scale,

@@ -76,6 +76,9 @@ class Bottleneck(nn.Module):
         object.__setattr__(self.conv2, "_psd_bn_in", self.bn1)
         object.__setattr__(self.conv3, "_psd_bn_in", self.bn2)
         object.__setattr__(self.conv1, "_psd_bn_in", None)
+        # bn3's input gradient can be folded into conv3's backward GEMMs (ops/conv.py _fold_backward)
+        if isinstance(self.conv3, Conv1x1) and not fp8:
+            object.__setattr__(self.bn3, "_psd_fold_conv", self.conv3)
         if fp8:  # bn1 / bn2 quantise their outputs for the fp8 conv2 / conv3 in their apply pass
             # (plain attributes: object.__setattr__ keeps the consumer from becoming a submodule)
             object.__setattr__(self.bn1, "_psd_q8_consumer", self.conv2)
@@ -87,7 +90,8 @@ class Bottleneck(nn.Module):
         it inside the BN kernels (no autograd add over the activation)."""
         xm = xd = x
         if (self.downsample is not None and prev_bn is not None and self.fuse_residual_grad
-                and torch.is_grad_enabled() and x.requires_grad and prev_bn.training and x.is_cuda):
+                and torch.is_grad_enabled() and x.requires_grad and prev_bn.training and x.is_cuda
+                and x.dtype == torch.bfloat16):  # (the fused BN kernels that consume the hand-over)
             xm, xd = _Fork.apply(x, prev_bn)  # downsample-branch gradient -> prev_bn's kernels
         if self.downsample is not None and self.fuse_residual_grad and len(self.downsample) == 2:
             # relu(bn3(conv3) + bn_ds(conv_ds)): the downsample BN is applied inside bn3's apply pass

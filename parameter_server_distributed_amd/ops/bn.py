@@ -22,6 +22,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import native
+from . import autotune as _at
 
 
 def _kernel_ok(x: torch.Tensor) -> bool:
@@ -66,6 +67,26 @@ def _q8_hand_over(mod, y: torch.Tensor, kw: dict) -> None:
         mod._psd_q8_consumer._psd_q8_pending = (y, kw["q8_out"], kw["q8_sinv"])
 
 
+def _fold_target(mod, x: torch.Tensor):
+    """The 1x1 convolution whose output ``x`` this BN consumed and whose backward can take the BN's
+    input gradient folded (ops/conv.py _fold_backward, kernels/bnfold.hip), or None. The convolution
+    records the output it produced through its fold-aware Function; a mismatch (another producer, a
+    stale record) means no fold."""
+    conv = getattr(mod, "_psd_fold_conv", None)
+    if conv is None or not _at.enabled("PSD_BN_FOLD"):
+        return None
+    rec = getattr(conv, "_psd_fold_out", None)
+    if rec is None or rec[0] != x.data_ptr() or rec[1] != tuple(x.shape):
+        return None
+    return conv
+
+
+def _hand_fold(conv, g, coef, x):
+    """Give ``conv``'s backward what replaces the BN input gradient: (g, coef, the BN input)."""
+    conv._psd_fold_out = None
+    conv._psd_fold_pending = (g, coef, x)
+
+
 class _FusedBNFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, mod, resid_to=None):
@@ -101,7 +122,27 @@ class _FusedBNFn(torch.autograd.Function):
             dgo, dbo = sink(mod.weight), sink(mod.bias)
         pre = getattr(mod, "_psd_bwd_pre", None)
         mod._psd_bwd_pre = None
-        if pre is not None and pre[0].data_ptr() == dy.data_ptr() and pre[0].shape == dy.shape:
+        if pre is not None and not (pre[0].data_ptr() == dy.data_ptr() and pre[0].shape == dy.shape):
+            pre = None
+        conv = _fold_target(mod, x) if (ctx.has_res and ctx.relu and mbits is not None and w is not None) else None
+        if conv is not None:
+            # BN-backward fold: reduction + finalize only; the producing 1x1 convolution's dgrad / wgrad
+            # take g and the coefficients (no elementwise pass, no input-gradient tensor)
+            if pre is not None:
+                g, coef, dg, db = native().bn_bwd_coef(pre[0], x, w, mean, invstd, part=pre[1], rows=pre[2],
+                                                       dgamma_out=dgo, dbeta_out=dbo)
+            else:
+                dy2 = mod._psd_pending_dr.pop() if getattr(mod, "_psd_pending_dr", None) else None
+                g, coef, dg, db = native().bn_bwd_coef(dy, x, w, mean, invstd, mbits=mbits, dy2=dy2, dgamma_out=dgo,
+                                                       dbeta_out=dbo)
+            _hand_fold(conv, g, coef, x)
+            res_grad = None
+            if ctx.resid_to is not None:
+                ctx.resid_to._psd_pending_dr.append(g)
+            else:
+                res_grad = g
+            return g, dg, db, res_grad, None, None
+        if pre is not None:
             # the consumer convolution's bwd-data epilogue reduced this BN's backward and wrote the
             # masked gradient g (= the residual-branch gradient for a residual BN): finalize + one
             # elementwise pass here
@@ -164,6 +205,12 @@ class _BNAddBNReluFn(torch.autograd.Function):
         dg3o, db3o = sinks(bn3)
         dgdo, dbdo = sinks(bnd)
         dy2 = bn3._psd_pending_dr.pop() if getattr(bn3, "_psd_pending_dr", None) else None
+        conv = _fold_target(bn3, x)
+        if conv is not None:  # bn3's input gradient folded into conv3's backward (see _FusedBNFn)
+            _, drr, dg3, db3, dgd, dbd, coef, g = C.bn_bwd_dual(dy, x, w3, mean, invstd, mbits, dy2, r, wd, mean_d,
+                                                                invstd_d, dg3o, db3o, dgdo, dbdo, fold=True)
+            _hand_fold(conv, g, coef, x)
+            return g, dg3, db3, drr, dgd, dbd, None, None
         # one reduce pass for both BNs (the downsample BN's upstream gradient is bn3's dr) and one
         # elementwise pass writing both input gradients (kernels/bn.hip, dual mode)
         dx, drr, dg3, db3, dgd, dbd = C.bn_bwd_dual(dy, x, w3, mean, invstd, mbits, dy2, r, wd, mean_d, invstd_d,

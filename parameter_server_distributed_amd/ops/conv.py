@@ -250,6 +250,30 @@ def _route(key: tuple, cands: dict, default: str, bn=None) -> str:
     return _at.choose(key + ("bnstats",), timed, default)
 
 
+def _convw_cands(dy, x, k: int, stride: int, pad: int) -> dict:
+    """{"psdw<v>": fn(into=None)} over the narrow weight-gradient kernel's tile variants
+    (kernels/convw.hip); fn writes dW in OHWI order into ``into`` (a contiguous [Cout, k*k*Cin] view,
+    e.g. the PS gradient sink) or a fresh tensor and returns the [Cout, Cin, k, k] channels_last view,
+    or None when the kernel declines."""
+    if not _at.enabled("PSD_CONVW"):
+        return {}
+    C = _native()
+    cout, cin = dy.shape[1], x.shape[1]
+    kk = k * k * cin
+    if cin < 64 or (cin & (cin - 1)) or not (cout in (64, 128) or cout % 256 == 0):
+        return {}
+
+    def make(v):
+        def fn(into=None):
+            o = into if into is not None else torch.empty(cout, kk, device=dy.device, dtype=dy.dtype)
+            if not C.convw_(dy, x, o, k, k, stride, pad, variant=v):
+                return None
+            return o.view(cout, k, k, cin).permute(0, 3, 1, 2)
+        return fn
+
+    return {f"psdw{v}": make(v) for v in range(C.convw_variants(cout, kk))}
+
+
 class DelayedScale:
     """Delayed fp8 scaling for one tensor role of one layer (its input activations, or its output
     gradient): each call quantises with the amax the previous call recorded (times ``margin``) and
@@ -284,6 +308,124 @@ def _sink_view(mod, weight):
     autograd would then add into the flat gradient buffer), or None."""
     sink = getattr(mod, "_psd_grad_sink", None) if mod is not None else None
     return sink(weight) if sink is not None else None
+
+
+def _fold_backward(ctx, fold, x, weight, need_x: bool, need_w: bool):
+    """conv3's backward with its consumer BN's input gradient folded in (kernels/bnfold.hip): the BN
+    handed over g (the masked upstream gradient) and the coefficients of dy = A g + B y + C, where
+    y = conv(x) is the BN input. dgrad runs on the narrow kernel with the K-concatenated operand
+    [g | x] (and the producing BN's backward reduction in its epilogue where that wins); wgrad on
+    the narrow wgrad kernel's fold mode (g^T x, x^T x, 1^T x in one pass) + the combination. The
+    unfolded path -- the BN elementwise pass, then the ordinary dgrad -- is one of the timed
+    candidates (and the correctness reference); when it wins, (None, None, dy) is returned and the
+    caller runs the ordinary backward on dy. Returns (dx, dw, None) when folded."""
+    g, coef, y = fold
+    C = _native()
+    n, cin, h, w = x.shape
+    cout = weight.shape[0]
+    M = n * h * w
+    keep = {}
+
+    def unfolded_dy():
+        if "dy" not in keep:
+            keep["dy"] = C.bn_elemt_coef(g, y, coef)
+        return keep["dy"]
+
+    dx = dw = None
+    how = "unfold"
+    frows = C.convw_fold_rows(cout, cin)
+    foldable = (_psdn_ok(cout, cin) and x.is_contiguous(memory_format=torch.channels_last) and cin >= 64
+                and (cin & (cin - 1)) == 0 and cout % 64 == 0 and frows > 0)
+    conv_bwd = torch.ops.aten.convolution_backward
+    wargs = (None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1)
+
+    def fold_wgrad(into):
+        P = torch.empty(frows, cin, device=g.device, dtype=torch.float32)
+        if not C.convw_(g, x, P, 1, 1, 1, 0, fold=True):
+            raise RuntimeError("convw_ declined a fold shape convw_fold_rows accepted")
+        C.bnfold_combine(P, weight, coef, into)
+
+    if need_x and foldable:
+        w2, bvec = C.bnfold_dgrad_weights(weight, coef)
+        wt = weight.reshape(cout, cin).t().contiguous()
+        fu = _bn_bwd_fusion(ctx.mod, x)
+        if fu is not None:
+            fu["dr"] = fu["bn"]._psd_pending_dr.pop() if fu["mode"] == 2 else None
+
+        # timed as dgrad + wgrad pairs: the unfolded path pays the BN elementwise pass and the plain
+        # wgrad on it, the folded one the K-concatenated dgrad and the fold wgrad + combination
+        timing = {"on": True}
+
+        def unfold():
+            out = torch.empty(M, cin, device=g.device, dtype=g.dtype)
+            keep.pop("dy", None)
+            if not C.convn_(unfolded_dy(), wt, out, 1, 1, 1, 0, variant=0):
+                raise RuntimeError("convn_ declined the unfolded dgrad")
+            if timing["on"] and need_w:
+                conv_bwd(keep["dy"], x, weight, *wargs, [False, True, False])
+            return _from_2d(out, n, h, w)
+
+        def make(v, fused):
+            def fn():
+                o = dgrad(v, fused)
+                if timing["on"] and need_w:
+                    fold_wgrad(torch.empty(cout, cin, device=g.device, dtype=g.dtype))
+                return o
+            return fn
+
+        def dgrad(v, fused):
+            out = torch.empty(M, cin, device=g.device, dtype=g.dtype)
+            if fused:
+                part = torch.empty(C.convn_stats_rows(M), 2, cin, device=g.device, dtype=torch.float32)
+                rows = C.convn_bwd_(g, w2, out, 1, 1, 1, 0, part, v, fu["mode"], fu["bx"], fu["mean"],
+                                    bss=fu.get("ss"), bdr=fu.get("dr"), bmbits=fu.get("mbits"), x2=x, bias=bvec)
+            else:
+                rows = C.convn_(g, w2, out, 1, 1, 1, 0, variant=v, x2=x, bias=bvec)
+            if rows == 0:
+                raise RuntimeError("convn_ declined the folded dgrad")
+            o = _from_2d(out, n, h, w)
+            if fused:
+                fu["bn"]._psd_bwd_pre = (o, part, rows)
+            return o
+
+        cands = {"unfold": unfold}
+        for v in range(C.convn_variants(cin)):
+            cands[f"psdnf{v}"] = make(v, False)
+            if fu is not None:
+                cands[f"psdnb{v}"] = make(v, True)
+        key = ("conv1x1", "dgrad_fold", M, cin, cout)
+        if fu is None:
+            how = _at.choose(key, cands, "unfold")
+        else:
+            timed = {nm: (fn if nm.startswith("psdnb") else _with_bn_bwd_reduce(fn, fu)) for nm, fn in cands.items()}
+            how = _at.choose(key + ("bnbwd",), timed, "unfold")
+        timing["on"] = False
+        if how != "unfold":
+            dx = cands[how]()
+            if not how.startswith("psdnb") and fu is not None:
+                fu["bn"]._psd_bwd_pre = None
+                if fu.get("dr") is not None:
+                    fu["bn"]._psd_pending_dr.append(fu["dr"])
+        elif fu is not None:
+            fu["bn"]._psd_bwd_pre = None  # (a timed fused candidate's hand-over)
+            if fu.get("dr") is not None:
+                fu["bn"]._psd_pending_dr.append(fu["dr"])  # the ordinary path pops it again
+    elif not need_x:
+        how = "fold" if foldable else "unfold"
+    if how == "unfold":
+        return None, None, unfolded_dy()
+    if need_w:
+        sv = _sink_view(ctx.mod, weight)
+        if sv is not None and sv.is_contiguous():
+            fold_wgrad(sv.view(cout, cin))
+            dw = sv
+        else:
+            o = torch.empty(cout, cin, device=g.device, dtype=g.dtype)
+            fold_wgrad(o)
+            dw = o.view(cout, cin, 1, 1)
+            if sv is not None:
+                dw = sv.copy_(dw)
+    return dx, dw, None
 
 
 class _Conv1x1Fn(torch.autograd.Function):
@@ -331,17 +473,31 @@ class _Conv1x1Fn(torch.autograd.Function):
         if _psdn_ok(cin, cout):
             bn = _bn_consumer(mod)
             cands.update(_convn_variants(x, w2 if w2.is_contiguous() else w2.contiguous(), 1, 1, 0, bn))
-        return cands[_route(("conv1x1",) + key, cands, "miopen", bn)]()
+        y = cands[_route(("conv1x1",) + key, cands, "miopen", bn)]()
+        if mod is not None:  # this output may have its consumer BN's backward folded (_fold_backward)
+            mod._psd_fold_out = (y.data_ptr(), tuple(y.shape))
+        return y
 
     @staticmethod
     def backward(ctx, dy):
         x, weight = ctx.saved_tensors
         n, cin, h, w = x.shape
         cout = weight.shape[0]
-        if not dy.is_contiguous(memory_format=torch.channels_last):
-            dy = dy.contiguous(memory_format=torch.channels_last)
         need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         dx = dw = None
+        fold = getattr(ctx.mod, "_psd_fold_pending", None) if ctx.mod is not None else None
+        if fold is not None:
+            ctx.mod._psd_fold_pending = None
+            if fold[0].data_ptr() != dy.data_ptr() or fold[0].shape != dy.shape:
+                raise RuntimeError("psd BN-backward fold: the gradient reaching the convolution is not the one its BN "
+                                   "handed over (its input gradient was never formed)")
+            dx, dw, dy = _fold_backward(ctx, fold, x, weight, need_x, need_w)
+            if dy is None:
+                return dx, dw, None, None
+            need_x = need_x and dx is None  # unfolded: dy now holds the BN input gradient
+            need_w = need_w and dw is None
+        if not dy.is_contiguous(memory_format=torch.channels_last):
+            dy = dy.contiguous(memory_format=torch.channels_last)
         conv_bwd = torch.ops.aten.convolution_backward
         args = (None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1)
         if need_x and ctx.fp8 and _fp8_ok(cout, cin) and _at.enabled("PSD_FP8_DGRAD"):
@@ -392,13 +548,25 @@ class _Conv1x1Fn(torch.autograd.Function):
             cands = {"miopen": miopen_w}
             if _psd_ok(cout, cin) and cout % 8 == 0:
                 cands["psd"] = psd_w
+            wcands = _convw_cands(dy, x, 1, 1, 0)
+            cands.update(wcands)
             how = _choose(("wgrad", n * h * w, cin, cout), cands)
             sv = _sink_view(ctx.mod, weight)
+            dw = None
             if sv is not None and how == "psd":  # split-K result reduced straight into the PS buffer
                 _native().gemm_splitk_(_as_2d(dy), _as_2d(x), False, False, sv.view(cout, cin))
                 dw = sv
-            else:
-                dw = cands[how]()
+            elif how in wcands:  # narrow wgrad kernel: its slab reduce writes the PS buffer / dW directly
+                if sv is not None and sv.is_contiguous():
+                    dw = wcands[how](sv.view(cout, cin))
+                    if dw is not None:
+                        dw = sv
+                else:
+                    dw = wcands[how]()
+                    if dw is not None and sv is not None:
+                        dw = sv.copy_(dw)
+            if dw is None:
+                dw = cands[how]() if how not in wcands else miopen_w()
                 if sv is not None:
                     dw = sv.copy_(dw)
                 elif how == "psd" and weight.is_contiguous(memory_format=torch.channels_last):
@@ -591,11 +759,24 @@ class _ConvFn(torch.autograd.Function):
             if (_at.enabled("PSD_CONV_WGRAD") and _wgrad_ok(cin, cout, k, dy)
                     and weight.is_contiguous(memory_format=torch.channels_last)):
                 cands["igemm"] = igemm_c
+            wcands = _convw_cands(dy, x, k, stride, pad) if weight.is_contiguous(
+                memory_format=torch.channels_last) else {}
+            cands.update(wcands)
             key = ("wgrad", n, cin, h, w, cout, k, stride)
             how = _at.choose(("conv",) + key, cands, "miopen") if len(cands) > 1 else "miopen"
             dw = None
             if how == "igemm":
                 dw = igemm_w(sv.permute(0, 2, 3, 1) if sv is not None else None)
+            elif how in wcands:
+                ohwi = sv.permute(0, 2, 3, 1) if sv is not None else None
+                if ohwi is not None and ohwi.is_contiguous():  # the sink itself, in the kernel's layout
+                    dw = wcands[how](ohwi.view(cout, -1))
+                    if dw is not None:
+                        dw = sv
+                else:
+                    dw = wcands[how]()
+                    if dw is not None and sv is not None:
+                        dw = sv.copy_(dw)
             if dw is None:
                 dw = miopen_w()
                 if sv is not None:

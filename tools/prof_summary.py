@@ -66,6 +66,7 @@ def main():
 CATEGORIES = [
     ("psd: batchnorm", r"psd::bn_"),
     ("psd: narrow conv (convn)", r"psd::convn_kernel"),
+    ("psd: narrow conv wgrad (convw)", r"psd::convw_"),
     ("psd: gemm", r"psd::.*(gemm|colsum|splitk)"),
     ("psd: fp8 quantise / amax", r"psd::.*(quant|amax|requant)"),
     ("psd: optimizer / PS apply", r"psd::.*(fused_apply|optim|multi_reduce|pack_cast|f32_to_bf16)"),
@@ -74,8 +75,9 @@ CATEGORIES = [
     ("MIOpen/CK conv bwd-data", r"bwd_data|igemm_bwd|bwd_gtc"),
     ("MIOpen/CK conv bwd-weight", r"wrw|bwd_weight"),
     ("CK batched GEMM (1x1 conv)", r"batched_gemm|gemm_xdl"),
-    ("hipBLASLt GEMM (1x1 conv fwd/dgrad, fc)", r"^Cijk_"),
+    ("hipBLASLt GEMM (1x1 conv fwd/dgrad, fc)", r"^(Custom_)?Cijk_"),
     ("MIOpen tensor ops / fills", r"SubTensorOp|fillBuffer|Transpose|transpose"),
+    ("HIP runtime copies", r"__amd_rocclr_copyBuffer"),
     ("torch elementwise / reduce", r"at::native"),
     ("RCCL", r"nccl|rccl"),
 ]
