@@ -82,7 +82,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("convn_bwd_", &convn_bwd_, py::arg("dy"), py::arg("w2"), py::arg("out"), py::arg("R"), py::arg("S"),
         py::arg("stride"), py::arg("pad"), py::arg("part"), py::arg("variant"), py::arg("mode"), py::arg("bx"),
         py::arg("bmean"), py::arg("bss") = py::none(), py::arg("bdr") = py::none(), py::arg("bmbits") = py::none(),
-        py::arg("x2") = py::none(), py::arg("bias") = py::none());
+        py::arg("x2") = py::none(), py::arg("bias") = py::none(), py::arg("bxd") = py::none(),
+        py::arg("bmean_d") = py::none(), py::arg("part_d") = py::none());
   m.def("bn_bwd_pre", &bn_bwd_pre, py::arg("g"), py::arg("x"), py::arg("gamma"), py::arg("save_mean"),
         py::arg("save_invstd"), py::arg("part"), py::arg("rows"), py::arg("dgamma_out") = py::none(),
         py::arg("dbeta_out") = py::none());
@@ -93,6 +94,10 @@ PYBIND11_MODULE(_C, m) {
         py::arg("stride"), py::arg("pad"), py::arg("splits") = 0);
   m.def("convw_", &convw_, py::arg("dy"), py::arg("x"), py::arg("out"), py::arg("R"), py::arg("S"), py::arg("stride"),
         py::arg("pad"), py::arg("variant") = -1, py::arg("accumulate") = false, py::arg("fold") = false);
+  m.def("bn_bwd_dual_pre", &bn_bwd_dual_pre, py::arg("g"), py::arg("x"), py::arg("gamma"), py::arg("save_mean"),
+        py::arg("save_invstd"), py::arg("part"), py::arg("part_d"), py::arg("rows"), py::arg("xd"), py::arg("gamma_d"),
+        py::arg("mean_d"), py::arg("invstd_d"), py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none(),
+        py::arg("dgamma_d_out") = py::none(), py::arg("dbeta_d_out") = py::none(), py::arg("fold") = false);
   m.def("bn_elemt_coef", &bn_elemt_coef, py::arg("g"), py::arg("x"), py::arg("coef"));
   m.def("convw_fold_rows", &convw_fold_rows, py::arg("Cout"), py::arg("Cin"));
   m.def("bnfold_dgrad_weights", &bnfold_dgrad_weights, py::arg("w"), py::arg("coef"));

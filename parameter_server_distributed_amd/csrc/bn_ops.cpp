@@ -760,4 +760,67 @@ at::Tensor bn_elemt_coef(const at::Tensor& g_in, const at::Tensor& x_in, const a
   return dx;  // empty_like keeps the channels_last layout
 }
 
+// Dual tail backward from convn bwd-mode-3 partials: {dx (undefined with fold), dxd, dgamma, dbeta,
+// dgamma_d, dbeta_d, coef} (kernels/bn.hip launch_bn_bwd_dual_pre)
+std::vector<at::Tensor> bn_bwd_dual_pre(const at::Tensor& g_in, const at::Tensor& x_in, const at::Tensor& gamma,
+                                        const at::Tensor& save_mean, const at::Tensor& save_invstd,
+                                        const at::Tensor& part, const at::Tensor& part_d, int64_t rows,
+                                        const at::Tensor& xd_in, const at::Tensor& gamma_d, const at::Tensor& mean_d,
+                                        const at::Tensor& invstd_d, c10::optional<at::Tensor> dgamma_out,
+                                        c10::optional<at::Tensor> dbeta_out, c10::optional<at::Tensor> dgamma_d_out,
+                                        c10::optional<at::Tensor> dbeta_d_out, bool fold) {
+  const c10::DeviceGuard dg(x_in.device());
+  at::Tensor x = nhwc(x_in), g = nhwc(g_in), xd = nhwc(xd_in);
+  const int64_t C = channels(x), M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0 && g.sizes() == x.sizes() && xd.sizes() == x.sizes() && g.scalar_type() == at::kBFloat16 &&
+                  x.scalar_type() == at::kBFloat16 && xd.scalar_type() == at::kBFloat16,
+              "psd bn_bwd_dual_pre: g / xd like x (bf16)");
+  for (const at::Tensor* t : {&save_mean, &save_invstd, &mean_d, &invstd_d})
+    TORCH_CHECK(t->numel() == C && t->scalar_type() == at::kFloat && t->is_contiguous(), "psd bn_bwd_dual_pre: stats");
+  for (const at::Tensor* t : {&part, &part_d})
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && rows > 0 && t->numel() >= rows * 2 * C,
+                "psd bn_bwd_dual_pre: partials must be fp32 [rows, 2, C]");
+  auto grad_buf = [&](const c10::optional<at::Tensor>& o) {
+    at::Tensor t = (o.has_value() && o->defined()) ? *o : at::empty({C}, x.options());
+    TORCH_CHECK(t.numel() == C && t.scalar_type() == at::kBFloat16 && t.is_contiguous(), "psd bn_bwd_dual_pre: grad buffer");
+    return t;
+  };
+  at::Tensor dgamma = grad_buf(dgamma_out), dbeta = grad_buf(dbeta_out);
+  at::Tensor dgamma_d = grad_buf(dgamma_d_out), dbeta_d = grad_buf(dbeta_d_out);
+  auto f32 = x.options().dtype(at::kFloat);
+  at::Tensor coef = at::empty({3 * C}, f32), coef_d = at::empty({3 * C}, f32);
+  const bool many = rows > kFoldRows;
+  at::Tensor fw = many ? at::empty({(int64_t)kFoldRows * 2 * C}, f32) : at::Tensor();
+  at::Tensor fwd = many ? at::empty({(int64_t)kFoldRows * 2 * C}, f32) : at::Tensor();
+  at::Tensor dx = fold ? at::Tensor() : at::empty_like(x), dxd = at::empty_like(x);
+  BnDualPreArgs a{};
+  a.g = reinterpret_cast<const uint16_t*>(g.data_ptr());
+  a.x = reinterpret_cast<const uint16_t*>(x.data_ptr());
+  a.xd = reinterpret_cast<const uint16_t*>(xd.data_ptr());
+  a.gamma = reinterpret_cast<const uint16_t*>(gamma.data_ptr());
+  a.gamma_d = reinterpret_cast<const uint16_t*>(gamma_d.data_ptr());
+  a.mean = save_mean.data_ptr<float>();
+  a.invstd = save_invstd.data_ptr<float>();
+  a.mean_d = mean_d.data_ptr<float>();
+  a.invstd_d = invstd_d.data_ptr<float>();
+  a.part = part.data_ptr<float>();
+  a.part_d = part_d.data_ptr<float>();
+  a.rows = (int)rows;
+  a.fold_ws = many ? fw.data_ptr<float>() : nullptr;
+  a.fold_ws_d = many ? fwd.data_ptr<float>() : nullptr;
+  a.dgamma = reinterpret_cast<uint16_t*>(dgamma.data_ptr());
+  a.dbeta = reinterpret_cast<uint16_t*>(dbeta.data_ptr());
+  a.dgamma_d = reinterpret_cast<uint16_t*>(dgamma_d.data_ptr());
+  a.dbeta_d = reinterpret_cast<uint16_t*>(dbeta_d.data_ptr());
+  a.coef = coef.data_ptr<float>();
+  a.coef_d = coef_d.data_ptr<float>();
+  a.dx = fold ? nullptr : reinterpret_cast<uint16_t*>(dx.data_ptr());
+  a.dxd = reinterpret_cast<uint16_t*>(dxd.data_ptr());
+  a.M = M;
+  a.C = (int)C;
+  const hipError_t e = launch_bn_bwd_dual_pre(a, stream_of(x));
+  TORCH_CHECK(e == hipSuccess, "psd bn_bwd_dual_pre: ", hipGetErrorString(e));
+  return {dx, dxd, dgamma, dbeta, dgamma_d, dbeta_d, coef};
+}
+
 }  // namespace psd

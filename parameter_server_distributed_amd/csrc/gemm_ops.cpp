@@ -316,14 +316,16 @@ int64_t convn_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_
 int64_t convn_bwd_(const at::Tensor& dy, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride,
                    int64_t pad, at::Tensor part, int64_t variant, int64_t mode, const at::Tensor& bx,
                    const at::Tensor& bmean, c10::optional<at::Tensor> bss, c10::optional<at::Tensor> bdr,
-                   c10::optional<at::Tensor> bmbits, c10::optional<at::Tensor> x2, c10::optional<at::Tensor> bias) {
+                   c10::optional<at::Tensor> bmbits, c10::optional<at::Tensor> x2, c10::optional<at::Tensor> bias,
+                   c10::optional<at::Tensor> bxd, c10::optional<at::Tensor> bmean_d, c10::optional<at::Tensor> part_d) {
   TORCH_CHECK(dy.is_cuda() && dy.dim() == 4 && dy.scalar_type() == at::kBFloat16 &&
                   dy.is_contiguous(at::MemoryFormat::ChannelsLast),
               "psd convn_bwd: dy must be a channels_last bf16 device tensor");
   TORCH_CHECK(w2.is_cuda() && w2.dim() == 2 && w2.scalar_type() == at::kBFloat16 && w2.is_contiguous(),
               "psd convn_bwd: w2 must be a contiguous bf16 [N, R*S*C] tensor");
   TORCH_CHECK(out.dim() == 2 && out.is_contiguous() && out.scalar_type() == at::kBFloat16, "psd convn_bwd: out");
-  TORCH_CHECK(mode == 1 || mode == 2, "psd convn_bwd: mode 1 (mask from x, ss) or 2 (bit-mask + dr)");
+  TORCH_CHECK(mode == 1 || mode == 2 || mode == 3,
+              "psd convn_bwd: mode 1 (mask from x, ss), 2 (bit-mask + dr) or 3 (2 + the dual tail's second BN)");
   const int64_t Nb = dy.size(0), C = dy.size(1), H = dy.size(2), W = dy.size(3);
   const int64_t Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
   const int64_t M = Nb * Ho * Wo, N = w2.size(0), K1 = R * S * C;
@@ -349,6 +351,16 @@ int64_t convn_bwd_(const at::Tensor& dy, const at::Tensor& w2, at::Tensor out, i
                     bss->is_contiguous(),
                 "psd convn_bwd: mode 1 needs ss fp32 [2N]");
   } else {
+    if (mode == 3) {
+      TORCH_CHECK(bxd.has_value() && bxd->defined() && bmean_d.has_value() && bmean_d->defined() &&
+                      part_d.has_value() && part_d->defined(),
+                  "psd convn_bwd: mode 3 needs bxd, bmean_d and part_d");
+      like_out(*bxd, "bxd");
+      TORCH_CHECK(bmean_d->scalar_type() == at::kFloat && bmean_d->numel() == N && bmean_d->is_contiguous(),
+                  "psd convn_bwd: bmean_d");
+      TORCH_CHECK(part_d->scalar_type() == at::kFloat && part_d->is_contiguous() && part_d->numel() >= part.numel(),
+                  "psd convn_bwd: part_d like part");
+    }
     TORCH_CHECK(bdr.has_value() && bdr->defined(), "psd convn_bwd: mode 2 needs dr");
     like_out(*bdr, "dr");
     TORCH_CHECK(bmbits.has_value() && bmbits->defined() && bmbits->scalar_type() == at::kByte &&
@@ -387,8 +399,13 @@ int64_t convn_bwd_(const at::Tensor& dy, const at::Tensor& w2, at::Tensor out, i
   a.bx = reinterpret_cast<const uint16_t*>(bx.data_ptr());
   a.bmean = bmean.data_ptr<float>();
   a.bss = mode == 1 ? bss->data_ptr<float>() : nullptr;
-  a.bdr = mode == 2 ? reinterpret_cast<const uint16_t*>(bdr->data_ptr()) : nullptr;
-  a.bmbits = mode == 2 ? bmbits->data_ptr<uint8_t>() : nullptr;
+  a.bdr = mode >= 2 ? reinterpret_cast<const uint16_t*>(bdr->data_ptr()) : nullptr;
+  a.bmbits = mode >= 2 ? bmbits->data_ptr<uint8_t>() : nullptr;
+  if (mode == 3) {
+    a.bxd = reinterpret_cast<const uint16_t*>(bxd->data_ptr());
+    a.bmean_d = bmean_d->data_ptr<float>();
+    a.part_d = part_d->data_ptr<float>();
+  }
   const hipError_t e = launch_convn(a, c10::hip::getCurrentHIPStream(dy.device().index()).stream());
   if (e == hipErrorNotSupported) return 0;
   TORCH_CHECK(e == hipSuccess, "psd convn_bwd: ", hipGetErrorString(e));

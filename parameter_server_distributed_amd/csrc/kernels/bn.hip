@@ -877,6 +877,41 @@ hipError_t launch_bn_elemt_coef(const uint16_t* g, const uint16_t* x, const floa
   return hipGetLastError();
 }
 
+// finalize from `rows` producer-reduced partial rows (folded to kFoldRows first when there are more)
+static void finalize_pre(const float* part, int rows, float* fold_ws, int64_t M, int C, const uint16_t* gamma,
+                         const float* mean, const float* invstd, uint16_t* dgamma, uint16_t* dbeta, float* coef,
+                         hipStream_t st) {
+  const float* p = part;
+  int nblk = rows;
+  if (rows > kFoldRows) {
+    hipLaunchKernelGGL(bn_part_fold_kernel, dim3(kFoldRows, (2 * C + 127) / 128), dim3(256), 0, st, part, rows, 2 * C,
+                       fold_ws, kFoldRows);
+    p = fold_ws;
+    nblk = kFoldRows;
+  }
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(256), 0, st, p, nblk, M, C, gamma,
+                     mean, invstd, dgamma, dbeta, coef);
+}
+
+// Dual tail relu(bn(x) + bnd(xd)) backward from partials reduced in the consumer convolution's
+// bwd-data epilogue (kernels/convn.hip bwd mode 3): finalize both BNs, then one elementwise pass (dx
+// may be null: bn's input gradient folded into its producer, ops/conv.py _fold_backward).
+hipError_t launch_bn_bwd_dual_pre(const BnDualPreArgs& a, hipStream_t st) {
+  if (a.M <= 0) return hipSuccess;
+  if (a.C % 8 != 0 || a.rows <= 0 || (a.rows > kFoldRows && (!a.fold_ws || !a.fold_ws_d))) return hipErrorInvalidValue;
+  finalize_pre(a.part, a.rows, a.fold_ws, a.M, a.C, a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta, a.coef, st);
+  finalize_pre(a.part_d, a.rows, a.fold_ws_d, a.M, a.C, a.gamma_d, a.mean_d, a.invstd_d, a.dgamma_d, a.dbeta_d,
+               a.coef_d, st);
+  const int64_t nvec = a.M * (a.C / 8);
+  if (a.dx)
+    hipLaunchKernelGGL(bn_bwd_elemt_dual_kernel<true>, dim3(elem_grid(nvec, a.C)), dim3(256), 0, st, a.g, a.x, a.coef,
+                       a.dx, a.xd, a.coef_d, a.dxd, nvec, a.C);
+  else
+    hipLaunchKernelGGL(bn_bwd_elemt_dual_kernel<false>, dim3(elem_grid(nvec, a.C)), dim3(256), 0, st, a.g, a.x,
+                       a.coef, a.dx, a.xd, a.coef_d, a.dxd, nvec, a.C);
+  return hipGetLastError();
+}
+
 hipError_t launch_bn_bwd(const BnBwdArgs& a, hipStream_t st) {
   if (a.M <= 0) return hipSuccess;
   if (a.C % 8 != 0) return hipErrorInvalidValue;

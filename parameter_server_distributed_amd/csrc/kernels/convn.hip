@@ -141,6 +141,8 @@ struct Geo {
 // convolution and the identity residual). The stored output is then g = mask (dX [+ dr]) -- the
 // masked gradient the BN's elementwise pass consumes and, for 2, the residual gradient handed on --
 // and the partials are sum g and sum g (x - mean) per channel (the layout of bn_bwd_reduce_kernel).
+// 3: as 2 for a bottleneck tail relu(bn3(x) + bnd(xd)) (the downsample block's dual BN, whose
+// upstream gradient g is shared): part_d also receives sum g and sum g (xd - mean_d) for bnd.
 template <int BM, int BN, int WNT, int NSLOT, bool STATS, int BWD = 0>
 __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
   using G = Geo<BM, BN, WNT, NSLOT>;
@@ -313,7 +315,12 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
   // BWD: this lane's 8 output channels are fixed (64 % CPR == 0): per-channel constants once
   const int my_c16 = lane % CPR;
   const int my_col = n0 + wc * WNT + my_c16 * 8;
-  float bmu[8], bsc[8], bsh[8], ga[8], gb[8];
+  float bmu[8], bsc[8], bsh[8], ga[8], gb[8], bmd[8], gd[8];
+  if constexpr (BWD == 3) {
+    load8_f32(a.bmean_d + my_col, bmd);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) gd[e] = 0.f;
+  }
   if constexpr (BWD != 0) {
     load8_f32(a.bmean + my_col, bmu);
     if constexpr (BWD == 1) {
@@ -349,7 +356,7 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
           float d[8], xv[8];
           load8_bf16(reinterpret_cast<const uint16_t*>(&v), d);
           load8_bf16(a.bx + (int64_t)m * a.N + my_col, xv);
-          if constexpr (BWD == 2) {
+          if constexpr (BWD >= 2) {
             float rv[8];
             load8_bf16(a.bdr + (int64_t)m * a.N + my_col, rv);
             const uint32_t bits = a.bmbits[((int64_t)m * a.N + my_col) >> 3];
@@ -368,6 +375,12 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
             const float gq = bf16_to_f32(f32_to_bf16(d[e]));  // the stored g
             ga[e] += gq;
             gb[e] = fmaf(gq, xv[e] - bmu[e], gb[e]);
+          }
+          if constexpr (BWD == 3) {
+            float dv[8];
+            load8_bf16(a.bxd + (int64_t)m * a.N + my_col, dv);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) gd[e] = fmaf(bf16_to_f32(f32_to_bf16(d[e])), dv[e] - bmd[e], gd[e]);
           }
         }
         *reinterpret_cast<u32x4*>(y + go) = v;
@@ -389,11 +402,22 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
       gb[e] += xor16(gb[e], lane);
       ga[e] += xor32(ga[e], lane);
       gb[e] += xor32(gb[e], lane);
+      if constexpr (BWD == 3) {
+        if constexpr (CPR == 4) gd[e] += ror_row<4>(gd[e]);
+        gd[e] += ror_row<8>(gd[e]);
+        gd[e] += xor16(gd[e], lane);
+        gd[e] += xor32(gd[e], lane);
+      }
     }
     if (lane < CPR) {
       float* pr = a.part + ((int64_t)tm * G::WM + wr) * 2 * a.N;
       store8_f32(pr + my_col, ga);
       store8_f32(pr + a.N + my_col, gb);
+      if constexpr (BWD == 3) {
+        float* pd = a.part_d + ((int64_t)tm * G::WM + wr) * 2 * a.N;
+        store8_f32(pd + my_col, ga);
+        store8_f32(pd + a.N + my_col, gd);
+      }
     }
   }
 }
@@ -422,6 +446,7 @@ template <int BM, int BN, int WNT, int NSLOT>
 static hipError_t convn_launch_s(const ConvnArgs& a, hipStream_t st) {
   if (a.bwd == 1) return convn_launch_t<BM, BN, WNT, NSLOT, false, 1>(a, st);
   if (a.bwd == 2) return convn_launch_t<BM, BN, WNT, NSLOT, false, 2>(a, st);
+  if (a.bwd == 3) return convn_launch_t<BM, BN, WNT, NSLOT, false, 3>(a, st);
   return a.part ? convn_launch_t<BM, BN, WNT, NSLOT, true, 0>(a, st)
                 : convn_launch_t<BM, BN, WNT, NSLOT, false, 0>(a, st);
 }
@@ -478,7 +503,9 @@ hipError_t launch_convn(const ConvnArgs& a_in, hipStream_t st) {
                   a.wbytes > 0 && a.variant < convn_variant_count(bn) &&
                   (a.bwd == 0 ? (!a.part || a.shift)
                               : (a.part && a.bx && a.bmean && a.ldc == a.N &&
-                                 (a.bwd == 1 ? a.bss != nullptr : (a.bwd == 2 && a.bdr && a.bmbits))));
+                                 (a.bwd == 1 ? a.bss != nullptr
+                                             : ((a.bwd == 2 || a.bwd == 3) && a.bdr && a.bmbits &&
+                                                (a.bwd == 2 || (a.bxd && a.bmean_d && a.part_d))))));
   if (!ok) return hipErrorNotSupported;
   const int v = a.variant >= 0 ? a.variant : default_variant(a, bn);
   switch (bn) {

@@ -98,6 +98,26 @@ hipError_t launch_bn_bwd_pre(const uint16_t* g, const uint16_t* x, const uint16_
                              const float* invstd, const float* part, int rows, float* fold_ws, uint16_t* dgamma,
                              uint16_t* dbeta, float* coef, uint16_t* dx, int64_t M, int C, hipStream_t stream);
 
+struct BnDualPreArgs {
+  const uint16_t* g;      // masked upstream gradient (= the residual-branch gradient) [M, C]
+  const uint16_t* x;      // bn's input
+  const uint16_t* xd;     // bnd's input
+  const uint16_t* gamma;
+  const uint16_t* gamma_d;
+  const float *mean, *invstd, *mean_d, *invstd_d;
+  const float* part;      // [rows][2][C] sum g, sum g (x - mean)
+  const float* part_d;    // [rows][2][C] sum g, sum g (xd - mean_d)
+  int rows;
+  float *fold_ws, *fold_ws_d;  // [kFoldRows * 2C] each when rows > kFoldRows
+  uint16_t *dgamma, *dbeta, *dgamma_d, *dbeta_d;
+  float *coef, *coef_d;   // [3C] each
+  uint16_t* dx;           // optional (null: folded)
+  uint16_t* dxd;
+  int64_t M;
+  int C;
+};
+hipError_t launch_bn_bwd_dual_pre(const BnDualPreArgs& a, hipStream_t stream);
+
 // BN-backward fold (bnfold.hip); bn_elemt_coef (bn.hip): dx = A g + B x + C from finalized coefficients
 hipError_t launch_bn_elemt_coef(const uint16_t* g, const uint16_t* x, const float* coef, uint16_t* dx, int64_t M, int C,
                                 hipStream_t stream);

@@ -26,6 +26,10 @@ struct ConvnArgs {
   const float* bss;       // bwd 1: [2N] its forward scale / shift (ReLU mask)
   const uint16_t* bdr;    // bwd 2: [M][N] the residual-branch gradient to add
   const uint8_t* bmbits;  // bwd 2: [M*N/8] the forward ReLU bit-mask
+  // bwd 3 (dual tail relu(bn(x) + bnd(xd))): bnd's input, its saved mean and its partials
+  const uint16_t* bxd;
+  const float* bmean_d;
+  float* part_d;
   // K-concatenated second operand (1x1 only): A(m, k) = x2[m][k - K1] for k >= K1, so
   // y = [x | x2] . w^T with w [N][K1 + C2] (the BN-backward fold of ops/bn.py: dgrad of a 1x1 conv
   // whose BN input gradient is never materialised)

@@ -39,6 +39,13 @@ std::vector<at::Tensor> bn_bwd_dual(const at::Tensor& dy, const at::Tensor& x, c
                                     c10::optional<at::Tensor> dgamma_out, c10::optional<at::Tensor> dbeta_out,
                                     c10::optional<at::Tensor> dgamma_d_out, c10::optional<at::Tensor> dbeta_d_out, bool fold);
 at::Tensor bn_elemt_coef(const at::Tensor& g, const at::Tensor& x, const at::Tensor& coef);
+std::vector<at::Tensor> bn_bwd_dual_pre(const at::Tensor& g, const at::Tensor& x, const at::Tensor& gamma,
+                                        const at::Tensor& save_mean, const at::Tensor& save_invstd,
+                                        const at::Tensor& part, const at::Tensor& part_d, int64_t rows,
+                                        const at::Tensor& xd, const at::Tensor& gamma_d, const at::Tensor& mean_d,
+                                        const at::Tensor& invstd_d, c10::optional<at::Tensor> dgamma_out,
+                                        c10::optional<at::Tensor> dbeta_out, c10::optional<at::Tensor> dgamma_d_out,
+                                        c10::optional<at::Tensor> dbeta_d_out, bool fold);
 std::vector<at::Tensor> bnfold_dgrad_weights(const at::Tensor& w, const at::Tensor& coef);
 void bnfold_combine(const at::Tensor& P, const at::Tensor& w, const at::Tensor& coef, at::Tensor out, bool accumulate);
 std::vector<at::Tensor> bn_bwd_coef(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& gamma,
@@ -71,7 +78,8 @@ int64_t convn_bwd_(const at::Tensor& dy, const at::Tensor& w2, at::Tensor out, i
                    int64_t pad, at::Tensor part, int64_t variant, int64_t mode, const at::Tensor& bx,
                    const at::Tensor& bmean, c10::optional<at::Tensor> bss, c10::optional<at::Tensor> bdr,
                    c10::optional<at::Tensor> bmbits, c10::optional<at::Tensor> x2,
-                   c10::optional<at::Tensor> bias);
+                   c10::optional<at::Tensor> bias, c10::optional<at::Tensor> bxd, c10::optional<at::Tensor> bmean_d,
+                   c10::optional<at::Tensor> part_d);
 std::vector<at::Tensor> bn_bwd_pre(const at::Tensor& g, const at::Tensor& x, c10::optional<at::Tensor> gamma,
                                    const at::Tensor& save_mean, const at::Tensor& save_invstd, const at::Tensor& part,
                                    int64_t rows, c10::optional<at::Tensor> dgamma_out,

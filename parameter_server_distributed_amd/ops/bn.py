@@ -99,7 +99,7 @@ class _FusedBNFn(torch.autograd.Function):
                                               **_stats_args(mod, x))
         _q8_hand_over(mod, y, q8)
         # for the consumer convolution's bwd-data epilogue (ops/conv.py _bn_bwd_fusion): ReLU BNs
-        mod._psd_fwd = (y, x, mean, ss, mbits if has_res else None) if mod.relu else None
+        mod._psd_fwd = (y, x, mean, ss, mbits if has_res else None, None, None) if mod.relu else None
         ctx.relu = mod.relu
         ctx.has_res = residual is not None
         ctx.mod = mod
@@ -188,6 +188,9 @@ class _BNAddBNReluFn(torch.autograd.Function):
                                              bn3.eps, bn3.num_batches_tracked, None, mask_out=True, residual_ss=ss_d,
                                              **q8, **_stats_args(bn3, x))
         _q8_hand_over(bn3, y, q8)
+        # for the consumer convolution's bwd-data epilogue (ops/conv.py _bn_bwd_fusion, mode 3): both
+        # BNs' backward reductions ride on it
+        bn3._psd_fwd = (y, x, mean, None, mbits, r, mean_d)
         ctx.bn3, ctx.bnd = bn3, bnd
         ctx.save_for_backward(x, mbits, w3, mean, invstd, r, wd, mean_d, invstd_d)
         return y
@@ -204,8 +207,22 @@ class _BNAddBNReluFn(torch.autograd.Function):
 
         dg3o, db3o = sinks(bn3)
         dgdo, dbdo = sinks(bnd)
-        dy2 = bn3._psd_pending_dr.pop() if getattr(bn3, "_psd_pending_dr", None) else None
+        bn3._psd_fwd = None
         conv = _fold_target(bn3, x)
+        pre = getattr(bn3, "_psd_bwd_pre", None)
+        bn3._psd_bwd_pre = None
+        if pre is not None and len(pre) == 4 and pre[0].data_ptr() == dy.data_ptr() and pre[0].shape == dy.shape:
+            # both reductions ran in the consumer convolution's bwd-data epilogue (convn mode 3): g is
+            # the masked gradient incl. the residual branch; finalize both + one elementwise pass
+            g, part, rows, part_d = pre
+            dx, drr, dg3, db3, dgd, dbd, coef = C.bn_bwd_dual_pre(g, x, w3, mean, invstd, part, part_d, rows, r, wd,
+                                                                  mean_d, invstd_d, dg3o, db3o, dgdo, dbdo,
+                                                                  fold=conv is not None)
+            if conv is not None:
+                _hand_fold(conv, g, coef, x)
+                return g, dg3, db3, drr, dgd, dbd, None, None
+            return dx, dg3, db3, drr, dgd, dbd, None, None
+        dy2 = bn3._psd_pending_dr.pop() if getattr(bn3, "_psd_pending_dr", None) else None
         if conv is not None:  # bn3's input gradient folded into conv3's backward (see _FusedBNFn)
             _, drr, dg3, db3, dgd, dbd, coef, g = C.bn_bwd_dual(dy, x, w3, mean, invstd, mbits, dy2, r, wd, mean_d,
                                                                 invstd_d, dg3o, db3o, dgdo, dbdo, fold=True)

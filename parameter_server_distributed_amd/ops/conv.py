@@ -168,12 +168,16 @@ def _bn_bwd_fusion(mod, x: torch.Tensor):
     st = getattr(bn, "_psd_fwd", None) if bn is not None else None
     if st is None or not _at.enabled("PSD_CONVN_BWD"):
         return None
-    y, bx, mean, ss, mbits = st
+    y, bx, mean, ss, mbits, xd, mean_d = st
     if y.data_ptr() != x.data_ptr() or y.shape != x.shape or y.stride() != x.stride():
         return None
     if mbits is not None:
         if not bn._psd_pending_dr:
             return None
+        if xd is not None:  # a downsample block's dual tail: both BNs' reductions (mode 3)
+            if not _at.enabled("PSD_CONVN_BWD3"):
+                return None
+            return dict(mode=3, bn=bn, bx=bx, mean=mean, mbits=mbits, bxd=xd, mean_d=mean_d)
         return dict(mode=2, bn=bn, bx=bx, mean=mean, mbits=mbits)
     return dict(mode=1, bn=bn, bx=bx, mean=mean, ss=ss)
 
@@ -191,12 +195,14 @@ def _convn_bwd_variants(dy, w2, k: int, pad: int, fu: dict, dr) -> dict:
         def fn():
             out = torch.empty(M, cout, device=dy.device, dtype=dy.dtype)
             part = torch.empty(C.convn_stats_rows(M), 2, cout, device=dy.device, dtype=torch.float32)
+            part_d = torch.empty_like(part) if fu["mode"] == 3 else None
             rows = C.convn_bwd_(dy, w2, out, k, k, 1, pad, part, v, fu["mode"], fu["bx"], fu["mean"],
-                                bss=fu.get("ss"), bdr=dr, bmbits=fu.get("mbits"))
+                                bss=fu.get("ss"), bdr=dr, bmbits=fu.get("mbits"), bxd=fu.get("bxd"),
+                                bmean_d=fu.get("mean_d"), part_d=part_d)
             if rows == 0:
                 raise RuntimeError("convn_bwd_ declined a shape _psdn_ok accepted")
             g = _from_2d(out, n, h, w)
-            fu["bn"]._psd_bwd_pre = (g, part, rows)
+            fu["bn"]._psd_bwd_pre = (g, part, rows) if part_d is None else (g, part, rows, part_d)
             return g
         return fn
 
@@ -350,7 +356,7 @@ def _fold_backward(ctx, fold, x, weight, need_x: bool, need_w: bool):
         wt = weight.reshape(cout, cin).t().contiguous()
         fu = _bn_bwd_fusion(ctx.mod, x)
         if fu is not None:
-            fu["dr"] = fu["bn"]._psd_pending_dr.pop() if fu["mode"] == 2 else None
+            fu["dr"] = fu["bn"]._psd_pending_dr.pop() if fu["mode"] >= 2 else None
 
         # timed as dgrad + wgrad pairs: the unfolded path pays the BN elementwise pass and the plain
         # wgrad on it, the folded one the K-concatenated dgrad and the fold wgrad + combination
@@ -375,17 +381,20 @@ def _fold_backward(ctx, fold, x, weight, need_x: bool, need_w: bool):
 
         def dgrad(v, fused):
             out = torch.empty(M, cin, device=g.device, dtype=g.dtype)
+            part_d = None
             if fused:
                 part = torch.empty(C.convn_stats_rows(M), 2, cin, device=g.device, dtype=torch.float32)
+                part_d = torch.empty_like(part) if fu["mode"] == 3 else None
                 rows = C.convn_bwd_(g, w2, out, 1, 1, 1, 0, part, v, fu["mode"], fu["bx"], fu["mean"],
-                                    bss=fu.get("ss"), bdr=fu.get("dr"), bmbits=fu.get("mbits"), x2=x, bias=bvec)
+                                    bss=fu.get("ss"), bdr=fu.get("dr"), bmbits=fu.get("mbits"), x2=x, bias=bvec,
+                                    bxd=fu.get("bxd"), bmean_d=fu.get("mean_d"), part_d=part_d)
             else:
                 rows = C.convn_(g, w2, out, 1, 1, 1, 0, variant=v, x2=x, bias=bvec)
             if rows == 0:
                 raise RuntimeError("convn_ declined the folded dgrad")
             o = _from_2d(out, n, h, w)
             if fused:
-                fu["bn"]._psd_bwd_pre = (o, part, rows)
+                fu["bn"]._psd_bwd_pre = (o, part, rows) if part_d is None else (o, part, rows, part_d)
             return o
 
         cands = {"unfold": unfold}
@@ -533,7 +542,7 @@ class _Conv1x1Fn(torch.autograd.Function):
                 cands.update(_convn_variants(dy, wt, 1, 1, 0))
                 fu = _bn_bwd_fusion(ctx.mod, x)
                 if fu is not None:
-                    fu["dr"] = fu["bn"]._psd_pending_dr.pop() if fu["mode"] == 2 else None
+                    fu["dr"] = fu["bn"]._psd_pending_dr.pop() if fu["mode"] >= 2 else None
                     cands.update(_convn_bwd_variants(dy, wt, 1, 0, fu, fu["dr"]))
             dx = _dgrad_route(("conv1x1",) + key, cands, "miopen", fu, x)
         if need_w:
@@ -733,7 +742,7 @@ class _ConvFn(torch.autograd.Function):
                     cands.update(_convn_variants(dy, wf, k, 1, pad))
                     fu = _bn_bwd_fusion(ctx.mod, x)
                     if fu is not None:
-                        fu["dr"] = fu["bn"]._psd_pending_dr.pop() if fu["mode"] == 2 else None
+                        fu["dr"] = fu["bn"]._psd_pending_dr.pop() if fu["mode"] >= 2 else None
                         cands.update(_convn_bwd_variants(dy, wf, k, pad, fu, fu["dr"]))
                 key = ("dgrad", n, cin, h, w, cout, k, stride)
                 dx = _dgrad_route(("conv",) + key, cands, "miopen", fu, x)

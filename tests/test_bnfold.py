@@ -74,11 +74,12 @@ def test_bnfold_weights_and_combine(gpu, cout, cin):
     torch.testing.assert_close(out.float().cpu(), want, rtol=2e-2, atol=2e-2 * float(want.abs().max()))
 
 
-def _resnet_grads(gpu, monkeypatch, fold: bool, force: str, fp32: bool = False):
+def _resnet_grads(gpu, monkeypatch, fold: bool, force: str, fp32: bool = False, convn: bool = True):
     from parameter_server_distributed_amd import models
     from parameter_server_distributed_amd.ops import autotune
 
     monkeypatch.setenv("PSD_BN_FOLD", "1" if fold else "0")
+    monkeypatch.setenv("PSD_CONVN", "1" if convn else "0")
     monkeypatch.setenv("PSD_AUTOTUNE_FORCE", force)
     autotune._DECISIONS.clear()
     torch.manual_seed(0)
@@ -199,3 +200,62 @@ def test_convw_fold_rows_contract(gpu):
     assert native().convw_fold_rows(512, 128) == 768
     assert native().convw_fold_rows(1024, 256) == 1408
     assert native().convw_fold_rows(2048, 512) == 0
+
+
+def _chain_grads(gpu, monkeypatch, mode: str):
+    """A downsample block feeding an identity block (the pattern of every layer's first two
+    blocks): mode 'fused' (every narrow-kernel fusion forced: the identity block's conv1 bwd-data
+    reduces the downsample block's dual-BN tail -- convn mode 3 -- and both bn3s fold), 'library'
+    (library convolutions, separate BN passes) or 'fp32' (the composite fp32 reference)."""
+    import torch.nn as nn
+
+    from parameter_server_distributed_amd.models.resnet import Bottleneck, _conv
+    from parameter_server_distributed_amd.ops import autotune
+    from parameter_server_distributed_amd.ops.bn import FusedBatchNorm2d
+
+    monkeypatch.setenv("PSD_BN_FOLD", "1" if mode == "fused" else "0")
+    monkeypatch.setenv("PSD_CONVN", "1" if mode == "fused" else "0")
+    monkeypatch.setenv("PSD_AUTOTUNE_FORCE", "psdnb0,psdnf0,psdn0" if mode == "fused" else "miopen")
+    autotune._DECISIONS.clear()
+    torch.manual_seed(2)
+    a = Bottleneck(64, 64, downsample=nn.Sequential(_conv(64, 256, 1), FusedBatchNorm2d(256)))
+    b = Bottleneck(256, 64)
+    g = torch.Generator().manual_seed(4)
+    blocks = nn.ModuleList([a, b])
+    for mod in blocks.modules():
+        if isinstance(mod, nn.Conv2d):
+            nn.init.kaiming_normal_(mod.weight, mode="fan_out", nonlinearity="relu")
+        if hasattr(mod, "running_mean") and mod.weight is not None:
+            mod.weight.data.copy_(0.5 + torch.rand(mod.weight.shape, generator=g))
+            mod.bias.data.copy_(0.2 * torch.randn(mod.bias.shape, generator=g))
+    blocks = blocks.to(gpu)
+    dt = torch.float32 if mode == "fp32" else torch.bfloat16
+    for p in blocks.parameters():
+        p.data = p.data.to(torch.bfloat16).to(dt)
+        if p.dim() == 4:
+            p.data = p.data.contiguous(memory_format=CL)
+    x = torch.randn(8, 64, 28, 28, generator=g).to(torch.bfloat16).to(gpu, dt).contiguous(memory_format=CL)
+    x.requires_grad_(True)
+    y = b(a(x), a.bn3)
+    gy = torch.randn(y.shape, generator=torch.Generator().manual_seed(6)).to(torch.bfloat16).to(gpu, dt)
+    y.backward(gy.contiguous(memory_format=CL))
+    picks = autotune.decisions()
+    autotune._DECISIONS.clear()
+    out = {n: p.grad.float().clone() for n, p in blocks.named_parameters()}
+    out["input"] = x.grad.float().clone()
+    return out, picks
+
+
+def test_chain_fusions_vs_fp32(gpu, monkeypatch):
+    """Downsample block -> identity block with every fusion (convn mode 3 on the dual tail, both
+    bn3 folds) vs the library path, both against fp32: the fused path's error stays at the library
+    path's bf16 level, parameter by parameter."""
+    gf, picks = _chain_grads(gpu, monkeypatch, "fused")
+    assert any(k[1] == "dgrad" and v.startswith("psdnb") for k, v in picks.items() if len(k) > 1), picks
+    gl, _ = _chain_grads(gpu, monkeypatch, "library")
+    gr, _ = _chain_grads(gpu, monkeypatch, "fp32")
+    ef, el = _rel(gf, gr), _rel(gl, gr)
+    print({n: (round(ef[n], 4), round(el[n], 4)) for n in ef})
+    for n in ef:
+        assert ef[n] < 0.15, (n, ef[n], el[n])
+        assert ef[n] <= 1.15 * el[n] + 3e-3, (n, ef[n], el[n])
