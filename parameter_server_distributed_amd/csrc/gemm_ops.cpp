@@ -324,8 +324,9 @@ int64_t convn_bwd_(const at::Tensor& dy, const at::Tensor& w2, at::Tensor out, i
   TORCH_CHECK(w2.is_cuda() && w2.dim() == 2 && w2.scalar_type() == at::kBFloat16 && w2.is_contiguous(),
               "psd convn_bwd: w2 must be a contiguous bf16 [N, R*S*C] tensor");
   TORCH_CHECK(out.dim() == 2 && out.is_contiguous() && out.scalar_type() == at::kBFloat16, "psd convn_bwd: out");
-  TORCH_CHECK(mode == 1 || mode == 2 || mode == 3,
-              "psd convn_bwd: mode 1 (mask from x, ss), 2 (bit-mask + dr) or 3 (2 + the dual tail's second BN)");
+  TORCH_CHECK(mode == 1 || mode == 2 || mode == 3 || mode == 5,
+              "psd convn_bwd: mode 1 (mask from x, ss), 2 (bit-mask + dr), 3 (2 + the dual tail's second BN) or 5 "
+              "(2 with dr on the stride-2 quarter grid)");
   const int64_t Nb = dy.size(0), C = dy.size(1), H = dy.size(2), W = dy.size(3);
   const int64_t Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
   const int64_t M = Nb * Ho * Wo, N = w2.size(0), K1 = R * S * C;
@@ -362,7 +363,14 @@ int64_t convn_bwd_(const at::Tensor& dy, const at::Tensor& w2, at::Tensor out, i
                   "psd convn_bwd: part_d like part");
     }
     TORCH_CHECK(bdr.has_value() && bdr->defined(), "psd convn_bwd: mode 2 needs dr");
-    like_out(*bdr, "dr");
+    if (mode == 5) {
+      TORCH_CHECK(bdr->scalar_type() == at::kBFloat16 && bdr->dim() == 4 && bdr->size(0) == Nb && bdr->size(1) == N &&
+                      bdr->size(2) * 2 == Ho && bdr->size(3) * 2 == Wo &&
+                      bdr->is_contiguous(at::MemoryFormat::ChannelsLast) && bdr->device() == dy.device(),
+                  "psd convn_bwd: mode 5 dr must be channels_last bf16 [Nb, N, Ho/2, Wo/2]");
+    } else {
+      like_out(*bdr, "dr");
+    }
     TORCH_CHECK(bmbits.has_value() && bmbits->defined() && bmbits->scalar_type() == at::kByte &&
                     bmbits->numel() == M * N / 8 && bmbits->is_contiguous(),
                 "psd convn_bwd: mode 2 needs the uint8 [M*N/8] bit-mask");

@@ -141,6 +141,8 @@ struct Geo {
 // convolution and the identity residual). The stored output is then g = mask (dX [+ dr]) -- the
 // masked gradient the BN's elementwise pass consumes and, for 2, the residual gradient handed on --
 // and the partials are sum g and sum g (x - mean) per channel (the layout of bn_bwd_reduce_kernel).
+// 5: as 2 with dr the stride-2 downsample convolution's bwd-data on the quarter grid (added at even
+// (h, w) only: the zero-filled full-size gradient is never written).
 // 3: as 2 for a bottleneck tail relu(bn3(x) + bnd(xd)) (the downsample block's dual BN, whose
 // upstream gradient g is shared): part_d also receives sum g and sum g (xd - mean_d) for bnd.
 template <int BM, int BN, int WNT, int NSLOT, bool STATS, int BWD = 0>
@@ -358,7 +360,20 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
           load8_bf16(a.bx + (int64_t)m * a.N + my_col, xv);
           if constexpr (BWD >= 2) {
             float rv[8];
-            load8_bf16(a.bdr + (int64_t)m * a.N + my_col, rv);
+            if constexpr (BWD == 5) {
+              // residual-branch gradient of a stride-2 1x1 (downsample) convolution, on the quarter
+              // grid: non-zero only at even (h, w) of this (Ho x Wo) output grid
+              const int hw = a.Ho * a.Wo, n = m / hw, rem = m - n * hw, h = rem / a.Wo, w = rem - h * a.Wo;
+              if (((h | w) & 1) == 0) {
+                const int64_t q = ((int64_t)n * (a.Ho >> 1) + (h >> 1)) * (a.Wo >> 1) + (w >> 1);
+                load8_bf16(a.bdr + q * a.N + my_col, rv);
+              } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) rv[e] = 0.f;
+              }
+            } else {
+              load8_bf16(a.bdr + (int64_t)m * a.N + my_col, rv);
+            }
             const uint32_t bits = a.bmbits[((int64_t)m * a.N + my_col) >> 3];
 #pragma unroll
             for (int e = 0; e < 8; ++e) d[e] = ((bits >> e) & 1u) ? d[e] + rv[e] : 0.f;
@@ -447,6 +462,7 @@ static hipError_t convn_launch_s(const ConvnArgs& a, hipStream_t st) {
   if (a.bwd == 1) return convn_launch_t<BM, BN, WNT, NSLOT, false, 1>(a, st);
   if (a.bwd == 2) return convn_launch_t<BM, BN, WNT, NSLOT, false, 2>(a, st);
   if (a.bwd == 3) return convn_launch_t<BM, BN, WNT, NSLOT, false, 3>(a, st);
+  if (a.bwd == 5) return convn_launch_t<BM, BN, WNT, NSLOT, false, 5>(a, st);
   return a.part ? convn_launch_t<BM, BN, WNT, NSLOT, true, 0>(a, st)
                 : convn_launch_t<BM, BN, WNT, NSLOT, false, 0>(a, st);
 }
@@ -504,8 +520,9 @@ hipError_t launch_convn(const ConvnArgs& a_in, hipStream_t st) {
                   (a.bwd == 0 ? (!a.part || a.shift)
                               : (a.part && a.bx && a.bmean && a.ldc == a.N &&
                                  (a.bwd == 1 ? a.bss != nullptr
-                                             : ((a.bwd == 2 || a.bwd == 3) && a.bdr && a.bmbits &&
-                                                (a.bwd == 2 || (a.bxd && a.bmean_d && a.part_d))))));
+                                             : ((a.bwd == 2 || a.bwd == 3 || a.bwd == 5) && a.bdr && a.bmbits &&
+                                                (a.bwd != 3 || (a.bxd && a.bmean_d && a.part_d)) &&
+                                                (a.bwd != 5 || (a.Ho % 2 == 0 && a.Wo % 2 == 0))))));
   if (!ok) return hipErrorNotSupported;
   const int v = a.variant >= 0 ? a.variant : default_variant(a, bn);
   switch (bn) {

@@ -36,7 +36,11 @@ class _Fork(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_main, g_ds):
+        if g_ds is not None and g_ds.dim() > 0 and all(st == 0 for st in g_ds.stride()):
+            g_ds = None  # the downsample conv queued its quarter-grid gradient itself (ops/conv.py)
         if g_main is None or g_ds is None:
+            if g_main is None and g_ds is None:
+                return None, None
             return (g_ds if g_main is None else g_main), None
         ctx.bn._psd_pending_dr.append(g_ds)
         return g_main, None
@@ -89,15 +93,24 @@ class Bottleneck(nn.Module):
         gradient of ``x`` -- the identity residual's, or the downsample conv's -- is then handed to
         it inside the BN kernels (no autograd add over the activation)."""
         xm = xd = x
+        forked = False
         if (self.downsample is not None and prev_bn is not None and self.fuse_residual_grad
                 and torch.is_grad_enabled() and x.requires_grad and prev_bn.training and x.is_cuda
                 and x.dtype == torch.bfloat16):  # (the fused BN kernels that consume the hand-over)
             xm, xd = _Fork.apply(x, prev_bn)  # downsample-branch gradient -> prev_bn's kernels
+            forked = True
         if self.downsample is not None and self.fuse_residual_grad and len(self.downsample) == 2:
-            # relu(bn3(conv3) + bn_ds(conv_ds)): the downsample BN is applied inside bn3's apply pass
+            # relu(bn3(conv3) + bn_ds(conv_ds)): the downsample BN is applied inside bn3's apply pass.
+            # The downsample conv runs last: autograd then runs its backward before conv1's, so a
+            # stride-2 one can queue its quarter-grid input gradient for conv1's bwd-data epilogue
+            # (ops/conv.py _strided_dgrad, kernels/convn.hip mode 5)
+            to = prev_bn if forked and isinstance(prev_bn, FusedBatchNorm2d) else None
+            # conv1's bwd-data may then run prev_bn's backward reduction with that gradient added
+            object.__setattr__(self.conv1, "_psd_bn_in", to if self.fuse_residual_grad else None)
+            y3 = self.conv3(self.bn2(self.conv2(self.bn1(self.conv1(xm)))))
+            object.__setattr__(self.downsample[0], "_psd_strided_to", to)
             r = self.downsample[0](xd)
-            out = self.bn2(self.conv2(self.bn1(self.conv1(xm))))
-            return bn_add_bn_relu(self.bn3, self.conv3(out), self.downsample[1], r)
+            return bn_add_bn_relu(self.bn3, y3, self.downsample[1], r)
         idt = x if self.downsample is None else self.downsample(xd)
         # identity block: x (prev_bn's output) feeds conv1 and the residual, whose gradient is handed
         # to prev_bn -- conv1's bwd-data can run prev_bn's backward reduction

@@ -67,6 +67,28 @@ def _q8_hand_over(mod, y: torch.Tensor, kw: dict) -> None:
         mod._psd_q8_consumer._psd_q8_pending = (y, kw["q8_out"], kw["q8_sinv"])
 
 
+class StridedDr:
+    """A residual-branch gradient handed to a BN (``_psd_pending_dr``) by a stride-2 1x1 (downsample)
+    convolution, kept on its quarter grid: ``t4`` = dY . W of the strided positions, [N, C, H/2, W/2]
+    channels_last. The full-size gradient is zero except at even (h, w); the consumer convolution's
+    bwd-data epilogue adds it there (kernels/convn.hip bwd mode 5) and only other consumers build the
+    full tensor (``full``)."""
+
+    def __init__(self, t4: torch.Tensor, H: int, W: int):
+        self.t4, self.H, self.W = t4, H, W
+
+    def full(self) -> torch.Tensor:
+        n, c = self.t4.shape[:2]
+        out = torch.zeros(n, self.H, self.W, c, device=self.t4.device, dtype=self.t4.dtype).permute(0, 3, 1, 2)
+        out[:, :, ::2, ::2] = self.t4
+        return out
+
+
+def take_dr(t):
+    """A pending residual gradient as a full-size tensor (StridedDr materialised)."""
+    return t.full() if isinstance(t, StridedDr) else t
+
+
 def _fold_target(mod, x: torch.Tensor):
     """The 1x1 convolution whose output ``x`` this BN consumed and whose backward can take the BN's
     input gradient folded (ops/conv.py _fold_backward, kernels/bnfold.hip), or None. The convolution
@@ -132,7 +154,7 @@ class _FusedBNFn(torch.autograd.Function):
                 g, coef, dg, db = native().bn_bwd_coef(pre[0], x, w, mean, invstd, part=pre[1], rows=pre[2],
                                                        dgamma_out=dgo, dbeta_out=dbo)
             else:
-                dy2 = mod._psd_pending_dr.pop() if getattr(mod, "_psd_pending_dr", None) else None
+                dy2 = take_dr(mod._psd_pending_dr.pop()) if getattr(mod, "_psd_pending_dr", None) else None
                 g, coef, dg, db = native().bn_bwd_coef(dy, x, w, mean, invstd, mbits=mbits, dy2=dy2, dgamma_out=dgo,
                                                        dbeta_out=dbo)
             _hand_fold(conv, g, coef, x)
@@ -157,7 +179,7 @@ class _FusedBNFn(torch.autograd.Function):
             return dx, (dg if w is not None else None), (db if w is not None else None), res_grad, None, None
         # residual-branch fusion: the identity-path gradient of this BN's output was stashed by the
         # next block's bn3 backward; fold it in here instead of an autograd add kernel
-        dy2 = mod._psd_pending_dr.pop() if getattr(mod, "_psd_pending_dr", None) else None
+        dy2 = take_dr(mod._psd_pending_dr.pop()) if getattr(mod, "_psd_pending_dr", None) else None
         dx, dr, dg, db = native().bn_bwd(dy, x, None, w, mean, invstd, ctx.relu, ctx.has_res, dgo, dbo, dy2, ss,
                                          mbits)
         res_grad = None
@@ -222,7 +244,7 @@ class _BNAddBNReluFn(torch.autograd.Function):
                 _hand_fold(conv, g, coef, x)
                 return g, dg3, db3, drr, dgd, dbd, None, None
             return dx, dg3, db3, drr, dgd, dbd, None, None
-        dy2 = bn3._psd_pending_dr.pop() if getattr(bn3, "_psd_pending_dr", None) else None
+        dy2 = take_dr(bn3._psd_pending_dr.pop()) if getattr(bn3, "_psd_pending_dr", None) else None
         if conv is not None:  # bn3's input gradient folded into conv3's backward (see _FusedBNFn)
             _, drr, dg3, db3, dgd, dbd, coef, g = C.bn_bwd_dual(dy, x, w3, mean, invstd, mbits, dy2, r, wd, mean_d,
                                                                 invstd_d, dg3o, db3o, dgdo, dbdo, fold=True)

@@ -37,6 +37,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import autotune as _at
+from .bn import StridedDr, take_dr
 
 
 def _enabled() -> bool:
@@ -174,6 +175,10 @@ def _bn_bwd_fusion(mod, x: torch.Tensor):
     if mbits is not None:
         if not bn._psd_pending_dr:
             return None
+        if isinstance(bn._psd_pending_dr[-1], StridedDr):  # a downsample conv's quarter-grid gradient
+            if xd is not None or x.shape[2] % 2 or x.shape[3] % 2 or not _at.enabled("PSD_CONVN_BWD5"):
+                return None
+            return dict(mode=5, bn=bn, bx=bx, mean=mean, mbits=mbits)
         if xd is not None:  # a downsample block's dual tail: both BNs' reductions (mode 3)
             if not _at.enabled("PSD_CONVN_BWD3"):
                 return None
@@ -197,7 +202,7 @@ def _convn_bwd_variants(dy, w2, k: int, pad: int, fu: dict, dr) -> dict:
             part = torch.empty(C.convn_stats_rows(M), 2, cout, device=dy.device, dtype=torch.float32)
             part_d = torch.empty_like(part) if fu["mode"] == 3 else None
             rows = C.convn_bwd_(dy, w2, out, k, k, 1, pad, part, v, fu["mode"], fu["bx"], fu["mean"],
-                                bss=fu.get("ss"), bdr=dr, bmbits=fu.get("mbits"), bxd=fu.get("bxd"),
+                                bss=fu.get("ss"), bdr=_dr_arg(dr), bmbits=fu.get("mbits"), bxd=fu.get("bxd"),
                                 bmean_d=fu.get("mean_d"), part_d=part_d)
             if rows == 0:
                 raise RuntimeError("convn_bwd_ declined a shape _psdn_ok accepted")
@@ -238,13 +243,19 @@ def _with_bn_reduce(fn, bn):
 def _with_bn_bwd_reduce(fn, fu):
     """Timing twin of an unfused bwd-data candidate: its output plus the BN backward reduction it
     leaves to the BN -- the same pass the BN then runs (mask from x and scale/shift, or the residual
-    BN's bit-mask with the handed-over residual gradient folded in and dr written)."""
+    BN's bit-mask with the handed-over residual gradient folded in and dr written; a quarter-grid
+    downsample gradient is materialised first, as the BN then does)."""
     def g():
         dx = fn()
-        _native().bn_bwd_reduce_(dx, fu["bx"], fu["mean"], ss=fu.get("ss"), dy2=fu.get("dr"),
+        _native().bn_bwd_reduce_(dx, fu["bx"], fu["mean"], ss=fu.get("ss"), dy2=take_dr(fu.get("dr")),
                                  mbits=fu.get("mbits"))
         return dx
     return g
+
+
+def _dr_arg(dr):
+    """The convn_bwd_ dr operand: a quarter-grid StridedDr's tensor (mode 5) or the full gradient."""
+    return dr.t4 if isinstance(dr, StridedDr) else dr
 
 
 def _route(key: tuple, cands: dict, default: str, bn=None) -> str:
@@ -386,7 +397,7 @@ def _fold_backward(ctx, fold, x, weight, need_x: bool, need_w: bool):
                 part = torch.empty(C.convn_stats_rows(M), 2, cin, device=g.device, dtype=torch.float32)
                 part_d = torch.empty_like(part) if fu["mode"] == 3 else None
                 rows = C.convn_bwd_(g, w2, out, 1, 1, 1, 0, part, v, fu["mode"], fu["bx"], fu["mean"],
-                                    bss=fu.get("ss"), bdr=fu.get("dr"), bmbits=fu.get("mbits"), x2=x, bias=bvec,
+                                    bss=fu.get("ss"), bdr=_dr_arg(fu.get("dr")), bmbits=fu.get("mbits"), x2=x, bias=bvec,
                                     bxd=fu.get("bxd"), bmean_d=fu.get("mean_d"), part_d=part_d)
             else:
                 rows = C.convn_(g, w2, out, 1, 1, 1, 0, variant=v, x2=x, bias=bvec)
@@ -662,6 +673,31 @@ def _igemm_fp8(x: torch.Tensor, w2: torch.Tensor, k: int, stride: int, pad: int,
     return _from_2d(out, n, ho, wo)
 
 
+def _strided_dgrad(mod, dy, weight, to, H: int, W: int):
+    """bwd-data of a stride-2 1x1 convolution kept on the quarter grid: t4 = dY . W ([N, Cin, H/2,
+    W/2]), queued on ``to`` (the BN that produced the input) as a StridedDr; returns the zero-stride
+    marker autograd passes to the block's _Fork (which then queues nothing itself)."""
+    n, cout, ho, wo = dy.shape
+    cin = weight.shape[1]
+    M4 = n * ho * wo
+    w2 = weight.reshape(cout, cin)
+    dy2 = _as_2d(dy)
+
+    def gemm():
+        return _from_2d(torch.mm(dy2, w2), n, ho, wo)
+
+    cands = {"gemm": gemm}
+    if _psdn_ok(cout, cin):
+        cands.update(_convn_variants(dy, w2.t().contiguous(), 1, 1, 0))
+    t4 = cands[_choose(("dgrad_s2", M4, cin, cout), cands)]()
+    if not t4.is_contiguous(memory_format=torch.channels_last):
+        t4 = t4.contiguous(memory_format=torch.channels_last)
+    to._psd_pending_dr.append(StridedDr(t4, H, W))
+    marker = torch.zeros((), device=dy.device, dtype=dy.dtype).expand(n, cin, H, W)
+    mod._psd_strided_marker = marker
+    return marker
+
+
 class _ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, stride, pad, f8=None, mod=None):
@@ -715,7 +751,14 @@ class _ConvFn(torch.autograd.Function):
         conv_bwd = torch.ops.aten.convolution_backward
         args = (None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1)
         dx = dw = None
-        if ctx.needs_input_grad[0]:
+        to = getattr(ctx.mod, "_psd_strided_to", None) if ctx.mod is not None else None
+        if (ctx.needs_input_grad[0] and to is not None and k == 1 and stride == 2 and pad == 0 and h % 2 == 0
+                and w % 2 == 0 and _at.enabled("PSD_CONVN_BWD5") and not ctx.fp8):
+            # downsample conv whose input gradient goes to the producing BN (the block's _Fork): dY . W
+            # on the quarter grid only, handed over as a StridedDr (the consumer convolution's bwd-data
+            # adds it at even pixels, kernels/convn.hip mode 5); autograd gets a zero-stride marker
+            dx = _strided_dgrad(ctx.mod, dy, weight, to, h, w)
+        if ctx.needs_input_grad[0] and dx is None:
             def miopen():
                 return conv_bwd(dy, x, weight, *args, [True, False, False])[0]
 

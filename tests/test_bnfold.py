@@ -202,7 +202,7 @@ def test_convw_fold_rows_contract(gpu):
     assert native().convw_fold_rows(2048, 512) == 0
 
 
-def _chain_grads(gpu, monkeypatch, mode: str):
+def _chain_grads(gpu, monkeypatch, mode: str, kind: str = "ds_id"):
     """A downsample block feeding an identity block (the pattern of every layer's first two
     blocks): mode 'fused' (every narrow-kernel fusion forced: the identity block's conv1 bwd-data
     reduces the downsample block's dual-BN tail -- convn mode 3 -- and both bn3s fold), 'library'
@@ -218,8 +218,14 @@ def _chain_grads(gpu, monkeypatch, mode: str):
     monkeypatch.setenv("PSD_AUTOTUNE_FORCE", "psdnb0,psdnf0,psdn0" if mode == "fused" else "miopen")
     autotune._DECISIONS.clear()
     torch.manual_seed(2)
-    a = Bottleneck(64, 64, downsample=nn.Sequential(_conv(64, 256, 1), FusedBatchNorm2d(256)))
-    b = Bottleneck(256, 64)
+    if kind == "ds_id":  # downsample block -> identity block (convn mode 3 on the dual tail)
+        a = Bottleneck(64, 64, downsample=nn.Sequential(_conv(64, 256, 1), FusedBatchNorm2d(256)))
+        b = Bottleneck(256, 64)
+        cin = 64
+    else:  # identity block -> stride-2 downsample block (mode 5: the quarter-grid downsample gradient)
+        a = Bottleneck(256, 64)
+        b = Bottleneck(256, 128, stride=2, downsample=nn.Sequential(_conv(256, 512, 1, 2), FusedBatchNorm2d(512)))
+        cin = 256
     g = torch.Generator().manual_seed(4)
     blocks = nn.ModuleList([a, b])
     for mod in blocks.modules():
@@ -234,7 +240,7 @@ def _chain_grads(gpu, monkeypatch, mode: str):
         p.data = p.data.to(torch.bfloat16).to(dt)
         if p.dim() == 4:
             p.data = p.data.contiguous(memory_format=CL)
-    x = torch.randn(8, 64, 28, 28, generator=g).to(torch.bfloat16).to(gpu, dt).contiguous(memory_format=CL)
+    x = torch.randn(8, cin, 28, 28, generator=g).to(torch.bfloat16).to(gpu, dt).contiguous(memory_format=CL)
     x.requires_grad_(True)
     y = b(a(x), a.bn3)
     gy = torch.randn(y.shape, generator=torch.Generator().manual_seed(6)).to(torch.bfloat16).to(gpu, dt)
@@ -246,14 +252,18 @@ def _chain_grads(gpu, monkeypatch, mode: str):
     return out, picks
 
 
-def test_chain_fusions_vs_fp32(gpu, monkeypatch):
-    """Downsample block -> identity block with every fusion (convn mode 3 on the dual tail, both
-    bn3 folds) vs the library path, both against fp32: the fused path's error stays at the library
-    path's bf16 level, parameter by parameter."""
-    gf, picks = _chain_grads(gpu, monkeypatch, "fused")
+@pytest.mark.parametrize("kind", ["ds_id", "id_ds"])
+def test_chain_fusions_vs_fp32(gpu, monkeypatch, kind):
+    """Two chained blocks with every fusion (ds_id: convn mode 3 on the downsample block's dual
+    tail; id_ds: mode 5, the stride-2 downsample conv's quarter-grid input gradient added in conv1's
+    bwd-data epilogue; both bn3 folds) vs the library path, both against fp32: the fused path's
+    error stays at the library path's bf16 level, parameter by parameter."""
+    gf, picks = _chain_grads(gpu, monkeypatch, "fused", kind)
     assert any(k[1] == "dgrad" and v.startswith("psdnb") for k, v in picks.items() if len(k) > 1), picks
-    gl, _ = _chain_grads(gpu, monkeypatch, "library")
-    gr, _ = _chain_grads(gpu, monkeypatch, "fp32")
+    if kind == "id_ds":
+        assert any(k[1] == "dgrad_s2" for k in picks if len(k) > 1), picks
+    gl, _ = _chain_grads(gpu, monkeypatch, "library", kind)
+    gr, _ = _chain_grads(gpu, monkeypatch, "fp32", kind)
     ef, el = _rel(gf, gr), _rel(gl, gr)
     print({n: (round(ef[n], 4), round(el[n], 4)) for n in ef})
     for n in ef:
