@@ -213,14 +213,14 @@ def main():
             except Exception as e:  # noqa: BLE001 -- a diagnostic must not cost the run
                 bucket_probe = {"error": str(e)[:200]}
     pull_dtype = a.pull_dtype or ("fp8" if a.model.startswith("wide") else "bf16")
-    mode = a.ps_mode if pull_dtype == "bf16" else "collective"  # fp8-published weights: collective plane
+    mode = a.ps_mode  # both planes publish MX e4m3 weights for the fp8 config
     fallback = None
     if mode == "async":
         from parameter_server_distributed_amd.parallel.async_ps import AsyncPS
 
         try:
             ps = AsyncPS(spec.model, optim, num_shards=shards, staleness=a.staleness, bucket_mb=a.bucket_mb,
-                         device=dev, overlap=not spec.tied_weights, **kw)
+                         device=dev, overlap=not spec.tied_weights, pull_dtype=pull_dtype, **kw)
         except RuntimeError as e:  # collective on every rank (AsyncPS._agree): fall back together
             fallback = str(e)[:300]
             mode = "collective"
@@ -337,7 +337,8 @@ def main():
             "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": (round(value / (REF_BASELINE[a.model] * n_workers), 2)
                             if a.model in REF_BASELINE else None),
-            "dtype": "fp8-e4m3 fwd convs / bf16" if fp8_compute else "bf16", "data": data,
+            "dtype": (("fp8 convs (MX e4m3 fwd, MX e5m2-dY bwd-data), bf16 rest" if os.environ.get("PSD_FP8_MX", "1") != "0"
+                       else "fp8-e4m3 fwd convs / bf16") if fp8_compute else "bf16"), "data": data,
             "config": {"model": a.model, "global_batch": a.batch * n_workers, "per_gpu_batch": a.batch,
                        "seq_len": a.seq_len if a.model.startswith("bert") else None,
                        "image_size": None if a.model.startswith("bert") else a.image_size,

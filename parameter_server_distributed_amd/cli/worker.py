@@ -134,7 +134,8 @@ def elastic_main(a) -> int:
         shards = a.ps_shards if 0 < a.ps_shards <= transport.world else transport.world
         if a.ps_plane == "async":
             return AsyncPS(model, optim, num_shards=shards, staleness=a.staleness, bucket_mb=a.bucket_mb, device=dev,
-                           overlap=not spec.tied_weights, param_dtype=dtype)
+                           overlap=not spec.tied_weights, param_dtype=dtype,
+                           pull_dtype=a.pull_dtype if dev.type == "cuda" else "bf16")
         return CollectivePS(model, optim, transport, num_shards=shards, staleness=a.staleness,
                             bucket_mb=a.bucket_mb, device=dev, overlap=not spec.tied_weights,
                             grad_dtype=dtype, param_dtype=dtype, pull_dtype=a.pull_dtype)

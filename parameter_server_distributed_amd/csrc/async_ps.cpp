@@ -14,6 +14,7 @@
 #include <cstring>
 #include <sstream>
 
+#include "kernels/launchers.h"
 #include "ops.h"
 
 namespace psd {
@@ -102,7 +103,7 @@ void* map_shm(const std::string& name, size_t bytes, bool create) {
 
 AsyncEngine::AsyncEngine(int rank, int world, std::vector<int> owners, std::vector<int> workers,
                          std::vector<int64_t> shard_off, std::vector<int64_t> shard_len, int staleness, int nbuf,
-                         std::string shm_name, bool create, int device, double timeout_s, int elem_bytes)
+                         std::string shm_name, bool create, int device, double timeout_s, int elem_bytes, bool mx)
     : rank_(rank),
       world_(world),
       S_(staleness),
@@ -110,6 +111,7 @@ AsyncEngine::AsyncEngine(int rank, int world, std::vector<int> owners, std::vect
       device_(device),
       timeout_s_(timeout_s),
       esz_(elem_bytes),
+      mx_(mx),
       owners_(std::move(owners)),
       workers_(std::move(workers)),
       shard_off_(std::move(shard_off)),
@@ -120,6 +122,12 @@ AsyncEngine::AsyncEngine(int rank, int world, std::vector<int> owners, std::vect
   TORCH_CHECK(P >= 1 && P <= kMaxShards, "psd async: 1..", kMaxShards, " shards");
   TORCH_CHECK(W >= 1 && W <= kMaxWorkers, "psd async: 1..", kMaxWorkers, " workers");
   TORCH_CHECK(S_ >= 0 && S_ + 1 <= kRing, "psd async: staleness bound must be in [0, ", kRing - 1, "]");
+  if (mx_) {
+    TORCH_CHECK(device >= 0 && esz_ == 2, "psd async: the MX fp8 publish needs a GPU engine with bf16 weights");
+    for (int k = 0; k < P; ++k)
+      TORCH_CHECK(shard_off_[k] % 32 == 0 && shard_len_[k] % 32 == 0,
+                  "psd async: MX shards must be 32-element aligned");
+  }
   TORCH_CHECK(nbuf_ >= 2 && nbuf_ <= kMaxBuf, "psd async: 2..", kMaxBuf, " publish buffers");
   TORCH_CHECK(esz_ == 2 || esz_ == 4, "psd async: bf16 (2) or fp32 (4) elements");
   TORCH_CHECK(world_ >= 1 && world_ <= kMaxRanks, "psd async: 1..", kMaxRanks, " ranks");
@@ -242,18 +250,30 @@ int AsyncEngine::worker_index(int rank) const {
   return -1;
 }
 
+// A shard's region: W * (S + 1) inbox slots, then nbuf publish slots; with MX a publish slot also
+// holds the e4m3 copy of the snapshot and its E8M0 scales (one per 32 elements) after the bf16 one.
+int64_t AsyncEngine::pub_slot_bytes(int shard) const {
+  const int64_t sb = round_up(shard_len_[shard] * esz_, kAlignBytes);
+  if (!mx_) return sb;
+  return sb + round_up(shard_len_[shard], kAlignBytes) + round_up(shard_len_[shard] / 32, kAlignBytes);
+}
+
+int64_t AsyncEngine::shard_region_bytes(int shard) const {
+  return (int64_t)workers_.size() * (S_ + 1) * round_up(shard_len_[shard] * esz_, kAlignBytes) +
+         nbuf_ * pub_slot_bytes(shard);
+}
+
 int64_t AsyncEngine::region_bytes_for(int rank) const {
   int64_t b = 0;
   for (size_t k = 0; k < owners_.size(); ++k)
-    if (owners_[k] == rank)
-      b += ((int64_t)workers_.size() * (S_ + 1) + nbuf_) * round_up(shard_len_[k] * esz_, kAlignBytes);
+    if (owners_[k] == rank) b += shard_region_bytes((int)k);
   return b;
 }
 
 int64_t AsyncEngine::shard_base(int rank, int shard) const {
   int64_t b = 0;
   for (int k = 0; k < shard; ++k)
-    if (owners_[k] == rank) b += ((int64_t)workers_.size() * (S_ + 1) + nbuf_) * round_up(shard_len_[k] * esz_, kAlignBytes);
+    if (owners_[k] == rank) b += shard_region_bytes(k);
   return b;
 }
 
@@ -268,7 +288,23 @@ char* AsyncEngine::publish_ptr(int shard, int buf) const {
   const int o = owners_[shard];
   TORCH_CHECK(peer_base_[o], "psd async: rank ", o, " memory not attached");
   const int64_t sb = round_up(shard_len_[shard] * esz_, kAlignBytes);
-  return peer_base_[o] + shard_base(o, shard) + ((int64_t)workers_.size() * (S_ + 1) + buf) * sb;
+  return peer_base_[o] + shard_base(o, shard) + (int64_t)workers_.size() * (S_ + 1) * sb + buf * pub_slot_bytes(shard);
+}
+
+char* AsyncEngine::publish_q_ptr(int shard, int buf) const {
+  return publish_ptr(shard, buf) + round_up(shard_len_[shard] * esz_, kAlignBytes);
+}
+
+char* AsyncEngine::publish_sc_ptr(int shard, int buf) const {
+  return publish_q_ptr(shard, buf) + round_up(shard_len_[shard], kAlignBytes);
+}
+
+// the MX e4m3 copy (+ E8M0 scales) of the fp32 master into publish slot `buf` (kernels/fp8.hip)
+void AsyncEngine::quant_publish(ShardState& st, int shard, int buf, void* stream) {
+  hip_ok(launch_quant_mx(st.master.data_ptr(), DT_F32, shard_len_[shard], 0,
+                         reinterpret_cast<uint8_t*>(publish_q_ptr(shard, buf)),
+                         reinterpret_cast<uint8_t*>(publish_sc_ptr(shard, buf)), static_cast<hipStream_t>(stream)),
+         "launch_quant_mx(publish)");
 }
 
 // ------------------------------------------------------------------ memory exchange
@@ -332,6 +368,7 @@ void AsyncEngine::publish_initial(int shard, int64_t version, std::vector<int64_
   TORCH_CHECK(version >= 0 && (clocks.empty() || clocks.size() == workers_.size()),
               "psd async: publish_initial takes a version >= 0 and one clock per worker");
   st.publish[0].copy_(st.master);
+  if (mx_) quant_publish(st, shard, 0, c10::hip::getCurrentHIPStream((c10::DeviceIndex)device_).stream());
   if (device_ >= 0) hip_ok(hipDeviceSynchronize(), "hipDeviceSynchronize");
   ShardCtl& s = ctl_->shard[shard];
   s.buf_version[0].store(version);
@@ -481,6 +518,7 @@ bool AsyncEngine::poll_once() {
         c10::hip::HIPStreamGuard sg(c10::hip::getStreamFromExternal(static_cast<hipStream_t>(ps_stream_),
                                                                     (c10::DeviceIndex)device_));
         apply_into(st, g, buf);
+        if (mx_) quant_publish(st, k, buf, ps_stream_);
         hip_ok(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
         hip_ok(hipEventRecord(ev, static_cast<hipStream_t>(ps_stream_)), "hipEventRecord");
       } else {
@@ -579,8 +617,21 @@ void AsyncEngine::fail(const std::string& msg) {
 }
 
 std::vector<int64_t> AsyncEngine::pull(int64_t step, at::Tensor params_flat, int64_t stream) {
-  TORCH_CHECK(my_wi_ >= 0, "psd async: rank ", rank_, " is not a worker");
   TORCH_CHECK(params_flat.is_contiguous() && params_flat.element_size() == esz_, "psd async: working buffer dtype");
+  return pull_impl(step, static_cast<char*>(params_flat.data_ptr()), nullptr, stream);
+}
+
+// the MX e4m3 snapshot (1 byte / parameter + 1 / 32) instead of the bf16 one (kernels/fp8.hip scales)
+std::vector<int64_t> AsyncEngine::pull_mx(int64_t step, at::Tensor q_flat, at::Tensor sc_flat, int64_t stream) {
+  TORCH_CHECK(mx_, "psd async: pull_mx on an engine without the MX publish");
+  TORCH_CHECK(q_flat.is_contiguous() && q_flat.element_size() == 1 && sc_flat.is_contiguous() &&
+                  sc_flat.element_size() == 1 && sc_flat.numel() * 32 == q_flat.numel(),
+              "psd async: pull_mx buffers (1-byte q [n], 1-byte scales [n / 32])");
+  return pull_impl(step, static_cast<char*>(q_flat.data_ptr()), static_cast<char*>(sc_flat.data_ptr()), stream);
+}
+
+std::vector<int64_t> AsyncEngine::pull_impl(int64_t step, char* dst, char* dst_sc, int64_t stream) {
+  TORCH_CHECK(my_wi_ >= 0, "psd async: rank ", rank_, " is not a worker");
   const double t0 = now_s();
   const int64_t need = step - S_;
   const int P = (int)owners_.size(), W = (int)workers_.size();
@@ -605,7 +656,6 @@ std::vector<int64_t> AsyncEngine::pull(int64_t step, at::Tensor params_flat, int
   }
   wait_us_.fetch_add((int64_t)((now_s() - t0) * 1e6));
   std::vector<int64_t> pulled(P);
-  char* dst = static_cast<char*>(params_flat.data_ptr());
   for (int k = 0; k < P; ++k) {
     ShardCtl& s = ctl_->shard[k];
     int b;
@@ -616,7 +666,12 @@ std::vector<int64_t> AsyncEngine::pull(int64_t step, at::Tensor params_flat, int
       s.readers[b].fetch_sub(1);
     }
     pulled[k] = s.buf_version[b].load();
-    copy(dst + shard_off_[k] * esz_, publish_ptr(k, b), shard_len_[k] * esz_, reinterpret_cast<void*>(stream));
+    if (dst_sc) {
+      copy(dst + shard_off_[k], publish_q_ptr(k, b), shard_len_[k], reinterpret_cast<void*>(stream));
+      copy(dst_sc + shard_off_[k] / 32, publish_sc_ptr(k, b), shard_len_[k] / 32, reinterpret_cast<void*>(stream));
+    } else {
+      copy(dst + shard_off_[k] * esz_, publish_ptr(k, b), shard_len_[k] * esz_, reinterpret_cast<void*>(stream));
+    }
     std::atomic<int32_t>* rd = &s.readers[b];
     defer(reinterpret_cast<void*>(stream), [rd] { rd->fetch_sub(1); });
   }

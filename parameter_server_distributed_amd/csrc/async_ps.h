@@ -55,7 +55,7 @@ class AsyncEngine {
  public:
   AsyncEngine(int rank, int world, std::vector<int> owners, std::vector<int> workers, std::vector<int64_t> shard_off,
               std::vector<int64_t> shard_len, int staleness, int nbuf, std::string shm_name, bool create, int device,
-              double timeout_s, int elem_bytes = 2);
+              double timeout_s, int elem_bytes = 2, bool mx = false);
   ~AsyncEngine();
 
   // -- memory exchange (collective through the caller's store) --
@@ -79,6 +79,8 @@ class AsyncEngine {
 
   // -- worker side --
   std::vector<int64_t> pull(int64_t step, at::Tensor params_flat, int64_t stream);
+  // MX engines: the e4m3 snapshot + E8M0 scales into (q_flat, sc_flat) instead of the bf16 one
+  std::vector<int64_t> pull_mx(int64_t step, at::Tensor q_flat, at::Tensor sc_flat, int64_t stream);
   void push(int64_t step, const at::Tensor& grads_flat, int64_t lo, int64_t hi, int64_t stream);
   void commit(int64_t step, std::vector<int64_t> pulled, int64_t stream);
   void wait_applied(int64_t nsteps);  // this worker's pushes 0..nsteps-1 applied at every shard
@@ -126,8 +128,14 @@ class AsyncEngine {
     std::vector<RoundItem> round;     // pushes taken from the mailboxes, not yet applied
   };
 
+  void quant_publish(ShardState& st, int shard, int buf, void* stream);
   int64_t slot_elems(int shard) const { return shard_len_[shard]; }
   int64_t region_bytes_for(int rank) const;
+  int64_t pub_slot_bytes(int shard) const;
+  int64_t shard_region_bytes(int shard) const;
+  char* publish_q_ptr(int shard, int buf) const;
+  char* publish_sc_ptr(int shard, int buf) const;
+  std::vector<int64_t> pull_impl(int64_t step, char* dst, char* dst_sc, int64_t stream);
   int64_t shard_base(int rank, int shard) const;  // byte offset of shard's region in rank's allocation
   char* inbox_ptr(int shard, int wi, int slot) const;
   char* publish_ptr(int shard, int buf) const;
@@ -149,6 +157,7 @@ class AsyncEngine {
   double timeout_s_;
   double dead_after_s_ = 10.0;  // a peer's engine silent this long is presumed dead (PSD_ASYNC_DEAD_S)
   int esz_;
+  bool mx_ = false;  // MX fp8 publish: each publish slot also holds e4m3 + E8M0 scales of the snapshot
   std::vector<int> owners_, workers_, my_shards_;
   std::vector<int64_t> shard_off_, shard_len_;
   int my_wi_ = -1;

@@ -258,10 +258,10 @@ PYBIND11_MODULE(_C, m) {
   // ---- asynchronous apply-on-arrival PS over peer memory ----
   py::class_<AsyncEngine>(m, "AsyncEngine")
       .def(py::init<int, int, std::vector<int>, std::vector<int>, std::vector<int64_t>, std::vector<int64_t>, int, int,
-                    std::string, bool, int, double, int>(),
+                    std::string, bool, int, double, int, bool>(),
            py::arg("rank"), py::arg("world"), py::arg("owners"), py::arg("workers"), py::arg("shard_off"),
            py::arg("shard_len"), py::arg("staleness"), py::arg("nbuf"), py::arg("shm_name"), py::arg("create"),
-           py::arg("device"), py::arg("timeout_s"), py::arg("elem_bytes") = 2)
+           py::arg("device"), py::arg("timeout_s"), py::arg("elem_bytes") = 2, py::arg("mx") = false)
       .def("local_desc", [](const AsyncEngine& e) { return py::bytes(e.local_desc()); })
       .def("attach_peer", [](AsyncEngine& e, int r, py::bytes d) { e.attach_peer(r, std::string(d)); })
       .def("set_shard_state", &AsyncEngine::set_shard_state)
@@ -273,6 +273,7 @@ PYBIND11_MODULE(_C, m) {
       .def("close_peers", &AsyncEngine::close_peers)
       .def("free_local", &AsyncEngine::free_local)
       .def("pull", &AsyncEngine::pull, py::call_guard<py::gil_scoped_release>())
+      .def("pull_mx", &AsyncEngine::pull_mx, py::call_guard<py::gil_scoped_release>())
       .def("push", &AsyncEngine::push, py::call_guard<py::gil_scoped_release>())
       .def("commit", &AsyncEngine::commit, py::call_guard<py::gil_scoped_release>())
       .def("wait_applied", &AsyncEngine::wait_applied, py::call_guard<py::gil_scoped_release>())

@@ -39,8 +39,8 @@ def _q8_args(mod, x: torch.Tensor) -> dict:
     # measured on Wide-ResNet-101-2 b512: 3,589 / 3,584 img/s with the hand-over vs 3,606 without
     # (same box, one call): the extra fp8 convert in the apply pass costs what the saved read of y
     # gains, so it is opt-in (PSD_FP8_HANDOVER=1)
-    if os.environ.get("PSD_FP8_HANDOVER", "0") != "1":
-        return {}
+    if os.environ.get("PSD_FP8_HANDOVER", "0") != "1" or _at.enabled("PSD_FP8_MX"):
+        return {}  # (the hand-over writes per-tensor e4m3; MX operands are quantised by the consumer)
     sc = cons._f8[0]
     if sc.hist is None or sc.hist.device != x.device:
         return {}

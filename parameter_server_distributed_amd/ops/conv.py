@@ -95,6 +95,42 @@ def _q8(t2: torch.Tensor, e5m2: bool = False, scaler: "DelayedScale | None" = No
     return quantize_fp8(t2, e5m2=e5m2)
 
 
+FP8_CALLS = {"fwd": 0, "dgrad": 0, "ps_weights": 0}  # fp8 kernel launches by role (tests / logs)
+
+
+def _mx_on() -> bool:
+    """MX block scaling for every fp8 operand (``PSD_FP8_MX``, default on): one E8M0 scale per 32
+    contiguous K-elements (kernels/fp8.hip quant_mx_kernel; the block-scaled MFMA consumes the
+    scales), no amax pass and no scale history; 0: per-tensor scales (delayed for activations and
+    gradients, just-in-time for weights)."""
+    return _at.enabled("PSD_FP8_MX")
+
+
+def _q_act(t: torch.Tensor, e5m2: bool = False, scaler: "DelayedScale | None" = None):
+    """fp8 activation / output-gradient operand: MX (q, uint8 scales) or per-tensor (q, fp32 scale)."""
+    if _mx_on():
+        from . import quantize_mx
+
+        return quantize_mx(t, e5m2=e5m2)
+    return _q8(t, e5m2=e5m2, scaler=scaler)
+
+
+def _q_weight(mod, w2: torch.Tensor):
+    """fp8 forward weight operand [Cout, K]: the MX copy the PS data plane published with the
+    weights this step's forward uses (``_psd_w8``, parallel/collective_ps.py / async_ps.py: no
+    per-step weight quantisation), else quantised here."""
+    if _mx_on():
+        pub = getattr(mod, "_psd_w8", None) if mod is not None else None
+        got = pub(w2) if pub is not None else None
+        if got is not None:
+            FP8_CALLS["ps_weights"] += 1
+            return got
+        from . import quantize_mx
+
+        return quantize_mx(w2)
+    return _q8(w2)
+
+
 def _take_q8(mod, x: torch.Tensor):
     """The e4m3 copy of ``x`` that the producing BN's apply pass wrote for this module (ops/bn.py,
     delayed scaling with this module's activation scaler), as (q [N, C, H, W] channels_last,
@@ -464,14 +500,15 @@ class _Conv1x1Fn(torch.autograd.Function):
         if fp8 and _fp8_ok(cin, cout):
             # fp8 forward: e4m3 operands on the MX-scaled MFMA (2x the bf16 rate), dequantised in the
             # epilogue; the weight gradient runs on the saved bf16 x and W
-            got = _take_q8(mod, x)
+            got = None if _mx_on() else _take_q8(mod, x)
             if got is not None:  # quantised by the producing BN's apply pass
                 xq, sx = got[0].permute(0, 2, 3, 1).reshape(n * h * w, cin), got[1]
             else:
-                xq, sx = _q8(x2, scaler=f8[0])
-            wq, sw = _q8(w2)
+                xq, sx = _q_act(x2, scaler=f8[0])
+            wq, sw = _q_weight(mod, w2)
             out = torch.empty(n * h * w, cout, device=x.device, dtype=x.dtype)
             _native().gemm_fp8_(xq, wq, sx, sw, out)
+            FP8_CALLS["fwd"] += 1
             return _from_2d(out, n, h, w)
         key = ("fwd", n * h * w, cin, cout)
 
@@ -522,10 +559,11 @@ class _Conv1x1Fn(torch.autograd.Function):
         args = (None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1)
         if need_x and ctx.fp8 and _fp8_ok(cout, cin) and _at.enabled("PSD_FP8_DGRAD"):
             # fp8 bwd-data: e5m2 dY (K-major [M, cout]) x e4m3 W^T ([cin, cout], K-major)
-            dyq, sdy = _q8(_as_2d(dy), e5m2=True, scaler=ctx.f8[1])
-            wtq, swt = _q8(weight.reshape(cout, cin).t().contiguous())
+            dyq, sdy = _q_act(_as_2d(dy), e5m2=True, scaler=ctx.f8[1])
+            wtq, swt = _q_act(weight.reshape(cout, cin).t().contiguous())
             out = torch.empty(n * h * w, cin, device=dy.device, dtype=dy.dtype)
             _native().gemm_fp8_(dyq, wtq, sdy, swt, out)
+            FP8_CALLS["dgrad"] += 1
             dx = _from_2d(out, n, h, w)
             need_x = False
         if need_x:
@@ -654,7 +692,7 @@ def _igemm(x: torch.Tensor, w2: torch.Tensor, k: int, stride: int, pad: int):
 
 
 def _igemm_fp8(x: torch.Tensor, w2: torch.Tensor, k: int, stride: int, pad: int, e5m2: bool = False,
-               scaler: "DelayedScale | None" = None, pre=None):
+               scaler: "DelayedScale | None" = None, pre=None, mod=None):
     """conv(x, w) with fp8 operands on the implicit-GEMM kernel (per-tensor just-in-time scales; x
     e4m3, or e5m2 when it is an output gradient), bf16 channels_last out, or None when the kernel
     declines the shape."""
@@ -665,11 +703,12 @@ def _igemm_fp8(x: torch.Tensor, w2: torch.Tensor, k: int, stride: int, pad: int,
     if pre is not None:  # (q channels_last [N, C, H, W], scale_inv) from the producing BN
         xq, sx = pre[0].permute(0, 2, 3, 1), pre[1]
     else:
-        xq, sx = _q8(x.permute(0, 2, 3, 1), e5m2=e5m2, scaler=scaler)  # the NHWC storage, in place order
-    wq, sw = _q8(w2)
+        xq, sx = _q_act(x.permute(0, 2, 3, 1), e5m2=e5m2, scaler=scaler)  # the NHWC storage, in place order
+    wq, sw = _q_weight(mod, w2) if mod is not None else _q_act(w2)
     out = torch.empty(n * ho * wo, w2.shape[0], device=x.device, dtype=x.dtype)
     if not native().conv_fwd_fp8_(xq.permute(0, 3, 1, 2), wq, sx, sw, out, k, k, stride, pad):
         return None
+    FP8_CALLS["dgrad" if e5m2 else "fwd"] += 1
     return _from_2d(out, n, ho, wo)
 
 
@@ -716,7 +755,7 @@ class _ConvFn(torch.autograd.Function):
         if fp8 and cin % 128 == 0 and _fp8_ok(k * k * cin, cout):
             w2 = weight.permute(0, 2, 3, 1).reshape(cout, k * k * cin)
             y = _igemm_fp8(x, w2 if w2.is_contiguous() else w2.contiguous(), k, stride, pad, scaler=f8[0],
-                           pre=_take_q8(mod, x))
+                           pre=None if _mx_on() else _take_q8(mod, x), mod=mod)
             if y is not None:
                 return y
 

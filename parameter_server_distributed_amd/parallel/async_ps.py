@@ -47,6 +47,7 @@ version, so none of this has a counterpart beyond the push/pull/apply roles.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 import uuid
 from dataclasses import dataclass, field
@@ -57,7 +58,7 @@ import torch.nn as nn
 
 from .. import native
 from ..ops.optim import OptimConfig, OptimDyn
-from .collective_ps import ALIGN, _flat_view, _round, zero_grads_, zero_plan
+from .collective_ps import ALIGN, _flat_view, _round, install_fp8_weights, zero_grads_, zero_plan
 
 _INSTANCE: dict = {}  # AsyncPS instances per rendezvous store (a new elastic generation starts at 0)
 
@@ -97,9 +98,14 @@ class AsyncPS:
                  bucket_mb: float = 16.0, device: torch.device | None = None, ps_ranks: list[int] | None = None,
                  worker_ranks: list[int] | None = None, param_dtype: torch.dtype = torch.bfloat16, nbuf: int = 4,
                  timeout_s: float | None = None, overlap: bool = True, store=None, log: bool = False,
-                 semantics: str = "round"):
+                 semantics: str = "round", pull_dtype: str = "bf16"):
         """``semantics``: "round" (K-batch async, default) or "push" (apply-on-arrival with the
-        per-push hyperparameters of csrc/async_hyper.h); see the module docstring."""
+        per-push hyperparameters of csrc/async_hyper.h); see the module docstring.
+        ``pull_dtype`` "fp8" (the Wide-ResNet fp8-weights config): each owner also publishes the MX
+        e4m3 copy of its snapshot (one E8M0 scale per 32 elements, quantised from the fp32 master
+        right after the apply, csrc/async_ps.cpp quant_publish); workers pull 1.03 bytes/parameter
+        instead of 2, dequantise the bf16 working copy locally and hand the e4m3 weights + scales to
+        the fp8 convolutions (no per-step weight quantisation on the worker)."""
         self.model = model
         self.cfg = optim
         st, self.rank, self.world = _store_and_group()
@@ -123,6 +129,9 @@ class AsyncPS:
         self.is_cuda = self.device.type == "cuda"
         if param_dtype not in (torch.bfloat16, torch.float32):
             raise ValueError("AsyncPS publishes bf16 or fp32 weights")
+        if pull_dtype not in ("bf16", "fp8"):
+            raise ValueError(f"pull_dtype must be bf16 or fp8, got {pull_dtype}")
+        self.pull_mx = pull_dtype == "fp8" and param_dtype == torch.bfloat16 and self.is_cuda
         self.param_dtype = param_dtype
         self.step_idx = 0
         self.pulled = [0] * self.P
@@ -168,6 +177,10 @@ class AsyncPS:
         if self.prefetch:
             self.pbufs.append(self.pbufs[0].clone())
         self.cb = 0
+        # MX pull targets (one per working buffer): e4m3 [total] + E8M0 scales [total / 32]
+        self.q8s = [torch.zeros(total, dtype=torch.float8_e4m3fn, device=dev) for _ in self.pbufs] if self.pull_mx else []
+        self.sc8s = [torch.full((total // 32,), 127, dtype=torch.uint8, device=dev) for _ in self.pbufs] \
+            if self.pull_mx else []
         self.grads = [torch.zeros(total, dtype=param_dtype, device=dev) for _ in range(2)]
         self.gb = 0
         f32 = dict(dtype=torch.float32, device=dev)
@@ -235,7 +248,7 @@ class AsyncPS:
             self.store.wait([f"{key}/ctl"])
         self.engine = C.AsyncEngine(self.rank, self.world, self.owners, self.worker_ranks, self.shard_off,
                                     self.shard_len, self.S, nbuf, shm, self.rank == 0, devidx, timeout_s,
-                                    torch.finfo(param_dtype).bits // 8)
+                                    torch.finfo(param_dtype).bits // 8, self.pull_mx)
         if self.rank == 0:
             self.store.set(f"{key}/ctl", b"1")
         try:
@@ -250,6 +263,8 @@ class AsyncPS:
         self.tracer = None
         self.closed = False
         self._ckpt_seq = 0
+        if self.pull_mx:  # the fp8 convolutions read the pulled e4m3 weights of the current buffer
+            install_fp8_weights(model, lambda: (self.q8s[self.cb], self.sc8s[self.cb], self.pbufs[self.cb]))
 
     def _connect(self, key, optim, log):
         """Exchange memory descriptors, map the peers, publish version 0, self-test, start."""
@@ -398,7 +413,19 @@ class AsyncPS:
                 if self.is_cuda:
                     torch.cuda.current_stream(self.device).wait_event(self.pull_done[self.cb])
                 return
-        self.pulled = list(self.engine.pull(t, self.params_flat, self._stream_ptr()))
+        self.pulled = self._pull_into(t, self.cb, None)
+
+    def _pull_into(self, t: int, nb: int, stream) -> list:
+        """Pull of step t into working buffer ``nb`` on ``stream`` (None: the current stream): the
+        bf16 snapshots, or with MX the e4m3 + scales, dequantised into the bf16 buffer on the same
+        stream."""
+        sptr = stream.cuda_stream if stream is not None else self._stream_ptr()
+        if not self.pull_mx:
+            return list(self.engine.pull(t, self.pbufs[nb], sptr))
+        pulled = list(self.engine.pull_mx(t, self.q8s[nb], self.sc8s[nb], sptr))
+        with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
+            native().dequant_mx_(self.q8s[nb], self.sc8s[nb], self.pbufs[nb])
+        return pulled
 
     def _prefetch_pull(self, t: int):
         """Issue the pull of step t (the next one) now: the SSP wait happens on the host here, the
@@ -407,7 +434,7 @@ class AsyncPS:
         if self.is_cuda:
             if self.step_done[nb] is not None:
                 self.pull_stream.wait_event(self.step_done[nb])
-            pulled = self.engine.pull(t, self.pbufs[nb], self.pull_stream.cuda_stream)
+            pulled = self._pull_into(t, nb, self.pull_stream)
             ev = torch.cuda.Event()
             ev.record(self.pull_stream)
             self.pull_done[nb] = ev
@@ -481,7 +508,7 @@ class AsyncPS:
         """After ``drain``: the working weights (the model's parameter views) = the latest applied
         snapshot. Workers otherwise hold the weights of their last pull, one round behind."""
         if self.is_worker and self.engine is not None:
-            self.pulled = list(self.engine.pull(0, self.params_flat, self._stream_ptr()))
+            self.pulled = self._pull_into(0, self.cb, None)
             if self.is_cuda:
                 torch.cuda.synchronize(self.device)
 

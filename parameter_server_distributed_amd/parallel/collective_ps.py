@@ -84,6 +84,32 @@ def zero_grads_(flat: torch.Tensor, plan) -> None:
         flat.narrow(0, off, n).zero_()
 
 
+def install_fp8_weights(model: nn.Module, resolve) -> None:
+    """Give every fp8 module (``fp8 = True``) a ``_psd_w8(w2)`` hook that returns the MX e4m3 copy
+    of its weight the data plane pulled with the bf16 working copy -- views (q [Cout, K], E8M0
+    scales [Cout*K/32]) into the flat fp8 buffers -- or None when the weight is not in them.
+    ``resolve()`` -> (q_flat, scale_flat, params_flat) of the current working buffers (AsyncPS
+    alternates two)."""
+    for m in model.modules():
+        w = getattr(m, "weight", None)
+        if not getattr(m, "fp8", False) or not isinstance(w, nn.Parameter):
+            continue
+
+        def pub(w2, m=m):
+            bufs = resolve()
+            if bufs is None:
+                return None
+            qf, sf, pf = bufs
+            wt = m.weight
+            off = (wt.data_ptr() - pf.data_ptr()) // wt.element_size()
+            n = wt.numel()
+            if off < 0 or off + n > pf.numel() or off % 32 or n % 32 or w2.numel() != n:
+                return None
+            return qf.narrow(0, off, n).view(w2.shape), sf.narrow(0, off // 32, n // 32)
+
+        m._psd_w8 = pub
+
+
 def _flat_view(flat: torch.Tensor, off: int, p: torch.Tensor) -> torch.Tensor:
     """View of ``flat[off:off+numel]`` with the same shape *and strides* as ``p`` (channels_last
     conv weights stay channels_last)."""
@@ -209,10 +235,15 @@ class CollectivePS:
         if pull_dtype not in ("bf16", "fp8"):
             raise ValueError(f"pull_dtype must be bf16 or fp8, got {pull_dtype}")
         self.pull_fp8 = pull_dtype == "fp8" and param_dtype == torch.bfloat16
+        # MX (default): one E8M0 scale per 32 elements (ALIGN = 64 keeps every tensor and every
+        # shard slice block-aligned, so slices quantise independently, with no amax reduction); the
+        # fp8 convolutions consume the pulled e4m3 weights + scales directly (install_fp8_weights)
+        self.pull_mx = self.pull_fp8 and os.environ.get("PSD_FP8_MX", "1") != "0" and self.is_cuda
         if self.pull_fp8:
             self.p8 = torch.zeros(self.total, dtype=torch.float8_e4m3fn, device=dev)
             self.p8_scale = torch.ones(len(buckets) * self.P, dtype=torch.float32, device=dev)
             self.p8_amax = torch.zeros(len(buckets) * self.P, dtype=torch.float32, device=dev)
+            self.p8_mx = torch.full((self.total // 32,), 127, dtype=torch.uint8, device=dev) if self.pull_mx else None
 
         # Modules that can write their parameter gradients straight into our flat buffer (fused BN)
         # get a grad sink; their params keep .grad = None so autograd adopts the written view
@@ -252,6 +283,8 @@ class CollectivePS:
         self._next = 0
         self.tracer = None  # utils.trace.StepTracer (set by the Trainer)
         self._sync_init()
+        if self.pull_mx:
+            install_fp8_weights(model, lambda: (self.p8, self.p8_mx, self.params_flat))
 
     # ------------------------------------------------------------------ setup
     def _sync_init(self):
@@ -444,6 +477,10 @@ class CollectivePS:
 
     def _quant_slice(self, b: Bucket, k: int, src: torch.Tensor):
         C = native()
+        if self.pull_mx:
+            lo = b.offset + k * b.slice_numel
+            C.quant_mx_(src, self.p8.narrow(0, lo, b.slice_numel), self.p8_mx.narrow(0, lo // 32, b.slice_numel // 32))
+            return
         i = b.index * self.P + k
         amax = self.p8_amax.narrow(0, i, 1)
         amax.zero_()
@@ -453,6 +490,21 @@ class CollectivePS:
 
     def _pull_fp8(self, b: Bucket):
         C = native()
+        if self.pull_mx:
+            q = self.p8.narrow(0, b.offset, b.numel)
+            mx = self.p8_mx.narrow(0, b.offset // 32, b.numel // 32)
+            if not self._trivial:
+                q8 = q.view(torch.uint8)
+                sl, sl32 = b.slice_numel, b.slice_numel // 32
+                if self.collective_rs:
+                    self.t.all_gather(q8.narrow(0, self.rank * sl, sl), q8)
+                    self.t.all_gather(mx.narrow(0, self.rank * sl32, sl32), mx)
+                else:
+                    for k, owner in enumerate(self.owners):
+                        self.t.broadcast(q8.narrow(0, k * sl, sl), owner)
+                        self.t.broadcast(mx.narrow(0, k * sl32, sl32), owner)
+            C.dequant_mx_(q, mx, self.params_flat.narrow(0, b.offset, b.numel))
+            return
         q = self.p8.narrow(0, b.offset, b.numel).view(torch.uint8)
         sc = self.p8_scale.narrow(0, b.index * self.P, self.P)
         if not self._trivial:
