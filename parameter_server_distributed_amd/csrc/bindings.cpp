@@ -55,7 +55,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("eps"), py::arg("counter"), py::arg("ss_eval"), py::arg("mask_out") = false,
         py::arg("residual_ss") = py::none(), py::arg("stats_only") = false, py::arg("q8_out") = py::none(),
         py::arg("q8_hist") = py::none(), py::arg("q8_sinv") = py::none(), py::arg("q8_margin") = 1.0,
-        py::arg("part_in") = py::none(), py::arg("part_rows") = 0);
+        py::arg("part_in") = py::none(), py::arg("part_rows") = 0, py::arg("q8_mx") = py::none());
   m.def("bn_reduce_", &bn_reduce_, py::arg("x"), py::arg("shift"));
   m.def("bn_bwd_reduce_", &bn_bwd_reduce_, py::arg("dy"), py::arg("x"), py::arg("save_mean"),
         py::arg("ss") = py::none(), py::arg("dy2") = py::none(), py::arg("mbits") = py::none());
@@ -68,7 +68,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("rows") = 0, py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none());
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("gamma"), py::arg("save_mean"),
         py::arg("save_invstd"), py::arg("relu"), py::arg("need_dr"), py::arg("dgamma_out"), py::arg("dbeta_out"),
-        py::arg("dy2") = py::none(), py::arg("ss") = py::none(), py::arg("mbits") = py::none());
+        py::arg("dy2") = py::none(), py::arg("ss") = py::none(), py::arg("mbits") = py::none(),
+        py::arg("dq") = py::none(), py::arg("dqmx") = py::none());
   m.def("gemm_", &gemm_, py::arg("A"), py::arg("B"), py::arg("a_kmajor"), py::arg("b_kmajor"), py::arg("out"),
         py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("aux") = py::none());
   m.def("gemm_splitk_", &gemm_splitk_, py::arg("A"), py::arg("B"), py::arg("a_kmajor"), py::arg("b_kmajor"),
@@ -86,7 +87,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("bmean_d") = py::none(), py::arg("part_d") = py::none());
   m.def("bn_bwd_pre", &bn_bwd_pre, py::arg("g"), py::arg("x"), py::arg("gamma"), py::arg("save_mean"),
         py::arg("save_invstd"), py::arg("part"), py::arg("rows"), py::arg("dgamma_out") = py::none(),
-        py::arg("dbeta_out") = py::none());
+        py::arg("dbeta_out") = py::none(), py::arg("dq") = py::none(), py::arg("dqmx") = py::none());
   m.def("convn_variants", &convn_variants_, py::arg("N"));
   m.def("conv_fwd_", &conv_fwd_, py::arg("x"), py::arg("w2"), py::arg("out"), py::arg("R"), py::arg("S"),
         py::arg("stride"), py::arg("pad"));

@@ -42,7 +42,7 @@ std::vector<at::Tensor> bn_fwd(const at::Tensor& x_in, c10::optional<at::Tensor>
                                c10::optional<at::Tensor> residual_ss, bool stats_only,
                                c10::optional<at::Tensor> q8_out, c10::optional<at::Tensor> q8_hist,
                                c10::optional<at::Tensor> q8_sinv, double q8_margin, c10::optional<at::Tensor> part_in,
-                               int64_t part_rows) {
+                               int64_t part_rows, c10::optional<at::Tensor> q8_mx) {
   TORCH_CHECK(x_in.is_cuda() && x_in.scalar_type() == at::kBFloat16, "psd bn: x must be a bf16 device tensor");
   const c10::DeviceGuard g(x_in.device());
   at::Tensor x = nhwc(x_in);
@@ -119,13 +119,20 @@ std::vector<at::Tensor> bn_fwd(const at::Tensor& x_in, c10::optional<at::Tensor>
     TORCH_CHECK(!stats_only && relu && q.scalar_type() == at::kFloat8_e4m3fn && q.sizes() == x.sizes() && laid &&
                     (reinterpret_cast<uintptr_t>(q.data_ptr()) & 7) == 0,
                 "psd bn: q8_out must be an e4m3fn tensor laid out like x (ReLU BNs)");
-    TORCH_CHECK(q8_hist.has_value() && q8_hist->numel() >= 2 && q8_hist->scalar_type() == at::kFloat &&
-                    q8_sinv.has_value() && q8_sinv->numel() >= 1 && q8_sinv->scalar_type() == at::kFloat,
-                "psd bn: q8_out needs q8_hist fp32[2] and q8_sinv fp32[1]");
     a.q8 = reinterpret_cast<uint8_t*>(q.data_ptr());
-    a.q8hist = q8_hist->data_ptr<float>();
-    a.q8sinv = q8_sinv->data_ptr<float>();
-    a.q8margin = (float)q8_margin;
+    if (q8_mx.has_value() && q8_mx->defined()) {  // MX: E8M0 per 32 channels, no history
+      TORCH_CHECK(q8_mx->scalar_type() == at::kByte && q8_mx->is_contiguous() && q8_mx->numel() * 32 == x.numel() &&
+                      C % 32 == 0 && q8_mx->device() == x.device(),
+                  "psd bn: q8_mx must be uint8 [numel / 32] (channels % 32 == 0)");
+      a.q8mx = q8_mx->data_ptr<uint8_t>();
+    } else {
+      TORCH_CHECK(q8_hist.has_value() && q8_hist->numel() >= 2 && q8_hist->scalar_type() == at::kFloat &&
+                      q8_sinv.has_value() && q8_sinv->numel() >= 1 && q8_sinv->scalar_type() == at::kFloat,
+                  "psd bn: q8_out needs q8_hist fp32[2] and q8_sinv fp32[1] (or MX scales)");
+      a.q8hist = q8_hist->data_ptr<float>();
+      a.q8sinv = q8_sinv->data_ptr<float>();
+      a.q8margin = (float)q8_margin;
+    }
   }
   hipError_t e = launch_bn_fwd(a, stream_of(x));
   TORCH_CHECK(e == hipSuccess, "psd bn fwd: ", hipGetErrorString(e));
@@ -146,12 +153,30 @@ at::Tensor bn_reduce_(const at::Tensor& x_in, const at::Tensor& shift) {
   return part;
 }
 
+namespace {
+// optional MX e5m2 side output of a BN backward elementwise pass (dq like x, E8M0 scales [numel/32])
+void set_dq(c10::optional<at::Tensor>& dq, c10::optional<at::Tensor>& dqmx, const at::Tensor& x, uint8_t*& q,
+            uint8_t*& sc) {
+  q = sc = nullptr;
+  if (!(dq.has_value() && dq->defined())) return;
+  const at::Tensor& t = *dq;
+  const bool laid = t.dim() == 4 ? t.is_contiguous(at::MemoryFormat::ChannelsLast) : t.is_contiguous();
+  TORCH_CHECK(t.scalar_type() == at::kFloat8_e5m2 && t.sizes() == x.sizes() && laid && dqmx.has_value() &&
+                  dqmx->defined() && dqmx->scalar_type() == at::kByte && dqmx->is_contiguous() &&
+                  dqmx->numel() * 32 == x.numel() && channels(x) % 32 == 0,
+              "psd bn bwd: dq must be e5m2 laid out like x with uint8 [numel / 32] scales (channels % 32 == 0)");
+  q = reinterpret_cast<uint8_t*>(t.data_ptr());
+  sc = dqmx->data_ptr<uint8_t>();
+}
+}  // namespace
+
 std::vector<at::Tensor> bn_bwd(const at::Tensor& dy_in, const at::Tensor& x_in, c10::optional<at::Tensor> y_in,
                                c10::optional<at::Tensor> gamma, const at::Tensor& save_mean,
                                const at::Tensor& save_invstd, bool relu, bool need_dr,
                                c10::optional<at::Tensor> dgamma_out, c10::optional<at::Tensor> dbeta_out,
                                c10::optional<at::Tensor> dy2_in, c10::optional<at::Tensor> ss_in,
-                               c10::optional<at::Tensor> mbits_in) {
+                               c10::optional<at::Tensor> mbits_in, c10::optional<at::Tensor> dq,
+                               c10::optional<at::Tensor> dqmx) {
   const c10::DeviceGuard g(x_in.device());
   at::Tensor x = nhwc(x_in), dy = nhwc(dy_in);
   at::Tensor dy2;
@@ -213,6 +238,7 @@ std::vector<at::Tensor> bn_bwd(const at::Tensor& dy_in, const at::Tensor& x_in, 
   a.M = M;
   a.C = (int32_t)C;
   a.relu = relu;
+  set_dq(dq, dqmx, x, a.dq, a.dqmx);
   hipError_t e = launch_bn_bwd(a, stream_of(x));
   TORCH_CHECK(e == hipSuccess, "psd bn bwd: ", hipGetErrorString(e));
   return {dx, dr, dgamma, dbeta};
@@ -272,7 +298,8 @@ at::Tensor bn_bwd_reduce_(const at::Tensor& dy_in, const at::Tensor& x_in, const
 std::vector<at::Tensor> bn_bwd_pre(const at::Tensor& g_in, const at::Tensor& x_in, c10::optional<at::Tensor> gamma,
                                    const at::Tensor& save_mean, const at::Tensor& save_invstd, const at::Tensor& part,
                                    int64_t rows, c10::optional<at::Tensor> dgamma_out,
-                                   c10::optional<at::Tensor> dbeta_out) {
+                                   c10::optional<at::Tensor> dbeta_out, c10::optional<at::Tensor> dq,
+                                   c10::optional<at::Tensor> dqmx) {
   const c10::DeviceGuard dg(x_in.device());
   at::Tensor x = nhwc(x_in), g = nhwc(g_in);
   const int64_t C = channels(x), M = x.numel() / C;
@@ -289,13 +316,15 @@ std::vector<at::Tensor> bn_bwd_pre(const at::Tensor& g_in, const at::Tensor& x_i
   }
   at::Tensor coef = at::empty({3 * C}, f32);
   at::Tensor fold = rows > kFoldRows ? at::empty({(int64_t)kFoldRows * 2 * C}, f32) : at::Tensor();
+  uint8_t *q8, *q8mx;
+  set_dq(dq, dqmx, x, q8, q8mx);
   const hipError_t e = launch_bn_bwd_pre(
       reinterpret_cast<const uint16_t*>(g.data_ptr()), reinterpret_cast<const uint16_t*>(x.data_ptr()),
       opt_ptr<const uint16_t>(gamma), save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(),
       part.data_ptr<float>(), (int)rows, fold.defined() ? fold.data_ptr<float>() : nullptr,
       dgamma.defined() ? reinterpret_cast<uint16_t*>(dgamma.data_ptr()) : nullptr,
       dbeta.defined() ? reinterpret_cast<uint16_t*>(dbeta.data_ptr()) : nullptr, coef.data_ptr<float>(),
-      reinterpret_cast<uint16_t*>(dx.data_ptr()), M, (int)C, stream_of(x));
+      reinterpret_cast<uint16_t*>(dx.data_ptr()), M, (int)C, stream_of(x), q8, q8mx);
   TORCH_CHECK(e == hipSuccess, "psd bn_bwd_pre: ", hipGetErrorString(e));
   return {dx, dgamma, dbeta};
 }

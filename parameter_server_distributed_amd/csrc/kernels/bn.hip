@@ -19,6 +19,7 @@
 // launch: correct for any workgroup->XCD placement, cdna_hip_programming.md G16).
 #include <hip/hip_fp8.h>
 #include "common.h"
+#include "mx_common.h"
 #include "launchers_bn.h"
 #include "pool_gather.h"
 
@@ -228,15 +229,18 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const float* __res
 // consumer's amax history q8hist[0] * margin, this pass's amax max-reduced into q8hist[1]; the
 // roll kernel after the launch moves it to q8hist[0]) -- the consumer's own quantise pass (a full
 // read of y) never runs.
-template <bool RELU, bool RES, bool MASK_OUT, bool RSS = false, bool Q8 = false>
+// Q8 == 2: the e4m3 copy with MX block scales instead (one E8M0 byte per 32 channels into q8mx:
+// 4 lanes hold one block, the block maximum is a DPP quad reduction; no history, no roll).
+template <bool RELU, bool RES, bool MASK_OUT, bool RSS = false, int Q8 = 0>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
                                                        const float* __restrict__ ss, uint16_t* __restrict__ y,
                                                        uint8_t* __restrict__ mbits, int pack4, int64_t nvec, int C,
                                                        const float* __restrict__ rss = nullptr,
                                                        uint8_t* __restrict__ q8 = nullptr, float* q8hist = nullptr,
-                                                       float q8margin = 1.f, float* __restrict__ q8sinv = nullptr) {
+                                                       float q8margin = 1.f, float* __restrict__ q8sinv = nullptr,
+                                                       uint8_t* __restrict__ q8mx = nullptr) {
   float q8scale = 0.f, q8max = 0.f;
-  if (Q8) {
+  if (Q8 == 1) {
     const float a = fmaxf(q8hist[0] * q8margin, 1e-12f);
     q8scale = 448.f / a;
     if (blockIdx.x == 0 && threadIdx.x == 0) *q8sinv = a / 448.f;
@@ -266,7 +270,16 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
       t[j] = o;
     }
     store8_bf16(y + v * 8, t);
-    if (Q8) {  // quantise the stored (bf16-rounded) values
+    if (Q8 == 2) {  // MX: the stored (bf16-rounded) values, block scale from the lane quad
+      float r[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = bf16_to_f32(f32_to_bf16(t[j]));
+      uint2 qb;
+      const int eb = mx_quant8<false>(r, qb);
+      *reinterpret_cast<uint2*>(q8 + v * 8) = qb;
+      if ((v & 3) == 0) q8mx[v >> 2] = (uint8_t)eb;
+    }
+    if (Q8 == 1) {  // quantise the stored (bf16-rounded) values
       uint32_t lo = 0, hi = 0;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -295,7 +308,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
       }
     }
   }
-  if (Q8) {
+  if (Q8 == 1) {
     for (int off = 32; off > 0; off >>= 1) q8max = fmaxf(q8max, __shfl_xor(q8max, off, kWave));
     if ((threadIdx.x & (kWave - 1)) == 0)
       atomicMax(reinterpret_cast<unsigned int*>(q8hist + 1), __float_as_uint(q8max));  // one per wave
@@ -440,11 +453,15 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
 
 // MODE 0: dy' = dy; MODE 1: dy' = dy * (y > 0); MODE 2: dy' = g (already masked, = dr);
 // MODE 3: dy' = dy * (x*scale + shift > 0) (mask recomputed, kMaskX)
-template <int MODE>
+// DQ: also write dx as MX e5m2 (one E8M0 byte per 32 channels) for the producing fp8 convolution's
+// bwd-data, whose own quantise pass (a full read of dx) then never runs (ops/bn.py _dq8_args)
+template <int MODE, bool DQ = false>
 __global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(const uint16_t* __restrict__ g, const uint16_t* __restrict__ g2,
                                                            const uint16_t* __restrict__ y, const float* __restrict__ ssf,
                                                            const uint16_t* __restrict__ x, const float* __restrict__ coef,
-                                                           uint16_t* __restrict__ dx, int64_t nvec, int C) {
+                                                           uint16_t* __restrict__ dx, int64_t nvec, int C,
+                                                           uint8_t* __restrict__ dq = nullptr,
+                                                           uint8_t* __restrict__ dqmx = nullptr) {
   const int tpc = C >> 3;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -480,6 +497,14 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(const uint16_t* __res
 #pragma unroll
     for (int j = 0; j < 8; ++j) gv[j] = fmaf(A[j], gv[j], fmaf(B[j], xv[j], Cc[j]));
     store8_bf16(dx + v * 8, gv);
+    if constexpr (DQ) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) gv[j] = bf16_to_f32(f32_to_bf16(gv[j]));  // the stored values
+      uint2 qb;
+      const int eb = mx_quant8<true>(gv, qb);
+      *reinterpret_cast<uint2*>(dq + v * 8) = qb;
+      if ((v & 3) == 0) dqmx[v >> 2] = (uint8_t)eb;
+    }
   }
 }
 
@@ -777,11 +802,23 @@ hipError_t launch_bn_fwd(const BnFwdArgs& a, hipStream_t st) {
 #define PSD_APPLY(R, S, B) \
   hipLaunchKernelGGL((bn_apply_kernel<R, S, B>), dim3(g), dim3(256), 0, st, a.x, a.res, a.ss, a.y, a.mbits, \
                      (int)(nvec % 4 == 0), nvec, a.C, nullptr)
+  if (a.q8 && a.q8mx) {  // MX fp8 side output (every lane quad = one 32-channel block)
+    if (!a.relu || a.C % 32 != 0 || nvec % 4 != 0) return hipErrorInvalidValue;
+#define PSD_APM(S, B, RS)                                                                                      \
+  hipLaunchKernelGGL((bn_apply_kernel<true, S, B, RS, 2>), dim3(g), dim3(256), 0, st, a.x, a.res, a.ss, a.y,    \
+                     a.mbits, 1, nvec, a.C, a.res_ss, a.q8, nullptr, 1.f, nullptr, a.q8mx)
+    if (a.res_ss && a.res && a.mbits) PSD_APM(true, true, true);
+    else if (a.res && a.mbits && !a.res_ss) PSD_APM(true, true, false);
+    else if (!a.res && !a.mbits && !a.res_ss) PSD_APM(false, false, false);
+    else return hipErrorInvalidValue;
+#undef PSD_APM
+    return hipGetLastError();
+  }
   if (a.q8) {  // fp8 side output for the consumer convolution (ReLU BNs: bn1 / bn2 / residual bn3)
     if (!a.relu || !a.q8hist || !a.q8sinv) return hipErrorInvalidValue;
     const int p4 = (int)(nvec % 4 == 0);
 #define PSD_APQ(S, B, RS)                                                                                      \
-  hipLaunchKernelGGL((bn_apply_kernel<true, S, B, RS, true>), dim3(g), dim3(256), 0, st, a.x, a.res, a.ss, a.y, \
+  hipLaunchKernelGGL((bn_apply_kernel<true, S, B, RS, 1>), dim3(g), dim3(256), 0, st, a.x, a.res, a.ss, a.y, \
                      a.mbits, p4, nvec, a.C, a.res_ss, a.q8, a.q8hist, a.q8margin, a.q8sinv)
     if (a.res_ss && a.res && a.mbits) PSD_APQ(true, true, true);
     else if (a.res && a.mbits && !a.res_ss) PSD_APQ(true, true, false);
@@ -844,7 +881,8 @@ static hipError_t launch_bn_bwd_pool(const BnBwdArgs& a, hipStream_t st) {
 // (and holds the residual-branch gradient), part holds `rows` rows of (sum g, sum g (x - mean)).
 hipError_t launch_bn_bwd_pre(const uint16_t* g, const uint16_t* x, const uint16_t* gamma, const float* mean,
                              const float* invstd, const float* part, int rows, float* fold_ws, uint16_t* dgamma,
-                             uint16_t* dbeta, float* coef, uint16_t* dx, int64_t M, int C, hipStream_t st) {
+                             uint16_t* dbeta, float* coef, uint16_t* dx, int64_t M, int C, hipStream_t st, uint8_t* dq,
+                             uint8_t* dqmx) {
   if (M <= 0) return hipSuccess;
   if (C % 8 != 0 || rows <= 0) return hipErrorInvalidValue;
   const float* p = part;
@@ -860,8 +898,14 @@ hipError_t launch_bn_bwd_pre(const uint16_t* g, const uint16_t* x, const uint16_
                      mean, invstd, dgamma, dbeta, coef);
   if (!dx) return hipGetLastError();  // coefficients only (BN-backward fold)
   const int64_t nvec = M * (C / 8);
-  hipLaunchKernelGGL(bn_bwd_elemt_kernel<2>, dim3(elem_grid(nvec, C)), dim3(256), 0, st, g, nullptr, nullptr, nullptr, x,
-                     coef, dx, nvec, C);
+  if (dq) {
+    if (!dqmx || C % 32 != 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((bn_bwd_elemt_kernel<2, true>), dim3(elem_grid(nvec, C)), dim3(256), 0, st, g, nullptr, nullptr,
+                       nullptr, x, coef, dx, nvec, C, dq, dqmx);
+  } else {
+    hipLaunchKernelGGL(bn_bwd_elemt_kernel<2>, dim3(elem_grid(nvec, C)), dim3(256), 0, st, g, nullptr, nullptr, nullptr,
+                       x, coef, dx, nvec, C);
+  }
   return hipGetLastError();
 }
 
@@ -954,13 +998,19 @@ hipError_t launch_bn_bwd(const BnBwdArgs& a, hipStream_t st) {
   else PSD_RED(kMaskNone, false);
 #undef PSD_RED
   if (a.reduce_only) return hipGetLastError();
+  if (a.dq && (!a.dqmx || a.C % 32 != 0)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((a.C + kFinCh - 1) / kFinCh), dim3(256), 0, st, a.part, gx, a.M, a.C, a.gamma,
                      a.save_mean, a.save_invstd, a.dgamma, a.dbeta, a.coef);
   if (a.coef_only) return hipGetLastError();  // coefficients for the consumer's BN-backward fold
   const int64_t nvec = a.M * (a.C / 8);
   const int g = elem_grid(nvec, a.C);
-#define PSD_EL(MODE, G, G2) \
-  hipLaunchKernelGGL(bn_bwd_elemt_kernel<MODE>, dim3(g), dim3(256), 0, st, G, G2, a.y, a.ss, a.x, a.coef, a.dx, nvec, a.C)
+#define PSD_EL(MODE, G, G2)                                                                                         \
+  if (a.dq)                                                                                                       \
+    hipLaunchKernelGGL((bn_bwd_elemt_kernel<MODE, true>), dim3(g), dim3(256), 0, st, G, G2, a.y, a.ss, a.x, a.coef, \
+                       a.dx, nvec, a.C, a.dq, a.dqmx);                                                              \
+  else                                                                                                            \
+    hipLaunchKernelGGL((bn_bwd_elemt_kernel<MODE>), dim3(g), dim3(256), 0, st, G, G2, a.y, a.ss, a.x, a.coef, a.dx, \
+                       nvec, a.C)
   if (a.dr) PSD_EL(2, a.dr, nullptr);
   else if (mask == kMaskY) PSD_EL(1, a.dy, a.dy2);
   else if (mask == kMaskX) PSD_EL(3, a.dy, a.dy2);

@@ -4,6 +4,7 @@
 #include <hip/hip_fp8.h>
 #include "common.h"
 #include "launchers.h"
+#include "mx_common.h"
 
 namespace psd {
 
@@ -14,18 +15,6 @@ __device__ __forceinline__ float e4m3_to_f32(uint8_t b) {
   if (e == 0) v = (float)m * 0.001953125f;                      // m/8 * 2^-6
   else v = __uint_as_float(((e + 120u) << 23) | (m << 20));     // (1+m/8) * 2^(e-7)
   return s ? -v : v;
-}
-
-__device__ __forceinline__ uint8_t f32_to_e4m3(float x) {
-  return (uint8_t)__hip_cvt_float_to_fp8(x, __HIP_SATFINITE, __HIP_E4M3);
-}
-__device__ __forceinline__ uint8_t f32_to_e5m2(float x) {
-  return (uint8_t)__hip_cvt_float_to_fp8(x, __HIP_SATFINITE, __HIP_E5M2);
-}
-template <bool E5>
-__device__ __forceinline__ uint8_t f32_to_f8(float x) {
-  if constexpr (E5) return f32_to_e5m2(x);
-  else return f32_to_e4m3(x);
 }
 
 template <int DT>
@@ -337,14 +326,6 @@ hipError_t launch_dequant_fp8(const uint8_t* x, int64_t n, const float* scale_in
 // rows of a multiple of 32 elements keep every block inside one GEMM row: tools/probes/mx_probe.hip
 // pins the lane map), and an activation is quantised in the pass that produces it.
 // Scale choice: the smallest power of two with amax * 2^-e <= fp8 max (no saturation in the block).
-__device__ __forceinline__ int mx_exp_byte(float amax, float fmax) {
-  if (!(amax > 0.f) || !(amax < 3.0e38f)) return 127;  // zero / non-finite block: unit scale
-  int p;
-  const float m = frexpf(amax / fmax, &p);  // amax / fmax = m 2^p, m in [0.5, 1)
-  int e = (m == 0.5f) ? p - 1 : p;
-  e = e < -127 ? -127 : (e > 127 ? 127 : e);
-  return e + 127;
-}
 
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v) {
@@ -356,27 +337,15 @@ __device__ __forceinline__ float dpp_f(float v) {
 template <int DT, bool E5>
 __global__ __launch_bounds__(256) void quant_mx_kernel(const void* __restrict__ x, int64_t n, uint8_t* __restrict__ q,
                                                        uint8_t* __restrict__ sc) {
-  const float fmax = E5 ? 57344.f : 448.f;
   const int64_t nvec = n >> 3;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
     float t[8];
     if (DT == DT_BF16) load8_bf16(static_cast<const uint16_t*>(x) + (v << 3), t);
     else load8_f32(static_cast<const float*>(x) + (v << 3), t);
-    float m = 0.f;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(t[e]));
-    m = fmaxf(m, dpp_f<0xB1>(m));  // quad_perm [1,0,3,2]
-    m = fmaxf(m, dpp_f<0x4E>(m));  // quad_perm [2,3,0,1]: the block's 4 lanes agree
-    const int eb = mx_exp_byte(m, fmax);
-    const float inv = __uint_as_float((uint32_t)(254 - eb) << 23);  // 2^(127 - eb)
-    uint32_t lo = 0, hi = 0;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      lo |= (uint32_t)f32_to_f8<E5>(t[e] * inv) << (8 * e);
-      hi |= (uint32_t)f32_to_f8<E5>(t[e + 4] * inv) << (8 * e);
-    }
-    *reinterpret_cast<uint2*>(q + (v << 3)) = make_uint2(lo, hi);
+    uint2 qb;
+    const int eb = mx_quant8<E5>(t, qb);
+    *reinterpret_cast<uint2*>(q + (v << 3)) = qb;
     if ((v & 3) == 0) sc[v >> 2] = (uint8_t)eb;
   }
 }

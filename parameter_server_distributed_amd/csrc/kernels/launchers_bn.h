@@ -27,6 +27,7 @@ struct BnFwdArgs {
   float* q8hist;          // [2] the consumer's amax history (scale from [0]; this pass's amax -> [0])
   float q8margin;
   float* q8sinv;          // [1] out: the dequant factor of q8
+  uint8_t* q8mx;          // MX instead of per-tensor: [M * C / 32] E8M0 block scales of q8 (no history)
   uint8_t* pool_arg;      // stem fusion: y = maxpool3x3s2(relu(bn(x))) [N, H/2, W/2, C] + argmax (optional)
   int32_t N, H, W;        // x as [N, H, W, C] (pool fusion only)
   int64_t M;
@@ -80,6 +81,9 @@ struct BnBwdArgs {
   // reduction + finalize only (coef, dgamma, dbeta; dr when given): the consumer convolution folds
   // the elementwise pass into its backward GEMMs (ops/bn.py, kernels/bnfold.hip)
   int32_t coef_only;
+  // MX e5m2 copy of dx (+ E8M0 scales per 32 channels) for the producing fp8 convolution's bwd-data
+  uint8_t* dq;
+  uint8_t* dqmx;
 };
 
 // true when the fused stem BN+ReLU+max-pool kernels support this shape
@@ -96,7 +100,8 @@ hipError_t launch_bn_bwd(const BnBwdArgs& a, hipStream_t stream);
 // fold (> kFoldRows partial rows: fold_ws [kFoldRows * 2C]) + finalize + dx = A g + B x + C
 hipError_t launch_bn_bwd_pre(const uint16_t* g, const uint16_t* x, const uint16_t* gamma, const float* mean,
                              const float* invstd, const float* part, int rows, float* fold_ws, uint16_t* dgamma,
-                             uint16_t* dbeta, float* coef, uint16_t* dx, int64_t M, int C, hipStream_t stream);
+                             uint16_t* dbeta, float* coef, uint16_t* dx, int64_t M, int C, hipStream_t stream,
+                             uint8_t* dq = nullptr, uint8_t* dqmx = nullptr);
 
 struct BnDualPreArgs {
   const uint16_t* g;      // masked upstream gradient (= the residual-branch gradient) [M, C]

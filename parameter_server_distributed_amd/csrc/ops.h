@@ -26,7 +26,7 @@ std::vector<at::Tensor> bn_fwd(const at::Tensor& x, c10::optional<at::Tensor> ga
                                bool mask_out, c10::optional<at::Tensor> residual_ss, bool stats_only,
                                c10::optional<at::Tensor> q8_out, c10::optional<at::Tensor> q8_hist,
                                c10::optional<at::Tensor> q8_sinv, double q8_margin, c10::optional<at::Tensor> part_in,
-                               int64_t part_rows);
+                               int64_t part_rows, c10::optional<at::Tensor> q8_mx);
 // statistics pass of the BN forward alone: shifted sums of x [M, C] into a fresh [rows, 2, C] fp32
 at::Tensor bn_reduce_(const at::Tensor& x, const at::Tensor& shift);
 at::Tensor bn_bwd_reduce_(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& save_mean,
@@ -58,7 +58,7 @@ std::vector<at::Tensor> bn_bwd(const at::Tensor& dy, const at::Tensor& x, c10::o
                                const at::Tensor& save_invstd, bool relu, bool need_dr,
                                c10::optional<at::Tensor> dgamma_out, c10::optional<at::Tensor> dbeta_out,
                                c10::optional<at::Tensor> dy2, c10::optional<at::Tensor> ss,
-                               c10::optional<at::Tensor> mbits);
+                               c10::optional<at::Tensor> mbits, c10::optional<at::Tensor> dq, c10::optional<at::Tensor> dqmx);
 
 void gemm_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool b_kmajor, at::Tensor out,
            c10::optional<at::Tensor> bias, int64_t act, c10::optional<at::Tensor> aux);
@@ -83,7 +83,8 @@ int64_t convn_bwd_(const at::Tensor& dy, const at::Tensor& w2, at::Tensor out, i
 std::vector<at::Tensor> bn_bwd_pre(const at::Tensor& g, const at::Tensor& x, c10::optional<at::Tensor> gamma,
                                    const at::Tensor& save_mean, const at::Tensor& save_invstd, const at::Tensor& part,
                                    int64_t rows, c10::optional<at::Tensor> dgamma_out,
-                                   c10::optional<at::Tensor> dbeta_out);
+                                   c10::optional<at::Tensor> dbeta_out, c10::optional<at::Tensor> dq,
+                                   c10::optional<at::Tensor> dqmx);
 int64_t convn_variants_(int64_t N);
 bool conv_fwd_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride,
                int64_t pad);

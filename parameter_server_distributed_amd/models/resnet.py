@@ -87,6 +87,10 @@ class Bottleneck(nn.Module):
             # (plain attributes: object.__setattr__ keeps the consumer from becoming a submodule)
             object.__setattr__(self.bn1, "_psd_q8_consumer", self.conv2)
             object.__setattr__(self.bn2, "_psd_q8_consumer", self.conv3)
+            # and each BN's backward quantises its input gradient for the producing conv's fp8 bwd-data
+            for conv, bn in ((self.conv1, self.bn1), (self.conv2, self.bn2), (self.conv3, self.bn3)):
+                if hasattr(conv, "psd_fp8_dgrad"):
+                    object.__setattr__(bn, "_psd_dq8_producer", conv)
 
     def forward(self, x, prev_bn=None):
         """``prev_bn``: the fused BN that produced ``x`` (the previous block's bn3). The second

@@ -36,6 +36,14 @@ def _q8_args(mod, x: torch.Tensor) -> dict:
     cons = getattr(mod, "_psd_q8_consumer", None)
     if cons is None or not mod.relu or x.dim() != 4 or not cons.psd_fp8_consumes(x.shape[1]):
         return {}
+    if _at.enabled("PSD_FP8_MX"):
+        # MX operands: the apply pass writes e4m3 + one E8M0 scale per 32 channels (a lane quad's
+        # block maximum, kernels/bn.hip Q8 == 2) -- the consumer's own quantise pass (a full read of
+        # y) never runs. PSD_FP8_MX_HANDOVER=0: the consumer quantises.
+        if x.shape[1] % 32 or not _at.enabled("PSD_FP8_MX_HANDOVER"):
+            return {}
+        q = torch.empty_like(x, dtype=torch.float8_e4m3fn, memory_format=torch.channels_last)
+        return {"q8_out": q, "q8_mx": torch.empty(x.numel() // 32, dtype=torch.uint8, device=x.device)}
     # measured on Wide-ResNet-101-2 b512: 3,589 / 3,584 img/s with the hand-over vs 3,606 without
     # (same box, one call): the extra fp8 convert in the apply pass costs what the saved read of y
     # gains, so it is opt-in (PSD_FP8_HANDOVER=1)
@@ -62,9 +70,27 @@ def _stats_args(mod, x: torch.Tensor) -> dict:
     return {"part_in": part, "part_rows": rows}
 
 
-def _q8_hand_over(mod, y: torch.Tensor, kw: dict) -> None:
+def _dq8_args(mod, x: torch.Tensor) -> dict:
+    """If ``mod``'s input gradient is the output gradient of an fp8 convolution that runs its
+    bwd-data in fp8 (``_psd_dq8_producer``, wired by the model), the BN's elementwise backward pass
+    also writes the MX e5m2 copy of it (kernels/bn.hip bn_bwd_elemt_kernel DQ): the convolution's own
+    quantise pass (a full read of dY) never runs."""
+    prod = getattr(mod, "_psd_dq8_producer", None)
+    if (prod is None or x.dim() != 4 or x.shape[1] % 32 or not _at.enabled("PSD_FP8_MX")
+            or not _at.enabled("PSD_FP8_MX_HANDOVER") or not prod.psd_fp8_dgrad()):
+        return {}
+    q = torch.empty_like(x, dtype=torch.float8_e5m2, memory_format=torch.channels_last)
+    return {"dq": q, "dqmx": torch.empty(x.numel() // 32, dtype=torch.uint8, device=x.device)}
+
+
+def _dq8_hand_over(mod, dx: torch.Tensor, kw: dict) -> None:
     if kw:
-        mod._psd_q8_consumer._psd_q8_pending = (y, kw["q8_out"], kw["q8_sinv"])
+        mod._psd_dq8_producer._psd_dq8_pending = (dx, kw["dq"], kw["dqmx"])
+
+
+def _q8_hand_over(mod, y: torch.Tensor, kw: dict) -> None:
+    if kw:  # (y, e4m3 copy, its scale: fp32 [1] per-tensor or uint8 [numel / 32] MX)
+        mod._psd_q8_consumer._psd_q8_pending = (y, kw["q8_out"], kw["q8_mx"] if "q8_mx" in kw else kw["q8_sinv"])
 
 
 class StridedDr:
@@ -169,7 +195,9 @@ class _FusedBNFn(torch.autograd.Function):
             # masked gradient g (= the residual-branch gradient for a residual BN): finalize + one
             # elementwise pass here
             g, part, rows = pre
-            dx, dg, db = native().bn_bwd_pre(g, x, w, mean, invstd, part, rows, dgo, dbo)
+            dq8 = _dq8_args(mod, x)
+            dx, dg, db = native().bn_bwd_pre(g, x, w, mean, invstd, part, rows, dgo, dbo, **dq8)
+            _dq8_hand_over(mod, dx, dq8)
             res_grad = None
             if ctx.has_res:
                 if ctx.resid_to is not None:
@@ -180,8 +208,10 @@ class _FusedBNFn(torch.autograd.Function):
         # residual-branch fusion: the identity-path gradient of this BN's output was stashed by the
         # next block's bn3 backward; fold it in here instead of an autograd add kernel
         dy2 = take_dr(mod._psd_pending_dr.pop()) if getattr(mod, "_psd_pending_dr", None) else None
+        dq8 = _dq8_args(mod, x)
         dx, dr, dg, db = native().bn_bwd(dy, x, None, w, mean, invstd, ctx.relu, ctx.has_res, dgo, dbo, dy2, ss,
-                                         mbits)
+                                         mbits, **dq8)
+        _dq8_hand_over(mod, dx, dq8)
         res_grad = None
         if ctx.has_res:
             if ctx.resid_to is not None:

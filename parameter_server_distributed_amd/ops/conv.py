@@ -131,6 +131,19 @@ def _q_weight(mod, w2: torch.Tensor):
     return _q8(w2)
 
 
+def _take_dq8(mod, dy: torch.Tensor):
+    """The MX e5m2 copy of ``dy`` the consumer BN's backward pass wrote for this module (ops/bn.py
+    _dq8_args): (q [N, C, H, W] channels_last, uint8 scales), or None. Consumed once."""
+    pend = getattr(mod, "_psd_dq8_pending", None) if mod is not None else None
+    if pend is None:
+        return None
+    mod._psd_dq8_pending = None
+    d, q, sc = pend
+    if d.data_ptr() != dy.data_ptr() or d.shape != dy.shape or d.stride() != dy.stride():
+        return None
+    return q, sc
+
+
 def _take_q8(mod, x: torch.Tensor):
     """The e4m3 copy of ``x`` that the producing BN's apply pass wrote for this module (ops/bn.py,
     delayed scaling with this module's activation scaler), as (q [N, C, H, W] channels_last,
@@ -500,7 +513,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         if fp8 and _fp8_ok(cin, cout):
             # fp8 forward: e4m3 operands on the MX-scaled MFMA (2x the bf16 rate), dequantised in the
             # epilogue; the weight gradient runs on the saved bf16 x and W
-            got = None if _mx_on() else _take_q8(mod, x)
+            got = _take_q8(mod, x)
             if got is not None:  # quantised by the producing BN's apply pass
                 xq, sx = got[0].permute(0, 2, 3, 1).reshape(n * h * w, cin), got[1]
             else:
@@ -559,7 +572,11 @@ class _Conv1x1Fn(torch.autograd.Function):
         args = (None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1)
         if need_x and ctx.fp8 and _fp8_ok(cout, cin) and _at.enabled("PSD_FP8_DGRAD"):
             # fp8 bwd-data: e5m2 dY (K-major [M, cout]) x e4m3 W^T ([cin, cout], K-major)
-            dyq, sdy = _q_act(_as_2d(dy), e5m2=True, scaler=ctx.f8[1])
+            got = _take_dq8(ctx.mod, dy) if _mx_on() else None
+            if got is not None:  # written by the consumer BN's backward pass
+                dyq, sdy = got[0].permute(0, 2, 3, 1).reshape(n * h * w, cout), got[1]
+            else:
+                dyq, sdy = _q_act(_as_2d(dy), e5m2=True, scaler=ctx.f8[1])
             wtq, swt = _q_act(weight.reshape(cout, cin).t().contiguous())
             out = torch.empty(n * h * w, cin, device=dy.device, dtype=dy.dtype)
             _native().gemm_fp8_(dyq, wtq, sdy, swt, out)
@@ -647,6 +664,11 @@ class Conv1x1(nn.Conv2d):
     def psd_fp8_consumes(self, cin: int) -> bool:
         """True when this module's forward quantises its input (so a producer may do it instead)."""
         return self.fp8 and _fp8_ok(cin, self.out_channels) and _enabled()
+
+    def psd_fp8_dgrad(self) -> bool:
+        """True when this module's bwd-data runs in fp8 (quantising its output gradient)."""
+        return (self.fp8 and _fp8_ok(self.out_channels, self.in_channels) and _enabled()
+                and _at.enabled("PSD_FP8_DGRAD"))
 
     def forward(self, x):
         if (_enabled() and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
@@ -755,7 +777,7 @@ class _ConvFn(torch.autograd.Function):
         if fp8 and cin % 128 == 0 and _fp8_ok(k * k * cin, cout):
             w2 = weight.permute(0, 2, 3, 1).reshape(cout, k * k * cin)
             y = _igemm_fp8(x, w2 if w2.is_contiguous() else w2.contiguous(), k, stride, pad, scaler=f8[0],
-                           pre=None if _mx_on() else _take_q8(mod, x), mod=mod)
+                           pre=_take_q8(mod, x), mod=mod)
             if y is not None:
                 return y
 
@@ -805,7 +827,8 @@ class _ConvFn(torch.autograd.Function):
                     and _fp8_ok(k * k * cout, cin) and _at.enabled("PSD_FP8_DGRAD"):
                 # fp8 bwd-data: e5m2 dY gathered by the implicit GEMM, e4m3 flipped weights
                 wf = weight.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, k * k * cout).contiguous()
-                dx = _igemm_fp8(dy, wf, k, 1, pad, e5m2=True, scaler=ctx.f8[1])
+                got = _take_dq8(ctx.mod, dy) if _mx_on() else None
+                dx = _igemm_fp8(dy, wf, k, 1, pad, e5m2=True, scaler=ctx.f8[1], pre=got)
                 if dx is None:
                     dx = miopen()
             elif stride == 1 and (_igemm_ok(cout, cin) or _psdn_ok(cout, cin)) and 2 * pad == k - 1:
@@ -887,6 +910,13 @@ class ConvNHWC(nn.Conv2d):
 
     def psd_direct_grad_params(self):
         return [self.weight]
+
+    def psd_fp8_dgrad(self) -> bool:
+        """True when this module's stride-1 bwd-data runs in fp8 (implicit GEMM on e5m2 dY)."""
+        k, cin, cout = self.kernel_size[0], self.in_channels, self.out_channels
+        return (self.fp8 and self.stride[0] == 1 and 2 * self.padding[0] == k - 1 and _igemm_ok(cout, cin)
+                and cout % 128 == 0 and _fp8_ok(k * k * cout, cin) and _enabled() and _at.enabled("PSD_FP8_DGRAD")
+                and _at.enabled("PSD_CONV_IGEMM"))
 
     def psd_fp8_consumes(self, cin: int) -> bool:
         k = self.kernel_size[0]

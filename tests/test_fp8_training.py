@@ -86,6 +86,7 @@ def test_bn_apply_writes_the_consumers_fp8_input(gpu, monkeypatch):
     from parameter_server_distributed_amd.ops.conv import Conv1x1, DelayedScale
 
     monkeypatch.setenv("PSD_FP8_HANDOVER", "1")
+    monkeypatch.setenv("PSD_FP8_MX", "0")  # (the per-tensor delayed-scaling hand-over)
     torch.manual_seed(2)
     bn = FusedBatchNorm2d(256, relu=True).to(gpu)
     bn.weight.data = bn.weight.data.to(torch.bfloat16)
@@ -129,3 +130,60 @@ def test_delayed_scale_recovers_from_zero_history(gpu, e5m2):
     assert rel < (0.15 if e5m2 else 0.08), rel
     q2, sinv2 = sc.quantize(x, e5m2)  # now a valid delayed history: the same scale as just-in-time
     assert float((q2.float() * sinv2 - x.float()).norm() / x.float().norm()) < (0.15 if e5m2 else 0.08)
+
+
+def test_bn_apply_writes_the_consumers_mx_input(gpu):
+    """MX hand-over: a ReLU BN feeding an fp8 convolution writes the e4m3 copy of its output with one
+    E8M0 scale per 32 channels in the apply pass -- bit-equal to quantising the stored output with
+    quant_mx_ (the consumer's own pass, which then never runs)."""
+    from parameter_server_distributed_amd.ops import quantize_mx
+    from parameter_server_distributed_amd.ops.bn import FusedBatchNorm2d
+    from parameter_server_distributed_amd.ops.conv import Conv1x1
+
+    torch.manual_seed(2)
+    for res in (False, True):
+        bn = FusedBatchNorm2d(256, relu=True).to(gpu)
+        bn.weight.data = (0.5 + torch.rand(256, device=gpu)).to(torch.bfloat16)
+        bn.bias.data = (0.2 * torch.randn(256, device=gpu)).to(torch.bfloat16)
+        cons = Conv1x1(256, 512, fp8=True).to(gpu, torch.bfloat16).to(memory_format=torch.channels_last)
+        object.__setattr__(bn, "_psd_q8_consumer", cons)
+        x = (torch.randn(4, 256, 14, 14, device=gpu) * 3).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        x.requires_grad_(True)
+        r = torch.randn_like(x).requires_grad_(True) if res else None
+        y = bn(x, r)
+        pend = cons._psd_q8_pending
+        assert pend is not None and pend[0].data_ptr() == y.data_ptr() and pend[2].dtype == torch.uint8
+        q, s = quantize_mx(y.detach().permute(0, 2, 3, 1).contiguous())
+        assert torch.equal(pend[2], s)
+        assert torch.equal(pend[1].permute(0, 2, 3, 1).contiguous().view(torch.uint8).flatten(),
+                           q.view(torch.uint8).flatten())
+
+
+def test_bn_backward_writes_the_producers_mx_dy(gpu):
+    """MX backward hand-over: a BN whose input came from an fp8 convolution writes the e5m2 copy of
+    its input gradient (one E8M0 scale per 32 channels) in its elementwise backward pass -- bit-equal
+    to quantising the stored gradient with quant_mx_ -- for the convolution's fp8 bwd-data."""
+    from parameter_server_distributed_amd.ops import quantize_mx
+    from parameter_server_distributed_amd.ops.bn import FusedBatchNorm2d
+    from parameter_server_distributed_amd.ops.conv import Conv1x1
+
+    torch.manual_seed(3)
+    bn = FusedBatchNorm2d(256, relu=True).to(gpu)
+    bn.weight.data = (0.5 + torch.rand(256, device=gpu)).to(torch.bfloat16)
+    bn.bias.data = (0.2 * torch.randn(256, device=gpu)).to(torch.bfloat16)
+    prod = Conv1x1(256, 256, fp8=True).to(gpu, torch.bfloat16).to(memory_format=torch.channels_last)
+    assert prod.psd_fp8_dgrad()
+    object.__setattr__(bn, "_psd_dq8_producer", prod)
+    x = (torch.randn(4, 256, 14, 14, device=gpu) * 2).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    xi = x * 1.0  # a non-leaf input: its gradient reaches the hook as the BN's own dx tensor
+    seen = []
+    xi.register_hook(lambda g: seen.append(g))
+    y = bn(xi)
+    y.backward(torch.randn_like(y))
+    pend = prod._psd_dq8_pending
+    assert pend is not None and pend[0].data_ptr() == seen[0].data_ptr()
+    q, s = quantize_mx(seen[0].permute(0, 2, 3, 1).contiguous(), e5m2=True)
+    assert torch.equal(pend[2], s)
+    assert torch.equal(pend[1].permute(0, 2, 3, 1).contiguous().view(torch.uint8).flatten(),
+                       q.view(torch.uint8).flatten())
