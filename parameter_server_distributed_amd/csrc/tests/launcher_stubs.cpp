@@ -29,4 +29,10 @@ hipError_t launch_quant_fp8_delayed(const void*, int32_t, int64_t, float*, float
 hipError_t launch_dequant_fp8(const uint8_t*, int64_t, const float*, void*, int32_t, hipStream_t) {
   return hipErrorNotSupported;
 }
+hipError_t launch_quant_mx(const void*, int32_t, int64_t, int, uint8_t*, uint8_t*, hipStream_t) {
+  return hipErrorNotSupported;
+}
+hipError_t launch_dequant_mx(const uint8_t*, const uint8_t*, int64_t, void*, int32_t, hipStream_t) {
+  return hipErrorNotSupported;
+}
 }  // namespace psd
