@@ -71,15 +71,22 @@ PYBIND11_MODULE(_C, m) {
         py::arg("dy2") = py::none(), py::arg("ss") = py::none(), py::arg("mbits") = py::none(),
         py::arg("dq") = py::none(), py::arg("dqmx") = py::none());
   m.def("gemm_", &gemm_, py::arg("A"), py::arg("B"), py::arg("a_kmajor"), py::arg("b_kmajor"), py::arg("out"),
-        py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("aux") = py::none());
+        py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("aux") = py::none(), py::arg("part") = py::none(),
+        py::arg("shift") = py::none());
+  m.def("gemm_stats_rows", &gemm_stats_rows_, py::arg("M"));
   m.def("gemm_splitk_", &gemm_splitk_, py::arg("A"), py::arg("B"), py::arg("a_kmajor"), py::arg("b_kmajor"),
         py::arg("out"), py::arg("accumulate") = false, py::arg("scale") = 1.0, py::arg("splits") = 0);
   m.def("gemm_fp8_", &gemm_fp8_, py::arg("A"), py::arg("B"), py::arg("a_scale"), py::arg("b_scale"), py::arg("out"),
-        py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("aux") = py::none());
+        py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("aux") = py::none(), py::arg("part") = py::none(),
+        py::arg("shift") = py::none());
   m.def("convn_", &convn_, py::arg("x"), py::arg("w2"), py::arg("out"), py::arg("R"), py::arg("S"), py::arg("stride"),
         py::arg("pad"), py::arg("part") = py::none(), py::arg("shift") = py::none(), py::arg("variant") = -1,
         py::arg("x2") = py::none(), py::arg("bias") = py::none());
   m.def("convn_stats_rows", &convn_stats_rows_, py::arg("M"));
+  m.def("convn_part_rows", &convn_part_rows_, py::arg("M"), py::arg("N"), py::arg("variant"), py::arg("Ho"),
+        py::arg("Wo"), py::arg("R"));
+  m.def("convn_variant_ok", &convn_variant_ok_, py::arg("N"), py::arg("variant"), py::arg("R"), py::arg("S"),
+        py::arg("stride"), py::arg("pad"), py::arg("Wo"), py::arg("has_x2") = false);
   m.def("convn_bwd_", &convn_bwd_, py::arg("dy"), py::arg("w2"), py::arg("out"), py::arg("R"), py::arg("S"),
         py::arg("stride"), py::arg("pad"), py::arg("part"), py::arg("variant"), py::arg("mode"), py::arg("bx"),
         py::arg("bmean"), py::arg("bss") = py::none(), py::arg("bdr") = py::none(), py::arg("bmbits") = py::none(),
@@ -90,7 +97,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("dbeta_out") = py::none(), py::arg("dq") = py::none(), py::arg("dqmx") = py::none());
   m.def("convn_variants", &convn_variants_, py::arg("N"));
   m.def("conv_fwd_", &conv_fwd_, py::arg("x"), py::arg("w2"), py::arg("out"), py::arg("R"), py::arg("S"),
-        py::arg("stride"), py::arg("pad"));
+        py::arg("stride"), py::arg("pad"), py::arg("part") = py::none(), py::arg("shift") = py::none());
   m.def("conv_wgrad_", &conv_wgrad_, py::arg("dy"), py::arg("x"), py::arg("out"), py::arg("R"), py::arg("S"),
         py::arg("stride"), py::arg("pad"), py::arg("splits") = 0);
   m.def("convw_", &convw_, py::arg("dy"), py::arg("x"), py::arg("out"), py::arg("R"), py::arg("S"), py::arg("stride"),
@@ -106,7 +113,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("accumulate") = false);
   m.def("convw_variants", &convw_variants_, py::arg("Cout"), py::arg("KK"));
   m.def("conv_fwd_fp8_", &conv_fwd_fp8_, py::arg("x"), py::arg("w2"), py::arg("x_scale"), py::arg("w_scale"),
-        py::arg("out"), py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"));
+        py::arg("out"), py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("part") = py::none(),
+        py::arg("shift") = py::none());
   m.def("gelu_bwd_colsum_", &gelu_bwd_colsum_, py::arg("dy"), py::arg("pre"), py::arg("dx"), py::arg("out"),
         py::arg("accumulate") = false);
   m.def("colsum_", &colsum_, py::arg("x"), py::arg("out"), py::arg("accumulate") = false);

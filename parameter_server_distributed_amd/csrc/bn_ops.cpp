@@ -749,7 +749,7 @@ std::vector<at::Tensor> bnfold_dgrad_weights(const at::Tensor& w_in, const at::T
                                     reinterpret_cast<uint16_t*>(bw.data_ptr()), bvec.data_ptr<float>(), stream_of(w));
   TORCH_CHECK(e == hipSuccess, "psd bnfold prep: ", hipGetErrorString(e));
   // M = (B o W)^T W (Cin x Cin, symmetric) into the right block of w2 (the MFMA GEMM, TN layout)
-  gemm_(bw, w, false, false, w2.narrow(1, Cout, Cin), c10::nullopt, 0, c10::nullopt);
+  gemm_(bw, w, false, false, w2.narrow(1, Cout, Cin), c10::nullopt, 0, c10::nullopt, c10::nullopt, c10::nullopt);
   return {w2, bvec};
 }
 

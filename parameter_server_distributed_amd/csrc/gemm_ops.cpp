@@ -1,5 +1,7 @@
 // Tensor glue for the MFMA GEMM (kernels/gemm.hip).
 #include <ATen/ATen.h>
+
+#include <algorithm>
 #include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
 
@@ -18,9 +20,32 @@ void chk2d(const at::Tensor& t, const char* n) {
 }
 }  // namespace
 
-// out[M,N] = A op B (+bias)(act). A: a_kmajor ? [M,K] : [K,M]; B: b_kmajor ? [N,K] : [K,N].
-void gemm_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool b_kmajor, at::Tensor out,
-           c10::optional<at::Tensor> bias, int64_t act, c10::optional<at::Tensor> aux) {
+int64_t gemm_stats_rows_(int64_t M) { return (M + 127) / 128 * 2; }
+
+// the consumer BN's statistics partials in the 8-phase epilogue: part fp32 >= gemm_stats_rows(M) x 2 x N,
+// shift fp32 [N] (the BN's running mean)
+static void set_stats(GemmArgs& a, const c10::optional<at::Tensor>& part, const c10::optional<at::Tensor>& shift,
+                      const at::Tensor& out, int* rows) {
+  if (!part.has_value() || !part->defined()) return;
+  const int64_t M = out.size(0), N = out.size(1);
+  TORCH_CHECK(part->scalar_type() == at::kFloat && part->is_contiguous() && part->device() == out.device() &&
+                  part->numel() >= gemm_stats_rows_(M) * 2 * N,
+              "psd gemm: part must be fp32 contiguous with >= gemm_stats_rows(M) x 2 x N elements");
+  TORCH_CHECK(shift.has_value() && shift->defined() && shift->scalar_type() == at::kFloat && shift->is_contiguous() &&
+                  shift->numel() == N && shift->device() == out.device(),
+              "psd gemm: statistics need shift fp32 [N]");
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16, "psd gemm: statistics need a bf16 output");
+  a.part = part->data_ptr<float>();
+  a.shift = shift->data_ptr<float>();
+  a.rows_out = rows;
+}
+
+// out[M,N] = A op B (+bias)(act). A: a_kmajor ? [M,K] : [K,M]; B: b_kmajor ? [N,K] : [K,N]. With
+// part/shift also the consumer BN's statistics partials: returns the partial rows written, 0 when the
+// shape cannot carry them (nothing launched); 1 without statistics.
+int64_t gemm_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool b_kmajor, at::Tensor out,
+              c10::optional<at::Tensor> bias, int64_t act, c10::optional<at::Tensor> aux,
+              c10::optional<at::Tensor> part, c10::optional<at::Tensor> shift) {
   chk2d(A, "A");
   chk2d(B, "B");
   const int64_t M = a_kmajor ? A.size(0) : A.size(1), K = a_kmajor ? A.size(1) : A.size(0);
@@ -50,8 +75,12 @@ void gemm_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool b_kmajo
   a.b_kmajor = b_kmajor;
   a.act = (int)act;
   a.c_f32 = out.scalar_type() == at::kFloat;
+  int rows = 0;
+  set_stats(a, part, shift, out, &rows);
   hipError_t e = launch_gemm(a, stream_of(A));
+  if (a.part && e == hipErrorNotSupported) return 0;
   TORCH_CHECK(e == hipSuccess, "psd gemm: ", hipGetErrorString(e));
+  return a.part ? rows : 1;
 }
 
 // out[M,N] (+)= scale * (A op B) via split-K fp32 slabs (weight gradients: K = tokens).
@@ -85,8 +114,9 @@ void gemm_splitk_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool 
 }
 
 // out[M,N] = (A_q . B_q^T) * a_scale * b_scale (+bias)(act): A [M,K], B [N,K] OCP e4m3fn, K % 128 == 0
-void gemm_fp8_(const at::Tensor& A, const at::Tensor& B, const at::Tensor& a_scale, const at::Tensor& b_scale,
-               at::Tensor out, c10::optional<at::Tensor> bias, int64_t act, c10::optional<at::Tensor> aux) {
+int64_t gemm_fp8_(const at::Tensor& A, const at::Tensor& B, const at::Tensor& a_scale, const at::Tensor& b_scale,
+                  at::Tensor out, c10::optional<at::Tensor> bias, int64_t act, c10::optional<at::Tensor> aux,
+                  c10::optional<at::Tensor> part, c10::optional<at::Tensor> shift) {
   for (const at::Tensor* t : {&A, &B})
     TORCH_CHECK(t->is_cuda() && t->dim() == 2 && t->stride(1) == 1 && t->stride(0) % 16 == 0 &&
                     (reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0,
@@ -136,8 +166,12 @@ void gemm_fp8_(const at::Tensor& A, const at::Tensor& B, const at::Tensor& a_sca
     a.b_scale = b_scale.data_ptr<float>();
   }
   a.f8a = A.scalar_type() == at::kFloat8_e5m2 ? 1 : 0;
+  int rows = 0;
+  set_stats(a, part, shift, out, &rows);
   hipError_t e = launch_gemm_fp8(a, stream_of(A));
+  if (a.part && e == hipErrorNotSupported) return 0;
   TORCH_CHECK(e == hipSuccess, "psd gemm_fp8: ", hipGetErrorString(e));
+  return a.part ? rows : 1;
 }
 
 // Implicit-GEMM NHWC convolution forward on the persistent 8-phase MFMA kernel (no bias/activation):
@@ -145,8 +179,9 @@ void gemm_fp8_(const at::Tensor& A, const at::Tensor& B, const at::Tensor& a_sca
 // 2-D), out [Nb*Ho*Wo, Cout] bf16 (an NHWC output's 2-D view). bf16 operands, or OCP e4m3 ones with
 // per-tensor dequant scales (xs, ws: fp32 device scalars). Returns false (nothing launched) when the
 // shape is outside the kernel's contract -- the caller falls back.
-static bool conv_fwd_impl(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S,
-                          int64_t stride, int64_t pad, const at::Tensor* xs, const at::Tensor* ws) {
+static int64_t conv_fwd_impl(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S,
+                             int64_t stride, int64_t pad, const at::Tensor* xs, const at::Tensor* ws,
+                             const c10::optional<at::Tensor>& part, const c10::optional<at::Tensor>& shift) {
   const bool f8 = xs != nullptr;
   const auto dt = f8 ? at::kFloat8_e4m3fn : at::kBFloat16;
   const bool x_e5 = f8 && x.scalar_type() == at::kFloat8_e5m2;  // bwd-data: e5m2 dY
@@ -176,7 +211,7 @@ static bool conv_fwd_impl(const at::Tensor& x, const at::Tensor& w2, at::Tensor 
   TORCH_CHECK(out.size(0) == M && out.size(1) == Cout, "psd conv_fwd: out must be [Nb*Ho*Wo, Cout]");
   const int64_t xbytes = x.numel() * esz;
   if ((C & (C - 1)) != 0 || C < (f8 ? 128 : 64) || xbytes >= ((int64_t)1 << 32) || M >= ((int64_t)1 << 31))
-    return false;
+    return 0;
   int logc = 0;
   while ((1 << logc) < C) ++logc;
   const c10::DeviceGuard g(x.device());
@@ -209,13 +244,23 @@ static bool conv_fwd_impl(const at::Tensor& x, const at::Tensor& w2, at::Tensor 
     a.b_scale = ws->data_ptr<float>();
     a.f8a = x_e5 ? 1 : 0;
   }
+  int rows = 0;
+  set_stats(a, part, shift, out, &rows);
   hipError_t e = f8 ? launch_conv_fwd_fp8(a, stream_of(x)) : launch_conv_fwd(a, stream_of(x));
-  if (e == hipErrorNotSupported) return false;
+  if (e == hipErrorNotSupported) return 0;
   TORCH_CHECK(e == hipSuccess, "psd conv_fwd: ", hipGetErrorString(e));
-  return true;
+  return a.part ? rows : 1;
 }
 
 int64_t convn_stats_rows_(int64_t M) { return convn_stats_rows((int)M); }
+// partial rows a launch of this variant writes (allocate at least this many: HALO variants tile by rows)
+int64_t convn_part_rows_(int64_t M, int64_t N, int64_t v, int64_t Ho, int64_t Wo, int64_t R) {
+  return convn_part_rows_geo((int)M, (int)N, (int)v, (int)Ho, (int)Wo, (int)R);
+}
+bool convn_variant_ok_(int64_t N, int64_t v, int64_t R, int64_t S, int64_t stride, int64_t pad, int64_t Wo,
+                       bool has_x2) {
+  return convn_variant_ok((int)N, (int)v, (int)R, (int)S, (int)stride, (int)pad, (int)Wo, has_x2);
+}
 int64_t convn_variants_(int64_t N) { return convn_variants((int)N); }
 
 namespace {
@@ -271,8 +316,11 @@ int64_t convn_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_
                     shift->is_contiguous() && shift->device() == x.device(),
                 "psd convn: statistics need an fp32 [Cout] shift on x's device");
     TORCH_CHECK(part->scalar_type() == at::kFloat && part->is_contiguous() && part->device() == x.device() &&
-                    part->numel() >= (int64_t)convn_stats_rows((int)M) * 2 * Cout,
-                "psd convn: part must be fp32 [convn_stats_rows(M), 2, Cout]");
+                    part->numel() >= (int64_t)std::max(convn_stats_rows((int)M),
+                                                       convn_part_rows_geo((int)M, (int)Cout,
+                                                                           (int)std::max<int64_t>(variant, 0), (int)Ho,
+                                                                           (int)Wo, (int)R)) * 2 * Cout,
+                "psd convn: part must be fp32 [convn_part_rows(...), 2, Cout]");
   }
   const int64_t xbytes = x.numel() * 2, wbytes = w2.numel() * 2;
   if ((C & (C - 1)) != 0 || C < 64 || xbytes > 0xFFFFFF00ll || wbytes >= ((int64_t)1 << 32) ||
@@ -307,7 +355,8 @@ int64_t convn_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_
   const hipError_t e = launch_convn(a, c10::hip::getCurrentHIPStream(x.device().index()).stream());
   if (e == hipErrorNotSupported) return 0;
   TORCH_CHECK(e == hipSuccess, "psd convn: ", hipGetErrorString(e));
-  return stats ? convn_part_rows((int)M, (int)Cout, (int)variant) : 1;
+  return stats ? convn_part_rows_geo((int)M, (int)Cout, (int)std::max<int64_t>(variant, 0), (int)Ho, (int)Wo, (int)R)
+               : 1;
 }
 
 // bwd-data on the narrow kernel with the producing BN's backward reduction in the epilogue
@@ -345,8 +394,10 @@ int64_t convn_bwd_(const at::Tensor& dy, const at::Tensor& w2, at::Tensor out, i
   like_out(bx, "bx");
   TORCH_CHECK(bmean.scalar_type() == at::kFloat && bmean.numel() == N && bmean.is_contiguous(), "psd convn_bwd: bmean");
   TORCH_CHECK(part.scalar_type() == at::kFloat && part.is_contiguous() &&
-                  part.numel() >= (int64_t)convn_stats_rows((int)M) * 2 * N,
-              "psd convn_bwd: part must be fp32 [convn_stats_rows(M), 2, N]");
+                  part.numel() >= (int64_t)std::max(convn_stats_rows((int)M),
+                                                    convn_part_rows_geo((int)M, (int)N, (int)std::max<int64_t>(variant, 0),
+                                                                        (int)Ho, (int)Wo, (int)R)) * 2 * N,
+              "psd convn_bwd: part must be fp32 [convn_part_rows(...), 2, N]");
   if (mode == 1) {
     TORCH_CHECK(bss.has_value() && bss->defined() && bss->numel() == 2 * N && bss->scalar_type() == at::kFloat &&
                     bss->is_contiguous(),
@@ -417,17 +468,18 @@ int64_t convn_bwd_(const at::Tensor& dy, const at::Tensor& w2, at::Tensor out, i
   const hipError_t e = launch_convn(a, c10::hip::getCurrentHIPStream(dy.device().index()).stream());
   if (e == hipErrorNotSupported) return 0;
   TORCH_CHECK(e == hipSuccess, "psd convn_bwd: ", hipGetErrorString(e));
-  return convn_part_rows((int)M, (int)N, (int)variant);
+  return convn_part_rows_geo((int)M, (int)N, (int)std::max<int64_t>(variant, 0), (int)Ho, (int)Wo, (int)R);
 }
 
-bool conv_fwd_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride,
-               int64_t pad) {
-  return conv_fwd_impl(x, w2, out, R, S, stride, pad, nullptr, nullptr);
+int64_t conv_fwd_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride,
+                  int64_t pad, c10::optional<at::Tensor> part, c10::optional<at::Tensor> shift) {
+  return conv_fwd_impl(x, w2, out, R, S, stride, pad, nullptr, nullptr, part, shift);
 }
 
-bool conv_fwd_fp8_(const at::Tensor& x, const at::Tensor& w2, const at::Tensor& x_scale, const at::Tensor& w_scale,
-                   at::Tensor out, int64_t R, int64_t S, int64_t stride, int64_t pad) {
-  return conv_fwd_impl(x, w2, out, R, S, stride, pad, &x_scale, &w_scale);
+int64_t conv_fwd_fp8_(const at::Tensor& x, const at::Tensor& w2, const at::Tensor& x_scale, const at::Tensor& w_scale,
+                      at::Tensor out, int64_t R, int64_t S, int64_t stride, int64_t pad, c10::optional<at::Tensor> part,
+                      c10::optional<at::Tensor> shift) {
+  return conv_fwd_impl(x, w2, out, R, S, stride, pad, &x_scale, &w_scale, part, shift);
 }
 
 // Implicit-GEMM convolution weight gradient: out [Cout, R*S*C] (an OHWI weight viewed 2-D, bf16) =

@@ -37,6 +37,14 @@
 //     shift: a load issued in the epilogue of a one-K-tile convolution is pure exposed latency).
 // The same kernel runs a stride-1 bwd-data (conv of dY with the flipped, transposed weights) and
 // a 1x1 bwd-data (dY . W as a 1x1 conv of dY with W^T).
+//
+// HALO variants (stride-1 RxR convolutions, pad R/2, Wo + R - 1 <= 64): gathering every K-tile's
+// A rows re-reads each input pixel R*R times through L2 (layer1's 3x3: 9 x 0.41 GB per pass, the
+// L2 -> LDS stream was the limit: ~550 us for 0.82 GB of HBM traffic). A HALO tile is RPT = BM / SW
+// whole output rows of one image, each padded to SW slots (SW = 16 / 32 / 64 >= Wo + R - 1); per
+// 64-channel block the (RPT + R - 1) x SW input window -- zero-padded by the out-of-range DMA --
+// is staged once and all R*R taps read their A fragments from it at row offset (r * SW + s). Only
+// the weight tiles stream through the ring. Slots past Wo compute garbage that is never stored.
 #include "common.h"
 #include "launchers_convn.h"
 
@@ -69,6 +77,17 @@ template <int N>
 __device__ __forceinline__ void wait_vm() {
   static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// wait until at most `ahead` K-tiles (DPSK loads each) of this wave are still in flight
+template <int DPSK, int A>
+__device__ __forceinline__ void wait_ahead(int ahead) {
+  if constexpr (A <= 0) {
+    wait_vm<0>();
+  } else {
+    if (ahead >= A) wait_vm<A * DPSK>();
+    else wait_ahead<DPSK, A - 1>(ahead);
+  }
 }
 
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
@@ -125,12 +144,13 @@ struct Geo {
   static constexpr int AB = BM * 128;        // A bytes per K-tile
   static constexpr int SLOT = AB + BN * 128;
   static constexpr int STG = 2048;           // per-wave epilogue staging (16 rows x <= 128 B)
-  static constexpr int LDS_MAX = NSLOT * SLOT + NW * STG;
   static_assert((BM / 8) % NW == 0 && (BN / 8) % NW == 0 && APW >= 1 && BPW >= 1, "DMA pieces per wave");
-  static_assert(DPS * (NSLOT - 2) < 64, "vmcnt is 6 bits");
-  static_assert(LDS_MAX <= 160 * 1024, "LDS");
+  static_assert(DPS * (NSLOT - 2) < 64, "vmcnt is 6 bits");  // (the LDS bound: convn_launch_t)
   static_assert(WNT == 32 || WNT == 64, "wave tile width");
 };
+
+// HALO window bytes: (rpt + R - 1) * sw rows + 2 overrun rows, bounded for R <= 3, sw <= 64
+constexpr int halo_win_bytes(int bm) { return (bm + 2 * 64 + 8) * 128; }
 
 }  // namespace
 
@@ -145,13 +165,29 @@ struct Geo {
 // (h, w) only: the zero-filled full-size gradient is never written).
 // 3: as 2 for a bottleneck tail relu(bn3(x) + bnd(xd)) (the downsample block's dual BN, whose
 // upstream gradient g is shared): part_d also receives sum g and sum g (xd - mean_d) for bnd.
-template <int BM, int BN, int WNT, int NSLOT, bool STATS, int BWD = 0>
+template <int BM, int BN, int WNT, int NSLOT, bool STATS, int BWD = 0, bool HALO = false>
 __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
   using G = Geo<BM, BN, WNT, NSLOT>;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int tiles_m = gridDim.x;
   const int tm = xcd_remap(blockIdx.x, tiles_m);
   const int m0 = tm * BM, n0 = blockIdx.y * BN;
+  // HALO geometry: tile = RPT output rows (ho0 ..) of image hn, SW slots per row
+  constexpr int SLOTB = HALO ? BN * 128 : G::SLOT;  // ring slot bytes (HALO: weights only)
+  const int lsw = a.log_sw, sw = 1 << lsw;
+  const int rpt = BM >> lsw;
+  const int tpi = HALO ? (a.Ho + rpt - 1) / rpt : 1;
+  const int hn = HALO ? tm / tpi : 0, ho0 = HALO ? (tm - hn * tpi) * rpt : 0;
+  uint8_t* win = smem + a.nslot * SLOTB;
+  // output pixel of tile row p (-1: past M / a padding slot)
+  auto pix = [&](int p) -> int {
+    if constexpr (HALO) {
+      const int j = p >> lsw, wo = p & (sw - 1);
+      return (wo < a.Wo && ho0 + j < a.Ho) ? (hn * a.Ho + ho0 + j) * a.Wo + wo : -1;
+    } else {
+      return m0 + p < a.M ? m0 + p : -1;
+    }
+  };
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wid / G::NWC, wc = wid % G::NWC;
@@ -170,7 +206,7 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
   // this lane's A rows (one per DMA piece): window origin p0 = top-left input pixel index,
   // hw = (h0 << 16) | (w0 & 0xffff); rows past M get h0 = -32768 (never in the image)
   int p0[G::APW], hw[G::APW];
-  {
+  if constexpr (!HALO) {
     const int howo = a.Ho * a.Wo;
 #pragma unroll
     for (int i = 0; i < G::APW; ++i) {
@@ -189,10 +225,13 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
   const int cmask = (1 << a.logC) - 1;
   const int nslot = a.nslot;  // ring depth of this launch: min(NSLOT, K-tiles)
 
+  const int ntap = a.R * a.S;
   auto stage = [&](int t) {
-    uint8_t* slot = smem + (t % nslot) * G::SLOT;
-    const int k0 = t * kBK;
-    if (k0 >= a.K1) {  // K-concatenated second operand (1x1: the row is the output pixel itself)
+    uint8_t* slot = smem + (t % nslot) * SLOTB;
+    // HALO: K-tile t = (channel block t / taps, tap t % taps); the weight row offset of that tap
+    const int k0 = HALO ? (t % ntap) * (1 << a.logC) + (t / ntap) * kBK : t * kBK;
+    if constexpr (HALO) {
+    } else if (k0 >= a.K1) {  // K-concatenated second operand (1x1: the row is the output pixel itself)
       const int c0 = k0 - a.K1;
 #pragma unroll
       for (int i = 0; i < G::APW; ++i) {
@@ -228,8 +267,25 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
       const int kc = (lane & 7) ^ ((row >> 1) & 7);
       const uint32_t off = ((uint32_t)(n0 + row) * (uint32_t)a.K + (uint32_t)(k0 + kc * 8)) * 2u;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs,
-                                               (__attribute__((address_space(3))) void*)(slot + G::AB + piece * 1024),
+                                               (__attribute__((address_space(3))) void*)(slot + (SLOTB - BN * 128) +
+                                                                                        piece * 1024),
                                                16, off, 0, 0, 0);
+    }
+  };
+
+  // HALO: the (rpt + R - 1) x sw input window of channel block cb (zero outside the image)
+  auto stage_window = [&](int cb) {
+    const int pieces = ((rpt + a.R - 1) << lsw) >> 3;
+    for (int pc = wid; pc < pieces; pc += G::NW) {
+      const int row = pc * 8 + (lane >> 3);
+      const int jj = row >> lsw, ws = row & (sw - 1);
+      const int hi = ho0 - a.pad + jj, wi = ws - a.pad;
+      const int kc = (lane & 7) ^ ((row >> 1) & 7);
+      const bool ok = (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+      const uint32_t off =
+          ok ? ((((uint32_t)((hn * a.H + hi) * a.W + wi)) << a.logC) + (uint32_t)(cb * kBK + kc * 8)) * 2u : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(win + pc * 1024), 16, off,
+                                               0, 0, 0);
     }
   };
 
@@ -242,29 +298,42 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
   const int nt = a.K / kBK;
   const int D = nslot - 1 > 0 ? nslot - 1 : 1;  // K-tiles issued ahead
   for (int p = 0; p < D && p < nt; ++p) stage(p);
+  constexpr int DPSK = HALO ? G::BPW : G::DPS;  // this wave's DMA per K-tile
   for (int t = 0; t < nt; ++t) {
-    // K-tile t landed (this wave's DMA): leave the (up to D-1) later K-tiles in flight
-    const int ahead = min(nt - 1 - t, D - 1);
-    if constexpr (NSLOT >= 4) {
-      if (ahead >= 2) wait_vm<2 * G::DPS>();
-      else if (ahead == 1) wait_vm<G::DPS>();
-      else wait_vm<0>();
+    if (HALO && t % ntap == 0) {
+      // a new channel block: every wave is done with the old window, then stage the new one and
+      // drain (the in-flight weight tiles land with it)
+      if (t > 0) __builtin_amdgcn_s_barrier();
+      stage_window(t / ntap);
+      wait_vm<0>();
     } else {
-      if (ahead >= 1) wait_vm<G::DPS>();
-      else wait_vm<0>();
+      // K-tile t landed (this wave's DMA): leave the (up to D-1) later K-tiles in flight
+      wait_ahead<DPSK, NSLOT - 2>(min(nt - 1 - t, D - 1));
     }
     __builtin_amdgcn_s_barrier();  // every wave: tile t published, tile t-1 no longer read
     __builtin_amdgcn_sched_barrier(0);
     if (t + D < nt) stage(t + D);
-    const uint8_t* As = smem + (t % nslot) * G::SLOT;
-    const uint8_t* Bs = As + G::AB;
+    const uint8_t* As = smem + (t % nslot) * SLOTB;
+    const uint8_t* Bs = As + (SLOTB - BN * 128);
+    const int tap = HALO ? t % ntap : 0;
+    const int tr = HALO ? tap / a.S : 0, ts = HALO ? tap - tr * a.S : 0;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 af[4], bf[G::JN];
 #pragma unroll
       for (int j = 0; j < G::JN; ++j) bf[j] = frag(Bs, wc * G::JN + j, ks, lane);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = frag(As, wr * 4 + i, ks, lane);
+      for (int i = 0; i < 4; ++i) {
+        if constexpr (HALO) {
+          // slot p of the tile reads window row (p / sw + r) * sw + p % sw + s
+          const int p = (wr * 4 + i) * 16 + (lane & 15);
+          const int row = (((p >> lsw) + tr) << lsw) + (p & (sw - 1)) + ts;
+          af[i] = __builtin_bit_cast(bf16x8,
+                                     *reinterpret_cast<const u32x4*>(win + kmaj_off(row, ks * 4 + (lane >> 4))));
+        } else {
+          af[i] = frag(As, wr * 4 + i, ks, lane);
+        }
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -292,7 +361,7 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float d = bf16_to_f32(f32_to_bf16(acc[i][j][r])) - kshift[j];
-          const bool ok = m0 + wr * 64 + i * 16 + rq + r < a.M;
+          const bool ok = pix(wr * 64 + i * 16 + rq + r) >= 0;
           s1 += ok ? d : 0.f;
           s2 = ok ? fmaf(d, d, s2) : s2;
         }
@@ -308,7 +377,7 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
       }
     }
   }
-  uint8_t* stg = smem + a.nslot * G::SLOT + wid * G::STG;
+  uint8_t* stg = smem + a.nslot * SLOTB + (HALO ? halo_win_bytes(BM) : 0) + wid * G::STG;
   const int L = cl & 3;
   constexpr int RB = WNT * 2;       // staged row bytes (one 16-row block)
   constexpr int CPR = RB / 16;      // 16-byte chunks per staged row
@@ -351,8 +420,8 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
       const int rr = c / CPR, c16 = c % CPR;
       const int off = rr * RB + (((2 * c16) ^ ((rr & 7) << 1)) & (RB / 8 - 1)) * 8;
       u32x4 v = *reinterpret_cast<const u32x4*>(stg + off);
-      const int m = m0 + wr * 64 + i * 16 + rr;
-      if (m < a.M) {
+      const int m = pix(wr * 64 + i * 16 + rr);
+      if (m >= 0) {
         const int64_t go = (int64_t)m * a.ldc + n0 + wc * WNT + c16 * 8;
         if constexpr (BWD != 0) {
           float d[8], xv[8];
@@ -438,33 +507,42 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
 }
 
 // ------------------------------------------------------------------ host side
-template <int BM, int BN, int WNT, int NSLOT, bool STATS, int BWD>
+template <int BM, int BN, int WNT, int NSLOT, bool STATS, int BWD, bool HALO>
 static hipError_t convn_launch_t(const ConvnArgs& a0, hipStream_t st) {
   using G = Geo<BM, BN, WNT, NSLOT>;
+  constexpr int SLOTB = HALO ? BN * 128 : G::SLOT;
+  constexpr int WINB = HALO ? halo_win_bytes(BM) : 0;
+  constexpr int LDS_MAX = NSLOT * SLOTB + WINB + G::NW * G::STG;
+  static_assert(LDS_MAX <= 160 * 1024, "LDS");
   static bool attr = false;
   if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)convn_kernel<BM, BN, WNT, NSLOT, STATS, BWD>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_MAX);
+    const hipError_t e = hipFuncSetAttribute((const void*)convn_kernel<BM, BN, WNT, NSLOT, STATS, BWD, HALO>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     if (e != hipSuccess) return e;
     attr = true;
   }
   ConvnArgs a = a0;
   const int nt = a.K / kBK;
   a.nslot = nt < NSLOT ? (nt < 2 ? 1 : nt) : NSLOT;
-  const int lds = a.nslot * G::SLOT + G::NW * G::STG;
-  const int tiles_m = (a.M + BM - 1) / BM;
-  hipLaunchKernelGGL((convn_kernel<BM, BN, WNT, NSLOT, STATS, BWD>), dim3(tiles_m, a.N / BN), dim3(G::NT), lds, st, a);
+  const int lds = a.nslot * SLOTB + WINB + G::NW * G::STG;
+  int tiles_m = (a.M + BM - 1) / BM;
+  if (HALO) {
+    const int rpt = BM >> a.log_sw;
+    tiles_m = (a.M / (a.Ho * a.Wo)) * ((a.Ho + rpt - 1) / rpt);
+  }
+  hipLaunchKernelGGL((convn_kernel<BM, BN, WNT, NSLOT, STATS, BWD, HALO>), dim3(tiles_m, a.N / BN), dim3(G::NT), lds,
+                     st, a);
   return hipGetLastError();
 }
 
-template <int BM, int BN, int WNT, int NSLOT>
+template <int BM, int BN, int WNT, int NSLOT, bool HALO = false>
 static hipError_t convn_launch_s(const ConvnArgs& a, hipStream_t st) {
-  if (a.bwd == 1) return convn_launch_t<BM, BN, WNT, NSLOT, false, 1>(a, st);
-  if (a.bwd == 2) return convn_launch_t<BM, BN, WNT, NSLOT, false, 2>(a, st);
-  if (a.bwd == 3) return convn_launch_t<BM, BN, WNT, NSLOT, false, 3>(a, st);
-  if (a.bwd == 5) return convn_launch_t<BM, BN, WNT, NSLOT, false, 5>(a, st);
-  return a.part ? convn_launch_t<BM, BN, WNT, NSLOT, true, 0>(a, st)
-                : convn_launch_t<BM, BN, WNT, NSLOT, false, 0>(a, st);
+  if (a.bwd == 1) return convn_launch_t<BM, BN, WNT, NSLOT, false, 1, HALO>(a, st);
+  if (a.bwd == 2) return convn_launch_t<BM, BN, WNT, NSLOT, false, 2, HALO>(a, st);
+  if (a.bwd == 3) return convn_launch_t<BM, BN, WNT, NSLOT, false, 3, HALO>(a, st);
+  if (a.bwd == 5) return convn_launch_t<BM, BN, WNT, NSLOT, false, 5, HALO>(a, st);
+  return a.part ? convn_launch_t<BM, BN, WNT, NSLOT, true, 0, HALO>(a, st)
+                : convn_launch_t<BM, BN, WNT, NSLOT, false, 0, HALO>(a, st);
 }
 
 int convn_tile_n(int N) {
@@ -474,8 +552,13 @@ int convn_tile_n(int N) {
   return 0;
 }
 
-// variants (tile geometry) per output width; a.variant < 0 picks the default
-static int convn_variant_count(int bn) { return bn == 256 ? 2 : 4; }
+// variants (tile geometry) per output width: the gathered ones, then the HALO ones
+static int plain_count(int bn) { return bn == 256 ? 2 : 4; }
+// HALO variants' BM per output width (must match the dispatch in launch_convn)
+static constexpr int kHaloBm64[] = {128, 256, 128, 128, 256};
+static constexpr int kHaloBm128[] = {128, 256, 128, 128};
+static int halo_count(int bn) { return bn == 256 ? 1 : bn == 128 ? 4 : 5; }
+static int convn_variant_count(int bn) { return plain_count(bn) + halo_count(bn); }
 
 int convn_variants(int N) {
   const int bn = convn_tile_n(N);
@@ -489,20 +572,44 @@ static int default_variant(const ConvnArgs& a, int bn) {
 }
 
 // BM of each variant (must match the dispatch in launch_convn)
-static int stats_bm(int bn, int v) {
+static int variant_bm(int bn, int v) {
+  const int h = v - plain_count(bn);
+  if (h >= 0) return bn == 64 ? kHaloBm64[h] : bn == 128 ? kHaloBm128[h] : 128;
   if (bn == 64) return (v == 2 || v == 3) ? 256 : 128;
   if (bn == 128) return v == 2 ? 256 : 128;
   return 128;
 }
 
-int convn_stats_rows(int M) { return 4 * ((M + 255) / 256) + 4; }  // >= (BM/64) * tiles for every variant
+// HALO slot width for an output row of Wo pixels and an R-wide kernel (0: no HALO tiling)
+static int halo_sw(int Wo, int R) {
+  const int need = Wo + R - 1;
+  return need <= 16 ? 16 : need <= 32 ? 32 : need <= 64 ? 64 : 0;
+}
 
-int convn_part_rows(int M, int N, int variant) {
+bool convn_variant_ok(int N, int v, int R, int S, int stride, int pad, int Wo, bool has_x2) {
+  const int bn = convn_tile_n(N);
+  if (!bn || v < 0 || v >= convn_variant_count(bn)) return false;
+  if (v < plain_count(bn)) return true;
+  const int sw = halo_sw(Wo, R);
+  return !has_x2 && R == S && R > 1 && R <= 3 && stride == 1 && 2 * pad == R - 1 && sw > 0 && variant_bm(bn, v) >= sw;
+}
+
+int convn_stats_rows(int M) { return 4 * ((M + 255) / 256) + 4; }  // >= (BM/64) * tiles for the gathered variants
+
+int convn_part_rows_geo(int M, int N, int variant, int Ho, int Wo, int R) {
   const int bn = convn_tile_n(N);
   if (!bn) return 0;
-  const int bm = stats_bm(bn, variant);
+  const int bm = variant_bm(bn, variant);
+  if (variant >= plain_count(bn)) {
+    const int sw = halo_sw(Wo, R);
+    if (!sw || Ho <= 0 || Wo <= 0) return 0;
+    const int rpt = bm / sw;
+    return (bm / 64) * ((M / (Ho * Wo)) * ((Ho + rpt - 1) / rpt));
+  }
   return (bm / 64) * ((M + bm - 1) / bm);
 }
+
+int convn_part_rows(int M, int N, int variant) { return convn_part_rows_geo(M, N, variant, 0, 0, 1); }
 
 hipError_t launch_convn(const ConvnArgs& a_in, hipStream_t st) {
   if (a_in.M <= 0) return hipSuccess;
@@ -525,6 +632,28 @@ hipError_t launch_convn(const ConvnArgs& a_in, hipStream_t st) {
                                                 (a.bwd != 5 || (a.Ho % 2 == 0 && a.Wo % 2 == 0))))));
   if (!ok) return hipErrorNotSupported;
   const int v = a.variant >= 0 ? a.variant : default_variant(a, bn);
+  if (v >= plain_count(bn)) {  // HALO
+    if (!convn_variant_ok(a.N, v, a.R, a.S, a.stride, a.pad, a.Wo, two) || a.Ho != a.H || a.Wo != a.W)
+      return hipErrorNotSupported;
+    const int sw = halo_sw(a.Wo, a.R);
+    a.log_sw = sw == 16 ? 4 : sw == 32 ? 5 : 6;
+    const int h = v - plain_count(bn);
+    switch (bn) {
+      case 64:  // deeper weight rings: a tap's K-tile is only BN x 64, its L2 latency is the limit
+        if (h == 0) return convn_launch_s<128, 64, 32, 3, true>(a, st);
+        if (h == 1) return convn_launch_s<256, 64, 64, 3, true>(a, st);
+        if (h == 2) return convn_launch_s<128, 64, 32, 4, true>(a, st);
+        if (h == 3) return convn_launch_s<128, 64, 32, 8, true>(a, st);
+        return convn_launch_s<256, 64, 64, 6, true>(a, st);
+      case 128:
+        if (h == 0) return convn_launch_s<128, 128, 32, 3, true>(a, st);
+        if (h == 1) return convn_launch_s<256, 128, 64, 2, true>(a, st);
+        if (h == 2) return convn_launch_s<128, 128, 64, 4, true>(a, st);
+        return convn_launch_s<128, 128, 32, 6, true>(a, st);
+      default:
+        return convn_launch_s<128, 256, 64, 3, true>(a, st);
+    }
+  }
   switch (bn) {
     case 64:  // 4 waves of 64x32 (3 / 2 slots) | 4 waves of 64x64 (BM 256) | 8 waves of 64x32 (BM 256)
       if (v == 0) return convn_launch_s<128, 64, 32, 3>(a, st);

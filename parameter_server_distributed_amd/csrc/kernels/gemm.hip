@@ -694,6 +694,20 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
   return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
 }
 
+// lane-group sums for the statistics epilogue: x of lane ^ 8 (DPP row rotate by 8 within a 16-lane
+// row), lane ^ 16 / lane ^ 32 (the gfx950 half-row / half-wave swaps)
+__device__ __forceinline__ float st_xor8(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x128, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float st_xor16(float x, int lane) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float((lane & 16) ? r[0] : r[1]);
+}
+__device__ __forceinline__ float st_xor32(float x, int lane) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float((lane & 32) ? r[0] : r[1]);
+}
+
 // grouped tile order inside one XCD's contiguous range: 4 tile-rows share each B panel
 __device__ __forceinline__ void tile_of(int wg, int tiles_m, int tiles_n, int& tm, int& tn) {
   constexpr int G = 4;
@@ -763,13 +777,19 @@ __device__ __forceinline__ float act_apply(float x) {
 // output pixels whose (r, s)-shifted input pixel is computed per K-tile (one (r, s) per K-tile:
 // C % 64 == 0); pixels outside the image get an offset past the descriptor, i.e. the zero padding.
 // F8A: the A operand's fp8 format (0 e4m3, 1 e5m2: bwd-data of the fp8 convolutions takes e5m2 dY)
+// ST: the consumer BatchNorm's batch statistics in the bf16 epilogue (g.part / g.shift): per output
+// channel the shifted sums sum(y - shift) and sum((y - shift)^2) of the stored bf16 values over each
+// wave row's BM / 2 rows -> partial row (tile_m * 2 + wave row) of part [rows][2][N] (the layout of
+// kernels/bn.hip bn_fwd_reduce_kernel), so the BN forward skips its statistics pass. The shift (the
+// running mean) arrives by LDS-DMA with the bias, 4 B per lane.
 // GB: B is gathered as the im2col image of a convolution input for the weight gradient (MODE 1):
 // dW[cout][(r, s, ci)] = sum over output pixels p of dY[p][cout] * x[pixel(p) + (r, s)][ci], A = dY
 // M-major ([pixels][cout]), B = the gathered [pixels][R*S*C] N-major image (each lane's 16 bytes are
 // 8 channels of one shifted input pixel; pixels outside the image load zeros).
 template <int BM, bool AK, bool BKM, int MODE, bool F8 = false, int ACT = 0, bool GA = false, int F8A = 0,
-          bool GB = false, bool MX = false>
+          bool GB = false, bool MX = false, bool ST = false>
 __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
+  static_assert(!ST || (MODE == 0 && !GB && ACT == 0), "statistics epilogue: single split, bf16 out, no activation");
   static_assert(!MX || (F8 && BM == 128 && MODE == 0), "MX: fp8, 128-row tiles (LDS), single split");
   static_assert(!GB || (!AK && !BKM && MODE == 1 && !F8 && !GA), "implicit-GEMM wgrad: M-major dY, split-K");
   static_assert(!F8 || (AK && BKM), "fp8 GEMM takes K-major operands");
@@ -1019,7 +1039,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
 
   // VMEM stores of one tile's epilogue, per lane, in both output paths (exact: every store is
   // issued unconditionally, out-of-range rows/cols go to an offset outside the buffer descriptor)
-  constexpr int kEpiStores = 8 * IM;
+  constexpr int kEpiStores = 8 * IM + (ST ? 4 : 0);
   // One K-tile of the 8-phase schedule at stream index u (= base + t); (am1, ak1) is the A source
   // of K-tile u+1, (am2, bn2, ak2) the A/B sources of K-tile u+2. first: the K-tile right after an
   // epilogue, whose phase-0 DMA was issued before the epilogue's stores; its phase-3 wait leaves
@@ -1085,6 +1105,10 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(make_rsrc(g.bias, (uint32_t)g.N * 2),
                                                (__attribute__((address_space(3))) void*)stg, 4,
                                                (uint32_t)(cn0 + wc * 64 + 2 * lane) * 2, 0, 0, 0);
+    if constexpr (ST)  // the statistics shift of the wave's 64 columns -> staging slot bytes 256..511
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(make_rsrc(g.shift, (uint32_t)g.N * 4),
+                                               (__attribute__((address_space(3))) void*)(stg + 256), 4,
+                                               (uint32_t)(cn0 + wc * 64 + lane) * 4, 0, 0, 0);
     // K-tiles nt, nt+1 of this tile's stream = the next tile's first two K-tiles (past the
     // workgroup's last tile: the last valid K-tile again, same DMA count, never read)
     const bool more = jt + 1 < ntl;
@@ -1146,6 +1170,15 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
       // issued against an empty descriptor (dropped) to keep the store count exact.
       const rsrc_t ra = make_rsrc(want_aux ? g.aux : g.C, want_aux ? cbytes : 0u);
       const int rrow = lane >> 3, c16 = lane & 7;  // read side: 8 rows x 8 16-byte chunks per pass
+      float shv[8], s1[8], s2[8];
+      if constexpr (ST) {
+        const f32x4 h0 = *reinterpret_cast<const f32x4*>(stg + 256 + c16 * 32);
+        const f32x4 h1 = *reinterpret_cast<const f32x4*>(stg + 256 + c16 * 32 + 16);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) shv[e] = h0[e], shv[4 + e] = h1[e];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
+      }
 #pragma unroll
       for (int qm = 0; qm < 2; ++qm)
 #pragma unroll
@@ -1183,8 +1216,52 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
             const uint32_t go = (m < g.M && n < g.N) ? ((uint32_t)m * ldo + n) * 2 : kOOB;
             __builtin_amdgcn_raw_buffer_store_b128(v, rc, go, 0, 0);
             __builtin_amdgcn_raw_buffer_store_b128(va, ra, go, 0, 0);
+            if constexpr (ST) {
+              if (m < g.M) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  const float d0 = __uint_as_float(v[e] << 16) - shv[2 * e];
+                  const float d1 = __uint_as_float(v[e] & 0xFFFF0000u) - shv[2 * e + 1];
+                  s1[2 * e] += d0;
+                  s1[2 * e + 1] += d1;
+                  s2[2 * e] = fmaf(d0, d0, s2[2 * e]);
+                  s2[2 * e + 1] = fmaf(d1, d1, s2[2 * e + 1]);
+                }
+              }
+            }
           }
         }
+      if constexpr (ST) {
+        // lanes with equal c16 hold the same 8 columns: sum over lane bits 3..5, lanes 0..7 store
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          s1[e] += st_xor8(s1[e]);
+          s2[e] += st_xor8(s2[e]);
+          s1[e] += st_xor16(s1[e], lane);
+          s2[e] += st_xor16(s2[e], lane);
+          s1[e] += st_xor32(s1[e], lane);
+          s2[e] += st_xor32(s2[e], lane);
+        }
+        const int prow = (cm0 / BM) * 2 + wr;
+        const int n = cn0 + wc * 64 + c16 * 8;
+        const int prows = (g.M + BM - 1) / BM * 2;
+        const rsrc_t rp = make_rsrc(g.part, (uint32_t)prows * 2u * (uint32_t)g.N * 4u);
+        const bool mine = lane < 8 && n < g.N;
+        const uint32_t o1 = mine ? ((uint32_t)prow * 2u * (uint32_t)g.N + (uint32_t)n) * 4u : kOOB;
+        const uint32_t o2 = mine ? o1 + (uint32_t)g.N * 4u : kOOB;
+        __builtin_amdgcn_raw_buffer_store_b128(
+            u32x4{__float_as_uint(s1[0]), __float_as_uint(s1[1]), __float_as_uint(s1[2]), __float_as_uint(s1[3])}, rp,
+            o1, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(
+            u32x4{__float_as_uint(s1[4]), __float_as_uint(s1[5]), __float_as_uint(s1[6]), __float_as_uint(s1[7])}, rp,
+            mine ? o1 + 16u : kOOB, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(
+            u32x4{__float_as_uint(s2[0]), __float_as_uint(s2[1]), __float_as_uint(s2[2]), __float_as_uint(s2[3])}, rp,
+            o2, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(
+            u32x4{__float_as_uint(s2[4]), __float_as_uint(s2[5]), __float_as_uint(s2[6]), __float_as_uint(s2[7])}, rp,
+            mine ? o2 + 16u : kOOB, 0, 0);
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staging reads retired: clean lgkm count
 #pragma unroll
@@ -1415,12 +1492,23 @@ static int persistent_grid() {
 }
 
 template <int BM, bool AK, bool BKM, int MODE, bool F8, int ACT, bool GA = false, int F8A = 0, bool GB = false,
-          bool MX = false>
+          bool MX = false, bool ST = false>
 static hipError_t launch_8p_act(const GemmArgs& g, int splits, hipStream_t st) {
+  if constexpr (!ST) {
+    if (g.part) {  // the consumer BN's statistics in the epilogue
+      if constexpr (MODE == 0 && !GB && ACT == 0) {
+        if (g.c_f32 || g.bias || !g.shift || splits != 1) return hipErrorNotSupported;
+        if (g.rows_out) *g.rows_out = (g.M + BM - 1) / BM * 2;
+        return launch_8p_act<BM, AK, BKM, MODE, F8, ACT, GA, F8A, GB, MX, true>(g, splits, st);
+      } else {
+        return hipErrorNotSupported;
+      }
+    }
+  }
   constexpr int lds = P8<BM, MX>::LDS;
   static bool attr_set = false;  // per instantiation: set the >64 KiB LDS limit once
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT, GA, F8A, GB, MX>,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT, GA, F8A, GB, MX, ST>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     attr_set = true;
@@ -1437,8 +1525,8 @@ static hipError_t launch_8p_act(const GemmArgs& g, int splits, hipStream_t st) {
   }();
   GemmArgs ga = g;
   ga.dbg = dbg;
-  hipLaunchKernelGGL((gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT, GA, F8A, GB, MX>), dim3(grid, 1, splits), dim3(512), lds,
-                     st, ga);
+  hipLaunchKernelGGL((gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT, GA, F8A, GB, MX, ST>), dim3(grid, 1, splits), dim3(512),
+                     lds, st, ga);
   return hipGetLastError();
 }
 
@@ -1476,6 +1564,7 @@ static int pick_bm(int M, int N, int splits, bool a_kmajor = true) {
 template <bool AK, bool BKM, int MODE>
 static hipError_t launch_big(const GemmArgs& g, int splits, hipStream_t st) {
   const int var = big_variant();
+  if (g.part && var != 2) return hipErrorNotSupported;  // statistics: the 8-phase epilogue only
   if (var == 2) {
     if constexpr (AK) {
       if (pick_bm(g.M, g.N, splits) == 128) return launch_8p<128, AK, BKM, MODE>(g, splits, st);
@@ -1526,6 +1615,7 @@ template <bool AK, bool BKM, int MODE>
 static hipError_t launch_layout(const GemmArgs& g, int splits, hipStream_t st) {
   if (big_ok(g, MODE == 1 ? g.k_per_split : g.K) && (MODE == 1 || g.K % 64 == 0))
     return launch_big<AK, BKM, MODE>(g, splits, st);
+  if (g.part) return hipErrorNotSupported;  // statistics: the 8-phase epilogue only
   // tile choice: 128x128 by default, 128x64 / 64x128 for narrow operands (more tiles)
   if (g.N <= 64 && g.M > 64) return launch_t<2, 1, AK, BKM, MODE>(g, splits, st);
   if (g.M <= 64 && g.N > 64) return launch_t<1, 2, AK, BKM, MODE>(g, splits, st);

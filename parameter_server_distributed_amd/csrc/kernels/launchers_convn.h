@@ -18,6 +18,7 @@ struct ConvnArgs {
   int ldc;
   int variant;  // tile geometry (convn_variants(N) of them); -1: the default
   int nslot;    // set by the launcher
+  int log_sw;   // set by the launcher (HALO variants: log2 of the slots per output row)
   // bwd-data with the producing BN's backward reduction in the epilogue (bwd 1 / 2, convn.hip);
   // part then receives sum g and sum g (x - mean) per channel
   int bwd;
@@ -43,8 +44,13 @@ struct ConvnArgs {
 int convn_tile_n(int N);
 // rows to allocate for the statistics partials of M output pixels (any variant)
 int convn_stats_rows(int M);
-// rows a launch with this variant writes (one per 64-pixel wave row of every tile)
+// rows a launch with this variant writes (one per 64-pixel wave row of every tile); HALO variants
+// tile by output rows: _geo with the convolution's output height / width and kernel size
 int convn_part_rows(int M, int N, int variant);
+int convn_part_rows_geo(int M, int N, int variant, int Ho, int Wo, int R);
+// variant v of an N-wide output is usable for this convolution (HALO: stride 1, R = S <= 3, pad
+// R / 2, Wo + R - 1 <= 64, no second operand)
+bool convn_variant_ok(int N, int v, int R, int S, int stride, int pad, int Wo, bool has_x2);
 int convn_variants(int N);
 // hipErrorNotSupported outside the kernel's contract (nothing launched)
 hipError_t launch_convn(const ConvnArgs& a, hipStream_t stream);

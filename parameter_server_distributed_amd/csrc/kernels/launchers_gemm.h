@@ -29,6 +29,11 @@ struct GemmArgs {
   // K-elements, A [M][K/32] (implicit-GEMM conv: of the input, [pixels][C/32]), B [N][K/32]
   const uint8_t* a_mx;
   const uint8_t* b_mx;
+  // the consumer BatchNorm's batch statistics in the epilogue (single-split bf16 8-phase GEMMs, no
+  // bias / activation): part [rows][2][N] fp32 shifted sums, shift [N] fp32; *rows_out <- rows
+  float* part;
+  const float* shift;
+  int* rows_out;
 };
 
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t stream);

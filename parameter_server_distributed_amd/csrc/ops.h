@@ -60,8 +60,11 @@ std::vector<at::Tensor> bn_bwd(const at::Tensor& dy, const at::Tensor& x, c10::o
                                c10::optional<at::Tensor> dy2, c10::optional<at::Tensor> ss,
                                c10::optional<at::Tensor> mbits, c10::optional<at::Tensor> dq, c10::optional<at::Tensor> dqmx);
 
-void gemm_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool b_kmajor, at::Tensor out,
-           c10::optional<at::Tensor> bias, int64_t act, c10::optional<at::Tensor> aux);
+int64_t gemm_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool b_kmajor, at::Tensor out,
+              c10::optional<at::Tensor> bias, int64_t act, c10::optional<at::Tensor> aux,
+              c10::optional<at::Tensor> part, c10::optional<at::Tensor> shift);
+// statistics partial rows to allocate for a gemm_ / gemm_fp8_ / conv_fwd_ with part (any tile height)
+int64_t gemm_stats_rows_(int64_t M);
 void gemm_splitk_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool b_kmajor, at::Tensor out,
                   bool accumulate, double scale, int64_t splits);
 void colsum_(const at::Tensor& x, at::Tensor out, bool accumulate);
@@ -70,6 +73,8 @@ void gelu_bwd_colsum_(const at::Tensor& dy, const at::Tensor& pre, at::Tensor dx
 // w2 [Cout, R*S*C]; with part/shift also the consumer BN's shifted statistics partials (a buffer of
 // convn_stats_rows(M) x 2 x Cout). Returns 0 (nothing launched) outside the kernel's contract, else
 // the partial rows written (1 without statistics).
+int64_t convn_part_rows_(int64_t M, int64_t N, int64_t v, int64_t Ho, int64_t Wo, int64_t R);
+bool convn_variant_ok_(int64_t N, int64_t v, int64_t R, int64_t S, int64_t stride, int64_t pad, int64_t Wo, bool has_x2);
 int64_t convn_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride,
                int64_t pad, c10::optional<at::Tensor> part, c10::optional<at::Tensor> shift, int64_t variant,
                c10::optional<at::Tensor> x2, c10::optional<at::Tensor> bias);
@@ -86,18 +91,20 @@ std::vector<at::Tensor> bn_bwd_pre(const at::Tensor& g, const at::Tensor& x, c10
                                    c10::optional<at::Tensor> dbeta_out, c10::optional<at::Tensor> dq,
                                    c10::optional<at::Tensor> dqmx);
 int64_t convn_variants_(int64_t N);
-bool conv_fwd_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride,
-               int64_t pad);
+int64_t conv_fwd_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride,
+                  int64_t pad, c10::optional<at::Tensor> part, c10::optional<at::Tensor> shift);
 bool conv_wgrad_(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64_t R, int64_t S, int64_t stride,
                  int64_t pad, int64_t splits);
 bool convw_(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64_t R, int64_t S, int64_t stride,
             int64_t pad, int64_t variant, bool accumulate, bool fold);
 int64_t convw_fold_rows(int64_t Cout, int64_t Cin);
 int64_t convw_variants_(int64_t Cout, int64_t KK);
-bool conv_fwd_fp8_(const at::Tensor& x, const at::Tensor& w2, const at::Tensor& x_scale, const at::Tensor& w_scale,
-                   at::Tensor out, int64_t R, int64_t S, int64_t stride, int64_t pad);
-void gemm_fp8_(const at::Tensor& A, const at::Tensor& B, const at::Tensor& a_scale, const at::Tensor& b_scale,
-               at::Tensor out, c10::optional<at::Tensor> bias, int64_t act, c10::optional<at::Tensor> aux);
+int64_t conv_fwd_fp8_(const at::Tensor& x, const at::Tensor& w2, const at::Tensor& x_scale, const at::Tensor& w_scale,
+                      at::Tensor out, int64_t R, int64_t S, int64_t stride, int64_t pad, c10::optional<at::Tensor> part,
+                      c10::optional<at::Tensor> shift);
+int64_t gemm_fp8_(const at::Tensor& A, const at::Tensor& B, const at::Tensor& a_scale, const at::Tensor& b_scale,
+                  at::Tensor out, c10::optional<at::Tensor> bias, int64_t act, c10::optional<at::Tensor> aux,
+                  c10::optional<at::Tensor> part, c10::optional<at::Tensor> shift);
 std::vector<at::Tensor> maxpool3s2_fwd(const at::Tensor& x);
 at::Tensor maxpool3s2_bwd(const at::Tensor& dy, const at::Tensor& arg, int64_t H, int64_t W,
                           const c10::optional<at::Tensor>& dy2);

@@ -194,7 +194,7 @@ def _convn_variants(x, w2, k: int, stride: int, pad: int, bn=None) -> dict:
             out = torch.empty(M, cout, device=x.device, dtype=x.dtype)
             part = None
             if bn is not None:
-                part = torch.empty(C.convn_stats_rows(M), 2, cout, device=x.device, dtype=torch.float32)
+                part = torch.empty(_part_rows(M, cout, v, ho, wo, k), 2, cout, device=x.device, dtype=torch.float32)
             rows = C.convn_(x, w2, out, k, k, stride, pad, part=part,
                             shift=bn.running_mean if bn is not None else None, variant=v)
             if rows == 0:
@@ -205,7 +205,23 @@ def _convn_variants(x, w2, k: int, stride: int, pad: int, bn=None) -> dict:
             return y
         return fn
 
-    return {f"psdn{v}": make(v) for v in range(C.convn_variants(cout))}
+    return {f"psdn{v}": make(v) for v in range(C.convn_variants(cout)) if _variant_ok(cout, v, k, stride, pad, wo)}
+
+
+def _variant_ok(cout: int, v: int, k: int, stride: int, pad: int, wo: int) -> bool:
+    """Variant v of the narrow kernel takes this shape (HALO variants -- the ones a 1x1 shape
+    declines -- only with PSD_CONVN_HALO on)."""
+    C = _native()
+    if not C.convn_variant_ok(cout, v, k, k, stride, pad, wo):
+        return False
+    return C.convn_variant_ok(cout, v, 1, 1, 1, 0, 1) or _at.enabled("PSD_CONVN_HALO")
+
+
+def _part_rows(M: int, N: int, v: int, ho: int, wo: int, k: int) -> int:
+    """Statistics partial rows to allocate for a convn launch of variant v (HALO variants tile by
+    output rows, kernels/convn.hip)."""
+    C = _native()
+    return max(C.convn_stats_rows(M), C.convn_part_rows(M, N, v, ho, wo, k))
 
 
 def _bn_bwd_fusion(mod, x: torch.Tensor):
@@ -248,7 +264,7 @@ def _convn_bwd_variants(dy, w2, k: int, pad: int, fu: dict, dr) -> dict:
     def make(v):
         def fn():
             out = torch.empty(M, cout, device=dy.device, dtype=dy.dtype)
-            part = torch.empty(C.convn_stats_rows(M), 2, cout, device=dy.device, dtype=torch.float32)
+            part = torch.empty(_part_rows(M, cout, v, h, w, k), 2, cout, device=dy.device, dtype=torch.float32)
             part_d = torch.empty_like(part) if fu["mode"] == 3 else None
             rows = C.convn_bwd_(dy, w2, out, k, k, 1, pad, part, v, fu["mode"], fu["bx"], fu["mean"],
                                 bss=fu.get("ss"), bdr=_dr_arg(dr), bmbits=fu.get("mbits"), bxd=fu.get("bxd"),
@@ -260,7 +276,7 @@ def _convn_bwd_variants(dy, w2, k: int, pad: int, fu: dict, dr) -> dict:
             return g
         return fn
 
-    return {f"psdnb{v}": make(v) for v in range(C.convn_variants(cout))}
+    return {f"psdnb{v}": make(v) for v in range(C.convn_variants(cout)) if _variant_ok(cout, v, k, 1, pad, w)}
 
 
 def _dgrad_route(key: tuple, cands: dict, default: str, fu, dy_like) -> torch.Tensor:
@@ -302,6 +318,20 @@ def _with_bn_bwd_reduce(fn, fu):
     return g
 
 
+def _stats_part(bn, M: int, cout: int, device):
+    """Statistics-partials buffer for an 8-phase GEMM / implicit-GEMM launch whose epilogue reduces
+    the consumer BN's batch statistics (kernels/gemm.hip ST), or None without a consumer BN."""
+    if bn is None or not _at.enabled("PSD_GEMM_STATS"):
+        return None
+    return torch.empty(_native().gemm_stats_rows(M), 2, cout, device=device, dtype=torch.float32)
+
+
+def _hand_stats(bn, y, part, rows: int):
+    """Queue the partials a GEMM epilogue reduced for ``y`` on its consumer BN (skips its reduce)."""
+    if part is not None and rows > 0:
+        bn._psd_stats_pending = (y, part, rows)
+
+
 def _dr_arg(dr):
     """The convn_bwd_ dr operand: a quarter-grid StridedDr's tensor (mode 5) or the full gradient."""
     return dr.t4 if isinstance(dr, StridedDr) else dr
@@ -312,7 +342,8 @@ def _route(key: tuple, cands: dict, default: str, bn=None) -> str:
     the statistics pass they leave behind (the psdn ones reduce it in their epilogue)."""
     if bn is None:
         return _at.choose(key, cands, default)
-    timed = {name: (fn if name.startswith("psdn") else _with_bn_reduce(fn, bn)) for name, fn in cands.items()}
+    timed = {name: (fn if name.startswith(("psdn", "psds")) else _with_bn_reduce(fn, bn))
+             for name, fn in cands.items()}
     return _at.choose(key + ("bnstats",), timed, default)
 
 
@@ -459,6 +490,8 @@ def _fold_backward(ctx, fold, x, weight, need_x: bool, need_w: bool):
 
         cands = {"unfold": unfold}
         for v in range(C.convn_variants(cin)):
+            if not C.convn_variant_ok(cin, v, 1, 1, 1, 0, w, True):
+                continue
             cands[f"psdnf{v}"] = make(v, False)
             if fu is not None:
                 cands[f"psdnb{v}"] = make(v, True)
@@ -520,9 +553,17 @@ class _Conv1x1Fn(torch.autograd.Function):
                 xq, sx = _q_act(x2, scaler=f8[0])
             wq, sw = _q_weight(mod, w2)
             out = torch.empty(n * h * w, cout, device=x.device, dtype=x.dtype)
-            _native().gemm_fp8_(xq, wq, sx, sw, out)
+            bn = _bn_consumer(mod)
+            part = _stats_part(bn, n * h * w, cout, x.device)
+            rows = _native().gemm_fp8_(xq, wq, sx, sw, out, part=part,
+                                       shift=bn.running_mean if part is not None else None)
+            if rows == 0:  # the statistics epilogue declined the shape: plain launch, the BN reduces
+                part = None
+                _native().gemm_fp8_(xq, wq, sx, sw, out)
             FP8_CALLS["fwd"] += 1
-            return _from_2d(out, n, h, w)
+            y = _from_2d(out, n, h, w)
+            _hand_stats(bn, y, part, rows)
+            return y
         key = ("fwd", n * h * w, cin, cout)
 
         def gemm():
@@ -536,14 +577,26 @@ class _Conv1x1Fn(torch.autograd.Function):
             _native().gemm_(x2, w2, True, True, out)
             return _from_2d(out, n, h, w)
 
+        def psds():  # the same with the consumer BN's statistics in its epilogue
+            out = torch.empty(n * h * w, cout, device=x.device, dtype=x.dtype)
+            part = _stats_part(bn, n * h * w, cout, x.device)
+            rows = _native().gemm_(x2, w2, True, True, out, part=part, shift=bn.running_mean)
+            if rows == 0:
+                raise RuntimeError("gemm_ declined the statistics epilogue on a shape it ran before")
+            y = _from_2d(out, n, h, w)
+            _hand_stats(bn, y, part, rows)
+            return y
+
         cands = {"gemm": gemm, "miopen": miopen}
+        bn = _bn_consumer(mod)
         if _psd_ok(cin, cout):
             cands["psd"] = psd
-        bn = None
+            if bn is not None and _at.enabled("PSD_GEMM_STATS") and n * h * w >= 128 and cout >= 256 and cin >= 256 \
+                    and cin % 64 == 0:
+                cands["psds"] = psds
         if _psdn_ok(cin, cout):
-            bn = _bn_consumer(mod)
             cands.update(_convn_variants(x, w2 if w2.is_contiguous() else w2.contiguous(), 1, 1, 0, bn))
-        y = cands[_route(("conv1x1",) + key, cands, "miopen", bn)]()
+        y = cands[_route(("conv1x1",) + key, cands, "miopen", bn if len(cands) > 2 else None)]()
         if mod is not None:  # this output may have its consumer BN's backward folded (_fold_backward)
             mod._psd_fold_out = (y.data_ptr(), tuple(y.shape))
         return y
@@ -700,21 +753,27 @@ def _wgrad_ok(cin: int, cout: int, k: int, dy: torch.Tensor) -> bool:
             and n * ho * wo >= 128)
 
 
-def _igemm(x: torch.Tensor, w2: torch.Tensor, k: int, stride: int, pad: int):
+def _igemm(x: torch.Tensor, w2: torch.Tensor, k: int, stride: int, pad: int, bn=None):
     """conv(x, w) on the implicit-GEMM kernel, as a channels_last [N, Cout, Ho, Wo] tensor, or None
-    when the kernel declines the shape."""
+    when the kernel declines the shape. With a consumer ``bn`` the epilogue also reduces its batch
+    statistics (handed over as for the narrow kernel)."""
     from .. import native
 
     n, _, h, w = x.shape
     ho, wo = (h + 2 * pad - k) // stride + 1, (w + 2 * pad - k) // stride + 1
     out = torch.empty(n * ho * wo, w2.shape[0], device=x.device, dtype=x.dtype)
-    if not native().conv_fwd_(x, w2, out, k, k, stride, pad):
+    part = _stats_part(bn, n * ho * wo, w2.shape[0], x.device)
+    rows = native().conv_fwd_(x, w2, out, k, k, stride, pad, part=part,
+                              shift=bn.running_mean if part is not None else None)
+    if not rows:
         return None
-    return _from_2d(out, n, ho, wo)
+    y = _from_2d(out, n, ho, wo)
+    _hand_stats(bn, y, part, rows)
+    return y
 
 
 def _igemm_fp8(x: torch.Tensor, w2: torch.Tensor, k: int, stride: int, pad: int, e5m2: bool = False,
-               scaler: "DelayedScale | None" = None, pre=None, mod=None):
+               scaler: "DelayedScale | None" = None, pre=None, mod=None, bn=None):
     """conv(x, w) with fp8 operands on the implicit-GEMM kernel (per-tensor just-in-time scales; x
     e4m3, or e5m2 when it is an output gradient), bf16 channels_last out, or None when the kernel
     declines the shape."""
@@ -728,10 +787,15 @@ def _igemm_fp8(x: torch.Tensor, w2: torch.Tensor, k: int, stride: int, pad: int,
         xq, sx = _q_act(x.permute(0, 2, 3, 1), e5m2=e5m2, scaler=scaler)  # the NHWC storage, in place order
     wq, sw = _q_weight(mod, w2) if mod is not None else _q_act(w2)
     out = torch.empty(n * ho * wo, w2.shape[0], device=x.device, dtype=x.dtype)
-    if not native().conv_fwd_fp8_(xq.permute(0, 3, 1, 2), wq, sx, sw, out, k, k, stride, pad):
+    part = _stats_part(bn, n * ho * wo, w2.shape[0], x.device)
+    rows = native().conv_fwd_fp8_(xq.permute(0, 3, 1, 2), wq, sx, sw, out, k, k, stride, pad, part=part,
+                                  shift=bn.running_mean if part is not None else None)
+    if not rows:
         return None
     FP8_CALLS["dgrad" if e5m2 else "fwd"] += 1
-    return _from_2d(out, n, ho, wo)
+    y = _from_2d(out, n, ho, wo)
+    _hand_stats(bn, y, part, rows)
+    return y
 
 
 def _strided_dgrad(mod, dy, weight, to, H: int, W: int):
@@ -777,7 +841,7 @@ class _ConvFn(torch.autograd.Function):
         if fp8 and cin % 128 == 0 and _fp8_ok(k * k * cin, cout):
             w2 = weight.permute(0, 2, 3, 1).reshape(cout, k * k * cin)
             y = _igemm_fp8(x, w2 if w2.is_contiguous() else w2.contiguous(), k, stride, pad, scaler=f8[0],
-                           pre=_take_q8(mod, x), mod=mod)
+                           pre=_take_q8(mod, x), mod=mod, bn=_bn_consumer(mod))
             if y is not None:
                 return y
 
@@ -791,15 +855,23 @@ class _ConvFn(torch.autograd.Function):
             y = _igemm(x, w2, k, stride, pad)
             return miopen() if y is None else y
 
+        bn = _bn_consumer(mod)
+
+        def igemm_stats():  # the implicit GEMM with the consumer BN's statistics in its epilogue
+            y = _igemm(x, w2, k, stride, pad, bn)
+            if y is None:
+                raise RuntimeError("conv_fwd_ declined the statistics epilogue on a shape it ran before")
+            return y
+
         cands = {"miopen": miopen}
         if _igemm_ok(cin, cout):
             cands["igemm"] = igemm
-        bn = None
+            if bn is not None and _at.enabled("PSD_GEMM_STATS"):
+                cands["psds_igemm"] = igemm_stats
         if _psdn_ok(cin, cout):
-            bn = _bn_consumer(mod)
             cands.update(_convn_variants(x, w2, k, stride, pad, bn))
         key = ("fwd", n, cin, h, w, cout, k, stride)
-        return cands[_route(("conv",) + key, cands, "miopen", bn)]()
+        return cands[_route(("conv",) + key, cands, "miopen", bn if len(cands) > 1 else None)]()
 
     @staticmethod
     def backward(ctx, dy):

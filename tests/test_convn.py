@@ -49,6 +49,8 @@ def test_convn_exact(gpu, case):
     nv = native().convn_variants(Cout)
     assert nv >= 2
     for v in range(nv):
+        if not native().convn_variant_ok(Cout, v, R, R, stride, pad, Wo):
+            continue
         out = torch.full((Nb * Ho * Wo, Cout), 7.0, device=gpu, dtype=torch.bfloat16)
         assert native().convn_(xd, w2, out, R, R, stride, pad, variant=v) == 1
         torch.testing.assert_close(out.float().cpu(), want, rtol=0, atol=0, msg=lambda m: f"variant {v}: {m}")
@@ -62,8 +64,12 @@ def test_convn_stats_partials(gpu, case):
     x, w, ref, xd = _case(case, gpu, seed=11)
     M = ref.numel() // Cout
     shift = torch.randint(-3, 4, (Cout,)).float().to(gpu)
+    Ho, Wo = ref.shape[2], ref.shape[3]
     for v in range(native().convn_variants(Cout)):
-        part = torch.full((native().convn_stats_rows(M), 2, Cout), float("nan"), device=gpu)
+        if not native().convn_variant_ok(Cout, v, R, R, stride, pad, Wo):
+            continue
+        nrow = max(native().convn_stats_rows(M), native().convn_part_rows(M, Cout, v, Ho, Wo, R))
+        part = torch.full((nrow, 2, Cout), float("nan"), device=gpu)
         out = torch.empty(M, Cout, device=gpu, dtype=torch.bfloat16)
         rows = native().convn_(xd, _w2(w.to(gpu, torch.bfloat16)), out, R, R, stride, pad, part=part, shift=shift,
                                variant=v)
@@ -198,3 +204,46 @@ def test_resnet_convn_fusions_match_library_path(gpu, monkeypatch):
         assert ((a - b).norm() / b.norm()).item() < 0.1, n
     for n in res[1][2]:
         torch.testing.assert_close(res[0][2][n], res[1][2][n], rtol=2e-2, atol=2e-3, msg=n)
+
+
+HALO_CASES = [  # Nb, C, H(=W), Cout: stride-1 3x3, slot widths 64 / 32 / 16 (Wo 7: 16 slots, 7 valid)
+    (2, 64, 56, 64), (3, 128, 28, 128), (2, 256, 14, 256), (4, 128, 7, 128), (2, 64, 30, 128), (2, 128, 9, 64),
+]
+
+
+@pytest.mark.parametrize("case", HALO_CASES, ids=lambda c: "x".join(map(str, c)))
+def test_convn_halo_exact_with_stats(gpu, case):
+    """HALO variants (input window staged once per channel block, taps read as shifted rows):
+    exact against fp32 F.conv2d, and their statistics partials (rows per output-row tile) sum to
+    the fp32 sums of the stored output."""
+    Nb, C, H, Cout = case
+    x, w, ref, xd = _case((Nb, C, H, H, Cout, 3, 1, 1), gpu)
+    M = Nb * H * H
+    want = ref.permute(0, 2, 3, 1).reshape(-1, Cout).bfloat16().float()
+    w2 = _w2(w.to(gpu, torch.bfloat16))
+    C_ = native()
+    halo = [v for v in range(C_.convn_variants(Cout)) if v >= (2 if Cout % 256 == 0 else 4)]
+    assert halo and all(C_.convn_variant_ok(Cout, v, 3, 3, 1, 1, H) for v in halo)
+    shift = torch.zeros(Cout, device=gpu)
+    for v in halo:
+        out = torch.full((M, Cout), 7.0, device=gpu, dtype=torch.bfloat16)
+        assert C_.convn_(xd, w2, out, 3, 3, 1, 1, variant=v) == 1
+        torch.testing.assert_close(out.float().cpu(), want, rtol=0, atol=0, msg=lambda m: f"variant {v}: {m}")
+        rows_alloc = max(C_.convn_stats_rows(M), C_.convn_part_rows(M, Cout, v, H, H, 3))
+        part = torch.full((rows_alloc, 2, Cout), float("nan"), device=gpu)
+        rows = C_.convn_(xd, w2, out, 3, 3, 1, 1, part=part, shift=shift, variant=v)
+        assert rows == C_.convn_part_rows(M, Cout, v, H, H, 3)
+        s1 = part[:rows, 0].double().sum(0).cpu()
+        s2 = part[:rows, 1].double().sum(0).cpu()
+        o = out.double().cpu()
+        torch.testing.assert_close(s1, o.sum(0), rtol=1e-6, atol=1e-3)
+        torch.testing.assert_close(s2, (o * o).sum(0), rtol=1e-6, atol=1e-3)
+
+
+def test_convn_halo_declines_where_it_cannot_tile(gpu):
+    C_ = native()
+    hv = 4  # first HALO variant of a 64-wide output
+    assert not C_.convn_variant_ok(64, hv, 3, 3, 2, 1, 28)   # strided
+    assert not C_.convn_variant_ok(64, hv, 1, 1, 1, 0, 56)   # 1x1
+    assert not C_.convn_variant_ok(64, hv, 3, 3, 1, 1, 63)   # Wo + 2 > 64
+    assert C_.convn_variant_ok(64, hv, 3, 3, 1, 1, 62)

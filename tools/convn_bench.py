@@ -31,6 +31,7 @@ SHAPES = [  # name, C, H, Cout, R, stride
     ("l2.conv3 1x1 128->512", 128, 28, 512, 1, 1),
     ("l2.ds 1x1/2 256->512", 256, 56, 512, 1, 2),
     ("l3.conv2 3x3 256->256", 256, 14, 256, 3, 1),
+    ("l4.conv2 3x3 512->512", 512, 7, 512, 3, 1),
     ("l3.conv3 1x1 256->1024", 256, 14, 1024, 1, 1),
 ]
 
@@ -74,9 +75,12 @@ def main():
         ok = C_.convn_(x, w2, out, R, R, stride, pad)
         tv = {}
         for v in range(C_.convn_variants(Cout) if ok else 0):
+            if not C_.convn_variant_ok(Cout, v, R, R, stride, pad, Ho):
+                continue
             tv[v] = timeit(lambda: C_.convn_(x, w2, out, R, R, stride, pad, variant=v), a.reps)
         best = min(tv, key=tv.get) if tv else 0
         t_cn = tv[best] if tv else float("nan")
+        part = torch.empty(max(rows, C_.convn_part_rows(M, Cout, best, Ho, Ho, R)), 2, Cout, device=dev)
         t_cs = timeit(lambda: C_.convn_(x, w2, out, R, R, stride, pad, part=part, shift=shift, variant=best),
                       a.reps) if ok else float("nan")
         y = F.conv2d(x, w, stride=stride, padding=pad)
@@ -88,7 +92,7 @@ def main():
             assert err < 2e-2, (name, err)
         gf = 2.0 * M * Cout * R * R * C / 1e9
         mb = (x.numel() + M * Cout) * 2 / 1e6
-        vs = " / ".join(f"{t:.0f}" for t in tv.values())
+        vs = " / ".join(f"v{v}:{t:.0f}" for v, t in tv.items())
         print(f"| {name} | {M} | {gf:.0f} | {mb:.0f} | {t_mi:.0f} | {vs} | v{best} {t_cn:.0f} | {t_cs:.0f} | {t_mi + t_red:.0f} | "
               f"{gf / t_cn * 1e3:.0f} | {mb / t_cn * 1e3:.0f} |", flush=True)
         del x, w, w2, out, y, part
