@@ -694,11 +694,10 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
   return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
 }
 
-// lane-group sums for the statistics epilogue: x of lane ^ 8 (DPP row rotate by 8 within a 16-lane
-// row), lane ^ 16 / lane ^ 32 (the gfx950 half-row / half-wave swaps)
-__device__ __forceinline__ float st_xor8(float x) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x128, 0xF, 0xF, true));
-}
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// lane-group sums for the statistics epilogue: x of lane ^ 16 / lane ^ 32 (the gfx950 half-row /
+// half-wave swaps)
 __device__ __forceinline__ float st_xor16(float x, int lane) {
   const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   return __uint_as_float((lane & 16) ? r[0] : r[1]);
@@ -778,8 +777,10 @@ __device__ __forceinline__ float act_apply(float x) {
 // C % 64 == 0); pixels outside the image get an offset past the descriptor, i.e. the zero padding.
 // F8A: the A operand's fp8 format (0 e4m3, 1 e5m2: bwd-data of the fp8 convolutions takes e5m2 dY)
 // ST: the consumer BatchNorm's batch statistics in the bf16 epilogue (g.part / g.shift): per output
-// channel the shifted sums sum(y - shift) and sum((y - shift)^2) of the stored bf16 values over each
-// wave row's BM / 2 rows -> partial row (tile_m * 2 + wave row) of part [rows][2][N] (the layout of
+// channel the shifted sums sum(y - shift) and sum((y - shift)^2) of the fp32 accumulators (before the
+// bf16 rounding of the store: within 2^-9 per element of the stored tensor's; formed from the plain
+// sums of the wave row, exact for |mean - shift| up to ~100 standard deviations) over each wave row's
+// BM / 2 rows -> partial row (tile_m * 2 + wave row) of part [rows][2][N] (the layout of
 // kernels/bn.hip bn_fwd_reduce_kernel), so the BN forward skips its statistics pass. The shift (the
 // running mean) arrives by LDS-DMA with the bias, 4 B per lane.
 // GB: B is gathered as the im2col image of a convolution input for the weight gradient (MODE 1):
@@ -789,7 +790,8 @@ __device__ __forceinline__ float act_apply(float x) {
 template <int BM, bool AK, bool BKM, int MODE, bool F8 = false, int ACT = 0, bool GA = false, int F8A = 0,
           bool GB = false, bool MX = false, bool ST = false>
 __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
-  static_assert(!ST || (MODE == 0 && !GB && ACT == 0), "statistics epilogue: single split, bf16 out, no activation");
+  static_assert(!ST || (MODE == 0 && !GB && ACT == 0 && AK),
+                "statistics epilogue: single split, bf16 out, no activation, K-major A (zero rows past M)");
   static_assert(!MX || (F8 && BM == 128 && MODE == 0), "MX: fp8, 128-row tiles (LDS), single split");
   static_assert(!GB || (!AK && !BKM && MODE == 1 && !F8 && !GA), "implicit-GEMM wgrad: M-major dY, split-K");
   static_assert(!F8 || (AK && BKM), "fp8 GEMM takes K-major operands");
@@ -1039,7 +1041,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
 
   // VMEM stores of one tile's epilogue, per lane, in both output paths (exact: every store is
   // issued unconditionally, out-of-range rows/cols go to an offset outside the buffer descriptor)
-  constexpr int kEpiStores = 8 * IM + (ST ? 4 : 0);
+  constexpr int kEpiStores = 8 * IM + (ST ? 8 : 0);
   // One K-tile of the 8-phase schedule at stream index u (= base + t); (am1, ak1) is the A source
   // of K-tile u+1, (am2, bn2, ak2) the A/B sources of K-tile u+2. first: the K-tile right after an
   // epilogue, whose phase-0 DMA was issued before the epilogue's stores; its phase-3 wait leaves
@@ -1170,14 +1172,18 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
       // issued against an empty descriptor (dropped) to keep the store count exact.
       const rsrc_t ra = make_rsrc(want_aux ? g.aux : g.C, want_aux ? cbytes : 0u);
       const int rrow = lane >> 3, c16 = lane & 7;  // read side: 8 rows x 8 16-byte chunks per pass
-      float shv[8], s1[8], s2[8];
+      // ST: per lane, the plain sums sum y and sum y^2 of its 4 columns (qn, j) over its rows, on the
+      // fp32 accumulators before the transpose (column cl, 4 consecutive rows per block), as packed
+      // fp32 pairs (2 v_pk_add + 2 v_pk_fma per 16x16 block: the epilogue is not overlapped with the
+      // MFMA pipeline, so every instruction here is paid per tile); shifted once per wave row at the end
+      // (rows past M need no mask: their A rows load as zeros -- K-major A past the descriptor, or the
+      // implicit GEMM's out-of-image sentinel -- so their accumulators are exactly 0)
+      f32x2 t1[2][2], t2[2][2];
       if constexpr (ST) {
-        const f32x4 h0 = *reinterpret_cast<const f32x4*>(stg + 256 + c16 * 32);
-        const f32x4 h1 = *reinterpret_cast<const f32x4*>(stg + 256 + c16 * 32 + 16);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) shv[e] = h0[e], shv[4 + e] = h1[e];
+        for (int qn = 0; qn < 2; ++qn)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
+          for (int j = 0; j < 2; ++j) t1[qn][j] = t2[qn][j] = f32x2{0.f, 0.f};
       }
 #pragma unroll
       for (int qm = 0; qm < 2; ++qm)
@@ -1188,6 +1194,13 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
           for (int qn = 0; qn < 2; ++qn)
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
+              if constexpr (ST) {
+                const f32x4 a = acc[((qm * 2 + qn) * IM + i) * 2 + j];
+                const f32x2 lo = __builtin_shufflevector(a, a, 0, 1), hi = __builtin_shufflevector(a, a, 2, 3);
+                t1[qn][j] += lo + hi;
+                t2[qn][j] = __builtin_elementwise_fma(lo, lo, t2[qn][j]);
+                t2[qn][j] = __builtin_elementwise_fma(hi, hi, t2[qn][j]);
+              }
               float w[4];
               quad_t4(acc[((qm * 2 + qn) * IM + i) * 2 + j] + bv[qn][j], L, w);
               const int gcol = (qn * 32 + j * 16 + (cl & ~3)) >> 2;  // 8-byte group 0..15
@@ -1216,51 +1229,33 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
             const uint32_t go = (m < g.M && n < g.N) ? ((uint32_t)m * ldo + n) * 2 : kOOB;
             __builtin_amdgcn_raw_buffer_store_b128(v, rc, go, 0, 0);
             __builtin_amdgcn_raw_buffer_store_b128(va, ra, go, 0, 0);
-            if constexpr (ST) {
-              if (m < g.M) {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                  const float d0 = __uint_as_float(v[e] << 16) - shv[2 * e];
-                  const float d1 = __uint_as_float(v[e] & 0xFFFF0000u) - shv[2 * e + 1];
-                  s1[2 * e] += d0;
-                  s1[2 * e + 1] += d1;
-                  s2[2 * e] = fmaf(d0, d0, s2[2 * e]);
-                  s2[2 * e + 1] = fmaf(d1, d1, s2[2 * e + 1]);
-                }
-              }
-            }
           }
         }
       if constexpr (ST) {
-        // lanes with equal c16 hold the same 8 columns: sum over lane bits 3..5, lanes 0..7 store
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          s1[e] += st_xor8(s1[e]);
-          s2[e] += st_xor8(s2[e]);
-          s1[e] += st_xor16(s1[e], lane);
-          s2[e] += st_xor16(s2[e], lane);
-          s1[e] += st_xor32(s1[e], lane);
-          s2[e] += st_xor32(s2[e], lane);
-        }
+        // lanes with equal cl hold the same 4 columns: sum over lane bits 4..5, lanes 0..15 store
         const int prow = (cm0 / BM) * 2 + wr;
-        const int n = cn0 + wc * 64 + c16 * 8;
         const int prows = (g.M + BM - 1) / BM * 2;
         const rsrc_t rp = make_rsrc(g.part, (uint32_t)prows * 2u * (uint32_t)g.N * 4u);
-        const bool mine = lane < 8 && n < g.N;
-        const uint32_t o1 = mine ? ((uint32_t)prow * 2u * (uint32_t)g.N + (uint32_t)n) * 4u : kOOB;
-        const uint32_t o2 = mine ? o1 + (uint32_t)g.N * 4u : kOOB;
-        __builtin_amdgcn_raw_buffer_store_b128(
-            u32x4{__float_as_uint(s1[0]), __float_as_uint(s1[1]), __float_as_uint(s1[2]), __float_as_uint(s1[3])}, rp,
-            o1, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(
-            u32x4{__float_as_uint(s1[4]), __float_as_uint(s1[5]), __float_as_uint(s1[6]), __float_as_uint(s1[7])}, rp,
-            mine ? o1 + 16u : kOOB, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(
-            u32x4{__float_as_uint(s2[0]), __float_as_uint(s2[1]), __float_as_uint(s2[2]), __float_as_uint(s2[3])}, rp,
-            o2, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(
-            u32x4{__float_as_uint(s2[4]), __float_as_uint(s2[5]), __float_as_uint(s2[6]), __float_as_uint(s2[7])}, rp,
-            mine ? o2 + 16u : kOOB, 0, 0);
+        // the wave row's valid rows, then sum (y - k) = S1 - c k, sum (y - k)^2 = S2 - k (2 S1 - c k)
+        const float cnt = (float)max(0, min(BM / 2, g.M - (cm0 + wr * (BM / 2))));
+#pragma unroll
+        for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            float a1 = t1[qn][j][0] + t1[qn][j][1], a2 = t2[qn][j][0] + t2[qn][j][1];
+            a1 += st_xor16(a1, lane);
+            a2 += st_xor16(a2, lane);
+            a1 += st_xor32(a1, lane);
+            a2 += st_xor32(a2, lane);
+            const float k = reinterpret_cast<const float*>(stg + 256)[qn * 32 + j * 16 + cl];
+            a2 = fmaf(-k, fmaf(-cnt, k, 2.f * a1), a2);
+            a1 = fmaf(-cnt, k, a1);
+            const int n = cn0 + wc * 64 + qn * 32 + j * 16 + cl;
+            const bool mine = lane < 16 && n < g.N;
+            const uint32_t o1 = mine ? ((uint32_t)prow * 2u * (uint32_t)g.N + (uint32_t)n) * 4u : kOOB;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(a1), rp, o1, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(a2), rp, mine ? o1 + (uint32_t)g.N * 4u : kOOB, 0, 0);
+          }
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staging reads retired: clean lgkm count
@@ -1496,7 +1491,7 @@ template <int BM, bool AK, bool BKM, int MODE, bool F8, int ACT, bool GA = false
 static hipError_t launch_8p_act(const GemmArgs& g, int splits, hipStream_t st) {
   if constexpr (!ST) {
     if (g.part) {  // the consumer BN's statistics in the epilogue
-      if constexpr (MODE == 0 && !GB && ACT == 0) {
+      if constexpr (MODE == 0 && !GB && ACT == 0 && AK) {
         if (g.c_f32 || g.bias || !g.shift || splits != 1) return hipErrorNotSupported;
         if (g.rows_out) *g.rows_out = (g.M + BM - 1) / BM * 2;
         return launch_8p_act<BM, AK, BKM, MODE, F8, ACT, GA, F8A, GB, MX, true>(g, splits, st);

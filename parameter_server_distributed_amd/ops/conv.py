@@ -32,6 +32,8 @@ src/worker.cpp:316-329). This is worker-side compute for the BASELINE.json ResNe
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -210,11 +212,12 @@ def _convn_variants(x, w2, k: int, stride: int, pad: int, bn=None) -> dict:
 
 def _variant_ok(cout: int, v: int, k: int, stride: int, pad: int, wo: int) -> bool:
     """Variant v of the narrow kernel takes this shape (HALO variants -- the ones a 1x1 shape
-    declines -- only with PSD_CONVN_HALO on)."""
+    declines -- only with PSD_CONVN_HALO=1: on the ResNet-50 shapes they measured no faster than the
+    gathered variants, profiles/convn_halo_r3.md, so by default they are not autotuned)."""
     C = _native()
     if not C.convn_variant_ok(cout, v, k, k, stride, pad, wo):
         return False
-    return C.convn_variant_ok(cout, v, 1, 1, 1, 0, 1) or _at.enabled("PSD_CONVN_HALO")
+    return C.convn_variant_ok(cout, v, 1, 1, 1, 0, 1) or os.environ.get("PSD_CONVN_HALO", "0") == "1"
 
 
 def _part_rows(M: int, N: int, v: int, ho: int, wo: int, k: int) -> int:

@@ -4,8 +4,9 @@ that feeds a BN -- the bf16 GEMM (1x1 convolutions), the implicit-GEMM convoluti
 forms (per-tensor and MX block scales) -- vs fp64 sums of the output read back; and the module route
 (the BN consumes the partials and skips its reduce) vs an fp32 reference.
 
-Operands are small integers: every product and the fp32 partial sums are exact, so the partials
-must match the fp64 sums of the stored output to rounding of the final fp64 comparison only."""
+Operands are small integers: every product, the fp32 accumulators and the fp32 partial sums are
+exact, so the partials (taken from the accumulators, before the bf16 rounding of the store) must
+match the fp64 sums of the exact product to rounding of the final fp64 comparison only."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -20,9 +21,9 @@ def _ints(shape, gen, lo=-2, hi=3):
     return torch.randint(lo, hi, shape, generator=gen).float()
 
 
-def _check(out2d, part, rows, shift):
+def _check(exact2d, part, rows, shift):
     assert rows > 0
-    y = out2d.double().cpu()
+    y = exact2d.double().cpu()
     d = y - shift.double().cpu()
     got = part[:rows].double().cpu().sum(0)
     assert torch.isfinite(got).all()
@@ -38,8 +39,9 @@ def test_gemm_stats_bf16(gpu, M, N, K):
     out = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
     part = torch.full((native().gemm_stats_rows(M), 2, N), float("nan"), device=gpu)
     rows = native().gemm_(A, B, True, True, out, part=part, shift=shift)
-    torch.testing.assert_close(out.float().cpu(), (A.float() @ B.float().t()).bfloat16().float().cpu(), rtol=0, atol=0)
-    _check(out, part, rows, shift)
+    exact = A.double().cpu() @ B.double().cpu().t()
+    torch.testing.assert_close(out.float().cpu(), exact.float().bfloat16().float(), rtol=0, atol=0)
+    _check(exact, part, rows, shift)
 
 
 def test_gemm_stats_declines_small(gpu):
@@ -67,8 +69,9 @@ def test_gemm_fp8_stats(gpu, mx):
     out = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
     part = torch.full((native().gemm_stats_rows(M), 2, N), float("nan"), device=gpu)
     rows = native().gemm_fp8_(Aq, Bq, sa, sb, out, part=part, shift=shift)
-    torch.testing.assert_close(out.float().cpu(), (A @ B.t()).bfloat16().float(), rtol=0, atol=0)
-    _check(out, part, rows, shift)
+    exact = A.double() @ B.double().t()
+    torch.testing.assert_close(out.float().cpu(), exact.float().bfloat16().float(), rtol=0, atol=0)
+    _check(exact, part, rows, shift)
 
 
 @pytest.mark.parametrize("fp8", [None, "tensor", "mx"])
@@ -96,7 +99,7 @@ def test_conv_fwd_stats(gpu, fp8):
             sx, sw = torch.ones(1, device=gpu), torch.ones(1, device=gpu)
         rows = native().conv_fwd_fp8_(xq, wq, sx, sw, out, 3, 3, 1, 1, part=part, shift=shift)
     torch.testing.assert_close(out.float().cpu(), ref.bfloat16().float(), rtol=0, atol=0)
-    _check(out, part, rows, shift)
+    _check(ref, part, rows, shift)
 
 
 @pytest.mark.parametrize("k,cin,cout,force", [(1, 256, 256, "psds"), (3, 64, 256, "psds_igemm")])
@@ -144,6 +147,8 @@ def test_fp8_conv_bn_stats_handover_matches_reduce(gpu, monkeypatch):
         torch.manual_seed(5)
         conv = Conv1x1(256, 512, fp8=True).to(gpu, torch.bfloat16).to(memory_format=CL)
         bn = FusedBatchNorm2d(512, relu=True).to(gpu)
+        bn.weight.data = bn.weight.data.to(torch.bfloat16)
+        bn.bias.data = bn.bias.data.to(torch.bfloat16)
         object.__setattr__(conv, "_psd_bn", bn)
         x = torch.randn(16, 256, 32, 32, device=gpu).to(torch.bfloat16).contiguous(memory_format=CL)
         x.requires_grad_(True)
