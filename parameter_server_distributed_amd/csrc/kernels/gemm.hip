@@ -1179,11 +1179,15 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
       // (rows past M need no mask: their A rows load as zeros -- K-major A past the descriptor, or the
       // implicit GEMM's out-of-image sentinel -- so their accumulators are exactly 0)
       f32x2 t1[2][2], t2[2][2];
+      float shk[2][2];  // the shift of this lane's 4 columns (read before the staging overwrites it)
       if constexpr (ST) {
 #pragma unroll
         for (int qn = 0; qn < 2; ++qn)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) t1[qn][j] = t2[qn][j] = f32x2{0.f, 0.f};
+          for (int j = 0; j < 2; ++j) {
+            shk[qn][j] = reinterpret_cast<const float*>(stg + 256)[qn * 32 + j * 16 + cl];
+            t1[qn][j] = t2[qn][j] = f32x2{0.f, 0.f};
+          }
       }
 #pragma unroll
       for (int qm = 0; qm < 2; ++qm)
@@ -1247,7 +1251,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
             a2 += st_xor16(a2, lane);
             a1 += st_xor32(a1, lane);
             a2 += st_xor32(a2, lane);
-            const float k = reinterpret_cast<const float*>(stg + 256)[qn * 32 + j * 16 + cl];
+            const float k = shk[qn][j];
             a2 = fmaf(-k, fmaf(-cnt, k, 2.f * a1), a2);
             a1 = fmaf(-cnt, k, a1);
             const int n = cn0 + wc * 64 + qn * 32 + j * 16 + cl;
