@@ -584,8 +584,8 @@ class _Conv1x1Fn(torch.autograd.Function):
             out = torch.empty(n * h * w, cout, device=x.device, dtype=x.dtype)
             part = _stats_part(bn, n * h * w, cout, x.device)
             rows = _native().gemm_(x2, w2, True, True, out, part=part, shift=bn.running_mean)
-            if rows == 0:
-                raise RuntimeError("gemm_ declined the statistics epilogue on a shape it ran before")
+            if rows == 0:  # too few tiles for the 8-phase kernel: the plain GEMM, the BN reduces
+                _native().gemm_(x2, w2, True, True, out)
             y = _from_2d(out, n, h, w)
             _hand_stats(bn, y, part, rows)
             return y
@@ -862,9 +862,7 @@ class _ConvFn(torch.autograd.Function):
 
         def igemm_stats():  # the implicit GEMM with the consumer BN's statistics in its epilogue
             y = _igemm(x, w2, k, stride, pad, bn)
-            if y is None:
-                raise RuntimeError("conv_fwd_ declined the statistics epilogue on a shape it ran before")
-            return y
+            return miopen() if y is None else y
 
         cands = {"miopen": miopen}
         if _igemm_ok(cin, cout):

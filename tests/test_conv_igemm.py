@@ -42,7 +42,7 @@ def test_conv_fwd_declines_unsupported(gpu):
     x = torch.zeros(2, 96, 8, 8, device=gpu, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
     w2 = torch.zeros(256, 9 * 96, device=gpu, dtype=torch.bfloat16)
     out = torch.empty(2 * 64, 256, device=gpu, dtype=torch.bfloat16)
-    assert native().conv_fwd_(x, w2, out, 3, 3, 1, 1) is False  # C not a power of two
+    assert not native().conv_fwd_(x, w2, out, 3, 3, 1, 1)  # C not a power of two
 
 
 @pytest.mark.parametrize("stride", [1, 2])
@@ -137,7 +137,7 @@ def test_conv_fwd_fp8_declines_small_c(gpu):
     wq = torch.zeros(256, 9 * 64, device=gpu).to(torch.float8_e4m3fn)
     one = torch.ones(1, device=gpu)
     out = torch.empty(2 * 64, 256, device=gpu, dtype=torch.bfloat16)
-    assert native().conv_fwd_fp8_(xq, wq, one, one, out, 3, 3, 1, 1) is False  # C < 128
+    assert not native().conv_fwd_fp8_(xq, wq, one, one, out, 3, 3, 1, 1)  # C < 128
 
 
 @pytest.mark.parametrize("kind", ["3x3", "3x3s2", "1x1"])
