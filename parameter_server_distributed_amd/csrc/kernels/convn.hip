@@ -131,6 +131,16 @@ __device__ __forceinline__ float ror_row(float x) {  // x of lane (l + N) mod 16
   return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x120 + N, 0xF, 0xF, true));
 }
 
+// x / d for 0 <= x < 2^24 through the fp32 reciprocal (exact after one correction step: the
+// product's error is below one unit there) -- the per-row integer divisions of an epilogue that
+// maps output rows back to (n, h, w) cost ~40 instructions each
+__device__ __forceinline__ int fdiv(int x, int d, float inv) {
+  int q = (int)((float)x * inv);
+  const int r = x - q * d;
+  q += (r >= d ? 1 : 0) - (r < 0 ? 1 : 0);
+  return q;
+}
+
 template <int BM, int BN, int WNT, int NSLOT>
 struct Geo {
   static constexpr int WM = BM / 64;         // wave rows (64 output pixels each)
@@ -392,6 +402,12 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
   const int my_c16 = lane % CPR;
   const int my_col = n0 + wc * WNT + my_c16 * 8;
   float bmu[8], bsc[8], bsh[8], ga[8], gb[8], bmd[8], gd[8];
+  float inv_hw = 0.f, inv_wo = 0.f;
+  const bool fast_div = a.M < (1 << 24);
+  if constexpr (BWD == 5) {
+    inv_hw = 1.f / (float)(a.Ho * a.Wo);
+    inv_wo = 1.f / (float)a.Wo;
+  }
   if constexpr (BWD == 3) {
     load8_f32(a.bmean_d + my_col, bmd);
 #pragma unroll
@@ -437,7 +453,9 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
             if constexpr (BWD == 5) {
               // residual-branch gradient of a stride-2 1x1 (downsample) convolution, on the quarter
               // grid: non-zero only at even (h, w) of this (Ho x Wo) output grid
-              const int hw = a.Ho * a.Wo, n = m / hw, rem = m - n * hw, h = rem / a.Wo, w = rem - h * a.Wo;
+              const int hw = a.Ho * a.Wo;
+              const int n = fast_div ? fdiv(m, hw, inv_hw) : m / hw, rem = m - n * hw;
+              const int h = fast_div ? fdiv(rem, a.Wo, inv_wo) : rem / a.Wo, w = rem - h * a.Wo;
               if (((h | w) & 1) == 0) {
                 const int64_t q = ((int64_t)n * (a.Ho >> 1) + (h >> 1)) * (a.Wo >> 1) + (w >> 1);
                 load8_bf16(a.bdr + q * a.N + my_col, rv);
