@@ -78,8 +78,10 @@ def parse():
                          "(parallel/async_ps.py); collective: lock-step RCCL reduce-scatter/all-gather with a "
                          "fixed S-step gradient delay (parallel/collective_ps.py)")
     ap.add_argument("--bucket-mb", type=float, default=0.0,
-                    help="push bucket size; 0 (default): at N > 1 probe the per-link p2p bandwidth vs size over "
-                         "RCCL before building the PS and take the knee (parallel/bucketing.py), 16 MB at N = 1")
+                    help="push bucket size; 0 (default): at N > 1 probe the bandwidth vs size of the transport the "
+                         "chosen plane pushes with (async: the engine's peer DMA into the owners' inboxes; "
+                         "collective: RCCL send/recv) before the timed steps and take the knee "
+                         "(parallel/bucketing.py), 16 MB at N = 1")
     ap.add_argument("--fp8-compute", type=int, default=-1,
                     help="fp8 (e4m3 MFMA) forward of the bottleneck convolutions, bf16 backward "
                          "(1/0; -1: on for Wide-ResNet-101-2, the BASELINE 'CDNA4 fp8 MFMA' config)")
@@ -164,6 +166,21 @@ def autotune_summary() -> dict:
     return out
 
 
+def _autotune_source() -> dict:
+    """Per-rank decision sources (ops/autotune.py source()), summed over ranks: at N > 1 every
+    shape is timed by exactly one rank ("claimed") and taken by the others ("peer")."""
+    from parameter_server_distributed_amd.ops import autotune
+
+    src = autotune.source()
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        t = torch.tensor([src[k] for k in sorted(src)], dtype=torch.float64)
+        if dist.get_backend() == "nccl":
+            t = t.cuda()
+        dist.all_reduce(t)
+        src = {k: int(v) for k, v in zip(sorted(src), t.tolist())}
+    return src
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -201,17 +218,11 @@ def main():
     else:
         shards = max(1, min(a.ps_shards, world))
     bucket_probe = None
-    if a.bucket_mb <= 0:
+    bucket_transport = None
+    auto_bucket = a.bucket_mb <= 0
+    if auto_bucket:
         a.bucket_mb = 16.0
-        if world > 1 and a.backend == "nccl":
-            from parameter_server_distributed_amd.parallel import bucketing
-
-            try:
-                bucket_probe = bucketing.probe_p2p(dev)
-                model_mb = sum(p.numel() for p in spec.model.parameters()) * 2 / 2**20
-                a.bucket_mb = bucketing.choose_bucket_mb(bucket_probe, model_mb)
-            except Exception as e:  # noqa: BLE001 -- a diagnostic must not cost the run
-                bucket_probe = {"error": str(e)[:200]}
+    model_mb = sum(p.numel() for p in spec.model.parameters()) * 2 / 2**20
     pull_dtype = a.pull_dtype or ("fp8" if a.model.startswith("wide") else "bf16")
     mode = a.ps_mode  # both planes publish MX e4m3 weights for the fp8 config
     fallback = None
@@ -230,6 +241,27 @@ def main():
             torch.manual_seed(1234)
             spec = models.build(a.model, dev, torch.bfloat16, image_size=a.image_size, seq_len=a.seq_len,
                                 fp8=fp8_compute)
+    if mode == "async" and auto_bucket and world > 1:
+        # bucket size from the transport this plane pushes with (engine DMA into the owners'
+        # inboxes, alternating push streams), probed before the timed steps (parallel/bucketing.py)
+        from parameter_server_distributed_amd.parallel import bucketing
+
+        try:
+            bucket_probe = ps.probe_push_sizes()
+            bucket_transport = "async engine peer DMA (hipMemcpyAsync into the owners' IPC inboxes)"
+            a.bucket_mb = bucketing.choose_bucket_mb(bucket_probe, model_mb)
+            ps.rebucket(a.bucket_mb)
+        except Exception as e:  # noqa: BLE001 -- a diagnostic must not cost the run
+            bucket_probe = {"error": str(e)[:200]}
+    if mode == "collective" and auto_bucket and world > 1 and a.backend == "nccl":
+        from parameter_server_distributed_amd.parallel import bucketing
+
+        try:  # the collective plane's transport: RCCL point-to-point over xGMI
+            bucket_probe = bucketing.probe_p2p(dev)
+            bucket_transport = "RCCL send/recv"
+            a.bucket_mb = bucketing.choose_bucket_mb(bucket_probe, model_mb)
+        except Exception as e:  # noqa: BLE001
+            bucket_probe = {"error": str(e)[:200]}
     if mode == "collective":
         transport = make_transport(a.transport, dev)
         ps = CollectivePS(spec.model, optim, transport, num_shards=shards, staleness=a.staleness,
@@ -326,6 +358,7 @@ def main():
     if world > 1:
         dist.all_reduce(finite, op=dist.ReduceOp.MIN)
     params_finite = bool(finite.item() > 0)
+    at_src = _autotune_source()  # (a collective at N > 1: every rank)
     if not params_finite and rank == 0:
         print("WARNING: non-finite weights or loss at the end of the timed steps", file=sys.stderr, flush=True)
     if rank == 0:
@@ -359,10 +392,12 @@ def main():
                                  f"up to {a.staleness + 1} steps stale (SSP bound {a.staleness})"
                                  if a.model in REF_BASELINE else None),
             "bucket_mb_chosen": a.bucket_mb, "bucket_probe_GBps": bucket_probe,
+            "bucket_probe_transport": bucket_transport,
             "staleness_p50": p50, "staleness_hist": hist, "final_loss": round(final_loss, 4),
             "params_finite": params_finite, "comm_probe_busbw_GBps": probe, "async_plane_bw": async_bw,
             "warmup_s": round(t_w, 2), "peak_mem_gb": round(mem_peak / 2**30, 2),
             "autotune": autotune_summary(),
+            "autotune_source": at_src,
         }
         line = json.dumps(rec)
         print(line, flush=True)

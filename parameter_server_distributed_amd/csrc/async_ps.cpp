@@ -43,6 +43,7 @@ struct alignas(64) ShardCtl {
   std::atomic<int64_t> version;  // applies completed
   std::atomic<int32_t> latest;   // publish buffer holding `version`
   int32_t pad;
+  std::atomic<int64_t> base_version;  // the version publish_initial published (fixed-schedule pulls)
   std::atomic<int64_t> buf_version[kMaxBuf];
   std::atomic<int32_t> readers[kMaxBuf];
   std::atomic<int64_t> clock[kMaxWorkers];  // pushes of worker wi applied at this shard
@@ -371,9 +372,11 @@ void AsyncEngine::publish_initial(int shard, int64_t version, std::vector<int64_
   if (mx_) quant_publish(st, shard, 0, c10::hip::getCurrentHIPStream((c10::DeviceIndex)device_).stream());
   if (device_ >= 0) hip_ok(hipDeviceSynchronize(), "hipDeviceSynchronize");
   ShardCtl& s = ctl_->shard[shard];
+  for (int b = 1; b < nbuf_; ++b) s.buf_version[b].store(-1);
   s.buf_version[0].store(version);
   s.latest.store(0);
   s.version.store(version);
+  s.base_version.store(version);
   for (size_t wi = 0; wi < clocks.size(); ++wi) s.clock[wi].store(clocks[wi]);
   st.enq = version;
   st.round.clear();
@@ -381,18 +384,51 @@ void AsyncEngine::publish_initial(int shard, int64_t version, std::vector<int64_
 
 void AsyncEngine::set_round(int k) {
   TORCH_CHECK(!running_, "psd async: set_round while the engine runs");
-  TORCH_CHECK(k >= 1 && k <= (int)workers_.size() && k <= kMaxSources, "psd async: round size must be in [1, min(W, ",
-              kMaxSources, ")], got ", k);
+  TORCH_CHECK(k >= 1 && k <= (int)workers_.size(), "psd async: round size must be in [1, W = ", workers_.size(),
+              "], got ", k);
   round_ = k;
 }
 
+void AsyncEngine::set_fixed_schedule(bool on) {
+  TORCH_CHECK(!running_, "psd async: set_fixed_schedule while the engine runs");
+  TORCH_CHECK(!on || round_ == (int)workers_.size(), "psd async: the fixed schedule needs rounds of K = W pushes");
+  TORCH_CHECK(!on || nbuf_ >= S_ + 2, "psd async: the fixed schedule keeps S + 1 versions: nbuf >= S + 2 (nbuf ",
+              nbuf_, ", S ", S_, ")");
+  fixed_ = on;
+}
+
+// The least recently published free buffer (not the latest, no enqueued apply, no reader): the
+// fixed schedule's readers need the last S + 1 versions to stay until they are older than that.
 int AsyncEngine::free_buf(int shard) const {
   const ShardState& st = shards_[shard];
   const ShardCtl& s = ctl_->shard[shard];
   const int latest = s.latest.load();
-  for (int b = 0; b < nbuf_; ++b)
-    if (b != latest && !st.busy[b] && s.readers[b].load() == 0) return b;
-  return -1;
+  int best = -1;
+  int64_t best_v = 0;
+  for (int b = 0; b < nbuf_; ++b) {
+    if (b == latest || st.busy[b] || s.readers[b].load() != 0) continue;
+    const int64_t v = s.buf_version[b].load();
+    if (best < 0 || v < best_v) {
+      best = b;
+      best_v = v;
+    }
+  }
+  return best;
+}
+
+// Claim free buffer b for an apply: invalidate its version, then re-check its reader count. A
+// fixed-schedule reader pins (readers++) and then checks the version, so with these two
+// sequentially consistent store -> load orders at least one side sees the other: the reader backs
+// off, or the claim is dropped (the version is restored) and the round waits.
+bool AsyncEngine::claim_buf(int shard, int b) {
+  ShardCtl& s = ctl_->shard[shard];
+  const int64_t v = s.buf_version[b].load();
+  s.buf_version[b].store(-1);
+  if (s.readers[b].load() != 0) {
+    s.buf_version[b].store(v);
+    return false;
+  }
+  return true;
 }
 
 void AsyncEngine::start() {
@@ -491,10 +527,14 @@ bool AsyncEngine::poll_once() {
       Mailbox& mb = ctl_->mb[k][wi];
       const int64_t t = mb.tail.load();
       if (t >= mb.head.load()) continue;
+      // fixed schedule: round r takes exactly every worker's step-r push (a faster worker's next
+      // push waits in its mailbox) -- the round composition no longer depends on arrival timing
+      if (fixed_ && mb.ring[t % kRing].step != st.enq) continue;
       const bool completes = (int)st.round.size() + 1 >= round_;
       int buf = -1;
       if (completes) {
         buf = free_buf(k);
+        if (buf >= 0 && !claim_buf(k, buf)) buf = -1;
         if (buf < 0) break;  // every snapshot is pinned or in flight: retry after completions
       }
       const Msg m = mb.ring[t % kRing];
@@ -534,7 +574,24 @@ bool AsyncEngine::poll_once() {
 // One update: optimizer step counter, fused apply of the round's inbox slots (summed in registers,
 // scaled by the dyn grad_scale = 1/K) onto the fp32 master, and the new snapshot written into
 // publish buffer `buf` (bf16: by the apply kernel itself).
-void AsyncEngine::apply_into(ShardState& st, const std::vector<at::Tensor>& g, int buf) {
+void AsyncEngine::apply_into(ShardState& st, const std::vector<at::Tensor>& g_in, int buf) {
+  // a round of more than 16 pushes (the fused apply kernel's source limit): each group of 16
+  // inbox slots (worker order) is summed into an fp32 workspace and the apply takes the group sums
+  // (fixed order, so rounds stay bitwise reproducible). With K = W every round completes -- a
+  // partial round stranded at W > 16 would hold a worker's clock back forever.
+  std::vector<at::Tensor> g = g_in;
+  if (g.size() > (size_t)kMaxSources) {
+    const size_t ng = (g.size() + kMaxSources - 1) / kMaxSources;
+    TORCH_CHECK(ng <= (size_t)kMaxSources, "psd async: at most 256 pushes per round");
+    while (st.acc.size() < ng) st.acc.push_back(at::empty({st.master.numel()}, st.master.options().dtype(at::kFloat)));
+    std::vector<at::Tensor> sums;
+    for (size_t gi = 0; gi < ng; ++gi) {
+      const size_t b = gi * kMaxSources, e = std::min(g.size(), b + kMaxSources);
+      multi_reduce_(st.acc[gi], std::vector<at::Tensor>(g.begin() + b, g.begin() + e), 1.0);
+      sums.push_back(st.acc[gi]);
+    }
+    g = std::move(sums);
+  }
   optim_advance_(st.dyn, st.hyper.beta1, st.hyper.beta2);
   const bool bf16 = esz_ == 2;
   fused_apply_(st.master, g, st.s1.defined() ? c10::optional<at::Tensor>(st.s1) : c10::nullopt,
@@ -658,12 +715,32 @@ std::vector<int64_t> AsyncEngine::pull_impl(int64_t step, char* dst, char* dst_s
   std::vector<int64_t> pulled(P);
   for (int k = 0; k < P; ++k) {
     ShardCtl& s = ctl_->shard[k];
-    int b;
-    for (;;) {  // pin the latest snapshot (re-check: the owner never writes the latest or a pinned one)
-      b = s.latest.load();
-      s.readers[b].fetch_add(1);
-      if (s.latest.load() == b) break;
-      s.readers[b].fetch_sub(1);
+    int b = -1;
+    if (fixed_) {
+      // fixed schedule: exactly version max(step - S, base) -- the SSP bound's oldest admissible
+      // snapshot, whatever the timing (deterministic staleness S). Pin, then check the version
+      // (claim_buf's protocol); the owner keeps the last S + 1 versions (LRU reuse, nbuf >= S + 2)
+      const int64_t want = std::max(step - (int64_t)S_, s.base_version.load());
+      for (int bb = 0; bb < nbuf_ && b < 0; ++bb) {
+        s.readers[bb].fetch_add(1);
+        if (s.buf_version[bb].load() == want) b = bb;
+        else s.readers[bb].fetch_sub(1);
+      }
+      if (b < 0) {
+        const std::string m = "fixed-schedule pull of step " + std::to_string(step) + " on rank " +
+                              std::to_string(rank_) + ": version " + std::to_string(want) + " of shard " +
+                              std::to_string(k) + " is no longer published (latest " +
+                              std::to_string(s.version.load()) + ")";
+        fail(m);
+        TORCH_CHECK(false, "psd async: ", m);
+      }
+    } else {
+      for (;;) {  // pin the latest snapshot (re-check: the owner never writes the latest or a pinned one)
+        b = s.latest.load();
+        s.readers[b].fetch_add(1);
+        if (s.latest.load() == b) break;
+        s.readers[b].fetch_sub(1);
+      }
     }
     pulled[k] = s.buf_version[b].load();
     if (dst_sc) {

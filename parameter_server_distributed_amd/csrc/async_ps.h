@@ -69,7 +69,12 @@ class AsyncEngine {
   // bf16(master) -> publish buffer 0 as the shard's snapshot `version` (blocking); with `clocks`
   // (one per worker) the SSP clocks are restored too (checkpoint resume)
   void publish_initial(int shard, int64_t version = 0, std::vector<int64_t> clocks = {});
-  void set_round(int k);            // pushes per optimizer step (1..min(W, 16)); before start()
+  void set_round(int k);            // pushes per optimizer step (1..W); before start()
+  // fixed schedule (before start(); needs K = W and nbuf >= S + 2): round r holds exactly every
+  // worker's step-r push and a pull of step t takes exactly version max(t - S, base). The staleness
+  // is then S for every gradient after the first S steps, independent of timing: the trajectory
+  // is synchronous SGD with S-step-delayed gradients, bit-for-bit reproducible (tests, debugging).
+  void set_fixed_schedule(bool on);
   void start();
   void stop();
   // teardown in two collective phases (barrier between): unmap the peers' memory, then free our
@@ -126,6 +131,7 @@ class AsyncEngine {
     std::vector<bool> busy;           // publish buffer is the target of an enqueued apply
     int64_t enq = 0;                  // applies enqueued (the version the next apply starts from)
     std::vector<RoundItem> round;     // pushes taken from the mailboxes, not yet applied
+    std::vector<at::Tensor> acc;      // fp32 group sums (rounds of more than 16 pushes)
   };
 
   void quant_publish(ShardState& st, int shard, int buf, void* stream);
@@ -141,6 +147,7 @@ class AsyncEngine {
   char* publish_ptr(int shard, int buf) const;
   void apply_into(ShardState& st, const std::vector<at::Tensor>& g, int buf);
   int free_buf(int shard) const;
+  bool claim_buf(int shard, int b);
   static bool done(void* event);
   void run();
   bool poll_once();
@@ -154,6 +161,7 @@ class AsyncEngine {
 
   int rank_, world_, S_, nbuf_, device_;
   int round_ = 1;
+  bool fixed_ = false;
   double timeout_s_;
   double dead_after_s_ = 10.0;  // a peer's engine silent this long is presumed dead (PSD_ASYNC_DEAD_S)
   int esz_;

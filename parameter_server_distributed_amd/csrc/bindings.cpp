@@ -96,6 +96,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("save_invstd"), py::arg("part"), py::arg("rows"), py::arg("dgamma_out") = py::none(),
         py::arg("dbeta_out") = py::none(), py::arg("dq") = py::none(), py::arg("dqmx") = py::none());
   m.def("convn_variants", &convn_variants_, py::arg("N"));
+  m.def("convn_variant_kind", &convn_variant_kind_, py::arg("N"), py::arg("variant"));
   m.def("conv_fwd_", &conv_fwd_, py::arg("x"), py::arg("w2"), py::arg("out"), py::arg("R"), py::arg("S"),
         py::arg("stride"), py::arg("pad"), py::arg("part") = py::none(), py::arg("shift") = py::none());
   m.def("conv_wgrad_", &conv_wgrad_, py::arg("dy"), py::arg("x"), py::arg("out"), py::arg("R"), py::arg("S"),
@@ -277,6 +278,7 @@ PYBIND11_MODULE(_C, m) {
       .def("publish_initial", &AsyncEngine::publish_initial, py::arg("shard"), py::arg("version") = 0,
            py::arg("clocks") = std::vector<int64_t>{})
       .def("set_round", &AsyncEngine::set_round)
+      .def("set_fixed_schedule", &AsyncEngine::set_fixed_schedule)
       .def("start", &AsyncEngine::start)
       .def("stop", &AsyncEngine::stop, py::call_guard<py::gil_scoped_release>())
       .def("close_peers", &AsyncEngine::close_peers)

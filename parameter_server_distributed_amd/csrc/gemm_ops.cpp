@@ -262,6 +262,7 @@ bool convn_variant_ok_(int64_t N, int64_t v, int64_t R, int64_t S, int64_t strid
   return convn_variant_ok((int)N, (int)v, (int)R, (int)S, (int)stride, (int)pad, (int)Wo, has_x2);
 }
 int64_t convn_variants_(int64_t N) { return convn_variants((int)N); }
+int64_t convn_variant_kind_(int64_t N, int64_t v) { return convn_variant_kind((int)N, (int)v); }
 
 namespace {
 // K-concatenated second operand + epilogue bias of a convn launch (the BN-backward fold); returns the

@@ -557,71 +557,27 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_dual_kernel(const uint16_t* 
 // two), so each pooled gradient is loaded once per block instead of once per covered input.
 __global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(const uint16_t* __restrict__ x, const float* __restrict__ ss,
                                                               uint16_t* __restrict__ y, uint8_t* __restrict__ arg, int N,
-                                                              int H, int W, int C, int Ho, int Wo) {
-  const int c8n = C >> 3;
-  const int64_t total = (int64_t)N * Ho * Wo * c8n;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    const int c8 = (int)(t % c8n);
-    int64_t r = t / c8n;
-    const int wo = (int)(r % Wo);
-    r /= Wo;
-    const int ho = (int)(r % Ho);
-    const int n = (int)(r / Ho);
+                                                              int H, int W, int C, int Ho, int Wo, FastDiv dc8,
+                                                              FastDiv dwo, FastDiv dho) {
+  // 32-bit item index (host: total < 2^31) split by fast division: (n, ho, wo, c8)
+  const uint32_t total = (uint32_t)N * Ho * Wo * dc8.d;
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    const uint32_t r = fdiv_q(t, dc8);
+    const int c8 = (int)(t - r * dc8.d);
+    const uint32_t r2 = fdiv_q(r, dwo);
+    const int wo = (int)(r - r2 * dwo.d);
+    const uint32_t n = fdiv_q(r2, dho);
+    const int ho = (int)(r2 - n * dho.d);
     float sc[8], sh[8];
     load8_f32(ss + c8 * 8, sc);
     load8_f32(ss + C + c8 * 8, sh);
     float best[8];
     uint8_t bi[8];
     maxpool3s2_max8(
-        x, n, ho, wo, c8, H, W, C,
+        x, (int)n, ho, wo, c8, H, W, C,
         [&](float v, int e) { return bf16_to_f32(f32_to_bf16(relu_nan(fmaf(v, sc[e], sh[e])))); }, best, bi);
-    store8_bf16(y + t * 8, best);
-    store_argmax8(arg + t * 8, bi);
-  }
-}
-
-// Pool gradient of the 2x2 input block (2k.., 2j..) for 8 channels: g[q][8], q = 2*(row parity) + col parity.
-__device__ __forceinline__ void pool_grad_block(const uint16_t* __restrict__ gp, const uint16_t* __restrict__ gp2,
-                                                const uint8_t* __restrict__ arg, int n, int k, int j, int c8, int C,
-                                                int Ho, int Wo, float g[4][8]) {
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) g[q][e] = 0.f;
-  // output (k + a, j + b) -> input (2k + pr, 2j + pc) through window offset (dh, dw) = (pr + 1 - 2a, pc + 1 - 2b)
-#pragma unroll
-  for (int a = 0; a < 2; ++a) {
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int ho = k + a, wo = j + b;
-      if (ho >= Ho || wo >= Wo) continue;
-      const int64_t o = (((int64_t)n * Ho + ho) * Wo + wo) * C + c8 * 8;
-      const uint2 ai = *reinterpret_cast<const uint2*>(arg + o);
-      float v[8];
-      load8_bf16(gp + o, v);
-      if (gp2) {
-        float v2[8];
-        load8_bf16(gp2 + o, v2);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += v2[e];
-      }
-#pragma unroll
-      for (int pr = 0; pr < 2; ++pr) {
-        const int dh = pr + 1 - 2 * a;
-        if (dh < 0) continue;
-#pragma unroll
-        for (int pc = 0; pc < 2; ++pc) {
-          const int dw = pc + 1 - 2 * b;
-          if (dw < 0) continue;
-          const uint8_t want = (uint8_t)(dh * 3 + dw);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const uint8_t ae = (uint8_t)(((e < 4 ? ai.x : ai.y) >> (8 * (e & 3))) & 0xff);
-            if (ae == want) g[2 * pr + pc][e] += v[e];
-          }
-        }
-      }
-    }
+    store8_bf16(y + (int64_t)t * 8, best);
+    store_argmax8(arg + (int64_t)t * 8, bi);
   }
 }
 
@@ -633,7 +589,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_pool_kernel(const uint16_t*
                                                                  const float* __restrict__ ssf,
                                                                  const uint16_t* __restrict__ x,
                                                                  const float* __restrict__ mean, int N, int H, int W,
-                                                                 int C, float* __restrict__ part) {
+                                                                 int C, float* __restrict__ part, FastDiv dwo,
+                                                                 FastDiv dho) {
   const Map m = make_map(C);
   const int Ho = H / 2, Wo = W / 2;
   float a[8], b[8], mu[8], sc[8], sh[8];
@@ -643,15 +600,15 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_pool_kernel(const uint16_t*
     load8_f32(mean + m.cg * 8, mu);
     load8_f32(ssf + m.cg * 8, sc);
     load8_f32(ssf + C + m.cg * 8, sh);
-    const int64_t items = (int64_t)N * Ho * Wo;
-    const int64_t stride = (int64_t)gridDim.x * m.rpi;
-    for (int64_t it = (int64_t)blockIdx.x * m.rpi + m.r0; it < items; it += stride) {
-      const int j = (int)(it % Wo);
-      const int64_t q = it / Wo;
-      const int k = (int)(q % Ho);
-      const int n = (int)(q / Ho);
+    const uint32_t items = (uint32_t)N * Ho * Wo;  // host: < 2^31
+    const uint32_t stride = gridDim.x * m.rpi;
+    for (uint32_t it = blockIdx.x * m.rpi + m.r0; it < items; it += stride) {
+      const uint32_t q = fdiv_q(it, dwo);
+      const int j = (int)(it - q * dwo.d);
+      const uint32_t n = fdiv_q(q, dho);
+      const int k = (int)(q - n * dho.d);
       float g[4][8];
-      pool_grad_block(gp, gp2, arg, n, k, j, m.cg, C, Ho, Wo, g);
+      pool_grad_block(gp, gp2, arg, (int)n, k, j, m.cg, C, Ho, Wo, g);
 #pragma unroll
       for (int pq = 0; pq < 4; ++pq) {
         const int h = 2 * k + (pq >> 1), w = 2 * j + (pq & 1);
@@ -675,13 +632,13 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_pool_kernel(const uint16_t* 
                                                                 const float* __restrict__ ssf,
                                                                 const uint16_t* __restrict__ x,
                                                                 const float* __restrict__ coef,
-                                                                uint16_t* __restrict__ dx, int N, int H, int W, int C) {
-  const int c8n = C >> 3;
+                                                                uint16_t* __restrict__ dx, int N, int H, int W, int C,
+                                                                FastDiv dc8, FastDiv dwo, FastDiv dho) {
   const int Ho = H / 2, Wo = W / 2;
-  const int64_t total = (int64_t)N * Ho * Wo * c8n;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;  // host: stride % c8n == 0
-  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int c8 = (int)(t % c8n);
+  const uint32_t total = (uint32_t)N * Ho * Wo * dc8.d;  // host: < 2^31
+  const uint32_t stride = gridDim.x * blockDim.x;        // host: stride % c8n == 0
+  uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c8 = (int)(t - fdiv_q(t, dc8) * dc8.d);
   float A[8], B[8], Cc[8], sc[8], sh[8];
   load8_f32(coef + c8 * 8, A);
   load8_f32(coef + C + c8 * 8, B);
@@ -689,13 +646,13 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_pool_kernel(const uint16_t* 
   load8_f32(ssf + c8 * 8, sc);
   load8_f32(ssf + C + c8 * 8, sh);
   for (; t < total; t += stride) {
-    const int64_t it = t / c8n;
-    const int j = (int)(it % Wo);
-    const int64_t q = it / Wo;
-    const int k = (int)(q % Ho);
-    const int n = (int)(q / Ho);
+    const uint32_t it = fdiv_q(t, dc8);
+    const uint32_t q = fdiv_q(it, dwo);
+    const int j = (int)(it - q * dwo.d);
+    const uint32_t n = fdiv_q(q, dho);
+    const int k = (int)(q - n * dho.d);
     float g[4][8];
-    pool_grad_block(gp, gp2, arg, n, k, j, c8, C, Ho, Wo, g);
+    pool_grad_block(gp, gp2, arg, (int)n, k, j, c8, C, Ho, Wo, g);
 #pragma unroll
     for (int pq = 0; pq < 4; ++pq) {
       const int h = 2 * k + (pq >> 1), w = 2 * j + (pq & 1);
@@ -793,8 +750,10 @@ hipError_t launch_bn_fwd(const BnFwdArgs& a, hipStream_t st) {
       return hipErrorInvalidValue;
     const int Ho = a.H / 2, Wo = a.W / 2;
     const int64_t total = (int64_t)a.N * Ho * Wo * (a.C / 8);
+    if (total >= ((int64_t)1 << 31) - 2048 * 256) return hipErrorInvalidValue;  // 32-bit item indices
     hipLaunchKernelGGL(bn_relu_maxpool_kernel, dim3(stream_grid(total, 256)), dim3(256), 0, st, a.x, a.ss, a.y,
-                       a.pool_arg, a.N, a.H, a.W, a.C, Ho, Wo);
+                       a.pool_arg, a.N, a.H, a.W, a.C, Ho, Wo, make_fastdiv((uint32_t)(a.C / 8)),
+                       make_fastdiv((uint32_t)Wo), make_fastdiv((uint32_t)Ho));
     return hipGetLastError();
   }
   const int64_t nvec = a.M * (a.C / 8);
@@ -865,15 +824,18 @@ int bn_pool_reduce_blocks(int N, int H, int W, int C) {
 static hipError_t launch_bn_bwd_pool(const BnBwdArgs& a, hipStream_t st) {
   if (!a.relu || !a.ss || a.dr || a.dy2 || !bn_pool_supported(a.H, a.W, a.C) || (int64_t)a.N * a.H * a.W != a.M)
     return hipErrorInvalidValue;
+  const int64_t total = (int64_t)a.N * (a.H / 2) * (a.W / 2) * (a.C / 8);
+  if (total >= ((int64_t)1 << 31) - 2048 * 256) return hipErrorInvalidValue;  // 32-bit item indices
+  const FastDiv dc8 = make_fastdiv((uint32_t)(a.C / 8)), dwo = make_fastdiv((uint32_t)(a.W / 2)),
+                dho = make_fastdiv((uint32_t)(a.H / 2));
   const int gx = bn_pool_reduce_blocks(a.N, a.H, a.W, a.C), gy = 1;  // the caller sized part for this
   hipLaunchKernelGGL(bn_bwd_reduce_pool_kernel, dim3(gx, gy), dim3(256), 0, st, a.gpool, a.gpool2, a.pool_arg, a.ss, a.x,
-                     a.save_mean, a.N, a.H, a.W, a.C, a.part);
+                     a.save_mean, a.N, a.H, a.W, a.C, a.part, dwo, dho);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((a.C + kFinCh - 1) / kFinCh), dim3(256), 0, st, a.part, gx, a.M, a.C,
                      a.gamma, a.save_mean, a.save_invstd, a.dgamma, a.dbeta, a.coef);
-  const int64_t total = (int64_t)a.N * (a.H / 2) * (a.W / 2) * (a.C / 8);
   const int g = elem_grid(total, a.C);
   hipLaunchKernelGGL(bn_bwd_elemt_pool_kernel, dim3(g), dim3(256), 0, st, a.gpool, a.gpool2, a.pool_arg, a.ss, a.x,
-                     a.coef, a.dx, a.N, a.H, a.W, a.C);
+                     a.coef, a.dx, a.N, a.H, a.W, a.C, dc8, dwo, dho);
   return hipGetLastError();
 }
 

@@ -56,6 +56,21 @@ __device__ __forceinline__ void store8_bf16(uint16_t* p, const float v[8]) {
   *reinterpret_cast<u32x4*>(p) = u32x4{ws[0], ws[1], ws[2], ws[3]};
 }
 
+// Division by a run-time-invariant divisor d >= 1 for 0 <= x < 2^31 (Granlund-Montgomery
+// round-up form): q = (umulhi(x, m) + x) >> s, m and s computed once on the host. A 64-bit `/` or
+// `%` is a ~100-instruction software sequence on the VALU; the grid-stride index maps of the stem's
+// pool kernels did five of them per 16-byte item (1,365 VALU per wave-iteration, profiles/pmc_r1.md).
+struct FastDiv {
+  uint32_t d, m, s;
+};
+inline FastDiv make_fastdiv(uint32_t d) {
+  uint32_t s = 0;
+  while ((1ull << s) < d) ++s;
+  const uint64_t m = ((uint64_t)1 << 32) * ((1ull << s) - d) / d + 1;
+  return FastDiv{d, (uint32_t)m, s};
+}
+__device__ __forceinline__ uint32_t fdiv_q(uint32_t x, const FastDiv& f) { return (__umulhi(x, f.m) + x) >> f.s; }
+
 // Grid size for a grid-stride streaming kernel: enough blocks to fill 256 CUs several times
 // over, capped so that launch + tail cost stays small (guide G11: <= ~2048 blocks).
 inline int stream_grid(int64_t work_items, int block) {

@@ -164,6 +164,212 @@ constexpr int halo_win_bytes(int bm) { return (bm + 2 * 64 + 8) * 128; }
 
 }  // namespace
 
+// Epilogue of one wave's 64 x WNT accumulator block (shared by the gathered / HALO kernel and the
+// persistent HALO kernel): per-wave, no barrier (``stg`` is this wave's own 2 KiB of LDS). C layout
+// of a 16x16 block: col = lane & 15, row = 4 * (lane >> 4) + r. ``pix(p)``: output pixel of tile row
+// p (-1: none); partial-statistics rows are (tm * WM + wr).
+template <int BM, int BN, int WNT, bool STATS, int BWD, typename Pix>
+__device__ __forceinline__ void convn_epilogue(const ConvnArgs& a, f32x4 (&acc)[4][WNT / 16],
+                                               const float (&kshift)[WNT / 16], int tm, int wr, int wc, int lane,
+                                               uint8_t* stg, Pix pix, int n0) {
+  constexpr int JN = WNT / 16;
+  constexpr int WM = BM / 64;
+  const int cl = lane & 15, rq = (lane >> 4) * 4;
+  // ---- epilogue (per wave, no barrier: the staging slot is this wave's own): C layout of a
+  // 16x16 block col = lane & 15, row = 4 * (lane >> 4) + r
+  if (a.bias) {  // per-output-channel bias (the BN-backward fold's constant term)
+#pragma unroll
+    for (int j = 0; j < JN; ++j) {
+      const float bv = a.bias[n0 + wc * WNT + j * 16 + cl];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i][j] += f32x4{bv, bv, bv, bv};
+    }
+  }
+  if constexpr (STATS) {
+#pragma unroll
+    for (int j = 0; j < JN; ++j) {
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float d = bf16_to_f32(f32_to_bf16(acc[i][j][r])) - kshift[j];
+          const bool ok = pix(wr * 64 + i * 16 + rq + r) >= 0;
+          s1 += ok ? d : 0.f;
+          s2 = ok ? fmaf(d, d, s2) : s2;
+        }
+      s1 += xor16(s1, lane);
+      s2 += xor16(s2, lane);
+      s1 += xor32(s1, lane);
+      s2 += xor32(s2, lane);
+      if (lane < 16) {
+        float* pr = a.part + ((int64_t)tm * WM + wr) * 2 * a.N;
+        const int col = n0 + wc * WNT + j * 16 + cl;
+        pr[col] = s1;
+        pr[a.N + col] = s2;
+      }
+    }
+  }
+  const int L = cl & 3;
+  constexpr int RB = WNT * 2;       // staged row bytes (one 16-row block)
+  constexpr int CPR = RB / 16;      // 16-byte chunks per staged row
+  constexpr int PASSES = 16 * CPR / 64;
+  uint16_t* y = reinterpret_cast<uint16_t*>(a.y);
+  // BWD: this lane's 8 output channels are fixed (64 % CPR == 0): per-channel constants once
+  const int my_c16 = lane % CPR;
+  const int my_col = n0 + wc * WNT + my_c16 * 8;
+  float bmu[8], bsc[8], bsh[8], ga[8], gb[8], bmd[8], gd[8];
+  float inv_hw = 0.f, inv_wo = 0.f;
+  const bool fast_div = a.M < (1 << 24);
+  if constexpr (BWD == 5) {
+    inv_hw = 1.f / (float)(a.Ho * a.Wo);
+    inv_wo = 1.f / (float)a.Wo;
+  }
+  if constexpr (BWD == 3) {
+    load8_f32(a.bmean_d + my_col, bmd);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) gd[e] = 0.f;
+  }
+  if constexpr (BWD != 0) {
+    load8_f32(a.bmean + my_col, bmu);
+    if constexpr (BWD == 1) {
+      load8_f32(a.bss + my_col, bsc);
+      load8_f32(a.bss + a.N + my_col, bsh);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ga[e] = gb[e] = 0.f;
+  }
+  // BWD: the epilogue operands of all this wave's rows (x, dr, mask bits, xd) are requested here,
+  // before the first is used -- the compiler cannot hoist them above the y stores (possible alias),
+  // and at one workgroup per CU (LDS) the per-row load -> use latency was the epilogue's cost
+  int mm[4][PASSES];
+  u32x4 exr[4][PASSES], rv4[4][PASSES], dv4[4][PASSES];
+  uint32_t bt[4][PASSES];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int ps = 0; ps < PASSES; ++ps) {
+      const int c = ps * 64 + lane;
+      const int rr = c / CPR;
+      const int m = pix(wr * 64 + i * 16 + rr);
+      mm[i][ps] = m;
+      if constexpr (BWD != 0) {
+        exr[i][ps] = rv4[i][ps] = dv4[i][ps] = u32x4{0u, 0u, 0u, 0u};
+        bt[i][ps] = 0u;
+        if (m >= 0) {
+          exr[i][ps] = *reinterpret_cast<const u32x4*>(a.bx + (int64_t)m * a.N + my_col);
+          if constexpr (BWD >= 2) {
+            if constexpr (BWD == 5) {
+              // residual-branch gradient of a stride-2 1x1 (downsample) convolution, on the quarter
+              // grid: non-zero only at even (h, w) of this (Ho x Wo) output grid
+              const int hw = a.Ho * a.Wo;
+              const int n = fast_div ? fdiv(m, hw, inv_hw) : m / hw, rem = m - n * hw;
+              const int h = fast_div ? fdiv(rem, a.Wo, inv_wo) : rem / a.Wo, w = rem - h * a.Wo;
+              if (((h | w) & 1) == 0) {
+                const int64_t q = ((int64_t)n * (a.Ho >> 1) + (h >> 1)) * (a.Wo >> 1) + (w >> 1);
+                rv4[i][ps] = *reinterpret_cast<const u32x4*>(a.bdr + q * a.N + my_col);
+              }
+            } else {
+              rv4[i][ps] = *reinterpret_cast<const u32x4*>(a.bdr + (int64_t)m * a.N + my_col);
+            }
+            bt[i][ps] = a.bmbits[((int64_t)m * a.N + my_col) >> 3];
+          }
+          if constexpr (BWD == 3) dv4[i][ps] = *reinterpret_cast<const u32x4*>(a.bxd + (int64_t)m * a.N + my_col);
+        }
+      }
+    }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = rq + L;  // this lane's row within the 16-row block after quad_t4
+#pragma unroll
+    for (int j = 0; j < JN; ++j) {
+      float w[4];
+      quad_t4(acc[i][j], L, w);
+      const int c8 = (j * 16 + (cl & ~3)) >> 2;  // 8-byte column group within the staged row
+      const int off = r * RB + ((c8 ^ ((r & 7) << 1)) & (RB / 8 - 1)) * 8;
+      const uint32_t lo = pack_bf16x2_rne(w[0], w[1]), hi = pack_bf16x2_rne(w[2], w[3]);
+      *reinterpret_cast<uint64_t*>(stg + off) = (uint64_t)lo | ((uint64_t)hi << 32);
+    }
+    // one wave's LDS ops complete in order: the reads below see the writes above
+#pragma unroll
+    for (int ps = 0; ps < PASSES; ++ps) {
+      const int c = ps * 64 + lane;
+      const int rr = c / CPR, c16 = c % CPR;
+      const int off = rr * RB + (((2 * c16) ^ ((rr & 7) << 1)) & (RB / 8 - 1)) * 8;
+      u32x4 v = *reinterpret_cast<const u32x4*>(stg + off);
+      const int m = mm[i][ps];
+      if (m >= 0) {
+        const int64_t go = (int64_t)m * a.ldc + n0 + wc * WNT + c16 * 8;
+        if constexpr (BWD != 0) {
+          float d[8], xv[8];
+          load8_bf16(reinterpret_cast<const uint16_t*>(&v), d);
+          load8_bf16(reinterpret_cast<const uint16_t*>(&exr[i][ps]), xv);
+          if constexpr (BWD >= 2) {
+            float rv[8];
+            load8_bf16(reinterpret_cast<const uint16_t*>(&rv4[i][ps]), rv);
+            const uint32_t bits = bt[i][ps];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) d[e] = ((bits >> e) & 1u) ? d[e] + rv[e] : 0.f;
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) d[e] = fmaf(xv[e], bsc[e], bsh[e]) > 0.f ? d[e] : 0.f;
+          }
+          uint32_t pk[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) pk[e] = pack_bf16x2_rne(d[2 * e], d[2 * e + 1]);
+          v = u32x4{pk[0], pk[1], pk[2], pk[3]};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float gq = bf16_to_f32(f32_to_bf16(d[e]));  // the stored g
+            ga[e] += gq;
+            gb[e] = fmaf(gq, xv[e] - bmu[e], gb[e]);
+          }
+          if constexpr (BWD == 3) {
+            float dv[8];
+            load8_bf16(reinterpret_cast<const uint16_t*>(&dv4[i][ps]), dv);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) gd[e] = fmaf(bf16_to_f32(f32_to_bf16(d[e])), dv[e] - bmd[e], gd[e]);
+          }
+        }
+        *reinterpret_cast<u32x4*>(y + go) = v;
+      }
+    }
+  }
+  if constexpr (BWD != 0) {
+    // lanes sharing this lane's channels: lane % CPR equal -> rotate-sum within the 16-lane row,
+    // then across rows
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if constexpr (CPR == 4) {
+        ga[e] += ror_row<4>(ga[e]);
+        gb[e] += ror_row<4>(gb[e]);
+      }
+      ga[e] += ror_row<8>(ga[e]);
+      gb[e] += ror_row<8>(gb[e]);
+      ga[e] += xor16(ga[e], lane);
+      gb[e] += xor16(gb[e], lane);
+      ga[e] += xor32(ga[e], lane);
+      gb[e] += xor32(gb[e], lane);
+      if constexpr (BWD == 3) {
+        if constexpr (CPR == 4) gd[e] += ror_row<4>(gd[e]);
+        gd[e] += ror_row<8>(gd[e]);
+        gd[e] += xor16(gd[e], lane);
+        gd[e] += xor32(gd[e], lane);
+      }
+    }
+    if (lane < CPR) {
+      float* pr = a.part + ((int64_t)tm * WM + wr) * 2 * a.N;
+      store8_f32(pr + my_col, ga);
+      store8_f32(pr + a.N + my_col, gb);
+      if constexpr (BWD == 3) {
+        float* pd = a.part_d + ((int64_t)tm * WM + wr) * 2 * a.N;
+        store8_f32(pd + my_col, ga);
+        store8_f32(pd + a.N + my_col, gd);
+      }
+    }
+  }
+}
+
 // BWD (bwd-data of a convolution whose input came out of a BatchNorm + ReLU): the epilogue also runs
 // that BN's backward reduction. 1: ReLU mask recomputed from the BN input x and the forward
 // scale/shift (bn1 / bn2 of a bottleneck); 2: the output plus the handed-over residual-branch
@@ -357,176 +563,160 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
     __builtin_amdgcn_sched_barrier(0);
   }
 
-  // ---- epilogue (per wave, no barrier: the staging slot is this wave's own): C layout of a
-  // 16x16 block col = lane & 15, row = 4 * (lane >> 4) + r
-  if (a.bias) {  // per-output-channel bias (the BN-backward fold's constant term)
-#pragma unroll
-    for (int j = 0; j < G::JN; ++j) {
-      const float bv = a.bias[n0 + wc * WNT + j * 16 + cl];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) acc[i][j] += f32x4{bv, bv, bv, bv};
-    }
-  }
+  convn_epilogue<BM, BN, WNT, STATS, BWD>(a, acc, kshift, tm, wr, wc, lane,
+                                          smem + a.nslot * SLOTB + (HALO ? halo_win_bytes(BM) : 0) + wid * G::STG, pix,
+                                          n0);
+}
+
+
+// ------------------------------------------------------------------ persistent HALO (layer1 3x3)
+// The ResNet layer1 3x3 convolution (C = 64 -> N = 64, stride 1, pad 1, 56 x 56) and its bwd-data
+// run at ~20 % of the MFMA rate on the gathered kernel above: every K-tile re-gathers 128 input
+// rows through L2 -> LDS (9 per output pixel) and the per-CU fill rate (~46 GB/s, TD busy 67 %,
+// profiles/convn_pmc_r4.md) bounds it; the plain HALO variant stages the window once per tile but
+// waits for it before computing (one channel block: nothing to overlap it with).
+// This kernel is persistent (one 256-thread workgroup per CU, a contiguous run of tiles each):
+//   * the whole weight tensor (64 x 576 bf16 = 72 KiB, nine 64x64 tap images) is loaded into LDS
+//     once per workgroup;
+//   * tile = 2 output rows of one image x 64 slots (Wo <= 62 valid); its input window (4 rows x 64
+//     slots x 64 channels = 32 KiB, zero outside the image by the out-of-range DMA) is double
+//     buffered: tile i+1's window is DMA'd while tile i's nine taps run, one barrier per tile;
+//   * 4 waves = 2 output rows x 2 x 32 channels, v_mfma_f32_16x16x32_bf16, A fragments read from the
+//     window at row offset (r * 64 + s) (the tap shift), B fragments from the resident weights;
+//   * the epilogue (statistics / bwd reductions / stores) is the shared one; the next window's DMA
+//     is in flight underneath it.
+constexpr int kHxWin = 4 * 64 * 128;          // window bytes (4 rows x 64 slots x 128 B)
+constexpr int kHxW = 9 * 64 * 128;            // resident weights (9 taps x 64 rows x 128 B)
+constexpr int kHxLds = kHxW + 2 * kHxWin + 4 * 2048 + 512;  // + 4 wave staging areas, + tap overrun
+
+template <bool STATS, int BWD>
+__global__ __launch_bounds__(256) void convh_kernel(ConvnArgs a, int ntiles) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* wlds = smem;
+  auto winb = [&](int b) { return smem + kHxW + b * kHxWin; };
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+  const int cl = lane & 15;
+  const int tpi = (a.Ho + 1) >> 1;  // tiles per image
+  // a contiguous run of tiles per workgroup: consecutive tiles share two window rows (L2 hits)
+  const int t_begin = (int)(((int64_t)blockIdx.x * ntiles) / gridDim.x);
+  const int t_end = (int)(((int64_t)(blockIdx.x + 1) * ntiles) / gridDim.x);
+  if (t_begin >= t_end) return;
+  float kshift[2] = {0.f, 0.f};
   if constexpr (STATS) {
 #pragma unroll
-    for (int j = 0; j < G::JN; ++j) {
-      float s1 = 0.f, s2 = 0.f;
+    for (int j = 0; j < 2; ++j) kshift[j] = a.shift[wc * 32 + j * 16 + cl];
+  }
+  const rsrc_t xr = make_rsrc(a.x, a.xbytes);
+  const rsrc_t wrs = make_rsrc(a.w, a.wbytes);
+  // weights: tap t rows n = 0..63 of k = t*64 .. t*64+63, K-major swizzled images (72 pieces of 1 KiB)
+  for (int pc = wid; pc < 72; pc += 4) {
+    const int t = pc >> 3, row = (pc & 7) * 8 + (lane >> 3);
+    const int kc = (lane & 7) ^ ((row >> 1) & 7);
+    const uint32_t off = ((uint32_t)row * (uint32_t)a.K + (uint32_t)(t * 64 + kc * 8)) * 2u;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)(wlds + pc * 1024), 16, off,
+                                             0, 0, 0);
+  }
+  // the input window of tile `tile` into buffer b: rows ho0-1 .. ho0+2, slots wi = -1 .. 62
+  auto stage = [&](int tile, int b) {
+    const int n = tile / tpi, ho0 = (tile - n * tpi) * 2;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 8; ++i) {
+      const int pc = i * 4 + wid;
+      const int row = pc * 8 + (lane >> 3);
+      const int jj = row >> 6, ws = row & 63;
+      const int hi = ho0 - 1 + jj, wi = ws - 1;
+      const int kc = (lane & 7) ^ ((row >> 1) & 7);
+      const bool ok = (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+      const uint32_t off = ok ? ((((uint32_t)((n * a.H + hi) * a.W + wi)) << 6) + (uint32_t)(kc * 8)) * 2u : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(winb(b) + pc * 1024), 16,
+                                               off, 0, 0, 0);
+    }
+  };
+  stage(t_begin, 0);
+  wait_vm<0>();
+  __syncthreads();
+  uint8_t* stg = smem + kHxW + 2 * kHxWin + wid * 2048;
+  for (int tile = t_begin, it = 0; tile < t_end; ++tile, ++it) {
+    const int b = it & 1;
+    if (tile + 1 < t_end) stage(tile + 1, b ^ 1);  // lands under this tile's taps + epilogue
+    const uint8_t* win = winb(b);
+    f32x4 acc[4][2];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float d = bf16_to_f32(f32_to_bf16(acc[i][j][r])) - kshift[j];
-          const bool ok = pix(wr * 64 + i * 16 + rq + r) >= 0;
-          s1 += ok ? d : 0.f;
-          s2 = ok ? fmaf(d, d, s2) : s2;
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int tr = tap / 3, ts = tap - tr * 3;
+      const uint8_t* Bs = wlds + tap * 8192;
+      bf16x8 af[2][4], bf[2][2];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bf[ks][j] = frag(Bs, wc * 2 + j, ks, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = (wr + tr) * 64 + i * 16 + (lane & 15) + ts;
+          af[ks][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(win + kmaj_off(row, ks * 4 + (lane >> 4))));
         }
-      s1 += xor16(s1, lane);
-      s2 += xor16(s2, lane);
-      s1 += xor32(s1, lane);
-      s2 += xor32(s2, lane);
-      if (lane < 16) {
-        float* pr = a.part + ((int64_t)tm * G::WM + wr) * 2 * a.N;
-        const int col = n0 + wc * WNT + j * 16 + cl;
-        pr[col] = s1;
-        pr[a.N + col] = s2;
       }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][i], bf[ks][j], acc[i][j], 0, 0, 0);
     }
+    const int n = tile / tpi, ho0 = (tile - n * tpi) * 2;
+    auto pix = [&](int p) -> int {
+      const int j = p >> 6, wo = p & 63;
+      return (wo < a.Wo && ho0 + j < a.Ho) ? (n * a.Ho + ho0 + j) * a.Wo + wo : -1;
+    };
+    convn_epilogue<128, 64, 32, STATS, BWD>(a, acc, kshift, tile, wr, wc, lane, stg, pix, 0);
+    wait_vm<0>();     // this wave's DMA of the next window (and the epilogue's loads) landed
+    __syncthreads();  // every wave's: the next window is complete and this one no longer read
   }
-  uint8_t* stg = smem + a.nslot * SLOTB + (HALO ? halo_win_bytes(BM) : 0) + wid * G::STG;
-  const int L = cl & 3;
-  constexpr int RB = WNT * 2;       // staged row bytes (one 16-row block)
-  constexpr int CPR = RB / 16;      // 16-byte chunks per staged row
-  constexpr int PASSES = 16 * CPR / 64;
-  uint16_t* y = reinterpret_cast<uint16_t*>(a.y);
-  // BWD: this lane's 8 output channels are fixed (64 % CPR == 0): per-channel constants once
-  const int my_c16 = lane % CPR;
-  const int my_col = n0 + wc * WNT + my_c16 * 8;
-  float bmu[8], bsc[8], bsh[8], ga[8], gb[8], bmd[8], gd[8];
-  float inv_hw = 0.f, inv_wo = 0.f;
-  const bool fast_div = a.M < (1 << 24);
-  if constexpr (BWD == 5) {
-    inv_hw = 1.f / (float)(a.Ho * a.Wo);
-    inv_wo = 1.f / (float)a.Wo;
+}
+
+static bool convh_ok(const ConvnArgs& a) {
+  return a.N == 64 && a.logC == 6 && a.R == 3 && a.S == 3 && a.stride == 1 && a.pad == 1 && a.H == a.Ho &&
+         a.W == a.Wo && a.Wo + 2 <= 64 && !a.x2 && a.K == 576 && a.ldc == 64;
+}
+
+static int convh_grid(int ntiles) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || cus <= 0)
+      cus = 256;
   }
-  if constexpr (BWD == 3) {
-    load8_f32(a.bmean_d + my_col, bmd);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) gd[e] = 0.f;
+  return ntiles < cus ? ntiles : cus;
+}
+
+template <bool STATS, int BWD>
+static hipError_t convh_launch_t(const ConvnArgs& a, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e =
+        hipFuncSetAttribute((const void*)convh_kernel<STATS, BWD>, hipFuncAttributeMaxDynamicSharedMemorySize, kHxLds);
+    if (e != hipSuccess) return e;
+    attr = true;
   }
-  if constexpr (BWD != 0) {
-    load8_f32(a.bmean + my_col, bmu);
-    if constexpr (BWD == 1) {
-      load8_f32(a.bss + my_col, bsc);
-      load8_f32(a.bss + a.N + my_col, bsh);
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) ga[e] = gb[e] = 0.f;
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = rq + L;  // this lane's row within the 16-row block after quad_t4
-#pragma unroll
-    for (int j = 0; j < G::JN; ++j) {
-      float w[4];
-      quad_t4(acc[i][j], L, w);
-      const int c8 = (j * 16 + (cl & ~3)) >> 2;  // 8-byte column group within the staged row
-      const int off = r * RB + ((c8 ^ ((r & 7) << 1)) & (RB / 8 - 1)) * 8;
-      const uint32_t lo = pack_bf16x2_rne(w[0], w[1]), hi = pack_bf16x2_rne(w[2], w[3]);
-      *reinterpret_cast<uint64_t*>(stg + off) = (uint64_t)lo | ((uint64_t)hi << 32);
-    }
-    // one wave's LDS ops complete in order: the reads below see the writes above
-#pragma unroll
-    for (int ps = 0; ps < PASSES; ++ps) {
-      const int c = ps * 64 + lane;
-      const int rr = c / CPR, c16 = c % CPR;
-      const int off = rr * RB + (((2 * c16) ^ ((rr & 7) << 1)) & (RB / 8 - 1)) * 8;
-      u32x4 v = *reinterpret_cast<const u32x4*>(stg + off);
-      const int m = pix(wr * 64 + i * 16 + rr);
-      if (m >= 0) {
-        const int64_t go = (int64_t)m * a.ldc + n0 + wc * WNT + c16 * 8;
-        if constexpr (BWD != 0) {
-          float d[8], xv[8];
-          load8_bf16(reinterpret_cast<const uint16_t*>(&v), d);
-          load8_bf16(a.bx + (int64_t)m * a.N + my_col, xv);
-          if constexpr (BWD >= 2) {
-            float rv[8];
-            if constexpr (BWD == 5) {
-              // residual-branch gradient of a stride-2 1x1 (downsample) convolution, on the quarter
-              // grid: non-zero only at even (h, w) of this (Ho x Wo) output grid
-              const int hw = a.Ho * a.Wo;
-              const int n = fast_div ? fdiv(m, hw, inv_hw) : m / hw, rem = m - n * hw;
-              const int h = fast_div ? fdiv(rem, a.Wo, inv_wo) : rem / a.Wo, w = rem - h * a.Wo;
-              if (((h | w) & 1) == 0) {
-                const int64_t q = ((int64_t)n * (a.Ho >> 1) + (h >> 1)) * (a.Wo >> 1) + (w >> 1);
-                load8_bf16(a.bdr + q * a.N + my_col, rv);
-              } else {
-#pragma unroll
-                for (int e = 0; e < 8; ++e) rv[e] = 0.f;
-              }
-            } else {
-              load8_bf16(a.bdr + (int64_t)m * a.N + my_col, rv);
-            }
-            const uint32_t bits = a.bmbits[((int64_t)m * a.N + my_col) >> 3];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) d[e] = ((bits >> e) & 1u) ? d[e] + rv[e] : 0.f;
-          } else {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) d[e] = fmaf(xv[e], bsc[e], bsh[e]) > 0.f ? d[e] : 0.f;
-          }
-          uint32_t pk[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) pk[e] = pack_bf16x2_rne(d[2 * e], d[2 * e + 1]);
-          v = u32x4{pk[0], pk[1], pk[2], pk[3]};
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float gq = bf16_to_f32(f32_to_bf16(d[e]));  // the stored g
-            ga[e] += gq;
-            gb[e] = fmaf(gq, xv[e] - bmu[e], gb[e]);
-          }
-          if constexpr (BWD == 3) {
-            float dv[8];
-            load8_bf16(a.bxd + (int64_t)m * a.N + my_col, dv);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) gd[e] = fmaf(bf16_to_f32(f32_to_bf16(d[e])), dv[e] - bmd[e], gd[e]);
-          }
-        }
-        *reinterpret_cast<u32x4*>(y + go) = v;
-      }
-    }
-  }
-  if constexpr (BWD != 0) {
-    // lanes sharing this lane's channels: lane % CPR equal -> rotate-sum within the 16-lane row,
-    // then across rows
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      if constexpr (CPR == 4) {
-        ga[e] += ror_row<4>(ga[e]);
-        gb[e] += ror_row<4>(gb[e]);
-      }
-      ga[e] += ror_row<8>(ga[e]);
-      gb[e] += ror_row<8>(gb[e]);
-      ga[e] += xor16(ga[e], lane);
-      gb[e] += xor16(gb[e], lane);
-      ga[e] += xor32(ga[e], lane);
-      gb[e] += xor32(gb[e], lane);
-      if constexpr (BWD == 3) {
-        if constexpr (CPR == 4) gd[e] += ror_row<4>(gd[e]);
-        gd[e] += ror_row<8>(gd[e]);
-        gd[e] += xor16(gd[e], lane);
-        gd[e] += xor32(gd[e], lane);
-      }
-    }
-    if (lane < CPR) {
-      float* pr = a.part + ((int64_t)tm * G::WM + wr) * 2 * a.N;
-      store8_f32(pr + my_col, ga);
-      store8_f32(pr + a.N + my_col, gb);
-      if constexpr (BWD == 3) {
-        float* pd = a.part_d + ((int64_t)tm * G::WM + wr) * 2 * a.N;
-        store8_f32(pd + my_col, ga);
-        store8_f32(pd + a.N + my_col, gd);
-      }
-    }
-  }
+  const int ntiles = (a.M / (a.Ho * a.Wo)) * ((a.Ho + 1) / 2);
+  hipLaunchKernelGGL((convh_kernel<STATS, BWD>), dim3(convh_grid(ntiles)), dim3(256), kHxLds, st, a, ntiles);
+  return hipGetLastError();
+}
+
+static hipError_t convh_launch(const ConvnArgs& a, hipStream_t st) {
+  if (a.bwd == 1) return convh_launch_t<false, 1>(a, st);
+  if (a.bwd == 2) return convh_launch_t<false, 2>(a, st);
+  if (a.bwd == 3) return convh_launch_t<false, 3>(a, st);
+  if (a.bwd == 5) return convh_launch_t<false, 5>(a, st);
+  return a.part ? convh_launch_t<true, 0>(a, st) : convh_launch_t<false, 0>(a, st);
 }
 
 // ------------------------------------------------------------------ host side
@@ -581,7 +771,16 @@ static int plain_count(int bn) { return bn == 256 ? 2 : 4; }
 static constexpr int kHaloBm64[] = {128, 256, 128};
 static constexpr int kHaloBm128[] = {128, 256};
 static int halo_count(int bn) { return bn == 256 ? 1 : bn == 128 ? 2 : 3; }
-static int convn_variant_count(int bn) { return plain_count(bn) + halo_count(bn); }
+// + the persistent HALO variant (convh_kernel) for the 64-wide outputs
+static int persist_count(int bn) { return bn == 64 ? 1 : 0; }
+static int convn_variant_count(int bn) { return plain_count(bn) + halo_count(bn) + persist_count(bn); }
+static bool is_persist(int bn, int v) { return v >= plain_count(bn) + halo_count(bn); }
+
+int convn_variant_kind(int N, int v) {
+  const int bn = convn_tile_n(N);
+  if (!bn || v < 0 || v >= convn_variant_count(bn)) return -1;
+  return v < plain_count(bn) ? 0 : is_persist(bn, v) ? 2 : 1;
+}
 
 int convn_variants(int N) {
   const int bn = convn_tile_n(N);
@@ -596,6 +795,7 @@ static int default_variant(const ConvnArgs& a, int bn) {
 
 // BM of each variant (must match the dispatch in launch_convn)
 static int variant_bm(int bn, int v) {
+  if (is_persist(bn, v)) return 128;
   const int h = v - plain_count(bn);
   if (h >= 0) return bn == 64 ? kHaloBm64[h] : bn == 128 ? kHaloBm128[h] : 128;
   if (bn == 64) return (v == 2 || v == 3) ? 256 : 128;
@@ -613,6 +813,8 @@ bool convn_variant_ok(int N, int v, int R, int S, int stride, int pad, int Wo, b
   const int bn = convn_tile_n(N);
   if (!bn || v < 0 || v >= convn_variant_count(bn)) return false;
   if (v < plain_count(bn)) return true;
+  if (is_persist(bn, v))  // (C = 64 and H = Ho are checked at launch: the predicate has no C)
+    return !has_x2 && N == 64 && R == 3 && S == 3 && stride == 1 && pad == 1 && Wo + 2 <= 64;
   const int sw = halo_sw(Wo, R);
   return !has_x2 && R == S && R > 1 && R <= 3 && stride == 1 && 2 * pad == R - 1 && sw > 0 && variant_bm(bn, v) >= sw;
 }
@@ -623,6 +825,10 @@ int convn_part_rows_geo(int M, int N, int variant, int Ho, int Wo, int R) {
   const int bn = convn_tile_n(N);
   if (!bn) return 0;
   const int bm = variant_bm(bn, variant);
+  if (is_persist(bn, variant)) {
+    if (Ho <= 0 || Wo <= 0) return 0;
+    return 2 * ((M / (Ho * Wo)) * ((Ho + 1) / 2));
+  }
   if (variant >= plain_count(bn)) {
     const int sw = halo_sw(Wo, R);
     if (!sw || Ho <= 0 || Wo <= 0) return 0;
@@ -655,6 +861,10 @@ hipError_t launch_convn(const ConvnArgs& a_in, hipStream_t st) {
                                                 (a.bwd != 5 || (a.Ho % 2 == 0 && a.Wo % 2 == 0))))));
   if (!ok) return hipErrorNotSupported;
   const int v = a.variant >= 0 ? a.variant : default_variant(a, bn);
+  if (is_persist(bn, v)) {
+    if (!convh_ok(a)) return hipErrorNotSupported;
+    return convh_launch(a, st);
+  }
   if (v >= plain_count(bn)) {  // HALO
     if (!convn_variant_ok(a.N, v, a.R, a.S, a.stride, a.pad, a.Wo, two) || a.Ho != a.H || a.Wo != a.W)
       return hipErrorNotSupported;

@@ -91,6 +91,7 @@ std::vector<at::Tensor> bn_bwd_pre(const at::Tensor& g, const at::Tensor& x, c10
                                    c10::optional<at::Tensor> dbeta_out, c10::optional<at::Tensor> dq,
                                    c10::optional<at::Tensor> dqmx);
 int64_t convn_variants_(int64_t N);
+int64_t convn_variant_kind_(int64_t N, int64_t v);
 int64_t conv_fwd_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride,
                   int64_t pad, c10::optional<at::Tensor> part, c10::optional<at::Tensor> shift);
 bool conv_wgrad_(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64_t R, int64_t S, int64_t stride,

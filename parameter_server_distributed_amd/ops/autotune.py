@@ -6,6 +6,15 @@ eager call of a shape times every candidate (one warm call + 3 timed), caches th
 uses it from then on. Inside a hipGraph capture nothing is timed: an undecided shape takes the
 ``default`` candidate (the Trainer always runs eager warmup steps before it captures).
 
+Across ranks (torch.distributed initialised, world > 1) every rank runs the same choice: the first
+rank to reach a key claims it through the rendezvous store (an atomic ``add``), times and validates
+the candidates and publishes the winner; every other rank waits for that decision instead of
+timing on its own. Independent per-rank timing picked different kernels on different ranks (3
+timed reps are noisy), so the ranks' step times and numerics differed and the SSP bound tied
+everyone to the slowest rank's choices. ``PSD_AUTOTUNE_FILE``: a JSON file of decisions
+(``save_decisions``) loaded at import, which pins every listed key on every rank with no timing.
+``source()`` reports which of these decided.
+
 Like MIOpen's Find, a candidate must also be *correct* to be chosen: the outputs of its warm call
 and of its last timed call are compared with the default candidate's (finite wherever the default
 is finite, max |diff| <= 5 % of max |ref|). A library solution that returns garbage is dropped.
@@ -16,11 +25,17 @@ finite loss on broken weights (tools/rank_check.py, tools/gemm_nan_probe.py; REA
 """
 from __future__ import annotations
 
+import ast
+import datetime
+import json
 import os
+import time
 
 import torch
 
 _DECISIONS: dict[tuple, str] = {}
+_SOURCE = {"local": 0, "claimed": 0, "peer": 0, "file": 0}
+_FILE_KEYS: set = set()
 
 
 def enabled(var: str) -> bool:
@@ -28,6 +43,13 @@ def enabled(var: str) -> bool:
 
 
 _REJECTED: dict[tuple, list] = {}
+
+
+class Declined(RuntimeError):
+    """Raised by a candidate whose kernel does not take this shape. While a key is being timed
+    the candidate is simply left out (recorded in ``rejected()`` as "declined:<name>"); a candidate
+    that was chosen and then declines is an error -- never a silent switch to another kernel
+    behind the recorded decision."""
 _TIMES: dict[tuple, dict] = {}
 
 
@@ -40,6 +62,13 @@ def _snap(out, probe):
 def _time_ms(fn, reps: int = 3, probe=None):
     """(ms per call, [output of the warm call, output of the last timed call])."""
     outs = [_snap(fn(), probe)]  # warm (library heuristics / kernel load)
+    if not torch.cuda.is_available():  # host candidates (CPU tests of the selection protocol)
+        t0 = time.perf_counter()
+        last = None
+        for _ in range(reps):
+            last = fn()
+        outs.append(_snap(last, probe))
+        return (time.perf_counter() - t0) * 1e3 / reps, outs
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
     last = None
@@ -71,6 +100,26 @@ def rejected() -> dict:
     return dict(_REJECTED)
 
 
+def _store():
+    """The rendezvous store when this process is one rank of several, else None."""
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() <= 1:
+        return None
+    if os.environ.get("PSD_AUTOTUNE_PER_RANK") == "1":  # A/B: the old independent per-rank timing
+        return None
+    return dist.distributed_c10d._get_default_store()
+
+
+def _peer_decision(st, skey: str, candidates: dict) -> str | None:
+    """Another rank claimed ``skey``: wait for its published choice."""
+    st.wait([f"psd/autotune/d/{skey}"], datetime.timedelta(seconds=float(os.environ.get("PSD_AUTOTUNE_WAIT_S", "900"))))
+    name = st.get(f"psd/autotune/d/{skey}").decode()
+    if name not in candidates:
+        raise RuntimeError(f"autotune: rank decision {name!r} for {skey} is not a candidate here {sorted(candidates)}")
+    return name
+
+
 def choose(key: tuple, candidates: dict, default: str, probe=None) -> str:
     """Name of the fastest *correct* candidate for ``key`` (timed and validated once, cached).
     ``probe``: returns the output tensor of a candidate that writes into a preallocated buffer
@@ -84,9 +133,35 @@ def choose(key: tuple, candidates: dict, default: str, probe=None) -> str:
         if forced and forced in candidates:
             _DECISIONS[key] = forced
             return forced
-    if torch.cuda.is_current_stream_capturing():
+    if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
         return default
-    runs = {name: _time_ms(fn, probe=probe) for name, fn in candidates.items()}
+    st = _store()
+    skey = repr(key)
+    if st is not None and int(st.add(f"psd/autotune/c/{skey}", 1)) > 1:
+        best = _peer_decision(st, skey, candidates)
+        _DECISIONS[key] = best
+        _SOURCE["peer"] += 1
+        return best
+    best = _time_and_pick(key, candidates, default, probe)
+    if st is not None:
+        st.set(f"psd/autotune/d/{skey}", best)
+        _SOURCE["claimed"] += 1
+    else:
+        _SOURCE["local"] += 1
+    return best
+
+
+def _time_and_pick(key: tuple, candidates: dict, default: str, probe) -> str:
+    runs, declined = {}, []
+    for name, fn in candidates.items():
+        try:
+            runs[name] = _time_ms(fn, probe=probe)
+        except Declined:
+            declined.append(name)
+    if declined:
+        _REJECTED[key] = [f"declined:{n}" for n in declined]
+    if not runs:
+        raise Declined(f"autotune {key}: every candidate declined ({declined})")
     ref_name = default if default in runs else next(iter(runs))
     ref = runs[ref_name][1]
     if any(o is not None and not bool(torch.isfinite(o).all()) for o in ref):
@@ -97,13 +172,41 @@ def choose(key: tuple, candidates: dict, default: str, probe=None) -> str:
     ok = {n: r[0] for n, r in runs.items() if n == ref_name or _agrees(r[1], ref)}
     bad = [n for n in runs if n not in ok]
     if bad:
-        _REJECTED[key] = bad
+        _REJECTED[key] = _REJECTED.get(key, []) + bad
     best = min(ok, key=ok.get)
     _DECISIONS[key] = best
     _TIMES[key] = {n: round(r[0], 4) for n, r in runs.items()}
     if os.environ.get("PSD_AUTOTUNE_LOG"):
         print(f"[autotune] {key}: {_TIMES[key]} -> {best}" + (f" (rejected {bad})" if bad else ""), flush=True)
     return best
+
+
+def source() -> dict:
+    """How this rank's decisions were made: timed here with no peers ("local"), timed here for
+    every rank ("claimed"), taken from the rank that timed them ("peer"), or loaded ("file")."""
+    return dict(_SOURCE)
+
+
+def save_decisions(path: str) -> None:
+    """Write this process's decisions as JSON (``PSD_AUTOTUNE_FILE`` loads them)."""
+    with open(path, "w") as f:
+        json.dump({repr(k): v for k, v in sorted(_DECISIONS.items(), key=lambda kv: repr(kv[0]))}, f, indent=1)
+
+
+def load_decisions(path: str) -> int:
+    """Pin the decisions of a ``save_decisions`` file; returns how many were loaded."""
+    with open(path) as f:
+        raw = json.load(f)
+    for k, v in raw.items():
+        key = ast.literal_eval(k)
+        _DECISIONS[key] = v
+        _FILE_KEYS.add(key)
+    _SOURCE["file"] = len(_FILE_KEYS)
+    return len(raw)
+
+
+if os.environ.get("PSD_AUTOTUNE_FILE"):
+    load_decisions(os.environ["PSD_AUTOTUNE_FILE"])
 
 
 def times() -> dict:

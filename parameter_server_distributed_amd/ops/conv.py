@@ -207,17 +207,24 @@ def _convn_variants(x, w2, k: int, stride: int, pad: int, bn=None) -> dict:
             return y
         return fn
 
-    return {f"psdn{v}": make(v) for v in range(C.convn_variants(cout)) if _variant_ok(cout, v, k, stride, pad, wo)}
+    return {f"psdn{v}": make(v) for v in range(C.convn_variants(cout))
+            if _variant_ok(cout, v, k, stride, pad, wo, x.shape[1], h)}
 
 
-def _variant_ok(cout: int, v: int, k: int, stride: int, pad: int, wo: int) -> bool:
-    """Variant v of the narrow kernel takes this shape (HALO variants -- the ones a 1x1 shape
-    declines -- only with PSD_CONVN_HALO=1: on the ResNet-50 shapes they measured no faster than the
-    gathered variants, profiles/convn_halo_r3.md, so by default they are not autotuned)."""
+def _variant_ok(cout: int, v: int, k: int, stride: int, pad: int, wo: int, cin: int | None = None,
+                h: int | None = None) -> bool:
+    """Variant v of the narrow kernel takes this shape. The plain HALO variants (kind 1) only with
+    PSD_CONVN_HALO=1: on the ResNet-50 shapes they measured no faster than the gathered variants,
+    profiles/convn_halo_r3.md, so by default they are not autotuned. The persistent HALO variant
+    (kind 2, C = N = 64 3x3 stride 1, H = Ho) is a candidate whenever its contract holds
+    (PSD_CONVN_PERSIST=0: off, A/B)."""
     C = _native()
     if not C.convn_variant_ok(cout, v, k, k, stride, pad, wo):
         return False
-    return C.convn_variant_ok(cout, v, 1, 1, 1, 0, 1) or os.environ.get("PSD_CONVN_HALO", "0") == "1"
+    kind = C.convn_variant_kind(cout, v)
+    if kind == 2:
+        return _at.enabled("PSD_CONVN_PERSIST") and cin == 64 and (h is None or h == wo)
+    return kind == 0 or os.environ.get("PSD_CONVN_HALO", "0") == "1"
 
 
 def _part_rows(M: int, N: int, v: int, ho: int, wo: int, k: int) -> int:
@@ -227,13 +234,22 @@ def _part_rows(M: int, N: int, v: int, ho: int, wo: int, k: int) -> int:
     return max(C.convn_stats_rows(M), C.convn_part_rows(M, N, v, ho, wo, k))
 
 
-def _bn_bwd_fusion(mod, x: torch.Tensor):
-    """When ``mod``'s input ``x`` is exactly the output of a FusedBatchNorm2d + ReLU (wired by the
-    model as ``_psd_bn_in``) whose only autograd consumer is ``mod``, the bwd-data epilogue can run
+def _fwd_records(ctx, mod) -> None:
+    """Capture at forward the model wiring the backward consults (``_psd_bn_in``: the BN whose
+    output this convolution consumes; ``_psd_strided_to``: where a downsample convolution hands its
+    quarter-grid input gradient). The model rewrites these attributes on every forward, so reading
+    them from the module at backward time could pick up a later forward's wiring."""
+    ctx.bn_in = getattr(mod, "_psd_bn_in", None) if mod is not None else None
+    ctx.strided_to = getattr(mod, "_psd_strided_to", None) if mod is not None else None
+
+
+def _bn_bwd_fusion(bn, x: torch.Tensor):
+    """When the convolution's input ``x`` is exactly the output of a FusedBatchNorm2d + ReLU ``bn``
+    (wired by the model as ``_psd_bn_in``, recorded at forward) whose only autograd consumer is the
+    convolution, the bwd-data epilogue can run
     that BN's backward reduction (kernels/convn.hip bwd modes): mode 1 (no residual: ReLU mask from
     its x and scale/shift) or mode 2 (a residual BN: bit-mask, plus the residual-branch gradient
     handed over by the next block). Returns the arguments, or None."""
-    bn = getattr(mod, "_psd_bn_in", None) if mod is not None else None
     st = getattr(bn, "_psd_fwd", None) if bn is not None else None
     if st is None or not _at.enabled("PSD_CONVN_BWD"):
         return None
@@ -279,7 +295,8 @@ def _convn_bwd_variants(dy, w2, k: int, pad: int, fu: dict, dr) -> dict:
             return g
         return fn
 
-    return {f"psdnb{v}": make(v) for v in range(C.convn_variants(cout)) if _variant_ok(cout, v, k, 1, pad, w)}
+    return {f"psdnb{v}": make(v) for v in range(C.convn_variants(cout))
+            if _variant_ok(cout, v, k, 1, pad, w, dy.shape[1], h)}
 
 
 def _dgrad_route(key: tuple, cands: dict, default: str, fu, dy_like) -> torch.Tensor:
@@ -353,8 +370,8 @@ def _route(key: tuple, cands: dict, default: str, bn=None) -> str:
 def _convw_cands(dy, x, k: int, stride: int, pad: int) -> dict:
     """{"psdw<v>": fn(into=None)} over the narrow weight-gradient kernel's tile variants
     (kernels/convw.hip); fn writes dW in OHWI order into ``into`` (a contiguous [Cout, k*k*Cin] view,
-    e.g. the PS gradient sink) or a fresh tensor and returns the [Cout, Cin, k, k] channels_last view,
-    or None when the kernel declines."""
+    e.g. the PS gradient sink) or a fresh tensor and returns the [Cout, Cin, k, k] channels_last view;
+    raises autotune.Declined when the kernel does not take the shape."""
     if not _at.enabled("PSD_CONVW"):
         return {}
     C = _native()
@@ -367,7 +384,7 @@ def _convw_cands(dy, x, k: int, stride: int, pad: int) -> dict:
         def fn(into=None):
             o = into if into is not None else torch.empty(cout, kk, device=dy.device, dtype=dy.dtype)
             if not C.convw_(dy, x, o, k, k, stride, pad, variant=v):
-                return None
+                raise _at.Declined(f"convw_ variant {v}")
             return o.view(cout, k, k, cin).permute(0, 3, 1, 2)
         return fn
 
@@ -448,7 +465,7 @@ def _fold_backward(ctx, fold, x, weight, need_x: bool, need_w: bool):
     if need_x and foldable:
         w2, bvec = C.bnfold_dgrad_weights(weight, coef)
         wt = weight.reshape(cout, cin).t().contiguous()
-        fu = _bn_bwd_fusion(ctx.mod, x)
+        fu = _bn_bwd_fusion(ctx.bn_in, x)
         if fu is not None:
             fu["dr"] = fu["bn"]._psd_pending_dr.pop() if fu["mode"] >= 2 else None
 
@@ -540,6 +557,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         module, whose ``_psd_grad_sink`` (installed by the PS data plane) receives dW directly."""
         fp8 = f8 is not None
         ctx.mod = mod
+        _fwd_records(ctx, mod)
         n, cin, h, w = x.shape
         cout = weight.shape[0]
         w2 = weight.reshape(cout, cin)
@@ -584,8 +602,8 @@ class _Conv1x1Fn(torch.autograd.Function):
             out = torch.empty(n * h * w, cout, device=x.device, dtype=x.dtype)
             part = _stats_part(bn, n * h * w, cout, x.device)
             rows = _native().gemm_(x2, w2, True, True, out, part=part, shift=bn.running_mean)
-            if rows == 0:  # too few tiles for the 8-phase kernel: the plain GEMM, the BN reduces
-                _native().gemm_(x2, w2, True, True, out)
+            if rows == 0:  # too few tiles for the statistics epilogue: not a candidate for this shape
+                raise _at.Declined("gemm_ statistics epilogue")
             y = _from_2d(out, n, h, w)
             _hand_stats(bn, y, part, rows)
             return y
@@ -662,7 +680,7 @@ class _Conv1x1Fn(torch.autograd.Function):
             if _psdn_ok(cout, cin):  # dX = dY . W as a 1x1 convolution of dY with W^T [cin, cout]
                 wt = w2.t().contiguous()
                 cands.update(_convn_variants(dy, wt, 1, 1, 0))
-                fu = _bn_bwd_fusion(ctx.mod, x)
+                fu = _bn_bwd_fusion(ctx.bn_in, x)
                 if fu is not None:
                     fu["dr"] = fu["bn"]._psd_pending_dr.pop() if fu["mode"] >= 2 else None
                     cands.update(_convn_bwd_variants(dy, wt, 1, 0, fu, fu["dr"]))
@@ -833,6 +851,7 @@ class _ConvFn(torch.autograd.Function):
         _Conv1x1Fn (dW straight into the PS gradient buffer)."""
         fp8 = f8 is not None
         ctx.mod = mod
+        _fwd_records(ctx, mod)
         cout, cin, k, _ = weight.shape
         n, _, h, w = x.shape
         ctx.stride, ctx.pad, ctx.fp8, ctx.f8 = stride, pad, fp8, f8
@@ -845,8 +864,9 @@ class _ConvFn(torch.autograd.Function):
             w2 = weight.permute(0, 2, 3, 1).reshape(cout, k * k * cin)
             y = _igemm_fp8(x, w2 if w2.is_contiguous() else w2.contiguous(), k, stride, pad, scaler=f8[0],
                            pre=_take_q8(mod, x), mod=mod, bn=_bn_consumer(mod))
-            if y is not None:
-                return y
+            if y is None:  # the guard above is the kernel's contract: a decline is a bug, not a bf16 run
+                raise RuntimeError(f"conv_fwd_fp8_ declined {tuple(x.shape)} x {tuple(weight.shape)}")
+            return y
 
         if not _igemm_ok(cin, cout) and not _psdn_ok(cin, cout):
             return miopen()
@@ -856,13 +876,17 @@ class _ConvFn(torch.autograd.Function):
 
         def igemm():
             y = _igemm(x, w2, k, stride, pad)
-            return miopen() if y is None else y
+            if y is None:
+                raise _at.Declined("conv_fwd_")
+            return y
 
         bn = _bn_consumer(mod)
 
         def igemm_stats():  # the implicit GEMM with the consumer BN's statistics in its epilogue
             y = _igemm(x, w2, k, stride, pad, bn)
-            return miopen() if y is None else y
+            if y is None:
+                raise _at.Declined("conv_fwd_ statistics epilogue")
+            return y
 
         cands = {"miopen": miopen}
         if _igemm_ok(cin, cout):
@@ -885,7 +909,7 @@ class _ConvFn(torch.autograd.Function):
         conv_bwd = torch.ops.aten.convolution_backward
         args = (None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1)
         dx = dw = None
-        to = getattr(ctx.mod, "_psd_strided_to", None) if ctx.mod is not None else None
+        to = ctx.strided_to
         if (ctx.needs_input_grad[0] and to is not None and k == 1 and stride == 2 and pad == 0 and h % 2 == 0
                 and w % 2 == 0 and _at.enabled("PSD_CONVN_BWD5") and not ctx.fp8):
             # downsample conv whose input gradient goes to the producing BN (the block's _Fork): dY . W
@@ -903,14 +927,16 @@ class _ConvFn(torch.autograd.Function):
                 got = _take_dq8(ctx.mod, dy) if _mx_on() else None
                 dx = _igemm_fp8(dy, wf, k, 1, pad, e5m2=True, scaler=ctx.f8[1], pre=got)
                 if dx is None:
-                    dx = miopen()
+                    raise RuntimeError(f"conv_fwd_fp8_ (bwd-data) declined {tuple(dy.shape)} x {tuple(weight.shape)}")
             elif stride == 1 and (_igemm_ok(cout, cin) or _psdn_ok(cout, cin)) and 2 * pad == k - 1:
                 # dX = conv(dY, W'), W'[ci, r, s, co] = W[co, ci, k-1-r, k-1-s]: same kernel, same padding
                 wf = weight.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, k * k * cout).contiguous()
 
                 def igemm():
                     y = _igemm(dy, wf, k, 1, pad)
-                    return miopen() if y is None else y
+                    if y is None:
+                        raise _at.Declined("conv_fwd_ (bwd-data)")
+                    return y
 
                 cands = {"miopen": miopen}
                 if _igemm_ok(cout, cin):
@@ -918,7 +944,7 @@ class _ConvFn(torch.autograd.Function):
                 fu = None
                 if _psdn_ok(cout, cin):
                     cands.update(_convn_variants(dy, wf, k, 1, pad))
-                    fu = _bn_bwd_fusion(ctx.mod, x)
+                    fu = _bn_bwd_fusion(ctx.bn_in, x)
                     if fu is not None:
                         fu["dr"] = fu["bn"]._psd_pending_dr.pop() if fu["mode"] >= 2 else None
                         cands.update(_convn_bwd_variants(dy, wf, k, pad, fu, fu["dr"]))
@@ -940,7 +966,9 @@ class _ConvFn(torch.autograd.Function):
 
             def igemm_c():
                 y = igemm_w()
-                return miopen_w() if y is None else y
+                if y is None:
+                    raise _at.Declined("conv_wgrad_")
+                return y
 
             cands = {"miopen": miopen_w}
             if (_at.enabled("PSD_CONV_WGRAD") and _wgrad_ok(cin, cout, k, dy)
@@ -951,9 +979,10 @@ class _ConvFn(torch.autograd.Function):
             cands.update(wcands)
             key = ("wgrad", n, cin, h, w, cout, k, stride)
             how = _at.choose(("conv",) + key, cands, "miopen") if len(cands) > 1 else "miopen"
-            dw = None
             if how == "igemm":
                 dw = igemm_w(sv.permute(0, 2, 3, 1) if sv is not None else None)
+                if dw is None:
+                    raise RuntimeError(f"conv_wgrad_ declined {key} after it was chosen")
             elif how in wcands:
                 ohwi = sv.permute(0, 2, 3, 1) if sv is not None else None
                 if ohwi is not None and ohwi.is_contiguous():  # the sink itself, in the kernel's layout
@@ -964,7 +993,9 @@ class _ConvFn(torch.autograd.Function):
                     dw = wcands[how]()
                     if dw is not None and sv is not None:
                         dw = sv.copy_(dw)
-            if dw is None:
+                if dw is None:
+                    raise RuntimeError(f"convw_ {how} declined {key} after it was chosen")
+            else:
                 dw = miopen_w()
                 if sv is not None:
                     dw = sv.copy_(dw)

@@ -22,10 +22,10 @@ histogram (staleness = shard version at apply - version the gradient was compute
 
 Optimizer semantics (``semantics``):
 
-  "round" (default): K-batch asynchronous SGD with K = W (min(W, 16)). Each shard takes the pushes
+  "round" (default): K-batch asynchronous SGD with K = W. Each shard takes the pushes
           in arrival order, from whichever workers, and every K of them make ONE optimizer step on
           their average with the synchronous hyperparameters (the K inbox slots are summed inside
-          the fused apply kernel). A worker's clock advances when the round holding its push has
+          the fused apply kernel; above 16, in groups of 16 into fp32 partials first). A worker's clock advances when the round holding its push has
           been applied. At SSP bound 0 the rounds are exactly the synchronous steps (a worker
           cannot push step t+1 before every step-t push is applied), so the trajectory equals the
           synchronous one; at S >= 1 a round may mix steps (stale gradients, bounded by S).
@@ -49,6 +49,7 @@ from __future__ import annotations
 
 import contextlib
 import os
+import time
 import uuid
 from dataclasses import dataclass, field
 
@@ -60,7 +61,6 @@ from .. import native
 from ..ops.optim import OptimConfig, OptimDyn
 from .collective_ps import ALIGN, _flat_view, _round, install_fp8_weights, zero_grads_, zero_plan
 
-_INSTANCE: dict = {}  # AsyncPS instances per rendezvous store (a new elastic generation starts at 0)
 
 
 class _NoTransport:
@@ -98,9 +98,14 @@ class AsyncPS:
                  bucket_mb: float = 16.0, device: torch.device | None = None, ps_ranks: list[int] | None = None,
                  worker_ranks: list[int] | None = None, param_dtype: torch.dtype = torch.bfloat16, nbuf: int = 4,
                  timeout_s: float | None = None, overlap: bool = True, store=None, log: bool = False,
-                 semantics: str = "round", pull_dtype: str = "bf16"):
+                 semantics: str = "round", pull_dtype: str = "bf16", schedule: str = "free"):
         """``semantics``: "round" (K-batch async, default) or "push" (apply-on-arrival with the
         per-push hyperparameters of csrc/async_hyper.h); see the module docstring.
+        ``schedule`` "fixed" ("round" semantics only): round r holds exactly every worker's step-r
+        push and the pull of step t takes exactly version max(t - S, 0) -- every gradient is
+        S rounds stale whatever the timing, so an S >= 1 run is bit-for-bit reproducible and equals
+        synchronous SGD with S-step-delayed gradients (csrc/async_ps.h set_fixed_schedule). "free"
+        (default): rounds in arrival order, pulls of the latest admissible snapshot.
         ``pull_dtype`` "fp8" (the Wide-ResNet fp8-weights config): each owner also publishes the MX
         e4m3 copy of its snapshot (one E8M0 scale per 32 elements, quantised from the fp32 master
         right after the apply, csrc/async_ps.cpp quant_publish); workers pull 1.03 bytes/parameter
@@ -134,6 +139,11 @@ class AsyncPS:
         self.pull_mx = pull_dtype == "fp8" and param_dtype == torch.bfloat16 and self.is_cuda
         self.param_dtype = param_dtype
         self.step_idx = 0
+        if schedule not in ("free", "fixed") or (schedule == "fixed" and semantics != "round"):
+            raise ValueError(f"schedule must be 'free' or 'fixed' (fixed: round semantics), got {schedule!r}")
+        self.schedule = schedule
+        if schedule == "fixed":
+            nbuf = max(nbuf, self.S + 2)  # the last S + 1 versions stay published
         self.pulled = [0] * self.P
         timeout_s = float(os.environ.get("PSD_ASYNC_TIMEOUT", timeout_s or 600.0))
 
@@ -151,20 +161,7 @@ class AsyncPS:
         bounds = [_round(total * k // self.P, ALIGN) for k in range(self.P)] + [total]
         self.shard_off = bounds[:-1]
         self.shard_len = [bounds[k + 1] - bounds[k] for k in range(self.P)]
-        # push buckets: consecutive parameter ranges of ~bucket_mb
-        elem = torch.finfo(param_dtype).bits // 8
-        cap = max(ALIGN, int(bucket_mb * (1 << 20)) // elem)
-        self.buckets: list[_Bucket] = []
-        cur = _Bucket(0, lo=0)
-        for n, p, o, k in layout:
-            cur.params.append((n, p, o, k))
-            cur.hi = o + _round(k, ALIGN)
-            if cur.hi - cur.lo >= cap:
-                self.buckets.append(cur)
-                cur = _Bucket(len(self.buckets), lo=cur.hi)
-        if cur.params:
-            self.buckets.append(cur)
-        self.buckets[-1].hi = total  # the tail padding travels with the last bucket
+        self._build_buckets(layout, bucket_mb)
 
         dev = self.device
         init = torch.zeros(total, dtype=torch.float32, device=dev)
@@ -188,7 +185,9 @@ class AsyncPS:
         if semantics not in ("round", "push"):
             raise ValueError(f"semantics must be 'round' or 'push', got {semantics!r}")
         self.semantics = semantics
-        self.round = min(self.W, 16) if semantics == "round" else 1
+        # K = W: every round completes (a cap below W would strand a partial round at W > 16 and
+        # hold a worker's clock back forever); the engine pre-reduces above 16 sources
+        self.round = self.W if semantics == "round" else 1
         if semantics == "push":
             self.hyper = native().async_hyper(optim.code, self.W, optim.momentum, optim.beta1, optim.beta2,
                                               optim.weight_decay)
@@ -216,10 +215,6 @@ class AsyncPS:
         self._layout = layout
         self._zero_plan = zero_plan([(o, p.numel()) for (_n, p, o, _k) in layout if id(p) not in self._direct], total)
         self._arrived: set = set()
-        self._p2b = {}
-        for b in self.buckets:
-            for _, p, _o, _n in b.params:
-                self._p2b[id(p)] = b
         self._pviews = [[_flat_view(b, o, p) for (_n, p, o, _k) in layout] for b in self.pbufs]
         for (n, p, o, k), v in zip(layout, self._pviews[0]):
             p.data = v
@@ -227,7 +222,11 @@ class AsyncPS:
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for _, p, _o, _n in layout]
         self._next = 0
         if self.is_cuda:
+            # push copies alternate over two streams (bucket i on stream i % 2), so two buckets'
+            # DMAs -- to different owners' links, or one large bucket after another -- can be in
+            # flight together; the commit waits for both
             self.comm_stream = torch.cuda.Stream(device=dev)
+            self.comm_streams = [self.comm_stream, torch.cuda.Stream(device=dev)]
             self.pull_stream = torch.cuda.Stream(device=dev)
             self.push_done = [None, None]
             self.step_done = [None, None]  # end of a step's work on the compute stream, per buffer
@@ -235,8 +234,10 @@ class AsyncPS:
         self._prefetched = None  # (step, pulled versions) of the pull issued ahead
 
         # ---- native engine: control block (rank 0 creates), memory exchange, initial publish
-        n = _INSTANCE.get(id(self.store), 0) + 1
-        _INSTANCE[id(self.store)] = n
+        # instance sequence number from the store itself (a per-rank counter key): every rank
+        # agrees on it for any store lifetime -- an id(store)-keyed local count could collide when
+        # a freed elastic generation's store address is reused on some ranks only
+        n = int(self.store.add(f"psd/async/seq/{self.rank}", 1))
         key = f"psd/async/{n}"
         if self.rank == 0:
             self.store.set(f"{key}/shm", f"/psd_{os.getpid()}_{uuid.uuid4().hex[:12]}")
@@ -284,6 +285,7 @@ class AsyncPS:
                                         h["weight_decay"], h["beta1"], h["beta2"], optim.eps)
             self.engine.publish_initial(k)
         self.engine.set_round(self.round)
+        self.engine.set_fixed_schedule(self.schedule == "fixed")
         if log:
             self.engine.enable_log(True)
         self._barrier("init")
@@ -465,8 +467,9 @@ class AsyncPS:
         if self.is_cuda:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.device))
-            self.comm_stream.wait_event(ev)
-            self.engine.push(self.step_idx, g, b.lo, b.hi, self.comm_stream.cuda_stream)
+            cs = self.comm_streams[b.index % len(self.comm_streams)]
+            cs.wait_event(ev)
+            self.engine.push(self.step_idx, g, b.lo, b.hi, cs.cuda_stream)
         else:
             self.engine.push(self.step_idx, g, b.lo, b.hi, 0)
 
@@ -477,6 +480,10 @@ class AsyncPS:
             self._push(self.buckets[self._next])
             self._next += 1
         if self.is_cuda:
+            for cs in self.comm_streams[1:]:  # the commit posts after every push copy has landed
+                ev = torch.cuda.Event()
+                ev.record(cs)
+                self.comm_stream.wait_event(ev)
             self.engine.commit(self.step_idx, self.pulled, self.comm_stream.cuda_stream)
             ev = torch.cuda.Event()
             ev.record(self.comm_stream)
@@ -511,6 +518,66 @@ class AsyncPS:
             self.pulled = self._pull_into(0, self.cb, None)
             if self.is_cuda:
                 torch.cuda.synchronize(self.device)
+
+    def _build_buckets(self, layout, bucket_mb: float):
+        """Push buckets: consecutive parameter ranges of ~``bucket_mb`` (the tail padding travels
+        with the last bucket)."""
+        elem = torch.finfo(self.param_dtype).bits // 8
+        cap = max(ALIGN, int(bucket_mb * (1 << 20)) // elem)
+        self.buckets: list[_Bucket] = []
+        cur = _Bucket(0, lo=0)
+        for n, p, o, k in layout:
+            cur.params.append((n, p, o, k))
+            cur.hi = o + _round(k, ALIGN)
+            if cur.hi - cur.lo >= cap:
+                self.buckets.append(cur)
+                cur = _Bucket(len(self.buckets), lo=cur.hi)
+        if cur.params:
+            self.buckets.append(cur)
+        self.buckets[-1].hi = self.total
+        self.bucket_mb = float(bucket_mb)
+        self._p2b = {id(p): b for b in self.buckets for _n, p, _o, _k in b.params}
+
+    def rebucket(self, bucket_mb: float):
+        """Rebuild the push buckets at another size (between steps; every rank the same size)."""
+        self._build_buckets(self._layout, bucket_mb)
+
+    def probe_push_sizes(self, sizes_mb=(1, 2, 4, 8, 16, 32, 64), reps: int = 3) -> dict:
+        """The bandwidth of THIS plane's push transport vs bucket size, measured before training
+        (collective, every rank): each worker DMA-copies its whole gradient buffer into its inbox
+        slot on every owner in chunks of ``size`` MB -- one engine push per chunk on alternating
+        push streams, exactly what a step's bucket pushes do (no commit: nothing is applied) --
+        and the max over ranks of the time gives {MB: GB/s}. The RCCL send/recv probe
+        (parallel/bucketing.py probe_p2p) measures the collective plane's transport, not this one."""
+        out = {}
+        g = self.grads[0]
+        elem = g.element_size()
+        for mb in sizes_mb:
+            n = max(ALIGN, int(mb * (1 << 20)) // elem)
+            el = 0.0
+            if self.is_worker:
+                def run():
+                    for i, lo in enumerate(range(0, self.total, n)):
+                        cs = self.comm_streams[i % len(self.comm_streams)] if self.is_cuda else None
+                        self.engine.push(self.step_idx, g, lo, min(lo + n, self.total),
+                                         cs.cuda_stream if cs is not None else 0)
+                    if self.is_cuda:
+                        for cs in self.comm_streams:
+                            cs.synchronize()
+
+                run()
+                t0 = time.perf_counter()
+                for _ in range(reps):
+                    run()
+                el = (time.perf_counter() - t0) / reps
+            t = torch.tensor([el], dtype=torch.float64)
+            if self.world > 1 and dist.is_initialized():
+                if dist.get_backend() == "nccl":
+                    t = t.to(self.device)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+            out[mb] = round(self.total * elem * self.P / max(el, 1e-9) / 1e9, 1) if el > 0 else None
+        return out
 
     def probe_bandwidth(self, reps: int = 3) -> dict:
         """After ``drain``: time this worker's full push (DMA of the whole gradient into its inbox slot
@@ -723,8 +790,9 @@ class AsyncPS:
             torch.cuda.synchronize(self.device)
         self._barrier(f"ckpt-load-{self._ckpt_seq}")
         self._ckpt_seq += 1
-        if self.is_worker:  # working weights = the restored snapshot (forward hooks, eval before a step)
-            self.pulled = list(self.engine.pull(0, self.params_flat, self._stream_ptr()))
+        if self.is_worker:  # working weights = the restored snapshot (forward hooks, eval before a step);
+            # with MX pulls the e4m3 copy the fp8 convolutions read (install_fp8_weights) is pulled too
+            self.pulled = self._pull_into(0, self.cb, None)
             if self.is_cuda:
                 torch.cuda.synchronize(self.device)
 
@@ -810,6 +878,11 @@ class AsyncPS:
         self.params_flat.copy_(full["master"].to(self.param_dtype))
         for b in self.pbufs[1:]:
             b.copy_(self.params_flat)
+        for q, sc, b in zip(self.q8s, self.sc8s, self.pbufs):
+            # MX pulls: the e4m3 weights the fp8 convolutions read, and the working bf16 copy as a
+            # pull would leave it (dequantised)
+            native().quant_mx_(full["master"], q, sc)
+            native().dequant_mx_(q, sc, b)
         self.step_idx = 0
         self._prefetched = None
         if self.is_cuda:

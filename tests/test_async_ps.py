@@ -77,7 +77,7 @@ def _replay_and_check(out_dir, world, stale, bf16=False):
     workers, owners = R[0]["workers"], R[0]["owners"]
     off, ln = R[0]["shard_off"], R[0]["shard_len"]
     W = len(workers)
-    K = min(W, 16)  # "round" semantics: K pushes per optimizer step
+    K = W  # "round" semantics: K = W pushes per optimizer step (grouped by 16 inside the engine)
     recs = {R[r]["rank"]: {e["step"]: e for e in R[r]["rec"]} for r in range(world)}
     hist_total = [0] * 64
     for k, o in enumerate(owners):
@@ -119,6 +119,30 @@ def test_async_matches_replay_of_apply_order(tmp_path, world, shards, stale):
     mp.spawn(_worker, args=(world, _port(), shards, stale, 5, str(tmp_path), -1, 0.0, False), nprocs=world,
              join=True)
     _replay_and_check(str(tmp_path), world, stale)
+
+
+@pytest.mark.slow
+def test_async_w17_round_semantics_completes(tmp_path):
+    """with K = min(W, 16) a 17-worker round left one push of every step stranded and
+    that worker's clock behind forever (every later pull timed out). K = W now, with the engine
+    summing the inbox slots in groups of 16 into fp32 partials: 17 workers at SSP bound 0 finish
+    and match the replay."""
+    world = 17
+    mp.spawn(_worker, args=(world, _port(), 2, 0, 3, str(tmp_path), -1, 0.0, False), nprocs=world, join=True)
+    _replay_and_check(str(tmp_path), world, 0)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("disjoint", [False, True], ids=["2owners_8workers", "4ps_4workers_disjoint"])
+def test_async_world8_baseline_layouts(tmp_path, disjoint):
+    """World 8 on the CPU plane, the BASELINE layouts the driver's 8-GPU run uses: config 3 (2 PS
+    shards colocated on ranks 0 and 4, all 8 ranks workers, SSP bound 1) and config 4 (4 PS-only
+    ranks + 4 worker ranks, disjoint). Replay-checked like every async run."""
+    world = 8
+    shards = 4 if disjoint else 2
+    mp.spawn(_worker, args=(world, _port(), shards, 1, 4, str(tmp_path), 3, 0.02, disjoint), nprocs=world,
+             join=True)
+    _replay_and_check(str(tmp_path), world, 1)
 
 
 @pytest.mark.slow
@@ -179,8 +203,11 @@ def test_async_gpu_ipc_matches_replay(tmp_path, gpu, world, stale):
 
 
 SEM_STEPS = 30
-SEM_CFGS = {"momentum": dict(kind="momentum", lr=0.02, momentum=0.9),
-            "adamw": dict(kind="adamw", lr=2e-3, weight_decay=0.01)}
+# learning rates at which the synchronous run with gradients delayed by 0, 1 or 2 steps all train
+# to 0.53-0.57 of the initial loss (at lr 0.02 / 2e-3 a fixed 1-step delay alone left the momentum
+# run at 0.96 of it: no useful bar for S >= 1)
+SEM_CFGS = {"momentum": dict(kind="momentum", lr=0.002, momentum=0.9),
+            "adamw": dict(kind="adamw", lr=5e-4, weight_decay=0.01)}
 
 
 def _sem_batches(W):
@@ -231,42 +258,105 @@ def _sem_sync(kind, delay=0):
     return losses
 
 
-def _sem_worker(rank, world, port, kind, semantics, stale, out_dir):
+def _sem_worker(rank, world, port, kind, semantics, stale, out_dir, schedule="free", slow_rank=-1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.manual_seed(0)
     spec = models.build("mlp", torch.device("cpu"), torch.float32, hidden=64)
     ps = AsyncPS(spec.model, OptimConfig(**SEM_CFGS[kind]), num_shards=2, staleness=stale, bucket_mb=0.0005,
-                 param_dtype=torch.float32, semantics=semantics)
+                 param_dtype=torch.float32, semantics=semantics, schedule=schedule)
     batches = _sem_batches(world)
     x, y = batches[rank]
-    for _ in range(SEM_STEPS):
+    pulled = []
+    for t in range(SEM_STEPS):
+        if rank == slow_rank and t % 3 == 0:
+            time.sleep(0.02)  # uneven timing: must not change a fixed-schedule run
         ps.begin_step()
+        pulled.append(list(ps.pulled))
         spec.loss(spec.model(x), y).backward()
         ps.finish_step()
     ps.drain()
-    ps.engine.pull(0, ps.params_flat, 0)  # the final version (no SSP wait: everything is applied)
+    if schedule == "fixed":  # the final version (the fixed pull of step T + S)
+        ps.engine.pull(SEM_STEPS + stale, ps.params_flat, 0)
+    else:
+        ps.engine.pull(0, ps.params_flat, 0)  # the final version (no SSP wait: everything is applied)
     if rank == 0:
         with open(os.path.join(out_dir, "loss.txt"), "w") as f:
             f.write(repr(_sem_loss(spec, batches)))
+        torch.save({"params": ps.params_flat.clone(), "pulled": pulled}, os.path.join(out_dir, "final.pt"))
     ps.close()
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _sem_sync_params(kind, delay):
+    """Final flat parameters of the delayed synchronous reference (the AsyncPS layout order)."""
+    torch.manual_seed(0)
+    spec = models.build("mlp", torch.device("cpu"), torch.float32, hidden=64)
+    c = SEM_CFGS[kind]
+    ps = list(spec.model.parameters())
+    opt = torch.optim.SGD(ps, lr=c["lr"], momentum=c["momentum"]) if kind == "momentum" else \
+        torch.optim.AdamW(ps, lr=c["lr"], weight_decay=c["weight_decay"])
+    batches = _sem_batches(4)
+    hist = [[p.detach().clone() for p in ps]]
+    for _ in range(SEM_STEPS):
+        cur = [p.detach().clone() for p in ps]
+        with torch.no_grad():
+            for p, o in zip(ps, hist[max(0, len(hist) - 1 - delay)]):
+                p.copy_(o)
+        opt.zero_grad()
+        sum(spec.loss(spec.model(x), y) for x, y in batches).div(len(batches)).backward()
+        with torch.no_grad():
+            for p, o in zip(ps, cur):
+                p.copy_(o)
+        opt.step()
+        hist.append([p.detach().clone() for p in ps])
+    return {n: p.detach().clone() for n, p in spec.model.named_parameters()}
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("kind", ["momentum", "adamw"])
+def test_async_fixed_schedule_is_delayed_sync_and_deterministic(tmp_path, kind):
+    """the asynchronous plane at SSP bound 1 under the fixed schedule (round r =
+    every worker's step-r push; the pull of step t = exactly version t - 1), with one worker
+    sleeping on every third step to perturb the timing:
+      * every step's pulled versions are exactly max(t - 1, 0) at both shards;
+      * two runs end bitwise identical (the schedule, not the thread timing, decides everything);
+      * the final weights equal synchronous SGD whose gradients are computed one step late
+        (torch.optim, fp32) to 1e-4 relative, and the loss is below 0.7 of the initial one."""
+    res = []
+    for run in range(2):
+        d = tmp_path / f"run{run}"
+        d.mkdir()
+        mp.spawn(_sem_worker, args=(4, _port(), kind, "round", 1, str(d), "fixed", 2), nprocs=4, join=True)
+        res.append((float(open(d / "loss.txt").read()), torch.load(d / "final.pt", weights_only=True)))
+    (l0, f0), (l1, f1) = res
+    assert torch.equal(f0["params"], f1["params"]) and l0 == l1
+    assert f0["pulled"] == [[max(t - 1, 0)] * 2 for t in range(SEM_STEPS)]
+    want = _sem_sync_params(kind, 1)
+    torch.manual_seed(0)
+    spec = models.build("mlp", torch.device("cpu"), torch.float32, hidden=64)
+    ps = AsyncPS(spec.model, OptimConfig(**SEM_CFGS[kind]), staleness=0, bucket_mb=0.0005, param_dtype=torch.float32)
+    ps.params_flat.copy_(f0["params"])
+    for n, p in spec.model.named_parameters():
+        assert (p.detach() - want[n]).norm() <= 1e-4 * want[n].norm() + 1e-7, n
+    ps.close()
+    ref = _sem_sync(kind, 1)[-1]
+    assert abs(l0 - ref) <= 1e-4 * ref, (l0, ref)
+    assert l0 < 0.7 * _sem_loss_init(), l0
 
 
 @pytest.mark.slow
 @pytest.mark.parametrize("kind", ["momentum", "adamw"])
 def test_async_w4_tracks_sync_trajectory(tmp_path, kind):
     """W = 4 workers on shards of one learnable task, 2 PS shards, against synchronous SGD
-    (torch.optim on the averaged gradient):
+    (torch.optim on the averaged gradient), free-running (arrival-order) schedule:
       * "round" semantics at SSP bound 0 reproduce the synchronous trajectory -- the rounds are
         exactly the synchronous steps, so the final loss agrees to 1e-3;
-      * at bound 1 every gradient is 0-2 rounds stale. "round" and "push" must train (final loss
-        < 95 % of the initial one) and end no worse than 1.1 x the worst synchronous run whose
-        gradients are delayed by a fixed 0, 1 or 2 steps (this task is very sensitive to gradient
-        delay: a fixed 1-step delay alone moves the 30-step momentum loss from 1.22 to 2.31 of an
-        initial 2.41, so neither delay-free sync nor a large drop is the right bar for S >= 1; the
-        staleness pattern, and with it the result, depends on thread timing)."""
+      * at bound 1 every gradient is 0-2 rounds stale, in a timing-dependent pattern. "round" and
+        "push" must train (final loss < 0.7 of the initial one) and end no worse than 1.1 x the
+        worst synchronous run whose gradients are delayed by a fixed 0, 1 or 2 steps. The exact S = 1
+        semantics are pinned by the fixed-schedule test above."""
     sync = _sem_sync(kind)
     worst_delayed = max(_sem_sync(kind, d)[-1] for d in (0, 1, 2))
     res = {}
@@ -280,7 +370,7 @@ def test_async_w4_tracks_sync_trajectory(tmp_path, kind):
     assert ref < 0.6 * start, (start, ref)  # the reference is actually training
     assert abs(res[("round", 0)] - ref) < 1e-3 * ref, (kind, ref, res)
     for key in (("round", 1), ("push", 1)):
-        assert res[key] < 0.95 * start, (kind, start, res)
+        assert res[key] < 0.7 * start, (kind, start, res)
         assert res[key] < 1.1 * worst_delayed, (kind, worst_delayed, res)
 
 

@@ -1,0 +1,57 @@
+"""Cross-rank agreement of the per-shape kernel choice (ops/autotune.py): at N > 1 the first rank
+to reach a key times it and every other rank takes that decision through the store. Two gloo
+ranks whose candidates time in opposite orders (each alone would pick a different one) must run
+the same candidate; and a saved decision file pins choices with no timing."""
+import os
+import socket
+import time
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from parameter_server_distributed_amd.ops import autotune as at
+
+    picks = []
+    for i in range(3):
+        slow_a = (rank + i) % 2 == 0  # rank-dependent: local timing would disagree across ranks
+
+        def a():
+            time.sleep(0.02 if slow_a else 0.0)
+            return torch.ones(4)
+
+        def b():
+            time.sleep(0.0 if slow_a else 0.02)
+            return torch.ones(4)
+
+        picks.append(at.choose(("test", i), {"a": a, "b": b}, "a"))
+    with open(os.path.join(out_dir, f"r{rank}.txt"), "w") as f:
+        f.write(repr((picks, at.source())))
+    if rank == 0:
+        at.save_decisions(os.path.join(out_dir, "dec.json"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_autotune_ranks_agree_and_file_roundtrip(tmp_path):
+    mp.spawn(_rank, args=(2, _port(), str(tmp_path)), nprocs=2, join=True)
+    (p0, s0), (p1, s1) = (eval(open(tmp_path / f"r{r}.txt").read()) for r in range(2))
+    assert p0 == p1, (p0, p1)
+    assert s0["claimed"] + s1["claimed"] == 3 and s0["peer"] + s1["peer"] == 3, (s0, s1)
+    from parameter_server_distributed_amd.ops import autotune as at
+
+    n = at.load_decisions(str(tmp_path / "dec.json"))
+    assert n == 3
+    for i in range(3):
+        assert at.choose(("test", i), {"a": None, "b": None}, "a") == p0[i]
+        at.set_decision(("test", i), None)

@@ -222,7 +222,8 @@ def test_convn_halo_exact_with_stats(gpu, case):
     want = ref.permute(0, 2, 3, 1).reshape(-1, Cout).bfloat16().float()
     w2 = _w2(w.to(gpu, torch.bfloat16))
     C_ = native()
-    halo = [v for v in range(C_.convn_variants(Cout)) if v >= (2 if Cout % 256 == 0 else 4)]
+    halo = [v for v in range(C_.convn_variants(Cout))
+            if C_.convn_variant_kind(Cout, v) == 1 or (C_.convn_variant_kind(Cout, v) == 2 and C == 64)]
     assert halo and all(C_.convn_variant_ok(Cout, v, 3, 3, 1, 1, H) for v in halo)
     shift = torch.zeros(Cout, device=gpu)
     for v in halo:
@@ -247,3 +248,108 @@ def test_convn_halo_declines_where_it_cannot_tile(gpu):
     assert not C_.convn_variant_ok(64, hv, 1, 1, 1, 0, 56)   # 1x1
     assert not C_.convn_variant_ok(64, hv, 3, 3, 1, 1, 63)   # Wo + 2 > 64
     assert C_.convn_variant_ok(64, hv, 3, 3, 1, 1, 62)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,N,H", [(1, 256, 14), (2, 256, 14), (5, 256, 14), (2, 128, 10), (5, 64, 12), (1, 64, 9)])
+def test_convn_bwd_epilogue_exact(gpu, mode, N, H):
+    """The bwd-data epilogue of a 1x1 convolution (out = dY . W^T, K = 64) against an fp64 reference:
+    mode 1 g = (x * scale + shift > 0) ? out : 0; mode 2 g = bit ? out + dr : 0; mode 5 as 2 with dr
+    on the stride-2 quarter grid (added at even (h, w) only); partials sum g and sum g (x - mean) per
+    channel, every tile variant. Small-integer operands: every value is exact in bf16 and fp32."""
+    Nb, K = 3, 64
+    g = torch.Generator().manual_seed(21)
+    dy = torch.randint(-1, 2, (Nb, K, H, H), generator=g).float()
+    w2 = torch.randint(-1, 2, (N, K), generator=g).float()
+    M = Nb * H * H
+    out_ref = dy.permute(0, 2, 3, 1).reshape(M, K).double() @ w2.double().t()
+    bx = torch.randint(-3, 4, (M, N), generator=g).float()
+    mean = torch.randint(-2, 3, (N,), generator=g).float()
+    C_ = native()
+    args = {}
+    if mode == 1:
+        scale = torch.randint(1, 3, (N,), generator=g).float()
+        shift = torch.randint(-3, 4, (N,), generator=g).float() + 0.5  # never exactly zero
+        keep = (bx * scale + shift) > 0
+        gref = torch.where(keep, out_ref, torch.zeros_like(out_ref))
+        args["bss"] = torch.cat([scale, shift]).to(gpu)
+    else:
+        bits = torch.randint(0, 2, (M, N), generator=g).bool()
+        packed = (bits.view(M * N // 8, 8).to(torch.uint8) << torch.arange(8, dtype=torch.uint8)).sum(1).to(torch.uint8)
+        args["bmbits"] = packed.to(gpu)
+        if mode == 2:
+            dr = torch.randint(-2, 3, (M, N), generator=g).float()
+            add = dr.double()
+            args["bdr"] = dr.to(gpu, torch.bfloat16)
+        else:
+            dr4 = torch.randint(-2, 3, (Nb, N, H // 2, H // 2), generator=g).float()
+            full = torch.zeros(Nb, N, H, H)
+            full[:, :, ::2, ::2] = dr4
+            add = full.permute(0, 2, 3, 1).reshape(M, N).double()
+            args["bdr"] = dr4.to(gpu, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        gref = torch.where(bits, out_ref + add, torch.zeros_like(out_ref))
+    s1 = gref.sum(0)
+    s2 = (gref * (bx.double() - mean.double())).sum(0)
+    dyd = dy.to(gpu, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w2d = w2.to(gpu, torch.bfloat16)
+    nvar = 0
+    for v in range(C_.convn_variants(N)):
+        if not C_.convn_variant_ok(N, v, 1, 1, 1, 0, H):
+            continue
+        nvar += 1
+        out = torch.full((M, N), 7.0, device=gpu, dtype=torch.bfloat16)
+        part = torch.full((max(C_.convn_stats_rows(M), C_.convn_part_rows(M, N, v, H, H, 1)), 2, N), float("nan"),
+                          device=gpu)
+        rows = C_.convn_bwd_(dyd, w2d, out, 1, 1, 1, 0, part, v, mode, bx.to(gpu, torch.bfloat16), mean.to(gpu),
+                             **args)
+        assert rows > 0, v
+        torch.testing.assert_close(out.double().cpu(), gref, rtol=0, atol=0, msg=lambda m: f"variant {v}: {m}")
+        got = part[:rows].double().cpu().sum(0)
+        torch.testing.assert_close(got[0], s1, rtol=0, atol=1e-6, msg=lambda m: f"variant {v} sum g: {m}")
+        torch.testing.assert_close(got[1], s2, rtol=0, atol=1e-6, msg=lambda m: f"variant {v} sum g(x-mean): {m}")
+    assert nvar >= 2
+
+
+@pytest.mark.parametrize("Nb,H", [(2, 56), (3, 13), (1, 62), (2, 2)])
+@pytest.mark.parametrize("mode", [1, 2])
+def test_convn_persistent_bwd_matches_gathered(gpu, Nb, H, mode):
+    """The persistent HALO variant (kind 2: C = N = 64 3x3, resident weights, double-buffered
+    windows) as a stride-1 bwd-data with the producing BN's backward reduction in the epilogue
+    (mode 1: ReLU mask from x and scale/shift; mode 2: bit-mask + handed-over residual gradient):
+    output and summed partials equal the gathered variant's exactly (small-integer operands: every
+    value and sum is exact). Odd and tiny images: partial last tiles, one-row images."""
+    C_ = native()
+    g = torch.Generator().manual_seed(5)
+    dy = torch.randint(-1, 2, (Nb, 64, H, H), generator=g).float()
+    w = torch.randint(-1, 2, (64, 64, 3, 3), generator=g).float()
+    M = Nb * H * H
+    bx = torch.randint(-3, 4, (M, 64), generator=g).to(gpu, torch.bfloat16)
+    mean = torch.randint(-2, 3, (64,), generator=g).float().to(gpu)
+    args = {}
+    if mode == 1:
+        args["bss"] = torch.cat([torch.randint(1, 3, (64,), generator=g).float(),
+                                 torch.randint(-3, 4, (64,), generator=g).float() + 0.5]).to(gpu)
+    else:
+        bits = torch.randint(0, 2, (M * 64,), generator=g).bool().view(-1, 8)
+        args["bmbits"] = (bits.to(torch.uint8) << torch.arange(8, dtype=torch.uint8)).sum(1).to(torch.uint8).to(gpu)
+        args["bdr"] = torch.randint(-2, 3, (M, 64), generator=g).to(gpu, torch.bfloat16)
+    dyd = dy.to(gpu, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    wf = _w2(w.flip(2, 3).permute(1, 0, 2, 3).contiguous().to(gpu, torch.bfloat16))
+    pv = [v for v in range(C_.convn_variants(64)) if C_.convn_variant_kind(64, v) == 2]
+    assert len(pv) == 1 and C_.convn_variant_ok(64, pv[0], 3, 3, 1, 1, H)
+    res = {}
+    for v in (0, pv[0]):
+        out = torch.full((M, 64), 7.0, device=gpu, dtype=torch.bfloat16)
+        part = torch.full((max(C_.convn_stats_rows(M), C_.convn_part_rows(M, 64, v, H, H, 3)), 2, 64), float("nan"),
+                          device=gpu)
+        rows = C_.convn_bwd_(dyd, wf, out, 3, 3, 1, 1, part, v, mode, bx, mean, **args)
+        assert rows == C_.convn_part_rows(M, 64, v, H, H, 3) > 0
+        res[v] = (out.float().cpu(), part[:rows].double().sum(0).cpu())
+    ref = F.conv_transpose2d(dy, w, padding=1)  # dX of conv(x, w): the bwd-data the kernel computes
+    o0, p0 = res[0]
+    assert torch.isfinite(p0).all()
+    o1, p1 = res[pv[0]]
+    torch.testing.assert_close(o1, o0, rtol=0, atol=0)
+    torch.testing.assert_close(p1, p0, rtol=0, atol=1e-6)
+    raw = ref.permute(0, 2, 3, 1).reshape(M, 64)
+    assert ((o0 == 0) | (o0 == raw) | (mode == 2)).all()  # mode 1: masked copy of dX
