@@ -256,11 +256,9 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
     load8_f32(rss + cg * 8, rsc);
     load8_f32(rss + C + cg * 8, rsh);
   }
-  for (; v < nvec; v += stride) {
-    float t[8];
-    load8_bf16(x + v * 8, t);
-    float rr[8];
-    if (RES) load8_bf16(res + v * 8, rr);
+  // two items in flight per lane (both items' loads issued before either is used: the streaming
+  // passes sat at ~4.8 TB/s with one 16-byte load per lane outstanding)
+  auto apply = [&](int64_t v, float (&t)[8], const float (&rr)[8]) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float o = fmaf(t[j], sc[j], sh[j]);
@@ -307,6 +305,23 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
         mbits[v] = (uint8_t)bits;
       }
     }
+  };
+  for (; v + stride < nvec; v += 2 * stride) {  // (lane quads stay together: nvec, stride % 4 == 0)
+    float t0[8], t1[8], r0[8], r1[8];
+    load8_bf16(x + v * 8, t0);
+    load8_bf16(x + (v + stride) * 8, t1);
+    if (RES) {
+      load8_bf16(res + v * 8, r0);
+      load8_bf16(res + (v + stride) * 8, r1);
+    }
+    apply(v, t0, r0);
+    apply(v + stride, t1, r1);
+  }
+  for (; v < nvec; v += stride) {
+    float t[8], rr[8];
+    load8_bf16(x + v * 8, t);
+    if (RES) load8_bf16(res + v * 8, rr);
+    apply(v, t, rr);
   }
   if (Q8 == 1) {
     for (int off = 32; off > 0; off >>= 1) q8max = fmaxf(q8max, __shfl_xor(q8max, off, kWave));
@@ -474,19 +489,12 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(const uint16_t* __res
     load8_f32(ssf + cg * 8, sc);
     load8_f32(ssf + C + cg * 8, sh);
   }
-  for (; v < nvec; v += stride) {
-    float gv[8], xv[8];
-    load8_bf16(g + v * 8, gv);
-    load8_bf16(x + v * 8, xv);
+  auto elemt = [&](int64_t v, float (&gv)[8], const float (&xv)[8], const float (&h)[8], const float (&yv)[8]) {
     if (MODE != 2 && g2) {
-      float h[8];
-      load8_bf16(g2 + v * 8, h);
 #pragma unroll
       for (int j = 0; j < 8; ++j) gv[j] += h[j];
     }
     if (MODE == 1) {
-      float yv[8];
-      load8_bf16(y + v * 8, yv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) gv[j] = yv[j] > 0.f ? gv[j] : 0.f;
     }
@@ -505,6 +513,32 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(const uint16_t* __res
       *reinterpret_cast<uint2*>(dq + v * 8) = qb;
       if ((v & 3) == 0) dqmx[v >> 2] = (uint8_t)eb;
     }
+  };
+  // two items in flight per lane (all loads of both before either is used)
+  for (; v + stride < nvec; v += 2 * stride) {
+    float g0[8], g1[8], x0[8], x1[8], h0[8], h1[8], y0[8], y1[8];
+    load8_bf16(g + v * 8, g0);
+    load8_bf16(g + (v + stride) * 8, g1);
+    load8_bf16(x + v * 8, x0);
+    load8_bf16(x + (v + stride) * 8, x1);
+    if (MODE != 2 && g2) {
+      load8_bf16(g2 + v * 8, h0);
+      load8_bf16(g2 + (v + stride) * 8, h1);
+    }
+    if (MODE == 1) {
+      load8_bf16(y + v * 8, y0);
+      load8_bf16(y + (v + stride) * 8, y1);
+    }
+    elemt(v, g0, x0, h0, y0);
+    elemt(v + stride, g1, x1, h1, y1);
+  }
+  for (; v < nvec; v += stride) {
+    float gv[8], xv[8], h[8], yv[8];
+    load8_bf16(g + v * 8, gv);
+    load8_bf16(x + v * 8, xv);
+    if (MODE != 2 && g2) load8_bf16(g2 + v * 8, h);
+    if (MODE == 1) load8_bf16(y + v * 8, yv);
+    elemt(v, gv, xv, h, yv);
   }
 }
 
@@ -528,13 +562,9 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_dual_kernel(const uint16_t* 
   load8_f32(coef_d + cg * 8, Ad);
   load8_f32(coef_d + C + cg * 8, Bd);
   load8_f32(coef_d + 2 * C + cg * 8, Cd);
-  for (; v < nvec; v += stride) {
-    float gv[8], dv[8], o[8];
-    load8_bf16(g + v * 8, gv);
-    load8_bf16(xd + v * 8, dv);
+  auto dual = [&](int64_t v, const float (&gv)[8], const float (&dv)[8], const float (&xv)[8]) {
+    float o[8];
     if constexpr (WDX) {
-      float xv[8];
-      load8_bf16(x + v * 8, xv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = fmaf(A[j], gv[j], fmaf(B[j], xv[j], Cc[j]));
       store8_bf16(dx + v * 8, o);
@@ -542,6 +572,26 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_dual_kernel(const uint16_t* 
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = fmaf(Ad[j], gv[j], fmaf(Bd[j], dv[j], Cd[j]));
     store8_bf16(dxd + v * 8, o);
+  };
+  for (; v + stride < nvec; v += 2 * stride) {  // two items in flight per lane
+    float g0[8], g1[8], d0[8], d1[8], x0[8], x1[8];
+    load8_bf16(g + v * 8, g0);
+    load8_bf16(g + (v + stride) * 8, g1);
+    load8_bf16(xd + v * 8, d0);
+    load8_bf16(xd + (v + stride) * 8, d1);
+    if constexpr (WDX) {
+      load8_bf16(x + v * 8, x0);
+      load8_bf16(x + (v + stride) * 8, x1);
+    }
+    dual(v, g0, d0, x0);
+    dual(v + stride, g1, d1, x1);
+  }
+  for (; v < nvec; v += stride) {
+    float gv[8], dv[8], xv[8];
+    load8_bf16(g + v * 8, gv);
+    load8_bf16(xd + v * 8, dv);
+    if constexpr (WDX) load8_bf16(x + v * 8, xv);
+    dual(v, gv, dv, xv);
   }
 }
 

@@ -249,6 +249,120 @@ __global__ __launch_bounds__(512) void convw_kernel(ConvwArgs a) {
     }
 }
 
+
+// ------------------------------------------------------------------ persistent HALO (layer1 3x3)
+// The weight gradient of the C = 64 -> N = 64 3x3 / stride 1 / pad 1 convolution (ResNet layer1
+// conv2, 56 x 56): the tiled kernel above gathers the shifted input rows of every (r, s) K-block
+// through L2 (9 x the input per pass) and re-reads dY once per column tile; MIOpen's igemm_wrw took
+// 0.55 ms at b1024 (profiles/resnet50_b1024_r3_final_kernels.md). Here one workgroup per CU runs a
+// contiguous run of output-row tiles (2 rows x 64 slots) and keeps the WHOLE 64 x 576 gradient of
+// its run in registers (4 waves; wave w owns input channels 16w..16w+15 of all 9 taps and all 64
+// output channels: 36 16x16 accumulators):
+//   * per tile the dY rows ([128 slots][64 n], zero past Wo) and the input window (4 rows x 64 slots
+//     x 64 channels, zero outside the image) are DMA'd once into LDS, double-buffered under the
+//     previous tile's MFMA work -- 48 KiB per 128 output pixels instead of ~200;
+//   * per 32-pixel k-step: 4 dY^T fragments (shared by the 9 taps) and 9 window fragments (the tap
+//     shift is a row offset into the window), all with the transpose read ds_read_b64_tr_b16,
+//     36 MFMAs;
+//   * the workgroup's fp32 partial gradient goes to its slab row once at the end; the deterministic
+//     slab reduce (gemm.hip) sums the workgroups and writes bf16 dW.
+constexpr int kHwDy = 128 * 128;       // dY tile: 128 slots x 64 channels bf16
+constexpr int kHwWin = 4 * 64 * 128;   // input window
+constexpr int kHwBuf = kHwDy + kHwWin;
+constexpr int kHwLds = 2 * kHwBuf + 1024;  // + the tap overrun past the last window row
+
+// transpose-read fragment of rows rbase + 8g + q (and + 4) of a pixel-major [rows][64 ch] image,
+// channel block cb (lane -> channel cb*16 + (lane & 15))
+__device__ __forceinline__ bf16x8 trfrag_rows(const uint8_t* img, int rbase, int cb, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int r0 = rbase + 8 * g + q, r1 = r0 + 4;
+  const int c = 2 * cb + (p >> 1), b = (p & 1) * 8;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + r0 * 128 + ((c ^ swz(r0)) << 4) + b));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + r1 * 128 + ((c ^ swz(r1)) << 4) + b));
+  const s16x4 both[2] = {lo, hi};
+  return __builtin_bit_cast(bf16x8, both);
+}
+
+__global__ __launch_bounds__(256) void convhw_kernel(ConvwArgs a, int ntiles) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tpi = (a.Ho + 1) >> 1;
+  const int t_begin = (int)(((int64_t)blockIdx.x * ntiles) / gridDim.x);
+  const int t_end = (int)(((int64_t)(blockIdx.x + 1) * ntiles) / gridDim.x);
+  const rsrc_t dyr = make_rsrc(a.dy, a.dybytes);
+  const rsrc_t xr = make_rsrc(a.x, a.xbytes);
+  auto buf = [&](int b) { return smem + b * kHwBuf; };
+  // tile `tile` into buffer b: 16 dY pieces + 32 window pieces of 1 KiB (12 per wave)
+  auto stage = [&](int tile, int b) {
+    const int n = tile / tpi, ho0 = (tile - n * tpi) * 2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // dY: image rows = tile slots (row j, slot ws)
+      const int pc = i * 4 + wid;
+      const int row = pc * 8 + (lane >> 3);
+      const int j = row >> 6, ws = row & 63;
+      const int kc = (lane & 7) ^ swz(row);
+      const bool ok = ws < a.Wo && ho0 + j < a.Ho;
+      const uint32_t off = ok ? ((uint32_t)(((n * a.Ho + ho0 + j) * a.Wo + ws)) * 64u + (uint32_t)(kc * 8)) * 2u : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(dyr, (__attribute__((address_space(3))) void*)(buf(b) + pc * 1024), 16,
+                                               off, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {  // window: rows ho0-1 .. ho0+2, slot ws = input column ws - 1
+      const int pc = i * 4 + wid;
+      const int row = pc * 8 + (lane >> 3);
+      const int jj = row >> 6, ws = row & 63;
+      const int hi = ho0 - 1 + jj, wi = ws - 1;
+      const int kc = (lane & 7) ^ swz(row);
+      const bool ok = (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+      const uint32_t off = ok ? ((uint32_t)((n * a.H + hi) * a.W + wi) * 64u + (uint32_t)(kc * 8)) * 2u : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(buf(b) + kHwDy + pc * 1024),
+                                               16, off, 0, 0, 0);
+    }
+  };
+  f32x4 acc[9][4];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) acc[t][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (t_begin < t_end) {
+    stage(t_begin, 0);
+    wait_vm<0>();
+    __syncthreads();
+  }
+  for (int tile = t_begin, it = 0; tile < t_end; ++tile, ++it) {
+    const int b = it & 1;
+    if (tile + 1 < t_end) stage(tile + 1, b ^ 1);  // lands under this tile's MFMA work
+    const uint8_t* dyi = buf(b);
+    const uint8_t* win = buf(b) + kHwDy;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {  // 32 output pixels: row j = ks / 2, slots (ks % 2) * 32 ..
+      bf16x8 af[4];
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) af[nb] = trfrag_rows(dyi, ks * 32, nb, lane);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int r = t / 3, sx = t - r * 3;
+        const bf16x8 bfr = trfrag_rows(win, ((ks >> 1) + r) * 64 + (ks & 1) * 32 + sx, wid, lane);
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb) acc[t][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[nb], bfr, acc[t][nb], 0, 0, 0);
+      }
+    }
+    wait_vm<0>();     // this wave's DMA of the next tile landed
+    __syncthreads();  // every wave's: the next tile is complete and this one no longer read
+  }
+  // this workgroup's partial gradient -> its slab: D[n][c] of 16x16 block (nb, wid) of tap t is
+  // row n = nb*16 + 4*(lane >> 4) + i, column kk = t*64 + wid*16 + (lane & 15)
+  float* sl = a.slab + (int64_t)blockIdx.x * 64 * 576;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        sl[(nb * 16 + 4 * (lane >> 4) + i) * 576 + t * 64 + wid * 16 + (lane & 15)] = acc[t][nb][i];
+}
+
 // ------------------------------------------------------------------ host side
 namespace {
 
@@ -318,13 +432,25 @@ hipError_t launch_t(const ConvwArgs& a, int grid, hipStream_t st) {
 
 }  // namespace
 
-int convw_variants(int Cout, int KK) {
+static int tiled_variants(int Cout, int KK) {
   const int tco = tile_co(Cout);  // plain launches (fold launches have one fixed tile)
   if (!tco || KK <= 0 || KK % 64 != 0) return 0;
   int n = 0;
   while (pick_tkk(tco, KK, n)) ++n;
   return n;
 }
+
+// + the persistent HALO variant (convhw_kernel) for the 64 -> 64 3x3 shape (KK = 576)
+int convw_variants(int Cout, int KK) { return tiled_variants(Cout, KK) + (Cout == 64 && KK == 576 ? 1 : 0); }
+
+static bool is_persist_w(const ConvwArgs& a) {
+  return !a.fold && a.Cout == 64 && a.KK == 576 && a.variant == tiled_variants(64, 576);
+}
+static bool persist_w_ok(const ConvwArgs& a) {
+  return is_persist_w(a) && a.logC == 6 && a.S == 3 && a.stride == 1 && a.pad == 1 && a.H == a.Ho && a.W == a.Wo &&
+         a.Wo + 2 <= 64 && !a.accumulate;
+}
+static int persist_w_tiles(const ConvwArgs& a) { return (a.M / (a.Ho * a.Wo)) * ((a.Ho + 1) / 2); }
 
 // (tco, tkk) of a launch, 0 when unsupported; fold launches take the whole KK in one tile
 static void tile_of(const ConvwArgs& a, int& tco, int& tkk) {
@@ -363,6 +489,13 @@ bool convw_fold_ok(int Cout, int KK, int Arows) {
 
 ConvwPlan convw_plan(const ConvwArgs& a) {
   ConvwPlan p{0, 0};
+  if (is_persist_w(a)) {  // one slab per workgroup (one workgroup per CU)
+    if (!persist_w_ok(a) || a.M <= 0) return p;
+    p.splits = std::min(cu_count(), persist_w_tiles(a));
+    const int64_t mn = 64 * 576;
+    p.slab_floats = (int64_t)p.splits * mn + splitk_tree_floats(p.splits, mn);
+    return p;
+  }
   int tco, tkk;
   tile_of(a, tco, tkk);
   if (!tkk || a.M <= 0) return p;
@@ -382,6 +515,25 @@ ConvwPlan convw_plan(const ConvwArgs& a) {
 
 hipError_t launch_convw(const ConvwArgs& a_in, hipStream_t st) {
   if (a_in.M <= 0) return hipSuccess;
+  if (is_persist_w(a_in)) {
+    if (!persist_w_ok(a_in) || !a_in.slab || !a_in.out || a_in.dybytes == 0 || a_in.xbytes == 0)
+      return hipErrorNotSupported;
+    static bool attr = false;
+    if (!attr) {
+      const hipError_t e = hipFuncSetAttribute((const void*)convhw_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               kHwLds);
+      if (e != hipSuccess) return e;
+      attr = true;
+    }
+    const ConvwPlan p = convw_plan(a_in);
+    ConvwArgs a = a_in;
+    a.splits = p.splits;
+    hipLaunchKernelGGL(convhw_kernel, dim3(p.splits), dim3(256), kHwLds, st, a, persist_w_tiles(a));
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int64_t mn = 64 * 576;
+    return launch_splitk_reduce(a.slab, a.splits, mn, a.out, 1, 0, 1.f, st, a.slab + (int64_t)a.splits * mn);
+  }
   ConvwArgs a0 = a_in;
   if (!a0.fold) a0.Arows = a0.Cout;
   int tco, tkk;

@@ -860,7 +860,8 @@ class _ConvFn(torch.autograd.Function):
         def miopen():
             return F.conv2d(x, weight, stride=stride, padding=pad)
 
-        if fp8 and cin % 128 == 0 and _fp8_ok(k * k * cin, cout):
+        ho_, wo_ = (h + 2 * pad - k) // stride + 1, (w + 2 * pad - k) // stride + 1
+        if fp8 and cin % 128 == 0 and _fp8_ok(k * k * cin, cout) and n * ho_ * wo_ >= 128:  # (kernel contract)
             w2 = weight.permute(0, 2, 3, 1).reshape(cout, k * k * cin)
             y = _igemm_fp8(x, w2 if w2.is_contiguous() else w2.contiguous(), k, stride, pad, scaler=f8[0],
                            pre=_take_q8(mod, x), mod=mod, bn=_bn_consumer(mod))
@@ -921,7 +922,7 @@ class _ConvFn(torch.autograd.Function):
                 return conv_bwd(dy, x, weight, *args, [True, False, False])[0]
 
             if stride == 1 and _igemm_ok(cout, cin) and 2 * pad == k - 1 and ctx.fp8 and cout % 128 == 0 \
-                    and _fp8_ok(k * k * cout, cin) and _at.enabled("PSD_FP8_DGRAD"):
+                    and _fp8_ok(k * k * cout, cin) and n * h * w >= 128 and _at.enabled("PSD_FP8_DGRAD"):
                 # fp8 bwd-data: e5m2 dY gathered by the implicit GEMM, e4m3 flipped weights
                 wf = weight.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, k * k * cout).contiguous()
                 got = _take_dq8(ctx.mod, dy) if _mx_on() else None

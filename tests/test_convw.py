@@ -69,11 +69,12 @@ def test_convw_random_bf16(gpu):
     x = torch.randn(8, 64, 56, 56, device=gpu).bfloat16().contiguous(memory_format=torch.channels_last)
     dy = torch.randn(8, 64, 56, 56, device=gpu).bfloat16().contiguous(memory_format=torch.channels_last)
     ref = torch.nn.grad.conv2d_weight(x.float(), (64, 64, 3, 3), dy.float(), padding=1)
-    out = torch.empty(64, 576, device=gpu, dtype=torch.bfloat16)
-    assert native().convw_(dy, x, out, 3, 3, 1, 1)
-    got = out.float().view(64, 3, 3, 64).permute(0, 3, 1, 2)
-    err = (got - ref).norm() / ref.norm()
-    assert err < 4e-3, err
+    for v in range(native().convw_variants(64, 576)):  # incl. the persistent HALO variant (the last)
+        out = torch.empty(64, 576, device=gpu, dtype=torch.bfloat16)
+        assert native().convw_(dy, x, out, 3, 3, 1, 1, variant=v)
+        got = out.float().view(64, 3, 3, 64).permute(0, 3, 1, 2)
+        err = (got - ref).norm() / ref.norm()
+        assert err < 4e-3, (v, err)
 
 
 def test_convw_declines(gpu):
