@@ -81,7 +81,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("shift") = py::none());
   m.def("convn_", &convn_, py::arg("x"), py::arg("w2"), py::arg("out"), py::arg("R"), py::arg("S"), py::arg("stride"),
         py::arg("pad"), py::arg("part") = py::none(), py::arg("shift") = py::none(), py::arg("variant") = -1,
-        py::arg("x2") = py::none(), py::arg("bias") = py::none());
+        py::arg("x2") = py::none(), py::arg("bias") = py::none(), py::arg("no_store") = false,
+        py::arg("apply_ss") = py::none(), py::arg("apply_res") = py::none(), py::arg("apply_mask") = py::none());
   m.def("convn_stats_rows", &convn_stats_rows_, py::arg("M"));
   m.def("convn_part_rows", &convn_part_rows_, py::arg("M"), py::arg("N"), py::arg("variant"), py::arg("Ho"),
         py::arg("Wo"), py::arg("R"));
@@ -110,6 +111,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_elemt_coef", &bn_elemt_coef, py::arg("g"), py::arg("x"), py::arg("coef"));
   m.def("convw_fold_rows", &convw_fold_rows, py::arg("Cout"), py::arg("Cin"));
   m.def("bnfold_dgrad_weights", &bnfold_dgrad_weights, py::arg("w"), py::arg("coef"));
+  m.def("bnfold_rowdot", &bnfold_rowdot, py::arg("P"), py::arg("w"), py::arg("row"));
+  m.def("bn_finalize", &bn_finalize, py::arg("part"), py::arg("rows"), py::arg("M"), py::arg("gamma"),
+        py::arg("beta"), py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"), py::arg("eps"),
+        py::arg("counter") = py::none());
   m.def("bnfold_combine", &bnfold_combine, py::arg("P"), py::arg("w"), py::arg("coef"), py::arg("out"),
         py::arg("accumulate") = false);
   m.def("convw_variants", &convw_variants_, py::arg("Cout"), py::arg("KK"));

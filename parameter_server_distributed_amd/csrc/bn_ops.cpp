@@ -774,6 +774,63 @@ void bnfold_combine(const at::Tensor& P, const at::Tensor& w_in, const at::Tenso
   TORCH_CHECK(e == hipSuccess, "psd bnfold combine: ", hipGetErrorString(e));
 }
 
+// row [2, Cout] (a view into a partials buffer) = (0, sum_i W[c][i] P[c][i]): the sum g y of a BN
+// whose input y = x W^T was never stored (ops/tail.py)
+void bnfold_rowdot(const at::Tensor& P, const at::Tensor& w_in, at::Tensor row) {
+  const c10::DeviceGuard dg(w_in.device());
+  const at::Tensor w = fold_w2d(w_in);
+  const int64_t Cout = w.size(0), Cin = w.size(1);
+  TORCH_CHECK(P.scalar_type() == at::kFloat && P.is_contiguous() && P.dim() == 2 && P.size(1) == Cin &&
+                  P.size(0) >= Cout && P.device() == w.device(),
+              "psd bnfold rowdot: P must be the fp32 convw fold result [rows, Cin]");
+  TORCH_CHECK(row.scalar_type() == at::kFloat && row.is_contiguous() && row.numel() == 2 * Cout &&
+                  row.device() == w.device(),
+              "psd bnfold rowdot: row must be a contiguous fp32 [2, Cout]");
+  hipError_t e = launch_bnfold_rowdot(P.data_ptr<float>(), reinterpret_cast<const uint16_t*>(w.data_ptr()), (int)Cout,
+                                      (int)Cin, row.data_ptr<float>(), stream_of(w));
+  TORCH_CHECK(e == hipSuccess, "psd bnfold rowdot: ", hipGetErrorString(e));
+}
+
+// Training-mode BN statistics from producer partials only (no activation is read): returns
+// {mean, invstd, ss [2C]} and updates the running statistics, as bn_fwd with stats_only.
+std::vector<at::Tensor> bn_finalize(const at::Tensor& part, int64_t rows, int64_t M, const at::Tensor& gamma,
+                                    const at::Tensor& beta, at::Tensor running_mean, at::Tensor running_var,
+                                    double momentum, double eps, c10::optional<at::Tensor> counter) {
+  const c10::DeviceGuard dg(part.device());
+  const int64_t C = running_mean.numel();
+  check_vec(gamma, C, at::kBFloat16, "gamma");
+  check_vec(beta, C, at::kBFloat16, "beta");
+  check_vec(running_mean, C, at::kFloat, "running_mean");
+  check_vec(running_var, C, at::kFloat, "running_var");
+  TORCH_CHECK(C % 8 == 0 && M > 0 && rows > 0 && part.scalar_type() == at::kFloat && part.is_contiguous() &&
+                  part.numel() >= rows * 2 * C && part.device() == running_mean.device(),
+              "psd bn_finalize: part must be fp32 [rows, 2, C]");
+  auto f32 = part.options();
+  at::Tensor mean = at::empty({C}, f32), invstd = at::empty({C}, f32), ss = at::empty({2 * C}, f32);
+  at::Tensor fold = rows > kFoldRows ? at::empty({(int64_t)kFoldRows * 2 * C}, f32) : at::Tensor();
+  BnFwdArgs a{};
+  a.gamma = opt_ptr<const uint16_t>(gamma);
+  a.beta = opt_ptr<const uint16_t>(beta);
+  a.running_mean = running_mean.data_ptr<float>();
+  a.running_var = running_var.data_ptr<float>();
+  a.save_mean = mean.data_ptr<float>();
+  a.save_invstd = invstd.data_ptr<float>();
+  a.ss = ss.data_ptr<float>();
+  a.part = part.data_ptr<float>();
+  a.part_ready = (int32_t)rows;
+  a.fold_ws = fold.defined() ? fold.data_ptr<float>() : nullptr;
+  a.counter = opt_ptr<int64_t>(counter);
+  a.M = M;
+  a.C = (int32_t)C;
+  a.training = true;
+  a.momentum = (float)momentum;
+  a.eps = (float)eps;
+  a.stats_only = true;
+  const hipError_t e = launch_bn_fwd(a, stream_of(part));
+  TORCH_CHECK(e == hipSuccess, "psd bn_finalize: ", hipGetErrorString(e));
+  return {mean, invstd, ss};
+}
+
 at::Tensor bn_elemt_coef(const at::Tensor& g_in, const at::Tensor& x_in, const at::Tensor& coef) {
   const c10::DeviceGuard dg(x_in.device());
   at::Tensor x = nhwc(x_in), g = nhwc(g_in);

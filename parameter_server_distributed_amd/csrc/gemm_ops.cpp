@@ -293,15 +293,18 @@ int64_t convn_x2(ConvnArgs& a, const at::Tensor& x, c10::optional<at::Tensor> x2
 
 int64_t convn_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride,
                int64_t pad, c10::optional<at::Tensor> part, c10::optional<at::Tensor> shift, int64_t variant,
-               c10::optional<at::Tensor> x2, c10::optional<at::Tensor> bias) {
+               c10::optional<at::Tensor> x2, c10::optional<at::Tensor> bias, bool no_store,
+               c10::optional<at::Tensor> apply_ss, c10::optional<at::Tensor> apply_res,
+               c10::optional<at::Tensor> apply_mask) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.scalar_type() == at::kBFloat16 &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast),
               "psd convn: x must be a channels_last bf16 device tensor");
   TORCH_CHECK(w2.is_cuda() && w2.dim() == 2 && w2.scalar_type() == at::kBFloat16 && w2.is_contiguous(),
               "psd convn: w2 must be a contiguous bf16 [Cout, R*S*C] device tensor");
-  TORCH_CHECK(out.is_cuda() && out.dim() == 2 && out.stride(1) == 1 && out.scalar_type() == at::kBFloat16 &&
-                  (reinterpret_cast<uintptr_t>(out.data_ptr()) & 15) == 0,
+  TORCH_CHECK(no_store || (out.is_cuda() && out.dim() == 2 && out.stride(1) == 1 && out.scalar_type() == at::kBFloat16 &&
+                           (reinterpret_cast<uintptr_t>(out.data_ptr()) & 15) == 0),
               "psd convn: out must be a bf16 [M, Cout] device tensor, 16-B aligned");
+  const bool apply = apply_ss.has_value() && apply_ss->defined();
   const int64_t Nb = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
   const int64_t Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
   const int64_t M = Nb * Ho * Wo, Cout = w2.size(0), K1 = R * S * C;
@@ -310,8 +313,23 @@ int64_t convn_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_
   if (C2 < 0) return 0;
   const int64_t K = K1 + C2;
   TORCH_CHECK(w2.size(1) == K, "psd convn: w2 must be [Cout, R*S*C (+ C2)]");
-  TORCH_CHECK(out.size(0) == M && out.size(1) == Cout, "psd convn: out must be [Nb*Ho*Wo, Cout]");
+  TORCH_CHECK(no_store || (out.size(0) == M && out.size(1) == Cout), "psd convn: out must be [Nb*Ho*Wo, Cout]");
   const bool stats = part.has_value() && part->defined();
+  TORCH_CHECK(!no_store || (stats && !apply), "psd convn: no_store is a statistics-only pass");
+  if (apply) {
+    TORCH_CHECK(!stats && apply_ss->scalar_type() == at::kFloat && apply_ss->numel() == 2 * Cout &&
+                    apply_ss->is_contiguous() && apply_ss->device() == x.device(),
+                "psd convn: apply_ss must be fp32 [2 Cout] (no statistics in an apply pass)");
+    TORCH_CHECK(apply_res.has_value() && apply_res->defined() && apply_res->scalar_type() == at::kBFloat16 &&
+                    apply_res->numel() == M * Cout && apply_res->device() == x.device() &&
+                    (apply_res->dim() == 4 ? apply_res->is_contiguous(at::MemoryFormat::ChannelsLast)
+                                           : apply_res->is_contiguous()),
+                "psd convn: apply_res must be a bf16 [M, Cout] (or channels_last) residual");
+    TORCH_CHECK(apply_mask.has_value() && apply_mask->defined() && apply_mask->scalar_type() == at::kByte &&
+                    apply_mask->numel() == M * Cout / 8 && apply_mask->is_contiguous(),
+                "psd convn: apply_mask must be uint8 [M * Cout / 8]");
+    TORCH_CHECK(out.stride(0) == Cout, "psd convn: the apply pass writes a dense [M, Cout] output");
+  }
   if (stats) {
     TORCH_CHECK(shift.has_value() && shift->defined() && shift->numel() == Cout && shift->scalar_type() == at::kFloat &&
                     shift->is_contiguous() && shift->device() == x.device(),
@@ -325,8 +343,8 @@ int64_t convn_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_
   }
   const int64_t xbytes = x.numel() * 2, wbytes = w2.numel() * 2;
   if ((C & (C - 1)) != 0 || C < 64 || xbytes > 0xFFFFFF00ll || wbytes >= ((int64_t)1 << 32) ||
-      M >= ((int64_t)1 << 31) - 256 || convn_tile_n((int)Cout) == 0 || out.stride(0) % 8 != 0 || Ho <= 0 || Wo <= 0 ||
-      variant >= convn_variants((int)Cout))
+      M >= ((int64_t)1 << 31) - 256 || convn_tile_n((int)Cout) == 0 || (!no_store && out.stride(0) % 8 != 0) ||
+      Ho <= 0 || Wo <= 0 || variant >= convn_variants((int)Cout))
     return 0;
   int logc = 0;
   while ((1 << logc) < C) ++logc;
@@ -334,9 +352,15 @@ int64_t convn_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_
   a.K1 = (int)K1;
   a.x = x.data_ptr();
   a.w = w2.data_ptr();
-  a.y = out.data_ptr();
+  a.y = no_store ? nullptr : out.data_ptr();
   a.part = stats ? part->data_ptr<float>() : nullptr;
   a.shift = stats ? shift->data_ptr<float>() : nullptr;
+  if (apply) {
+    a.bwd = 8;
+    a.bss = apply_ss->data_ptr<float>();
+    a.ares = reinterpret_cast<const uint16_t*>(apply_res->data_ptr());
+    a.amask = apply_mask->data_ptr<uint8_t>();
+  }
   a.xbytes = (uint32_t)xbytes;
   a.wbytes = (uint32_t)wbytes;
   a.M = (int)M;
@@ -351,7 +375,7 @@ int64_t convn_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_
   a.S = (int)S;
   a.stride = (int)stride;
   a.pad = (int)pad;
-  a.ldc = (int)out.stride(0);
+  a.ldc = no_store ? (int)Cout : (int)out.stride(0);
   a.variant = (int)variant;
   const hipError_t e = launch_convn(a, c10::hip::getCurrentHIPStream(x.device().index()).stream());
   if (e == hipErrorNotSupported) return 0;
@@ -364,7 +388,7 @@ int64_t convn_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_
 // (kernels/convn.hip bwd modes): out = g = mask (conv(dy, w2) [+ dr]); part gets the partials.
 // Returns the partial rows written, 0 when the kernel declines (nothing launched).
 int64_t convn_bwd_(const at::Tensor& dy, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride,
-                   int64_t pad, at::Tensor part, int64_t variant, int64_t mode, const at::Tensor& bx,
+                   int64_t pad, at::Tensor part, int64_t variant, int64_t mode, c10::optional<at::Tensor> bx,
                    const at::Tensor& bmean, c10::optional<at::Tensor> bss, c10::optional<at::Tensor> bdr,
                    c10::optional<at::Tensor> bmbits, c10::optional<at::Tensor> x2, c10::optional<at::Tensor> bias,
                    c10::optional<at::Tensor> bxd, c10::optional<at::Tensor> bmean_d, c10::optional<at::Tensor> part_d) {
@@ -392,7 +416,9 @@ int64_t convn_bwd_(const at::Tensor& dy, const at::Tensor& w2, at::Tensor out, i
                 "psd convn_bwd: ", what, " must be a contiguous bf16 [M, N] (or channels_last) tensor");
     (void)u;
   };
-  like_out(bx, "bx");
+  const bool has_bx = bx.has_value() && bx->defined();
+  TORCH_CHECK(has_bx || mode == 2 || mode == 5, "psd convn_bwd: only modes 2 and 5 run without the BN input bx");
+  if (has_bx) like_out(*bx, "bx");
   TORCH_CHECK(bmean.scalar_type() == at::kFloat && bmean.numel() == N && bmean.is_contiguous(), "psd convn_bwd: bmean");
   TORCH_CHECK(part.scalar_type() == at::kFloat && part.is_contiguous() &&
                   part.numel() >= (int64_t)std::max(convn_stats_rows((int)M),
@@ -456,7 +482,7 @@ int64_t convn_bwd_(const at::Tensor& dy, const at::Tensor& w2, at::Tensor out, i
   a.ldc = (int)N;
   a.variant = (int)variant;
   a.bwd = (int)mode;
-  a.bx = reinterpret_cast<const uint16_t*>(bx.data_ptr());
+  a.bx = has_bx ? reinterpret_cast<const uint16_t*>(bx->data_ptr()) : nullptr;
   a.bmean = bmean.data_ptr<float>();
   a.bss = mode == 1 ? bss->data_ptr<float>() : nullptr;
   a.bdr = mode >= 2 ? reinterpret_cast<const uint16_t*>(bdr->data_ptr()) : nullptr;

@@ -15,8 +15,9 @@
 // Backward:            reduce (sum dy', sum dy'(x-mean); writes dr = dy' for the residual branch)
 //                      -> finalize (dgamma/dbeta straight into the parameter-gradient buffers,
 //                      3 coefficients) -> elementwise dx = A dy' + B x + C.
-// Block partials are combined by a separate finalize launch (no cross-workgroup hand-off inside a
-// launch: correct for any workgroup->XCD placement, cdna_hip_programming.md G16).
+// Block partials are combined by a separate finalize launch; a producer's many partial rows (one per
+// convolution output tile) are summed and finalized in one ticketed launch (bn_fold_finalize_kernel:
+// the agent-scope release / acquire hand-off, correct for any workgroup->XCD placement).
 #include <hip/hip_fp8.h>
 #include "common.h"
 #include "mx_common.h"
@@ -24,6 +25,7 @@
 #include "pool_gather.h"
 
 #include <cstdlib>
+#include <mutex>
 
 namespace psd {
 
@@ -165,59 +167,51 @@ __global__ __launch_bounds__(256) void bn_fwd_reduce_kernel(const uint16_t* __re
   block_partials(m, C, a, b, part);
 }
 
-// Fold many partial rows (a producer epilogue writes one per output tile: ~50k rows for a b1024
-// layer1 convolution) into F rows before the finalize, which would otherwise sum them with 8
-// blocks: out[f][c] = sum of the rows r = f (mod F). Block = 8 row groups x 32 column quads,
-// independent 16-byte loads, rows combined in LDS in a fixed order (deterministic).
-__global__ __launch_bounds__(256) void bn_part_fold_kernel(const float* __restrict__ in, int nblk, int C2,
-                                                           float* __restrict__ out, int F) {
-  const int cq = threadIdx.x & 31, rg = threadIdx.x >> 5;
-  const int c = (blockIdx.y * 32 + cq) * 4;
-  const int f = blockIdx.x;
-  f32x4 s = {0.f, 0.f, 0.f, 0.f};
-  if (c < C2)
-    for (int r = f + F * rg; r < nblk; r += F * 8) s += *reinterpret_cast<const f32x4*>(in + (int64_t)r * C2 + c);
-  __shared__ f32x4 red[8][32];
-  red[rg][cq] = s;
-  __syncthreads();
-  if (rg == 0 && c < C2) {
-#pragma unroll
-    for (int k = 1; k < 8; ++k) s += red[k][cq];
-    *reinterpret_cast<f32x4*>(out + (int64_t)f * C2 + c) = s;
+// Forward finalize of channel c from its totals s = sum (x - k), q = sum (x - k)^2 (k = shift_k[c]):
+// saved mean / invstd, scale / shift, running statistics. shift_k aliases running_mean (read, then
+// updated by the same lane): no __restrict__ on either.
+struct FinFwd {
+  int64_t M;
+  int C;
+  const float* shift_k;
+  const uint16_t* gamma;
+  const uint16_t* beta;
+  float* running_mean;
+  float* running_var;
+  float momentum, eps;
+  float* save_mean;
+  float* save_invstd;
+  float* ss;
+  int64_t* counter;
+};
+
+__device__ __forceinline__ void fin_fwd(const FinFwd& f, int c, double s, double q) {
+  const double ms = s / (double)f.M;
+  double var = q / (double)f.M - ms * ms;
+  if (var < 0) var = 0;
+  const float k = f.shift_k ? f.shift_k[c] : 0.f;
+  const float mean = (float)(ms + (double)k);
+  const float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
+  f.save_mean[c] = mean;
+  f.save_invstd[c] = invstd;
+  const float g = f.gamma ? bf16_to_f32(f.gamma[c]) : 1.f;
+  const float bt = f.beta ? bf16_to_f32(f.beta[c]) : 0.f;
+  const float scale = g * invstd;
+  f.ss[c] = scale;
+  f.ss[f.C + c] = bt - mean * scale;
+  if (f.running_mean) f.running_mean[c] = (1.f - f.momentum) * f.running_mean[c] + f.momentum * mean;
+  if (f.running_var) {
+    const double unbiased = f.M > 1 ? var * (double)f.M / (double)(f.M - 1) : var;
+    f.running_var[c] = (1.f - f.momentum) * f.running_var[c] + f.momentum * (float)unbiased;
   }
 }
 
-// shift_k aliases running_mean (read, then updated by the same lane): no __restrict__ on either.
-__global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const float* __restrict__ part, int nblk, int64_t M, int C,
-                                                              const float* shift_k,
-                                                              const uint16_t* __restrict__ gamma,
-                                                              const uint16_t* __restrict__ beta, float* running_mean,
-                                                              float* running_var, float momentum, float eps,
-                                                              float* __restrict__ save_mean,
-                                                              float* __restrict__ save_invstd, float* __restrict__ ss,
-                                                              int64_t* counter) {
+__global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const float* __restrict__ part, int nblk, FinFwd f) {
   const int c = blockIdx.x * kFinCh + threadIdx.x;
-  if (blockIdx.x == 0 && threadIdx.x == 0 && counter) *counter += 1;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && f.counter) *f.counter += 1;
   double s, q;
-  if (!sum_partials(part, nblk, C, blockIdx.x * kFinCh, s, q)) return;
-  const double ms = s / (double)M;
-  double var = q / (double)M - ms * ms;
-  if (var < 0) var = 0;
-  const float k = shift_k ? shift_k[c] : 0.f;
-  const float mean = (float)(ms + (double)k);
-  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
-  save_mean[c] = mean;
-  save_invstd[c] = invstd;
-  const float g = gamma ? bf16_to_f32(gamma[c]) : 1.f;
-  const float bt = beta ? bf16_to_f32(beta[c]) : 0.f;
-  const float scale = g * invstd;
-  ss[c] = scale;
-  ss[C + c] = bt - mean * scale;
-  if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
-  if (running_var) {
-    const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
-    running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unbiased;
-  }
+  if (!sum_partials(part, nblk, f.C, blockIdx.x * kFinCh, s, q)) return;
+  fin_fwd(f, c, s, q);
 }
 
 // MASK_OUT: also write the ReLU mask as one bit per element (one byte per 8-channel vector, so a
@@ -445,25 +439,142 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
   }
 }
 
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, int64_t M, int C,
-                                                              const uint16_t* __restrict__ gamma,
-                                                              const float* __restrict__ mean,
-                                                              const float* __restrict__ invstd,
-                                                              uint16_t* __restrict__ dgamma, uint16_t* __restrict__ dbeta,
-                                                              float* __restrict__ coef) {
+// Backward finalize of channel c from s1 = sum g, s2 = sum g (x - mean): dgamma / dbeta straight
+// into the parameter-gradient buffers and the coefficients of dx = A g + B x + C.
+struct FinBwd {
+  int64_t M;
+  int C;
+  const uint16_t* gamma;
+  const float* mean;
+  const float* invstd;
+  uint16_t* dgamma;
+  uint16_t* dbeta;
+  float* coef;
+};
+
+__device__ __forceinline__ void fin_bwd(const FinBwd& f, int c, double s1, double s2) {
+  const float is = f.invstd[c];
+  if (f.dgamma) f.dgamma[c] = f32_to_bf16((float)(s2 * is));
+  if (f.dbeta) f.dbeta[c] = f32_to_bf16((float)s1);
+  const float g = f.gamma ? bf16_to_f32(f.gamma[c]) : 1.f;
+  const float k1 = g * is;
+  const float k3 = (float)(s2 * (double)is * (double)is / (double)f.M);
+  const float k2 = (float)(s1 / (double)f.M);
+  f.coef[c] = k1;                                       // A
+  f.coef[f.C + c] = -k1 * k3;                           // B
+  f.coef[2 * f.C + c] = -k1 * k2 + k1 * k3 * f.mean[c];  // C
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, FinBwd f) {
   const int c = blockIdx.x * kFinCh + threadIdx.x;
   double s1, s2;
-  if (!sum_partials(part, nblk, C, blockIdx.x * kFinCh, s1, s2)) return;
-  const float is = invstd[c];
-  if (dgamma) dgamma[c] = f32_to_bf16((float)(s2 * is));
-  if (dbeta) dbeta[c] = f32_to_bf16((float)s1);
-  const float g = gamma ? bf16_to_f32(gamma[c]) : 1.f;
-  const float k1 = g * is;
-  const float k3 = (float)(s2 * (double)is * (double)is / (double)M);
-  const float k2 = (float)(s1 / (double)M);
-  coef[c] = k1;                                 // A
-  coef[C + c] = -k1 * k3;                       // B
-  coef[2 * C + c] = -k1 * k2 + k1 * k3 * mean[c];  // C
+  if (!sum_partials(part, nblk, f.C, blockIdx.x * kFinCh, s1, s2)) return;
+  fin_bwd(f, c, s1, s2);
+}
+
+// Many producer partial rows (a convolution epilogue writes one per output tile: ~50k for a b1024
+// layer1 convolution) summed and finalized in ONE launch: block (f, cg) sums rows [f * chunk, ..)
+// of the 32 channels of column group cg into a slab row ws[cg][f], then draws a ticket; the block
+// that draws the last one sums the slab rows in a fixed order (deterministic) and runs the
+// finalize. The hand-off is cdna_hip_programming.md's in-launch split-K recipe: writer stores ->
+// vmcnt(0) -> barrier -> one agent-scope release -> vmcnt(0) -> relaxed agent-scope ticket; the
+// reducer one agent-scope acquire before its loads. Replaces part_fold + finalize (two launches,
+// ~12 + ~11 us each, 64 + 105 of them per ResNet-50 step).
+constexpr int kFfCh = 32;    // channels per column group (64 floats per partial row: s and q)
+constexpr int kFfMaxF = 256;  // slab rows per column group
+template <bool BWD>
+__global__ __launch_bounds__(256) void bn_fold_finalize_kernel(const float* __restrict__ part, int rows, int chunk,
+                                                               float* __restrict__ ws, unsigned int* __restrict__ cnt,
+                                                               FinFwd ff, FinBwd fb) {
+  const int C = BWD ? fb.C : ff.C;
+  const int f = blockIdx.x, cg = blockIdx.y, F = gridDim.x;
+  const int col = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = cg * kFfCh + (col & 31);
+  const bool cok = c < C;
+  const int64_t coff = (int64_t)(col >> 5) * C + c;
+  const int r0 = f * chunk, r1 = min(rows, r0 + chunk);
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (cok) {
+    int r = r0 + rg;
+    for (; r + 12 < r1; r += 16) {  // 4 independent loads in flight per lane
+      a0 += part[(int64_t)r * 2 * C + coff];
+      a1 += part[(int64_t)(r + 4) * 2 * C + coff];
+      a2 += part[(int64_t)(r + 8) * 2 * C + coff];
+      a3 += part[(int64_t)(r + 12) * 2 * C + coff];
+    }
+    for (; r < r1; r += 4) a0 += part[(int64_t)r * 2 * C + coff];
+  }
+  __shared__ float red[4][64];
+  __shared__ double tot[4][64];
+  __shared__ unsigned int ticket;
+  red[rg][col] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  float* slab = ws + (int64_t)cg * kFfMaxF * 64;
+  if (rg == 0) slab[f * 64 + col] = ((red[0][col] + red[1][col]) + red[2][col]) + red[3][col];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ticket = __hip_atomic_fetch_add(&cnt[cg], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (ticket != (unsigned int)(F - 1)) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(&cnt[cg], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // reusable by the next launch
+  }
+  __syncthreads();
+  double t = 0.0;
+  for (int k = rg; k < F; k += 4) t += (double)slab[k * 64 + col];
+  tot[rg][col] = t;
+  __syncthreads();
+  if (threadIdx.x < kFfCh && cok) {
+    const int j = threadIdx.x;
+    const double s = ((tot[0][j] + tot[1][j]) + tot[2][j]) + tot[3][j];
+    const double q = ((tot[0][32 + j] + tot[1][32 + j]) + tot[2][32 + j]) + tot[3][32 + j];
+    if (BWD) fin_bwd(fb, c, s, q);
+    else fin_fwd(ff, c, s, q);
+  }
+  if (!BWD && cg == 0 && threadIdx.x == 0 && ff.counter) *ff.counter += 1;
+}
+
+// per-device ticket counters of bn_fold_finalize_kernel: zero between launches (the reducing block
+// resets its own); consecutive launches take disjoint slot ranges of the ring
+static unsigned int* ff_counters(int need) {
+  static std::mutex mu;
+  const std::lock_guard<std::mutex> lock(mu);
+  constexpr int kSlots = 1 << 16;
+  static unsigned int* base[16] = {};
+  static int next[16] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
+  if (!base[dev]) {
+    if (hipMalloc(&base[dev], kSlots * sizeof(unsigned int)) != hipSuccess) return nullptr;
+    if (hipMemset(base[dev], 0, kSlots * sizeof(unsigned int)) != hipSuccess) return nullptr;
+  }
+  if (next[dev] + need > kSlots) next[dev] = 0;
+  unsigned int* p = base[dev] + next[dev];
+  next[dev] += (need + 63) & ~63;
+  return p;
+}
+
+// fold + finalize of `rows` partial rows in one launch (ws: >= kFfMaxF * 64 * column groups floats)
+template <bool BWD>
+static hipError_t fold_finalize(const float* part, int rows, float* ws, const FinFwd& ff, const FinBwd& fb,
+                                hipStream_t st) {
+  const int C = BWD ? fb.C : ff.C;
+  const int ncg = (C + kFfCh - 1) / kFfCh;
+  int F = (rows + 63) / 64;  // >= 64 rows per block
+  F = F < 1 ? 1 : (F > kFfMaxF ? kFfMaxF : F);
+  const int chunk = (rows + F - 1) / F;
+  F = (rows + chunk - 1) / chunk;
+  unsigned int* cnt = ff_counters(ncg);
+  if (!cnt) return hipErrorOutOfMemory;
+  hipLaunchKernelGGL((bn_fold_finalize_kernel<BWD>), dim3(F, ncg), dim3(256), 0, st, part, rows, chunk, ws, cnt, ff,
+                     fb);
+  return hipGetLastError();
 }
 
 // MODE 0: dy' = dy; MODE 1: dy' = dy * (y > 0); MODE 2: dy' = g (already masked, = dr);
@@ -778,21 +889,20 @@ hipError_t launch_bn_fwd(const BnFwdArgs& a, hipStream_t st) {
   int gx, gy;
   reduce_grid(a.M, a.C, gx, gy);
   if (a.training) {
-    const float* part = a.part;
-    if (a.part_ready > kFoldRows && a.fold_ws) {  // many producer partial rows (convolution epilogue): fold first
-      hipLaunchKernelGGL(bn_part_fold_kernel, dim3(kFoldRows, (2 * a.C + 127) / 128), dim3(256), 0, st, a.part,
-                         a.part_ready, 2 * a.C, a.fold_ws, kFoldRows);
-      part = a.fold_ws;
-      gx = kFoldRows;
-    } else if (a.part_ready > 0) {  // statistics already reduced by the producing kernel (stem conv epilogue)
-      gx = a.part_ready;
+    const FinFwd ff{a.M, a.C, a.running_mean, a.gamma, a.beta, a.running_mean, a.running_var, a.momentum, a.eps,
+                    a.save_mean, a.save_invstd, a.ss, a.counter};
+    if (a.part_ready > kFoldRows && a.fold_ws) {  // many producer partial rows (convolution epilogue)
+      const hipError_t e = fold_finalize<false>(a.part, a.part_ready, a.fold_ws, ff, FinBwd{}, st);
+      if (e != hipSuccess) return e;
     } else {
-      hipLaunchKernelGGL(bn_fwd_reduce_kernel, dim3(gx, gy), dim3(256), 0, st, a.x, a.M, a.C, a.running_mean, a.part,
-                         bn_reverse());
+      if (a.part_ready > 0) {  // statistics already reduced by the producing kernel (stem conv epilogue)
+        gx = a.part_ready;
+      } else {
+        hipLaunchKernelGGL(bn_fwd_reduce_kernel, dim3(gx, gy), dim3(256), 0, st, a.x, a.M, a.C, a.running_mean,
+                           a.part, bn_reverse());
+      }
+      hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((a.C + kFinCh - 1) / kFinCh), dim3(256), 0, st, a.part, gx, ff);
     }
-    hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((a.C + kFinCh - 1) / kFinCh), dim3(256), 0, st, part, gx, a.M, a.C,
-                       a.running_mean, a.gamma, a.beta, a.running_mean, a.running_var, a.momentum, a.eps, a.save_mean,
-                       a.save_invstd, a.ss, a.counter);
     if (a.stats_only) return hipGetLastError();
   }
   if (a.pool_arg) {  // stem: y is the pooled output, the BN output is never written
@@ -881,11 +991,22 @@ static hipError_t launch_bn_bwd_pool(const BnBwdArgs& a, hipStream_t st) {
   const int gx = bn_pool_reduce_blocks(a.N, a.H, a.W, a.C), gy = 1;  // the caller sized part for this
   hipLaunchKernelGGL(bn_bwd_reduce_pool_kernel, dim3(gx, gy), dim3(256), 0, st, a.gpool, a.gpool2, a.pool_arg, a.ss, a.x,
                      a.save_mean, a.N, a.H, a.W, a.C, a.part, dwo, dho);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((a.C + kFinCh - 1) / kFinCh), dim3(256), 0, st, a.part, gx, a.M, a.C,
-                     a.gamma, a.save_mean, a.save_invstd, a.dgamma, a.dbeta, a.coef);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((a.C + kFinCh - 1) / kFinCh), dim3(256), 0, st, a.part, gx,
+                     FinBwd{a.M, a.C, a.gamma, a.save_mean, a.save_invstd, a.dgamma, a.dbeta, a.coef});
   const int g = elem_grid(total, a.C);
   hipLaunchKernelGGL(bn_bwd_elemt_pool_kernel, dim3(g), dim3(256), 0, st, a.gpool, a.gpool2, a.pool_arg, a.ss, a.x,
                      a.coef, a.dx, a.N, a.H, a.W, a.C, dc8, dwo, dho);
+  return hipGetLastError();
+}
+
+// finalize from `rows` producer-reduced partial rows (more than kFoldRows: summed and finalized in
+// one ticketed launch, fold_ws its slab workspace)
+static hipError_t finalize_pre(const float* part, int rows, float* fold_ws, int64_t M, int C, const uint16_t* gamma,
+                               const float* mean, const float* invstd, uint16_t* dgamma, uint16_t* dbeta, float* coef,
+                               hipStream_t st) {
+  const FinBwd fb{M, C, gamma, mean, invstd, dgamma, dbeta, coef};
+  if (rows > kFoldRows) return fold_finalize<true>(part, rows, fold_ws, FinFwd{}, fb, st);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(256), 0, st, part, rows, fb);
   return hipGetLastError();
 }
 
@@ -897,17 +1018,9 @@ hipError_t launch_bn_bwd_pre(const uint16_t* g, const uint16_t* x, const uint16_
                              uint8_t* dqmx) {
   if (M <= 0) return hipSuccess;
   if (C % 8 != 0 || rows <= 0) return hipErrorInvalidValue;
-  const float* p = part;
-  int nblk = rows;
-  if (rows > kFoldRows) {
-    if (!fold_ws) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(bn_part_fold_kernel, dim3(kFoldRows, (2 * C + 127) / 128), dim3(256), 0, st, part, rows, 2 * C,
-                       fold_ws, kFoldRows);
-    p = fold_ws;
-    nblk = kFoldRows;
-  }
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(256), 0, st, p, nblk, M, C, gamma,
-                     mean, invstd, dgamma, dbeta, coef);
+  if (rows > kFoldRows && !fold_ws) return hipErrorInvalidValue;
+  const hipError_t fe = finalize_pre(part, rows, fold_ws, M, C, gamma, mean, invstd, dgamma, dbeta, coef, st);
+  if (fe != hipSuccess) return fe;
   if (!dx) return hipGetLastError();  // coefficients only (BN-backward fold)
   const int64_t nvec = M * (C / 8);
   if (dq) {
@@ -933,21 +1046,7 @@ hipError_t launch_bn_elemt_coef(const uint16_t* g, const uint16_t* x, const floa
   return hipGetLastError();
 }
 
-// finalize from `rows` producer-reduced partial rows (folded to kFoldRows first when there are more)
-static void finalize_pre(const float* part, int rows, float* fold_ws, int64_t M, int C, const uint16_t* gamma,
-                         const float* mean, const float* invstd, uint16_t* dgamma, uint16_t* dbeta, float* coef,
-                         hipStream_t st) {
-  const float* p = part;
-  int nblk = rows;
-  if (rows > kFoldRows) {
-    hipLaunchKernelGGL(bn_part_fold_kernel, dim3(kFoldRows, (2 * C + 127) / 128), dim3(256), 0, st, part, rows, 2 * C,
-                       fold_ws, kFoldRows);
-    p = fold_ws;
-    nblk = kFoldRows;
-  }
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(256), 0, st, p, nblk, M, C, gamma,
-                     mean, invstd, dgamma, dbeta, coef);
-}
+
 
 // Dual tail relu(bn(x) + bnd(xd)) backward from partials reduced in the consumer convolution's
 // bwd-data epilogue (kernels/convn.hip bwd mode 3): finalize both BNs, then one elementwise pass (dx
@@ -955,9 +1054,12 @@ static void finalize_pre(const float* part, int rows, float* fold_ws, int64_t M,
 hipError_t launch_bn_bwd_dual_pre(const BnDualPreArgs& a, hipStream_t st) {
   if (a.M <= 0) return hipSuccess;
   if (a.C % 8 != 0 || a.rows <= 0 || (a.rows > kFoldRows && (!a.fold_ws || !a.fold_ws_d))) return hipErrorInvalidValue;
-  finalize_pre(a.part, a.rows, a.fold_ws, a.M, a.C, a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta, a.coef, st);
-  finalize_pre(a.part_d, a.rows, a.fold_ws_d, a.M, a.C, a.gamma_d, a.mean_d, a.invstd_d, a.dgamma_d, a.dbeta_d,
-               a.coef_d, st);
+  hipError_t fe = finalize_pre(a.part, a.rows, a.fold_ws, a.M, a.C, a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta,
+                               a.coef, st);
+  if (fe == hipSuccess)
+    fe = finalize_pre(a.part_d, a.rows, a.fold_ws_d, a.M, a.C, a.gamma_d, a.mean_d, a.invstd_d, a.dgamma_d, a.dbeta_d,
+                      a.coef_d, st);
+  if (fe != hipSuccess) return fe;
   const int64_t nvec = a.M * (a.C / 8);
   if (a.dx)
     hipLaunchKernelGGL(bn_bwd_elemt_dual_kernel<true>, dim3(elem_grid(nvec, a.C)), dim3(256), 0, st, a.g, a.x, a.coef,
@@ -984,10 +1086,10 @@ hipError_t launch_bn_bwd(const BnBwdArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<kMaskBits, true, true>), dim3(gx, gy), dim3(256), 0, st, a.dy, a.dy2, a.y,
                        a.mbits, a.ss, a.x, a.save_mean, a.dr, a.M, a.C, a.part, bn_reverse(), a.xd, a.mean_d, a.part_d);
     const dim3 fg((a.C + kFinCh - 1) / kFinCh);
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, fg, dim3(256), 0, st, a.part, gx, a.M, a.C, a.gamma, a.save_mean,
-                       a.save_invstd, a.dgamma, a.dbeta, a.coef);
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, fg, dim3(256), 0, st, a.part_d, gx, a.M, a.C, a.gamma_d, a.mean_d,
-                       a.invstd_d, a.dgamma_d, a.dbeta_d, a.coef_d);
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, fg, dim3(256), 0, st, a.part, gx,
+                       FinBwd{a.M, a.C, a.gamma, a.save_mean, a.save_invstd, a.dgamma, a.dbeta, a.coef});
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, fg, dim3(256), 0, st, a.part_d, gx,
+                       FinBwd{a.M, a.C, a.gamma_d, a.mean_d, a.invstd_d, a.dgamma_d, a.dbeta_d, a.coef_d});
     const int64_t nvec = a.M * (a.C / 8);
     if (a.dx)
       hipLaunchKernelGGL(bn_bwd_elemt_dual_kernel<true>, dim3(elem_grid(nvec, a.C)), dim3(256), 0, st, a.dr, a.x, a.coef,
@@ -1011,8 +1113,8 @@ hipError_t launch_bn_bwd(const BnBwdArgs& a, hipStream_t st) {
 #undef PSD_RED
   if (a.reduce_only) return hipGetLastError();
   if (a.dq && (!a.dqmx || a.C % 32 != 0)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((a.C + kFinCh - 1) / kFinCh), dim3(256), 0, st, a.part, gx, a.M, a.C, a.gamma,
-                     a.save_mean, a.save_invstd, a.dgamma, a.dbeta, a.coef);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((a.C + kFinCh - 1) / kFinCh), dim3(256), 0, st, a.part, gx,
+                     FinBwd{a.M, a.C, a.gamma, a.save_mean, a.save_invstd, a.dgamma, a.dbeta, a.coef});
   if (a.coef_only) return hipGetLastError();  // coefficients for the consumer's BN-backward fold
   const int64_t nvec = a.M * (a.C / 8);
   const int g = elem_grid(nvec, a.C);

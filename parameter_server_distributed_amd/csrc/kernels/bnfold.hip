@@ -75,6 +75,37 @@ __global__ __launch_bounds__(256) void bnfold_combine_kernel(const float* __rest
   }
 }
 
+// sum_m g[m][c] y[m][c] for y = x W^T that was never stored (ops/tail.py): with P[:Cout] = g^T x
+// from the fold wgrad, sum_m g y = sum_i W[c][i] P[c][i]. One wave per output channel, the row's
+// bf16 weights and fp32 P entries in 8-wide lane chunks; writes the partial row (0, that sum) that
+// completes the BN-backward partials of an epilogue that ran without the BN input (convn bwd modes
+// 2 / 5 with bx null: sum g, -mean sum g).
+__global__ __launch_bounds__(256) void bnfold_rowdot_kernel(const float* __restrict__ P, const uint16_t* __restrict__ W,
+                                                            int Cout, int Wd, float* __restrict__ row) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= Cout) return;
+  float acc = 0.f;
+  for (int i = lane * 8; i < Wd; i += 64 * 8) {
+    float w[8], p[8];
+    load8_bf16(W + (int64_t)c * Wd + i, w);
+    load8_f32(P + (int64_t)c * Wd + i, p);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc = fmaf(w[e], p[e], acc);
+  }
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  if (lane == 0) {
+    row[c] = 0.f;
+    row[Cout + c] = acc;
+  }
+}
+
+hipError_t launch_bnfold_rowdot(const float* P, const uint16_t* W, int Cout, int Wd, float* row, hipStream_t st) {
+  if (Cout <= 0 || Wd <= 0 || Wd % 8 != 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bnfold_rowdot_kernel, dim3((Cout + 3) / 4), dim3(256), 0, st, P, W, Cout, Wd, row);
+  return hipGetLastError();
+}
+
 hipError_t launch_bnfold_prep(const uint16_t* W, const float* coef, int Cout, int Wd, uint16_t* w2, int ldw,
                               uint16_t* bw, float* bvec, hipStream_t st) {
   if (Cout <= 0 || Wd <= 0 || ldw < Cout) return hipErrorInvalidValue;

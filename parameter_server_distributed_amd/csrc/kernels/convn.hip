@@ -164,19 +164,95 @@ constexpr int halo_win_bytes(int bm) { return (bm + 2 * 64 + 8) * 128; }
 
 }  // namespace
 
+// Per-lane running sums of an epilogue's reductions: STATS in the C layout (this lane's column of
+// each 16-column block, summed over its 16 rows), BWD over this lane's 8 channels. A one-tile kernel
+// flushes them per tile; the persistent kernel keeps them across all its tiles and flushes once
+// (one partial row per wave row per workgroup instead of per tile: no per-tile cross-lane reduction
+// or store, and few enough rows that the BN finalize needs no fold pass).
+template <int JN>
+struct EpiSums {
+  float s1[JN], s2[JN];
+  float ga[8], gb[8], gd[8];
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int j = 0; j < JN; ++j) s1[j] = s2[j] = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ga[e] = gb[e] = gd[e] = 0.f;
+  }
+};
+
+// Cross-lane reduction of the sums and the store of partial row `prow` (part / part_d layout
+// [rows][2][N]).
+template <int WNT, bool STATS, int BWD>
+__device__ __forceinline__ void convn_flush(const ConvnArgs& a, EpiSums<WNT / 16>& es, int64_t prow, int wc, int lane,
+                                            int n0) {
+  constexpr int JN = WNT / 16;
+  const int cl = lane & 15;
+  if constexpr (STATS) {
+#pragma unroll
+    for (int j = 0; j < JN; ++j) {
+      float s1 = es.s1[j], s2 = es.s2[j];
+      s1 += xor16(s1, lane);
+      s2 += xor16(s2, lane);
+      s1 += xor32(s1, lane);
+      s2 += xor32(s2, lane);
+      if (lane < 16) {
+        float* pr = a.part + prow * 2 * a.N;
+        const int col = n0 + wc * WNT + j * 16 + cl;
+        pr[col] = s1;
+        pr[a.N + col] = s2;
+      }
+    }
+  }
+  if constexpr (BWD >= 1 && BWD <= 5) {
+    constexpr int CPR = WNT * 2 / 16;  // 16-byte chunks per staged row
+    const int my_col = n0 + wc * WNT + (lane % CPR) * 8;
+    // lanes sharing this lane's channels: lane % CPR equal -> rotate-sum within the 16-lane row,
+    // then across rows
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if constexpr (CPR == 4) {
+        es.ga[e] += ror_row<4>(es.ga[e]);
+        es.gb[e] += ror_row<4>(es.gb[e]);
+      }
+      es.ga[e] += ror_row<8>(es.ga[e]);
+      es.gb[e] += ror_row<8>(es.gb[e]);
+      es.ga[e] += xor16(es.ga[e], lane);
+      es.gb[e] += xor16(es.gb[e], lane);
+      es.ga[e] += xor32(es.ga[e], lane);
+      es.gb[e] += xor32(es.gb[e], lane);
+      if constexpr (BWD == 3) {
+        if constexpr (CPR == 4) es.gd[e] += ror_row<4>(es.gd[e]);
+        es.gd[e] += ror_row<8>(es.gd[e]);
+        es.gd[e] += xor16(es.gd[e], lane);
+        es.gd[e] += xor32(es.gd[e], lane);
+      }
+    }
+    if (lane < CPR) {
+      float* pr = a.part + prow * 2 * a.N;
+      store8_f32(pr + my_col, es.ga);
+      store8_f32(pr + a.N + my_col, es.gb);
+      if constexpr (BWD == 3) {
+        float* pd = a.part_d + prow * 2 * a.N;
+        store8_f32(pd + my_col, es.ga);
+        store8_f32(pd + a.N + my_col, es.gd);
+      }
+    }
+  }
+}
+
 // Epilogue of one wave's 64 x WNT accumulator block (shared by the gathered / HALO kernel and the
 // persistent HALO kernel): per-wave, no barrier (``stg`` is this wave's own 2 KiB of LDS). C layout
 // of a 16x16 block: col = lane & 15, row = 4 * (lane >> 4) + r. ``pix(p)``: output pixel of tile row
-// p (-1: none); partial-statistics rows are (tm * WM + wr).
-template <int BM, int BN, int WNT, bool STATS, int BWD, typename Pix>
+// p (-1: none). The reductions accumulate into ``es``; without DEFER they are flushed here to
+// partial row (tm * WM + wr).
+template <int BM, int BN, int WNT, bool STATS, int BWD, bool DEFER = false, typename Pix>
 __device__ __forceinline__ void convn_epilogue(const ConvnArgs& a, f32x4 (&acc)[4][WNT / 16],
                                                const float (&kshift)[WNT / 16], int tm, int wr, int wc, int lane,
-                                               uint8_t* stg, Pix pix, int n0) {
+                                               uint8_t* stg, Pix pix, int n0, EpiSums<WNT / 16>& es) {
   constexpr int JN = WNT / 16;
   constexpr int WM = BM / 64;
   const int cl = lane & 15, rq = (lane >> 4) * 4;
-  // ---- epilogue (per wave, no barrier: the staging slot is this wave's own): C layout of a
-  // 16x16 block col = lane & 15, row = 4 * (lane >> 4) + r
   if (a.bias) {  // per-output-channel bias (the BN-backward fold's constant term)
 #pragma unroll
     for (int j = 0; j < JN; ++j) {
@@ -186,28 +262,42 @@ __device__ __forceinline__ void convn_epilogue(const ConvnArgs& a, f32x4 (&acc)[
     }
   }
   if constexpr (STATS) {
+    // the statistics of the stored (bf16-rounded) values: one paired conversion, two unpacks. A
+    // 16-row block whose last row is valid is valid throughout (pix is monotone within a block):
+    // the wave-uniform test skips the per-row masks there (row validity held per element across
+    // both column blocks overflowed the SGPR file: 64-bit lane masks, spilled to VGPR lanes)
 #pragma unroll
-    for (int j = 0; j < JN; ++j) {
-      float s1 = 0.f, s2 = 0.f;
+    for (int i = 0; i < 4; ++i) {
+      const bool full = pix(wr * 64 + i * 16 + 15) >= 0;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < JN; ++j) {
+        float s1 = 0.f, s2 = 0.f, t1 = 0.f, t2 = 0.f;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float d = bf16_to_f32(f32_to_bf16(acc[i][j][r])) - kshift[j];
-          const bool ok = pix(wr * 64 + i * 16 + rq + r) >= 0;
-          s1 += ok ? d : 0.f;
-          s2 = ok ? fmaf(d, d, s2) : s2;
+        for (int r = 0; r < 4; r += 2) {
+          const uint32_t pk = pack_bf16x2_rne(acc[i][j][r], acc[i][j][r + 1]);
+          float d0 = __uint_as_float(pk << 16) - kshift[j];
+          float d1 = __uint_as_float(pk & 0xFFFF0000u) - kshift[j];
+          if (!full) {
+            d0 = pix(wr * 64 + i * 16 + rq + r) >= 0 ? d0 : 0.f;
+            d1 = pix(wr * 64 + i * 16 + rq + r + 1) >= 0 ? d1 : 0.f;
+          }
+          s1 += d0;
+          t1 += d1;
+          s2 = fmaf(d0, d0, s2);
+          t2 = fmaf(d1, d1, t2);
         }
-      s1 += xor16(s1, lane);
-      s2 += xor16(s2, lane);
-      s1 += xor32(s1, lane);
-      s2 += xor32(s2, lane);
-      if (lane < 16) {
-        float* pr = a.part + ((int64_t)tm * WM + wr) * 2 * a.N;
-        const int col = n0 + wc * WNT + j * 16 + cl;
-        pr[col] = s1;
-        pr[a.N + col] = s2;
+        es.s1[j] += s1 + t1;
+        es.s2[j] += s2 + t2;
       }
+    }
+  }
+  // reductions of the producing BN's backward (modes 1-5); mode 8 is the forward BN apply
+  constexpr bool BRED = BWD >= 1 && BWD <= 5;
+  constexpr bool APPLY = BWD == 8;
+  if constexpr (STATS && !BRED && !APPLY) {
+    if (a.y == nullptr) {  // statistics-only pass (the output is recomputed by an apply pass)
+      if constexpr (!DEFER) convn_flush<WNT, STATS, BWD>(a, es, (int64_t)tm * WM + wr, wc, lane, n0);
+      return;
     }
   }
   const int L = cl & 3;
@@ -218,27 +308,22 @@ __device__ __forceinline__ void convn_epilogue(const ConvnArgs& a, f32x4 (&acc)[
   // BWD: this lane's 8 output channels are fixed (64 % CPR == 0): per-channel constants once
   const int my_c16 = lane % CPR;
   const int my_col = n0 + wc * WNT + my_c16 * 8;
-  float bmu[8], bsc[8], bsh[8], ga[8], gb[8], bmd[8], gd[8];
+  float bmu[8], bsc[8], bsh[8], bmd[8];
   float inv_hw = 0.f, inv_wo = 0.f;
   const bool fast_div = a.M < (1 << 24);
   if constexpr (BWD == 5) {
     inv_hw = 1.f / (float)(a.Ho * a.Wo);
     inv_wo = 1.f / (float)a.Wo;
   }
-  if constexpr (BWD == 3) {
-    load8_f32(a.bmean_d + my_col, bmd);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) gd[e] = 0.f;
+  if constexpr (BWD == 3) load8_f32(a.bmean_d + my_col, bmd);
+  if constexpr (BRED) load8_f32(a.bmean + my_col, bmu);
+  if constexpr (BWD == 1 || APPLY) {
+    load8_f32(a.bss + my_col, bsc);
+    load8_f32(a.bss + a.N + my_col, bsh);
   }
-  if constexpr (BWD != 0) {
-    load8_f32(a.bmean + my_col, bmu);
-    if constexpr (BWD == 1) {
-      load8_f32(a.bss + my_col, bsc);
-      load8_f32(a.bss + a.N + my_col, bsh);
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) ga[e] = gb[e] = 0.f;
-  }
+  // modes 2 / 3 / 5 without the BN input (bx null: a BN whose input was never stored, ops/tail.py):
+  // x is taken as 0, so the second partial is -mean * sum g (the caller adds sum g x itself)
+  const bool has_bx = !BRED || a.bx != nullptr;
   // BWD: the epilogue operands of all this wave's rows (x, dr, mask bits, xd) are requested here,
   // before the first is used -- the compiler cannot hoist them above the y stores (possible alias),
   // and at one workgroup per CU (LDS) the per-row load -> use latency was the epilogue's cost
@@ -253,11 +338,15 @@ __device__ __forceinline__ void convn_epilogue(const ConvnArgs& a, f32x4 (&acc)[
       const int rr = c / CPR;
       const int m = pix(wr * 64 + i * 16 + rr);
       mm[i][ps] = m;
-      if constexpr (BWD != 0) {
+      if constexpr (APPLY) {
+        rv4[i][ps] = u32x4{0u, 0u, 0u, 0u};
+        if (m >= 0) rv4[i][ps] = *reinterpret_cast<const u32x4*>(a.ares + (int64_t)m * a.N + my_col);
+      }
+      if constexpr (BRED) {
         exr[i][ps] = rv4[i][ps] = dv4[i][ps] = u32x4{0u, 0u, 0u, 0u};
         bt[i][ps] = 0u;
         if (m >= 0) {
-          exr[i][ps] = *reinterpret_cast<const u32x4*>(a.bx + (int64_t)m * a.N + my_col);
+          if (has_bx) exr[i][ps] = *reinterpret_cast<const u32x4*>(a.bx + (int64_t)m * a.N + my_col);
           if constexpr (BWD >= 2) {
             if constexpr (BWD == 5) {
               // residual-branch gradient of a stride-2 1x1 (downsample) convolution, on the quarter
@@ -300,7 +389,26 @@ __device__ __forceinline__ void convn_epilogue(const ConvnArgs& a, f32x4 (&acc)[
       const int m = mm[i][ps];
       if (m >= 0) {
         const int64_t go = (int64_t)m * a.ldc + n0 + wc * WNT + c16 * 8;
-        if constexpr (BWD != 0) {
+        if constexpr (APPLY) {
+          // y = relu(bf16(acc) * scale + shift + residual) and its ReLU bit-mask: bn_apply_kernel's
+          // arithmetic on the stored (bf16-rounded) convolution output, which is never written
+          float d[8], rv[8];
+          load8_bf16(reinterpret_cast<const uint16_t*>(&v), d);
+          load8_bf16(reinterpret_cast<const uint16_t*>(&rv4[i][ps]), rv);
+          uint32_t bits = 0;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float o = relu_nan(fmaf(d[e], bsc[e], bsh[e]) + rv[e]);
+            d[e] = o;
+            bits |= (o > 0.f ? 1u : 0u) << e;
+          }
+          uint32_t pk[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) pk[e] = pack_bf16x2_rne(d[2 * e], d[2 * e + 1]);
+          v = u32x4{pk[0], pk[1], pk[2], pk[3]};
+          a.amask[((int64_t)m * a.N + my_col) >> 3] = (uint8_t)bits;
+        }
+        if constexpr (BRED) {
           float d[8], xv[8];
           load8_bf16(reinterpret_cast<const uint16_t*>(&v), d);
           load8_bf16(reinterpret_cast<const uint16_t*>(&exr[i][ps]), xv);
@@ -318,56 +426,25 @@ __device__ __forceinline__ void convn_epilogue(const ConvnArgs& a, f32x4 (&acc)[
 #pragma unroll
           for (int e = 0; e < 4; ++e) pk[e] = pack_bf16x2_rne(d[2 * e], d[2 * e + 1]);
           v = u32x4{pk[0], pk[1], pk[2], pk[3]};
+          float gq[8];  // the stored g
+          load8_bf16(reinterpret_cast<const uint16_t*>(&v), gq);
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            const float gq = bf16_to_f32(f32_to_bf16(d[e]));  // the stored g
-            ga[e] += gq;
-            gb[e] = fmaf(gq, xv[e] - bmu[e], gb[e]);
+            es.ga[e] += gq[e];
+            es.gb[e] = fmaf(gq[e], xv[e] - bmu[e], es.gb[e]);
           }
           if constexpr (BWD == 3) {
             float dv[8];
             load8_bf16(reinterpret_cast<const uint16_t*>(&dv4[i][ps]), dv);
 #pragma unroll
-            for (int e = 0; e < 8; ++e) gd[e] = fmaf(bf16_to_f32(f32_to_bf16(d[e])), dv[e] - bmd[e], gd[e]);
+            for (int e = 0; e < 8; ++e) es.gd[e] = fmaf(gq[e], dv[e] - bmd[e], es.gd[e]);
           }
         }
         *reinterpret_cast<u32x4*>(y + go) = v;
       }
     }
   }
-  if constexpr (BWD != 0) {
-    // lanes sharing this lane's channels: lane % CPR equal -> rotate-sum within the 16-lane row,
-    // then across rows
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      if constexpr (CPR == 4) {
-        ga[e] += ror_row<4>(ga[e]);
-        gb[e] += ror_row<4>(gb[e]);
-      }
-      ga[e] += ror_row<8>(ga[e]);
-      gb[e] += ror_row<8>(gb[e]);
-      ga[e] += xor16(ga[e], lane);
-      gb[e] += xor16(gb[e], lane);
-      ga[e] += xor32(ga[e], lane);
-      gb[e] += xor32(gb[e], lane);
-      if constexpr (BWD == 3) {
-        if constexpr (CPR == 4) gd[e] += ror_row<4>(gd[e]);
-        gd[e] += ror_row<8>(gd[e]);
-        gd[e] += xor16(gd[e], lane);
-        gd[e] += xor32(gd[e], lane);
-      }
-    }
-    if (lane < CPR) {
-      float* pr = a.part + ((int64_t)tm * WM + wr) * 2 * a.N;
-      store8_f32(pr + my_col, ga);
-      store8_f32(pr + a.N + my_col, gb);
-      if constexpr (BWD == 3) {
-        float* pd = a.part_d + ((int64_t)tm * WM + wr) * 2 * a.N;
-        store8_f32(pd + my_col, ga);
-        store8_f32(pd + a.N + my_col, gd);
-      }
-    }
-  }
+  if constexpr (!DEFER) convn_flush<WNT, STATS, BWD>(a, es, (int64_t)tm * WM + wr, wc, lane, n0);
 }
 
 // BWD (bwd-data of a convolution whose input came out of a BatchNorm + ReLU): the epilogue also runs
@@ -399,7 +476,7 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
   auto pix = [&](int p) -> int {
     if constexpr (HALO) {
       const int j = p >> lsw, wo = p & (sw - 1);
-      return (wo < a.Wo && ho0 + j < a.Ho) ? (hn * a.Ho + ho0 + j) * a.Wo + wo : -1;
+      return ((wo < a.Wo) & (ho0 + j < a.Ho)) ? (hn * a.Ho + ho0 + j) * a.Wo + wo : -1;
     } else {
       return m0 + p < a.M ? m0 + p : -1;
     }
@@ -563,9 +640,11 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
     __builtin_amdgcn_sched_barrier(0);
   }
 
+  EpiSums<G::JN> es;
+  es.zero();
   convn_epilogue<BM, BN, WNT, STATS, BWD>(a, acc, kshift, tm, wr, wc, lane,
                                           smem + a.nslot * SLOTB + (HALO ? halo_win_bytes(BM) : 0) + wid * G::STG, pix,
-                                          n0);
+                                          n0, es);
 }
 
 
@@ -585,6 +664,15 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
 //     window at row offset (r * 64 + s) (the tap shift), B fragments from the resident weights;
 //   * the epilogue (statistics / bwd reductions / stores) is the shared one; the next window's DMA
 //     is in flight underneath it.
+// LDS image of the persistent kernel: [rows][64] bf16, 16-byte chunk c of row r at chunk
+// c ^ (2 * ((r >> 1) & 3)). The taps read 16 consecutive rows from any start row (the tap shift s =
+// 0..2 and the row offsets); with the gathered kernels' c ^ ((r >> 1) & 7) an odd start put two
+// lanes of one ds_read_b128 lane group on one bank (SQ_LDS_BANK_CONFLICT 2.2e7 per launch,
+// gpurun_out/convh pmc1); this one is conflict-free for every start row (exhaustive check over the
+// four lane groups, both k-steps).
+__device__ __forceinline__ int hx_swz(int row) { return ((row >> 1) & 3) << 1; }
+__device__ __forceinline__ int hx_off(int row, int kc) { return row * 128 + ((kc ^ hx_swz(row)) << 4); }
+
 constexpr int kHxWin = 4 * 64 * 128;          // window bytes (4 rows x 64 slots x 128 B)
 constexpr int kHxW = 9 * 64 * 128;            // resident weights (9 taps x 64 rows x 128 B)
 constexpr int kHxLds = kHxW + 2 * kHxWin + 4 * 2048 + 512;  // + 4 wave staging areas, + tap overrun
@@ -613,7 +701,7 @@ __global__ __launch_bounds__(256) void convh_kernel(ConvnArgs a, int ntiles) {
   // weights: tap t rows n = 0..63 of k = t*64 .. t*64+63, K-major swizzled images (72 pieces of 1 KiB)
   for (int pc = wid; pc < 72; pc += 4) {
     const int t = pc >> 3, row = (pc & 7) * 8 + (lane >> 3);
-    const int kc = (lane & 7) ^ ((row >> 1) & 7);
+    const int kc = (lane & 7) ^ hx_swz(row);
     const uint32_t off = ((uint32_t)row * (uint32_t)a.K + (uint32_t)(t * 64 + kc * 8)) * 2u;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)(wlds + pc * 1024), 16, off,
                                              0, 0, 0);
@@ -627,7 +715,7 @@ __global__ __launch_bounds__(256) void convh_kernel(ConvnArgs a, int ntiles) {
       const int row = pc * 8 + (lane >> 3);
       const int jj = row >> 6, ws = row & 63;
       const int hi = ho0 - 1 + jj, wi = ws - 1;
-      const int kc = (lane & 7) ^ ((row >> 1) & 7);
+      const int kc = (lane & 7) ^ hx_swz(row);
       const bool ok = (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
       const uint32_t off = ok ? ((((uint32_t)((n * a.H + hi) * a.W + wi)) << 6) + (uint32_t)(kc * 8)) * 2u : kOOB;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(winb(b) + pc * 1024), 16,
@@ -638,6 +726,8 @@ __global__ __launch_bounds__(256) void convh_kernel(ConvnArgs a, int ntiles) {
   wait_vm<0>();
   __syncthreads();
   uint8_t* stg = smem + kHxW + 2 * kHxWin + wid * 2048;
+  EpiSums<2> es;  // this wave's reductions over all its tiles: one partial row per (workgroup, wave row)
+  es.zero();
   for (int tile = t_begin, it = 0; tile < t_end; ++tile, ++it) {
     const int b = it & 1;
     if (tile + 1 < t_end) stage(tile + 1, b ^ 1);  // lands under this tile's taps + epilogue
@@ -655,11 +745,13 @@ __global__ __launch_bounds__(256) void convh_kernel(ConvnArgs a, int ntiles) {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j) bf[ks][j] = frag(Bs, wc * 2 + j, ks, lane);
+        for (int j = 0; j < 2; ++j)
+          bf[ks][j] = __builtin_bit_cast(
+              bf16x8, *reinterpret_cast<const u32x4*>(Bs + hx_off((wc * 2 + j) * 16 + (lane & 15), ks * 4 + (lane >> 4))));
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int row = (wr + tr) * 64 + i * 16 + (lane & 15) + ts;
-          af[ks][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(win + kmaj_off(row, ks * 4 + (lane >> 4))));
+          af[ks][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(win + hx_off(row, ks * 4 + (lane >> 4))));
         }
       }
 #pragma unroll
@@ -673,12 +765,13 @@ __global__ __launch_bounds__(256) void convh_kernel(ConvnArgs a, int ntiles) {
     const int n = tile / tpi, ho0 = (tile - n * tpi) * 2;
     auto pix = [&](int p) -> int {
       const int j = p >> 6, wo = p & 63;
-      return (wo < a.Wo && ho0 + j < a.Ho) ? (n * a.Ho + ho0 + j) * a.Wo + wo : -1;
+      return ((wo < a.Wo) & (ho0 + j < a.Ho)) ? (n * a.Ho + ho0 + j) * a.Wo + wo : -1;
     };
-    convn_epilogue<128, 64, 32, STATS, BWD>(a, acc, kshift, tile, wr, wc, lane, stg, pix, 0);
+    convn_epilogue<128, 64, 32, STATS, BWD, true>(a, acc, kshift, tile, wr, wc, lane, stg, pix, 0, es);
     wait_vm<0>();     // this wave's DMA of the next window (and the epilogue's loads) landed
     __syncthreads();  // every wave's: the next window is complete and this one no longer read
   }
+  convn_flush<32, STATS, BWD>(a, es, (int64_t)blockIdx.x * 2 + wr, wc, lane, 0);
 }
 
 static bool convh_ok(const ConvnArgs& a) {
@@ -754,6 +847,10 @@ static hipError_t convn_launch_s(const ConvnArgs& a, hipStream_t st) {
   if (a.bwd == 2) return convn_launch_t<BM, BN, WNT, NSLOT, false, 2, HALO>(a, st);
   if (a.bwd == 3) return convn_launch_t<BM, BN, WNT, NSLOT, false, 3, HALO>(a, st);
   if (a.bwd == 5) return convn_launch_t<BM, BN, WNT, NSLOT, false, 5, HALO>(a, st);
+  if (a.bwd == 8) {  // (1x1 tails only: no HALO instantiation)
+    if constexpr (HALO) return hipErrorNotSupported;
+    else return convn_launch_t<BM, BN, WNT, NSLOT, false, 8, false>(a, st);
+  }
   return a.part ? convn_launch_t<BM, BN, WNT, NSLOT, true, 0, HALO>(a, st)
                 : convn_launch_t<BM, BN, WNT, NSLOT, false, 0, HALO>(a, st);
 }
@@ -825,9 +922,9 @@ int convn_part_rows_geo(int M, int N, int variant, int Ho, int Wo, int R) {
   const int bn = convn_tile_n(N);
   if (!bn) return 0;
   const int bm = variant_bm(bn, variant);
-  if (is_persist(bn, variant)) {
+  if (is_persist(bn, variant)) {  // one row per (workgroup, wave row): convh_kernel's flush
     if (Ho <= 0 || Wo <= 0) return 0;
-    return 2 * ((M / (Ho * Wo)) * ((Ho + 1) / 2));
+    return 2 * convh_grid((M / (Ho * Wo)) * ((Ho + 1) / 2));
   }
   if (variant >= plain_count(bn)) {
     const int sw = halo_sw(Wo, R);
@@ -853,8 +950,10 @@ hipError_t launch_convn(const ConvnArgs& a_in, hipStream_t st) {
                             a.K == K1 + (1 << a.logC2) && a.x2bytes > 0 && a.x2bytes <= 0xFFFFFF00u)) &&
                   a.ldc >= a.N && a.H < 32768 && a.W < 32768 && a.xbytes > 0 && a.xbytes <= 0xFFFFFF00u &&
                   a.wbytes > 0 && a.variant < convn_variant_count(bn) &&
+                  (a.y || (a.bwd == 0 && a.part)) &&
                   (a.bwd == 0 ? (!a.part || a.shift)
-                              : (a.part && a.bx && a.bmean && a.ldc == a.N &&
+                   : a.bwd == 8 ? (!a.part && a.bss && a.ares && a.amask && a.ldc == a.N && a.N % 8 == 0)
+                              : (a.part && (a.bx || a.bwd >= 2) && a.bmean && a.ldc == a.N &&
                                  (a.bwd == 1 ? a.bss != nullptr
                                              : ((a.bwd == 2 || a.bwd == 3 || a.bwd == 5) && a.bdr && a.bmbits &&
                                                 (a.bwd != 3 || (a.bxd && a.bmean_d && a.part_d)) &&
@@ -862,7 +961,7 @@ hipError_t launch_convn(const ConvnArgs& a_in, hipStream_t st) {
   if (!ok) return hipErrorNotSupported;
   const int v = a.variant >= 0 ? a.variant : default_variant(a, bn);
   if (is_persist(bn, v)) {
-    if (!convh_ok(a)) return hipErrorNotSupported;
+    if (!convh_ok(a) || a.bwd == 8 || !a.y) return hipErrorNotSupported;
     return convh_launch(a, st);
   }
   if (v >= plain_count(bn)) {  // HALO

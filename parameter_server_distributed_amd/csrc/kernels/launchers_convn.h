@@ -38,6 +38,11 @@ struct ConvnArgs {
   uint32_t x2bytes;
   int K1, logC2;
   const float* bias;      // optional fp32 [N] added to the output in the epilogue (before bwd / stats)
+  // bwd 8 (a forward epilogue, despite the field name): y = relu(bf16(conv) * bss[c] + bss[N + c] +
+  // ares) with its ReLU bit-mask into amask [M*N/8] -- the BN apply of a convolution output that is
+  // never stored (ops/tail.py: statistics pass with y = nullptr, then this apply pass)
+  const uint16_t* ares;
+  uint8_t* amask;
 };
 
 // output-channel tile of the kernel for N output channels (64, 128, 256 for N % 256 == 0), 0: unsupported

@@ -48,6 +48,10 @@ std::vector<at::Tensor> bn_bwd_dual_pre(const at::Tensor& g, const at::Tensor& x
                                         c10::optional<at::Tensor> dbeta_d_out, bool fold);
 std::vector<at::Tensor> bnfold_dgrad_weights(const at::Tensor& w, const at::Tensor& coef);
 void bnfold_combine(const at::Tensor& P, const at::Tensor& w, const at::Tensor& coef, at::Tensor out, bool accumulate);
+void bnfold_rowdot(const at::Tensor& P, const at::Tensor& w, at::Tensor row);
+std::vector<at::Tensor> bn_finalize(const at::Tensor& part, int64_t rows, int64_t M, const at::Tensor& gamma,
+                                    const at::Tensor& beta, at::Tensor running_mean, at::Tensor running_var,
+                                    double momentum, double eps, c10::optional<at::Tensor> counter);
 std::vector<at::Tensor> bn_bwd_coef(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& gamma,
                                     const at::Tensor& save_mean, const at::Tensor& save_invstd,
                                     c10::optional<at::Tensor> mbits, c10::optional<at::Tensor> dy2,
@@ -75,12 +79,16 @@ void gelu_bwd_colsum_(const at::Tensor& dy, const at::Tensor& pre, at::Tensor dx
 // the partial rows written (1 without statistics).
 int64_t convn_part_rows_(int64_t M, int64_t N, int64_t v, int64_t Ho, int64_t Wo, int64_t R);
 bool convn_variant_ok_(int64_t N, int64_t v, int64_t R, int64_t S, int64_t stride, int64_t pad, int64_t Wo, bool has_x2);
+// no_store: statistics only (out unused); apply_ss / apply_res / apply_mask: the BN apply epilogue
+// out = relu(bf16(conv) * ss[c] + ss[Cout + c] + res) + its ReLU bit-mask (bwd mode 8)
 int64_t convn_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride,
                int64_t pad, c10::optional<at::Tensor> part, c10::optional<at::Tensor> shift, int64_t variant,
-               c10::optional<at::Tensor> x2, c10::optional<at::Tensor> bias);
+               c10::optional<at::Tensor> x2, c10::optional<at::Tensor> bias, bool no_store,
+               c10::optional<at::Tensor> apply_ss, c10::optional<at::Tensor> apply_res,
+               c10::optional<at::Tensor> apply_mask);
 int64_t convn_stats_rows_(int64_t M);
 int64_t convn_bwd_(const at::Tensor& dy, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride,
-                   int64_t pad, at::Tensor part, int64_t variant, int64_t mode, const at::Tensor& bx,
+                   int64_t pad, at::Tensor part, int64_t variant, int64_t mode, c10::optional<at::Tensor> bx,
                    const at::Tensor& bmean, c10::optional<at::Tensor> bss, c10::optional<at::Tensor> bdr,
                    c10::optional<at::Tensor> bmbits, c10::optional<at::Tensor> x2,
                    c10::optional<at::Tensor> bias, c10::optional<at::Tensor> bxd, c10::optional<at::Tensor> bmean_d,

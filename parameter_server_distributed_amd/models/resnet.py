@@ -20,6 +20,7 @@ import torch.nn as nn
 from ..ops.bn import FusedBatchNorm2d, bn_add_bn_relu
 from ..ops.conv import Conv1x1, ConvNHWC, stem_forward
 from ..ops.pool import MaxPool3x3s2, global_avg_pool
+from ..ops.tail import conv_bn_tail, tail_ok
 
 
 class _Fork(torch.autograd.Function):
@@ -123,6 +124,9 @@ class Bottleneck(nn.Module):
         out = self.bn1(self.conv1(xm))
         out = self.bn2(self.conv2(out))
         fuse = prev_bn if (self.downsample is None and self.fuse_residual_grad) else None
+        if self.downsample is None and tail_ok(self.conv3, self.bn3, out, idt):
+            # conv3's output is never stored: statistics pass + apply pass, recomputed (ops/tail.py)
+            return conv_bn_tail(self.conv3, self.bn3, out, idt, fuse)
         return self.bn3(self.conv3(out), idt, resid_grad_to=fuse)
 
 

@@ -183,32 +183,38 @@ def _bn_consumer(mod):
 
 def _convn_variants(x, w2, k: int, stride: int, pad: int, bn=None) -> dict:
     """{"psdn<v>": fn} over the kernel's tile variants; fn() -> the channels_last conv output. With a
-    consumer ``bn`` every call also reduces the BN's statistics partials in its epilogue and hands
-    them to the BN (``_psd_stats_pending``: its forward then skips the statistics pass)."""
+    consumer ``bn`` every "psdn" call also reduces the BN's statistics partials in its epilogue and
+    hands them to the BN (``_psd_stats_pending``: its forward then skips the statistics pass), and
+    "psdu<v>" candidates run the same variants without that epilogue."""
     C = _native()
     n, _, h, w = x.shape
     cout = w2.shape[0]
     ho, wo = (h + 2 * pad - k) // stride + 1, (w + 2 * pad - k) // stride + 1
     M = n * ho * wo
 
-    def make(v):
+    def make(v, stats):
         def fn():
             out = torch.empty(M, cout, device=x.device, dtype=x.dtype)
             part = None
-            if bn is not None:
+            if stats:
                 part = torch.empty(_part_rows(M, cout, v, ho, wo, k), 2, cout, device=x.device, dtype=torch.float32)
             rows = C.convn_(x, w2, out, k, k, stride, pad, part=part,
-                            shift=bn.running_mean if bn is not None else None, variant=v)
+                            shift=bn.running_mean if stats else None, variant=v)
             if rows == 0:
                 raise RuntimeError("convn_ declined a shape _psdn_ok accepted")
             y = _from_2d(out, n, ho, wo)
-            if bn is not None:
+            if stats:
                 bn._psd_stats_pending = (y, part, rows)
             return y
         return fn
 
-    return {f"psdn{v}": make(v) for v in range(C.convn_variants(cout))
-            if _variant_ok(cout, v, k, stride, pad, wo, x.shape[1], h)}
+    ok = [v for v in range(C.convn_variants(cout)) if _variant_ok(cout, v, k, stride, pad, wo, x.shape[1], h)]
+    cands = {f"psdn{v}": make(v, bn is not None) for v in ok}
+    if bn is not None:
+        # the same kernels without the statistics epilogue ("psdu": the BN then runs its own reduce
+        # pass, and _route times them with it)
+        cands.update({f"psdu{v}": make(v, False) for v in ok})
+    return cands
 
 
 def _variant_ok(cout: int, v: int, k: int, stride: int, pad: int, wo: int, cin: int | None = None,
@@ -283,7 +289,8 @@ def _convn_bwd_variants(dy, w2, k: int, pad: int, fu: dict, dr) -> dict:
     def make(v):
         def fn():
             out = torch.empty(M, cout, device=dy.device, dtype=dy.dtype)
-            part = torch.empty(_part_rows(M, cout, v, h, w, k), 2, cout, device=dy.device, dtype=torch.float32)
+            # (+ 1 row: a BN whose input was never stored completes its partials there, ops/tail.py)
+            part = torch.empty(_part_rows(M, cout, v, h, w, k) + 1, 2, cout, device=dy.device, dtype=torch.float32)
             part_d = torch.empty_like(part) if fu["mode"] == 3 else None
             rows = C.convn_bwd_(dy, w2, out, k, k, 1, pad, part, v, fu["mode"], fu["bx"], fu["mean"],
                                 bss=fu.get("ss"), bdr=_dr_arg(dr), bmbits=fu.get("mbits"), bxd=fu.get("bxd"),
@@ -305,6 +312,12 @@ def _dgrad_route(key: tuple, cands: dict, default: str, fu, dy_like) -> torch.Te
     returns the handed-over residual gradient to the BN's queue."""
     if fu is None:
         return cands[_at.choose(key, cands, default)]()
+    if fu.get("bx") is None:
+        # the BN's input was never stored (ops/tail.py): only the fused epilogue can reduce its backward
+        cands = {name: fn for name, fn in cands.items() if name.startswith("psdnb")}
+        if not cands:
+            raise RuntimeError("psd: a BN without its stored input needs the fused bwd-data epilogue")
+        key, default = key + ("nobx",), next(iter(cands))
     timed = {name: (fn if name.startswith("psdnb") else _with_bn_bwd_reduce(fn, fu)) for name, fn in cands.items()}
     how = _at.choose(key + ("bnbwd",), timed, default)
     out = cands[how]()
@@ -364,7 +377,9 @@ def _route(key: tuple, cands: dict, default: str, bn=None) -> str:
         return _at.choose(key, cands, default)
     timed = {name: (fn if name.startswith(("psdn", "psds")) else _with_bn_reduce(fn, bn))
              for name, fn in cands.items()}
-    return _at.choose(key + ("bnstats",), timed, default)
+    how = _at.choose(key + ("bnstats",), timed, default)
+    bn._psd_stats_pending = None  # (a timed candidate's hand-over; the chosen one, run next, sets its own)
+    return how
 
 
 def _convw_cands(dy, x, k: int, stride: int, pad: int) -> dict:
@@ -427,7 +442,15 @@ def _sink_view(mod, weight):
     return sink(weight) if sink is not None else None
 
 
-def _fold_backward(ctx, fold, x, weight, need_x: bool, need_w: bool):
+def fold_ok(cin: int, cout: int) -> bool:
+    """The BN-backward fold of a 1x1 convolution (cin -> cout) runs on our kernels for this shape:
+    the K-concatenated dgrad on the narrow kernel and the fold wgrad (kernels/convw.hip)."""
+    C = _native()
+    return (_psdn_ok(cout, cin) and cin >= 64 and (cin & (cin - 1)) == 0 and cout % 64 == 0
+            and C.convw_fold_rows(cout, cin) > 0)
+
+
+def _fold_backward(ctx, fold, x, weight, need_x: bool, need_w: bool, P=None):
     """conv3's backward with its consumer BN's input gradient folded in (kernels/bnfold.hip): the BN
     handed over g (the masked upstream gradient) and the coefficients of dy = A g + B y + C, where
     y = conv(x) is the BN input. dgrad runs on the narrow kernel with the K-concatenated operand
@@ -435,7 +458,10 @@ def _fold_backward(ctx, fold, x, weight, need_x: bool, need_w: bool):
     the narrow wgrad kernel's fold mode (g^T x, x^T x, 1^T x in one pass) + the combination. The
     unfolded path -- the BN elementwise pass, then the ordinary dgrad -- is one of the timed
     candidates (and the correctness reference); when it wins, (None, None, dy) is returned and the
-    caller runs the ordinary backward on dy. Returns (dx, dw, None) when folded."""
+    caller runs the ordinary backward on dy. Returns (dx, dw, None) when folded.
+
+    y None (ops/tail.py: the BN input was never stored): only the folded candidates; ``P`` the fold
+    wgrad products the caller already ran (its BN statistics needed g^T x), combined here."""
     g, coef, y = fold
     C = _native()
     n, cin, h, w = x.shape
@@ -451,16 +477,19 @@ def _fold_backward(ctx, fold, x, weight, need_x: bool, need_w: bool):
     dx = dw = None
     how = "unfold"
     frows = C.convw_fold_rows(cout, cin)
-    foldable = (_psdn_ok(cout, cin) and x.is_contiguous(memory_format=torch.channels_last) and cin >= 64
-                and (cin & (cin - 1)) == 0 and cout % 64 == 0 and frows > 0)
+    foldable = fold_ok(cin, cout) and x.is_contiguous(memory_format=torch.channels_last)
+    if y is None and not foldable:
+        raise RuntimeError("psd BN-backward fold without the BN input needs a foldable shape")
     conv_bwd = torch.ops.aten.convolution_backward
     wargs = (None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1)
 
     def fold_wgrad(into):
-        P = torch.empty(frows, cin, device=g.device, dtype=torch.float32)
-        if not C.convw_(g, x, P, 1, 1, 1, 0, fold=True):
-            raise RuntimeError("convw_ declined a fold shape convw_fold_rows accepted")
-        C.bnfold_combine(P, weight, coef, into)
+        Pw = P
+        if Pw is None:
+            Pw = torch.empty(frows, cin, device=g.device, dtype=torch.float32)
+            if not C.convw_(g, x, Pw, 1, 1, 1, 0, fold=True):
+                raise RuntimeError("convw_ declined a fold shape convw_fold_rows accepted")
+        C.bnfold_combine(Pw, weight, coef, into)
 
     if need_x and foldable:
         w2, bvec = C.bnfold_dgrad_weights(weight, coef)
@@ -508,19 +537,20 @@ def _fold_backward(ctx, fold, x, weight, need_x: bool, need_w: bool):
                 fu["bn"]._psd_bwd_pre = (o, part, rows) if part_d is None else (o, part, rows, part_d)
             return o
 
-        cands = {"unfold": unfold}
+        cands = {"unfold": unfold} if y is not None else {}
         for v in range(C.convn_variants(cin)):
             if not C.convn_variant_ok(cin, v, 1, 1, 1, 0, w, True):
                 continue
             cands[f"psdnf{v}"] = make(v, False)
             if fu is not None:
                 cands[f"psdnb{v}"] = make(v, True)
-        key = ("conv1x1", "dgrad_fold", M, cin, cout)
+        key = ("conv1x1", "dgrad_fold", M, cin, cout) + (() if y is not None else ("noy",))
+        default = "unfold" if y is not None else next(iter(cands))
         if fu is None:
-            how = _at.choose(key, cands, "unfold")
+            how = _at.choose(key, cands, default)
         else:
             timed = {nm: (fn if nm.startswith("psdnb") else _with_bn_bwd_reduce(fn, fu)) for nm, fn in cands.items()}
-            how = _at.choose(key + ("bnbwd",), timed, "unfold")
+            how = _at.choose(key + ("bnbwd",), timed, default)
         timing["on"] = False
         if how != "unfold":
             dx = cands[how]()

@@ -1,0 +1,207 @@
+"""The recomputing bottleneck tail (ops/tail.py): conv3's output is never stored.
+
+Kernel level (small-integer operands: every product and sum is exact in bf16 / fp32, so the checks
+are exact against fp32 PyTorch): the narrow kernel's statistics-only pass, its BN-apply epilogue
+(bwd mode 8: relu(bf16(y) * scale + shift + residual) + ReLU bit-mask), the bwd-data epilogue
+without the BN input (modes 2 / 5 with bx None) and the rowdot kernel that supplies the missing
+sum g y. Model level: ResNet-50 with the tail on vs off -- loss, every gradient, running stats."""
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from parameter_server_distributed_amd import native
+
+pytestmark = pytest.mark.gpu
+
+
+def _ints(shape, lo, hi, g):
+    return torch.randint(lo, hi + 1, shape, generator=g).float()
+
+
+@pytest.mark.parametrize("Nb,H,cin,cout", [(2, 14, 64, 256), (3, 7, 128, 512), (1, 9, 256, 1024)])
+def test_convn_stats_only_and_apply_epilogue_exact(gpu, Nb, H, cin, cout):
+    C = native()
+    g = torch.Generator().manual_seed(3)
+    x = _ints((Nb, cin, H, H), -1, 1, g)
+    w = _ints((cout, cin), -1, 1, g)
+    M = Nb * H * H
+    y = (x.permute(0, 2, 3, 1).reshape(M, cin).double() @ w.double().t())  # exact
+    sc = _ints((cout,), 1, 2, g)
+    sh = _ints((cout,), -3, 3, g) + 0.5
+    res = _ints((M, cout), -4, 4, g)
+    o = torch.relu(y * sc.double() + sh.double() + res.double())
+    want_out = o.float().bfloat16().float()
+    want_bits = (o > 0).view(M * cout // 8, 8)
+    xd = x.to(gpu, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    wd = w.to(gpu, torch.bfloat16)
+    shift = torch.zeros(cout, device=gpu)
+    nv = 0
+    for v in range(C.convn_variants(cout)):
+        if C.convn_variant_kind(cout, v) != 0 or not C.convn_variant_ok(cout, v, 1, 1, 1, 0, H):
+            continue
+        nv += 1
+        rows_alloc = max(C.convn_stats_rows(M), C.convn_part_rows(M, cout, v, H, H, 1))
+        part = torch.full((rows_alloc, 2, cout), float("nan"), device=gpu)
+        rows = C.convn_(xd, wd, part, 1, 1, 1, 0, part=part, shift=shift, variant=v, no_store=True)
+        assert rows > 0
+        got = part[:rows].double().sum(0).cpu()
+        torch.testing.assert_close(got[0], y.sum(0), rtol=0, atol=1e-3, msg=lambda m: f"v{v} sum: {m}")
+        torch.testing.assert_close(got[1], (y * y).sum(0), rtol=1e-7, atol=1e-3, msg=lambda m: f"v{v} sumsq: {m}")
+        out = torch.full((M, cout), 7.0, device=gpu, dtype=torch.bfloat16)
+        mb = torch.zeros(M * cout // 8, device=gpu, dtype=torch.uint8)
+        ss = torch.cat([sc, sh]).to(gpu)
+        assert C.convn_(xd, wd, out, 1, 1, 1, 0, variant=v, apply_ss=ss, apply_res=res.to(gpu, torch.bfloat16),
+                        apply_mask=mb) == 1
+        torch.testing.assert_close(out.float().cpu(), want_out, rtol=0, atol=0, msg=lambda m: f"v{v} out: {m}")
+        bits = ((mb.cpu()[:, None] >> torch.arange(8, dtype=torch.uint8)) & 1).bool()
+        assert torch.equal(bits, want_bits), v
+    assert nv >= 2
+
+
+@pytest.mark.parametrize("mode", [2, 5])
+def test_convn_bwd_epilogue_without_bn_input(gpu, mode):
+    """Modes 2 / 5 with bx None: g as with bx, the second partial is sum g (0 - mean)."""
+    C = native()
+    Nb, H, K, N = 2, 12, 64, 128
+    g = torch.Generator().manual_seed(9)
+    dy = _ints((Nb, K, H, H), -1, 1, g)
+    w2 = _ints((N, K), -1, 1, g)
+    M = Nb * H * H
+    out_ref = dy.permute(0, 2, 3, 1).reshape(M, K).double() @ w2.double().t()
+    mean = _ints((N,), -2, 2, g)
+    bits = torch.randint(0, 2, (M, N), generator=g).bool()
+    packed = (bits.view(M * N // 8, 8).to(torch.uint8) << torch.arange(8, dtype=torch.uint8)).sum(1).to(torch.uint8)
+    if mode == 2:
+        dr = _ints((M, N), -2, 2, g)
+        add = dr.double()
+        bdr = dr.to(gpu, torch.bfloat16)
+    else:
+        dr4 = _ints((Nb, N, H // 2, H // 2), -2, 2, g)
+        full = torch.zeros(Nb, N, H, H)
+        full[:, :, ::2, ::2] = dr4
+        add = full.permute(0, 2, 3, 1).reshape(M, N).double()
+        bdr = dr4.to(gpu, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    gref = torch.where(bits, out_ref + add, torch.zeros_like(out_ref))
+    s1 = gref.sum(0)
+    dyd = dy.to(gpu, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    for v in range(C.convn_variants(N)):
+        if C.convn_variant_kind(N, v) != 0:
+            continue
+        out = torch.full((M, N), 7.0, device=gpu, dtype=torch.bfloat16)
+        part = torch.full((max(C.convn_stats_rows(M), C.convn_part_rows(M, N, v, H, H, 1)), 2, N), float("nan"),
+                          device=gpu)
+        rows = C.convn_bwd_(dyd, w2.to(gpu, torch.bfloat16), out, 1, 1, 1, 0, part, v, mode, None, mean.to(gpu),
+                            bdr=bdr, bmbits=packed.to(gpu))
+        assert rows > 0
+        torch.testing.assert_close(out.double().cpu(), gref, rtol=0, atol=0)
+        got = part[:rows].double().cpu().sum(0)
+        torch.testing.assert_close(got[0], s1, rtol=0, atol=1e-6)
+        torch.testing.assert_close(got[1], -mean.double() * s1, rtol=0, atol=1e-6)
+
+
+def test_bnfold_rowdot(gpu):
+    C = native()
+    g = torch.Generator().manual_seed(4)
+    cout, cin = 256, 64
+    P = torch.randn(cout + cin + 1, cin, generator=g)
+    w = torch.randn(cout, cin, generator=g).bfloat16()
+    row = torch.full((2, cout), float("nan"), device=gpu)
+    C.bnfold_rowdot(P.to(gpu), w.to(gpu), row)
+    want = (w.double() * P[:cout].double()).sum(1)
+    assert torch.equal(row[0].cpu(), torch.zeros(cout))
+    torch.testing.assert_close(row[1].double().cpu(), want, rtol=1e-5, atol=1e-4)
+
+
+def test_resnet_tail_matches_unfused(gpu, monkeypatch):
+    """ResNet-50 (64x64 images) with the recomputing tail on vs off: loss, every parameter gradient
+    and the running statistics; the fused backward (consumer epilogue + rowdot) and the recompute
+    fallback (the last block feeds the pooling) both ran."""
+    from parameter_server_distributed_amd import models
+    from parameter_server_distributed_amd.models.resnet import Bottleneck
+    from parameter_server_distributed_amd.ops import autotune, tail
+
+    res = []
+    for on in (True, False):
+        monkeypatch.setenv("PSD_TAIL_RECOMPUTE", "1" if on else "0")
+        autotune._DECISIONS.clear()
+        for k in tail.TAIL_CALLS:
+            tail.TAIL_CALLS[k] = 0
+        torch.manual_seed(0)
+        spec = models.build("resnet50", gpu, torch.bfloat16, image_size=64, num_classes=10)
+        m = spec.model
+        for mod in m.modules():  # non-zero bn3 scales: the tail's gradients are then not trivially 0
+            if isinstance(mod, Bottleneck):
+                nn.init.uniform_(mod.bn3.weight, 0.5, 1.5)
+        for p in m.parameters():
+            p.data = p.data.to(torch.bfloat16)
+        x, y = spec.make_batch(8, gpu, seed=3)
+        loss = spec.loss(m(x), y)
+        loss.backward()
+        res.append((float(loss), {n: p.grad.float().clone() for n, p in m.named_parameters()},
+                    {n: b.clone() for n, b in m.named_buffers() if "running" in n}))
+        if on:
+            # ResNet-50's identity blocks whose conv3 shape the fold takes (layer1-3: 10 of 12); each
+            # backward either fused (the next conv1's epilogue) or recomputed (no fused consumer)
+            calls = dict(tail.TAIL_CALLS)
+            assert calls["fwd"] >= 10, calls
+            assert calls["bwd_fused"] + calls["bwd_recompute"] == calls["fwd"] and calls["bwd_fused"] >= 9, calls
+    autotune._DECISIONS.clear()
+    assert abs(res[0][0] - res[1][0]) < 0.02 * abs(res[1][0]) + 1e-3, (res[0][0], res[1][0])
+    bad = {}
+    for n in res[1][1]:
+        a, b = res[0][1][n], res[1][1][n]
+        rel = ((a - b).norm() / b.norm().clamp_min(1e-12)).item() if b.norm() > 0 else a.norm().item()
+        if not rel < (0.05 if b.norm() > 0 else 1e-3):
+            bad[n] = round(rel, 4)
+    assert not bad, bad
+    for n in res[1][2]:
+        torch.testing.assert_close(res[0][2][n], res[1][2][n], rtol=2e-2, atol=2e-3, msg=n)
+
+
+def test_tail_recompute_fallback_matches_unfused(gpu, monkeypatch):
+    """A tail whose output has no fused consumer (here: a weighted sum, as before the pooling):
+    the backward recomputes y3 once and runs the ordinary BN backward + fold. Gradients of a2, W3,
+    gamma, beta and the residual vs the unfused conv3 -> bn3 module pair."""
+    from parameter_server_distributed_amd.ops import autotune, tail
+    from parameter_server_distributed_amd.ops.bn import FusedBatchNorm2d
+    from parameter_server_distributed_amd.ops.conv import Conv1x1
+
+    torch.manual_seed(1)
+    n, cin, cout, h = 4, 64, 256, 14
+    conv = Conv1x1(cin, cout).to(gpu).to(memory_format=torch.channels_last)
+    conv.weight.data = conv.weight.data.bfloat16()
+    bn = FusedBatchNorm2d(cout, relu=True).to(gpu)
+    nn.init.uniform_(bn.weight, 0.5, 1.5)
+    nn.init.uniform_(bn.bias, -0.2, 0.2)
+    bn.weight.data, bn.bias.data = bn.weight.data.bfloat16(), bn.bias.data.bfloat16()
+    a2 = torch.randn(n, cin, h, h, device=gpu).relu().bfloat16().contiguous(memory_format=torch.channels_last)
+    idt = torch.randn(n, cout, h, h, device=gpu).bfloat16().contiguous(memory_format=torch.channels_last)
+    r = torch.randn(n, cout, h, h, device=gpu).bfloat16()
+    res = []
+    for on in (True, False):
+        monkeypatch.setenv("PSD_TAIL_RECOMPUTE", "1" if on else "0")
+        autotune._DECISIONS.clear()
+        for k in tail.TAIL_CALLS:
+            tail.TAIL_CALLS[k] = 0
+        for p in (conv.weight, bn.weight, bn.bias):
+            p.grad = None
+        bn.running_mean.zero_()
+        bn.running_var.fill_(1)
+        x = a2.clone().requires_grad_(True)
+        i = idt.clone().requires_grad_(True)
+        if on:
+            assert tail.tail_ok(conv, bn, x, i)
+            y = tail.conv_bn_tail(conv, bn, x, i)
+        else:
+            y = bn(conv(x), i)
+        (y.float() * r.float()).sum().backward()
+        res.append([t.float().clone() for t in (y, x.grad, i.grad, conv.weight.grad, bn.weight.grad, bn.bias.grad,
+                                                 bn.running_mean, bn.running_var)])
+        if on:
+            assert tail.TAIL_CALLS == {"fwd": 1, "bwd_fused": 0, "bwd_recompute": 1}, tail.TAIL_CALLS
+    autotune._DECISIONS.clear()
+    names = ("y", "da2", "didt", "dW3", "dgamma", "dbeta", "running_mean", "running_var")
+    for nm, a, b in zip(names, res[0], res[1]):
+        rel = ((a - b).norm() / b.norm().clamp_min(1e-6)).item()
+        assert rel < 2e-2, (nm, rel)
