@@ -308,10 +308,14 @@ def main():
     mem_peak = torch.cuda.max_memory_allocated(dev)
 
     barrier()
+    step_log = os.environ.get("PSD_STEP_LOG", "0") == "1"  # host time of each step() call (diagnosis)
+    ts = []
     t0 = time.perf_counter()
     loss = None
     for _ in range(a.steps):
         loss = tr.step()
+        if step_log:
+            ts.append(time.perf_counter())
     torch.cuda.synchronize(dev)
     barrier()
     el = time.perf_counter() - t0
@@ -320,6 +324,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     ms = el / max(a.steps, 1) * 1e3
+    if step_log and rank == 0:
+        prev = t0
+        print("step host ms: " + " ".join(f"{(t - p) * 1e3:.1f}" for p, t in zip([t0] + ts[:-1], ts)), file=sys.stderr)
     if mode == "async":
         ps.drain()  # outside the timed region: every push of the run applied before reporting
     samples = a.batch * n_workers * a.steps

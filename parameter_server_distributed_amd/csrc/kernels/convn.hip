@@ -648,6 +648,124 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
 }
 
 
+// ------------------------------------------------------------------ persistent 1x1 (stride 1)
+// The 1x1 convolutions of the bottleneck ends (conv3 forward / statistics / BN-apply passes, conv1
+// bwd-data with the producing BN's reduction) have K = 64..512 against M = 0.8-3.2M rows: a
+// one-tile-per-workgroup launch of the kernel above is latency-bound there (the tail's
+// statistics-only pass over layer1, 0.4 GB of input, took 500 us: every workgroup waits for its
+// one DMA, computes 1-2 K-tiles and drains). Here a workgroup runs a contiguous run of 128-row
+// tiles through the same ring of K-tile slots: the ring keeps streaming across tile boundaries, so
+// the next tiles' A (and B) K-tiles land while this tile's MFMAs and epilogue run; the epilogue's
+// reductions accumulate over the run (one partial row per wave row per workgroup). A [M][C] with
+// row m the output pixel itself (and the K-concatenated x2 of the BN-backward fold).
+template <int BN, int WNT, int NSLOT, bool STATS, int BWD>
+__global__ __launch_bounds__(512) void convp_kernel(ConvnArgs a, int tiles_m) {
+  constexpr int BM = 128;
+  using G = Geo<BM, BN, WNT, NSLOT>;
+  constexpr int SLOTB = G::SLOT;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int n0 = blockIdx.y * BN;
+  const int gx = gridDim.x;
+  const int bq = xcd_remap(blockIdx.x, gx);  // a contiguous run of tiles per workgroup, XCD-grouped
+  const int t_begin = (int)(((int64_t)bq * tiles_m) / gx);
+  const int t_end = (int)(((int64_t)(bq + 1) * tiles_m) / gx);
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid / G::NWC, wc = wid % G::NWC;
+  const int cl = lane & 15;
+  float kshift[G::JN];
+#pragma unroll
+  for (int j = 0; j < G::JN; ++j) kshift[j] = 0.f;
+  if constexpr (STATS) {
+#pragma unroll
+    for (int j = 0; j < G::JN; ++j) kshift[j] = a.shift[n0 + wc * WNT + j * 16 + cl];
+  }
+  const rsrc_t xr = make_rsrc(a.x, a.xbytes);
+  const rsrc_t x2r = make_rsrc(a.x2 ? a.x2 : a.x, a.x2 ? a.x2bytes : 0u);
+  const rsrc_t wrs = make_rsrc(a.w, a.wbytes);
+  const int nslot = a.nslot;
+  const int nt = a.K / kBK;
+  const int total = (t_end - t_begin) * nt;
+  // K-tile T of the run: tile t_begin + T / nt, k-block T % nt
+  auto stage = [&](int T) {
+    uint8_t* slot = smem + (T % nslot) * SLOTB;
+    const int tile = t_begin + T / nt;
+    const int k0 = (T % nt) * kBK;
+    const int m0 = tile * BM;
+    const bool second = k0 >= a.K1;
+    const int c0 = second ? k0 - a.K1 : k0;
+    const int lc = second ? a.logC2 : a.logC;
+#pragma unroll
+    for (int i = 0; i < G::APW; ++i) {
+      const int piece = i * G::NW + wid;
+      const int row = piece * 8 + (lane >> 3);
+      const int kc = (lane & 7) ^ ((row >> 1) & 7);
+      const int m = m0 + row;
+      const uint32_t off = m < a.M ? ((((uint32_t)m) << lc) + (uint32_t)(c0 + kc * 8)) * 2u : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(second ? x2r : xr,
+                                               (__attribute__((address_space(3))) void*)(slot + piece * 1024), 16, off,
+                                               0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < G::BPW; ++i) {
+      const int piece = i * G::NW + wid;
+      const int row = piece * 8 + (lane >> 3);
+      const int kc = (lane & 7) ^ ((row >> 1) & 7);
+      const uint32_t off = ((uint32_t)(n0 + row) * (uint32_t)a.K + (uint32_t)(k0 + kc * 8)) * 2u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          wrs, (__attribute__((address_space(3))) void*)(slot + (SLOTB - BN * 128) + piece * 1024), 16, off, 0, 0, 0);
+    }
+  };
+  f32x4 acc[4][G::JN];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < G::JN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  EpiSums<G::JN> es;
+  es.zero();
+  uint8_t* stg = smem + nslot * SLOTB + wid * G::STG;
+  const int D = nslot - 1;  // K-tiles issued ahead (nslot >= 2)
+  for (int p = 0; p < D && p < total; ++p) stage(p);
+  for (int T = 0; T < total; ++T) {
+    wait_ahead<G::DPS, NSLOT - 2>(min(total - 1 - T, D - 1));
+    __builtin_amdgcn_s_barrier();  // every wave: K-tile T published, K-tile T-1 no longer read
+    __builtin_amdgcn_sched_barrier(0);
+    if (T + D < total) stage(T + D);
+    const uint8_t* As = smem + (T % nslot) * SLOTB;
+    const uint8_t* Bs = As + (SLOTB - BN * 128);
+    bf16x8 af[2][4], bf[2][G::JN];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int j = 0; j < G::JN; ++j) bf[ks][j] = frag(Bs, wc * G::JN + j, ks, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[ks][i] = frag(As, wr * 4 + i, ks, lane);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < G::JN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][i], bf[ks][j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (T % nt == nt - 1) {  // the tile's last K-tile: its epilogue (the ring keeps streaming underneath)
+      const int tile = t_begin + T / nt;
+      const int m0 = tile * BM;
+      auto pix = [&](int p) -> int { return m0 + p < a.M ? m0 + p : -1; };
+      convn_epilogue<BM, BN, WNT, STATS, BWD, true>(a, acc, kshift, tile, wr, wc, lane, stg, pix, n0, es);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < G::JN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      // the epilogue's stores / loads sit behind the ring's DMA in this wave's vmcnt: drain here, so
+      // the counted waits above only ever see K-tile DMA (issued a K-tile or more earlier: landed)
+      wait_vm<0>();
+    }
+  }
+  convn_flush<WNT, STATS, BWD>(a, es, (int64_t)blockIdx.x * G::WM + wr, wc, lane, n0);
+}
+
 // ------------------------------------------------------------------ persistent HALO (layer1 3x3)
 // The ResNet layer1 3x3 convolution (C = 64 -> N = 64, stride 1, pad 1, 56 x 56) and its bwd-data
 // run at ~20 % of the MFMA rate on the gathered kernel above: every K-tile re-gathers 128 input
@@ -737,11 +855,10 @@ __global__ __launch_bounds__(256) void convh_kernel(ConvnArgs a, int ntiles) {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
+    // the 12 fragments of one tap (A: 4 row blocks, B: 2 column blocks, 2 k-steps each)
+    auto load_tap = [&](int tap, bf16x8 (&af)[2][4], bf16x8 (&bf)[2][2]) {
       const int tr = tap / 3, ts = tap - tr * 3;
       const uint8_t* Bs = wlds + tap * 8192;
-      bf16x8 af[2][4], bf[2][2];
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
 #pragma unroll
@@ -754,13 +871,25 @@ __global__ __launch_bounds__(256) void convh_kernel(ConvnArgs a, int ntiles) {
           af[ks][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(win + hx_off(row, ks * 4 + (lane >> 4))));
         }
       }
+    };
+    // software pipeline over the taps: tap t+1's fragments are read while tap t's 16 MFMAs run (one
+    // wave per SIMD: nothing else hides the LDS latency; left to itself hipcc re-used 16 VGPRs and
+    // waited on the LDS before every MFMA pair)
+    bf16x8 fa[2][2][4], fb[2][2][2];
+    load_tap(0, fa[0], fb[0]);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int cb = tap & 1;
+      if (tap + 1 < 9) load_tap(tap + 1, fa[cb ^ 1], fb[cb ^ 1]);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][i], bf[ks][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[cb][ks][i], fb[cb][ks][j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
     }
     const int n = tile / tpi, ho0 = (tile - n * tpi) * 2;
     auto pix = [&](int p) -> int {
@@ -810,6 +939,89 @@ static hipError_t convh_launch(const ConvnArgs& a, hipStream_t st) {
   if (a.bwd == 3) return convh_launch_t<false, 3>(a, st);
   if (a.bwd == 5) return convh_launch_t<false, 5>(a, st);
   return a.part ? convh_launch_t<true, 0>(a, st) : convh_launch_t<false, 0>(a, st);
+}
+
+// ------------------------------------------------------------------ persistent 1x1: host side
+static int cu_count_cached() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  return cus;
+}
+
+// convp geometry per output-tile width: (WNT, waves, LDS bytes) -- NSLOT 3 ring
+template <int BN>
+struct P1Cfg;
+template <>
+struct P1Cfg<256> {
+  static constexpr int WNT = 64;
+};
+template <>
+struct P1Cfg<128> {
+  static constexpr int WNT = 32;
+};
+template <>
+struct P1Cfg<64> {
+  static constexpr int WNT = 32;
+};
+constexpr int kP1Slots = 3;
+template <int BN>
+constexpr int p1_lds() {
+  using G = Geo<128, BN, P1Cfg<BN>::WNT, kP1Slots>;
+  return kP1Slots * G::SLOT + G::NW * G::STG;
+}
+
+// workgroups along M: one round of the whole grid (column tiles x this) over the CUs at the
+// occupancy the LDS allows, never more than the M tiles
+static int convp_grid_x(int bn, int tiles_m, int tiles_n) {
+  const int lds = bn == 256 ? p1_lds<256>() : bn == 128 ? p1_lds<128>() : p1_lds<64>();
+  int per_cu = (160 * 1024) / lds;
+  if (per_cu < 1) per_cu = 1;
+  int g = cu_count_cached() * per_cu / (tiles_n > 0 ? tiles_n : 1);
+  if (g < 1) g = 1;
+  return g < tiles_m ? g : tiles_m;
+}
+
+template <int BN, bool STATS, int BWD>
+static hipError_t convp_launch_t(const ConvnArgs& a0, hipStream_t st) {
+  constexpr int WNT = P1Cfg<BN>::WNT;
+  using G = Geo<128, BN, WNT, kP1Slots>;
+  constexpr int LDS = p1_lds<BN>();
+  static_assert(LDS <= 160 * 1024, "LDS");
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)convp_kernel<BN, WNT, kP1Slots, STATS, BWD>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  ConvnArgs a = a0;
+  a.nslot = kP1Slots;
+  const int tiles_m = (a.M + 127) / 128, tiles_n = a.N / BN;
+  hipLaunchKernelGGL((convp_kernel<BN, WNT, kP1Slots, STATS, BWD>), dim3(convp_grid_x(BN, tiles_m, tiles_n), tiles_n),
+                     dim3(G::NT), LDS, st, a, tiles_m);
+  return hipGetLastError();
+}
+
+template <int BN>
+static hipError_t convp_launch_s(const ConvnArgs& a, hipStream_t st) {
+  if (a.bwd == 1) return convp_launch_t<BN, false, 1>(a, st);
+  if (a.bwd == 2) return convp_launch_t<BN, false, 2>(a, st);
+  if (a.bwd == 3) return convp_launch_t<BN, false, 3>(a, st);
+  if (a.bwd == 5) return convp_launch_t<BN, false, 5>(a, st);
+  if (a.bwd == 8) return convp_launch_t<BN, false, 8>(a, st);
+  return a.part ? convp_launch_t<BN, true, 0>(a, st) : convp_launch_t<BN, false, 0>(a, st);
+}
+
+static hipError_t convp_launch(const ConvnArgs& a, int bn, hipStream_t st) {
+  if (a.R != 1 || a.S != 1 || a.stride != 1 || a.pad != 0 || a.Ho != a.H || a.Wo != a.W) return hipErrorNotSupported;
+  if (bn == 256) return convp_launch_s<256>(a, st);
+  if (bn == 128) return convp_launch_s<128>(a, st);
+  return convp_launch_s<64>(a, st);
 }
 
 // ------------------------------------------------------------------ host side
@@ -870,13 +1082,19 @@ static constexpr int kHaloBm128[] = {128, 256};
 static int halo_count(int bn) { return bn == 256 ? 1 : bn == 128 ? 2 : 3; }
 // + the persistent HALO variant (convh_kernel) for the 64-wide outputs
 static int persist_count(int bn) { return bn == 64 ? 1 : 0; }
-static int convn_variant_count(int bn) { return plain_count(bn) + halo_count(bn) + persist_count(bn); }
-static bool is_persist(int bn, int v) { return v >= plain_count(bn) + halo_count(bn); }
+// + the persistent 1x1 variant (convp_kernel), every width
+static int p1_count(int bn) { return bn ? 1 : 0; }
+static int convn_variant_count(int bn) { return plain_count(bn) + halo_count(bn) + persist_count(bn) + p1_count(bn); }
+static bool is_persist(int bn, int v) {
+  const int b = plain_count(bn) + halo_count(bn);
+  return v >= b && v < b + persist_count(bn);
+}
+static bool is_p1(int bn, int v) { return v == plain_count(bn) + halo_count(bn) + persist_count(bn); }
 
 int convn_variant_kind(int N, int v) {
   const int bn = convn_tile_n(N);
   if (!bn || v < 0 || v >= convn_variant_count(bn)) return -1;
-  return v < plain_count(bn) ? 0 : is_persist(bn, v) ? 2 : 1;
+  return v < plain_count(bn) ? 0 : is_persist(bn, v) ? 2 : is_p1(bn, v) ? 3 : 1;
 }
 
 int convn_variants(int N) {
@@ -892,7 +1110,7 @@ static int default_variant(const ConvnArgs& a, int bn) {
 
 // BM of each variant (must match the dispatch in launch_convn)
 static int variant_bm(int bn, int v) {
-  if (is_persist(bn, v)) return 128;
+  if (is_persist(bn, v) || is_p1(bn, v)) return 128;
   const int h = v - plain_count(bn);
   if (h >= 0) return bn == 64 ? kHaloBm64[h] : bn == 128 ? kHaloBm128[h] : 128;
   if (bn == 64) return (v == 2 || v == 3) ? 256 : 128;
@@ -910,6 +1128,7 @@ bool convn_variant_ok(int N, int v, int R, int S, int stride, int pad, int Wo, b
   const int bn = convn_tile_n(N);
   if (!bn || v < 0 || v >= convn_variant_count(bn)) return false;
   if (v < plain_count(bn)) return true;
+  if (is_p1(bn, v)) return R == 1 && S == 1 && stride == 1 && pad == 0;
   if (is_persist(bn, v))  // (C = 64 and H = Ho are checked at launch: the predicate has no C)
     return !has_x2 && N == 64 && R == 3 && S == 3 && stride == 1 && pad == 1 && Wo + 2 <= 64;
   const int sw = halo_sw(Wo, R);
@@ -926,6 +1145,7 @@ int convn_part_rows_geo(int M, int N, int variant, int Ho, int Wo, int R) {
     if (Ho <= 0 || Wo <= 0) return 0;
     return 2 * convh_grid((M / (Ho * Wo)) * ((Ho + 1) / 2));
   }
+  if (is_p1(bn, variant)) return 2 * convp_grid_x(bn, (M + 127) / 128, N / bn);
   if (variant >= plain_count(bn)) {
     const int sw = halo_sw(Wo, R);
     if (!sw || Ho <= 0 || Wo <= 0) return 0;
@@ -960,6 +1180,7 @@ hipError_t launch_convn(const ConvnArgs& a_in, hipStream_t st) {
                                                 (a.bwd != 5 || (a.Ho % 2 == 0 && a.Wo % 2 == 0))))));
   if (!ok) return hipErrorNotSupported;
   const int v = a.variant >= 0 ? a.variant : default_variant(a, bn);
+  if (is_p1(bn, v)) return convp_launch(a, bn, st);
   if (is_persist(bn, v)) {
     if (!convh_ok(a) || a.bwd == 8 || !a.y) return hipErrorNotSupported;
     return convh_launch(a, st);

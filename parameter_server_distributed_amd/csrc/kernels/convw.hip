@@ -335,18 +335,31 @@ __global__ __launch_bounds__(256) void convhw_kernel(ConvwArgs a, int ntiles) {
     if (tile + 1 < t_end) stage(tile + 1, b ^ 1);  // lands under this tile's MFMA work
     const uint8_t* dyi = buf(b);
     const uint8_t* win = buf(b) + kHwDy;
+    // 4 k-steps of 32 output pixels (row j = ks / 2, slots (ks % 2) * 32 ..) x 9 taps = 36 steps of 4
+    // MFMAs, software-pipelined: the window fragment of step s + 2 and the dY fragments of the next
+    // k-step are read while step s's MFMAs run (one wave per SIMD: nothing else hides the LDS latency)
+    auto wfrag = [&](int st) {
+      const int ks = st / 9, t = st - ks * 9, r = t / 3, sx = t - r * 3;
+      return trfrag_rows(win, ((ks >> 1) + r) * 64 + (ks & 1) * 32 + sx, wid, lane);
+    };
+    bf16x8 af[2][4], bw[3];
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {  // 32 output pixels: row j = ks / 2, slots (ks % 2) * 32 ..
-      bf16x8 af[4];
+    for (int nb = 0; nb < 4; ++nb) af[0][nb] = trfrag_rows(dyi, 0, nb, lane);
+    bw[0] = wfrag(0);
+    bw[1] = wfrag(1);
 #pragma unroll
-      for (int nb = 0; nb < 4; ++nb) af[nb] = trfrag_rows(dyi, ks * 32, nb, lane);
+    for (int st = 0; st < 36; ++st) {
+      const int ks = st / 9, t = st - ks * 9;
+      if (st + 2 < 36) bw[(st + 2) % 3] = wfrag(st + 2);
+      if (t == 0 && ks + 1 < 4) {
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int r = t / 3, sx = t - r * 3;
-        const bf16x8 bfr = trfrag_rows(win, ((ks >> 1) + r) * 64 + (ks & 1) * 32 + sx, wid, lane);
-#pragma unroll
-        for (int nb = 0; nb < 4; ++nb) acc[t][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[nb], bfr, acc[t][nb], 0, 0, 0);
+        for (int nb = 0; nb < 4; ++nb) af[(ks + 1) & 1][nb] = trfrag_rows(dyi, (ks + 1) * 32, nb, lane);
       }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb)
+        acc[t][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks & 1][nb], bw[st % 3], acc[t][nb], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
     }
     wait_vm<0>();     // this wave's DMA of the next tile landed
     __syncthreads();  // every wave's: the next tile is complete and this one no longer read

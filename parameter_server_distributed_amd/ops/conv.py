@@ -222,14 +222,16 @@ def _variant_ok(cout: int, v: int, k: int, stride: int, pad: int, wo: int, cin: 
     """Variant v of the narrow kernel takes this shape. The plain HALO variants (kind 1) only with
     PSD_CONVN_HALO=1: on the ResNet-50 shapes they measured no faster than the gathered variants,
     profiles/convn_halo_r3.md, so by default they are not autotuned. The persistent HALO variant
-    (kind 2, C = N = 64 3x3 stride 1, H = Ho) is a candidate whenever its contract holds
-    (PSD_CONVN_PERSIST=0: off, A/B)."""
+    (kind 2, C = N = 64 3x3 stride 1, H = Ho) and the persistent 1x1 variant (kind 3) are
+    candidates whenever their contract holds (PSD_CONVN_PERSIST=0 / PSD_CONVN_P1=0: off, A/B)."""
     C = _native()
     if not C.convn_variant_ok(cout, v, k, k, stride, pad, wo):
         return False
     kind = C.convn_variant_kind(cout, v)
     if kind == 2:
         return _at.enabled("PSD_CONVN_PERSIST") and cin == 64 and (h is None or h == wo)
+    if kind == 3:  # persistent 1x1 (convp_kernel)
+        return _at.enabled("PSD_CONVN_P1")
     return kind == 0 or os.environ.get("PSD_CONVN_HALO", "0") == "1"
 
 
@@ -403,7 +405,10 @@ def _convw_cands(dy, x, k: int, stride: int, pad: int) -> dict:
             return o.view(cout, k, k, cin).permute(0, 3, 1, 2)
         return fn
 
-    return {f"psdw{v}": make(v) for v in range(C.convw_variants(cout, kk))}
+    nv = C.convw_variants(cout, kk)
+    if cout == 64 and kk == 576 and not _at.enabled("PSD_CONVW_PERSIST"):
+        nv -= 1  # the persistent HALO wgrad is the last variant of this shape (A/B switch)
+    return {f"psdw{v}": make(v) for v in range(nv)}
 
 
 class DelayedScale:

@@ -30,8 +30,6 @@ bottleneck tail ResNet-50 training needs.
 """
 from __future__ import annotations
 
-import os
-
 import torch
 
 from . import autotune as _at
@@ -46,7 +44,7 @@ TAIL_CALLS = {"fwd": 0, "bwd_fused": 0, "bwd_recompute": 0}
 def tail_ok(conv, bn, a2: torch.Tensor, idt: torch.Tensor) -> bool:
     """The recomputing tail applies: a bf16 Conv1x1 (no fp8) into a training ReLU FusedBatchNorm2d
     with an identity residual, channels_last operands, a shape the narrow kernel and the fold take."""
-    if os.environ.get("PSD_TAIL_RECOMPUTE", "0") != "1" or not isinstance(conv, Conv1x1) or conv.fp8:
+    if not _at.enabled("PSD_TAIL_RECOMPUTE") or not isinstance(conv, Conv1x1) or conv.fp8:
         return False
     if not isinstance(bn, FusedBatchNorm2d) or not bn.relu or not bn.training or bn.weight is None:
         return False
@@ -83,7 +81,7 @@ def _variant(a2, w2, M: int, cin: int, cout: int, h: int, w: int, shift) -> int:
         return fn
 
     cands = {f"psdn{v}": make(v) for v in range(C.convn_variants(cout))
-             if C.convn_variant_kind(cout, v) == 0 and C.convn_variant_ok(cout, v, 1, 1, 1, 0, w)}
+             if C.convn_variant_kind(cout, v) in (0, 3) and C.convn_variant_ok(cout, v, 1, 1, 1, 0, w)}
     how = _at.choose(("tail", "conv1x1_bn_res_relu", M, cin, cout), cands, next(iter(cands)))
     return int(how[4:])
 

@@ -222,11 +222,15 @@ class AsyncPS:
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for _, p, _o, _n in layout]
         self._next = 0
         if self.is_cuda:
-            # push copies alternate over two streams (bucket i on stream i % 2), so two buckets'
-            # DMAs -- to different owners' links, or one large bucket after another -- can be in
-            # flight together; the commit waits for both
+            # push copies on PSD_ASYNC_PUSH_STREAMS streams (bucket i on stream i % n; the commit
+            # waits for all). Default 1: HIP maps a process's streams onto GPU_MAX_HW_QUEUES = 4
+            # hardware queues, and compute + engine apply + push + pull already take four -- a fifth
+            # stream shares a queue with one of them and serialises behind its work (ResNet-50
+            # b1024 async S = 1: 91-95 ms/step with two push streams vs 78 ms synchronous,
+            # gpurun_out/adiag2). 2+ only where the copies of several owners' links must overlap.
             self.comm_stream = torch.cuda.Stream(device=dev)
-            self.comm_streams = [self.comm_stream, torch.cuda.Stream(device=dev)]
+            n_push = max(1, int(os.environ.get("PSD_ASYNC_PUSH_STREAMS", "1")))
+            self.comm_streams = [self.comm_stream] + [torch.cuda.Stream(device=dev) for _ in range(n_push - 1)]
             self.pull_stream = torch.cuda.Stream(device=dev)
             self.push_done = [None, None]
             self.step_done = [None, None]  # end of a step's work on the compute stream, per buffer

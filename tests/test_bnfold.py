@@ -271,3 +271,53 @@ def test_chain_fusions_vs_fp32(gpu, monkeypatch, kind):
     for n in ef:
         assert ef[n] < 0.15, (n, ef[n], el[n])
         assert ef[n] <= 1.15 * el[n] + 3e-3, (n, ef[n], el[n])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows,C", [(300, 64), (5000, 64), (20011, 256), (777, 2048)])
+def test_fold_finalize_many_partial_rows(gpu, rows, C):
+    """BN finalize from many producer partial rows (> 512: the ticketed one-launch fold + finalize,
+    kernels/bn.hip bn_fold_finalize_kernel) vs fp64 sums of the same partials: forward (mean,
+    invstd, scale / shift, running statistics) and backward (dgamma, dbeta, coefficients). Run
+    twice in a row: the ticket counters must be back at zero for the next launch."""
+    from parameter_server_distributed_amd import native as _n
+    C_ = _n()
+    g = torch.Generator().manual_seed(rows)
+    M = rows * 64
+    part = torch.randn(rows, 2, C, generator=g)
+    part[:, 1] = part[:, 1].abs() * 4 + 64  # sum of squares: positive, variance > 0
+    gamma = (torch.rand(C, generator=g) + 0.5).bfloat16()
+    beta = (torch.rand(C, generator=g) - 0.5).bfloat16()
+    k = torch.randn(C, generator=g) * 0.1
+    s = part[:, 0].double().sum(0)
+    q = part[:, 1].double().sum(0)
+    ms = s / M
+    var = (q / M - ms * ms).clamp_min(0)
+    mean = ms + k.double()
+    invstd = 1.0 / torch.sqrt(var + 1e-5)
+    for rep in range(2):
+        rm, rv = k.clone().to(gpu), torch.ones(C, device=gpu)
+        mu, ist, ss = C_.bn_finalize(part.to(gpu), rows, M, gamma.to(gpu), beta.to(gpu), rm, rv, 0.1, 1e-5)
+        torch.testing.assert_close(mu.double().cpu(), mean, rtol=1e-5, atol=1e-5, msg=lambda m: f"rep {rep}: {m}")
+        torch.testing.assert_close(ist.double().cpu(), invstd, rtol=1e-4, atol=1e-5)
+        sc = gamma.double() * invstd
+        torch.testing.assert_close(ss[:C].double().cpu(), sc, rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(ss[C:].double().cpu(), beta.double() - mean * sc, rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(rm.double().cpu(), 0.9 * k.double() + 0.1 * mean, rtol=1e-5, atol=1e-5)
+    # backward: part rows (sum g, sum g (x - mean))
+    gm = torch.randn(C, generator=g)
+    gi = torch.rand(C, generator=g) + 0.5
+    xdummy = torch.zeros(1, C, 1, M, device=gpu, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    for rep in range(2):
+        _, coef, dgam, dbet = C_.bn_bwd_coef(xdummy, xdummy, gamma.to(gpu), gm.to(gpu), gi.to(gpu), part=part.to(gpu),
+                                             rows=rows)
+        s1, s2 = s, q
+        torch.testing.assert_close(dbet.double().cpu(), s1, rtol=1e-2, atol=1e-2)
+        torch.testing.assert_close(dgam.double().cpu(), s2 * gi.double(), rtol=1e-2, atol=1e-2)
+        k1 = gamma.double() * gi.double()
+        k3 = s2 * gi.double() ** 2 / M
+        k2 = s1 / M
+        torch.testing.assert_close(coef[:C].double().cpu(), k1, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(coef[C:2 * C].double().cpu(), -k1 * k3, rtol=1e-4, atol=1e-6)
+        torch.testing.assert_close(coef[2 * C:].double().cpu(), -k1 * k2 + k1 * k3 * gm.double(), rtol=1e-4,
+                                   atol=1e-5)
