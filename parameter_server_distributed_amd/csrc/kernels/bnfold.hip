@@ -39,43 +39,62 @@ __global__ __launch_bounds__(256) void bnfold_prep_kernel(const uint16_t* __rest
   if (threadIdx.x == 0) bvec[j] = red[0];
 }
 
-// dW[c][i] = A_c P[c][i] + B_c sum_k W[c][k] P[Cout + k][i] + C_c P[Cout + Wd][i]. Block = 32 output
-// rows x 256 columns (one per lane): the 32 weight rows are staged in LDS (broadcast reads), each
-// G = x^T x element loaded once feeds 32 FMAs. (8 rows per block with every block streaming all of
-// G: 67 us per call on average, 0.9 ms per ResNet-50 step -- profiles/resnet50 s4 trace.)
-constexpr int kCombRows = 32;
-constexpr int kCombCols = 256;
+// dW[c][i] = A_c P[c][i] + B_c sum_k W[c][k] G[k][i] + C_c s[i]  (G = P[Cout:Cout+Wd] = x^T x,
+// s = P[Cout+Wd] = 1^T x). The W G product is a small fp32 GEMM: 64 x 64 output tiles, k in chunks of
+// 32 staged through LDS (W transposed, so a thread's 4 rows are one float4), 4 x 4 outputs per lane
+// (16 FMAs per two LDS reads). The row-per-lane version streamed G once per 8 (later 32) output
+// rows from L2 and issued one LDS read per FMA: 67-111 us per call, 0.9-1.4 ms per ResNet-50 step
+// (profiles/resnet50_b1024_r4_kernels.md).
+constexpr int kCT = 64, kCK = 32;
 __global__ __launch_bounds__(256) void bnfold_combine_kernel(const float* __restrict__ P, const uint16_t* __restrict__ W,
                                                              const float* __restrict__ coef, int Cout, int Wd,
                                                              uint16_t* __restrict__ out, int accumulate) {
-  extern __shared__ float wrow[];  // [kCombRows][Wd]
-  const int c0 = blockIdx.x * kCombRows;
-  for (int e = threadIdx.x; e < kCombRows * Wd; e += blockDim.x) {
-    const int r = e / Wd, k = e - r * Wd;
-    wrow[e] = c0 + r < Cout ? bf16_to_f32(W[(int64_t)(c0 + r) * Wd + k]) : 0.f;
-  }
-  __syncthreads();
-  const int i = blockIdx.y * kCombCols + threadIdx.x;
-  if (i >= Wd) return;
+  __shared__ __attribute__((aligned(16))) float ws[kCK][kCT];  // W^T chunk: ws[k][r]
+  __shared__ __attribute__((aligned(16))) float gs[kCK][kCT];  // G chunk: gs[k][i]
+  const int r0 = blockIdx.x * kCT, i0 = blockIdx.y * kCT;
+  const int tr = threadIdx.x >> 4, tc = threadIdx.x & 15;
   const float* G = P + (int64_t)Cout * Wd;
   const float* s = G + (int64_t)Wd * Wd;
-  float t[kCombRows];
+  float t[4][4];
 #pragma unroll
-  for (int r = 0; r < kCombRows; ++r) t[r] = 0.f;
-  for (int k = 0; k < Wd; ++k) {
-    const float gk = G[(int64_t)k * Wd + i];
+  for (int a = 0; a < 4; ++a)
 #pragma unroll
-    for (int r = 0; r < kCombRows; ++r) t[r] = fmaf(wrow[r * Wd + k], gk, t[r]);
+    for (int b = 0; b < 4; ++b) t[a][b] = 0.f;
+  for (int k0 = 0; k0 < Wd; k0 += kCK) {
+    for (int e = threadIdx.x; e < kCK * kCT; e += 256) {
+      const int r = e / kCK, k = e - r * kCK;  // consecutive lanes: consecutive k of one W row
+      ws[k][r] = (r0 + r < Cout && k0 + k < Wd) ? bf16_to_f32(W[(int64_t)(r0 + r) * Wd + k0 + k]) : 0.f;
+    }
+    for (int e = threadIdx.x; e < kCK * kCT; e += 256) {
+      const int k = e / kCT, i = e - k * kCT;
+      gs[k][i] = (k0 + k < Wd && i0 + i < Wd) ? G[(int64_t)(k0 + k) * Wd + i0 + i] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int k = 0; k < kCK; ++k) {
+      const float4 wa = *reinterpret_cast<const float4*>(&ws[k][tr * 4]);
+      const float4 gb = *reinterpret_cast<const float4*>(&gs[k][tc * 4]);
+      const float wv[4] = {wa.x, wa.y, wa.z, wa.w}, gv[4] = {gb.x, gb.y, gb.z, gb.w};
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) t[a][b] = fmaf(wv[a], gv[b], t[a][b]);
+    }
+    __syncthreads();
   }
-  const float si = s[i];
 #pragma unroll
-  for (int r = 0; r < kCombRows; ++r) {
-    const int c = c0 + r;
+  for (int a = 0; a < 4; ++a) {
+    const int c = r0 + tr * 4 + a;
     if (c >= Cout) break;
-    float v = coef[c] * P[(int64_t)c * Wd + i] + coef[Cout + c] * t[r] + coef[2 * Cout + c] * si;
-    uint16_t* o = out + (int64_t)c * Wd + i;
-    if (accumulate) v += bf16_to_f32(*o);
-    *o = f32_to_bf16(v);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int i = i0 + tc * 4 + b;
+      if (i >= Wd) break;
+      float v = coef[c] * P[(int64_t)c * Wd + i] + coef[Cout + c] * t[a][b] + coef[2 * Cout + c] * s[i];
+      uint16_t* o = out + (int64_t)c * Wd + i;
+      if (accumulate) v += bf16_to_f32(*o);
+      *o = f32_to_bf16(v);
+    }
   }
 }
 
@@ -119,9 +138,9 @@ hipError_t launch_bnfold_prep(const uint16_t* W, const float* coef, int Cout, in
 
 hipError_t launch_bnfold_combine(const float* P, const uint16_t* W, const float* coef, int Cout, int Wd,
                                  uint16_t* out, int accumulate, hipStream_t st) {
-  if (Cout <= 0 || Wd <= 0 || Wd > 512) return hipErrorInvalidValue;  // (LDS: 32 rows x Wd fp32 <= 64 KiB)
-  hipLaunchKernelGGL(bnfold_combine_kernel, dim3((Cout + kCombRows - 1) / kCombRows, (Wd + kCombCols - 1) / kCombCols),
-                     dim3(256), kCombRows * Wd * sizeof(float), st, P, W, coef, Cout, Wd, out, accumulate);
+  if (Cout <= 0 || Wd <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bnfold_combine_kernel, dim3((Cout + kCT - 1) / kCT, (Wd + kCT - 1) / kCT), dim3(256), 0, st, P, W,
+                     coef, Cout, Wd, out, accumulate);
   return hipGetLastError();
 }
 

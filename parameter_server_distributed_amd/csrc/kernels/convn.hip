@@ -758,9 +758,11 @@ __global__ __launch_bounds__(512) void convp_kernel(ConvnArgs a, int tiles_m) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < G::JN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      // the epilogue's stores / loads sit behind the ring's DMA in this wave's vmcnt: drain here, so
-      // the counted waits above only ever see K-tile DMA (issued a K-tile or more earlier: landed)
-      wait_vm<0>();
+      // (no drain: the epilogue's stores and loads also count in vmcnt, but loads return in issue
+      // order, so "at most (D - 1) * DPS outstanding" above still means at most that many LOADS --
+      // the K-tile DMA issued after K-tile T+1's -- are in flight: K-tile T+1 has landed. Stores
+      // still pending only make that wait longer, never short. A full drain here cost the stats-only
+      // pass its whole prefetch: 372 us vs ~100 for its 0.4 GB, profiles/resnet50_b1024_r4_kernels.md)
     }
   }
   convn_flush<WNT, STATS, BWD>(a, es, (int64_t)blockIdx.x * G::WM + wr, wc, lane, n0);
@@ -896,8 +898,10 @@ __global__ __launch_bounds__(256) void convh_kernel(ConvnArgs a, int ntiles) {
       const int j = p >> 6, wo = p & 63;
       return ((wo < a.Wo) & (ho0 + j < a.Ho)) ? (n * a.Ho + ho0 + j) * a.Wo + wo : -1;
     };
+    // this wave's DMA of the next window landed (issued before the taps: nothing to wait for by
+    // now) -- BEFORE the epilogue, so the drain never waits on the epilogue's own stores
+    wait_vm<0>();
     convn_epilogue<128, 64, 32, STATS, BWD, true>(a, acc, kshift, tile, wr, wc, lane, stg, pix, 0, es);
-    wait_vm<0>();     // this wave's DMA of the next window (and the epilogue's loads) landed
     __syncthreads();  // every wave's: the next window is complete and this one no longer read
   }
   convn_flush<32, STATS, BWD>(a, es, (int64_t)blockIdx.x * 2 + wr, wc, lane, 0);

@@ -62,6 +62,6 @@ def probe_p2p(dev: torch.device, sizes_mb=(1, 2, 4, 8, 16, 32, 64), iters: int =
         torch.cuda.synchronize(dev)
         el = torch.tensor([(time.perf_counter() - t0) / iters], device=dev, dtype=torch.float64)
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
-        out[mb] = round(n * 2 / float(el.item()) / 1e9, 1)
+        out[mb] = float(f"{n * 2 / float(el.item()) / 1e9:.3g}")  # (3 significant digits: a slow gloo link is not 0)
         del a, b
     return out

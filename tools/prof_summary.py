@@ -65,8 +65,8 @@ def main():
 
 CATEGORIES = [
     ("psd: batchnorm", r"psd::bn_"),
-    ("psd: narrow conv (convn)", r"psd::convn_kernel"),
-    ("psd: narrow conv wgrad (convw)", r"psd::convw_"),
+    ("psd: narrow conv (convn / convp / convh)", r"psd::conv[nph]_kernel"),
+    ("psd: narrow conv wgrad (convw / convhw)", r"psd::convh?w_"),
     ("psd: gemm", r"psd::.*(gemm|colsum|splitk)"),
     ("psd: fp8 quantise / amax", r"psd::.*(quant|amax|requant)"),
     ("psd: optimizer / PS apply", r"psd::.*(fused_apply|optim|multi_reduce|pack_cast|f32_to_bf16)"),
