@@ -268,8 +268,12 @@ __global__ __launch_bounds__(512) void convw_kernel(ConvwArgs a) {
 //     slab reduce (gemm.hip) sums the workgroups and writes bf16 dW.
 constexpr int kHwDy = 128 * 128;       // dY tile: 128 slots x 64 channels bf16
 constexpr int kHwWin = 4 * 64 * 128;   // input window
+// buffer = [window | dY]: the last k-step's taps read up to 2 rows past the 4-row window, i.e. the
+// first rows of the SAME buffer's dY tile (staged by the same DMA: finite) -- those products meet dY
+// rows of padding slots, which are 0. (dY first put the overrun into the other buffer, or past the
+// end, where uninitialised LDS holding a NaN pattern made 0 x NaN = NaN in valid gradient entries.)
 constexpr int kHwBuf = kHwDy + kHwWin;
-constexpr int kHwLds = 2 * kHwBuf + 1024;  // + the tap overrun past the last window row
+constexpr int kHwLds = 2 * kHwBuf;
 
 // transpose-read fragment of rows rbase + 8g + q (and + 4) of a pixel-major [rows][64 ch] image,
 // channel block cb (lane -> channel cb*16 + (lane & 15))
@@ -304,8 +308,8 @@ __global__ __launch_bounds__(256) void convhw_kernel(ConvwArgs a, int ntiles) {
       const int kc = (lane & 7) ^ swz(row);
       const bool ok = ws < a.Wo && ho0 + j < a.Ho;
       const uint32_t off = ok ? ((uint32_t)(((n * a.Ho + ho0 + j) * a.Wo + ws)) * 64u + (uint32_t)(kc * 8)) * 2u : kOOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(dyr, (__attribute__((address_space(3))) void*)(buf(b) + pc * 1024), 16,
-                                               off, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(dyr, (__attribute__((address_space(3))) void*)(buf(b) + kHwWin + pc * 1024),
+                                               16, off, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {  // window: rows ho0-1 .. ho0+2, slot ws = input column ws - 1
@@ -316,8 +320,8 @@ __global__ __launch_bounds__(256) void convhw_kernel(ConvwArgs a, int ntiles) {
       const int kc = (lane & 7) ^ swz(row);
       const bool ok = (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
       const uint32_t off = ok ? ((uint32_t)((n * a.H + hi) * a.W + wi) * 64u + (uint32_t)(kc * 8)) * 2u : kOOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(buf(b) + kHwDy + pc * 1024),
-                                               16, off, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(buf(b) + pc * 1024), 16,
+                                               off, 0, 0, 0);
     }
   };
   f32x4 acc[9][4];
@@ -333,8 +337,8 @@ __global__ __launch_bounds__(256) void convhw_kernel(ConvwArgs a, int ntiles) {
   for (int tile = t_begin, it = 0; tile < t_end; ++tile, ++it) {
     const int b = it & 1;
     if (tile + 1 < t_end) stage(tile + 1, b ^ 1);  // lands under this tile's MFMA work
-    const uint8_t* dyi = buf(b);
-    const uint8_t* win = buf(b) + kHwDy;
+    const uint8_t* win = buf(b);
+    const uint8_t* dyi = buf(b) + kHwWin;
     // 4 k-steps of 32 output pixels (row j = ks / 2, slots (ks % 2) * 32 ..) x 9 taps = 36 steps of 4
     // MFMAs, software-pipelined: the window fragment of step s + 2 and the dY fragments of the next
     // k-step are read while step s's MFMAs run (one wave per SIMD: nothing else hides the LDS latency)
