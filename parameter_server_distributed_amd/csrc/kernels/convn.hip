@@ -768,6 +768,120 @@ __global__ __launch_bounds__(512) void convp_kernel(ConvnArgs a, int tiles_m) {
   convn_flush<WNT, STATS, BWD>(a, es, (int64_t)blockIdx.x * G::WM + wr, wc, lane, n0);
 }
 
+// Resident-B form (K <= 128 with the weight tile [BN][K] kept in LDS): the ring carries the A
+// K-tiles only (16 KiB each), up to kPrMaxSlots deep. With K = 64 and BN = 256 the streamed form
+// re-DMA'd the 32 KiB weight tile for every 16 KiB of input and kept 2 tiles in flight: the tail's
+// statistics-only pass over layer1 ran at 1.4 TB/s of input (288 us, profiles/tail_passes_r4.md).
+constexpr int kPrMaxSlots = 6;
+template <int BN, int WNT, bool STATS, int BWD>
+__global__ __launch_bounds__(512) void convpr_kernel(ConvnArgs a, int tiles_m) {
+  constexpr int BM = 128;
+  using G = Geo<BM, BN, WNT, 3>;
+  constexpr int AB = BM * 128;  // one A K-tile
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int n0 = blockIdx.y * BN;
+  const int gx = gridDim.x;
+  const int bq = xcd_remap(blockIdx.x, gx);
+  const int t_begin = (int)(((int64_t)bq * tiles_m) / gx);
+  const int t_end = (int)(((int64_t)(bq + 1) * tiles_m) / gx);
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid / G::NWC, wc = wid % G::NWC;
+  const int cl = lane & 15;
+  float kshift[G::JN];
+#pragma unroll
+  for (int j = 0; j < G::JN; ++j) kshift[j] = 0.f;
+  if constexpr (STATS) {
+#pragma unroll
+    for (int j = 0; j < G::JN; ++j) kshift[j] = a.shift[n0 + wc * WNT + j * 16 + cl];
+  }
+  const rsrc_t xr = make_rsrc(a.x, a.xbytes);
+  const rsrc_t x2r = make_rsrc(a.x2 ? a.x2 : a.x, a.x2 ? a.x2bytes : 0u);
+  const rsrc_t wrs = make_rsrc(a.w, a.wbytes);
+  const int nslot = a.nslot;
+  const int nt = a.K / kBK;
+  uint8_t* bres = smem;                              // [nt][BN rows x 128 B] resident weights
+  uint8_t* ring = smem + nt * BN * 128;              // nslot A K-tiles
+  uint8_t* stg = ring + nslot * AB + wid * G::STG;   // this wave's epilogue staging
+  // the weight tile of every K-tile, once (BN / 8 pieces of 1 KiB per K-tile over the waves)
+  for (int pc = wid; pc < nt * (BN / 8); pc += G::NW) {
+    const int kt = pc / (BN / 8), rp = pc - kt * (BN / 8);
+    const int row = rp * 8 + (lane >> 3);
+    const int kc = (lane & 7) ^ ((row >> 1) & 7);
+    const uint32_t off = ((uint32_t)(n0 + row) * (uint32_t)a.K + (uint32_t)(kt * kBK + kc * 8)) * 2u;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)(bres + pc * 1024), 16, off, 0,
+                                             0, 0);
+  }
+  wait_vm<0>();  // (the weights land before the ring's counted waits start)
+  const int total = (t_end - t_begin) * nt;
+  auto stage = [&](int T) {
+    uint8_t* slot = ring + (T % nslot) * AB;
+    const int tile = t_begin + T / nt;
+    const int k0 = (T % nt) * kBK;
+    const int m0 = tile * BM;
+    const bool second = k0 >= a.K1;
+    const int c0 = second ? k0 - a.K1 : k0;
+    const int lc = second ? a.logC2 : a.logC;
+#pragma unroll
+    for (int i = 0; i < G::APW; ++i) {
+      const int piece = i * G::NW + wid;
+      const int row = piece * 8 + (lane >> 3);
+      const int kc = (lane & 7) ^ ((row >> 1) & 7);
+      const int m = m0 + row;
+      const uint32_t off = m < a.M ? ((((uint32_t)m) << lc) + (uint32_t)(c0 + kc * 8)) * 2u : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(second ? x2r : xr,
+                                               (__attribute__((address_space(3))) void*)(slot + piece * 1024), 16, off,
+                                               0, 0, 0);
+    }
+  };
+  f32x4 acc[4][G::JN];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < G::JN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  EpiSums<G::JN> es;
+  es.zero();
+  const int D = nslot - 1;
+  for (int p = 0; p < D && p < total; ++p) stage(p);
+  for (int T = 0; T < total; ++T) {
+    // K-tile T landed: at most (D - 1) later K-tiles' A DMA in flight (loads return in issue order;
+    // the epilogue's stores in the count only lengthen the wait)
+    wait_ahead<G::APW, kPrMaxSlots - 2>(min(total - 1 - T, D - 1));
+    __builtin_amdgcn_s_barrier();  // every wave: K-tile T published, K-tile T-1 no longer read
+    __builtin_amdgcn_sched_barrier(0);
+    if (T + D < total) stage(T + D);
+    const uint8_t* As = ring + (T % nslot) * AB;
+    const uint8_t* Bs = bres + (T % nt) * BN * 128;
+    bf16x8 af[2][4], bf[2][G::JN];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int j = 0; j < G::JN; ++j) bf[ks][j] = frag(Bs, wc * G::JN + j, ks, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[ks][i] = frag(As, wr * 4 + i, ks, lane);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < G::JN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][i], bf[ks][j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (T % nt == nt - 1) {
+      const int tile = t_begin + T / nt;
+      const int m0 = tile * BM;
+      auto pix = [&](int p) -> int { return m0 + p < a.M ? m0 + p : -1; };
+      convn_epilogue<BM, BN, WNT, STATS, BWD, true>(a, acc, kshift, tile, wr, wc, lane, stg, pix, n0, es);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < G::JN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  convn_flush<WNT, STATS, BWD>(a, es, (int64_t)blockIdx.x * G::WM + wr, wc, lane, n0);
+}
+
 // ------------------------------------------------------------------ persistent HALO (layer1 3x3)
 // The ResNet layer1 3x3 convolution (C = 64 -> N = 64, stride 1, pad 1, 56 x 56) and its bwd-data
 // run at ~20 % of the MFMA rate on the gathered kernel above: every K-tile re-gathers 128 input
@@ -981,11 +1095,11 @@ constexpr int p1_lds() {
 
 // workgroups along M: one round of the whole grid (column tiles x this) over the CUs at the
 // occupancy the LDS allows, never more than the M tiles
-static int convp_grid_x(int bn, int tiles_m, int tiles_n) {
-  const int lds = bn == 256 ? p1_lds<256>() : bn == 128 ? p1_lds<128>() : p1_lds<64>();
-  int per_cu = (160 * 1024) / lds;
-  if (per_cu < 1) per_cu = 1;
-  int g = cu_count_cached() * per_cu / (tiles_n > 0 ? tiles_n : 1);
+// workgroups along M: one workgroup per CU over the whole grid (column tiles x this), never more
+// than the M tiles -- both forms run one 512-thread workgroup per CU (LDS), and the partial-row
+// count (convn_part_rows) must not depend on which form the launch takes
+static int convp_grid_x(int tiles_m, int tiles_n) {
+  int g = cu_count_cached() / (tiles_n > 0 ? tiles_n : 1);
   if (g < 1) g = 1;
   return g < tiles_m ? g : tiles_m;
 }
@@ -1006,13 +1120,55 @@ static hipError_t convp_launch_t(const ConvnArgs& a0, hipStream_t st) {
   ConvnArgs a = a0;
   a.nslot = kP1Slots;
   const int tiles_m = (a.M + 127) / 128, tiles_n = a.N / BN;
-  hipLaunchKernelGGL((convp_kernel<BN, WNT, kP1Slots, STATS, BWD>), dim3(convp_grid_x(BN, tiles_m, tiles_n), tiles_n),
+  hipLaunchKernelGGL((convp_kernel<BN, WNT, kP1Slots, STATS, BWD>), dim3(convp_grid_x(tiles_m, tiles_n), tiles_n),
                      dim3(G::NT), LDS, st, a, tiles_m);
   return hipGetLastError();
 }
 
+// resident-B LDS: weights nt * BN * 128 + ring slots x 16 KiB + staging; 0 when even 3 slots do
+// not fit (then the streamed ring)
+template <int BN>
+static int pr_slots(int K) {
+  using G = Geo<128, BN, P1Cfg<BN>::WNT, 3>;
+  const int fixed = (K / kBK) * BN * 128 + G::NW * G::STG;
+  int ns = (160 * 1024 - fixed) / (128 * 128);
+  if (ns > kPrMaxSlots) ns = kPrMaxSlots;
+  return ns >= 3 ? ns : 0;
+}
+
+template <int BN, bool STATS, int BWD>
+static hipError_t convpr_launch_t(const ConvnArgs& a0, int ns, hipStream_t st) {
+  constexpr int WNT = P1Cfg<BN>::WNT;
+  using G = Geo<128, BN, WNT, 3>;
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)convpr_kernel<BN, WNT, STATS, BWD>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  ConvnArgs a = a0;
+  a.nslot = ns;
+  const int lds = (a.K / kBK) * BN * 128 + ns * 128 * 128 + G::NW * G::STG;
+  const int tiles_m = (a.M + 127) / 128, tiles_n = a.N / BN;
+  hipLaunchKernelGGL((convpr_kernel<BN, WNT, STATS, BWD>), dim3(convp_grid_x(tiles_m, tiles_n), tiles_n),
+                     dim3(G::NT), lds, st, a, tiles_m);
+  return hipGetLastError();
+}
+
+template <int BN>
+static hipError_t convpr_launch_s(const ConvnArgs& a, int ns, hipStream_t st) {
+  if (a.bwd == 1) return convpr_launch_t<BN, false, 1>(a, ns, st);
+  if (a.bwd == 2) return convpr_launch_t<BN, false, 2>(a, ns, st);
+  if (a.bwd == 3) return convpr_launch_t<BN, false, 3>(a, ns, st);
+  if (a.bwd == 5) return convpr_launch_t<BN, false, 5>(a, ns, st);
+  if (a.bwd == 8) return convpr_launch_t<BN, false, 8>(a, ns, st);
+  return a.part ? convpr_launch_t<BN, true, 0>(a, ns, st) : convpr_launch_t<BN, false, 0>(a, ns, st);
+}
+
 template <int BN>
 static hipError_t convp_launch_s(const ConvnArgs& a, hipStream_t st) {
+  if (const int ns = pr_slots<BN>(a.K)) return convpr_launch_s<BN>(a, ns, st);
   if (a.bwd == 1) return convp_launch_t<BN, false, 1>(a, st);
   if (a.bwd == 2) return convp_launch_t<BN, false, 2>(a, st);
   if (a.bwd == 3) return convp_launch_t<BN, false, 3>(a, st);
@@ -1149,7 +1305,7 @@ int convn_part_rows_geo(int M, int N, int variant, int Ho, int Wo, int R) {
     if (Ho <= 0 || Wo <= 0) return 0;
     return 2 * convh_grid((M / (Ho * Wo)) * ((Ho + 1) / 2));
   }
-  if (is_p1(bn, variant)) return 2 * convp_grid_x(bn, (M + 127) / 128, N / bn);
+  if (is_p1(bn, variant)) return 2 * convp_grid_x((M + 127) / 128, N / bn);
   if (variant >= plain_count(bn)) {
     const int sw = halo_sw(Wo, R);
     if (!sw || Ho <= 0 || Wo <= 0) return 0;
