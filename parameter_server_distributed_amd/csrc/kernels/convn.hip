@@ -262,32 +262,38 @@ __device__ __forceinline__ void convn_epilogue(const ConvnArgs& a, f32x4 (&acc)[
     }
   }
   if constexpr (STATS) {
-    // the statistics of the stored (bf16-rounded) values: one paired conversion, two unpacks. A
-    // 16-row block whose last row is valid is valid throughout (pix is monotone within a block):
-    // the wave-uniform test skips the per-row masks there (row validity held per element across
-    // both column blocks overflowed the SGPR file: 64-bit lane masks, spilled to VGPR lanes)
+    // the statistics of the stored (bf16-rounded) values; a statistics-only pass (y null: the tail's
+    // apply pass recomputes the output) takes the fp32 accumulators as they are. Packed fp32 pairs
+    // (v_pk_add / v_pk_fma): at two waves per SIMD the statistics-only pass was instruction-issue
+    // bound (~460 VALU per wave-tile, profiles/convp_pmc_r4.md). A 16-row block whose last row is
+    // valid is valid throughout (pix is monotone within a block): the wave-uniform test skips the
+    // per-row masks there.
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    const bool rnd = a.y != nullptr;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const bool full = pix(wr * 64 + i * 16 + 15) >= 0;
 #pragma unroll
       for (int j = 0; j < JN; ++j) {
-        float s1 = 0.f, s2 = 0.f, t1 = 0.f, t2 = 0.f;
+        const f32x2 k2 = {kshift[j], kshift[j]};
+        f32x2 s1 = {0.f, 0.f}, s2 = {0.f, 0.f};
 #pragma unroll
         for (int r = 0; r < 4; r += 2) {
-          const uint32_t pk = pack_bf16x2_rne(acc[i][j][r], acc[i][j][r + 1]);
-          float d0 = __uint_as_float(pk << 16) - kshift[j];
-          float d1 = __uint_as_float(pk & 0xFFFF0000u) - kshift[j];
-          if (!full) {
-            d0 = pix(wr * 64 + i * 16 + rq + r) >= 0 ? d0 : 0.f;
-            d1 = pix(wr * 64 + i * 16 + rq + r + 1) >= 0 ? d1 : 0.f;
+          f32x2 v = {acc[i][j][r], acc[i][j][r + 1]};
+          if (rnd) {
+            const uint32_t pk = pack_bf16x2_rne(v[0], v[1]);
+            v = f32x2{__uint_as_float(pk << 16), __uint_as_float(pk & 0xFFFF0000u)};
           }
-          s1 += d0;
-          t1 += d1;
-          s2 = fmaf(d0, d0, s2);
-          t2 = fmaf(d1, d1, t2);
+          f32x2 d = v - k2;
+          if (!full) {
+            d[0] = pix(wr * 64 + i * 16 + rq + r) >= 0 ? d[0] : 0.f;
+            d[1] = pix(wr * 64 + i * 16 + rq + r + 1) >= 0 ? d[1] : 0.f;
+          }
+          s1 += d;
+          s2 = __builtin_elementwise_fma(d, d, s2);
         }
-        es.s1[j] += s1 + t1;
-        es.s2[j] += s2 + t2;
+        es.s1[j] += s1[0] + s1[1];
+        es.s2[j] += s2[0] + s2[1];
       }
     }
   }
