@@ -110,8 +110,12 @@ PYBIND11_MODULE(_C, m) {
         py::arg("dgamma_d_out") = py::none(), py::arg("dbeta_d_out") = py::none(), py::arg("fold") = false);
   m.def("bn_elemt_coef", &bn_elemt_coef, py::arg("g"), py::arg("x"), py::arg("coef"));
   m.def("convw_fold_rows", &convw_fold_rows, py::arg("Cout"), py::arg("Cin"));
+  m.def("convw_gram_rows", &convw_gram_rows_, py::arg("C"));
+  m.def("convw_gram_", &convw_gram_, py::arg("x"), py::arg("out"));
   m.def("bnfold_dgrad_weights", &bnfold_dgrad_weights, py::arg("w"), py::arg("coef"));
   m.def("bnfold_rowdot", &bnfold_rowdot, py::arg("P"), py::arg("w"), py::arg("row"));
+  m.def("bnfold_gram_stats", &bnfold_gram_stats, py::arg("P"), py::arg("w"), py::arg("shift"), py::arg("M"),
+        py::arg("row"));
   m.def("bn_finalize", &bn_finalize, py::arg("part"), py::arg("rows"), py::arg("M"), py::arg("gamma"),
         py::arg("beta"), py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"), py::arg("eps"),
         py::arg("counter") = py::none());

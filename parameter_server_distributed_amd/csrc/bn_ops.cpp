@@ -791,6 +791,27 @@ void bnfold_rowdot(const at::Tensor& P, const at::Tensor& w_in, at::Tensor row) 
   TORCH_CHECK(e == hipSuccess, "psd bnfold rowdot: ", hipGetErrorString(e));
 }
 
+// row [2, Cout] = the shifted batch statistics of y = x W^T from P = convw(x, x) in fold mode (the
+// Gram matrix and column sums of x), without forming y (ops/tail.py)
+void bnfold_gram_stats(const at::Tensor& P, const at::Tensor& w_in, const at::Tensor& shift, int64_t M, at::Tensor row) {
+  const c10::DeviceGuard dg(w_in.device());
+  const at::Tensor w = fold_w2d(w_in);
+  const int64_t Cout = w.size(0), Cin = w.size(1);
+  TORCH_CHECK(P.scalar_type() == at::kFloat && P.is_contiguous() && P.dim() == 2 && P.size(1) == Cin &&
+                  P.size(0) > Cin && P.device() == w.device() && (Cin == 64 || Cin == 128 || Cin == 256) &&
+                  Cout % 4 == 0,
+              "psd bnfold gram stats: P must be the fp32 convw_gram_ result [rows > Cin, Cin], Cin 64/128/256, "
+              "Cout % 4 == 0");
+  TORCH_CHECK(shift.scalar_type() == at::kFloat && shift.numel() == Cout && shift.is_contiguous(),
+              "psd bnfold gram stats: shift must be fp32 [Cout]");
+  TORCH_CHECK(row.scalar_type() == at::kFloat && row.is_contiguous() && row.numel() == 2 * Cout,
+              "psd bnfold gram stats: row must be a contiguous fp32 [2, Cout]");
+  hipError_t e = launch_bnfold_gram_stats(P.data_ptr<float>(), reinterpret_cast<const uint16_t*>(w.data_ptr()),
+                                          shift.data_ptr<float>(), (int)Cout, (int)Cin, M, row.data_ptr<float>(),
+                                          stream_of(w));
+  TORCH_CHECK(e == hipSuccess, "psd bnfold gram stats: ", hipGetErrorString(e));
+}
+
 // Training-mode BN statistics from producer partials only (no activation is read): returns
 // {mean, invstd, ss [2C]} and updates the running statistics, as bn_fwd with stats_only.
 std::vector<at::Tensor> bn_finalize(const at::Tensor& part, int64_t rows, int64_t M, const at::Tensor& gamma,

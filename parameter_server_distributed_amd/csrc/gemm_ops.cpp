@@ -665,4 +665,51 @@ bool convw_(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64_t R
   return true;
 }
 
+int64_t convw_gram_rows_(int64_t C) { return convw_gram_rows((int)C); }
+
+// out = fp32 [convw_gram_rows(C), C]: rows [0, C) the Gram matrix x^T x of the [M, C] pixel rows of
+// x, row C their column sums -- one read of x (the BN statistics of y = x W^T without forming y:
+// ops/tail.py). False when the shape is unsupported.
+bool convw_gram_(const at::Tensor& x, at::Tensor out) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.scalar_type() == at::kBFloat16 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "psd convw_gram: x must be a channels_last bf16 tensor");
+  const int64_t Nb = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), M = Nb * H * W;
+  const int64_t rows = convw_gram_rows((int)C);
+  TORCH_CHECK(out.is_cuda() && out.device() == x.device() && out.dim() == 2 && out.size(0) == rows &&
+                  out.size(1) == C && out.is_contiguous() && out.scalar_type() == at::kFloat &&
+                  (reinterpret_cast<uintptr_t>(out.data_ptr()) & 15) == 0,
+              "psd convw_gram: out must be a contiguous fp32 [convw_gram_rows(C), C] tensor on x's device");
+  const int64_t xbytes = x.numel() * 2;
+  if (rows == 0 || xbytes > 0xFFFFFF00ll || M >= ((int64_t)1 << 31) || M == 0) return false;
+  int logc = 0;
+  while ((1 << logc) < C) ++logc;
+  const c10::DeviceGuard g(x.device());
+  ConvwArgs a{};
+  a.dy = x.data_ptr();
+  a.x = x.data_ptr();
+  a.out = out.data_ptr();
+  a.dybytes = (uint32_t)xbytes;
+  a.xbytes = (uint32_t)xbytes;
+  a.M = (int)M;
+  a.Cout = 0;
+  a.KK = (int)C;
+  a.H = a.Ho = (int)H;
+  a.W = a.Wo = (int)W;
+  a.logC = logc;
+  a.S = 1;
+  a.stride = 1;
+  a.pad = 0;
+  a.fold = 2;
+  a.Arows = (int)rows;
+  const ConvwPlan p = convw_plan(a);
+  if (p.splits <= 0) return false;
+  at::Tensor slab = at::empty({p.slab_floats}, x.options().dtype(at::kFloat));
+  a.slab = slab.data_ptr<float>();
+  const hipError_t e = launch_convw(a, stream_of(x));
+  if (e == hipErrorNotSupported) return false;
+  TORCH_CHECK(e == hipSuccess, "psd convw_gram: ", hipGetErrorString(e));
+  return true;
+}
+
 }  // namespace psd

@@ -123,6 +123,79 @@ __global__ __launch_bounds__(256) void bnfold_rowdot_kernel(const float* __restr
   }
 }
 
+// Batch statistics of y = x W^T without forming y (ops/tail.py's statistics pass): with the Gram
+// matrix G = x^T x and the column sums s = 1^T x (P from the Gram launch convw_gram_: rows [0, Wd) =
+// G, row Wd = s), sum_m y_c = W_c . s and sum_m y_c^2 = W_c^T G W_c. Writes the shifted partial row
+// (sum (y - k), sum (y - k)^2), k = shift (the running mean the finalize expects), the shift applied
+// in fp64. A wave owns kGsCh output channels (their W rows staged in LDS as fp32, read as
+// broadcasts) and streams G once for all of them: lane j holds u[c][j] = sum_i W[c][i] G[i][j].
+constexpr int kGsCh = 4;
+
+template <int JT>
+__global__ __launch_bounds__(256) void bnfold_gram_stats_kernel(const float* __restrict__ P, const uint16_t* __restrict__ W,
+                                                                const float* __restrict__ shift, int Cout, int Wd,
+                                                                double M, float* __restrict__ row) {
+  __shared__ float ws[4][kGsCh][JT * 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c0 = (blockIdx.x * 4 + wv) * kGsCh;
+  if (c0 >= Cout) return;  // Cout % kGsCh == 0 (host): a live wave owns kGsCh real channels
+#pragma unroll
+  for (int k = 0; k < kGsCh; ++k)
+#pragma unroll
+    for (int t = 0; t < JT; ++t) ws[wv][k][t * 64 + lane] = bf16_to_f32(W[(int64_t)(c0 + k) * Wd + t * 64 + lane]);
+  __builtin_amdgcn_wave_barrier();  // the wave reads back only its own rows
+  const float* G = P;
+  const float* cs = P + (int64_t)Wd * Wd;
+  float u[kGsCh][JT];
+#pragma unroll
+  for (int k = 0; k < kGsCh; ++k)
+#pragma unroll
+    for (int t = 0; t < JT; ++t) u[k][t] = 0.f;
+#pragma unroll 4
+  for (int i = 0; i < Wd; ++i) {
+    float g[JT];
+#pragma unroll
+    for (int t = 0; t < JT; ++t) g[t] = G[(int64_t)i * Wd + t * 64 + lane];
+#pragma unroll
+    for (int k = 0; k < kGsCh; ++k) {
+      const float wk = ws[wv][k][i];
+#pragma unroll
+      for (int t = 0; t < JT; ++t) u[k][t] = fmaf(wk, g[t], u[k][t]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kGsCh; ++k) {
+    double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+    for (int t = 0; t < JT; ++t) {
+      const double wj = (double)ws[wv][k][t * 64 + lane];
+      s2 += wj * (double)u[k][t];
+      s1 += wj * (double)cs[t * 64 + lane];
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      s1 += __shfl_xor(s1, off, 64);
+      s2 += __shfl_xor(s2, off, 64);
+    }
+    if (lane == 0) {
+      const int c = c0 + k;
+      const double kc = shift ? (double)shift[c] : 0.0;
+      row[c] = (float)(s1 - M * kc);
+      row[Cout + c] = (float)(s2 - 2.0 * kc * s1 + M * kc * kc);
+    }
+  }
+}
+
+hipError_t launch_bnfold_gram_stats(const float* P, const uint16_t* W, const float* shift, int Cout, int Wd, int64_t M,
+                                    float* row, hipStream_t st) {
+  if (Cout <= 0 || Cout % kGsCh != 0 || M <= 0) return hipErrorInvalidValue;
+  const dim3 grid((Cout / kGsCh + 3) / 4);
+  if (Wd == 64) hipLaunchKernelGGL(bnfold_gram_stats_kernel<1>, grid, dim3(256), 0, st, P, W, shift, Cout, Wd, (double)M, row);
+  else if (Wd == 128) hipLaunchKernelGGL(bnfold_gram_stats_kernel<2>, grid, dim3(256), 0, st, P, W, shift, Cout, Wd, (double)M, row);
+  else if (Wd == 256) hipLaunchKernelGGL(bnfold_gram_stats_kernel<4>, grid, dim3(256), 0, st, P, W, shift, Cout, Wd, (double)M, row);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
 hipError_t launch_bnfold_rowdot(const float* P, const uint16_t* W, int Cout, int Wd, float* row, hipStream_t st) {
   if (Cout <= 0 || Wd <= 0 || Wd % 8 != 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(bnfold_rowdot_kernel, dim3((Cout + 3) / 4), dim3(256), 0, st, P, W, Cout, Wd, row);

@@ -262,14 +262,14 @@ __device__ __forceinline__ void convn_epilogue(const ConvnArgs& a, f32x4 (&acc)[
     }
   }
   if constexpr (STATS) {
-    // the statistics of the stored (bf16-rounded) values; a statistics-only pass (y null: the tail's
-    // apply pass recomputes the output) takes the fp32 accumulators as they are. Packed fp32 pairs
+    // the statistics of the bf16-rounded values (stored, or -- statistics-only pass -- the values the
+    // tail's apply pass rounds before normalising: fp32 accumulators here put the chained-block
+    // gradients past the library path's error level, tests/test_bnfold.py). Packed fp32 pairs
     // (v_pk_add / v_pk_fma): at two waves per SIMD the statistics-only pass was instruction-issue
     // bound (~460 VALU per wave-tile, profiles/convp_pmc_r4.md). A 16-row block whose last row is
     // valid is valid throughout (pix is monotone within a block): the wave-uniform test skips the
     // per-row masks there.
     typedef float f32x2 __attribute__((ext_vector_type(2)));
-    const bool rnd = a.y != nullptr;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const bool full = pix(wr * 64 + i * 16 + 15) >= 0;
@@ -279,12 +279,8 @@ __device__ __forceinline__ void convn_epilogue(const ConvnArgs& a, f32x4 (&acc)[
         f32x2 s1 = {0.f, 0.f}, s2 = {0.f, 0.f};
 #pragma unroll
         for (int r = 0; r < 4; r += 2) {
-          f32x2 v = {acc[i][j][r], acc[i][j][r + 1]};
-          if (rnd) {
-            const uint32_t pk = pack_bf16x2_rne(v[0], v[1]);
-            v = f32x2{__uint_as_float(pk << 16), __uint_as_float(pk & 0xFFFF0000u)};
-          }
-          f32x2 d = v - k2;
+          const uint32_t pk = pack_bf16x2_rne(acc[i][j][r], acc[i][j][r + 1]);
+          f32x2 d = f32x2{__uint_as_float(pk << 16), __uint_as_float(pk & 0xFFFF0000u)} - k2;
           if (!full) {
             d[0] = pix(wr * 64 + i * 16 + rq + r) >= 0 ? d[0] : 0.f;
             d[1] = pix(wr * 64 + i * 16 + rq + r + 1) >= 0 ? d[1] : 0.f;

@@ -504,8 +504,67 @@ bool convw_fold_ok(int Cout, int KK, int Arows) {
   return tkk == KK && tco > 0 && Arows % tco == 0 && Cout % 64 == 0 && KK >= 64 && (KK & (KK - 1)) == 0;
 }
 
+// Gram launch (fold == 2, 1x1, Cout = 0): A rows = [x (KK rows) | ones (the rest of Arows)], so
+// out = fp32 [Arows][KK] holds x^T x and (row KK) the column sums of x from ONE read of x -- the
+// stage carries no dY sub-images (NAR = 0), only the x sub-images both operands are read from.
+// (tco, tkk, ring depth) per channel count; 0 when unsupported
+static void gram_tile(int C, int& tco, int& tkk, int& nslot) {
+  tco = tkk = nslot = 0;
+  if (C == 64) tco = 128, tkk = 64, nslot = 5;
+  else if (C == 128) tco = 256, tkk = 128, nslot = 5;
+  else if (C == 256) tco = 128, tkk = 256, nslot = 4;
+}
+
+int convw_gram_rows(int C) {
+  int tco, tkk, ns;
+  gram_tile(C, tco, tkk, ns);
+  return tco ? (C + 16 + tco - 1) / tco * tco : 0;
+}
+
+static ConvwPlan gram_plan(const ConvwArgs& a) {
+  ConvwPlan p{0, 0};
+  int tco, tkk, ns;
+  gram_tile(a.KK, tco, tkk, ns);
+  if (!tco || a.M <= 0 || a.Arows != convw_gram_rows(a.KK)) return p;
+  const int ntile = a.Arows / tco;
+  const int occ = std::max(1, std::min(2, (160 * 1024) / (ns * tkk / 64 * kSub)));
+  const int total = (a.M + kBP - 1) / kBP;
+  int splits = std::max(1, (cu_count() * occ) / ntile);
+  splits = std::min(splits, std::max(1, total / 4));
+  const int sps = (total + splits - 1) / splits;
+  p.splits = (total + sps - 1) / sps;
+  const int64_t mn = (int64_t)a.Arows * a.KK;
+  p.slab_floats = (int64_t)p.splits * mn + splitk_tree_floats(p.splits, mn);
+  return p;
+}
+
+static hipError_t launch_gram(const ConvwArgs& a_in, hipStream_t st) {
+  int tco, tkk, ns;
+  gram_tile(a_in.KK, tco, tkk, ns);
+  const bool ok = tco > 0 && a_in.Cout == 0 && a_in.KK == (1 << a_in.logC) && a_in.S == 1 && a_in.stride == 1 &&
+                  a_in.pad == 0 && a_in.H == a_in.Ho && a_in.W == a_in.Wo && !a_in.accumulate &&
+                  a_in.Arows == convw_gram_rows(a_in.KK) && a_in.xbytes > 0 && a_in.xbytes <= 0xFFFFFF00u &&
+                  a_in.dybytes > 0 && (int64_t)a_in.M * a_in.KK * 2 <= (int64_t)a_in.xbytes && a_in.slab && a_in.out;
+  if (!ok) return hipErrorNotSupported;
+  ConvwArgs a = a_in;
+  const ConvwPlan p = gram_plan(a);
+  if (p.splits <= 0) return hipErrorNotSupported;
+  const int total = (a.M + kBP - 1) / kBP;
+  a.splits = p.splits;
+  a.stages_per_split = (total + p.splits - 1) / p.splits;
+  const int grid = p.splits * (a.Arows / tco);
+  hipError_t e;
+  if (a.KK == 64) e = launch_t<128, 64, 4, 5, 0>(a, grid, st);
+  else if (a.KK == 128) e = launch_t<256, 128, 4, 5, 0>(a, grid, st);
+  else e = launch_t<128, 256, 2, 4, 0>(a, grid, st);
+  if (e != hipSuccess) return e;
+  const int64_t mn = (int64_t)a.Arows * a.KK;
+  return launch_splitk_reduce(a.slab, a.splits, mn, a.out, 0, 0, 1.f, st, a.slab + (int64_t)a.splits * mn);
+}
+
 ConvwPlan convw_plan(const ConvwArgs& a) {
   ConvwPlan p{0, 0};
+  if (a.fold == 2) return gram_plan(a);
   if (is_persist_w(a)) {  // one slab per workgroup (one workgroup per CU)
     if (!persist_w_ok(a) || a.M <= 0) return p;
     p.splits = std::min(cu_count(), persist_w_tiles(a));
@@ -532,6 +591,7 @@ ConvwPlan convw_plan(const ConvwArgs& a) {
 
 hipError_t launch_convw(const ConvwArgs& a_in, hipStream_t st) {
   if (a_in.M <= 0) return hipSuccess;
+  if (a_in.fold == 2) return launch_gram(a_in, st);
   if (is_persist_w(a_in)) {
     if (!persist_w_ok(a_in) || !a_in.slab || !a_in.out || a_in.dybytes == 0 || a_in.xbytes == 0)
       return hipErrorNotSupported;

@@ -126,6 +126,8 @@ hipError_t launch_bn_bwd_dual_pre(const BnDualPreArgs& a, hipStream_t stream);
 // BN-backward fold (bnfold.hip); bn_elemt_coef (bn.hip): dx = A g + B x + C from finalized coefficients
 hipError_t launch_bn_elemt_coef(const uint16_t* g, const uint16_t* x, const float* coef, uint16_t* dx, int64_t M, int C,
                                 hipStream_t stream);
+hipError_t launch_bnfold_gram_stats(const float* P, const uint16_t* W, const float* shift, int Cout, int Wd, int64_t M,
+                                    float* row, hipStream_t st);
 hipError_t launch_bnfold_rowdot(const float* P, const uint16_t* W, int Cout, int Wd, float* row, hipStream_t st);
 hipError_t launch_bnfold_prep(const uint16_t* W, const float* coef, int Cout, int Wd, uint16_t* w2, int ldw,
                               uint16_t* bw, float* bvec, hipStream_t stream);

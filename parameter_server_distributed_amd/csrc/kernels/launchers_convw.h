@@ -18,7 +18,8 @@ struct ConvwArgs {
   int accumulate;      // out += result (bf16) instead of out = result
   // BN-backward fold (ops/bn.py): the A rows are [dY (Cout rows) | x (KK rows) | ones (the rest of
   // Arows)], so out = fp32 [Arows][KK] holds dY^T x, the Gram matrix x^T x and the column sums of x
-  // (1x1 only, the whole KK in one tile). 0: plain (Arows = Cout, bf16 out)
+  // (1x1 only, the whole KK in one tile). 0: plain (Arows = Cout, bf16 out). 2: the Gram launch
+  // (Cout = 0, Arows = convw_gram_rows(KK)): x^T x and the column sums of x from one read of x
   int fold;
   int Arows;
   // set by the launcher
@@ -34,6 +35,8 @@ struct ConvwPlan {
 int convw_variants(int Cout, int KK);
 // a fold launch (1x1, Cout dY rows, KK = Cin, Arows = convw_fold_rows) is supported
 bool convw_fold_ok(int Cout, int KK, int Arows);
+// rows of a Gram launch's fp32 result [x^T x (C rows) | column sums (row C) | padding]; 0: unsupported
+int convw_gram_rows(int C);
 // split plan of a launch (the caller allocates slab_floats fp32 for it)
 ConvwPlan convw_plan(const ConvwArgs& a);
 // hipErrorNotSupported outside the kernel's contract (nothing launched)

@@ -49,6 +49,7 @@ std::vector<at::Tensor> bn_bwd_dual_pre(const at::Tensor& g, const at::Tensor& x
 std::vector<at::Tensor> bnfold_dgrad_weights(const at::Tensor& w, const at::Tensor& coef);
 void bnfold_combine(const at::Tensor& P, const at::Tensor& w, const at::Tensor& coef, at::Tensor out, bool accumulate);
 void bnfold_rowdot(const at::Tensor& P, const at::Tensor& w, at::Tensor row);
+void bnfold_gram_stats(const at::Tensor& P, const at::Tensor& w, const at::Tensor& shift, int64_t M, at::Tensor row);
 std::vector<at::Tensor> bn_finalize(const at::Tensor& part, int64_t rows, int64_t M, const at::Tensor& gamma,
                                     const at::Tensor& beta, at::Tensor running_mean, at::Tensor running_var,
                                     double momentum, double eps, c10::optional<at::Tensor> counter);
@@ -107,6 +108,8 @@ bool conv_wgrad_(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int6
 bool convw_(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64_t R, int64_t S, int64_t stride,
             int64_t pad, int64_t variant, bool accumulate, bool fold);
 int64_t convw_fold_rows(int64_t Cout, int64_t Cin);
+int64_t convw_gram_rows_(int64_t C);
+bool convw_gram_(const at::Tensor& x, at::Tensor out);
 int64_t convw_variants_(int64_t Cout, int64_t KK);
 int64_t conv_fwd_fp8_(const at::Tensor& x, const at::Tensor& w2, const at::Tensor& x_scale, const at::Tensor& w_scale,
                       at::Tensor out, int64_t R, int64_t S, int64_t stride, int64_t pad, c10::optional<at::Tensor> part,

@@ -44,7 +44,8 @@ TAIL_CALLS = {"fwd": 0, "bwd_fused": 0, "bwd_recompute": 0}
 def tail_ok(conv, bn, a2: torch.Tensor, idt: torch.Tensor) -> bool:
     """The recomputing tail applies: a bf16 Conv1x1 (no fp8) into a training ReLU FusedBatchNorm2d
     with an identity residual, channels_last operands, a shape the narrow kernel and the fold take."""
-    if not _at.enabled("PSD_TAIL_RECOMPUTE") or not isinstance(conv, Conv1x1) or conv.fp8:
+    if not (_at.enabled("PSD_TAIL_RECOMPUTE") and _at.enabled("PSD_CONVN")) or not isinstance(conv, Conv1x1) \
+            or conv.fp8:
         return False
     if not isinstance(bn, FusedBatchNorm2d) or not bn.relu or not bn.training or bn.weight is None:
         return False
@@ -86,6 +87,34 @@ def _variant(a2, w2, M: int, cin: int, cout: int, h: int, w: int, shift) -> int:
     return int(how[4:])
 
 
+def _stats_route(a2, w2, M: int, cin: int, cout: int, v: int, h: int, w: int, shift) -> str:
+    """The tail's statistics: "gram" (one pass over a2 for its Gram matrix and column sums, then
+    W^T G W per channel: kernels/bnfold.hip gram stats) or "pass" (the narrow kernel's
+    statistics-only pass recomputing the GEMM), timed per shape. The Gram statistics are those of the
+    fp32 product, the pass's those of the bf16-rounded one (what the apply pass normalises)."""
+    C = _native()
+    if not _at.enabled("PSD_TAIL_GRAM") or C.convw_gram_rows(cin) <= 0 or cout % 4:
+        return "pass"
+    dev = a2.device
+
+    def gram():
+        P = torch.empty(C.convw_gram_rows(cin), cin, device=dev, dtype=torch.float32)
+        if not C.convw_gram_(a2, P):
+            raise _at.Declined("convw Gram launch")
+        row = torch.empty(2, cout, device=dev, dtype=torch.float32)
+        C.bnfold_gram_stats(P, w2, shift, M, row)
+        return row
+
+    def pas():
+        part = torch.empty(_part_rows(M, cout, v, h, w, 1), 2, cout, device=dev, dtype=torch.float32)
+        rows = C.convn_(a2, w2, part, 1, 1, 1, 0, part=part, shift=shift, variant=v, no_store=True)
+        if rows == 0:
+            raise _at.Declined("convn statistics-only pass")
+        return part[:rows].sum(0)  # comparable with the Gram row (same shifted sums)
+
+    return _at.choose(("tail", "stats", M, cin, cout), {"gram": gram, "pass": pas}, "pass")
+
+
 class _TailFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, a2, weight, gamma, beta, idt, conv, bn, resid_to):
@@ -97,10 +126,20 @@ class _TailFn(torch.autograd.Function):
         if not w2.is_contiguous():
             w2 = w2.contiguous()
         v = _variant(a2, w2, M, cin, cout, h, w, bn.running_mean)
-        part = torch.empty(_part_rows(M, cout, v, h, w, 1), 2, cout, device=a2.device, dtype=torch.float32)
-        rows = C.convn_(a2, w2, part, 1, 1, 1, 0, part=part, shift=bn.running_mean, variant=v, no_store=True)
-        if rows == 0:
-            raise RuntimeError("psd tail: convn declined the statistics-only pass")
+        if _stats_route(a2, w2, M, cin, cout, v, h, w, bn.running_mean) == "gram":
+            # sum y = W s, sum y^2 = W^T G W from one read of a2 (G = a2^T a2, s = 1^T a2: the Gram
+            # launch of the weight-gradient kernel) -- the GEMM is not recomputed for the statistics
+            P = torch.empty(C.convw_gram_rows(cin), cin, device=a2.device, dtype=torch.float32)
+            if not C.convw_gram_(a2, P):
+                raise RuntimeError("psd tail: convw declined the Gram launch")
+            part = torch.empty(1, 2, cout, device=a2.device, dtype=torch.float32)
+            C.bnfold_gram_stats(P, w2, bn.running_mean, M, part[0])
+            rows = 1
+        else:
+            part = torch.empty(_part_rows(M, cout, v, h, w, 1), 2, cout, device=a2.device, dtype=torch.float32)
+            rows = C.convn_(a2, w2, part, 1, 1, 1, 0, part=part, shift=bn.running_mean, variant=v, no_store=True)
+            if rows == 0:
+                raise RuntimeError("psd tail: convn declined the statistics-only pass")
         mean, invstd, ss = C.bn_finalize(part, rows, M, gamma, beta, bn.running_mean, bn.running_var,
                                          bn.momentum if bn.momentum is not None else 0.1, bn.eps,
                                          bn.num_batches_tracked)

@@ -12,5 +12,6 @@ timeout -k 10 300 python3 tools/tail_bench.py > "$OUT/tail_bench.md" 2>&1 || { t
 cat "$OUT/tail_bench.md"
 timeout -k 10 300 python3 tools/convh_bench.py > "$OUT/convh_bench.md" 2>&1 || { tail -20 "$OUT/convh_bench.md"; exit 1; }
 grep "|" "$OUT/convh_bench.md"
-PSD_STEP_LOG=1 timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --out "$OUT/bench.json" > "$OUT/bench.log" 2>&1 || { tail -20 "$OUT/bench.log"; exit 1; }
+PSD_AUTOTUNE_LOG=1 PSD_STEP_LOG=1 timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --out "$OUT/bench.json" > "$OUT/bench.log" 2>&1 || { tail -20 "$OUT/bench.log"; exit 1; }
 python3 -c "import json;d=json.load(open('$OUT/bench.json'));print('bench', d['value'], d['ms_per_step'], d['final_loss'], d['params_finite'])"
+grep "tail" "$OUT/bench.log" | head -20

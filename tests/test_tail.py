@@ -113,6 +113,32 @@ def test_bnfold_rowdot(gpu):
     torch.testing.assert_close(row[1].double().cpu(), want, rtol=1e-5, atol=1e-4)
 
 
+@pytest.mark.parametrize("Nb,H,cin,cout", [(2, 14, 64, 256), (3, 7, 128, 512), (1, 9, 256, 1024)])
+def test_bnfold_gram_stats_exact(gpu, Nb, H, cin, cout):
+    """Gram statistics: the Gram launch gives G = x^T x and s = 1^T x from one read of x; then per
+    channel (sum y - M k, sum y^2 - 2 k sum y + M k^2) = shifted sums of y = x W^T, never formed."""
+    C = native()
+    assert C.convw_gram_rows(cin) > 0
+    g = torch.Generator().manual_seed(5)
+    x = _ints((Nb, cin, H, H), -1, 1, g)
+    w = _ints((cout, cin), -1, 1, g)
+    k = _ints((cout,), -2, 2, g)
+    M = Nb * H * H
+    y = x.permute(0, 2, 3, 1).reshape(M, cin).double() @ w.double().t()
+    d = y - k.double()
+    xd = x.to(gpu, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    P = torch.full((C.convw_gram_rows(cin), cin), float("nan"), device=gpu)
+    assert C.convw_gram_(xd, P)
+    xm = x.permute(0, 2, 3, 1).reshape(M, cin).double()
+    torch.testing.assert_close(P[:cin].double().cpu(), xm.t() @ xm, rtol=0, atol=0)
+    torch.testing.assert_close(P[cin].double().cpu(), xm.sum(0), rtol=0, atol=0)
+    row = torch.full((2, cout), float("nan"), device=gpu)
+    C.bnfold_gram_stats(P, w.to(gpu, torch.bfloat16), k.to(gpu), M, row)
+    got = row.double().cpu()
+    torch.testing.assert_close(got[0], d.sum(0), rtol=0, atol=0)
+    torch.testing.assert_close(got[1], (d * d).sum(0), rtol=0, atol=0)
+
+
 def test_resnet_tail_matches_unfused(gpu, monkeypatch):
     """ResNet-50 (64x64 images, non-zero bn3 scales) with the recomputing tail on vs off, each
     against an fp32 run of the same weights (PyTorch composite ops): bf16 rounding differences grow

@@ -53,6 +53,13 @@ def main():
         dr = torch.randn(M, cout, device=dev).bfloat16()
         ain, aout = M * cin * 2, M * cout * 2
         ref = None
+        if C.convw_gram_rows(cin) > 0:
+            P = torch.empty(C.convw_gram_rows(cin), cin, device=dev)
+            grow = torch.empty(2, cout, device=dev)
+            us = t_us(lambda: C.convw_gram_(x, P))
+            print(f"| {name} | Gram launch (x^T x, 1^T x) | - | {us:.0f} | {ain / us / 1e3:.0f} |")
+            us = t_us(lambda: C.bnfold_gram_stats(P, w, shift, M, grow))
+            print(f"| {name} | W^T G W per channel | - | {us:.0f} | - |")
         for v in range(C.convn_variants(cout)):
             kind = C.convn_variant_kind(cout, v)
             if kind not in (0, 3) or not C.convn_variant_ok(cout, v, 1, 1, 1, 0, hw):
