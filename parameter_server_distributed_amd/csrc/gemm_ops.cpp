@@ -83,6 +83,54 @@ int64_t gemm_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool b_km
   return a.part ? rows : 1;
 }
 
+// GELU-backward GEMM: out[M,N] = bf16(bf16(A op B) * gelu'(pre)) with the bias gradient
+// db[N] (+)= colsum(out) from the epilogue's per-tile partials (kernels/gemm.hip ACT 3): the
+// gradient of a GELU Linear's output computed by the next Linear's bwd-data GEMM goes straight to
+// the pre-activation gradient. False (nothing launched) when the shape is not on the 8-phase kernel.
+bool gemm_gelu_bwd_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool b_kmajor, const at::Tensor& pre,
+                    at::Tensor out, at::Tensor db, bool accumulate) {
+  chk2d(A, "A");
+  chk2d(B, "B");
+  chk2d(pre, "pre");
+  const int64_t M = a_kmajor ? A.size(0) : A.size(1), K = a_kmajor ? A.size(1) : A.size(0);
+  const int64_t N = b_kmajor ? B.size(0) : B.size(1), K2 = b_kmajor ? B.size(1) : B.size(0);
+  TORCH_CHECK(K == K2, "psd gemm_gelu_bwd: K mismatch ", K, " vs ", K2);
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 && out.is_contiguous() && out.dim() == 2 && out.size(0) == M &&
+                  out.size(1) == N && pre.is_contiguous() && pre.sizes() == out.sizes(),
+              "psd gemm_gelu_bwd: out and pre must be contiguous bf16 [M, N]");
+  TORCH_CHECK(db.numel() == N && db.is_contiguous() &&
+                  (db.scalar_type() == at::kBFloat16 || db.scalar_type() == at::kFloat),
+              "psd gemm_gelu_bwd: db must be [N] bf16/fp32");
+  if (N % 8 != 0 || K % 8 != 0 || (!a_kmajor && M % 8 != 0)) return false;
+  const c10::DeviceGuard g(A.device());
+  at::Tensor part = at::empty({gemm_stats_rows_(M) * N}, A.options().dtype(at::kFloat));
+  GemmArgs a{};
+  a.A = A.data_ptr();
+  a.B = B.data_ptr();
+  a.C = out.data_ptr();
+  a.aux = const_cast<void*>(pre.data_ptr());
+  a.M = (int)M;
+  a.N = (int)N;
+  a.K = (int)K;
+  a.lda = (int)A.stride(0);
+  a.ldb = (int)B.stride(0);
+  a.ldc = (int)N;
+  a.a_kmajor = a_kmajor;
+  a.b_kmajor = b_kmajor;
+  a.act = 3;
+  a.part = part.data_ptr<float>();
+  int rows = 0;
+  a.rows_out = &rows;
+  hipError_t e = launch_gemm(a, stream_of(A));
+  if (e == hipErrorNotSupported) return false;
+  TORCH_CHECK(e == hipSuccess, "psd gemm_gelu_bwd: ", hipGetErrorString(e));
+  TORCH_CHECK(rows > 0 && rows <= gemm_stats_rows_(M), "psd gemm_gelu_bwd: partial rows ", rows);
+  e = launch_colsum_final(part.data_ptr<float>(), rows, (int)N, db.data_ptr(), db.scalar_type() == at::kBFloat16,
+                          accumulate, stream_of(A));
+  TORCH_CHECK(e == hipSuccess, "psd gemm_gelu_bwd colsum: ", hipGetErrorString(e));
+  return true;
+}
+
 // out[M,N] (+)= scale * (A op B) via split-K fp32 slabs (weight gradients: K = tokens).
 void gemm_splitk_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool b_kmajor, at::Tensor out,
                   bool accumulate, double scale, int64_t splits) {

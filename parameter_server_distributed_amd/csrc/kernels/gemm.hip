@@ -55,6 +55,14 @@ __device__ __forceinline__ float gelu_tanh(float x) {
   return x * __builtin_amdgcn_rcpf(1.f + e);
 }
 
+// GELU(tanh) derivative: s = sigmoid(2u), d/dx [x s] = s + 2 x s (1 - s) u'(x)
+__device__ __forceinline__ float gelu_tanh_grad(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float u = k0 * (x + k1 * x * x * x);
+  const float sg = __builtin_amdgcn_rcpf(1.f + __expf(-2.f * u));
+  return sg + 2.f * x * sg * (1.f - sg) * k0 * (1.f + 3.f * k1 * x * x);
+}
+
 // Stage loader: each lane moves ROWS*8/256 16-byte chunks global -> registers.
 template <int ROWS, bool KMAJ>
 struct Stage {
@@ -783,6 +791,11 @@ __device__ __forceinline__ float act_apply(float x) {
 // BM / 2 rows -> partial row (tile_m * 2 + wave row) of part [rows][2][N] (the layout of
 // kernels/bn.hip bn_fwd_reduce_kernel), so the BN forward skips its statistics pass. The shift (the
 // running mean) arrives by LDS-DMA with the bias, 4 B per lane.
+// ACT 3 (GELU backward of the Linear that produced this GEMM's A-side input: C = dY W is d(gelu
+// output)): the bf16 epilogue multiplies each stored element by gelu'(pre) (g.aux = the saved
+// pre-activation, read 16 B per lane on the store side), stores g = bf16(C gelu'(pre)) and sums its
+// columns per wave row -> g.part [rows][N] fp32 (the bias gradient's partials; one row per wave row
+// of each 256 / 128-row tile). The separate GELU-backward + column-sum pass over C and pre is gone.
 // GB: B is gathered as the im2col image of a convolution input for the weight gradient (MODE 1):
 // dW[cout][(r, s, ci)] = sum over output pixels p of dY[p][cout] * x[pixel(p) + (r, s)][ci], A = dY
 // M-major ([pixels][cout]), B = the gathered [pixels][R*S*C] N-major image (each lane's 16 bytes are
@@ -793,6 +806,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
   static_assert(!ST || (MODE == 0 && !GB && ACT == 0 && AK),
                 "statistics epilogue: single split, bf16 out, no activation, K-major A (zero rows past M)");
   static_assert(!MX || (F8 && BM == 128 && MODE == 0), "MX: fp8, 128-row tiles (LDS), single split");
+  static_assert(ACT != 3 || (MODE == 0 && !F8 && !GA && !GB && !ST), "GELU-backward epilogue: bf16 single-split GEMM");
   static_assert(!GB || (!AK && !BKM && MODE == 1 && !F8 && !GA), "implicit-GEMM wgrad: M-major dY, split-K");
   static_assert(!F8 || (AK && BKM), "fp8 GEMM takes K-major operands");
   static_assert(!GA || (AK && MODE == 0), "implicit-GEMM convolution: K-major A, single split");
@@ -1180,6 +1194,26 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
       // implicit GEMM's out-of-image sentinel -- so their accumulators are exactly 0)
       f32x2 t1[2][2], t2[2][2];
       float shk[2][2];  // the shift of this lane's 4 columns (read before the staging overwrites it)
+      float gs[8];      // ACT 3: column sums of g over the lane's stored rows (8 columns c16*8..+7)
+      // ACT 3: the tile's pre-activation, every 16-B piece this lane stores, loaded up front (one
+      // wait for all of them -- a load per store would wait on the pipeline's DMA in flight each time)
+      u32x4 pv[2][IM][2];
+      if constexpr (ACT == 3) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) gs[e] = 0.f;
+        const int n = cn0 + wc * 64 + c16 * 8;
+#pragma unroll
+        for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+          for (int i = 0; i < IM; ++i)
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+              const int m = cm0 + wr * (BM / 2) + qm * P::QA + i * 16 + k * 8 + rrow;
+              pv[qm][i][k] = u32x4{0u, 0u, 0u, 0u};
+              if (m < g.M && n < g.N)
+                pv[qm][i][k] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint16_t*>(g.aux) + (int64_t)m * ldo + n);
+            }
+      }
       if constexpr (ST) {
 #pragma unroll
         for (int qn = 0; qn < 2; ++qn)
@@ -1228,13 +1262,43 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
             const int rr = k * 8 + rrow;
             const int off = rr * 128 + (((2 * c16) ^ ((rr & 7) << 1)) << 3);
             const int m = mb + rr;
-            const u32x4 v = *reinterpret_cast<const u32x4*>(stg + off);
+            u32x4 v = *reinterpret_cast<const u32x4*>(stg + off);
             const u32x4 va = *reinterpret_cast<const u32x4*>(stg + 2048 + off);
             const uint32_t go = (m < g.M && n < g.N) ? ((uint32_t)m * ldo + n) * 2 : kOOB;
+            if constexpr (ACT == 3) {
+              const u32x4 p = pv[qm][i][k];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const float g0 = bf16_to_f32(f32_to_bf16(bf16_to_f32((uint16_t)(v[e] & 0xFFFFu)) *
+                                                         gelu_tanh_grad(bf16_to_f32((uint16_t)(p[e] & 0xFFFFu)))));
+                const float g1 = bf16_to_f32(f32_to_bf16(bf16_to_f32((uint16_t)(v[e] >> 16)) *
+                                                         gelu_tanh_grad(bf16_to_f32((uint16_t)(p[e] >> 16)))));
+                gs[2 * e] += g0;
+                gs[2 * e + 1] += g1;
+                v[e] = pack_bf16x2(g0, g1);
+              }
+            }
             __builtin_amdgcn_raw_buffer_store_b128(v, rc, go, 0, 0);
             __builtin_amdgcn_raw_buffer_store_b128(va, ra, go, 0, 0);
           }
         }
+      if constexpr (ACT == 3) {
+        // lanes with equal c16 (lane bits 0..2) hold the same 8 columns: sum over lane bits 3..5,
+        // lanes 0..7 store the wave row's partial row (rows past M / columns past N summed zeros)
+        const int prow = (cm0 / BM) * 2 + wr;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          gs[e] += __shfl_xor(gs[e], 8, 64);
+          gs[e] += __shfl_xor(gs[e], 16, 64);
+          gs[e] += __shfl_xor(gs[e], 32, 64);
+        }
+        const int n = cn0 + wc * 64 + c16 * 8;
+        if (lane < 8 && n < g.N) {
+          float* pp = g.part + (int64_t)prow * g.N + n;
+          *reinterpret_cast<f32x4*>(pp) = f32x4{gs[0], gs[1], gs[2], gs[3]};
+          *reinterpret_cast<f32x4*>(pp + 4) = f32x4{gs[4], gs[5], gs[6], gs[7]};
+        }
+      }
       if constexpr (ST) {
         // lanes with equal cl hold the same 4 columns: sum over lane bits 4..5, lanes 0..15 store
         const int prow = (cm0 / BM) * 2 + wr;
@@ -1339,13 +1403,6 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 // column sums of a [M][N] bf16 matrix (bias gradient), deterministic two-pass: block partials
 // (lane = 8 columns, 4 rows in flight) -> one finalize lane per column summing <= 64 partial rows.
 constexpr int kColsumMaxBlocks = kColsumPartRows;  // partial rows (the caller's workspace: [kColsumPartRows * N] fp32)
-// GELU(tanh) derivative: s = sigmoid(2u), d/dx [x s] = s + 2 x s (1 - s) u'(x)
-__device__ __forceinline__ float gelu_tanh_grad(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  const float u = k0 * (x + k1 * x * x * x);
-  const float sg = __builtin_amdgcn_rcpf(1.f + __expf(-2.f * u));
-  return sg + 2.f * x * sg * (1.f - sg) * k0 * (1.f + 3.f * k1 * x * x);
-}
 
 // Column partial sums of x[M, N] (bias gradients). GELU: x = bf16(dy * gelu'(pre)) is computed on
 // the fly from dy and the saved pre-activation, written to xo, and summed as written (the GELU
@@ -1493,7 +1550,10 @@ static int persistent_grid() {
 template <int BM, bool AK, bool BKM, int MODE, bool F8, int ACT, bool GA = false, int F8A = 0, bool GB = false,
           bool MX = false, bool ST = false>
 static hipError_t launch_8p_act(const GemmArgs& g, int splits, hipStream_t st) {
-  if constexpr (!ST) {
+  if constexpr (ACT == 3) {  // GELU backward + bias-gradient partials (g.aux = pre, g.part = [rows][N])
+    if (!g.part || !g.aux || g.c_f32 || g.bias || splits != 1) return hipErrorNotSupported;
+    if (g.rows_out) *g.rows_out = (g.M + BM - 1) / BM * 2;
+  } else if constexpr (!ST) {
     if (g.part) {  // the consumer BN's statistics in the epilogue
       if constexpr (MODE == 0 && !GB && ACT == 0 && AK) {
         if (g.c_f32 || g.bias || !g.shift || splits != 1) return hipErrorNotSupported;
@@ -1534,7 +1594,11 @@ static hipError_t launch_8p(const GemmArgs& g, int splits, hipStream_t st) {
   if constexpr (MODE == 0) {
     if (g.act == 1) return launch_8p_act<BM, AK, BKM, MODE, F8, 1>(g, splits, st);
     if (g.act == 2) return launch_8p_act<BM, AK, BKM, MODE, F8, 2>(g, splits, st);
+    if constexpr (!F8) {
+      if (g.act == 3) return launch_8p_act<BM, AK, BKM, MODE, F8, 3>(g, splits, st);
+    }
   }
+  if (g.act == 3) return hipErrorNotSupported;
   return launch_8p_act<BM, AK, BKM, MODE, F8, 0>(g, splits, st);
 }
 
@@ -1818,6 +1882,14 @@ hipError_t launch_splitk_reduce(float* slab, int splits, int64_t mn, void* out, 
   else
     hipLaunchKernelGGL(splitk_reduce_kernel<false>, dim3(grid), dim3(256), 0, st, slab, splits, mn, out, accumulate,
                        scale);
+  return hipGetLastError();
+}
+
+hipError_t launch_colsum_final(const float* part, int rows, int N, void* out, int out_bf16, int accumulate,
+                               hipStream_t st) {
+  if (N % 8 != 0 || rows <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((N + 7) / 8), dim3(1024), 0, st, part, rows, N, out, out_bf16,
+                     accumulate);
   return hipGetLastError();
 }
 

@@ -14,7 +14,7 @@ struct GemmArgs {
   int M, N, K;
   int lda, ldb, ldc;
   int a_kmajor, b_kmajor;
-  int act;           // 0 none, 1 relu, 2 gelu(tanh)
+  int act;           // 0 none, 1 relu, 2 gelu(tanh), 3 GELU backward (aux = pre in, part = colsum partials)
   int c_f32;
   int k_per_split;
   const float* a_scale;  // fp8 GEMM: dequant factors (device scalars), else unused
@@ -61,6 +61,9 @@ hipError_t launch_gemm_splitk(const GemmArgs& g, float* slab, int splits, void* 
 // out[n] (+)= sum_m x[m][n]; part is an fp32 [kColsumPartRows * N] scratch
 constexpr int kColsumPartRows = 2048;
 // pre/xo (optional): x is dy of a GELU(tanh) output; xo = bf16(dy * gelu'(pre)) is written and summed
+// out[n] (+)= sum of the rows rows of part[rows][N] (the second pass of launch_colsum)
+hipError_t launch_colsum_final(const float* part, int rows, int N, void* out, int out_bf16, int accumulate,
+                               hipStream_t stream);
 hipError_t launch_colsum(const uint16_t* x, int64_t M, int N, float* part, void* out, int out_bf16,
                          int accumulate, hipStream_t stream, const uint16_t* pre = nullptr, uint16_t* xo = nullptr);
 

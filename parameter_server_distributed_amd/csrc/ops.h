@@ -70,6 +70,8 @@ int64_t gemm_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool b_km
               c10::optional<at::Tensor> part, c10::optional<at::Tensor> shift);
 // statistics partial rows to allocate for a gemm_ / gemm_fp8_ / conv_fwd_ with part (any tile height)
 int64_t gemm_stats_rows_(int64_t M);
+bool gemm_gelu_bwd_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool b_kmajor, const at::Tensor& pre,
+                    at::Tensor out, at::Tensor db, bool accumulate);
 void gemm_splitk_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool b_kmajor, at::Tensor out,
                   bool accumulate, double scale, int64_t splits);
 void colsum_(const at::Tensor& x, at::Tensor out, bool accumulate);

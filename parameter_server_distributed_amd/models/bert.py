@@ -36,6 +36,9 @@ class BertLayer(nn.Module):
         self.ln1 = FusedAddLayerNorm(hidden, eps=1e-12, p=dropout, seed=2 * index + 1)
         self.ffn1 = MfmaLinear(hidden, ffn, act="gelu")
         self.ffn2 = MfmaLinear(ffn, hidden)
+        # ffn1's output feeds only ffn2: ffn2's bwd-data GEMM applies the GELU backward and sums
+        # ffn1's bias gradient in its epilogue (ops/linear.py)
+        self.ffn2.psd_gelu_input_from(self.ffn1)
         self.ln2 = FusedAddLayerNorm(hidden, eps=1e-12, p=dropout, seed=2 * index + 2)
         self.p = dropout
 

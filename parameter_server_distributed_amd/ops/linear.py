@@ -69,6 +69,36 @@ def _dgrad_route(key: tuple, dy2: torch.Tensor, w: torch.Tensor, dx: torch.Tenso
     return cands[_at.choose(("linear",) + key, cands, "mfma", lambda: dx)]
 
 
+def _gelu_dgrad(ctx, dy2, w, pre, M: int, K: int, N: int) -> bool:
+    """Bwd-data GEMM with the producing GELU Linear's backward in its epilogue: g = dY W * gelu'(pre)
+    and that Linear's bias gradient (into its grad sink when the data plane installed one), handed
+    over with the producer's forward token; False when the kernel declines the shape (nothing ran)."""
+    C = native()
+    src = ctx.gelu_src
+    g = torch.empty(M, K, dtype=dy2.dtype, device=dy2.device)
+    sink = getattr(src, "_psd_grad_sink", None)
+    db = sink(src.bias) if (sink is not None and src.bias is not None) else None
+    if db is None:
+        db = torch.empty(K, dtype=w.dtype, device=w.device)
+
+    def nn_():
+        if not C.gemm_gelu_bwd_(dy2, w, True, False, pre, g, db):
+            raise _at.Declined("gelu-bwd GEMM (NN)")
+
+    def nt_():
+        if not C.gemm_gelu_bwd_(dy2, w.t().contiguous(), True, True, pre, g, db):
+            raise _at.Declined("gelu-bwd GEMM (NT)")
+
+    try:
+        fn = {"nn": nn_, "nt": nt_}[_at.choose(("linear", "dgrad_gelu", M, K, N), {"nn": nn_, "nt": nt_}, "nn",
+                                              lambda: g)]
+        fn()
+    except _at.Declined:
+        return False
+    src._psd_gelu_hand = (ctx.gelu_tok, g, db if src.bias is not None else None)
+    return True
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, mod):
@@ -110,17 +140,36 @@ class _LinearFn(torch.autograd.Function):
         ctx.tok = mod._psd_tok = getattr(mod, "_psd_tok", 0) + 1
         ctx.has_bias = bias is not None
         ctx.in_shape = shp
-        ctx.save_for_backward(x2, weight, y if act == 1 else aux)
-        return y.view(*shp[:-1], N)
+        # GELU hand-over (MfmaLinear.psd_gelu_input_from): this Linear's bwd-data GEMM applies the
+        # producing GELU Linear's activation backward in its epilogue when x is that Linear's output
+        # of the current forward
+        src = getattr(mod, "_psd_gelu_from", None)
+        fuse = (src is not None and _at.enabled("PSD_GELU_FUSE") and getattr(x, "_psd_gelu_tok", None) is not None
+                and x._psd_gelu_tok == (id(src), src._psd_tok) and getattr(src, "_psd_gelu_pre", None) is not None)
+        ctx.gelu_src = src if fuse else None
+        ctx.gelu_tok = src._psd_tok if fuse else None
+        pre_src = src._psd_gelu_pre if fuse else None
+        ctx.save_for_backward(x2, weight, y if act == 1 else aux, pre_src)
+        out = y.view(*shp[:-1], N)
+        if act == 2:
+            mod._psd_gelu_pre = aux  # what a fused consumer's backward reads (also saved in this ctx)
+            out._psd_gelu_tok = (id(mod), ctx.tok)
+        return out
 
     @staticmethod
     def backward(ctx, dy):
         C = native()
-        x2, w, keep = ctx.saved_tensors
+        x2, w, keep, pre_src = ctx.saved_tensors
         dy2 = dy.reshape(-1, w.shape[0]).contiguous()
         sink = getattr(ctx.mod, "_psd_grad_sink", None)
         db = None
-        if ctx.act == 1:
+        hand = getattr(ctx.mod, "_psd_gelu_hand", None)
+        ctx.mod._psd_gelu_hand = None
+        if ctx.act == 2 and hand is not None and hand[0] == ctx.tok and hand[1].data_ptr() == dy2.data_ptr():
+            # the consumer's bwd-data GEMM already applied this GELU's backward and summed the bias
+            # gradient (gemm_gelu_bwd_): dy IS the pre-activation gradient
+            db = hand[2]
+        elif ctx.act == 1:
             dy2 = dy2 * (keep > 0)
         elif ctx.act == 2 and ctx.has_bias and ctx.needs_input_grad[2] and dy2.shape[1] % 8 == 0:
             # GELU backward and the bias gradient in one pass over dy / pre (kernels/gemm.hip)
@@ -147,6 +196,8 @@ class _LinearFn(torch.autograd.Function):
             dx = got.view(M, K)
             dx.addmm_(dy2, w)
             dx = dx.view(ctx.in_shape)
+        elif ctx.needs_input_grad[0] and ctx.gelu_src is not None and _gelu_dgrad(ctx, dy2, w, pre_src, M, K, N):
+            dx = ctx.gelu_src._psd_gelu_hand[1].view(ctx.in_shape)
         elif ctx.needs_input_grad[0]:
             dx = torch.empty(x2.shape, dtype=dy2.dtype, device=dy2.device)
             _dgrad_route(("dgrad", M, K, N), dy2, w, dx)()
@@ -174,6 +225,17 @@ class MfmaLinear(nn.Linear):
         self.act = act
         self.fp8 = fp8
         self._psd_pending_dx: list = []  # gradients of the input handed over by a residual LayerNorm
+        self._psd_gelu_from = None  # psd_gelu_input_from: the GELU Linear whose output is this one's input
+        self._psd_gelu_hand = None  # (forward token, pre-activation gradient, bias gradient) from the consumer
+        self._psd_gelu_pre = None
+
+    def psd_gelu_input_from(self, src: "MfmaLinear") -> None:
+        """Declare that this Linear's input is ``src``'s GELU output and nothing else reads it: the
+        bwd-data GEMM here then returns d(pre-activation) with the GELU backward and src's bias
+        gradient fused in its epilogue (src's backward skips both). Only valid when src's output
+        has no other consumer (e.g. BERT's FFN: ffn2(ffn1(x)))."""
+        assert src.act == "gelu"
+        self._psd_gelu_from = src
 
     def psd_takes_pending_dx(self, x) -> bool:
         """True when this module's forward on ``x`` ran the autograd Function whose backward folds a
