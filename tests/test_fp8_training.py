@@ -187,3 +187,39 @@ def test_bn_backward_writes_the_producers_mx_dy(gpu):
     assert torch.equal(pend[2], s)
     assert torch.equal(pend[1].permute(0, 2, 3, 1).contiguous().view(torch.uint8).flatten(),
                        q.view(torch.uint8).flatten())
+
+
+def test_fp8_wide_resnet_300_step_convergence(gpu, monkeypatch):
+    """300 SGD-momentum steps of a short Wide-ResNet on a fixed learnable synthetic set (8 batches),
+    MX fp8 compute vs bf16 from the same init and batch order (tools/fp8_convergence.py's setup):
+    both fit the set, the fp8 loss curve tracks the bf16 one (mean loss over the run and the step
+    at which the loss halves within 10 %), and the final losses agree."""
+    from parameter_server_distributed_amd.models import prepare
+    from parameter_server_distributed_amd.models.resnet import ResNet
+    from parameter_server_distributed_amd.ops import conv as conv_ops
+
+    monkeypatch.setenv("PSD_FP8_MX", "1")
+    g = torch.Generator().manual_seed(1)
+    batches = [(torch.randn(64, 3, 64, 64, generator=g).to(gpu, torch.bfloat16).contiguous(memory_format=torch.channels_last),
+                torch.randint(0, 100, (64,), generator=g).to(gpu)) for _ in range(8)]
+    curves = {}
+    before = dict(conv_ops.FP8_CALLS)
+    for fp8 in (False, True):
+        torch.manual_seed(0)
+        m = prepare(ResNet((2, 2, 2, 2), num_classes=100, width_per_group=128, fp8=fp8), gpu, torch.bfloat16,
+                    channels_last=True)
+        for p in m.parameters():
+            p.data = p.data.to(torch.bfloat16)
+        m.train()
+        curves[fp8] = _train(m, batches, 300)
+    assert conv_ops.FP8_CALLS["fwd"] - before["fwd"] >= 300 * 6, "fp8 forward kernels did not run"
+    lb, l8 = curves[False], curves[True]
+    avg = lambda L, a, b: sum(L[a:b]) / (b - a)  # noqa: E731
+    half = lambda L: next(i for i, v in enumerate(L) if v < 0.5 * avg(L, 0, 8))  # noqa: E731
+    print(f"bf16: start {avg(lb, 0, 8):.3f} mean {avg(lb, 0, 300):.4f} final {avg(lb, 275, 300):.5f} half@{half(lb)}; "
+          f"fp8: start {avg(l8, 0, 8):.3f} mean {avg(l8, 0, 300):.4f} final {avg(l8, 275, 300):.5f} half@{half(l8)}")
+    for L in (lb, l8):
+        assert avg(L, 275, 300) < 0.1 * avg(L, 0, 8), L[-25:]  # fits the set
+    assert abs(avg(l8, 0, 300) - avg(lb, 0, 300)) <= 0.10 * avg(lb, 0, 300)
+    assert abs(half(l8) - half(lb)) <= max(3, 0.10 * half(lb))
+    assert abs(avg(l8, 275, 300) - avg(lb, 275, 300)) <= 0.05 * avg(lb, 0, 8)
