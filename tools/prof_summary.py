@@ -65,7 +65,7 @@ def main():
 
 CATEGORIES = [
     ("psd: batchnorm", r"psd::bn_"),
-    ("psd: narrow conv (convn / convp / convh)", r"psd::conv[nph]_kernel"),
+    ("psd: narrow conv (convn / convp / convpr / convh)", r"psd::conv(n|p|pr|h)_kernel"),
     ("psd: narrow conv wgrad (convw / convhw)", r"psd::convh?w_"),
     ("psd: gemm", r"psd::.*(gemm|colsum|splitk)"),
     ("psd: fp8 quantise / amax", r"psd::.*(quant|amax|requant)"),
