@@ -48,6 +48,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("quant_fp8_jit_", &quant_fp8_jit_, py::arg("x"), py::arg("out"), py::arg("scale_inv"));
   m.def("quant_fp8_delayed_", &quant_fp8_delayed_, py::arg("x"), py::arg("out"), py::arg("scale_inv"),
         py::arg("hist"), py::arg("margin") = 1.0);
+  m.def("embed_bwd_", &embed_bwd_, py::arg("sorted"), py::arg("perm"), py::arg("dy"), py::arg("out"));
   m.def("xent_fwd", &xent_fwd, py::arg("x"), py::arg("labels"));
   m.def("xent_bwd", &xent_bwd, py::arg("x"), py::arg("labels"), py::arg("lse"), py::arg("scale"));
   m.def("bn_fwd", &bn_fwd, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("running_mean"),

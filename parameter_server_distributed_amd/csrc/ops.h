@@ -146,6 +146,7 @@ std::vector<at::Tensor> bn_pool_bwd(const at::Tensor& gpool, c10::optional<at::T
 at::Tensor gap_bwd(const at::Tensor& dy, int64_t H, int64_t W);
 
 // fused softmax cross-entropy on bf16 logits (xent_ops.cpp)
+void embed_bwd_(const at::Tensor& sorted, const at::Tensor& perm, const at::Tensor& dy, at::Tensor out);
 std::vector<at::Tensor> xent_fwd(const at::Tensor& x, const at::Tensor& labels);
 at::Tensor xent_bwd(const at::Tensor& x, const at::Tensor& labels, const at::Tensor& lse, const at::Tensor& scale);
 

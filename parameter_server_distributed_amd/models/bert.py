@@ -17,6 +17,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.attention import FusedSelfAttention
+from ..ops.embedding import FusedEmbedding
 from ..ops.layernorm import FusedAddLayerNorm, bump_step
 from ..ops.linear import MfmaLinear
 from ..ops.loss import cross_entropy
@@ -53,9 +54,11 @@ class BertForMLM(nn.Module):
     def __init__(self, layers=12, hidden=768, heads=12, vocab=VOCAB, max_pos=512, dropout=0.1):
         super().__init__()
         self.vocab = vocab
-        self.word = nn.Embedding(vocab, hidden)
+        # deterministic gfx950 weight gradients (ops/embedding.py); the position table's gradient is
+        # first summed over the batch by autograd's broadcast, so it stays on nn.Embedding
+        self.word = FusedEmbedding(vocab, hidden)
         self.pos = nn.Embedding(max_pos, hidden)
-        self.tok_type = nn.Embedding(2, hidden)
+        self.tok_type = FusedEmbedding(2, hidden)
         self.ln = nn.LayerNorm(hidden, eps=1e-12)
         self.layers = nn.ModuleList([BertLayer(hidden, heads, 4 * hidden, dropout, i) for i in range(layers)])
         self.head = MfmaLinear(hidden, hidden, act="gelu")

@@ -1,0 +1,55 @@
+"""Embedding with a deterministic gfx950 weight gradient (kernels/embed.hip).
+
+forward   F.embedding (a gather)
+backward  large vocabularies: stable sort of the ids, then one wave per run of equal ids sums the
+          run's output-gradient rows in token order (fp32) into the zero-filled table gradient --
+          no atomics, so the gradient is bitwise reproducible;
+          small vocabularies (<= 16 rows, e.g. BERT's token types): onehot(ids)^T . dy on the GEMM
+          (a per-row sum over thousands of tokens is one long run, which the per-run kernel would
+          sum serially)
+CPU tensors, non-bf16 tables or widths off the kernel's grid (Hd % 256) use nn.Embedding's path.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import native
+
+SMALL_VOCAB = 16
+
+
+class _EmbedFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, weight):
+        ctx.save_for_backward(ids)
+        ctx.shape = weight.shape
+        return F.embedding(ids, weight)
+
+    @staticmethod
+    def backward(ctx, g):
+        (ids,) = ctx.saved_tensors
+        V, Hd = ctx.shape
+        g2 = g.reshape(-1, Hd).contiguous()
+        flat = ids.reshape(-1)
+        if V <= SMALL_VOCAB:
+            onehot = F.one_hot(flat, V).to(g2.dtype)
+            return None, torch.mm(onehot.t(), g2)
+        s, perm = torch.sort(flat, stable=True)
+        dw = torch.zeros(V, Hd, dtype=g2.dtype, device=g2.device)
+        native().embed_bwd_(s, perm, g2, dw)
+        return None, dw
+
+
+class FusedEmbedding(nn.Embedding):
+    """``nn.Embedding`` (no padding_idx / max_norm / sparse) whose weight gradient runs on the
+    deterministic gfx950 kernel for bf16 device tables."""
+
+    def forward(self, ids):
+        w = self.weight
+        if (w.is_cuda and w.dtype == torch.bfloat16 and torch.is_grad_enabled() and w.requires_grad
+                and self.padding_idx is None and self.max_norm is None and not self.sparse
+                and (w.shape[0] <= SMALL_VOCAB or (w.shape[1] % 256 == 0 and w.shape[1] <= 2048))):
+            return _EmbedFn.apply(ids, w)
+        return super().forward(ids)
