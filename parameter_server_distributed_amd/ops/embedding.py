@@ -22,9 +22,10 @@ SMALL_VOCAB = 16
 
 class _EmbedFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, ids, weight):
+    def forward(ctx, ids, weight, mod):
         ctx.save_for_backward(ids)
         ctx.shape = weight.shape
+        ctx.mod = mod
         return F.embedding(ids, weight)
 
     @staticmethod
@@ -33,13 +34,19 @@ class _EmbedFn(torch.autograd.Function):
         V, Hd = ctx.shape
         g2 = g.reshape(-1, Hd).contiguous()
         flat = ids.reshape(-1)
+        # straight into the PS flat-gradient buffer when the data plane installed a sink (the table
+        # gradient is then neither zeroed by the data plane nor accumulated into it)
+        sink = getattr(ctx.mod, "_psd_grad_sink", None)
+        dw = sink(ctx.mod.weight) if sink is not None else None
+        if dw is None or not dw.is_contiguous():
+            dw = torch.empty(V, Hd, dtype=g2.dtype, device=g2.device)
         if V <= SMALL_VOCAB:
-            onehot = F.one_hot(flat, V).to(g2.dtype)
-            return None, torch.mm(onehot.t(), g2)
+            torch.mm(F.one_hot(flat, V).to(g2.dtype).t(), g2, out=dw)
+            return None, dw, None
         s, perm = torch.sort(flat, stable=True)
-        dw = torch.zeros(V, Hd, dtype=g2.dtype, device=g2.device)
+        dw.zero_()
         native().embed_bwd_(s, perm, g2, dw)
-        return None, dw
+        return None, dw, None
 
 
 class FusedEmbedding(nn.Embedding):
@@ -51,5 +58,8 @@ class FusedEmbedding(nn.Embedding):
         if (w.is_cuda and w.dtype == torch.bfloat16 and torch.is_grad_enabled() and w.requires_grad
                 and self.padding_idx is None and self.max_norm is None and not self.sparse
                 and (w.shape[0] <= SMALL_VOCAB or (w.shape[1] % 256 == 0 and w.shape[1] <= 2048))):
-            return _EmbedFn.apply(ids, w)
+            return _EmbedFn.apply(ids, w, self)
         return super().forward(ids)
+
+    def psd_direct_grad_params(self):
+        return [self.weight]
