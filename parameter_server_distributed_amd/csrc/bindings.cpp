@@ -148,7 +148,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("seed"), py::arg("step") = py::none());
   m.def("ln_bwd", &ln_bwd, py::arg("dy"), py::arg("s"), py::arg("mean"), py::arg("rstd"), py::arg("gamma"), py::arg("p"),
         py::arg("seed"), py::arg("step") = py::none(), py::arg("dgamma_out") = py::none(),
-        py::arg("dbeta_out") = py::none());
+        py::arg("dbeta_out") = py::none(), py::arg("dhsum_out") = py::none());
   m.def("bn_pool_bwd", &bn_pool_bwd, py::arg("gpool"), py::arg("gpool2"), py::arg("arg"), py::arg("x"), py::arg("gamma"),
         py::arg("save_mean"), py::arg("save_invstd"), py::arg("ss"), py::arg("dgamma_out") = py::none(),
         py::arg("dbeta_out") = py::none());

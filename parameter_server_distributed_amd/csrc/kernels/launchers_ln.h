@@ -18,7 +18,8 @@ struct LnArgs {
   uint16_t* dh;           // bwd out: gradient of h (dropout mask applied)
   uint16_t* dgamma;       // bwd out [H] bf16 (may be the PS gradient sink)
   uint16_t* dbeta;        // bwd out [H] bf16
-  float* part;            // bwd workspace [ln_bwd_blocks(rows)][2][H] fp32
+  uint16_t* dhsum;        // bwd out [H] bf16 or null: column sums of dh (the branch Linear's bias gradient)
+  float* part;            // bwd workspace [ln_bwd_blocks(rows)][3][H] fp32 ([2] without dhsum)
   const int64_t* step;    // device step counter mixed into the dropout hash (may be null)
   int64_t rows;
   int32_t H;

@@ -116,7 +116,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const uint16_t* __restrict_
   }
 }
 
-template <int E>
+// HS: also the column sums of dh (the bias gradient of the Linear that produced h, which then skips
+// its own column-sum pass: ops/layernorm.py): a third partial row per block
+template <int E, bool HS>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ s,
                                                      const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
                                                      const uint16_t* __restrict__ gamma, uint16_t* __restrict__ dx,
@@ -126,10 +128,11 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
   constexpr int H = 64 * E;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int c0 = lane * E;
-  float g[E], pg[E], pb[E];
+  constexpr int NP = HS ? 3 : 2;
+  float g[E], pg[E], pb[E], ph[E];
   load_e<E>(gamma + c0, g);
 #pragma unroll
-  for (int i = 0; i < E; ++i) pg[i] = pb[i] = 0.f;
+  for (int i = 0; i < E; ++i) pg[i] = pb[i] = ph[i] = 0.f;
   const uint32_t key = dropout_key(seed, step);
   const int64_t wstride = (int64_t)gridDim.x * (blockDim.x >> 6);
   // software-pipelined: the next row's dy / s / stats loads are issued before this row's two wave
@@ -174,21 +177,24 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
     for (int i = 0; i < E; ++i) dv[i] = rstd * (dv[i] - a - sv[i] * bsum);  // d s
     store_e<E>(dx + off, dv);
 #pragma unroll
-    for (int i = 0; i < E; ++i)
+    for (int i = 0; i < E; ++i) {
       dv[i] = (thresh == 0u || keep_elem(key, (uint64_t)(off + i), thresh)) ? dv[i] * scale : 0.f;
+      if constexpr (HS) ph[i] += dv[i];
+    }
     store_e<E>(dh + off, dv);
   }
-  // block partials of dgamma / dbeta: [blk][2][H], waves summed in a fixed order
-  __shared__ float red[4][2][H];
+  // block partials of dgamma / dbeta (/ the dh column sums): [blk][NP][H], waves summed in a fixed order
+  __shared__ float red[4][NP][H];
 #pragma unroll
   for (int i = 0; i < E; ++i) {
     red[wv][0][c0 + i] = pg[i];
     red[wv][1][c0 + i] = pb[i];
+    if constexpr (HS) red[wv][2][c0 + i] = ph[i];
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < 2 * H; c += blockDim.x) {
+  for (int c = threadIdx.x; c < NP * H; c += blockDim.x) {
     const int which = c / H, col = c - which * H;
-    part[((int64_t)blockIdx.x * 2 + which) * H + col] =
+    part[((int64_t)blockIdx.x * NP + which) * H + col] =
         (red[0][which][col] + red[1][which][col]) + (red[2][which][col] + red[3][which][col]);
   }
 }
@@ -196,29 +202,30 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
 // dgamma/dbeta[c] = sum over blocks of part[blk][which][c] -> bf16 (into the PS sink). Block =
 // 32 outputs x 8 partial-row lanes, combined in a fixed order (deterministic); one lane per output
 // walking all 256 partials was latency-bound at ~43 us.
-__global__ __launch_bounds__(256) void ln_param_grad_kernel(const float* __restrict__ part, int nblk, int H,
-                                                            uint16_t* __restrict__ dgamma, uint16_t* __restrict__ dbeta) {
+__global__ __launch_bounds__(256) void ln_param_grad_kernel(const float* __restrict__ part, int nblk, int H, int NP,
+                                                            uint16_t* __restrict__ dgamma, uint16_t* __restrict__ dbeta,
+                                                            uint16_t* __restrict__ dhsum) {
   const int cl = threadIdx.x & 31, rl = threadIdx.x >> 5;
   const int t = blockIdx.x * 32 + cl;  // t = which * H + col
   float s0 = 0.f;
-  if (t < 2 * H) {
+  if (t < NP * H) {
     const int which = t / H, col = t - which * H;
     float s4[4] = {0.f, 0.f, 0.f, 0.f};  // independent loads: nblk/32 round trips, not nblk/8
     int b = rl;
     for (; b + 24 < nblk; b += 32)
 #pragma unroll
-      for (int u = 0; u < 4; ++u) s4[u] += part[((int64_t)(b + 8 * u) * 2 + which) * H + col];
-    for (; b < nblk; b += 8) s4[0] += part[((int64_t)b * 2 + which) * H + col];
+      for (int u = 0; u < 4; ++u) s4[u] += part[((int64_t)(b + 8 * u) * NP + which) * H + col];
+    for (; b < nblk; b += 8) s4[0] += part[((int64_t)b * NP + which) * H + col];
     s0 = (s4[0] + s4[1]) + (s4[2] + s4[3]);
   }
   __shared__ float red[8][33];
   red[rl][cl] = s0;
   __syncthreads();
-  if (rl != 0 || t >= 2 * H) return;
+  if (rl != 0 || t >= NP * H) return;
 #pragma unroll
   for (int r = 1; r < 8; ++r) s0 += red[r][cl];
   const int which = t / H, col = t - which * H;
-  (which ? dbeta : dgamma)[col] = f32_to_bf16(s0);
+  (which == 0 ? dgamma : which == 1 ? dbeta : dhsum)[col] = f32_to_bf16(s0);
 }
 
 int ln_bwd_blocks(int64_t rows) {
@@ -254,14 +261,21 @@ hipError_t launch_ln_bwd(const LnArgs& a, hipStream_t st) {
   const int blocks = ln_bwd_blocks(a.rows);
   const uint32_t th = keep_thresh(a.p);
   const float sc = a.p > 0.f ? 1.f / (1.f - a.p) : 1.f;
-#define PSD_LNB(E)                                                                                                  \
-  hipLaunchKernelGGL(ln_bwd_kernel<E>, dim3(blocks), dim3(256), 0, st, a.dy, a.s, a.mean, a.rstd, a.gamma, a.dx, \
-                     a.dh, a.part, a.rows, a.seed, a.step, th, sc)
-  if (a.H == 768) PSD_LNB(12);
-  else PSD_LNB(16);
+#define PSD_LNB(E, HS)                                                                                              \
+  hipLaunchKernelGGL((ln_bwd_kernel<E, HS>), dim3(blocks), dim3(256), 0, st, a.dy, a.s, a.mean, a.rstd, a.gamma, \
+                     a.dx, a.dh, a.part, a.rows, a.seed, a.step, th, sc)
+  const bool hs = a.dhsum != nullptr;
+  if (a.H == 768) {
+    if (hs) PSD_LNB(12, true);
+    else PSD_LNB(12, false);
+  } else {
+    if (hs) PSD_LNB(16, true);
+    else PSD_LNB(16, false);
+  }
 #undef PSD_LNB
-  hipLaunchKernelGGL(ln_param_grad_kernel, dim3((2 * a.H + 31) / 32), dim3(256), 0, st, a.part, blocks, a.H,
-                     a.dgamma, a.dbeta);
+  const int np = hs ? 3 : 2;
+  hipLaunchKernelGGL(ln_param_grad_kernel, dim3((np * a.H + 31) / 32), dim3(256), 0, st, a.part, blocks, a.H, np,
+                     a.dgamma, a.dbeta, a.dhsum);
   return hipGetLastError();
 }
 

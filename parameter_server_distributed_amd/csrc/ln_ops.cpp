@@ -56,7 +56,7 @@ std::vector<at::Tensor> ln_fwd(const at::Tensor& x, const at::Tensor& h, const a
 std::vector<at::Tensor> ln_bwd(const at::Tensor& dy_in, const at::Tensor& s, const at::Tensor& mean,
                                const at::Tensor& rstd, const at::Tensor& gamma, double p, int64_t seed,
                                c10::optional<at::Tensor> step, c10::optional<at::Tensor> dgamma_out,
-                               c10::optional<at::Tensor> dbeta_out) {
+                               c10::optional<at::Tensor> dbeta_out, c10::optional<at::Tensor> dhsum_out) {
   at::Tensor dy = dy_in.contiguous();
   check_bf16(dy, "dy");
   check_bf16(s, "s");
@@ -71,7 +71,12 @@ std::vector<at::Tensor> ln_bwd(const at::Tensor& dy_in, const at::Tensor& s, con
   at::Tensor dbeta = (dbeta_out.has_value() && dbeta_out->defined()) ? *dbeta_out : at::empty({H}, s.options());
   check_bf16(dgamma, "dgamma");
   check_bf16(dbeta, "dbeta");
-  at::Tensor part = at::empty({(int64_t)ln_bwd_blocks(rows) * 2 * H}, s.options().dtype(at::kFloat));
+  const bool hs = dhsum_out.has_value() && dhsum_out->defined();
+  if (hs) {
+    check_bf16(*dhsum_out, "dhsum");
+    TORCH_CHECK(dhsum_out->numel() == H, "psd ln bwd: dhsum must be [H]");
+  }
+  at::Tensor part = at::empty({(int64_t)ln_bwd_blocks(rows) * (hs ? 3 : 2) * H}, s.options().dtype(at::kFloat));
   LnArgs a{};
   a.dy = cu16(dy);
   a.s = u16(s);
@@ -83,6 +88,7 @@ std::vector<at::Tensor> ln_bwd(const at::Tensor& dy_in, const at::Tensor& s, con
   a.dgamma = u16(dgamma);
   a.dbeta = u16(dbeta);
   a.part = part.data_ptr<float>();
+  a.dhsum = hs ? u16(*dhsum_out) : nullptr;
   a.step = (step.has_value() && step->defined()) ? step->data_ptr<int64_t>() : nullptr;
   a.rows = rows;
   a.H = (int32_t)H;

@@ -27,6 +27,12 @@ class _AddLNFn(torch.autograd.Function):
         y, s, mean, rstd = C.ln_fwd(x.contiguous(), h.contiguous(), weight, bias, mod.eps, p, mod.seed, mod.step)
         ctx.mod, ctx.p, ctx.x_grad_to = mod, p, x_grad_to
         ctx.tok = getattr(x_grad_to, "_psd_tok", None) if x_grad_to is not None else None
+        # h straight from an MfmaLinear with a bias and no activation (ops/linear.py tags its
+        # output): the backward sums dh's columns in its own pass -- that Linear's bias gradient --
+        # and hands it over, so the Linear skips its column-sum kernels
+        src = getattr(h, "_psd_src", None)
+        ctx.h_src = src if (src is not None and src[0].bias is not None and src[0].act in (None, "none")
+                            and src[0]._psd_tok == src[1]) else None
         ctx.save_for_backward(s, mean, rstd, weight)
         return y.view(shp)
 
@@ -38,7 +44,16 @@ class _AddLNFn(torch.autograd.Function):
         dgo = dbo = None
         if sink is not None:
             dgo, dbo = sink(mod.weight), sink(mod.bias)
-        dx, dh, dg, db = native().ln_bwd(dy, s, mean, rstd, w, ctx.p, mod.seed, mod.step, dgo, dbo)
+        dhs = None
+        if ctx.h_src is not None:
+            lin = ctx.h_src[0]
+            lsink = getattr(lin, "_psd_grad_sink", None)
+            dhs = lsink(lin.bias) if lsink is not None else None
+            if dhs is None:
+                dhs = torch.empty_like(lin.bias)
+        dx, dh, dg, db = native().ln_bwd(dy, s, mean, rstd, w, ctx.p, mod.seed, mod.step, dgo, dbo, dhs)
+        if dhs is not None:
+            ctx.h_src[0]._psd_bias_hand = (ctx.h_src[1], dh.data_ptr(), dhs)
         if ctx.x_grad_to is not None:
             # residual-branch gradient handed to the Linear that also consumes x: its dgrad GEMM
             # accumulates onto it (beta = 1) instead of autograd adding the two [M, H] gradients

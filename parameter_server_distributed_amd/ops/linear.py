@@ -151,6 +151,7 @@ class _LinearFn(torch.autograd.Function):
         pre_src = src._psd_gelu_pre if fuse else None
         ctx.save_for_backward(x2, weight, y if act == 1 else aux, pre_src)
         out = y.view(*shp[:-1], N)
+        out._psd_src = (mod, ctx.tok)  # a consumer that can hand this Linear its bias gradient
         if act == 2:
             mod._psd_gelu_pre = aux  # what a fused consumer's backward reads (also saved in this ctx)
             out._psd_gelu_tok = (id(mod), ctx.tok)
@@ -209,6 +210,10 @@ class _LinearFn(torch.autograd.Function):
                 dw = torch.empty(w.shape, dtype=w.dtype, device=w.device)
             _route(("wgrad", M, K, N), lambda: C.gemm_splitk_(dy2, x2, False, False, dw, False, 1.0, 0),
                    lambda: torch.mm(dy2.t(), x2, out=dw), dw)()
+        bh = getattr(ctx.mod, "_psd_bias_hand", None)
+        ctx.mod._psd_bias_hand = None
+        if db is None and bh is not None and bh[0] == ctx.tok and bh[1] == dy2.data_ptr():
+            db = bh[2]  # summed by the consumer LayerNorm's backward (ops/layernorm.py)
         if ctx.has_bias and ctx.needs_input_grad[2] and db is None:
             db = sink(ctx.mod.bias) if sink is not None else None
             if db is None:
@@ -228,6 +233,7 @@ class MfmaLinear(nn.Linear):
         self._psd_gelu_from = None  # psd_gelu_input_from: the GELU Linear whose output is this one's input
         self._psd_gelu_hand = None  # (forward token, pre-activation gradient, bias gradient) from the consumer
         self._psd_gelu_pre = None
+        self._psd_bias_hand = None  # (forward token, dy data pointer, bias gradient) from a consumer LayerNorm
 
     def psd_gelu_input_from(self, src: "MfmaLinear") -> None:
         """Declare that this Linear's input is ``src``'s GELU output and nothing else reads it: the

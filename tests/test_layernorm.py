@@ -101,3 +101,36 @@ def test_residual_grad_handoff_matches_autograd_add(gpu, monkeypatch):
     torch.testing.assert_close(gx, rx, rtol=2e-2, atol=2e-2 * float(rx.abs().max()))
     for n in rp:
         torch.testing.assert_close(gp[n], rp[n], rtol=2e-2, atol=2e-2 * float(rp[n].abs().max()) + 1e-6, msg=n)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_branch_bias_grad_from_layernorm_matches_colsum(gpu, monkeypatch, p):
+    """The residual LayerNorm's backward sums dh's columns (the branch Linear's bias gradient) and
+    hands them to that Linear, which skips its column-sum kernels: every gradient matches the path
+    without the hand-over (h detached from its producer's tag), and bias.grad matches dh's colsum."""
+    from parameter_server_distributed_amd.ops.layernorm import FusedAddLayerNorm
+    from parameter_server_distributed_amd.ops.linear import MfmaLinear
+
+    torch.manual_seed(3)
+    lin = MfmaLinear(3072, 768).to(gpu).to(torch.bfloat16)
+    ln = FusedAddLayerNorm(768, p=p, seed=5).to(gpu).to(torch.bfloat16)
+    ln.step = torch.tensor([2], device=gpu, dtype=torch.int64)
+    x0 = torch.randn(2048, 768, device=gpu).to(torch.bfloat16)
+    a0 = torch.randn(2048, 3072, device=gpu).to(torch.bfloat16)
+    gy = torch.randn(2048, 768, device=gpu).to(torch.bfloat16)
+
+    def run(hand):
+        for t in (lin.weight, lin.bias, ln.weight, ln.bias):
+            t.grad = None
+        x, a = x0.clone().requires_grad_(True), a0.clone().requires_grad_(True)
+        h = lin(a)
+        if not hand:
+            h = h * 1  # a fresh tensor without the producer tag
+        ln(x, h).backward(gy)
+        return [t.grad.float().clone() for t in (x, a, lin.weight, lin.bias, ln.weight, ln.bias)]
+
+    got, ref = run(True), run(False)
+    assert lin._psd_bias_hand is None  # consumed
+    for g, r in zip(got, ref):
+        torch.testing.assert_close(g, r, rtol=1e-2, atol=1e-2 * float(r.abs().max()) + 1e-6)
