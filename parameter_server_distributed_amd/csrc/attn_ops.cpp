@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "kernels/launchers_attn.h"
+#include "kernels/launchers_gemm.h"
 
 namespace psd {
 
@@ -51,8 +52,11 @@ std::vector<at::Tensor> attn_fwd(const at::Tensor& qkv, int64_t heads, double p,
   return {o, lse};
 }
 
+// bias_out (optional, [3*H*Dh] bf16/fp32): also the QKV Linear's bias gradient = the column sums of
+// dqkv, from per-sequence partials the kernel writes + one deterministic column reduce
 at::Tensor attn_bwd(const at::Tensor& dout_in, const at::Tensor& qkv, const at::Tensor& o, const at::Tensor& lse,
-                    int64_t heads, double p, int64_t seed, c10::optional<at::Tensor> step) {
+                    int64_t heads, double p, int64_t seed, c10::optional<at::Tensor> step,
+                    c10::optional<at::Tensor> bias_out) {
   at::Tensor dout = dout_in.contiguous();
   check_attn(dout, "dout");
   check_attn(qkv, "qkv");
@@ -70,8 +74,22 @@ at::Tensor attn_bwd(const at::Tensor& dout_in, const at::Tensor& qkv, const at::
   a.lse = lse.data_ptr<float>();
   a.dout = reinterpret_cast<const uint16_t*>(dout.data_ptr());
   a.dqkv = reinterpret_cast<uint16_t*>(dqkv.data_ptr());
+  const bool bias = bias_out.has_value() && bias_out->defined();
+  at::Tensor bpart;
+  if (bias) {
+    TORCH_CHECK(bias_out->is_cuda() && bias_out->is_contiguous() && bias_out->numel() == qkv.size(2) &&
+                    (bias_out->scalar_type() == at::kBFloat16 || bias_out->scalar_type() == at::kFloat),
+                "psd attn bwd: bias_out must be a contiguous [3*H*Dh] bf16/fp32 tensor");
+    bpart = at::empty({(int64_t)a.B, qkv.size(2)}, qkv.options().dtype(at::kFloat));
+    a.bpart = bpart.data_ptr<float>();
+  }
   hipError_t e = launch_attn_bwd(a, attn_stream(qkv));
   TORCH_CHECK(e == hipSuccess, "psd attn bwd: ", hipGetErrorString(e));
+  if (bias) {
+    e = launch_colsum_final(a.bpart, a.B, (int)qkv.size(2), bias_out->data_ptr(),
+                            bias_out->scalar_type() == at::kBFloat16, 0, attn_stream(qkv));
+    TORCH_CHECK(e == hipSuccess, "psd attn bwd bias: ", hipGetErrorString(e));
+  }
   return dqkv;
 }
 

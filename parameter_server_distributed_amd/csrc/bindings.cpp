@@ -143,7 +143,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("heads"), py::arg("p"), py::arg("seed"),
         py::arg("step") = py::none());
   m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("qkv"), py::arg("o"), py::arg("lse"), py::arg("heads"),
-        py::arg("p"), py::arg("seed"), py::arg("step") = py::none());
+        py::arg("p"), py::arg("seed"), py::arg("step") = py::none(), py::arg("bias_out") = py::none());
   m.def("ln_fwd", &ln_fwd, py::arg("x"), py::arg("h"), py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("p"),
         py::arg("seed"), py::arg("step") = py::none());
   m.def("ln_bwd", &ln_bwd, py::arg("dy"), py::arg("s"), py::arg("mean"), py::arg("rstd"), py::arg("gamma"), py::arg("p"),

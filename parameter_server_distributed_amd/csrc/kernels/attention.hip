@@ -250,6 +250,7 @@ __global__ __launch_bounds__(128 * NW) void attn_bwd_kernel(AttnArgs a) {
   uint8_t* dS = Pd + S * LDP * 2;   // dS = P (dP - D) [q][key]
   float* lse_s = reinterpret_cast<float*>(dS + S * LDP * 2);
   float* D_s = lse_s + S;
+  float* cs_s = D_s + S;  // [NW][3][64] per-key/query-block column sums of dq, dk, dv (bpart)
 
   const int lane = threadIdx.x & 63, hh = lane >> 5;
   const int w = threadIdx.x >> 7, sub = (threadIdx.x >> 6) & 1;  // 32-row block, half of its work
@@ -361,11 +362,22 @@ __global__ __launch_bounds__(128 * NW) void attn_bwd_kernel(AttnArgs a) {
         dk = mfma(trfrag(dS, LDP * 2, 16 * ks, k0), trfrag(Qs, LDT * 2, 16 * ks, 32 * dt), dk);
       }
       const int d = 32 * dt + (lane & 31);
+      float sk = 0.f, sv = 0.f;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int64_t r = (int64_t)(k0 + acc_row(i, hh)) * qkv_rs + d;
         dq_base[r + HD] = f32_to_bf16(dk[i] * a.scale);
         dq_base[r + 2 * HD] = f32_to_bf16(dv[i]);
+        sk += dk[i];
+        sv += dv[i];
+      }
+      if (a.bpart) {  // this wave's 32 keys: the two lane halves hold 16 rows each
+        sk += __shfl_xor(sk, 32);
+        sv += __shfl_xor(sv, 32);
+        if (hh == 0) {
+          cs_s[(w * 3 + 1) * 64 + d] = sk * a.scale;
+          cs_s[(w * 3 + 2) * 64 + d] = sv;
+        }
       }
     }
     // phase 3: waves (w, sub) own queries q0..q0+31, head dims 32*sub..: dQ = scale * dS K
@@ -376,8 +388,26 @@ __global__ __launch_bounds__(128 * NW) void attn_bwd_kernel(AttnArgs a) {
 #pragma unroll
       for (int ks = 0; ks < S / 16; ++ks) dq = mfma(rowfrag(dS, LDP * 2, q0, 16 * ks), trfrag(Ks, LDT * 2, 16 * ks, 32 * dt), dq);
       const int d = 32 * dt + (lane & 31);
+      float sq = 0.f;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) dq_base[(int64_t)(q0 + acc_row(i, hh)) * qkv_rs + d] = f32_to_bf16(dq[i] * a.scale);
+      for (int i = 0; i < 16; ++i) {
+        dq_base[(int64_t)(q0 + acc_row(i, hh)) * qkv_rs + d] = f32_to_bf16(dq[i] * a.scale);
+        sq += dq[i];
+      }
+      if (a.bpart) {
+        sq += __shfl_xor(sq, 32);
+        if (hh == 0) cs_s[(w * 3 + 0) * 64 + d] = sq * a.scale;
+      }
+    }
+    if (a.bpart) {  // the item's column sums in a fixed order over the blocks -> bpart[b][t * HD + h * 64 + d]
+      __syncthreads();
+      if ((int)threadIdx.x < 3 * 64) {
+        const int t = threadIdx.x >> 6, d = threadIdx.x & 63;
+        float acc = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < NW; ++ww) acc += cs_s[(ww * 3 + t) * 64 + d];
+        a.bpart[(int64_t)b * 3 * HD + t * HD + h * D + d] = acc;
+      }
     }
     __syncthreads();  // every read of this item's LDS done before the next item overwrites it
   }
@@ -387,7 +417,7 @@ __global__ __launch_bounds__(128 * NW) void attn_bwd_kernel(AttnArgs a) {
 bool attn_supported(int S, int head_dim) { return head_dim == D && S >= 32 && S <= 128 && S % 32 == 0; }
 
 static int fwd_lds(int S) { return 2 * S * LDT * 2; }
-static int bwd_lds(int S) { return 4 * S * LDT * 2 + 2 * S * (S + 8) * 2 + 2 * S * 4; }
+static int bwd_lds(int S) { return 4 * S * LDT * 2 + 2 * S * (S + 8) * 2 + 2 * S * 4 + (S / 32) * 3 * 64 * 4; }
 
 template <int NW>
 static hipError_t launch_fwd_t(const AttnArgs& a, hipStream_t st) {

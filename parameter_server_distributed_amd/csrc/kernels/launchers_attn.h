@@ -11,6 +11,8 @@ struct AttnArgs {
   float* lse;             // fwd out / bwd in: [B, H, S] fp32 (natural-log row log-sum-exp)
   const uint16_t* dout;   // bwd in: [B, S, H, 64] bf16
   uint16_t* dqkv;         // bwd out: [B, S, 3, H, 64] bf16
+  float* bpart;           // bwd out or null: [B][3*H*64] fp32 column sums of dqkv over each sequence
+                          // (the QKV Linear's bias gradient, summed over B by the caller)
   const int64_t* step;    // device step counter mixed into the dropout hash (may be null)
   int32_t B, S, H;
   float scale;            // softmax scale (1/sqrt(64))

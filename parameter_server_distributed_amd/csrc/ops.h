@@ -133,7 +133,8 @@ at::Tensor stem_wgrad(const at::Tensor& x, const at::Tensor& dy);
 std::vector<at::Tensor> attn_fwd(const at::Tensor& qkv, int64_t heads, double p, int64_t seed,
                                  c10::optional<at::Tensor> step);
 at::Tensor attn_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor& o, const at::Tensor& lse,
-                    int64_t heads, double p, int64_t seed, c10::optional<at::Tensor> step);
+                    int64_t heads, double p, int64_t seed, c10::optional<at::Tensor> step,
+                    c10::optional<at::Tensor> bias_out);
 std::vector<at::Tensor> ln_fwd(const at::Tensor& x, const at::Tensor& h, const at::Tensor& gamma, const at::Tensor& beta,
                                double eps, double p, int64_t seed, c10::optional<at::Tensor> step);
 std::vector<at::Tensor> ln_bwd(const at::Tensor& dy, const at::Tensor& s, const at::Tensor& mean, const at::Tensor& rstd,

@@ -15,6 +15,8 @@ the tests compare against.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -25,6 +27,11 @@ from .. import native
 class _AttnFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv, mod, p):
+        # qkv straight from an MfmaLinear with a bias (ops/linear.py tags its output): backward also
+        # sums dqkv's columns -- that Linear's bias gradient -- and hands it over
+        src = getattr(qkv, "_psd_src", None) if os.environ.get("PSD_ATTN_BIAS", "1") != "0" else None
+        ctx.src = src if (src is not None and src[0].bias is not None and src[0].act in (None, "none")
+                          and src[0]._psd_tok == src[1]) else None
         qkv = qkv.contiguous()
         o, lse = native().attn_fwd(qkv, mod.heads, p, mod.seed, mod.step)
         ctx.mod, ctx.p = mod, p
@@ -35,7 +42,17 @@ class _AttnFn(torch.autograd.Function):
     def backward(ctx, do):
         qkv, o, lse = ctx.saved_tensors
         mod = ctx.mod
-        return native().attn_bwd(do, qkv, o, lse, mod.heads, ctx.p, mod.seed, mod.step), None, None
+        db = None
+        if ctx.src is not None:
+            lin = ctx.src[0]
+            sink = getattr(lin, "_psd_grad_sink", None)
+            db = sink(lin.bias) if sink is not None else None
+            if db is None:
+                db = torch.empty_like(lin.bias)
+        dqkv = native().attn_bwd(do, qkv, o, lse, mod.heads, ctx.p, mod.seed, mod.step, db)
+        if db is not None:
+            ctx.src[0]._psd_bias_hand = (ctx.src[1], dqkv.data_ptr(), db)
+        return dqkv, None, None
 
 
 class FusedSelfAttention(nn.Module):

@@ -5,7 +5,7 @@ R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 OUT=$R/gpurun_out/attn
 mkdir -p "$OUT"
 cd "$R"
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_attention.py tests/test_embedding.py > "$OUT/tests.txt" 2>&1
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_attention.py tests/test_embedding.py tests/test_layernorm.py > "$OUT/tests.txt" 2>&1
 rc=$?; tail -2 "$OUT/tests.txt"
 if [ $rc -ne 0 ]; then grep -E "^E  |FAILED" "$OUT/tests.txt" | head -20; exit $rc; fi
 timeout -k 10 400 python3 bench.py --model bert_base --steps 20 --warmup 5 --out "$OUT/bert.json" > "$OUT/bert.log" 2>&1 || { tail -20 "$OUT/bert.log"; exit 1; }

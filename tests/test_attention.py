@@ -95,3 +95,33 @@ def test_bert_layer_uses_fused_attention(gpu):
     a = F.scaled_dot_product_attention(q, k, v).transpose(1, 2).reshape(B, S, 768)
     torch.testing.assert_close(layer.attn(qkv).float(), a, atol=2e-2, rtol=2e-2)
     assert torch.isfinite(x.grad).all()
+
+
+@pytest.mark.gpu
+def test_qkv_bias_grad_from_attention_matches_colsum(gpu):
+    """The attention backward also sums dQKV's columns (per-sequence partials + one column reduce)
+    and hands them to the QKV Linear as its bias gradient: every gradient matches the path where the
+    Linear sums them itself."""
+    from parameter_server_distributed_amd.ops.attention import FusedSelfAttention
+    from parameter_server_distributed_amd.ops.linear import MfmaLinear
+
+    torch.manual_seed(4)
+    B, S, H = 8, 128, 4
+    lin = MfmaLinear(256, 3 * H * 64).to(gpu).to(torch.bfloat16)
+    att = FusedSelfAttention(H, p=0.0).to(gpu)
+    x0 = torch.randn(B, S, 256, device=gpu).to(torch.bfloat16)
+    g = torch.randn(B, S, H * 64, device=gpu).to(torch.bfloat16)
+
+    def run(hand):
+        lin.weight.grad = lin.bias.grad = None
+        x = x0.clone().requires_grad_(True)
+        qkv = lin(x)
+        if not hand:
+            qkv = qkv * 1  # untagged: the Linear sums its own bias gradient
+        att(qkv).backward(g)
+        return [t.float().clone() for t in (x.grad, lin.weight.grad, lin.bias.grad)]
+
+    got, ref = run(True), run(False)
+    assert lin._psd_bias_hand is None
+    for a, b in zip(got, ref):
+        torch.testing.assert_close(a, b, rtol=1e-2, atol=1e-2 * float(b.abs().max()) + 1e-6)
