@@ -875,7 +875,7 @@ std::vector<at::Tensor> bn_bwd_dual_pre(const at::Tensor& g_in, const at::Tensor
                                         const at::Tensor& xd_in, const at::Tensor& gamma_d, const at::Tensor& mean_d,
                                         const at::Tensor& invstd_d, c10::optional<at::Tensor> dgamma_out,
                                         c10::optional<at::Tensor> dbeta_out, c10::optional<at::Tensor> dgamma_d_out,
-                                        c10::optional<at::Tensor> dbeta_d_out, bool fold) {
+                                        c10::optional<at::Tensor> dbeta_d_out, bool fold, bool fold_d) {
   const c10::DeviceGuard dg(x_in.device());
   at::Tensor x = nhwc(x_in), g = nhwc(g_in), xd = nhwc(xd_in);
   const int64_t C = channels(x), M = x.numel() / C;
@@ -899,7 +899,10 @@ std::vector<at::Tensor> bn_bwd_dual_pre(const at::Tensor& g_in, const at::Tensor
   const bool many = rows > kFoldRows;
   at::Tensor fw = many ? at::empty({(int64_t)kFoldRows * 2 * C}, f32) : at::Tensor();
   at::Tensor fwd = many ? at::empty({(int64_t)kFoldRows * 2 * C}, f32) : at::Tensor();
-  at::Tensor dx = fold ? at::Tensor() : at::empty_like(x), dxd = at::empty_like(x);
+  // fold / fold_d: the BN input gradient of bn3 / of the downsample BN is folded into its
+  // convolution's backward (ops/conv.py _fold_backward): not written here
+  TORCH_CHECK(!fold_d || fold, "psd bn_bwd_dual_pre: fold_d needs fold");
+  at::Tensor dx = fold ? at::Tensor() : at::empty_like(x), dxd = fold_d ? at::Tensor() : at::empty_like(x);
   BnDualPreArgs a{};
   a.g = reinterpret_cast<const uint16_t*>(g.data_ptr());
   a.x = reinterpret_cast<const uint16_t*>(x.data_ptr());
@@ -922,12 +925,12 @@ std::vector<at::Tensor> bn_bwd_dual_pre(const at::Tensor& g_in, const at::Tensor
   a.coef = coef.data_ptr<float>();
   a.coef_d = coef_d.data_ptr<float>();
   a.dx = fold ? nullptr : reinterpret_cast<uint16_t*>(dx.data_ptr());
-  a.dxd = reinterpret_cast<uint16_t*>(dxd.data_ptr());
+  a.dxd = fold_d ? nullptr : reinterpret_cast<uint16_t*>(dxd.data_ptr());
   a.M = M;
   a.C = (int)C;
   const hipError_t e = launch_bn_bwd_dual_pre(a, stream_of(x));
   TORCH_CHECK(e == hipSuccess, "psd bn_bwd_dual_pre: ", hipGetErrorString(e));
-  return {dx, dxd, dgamma, dbeta, dgamma_d, dbeta_d, coef};
+  return {dx, dxd, dgamma, dbeta, dgamma_d, dbeta_d, coef, coef_d};
 }
 
 }  // namespace psd

@@ -1060,6 +1060,8 @@ hipError_t launch_bn_bwd_dual_pre(const BnDualPreArgs& a, hipStream_t st) {
     fe = finalize_pre(a.part_d, a.rows, a.fold_ws_d, a.M, a.C, a.gamma_d, a.mean_d, a.invstd_d, a.dgamma_d, a.dbeta_d,
                       a.coef_d, st);
   if (fe != hipSuccess) return fe;
+  if (!a.dx && !a.dxd) return hipSuccess;  // both BN input gradients folded into their convolutions
+  if (!a.dxd) return hipErrorInvalidValue;
   const int64_t nvec = a.M * (a.C / 8);
   if (a.dx)
     hipLaunchKernelGGL(bn_bwd_elemt_dual_kernel<true>, dim3(elem_grid(nvec, a.C)), dim3(256), 0, st, a.g, a.x, a.coef,

@@ -84,6 +84,9 @@ class Bottleneck(nn.Module):
         # bn3's input gradient can be folded into conv3's backward GEMMs (ops/conv.py _fold_backward)
         if isinstance(self.conv3, Conv1x1) and not fp8:
             object.__setattr__(self.bn3, "_psd_fold_conv", self.conv3)
+            # and a stride-1 downsample BN's into the downsample conv (layer 1's first block)
+            if downsample is not None and len(downsample) == 2 and isinstance(downsample[0], Conv1x1):
+                object.__setattr__(downsample[1], "_psd_fold_conv", downsample[0])
         if fp8:  # bn1 / bn2 quantise their outputs for the fp8 conv2 / conv3 in their apply pass
             # (plain attributes: object.__setattr__ keeps the consumer from becoming a submodule)
             object.__setattr__(self.bn1, "_psd_q8_consumer", self.conv2)

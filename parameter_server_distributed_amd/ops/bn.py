@@ -267,11 +267,17 @@ class _BNAddBNReluFn(torch.autograd.Function):
             # both reductions ran in the consumer convolution's bwd-data epilogue (convn mode 3): g is
             # the masked gradient incl. the residual branch; finalize both + one elementwise pass
             g, part, rows, part_d = pre
-            dx, drr, dg3, db3, dgd, dbd, coef = C.bn_bwd_dual_pre(g, x, w3, mean, invstd, part, part_d, rows, r, wd,
-                                                                  mean_d, invstd_d, dg3o, db3o, dgdo, dbdo,
-                                                                  fold=conv is not None)
+            # the downsample BN folded into its (stride-1 1x1) convolution too: no elementwise pass
+            # at all -- both convolutions take g and their BN's coefficients (ops/conv.py _fold_backward)
+            convd = _fold_target(bnd, r) if conv is not None and _at.enabled("PSD_BN_FOLD_DS") else None
+            dx, drr, dg3, db3, dgd, dbd, coef, coef_d = C.bn_bwd_dual_pre(
+                g, x, w3, mean, invstd, part, part_d, rows, r, wd, mean_d, invstd_d, dg3o, db3o, dgdo, dbdo,
+                fold=conv is not None, fold_d=convd is not None)
             if conv is not None:
                 _hand_fold(conv, g, coef, x)
+                if convd is not None:
+                    _hand_fold(convd, g, coef_d, r)
+                    return g, dg3, db3, g, dgd, dbd, None, None
                 return g, dg3, db3, drr, dgd, dbd, None, None
             return dx, dg3, db3, drr, dgd, dbd, None, None
         dy2 = take_dr(bn3._psd_pending_dr.pop()) if getattr(bn3, "_psd_pending_dr", None) else None
