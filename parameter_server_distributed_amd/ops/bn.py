@@ -129,10 +129,30 @@ def _fold_target(mod, x: torch.Tensor):
     return conv
 
 
-def _hand_fold(conv, g, coef, x):
-    """Give ``conv``'s backward what replaces the BN input gradient: (g, coef, the BN input)."""
+def _hand_fold(conv, g, coef, x, P=None):
+    """Give ``conv``'s backward what replaces the BN input gradient: (g, coef, the BN input[, the
+    fold wgrad products [g | x | 1]^T x_in already taken])."""
     conv._psd_fold_out = None
-    conv._psd_fold_pending = (g, coef, x)
+    conv._psd_fold_x = None
+    conv._psd_fold_pending = (g, coef, x) if P is None else (g, coef, x, P)
+
+
+def _fold_pair_ok(bn3, x, bnd, r):
+    """Both tail BNs fold into stride-1 1x1 convolutions whose fold wgrad takes their whole input:
+    the dual tail can then take sum g y3 / sum g yd from g^T a2 / g^T x_in (rowdot) instead of
+    reading y3 / yd in the consumer's epilogue. Returns (conv3, convd) or None."""
+    if not (_at.enabled("PSD_BN_FOLD_DS") and os.environ.get("PSD_DUAL_NOBX", "0") == "1"):
+        return None
+    c3, cd = _fold_target(bn3, x), _fold_target(bnd, r)
+    if c3 is None or cd is None:
+        return None
+    C = native()
+    for conv in (c3, cd):
+        xin = getattr(conv, "_psd_fold_x", None)
+        if xin is None or not xin.is_contiguous(memory_format=torch.channels_last) \
+                or C.convw_fold_rows(conv.weight.shape[0], conv.weight.shape[1]) <= 0:
+            return None
+    return c3, cd
 
 
 class _FusedBNFn(torch.autograd.Function):
@@ -241,8 +261,12 @@ class _BNAddBNReluFn(torch.autograd.Function):
                                              **q8, **_stats_args(bn3, x))
         _q8_hand_over(bn3, y, q8)
         # for the consumer convolution's bwd-data epilogue (ops/conv.py _bn_bwd_fusion, mode 3): both
-        # BNs' backward reductions ride on it
-        bn3._psd_fwd = (y, x, mean, None, mbits, r, mean_d)
+        # BNs' backward reductions ride on it. With both BNs folded (layer 1) the epilogue reduces
+        # only sum g (mode 2 without the BN input) and backward completes sum g y3 / sum g yd from
+        # the fold products: y3 and yd are not read there
+        pair = _fold_pair_ok(bn3, x, bnd, r)
+        ctx.pair = None if pair is None else (pair[0], pair[1], pair[0]._psd_fold_x, pair[1]._psd_fold_x)
+        bn3._psd_fwd = (y, x, mean, None, mbits, r, mean_d) if pair is None else (y, None, mean, None, mbits, None, None)
         ctx.bn3, ctx.bnd = bn3, bnd
         ctx.save_for_backward(x, mbits, w3, mean, invstd, r, wd, mean_d, invstd_d)
         return y
@@ -263,6 +287,33 @@ class _BNAddBNReluFn(torch.autograd.Function):
         conv = _fold_target(bn3, x)
         pre = getattr(bn3, "_psd_bwd_pre", None)
         bn3._psd_bwd_pre = None
+        pair = ctx.pair
+        ctx.pair = None
+        if pair is not None and pre is not None and len(pre) == 3 and pre[0].data_ptr() == dy.data_ptr() \
+                and pre[0].shape == dy.shape and conv is pair[0] and _fold_target(bnd, r) is pair[1]:
+            # the consumer reduced (sum g, -mean3 sum g); sum g y3 = sum_i W3 (g^T a2), sum g yd =
+            # sum_i Wd (g^T x_in) from the fold wgrads taken now (and handed on, not retaken)
+            g, part, rows = pre
+            if part.shape[0] <= rows:
+                raise RuntimeError("psd dual tail: the partials buffer has no row for sum g y")
+            (c3, cd, a2, xin) = pair
+            Ps = []
+            for conv_, xin_ in ((c3, a2), (cd, xin)):
+                P = torch.empty(C.convw_fold_rows(conv_.weight.shape[0], conv_.weight.shape[1]), xin_.shape[1],
+                                device=g.device, dtype=torch.float32)
+                if not C.convw_(g, xin_, P, 1, 1, 1, 0, fold=True):
+                    raise RuntimeError("psd dual tail: convw_ declined the fold wgrad")
+                Ps.append(P)
+            part_d = part.clone()
+            part_d[:rows, 1] = part[:rows, 0] * (-mean_d)
+            C.bnfold_rowdot(Ps[0], c3.weight, part[rows])
+            C.bnfold_rowdot(Ps[1], cd.weight, part_d[rows])
+            _, _, dg3, db3, dgd, dbd, coef, coef_d = C.bn_bwd_dual_pre(
+                g, x, w3, mean, invstd, part, part_d, rows + 1, r, wd, mean_d, invstd_d, dg3o, db3o, dgdo, dbdo,
+                fold=True, fold_d=True)
+            _hand_fold(c3, g, coef, x, Ps[0])
+            _hand_fold(cd, g, coef_d, r, Ps[1])
+            return g, dg3, db3, g, dgd, dbd, None, None
         if pre is not None and len(pre) == 4 and pre[0].data_ptr() == dy.data_ptr() and pre[0].shape == dy.shape:
             # both reductions ran in the consumer convolution's bwd-data epilogue (convn mode 3): g is
             # the masked gradient incl. the residual branch; finalize both + one elementwise pass

@@ -655,6 +655,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         y = cands[_route(("conv1x1",) + key, cands, "miopen", bn if len(cands) > 2 else None)]()
         if mod is not None:  # this output may have its consumer BN's backward folded (_fold_backward)
             mod._psd_fold_out = (y.data_ptr(), tuple(y.shape))
+            mod._psd_fold_x = x  # (a dual tail takes g^T x before the BN finalize: ops/bn.py)
         return y
 
     @staticmethod
@@ -670,7 +671,7 @@ class _Conv1x1Fn(torch.autograd.Function):
             if fold[0].data_ptr() != dy.data_ptr() or fold[0].shape != dy.shape:
                 raise RuntimeError("psd BN-backward fold: the gradient reaching the convolution is not the one its BN "
                                    "handed over (its input gradient was never formed)")
-            dx, dw, dy = _fold_backward(ctx, fold, x, weight, need_x, need_w)
+            dx, dw, dy = _fold_backward(ctx, fold[:3], x, weight, need_x, need_w, P=fold[3] if len(fold) > 3 else None)
             if dy is None:
                 return dx, dw, None, None
             need_x = need_x and dx is None  # unfolded: dy now holds the BN input gradient
