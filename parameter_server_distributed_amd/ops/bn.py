@@ -141,7 +141,7 @@ def _fold_pair_ok(bn3, x, bnd, r):
     """Both tail BNs fold into stride-1 1x1 convolutions whose fold wgrad takes their whole input:
     the dual tail can then take sum g y3 / sum g yd from g^T a2 / g^T x_in (rowdot) instead of
     reading y3 / yd in the consumer's epilogue. Returns (conv3, convd) or None."""
-    if not (_at.enabled("PSD_BN_FOLD_DS") and os.environ.get("PSD_DUAL_NOBX", "0") == "1"):
+    if not (_at.enabled("PSD_BN_FOLD_DS") and os.environ.get("PSD_DUAL_NOBX", "1") != "0"):
         return None
     c3, cd = _fold_target(bn3, x), _fold_target(bnd, r)
     if c3 is None or cd is None:
