@@ -20,9 +20,11 @@ void embed_bwd_(const at::Tensor& sorted, const at::Tensor& perm, const at::Tens
                   out.size(1) == dy.size(1) && out.device() == dy.device(),
               "psd embed_bwd: out must be contiguous bf16 [V, Hd] on dy's device");
   const c10::DeviceGuard g(dy.device());
+  const int64_t T = dy.size(0);
+  at::Tensor part = at::empty({(T + kEmbedChunk - 1) / kEmbedChunk, dy.size(1)}, dy.options().dtype(at::kFloat));
   hipError_t e = launch_embed_bwd(sorted.data_ptr<int64_t>(), perm.data_ptr<int64_t>(),
-                                  reinterpret_cast<const uint16_t*>(dy.data_ptr()), dy.size(0), (int)dy.size(1),
-                                  reinterpret_cast<uint16_t*>(out.data_ptr()),
+                                  reinterpret_cast<const uint16_t*>(dy.data_ptr()), T, (int)dy.size(1),
+                                  part.data_ptr<float>(), reinterpret_cast<uint16_t*>(out.data_ptr()),
                                   c10::hip::getCurrentHIPStream(dy.device().index()).stream());
   TORCH_CHECK(e == hipSuccess, "psd embed_bwd: ", hipGetErrorString(e));
 }

@@ -34,6 +34,9 @@ import time
 import torch
 
 _DECISIONS: dict[tuple, str] = {}
+_DECLINED_KEYS: set = set()  # keys where every candidate declined (decided once, for every rank)
+_DECLINED = "__declined__"
+_FAILED = "__failed__"
 _SOURCE = {"local": 0, "claimed": 0, "peer": 0, "file": 0}
 _FILE_KEYS: set = set()
 
@@ -115,6 +118,10 @@ def _peer_decision(st, skey: str, candidates: dict) -> str | None:
     """Another rank claimed ``skey``: wait for its published choice."""
     st.wait([f"psd/autotune/d/{skey}"], datetime.timedelta(seconds=float(os.environ.get("PSD_AUTOTUNE_WAIT_S", "900"))))
     name = st.get(f"psd/autotune/d/{skey}").decode()
+    if name == _DECLINED:
+        raise Declined(f"autotune {skey}: every candidate declined on the deciding rank")
+    if name.startswith(_FAILED):
+        raise RuntimeError(f"autotune {skey}: the deciding rank failed: {name[len(_FAILED) + 1:]}")
     if name not in candidates:
         raise RuntimeError(f"autotune: rank decision {name!r} for {skey} is not a candidate here {sorted(candidates)}")
     return name
@@ -127,6 +134,8 @@ def choose(key: tuple, candidates: dict, default: str, probe=None) -> str:
     got = _DECISIONS.get(key)
     if got is not None and got in candidates:
         return got
+    if key in _DECLINED_KEYS:
+        raise Declined(f"autotune {key}: every candidate declined")
     # A/B runs: e.g. "mfma" / "blas" / "miopen" / "gemm", or a priority list "psdnb0,psdn0" (the
     # first name this op offers wins)
     for forced in os.environ.get("PSD_AUTOTUNE_FORCE", "").split(","):
@@ -138,11 +147,27 @@ def choose(key: tuple, candidates: dict, default: str, probe=None) -> str:
     st = _store()
     skey = repr(key)
     if st is not None and int(st.add(f"psd/autotune/c/{skey}", 1)) > 1:
-        best = _peer_decision(st, skey, candidates)
+        try:
+            best = _peer_decision(st, skey, candidates)
+        except Declined:
+            _DECLINED_KEYS.add(key)
+            raise
         _DECISIONS[key] = best
         _SOURCE["peer"] += 1
         return best
-    best = _time_and_pick(key, candidates, default, probe)
+    # The claiming rank always publishes -- a decision, "every candidate declined", or its error --
+    # so no peer waits on a key nobody will decide (and this rank never claims it again).
+    try:
+        best = _time_and_pick(key, candidates, default, probe)
+    except Declined:
+        _DECLINED_KEYS.add(key)
+        if st is not None:
+            st.set(f"psd/autotune/d/{skey}", _DECLINED)
+        raise
+    except BaseException as e:
+        if st is not None:
+            st.set(f"psd/autotune/d/{skey}", f"{_FAILED}:{type(e).__name__}: {e}"[:512])
+        raise
     if st is not None:
         st.set(f"psd/autotune/d/{skey}", best)
         _SOURCE["claimed"] += 1

@@ -1,9 +1,11 @@
 """Embedding with a deterministic gfx950 weight gradient (kernels/embed.hip).
 
 forward   F.embedding (a gather)
-backward  large vocabularies: stable sort of the ids, then one wave per run of equal ids sums the
-          run's output-gradient rows in token order (fp32) into the zero-filled table gradient --
-          no atomics, so the gradient is bitwise reproducible;
+backward  large vocabularies: stable sort of the ids; runs of equal ids are cut into segments of
+          at most 64 sorted positions, one wave sums a segment's output-gradient rows (fp32), and
+          the run's first wave adds the run's segment partials in order and writes the table row
+          -- no atomics, so the gradient is bitwise reproducible, and a skewed batch (thousands of
+          [PAD] tokens) costs no more than a uniform one;
           small vocabularies (<= 16 rows, e.g. BERT's token types): onehot(ids)^T . dy on the GEMM
           (a per-row sum over thousands of tokens is one long run, which the per-run kernel would
           sum serially)

@@ -55,3 +55,52 @@ def test_autotune_ranks_agree_and_file_roundtrip(tmp_path):
     for i in range(3):
         assert at.choose(("test", i), {"a": None, "b": None}, "a") == p0[i]
         at.set_decision(("test", i), None)
+
+
+def _rank_declined(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PSD_AUTOTUNE_WAIT_S="60")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from parameter_server_distributed_amd.ops import autotune as at
+
+    def nope():
+        raise at.Declined("shape not taken")
+
+    def boom():
+        raise MemoryError("simulated OOM")
+
+    res = []
+    for rep in range(2):  # the second pass must neither re-claim nor wait on the key
+        t0 = time.time()
+        try:
+            at.choose(("all_declined",), {"a": nope, "b": nope}, "a")
+            res.append("chosen")
+        except at.Declined:
+            res.append("declined")
+        res.append(time.time() - t0 < 30)
+    dist.barrier()
+    # a claiming rank that fails with a real error publishes it; the peer raises instead of hanging
+    if rank == 0:
+        try:
+            at.choose(("fails",), {"a": boom}, "a")
+        except MemoryError:
+            res.append("error")
+        dist.barrier()
+    else:
+        dist.barrier()  # rank 0 claims first
+        try:
+            at.choose(("fails",), {"a": boom}, "a")
+        except RuntimeError as e:
+            res.append("error" if "failed" in str(e) else repr(e))
+    with open(os.path.join(out_dir, f"d{rank}.txt"), "w") as f:
+        f.write(repr(res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_autotune_all_declined_publishes_to_peers(tmp_path):
+    """a claimed key whose candidates all decline (or whose timing raises) must be
+    published, so peers raise at once instead of waiting PSD_AUTOTUNE_WAIT_S on it."""
+    mp.spawn(_rank_declined, args=(2, _port(), str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        res = eval(open(tmp_path / f"d{r}.txt").read())
+        assert res == ["declined", True, "declined", True, "error"], (r, res)

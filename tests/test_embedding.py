@@ -38,3 +38,37 @@ def test_embedding_grad_matches_fp32(gpu, V, Hd, T):
     e.weight.grad = None
     e(ids).backward(g)
     assert torch.equal(e.weight.grad, first)  # deterministic
+
+
+@pytest.mark.gpu
+def test_embedding_skewed_ids_fast_and_exact(gpu):
+    """a heavily skewed batch (half the tokens one id, a Zipf tail) must be as exact as
+    a uniform one and not serialise a 10^4-row run on one wave."""
+    from parameter_server_distributed_amd.ops.embedding import FusedEmbedding
+
+    torch.manual_seed(2)
+    V, Hd, T = 30528, 768, 32768
+    e = FusedEmbedding(V, Hd).to(gpu, torch.bfloat16)
+    zipf = torch.distributions.Zipf if hasattr(torch.distributions, "Zipf") else None
+    ranks = (torch.rand(T, device=gpu) ** 4 * V).long().clamp_(0, V - 1)  # heavy head, long tail
+    skew = torch.where(torch.rand(T, device=gpu) < 0.5, torch.zeros_like(ranks), ranks).view(256, 128)
+    unif = torch.randint(0, V, (256, 128), device=gpu)
+    g = (torch.randint(-4, 5, (256, 128, Hd), device=gpu).float() / 8).to(torch.bfloat16)  # exact in fp32
+    times = {}
+    for name, ids in (("uniform", unif), ("skewed", skew)):
+        e.weight.grad = None
+        e(ids).backward(g)
+        ref = torch.zeros(V, Hd, device=gpu).index_add_(0, ids.reshape(-1), g.reshape(-1, Hd).float())
+        # integer eighths summed in fp32 are exact; the bf16 row is the rounded exact sum
+        assert torch.equal(e.weight.grad, ref.to(torch.bfloat16)), name
+        s, t = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        y = e(ids)
+        torch.cuda.synchronize()
+        s.record()
+        for _ in range(5):
+            y.backward(g, retain_graph=True)
+        t.record()
+        t.synchronize()
+        times[name] = s.elapsed_time(t) / 5
+    del zipf
+    assert times["skewed"] < 3 * times["uniform"] + 0.2, times
