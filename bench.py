@@ -251,7 +251,7 @@ def main():
             bucket_transport = "async engine peer DMA (hipMemcpyAsync into the owners' IPC inboxes)"
             a.bucket_mb = bucketing.choose_bucket_mb(bucket_probe, model_mb)
             ps.rebucket(a.bucket_mb)
-        except Exception as e:  # noqa: BLE001 -- a diagnostic must not cost the run
+        except Exception as e:  # noqa: BLE001 -- collective (every rank raises together): keep 16 MB
             bucket_probe = {"error": str(e)[:200]}
     if mode == "collective" and auto_bucket and world > 1 and a.backend == "nccl":
         from parameter_server_distributed_amd.parallel import bucketing

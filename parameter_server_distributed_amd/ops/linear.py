@@ -95,7 +95,9 @@ def _gelu_dgrad(ctx, dy2, w, pre, M: int, K: int, N: int) -> bool:
         fn()
     except _at.Declined:
         return False
-    src._psd_gelu_hand = (ctx.gelu_tok, g, db if src.bias is not None else None)
+    # keyed by the producer's forward token: its backward must find exactly this hand-over (a
+    # fused gradient consumed as an ordinary one would apply GELU' twice)
+    src._psd_gelu_hands[ctx.gelu_tok] = (g, db if src.bias is not None else None)
     return True
 
 
@@ -164,12 +166,18 @@ class _LinearFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, w.shape[0]).contiguous()
         sink = getattr(ctx.mod, "_psd_grad_sink", None)
         db = None
-        hand = getattr(ctx.mod, "_psd_gelu_hand", None)
-        ctx.mod._psd_gelu_hand = None
-        if ctx.act == 2 and hand is not None and hand[0] == ctx.tok and hand[1].data_ptr() == dy2.data_ptr():
+        hands = ctx.mod._psd_gelu_hands
+        hand = hands.pop(ctx.tok, None)
+        for t in [t for t in hands if t < ctx.tok]:  # left by an aborted backward
+            del hands[t]
+        if hand is not None:
+            if ctx.act != 2 or hand[0].data_ptr() != dy2.data_ptr():
+                raise RuntimeError(
+                    "psd MfmaLinear: the consumer fused this GELU's backward (psd_gelu_input_from) but the "
+                    "gradient reaching it is not the handed-over one -- the GELU output has another consumer")
             # the consumer's bwd-data GEMM already applied this GELU's backward and summed the bias
             # gradient (gemm_gelu_bwd_): dy IS the pre-activation gradient
-            db = hand[2]
+            db = hand[1]
         elif ctx.act == 1:
             dy2 = dy2 * (keep > 0)
         elif ctx.act == 2 and ctx.has_bias and ctx.needs_input_grad[2] and dy2.shape[1] % 8 == 0:
@@ -198,11 +206,13 @@ class _LinearFn(torch.autograd.Function):
             dx.addmm_(dy2, w)
             dx = dx.view(ctx.in_shape)
         elif ctx.needs_input_grad[0] and ctx.gelu_src is not None and _gelu_dgrad(ctx, dy2, w, pre_src, M, K, N):
-            dx = ctx.gelu_src._psd_gelu_hand[1].view(ctx.in_shape)
+            dx = ctx.gelu_src._psd_gelu_hands[ctx.gelu_tok][0].view(ctx.in_shape)
         elif ctx.needs_input_grad[0]:
             dx = torch.empty(x2.shape, dtype=dy2.dtype, device=dy2.device)
             _dgrad_route(("dgrad", M, K, N), dy2, w, dx)()
             dx = dx.view(ctx.in_shape)
+        if ctx.gelu_src is not None and ctx.gelu_src._psd_gelu_pre is pre_src:
+            ctx.gelu_src._psd_gelu_pre = None  # not kept alive between steps
         dw = None
         if ctx.needs_input_grad[1]:
             dw = sink(ctx.mod.weight) if sink is not None else None
@@ -231,7 +241,7 @@ class MfmaLinear(nn.Linear):
         self.fp8 = fp8
         self._psd_pending_dx: list = []  # gradients of the input handed over by a residual LayerNorm
         self._psd_gelu_from = None  # psd_gelu_input_from: the GELU Linear whose output is this one's input
-        self._psd_gelu_hand = None  # (forward token, pre-activation gradient, bias gradient) from the consumer
+        self._psd_gelu_hands: dict = {}  # forward token -> (pre-activation gradient, bias gradient) from the consumer
         self._psd_gelu_pre = None
         self._psd_bias_hand = None  # (forward token, dy data pointer, bias gradient) from a consumer LayerNorm
 

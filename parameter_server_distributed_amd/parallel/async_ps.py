@@ -558,7 +558,7 @@ class AsyncPS:
         elem = g.element_size()
         for mb in sizes_mb:
             n = max(ALIGN, int(mb * (1 << 20)) // elem)
-            el = 0.0
+            el, err = 0.0, None
             if self.is_worker:
                 def run():
                     for i, lo in enumerate(range(0, self.total, n)):
@@ -569,17 +569,22 @@ class AsyncPS:
                         for cs in self.comm_streams:
                             cs.synchronize()
 
-                run()
-                t0 = time.perf_counter()
-                for _ in range(reps):
+                try:  # a failure here must reach every rank (below), not strand them in the all_reduce
                     run()
-                el = (time.perf_counter() - t0) / reps
-            t = torch.tensor([el], dtype=torch.float64)
+                    t0 = time.perf_counter()
+                    for _ in range(reps):
+                        run()
+                    el = (time.perf_counter() - t0) / reps
+                except Exception as e:  # noqa: BLE001
+                    err = e
+            t = torch.tensor([el, 1.0 if err is not None else 0.0], dtype=torch.float64)
             if self.world > 1 and dist.is_initialized():
                 if dist.get_backend() == "nccl":
                     t = t.to(self.device)
                 dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el = float(t.item())
+            if float(t[1]) > 0:
+                raise RuntimeError(f"push-size probe failed on a rank{f': {err}' if err is not None else ''}")
+            el = float(t[0])
             out[mb] = round(self.total * elem * self.P / max(el, 1e-9) / 1e9, 1) if el > 0 else None
         return out
 
@@ -594,7 +599,9 @@ class AsyncPS:
         st = torch.cuda.current_stream(self.device)
         out = {}
         for name, fn in (("push", lambda: self.engine.push(self.step_idx, g, 0, self.total, st.cuda_stream)),
-                         ("pull", lambda: self.engine.pull(0, tmp, st.cuda_stream))):
+                         # step_idx: the latest admissible snapshot under both schedules (a fixed
+                         # schedule keeps only the last S + 1 versions; step 0's is long gone)
+                         ("pull", lambda: self.engine.pull(self.step_idx, tmp, st.cuda_stream))):
             fn()
             torch.cuda.synchronize(self.device)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
