@@ -248,7 +248,7 @@ def main():
 
         try:
             bucket_probe = ps.probe_push_sizes()
-            bucket_transport = "async engine peer DMA (hipMemcpyAsync into the owners' IPC inboxes)"
+            bucket_transport = f"async engine push into the owners' IPC inboxes ({ps.xfer_mode})"
             a.bucket_mb = bucketing.choose_bucket_mb(bucket_probe, model_mb)
             ps.rebucket(a.bucket_mb)
         except Exception as e:  # noqa: BLE001 -- collective (every rank raises together): keep 16 MB
@@ -386,6 +386,8 @@ def main():
                                        f"ps{shards}-{'delayed' if a.staleness else 'sync'}-s{a.staleness}-dp{n_workers}")
                                       + ("-disjoint" if kw else ""),
                        "ps_mode": mode, "async_fallback": fallback,
+                       "async_xfer": getattr(ps, "xfer_mode", None),
+                       "async_xfer_fallback": getattr(ps, "xfer_fallback", None),
                        "ps_shards": shards, "ps_owner_ranks": ps.owners, "worker_ranks": ps.worker_ranks,
                        "staleness_bound": a.staleness, "optimizer": f"{opt_kind} fused gfx950", "bucket_mb": a.bucket_mb,
                        "pull_dtype": pull_dtype, "fp8_compute": fp8_compute, "tunableop": tunable_mode,

@@ -15,6 +15,7 @@
 #include <sstream>
 
 #include "kernels/launchers.h"
+#include "kernels/launchers_xfer.h"
 #include "ops.h"
 
 namespace psd {
@@ -198,6 +199,7 @@ AsyncEngine::AsyncEngine(int rank, int world, std::vector<int> owners, std::vect
   }
   if (device_ >= 0) {
     ps_stream_ = c10::hip::getStreamFromPool(/*isHighPriority=*/true, (c10::DeviceIndex)device_).stream();
+    xfer_kernel_ = true;
   }
 }
 
@@ -675,19 +677,35 @@ void AsyncEngine::fail(const std::string& msg) {
 
 std::vector<int64_t> AsyncEngine::pull(int64_t step, at::Tensor params_flat, int64_t stream) {
   TORCH_CHECK(params_flat.is_contiguous() && params_flat.element_size() == esz_, "psd async: working buffer dtype");
-  return pull_impl(step, static_cast<char*>(params_flat.data_ptr()), nullptr, stream);
+  return pull_impl(step, static_cast<char*>(params_flat.data_ptr()), nullptr, nullptr, stream);
 }
 
-// the MX e4m3 snapshot (1 byte / parameter + 1 / 32) instead of the bf16 one (kernels/fp8.hip scales)
-std::vector<int64_t> AsyncEngine::pull_mx(int64_t step, at::Tensor q_flat, at::Tensor sc_flat, int64_t stream) {
+// the MX e4m3 snapshot (1 byte / parameter + 1 / 32) instead of the bf16 one (kernels/fp8.hip scales),
+// dequantised into the bf16 working weights `out` on the same stream
+std::vector<int64_t> AsyncEngine::pull_mx(int64_t step, at::Tensor q_flat, at::Tensor sc_flat, at::Tensor out,
+                                          int64_t stream) {
   TORCH_CHECK(mx_, "psd async: pull_mx on an engine without the MX publish");
   TORCH_CHECK(q_flat.is_contiguous() && q_flat.element_size() == 1 && sc_flat.is_contiguous() &&
                   sc_flat.element_size() == 1 && sc_flat.numel() * 32 == q_flat.numel(),
               "psd async: pull_mx buffers (1-byte q [n], 1-byte scales [n / 32])");
-  return pull_impl(step, static_cast<char*>(q_flat.data_ptr()), static_cast<char*>(sc_flat.data_ptr()), stream);
+  TORCH_CHECK(out.is_contiguous() && out.scalar_type() == at::kBFloat16 && out.numel() == q_flat.numel(),
+              "psd async: pull_mx output (bf16 [n])");
+  return pull_impl(step, static_cast<char*>(q_flat.data_ptr()), static_cast<char*>(sc_flat.data_ptr()),
+                   static_cast<uint16_t*>(out.data_ptr()), stream);
 }
 
-std::vector<int64_t> AsyncEngine::pull_impl(int64_t step, char* dst, char* dst_sc, int64_t stream) {
+void AsyncEngine::set_xfer(bool kernel) {
+  TORCH_CHECK(!kernel || device_ >= 0, "psd async: the scatter / gather kernels need a GPU engine");
+  xfer_kernel_ = kernel;
+}
+
+std::string AsyncEngine::xfer_mode() const {
+  if (device_ < 0) return "host-memcpy";
+  return xfer_kernel_ ? "kernel" : "hipMemcpyAsync";
+}
+
+std::vector<int64_t> AsyncEngine::pull_impl(int64_t step, char* dst, char* dst_sc, uint16_t* dst_bf16,
+                                            int64_t stream) {
   TORCH_CHECK(my_wi_ >= 0, "psd async: rank ", rank_, " is not a worker");
   const double t0 = now_s();
   const int64_t need = step - S_;
@@ -713,6 +731,7 @@ std::vector<int64_t> AsyncEngine::pull_impl(int64_t step, char* dst, char* dst_s
   }
   wait_us_.fetch_add((int64_t)((now_s() - t0) * 1e6));
   std::vector<int64_t> pulled(P);
+  std::vector<int> bufs(P, -1);
   for (int k = 0; k < P; ++k) {
     ShardCtl& s = ctl_->shard[k];
     int b = -1;
@@ -727,6 +746,7 @@ std::vector<int64_t> AsyncEngine::pull_impl(int64_t step, char* dst, char* dst_s
         else s.readers[bb].fetch_sub(1);
       }
       if (b < 0) {
+        for (int kk = 0; kk < k; ++kk) ctl_->shard[kk].readers[bufs[kk]].fetch_sub(1);
         const std::string m = "fixed-schedule pull of step " + std::to_string(step) + " on rank " +
                               std::to_string(rank_) + ": version " + std::to_string(want) + " of shard " +
                               std::to_string(k) + " is no longer published (latest " +
@@ -743,14 +763,56 @@ std::vector<int64_t> AsyncEngine::pull_impl(int64_t step, char* dst, char* dst_s
       }
     }
     pulled[k] = s.buf_version[b].load();
+    bufs[k] = b;
+  }
+  void* sp = reinterpret_cast<void*>(stream);
+  if (device_ >= 0 && xfer_kernel_) {
+    // every shard's snapshot in one gather launch: all owners' links at once (kernels/xfer.hip)
+    const c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device_));
     if (dst_sc) {
-      copy(dst + shard_off_[k], publish_q_ptr(k, b), shard_len_[k], reinterpret_cast<void*>(stream));
-      copy(dst_sc + shard_off_[k] / 32, publish_sc_ptr(k, b), shard_len_[k] / 32, reinterpret_cast<void*>(stream));
+      for (int k0 = 0; k0 < P; k0 += kMaxXferMxSeg) {
+        XferMxList L{};
+        int64_t mx = 0;
+        for (int k = k0; k < std::min(P, k0 + kMaxXferMxSeg); ++k) {
+          L.seg[L.count++] = XferMxSeg{reinterpret_cast<const uint8_t*>(publish_q_ptr(k, bufs[k])),
+                                       reinterpret_cast<const uint8_t*>(publish_sc_ptr(k, bufs[k])),
+                                       reinterpret_cast<uint8_t*>(dst + shard_off_[k]),
+                                       reinterpret_cast<uint8_t*>(dst_sc + shard_off_[k] / 32),
+                                       dst_bf16 + shard_off_[k], shard_len_[k]};
+          mx = std::max(mx, shard_len_[k]);
+        }
+        L.blocks_per_seg = xfer_blocks(mx, P == 1 ? 256 : 48);
+        hip_ok(launch_xfer_mx(L, static_cast<hipStream_t>(sp)), "launch_xfer_mx(pull)");
+      }
     } else {
-      copy(dst + shard_off_[k] * esz_, publish_ptr(k, b), shard_len_[k] * esz_, reinterpret_cast<void*>(stream));
+      XferList L{};
+      int64_t mx = 0;
+      for (int k = 0; k < P; ++k) {
+        L.seg[L.count++] = XferSeg{publish_ptr(k, bufs[k]), dst + shard_off_[k] * esz_, shard_len_[k] * esz_};
+        mx = std::max(mx, shard_len_[k] * esz_);
+      }
+      L.blocks_per_seg = xfer_blocks(mx, P == 1 ? 256 : 48);
+      L.nt_load = 1;
+      hip_ok(launch_xfer(L, static_cast<hipStream_t>(sp)), "launch_xfer(pull)");
     }
-    std::atomic<int32_t>* rd = &s.readers[b];
-    defer(reinterpret_cast<void*>(stream), [rd] { rd->fetch_sub(1); });
+  } else {
+    for (int k = 0; k < P; ++k) {
+      const int b = bufs[k];
+      if (dst_sc) {
+        copy(dst + shard_off_[k], publish_q_ptr(k, b), shard_len_[k], sp);
+        copy(dst_sc + shard_off_[k] / 32, publish_sc_ptr(k, b), shard_len_[k] / 32, sp);
+      } else {
+        copy(dst + shard_off_[k] * esz_, publish_ptr(k, b), shard_len_[k] * esz_, sp);
+      }
+    }
+    if (dst_sc && dst_bf16)
+      hip_ok(launch_dequant_mx(reinterpret_cast<const uint8_t*>(dst), reinterpret_cast<const uint8_t*>(dst_sc),
+                               shard_off_[P - 1] + shard_len_[P - 1], dst_bf16, DT_BF16, static_cast<hipStream_t>(sp)),
+             "launch_dequant_mx(pull)");
+  }
+  for (int k = 0; k < P; ++k) {
+    std::atomic<int32_t>* rd = &ctl_->shard[k].readers[bufs[k]];
+    defer(sp, [rd] { rd->fetch_sub(1); });
   }
   n_pulls_.fetch_add(1);
   return pulled;
@@ -762,6 +824,25 @@ void AsyncEngine::push(int64_t step, const at::Tensor& grads_flat, int64_t lo, i
   check_error();
   const char* src = static_cast<const char*>(grads_flat.data_ptr());
   const int slot = (int)(step % (S_ + 1));
+  if (device_ >= 0 && xfer_kernel_) {
+    // the bucket's slice for every owner it overlaps in one scatter launch (kernels/xfer.hip)
+    XferList L{};
+    int64_t mx = 0;
+    bool local_only = true;
+    for (size_t k = 0; k < owners_.size(); ++k) {
+      const int64_t a = std::max(lo, shard_off_[k]), b = std::min(hi, shard_off_[k] + shard_len_[k]);
+      if (a >= b) continue;
+      L.seg[L.count++] = XferSeg{src + a * esz_, inbox_ptr((int)k, my_wi_, slot) + (a - shard_off_[k]) * esz_,
+                                 (b - a) * esz_};
+      mx = std::max(mx, (b - a) * esz_);
+      local_only = local_only && owners_[k] == rank_;
+    }
+    L.blocks_per_seg = xfer_blocks(mx, local_only ? 256 : 48);
+    L.nt_store = 1;
+    const c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device_));
+    hip_ok(launch_xfer(L, reinterpret_cast<hipStream_t>(stream)), "launch_xfer(push)");
+    return;
+  }
   for (size_t k = 0; k < owners_.size(); ++k) {
     const int64_t a = std::max(lo, shard_off_[k]), b = std::min(hi, shard_off_[k] + shard_len_[k]);
     if (a >= b) continue;

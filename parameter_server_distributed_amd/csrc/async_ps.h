@@ -84,8 +84,13 @@ class AsyncEngine {
 
   // -- worker side --
   std::vector<int64_t> pull(int64_t step, at::Tensor params_flat, int64_t stream);
-  // MX engines: the e4m3 snapshot + E8M0 scales into (q_flat, sc_flat) instead of the bf16 one
-  std::vector<int64_t> pull_mx(int64_t step, at::Tensor q_flat, at::Tensor sc_flat, int64_t stream);
+  // MX engines: the e4m3 snapshot + E8M0 scales into (q_flat, sc_flat) instead of the bf16 one, and
+  // dequantised into the bf16 working weights `out`
+  std::vector<int64_t> pull_mx(int64_t step, at::Tensor q_flat, at::Tensor sc_flat, at::Tensor out, int64_t stream);
+  // push / pull transport: true (GPU default) = one scatter / gather kernel per push / pull over
+  // every owner's peer memory at once (kernels/xfer.hip); false = one hipMemcpyAsync per shard
+  void set_xfer(bool kernel);
+  std::string xfer_mode() const;
   void push(int64_t step, const at::Tensor& grads_flat, int64_t lo, int64_t hi, int64_t stream);
   void commit(int64_t step, std::vector<int64_t> pulled, int64_t stream);
   void wait_applied(int64_t nsteps);  // this worker's pushes 0..nsteps-1 applied at every shard
@@ -141,7 +146,7 @@ class AsyncEngine {
   int64_t shard_region_bytes(int shard) const;
   char* publish_q_ptr(int shard, int buf) const;
   char* publish_sc_ptr(int shard, int buf) const;
-  std::vector<int64_t> pull_impl(int64_t step, char* dst, char* dst_sc, int64_t stream);
+  std::vector<int64_t> pull_impl(int64_t step, char* dst, char* dst_sc, uint16_t* dst_bf16, int64_t stream);
   int64_t shard_base(int rank, int shard) const;  // byte offset of shard's region in rank's allocation
   char* inbox_ptr(int shard, int wi, int slot) const;
   char* publish_ptr(int shard, int buf) const;
@@ -162,6 +167,7 @@ class AsyncEngine {
   int rank_, world_, S_, nbuf_, device_;
   int round_ = 1;
   bool fixed_ = false;
+  bool xfer_kernel_ = false;  // set in the constructor: true on a GPU engine
   double timeout_s_;
   double dead_after_s_ = 10.0;  // a peer's engine silent this long is presumed dead (PSD_ASYNC_DEAD_S)
   int esz_;

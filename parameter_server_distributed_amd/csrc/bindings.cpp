@@ -308,6 +308,8 @@ PYBIND11_MODULE(_C, m) {
       .def("clocks", &AsyncEngine::clocks)
       .def("my_shards", &AsyncEngine::my_shards)
       .def("memory_kind", &AsyncEngine::memory_kind)
+      .def("set_xfer", &AsyncEngine::set_xfer)
+      .def("xfer_mode", &AsyncEngine::xfer_mode)
       .def("error", &AsyncEngine::error)
       .def("inject_error", &AsyncEngine::inject_error)
       .def("counters", &AsyncEngine::counters)

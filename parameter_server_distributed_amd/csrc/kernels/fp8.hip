@@ -8,15 +8,6 @@
 
 namespace psd {
 
-__device__ __forceinline__ float e4m3_to_f32(uint8_t b) {
-  const uint32_t s = b >> 7, e = (b >> 3) & 0xF, m = b & 7;
-  float v;
-  if (e == 0xF && m == 7) return __uint_as_float(0x7fc00000u);  // NaN (e4m3fn has no inf)
-  if (e == 0) v = (float)m * 0.001953125f;                      // m/8 * 2^-6
-  else v = __uint_as_float(((e + 120u) << 23) | (m << 20));     // (1+m/8) * 2^(e-7)
-  return s ? -v : v;
-}
-
 template <int DT>
 __global__ __launch_bounds__(256) void amax_kernel(const void* __restrict__ x, int64_t n, float* amax) {
   float m = 0.f;

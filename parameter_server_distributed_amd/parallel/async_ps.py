@@ -47,7 +47,6 @@ version, so none of this has a counterpart beyond the push/pull/apply roles.
 """
 from __future__ import annotations
 
-import contextlib
 import os
 import time
 import uuid
@@ -98,7 +97,7 @@ class AsyncPS:
                  bucket_mb: float = 16.0, device: torch.device | None = None, ps_ranks: list[int] | None = None,
                  worker_ranks: list[int] | None = None, param_dtype: torch.dtype = torch.bfloat16, nbuf: int = 4,
                  timeout_s: float | None = None, overlap: bool = True, store=None, log: bool = False,
-                 semantics: str = "round", pull_dtype: str = "bf16", schedule: str = "free"):
+                 semantics: str = "round", pull_dtype: str = "bf16", schedule: str = "free", xfer: str = "auto"):
         """``semantics``: "round" (K-batch async, default) or "push" (apply-on-arrival with the
         per-push hyperparameters of csrc/async_hyper.h); see the module docstring.
         ``schedule`` "fixed" ("round" semantics only): round r holds exactly every worker's step-r
@@ -110,7 +109,15 @@ class AsyncPS:
         e4m3 copy of its snapshot (one E8M0 scale per 32 elements, quantised from the fp32 master
         right after the apply, csrc/async_ps.cpp quant_publish); workers pull 1.03 bytes/parameter
         instead of 2, dequantise the bf16 working copy locally and hand the e4m3 weights + scales to
-        the fp8 convolutions (no per-step weight quantisation on the worker)."""
+        the fp8 convolutions (no per-step weight quantisation on the worker).
+        ``xfer`` (GPU): how pushes and pulls cross to the owners' memory -- "kernel": one scatter /
+        gather kernel per bucket push / pull that reads or writes every owner's peer-mapped memory
+        at once, one xGMI link per owner (kernels/xfer.hip); "copy": one hipMemcpyAsync per shard
+        (one link at a time); "auto" (default): the kernel, falling back to the copies (on every
+        rank together, logged in ``xfer_mode``) if its start-up self-test fails."""
+        if xfer not in ("auto", "kernel", "copy"):
+            raise ValueError(f"xfer must be auto, kernel or copy, got {xfer!r}")
+        self.xfer = xfer
         self.model = model
         self.cfg = optim
         st, self.rank, self.world = _store_and_group()
@@ -293,7 +300,18 @@ class AsyncPS:
         if log:
             self.engine.enable_log(True)
         self._barrier("init")
-        self.selftest()
+        self.xfer_fallback = None
+        if self.is_cuda:
+            self.engine.set_xfer(self.xfer != "copy")
+        try:
+            self.selftest()
+        except RuntimeError as e:  # collective: every rank sees the same failure
+            if not (self.is_cuda and self.xfer == "auto"):
+                raise
+            self.xfer_fallback = str(e)[:300]
+            self.engine.set_xfer(False)
+            self.selftest()
+        self.xfer_mode = self.engine.xfer_mode()
         self.engine.start()
 
     def selftest(self):
@@ -423,15 +441,12 @@ class AsyncPS:
 
     def _pull_into(self, t: int, nb: int, stream) -> list:
         """Pull of step t into working buffer ``nb`` on ``stream`` (None: the current stream): the
-        bf16 snapshots, or with MX the e4m3 + scales, dequantised into the bf16 buffer on the same
-        stream."""
+        bf16 snapshots, or with MX the e4m3 + scales and their bf16 dequantisation."""
         sptr = stream.cuda_stream if stream is not None else self._stream_ptr()
         if not self.pull_mx:
             return list(self.engine.pull(t, self.pbufs[nb], sptr))
-        pulled = list(self.engine.pull_mx(t, self.q8s[nb], self.sc8s[nb], sptr))
-        with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
-            native().dequant_mx_(self.q8s[nb], self.sc8s[nb], self.pbufs[nb])
-        return pulled
+        # the engine dequantises into the bf16 buffer on the same stream (fused into the gather)
+        return list(self.engine.pull_mx(t, self.q8s[nb], self.sc8s[nb], self.pbufs[nb], sptr))
 
     def _prefetch_pull(self, t: int):
         """Issue the pull of step t (the next one) now: the SSP wait happens on the host here, the
@@ -919,4 +934,4 @@ class AsyncPS:
     def describe(self) -> str:
         return (f"AsyncPS(world={self.world}, shards={self.P} on ranks {self.owners}, workers={self.worker_ranks}, "
                 f"SSP bound={self.S}, buckets={len(self.buckets)}, params={self.num_params() / 1e6:.2f}M, "
-                f"memory={self.engine.memory_kind()})")
+                f"memory={self.engine.memory_kind()}, xfer={self.xfer_mode})")
