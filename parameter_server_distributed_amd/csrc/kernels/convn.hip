@@ -262,14 +262,19 @@ __device__ __forceinline__ void convn_epilogue(const ConvnArgs& a, f32x4 (&acc)[
     }
   }
   if constexpr (STATS) {
-    // the statistics of the bf16-rounded values (stored, or -- statistics-only pass -- the values the
-    // tail's apply pass rounds before normalising: fp32 accumulators here put the chained-block
-    // gradients past the library path's error level, tests/test_bnfold.py). Packed fp32 pairs
-    // (v_pk_add / v_pk_fma): at two waves per SIMD the statistics-only pass was instruction-issue
+    // the statistics of the tensor the BN normalises: with a stored output, its bf16-rounded values
+    // (what bn_apply reads; fp32 accumulators here put the chained-block gradients past the library
+    // path's error level, tests/test_bnfold.py); in the statistics-only pass (a.y null: the recomputing
+    // tail, ops/tail.py) the fp32 product, which the apply pass (mode 8) normalises before any
+    // rounding -- the same values the tail's Gram statistics (sum y = W s, sum y^2 = W^T G W) describe,
+    // so both statistics routes agree with the normalised tensor (tools/probes/tail_stats_probe.py:
+    // normalising bf16(y) with the Gram moments of y moved the b8 test loss by 0.55 %). Packed fp32
+    // pairs (v_pk_add / v_pk_fma): at two waves per SIMD the statistics-only pass was instruction-issue
     // bound (~460 VALU per wave-tile, profiles/convp_pmc_r4.md). A 16-row block whose last row is
     // valid is valid throughout (pix is monotone within a block): the wave-uniform test skips the
     // per-row masks there.
     typedef float f32x2 __attribute__((ext_vector_type(2)));
+    const bool rnd = a.y != nullptr;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const bool full = pix(wr * 64 + i * 16 + 15) >= 0;
@@ -279,8 +284,13 @@ __device__ __forceinline__ void convn_epilogue(const ConvnArgs& a, f32x4 (&acc)[
         f32x2 s1 = {0.f, 0.f}, s2 = {0.f, 0.f};
 #pragma unroll
         for (int r = 0; r < 4; r += 2) {
-          const uint32_t pk = pack_bf16x2_rne(acc[i][j][r], acc[i][j][r + 1]);
-          f32x2 d = f32x2{__uint_as_float(pk << 16), __uint_as_float(pk & 0xFFFF0000u)} - k2;
+          f32x2 d;
+          if (rnd) {
+            const uint32_t pk = pack_bf16x2_rne(acc[i][j][r], acc[i][j][r + 1]);
+            d = f32x2{__uint_as_float(pk << 16), __uint_as_float(pk & 0xFFFF0000u)} - k2;
+          } else {
+            d = f32x2{acc[i][j][r], acc[i][j][r + 1]} - k2;
+          }
           if (!full) {
             d[0] = pix(wr * 64 + i * 16 + rq + r) >= 0 ? d[0] : 0.f;
             d[1] = pix(wr * 64 + i * 16 + rq + r + 1) >= 0 ? d[1] : 0.f;
@@ -302,6 +312,19 @@ __device__ __forceinline__ void convn_epilogue(const ConvnArgs& a, f32x4 (&acc)[
       return;
     }
   }
+  if constexpr (APPLY) {
+    // mode 8: the BN affine on the fp32 product in the accumulator layout (column = this lane's
+    // cl of block j), before the bf16 staging; the residual add + ReLU follow after the transpose
+#pragma unroll
+    for (int j = 0; j < JN; ++j) {
+      const int col = n0 + wc * WNT + j * 16 + cl;
+      const float sc = a.bss[col], sh = a.bss[a.N + col];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = fmaf(acc[i][j][r], sc, sh);
+    }
+  }
   const int L = cl & 3;
   constexpr int RB = WNT * 2;       // staged row bytes (one 16-row block)
   constexpr int CPR = RB / 16;      // 16-byte chunks per staged row
@@ -319,7 +342,7 @@ __device__ __forceinline__ void convn_epilogue(const ConvnArgs& a, f32x4 (&acc)[
   }
   if constexpr (BWD == 3) load8_f32(a.bmean_d + my_col, bmd);
   if constexpr (BRED) load8_f32(a.bmean + my_col, bmu);
-  if constexpr (BWD == 1 || APPLY) {
+  if constexpr (BWD == 1) {
     load8_f32(a.bss + my_col, bsc);
     load8_f32(a.bss + a.N + my_col, bsh);
   }
@@ -392,15 +415,15 @@ __device__ __forceinline__ void convn_epilogue(const ConvnArgs& a, f32x4 (&acc)[
       if (m >= 0) {
         const int64_t go = (int64_t)m * a.ldc + n0 + wc * WNT + c16 * 8;
         if constexpr (APPLY) {
-          // y = relu(bf16(acc) * scale + shift + residual) and its ReLU bit-mask: bn_apply_kernel's
-          // arithmetic on the stored (bf16-rounded) convolution output, which is never written
+          // y = relu(bf16(acc * scale + shift) + residual) and its ReLU bit-mask: the convolution
+          // output (never written) normalised in fp32 before its one rounding
           float d[8], rv[8];
           load8_bf16(reinterpret_cast<const uint16_t*>(&v), d);
           load8_bf16(reinterpret_cast<const uint16_t*>(&rv4[i][ps]), rv);
           uint32_t bits = 0;
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            const float o = relu_nan(fmaf(d[e], bsc[e], bsh[e]) + rv[e]);
+            const float o = relu_nan(d[e] + rv[e]);
             d[e] = o;
             bits |= (o > 0.f ? 1u : 0u) << e;
           }

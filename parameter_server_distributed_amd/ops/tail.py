@@ -19,10 +19,13 @@ Here y3 is recomputed instead of stored (kernels/convn.hip):
   Without that fused consumer (e.g. the network's last block, whose output feeds the pooling), the
   backward recomputes y3 once and runs the ordinary BN backward + fold.
 
-Numerics match the unfused tail: the same kernel computes y3 in both passes (deterministic, so the
-statistics are those of the values normalised), rounded to bf16 before the statistics and the apply
-exactly as the stored y3 was; the backward's sum g y3 uses the fp32 product instead of the rounded
-y3 (a rounding-level difference in one BN-backward coefficient).
+Numerics: the statistics (Gram moments or the statistics-only pass) and the apply pass all use the
+fp32 product y3 -- the apply normalises it before its one rounding to bf16 -- so the moments are
+exactly those of the normalised tensor (within 1e-5 of fp64 per layer,
+tests/test_tail.py::test_tail_statistics_match_fp64). The unfused tail normalises the bf16-rounded
+stored y3 instead: a rounding-level difference (normalising bf16(y3) with the Gram moments of the
+fp32 y3 moved the b8 ResNet-50 test loss by 0.55 %, tools/probes/tail_stats_probe.py). The
+backward's sum g y3 also uses the fp32 product.
 
 Reference: the reference's worker has no model at all (its "gradient" is a constant,
 /root/reference/src/worker.cpp:316-329); this is the MI355X data-movement design of the

@@ -140,11 +140,16 @@ def test_bnfold_gram_stats_exact(gpu, Nb, H, cin, cout):
 
 
 def test_resnet_tail_matches_unfused(gpu, monkeypatch):
-    """ResNet-50 (64x64 images, non-zero bn3 scales) with the recomputing tail on vs off, each
-    against an fp32 run of the same weights (PyTorch composite ops): bf16 rounding differences grow
-    through 16 residual blocks, so every parameter gradient of the tail run must be as close to the
-    fp32 reference as the unfused run's is (within 1.5x + 2 %), and the loss and running
-    statistics match the unfused run."""
+    """ResNet-50 (64x64 images, batch 8, non-zero bn3 scales) with the recomputing tail on vs off,
+    each against an fp32 run of the same weights (PyTorch composite ops): every parameter gradient
+    and running statistic of the tail run must be as close to the fp32 reference as the unfused
+    run's is (within 1.5x + 2 %), and the loss within the unfused run's distance from fp32 + 0.5 %.
+
+    bn3 scales are drawn from [0.1, 0.3]: with [0.5, 1.5] this network is chaotic at batch 8 --
+    the fp32 model's own loss moves by 4 % under relative 2^-9 (one bf16 ulp) noise on its input
+    (tools/probes/tail_chaos_probe.py, profiles/r5/tail_chaos_probe.txt), so no bf16 path can be
+    compared to fp32 there; at [0.1, 0.3] that spread is 0.05 %, unfused 0.02 % and the tail 0.06 %
+    from fp32."""
     import copy
     import json
 
@@ -156,15 +161,16 @@ def test_resnet_tail_matches_unfused(gpu, monkeypatch):
     spec = models.build("resnet50", gpu, torch.bfloat16, image_size=64, num_classes=10)
     for mod in spec.model.modules():  # non-zero bn3 scales: the tail's gradients are then not trivially 0
         if isinstance(mod, Bottleneck):
-            nn.init.uniform_(mod.bn3.weight, 0.5, 1.5)
+            nn.init.uniform_(mod.bn3.weight, 0.1, 0.3)
     for p in spec.model.parameters():
         p.data = p.data.to(torch.bfloat16)
     init = copy.deepcopy(spec.model.state_dict())
     x, y = spec.make_batch(8, gpu, seed=3)
 
-    def run(tail_on: bool, fp32: bool = False):
+    def run(tail_on: bool, fp32: bool = False, keep=None):
         monkeypatch.setenv("PSD_TAIL_RECOMPUTE", "1" if tail_on else "0")
         autotune._DECISIONS.clear()
+        autotune._DECISIONS.update(keep or {})
         for k in tail.TAIL_CALLS:
             tail.TAIL_CALLS[k] = 0
         m = spec.model
@@ -178,17 +184,23 @@ def test_resnet_tail_matches_unfused(gpu, monkeypatch):
                 {n: b.float().clone() for n, b in m.named_buffers() if "running" in n}, dict(tail.TAIL_CALLS))
 
     ref32 = run(False, fp32=True)
-    on, off = run(True), run(False)
+    autotune._DECISIONS.clear()
+    off = run(False)
+    # the tail run keeps every decision the unfused run made (the shared convolutions run the same
+    # kernels; only the tail's own keys are timed): re-autotuned kernels alone moved the b8 loss by
+    # ~2 % between bf16 runs (tools/probes/tail_stats_probe.py)
+    keep = dict(autotune._DECISIONS)
+    on = run(True, keep=keep)
     autotune._DECISIONS.clear()
     calls = on[3]
     # ResNet-50's identity blocks whose conv3 shape the fold takes (layer1-3: 10 of 12); each
     # backward either fused (the next conv1's epilogue) or recomputed (no fused consumer)
     assert calls["fwd"] >= 10, calls
     assert calls["bwd_fused"] + calls["bwd_recompute"] == calls["fwd"] and calls["bwd_fused"] >= 9, calls
-    # the loss: as close to the fp32 run's as the unfused run's is (the same rule as the gradients
-    # below; the runs re-autotune, and tiny-batch BN at layer 4 amplifies bf16 rounding)
+    # the loss: within the unfused run's distance from the fp32 run + 0.5 % (the
+    # per-layer statistics themselves are pinned against fp64 by test_tail_statistics_match_fp64)
     print("loss fp32 %.4f tail %.4f unfused %.4f" % (ref32[0], on[0], off[0]))
-    assert abs(on[0] - ref32[0]) <= 1.5 * abs(off[0] - ref32[0]) + 0.02 * abs(ref32[0]), (on[0], off[0], ref32[0])
+    assert abs(on[0] - ref32[0]) <= abs(off[0] - ref32[0]) + 0.005 * abs(ref32[0]), (on[0], off[0], ref32[0])
 
     def rel(a, b):
         return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
@@ -227,6 +239,16 @@ def test_tail_recompute_fallback_matches_unfused(gpu, monkeypatch):
     idt = torch.randn(n, cout, h, h, device=gpu).bfloat16().contiguous(memory_format=torch.channels_last)
     r = torch.randn(n, cout, h, h, device=gpu).bfloat16()
     res = []
+    # fp32 composite reference of the same math (conv -> batch-norm (batch statistics) -> + idt -> relu)
+    x32 = a2.float().requires_grad_(True)
+    i32 = idt.float().requires_grad_(True)
+    w32 = conv.weight.detach().float().requires_grad_(True)
+    g32 = bn.weight.detach().float().requires_grad_(True)
+    b32 = bn.bias.detach().float().requires_grad_(True)
+    rm, rv = torch.zeros(cout, device=gpu), torch.ones(cout, device=gpu)
+    y32 = torch.relu(F.batch_norm(F.conv2d(x32, w32), rm, rv, g32, b32, True, bn.momentum, bn.eps) + i32)
+    (y32 * r.float()).sum().backward()
+    ref = [y32.detach(), x32.grad, i32.grad, w32.grad, g32.grad, b32.grad, rm, rv]
     for on in (True, False):
         monkeypatch.setenv("PSD_TAIL_RECOMPUTE", "1" if on else "0")
         autotune._DECISIONS.clear()
@@ -250,6 +272,72 @@ def test_tail_recompute_fallback_matches_unfused(gpu, monkeypatch):
             assert tail.TAIL_CALLS == {"fwd": 1, "bwd_fused": 0, "bwd_recompute": 1}, tail.TAIL_CALLS
     autotune._DECISIONS.clear()
     names = ("y", "da2", "didt", "dW3", "dgamma", "dbeta", "running_mean", "running_var")
-    for nm, a, b in zip(names, res[0], res[1]):
-        rel = ((a - b).norm() / b.norm().clamp_min(1e-6)).item()
-        assert rel < 2e-2, (nm, rel)
+    for nm, a, b, f in zip(names, res[0], res[1], ref):
+        e_on = ((a - f).norm() / f.norm().clamp_min(1e-6)).item()
+        e_off = ((b - f).norm() / f.norm().clamp_min(1e-6)).item()
+        # the tail normalises the fp32 product, the unfused path the bf16-rounded one: each within the
+        # other's error level of the fp32 reference (a random upstream gradient makes near-cancelling
+        # BN-backward sums, so single-block bf16 gradients sit a few % from fp32)
+        assert e_on <= 1.5 * e_off + 1e-2, (nm, e_on, e_off)
+
+
+def test_tail_statistics_match_fp64(gpu, monkeypatch):
+    """the recomputing tail's BN statistics per identity block of ResNet-50
+    (64x64, batch 8, the test above), both routes -- the Gram moments (sum y = W s, sum y^2 =
+    W^T G W: convw_gram_ + bnfold_gram_stats) and the narrow kernel's statistics-only pass -- against
+    the fp64 mean / biased variance of y = a2 W^T from the same bf16 operands. No cancellation: the
+    Gram variance is within 1e-5 of fp64 where the inputs are post-ReLU (mean / std ~ 0.5)."""
+    from parameter_server_distributed_amd import models, native
+    from parameter_server_distributed_amd.models import resnet as R
+    from parameter_server_distributed_amd.models.resnet import Bottleneck
+    from parameter_server_distributed_amd.ops import autotune, tail
+
+    C = native()
+    torch.manual_seed(0)
+    spec = models.build("resnet50", gpu, torch.bfloat16, image_size=64, num_classes=10)
+    for mod in spec.model.modules():
+        if isinstance(mod, Bottleneck):
+            nn.init.uniform_(mod.bn3.weight, 0.5, 1.5)
+    for p in spec.model.parameters():
+        p.data = p.data.to(torch.bfloat16)
+    x, y = spec.make_batch(8, gpu, seed=3)
+    caps = []
+    orig = R.conv_bn_tail
+
+    def cap(conv, bn, a2, idt, resid_to=None):
+        caps.append((a2.detach().clone(), conv.weight.detach().clone()))
+        return orig(conv, bn, a2, idt, resid_to)
+
+    monkeypatch.setenv("PSD_TAIL_RECOMPUTE", "1")
+    monkeypatch.setattr(R, "conv_bn_tail", cap)
+    autotune._DECISIONS.clear()
+    spec.loss(spec.model(x), y).backward()
+    autotune._DECISIONS.clear()
+    assert len(caps) >= 10
+    for li, (a2, w) in enumerate(caps):
+        n, cin, h, wd = a2.shape
+        cout = w.shape[0]
+        M = n * h * wd
+        w2 = w.reshape(cout, cin).contiguous()
+        y64 = a2.permute(0, 2, 3, 1).reshape(M, cin).double() @ w2.double().t()
+        mu, var = y64.mean(0), y64.var(0, unbiased=False)
+        shift = torch.zeros(cout, device=gpu)
+        got = {}
+        P = torch.empty(C.convw_gram_rows(cin), cin, device=gpu, dtype=torch.float32)
+        assert C.convw_gram_(a2, P)
+        row = torch.empty(2, cout, device=gpu, dtype=torch.float32)
+        C.bnfold_gram_stats(P, w2, shift, M, row)
+        got["gram"] = row.double()
+        for v in range(C.convn_variants(cout)):
+            if C.convn_variant_kind(cout, v) in (0, 3) and C.convn_variant_ok(cout, v, 1, 1, 1, 0, wd):
+                part = torch.empty(tail._part_rows(M, cout, v, h, wd, 1), 2, cout, device=gpu, dtype=torch.float32)
+                rows = C.convn_(a2, w2, part, 1, 1, 1, 0, part=part, shift=shift, variant=v, no_store=True)
+                assert rows > 0
+                got[f"pass{v}"] = part[:rows].double().sum(0)
+        assert len(got) >= 2
+        for k, (s1, s2) in got.items():
+            m_k = s1 / M
+            v_k = s2 / M - m_k * m_k
+            dm = float(((m_k - mu).abs() / var.sqrt()).max())
+            dv = float(((v_k - var).abs() / var).max())
+            assert dm < 1e-5 and dv < 1e-5, (li, k, dm, dv)

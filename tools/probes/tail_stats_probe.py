@@ -38,6 +38,7 @@ def main():
     for p in spec.model.parameters():
         p.data = p.data.to(torch.bfloat16)
     init = copy.deepcopy(spec.model.state_dict())
+    m32 = copy.deepcopy(spec.model).float()  # before any forward leaves non-leaf tensors on modules
     x, y = spec.make_batch(8, dev, seed=3)
 
     caps = []
@@ -107,22 +108,40 @@ def main():
                 del autotune._DECISIONS[key]
         if stats is not None:
             os.environ["PSD_AUTOTUNE_FORCE"] = stats
-        m = spec.model
+        m = m32 if fp32 else spec.model
         m.load_state_dict(init)
         m.zero_grad(set_to_none=True)
-        if fp32:
-            m = copy.deepcopy(m).float()
-        loss = float(spec.loss(m(x.float() if fp32 else x), y))
+        loss = spec.loss(m(x.float() if fp32 else x), y)
+        loss.backward()
+        loss = float(loss)
         os.environ.pop("PSD_AUTOTUNE_FORCE", None)
         return loss
 
     ref = run(False, fp32=True)
     out = {"fp32": [ref]}
-    for name, kw in (("unfused", dict(tail_on=False)), ("tail_gram", dict(tail_on=True, stats="gram")),
+    for name, kw in (("unfused", dict(tail_on=False)), ("tail_auto", dict(tail_on=True)),
+                     ("tail_gram", dict(tail_on=True, stats="gram")),
                      ("tail_pass", dict(tail_on=True, stats="pass")), ("unfused_again", dict(tail_on=False))):
         out[name] = [run(**kw) for _ in range(3)]
     for k, v in out.items():
         print(f"loss {k:14s} " + " ".join(f"{l:.5f}" for l in v) + f"   (vs fp32 {max(abs(l - ref) for l in v) / ref:.2%})")
+
+    # how chaotic is this setting? the fp32 model's loss under bf16-rounding-sized perturbations
+    # (relative noise 2^-9 on the input / on every weight)
+    def fp32_loss(xin, noise_w=0.0, seed=0):
+        m32.load_state_dict(init)
+        if noise_w:
+            g = torch.Generator(device=dev).manual_seed(seed)
+            with torch.no_grad():
+                for p_ in m32.parameters():
+                    p_.mul_(1 + noise_w * torch.randn(p_.shape, device=dev, generator=g))
+        with torch.no_grad():
+            return float(spec.loss(m32(xin), y))
+    g = torch.Generator(device=dev).manual_seed(7)
+    xs = [x.float() * (1 + 2 ** -9 * torch.randn(x.shape, device=dev, generator=g)) for _ in range(3)]
+    print("fp32 loss, input x (1 + 2^-9 noise):", " ".join(f"{fp32_loss(xi):.5f}" for xi in xs))
+    print("fp32 loss, weights x (1 + 2^-9 noise):", " ".join(f"{fp32_loss(x.float(), 2 ** -9, s):.5f}" for s in range(3)))
+    print("fp32 loss, x rounded to bf16 only:", f"{fp32_loss(x.float()):.5f}", "(x is bf16 already)")
 
 
 if __name__ == "__main__":
