@@ -44,6 +44,7 @@ from parameter_server_distributed_amd.ops.optim import OptimConfig  # noqa: E402
 from parameter_server_distributed_amd.parallel.collective_ps import CollectivePS  # noqa: E402
 from parameter_server_distributed_amd.parallel.transport import make_transport  # noqa: E402
 from parameter_server_distributed_amd.runtime.trainer import Trainer  # noqa: E402
+from parameter_server_distributed_amd.utils.config import FEATURES, feature, features  # noqa: E402
 
 METRICS = {
     "resnet50": ("samples/sec (whole node) ResNet-50 async-SGD", "samples/s"),
@@ -377,7 +378,7 @@ def main():
             "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": (round(value / (REF_BASELINE[a.model] * n_workers), 2)
                             if a.model in REF_BASELINE else None),
-            "dtype": (("fp8 convs (MX e4m3 fwd, MX e5m2-dY bwd-data), bf16 rest" if os.environ.get("PSD_FP8_MX", "1") != "0"
+            "dtype": (("fp8 convs (MX e4m3 fwd, MX e5m2-dY bwd-data), bf16 rest" if feature("fp8_mx")
                        else "fp8-e4m3 fwd convs / bf16") if fp8_compute else "bf16"), "data": data,
             "config": {"model": a.model, "global_batch": a.batch * n_workers, "per_gpu_batch": a.batch,
                        "seq_len": a.seq_len if a.model.startswith("bert") else None,
@@ -387,6 +388,7 @@ def main():
                                       + ("-disjoint" if kw else ""),
                        "ps_mode": mode, "async_fallback": fallback,
                        "async_xfer": getattr(ps, "xfer_mode", None),
+                       "features_changed": {k: v for k, v in features().items() if v != FEATURES[k][0]},
                        "async_xfer_fallback": getattr(ps, "xfer_fallback", None),
                        "ps_shards": shards, "ps_owner_ranks": ps.owners, "worker_ranks": ps.worker_ranks,
                        "staleness_bound": a.staleness, "optimizer": f"{opt_kind} fused gfx950", "bucket_mb": a.bucket_mb,

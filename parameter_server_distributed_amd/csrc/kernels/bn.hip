@@ -831,16 +831,6 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_pool_kernel(const uint16_t* 
 }
 
 // ------------------------------------------------------------------ host launchers
-// PSD_BN_REVERSE=1 walks the reduce passes back to front (A/B switch; measured neutral on a
-// b1024 ResNet-50 step, so off by default).
-static int bn_reverse() {
-  static const int v = [] {
-    const char* e = getenv("PSD_BN_REVERSE");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
 static int gcd_i(int a, int b) { return b == 0 ? a : gcd_i(b, a % b); }
 
 static void reduce_grid(int64_t M, int C, int& gx, int& gy) {
@@ -865,7 +855,7 @@ hipError_t launch_bn_reduce(const uint16_t* x, int64_t M, int C, const float* sh
   if (M <= 0 || C % 8 != 0) return hipErrorInvalidValue;
   int gx, gy;
   reduce_grid(M, C, gx, gy);
-  hipLaunchKernelGGL(bn_fwd_reduce_kernel, dim3(gx, gy), dim3(256), 0, st, x, M, C, shift, part, bn_reverse());
+  hipLaunchKernelGGL(bn_fwd_reduce_kernel, dim3(gx, gy), dim3(256), 0, st, x, M, C, shift, part, 0);
   return hipGetLastError();
 }
 
@@ -899,7 +889,7 @@ hipError_t launch_bn_fwd(const BnFwdArgs& a, hipStream_t st) {
         gx = a.part_ready;
       } else {
         hipLaunchKernelGGL(bn_fwd_reduce_kernel, dim3(gx, gy), dim3(256), 0, st, a.x, a.M, a.C, a.running_mean,
-                           a.part, bn_reverse());
+                           a.part, 0);
       }
       hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((a.C + kFinCh - 1) / kFinCh), dim3(256), 0, st, a.part, gx, ff);
     }
@@ -1086,7 +1076,7 @@ hipError_t launch_bn_bwd(const BnBwdArgs& a, hipStream_t st) {
     if (mask != kMaskBits || !a.dxd || !a.coef_d || !a.part_d || !a.mean_d || !a.invstd_d)
       return hipErrorInvalidValue;
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<kMaskBits, true, true>), dim3(gx, gy), dim3(256), 0, st, a.dy, a.dy2, a.y,
-                       a.mbits, a.ss, a.x, a.save_mean, a.dr, a.M, a.C, a.part, bn_reverse(), a.xd, a.mean_d, a.part_d);
+                       a.mbits, a.ss, a.x, a.save_mean, a.dr, a.M, a.C, a.part, 0, a.xd, a.mean_d, a.part_d);
     const dim3 fg((a.C + kFinCh - 1) / kFinCh);
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, fg, dim3(256), 0, st, a.part, gx,
                        FinBwd{a.M, a.C, a.gamma, a.save_mean, a.save_invstd, a.dgamma, a.dbeta, a.coef});
@@ -1104,7 +1094,7 @@ hipError_t launch_bn_bwd(const BnBwdArgs& a, hipStream_t st) {
 #define PSD_RED(K, O)                                                                                              \
   hipLaunchKernelGGL((bn_bwd_reduce_kernel<K, O>), dim3(gx, gy), dim3(256), 0, st, a.dy, a.dy2, a.y, a.mbits, a.ss, \
                      a.x, a.save_mean, a.dr, a.M, a.C, a.part, \
-                     bn_reverse())
+                     0)
   if (mask == kMaskBits) PSD_RED(kMaskBits, true);
   else if (mask == kMaskY && a.dr) PSD_RED(kMaskY, true);
   else if (mask == kMaskY) PSD_RED(kMaskY, false);

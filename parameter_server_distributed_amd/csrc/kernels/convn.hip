@@ -38,13 +38,9 @@
 // The same kernel runs a stride-1 bwd-data (conv of dY with the flipped, transposed weights) and
 // a 1x1 bwd-data (dY . W as a 1x1 conv of dY with W^T).
 //
-// HALO variants (stride-1 RxR convolutions, pad R/2, Wo + R - 1 <= 64): gathering every K-tile's
-// A rows re-reads each input pixel R*R times through L2 (layer1's 3x3: 9 x 0.41 GB per pass, the
-// L2 -> LDS stream was the limit: ~550 us for 0.82 GB of HBM traffic). A HALO tile is RPT = BM / SW
-// whole output rows of one image, each padded to SW slots (SW = 16 / 32 / 64 >= Wo + R - 1); per
-// 64-channel block the (RPT + R - 1) x SW input window -- zero-padded by the out-of-range DMA --
-// is staged once and all R*R taps read their A fragments from it at row offset (r * SW + s). Only
-// the weight tiles stream through the ring. Slots past Wo compute garbage that is never stored.
+// Gathering every K-tile's A rows re-reads each input pixel R*R times through L2 (layer1's 3x3:
+// 9 x 0.41 GB per pass); the persistent HALO kernel below (convh_kernel) stages each input window
+// once and reads the taps as shifted rows.
 #include "common.h"
 #include "launchers_convn.h"
 
@@ -159,8 +155,6 @@ struct Geo {
   static_assert(WNT == 32 || WNT == 64, "wave tile width");
 };
 
-// HALO window bytes: (rpt + R - 1) * sw rows + 2 overrun rows, bounded for R <= 3, sw <= 64
-constexpr int halo_win_bytes(int bm) { return (bm + 2 * 64 + 8) * 128; }
 
 }  // namespace
 
@@ -241,8 +235,8 @@ __device__ __forceinline__ void convn_flush(const ConvnArgs& a, EpiSums<WNT / 16
   }
 }
 
-// Epilogue of one wave's 64 x WNT accumulator block (shared by the gathered / HALO kernel and the
-// persistent HALO kernel): per-wave, no barrier (``stg`` is this wave's own 2 KiB of LDS). C layout
+// Epilogue of one wave's 64 x WNT accumulator block (shared by the gathered kernel, the persistent
+// HALO kernel and the persistent 1x1 kernel): per-wave, no barrier (``stg`` is this wave's own 2 KiB of LDS). C layout
 // of a 16x16 block: col = lane & 15, row = 4 * (lane >> 4) + r. ``pix(p)``: output pixel of tile row
 // p (-1: none). The reductions accumulate into ``es``; without DEFER they are flushed here to
 // partial row (tm * WM + wr).
@@ -483,29 +477,16 @@ __device__ __forceinline__ void convn_epilogue(const ConvnArgs& a, f32x4 (&acc)[
 // (h, w) only: the zero-filled full-size gradient is never written).
 // 3: as 2 for a bottleneck tail relu(bn3(x) + bnd(xd)) (the downsample block's dual BN, whose
 // upstream gradient g is shared): part_d also receives sum g and sum g (xd - mean_d) for bnd.
-template <int BM, int BN, int WNT, int NSLOT, bool STATS, int BWD = 0, bool HALO = false>
+template <int BM, int BN, int WNT, int NSLOT, bool STATS, int BWD = 0>
 __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
   using G = Geo<BM, BN, WNT, NSLOT>;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int tiles_m = gridDim.x;
   const int tm = xcd_remap(blockIdx.x, tiles_m);
   const int m0 = tm * BM, n0 = blockIdx.y * BN;
-  // HALO geometry: tile = RPT output rows (ho0 ..) of image hn, SW slots per row
-  constexpr int SLOTB = HALO ? BN * 128 : G::SLOT;  // ring slot bytes (HALO: weights only)
-  const int lsw = a.log_sw, sw = 1 << lsw;
-  const int rpt = BM >> lsw;
-  const int tpi = HALO ? (a.Ho + rpt - 1) / rpt : 1;
-  const int hn = HALO ? tm / tpi : 0, ho0 = HALO ? (tm - hn * tpi) * rpt : 0;
-  uint8_t* win = smem + a.nslot * SLOTB;
-  // output pixel of tile row p (-1: past M / a padding slot)
-  auto pix = [&](int p) -> int {
-    if constexpr (HALO) {
-      const int j = p >> lsw, wo = p & (sw - 1);
-      return ((wo < a.Wo) & (ho0 + j < a.Ho)) ? (hn * a.Ho + ho0 + j) * a.Wo + wo : -1;
-    } else {
-      return m0 + p < a.M ? m0 + p : -1;
-    }
-  };
+  constexpr int SLOTB = G::SLOT;  // ring slot bytes
+  // output pixel of tile row p (-1: past M)
+  auto pix = [&](int p) -> int { return m0 + p < a.M ? m0 + p : -1; };
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wid / G::NWC, wc = wid % G::NWC;
@@ -524,7 +505,7 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
   // this lane's A rows (one per DMA piece): window origin p0 = top-left input pixel index,
   // hw = (h0 << 16) | (w0 & 0xffff); rows past M get h0 = -32768 (never in the image)
   int p0[G::APW], hw[G::APW];
-  if constexpr (!HALO) {
+  {
     const int howo = a.Ho * a.Wo;
 #pragma unroll
     for (int i = 0; i < G::APW; ++i) {
@@ -543,13 +524,10 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
   const int cmask = (1 << a.logC) - 1;
   const int nslot = a.nslot;  // ring depth of this launch: min(NSLOT, K-tiles)
 
-  const int ntap = a.R * a.S;
   auto stage = [&](int t) {
     uint8_t* slot = smem + (t % nslot) * SLOTB;
-    // HALO: K-tile t = (channel block t / taps, tap t % taps); the weight row offset of that tap
-    const int k0 = HALO ? (t % ntap) * (1 << a.logC) + (t / ntap) * kBK : t * kBK;
-    if constexpr (HALO) {
-    } else if (k0 >= a.K1) {  // K-concatenated second operand (1x1: the row is the output pixel itself)
+    const int k0 = t * kBK;
+    if (k0 >= a.K1) {  // K-concatenated second operand (1x1: the row is the output pixel itself)
       const int c0 = k0 - a.K1;
 #pragma unroll
       for (int i = 0; i < G::APW; ++i) {
@@ -591,22 +569,6 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
     }
   };
 
-  // HALO: the (rpt + R - 1) x sw input window of channel block cb (zero outside the image)
-  auto stage_window = [&](int cb) {
-    const int pieces = ((rpt + a.R - 1) << lsw) >> 3;
-    for (int pc = wid; pc < pieces; pc += G::NW) {
-      const int row = pc * 8 + (lane >> 3);
-      const int jj = row >> lsw, ws = row & (sw - 1);
-      const int hi = ho0 - a.pad + jj, wi = ws - a.pad;
-      const int kc = (lane & 7) ^ ((row >> 1) & 7);
-      const bool ok = (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
-      const uint32_t off =
-          ok ? ((((uint32_t)((hn * a.H + hi) * a.W + wi)) << a.logC) + (uint32_t)(cb * kBK + kc * 8)) * 2u : kOOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(win + pc * 1024), 16, off,
-                                               0, 0, 0);
-    }
-  };
-
   f32x4 acc[4][G::JN];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -616,25 +578,15 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
   const int nt = a.K / kBK;
   const int D = nslot - 1 > 0 ? nslot - 1 : 1;  // K-tiles issued ahead
   for (int p = 0; p < D && p < nt; ++p) stage(p);
-  constexpr int DPSK = HALO ? G::BPW : G::DPS;  // this wave's DMA per K-tile
+  constexpr int DPSK = G::DPS;  // this wave's DMA per K-tile
   for (int t = 0; t < nt; ++t) {
-    if (HALO && t % ntap == 0) {
-      // a new channel block: every wave is done with the old window, then stage the new one and
-      // drain (the in-flight weight tiles land with it)
-      if (t > 0) __builtin_amdgcn_s_barrier();
-      stage_window(t / ntap);
-      wait_vm<0>();
-    } else {
-      // K-tile t landed (this wave's DMA): leave the (up to D-1) later K-tiles in flight
-      wait_ahead<DPSK, NSLOT - 2>(min(nt - 1 - t, D - 1));
-    }
+    // K-tile t landed (this wave's DMA): leave the (up to D-1) later K-tiles in flight
+    wait_ahead<DPSK, NSLOT - 2>(min(nt - 1 - t, D - 1));
     __builtin_amdgcn_s_barrier();  // every wave: tile t published, tile t-1 no longer read
     __builtin_amdgcn_sched_barrier(0);
     if (t + D < nt) stage(t + D);
     const uint8_t* As = smem + (t % nslot) * SLOTB;
     const uint8_t* Bs = As + (SLOTB - BN * 128);
-    const int tap = HALO ? t % ntap : 0;
-    const int tr = HALO ? tap / a.S : 0, ts = HALO ? tap - tr * a.S : 0;
     // both k-steps' fragments are read before the first MFMA (one LDS latency per K-tile, not two:
     // at 1-2 waves per SIMD nothing else hides it)
     bf16x8 af[2][4], bf[2][G::JN];
@@ -643,17 +595,7 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
 #pragma unroll
       for (int j = 0; j < G::JN; ++j) bf[ks][j] = frag(Bs, wc * G::JN + j, ks, lane);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if constexpr (HALO) {
-          // slot p of the tile reads window row (p / sw + r) * sw + p % sw + s
-          const int p = (wr * 4 + i) * 16 + (lane & 15);
-          const int row = (((p >> lsw) + tr) << lsw) + (p & (sw - 1)) + ts;
-          af[ks][i] = __builtin_bit_cast(bf16x8,
-                                         *reinterpret_cast<const u32x4*>(win + kmaj_off(row, ks * 4 + (lane >> 4))));
-        } else {
-          af[ks][i] = frag(As, wr * 4 + i, ks, lane);
-        }
-      }
+      for (int i = 0; i < 4; ++i) af[ks][i] = frag(As, wr * 4 + i, ks, lane);
     }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
@@ -668,7 +610,7 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
   EpiSums<G::JN> es;
   es.zero();
   convn_epilogue<BM, BN, WNT, STATS, BWD>(a, acc, kshift, tm, wr, wc, lane,
-                                          smem + a.nslot * SLOTB + (HALO ? halo_win_bytes(BM) : 0) + wid * G::STG, pix,
+                                          smem + a.nslot * SLOTB + wid * G::STG, pix,
                                           n0, es);
 }
 
@@ -1210,16 +1152,14 @@ static hipError_t convp_launch(const ConvnArgs& a, int bn, hipStream_t st) {
 }
 
 // ------------------------------------------------------------------ host side
-template <int BM, int BN, int WNT, int NSLOT, bool STATS, int BWD, bool HALO>
+template <int BM, int BN, int WNT, int NSLOT, bool STATS, int BWD>
 static hipError_t convn_launch_t(const ConvnArgs& a0, hipStream_t st) {
   using G = Geo<BM, BN, WNT, NSLOT>;
-  constexpr int SLOTB = HALO ? BN * 128 : G::SLOT;
-  constexpr int WINB = HALO ? halo_win_bytes(BM) : 0;
-  constexpr int LDS_MAX = NSLOT * SLOTB + WINB + G::NW * G::STG;
+  constexpr int LDS_MAX = NSLOT * G::SLOT + G::NW * G::STG;
   static_assert(LDS_MAX <= 160 * 1024, "LDS");
   static bool attr = false;
   if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)convn_kernel<BM, BN, WNT, NSLOT, STATS, BWD, HALO>,
+    const hipError_t e = hipFuncSetAttribute((const void*)convn_kernel<BM, BN, WNT, NSLOT, STATS, BWD>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     if (e != hipSuccess) return e;
     attr = true;
@@ -1227,29 +1167,21 @@ static hipError_t convn_launch_t(const ConvnArgs& a0, hipStream_t st) {
   ConvnArgs a = a0;
   const int nt = a.K / kBK;
   a.nslot = nt < NSLOT ? (nt < 2 ? 1 : nt) : NSLOT;
-  const int lds = a.nslot * SLOTB + WINB + G::NW * G::STG;
-  int tiles_m = (a.M + BM - 1) / BM;
-  if (HALO) {
-    const int rpt = BM >> a.log_sw;
-    tiles_m = (a.M / (a.Ho * a.Wo)) * ((a.Ho + rpt - 1) / rpt);
-  }
-  hipLaunchKernelGGL((convn_kernel<BM, BN, WNT, NSLOT, STATS, BWD, HALO>), dim3(tiles_m, a.N / BN), dim3(G::NT), lds,
-                     st, a);
+  const int lds = a.nslot * G::SLOT + G::NW * G::STG;
+  const int tiles_m = (a.M + BM - 1) / BM;
+  hipLaunchKernelGGL((convn_kernel<BM, BN, WNT, NSLOT, STATS, BWD>), dim3(tiles_m, a.N / BN), dim3(G::NT), lds, st, a);
   return hipGetLastError();
 }
 
-template <int BM, int BN, int WNT, int NSLOT, bool HALO = false>
+template <int BM, int BN, int WNT, int NSLOT>
 static hipError_t convn_launch_s(const ConvnArgs& a, hipStream_t st) {
-  if (a.bwd == 1) return convn_launch_t<BM, BN, WNT, NSLOT, false, 1, HALO>(a, st);
-  if (a.bwd == 2) return convn_launch_t<BM, BN, WNT, NSLOT, false, 2, HALO>(a, st);
-  if (a.bwd == 3) return convn_launch_t<BM, BN, WNT, NSLOT, false, 3, HALO>(a, st);
-  if (a.bwd == 5) return convn_launch_t<BM, BN, WNT, NSLOT, false, 5, HALO>(a, st);
-  if (a.bwd == 8) {  // (1x1 tails only: no HALO instantiation)
-    if constexpr (HALO) return hipErrorNotSupported;
-    else return convn_launch_t<BM, BN, WNT, NSLOT, false, 8, false>(a, st);
-  }
-  return a.part ? convn_launch_t<BM, BN, WNT, NSLOT, true, 0, HALO>(a, st)
-                : convn_launch_t<BM, BN, WNT, NSLOT, false, 0, HALO>(a, st);
+  if (a.bwd == 1) return convn_launch_t<BM, BN, WNT, NSLOT, false, 1>(a, st);
+  if (a.bwd == 2) return convn_launch_t<BM, BN, WNT, NSLOT, false, 2>(a, st);
+  if (a.bwd == 3) return convn_launch_t<BM, BN, WNT, NSLOT, false, 3>(a, st);
+  if (a.bwd == 5) return convn_launch_t<BM, BN, WNT, NSLOT, false, 5>(a, st);
+  if (a.bwd == 8) return convn_launch_t<BM, BN, WNT, NSLOT, false, 8>(a, st);
+  return a.part ? convn_launch_t<BM, BN, WNT, NSLOT, true, 0>(a, st)
+                : convn_launch_t<BM, BN, WNT, NSLOT, false, 0>(a, st);
 }
 
 int convn_tile_n(int N) {
@@ -1259,27 +1191,21 @@ int convn_tile_n(int N) {
   return 0;
 }
 
-// variants (tile geometry) per output width: the gathered ones, then the HALO ones
+// variants (tile geometry) per output width: the gathered ones (kind 0), then the persistent HALO
+// variant (convh_kernel, kind 2) for the 64-wide outputs, then the persistent 1x1 variant
+// (convp_kernel, kind 3). (The one-tile HALO variants -- kind 1 -- measured no faster than the
+// gathered ones on the ResNet-50 shapes, profiles/convn_halo_r3.md, and were removed in round 5.)
 static int plain_count(int bn) { return bn == 256 ? 2 : 4; }
-// HALO variants' BM per output width (must match the dispatch in launch_convn)
-static constexpr int kHaloBm64[] = {128, 256, 128};
-static constexpr int kHaloBm128[] = {128, 256};
-static int halo_count(int bn) { return bn == 256 ? 1 : bn == 128 ? 2 : 3; }
-// + the persistent HALO variant (convh_kernel) for the 64-wide outputs
 static int persist_count(int bn) { return bn == 64 ? 1 : 0; }
-// + the persistent 1x1 variant (convp_kernel), every width
 static int p1_count(int bn) { return bn ? 1 : 0; }
-static int convn_variant_count(int bn) { return plain_count(bn) + halo_count(bn) + persist_count(bn) + p1_count(bn); }
-static bool is_persist(int bn, int v) {
-  const int b = plain_count(bn) + halo_count(bn);
-  return v >= b && v < b + persist_count(bn);
-}
-static bool is_p1(int bn, int v) { return v == plain_count(bn) + halo_count(bn) + persist_count(bn); }
+static int convn_variant_count(int bn) { return plain_count(bn) + persist_count(bn) + p1_count(bn); }
+static bool is_persist(int bn, int v) { return v >= plain_count(bn) && v < plain_count(bn) + persist_count(bn); }
+static bool is_p1(int bn, int v) { return v == plain_count(bn) + persist_count(bn); }
 
 int convn_variant_kind(int N, int v) {
   const int bn = convn_tile_n(N);
   if (!bn || v < 0 || v >= convn_variant_count(bn)) return -1;
-  return v < plain_count(bn) ? 0 : is_persist(bn, v) ? 2 : is_p1(bn, v) ? 3 : 1;
+  return v < plain_count(bn) ? 0 : is_persist(bn, v) ? 2 : 3;
 }
 
 int convn_variants(int N) {
@@ -1296,17 +1222,9 @@ static int default_variant(const ConvnArgs& a, int bn) {
 // BM of each variant (must match the dispatch in launch_convn)
 static int variant_bm(int bn, int v) {
   if (is_persist(bn, v) || is_p1(bn, v)) return 128;
-  const int h = v - plain_count(bn);
-  if (h >= 0) return bn == 64 ? kHaloBm64[h] : bn == 128 ? kHaloBm128[h] : 128;
   if (bn == 64) return (v == 2 || v == 3) ? 256 : 128;
   if (bn == 128) return v == 2 ? 256 : 128;
   return 128;
-}
-
-// HALO slot width for an output row of Wo pixels and an R-wide kernel (0: no HALO tiling)
-static int halo_sw(int Wo, int R) {
-  const int need = Wo + R - 1;
-  return need <= 16 ? 16 : need <= 32 ? 32 : need <= 64 ? 64 : 0;
 }
 
 bool convn_variant_ok(int N, int v, int R, int S, int stride, int pad, int Wo, bool has_x2) {
@@ -1314,10 +1232,8 @@ bool convn_variant_ok(int N, int v, int R, int S, int stride, int pad, int Wo, b
   if (!bn || v < 0 || v >= convn_variant_count(bn)) return false;
   if (v < plain_count(bn)) return true;
   if (is_p1(bn, v)) return R == 1 && S == 1 && stride == 1 && pad == 0;
-  if (is_persist(bn, v))  // (C = 64 and H = Ho are checked at launch: the predicate has no C)
-    return !has_x2 && N == 64 && R == 3 && S == 3 && stride == 1 && pad == 1 && Wo + 2 <= 64;
-  const int sw = halo_sw(Wo, R);
-  return !has_x2 && R == S && R > 1 && R <= 3 && stride == 1 && 2 * pad == R - 1 && sw > 0 && variant_bm(bn, v) >= sw;
+  // persistent HALO (C = 64 and H = Ho are checked at launch: the predicate has no C)
+  return !has_x2 && N == 64 && R == 3 && S == 3 && stride == 1 && pad == 1 && Wo + 2 <= 64;
 }
 
 int convn_stats_rows(int M) { return 4 * ((M + 255) / 256) + 4; }  // >= (BM/64) * tiles for the gathered variants
@@ -1331,12 +1247,6 @@ int convn_part_rows_geo(int M, int N, int variant, int Ho, int Wo, int R) {
     return 2 * convh_grid((M / (Ho * Wo)) * ((Ho + 1) / 2));
   }
   if (is_p1(bn, variant)) return 2 * convp_grid_x((M + 127) / 128, N / bn);
-  if (variant >= plain_count(bn)) {
-    const int sw = halo_sw(Wo, R);
-    if (!sw || Ho <= 0 || Wo <= 0) return 0;
-    const int rpt = bm / sw;
-    return (bm / 64) * ((M / (Ho * Wo)) * ((Ho + rpt - 1) / rpt));
-  }
   return (bm / 64) * ((M + bm - 1) / bm);
 }
 
@@ -1369,26 +1279,6 @@ hipError_t launch_convn(const ConvnArgs& a_in, hipStream_t st) {
   if (is_persist(bn, v)) {
     if (!convh_ok(a) || a.bwd == 8 || !a.y) return hipErrorNotSupported;
     return convh_launch(a, st);
-  }
-  if (v >= plain_count(bn)) {  // HALO
-    if (!convn_variant_ok(a.N, v, a.R, a.S, a.stride, a.pad, a.Wo, two) || a.Ho != a.H || a.Wo != a.W)
-      return hipErrorNotSupported;
-    const int sw = halo_sw(a.Wo, a.R);
-    a.log_sw = sw == 16 ? 4 : sw == 32 ? 5 : 6;
-    const int h = v - plain_count(bn);
-    switch (bn) {
-      case 64:  // (deeper weight rings, 6-8 slots at one workgroup per CU, measured no faster: 141-247 us
-                // vs 138 us for the best gathered variant, layer1 3x3 at b256 -- the L2 latency of the
-                // weight tiles is not what bounds this shape)
-        if (h == 0) return convn_launch_s<128, 64, 32, 3, true>(a, st);
-        if (h == 1) return convn_launch_s<256, 64, 64, 3, true>(a, st);
-        return convn_launch_s<128, 64, 32, 4, true>(a, st);
-      case 128:
-        if (h == 0) return convn_launch_s<128, 128, 32, 3, true>(a, st);
-        return convn_launch_s<256, 128, 64, 2, true>(a, st);
-      default:
-        return convn_launch_s<128, 256, 64, 3, true>(a, st);
-    }
   }
   switch (bn) {
     case 64:  // 4 waves of 64x32 (3 / 2 slots) | 4 waves of 64x64 (BM 256) | 8 waves of 64x32 (BM 256)

@@ -282,289 +282,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// 256x256 tile, 8 waves (2 x 4), global_load_lds (LDS-DMA, 16 B/lane) staging, 2 LDS stages.
-// Requirements: K % 64 == 0 (no K tail inside a stage); M/N edges clamp the source row (the
-// garbage rows/cols are never stored). Per stage each lane issues 4 A + 4 B LDS-DMA loads; the
-// next stage is issued before the current one's MFMAs and retired with a counted vmcnt(8) + raw
-// s_barrier (a __syncthreads() would drain the in-flight DMA: cdna_hip_programming.md §5).
-// The LDS image is lane-linear per 1 KiB DMA piece; the bank swizzle is applied to the per-lane
-// SOURCE address and the same involution on the fragment read (rule 21).
 namespace {
-constexpr int kBig = 256;
-constexpr int kBigStage = 2 * kBig * BK * 2;  // A + B bytes per stage (64 KiB)
-constexpr int kBigLdc = kBig + 8;
-constexpr int kBigLds = (2 * kBigStage > kBig * kBigLdc * 2) ? 2 * kBigStage : kBig * kBigLdc * 2;
-
-template <bool KMAJ>
-__device__ __forceinline__ void glds_stage(const uint16_t* __restrict__ src, int ld, int nrows, int r0, int k0,
-                                           uint8_t* lds, int wid, int lane) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int piece = i * 8 + wid;  // 32 x 1 KiB pieces per 32 KiB operand tile
-    const uint16_t* gp;
-    if (KMAJ) {  // [256 rows][64 k], 128-B rows: a piece is 8 rows
-      const int row = piece * 8 + (lane >> 3);
-      const int kc = (lane & 7) ^ ((row >> 1) & 7);
-      const int gr = min(r0 + row, nrows - 1);
-      gp = src + (int64_t)gr * ld + k0 + kc * 8;
-    } else {  // [64 k][256 cols], 512-B rows: a piece is 2 k-rows
-      const int k = piece * 2 + (lane >> 5);
-      const int col = ((lane & 31) * 8) ^ ((k & 3) << 5);
-      const int gc = min(r0 + col, nrows - 8);
-      gp = src + (int64_t)(k0 + k) * ld + gc;
-    }
-    __builtin_amdgcn_global_load_lds((const void*)gp, (__attribute__((address_space(3))) void*)(lds + piece * 1024), 16,
-                                     0, 0);
-  }
-}
+constexpr int kBig = 256;  // output tile width of the 8-phase kernel
 }  // namespace
-
-// Epilogue of the 256x256 kernels: fp32 slab / fp32 C direct stores, or bf16 C (+bias, +act)
-// staged through LDS and written as 16-byte row chunks.
-template <int MODE>
-__device__ __forceinline__ void big_epilogue(const GemmArgs& g, f32x16 (&acc)[4][2], int m0, int n0, int wm, int wn,
-                                             int lane, uint8_t* smem) {
-  const int hl = lane >> 5, cl = lane & 31;
-  if (MODE == 1 || g.c_f32) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = n0 + wn * 64 + j * 32 + cl;
-      if (n >= g.N) continue;
-      const float bias = (MODE == 0 && g.bias) ? bf16_to_f32(reinterpret_cast<const uint16_t*>(g.bias)[n]) : 0.f;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = m0 + wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-          if (m >= g.M) continue;
-          if (MODE == 1) {
-            reinterpret_cast<float*>(g.C)[(int64_t)blockIdx.z * g.M * g.N + (int64_t)m * g.N + n] = acc[i][j][r];
-          } else {
-            float v = acc[i][j][r] + bias;
-            if (g.act == 1) v = relu_nan(v);
-            else if (g.act == 2) v = gelu_tanh(v);
-            reinterpret_cast<float*>(g.C)[(int64_t)m * g.ldc + n] = v;
-          }
-        }
-    }
-    return;
-  }
-  uint16_t* cs = reinterpret_cast<uint16_t*>(smem);
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int nl = wn * 64 + j * 32 + cl;
-    const int n = n0 + nl;
-    const float bias = (g.bias && n < g.N) ? bf16_to_f32(reinterpret_cast<const uint16_t*>(g.bias)[n]) : 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int ml = wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-        float v = acc[i][j][r] + bias;
-        if (g.act == 2 && g.aux && n < g.N && m0 + ml < g.M)
-          reinterpret_cast<uint16_t*>(g.aux)[(int64_t)(m0 + ml) * g.ldc + n] = f32_to_bf16(v);
-        if (g.act == 1) v = relu_nan(v);
-        else if (g.act == 2) v = gelu_tanh(v);
-        cs[ml * kBigLdc + nl] = f32_to_bf16(v);
-      }
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < kBig * (kBig / 8); c += 512) {
-    const int ml = c >> 5, nl = (c & 31) * 8;
-    const int m = m0 + ml, n = n0 + nl;
-    if (m >= g.M || n >= g.N) continue;
-    uint16_t* o = reinterpret_cast<uint16_t*>(g.C) + (int64_t)m * g.ldc + n;
-    const uint16_t* src = cs + ml * kBigLdc + nl;
-    if (n + 8 <= g.N && ((reinterpret_cast<uintptr_t>(o) & 15) == 0))
-      *reinterpret_cast<u32x4*>(o) = *reinterpret_cast<const u32x4*>(src);
-    else
-      for (int e = 0; e < 8 && n + e < g.N; ++e) o[e] = src[e];
-  }
-}
-
-template <bool AK, bool BKM, int MODE>
-__global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int tiles_n = (g.N + kBig - 1) / kBig;
-  const int tiles_m = (g.M + kBig - 1) / kBig;
-  const int wg = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int m0 = (wg / tiles_n) * kBig, n0 = (wg % tiles_n) * kBig;
-  int kbeg = 0, kend = g.K;
-  if (MODE == 1) {
-    kbeg = blockIdx.z * g.k_per_split;
-    kend = min(g.K, kbeg + g.k_per_split);
-  }
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wid >> 2, wn = wid & 3;  // wave tile: rows wm*128.., cols wn*64..
-  const uint16_t* A = reinterpret_cast<const uint16_t*>(g.A);
-  const uint16_t* B = reinterpret_cast<const uint16_t*>(g.B);
-
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  const int nt = (kend - kbeg) / BK;
-  if (nt > 0) {
-    glds_stage<AK>(A, g.lda, g.M, m0, kbeg, smem, wid, lane);
-    glds_stage<BKM>(B, g.ldb, g.N, n0, kbeg, smem + kBig * BK * 2, wid, lane);
-  }
-  for (int t = 0; t < nt; ++t) {
-    uint8_t* cur = smem + (t & 1) * kBigStage;
-    if (t + 1 < nt) {
-      uint8_t* nxt = smem + ((t + 1) & 1) * kBigStage;
-      glds_stage<AK>(A, g.lda, g.M, m0, kbeg + (t + 1) * BK, nxt, wid, lane);
-      glds_stage<BKM>(B, g.ldb, g.N, n0, kbeg + (t + 1) * BK, nxt + kBig * BK * 2, wid, lane);
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // stage t landed, stage t+1 in flight
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    const uint8_t* As = cur;
-    const uint8_t* Bs = cur + kBig * BK * 2;
-#pragma unroll
-    for (int ks = 0; ks < BK / 16; ++ks) {
-      bf16x8 af[4], bfr[2];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = frag<kBig, AK>(As, wm * 128 + i * 32, ks);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) bfr[j] = frag<kBig, BKM>(Bs, wn * 64 + j * 32, ks);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();  // every wave done reading `cur` before it is re-filled
-  }
-
-  big_epilogue<MODE>(g, acc, m0, n0, wm, wn, lane, smem);
-}
-
-// ---------------------------------------------------------------------------------------------
-// 256x256 tile, ring-pipelined: the K loop runs over half-stages of 32 k (A 16 KiB + B 16 KiB),
-// kept in a 4-slot LDS ring (128 KiB). Three half-stages are in flight ahead of the one being
-// multiplied; one raw s_barrier per half-stage both publishes slot h (after this wave's counted
-// vmcnt) and releases slot h-1 for the DMA of half-stage h+3. Per half-stage each wave issues 12
-// (K-major) fragment reads and 16 v_mfma_f32_32x32x16_bf16, the MFMA cluster fenced with
-// s_setprio (cdna_hip_programming.md T5). K-major half-stage image: [256 rows][32 k] (64-B rows,
-// 16-B chunk XOR (row>>2)&3: conflict-free for the ds_read_b128 lane groups); M/N-major:
-// [32 k][256] read with ds_read_b64_tr_b16 (same image as the 2-stage kernel, 32 k-rows).
-namespace {
-constexpr int kHalfK = 32;
-constexpr int kHalfOp = kBig * kHalfK * 2;  // 16 KiB per operand per half-stage
-constexpr int kHalfSlot = 2 * kHalfOp;      // A + B
-
-__device__ __forceinline__ int kmaj32_off(int row, int c) { return row * 64 + ((c ^ ((row >> 2) & 3)) << 4); }
-
-template <bool KMAJ>
-__device__ __forceinline__ void glds_half(const uint16_t* __restrict__ src, int ld, int nrows, int r0, int k0,
-                                          uint8_t* lds, int wid, int lane) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int piece = i * 8 + wid;  // 16 x 1 KiB pieces per operand half-stage
-    const uint16_t* gp;
-    if (KMAJ) {  // a piece is 16 rows x 64 B
-      const int row = piece * 16 + (lane >> 2);
-      const int c = (lane & 3) ^ ((row >> 2) & 3);
-      const int gr = min(r0 + row, nrows - 1);
-      gp = src + (int64_t)gr * ld + k0 + c * 8;
-    } else {  // a piece is 2 k-rows x 512 B
-      const int k = piece * 2 + (lane >> 5);
-      const int col = ((lane & 31) * 8) ^ ((k & 3) << 5);
-      const int gc = min(r0 + col, nrows - 8);
-      gp = src + (int64_t)(k0 + k) * ld + gc;
-    }
-    __builtin_amdgcn_global_load_lds((const void*)gp, (__attribute__((address_space(3))) void*)(lds + piece * 1024), 16,
-                                     0, 0);
-  }
-}
-
-template <bool KMAJ>
-__device__ __forceinline__ bf16x8 frag_half(const uint8_t* lds, int r0, int ks, int lane) {
-  if (KMAJ) {
-    const int row = r0 + (lane & 31);
-    const u32x4 w = *reinterpret_cast<const u32x4*>(lds + kmaj32_off(row, ks * 2 + (lane >> 5)));
-    return __builtin_bit_cast(bf16x8, w);
-  } else {
-    return frag<kBig, false>(lds, r0, ks);
-  }
-}
-}  // namespace
-
-template <bool AK, bool BKM, int MODE>
-__global__ __launch_bounds__(512) void gemm256r_kernel(GemmArgs g) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int tiles_n = (g.N + kBig - 1) / kBig;
-  const int tiles_m = (g.M + kBig - 1) / kBig;
-  const int wg = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int m0 = (wg / tiles_n) * kBig, n0 = (wg % tiles_n) * kBig;
-  int kbeg = 0, kend = g.K;
-  if (MODE == 1) {
-    kbeg = blockIdx.z * g.k_per_split;
-    kend = min(g.K, kbeg + g.k_per_split);
-  }
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wid >> 2, wn = wid & 3;
-  const uint16_t* A = reinterpret_cast<const uint16_t*>(g.A);
-  const uint16_t* B = reinterpret_cast<const uint16_t*>(g.B);
-
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  const int nh = (kend - kbeg) / kHalfK;
-  auto stage = [&](int h) {
-    uint8_t* slot = smem + (h & 3) * kHalfSlot;
-    glds_half<AK>(A, g.lda, g.M, m0, kbeg + h * kHalfK, slot, wid, lane);
-    glds_half<BKM>(B, g.ldb, g.N, n0, kbeg + h * kHalfK, slot + kHalfOp, wid, lane);
-  };
-#pragma unroll
-  for (int p = 0; p < 3; ++p)
-    if (p < nh) stage(p);
-  for (int h = 0; h < nh; ++h) {
-    // half-stage h landed (this wave's DMA): leave min(2, nh-1-h) half-stages (4 DMA each) in flight
-    const int ahead = nh - 1 - h;
-    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // every wave: slot h published, slot h-1 no longer read
-    __builtin_amdgcn_sched_barrier(0);
-    if (h + 3 < nh) stage(h + 3);
-    const uint8_t* As = smem + (h & 3) * kHalfSlot;
-    const uint8_t* Bs = As + kHalfOp;
-    bf16x8 af[2][4], bfr[2][2];
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) bfr[ks][j] = frag_half<BKM>(Bs, wn * 64 + j * 32, ks, lane);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[ks][i] = frag_half<AK>(As, wm * 128 + i * 32, ks, lane);
-    }
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ks][i], bfr[ks][j], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  __builtin_amdgcn_s_barrier();  // the epilogue reuses the ring
-  big_epilogue<MODE>(g, acc, m0, n0, wm, wn, lane, smem);
-}
 
 // ---------------------------------------------------------------------------------------------
 // 256x256 tile, 8-phase ping-pong schedule (cdna_hip_programming.md §5 "256² 8-phase template",
@@ -1103,7 +823,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
   const bool f32out = MODE == 1 || g.c_f32;
   uint8_t* cbase = reinterpret_cast<uint8_t*>(g.C) + (MODE == 1 ? (int64_t)blockIdx.z * g.M * g.N * 4 : 0);
   const int ldo = MODE == 1 ? g.N : g.ldc;
-  const uint32_t cbytes = (g.dbg & 1) ? 0u : ((uint32_t)(g.M - 1) * ldo + g.N) * (f32out ? 4 : 2);
+  const uint32_t cbytes = ((uint32_t)(g.M - 1) * ldo + g.N) * (f32out ? 4 : 2);
   const bool want_aux = MODE == 0 && ACT == 2 && g.aux;
   uint8_t* stg = smem + 2 * P::BUF + wid * P::STG;  // this wave's epilogue staging slot
   float fmul = 1.f;
@@ -1157,8 +877,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
       for (int i = 0; i < 8 * IM; ++i) acc[i] *= fmul;
     }
     const rsrc_t rc = make_rsrc(cbase, cbytes);
-    if (g.dbg & 2) {
-    } else if (f32out) {  // fp32: 16-byte row segments straight from registers
+    if (f32out) {  // fp32: 16-byte row segments straight from registers
 #pragma unroll
       for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -1517,15 +1236,6 @@ static hipError_t launch_t(const GemmArgs& g, int splits, hipStream_t st) {
   return hipGetLastError();
 }
 
-// 256x256 kernel variant: 0 = 2-stage, 1 = half-stage ring, 2 = 8-phase ping-pong (default)
-static int big_variant() {
-  static const int v = [] {
-    const char* e = getenv("PSD_GEMM_BIG");
-    return e ? atoi(e) : 2;
-  }();
-  return v;
-}
-
 static int cu_count() {
   static const int n = [] {
     int dev = 0, cus = 0;
@@ -1537,15 +1247,8 @@ static int cu_count() {
   return n;
 }
 
-// workgroups of the persistent 8-phase grid: one per CU (the kernel's LDS allows no second);
-// PSD_GEMM_PERSIST=0 launches one workgroup per tile instead
-static int persistent_grid() {
-  static const int n = [] {
-    const char* e = getenv("PSD_GEMM_PERSIST");
-    return (e && atoi(e) == 0) ? (1 << 30) : cu_count();
-  }();
-  return n;
-}
+// workgroups of the persistent 8-phase grid: one per CU (the kernel's LDS allows no second)
+static int persistent_grid() { return cu_count(); }
 
 template <int BM, bool AK, bool BKM, int MODE, bool F8, int ACT, bool GA = false, int F8A = 0, bool GB = false,
           bool MX = false, bool ST = false>
@@ -1578,14 +1281,8 @@ static hipError_t launch_8p_act(const GemmArgs& g, int splits, hipStream_t st) {
   constexpr int KT = F8 ? 128 : BK;
   int grid = nwg;
   if (MODE == 0 && splits == 1 && g.K / KT >= 2) grid = std::min(nwg, persistent_grid());
-  static const int dbg = [] {
-    const char* e = getenv("PSD_GEMM_DBG");
-    return e ? atoi(e) : 0;
-  }();
-  GemmArgs ga = g;
-  ga.dbg = dbg;
   hipLaunchKernelGGL((gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT, GA, F8A, GB, MX, ST>), dim3(grid, 1, splits), dim3(512),
-                     lds, st, ga);
+                     lds, st, g);
   return hipGetLastError();
 }
 
@@ -1600,15 +1297,6 @@ static hipError_t launch_8p(const GemmArgs& g, int splits, hipStream_t st) {
   }
   if (g.act == 3) return hipErrorNotSupported;
   return launch_8p_act<BM, AK, BKM, MODE, F8, 0>(g, splits, st);
-}
-
-// A/B override of the fp8 tile height (PSD_GEMM_F8_BM=128|256; 0: the pick_bm heuristic)
-static int f8_bm_override() {
-  static const int v = [] {
-    const char* e = getenv("PSD_GEMM_F8_BM");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
 }
 
 // 8-phase tile height: a 128x256 tile costs ~0.55 of a 256x256 one, so narrow problems (few
@@ -1626,27 +1314,10 @@ static int pick_bm(int M, int N, int splits, bool a_kmajor = true) {
 
 template <bool AK, bool BKM, int MODE>
 static hipError_t launch_big(const GemmArgs& g, int splits, hipStream_t st) {
-  const int var = big_variant();
-  if (g.part && var != 2) return hipErrorNotSupported;  // statistics: the 8-phase epilogue only
-  if (var == 2) {
-    if constexpr (AK) {
-      if (pick_bm(g.M, g.N, splits) == 128) return launch_8p<128, AK, BKM, MODE>(g, splits, st);
-    }
-    return launch_8p<256, AK, BKM, MODE>(g, splits, st);
+  if constexpr (AK) {
+    if (pick_bm(g.M, g.N, splits) == 128) return launch_8p<128, AK, BKM, MODE>(g, splits, st);
   }
-  const void* fn = var == 1 ? (const void*)gemm256r_kernel<AK, BKM, MODE> : (const void*)gemm256_kernel<AK, BKM, MODE>;
-  static bool attr_set[2] = {false, false};
-  if (!attr_set[var == 1]) {
-    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kBigLds);
-    if (e != hipSuccess) return e;
-    attr_set[var == 1] = true;
-  }
-  const int nwg = ((g.M + kBig - 1) / kBig) * ((g.N + kBig - 1) / kBig);
-  if (var == 1)
-    hipLaunchKernelGGL((gemm256r_kernel<AK, BKM, MODE>), dim3(nwg, 1, splits), dim3(512), kBigLds, st, g);
-  else
-    hipLaunchKernelGGL((gemm256_kernel<AK, BKM, MODE>), dim3(nwg, 1, splits), dim3(512), kBigLds, st, g);
-  return hipGetLastError();
+  return launch_8p<256, AK, BKM, MODE>(g, splits, st);
 }
 
 // the 8-phase kernel addresses each operand through a buffer descriptor with 32-bit byte offsets
@@ -1659,19 +1330,15 @@ static bool fits_rsrc(const GemmArgs& g, int esz) {
 
 static bool big_ok(const GemmArgs& g, int kseg) {
   // enough big tiles to fill the chip, no K tail inside a stage, MN-major operands 8-aligned
-  if (getenv("PSD_GEMM_SMALL_ONLY")) return false;
-  if (big_variant() == 2 && !fits_rsrc(g, 2)) return false;
+  if (!fits_rsrc(g, 2)) return false;
   // 8-phase epilogue: 16-byte stores of 8 bf16 / 4 fp32 columns, whole or dropped
-  if (big_variant() == 2 && (g.N % 8 != 0 || (g.k_per_split == 0 && g.ldc % 8 != 0))) return false;
-  if (big_variant() == 2 && (reinterpret_cast<uintptr_t>(g.bias) & 3)) return false;  // bias: dword LDS-DMA
+  if (g.N % 8 != 0 || (g.k_per_split == 0 && g.ldc % 8 != 0)) return false;
+  if (reinterpret_cast<uintptr_t>(g.bias) & 3) return false;  // bias: dword LDS-DMA
   const int splits = g.k_per_split > 0 ? (g.K + g.k_per_split - 1) / g.k_per_split : 1;
-  if (big_variant() == 2) {  // 8-phase: BM 128 or 256, BN 256
-    const int bm = pick_bm(g.M, g.N, splits, g.a_kmajor);
-    const int64_t tiles = (int64_t)((g.M + bm - 1) / bm) * ((g.N + 255) / 256) * splits;
-    return g.M >= 128 && g.N >= 256 && kseg % 64 == 0 && tiles >= 64 && g.K >= 256;
-  }
-  const int64_t tiles = (int64_t)((g.M + 255) / 256) * ((g.N + 255) / 256) * splits;
-  return g.M >= 256 && g.N >= 256 && kseg % 64 == 0 && tiles >= 64 && g.K >= 256;
+  // 8-phase: BM 128 or 256, BN 256
+  const int bm = pick_bm(g.M, g.N, splits, g.a_kmajor);
+  const int64_t tiles = (int64_t)((g.M + bm - 1) / bm) * ((g.N + 255) / 256) * splits;
+  return g.M >= 128 && g.N >= 256 && kseg % 64 == 0 && tiles >= 64 && g.K >= 256;
 }
 
 template <bool AK, bool BKM, int MODE>
@@ -1702,7 +1369,7 @@ hipError_t launch_conv_fwd(const GemmArgs& g, hipStream_t st) {
                   g.M >= 128 && g.N >= 256 && g.N % 8 == 0 && g.ldc % 8 == 0 && !g.bias && g.act == 0 &&
                   (int64_t)(g.N - 1) * g.ldb + g.K < ((int64_t)1 << 31) && xbytes > 0 &&
                   (int64_t)(g.M - 1) * g.ldc + g.N < ((int64_t)1 << 31) && g.cv_S > 0 && g.cv_W < 32768 &&
-                  g.cv_H < 32768 && big_variant() == 2;
+                  g.cv_H < 32768;
   if (!ok) return hipErrorNotSupported;
   return pick_bm(g.M, g.N, 1) == 128 ? launch_8p_act<128, true, true, 0, false, 0, true>(g, 1, st)
                                      : launch_8p_act<256, true, true, 0, false, 0, true>(g, 1, st);
@@ -1727,12 +1394,8 @@ hipError_t launch_conv_fwd_fp8(const GemmArgs& g, hipStream_t st) {
   if (mx)  // block-scaled: 128-row tiles (the scale staging needs the LDS a 256-row tile leaves no room for)
     return g.f8a == 1 ? launch_8p_act<128, true, true, 0, true, 0, true, 1, false, true>(g, 1, st)
                       : launch_8p_act<128, true, true, 0, true, 0, true, 0, false, true>(g, 1, st);
-  const bool b128 = f8_bm_override() ? f8_bm_override() == 128 : true;
-  if (g.f8a == 1)
-    return b128 ? launch_8p_act<128, true, true, 0, true, 0, true, 1>(g, 1, st)
-                : launch_8p_act<256, true, true, 0, true, 0, true, 1>(g, 1, st);
-  return b128 ? launch_8p_act<128, true, true, 0, true, 0, true>(g, 1, st)
-              : launch_8p_act<256, true, true, 0, true, 0, true>(g, 1, st);
+  if (g.f8a == 1) return launch_8p_act<128, true, true, 0, true, 0, true, 1>(g, 1, st);
+  return launch_8p_act<128, true, true, 0, true, 0, true>(g, 1, st);
 }
 
 hipError_t launch_gemm_fp8(const GemmArgs& g, hipStream_t st) {
@@ -1769,7 +1432,7 @@ hipError_t launch_conv_wgrad(const GemmArgs& g0, float* slab, int splits, void* 
   const bool ok = !g0.a_kmajor && !g0.b_kmajor && g0.cv_logC >= 3 && g0.N % (1 << g0.cv_logC) == 0 &&
                   g0.M >= 256 && g0.M % 8 == 0 && g0.N >= 256 && g0.N % 8 == 0 && g0.K >= 128 &&
                   g0.cv_abytes > 0 && g0.cv_S > 0 && g0.cv_W < 32768 && g0.cv_H < 32768 && splits >= 1 &&
-                  (int64_t)(g0.K - 1) * g0.lda + g0.M < ((int64_t)1 << 31) && big_variant() == 2;
+                  (int64_t)(g0.K - 1) * g0.lda + g0.M < ((int64_t)1 << 31);
   if (!ok) return hipErrorNotSupported;
   GemmArgs g = g0;
   g.C = slab;

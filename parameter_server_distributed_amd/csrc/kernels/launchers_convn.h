@@ -18,7 +18,6 @@ struct ConvnArgs {
   int ldc;
   int variant;  // tile geometry (convn_variants(N) of them); -1: the default
   int nslot;    // set by the launcher
-  int log_sw;   // set by the launcher (HALO variants: log2 of the slots per output row)
   // bwd-data with the producing BN's backward reduction in the epilogue (bwd 1 / 2, convn.hip);
   // part then receives sum g and sum g (x - mean) per channel
   int bwd;

@@ -19,7 +19,6 @@ struct GemmArgs {
   int k_per_split;
   const float* a_scale;  // fp8 GEMM: dequant factors (device scalars), else unused
   const float* b_scale;
-  int dbg;  // timing experiments (PSD_GEMM_DBG): 1 drop the C stores, 2 skip the epilogue; 0 in production
   // implicit-GEMM convolution (launch_conv_fwd): A = NHWC input [Nb][H][W][C], M = Nb*Ho*Wo output
   // pixels, K = R*S*C ordered (r, s, ci), C a power of two >= 64; B = weights [Cout][R][S][C]
   int cv_H, cv_W, cv_logC, cv_Ho, cv_Wo, cv_S, cv_stride, cv_pad;

@@ -2,6 +2,7 @@
 // (only CPU tensors reach ops.cpp in those builds; a device call fails loudly instead of linking HIP
 // device code into a TSAN/ASAN binary).
 #include "../kernels/launchers.h"
+#include "../kernels/launchers_xfer.h"
 
 namespace psd {
 hipError_t launch_fused_apply(const OptimHyper&, const OptimDyn*, float*, const SourceList&, float*, float*, uint16_t*,
@@ -35,4 +36,6 @@ hipError_t launch_quant_mx(const void*, int32_t, int64_t, int, uint8_t*, uint8_t
 hipError_t launch_dequant_mx(const uint8_t*, const uint8_t*, int64_t, void*, int32_t, hipStream_t) {
   return hipErrorNotSupported;
 }
+hipError_t launch_xfer(const XferList&, hipStream_t) { return hipErrorNotSupported; }
+hipError_t launch_xfer_mx(const XferMxList&, hipStream_t) { return hipErrorNotSupported; }
 }  // namespace psd

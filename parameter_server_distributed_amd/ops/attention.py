@@ -15,12 +15,12 @@ the tests compare against.
 """
 from __future__ import annotations
 
-import os
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..utils.config import feature as _feat
 from .. import native
 
 
@@ -29,7 +29,7 @@ class _AttnFn(torch.autograd.Function):
     def forward(ctx, qkv, mod, p):
         # qkv straight from an MfmaLinear with a bias (ops/linear.py tags its output): backward also
         # sums dqkv's columns -- that Linear's bias gradient -- and hands it over
-        src = getattr(qkv, "_psd_src", None) if os.environ.get("PSD_ATTN_BIAS", "1") != "0" else None
+        src = getattr(qkv, "_psd_src", None) if _feat("attn_bias") else None
         ctx.src = src if (src is not None and src[0].bias is not None and src[0].act in (None, "none")
                           and src[0]._psd_tok == src[1]) else None
         qkv = qkv.contiguous()

@@ -41,10 +41,6 @@ _SOURCE = {"local": 0, "claimed": 0, "peer": 0, "file": 0}
 _FILE_KEYS: set = set()
 
 
-def enabled(var: str) -> bool:
-    return os.environ.get(var, "1") != "0"
-
-
 _REJECTED: dict[tuple, list] = {}
 
 
@@ -108,8 +104,6 @@ def _store():
     import torch.distributed as dist
 
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() <= 1:
-        return None
-    if os.environ.get("PSD_AUTOTUNE_PER_RANK") == "1":  # A/B: the old independent per-rank timing
         return None
     return dist.distributed_c10d._get_default_store()
 

@@ -15,14 +15,13 @@ compare the kernels against.
 """
 from __future__ import annotations
 
-import os
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..utils.config import feature as _feat
 from .. import native
-from . import autotune as _at
 
 
 def _kernel_ok(x: torch.Tensor) -> bool:
@@ -36,18 +35,18 @@ def _q8_args(mod, x: torch.Tensor) -> dict:
     cons = getattr(mod, "_psd_q8_consumer", None)
     if cons is None or not mod.relu or x.dim() != 4 or not cons.psd_fp8_consumes(x.shape[1]):
         return {}
-    if _at.enabled("PSD_FP8_MX"):
+    if _feat("fp8_mx"):
         # MX operands: the apply pass writes e4m3 + one E8M0 scale per 32 channels (a lane quad's
         # block maximum, kernels/bn.hip Q8 == 2) -- the consumer's own quantise pass (a full read of
-        # y) never runs. PSD_FP8_MX_HANDOVER=0: the consumer quantises.
-        if x.shape[1] % 32 or not _at.enabled("PSD_FP8_MX_HANDOVER"):
+        # y) never runs. feature fp8_mx_handover off: the consumer quantises.
+        if x.shape[1] % 32 or not _feat("fp8_mx_handover"):
             return {}
         q = torch.empty_like(x, dtype=torch.float8_e4m3fn, memory_format=torch.channels_last)
         return {"q8_out": q, "q8_mx": torch.empty(x.numel() // 32, dtype=torch.uint8, device=x.device)}
     # measured on Wide-ResNet-101-2 b512: 3,589 / 3,584 img/s with the hand-over vs 3,606 without
     # (same box, one call): the extra fp8 convert in the apply pass costs what the saved read of y
-    # gains, so it is opt-in (PSD_FP8_HANDOVER=1)
-    if os.environ.get("PSD_FP8_HANDOVER", "0") != "1" or _at.enabled("PSD_FP8_MX"):
+    # gains, so it is opt-in (feature fp8_handover)
+    if not _feat("fp8_handover") or _feat("fp8_mx"):
         return {}  # (the hand-over writes per-tensor e4m3; MX operands are quantised by the consumer)
     sc = cons._f8[0]
     if sc.hist is None or sc.hist.device != x.device:
@@ -76,8 +75,8 @@ def _dq8_args(mod, x: torch.Tensor) -> dict:
     also writes the MX e5m2 copy of it (kernels/bn.hip bn_bwd_elemt_kernel DQ): the convolution's own
     quantise pass (a full read of dY) never runs."""
     prod = getattr(mod, "_psd_dq8_producer", None)
-    if (prod is None or x.dim() != 4 or x.shape[1] % 32 or not _at.enabled("PSD_FP8_MX")
-            or not _at.enabled("PSD_FP8_MX_HANDOVER") or not prod.psd_fp8_dgrad()):
+    if (prod is None or x.dim() != 4 or x.shape[1] % 32 or not _feat("fp8_mx")
+            or not _feat("fp8_mx_handover") or not prod.psd_fp8_dgrad()):
         return {}
     q = torch.empty_like(x, dtype=torch.float8_e5m2, memory_format=torch.channels_last)
     return {"dq": q, "dqmx": torch.empty(x.numel() // 32, dtype=torch.uint8, device=x.device)}
@@ -121,7 +120,7 @@ def _fold_target(mod, x: torch.Tensor):
     records the output it produced through its fold-aware Function; a mismatch (another producer, a
     stale record) means no fold."""
     conv = getattr(mod, "_psd_fold_conv", None)
-    if conv is None or not _at.enabled("PSD_BN_FOLD"):
+    if conv is None or not _feat("bn_fold"):
         return None
     rec = getattr(conv, "_psd_fold_out", None)
     if rec is None or rec[0] != x.data_ptr() or rec[1] != tuple(x.shape):
@@ -141,7 +140,7 @@ def _fold_pair_ok(bn3, x, bnd, r):
     """Both tail BNs fold into stride-1 1x1 convolutions whose fold wgrad takes their whole input:
     the dual tail can then take sum g y3 / sum g yd from g^T a2 / g^T x_in (rowdot) instead of
     reading y3 / yd in the consumer's epilogue. Returns (conv3, convd) or None."""
-    if not (_at.enabled("PSD_BN_FOLD_DS") and os.environ.get("PSD_DUAL_NOBX", "1") != "0"):
+    if not (_feat("bn_fold_ds") and _feat("dual_nobx")):
         return None
     c3, cd = _fold_target(bn3, x), _fold_target(bnd, r)
     if c3 is None or cd is None:
@@ -320,7 +319,7 @@ class _BNAddBNReluFn(torch.autograd.Function):
             g, part, rows, part_d = pre
             # the downsample BN folded into its (stride-1 1x1) convolution too: no elementwise pass
             # at all -- both convolutions take g and their BN's coefficients (ops/conv.py _fold_backward)
-            convd = _fold_target(bnd, r) if conv is not None and _at.enabled("PSD_BN_FOLD_DS") else None
+            convd = _fold_target(bnd, r) if conv is not None and _feat("bn_fold_ds") else None
             dx, drr, dg3, db3, dgd, dbd, coef, coef_d = C.bn_bwd_dual_pre(
                 g, x, w3, mean, invstd, part, part_d, rows, r, wd, mean_d, invstd_d, dg3o, db3o, dgdo, dbdo,
                 fold=conv is not None, fold_d=convd is not None)

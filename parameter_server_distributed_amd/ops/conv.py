@@ -16,7 +16,7 @@ shape, wgrad is MIOpen's (hipBLASLt is 4-9x slower on the K = N*H*W reduction).
 So each shape is autotuned once, in the first eager step (the same role as MIOpen's own Find):
 forward and bwd-data pick MIOpen, hipBLASLt or our MFMA GEMM (kernels/gemm.hip), bwd-weight MIOpen
 or our split-K MFMA GEMM, by timing the candidates with HIP events (and validating their outputs). Decisions are cached per (M, cin, cout); inside a
-hipGraph capture no timing happens (an undecided shape takes MIOpen). ``PSD_CONV1X1=0`` turns the
+hipGraph capture no timing happens (an undecided shape takes MIOpen). feature ``conv1x1`` off (utils/config.py FEATURES) turns the
 GEMM routes off (A/B switch).
 
 Every other convolution (3x3 at any stride, strided 1x1 downsample) is a ``ConvNHWC``: forward
@@ -32,18 +32,18 @@ src/worker.cpp:316-329). This is worker-side compute for the BASELINE.json ResNe
 """
 from __future__ import annotations
 
-import os
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..utils.config import feature as _feat
 from . import autotune as _at
 from .bn import StridedDr, take_dr
 
 
 def _enabled() -> bool:
-    return _at.enabled("PSD_CONV1X1")
+    return _feat("conv1x1")
 
 
 def _choose(key: tuple, candidates: dict) -> str:
@@ -68,7 +68,7 @@ def _native():
 
 def _psd_ok(k: int, n: int) -> bool:
     """Shapes the MFMA GEMM takes as a 1x1 convolution (bf16 rows of 16-B multiples)."""
-    return k % 8 == 0 and n % 8 == 0 and _at.enabled("PSD_CONV1X1_PSD")
+    return k % 8 == 0 and n % 8 == 0 and _feat("conv1x1_mfma")
 
 
 def _as_2d(t: torch.Tensor) -> torch.Tensor:
@@ -83,7 +83,7 @@ def _from_2d(t2: torch.Tensor, n: int, h: int, w: int) -> torch.Tensor:
 
 def _fp8_ok(k: int, n: int) -> bool:
     """Shapes the fp8 MFMA GEMM / implicit-GEMM kernel takes (K a multiple of 128, >= 256 columns)."""
-    return k % 128 == 0 and k >= 256 and n >= 256 and n % 8 == 0 and _at.enabled("PSD_FP8_COMPUTE")
+    return k % 128 == 0 and k >= 256 and n >= 256 and n % 8 == 0 and _feat("fp8_compute")
 
 
 def _q8(t2: torch.Tensor, e5m2: bool = False, scaler: "DelayedScale | None" = None):
@@ -101,11 +101,11 @@ FP8_CALLS = {"fwd": 0, "dgrad": 0, "ps_weights": 0}  # fp8 kernel launches by ro
 
 
 def _mx_on() -> bool:
-    """MX block scaling for every fp8 operand (``PSD_FP8_MX``, default on): one E8M0 scale per 32
+    """MX block scaling for every fp8 operand (feature ``fp8_mx``, default on): one E8M0 scale per 32
     contiguous K-elements (kernels/fp8.hip quant_mx_kernel; the block-scaled MFMA consumes the
     scales), no amax pass and no scale history; 0: per-tensor scales (delayed for activations and
     gradients, just-in-time for weights)."""
-    return _at.enabled("PSD_FP8_MX")
+    return _feat("fp8_mx")
 
 
 def _q_act(t: torch.Tensor, e5m2: bool = False, scaler: "DelayedScale | None" = None):
@@ -167,7 +167,7 @@ def _take_q8(mod, x: torch.Tensor):
 def _psdn_ok(cin: int, cout: int) -> bool:
     """convn_'s contract: C a power of two >= 64, Cout 64 / 128 / a multiple of 256."""
     return cin >= 64 and (cin & (cin - 1)) == 0 and (cout in (64, 128) or cout % 256 == 0) and \
-        _at.enabled("PSD_CONVN")
+        _feat("convn")
 
 
 def _bn_consumer(mod):
@@ -176,7 +176,7 @@ def _bn_consumer(mod):
     bn = getattr(mod, "_psd_bn", None) if mod is not None else None
     # (no grad-mode test: this runs inside the autograd Function's forward, where grad mode is off;
     # the module's forward only takes the Function path with grad enabled)
-    if bn is None or not bn.training or bn.running_mean is None or not _at.enabled("PSD_CONVN_STATS"):
+    if bn is None or not bn.training or bn.running_mean is None or not _feat("convn_stats"):
         return None
     return bn
 
@@ -219,20 +219,18 @@ def _convn_variants(x, w2, k: int, stride: int, pad: int, bn=None) -> dict:
 
 def _variant_ok(cout: int, v: int, k: int, stride: int, pad: int, wo: int, cin: int | None = None,
                 h: int | None = None) -> bool:
-    """Variant v of the narrow kernel takes this shape. The plain HALO variants (kind 1) only with
-    PSD_CONVN_HALO=1: on the ResNet-50 shapes they measured no faster than the gathered variants,
-    profiles/convn_halo_r3.md, so by default they are not autotuned. The persistent HALO variant
-    (kind 2, C = N = 64 3x3 stride 1, H = Ho) and the persistent 1x1 variant (kind 3) are
-    candidates whenever their contract holds (PSD_CONVN_PERSIST=0 / PSD_CONVN_P1=0: off, A/B)."""
+    """Variant v of the narrow kernel takes this shape: the gathered variants (kind 0), the
+    persistent HALO variant (kind 2, C = N = 64 3x3 stride 1, H = Ho) and the persistent 1x1 variant
+    (kind 3) whenever their contract holds (features convn_persist / convn_p1)."""
     C = _native()
     if not C.convn_variant_ok(cout, v, k, k, stride, pad, wo):
         return False
     kind = C.convn_variant_kind(cout, v)
     if kind == 2:
-        return _at.enabled("PSD_CONVN_PERSIST") and cin == 64 and (h is None or h == wo)
+        return _feat("convn_persist") and cin == 64 and (h is None or h == wo)
     if kind == 3:  # persistent 1x1 (convp_kernel)
-        return _at.enabled("PSD_CONVN_P1")
-    return kind == 0 or os.environ.get("PSD_CONVN_HALO", "0") == "1"
+        return _feat("convn_p1")
+    return kind == 0
 
 
 def _part_rows(M: int, N: int, v: int, ho: int, wo: int, k: int) -> int:
@@ -259,7 +257,7 @@ def _bn_bwd_fusion(bn, x: torch.Tensor):
     its x and scale/shift) or mode 2 (a residual BN: bit-mask, plus the residual-branch gradient
     handed over by the next block). Returns the arguments, or None."""
     st = getattr(bn, "_psd_fwd", None) if bn is not None else None
-    if st is None or not _at.enabled("PSD_CONVN_BWD"):
+    if st is None or not _feat("convn_bwd"):
         return None
     y, bx, mean, ss, mbits, xd, mean_d = st
     if y.data_ptr() != x.data_ptr() or y.shape != x.shape or y.stride() != x.stride():
@@ -268,11 +266,11 @@ def _bn_bwd_fusion(bn, x: torch.Tensor):
         if not bn._psd_pending_dr:
             return None
         if isinstance(bn._psd_pending_dr[-1], StridedDr):  # a downsample conv's quarter-grid gradient
-            if xd is not None or x.shape[2] % 2 or x.shape[3] % 2 or not _at.enabled("PSD_CONVN_BWD5"):
+            if xd is not None or x.shape[2] % 2 or x.shape[3] % 2 or not _feat("convn_bwd5"):
                 return None
             return dict(mode=5, bn=bn, bx=bx, mean=mean, mbits=mbits)
         if xd is not None:  # a downsample block's dual tail: both BNs' reductions (mode 3)
-            if not _at.enabled("PSD_CONVN_BWD3"):
+            if not _feat("convn_bwd3"):
                 return None
             return dict(mode=3, bn=bn, bx=bx, mean=mean, mbits=mbits, bxd=xd, mean_d=mean_d)
         return dict(mode=2, bn=bn, bx=bx, mean=mean, mbits=mbits)
@@ -356,7 +354,7 @@ def _with_bn_bwd_reduce(fn, fu):
 def _stats_part(bn, M: int, cout: int, device):
     """Statistics-partials buffer for an 8-phase GEMM / implicit-GEMM launch whose epilogue reduces
     the consumer BN's batch statistics (kernels/gemm.hip ST), or None without a consumer BN."""
-    if bn is None or not _at.enabled("PSD_GEMM_STATS"):
+    if bn is None or not _feat("gemm_stats"):
         return None
     return torch.empty(_native().gemm_stats_rows(M), 2, cout, device=device, dtype=torch.float32)
 
@@ -389,7 +387,7 @@ def _convw_cands(dy, x, k: int, stride: int, pad: int) -> dict:
     (kernels/convw.hip); fn writes dW in OHWI order into ``into`` (a contiguous [Cout, k*k*Cin] view,
     e.g. the PS gradient sink) or a fresh tensor and returns the [Cout, Cin, k, k] channels_last view;
     raises autotune.Declined when the kernel does not take the shape."""
-    if not _at.enabled("PSD_CONVW"):
+    if not _feat("convw"):
         return {}
     C = _native()
     cout, cin = dy.shape[1], x.shape[1]
@@ -406,7 +404,7 @@ def _convw_cands(dy, x, k: int, stride: int, pad: int) -> dict:
         return fn
 
     nv = C.convw_variants(cout, kk)
-    if cout == 64 and kk == 576 and not _at.enabled("PSD_CONVW_PERSIST"):
+    if cout == 64 and kk == 576 and not _feat("convw_persist"):
         nv -= 1  # the persistent HALO wgrad is the last variant of this shape (A/B switch)
     return {f"psdw{v}": make(v) for v in range(nv)}
 
@@ -417,7 +415,7 @@ class DelayedScale:
     records its own in the same pass (kernels/fp8.hip quant_delayed_kernel), so the tensor is read
     once instead of twice (amax pass + quantise pass). The first call scales just-in-time and seeds
     the history. Values above the previous step's amax saturate at the fp8 maximum. The history is a
-    device tensor, so a captured hipGraph keeps updating it. ``PSD_FP8_DELAYED=0``: always
+    device tensor, so a captured hipGraph keeps updating it. feature ``fp8_delayed`` off: always
     just-in-time."""
 
     def __init__(self, margin: float = 1.0):
@@ -428,9 +426,9 @@ class DelayedScale:
         from . import FP8_E4M3_MAX, FP8_E5M2_MAX, quantize_fp8
 
         x = x.contiguous()
-        if self.hist is None or self.hist.device != x.device or not _at.enabled("PSD_FP8_DELAYED"):
+        if self.hist is None or self.hist.device != x.device or not _feat("fp8_delayed"):
             q, sinv = quantize_fp8(x, e5m2=e5m2)
-            if _at.enabled("PSD_FP8_DELAYED"):
+            if _feat("fp8_delayed"):
                 self.hist = torch.zeros(2, dtype=torch.float32, device=x.device)
                 self.hist[:1].copy_(sinv * (FP8_E5M2_MAX if e5m2 else FP8_E4M3_MAX) / self.margin)
             return q, sinv
@@ -647,7 +645,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         bn = _bn_consumer(mod)
         if _psd_ok(cin, cout):
             cands["psd"] = psd
-            if bn is not None and _at.enabled("PSD_GEMM_STATS") and n * h * w >= 128 and cout >= 256 and cin >= 256 \
+            if bn is not None and _feat("gemm_stats") and n * h * w >= 128 and cout >= 256 and cin >= 256 \
                     and cin % 64 == 0:
                 cands["psds"] = psds
         if _psdn_ok(cin, cout):
@@ -680,7 +678,7 @@ class _Conv1x1Fn(torch.autograd.Function):
             dy = dy.contiguous(memory_format=torch.channels_last)
         conv_bwd = torch.ops.aten.convolution_backward
         args = (None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1)
-        if need_x and ctx.fp8 and _fp8_ok(cout, cin) and _at.enabled("PSD_FP8_DGRAD"):
+        if need_x and ctx.fp8 and _fp8_ok(cout, cin) and _feat("fp8_dgrad"):
             # fp8 bwd-data: e5m2 dY (K-major [M, cout]) x e4m3 W^T ([cin, cout], K-major)
             got = _take_dq8(ctx.mod, dy) if _mx_on() else None
             if got is not None:  # written by the consumer BN's backward pass
@@ -778,7 +776,7 @@ class Conv1x1(nn.Conv2d):
     def psd_fp8_dgrad(self) -> bool:
         """True when this module's bwd-data runs in fp8 (quantising its output gradient)."""
         return (self.fp8 and _fp8_ok(self.out_channels, self.in_channels) and _enabled()
-                and _at.enabled("PSD_FP8_DGRAD"))
+                and _feat("fp8_dgrad"))
 
     def forward(self, x):
         if (_enabled() and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
@@ -928,7 +926,7 @@ class _ConvFn(torch.autograd.Function):
         cands = {"miopen": miopen}
         if _igemm_ok(cin, cout):
             cands["igemm"] = igemm
-            if bn is not None and _at.enabled("PSD_GEMM_STATS"):
+            if bn is not None and _feat("gemm_stats"):
                 cands["psds_igemm"] = igemm_stats
         if _psdn_ok(cin, cout):
             cands.update(_convn_variants(x, w2, k, stride, pad, bn))
@@ -948,7 +946,7 @@ class _ConvFn(torch.autograd.Function):
         dx = dw = None
         to = ctx.strided_to
         if (ctx.needs_input_grad[0] and to is not None and k == 1 and stride == 2 and pad == 0 and h % 2 == 0
-                and w % 2 == 0 and _at.enabled("PSD_CONVN_BWD5") and not ctx.fp8):
+                and w % 2 == 0 and _feat("convn_bwd5") and not ctx.fp8):
             # downsample conv whose input gradient goes to the producing BN (the block's _Fork): dY . W
             # on the quarter grid only, handed over as a StridedDr (the consumer convolution's bwd-data
             # adds it at even pixels, kernels/convn.hip mode 5); autograd gets a zero-stride marker
@@ -958,7 +956,7 @@ class _ConvFn(torch.autograd.Function):
                 return conv_bwd(dy, x, weight, *args, [True, False, False])[0]
 
             if stride == 1 and _igemm_ok(cout, cin) and 2 * pad == k - 1 and ctx.fp8 and cout % 128 == 0 \
-                    and _fp8_ok(k * k * cout, cin) and n * h * w >= 128 and _at.enabled("PSD_FP8_DGRAD"):
+                    and _fp8_ok(k * k * cout, cin) and n * h * w >= 128 and _feat("fp8_dgrad"):
                 # fp8 bwd-data: e5m2 dY gathered by the implicit GEMM, e4m3 flipped weights
                 wf = weight.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, k * k * cout).contiguous()
                 got = _take_dq8(ctx.mod, dy) if _mx_on() else None
@@ -1008,7 +1006,7 @@ class _ConvFn(torch.autograd.Function):
                 return y
 
             cands = {"miopen": miopen_w}
-            if (_at.enabled("PSD_CONV_WGRAD") and _wgrad_ok(cin, cout, k, dy)
+            if (_feat("conv_wgrad") and _wgrad_ok(cin, cout, k, dy)
                     and weight.is_contiguous(memory_format=torch.channels_last)):
                 cands["igemm"] = igemm_c
             wcands = _convw_cands(dy, x, k, stride, pad) if weight.is_contiguous(
@@ -1056,16 +1054,16 @@ class ConvNHWC(nn.Conv2d):
         """True when this module's stride-1 bwd-data runs in fp8 (implicit GEMM on e5m2 dY)."""
         k, cin, cout = self.kernel_size[0], self.in_channels, self.out_channels
         return (self.fp8 and self.stride[0] == 1 and 2 * self.padding[0] == k - 1 and _igemm_ok(cout, cin)
-                and cout % 128 == 0 and _fp8_ok(k * k * cout, cin) and _enabled() and _at.enabled("PSD_FP8_DGRAD")
-                and _at.enabled("PSD_CONV_IGEMM"))
+                and cout % 128 == 0 and _fp8_ok(k * k * cout, cin) and _enabled() and _feat("fp8_dgrad")
+                and _feat("conv_igemm"))
 
     def psd_fp8_consumes(self, cin: int) -> bool:
         k = self.kernel_size[0]
         return (self.fp8 and cin % 128 == 0 and _fp8_ok(k * k * cin, self.out_channels) and _enabled()
-                and _at.enabled("PSD_CONV_IGEMM"))
+                and _feat("conv_igemm"))
 
     def forward(self, x):
-        if (_enabled() and _at.enabled("PSD_CONV_IGEMM") and x.is_cuda and x.dtype == torch.bfloat16
+        if (_enabled() and _feat("conv_igemm") and x.is_cuda and x.dtype == torch.bfloat16
                 and x.dim() == 4 and self.weight.dtype == torch.bfloat16 and self.groups == 1
                 and self.dilation == (1, 1) and x.is_contiguous(memory_format=torch.channels_last)
                 and self.weight.is_contiguous(memory_format=torch.channels_last)):

@@ -17,7 +17,7 @@ Per-shape routing (ops/autotune.py): for bf16 the forward, dgrad and wgrad GEMMs
 once against hipBLASLt (torch.addmm / mm; bias + activation then run as separate passes) and the
 faster path is kept. Measured on BERT-base (M = 8192 tokens) hipBLASLt wins most forward / dgrad
 shapes, the split-K MFMA wgrad writing straight into the PS gradient buffer stays competitive.
-``PSD_LINEAR_TUNE=0`` pins everything to the MFMA kernels.
+Feature ``linear_tune`` off pins everything to the MFMA kernels.
 
 CPU tensors (and non-bf16 / unaligned shapes) use ``F.linear`` -- the reference the tests compare
 against.
@@ -28,6 +28,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..utils.config import feature as _feat
 from .. import native
 from . import autotune as _at
 
@@ -42,7 +43,7 @@ def _ok(x: torch.Tensor, w: torch.Tensor) -> bool:
 def _route(key: tuple, mfma, blas, out: torch.Tensor | None = None):
     """The faster of the MFMA kernel and hipBLASLt for this GEMM shape (ops/autotune.py); ``out``
     is the buffer both candidates write (validated against each other on the first call)."""
-    if not _at.enabled("PSD_LINEAR_TUNE"):
+    if not _feat("linear_tune"):
         return mfma
     probe = (lambda: out) if out is not None else None
     return mfma if _at.choose(("linear",) + key, {"mfma": mfma, "blas": blas}, "mfma", probe) == "mfma" else blas
@@ -63,7 +64,7 @@ def _dgrad_route(key: tuple, dy2: torch.Tensor, w: torch.Tensor, dx: torch.Tenso
     def blas():
         torch.mm(dy2, w, out=dx)
 
-    if not _at.enabled("PSD_LINEAR_TUNE"):
+    if not _feat("linear_tune"):
         return nn_
     cands = {"mfma": nn_, "mfma_t": nt_, "blas": blas}
     return cands[_at.choose(("linear",) + key, cands, "mfma", lambda: dx)]
@@ -146,7 +147,7 @@ class _LinearFn(torch.autograd.Function):
         # producing GELU Linear's activation backward in its epilogue when x is that Linear's output
         # of the current forward
         src = getattr(mod, "_psd_gelu_from", None)
-        fuse = (src is not None and _at.enabled("PSD_GELU_FUSE") and getattr(x, "_psd_gelu_tok", None) is not None
+        fuse = (src is not None and _feat("gelu_fuse") and getattr(x, "_psd_gelu_tok", None) is not None
                 and x._psd_gelu_tok == (id(src), src._psd_tok) and getattr(src, "_psd_gelu_pre", None) is not None)
         ctx.gelu_src = src if fuse else None
         ctx.gelu_tok = src._psd_tok if fuse else None

@@ -35,6 +35,7 @@ from __future__ import annotations
 
 import torch
 
+from ..utils.config import feature as _feat
 from . import autotune as _at
 from .conv import (Conv1x1, _fold_backward, _from_2d, _fwd_records, _native, _part_rows, _sink_view, fold_ok)
 from .bn import FusedBatchNorm2d, take_dr
@@ -47,7 +48,7 @@ TAIL_CALLS = {"fwd": 0, "bwd_fused": 0, "bwd_recompute": 0}
 def tail_ok(conv, bn, a2: torch.Tensor, idt: torch.Tensor) -> bool:
     """The recomputing tail applies: a bf16 Conv1x1 (no fp8) into a training ReLU FusedBatchNorm2d
     with an identity residual, channels_last operands, a shape the narrow kernel and the fold take."""
-    if not (_at.enabled("PSD_TAIL_RECOMPUTE") and _at.enabled("PSD_CONVN")) or not isinstance(conv, Conv1x1) \
+    if not (_feat("tail_recompute") and _feat("convn")) or not isinstance(conv, Conv1x1) \
             or conv.fp8:
         return False
     if not isinstance(bn, FusedBatchNorm2d) or not bn.relu or not bn.training or bn.weight is None:
@@ -96,7 +97,7 @@ def _stats_route(a2, w2, M: int, cin: int, cout: int, v: int, h: int, w: int, sh
     statistics-only pass recomputing the GEMM), timed per shape. The Gram statistics are those of the
     fp32 product, the pass's those of the bf16-rounded one (what the apply pass normalises)."""
     C = _native()
-    if not _at.enabled("PSD_TAIL_GRAM") or C.convw_gram_rows(cin) <= 0 or cout % 4:
+    if not _feat("tail_gram") or C.convw_gram_rows(cin) <= 0 or cout % 4:
         return "pass"
     dev = a2.device
 

@@ -58,6 +58,7 @@ import torch.nn as nn
 
 from .. import native
 from ..ops.optim import OptimConfig, OptimDyn
+from ..utils.config import fault
 from .collective_ps import ALIGN, _flat_view, _round, install_fp8_weights, zero_grads_, zero_plan
 
 
@@ -229,15 +230,14 @@ class AsyncPS:
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for _, p, _o, _n in layout]
         self._next = 0
         if self.is_cuda:
-            # push copies on PSD_ASYNC_PUSH_STREAMS streams (bucket i on stream i % n; the commit
-            # waits for all). Default 1: HIP maps a process's streams onto GPU_MAX_HW_QUEUES = 4
-            # hardware queues, and compute + engine apply + push + pull already take four -- a fifth
-            # stream shares a queue with one of them and serialises behind its work (ResNet-50
-            # b1024 async S = 1: 91-95 ms/step with two push streams vs 78 ms synchronous,
-            # gpurun_out/adiag2). 2+ only where the copies of several owners' links must overlap.
+            # ONE push stream: HIP maps a process's streams onto GPU_MAX_HW_QUEUES = 4 hardware
+            # queues, and compute + engine apply + push + pull already take four -- a fifth stream
+            # shares a queue with one of them and serialises behind its work (ResNet-50 b1024 async
+            # S = 1: 91-95 ms/step with two push streams vs 78 ms synchronous,
+            # profiles/async_push_streams_r4.md). The owners' links overlap inside one launch
+            # instead (kernels/xfer.hip).
             self.comm_stream = torch.cuda.Stream(device=dev)
-            n_push = max(1, int(os.environ.get("PSD_ASYNC_PUSH_STREAMS", "1")))
-            self.comm_streams = [self.comm_stream] + [torch.cuda.Stream(device=dev) for _ in range(n_push - 1)]
+            self.comm_streams = [self.comm_stream]
             self.pull_stream = torch.cuda.Stream(device=dev)
             self.push_done = [None, None]
             self.step_done = [None, None]  # end of a step's work on the compute stream, per buffer
@@ -340,7 +340,7 @@ class AsyncPS:
                 if abs(float(sl.sum()) - want_s) > 1e-6 * max(want_a, 1.0) or \
                         abs(float(sl.abs().sum()) - want_a) > 1e-6 * max(want_a, 1.0):
                     ok, why = False, f"rank {self.rank}: pulled shard {k} != its owner's snapshot"
-        if os.environ.get("PSD_ASYNC_SELFTEST_FAIL_RANK") == str(self.rank):  # fault injection (tests)
+        if fault("selftest_fail_rank") == self.rank:  # fault injection (tests)
             ok, why = False, f"rank {self.rank}: injected self-test failure"
         self._barrier("selftest-push")
         for k in self.my_shards:

@@ -38,6 +38,7 @@ import torch.nn as nn
 from .. import native
 from ..ops import multi_reduce_
 from ..ops.optim import OptimConfig, OptimDyn, advance_, apply_no_advance_
+from ..utils.config import feature
 from .transport import LocalTransport, Transport
 
 ALIGN = 64  # elements: every tensor starts 128-B aligned in the bf16 buffers
@@ -238,7 +239,7 @@ class CollectivePS:
         # MX (default): one E8M0 scale per 32 elements (ALIGN = 64 keeps every tensor and every
         # shard slice block-aligned, so slices quantise independently, with no amax reduction); the
         # fp8 convolutions consume the pulled e4m3 weights + scales directly (install_fp8_weights)
-        self.pull_mx = self.pull_fp8 and os.environ.get("PSD_FP8_MX", "1") != "0" and self.is_cuda
+        self.pull_mx = self.pull_fp8 and feature("fp8_mx") and self.is_cuda
         if self.pull_fp8:
             self.p8 = torch.zeros(self.total, dtype=torch.float8_e4m3fn, device=dev)
             self.p8_scale = torch.ones(len(buckets) * self.P, dtype=torch.float32, device=dev)

@@ -16,8 +16,8 @@ coordinator returns a consistent host:port (D1); initial parameters come from wo
 model through ``InitParameters`` (the reference let the first averaged gradient *become* the
 parameters, src/parameter_server.cpp:78-81 -- kept only in ``reference_compat`` mode).
 
-Fault injection (env): PSD_FAULT_STOP_HEARTBEAT_AFTER=n, PSD_FAULT_EXIT_AFTER_PUSH=k,
-PSD_FAULT_PUSH_DELAY_MS=ms.
+Fault injection (env): PSD_FAULT="stop_heartbeat_after=n,exit_after_push=k,push_delay_ms=ms"
+(utils/config.py FAULTS).
 """
 from __future__ import annotations
 
@@ -30,6 +30,7 @@ import torch
 
 from .. import models
 from ..rpc import schema, service
+from ..utils.config import fault
 from ..utils.log import get_logger
 
 cpb = schema.coordinator
@@ -124,7 +125,7 @@ class Worker:
 
     def _heartbeat_loop(self):
         n = 0
-        stop_after = int(os.environ.get("PSD_FAULT_STOP_HEARTBEAT_AFTER", "-1"))
+        stop_after = fault("stop_heartbeat_after")
         while not self._stop.wait(self.heartbeat_s):
             if not self._initialized.is_set():
                 continue
@@ -168,14 +169,14 @@ class Worker:
         return float(loss.detach().float()), [(n, p.grad.detach()) for n, p in self.model.named_parameters()]
 
     def push(self, iteration: int, grads):
-        delay = int(os.environ.get("PSD_FAULT_PUSH_DELAY_MS", "0"))
+        delay = fault("push_delay_ms")
         if delay:
             time.sleep(delay / 1000.0)
         up = ppb.GradientUpdate(worker_id=self.worker_id, iteration=iteration, pulled_version=max(self.version, 0))
         up.gradients.extend(service.tensors_to_protos(grads, raw=self.raw_wire, bf16=self.bf16_wire))
         r = self._retry(lambda: self.ps.ReceiveGradients(up))
         self.pushes += 1
-        k = int(os.environ.get("PSD_FAULT_EXIT_AFTER_PUSH", "-1"))
+        k = fault("exit_after_push")
         if 0 < k <= self.pushes:
             self.log.error("fault injection: exiting after push %d", self.pushes)
             os._exit(3)

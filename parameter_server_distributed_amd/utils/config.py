@@ -41,3 +41,111 @@ def apply_config(ap: argparse.ArgumentParser, argv: list[str] | None = None) -> 
     if unknown:
         raise SystemExit(f"{known.config}: unknown option(s) {unknown}")
     ap.set_defaults(**cfg)
+
+
+# ---------------------------------------------------------------------------------------------
+# Kernel-path features: one documented default each, one override variable.
+#
+# Every fused / hand-written path that has a library or unfused fallback is gated by a feature
+# here, so a test can pin the fallback as its reference and an A/B run can switch one path off
+# without a code change. Override with PSD_FEATURES="name=0,other=1" (the variable is re-read when
+# it changes: tests set it per case) or programmatically with set_feature(). The defaults are the
+# production paths; the switches are not separate environment variables.
+FEATURES: dict[str, tuple[bool, str]] = {
+    # convolutions (ops/conv.py, kernels/convn.hip, convw.hip, gemm.hip)
+    "conv1x1": (True, "per-shape routing of 1x1 convolutions (MIOpen / hipBLASLt / MFMA); off: MIOpen only"),
+    "conv1x1_mfma": (True, "the 8-phase MFMA GEMM as a 1x1-convolution candidate"),
+    "conv_igemm": (True, "implicit-GEMM MFMA convolution (gemm.hip) as a forward / bwd-data candidate"),
+    "conv_wgrad": (True, "implicit-GEMM MFMA weight gradient as a candidate"),
+    "convn": (True, "narrow implicit-GEMM convolution kernels (convn.hip) as candidates"),
+    "convn_stats": (True, "consumer-BN statistics in the narrow convolution's epilogue"),
+    "convn_persist": (True, "persistent layer-1 3x3 kernel (convh)"),
+    "convn_p1": (True, "persistent 1x1 kernels (convp / convpr)"),
+    "convn_bwd": (True, "producing BN's backward reduction in the bwd-data epilogue (modes 1/2)"),
+    "convn_bwd3": (True, "the dual-BN tail's reduction in the bwd-data epilogue (mode 3)"),
+    "convn_bwd5": (True, "stride-2 downsample gradient added on the quarter grid (mode 5)"),
+    "convw": (True, "narrow weight-gradient kernel (convw.hip) as a candidate"),
+    "convw_persist": (True, "persistent layer-1 3x3 weight gradient (convhw)"),
+    "gemm_stats": (True, "consumer-BN statistics in the 8-phase GEMM epilogue"),
+    # batch norm / bottleneck tail (ops/bn.py, ops/tail.py)
+    "bn_fold": (True, "bn3's backward folded into conv3's bwd-data / weight-gradient GEMMs"),
+    "bn_fold_ds": (True, "the stride-1 downsample BN folded into its convolution's backward"),
+    "dual_nobx": (True, "downsample blocks' dual tail without the BN inputs in the consumer epilogue"),
+    "tail_recompute": (True, "identity blocks' conv3 output recomputed instead of stored"),
+    "tail_gram": (True, "the recomputing tail's statistics from the Gram matrix of conv3's input"),
+    # fp8 (Wide-ResNet-101-2)
+    "fp8_compute": (True, "fp8 convolutions where the model asks for them"),
+    "fp8_mx": (True, "MX block scales for every fp8 operand; off: per-tensor scales"),
+    "fp8_mx_handover": (True, "BN passes write the consumer's MX e4m3 input / producer's MX e5m2 dY"),
+    "fp8_handover": (False, "per-tensor (non-MX) fp8 hand-over from the BN passes"),
+    "fp8_delayed": (True, "per-tensor fp8: delayed (previous-call amax) scaling"),
+    "fp8_dgrad": (True, "fp8 e5m2-dY bwd-data of the fp8 convolutions"),
+    # BERT (ops/linear.py, ops/attention.py)
+    "linear_tune": (True, "per-shape MFMA / hipBLASLt choice for Linear layers; off: MFMA only"),
+    "gelu_fuse": (True, "GELU backward in the consumer Linear's bwd-data GEMM epilogue"),
+    "attn_bias": (True, "QKV bias gradient handed over by the attention backward"),
+}
+
+_FEAT_ENV: str | None = None
+_FEAT_OVR: dict[str, bool] = {}
+_FEAT_SET: dict[str, bool] = {}
+
+
+def _feature_env() -> dict[str, bool]:
+    global _FEAT_ENV, _FEAT_OVR
+    raw = os.environ.get("PSD_FEATURES", "")
+    if raw != _FEAT_ENV:
+        ovr = {}
+        for item in filter(None, (t.strip() for t in raw.split(","))):
+            name, _, val = item.partition("=")
+            name = name.strip()
+            if name not in FEATURES:
+                raise ValueError(f"PSD_FEATURES: unknown feature {name!r} (known: {sorted(FEATURES)})")
+            ovr[name] = val.strip() not in ("0", "false", "off", "no")
+        _FEAT_ENV, _FEAT_OVR = raw, ovr
+    return _FEAT_OVR
+
+
+def feature(name: str) -> bool:
+    """Whether kernel-path feature ``name`` (FEATURES) is on: set_feature > PSD_FEATURES > default."""
+    if name in _FEAT_SET:
+        return _FEAT_SET[name]
+    ovr = _feature_env()
+    if name in ovr:
+        return ovr[name]
+    return FEATURES[name][0]
+
+
+def set_feature(name: str, on: bool | None) -> None:
+    """Pin feature ``name`` for this process (None: back to PSD_FEATURES / the default)."""
+    if name not in FEATURES:
+        raise ValueError(f"unknown feature {name!r}")
+    if on is None:
+        _FEAT_SET.pop(name, None)
+    else:
+        _FEAT_SET[name] = bool(on)
+
+
+def features() -> dict[str, bool]:
+    """Every feature's current value (bench JSON / logs)."""
+    return {n: feature(n) for n in FEATURES}
+
+
+# Fault injection (tests, chaos runs): PSD_FAULT="key=value,..." with the keys below; -1 / 0 = off.
+FAULTS: dict[str, tuple[int, str]] = {
+    "stop_heartbeat_after": (-1, "worker: stop sending coordinator heartbeats after n of them"),
+    "push_delay_ms": (0, "worker: sleep this long before every gradient push"),
+    "exit_after_push": (-1, "worker: exit the process right after its k-th push"),
+    "selftest_fail_rank": (-1, "async PS: this rank reports a failed start-up self-test"),
+}
+
+
+def fault(name: str) -> int:
+    """Integer value of fault-injection key ``name`` from PSD_FAULT (FAULTS default when unset)."""
+    if name not in FAULTS:
+        raise ValueError(f"unknown fault key {name!r}")
+    for item in filter(None, (t.strip() for t in os.environ.get("PSD_FAULT", "").split(","))):
+        k, _, v = item.partition("=")
+        if k.strip() == name:
+            return int(v)
+    return FAULTS[name][0]

@@ -31,8 +31,8 @@ def install(mode: str = "auto", path: str | None = None) -> str:
     tn.enable(True)
     if mode == "tune":
         tn.tuning_enable(True)
-        tn.set_max_tuning_duration(int(os.environ.get("PSD_TUNABLEOP_MS", "30")))
-        tn.set_max_tuning_iterations(int(os.environ.get("PSD_TUNABLEOP_ITERS", "20")))
+        tn.set_max_tuning_duration(30)  # ms per GEMM shape
+        tn.set_max_tuning_iterations(20)
         return "tune"
     tn.tuning_enable(False)
     tn.record_untuned_enable(False)

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Same-box A/B of bench.py: alternates two environment settings (ABAB), prints img/s per run.
-# Usage: scripts/gpu_ab.sh TAG "ENV_A" "ENV_B" [bench args...]   e.g. "PSD_BN_FOLD=0" "PSD_BN_FOLD=1"
+# Usage: scripts/gpu_ab.sh TAG "ENV_A" "ENV_B" [bench args...]   e.g. "PSD_FEATURES=bn_fold=0" "PSD_FEATURES=bn_fold=1"
 set -o pipefail
 TAG=$1; A=$2; B=$3; shift 3
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}

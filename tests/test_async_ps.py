@@ -528,7 +528,7 @@ def test_async_resume_rejects_other_layout(tmp_path):
 
 
 def _selftest_worker(rank, world, port, out_dir):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PSD_ASYNC_SELFTEST_FAIL_RANK="1")
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PSD_FAULT="selftest_fail_rank=1")
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.manual_seed(0)
     spec = models.build("mlp", torch.device("cpu"), torch.float32, hidden=64)

@@ -5,7 +5,7 @@ Pieces: the narrow conv kernel's K-concatenated second operand + bias (exact, sm
 wgrad kernel's fold products [g | x | 1]^T x (exact), the folded dgrad weights / bias and the wgrad
 combination (fp32 references of the same formulas). End to end: every parameter gradient of a
 ResNet-50 whose bn3 weights are non-zero (zero-init residual BNs would make the folded terms vanish)
-with the fold forced on vs PSD_BN_FOLD=0."""
+with the fold forced on vs feature bn_fold off."""
 import pytest
 import torch
 
@@ -80,8 +80,7 @@ def _resnet_grads(gpu, monkeypatch, fold: bool, force: str, fp32: bool = False, 
     from parameter_server_distributed_amd import models
     from parameter_server_distributed_amd.ops import autotune
 
-    monkeypatch.setenv("PSD_BN_FOLD", "1" if fold else "0")
-    monkeypatch.setenv("PSD_CONVN", "1" if convn else "0")
+    monkeypatch.setenv("PSD_FEATURES", f"bn_fold={int(fold)},convn={int(convn)}")
     monkeypatch.setenv("PSD_AUTOTUNE_FORCE", force)
     autotune._DECISIONS.clear()
     torch.manual_seed(0)
@@ -126,7 +125,7 @@ def _block_grads(gpu, monkeypatch, kind: str, mode: str):
     from parameter_server_distributed_amd.ops import autotune
     from parameter_server_distributed_amd.ops.bn import FusedBatchNorm2d
 
-    monkeypatch.setenv("PSD_BN_FOLD", "1" if mode == "fold" else "0")
+    monkeypatch.setenv("PSD_FEATURES", f"bn_fold={int(mode == 'fold')}")
     monkeypatch.setenv("PSD_AUTOTUNE_FORCE", "psdnf0,psdn0" if mode == "fold" else "psdn0")
     autotune._DECISIONS.clear()
     torch.manual_seed(2)
@@ -215,8 +214,7 @@ def _chain_grads(gpu, monkeypatch, mode: str, kind: str = "ds_id"):
     from parameter_server_distributed_amd.ops import autotune
     from parameter_server_distributed_amd.ops.bn import FusedBatchNorm2d
 
-    monkeypatch.setenv("PSD_BN_FOLD", "1" if mode == "fused" else "0")
-    monkeypatch.setenv("PSD_CONVN", "1" if mode == "fused" else "0")
+    monkeypatch.setenv("PSD_FEATURES", f"bn_fold={int(mode == 'fused')},convn={int(mode == 'fused')}")
     monkeypatch.setenv("PSD_AUTOTUNE_FORCE", "psdnb0,psdnf0,psdn0" if mode == "fused" else "miopen")
     autotune._DECISIONS.clear()
     torch.manual_seed(2)

@@ -37,7 +37,7 @@ def test_deploy_scale_up_down(tmp_path):
     env = dict(os.environ, CLUSTER_DIR=cd, WORKER_COUNT="2", ITERATIONS="80", NUM_GPUS="0",
                COORDINATOR_PORT=str(_port()), PS_PORT=str(_port()), CHECKPOINT_INTERVAL="0",
                PS_FLAGS="--optimizer momentum --lr 0.05", WORKER_FLAGS="--heartbeat-s 0.5 --batch 32",
-               PSD_FAULT_PUSH_DELAY_MS="40", PYTHONPATH=ROOT)
+               PSD_FAULT="push_delay_ms=40", PYTHONPATH=ROOT)
     try:
         subprocess.run(["bash", f"{ROOT}/scripts/deploy.sh"], env=env, check=True, timeout=60, capture_output=True)
         t0 = time.time()

@@ -28,7 +28,7 @@ def test_fp8_wide_resnet_tracks_bf16(gpu, monkeypatch, mx):
     from parameter_server_distributed_amd.models.resnet import ResNet
     from parameter_server_distributed_amd.ops import conv as conv_ops
 
-    monkeypatch.setenv("PSD_FP8_MX", "1" if mx else "0")
+    monkeypatch.setenv("PSD_FEATURES", f"fp8_mx={int(mx)}")
 
     # a short Wide-ResNet (width_per_group 128, two blocks per stage): stages 2-4 have fp8 shapes;
     # the same seed gives both models the same initial weights
@@ -85,8 +85,7 @@ def test_bn_apply_writes_the_consumers_fp8_input(gpu, monkeypatch):
     from parameter_server_distributed_amd.ops.bn import FusedBatchNorm2d
     from parameter_server_distributed_amd.ops.conv import Conv1x1, DelayedScale
 
-    monkeypatch.setenv("PSD_FP8_HANDOVER", "1")
-    monkeypatch.setenv("PSD_FP8_MX", "0")  # (the per-tensor delayed-scaling hand-over)
+    monkeypatch.setenv("PSD_FEATURES", "fp8_handover=1,fp8_mx=0")  # (the per-tensor delayed-scaling hand-over)
     torch.manual_seed(2)
     bn = FusedBatchNorm2d(256, relu=True).to(gpu)
     bn.weight.data = bn.weight.data.to(torch.bfloat16)
@@ -198,7 +197,7 @@ def test_fp8_wide_resnet_300_step_convergence(gpu, monkeypatch):
     from parameter_server_distributed_amd.models.resnet import ResNet
     from parameter_server_distributed_amd.ops import conv as conv_ops
 
-    monkeypatch.setenv("PSD_FP8_MX", "1")
+    monkeypatch.setenv("PSD_FEATURES", "fp8_mx=1")
     g = torch.Generator().manual_seed(1)
     batches = [(torch.randn(64, 3, 64, 64, generator=g).to(gpu, torch.bfloat16).contiguous(memory_format=torch.channels_last),
                 torch.randint(0, 100, (64,), generator=g).to(gpu)) for _ in range(8)]

@@ -293,7 +293,7 @@ def test_gemm_gelu_bwd_epilogue_matches_unfused(gpu, b_k, shape):
 
 def test_ffn_gelu_handover_matches_unfused(gpu, monkeypatch):
     """BERT FFN pair with ffn2.psd_gelu_input_from(ffn1): ffn2's bwd-data GEMM returns d(pre) and
-    ffn1's bias gradient; every gradient equals the unfused path (PSD_GELU_FUSE=0) and an fp32 reference."""
+    ffn1's bias gradient; every gradient equals the unfused path (feature gelu_fuse off) and an fp32 reference."""
     from parameter_server_distributed_amd.ops import linear as L
 
     torch.manual_seed(1)
@@ -313,7 +313,7 @@ def test_ffn_gelu_handover_matches_unfused(gpu, monkeypatch):
     monkeypatch.setattr(L, "_gelu_dgrad", counted)
 
     def run(fuse):
-        monkeypatch.setenv("PSD_GELU_FUSE", "1" if fuse else "0")
+        monkeypatch.setenv("PSD_FEATURES", f"gelu_fuse={int(fuse)}")
         for p in list(f1.parameters()) + list(f2.parameters()):
             p.grad = None
         x = x0.clone().requires_grad_(True)

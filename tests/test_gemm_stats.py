@@ -136,14 +136,14 @@ def test_module_route_with_gemm_stats_matches_fp32(gpu, monkeypatch, k, cin, cou
 
 def test_fp8_conv_bn_stats_handover_matches_reduce(gpu, monkeypatch):
     """An fp8 Conv1x1 + BN with the statistics from the fp8 GEMM epilogue vs the same with the BN's
-    own reduce pass (PSD_GEMM_STATS=0): identical conv output, so BN output and running stats agree
+    own reduce pass (feature gemm_stats off): identical conv output, so BN output and running stats agree
     to fp32 summation order."""
     from parameter_server_distributed_amd.ops.bn import FusedBatchNorm2d
     from parameter_server_distributed_amd.ops.conv import Conv1x1
 
     res = []
     for on in ("1", "0"):
-        monkeypatch.setenv("PSD_GEMM_STATS", on)
+        monkeypatch.setenv("PSD_FEATURES", f"gemm_stats={on}")
         torch.manual_seed(5)
         conv = Conv1x1(256, 512, fp8=True).to(gpu, torch.bfloat16).to(memory_format=CL)
         bn = FusedBatchNorm2d(512, relu=True).to(gpu)

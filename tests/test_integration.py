@@ -98,7 +98,7 @@ def test_worker_death_shrinks_barrier(cluster_factory):
                         ps_args=("--optimizer", "momentum", "--lr", "0.05"))
     w0 = c.worker(0, 6)
     w1 = c.worker(1, 6)
-    w2 = c.worker(2, 6, env=_env(PSD_FAULT_EXIT_AFTER_PUSH=2))
+    w2 = c.worker(2, 6, env=_env(PSD_FAULT="exit_after_push=2"))
     assert w2.wait(timeout=60) == 3  # fault injection exit code
     assert w0.wait(timeout=120) == 0, c.log("worker0.log")
     assert w1.wait(timeout=120) == 0, c.log("worker1.log")

@@ -67,7 +67,7 @@ def test_rccl_transport_graph_capture_matches_local(gpu, monkeypatch):
     from parameter_server_distributed_amd.parallel.transport import LocalTransport, RcclTransport
     from parameter_server_distributed_amd.runtime.trainer import Trainer
 
-    monkeypatch.setenv("PSD_LINEAR_TUNE", "0")  # same GEMM kernels in both runs
+    monkeypatch.setenv("PSD_FEATURES", "linear_tune=0")  # same GEMM kernels in both runs
     out = []
     for t in (LocalTransport(), RcclTransport(0, 1, gpu.index or 0, store=dist.HashStore())):
         torch.manual_seed(0)

@@ -168,7 +168,7 @@ def test_resnet_tail_matches_unfused(gpu, monkeypatch):
     x, y = spec.make_batch(8, gpu, seed=3)
 
     def run(tail_on: bool, fp32: bool = False, keep=None):
-        monkeypatch.setenv("PSD_TAIL_RECOMPUTE", "1" if tail_on else "0")
+        monkeypatch.setenv("PSD_FEATURES", f"tail_recompute={int(tail_on)}")
         autotune._DECISIONS.clear()
         autotune._DECISIONS.update(keep or {})
         for k in tail.TAIL_CALLS:
@@ -250,7 +250,7 @@ def test_tail_recompute_fallback_matches_unfused(gpu, monkeypatch):
     (y32 * r.float()).sum().backward()
     ref = [y32.detach(), x32.grad, i32.grad, w32.grad, g32.grad, b32.grad, rm, rv]
     for on in (True, False):
-        monkeypatch.setenv("PSD_TAIL_RECOMPUTE", "1" if on else "0")
+        monkeypatch.setenv("PSD_FEATURES", f"tail_recompute={int(on)}")
         autotune._DECISIONS.clear()
         for k in tail.TAIL_CALLS:
             tail.TAIL_CALLS[k] = 0
@@ -308,7 +308,7 @@ def test_tail_statistics_match_fp64(gpu, monkeypatch):
         caps.append((a2.detach().clone(), conv.weight.detach().clone()))
         return orig(conv, bn, a2, idt, resid_to)
 
-    monkeypatch.setenv("PSD_TAIL_RECOMPUTE", "1")
+    monkeypatch.setenv("PSD_FEATURES", "tail_recompute=1")
     monkeypatch.setattr(R, "conv_bn_tail", cap)
     autotune._DECISIONS.clear()
     spec.loss(spec.model(x), y).backward()

@@ -45,9 +45,9 @@ def main():
     grads(models["fp8"], x, y)
     ref2 = grads(models["bf16"], x, y)  # bf16 run-to-run (library nondeterminism)
     runs = {"bf16-again": ref2}
-    os.environ["PSD_FP8_DGRAD"] = "0"
+    os.environ["PSD_FEATURES"] = "fp8_dgrad=0"
     runs["fp8-fwd"] = grads(models["fp8"], x, y)
-    os.environ["PSD_FP8_DGRAD"] = "1"
+    os.environ["PSD_FEATURES"] = "fp8_dgrad=1"
     runs["fp8-fwd+dgrad"] = grads(models["fp8"], x, y)
     for name, gr in runs.items():
         num = sum(float((gr[n] - ref[n]).pow(2).sum()) for n in ref)

@@ -45,7 +45,7 @@ def one(batch, img, lo, hi):
     spread = max(abs(v - ref) for v in noisy) / ref
 
     def run(tail_on):
-        os.environ["PSD_TAIL_RECOMPUTE"] = "1" if tail_on else "0"
+        os.environ["PSD_FEATURES"] = f"tail_recompute={int(tail_on)}"
         m = spec.model
         m.load_state_dict(init)
         m.zero_grad(set_to_none=True)

@@ -50,7 +50,7 @@ def main():
 
     R.conv_bn_tail = cap
     import os
-    os.environ["PSD_TAIL_RECOMPUTE"] = "1"
+    os.environ["PSD_FEATURES"] = "tail_recompute=1"
     spec.model.load_state_dict(init)
     spec.loss(spec.model(x), y).backward()
     R.conv_bn_tail = orig
@@ -102,7 +102,7 @@ def main():
     print("worst relative variance error:", worst)
 
     def run(tail_on, fp32=False, stats=None):
-        os.environ["PSD_TAIL_RECOMPUTE"] = "1" if tail_on else "0"
+        os.environ["PSD_FEATURES"] = f"tail_recompute={int(tail_on)}"
         for key in list(autotune._DECISIONS):
             if key[:2] == ("tail", "stats"):
                 del autotune._DECISIONS[key]
