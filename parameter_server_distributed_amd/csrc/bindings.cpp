@@ -120,6 +120,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bnfold_rowdot", &bnfold_rowdot, py::arg("P"), py::arg("w"), py::arg("row"));
   m.def("bnfold_gram_stats", &bnfold_gram_stats, py::arg("P"), py::arg("w"), py::arg("shift"), py::arg("M"),
         py::arg("row"));
+  m.def("bnfold_dual_weights", &bnfold_dual_weights, py::arg("w3"), py::arg("wd"), py::arg("ss3"), py::arg("ssd"));
   m.def("bn_finalize", &bn_finalize, py::arg("part"), py::arg("rows"), py::arg("M"), py::arg("gamma"),
         py::arg("beta"), py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"), py::arg("eps"),
         py::arg("counter") = py::none());

@@ -812,6 +812,29 @@ void bnfold_gram_stats(const at::Tensor& P, const at::Tensor& w_in, const at::Te
   TORCH_CHECK(e == hipSuccess, "psd bnfold gram stats: ", hipGetErrorString(e));
 }
 
+// The dual tail's apply operands from both convolutions' weights and both BNs' scale/shift
+// (kernels/bnfold.hip bnfold_dual_weights_kernel): {wcat [Cout, C3 + Cd] bf16, ss [2 Cout] fp32}
+std::vector<at::Tensor> bnfold_dual_weights(const at::Tensor& w3_in, const at::Tensor& wd_in, const at::Tensor& ss3,
+                                            const at::Tensor& ssd) {
+  const c10::DeviceGuard dg(w3_in.device());
+  const at::Tensor w3 = fold_w2d(w3_in), wd = fold_w2d(wd_in);
+  const int64_t Cout = w3.size(0), C3 = w3.size(1), Cd = wd.size(1);
+  TORCH_CHECK(wd.size(0) == Cout && w3.scalar_type() == at::kBFloat16 && wd.scalar_type() == at::kBFloat16,
+              "psd bnfold dual weights: bf16 weights with one Cout");
+  for (const at::Tensor* t : {&ss3, &ssd})
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == 2 * Cout && t->device() == w3.device(),
+                "psd bnfold dual weights: ss must be fp32 [2 Cout]");
+  at::Tensor wcat = at::empty({Cout, C3 + Cd}, w3.options());
+  at::Tensor ss = at::empty({2 * Cout}, ss3.options());
+  hipError_t e = launch_bnfold_dual_weights(reinterpret_cast<const uint16_t*>(w3.data_ptr()),
+                                            reinterpret_cast<const uint16_t*>(wd.data_ptr()), ss3.data_ptr<float>(),
+                                            ssd.data_ptr<float>(), (int)Cout, (int)C3, (int)Cd,
+                                            reinterpret_cast<uint16_t*>(wcat.data_ptr()), ss.data_ptr<float>(),
+                                            stream_of(w3));
+  TORCH_CHECK(e == hipSuccess, "psd bnfold dual weights: ", hipGetErrorString(e));
+  return {wcat, ss};
+}
+
 // Training-mode BN statistics from producer partials only (no activation is read): returns
 // {mean, invstd, ss [2C]} and updates the running statistics, as bn_fwd with stats_only.
 std::vector<at::Tensor> bn_finalize(const at::Tensor& part, int64_t rows, int64_t M, const at::Tensor& gamma,

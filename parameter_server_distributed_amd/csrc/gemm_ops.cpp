@@ -368,11 +368,12 @@ int64_t convn_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_
     TORCH_CHECK(!stats && apply_ss->scalar_type() == at::kFloat && apply_ss->numel() == 2 * Cout &&
                     apply_ss->is_contiguous() && apply_ss->device() == x.device(),
                 "psd convn: apply_ss must be fp32 [2 Cout] (no statistics in an apply pass)");
-    TORCH_CHECK(apply_res.has_value() && apply_res->defined() && apply_res->scalar_type() == at::kBFloat16 &&
-                    apply_res->numel() == M * Cout && apply_res->device() == x.device() &&
-                    (apply_res->dim() == 4 ? apply_res->is_contiguous(at::MemoryFormat::ChannelsLast)
-                                           : apply_res->is_contiguous()),
-                "psd convn: apply_res must be a bf16 [M, Cout] (or channels_last) residual");
+    TORCH_CHECK(!(apply_res.has_value() && apply_res->defined()) ||
+                    (apply_res->scalar_type() == at::kBFloat16 && apply_res->numel() == M * Cout &&
+                     apply_res->device() == x.device() &&
+                     (apply_res->dim() == 4 ? apply_res->is_contiguous(at::MemoryFormat::ChannelsLast)
+                                            : apply_res->is_contiguous())),
+                "psd convn: apply_res must be a bf16 [M, Cout] (or channels_last) residual, or None");
     TORCH_CHECK(apply_mask.has_value() && apply_mask->defined() && apply_mask->scalar_type() == at::kByte &&
                     apply_mask->numel() == M * Cout / 8 && apply_mask->is_contiguous(),
                 "psd convn: apply_mask must be uint8 [M * Cout / 8]");
@@ -406,7 +407,8 @@ int64_t convn_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_
   if (apply) {
     a.bwd = 8;
     a.bss = apply_ss->data_ptr<float>();
-    a.ares = reinterpret_cast<const uint16_t*>(apply_res->data_ptr());
+    a.ares = (apply_res.has_value() && apply_res->defined()) ? reinterpret_cast<const uint16_t*>(apply_res->data_ptr())
+                                                             : nullptr;
     a.amask = apply_mask->data_ptr<uint8_t>();
   }
   a.xbytes = (uint32_t)xbytes;

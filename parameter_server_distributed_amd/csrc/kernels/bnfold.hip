@@ -185,6 +185,41 @@ __global__ __launch_bounds__(256) void bnfold_gram_stats_kernel(const float* __r
   }
 }
 
+// The dual tail's apply operands (ops/tail.py _DualTailFn): per output channel c the branch with the
+// larger |BN scale| keeps its bf16 weights, the other's are scaled by the ratio of the scales (fp32
+// product, one rounding); ss = [s_big | t3 + td]. One workgroup per 4 channels, one wave each.
+__global__ __launch_bounds__(256) void bnfold_dual_weights_kernel(const uint16_t* __restrict__ W3,
+                                                                  const uint16_t* __restrict__ Wd,
+                                                                  const float* __restrict__ ss3,
+                                                                  const float* __restrict__ ssd, int Cout, int C3, int Cd,
+                                                                  uint16_t* __restrict__ wcat, float* __restrict__ ss) {
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (c >= Cout) return;
+  const float s3 = ss3[c], sd = ssd[c];
+  const bool big3 = fabsf(s3) >= fabsf(sd);
+  const float sb = big3 ? s3 : sd;
+  float r3 = big3 ? 1.f : (sb != 0.f ? s3 / sb : 0.f);
+  float rd = big3 ? (sb != 0.f ? sd / sb : 0.f) : 1.f;
+  if (sb == 0.f) r3 = rd = 0.f;
+  const int K = C3 + Cd;
+  for (int k = lane; k < K; k += 64) {
+    const float v = k < C3 ? bf16_to_f32(W3[(int64_t)c * C3 + k]) * r3 : bf16_to_f32(Wd[(int64_t)c * Cd + k - C3]) * rd;
+    wcat[(int64_t)c * K + k] = f32_to_bf16(v);
+  }
+  if (lane == 0) {
+    ss[c] = sb;
+    ss[Cout + c] = ss3[Cout + c] + ssd[Cout + c];
+  }
+}
+
+hipError_t launch_bnfold_dual_weights(const uint16_t* W3, const uint16_t* Wd, const float* ss3, const float* ssd,
+                                      int Cout, int C3, int Cd, uint16_t* wcat, float* ss, hipStream_t st) {
+  if (Cout <= 0 || C3 <= 0 || Cd <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bnfold_dual_weights_kernel, dim3((Cout + 3) / 4), dim3(256), 0, st, W3, Wd, ss3, ssd, Cout, C3, Cd,
+                     wcat, ss);
+  return hipGetLastError();
+}
+
 hipError_t launch_bnfold_gram_stats(const float* P, const uint16_t* W, const float* shift, int Cout, int Wd, int64_t M,
                                     float* row, hipStream_t st) {
   if (Cout <= 0 || Cout % kGsCh != 0 || M <= 0) return hipErrorInvalidValue;

@@ -359,7 +359,7 @@ __device__ __forceinline__ void convn_epilogue(const ConvnArgs& a, f32x4 (&acc)[
       mm[i][ps] = m;
       if constexpr (APPLY) {
         rv4[i][ps] = u32x4{0u, 0u, 0u, 0u};
-        if (m >= 0) rv4[i][ps] = *reinterpret_cast<const u32x4*>(a.ares + (int64_t)m * a.N + my_col);
+        if (m >= 0 && a.ares) rv4[i][ps] = *reinterpret_cast<const u32x4*>(a.ares + (int64_t)m * a.N + my_col);
       }
       if constexpr (BRED) {
         exr[i][ps] = rv4[i][ps] = dv4[i][ps] = u32x4{0u, 0u, 0u, 0u};
@@ -1267,7 +1267,7 @@ hipError_t launch_convn(const ConvnArgs& a_in, hipStream_t st) {
                   a.wbytes > 0 && a.variant < convn_variant_count(bn) &&
                   (a.y || (a.bwd == 0 && a.part)) &&
                   (a.bwd == 0 ? (!a.part || a.shift)
-                   : a.bwd == 8 ? (!a.part && a.bss && a.ares && a.amask && a.ldc == a.N && a.N % 8 == 0)
+                   : a.bwd == 8 ? (!a.part && a.bss && a.amask && a.ldc == a.N && a.N % 8 == 0)
                               : (a.part && (a.bx || a.bwd >= 2) && a.bmean && a.ldc == a.N &&
                                  (a.bwd == 1 ? a.bss != nullptr
                                              : ((a.bwd == 2 || a.bwd == 3 || a.bwd == 5) && a.bdr && a.bmbits &&

@@ -128,6 +128,9 @@ hipError_t launch_bn_elemt_coef(const uint16_t* g, const uint16_t* x, const floa
                                 hipStream_t stream);
 hipError_t launch_bnfold_gram_stats(const float* P, const uint16_t* W, const float* shift, int Cout, int Wd, int64_t M,
                                     float* row, hipStream_t st);
+// dual tail apply operands: wcat [Cout, C3 + Cd] bf16 and ss [2 Cout] fp32 (ops/tail.py)
+hipError_t launch_bnfold_dual_weights(const uint16_t* W3, const uint16_t* Wd, const float* ss3, const float* ssd,
+                                      int Cout, int C3, int Cd, uint16_t* wcat, float* ss, hipStream_t st);
 hipError_t launch_bnfold_rowdot(const float* P, const uint16_t* W, int Cout, int Wd, float* row, hipStream_t st);
 hipError_t launch_bnfold_prep(const uint16_t* W, const float* coef, int Cout, int Wd, uint16_t* w2, int ldw,
                               uint16_t* bw, float* bvec, hipStream_t stream);

@@ -50,6 +50,8 @@ std::vector<at::Tensor> bnfold_dgrad_weights(const at::Tensor& w, const at::Tens
 void bnfold_combine(const at::Tensor& P, const at::Tensor& w, const at::Tensor& coef, at::Tensor out, bool accumulate);
 void bnfold_rowdot(const at::Tensor& P, const at::Tensor& w, at::Tensor row);
 void bnfold_gram_stats(const at::Tensor& P, const at::Tensor& w, const at::Tensor& shift, int64_t M, at::Tensor row);
+std::vector<at::Tensor> bnfold_dual_weights(const at::Tensor& w3, const at::Tensor& wd, const at::Tensor& ss3,
+                                            const at::Tensor& ssd);
 std::vector<at::Tensor> bn_finalize(const at::Tensor& part, int64_t rows, int64_t M, const at::Tensor& gamma,
                                     const at::Tensor& beta, at::Tensor running_mean, at::Tensor running_var,
                                     double momentum, double eps, c10::optional<at::Tensor> counter);

@@ -20,7 +20,7 @@ import torch.nn as nn
 from ..ops.bn import FusedBatchNorm2d, bn_add_bn_relu
 from ..ops.conv import Conv1x1, ConvNHWC, stem_forward
 from ..ops.pool import MaxPool3x3s2, global_avg_pool
-from ..ops.tail import conv_bn_tail, tail_ok
+from ..ops.tail import conv_bn_dual_tail, conv_bn_tail, dual_tail_ok, tail_ok
 
 
 class _Fork(torch.autograd.Function):
@@ -115,7 +115,12 @@ class Bottleneck(nn.Module):
             to = prev_bn if forked and isinstance(prev_bn, FusedBatchNorm2d) else None
             # conv1's bwd-data may then run prev_bn's backward reduction with that gradient added
             object.__setattr__(self.conv1, "_psd_bn_in", to if self.fuse_residual_grad else None)
-            y3 = self.conv3(self.bn2(self.conv2(self.bn1(self.conv1(xm)))))
+            a2 = self.bn2(self.conv2(self.bn1(self.conv1(xm))))
+            if dual_tail_ok(self.conv3, self.bn3, a2, self.downsample[0], self.downsample[1], xd):
+                # stride-1 downsample (layer 1): neither conv3's nor the downsample conv's output is
+                # stored -- Gram statistics, one K-concatenated apply GEMM (ops/tail.py)
+                return conv_bn_dual_tail(self.conv3, self.bn3, a2, self.downsample[0], self.downsample[1], xd)
+            y3 = self.conv3(a2)
             object.__setattr__(self.downsample[0], "_psd_strided_to", to)
             r = self.downsample[0](xd)
             return bn_add_bn_relu(self.bn3, y3, self.downsample[1], r)

@@ -33,6 +33,8 @@ bottleneck tail ResNet-50 training needs.
 """
 from __future__ import annotations
 
+import types
+
 import torch
 
 from ..utils.config import feature as _feat
@@ -40,9 +42,10 @@ from . import autotune as _at
 from .conv import (Conv1x1, _fold_backward, _from_2d, _fwd_records, _native, _part_rows, _sink_view, fold_ok)
 from .bn import FusedBatchNorm2d, take_dr
 
-__all__ = ["tail_ok", "conv_bn_tail", "TAIL_CALLS"]
+__all__ = ["tail_ok", "conv_bn_tail", "dual_tail_ok", "conv_bn_dual_tail", "TAIL_CALLS"]
 
-TAIL_CALLS = {"fwd": 0, "bwd_fused": 0, "bwd_recompute": 0}
+TAIL_CALLS = {"fwd": 0, "bwd_fused": 0, "bwd_recompute": 0, "dual_fwd": 0, "dual_bwd_fused": 0,
+              "dual_bwd_recompute": 0}
 
 
 def tail_ok(conv, bn, a2: torch.Tensor, idt: torch.Tensor) -> bool:
@@ -67,16 +70,15 @@ def tail_ok(conv, bn, a2: torch.Tensor, idt: torch.Tensor) -> bool:
 
 
 def _variant(a2, w2, M: int, cin: int, cout: int, h: int, w: int, shift) -> int:
-    """Narrow-kernel tile variant of the two tail passes (timed together on scratch buffers: the
-    statistics pass, then the apply pass with placeholder coefficients)."""
+    """Narrow-kernel tile variant of the tail's apply pass (timed on scratch buffers with placeholder
+    coefficients). Only the apply pass is timed: the statistics route is chosen on its own
+    (_stats_route), and with the Gram route -- the usual winner -- no statistics pass of this
+    variant runs at all (timing both passes together picked a slower apply variant)."""
     C = _native()
     dev = a2.device
 
     def make(v):
         def fn():
-            part = torch.empty(_part_rows(M, cout, v, h, w, 1), 2, cout, device=dev, dtype=torch.float32)
-            if C.convn_(a2, w2, part, 1, 1, 1, 0, part=part, shift=shift, variant=v, no_store=True) == 0:
-                raise _at.Declined("convn statistics-only pass")
             out = torch.empty(M, cout, device=dev, dtype=torch.bfloat16)
             ss = torch.zeros(2 * cout, device=dev, dtype=torch.float32)
             mb = torch.empty(M * cout // 8, device=dev, dtype=torch.uint8)
@@ -87,7 +89,7 @@ def _variant(a2, w2, M: int, cin: int, cout: int, h: int, w: int, shift) -> int:
 
     cands = {f"psdn{v}": make(v) for v in range(C.convn_variants(cout))
              if C.convn_variant_kind(cout, v) in (0, 3) and C.convn_variant_ok(cout, v, 1, 1, 1, 0, w)}
-    how = _at.choose(("tail", "conv1x1_bn_res_relu", M, cin, cout), cands, next(iter(cands)))
+    how = _at.choose(("tail", "apply", M, cin, cout), cands, next(iter(cands)))
     return int(how[4:])
 
 
@@ -225,3 +227,203 @@ def conv_bn_tail(conv, bn, a2: torch.Tensor, idt: torch.Tensor, resid_to=None) -
     """``relu(bn(conv(a2)) + idt)`` with conv's output never stored (see module docstring).
     ``resid_to``: the fused BN that produced ``idt`` (the residual gradient is handed to it)."""
     return _TailFn.apply(a2, conv.weight, bn.weight, bn.bias, idt, conv, bn, resid_to)
+
+
+# ---------------------------------------------------------------------------------------------
+# Downsample blocks: relu(bn3(conv3(a2)) + bnd(convd(x))) with NEITHER convolution output stored.
+#
+# The unfused dual tail writes y3 = conv3(a2) and yd = convd(x) (two 4x-wide activations: 1.6 GB
+# each at ResNet-50 b1024 layer 1), then one apply pass reads both and writes the block output. Here
+# (stride-1 downsample convolutions, i.e. layer 1's first block):
+#   forward   1. the two BNs' statistics from the Gram matrices of a2 and x (sum y = W s,
+#              sum y^2 = W^T G W: one read of each 64-wide input, the GEMMs are not recomputed)
+#             2. both BN finalizes
+#             3. ONE apply GEMM on the narrow kernel with the K-concatenated operand [a2 | x] and the
+#                weights [r3 o W3 | rd o Wd] (per channel the branch with the larger BN scale keeps
+#                its weights, the other is scaled by the ratio of the scales): out = relu(s_big . +
+#                t3 + td) and its ReLU bit-mask -- y3 and yd never reach HBM
+#   backward  as the folded dual tail (ops/bn.py _BNAddBNReluFn "pair" path): the consumer's
+#             bwd-data epilogue reduces sum g; sum g y3 / sum g yd come from the fold wgrads' g^T a2 /
+#             g^T x (rowdot); both BNs' input gradients are folded into their convolutions' backward.
+#             Without that fused consumer, y3 and yd are recomputed once for the ordinary dual BN
+#             backward.
+# The ratio-scaled weights are rounded once to bf16 (a K-concatenated GEMM has one accumulator, so
+# the per-channel scales of the two BNs cannot both be applied in the epilogue).
+
+
+def dual_tail_ok(conv3, bn3, a2: torch.Tensor, convd, bnd, xin: torch.Tensor) -> bool:
+    """The recomputing dual tail applies: bf16 Conv1x1 conv3 and a stride-1 Conv1x1 downsample into
+    training FusedBatchNorm2d bn3 (ReLU) / bnd (no ReLU), channels_last inputs of one spatial shape,
+    shapes the fold, the Gram statistics and the K-concatenated narrow kernel take."""
+    if not (_feat("tail_recompute") and _feat("dual_recompute") and _feat("convn") and _feat("bn_fold")):
+        return False
+    if not (isinstance(conv3, Conv1x1) and isinstance(convd, Conv1x1)) or conv3.fp8 or convd.fp8:
+        return False
+    if not (isinstance(bn3, FusedBatchNorm2d) and isinstance(bnd, FusedBatchNorm2d) and bn3.relu and not bnd.relu
+            and bn3.training and bnd.training and bn3.weight is not None and bnd.weight is not None):
+        return False
+    if getattr(bn3, "_psd_q8_consumer", None) is not None or not torch.is_grad_enabled():
+        return False
+    for t in (a2, xin):
+        if not (t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 4
+                and t.is_contiguous(memory_format=torch.channels_last)):
+            return False
+    if a2.shape[0] != xin.shape[0] or a2.shape[2:] != xin.shape[2:]:
+        return False
+    if conv3.weight.dtype != torch.bfloat16 or convd.weight.dtype != torch.bfloat16:
+        return False
+    c3, cd, cout = conv3.in_channels, convd.in_channels, conv3.out_channels
+    if convd.out_channels != cout or a2.shape[1] != c3 or xin.shape[1] != cd or cout % 4:
+        return False
+    C = _native()
+    if not (fold_ok(c3, cout) and fold_ok(cd, cout) and C.convw_gram_rows(c3) > 0 and C.convw_gram_rows(cd) > 0):
+        return False
+    n, _, h, w = a2.shape
+    return (n * h * w) % 8 == 0 and any(_dual_variants(cout, w))
+
+
+def _dual_variants(cout: int, w: int) -> list:
+    C = _native()
+    return [v for v in range(C.convn_variants(cout))
+            if C.convn_variant_kind(cout, v) in (0, 3) and C.convn_variant_ok(cout, v, 1, 1, 1, 0, w, True)]
+
+
+def _gram_moments(x, w2, shift, M: int) -> torch.Tensor:
+    """[1, 2, Cout] shifted moments of y = x w2^T from x's Gram matrix (kernels/bnfold.hip)."""
+    C = _native()
+    cin = x.shape[1]
+    P = torch.empty(C.convw_gram_rows(cin), cin, device=x.device, dtype=torch.float32)
+    if not C.convw_gram_(x, P):
+        raise RuntimeError("psd dual tail: convw declined the Gram launch")
+    part = torch.empty(1, 2, w2.shape[0], device=x.device, dtype=torch.float32)
+    C.bnfold_gram_stats(P, w2, shift, M, part[0])
+    return part
+
+
+def _finalize(bn, part, M: int):
+    return _native().bn_finalize(part, 1, M, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                 bn.momentum if bn.momentum is not None else 0.1, bn.eps, bn.num_batches_tracked)
+
+
+class _DualTailFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a2, w3, g3, b3, xin, wd, gd, bd, conv3, bn3, convd, bnd):
+        C = _native()
+        n, c3, h, w = a2.shape
+        cd, cout = xin.shape[1], w3.shape[0]
+        M = n * h * w
+        w3_2, wd_2 = w3.reshape(cout, c3).contiguous(), wd.reshape(cout, cd).contiguous()
+        mean3, invstd3, ss3 = _finalize(bn3, _gram_moments(a2, w3_2, bn3.running_mean, M), M)
+        mean_d, invstd_d, ss_d = _finalize(bnd, _gram_moments(xin, wd_2, bnd.running_mean, M), M)
+        # per output channel the branch with the larger BN scale keeps its bf16 weights exactly and
+        # the other one's are scaled by the ratio (|ratio| <= 1, fp32 product, one rounding); the
+        # epilogue applies the larger scale and the summed shift t3 + td:
+        #   out = s_big (a2 W3'^T + x Wd'^T) + t3 + td   (s3 = 0, e.g. zero-init gamma: W3' = 0)
+        s3, sd = ss3[:cout], ss_d[:cout]
+        big3 = s3.abs() >= sd.abs()
+        sbig = torch.where(big3, s3, sd)
+        safe = torch.where(sbig == 0, torch.ones_like(sbig), sbig)
+        r3 = torch.where(big3, torch.ones_like(s3), s3 / safe)
+        rd = torch.where(big3, sd / safe, torch.ones_like(sd))
+        r3 = torch.where(sbig == 0, torch.zeros_like(r3), r3)
+        rd = torch.where(sbig == 0, torch.zeros_like(rd), rd)
+        wcat = torch.cat([w3_2.float() * r3[:, None], wd_2.float() * rd[:, None]], 1).to(torch.bfloat16)
+        ssc = torch.cat([sbig, ss3[cout:] + ss_d[cout:]])
+        out = torch.empty(M, cout, device=a2.device, dtype=torch.bfloat16)
+        mbits = torch.empty(M * cout // 8, device=a2.device, dtype=torch.uint8)
+
+        def make(v):
+            def fn():
+                o = torch.empty(M, cout, device=a2.device, dtype=torch.bfloat16)
+                mb = torch.empty(M * cout // 8, device=a2.device, dtype=torch.uint8)
+                if C.convn_(a2, wcat, o, 1, 1, 1, 0, variant=v, x2=xin, apply_ss=ssc, apply_mask=mb) == 0:
+                    raise _at.Declined("convn dual apply pass")
+                return o
+            return fn
+
+        cands = {f"psdn{v}": make(v) for v in _dual_variants(cout, w)}
+        v = int(_at.choose(("tail", "dual_apply", M, c3, cd, cout), cands, next(iter(cands)))[4:])
+        if C.convn_(a2, wcat, out, 1, 1, 1, 0, variant=v, x2=xin, apply_ss=ssc, apply_mask=mbits) == 0:
+            raise RuntimeError("psd dual tail: convn declined the apply pass")
+        y = _from_2d(out, n, h, w)
+        # the consumer convolution's bwd-data epilogue reduces bn3's backward without its input
+        # (mode 2, bx None: sum g and -mean3 sum g); backward completes both BNs from the fold products
+        bn3._psd_fwd = (y, None, mean3, None, mbits, None, None)
+        ctx.r3, ctx.rd = types.SimpleNamespace(mod=conv3), types.SimpleNamespace(mod=convd)
+        _fwd_records(ctx.r3, conv3)
+        _fwd_records(ctx.rd, convd)
+        ctx.bn3, ctx.bnd, ctx.v = bn3, bnd, v
+        ctx.save_for_backward(a2, w3, g3, mean3, invstd3, xin, wd, gd, mean_d, invstd_d, mbits)
+        TAIL_CALLS["dual_fwd"] += 1
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        a2, w3, g3, mean3, invstd3, xin, wd, gd, mean_d, invstd_d, mbits = ctx.saved_tensors
+        C = _native()
+        bn3, bnd = ctx.bn3, ctx.bnd
+        bn3._psd_fwd = None
+
+        def sinks(m):
+            sink = getattr(m, "_psd_grad_sink", None)
+            return (sink(m.weight), sink(m.bias)) if sink is not None else (None, None)
+
+        dg3o, db3o = sinks(bn3)
+        dgdo, dbdo = sinks(bnd)
+        n, c3, h, w = a2.shape
+        cd, cout = xin.shape[1], w3.shape[0]
+        M = n * h * w
+        pre = getattr(bn3, "_psd_bwd_pre", None)
+        bn3._psd_bwd_pre = None
+        if pre is not None and not (len(pre) == 3 and pre[0].data_ptr() == dy.data_ptr() and pre[0].shape == dy.shape):
+            pre = None
+        need = ctx.needs_input_grad
+        if pre is not None:
+            g, part, rows = pre
+            if part.shape[0] <= rows:
+                raise RuntimeError("psd dual tail: the partials buffer has no row for sum g y")
+            Ps = []
+            for inp, cin in ((a2, c3), (xin, cd)):
+                P = torch.empty(C.convw_fold_rows(cout, cin), cin, device=g.device, dtype=torch.float32)
+                if not C.convw_(g, inp, P, 1, 1, 1, 0, fold=True):
+                    raise RuntimeError("psd dual tail: convw_ declined the fold wgrad")
+                Ps.append(P)
+            part_d = part.clone()
+            part_d[:rows, 1] = part[:rows, 0] * (-mean_d)
+            C.bnfold_rowdot(Ps[0], w3, part[rows])
+            C.bnfold_rowdot(Ps[1], wd, part_d[rows])
+            _, _, dg3, db3, dgd, dbd, coef, coef_d = C.bn_bwd_dual_pre(
+                g, g, g3, mean3, invstd3, part, part_d, rows + 1, g, gd, mean_d, invstd_d, dg3o, db3o, dgdo, dbdo,
+                fold=True, fold_d=True)
+            dxa, dw3, _ = _fold_backward(ctx.r3, (g, coef, None), a2, w3, need[0], need[1], P=Ps[0])
+            dxi, dwd, _ = _fold_backward(ctx.rd, (g, coef_d, None), xin, wd, need[4], need[5], P=Ps[1])
+            TAIL_CALLS["dual_bwd_fused"] += 1
+            return dxa, dw3, dg3, db3, dxi, dwd, dgd, dbd, None, None, None, None
+        # no fused consumer: recompute y3 and yd once, the ordinary dual BN backward (one reduce and
+        # one elementwise pass) and the two convolutions' backward
+        ys = []
+        for inp, wt, cin in ((a2, w3, c3), (xin, wd, cd)):
+            o = torch.empty(M, cout, device=dy.device, dtype=torch.bfloat16)
+            if C.convn_(inp, wt.reshape(cout, cin).contiguous(), o, 1, 1, 1, 0, variant=0) == 0:
+                raise RuntimeError("psd dual tail: convn declined the recompute")
+            ys.append(_from_2d(o, n, h, w))
+        dy2 = take_dr(bn3._psd_pending_dr.pop()) if getattr(bn3, "_psd_pending_dr", None) else None
+        dx3, dxd, dg3, db3, dgd, dbd = C.bn_bwd_dual(dy, ys[0], g3, mean3, invstd3, mbits, dy2, ys[1], gd, mean_d,
+                                                     invstd_d, dg3o, db3o, dgdo, dbdo)
+        conv_bwd = torch.ops.aten.convolution_backward
+        args = (None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1)
+        dxa, dw3, _ = conv_bwd(dx3, a2, w3, *args, [need[0], need[1], False])
+        dxi, dwd, _ = conv_bwd(dxd, xin, wd, *args, [need[4], need[5], False])
+        sv3, svd = _sink_view(ctx.r3.mod, w3), _sink_view(ctx.rd.mod, wd)
+        if dw3 is not None and sv3 is not None:
+            dw3 = sv3.copy_(dw3)
+        if dwd is not None and svd is not None:
+            dwd = svd.copy_(dwd)
+        TAIL_CALLS["dual_bwd_recompute"] += 1
+        return dxa, dw3, dg3, db3, dxi, dwd, dgd, dbd, None, None, None, None
+
+
+def conv_bn_dual_tail(conv3, bn3, a2: torch.Tensor, convd, bnd, xin: torch.Tensor) -> torch.Tensor:
+    """``relu(bn3(conv3(a2)) + bnd(convd(xin)))`` with neither convolution output stored (see above)."""
+    return _DualTailFn.apply(a2, conv3.weight, bn3.weight, bn3.bias, xin, convd.weight, bnd.weight, bnd.bias,
+                             conv3, bn3, convd, bnd)

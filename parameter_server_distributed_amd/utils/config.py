@@ -73,6 +73,7 @@ FEATURES: dict[str, tuple[bool, str]] = {
     "dual_nobx": (True, "downsample blocks' dual tail without the BN inputs in the consumer epilogue"),
     "tail_recompute": (True, "identity blocks' conv3 output recomputed instead of stored"),
     "tail_gram": (True, "the recomputing tail's statistics from the Gram matrix of conv3's input"),
+    "dual_recompute": (True, "stride-1 downsample blocks: neither conv3's nor the downsample conv's output stored"),
     # fp8 (Wide-ResNet-101-2)
     "fp8_compute": (True, "fp8 convolutions where the model asks for them"),
     "fp8_mx": (True, "MX block scales for every fp8 operand; off: per-tensor scales"),

@@ -197,6 +197,8 @@ def test_resnet_tail_matches_unfused(gpu, monkeypatch):
     # backward either fused (the next conv1's epilogue) or recomputed (no fused consumer)
     assert calls["fwd"] >= 10, calls
     assert calls["bwd_fused"] + calls["bwd_recompute"] == calls["fwd"] and calls["bwd_fused"] >= 9, calls
+    # layer 1's downsample block: the recomputing dual tail, its backward fused into block 2's conv1
+    assert calls["dual_fwd"] == 1 and calls["dual_bwd_fused"] == 1, calls
     # the loss: within the unfused run's distance from the fp32 run + 0.5 % (the
     # per-layer statistics themselves are pinned against fp64 by test_tail_statistics_match_fp64)
     print("loss fp32 %.4f tail %.4f unfused %.4f" % (ref32[0], on[0], off[0]))
@@ -269,7 +271,8 @@ def test_tail_recompute_fallback_matches_unfused(gpu, monkeypatch):
         res.append([t.float().clone() for t in (y, x.grad, i.grad, conv.weight.grad, bn.weight.grad, bn.bias.grad,
                                                  bn.running_mean, bn.running_var)])
         if on:
-            assert tail.TAIL_CALLS == {"fwd": 1, "bwd_fused": 0, "bwd_recompute": 1}, tail.TAIL_CALLS
+            calls = {k: v for k, v in tail.TAIL_CALLS.items() if not k.startswith("dual")}
+            assert calls == {"fwd": 1, "bwd_fused": 0, "bwd_recompute": 1}, tail.TAIL_CALLS
     autotune._DECISIONS.clear()
     names = ("y", "da2", "didt", "dW3", "dgamma", "dbeta", "running_mean", "running_var")
     for nm, a, b, f in zip(names, res[0], res[1], ref):
@@ -341,3 +344,72 @@ def test_tail_statistics_match_fp64(gpu, monkeypatch):
             dm = float(((m_k - mu).abs() / var.sqrt()).max())
             dv = float(((v_k - var).abs() / var).max())
             assert dm < 1e-5 and dv < 1e-5, (li, k, dm, dv)
+
+
+def test_dual_tail_fallback_matches_unfused_and_fp32(gpu, monkeypatch):
+    """The recomputing dual tail relu(bn3(conv3(a2)) + bnd(convd(x))) of a stride-1 downsample
+    block (ops/tail.py _DualTailFn) whose output has no fused consumer (a weighted sum): forward
+    output, running statistics and every gradient against an fp32 composite reference, within the
+    unfused path's error level (the dual tail scales the weights by the BN scales before its one
+    bf16 rounding; the unfused path rounds y3 / yd)."""
+    from parameter_server_distributed_amd.ops import autotune, tail
+    from parameter_server_distributed_amd.ops.bn import FusedBatchNorm2d, bn_add_bn_relu
+    from parameter_server_distributed_amd.ops.conv import Conv1x1
+
+    torch.manual_seed(5)
+    n, c3, cd, cout, h = 4, 64, 64, 256, 14
+    conv3 = Conv1x1(c3, cout).to(gpu).to(memory_format=torch.channels_last)
+    convd = Conv1x1(cd, cout).to(gpu).to(memory_format=torch.channels_last)
+    for cv in (conv3, convd):
+        cv.weight.data = cv.weight.data.bfloat16()
+    bn3 = FusedBatchNorm2d(cout, relu=True).to(gpu)
+    bnd = FusedBatchNorm2d(cout).to(gpu)
+    for bn in (bn3, bnd):
+        nn.init.uniform_(bn.weight, 0.5, 1.5)
+        nn.init.uniform_(bn.bias, -0.2, 0.2)
+        bn.weight.data, bn.bias.data = bn.weight.data.bfloat16(), bn.bias.data.bfloat16()
+    a2 = torch.randn(n, c3, h, h, device=gpu).relu().bfloat16().contiguous(memory_format=torch.channels_last)
+    xin = torch.randn(n, cd, h, h, device=gpu).relu().bfloat16().contiguous(memory_format=torch.channels_last)
+    r = torch.randn(n, cout, h, h, device=gpu).bfloat16()
+    params = (conv3.weight, convd.weight, bn3.weight, bn3.bias, bnd.weight, bnd.bias)
+
+    # fp32 composite reference
+    t = [p.detach().float().requires_grad_(True) for p in params]
+    a32, x32 = a2.float().requires_grad_(True), xin.float().requires_grad_(True)
+    rms = [torch.zeros(cout, device=gpu), torch.ones(cout, device=gpu), torch.zeros(cout, device=gpu),
+           torch.ones(cout, device=gpu)]
+    y32 = torch.relu(F.batch_norm(F.conv2d(a32, t[0]), rms[0], rms[1], t[2], t[3], True, 0.1, bn3.eps)
+                     + F.batch_norm(F.conv2d(x32, t[1]), rms[2], rms[3], t[4], t[5], True, 0.1, bnd.eps))
+    (y32 * r.float()).sum().backward()
+    ref = [y32.detach(), a32.grad, x32.grad] + [p.grad for p in t] + rms
+
+    res = []
+    for on in (True, False):
+        monkeypatch.setenv("PSD_FEATURES", f"dual_recompute={int(on)}")
+        autotune._DECISIONS.clear()
+        for k in tail.TAIL_CALLS:
+            tail.TAIL_CALLS[k] = 0
+        for p in params:
+            p.grad = None
+        for bn in (bn3, bnd):
+            bn.running_mean.zero_()
+            bn.running_var.fill_(1)
+        a = a2.clone().requires_grad_(True)
+        x = xin.clone().requires_grad_(True)
+        if on:
+            assert tail.dual_tail_ok(conv3, bn3, a, convd, bnd, x)
+            y = tail.conv_bn_dual_tail(conv3, bn3, a, convd, bnd, x)
+        else:
+            y = bn_add_bn_relu(bn3, conv3(a), bnd, convd(x))
+        (y.float() * r.float()).sum().backward()
+        res.append([y.float(), a.grad.float(), x.grad.float()] + [p.grad.float() for p in params]
+                   + [bn3.running_mean.clone(), bn3.running_var.clone(), bnd.running_mean.clone(),
+                      bnd.running_var.clone()])
+        if on:
+            assert tail.TAIL_CALLS["dual_fwd"] == 1 and tail.TAIL_CALLS["dual_bwd_recompute"] == 1, tail.TAIL_CALLS
+    autotune._DECISIONS.clear()
+    names = ("y", "da2", "dx", "dW3", "dWd", "dg3", "db3", "dgd", "dbd", "rm3", "rv3", "rmd", "rvd")
+    for nm, a, b, f in zip(names, res[0], res[1], ref):
+        e_on = ((a - f.float()).norm() / f.float().norm().clamp_min(1e-6)).item()
+        e_off = ((b - f.float()).norm() / f.float().norm().clamp_min(1e-6)).item()
+        assert e_on <= 1.5 * e_off + 1e-2, (nm, e_on, e_off)
