@@ -116,12 +116,12 @@ class Bottleneck(nn.Module):
             # conv1's bwd-data may then run prev_bn's backward reduction with that gradient added
             object.__setattr__(self.conv1, "_psd_bn_in", to if self.fuse_residual_grad else None)
             a2 = self.bn2(self.conv2(self.bn1(self.conv1(xm))))
+            object.__setattr__(self.downsample[0], "_psd_strided_to", to)
             if dual_tail_ok(self.conv3, self.bn3, a2, self.downsample[0], self.downsample[1], xd):
-                # stride-1 downsample (layer 1): neither conv3's nor the downsample conv's output is
-                # stored -- Gram statistics, one K-concatenated apply GEMM (ops/tail.py)
+                # 1x1 downsample of stride 1 or 2 (layers 1-2): neither conv3's nor the downsample
+                # conv's output is stored -- Gram statistics, one K-concatenated apply GEMM (ops/tail.py)
                 return conv_bn_dual_tail(self.conv3, self.bn3, a2, self.downsample[0], self.downsample[1], xd)
             y3 = self.conv3(a2)
-            object.__setattr__(self.downsample[0], "_psd_strided_to", to)
             r = self.downsample[0](xd)
             return bn_add_bn_relu(self.bn3, y3, self.downsample[1], r)
         idt = x if self.downsample is None else self.downsample(xd)

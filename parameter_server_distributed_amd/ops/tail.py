@@ -39,8 +39,9 @@ import torch
 
 from ..utils.config import feature as _feat
 from . import autotune as _at
-from .conv import (Conv1x1, _fold_backward, _from_2d, _fwd_records, _native, _part_rows, _sink_view, fold_ok)
-from .bn import FusedBatchNorm2d, take_dr
+from .conv import (Conv1x1, ConvNHWC, _fold_backward, _from_2d, _fwd_records, _native, _part_rows, _sink_view,
+                   fold_ok)
+from .bn import FusedBatchNorm2d, StridedDr, take_dr
 
 __all__ = ["tail_ok", "conv_bn_tail", "dual_tail_ok", "conv_bn_dual_tail", "TAIL_CALLS"]
 
@@ -234,7 +235,8 @@ def conv_bn_tail(conv, bn, a2: torch.Tensor, idt: torch.Tensor, resid_to=None) -
 #
 # The unfused dual tail writes y3 = conv3(a2) and yd = convd(x) (two 4x-wide activations: 1.6 GB
 # each at ResNet-50 b1024 layer 1), then one apply pass reads both and writes the block output. Here
-# (stride-1 downsample convolutions, i.e. layer 1's first block):
+# (1x1 downsample convolutions of stride 1 -- layer 1 -- or 2 -- layer 2, on the quarter grid of its
+# input; the Gram statistics take inputs of up to 256 channels):
 #   forward   1. the two BNs' statistics from the Gram matrices of a2 and x (sum y = W s,
 #              sum y^2 = W^T G W: one read of each 64-wide input, the GEMMs are not recomputed)
 #             2. both BN finalizes
@@ -257,7 +259,10 @@ def dual_tail_ok(conv3, bn3, a2: torch.Tensor, convd, bnd, xin: torch.Tensor) ->
     shapes the fold, the Gram statistics and the K-concatenated narrow kernel take."""
     if not (_feat("tail_recompute") and _feat("dual_recompute") and _feat("convn") and _feat("bn_fold")):
         return False
-    if not (isinstance(conv3, Conv1x1) and isinstance(convd, Conv1x1)) or conv3.fp8 or convd.fp8:
+    if not isinstance(conv3, Conv1x1) or conv3.fp8 or getattr(convd, "fp8", False):
+        return False
+    strided = _ds_stride(convd)
+    if strided is None:
         return False
     if not (isinstance(bn3, FusedBatchNorm2d) and isinstance(bnd, FusedBatchNorm2d) and bn3.relu and not bnd.relu
             and bn3.training and bnd.training and bn3.weight is not None and bnd.weight is not None):
@@ -268,7 +273,7 @@ def dual_tail_ok(conv3, bn3, a2: torch.Tensor, convd, bnd, xin: torch.Tensor) ->
         if not (t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 4
                 and t.is_contiguous(memory_format=torch.channels_last)):
             return False
-    if a2.shape[0] != xin.shape[0] or a2.shape[2:] != xin.shape[2:]:
+    if a2.shape[0] != xin.shape[0] or a2.shape[2] * strided != xin.shape[2] or a2.shape[3] * strided != xin.shape[3]:
         return False
     if conv3.weight.dtype != torch.bfloat16 or convd.weight.dtype != torch.bfloat16:
         return False
@@ -280,6 +285,17 @@ def dual_tail_ok(conv3, bn3, a2: torch.Tensor, convd, bnd, xin: torch.Tensor) ->
         return False
     n, _, h, w = a2.shape
     return (n * h * w) % 8 == 0 and any(_dual_variants(cout, w))
+
+
+def _ds_stride(convd):
+    """1 for a Conv1x1 downsample, 2 for a stride-2 1x1 ConvNHWC one (its input is subsampled to the
+    quarter grid first, the gradient handed back on the quarter grid), None otherwise."""
+    if isinstance(convd, Conv1x1):
+        return 1
+    if isinstance(convd, ConvNHWC) and convd.kernel_size == (1, 1) and convd.stride == (2, 2) \
+            and convd.padding == (0, 0) and convd.groups == 1:
+        return 2
+    return None
 
 
 def _dual_variants(cout: int, w: int) -> list:
@@ -307,8 +323,12 @@ def _finalize(bn, part, M: int):
 
 class _DualTailFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, a2, w3, g3, b3, xin, wd, gd, bd, conv3, bn3, convd, bnd):
+    def forward(ctx, a2, w3, g3, b3, xfull, wd, gd, bd, conv3, bn3, convd, bnd):
         C = _native()
+        ctx.full_hw = tuple(xfull.shape[2:])
+        ctx.stride = _ds_stride(convd)
+        # a stride-2 1x1 downsample is a stride-1 one on the quarter grid of its input
+        xin = xfull if ctx.stride == 1 else xfull[:, :, ::2, ::2].contiguous(memory_format=torch.channels_last)
         n, c3, h, w = a2.shape
         cd, cout = xin.shape[1], w3.shape[0]
         M = n * h * w
@@ -398,7 +418,7 @@ class _DualTailFn(torch.autograd.Function):
             dxa, dw3, _ = _fold_backward(ctx.r3, (g, coef, None), a2, w3, need[0], need[1], P=Ps[0])
             dxi, dwd, _ = _fold_backward(ctx.rd, (g, coef_d, None), xin, wd, need[4], need[5], P=Ps[1])
             TAIL_CALLS["dual_bwd_fused"] += 1
-            return dxa, dw3, dg3, db3, dxi, dwd, dgd, dbd, None, None, None, None
+            return dxa, dw3, dg3, db3, _DualTailFn._input_grad(ctx, dxi), dwd, dgd, dbd, None, None, None, None
         # no fused consumer: recompute y3 and yd once, the ordinary dual BN backward (one reduce and
         # one elementwise pass) and the two convolutions' backward
         ys = []
@@ -420,7 +440,25 @@ class _DualTailFn(torch.autograd.Function):
         if dwd is not None and svd is not None:
             dwd = svd.copy_(dwd)
         TAIL_CALLS["dual_bwd_recompute"] += 1
-        return dxa, dw3, dg3, db3, dxi, dwd, dgd, dbd, None, None, None, None
+        return dxa, dw3, dg3, db3, _DualTailFn._input_grad(ctx, dxi), dwd, dgd, dbd, None, None, None, None
+
+    @staticmethod
+    def _input_grad(ctx, dxi):
+        """The downsample branch's input gradient: as is for a stride-1 downsample; for a stride-2
+        one it lives on the quarter grid -- queued on the BN that produced the block input (the
+        consumer conv1's bwd-data epilogue adds it at even (h, w), kernels/convn.hip mode 5) with a
+        zero-stride marker returned to the block's _Fork, or materialised when nobody takes it."""
+        if dxi is None or ctx.stride == 1:
+            return dxi
+        H, W = ctx.full_hw
+        dr = StridedDr(dxi if dxi.is_contiguous(memory_format=torch.channels_last)
+                       else dxi.contiguous(memory_format=torch.channels_last), H, W)
+        to = ctx.rd.strided_to
+        if isinstance(to, FusedBatchNorm2d):
+            to._psd_pending_dr.append(dr)
+            n, c = dxi.shape[:2]
+            return torch.zeros((), device=dxi.device, dtype=dxi.dtype).expand(n, c, H, W)
+        return dr.full()
 
 
 def conv_bn_dual_tail(conv3, bn3, a2: torch.Tensor, convd, bnd, xin: torch.Tensor) -> torch.Tensor:

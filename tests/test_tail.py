@@ -346,20 +346,23 @@ def test_tail_statistics_match_fp64(gpu, monkeypatch):
             assert dm < 1e-5 and dv < 1e-5, (li, k, dm, dv)
 
 
-def test_dual_tail_fallback_matches_unfused_and_fp32(gpu, monkeypatch):
-    """The recomputing dual tail relu(bn3(conv3(a2)) + bnd(convd(x))) of a stride-1 downsample
-    block (ops/tail.py _DualTailFn) whose output has no fused consumer (a weighted sum): forward
-    output, running statistics and every gradient against an fp32 composite reference, within the
-    unfused path's error level (the dual tail scales the weights by the BN scales before its one
-    bf16 rounding; the unfused path rounds y3 / yd)."""
+@pytest.mark.parametrize("stride,c3,cd,cout", [(1, 64, 64, 256), (2, 128, 256, 512)])
+def test_dual_tail_fallback_matches_unfused_and_fp32(gpu, monkeypatch, stride, c3, cd, cout):
+    """The recomputing dual tail relu(bn3(conv3(a2)) + bnd(convd(x))) of a downsample block with a
+    stride-1 (layer 1) or stride-2 (layer 2: on the quarter grid) 1x1 downsample convolution
+    (ops/tail.py _DualTailFn) whose output has no fused consumer (a weighted sum): forward output,
+    running statistics and every gradient against an fp32 composite reference, within the unfused
+    path's error level (the dual tail ratio-scales one branch's weights before its one bf16
+    rounding; the unfused path rounds y3 / yd)."""
     from parameter_server_distributed_amd.ops import autotune, tail
     from parameter_server_distributed_amd.ops.bn import FusedBatchNorm2d, bn_add_bn_relu
-    from parameter_server_distributed_amd.ops.conv import Conv1x1
+    from parameter_server_distributed_amd.ops.conv import Conv1x1, ConvNHWC
 
     torch.manual_seed(5)
-    n, c3, cd, cout, h = 4, 64, 64, 256, 14
+    n, h = 4, 14
     conv3 = Conv1x1(c3, cout).to(gpu).to(memory_format=torch.channels_last)
-    convd = Conv1x1(cd, cout).to(gpu).to(memory_format=torch.channels_last)
+    convd = (Conv1x1(cd, cout) if stride == 1 else ConvNHWC(cd, cout, 1, 2)).to(gpu).to(
+        memory_format=torch.channels_last)
     for cv in (conv3, convd):
         cv.weight.data = cv.weight.data.bfloat16()
     bn3 = FusedBatchNorm2d(cout, relu=True).to(gpu)
@@ -369,7 +372,8 @@ def test_dual_tail_fallback_matches_unfused_and_fp32(gpu, monkeypatch):
         nn.init.uniform_(bn.bias, -0.2, 0.2)
         bn.weight.data, bn.bias.data = bn.weight.data.bfloat16(), bn.bias.data.bfloat16()
     a2 = torch.randn(n, c3, h, h, device=gpu).relu().bfloat16().contiguous(memory_format=torch.channels_last)
-    xin = torch.randn(n, cd, h, h, device=gpu).relu().bfloat16().contiguous(memory_format=torch.channels_last)
+    xin = torch.randn(n, cd, h * stride, h * stride, device=gpu).relu().bfloat16().contiguous(
+        memory_format=torch.channels_last)
     r = torch.randn(n, cout, h, h, device=gpu).bfloat16()
     params = (conv3.weight, convd.weight, bn3.weight, bn3.bias, bnd.weight, bnd.bias)
 
@@ -379,7 +383,8 @@ def test_dual_tail_fallback_matches_unfused_and_fp32(gpu, monkeypatch):
     rms = [torch.zeros(cout, device=gpu), torch.ones(cout, device=gpu), torch.zeros(cout, device=gpu),
            torch.ones(cout, device=gpu)]
     y32 = torch.relu(F.batch_norm(F.conv2d(a32, t[0]), rms[0], rms[1], t[2], t[3], True, 0.1, bn3.eps)
-                     + F.batch_norm(F.conv2d(x32, t[1]), rms[2], rms[3], t[4], t[5], True, 0.1, bnd.eps))
+                     + F.batch_norm(F.conv2d(x32, t[1], stride=stride), rms[2], rms[3], t[4], t[5], True, 0.1,
+                                    bnd.eps))
     (y32 * r.float()).sum().backward()
     ref = [y32.detach(), a32.grad, x32.grad] + [p.grad for p in t] + rms
 
