@@ -197,8 +197,8 @@ def test_resnet_tail_matches_unfused(gpu, monkeypatch):
     # backward either fused (the next conv1's epilogue) or recomputed (no fused consumer)
     assert calls["fwd"] >= 10, calls
     assert calls["bwd_fused"] + calls["bwd_recompute"] == calls["fwd"] and calls["bwd_fused"] >= 9, calls
-    # layer 1's downsample block: the recomputing dual tail, its backward fused into block 2's conv1
-    assert calls["dual_fwd"] == 1 and calls["dual_bwd_fused"] == 1, calls
+    # layers 1-2 downsample blocks: the recomputing dual tail, its backward fused into the next conv1
+    assert calls["dual_fwd"] == 2 and calls["dual_bwd_fused"] == 2, calls
     # the loss: within the unfused run's distance from the fp32 run + 0.5 % (the
     # per-layer statistics themselves are pinned against fp64 by test_tail_statistics_match_fp64)
     print("loss fp32 %.4f tail %.4f unfused %.4f" % (ref32[0], on[0], off[0]))
