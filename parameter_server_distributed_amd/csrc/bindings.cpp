@@ -155,6 +155,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("save_mean"), py::arg("save_invstd"), py::arg("ss"), py::arg("dgamma_out") = py::none(),
         py::arg("dbeta_out") = py::none());
   m.def("gap_bwd", &gap_bwd);
+  m.def("subsample2", &subsample2, py::arg("x"));
   m.attr("OPT_SGD") = (int)OPT_SGD;
   m.attr("OPT_MOMENTUM") = (int)OPT_MOMENTUM;
   m.attr("OPT_ADAM") = (int)OPT_ADAM;

@@ -721,6 +721,19 @@ at::Tensor gap_bwd(const at::Tensor& dy_in, int64_t H, int64_t W) {
   TORCH_CHECK(e == hipSuccess, "psd gap bwd: ", hipGetErrorString(e));
   return dx;
 }
+at::Tensor subsample2(const at::Tensor& x) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast) && x.size(1) % 8 == 0 && x.size(2) % 2 == 0 &&
+                  x.size(3) % 2 == 0,
+              "psd subsample2: channels_last bf16 [N, C, H, W], C % 8 == 0, H and W even");
+  const c10::DeviceGuard g(x.device());
+  at::Tensor y = at::empty({x.size(0), x.size(1), x.size(2) / 2, x.size(3) / 2},
+                           x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  hipError_t e = launch_subsample2(reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<uint16_t*>(y.data_ptr()),
+                                   (int)x.size(0), (int)x.size(2), (int)x.size(3), (int)x.size(1), stream_of(x));
+  TORCH_CHECK(e == hipSuccess, "psd subsample2: ", hipGetErrorString(e));
+  return y;
+}
 // ---- BN-backward fold of a 1x1 conv -> BN pair (kernels/bnfold.hip)
 
 namespace {

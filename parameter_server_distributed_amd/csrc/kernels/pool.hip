@@ -130,4 +130,31 @@ hipError_t launch_gap_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C
   return hipGetLastError();
 }
 
+
+// stride-2 subsample of an NHWC bf16 tensor: y[n][ho][wo][:] = x[n][2 ho][2 wo][:] (the quarter-grid
+// input of a stride-2 1x1 downsample convolution, ops/tail.py). 16-byte lanes; each output pixel's
+// channels are one contiguous run in both tensors.
+__global__ __launch_bounds__(256) void subsample2_kernel(const u32x4* __restrict__ x, u32x4* __restrict__ y, int64_t n16,
+                                                         int C16, int Ho, int Wo, int H, int W) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) {
+    const int64_t pix = i / C16;
+    const int c = (int)(i - pix * C16);
+    const int64_t n = pix / ((int64_t)Ho * Wo);
+    const int rem = (int)(pix - n * Ho * Wo);
+    const int ho = rem / Wo, wo = rem - ho * Wo;
+    y[i] = __builtin_nontemporal_load(x + ((n * H + 2 * ho) * (int64_t)W + 2 * wo) * C16 + c);
+  }
+}
+
+hipError_t launch_subsample2(const uint16_t* x, uint16_t* y, int N, int H, int W, int C, hipStream_t st) {
+  if (C % 8 != 0 || H % 2 != 0 || W % 2 != 0) return hipErrorInvalidValue;
+  const int Ho = H / 2, Wo = W / 2, C16 = C / 8;
+  const int64_t n16 = (int64_t)N * Ho * Wo * C16;
+  if (n16 <= 0) return hipSuccess;
+  hipLaunchKernelGGL(subsample2_kernel, dim3(stream_grid(n16, 256)), dim3(256), 0, st,
+                     reinterpret_cast<const u32x4*>(x), reinterpret_cast<u32x4*>(y), n16, C16, Ho, Wo, H, W);
+  return hipGetLastError();
+}
+
 }  // namespace psd

@@ -148,6 +148,7 @@ std::vector<at::Tensor> bn_pool_bwd(const at::Tensor& gpool, c10::optional<at::T
                                     const at::Tensor& save_invstd, const at::Tensor& ss,
                                     c10::optional<at::Tensor> dgamma_out, c10::optional<at::Tensor> dbeta_out);
 at::Tensor gap_bwd(const at::Tensor& dy, int64_t H, int64_t W);
+at::Tensor subsample2(const at::Tensor& x);
 
 // fused softmax cross-entropy on bf16 logits (xent_ops.cpp)
 void embed_bwd_(const at::Tensor& sorted, const at::Tensor& perm, const at::Tensor& dy, at::Tensor out);

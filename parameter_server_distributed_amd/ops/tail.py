@@ -77,13 +77,16 @@ def _variant(a2, w2, M: int, cin: int, cout: int, h: int, w: int, shift) -> int:
     variant runs at all (timing both passes together picked a slower apply variant)."""
     C = _native()
     dev = a2.device
+    # a residual operand of its own (reading the buffer being written, as an earlier version did,
+    # timed the pass with its residual reads hitting the cache and picked a slower variant)
+    res = torch.zeros(M, cout, device=dev, dtype=torch.bfloat16)
+    ss = torch.zeros(2 * cout, device=dev, dtype=torch.float32)
 
     def make(v):
         def fn():
             out = torch.empty(M, cout, device=dev, dtype=torch.bfloat16)
-            ss = torch.zeros(2 * cout, device=dev, dtype=torch.float32)
             mb = torch.empty(M * cout // 8, device=dev, dtype=torch.uint8)
-            if C.convn_(a2, w2, out, 1, 1, 1, 0, variant=v, apply_ss=ss, apply_res=out, apply_mask=mb) == 0:
+            if C.convn_(a2, w2, out, 1, 1, 1, 0, variant=v, apply_ss=ss, apply_res=res, apply_mask=mb) == 0:
                 raise _at.Declined("convn apply pass")
             return out
         return fn
@@ -328,7 +331,7 @@ class _DualTailFn(torch.autograd.Function):
         ctx.full_hw = tuple(xfull.shape[2:])
         ctx.stride = _ds_stride(convd)
         # a stride-2 1x1 downsample is a stride-1 one on the quarter grid of its input
-        xin = xfull if ctx.stride == 1 else xfull[:, :, ::2, ::2].contiguous(memory_format=torch.channels_last)
+        xin = xfull if ctx.stride == 1 else C.subsample2(xfull)
         n, c3, h, w = a2.shape
         cd, cout = xin.shape[1], w3.shape[0]
         M = n * h * w

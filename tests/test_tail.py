@@ -418,3 +418,12 @@ def test_dual_tail_fallback_matches_unfused_and_fp32(gpu, monkeypatch, stride, c
         e_on = ((a - f.float()).norm() / f.float().norm().clamp_min(1e-6)).item()
         e_off = ((b - f.float()).norm() / f.float().norm().clamp_min(1e-6)).item()
         assert e_on <= 1.5 * e_off + 1e-2, (nm, e_on, e_off)
+
+
+@pytest.mark.parametrize("shape", [(2, 256, 56, 56), (3, 64, 14, 10)])
+def test_subsample2_exact(gpu, shape):
+    """kernels/pool.hip subsample2: the quarter-grid input of a stride-2 1x1 downsample, bitwise."""
+    x = torch.randn(*shape, device=gpu).bfloat16().contiguous(memory_format=torch.channels_last)
+    y = native().subsample2(x)
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(y, x[:, :, ::2, ::2])
