@@ -87,6 +87,9 @@ def parse():
                     help="fp8 (e4m3 MFMA) forward of the bottleneck convolutions, bf16 backward "
                          "(1/0; -1: on for Wide-ResNet-101-2, the BASELINE 'CDNA4 fp8 MFMA' config)")
     ap.add_argument("--pull-dtype", default="", help="bf16|fp8 published-weight dtype (default: fp8 for WRN-101)")
+    ap.add_argument("--async-xfer", default="auto", choices=["auto", "kernel", "copy"],
+                    help="async plane push / pull transport: scatter / gather kernels over every owner's peer memory "
+                         "(auto: the kernels, copies if their self-test fails) or one hipMemcpyAsync per shard")
     ap.add_argument("--optimizer", default="", help="momentum|adam|adamw (default: momentum; adamw for BERT)")
     ap.add_argument("--lr", type=float, default=0.0)
     ap.add_argument("--graph", type=int, default=-1,
@@ -232,7 +235,7 @@ def main():
 
         try:
             ps = AsyncPS(spec.model, optim, num_shards=shards, staleness=a.staleness, bucket_mb=a.bucket_mb,
-                         device=dev, overlap=not spec.tied_weights, pull_dtype=pull_dtype, **kw)
+                         device=dev, overlap=not spec.tied_weights, pull_dtype=pull_dtype, xfer=a.async_xfer, **kw)
         except RuntimeError as e:  # collective on every rank (AsyncPS._agree): fall back together
             fallback = str(e)[:300]
             mode = "collective"

@@ -701,6 +701,7 @@ void AsyncEngine::set_xfer(bool kernel) {
 
 std::string AsyncEngine::xfer_mode() const {
   if (device_ < 0) return "host-memcpy";
+  // "kernel": peer segments by the scatter / gather kernels, this rank's own by hipMemcpyAsync
   return xfer_kernel_ ? "kernel" : "hipMemcpyAsync";
 }
 
@@ -766,7 +767,12 @@ std::vector<int64_t> AsyncEngine::pull_impl(int64_t step, char* dst, char* dst_s
     bufs[k] = b;
   }
   void* sp = reinterpret_cast<void*>(stream);
-  if (device_ >= 0 && xfer_kernel_) {
+  bool remote = false;  // any shard owned by another process (its peer-mapped memory)
+  for (int k = 0; k < P; ++k) remote = remote || owners_[k] != rank_;
+  // the gather kernel pays where it drives several peers' links at once; a pull of only this
+  // rank's own shards is a local copy, which the copy engine does without taking CUs from the
+  // compute stream (N = 1: ResNet-50 / BERT-base 0.2 % / 0.1 % faster with the copies)
+  if (device_ >= 0 && xfer_kernel_ && remote) {
     // every shard's snapshot in one gather launch: all owners' links at once (kernels/xfer.hip)
     const c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device_));
     if (dst_sc) {
@@ -781,7 +787,7 @@ std::vector<int64_t> AsyncEngine::pull_impl(int64_t step, char* dst, char* dst_s
                                        dst_bf16 + shard_off_[k], shard_len_[k]};
           mx = std::max(mx, shard_len_[k]);
         }
-        L.blocks_per_seg = xfer_blocks(mx, P == 1 ? 256 : 48);
+        L.blocks_per_seg = xfer_blocks(mx, 48);
         hip_ok(launch_xfer_mx(L, static_cast<hipStream_t>(sp)), "launch_xfer_mx(pull)");
       }
     } else {
@@ -791,7 +797,7 @@ std::vector<int64_t> AsyncEngine::pull_impl(int64_t step, char* dst, char* dst_s
         L.seg[L.count++] = XferSeg{publish_ptr(k, bufs[k]), dst + shard_off_[k] * esz_, shard_len_[k] * esz_};
         mx = std::max(mx, shard_len_[k] * esz_);
       }
-      L.blocks_per_seg = xfer_blocks(mx, P == 1 ? 256 : 48);
+      L.blocks_per_seg = xfer_blocks(mx, 48);
       L.nt_load = 1;
       hip_ok(launch_xfer(L, static_cast<hipStream_t>(sp)), "launch_xfer(pull)");
     }
@@ -824,20 +830,24 @@ void AsyncEngine::push(int64_t step, const at::Tensor& grads_flat, int64_t lo, i
   check_error();
   const char* src = static_cast<const char*>(grads_flat.data_ptr());
   const int slot = (int)(step % (S_ + 1));
-  if (device_ >= 0 && xfer_kernel_) {
-    // the bucket's slice for every owner it overlaps in one scatter launch (kernels/xfer.hip)
+  bool remote = false;
+  for (size_t k = 0; k < owners_.size(); ++k) {
+    const int64_t a = std::max(lo, shard_off_[k]), b = std::min(hi, shard_off_[k] + shard_len_[k]);
+    remote = remote || (a < b && owners_[k] != rank_);
+  }
+  if (device_ >= 0 && xfer_kernel_ && remote) {
+    // the bucket's slice for every owner it overlaps in one scatter launch (kernels/xfer.hip); a
+    // push into this rank's own inbox only is a local copy (see pull_impl)
     XferList L{};
     int64_t mx = 0;
-    bool local_only = true;
     for (size_t k = 0; k < owners_.size(); ++k) {
       const int64_t a = std::max(lo, shard_off_[k]), b = std::min(hi, shard_off_[k] + shard_len_[k]);
       if (a >= b) continue;
       L.seg[L.count++] = XferSeg{src + a * esz_, inbox_ptr((int)k, my_wi_, slot) + (a - shard_off_[k]) * esz_,
                                  (b - a) * esz_};
       mx = std::max(mx, (b - a) * esz_);
-      local_only = local_only && owners_[k] == rank_;
     }
-    L.blocks_per_seg = xfer_blocks(mx, local_only ? 256 : 48);
+    L.blocks_per_seg = xfer_blocks(mx, 48);
     L.nt_store = 1;
     const c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device_));
     hip_ok(launch_xfer(L, reinterpret_cast<hipStream_t>(stream)), "launch_xfer(push)");
