@@ -866,7 +866,14 @@ def _strided_dgrad(mod, dy, weight, to, H: int, W: int):
     def gemm():
         return _from_2d(torch.mm(dy2, w2), n, ho, wo)
 
+    def psd():  # the persistent 8-phase MFMA GEMM (kernels/gemm.hip)
+        out = torch.empty(M4, cin, device=dy.device, dtype=dy.dtype)
+        _native().gemm_(dy2, w2, True, False, out)
+        return _from_2d(out, n, ho, wo)
+
     cands = {"gemm": gemm}
+    if _psd_ok(cout, cin):
+        cands["psd"] = psd
     if _psdn_ok(cout, cin):
         cands.update(_convn_variants(dy, w2.t().contiguous(), 1, 1, 0))
     t4 = cands[_choose(("dgrad_s2", M4, cin, cout), cands)]()
