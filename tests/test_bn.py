@@ -106,10 +106,14 @@ def test_maxpool3s2_matches_torch(gpu, shape):
 
 
 @pytest.mark.gpu
-def test_resnet_residual_grad_fusion_matches_unfused(gpu):
-    """Identity-block residual gradients handed BN-to-BN inside the kernels == autograd's add."""
+def test_resnet_residual_grad_fusion_matches_unfused(gpu, monkeypatch):
+    """Identity-block residual gradients handed BN-to-BN inside the kernels == autograd's add.
+    (Stored-output tails in both runs: the recomputing tails change the forward rounding -- pinned
+    against fp32 in tests/test_tail.py -- and at batch 4 / 64x64, 16 samples per layer-4 BN channel,
+    a forward perturbation of one bf16 ulp moves the stem's gradient by ~10 %.)"""
     from parameter_server_distributed_amd import models
 
+    monkeypatch.setenv("PSD_FEATURES", "tail_recompute=0")
     torch.manual_seed(0)
     grads = []
     for fuse in (True, False):
@@ -342,9 +346,12 @@ def test_stem_wgrad_matches_fp32(gpu, shape):
 
 @pytest.mark.gpu
 def test_downsample_bn_applied_inside_bn3_matches_unfused(gpu):
-    """Bottleneck with a downsample branch: relu(bn3(conv3) + bn_ds(conv_ds)) with the downsample BN
-    applied inside bn3's apply pass (ops/bn.py bn_add_bn_relu) vs the unfused modules: output,
-    every gradient and both BNs' running statistics."""
+    """Bottleneck with a stride-2 downsample branch: relu(bn3(conv3) + bn_ds(conv_ds)) on the fused
+    path (the recomputing dual tail of ops/tail.py, or bn_add_bn_relu with the downsample BN inside
+    bn3's apply pass) vs the unfused modules, both against an fp32 composite run of the same block:
+    output, every gradient and both BNs' running statistics at the unfused path's bf16 error level
+    (two bf16 paths that round in different places differ by a few % on near-cancelling BN
+    gradient sums, so they are compared through fp32, not with each other)."""
     import copy
 
     import torch.nn as nn
@@ -364,18 +371,17 @@ def test_downsample_bn_applied_inside_bn3_matches_unfused(gpu):
                 m.bias.uniform_(-0.2, 0.2)
     ref = copy.deepcopy(blk)
     ref.fuse_residual_grad = False
+    ref32 = copy.deepcopy(blk).float()
     x0 = torch.randn(8, 64, 28, 28, device=gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     outs = []
-    for m in (blk, ref):
-        x = x0.clone().requires_grad_(True)
+    for m in (blk, ref, ref32):
+        x = (x0.float() if m is ref32 else x0).clone().requires_grad_(True)
         y = m(x)
         y.float().pow(2).mean().backward()
-        outs.append((y.float(), x.grad.float(), {n: p.grad.float() for n, p in m.named_parameters()},
-                     {n: b.float() for n, b in m.named_buffers() if b.is_floating_point()}))
-    (y, gx, gp, bufs), (yr, gxr, gpr, bufsr) = outs
-    torch.testing.assert_close(y, yr, rtol=2e-2, atol=2e-2 * float(yr.abs().max()))
-    torch.testing.assert_close(gx, gxr, rtol=2e-2, atol=2e-2 * float(gxr.abs().max()))
-    for n in gpr:
-        torch.testing.assert_close(gp[n], gpr[n], rtol=3e-2, atol=3e-2 * float(gpr[n].abs().max()) + 1e-6, msg=n)
-    for n in bufsr:
-        torch.testing.assert_close(bufs[n], bufsr[n], rtol=1e-3, atol=1e-3, msg=n)
+        outs.append({"y": y.float(), "dx": x.grad.float(), **{n: p.grad.float() for n, p in m.named_parameters()},
+                     **{n: b.float() for n, b in m.named_buffers() if b.is_floating_point()}})
+    f, u, r = outs
+    for n in r:
+        e_f = ((f[n] - r[n]).norm() / r[n].norm().clamp_min(1e-6)).item()
+        e_u = ((u[n] - r[n]).norm() / r[n].norm().clamp_min(1e-6)).item()
+        assert e_f <= 1.5 * e_u + 1e-2, (n, e_f, e_u)

@@ -171,13 +171,15 @@ def test_resnet_convn_fusions_match_library_path(gpu, monkeypatch):
     consumer BN's statistics in the epilogue, bwd-data with the producing BN's backward reduction
     in the epilogue (bn1 / bn2 from x and scale/shift; identity-block bn3 with the residual
     gradient added under the bit-mask) -- vs the same model with the kernel off (library
-    convolutions, separate BN passes): loss and every parameter gradient."""
+    convolutions, separate BN passes): loss and every parameter gradient. The recomputing tails
+    (ops/tail.py, pinned against fp32 in test_tail.py) are off on both sides: 16 bottlenecks at
+    batch 8 amplify their forward rounding differences past this bf16-vs-bf16 bound."""
     from parameter_server_distributed_amd import models
     from parameter_server_distributed_amd.ops import autotune
 
     res = []
     for on in (True, False):
-        monkeypatch.setenv("PSD_FEATURES", f"convn={int(on)}")
+        monkeypatch.setenv("PSD_FEATURES", f"convn={int(on)},tail_recompute=0")
         monkeypatch.setenv("PSD_AUTOTUNE_FORCE", "psdnb0,psdn0" if on else "miopen")
         autotune._DECISIONS.clear()
         torch.manual_seed(0)
