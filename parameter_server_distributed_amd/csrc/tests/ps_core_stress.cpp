@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <string>
 #include <thread>
+#include <unistd.h>
 #include <vector>
 
 #include "../kernels/launchers.h"
@@ -50,7 +51,9 @@ static int run(bool async_mode) {
     });
   }
   ts.emplace_back([&] {  // monitor + periodic checkpoint
-    const std::string path = std::string("/tmp/psd_stress_") + (async_mode ? "a" : "s") + ".ckpt";
+    // per-process path: the sanitizer variants of this binary run concurrently under pytest-xdist
+    const std::string path = std::string("/tmp/psd_stress_") + (async_mode ? "a" : "s") + "_" +
+                             std::to_string(static_cast<long>(getpid())) + ".ckpt";
     int k = 0;
     while (!stop.load()) {
       (void)ps.sync_status(ps.current_iteration());

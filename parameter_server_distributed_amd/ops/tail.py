@@ -78,12 +78,17 @@ def _variant(a2, w2, M: int, cin: int, cout: int, h: int, w: int, shift) -> int:
     C = _native()
     dev = a2.device
     # a residual operand of its own (reading the buffer being written, as an earlier version did,
-    # timed the pass with its residual reads hitting the cache and picked a slower variant)
-    res = torch.zeros(M, cout, device=dev, dtype=torch.bfloat16)
-    ss = torch.zeros(2 * cout, device=dev, dtype=torch.float32)
+    # timed the pass with its residual reads hitting the cache and picked a slower variant);
+    # allocated on the first timed call only -- once decided, every forward lands here and an
+    # eager [M, Cout] zero-fill per tail cost ~1 ms/step at batch 1024
+    scratch = []
 
     def make(v):
         def fn():
+            if not scratch:
+                scratch.extend((torch.zeros(M, cout, device=dev, dtype=torch.bfloat16),
+                                torch.zeros(2 * cout, device=dev, dtype=torch.float32)))
+            res, ss = scratch
             out = torch.empty(M, cout, device=dev, dtype=torch.bfloat16)
             mb = torch.empty(M * cout // 8, device=dev, dtype=torch.uint8)
             if C.convn_(a2, w2, out, 1, 1, 1, 0, variant=v, apply_ss=ss, apply_res=res, apply_mask=mb) == 0:

@@ -133,7 +133,7 @@ def test_collective_deploy_scale_up_down(tmp_path, plane):
                            text=True, timeout=60)
         assert r.returncode == 0, r.stdout + r.stderr
         pids = [int(_read(f"{cd}/worker_{i}.pid")) for i in range(3)]
-        assert _wait_exit(pids, 180)
+        assert _wait_exit(pids, 360)  # 4000 async steps: ~60 s idle, several times that on a loaded host
         logs = [_read(f"{cd}/worker_{i}.log") for i in range(3)]
         assert f"worker 0 finished {it} iterations" in logs[0], logs[0][-3000:]
         assert f"worker 1 finished {it} iterations" in logs[1], logs[1][-3000:]
