@@ -111,7 +111,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("save_invstd"), py::arg("part"), py::arg("part_d"), py::arg("rows"), py::arg("xd"), py::arg("gamma_d"),
         py::arg("mean_d"), py::arg("invstd_d"), py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none(),
         py::arg("dgamma_d_out") = py::none(), py::arg("dbeta_d_out") = py::none(), py::arg("fold") = false,
-        py::arg("fold_d") = false);
+        py::arg("fold_d") = false, py::arg("derive_d") = false);
   m.def("bn_elemt_coef", &bn_elemt_coef, py::arg("g"), py::arg("x"), py::arg("coef"));
   m.def("convw_fold_rows", &convw_fold_rows, py::arg("Cout"), py::arg("Cin"));
   m.def("convw_gram_rows", &convw_gram_rows_, py::arg("C"));

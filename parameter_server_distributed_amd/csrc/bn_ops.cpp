@@ -911,7 +911,7 @@ std::vector<at::Tensor> bn_bwd_dual_pre(const at::Tensor& g_in, const at::Tensor
                                         const at::Tensor& xd_in, const at::Tensor& gamma_d, const at::Tensor& mean_d,
                                         const at::Tensor& invstd_d, c10::optional<at::Tensor> dgamma_out,
                                         c10::optional<at::Tensor> dbeta_out, c10::optional<at::Tensor> dgamma_d_out,
-                                        c10::optional<at::Tensor> dbeta_d_out, bool fold, bool fold_d) {
+                                        c10::optional<at::Tensor> dbeta_d_out, bool fold, bool fold_d, bool derive_d) {
   const c10::DeviceGuard dg(x_in.device());
   at::Tensor x = nhwc(x_in), g = nhwc(g_in), xd = nhwc(xd_in);
   const int64_t C = channels(x), M = x.numel() / C;
@@ -921,8 +921,9 @@ std::vector<at::Tensor> bn_bwd_dual_pre(const at::Tensor& g_in, const at::Tensor
   for (const at::Tensor* t : {&save_mean, &save_invstd, &mean_d, &invstd_d})
     TORCH_CHECK(t->numel() == C && t->scalar_type() == at::kFloat && t->is_contiguous(), "psd bn_bwd_dual_pre: stats");
   for (const at::Tensor* t : {&part, &part_d})
-    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && rows > 0 && t->numel() >= rows * 2 * C,
-                "psd bn_bwd_dual_pre: partials must be fp32 [rows, 2, C]");
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && rows > 0 &&
+                    t->numel() >= (derive_d && t == &part_d ? 2 : rows * 2) * C,
+                "psd bn_bwd_dual_pre: partials must be fp32 [rows, 2, C] (derive_d: part_d [2, C])");
   auto grad_buf = [&](const c10::optional<at::Tensor>& o) {
     at::Tensor t = (o.has_value() && o->defined()) ? *o : at::empty({C}, x.options());
     TORCH_CHECK(t.numel() == C && t.scalar_type() == at::kBFloat16 && t.is_contiguous(), "psd bn_bwd_dual_pre: grad buffer");
@@ -934,7 +935,7 @@ std::vector<at::Tensor> bn_bwd_dual_pre(const at::Tensor& g_in, const at::Tensor
   at::Tensor coef = at::empty({3 * C}, f32), coef_d = at::empty({3 * C}, f32);
   const bool many = rows > kFoldRows;
   at::Tensor fw = many ? at::empty({(int64_t)kFoldRows * 2 * C}, f32) : at::Tensor();
-  at::Tensor fwd = many ? at::empty({(int64_t)kFoldRows * 2 * C}, f32) : at::Tensor();
+  at::Tensor fwd = many && !derive_d ? at::empty({(int64_t)kFoldRows * 2 * C}, f32) : at::Tensor();
   // fold / fold_d: the BN input gradient of bn3 / of the downsample BN is folded into its
   // convolution's backward (ops/conv.py _fold_backward): not written here
   TORCH_CHECK(!fold_d || fold, "psd bn_bwd_dual_pre: fold_d needs fold");
@@ -953,7 +954,8 @@ std::vector<at::Tensor> bn_bwd_dual_pre(const at::Tensor& g_in, const at::Tensor
   a.part_d = part_d.data_ptr<float>();
   a.rows = (int)rows;
   a.fold_ws = many ? fw.data_ptr<float>() : nullptr;
-  a.fold_ws_d = many ? fwd.data_ptr<float>() : nullptr;
+  a.fold_ws_d = many && !derive_d ? fwd.data_ptr<float>() : nullptr;
+  a.derive_d = derive_d ? 1 : 0;
   a.dgamma = reinterpret_cast<uint16_t*>(dgamma.data_ptr());
   a.dbeta = reinterpret_cast<uint16_t*>(dbeta.data_ptr());
   a.dgamma_d = reinterpret_cast<uint16_t*>(dgamma_d.data_ptr());

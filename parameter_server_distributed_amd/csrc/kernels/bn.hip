@@ -472,6 +472,23 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
   fin_bwd(f, c, s1, s2);
 }
 
+// The dual tail's second BN (the downsample branch) from the first one's sums: both see the same
+// masked gradient g, so sum g is shared, and sum g (yd - mean_d) = r2 (= sum g yd, the downsample
+// fold's rowdot row [0 | sum g yd]) - mean_d sum g. One pass over the partials for both BNs (the
+// second used to get a cloned partials buffer with its own -mean_d sum g column, and a pass of its own).
+__device__ __forceinline__ void fin_bwd_derived(const FinBwd& f2, const float* r2, int c, double s1) {
+  fin_bwd(f2, c, s1 + (double)r2[c], (double)r2[f2.C + c] - (double)f2.mean[c] * s1);
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_finalize_dual_kernel(const float* __restrict__ part, int nblk, FinBwd f,
+                                                                   FinBwd f2, const float* __restrict__ r2) {
+  const int c = blockIdx.x * kFinCh + threadIdx.x;
+  double s1, s2;
+  if (!sum_partials(part, nblk, f.C, blockIdx.x * kFinCh, s1, s2)) return;
+  fin_bwd(f, c, s1, s2);
+  fin_bwd_derived(f2, r2, c, s1);
+}
+
 // Many producer partial rows (a convolution epilogue writes one per output tile: ~50k for a b1024
 // layer1 convolution) summed and finalized in ONE launch: block (f, cg) sums rows [f * chunk, ..)
 // of the 32 channels of column group cg into a slab row ws[cg][f], then draws a ticket; the block
@@ -485,7 +502,8 @@ constexpr int kFfMaxF = 256;  // slab rows per column group
 template <bool BWD>
 __global__ __launch_bounds__(256) void bn_fold_finalize_kernel(const float* __restrict__ part, int rows, int chunk,
                                                                float* __restrict__ ws, unsigned int* __restrict__ cnt,
-                                                               FinFwd ff, FinBwd fb) {
+                                                               FinFwd ff, FinBwd fb, FinBwd fb2,
+                                                               const float* __restrict__ r2) {
   const int C = BWD ? fb.C : ff.C;
   const int f = blockIdx.x, cg = blockIdx.y, F = gridDim.x;
   const int col = threadIdx.x & 63, rg = threadIdx.x >> 6;
@@ -534,8 +552,12 @@ __global__ __launch_bounds__(256) void bn_fold_finalize_kernel(const float* __re
     const int j = threadIdx.x;
     const double s = ((tot[0][j] + tot[1][j]) + tot[2][j]) + tot[3][j];
     const double q = ((tot[0][32 + j] + tot[1][32 + j]) + tot[2][32 + j]) + tot[3][32 + j];
-    if (BWD) fin_bwd(fb, c, s, q);
-    else fin_fwd(ff, c, s, q);
+    if (BWD) {
+      fin_bwd(fb, c, s, q);
+      if (fb2.coef) fin_bwd_derived(fb2, r2, c, s);  // (the dual tail's downsample BN)
+    } else {
+      fin_fwd(ff, c, s, q);
+    }
   }
   if (!BWD && cg == 0 && threadIdx.x == 0 && ff.counter) *ff.counter += 1;
 }
@@ -563,7 +585,7 @@ static unsigned int* ff_counters(int need) {
 // fold + finalize of `rows` partial rows in one launch (ws: >= kFfMaxF * 64 * column groups floats)
 template <bool BWD>
 static hipError_t fold_finalize(const float* part, int rows, float* ws, const FinFwd& ff, const FinBwd& fb,
-                                hipStream_t st) {
+                                hipStream_t st, const FinBwd& fb2 = FinBwd{}, const float* r2 = nullptr) {
   const int C = BWD ? fb.C : ff.C;
   const int ncg = (C + kFfCh - 1) / kFfCh;
   int F = (rows + 63) / 64;  // >= 64 rows per block
@@ -573,7 +595,7 @@ static hipError_t fold_finalize(const float* part, int rows, float* ws, const Fi
   unsigned int* cnt = ff_counters(ncg);
   if (!cnt) return hipErrorOutOfMemory;
   hipLaunchKernelGGL((bn_fold_finalize_kernel<BWD>), dim3(F, ncg), dim3(256), 0, st, part, rows, chunk, ws, cnt, ff,
-                     fb);
+                     fb, fb2, r2);
   return hipGetLastError();
 }
 
@@ -993,10 +1015,14 @@ static hipError_t launch_bn_bwd_pool(const BnBwdArgs& a, hipStream_t st) {
 // one ticketed launch, fold_ws its slab workspace)
 static hipError_t finalize_pre(const float* part, int rows, float* fold_ws, int64_t M, int C, const uint16_t* gamma,
                                const float* mean, const float* invstd, uint16_t* dgamma, uint16_t* dbeta, float* coef,
-                               hipStream_t st) {
+                               hipStream_t st, const FinBwd& fb2 = FinBwd{}, const float* r2 = nullptr) {
   const FinBwd fb{M, C, gamma, mean, invstd, dgamma, dbeta, coef};
-  if (rows > kFoldRows) return fold_finalize<true>(part, rows, fold_ws, FinFwd{}, fb, st);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(256), 0, st, part, rows, fb);
+  if (rows > kFoldRows) return fold_finalize<true>(part, rows, fold_ws, FinFwd{}, fb, st, fb2, r2);
+  if (fb2.coef)
+    hipLaunchKernelGGL(bn_bwd_finalize_dual_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(256), 0, st, part, rows, fb,
+                       fb2, r2);
+  else
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(256), 0, st, part, rows, fb);
   return hipGetLastError();
 }
 
@@ -1043,12 +1069,19 @@ hipError_t launch_bn_elemt_coef(const uint16_t* g, const uint16_t* x, const floa
 // may be null: bn's input gradient folded into its producer, ops/conv.py _fold_backward).
 hipError_t launch_bn_bwd_dual_pre(const BnDualPreArgs& a, hipStream_t st) {
   if (a.M <= 0) return hipSuccess;
-  if (a.C % 8 != 0 || a.rows <= 0 || (a.rows > kFoldRows && (!a.fold_ws || !a.fold_ws_d))) return hipErrorInvalidValue;
-  hipError_t fe = finalize_pre(a.part, a.rows, a.fold_ws, a.M, a.C, a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta,
-                               a.coef, st);
-  if (fe == hipSuccess)
-    fe = finalize_pre(a.part_d, a.rows, a.fold_ws_d, a.M, a.C, a.gamma_d, a.mean_d, a.invstd_d, a.dgamma_d, a.dbeta_d,
-                      a.coef_d, st);
+  if (a.C % 8 != 0 || a.rows <= 0 || (a.rows > kFoldRows && (!a.fold_ws || (!a.fold_ws_d && !a.derive_d))))
+    return hipErrorInvalidValue;
+  hipError_t fe;
+  if (a.derive_d) {  // part_d = the downsample fold's rowdot row: both BNs from one pass over part
+    const FinBwd fb2{a.M, a.C, a.gamma_d, a.mean_d, a.invstd_d, a.dgamma_d, a.dbeta_d, a.coef_d};
+    fe = finalize_pre(a.part, a.rows, a.fold_ws, a.M, a.C, a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta, a.coef, st,
+                      fb2, a.part_d);
+  } else {
+    fe = finalize_pre(a.part, a.rows, a.fold_ws, a.M, a.C, a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta, a.coef, st);
+    if (fe == hipSuccess)
+      fe = finalize_pre(a.part_d, a.rows, a.fold_ws_d, a.M, a.C, a.gamma_d, a.mean_d, a.invstd_d, a.dgamma_d,
+                        a.dbeta_d, a.coef_d, st);
+  }
   if (fe != hipSuccess) return fe;
   if (!a.dx && !a.dxd) return hipSuccess;  // both BN input gradients folded into their convolutions
   if (!a.dxd) return hipErrorInvalidValue;

@@ -111,8 +111,9 @@ struct BnDualPreArgs {
   const uint16_t* gamma_d;
   const float *mean, *invstd, *mean_d, *invstd_d;
   const float* part;      // [rows][2][C] sum g, sum g (x - mean)
-  const float* part_d;    // [rows][2][C] sum g, sum g (xd - mean_d)
+  const float* part_d;    // [rows][2][C] sum g, sum g (xd - mean_d); derive_d: [2][C] = [0 | sum g yd]
   int rows;
+  int derive_d;           // the downsample BN's sums from part's sum g and part_d's sum g yd
   float *fold_ws, *fold_ws_d;  // [kFoldRows * 2C] each when rows > kFoldRows
   uint16_t *dgamma, *dbeta, *dgamma_d, *dbeta_d;
   float *coef, *coef_d;   // [3C] each

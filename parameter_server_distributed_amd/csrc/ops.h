@@ -45,7 +45,7 @@ std::vector<at::Tensor> bn_bwd_dual_pre(const at::Tensor& g, const at::Tensor& x
                                         const at::Tensor& xd, const at::Tensor& gamma_d, const at::Tensor& mean_d,
                                         const at::Tensor& invstd_d, c10::optional<at::Tensor> dgamma_out,
                                         c10::optional<at::Tensor> dbeta_out, c10::optional<at::Tensor> dgamma_d_out,
-                                        c10::optional<at::Tensor> dbeta_d_out, bool fold, bool fold_d);
+                                        c10::optional<at::Tensor> dbeta_d_out, bool fold, bool fold_d, bool derive_d);
 std::vector<at::Tensor> bnfold_dgrad_weights(const at::Tensor& w, const at::Tensor& coef);
 void bnfold_combine(const at::Tensor& P, const at::Tensor& w, const at::Tensor& coef, at::Tensor out, bool accumulate);
 void bnfold_rowdot(const at::Tensor& P, const at::Tensor& w, at::Tensor row);

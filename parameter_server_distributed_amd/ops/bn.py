@@ -303,13 +303,13 @@ class _BNAddBNReluFn(torch.autograd.Function):
                 if not C.convw_(g, xin_, P, 1, 1, 1, 0, fold=True):
                     raise RuntimeError("psd dual tail: convw_ declined the fold wgrad")
                 Ps.append(P)
-            part_d = part.clone()
-            part_d[:rows, 1] = part[:rows, 0] * (-mean_d)
+            # the downsample BN's sums derive from bn3's sum g (same masked g) and its own sum g yd
+            part_d = torch.empty(2, part.shape[-1], device=part.device, dtype=torch.float32)
             C.bnfold_rowdot(Ps[0], c3.weight, part[rows])
-            C.bnfold_rowdot(Ps[1], cd.weight, part_d[rows])
+            C.bnfold_rowdot(Ps[1], cd.weight, part_d)
             _, _, dg3, db3, dgd, dbd, coef, coef_d = C.bn_bwd_dual_pre(
                 g, x, w3, mean, invstd, part, part_d, rows + 1, r, wd, mean_d, invstd_d, dg3o, db3o, dgdo, dbdo,
-                fold=True, fold_d=True)
+                fold=True, fold_d=True, derive_d=True)
             _hand_fold(c3, g, coef, x, Ps[0])
             _hand_fold(cd, g, coef_d, r, Ps[1])
             return g, dg3, db3, g, dgd, dbd, None, None

@@ -181,6 +181,30 @@ def _bn_consumer(mod):
     return bn
 
 
+class _Lazy:
+    """A weight operand made on first use (``w.t().contiguous()`` for candidates the autotuner may
+    never pick: building it eagerly cost a copy launch per convolution per step). ``shape`` is known
+    up front; ``()`` returns the tensor."""
+    __slots__ = ("fn", "t", "shape")
+
+    def __init__(self, fn, shape):
+        self.fn, self.t, self.shape = fn, None, tuple(shape)
+
+    def __call__(self) -> torch.Tensor:
+        if self.t is None:
+            self.t = self.fn()
+        return self.t
+
+
+def _wt(w2: torch.Tensor) -> _Lazy:
+    """w2^T (contiguous), made on first use."""
+    return _Lazy(lambda: w2.t().contiguous(), (w2.shape[1], w2.shape[0]))
+
+
+def _get(w):
+    return w() if isinstance(w, _Lazy) else w
+
+
 def _convn_variants(x, w2, k: int, stride: int, pad: int, bn=None) -> dict:
     """{"psdn<v>": fn} over the kernel's tile variants; fn() -> the channels_last conv output. With a
     consumer ``bn`` every "psdn" call also reduces the BN's statistics partials in its epilogue and
@@ -198,7 +222,7 @@ def _convn_variants(x, w2, k: int, stride: int, pad: int, bn=None) -> dict:
             part = None
             if stats:
                 part = torch.empty(_part_rows(M, cout, v, ho, wo, k), 2, cout, device=x.device, dtype=torch.float32)
-            rows = C.convn_(x, w2, out, k, k, stride, pad, part=part,
+            rows = C.convn_(x, _get(w2), out, k, k, stride, pad, part=part,
                             shift=bn.running_mean if stats else None, variant=v)
             if rows == 0:
                 raise RuntimeError("convn_ declined a shape _psdn_ok accepted")
@@ -292,7 +316,7 @@ def _convn_bwd_variants(dy, w2, k: int, pad: int, fu: dict, dr) -> dict:
             # (+ 1 row: a BN whose input was never stored completes its partials there, ops/tail.py)
             part = torch.empty(_part_rows(M, cout, v, h, w, k) + 1, 2, cout, device=dy.device, dtype=torch.float32)
             part_d = torch.empty_like(part) if fu["mode"] == 3 else None
-            rows = C.convn_bwd_(dy, w2, out, k, k, 1, pad, part, v, fu["mode"], fu["bx"], fu["mean"],
+            rows = C.convn_bwd_(dy, _get(w2), out, k, k, 1, pad, part, v, fu["mode"], fu["bx"], fu["mean"],
                                 bss=fu.get("ss"), bdr=_dr_arg(dr), bmbits=fu.get("mbits"), bxd=fu.get("bxd"),
                                 bmean_d=fu.get("mean_d"), part_d=part_d)
             if rows == 0:
@@ -496,7 +520,7 @@ def _fold_backward(ctx, fold, x, weight, need_x: bool, need_w: bool, P=None):
 
     if need_x and foldable:
         w2, bvec = C.bnfold_dgrad_weights(weight, coef)
-        wt = weight.reshape(cout, cin).t().contiguous()
+        wt = _wt(weight.reshape(cout, cin))
         fu = _bn_bwd_fusion(ctx.bn_in, x)
         if fu is not None:
             fu["dr"] = fu["bn"]._psd_pending_dr.pop() if fu["mode"] >= 2 else None
@@ -508,7 +532,7 @@ def _fold_backward(ctx, fold, x, weight, need_x: bool, need_w: bool, P=None):
         def unfold():
             out = torch.empty(M, cin, device=g.device, dtype=g.dtype)
             keep.pop("dy", None)
-            if not C.convn_(unfolded_dy(), wt, out, 1, 1, 1, 0, variant=0):
+            if not C.convn_(unfolded_dy(), wt(), out, 1, 1, 1, 0, variant=0):
                 raise RuntimeError("convn_ declined the unfolded dgrad")
             if timing["on"] and need_w:
                 conv_bwd(keep["dy"], x, weight, *wargs, [False, True, False])
@@ -712,7 +736,7 @@ class _Conv1x1Fn(torch.autograd.Function):
                 cands["psd"] = psd
             fu = None
             if _psdn_ok(cout, cin):  # dX = dY . W as a 1x1 convolution of dY with W^T [cin, cout]
-                wt = w2.t().contiguous()
+                wt = _wt(w2)
                 cands.update(_convn_variants(dy, wt, 1, 1, 0))
                 fu = _bn_bwd_fusion(ctx.bn_in, x)
                 if fu is not None:
@@ -875,7 +899,7 @@ def _strided_dgrad(mod, dy, weight, to, H: int, W: int):
     if _psd_ok(cout, cin):
         cands["psd"] = psd
     if _psdn_ok(cout, cin):
-        cands.update(_convn_variants(dy, w2.t().contiguous(), 1, 1, 0))
+        cands.update(_convn_variants(dy, _wt(w2), 1, 1, 0))
     t4 = cands[_choose(("dgrad_s2", M4, cin, cout), cands)]()
     if not t4.is_contiguous(memory_format=torch.channels_last):
         t4 = t4.contiguous(memory_format=torch.channels_last)

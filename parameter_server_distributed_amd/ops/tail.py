@@ -329,6 +329,21 @@ def _finalize(bn, part, M: int):
                                  bn.momentum if bn.momentum is not None else 0.1, bn.eps, bn.num_batches_tracked)
 
 
+def dual_weights_reference(w3_2, wd_2, ss3, ss_d):
+    """torch-op form of C.bnfold_dual_weights (the numerics tests' reference): {wcat, ss}."""
+    cout = w3_2.shape[0]
+    s3, sd = ss3[:cout], ss_d[:cout]
+    big3 = s3.abs() >= sd.abs()
+    sbig = torch.where(big3, s3, sd)
+    safe = torch.where(sbig == 0, torch.ones_like(sbig), sbig)
+    r3 = torch.where(big3, torch.ones_like(s3), s3 / safe)
+    rd = torch.where(big3, sd / safe, torch.ones_like(sd))
+    r3 = torch.where(sbig == 0, torch.zeros_like(r3), r3)
+    rd = torch.where(sbig == 0, torch.zeros_like(rd), rd)
+    wcat = torch.cat([w3_2.float() * r3[:, None], wd_2.float() * rd[:, None]], 1).to(torch.bfloat16)
+    return wcat, torch.cat([sbig, ss3[cout:] + ss_d[cout:]])
+
+
 class _DualTailFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, a2, w3, g3, b3, xfull, wd, gd, bd, conv3, bn3, convd, bnd):
@@ -347,16 +362,8 @@ class _DualTailFn(torch.autograd.Function):
         # the other one's are scaled by the ratio (|ratio| <= 1, fp32 product, one rounding); the
         # epilogue applies the larger scale and the summed shift t3 + td:
         #   out = s_big (a2 W3'^T + x Wd'^T) + t3 + td   (s3 = 0, e.g. zero-init gamma: W3' = 0)
-        s3, sd = ss3[:cout], ss_d[:cout]
-        big3 = s3.abs() >= sd.abs()
-        sbig = torch.where(big3, s3, sd)
-        safe = torch.where(sbig == 0, torch.ones_like(sbig), sbig)
-        r3 = torch.where(big3, torch.ones_like(s3), s3 / safe)
-        rd = torch.where(big3, sd / safe, torch.ones_like(sd))
-        r3 = torch.where(sbig == 0, torch.zeros_like(r3), r3)
-        rd = torch.where(sbig == 0, torch.zeros_like(rd), rd)
-        wcat = torch.cat([w3_2.float() * r3[:, None], wd_2.float() * rd[:, None]], 1).to(torch.bfloat16)
-        ssc = torch.cat([sbig, ss3[cout:] + ss_d[cout:]])
+        # (one launch, kernels/bnfold.hip; dual_weights_reference above is the same in torch ops)
+        wcat, ssc = C.bnfold_dual_weights(w3_2, wd_2, ss3, ss_d)
         out = torch.empty(M, cout, device=a2.device, dtype=torch.bfloat16)
         mbits = torch.empty(M * cout // 8, device=a2.device, dtype=torch.uint8)
 
@@ -416,13 +423,13 @@ class _DualTailFn(torch.autograd.Function):
                 if not C.convw_(g, inp, P, 1, 1, 1, 0, fold=True):
                     raise RuntimeError("psd dual tail: convw_ declined the fold wgrad")
                 Ps.append(P)
-            part_d = part.clone()
-            part_d[:rows, 1] = part[:rows, 0] * (-mean_d)
+            # the downsample BN's sums derive from bn3's sum g (same masked g) and its own sum g yd
+            part_d = torch.empty(2, part.shape[-1], device=part.device, dtype=torch.float32)
             C.bnfold_rowdot(Ps[0], w3, part[rows])
-            C.bnfold_rowdot(Ps[1], wd, part_d[rows])
+            C.bnfold_rowdot(Ps[1], wd, part_d)
             _, _, dg3, db3, dgd, dbd, coef, coef_d = C.bn_bwd_dual_pre(
                 g, g, g3, mean3, invstd3, part, part_d, rows + 1, g, gd, mean_d, invstd_d, dg3o, db3o, dgdo, dbdo,
-                fold=True, fold_d=True)
+                fold=True, fold_d=True, derive_d=True)
             dxa, dw3, _ = _fold_backward(ctx.r3, (g, coef, None), a2, w3, need[0], need[1], P=Ps[0])
             dxi, dwd, _ = _fold_backward(ctx.rd, (g, coef_d, None), xin, wd, need[4], need[5], P=Ps[1])
             TAIL_CALLS["dual_bwd_fused"] += 1

@@ -427,3 +427,25 @@ def test_subsample2_exact(gpu, shape):
     y = native().subsample2(x)
     assert y.is_contiguous(memory_format=torch.channels_last)
     assert torch.equal(y, x[:, :, ::2, ::2])
+
+
+@pytest.mark.parametrize("cout,c3,cd", [(256, 64, 64), (512, 128, 256)])
+def test_dual_weights_kernel_matches_torch(gpu, cout, c3, cd):
+    """kernels/bnfold.hip bnfold_dual_weights (the dual tail's apply operands, one launch) == the
+    torch-op formula ops/tail.dual_weights_reference, bitwise: ratio-scaled weights of the smaller-
+    scale branch, s_big and the summed shift -- incl. ties, zero scales (zero-init gamma) and signs."""
+    from parameter_server_distributed_amd.ops.tail import dual_weights_reference
+
+    torch.manual_seed(0)
+    w3 = torch.randn(cout, c3, device=gpu).bfloat16()
+    wd = torch.randn(cout, cd, device=gpu).bfloat16()
+    ss3 = torch.randn(2 * cout, device=gpu)
+    ssd = torch.randn(2 * cout, device=gpu)
+    ss3[:8] = 0.0  # s3 = 0 (zero-init bn3 gamma)
+    ssd[4:12] = 0.0  # both zero on 4..7, sd = 0 on 8..11
+    ssd[16:24] = ss3[16:24]  # ties
+    ssd[24:32] = -ss3[24:32]  # |ties| with opposite signs
+    wcat, ss = native().bnfold_dual_weights(w3, wd, ss3, ssd)
+    wref, sref = dual_weights_reference(w3, wd, ss3, ssd)
+    assert torch.equal(wcat, wref)
+    assert torch.equal(ss, sref)

@@ -7,7 +7,7 @@ third under a TorchDispatchMode (the mode is propagated to the autograd device t
 tensor's shape and the innermost frames of this package on the Python stack (an empty stack =
 the autograd engine itself, e.g. materialized gradients of unused Function outputs).
 
-    python tools/probes/fill_probe.py [batch] [image]
+    python tools/probes/fill_probe.py [batch] [image] [--all]   (--all: every kernel-launching aten op)
 """
 import collections
 import os
@@ -22,6 +22,13 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspa
 from parameter_server_distributed_amd import models  # noqa: E402
 
 FILL_OPS = ("fill_", "zero_", "zeros", "zeros_like", "new_zeros", "full", "full_like", "fill")
+# with --all: every aten op that may launch a kernel (views, allocations and metadata ops skipped)
+NO_KERNEL = ("empty", "empty_like", "empty_strided", "new_empty", "new_empty_strided", "view", "_unsafe_view", "as_strided",
+             "expand", "permute", "t", "transpose", "reshape", "alias", "detach", "slice", "select", "unsqueeze",
+             "squeeze", "split", "split_with_sizes", "narrow", "_to_copy", "lift_fresh", "is_same_size", "size",
+             "stride", "sym_size", "sym_stride", "numel", "dim", "_local_scalar_dense", "item", "unbind", "set_",
+             "resize_", "contiguous", "clone_", "_reshape_alias", "view_as", "_has_compatible_shallow_copy_type")
+ALL = "--all" in sys.argv
 
 
 class FillLog(TorchDispatchMode):
@@ -32,8 +39,10 @@ class FillLog(TorchDispatchMode):
     def __torch_dispatch__(self, func, types, args=(), kwargs=None):
         out = func(*args, **(kwargs or {}))
         name = func.__name__.split(".")[0]
-        if name in FILL_OPS:
-            t = out if isinstance(out, torch.Tensor) else args[0]
+        if (name not in NO_KERNEL) if ALL else (name in FILL_OPS):
+            t = out if isinstance(out, torch.Tensor) else next((x for x in args if isinstance(x, torch.Tensor)), None)
+            if t is None or not t.is_cuda:
+                return out
             frames = [f"{os.path.basename(f.filename)}:{f.lineno}:{f.name}" for f in traceback.extract_stack()
                       if "parameter_server_distributed_amd" in f.filename][-3:]
             self.rows[(name, str(t.dtype).replace("torch.", ""), tuple(t.shape), " < ".join(reversed(frames)))] += 1
@@ -41,8 +50,9 @@ class FillLog(TorchDispatchMode):
 
 
 def main():
-    batch = int(sys.argv[1]) if len(sys.argv) > 1 else 64
-    img = int(sys.argv[2]) if len(sys.argv) > 2 else 224
+    pos = [a for a in sys.argv[1:] if not a.startswith("--")]
+    batch = int(pos[0]) if pos else 64
+    img = int(pos[1]) if len(pos) > 1 else 224
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     spec = models.build("resnet50", dev, torch.bfloat16, image_size=img)
