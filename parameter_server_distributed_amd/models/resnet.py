@@ -82,6 +82,9 @@ class Bottleneck(nn.Module):
         object.__setattr__(self.conv3, "_psd_bn_in", self.bn2)
         object.__setattr__(self.conv1, "_psd_bn_in", None)
         # bn3's input gradient can be folded into conv3's backward GEMMs (ops/conv.py _fold_backward)
+        if isinstance(self.conv1, Conv1x1) and not fp8:
+            # bn1's into conv1 (when conv2's bwd-data epilogue pre-reduced it: ops/bn.py)
+            object.__setattr__(self.bn1, "_psd_fold_conv", self.conv1)
         if isinstance(self.conv3, Conv1x1) and not fp8:
             object.__setattr__(self.bn3, "_psd_fold_conv", self.conv3)
             # and a stride-1 downsample BN's into the downsample conv (layer 1's first block)

@@ -191,7 +191,11 @@ class _FusedBNFn(torch.autograd.Function):
         mod._psd_bwd_pre = None
         if pre is not None and not (pre[0].data_ptr() == dy.data_ptr() and pre[0].shape == dy.shape):
             pre = None
-        conv = _fold_target(mod, x) if (ctx.has_res and ctx.relu and mbits is not None and w is not None) else None
+        # a residual BN (bn3) folds with its stored mask or pre-reduced partials; a plain ReLU BN (bn1,
+        # its mask recomputed from x) only with partials the consumer's bwd-data epilogue reduced
+        foldable = ctx.relu and w is not None and (
+            (ctx.has_res and mbits is not None) or (not ctx.has_res and pre is not None and _feat("bn1_fold")))
+        conv = _fold_target(mod, x) if foldable else None
         if conv is not None:
             # BN-backward fold: reduction + finalize only; the producing 1x1 convolution's dgrad / wgrad
             # take g and the coefficients (no elementwise pass, no input-gradient tensor)
@@ -204,10 +208,11 @@ class _FusedBNFn(torch.autograd.Function):
                                                        dbeta_out=dbo)
             _hand_fold(conv, g, coef, x)
             res_grad = None
-            if ctx.resid_to is not None:
-                ctx.resid_to._psd_pending_dr.append(g)
-            else:
-                res_grad = g
+            if ctx.has_res:
+                if ctx.resid_to is not None:
+                    ctx.resid_to._psd_pending_dr.append(g)
+                else:
+                    res_grad = g
             return g, dg, db, res_grad, None, None
         if pre is not None:
             # the consumer convolution's bwd-data epilogue reduced this BN's backward and wrote the

@@ -572,7 +572,14 @@ def _fold_backward(ctx, fold, x, weight, need_x: bool, need_w: bool, P=None):
             if fu is not None:
                 cands[f"psdnb{v}"] = make(v, True)
         key = ("conv1x1", "dgrad_fold", M, cin, cout) + (() if y is not None else ("noy",))
-        default = "unfold" if y is not None else next(iter(cands))
+        if fu is not None and fu.get("bx") is None:
+            # the producing BN's input was never stored (a recomputing tail, ops/tail.py): only the
+            # fused epilogue can reduce its backward (as in _dgrad_route)
+            cands = {nm: fn for nm, fn in cands.items() if nm.startswith("psdnb")}
+            if not cands:
+                raise RuntimeError("psd: a BN without its stored input needs the fused folded bwd-data epilogue")
+            key = key + ("nobx",)
+        default = "unfold" if "unfold" in cands else next(iter(cands))
         if fu is None:
             how = _at.choose(key, cands, default)
         else:

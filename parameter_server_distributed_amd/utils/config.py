@@ -70,6 +70,9 @@ FEATURES: dict[str, tuple[bool, str]] = {
     # batch norm / bottleneck tail (ops/bn.py, ops/tail.py)
     "bn_fold": (True, "bn3's backward folded into conv3's bwd-data / weight-gradient GEMMs"),
     "bn_fold_ds": (True, "the stride-1 downsample BN folded into its convolution's backward"),
+    "bn1_fold": (False, "bn1's backward folded into conv1's bwd-data / weight-gradient GEMMs (with the "
+                         "reduction pre-run in conv2's bwd-data epilogue); off: same-box ResNet-50 A/B "
+                         "70.9 vs 68.0 ms/step (profiles/r5/ab_bn1_fold.md)"),
     "dual_nobx": (True, "downsample blocks' dual tail without the BN inputs in the consumer epilogue"),
     "tail_recompute": (True, "identity blocks' conv3 output recomputed instead of stored"),
     "tail_gram": (True, "the recomputing tail's statistics from the Gram matrix of conv3's input"),
