@@ -91,6 +91,11 @@ PYBIND11_MODULE(_C, m) {
         py::arg("Wo"), py::arg("R"));
   m.def("convn_variant_ok", &convn_variant_ok_, py::arg("N"), py::arg("variant"), py::arg("R"), py::arg("S"),
         py::arg("stride"), py::arg("pad"), py::arg("Wo"), py::arg("has_x2") = false);
+  m.def("convn_dgrad_s2_", &convn_dgrad_s2_, py::arg("dy"), py::arg("wph"), py::arg("out"), py::arg("variant"),
+        py::arg("part") = py::none(), py::arg("bx") = py::none(), py::arg("bmean") = py::none(),
+        py::arg("bss") = py::none());
+  m.def("convn_dgrad_s2_rows", &convn_dgrad_s2_rows, py::arg("Nb"), py::arg("Ho"), py::arg("Wo"), py::arg("Ci"),
+        py::arg("variant"));
   m.def("convn_bwd_", &convn_bwd_, py::arg("dy"), py::arg("w2"), py::arg("out"), py::arg("R"), py::arg("S"),
         py::arg("stride"), py::arg("pad"), py::arg("part"), py::arg("variant"), py::arg("mode"), py::arg("bx"),
         py::arg("bmean"), py::arg("bss") = py::none(), py::arg("bdr") = py::none(), py::arg("bmbits") = py::none(),

@@ -434,6 +434,110 @@ int64_t convn_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_
                : 1;
 }
 
+// Stride-2 3x3 (pad 1) bwd-data as four phase launches of the gathered narrow kernel: output parity
+// class (ph, pw) of dX[2i + ph][2j + pw] gathers dY rows {i, i + 1}^ph x columns {j, j + 1}^pw, i.e. a
+// stride-1 / pad-0 convolution of dY with a (1 + ph) x (1 + pw) tap subset of the weights
+// (wph[k], k = ph << 1 | pw, bf16 [Ci, (1 + ph)(1 + pw) Co], ordered (dr, ds, co): ops/conv.py
+// _dgrad_s2_phases), written at its own pixels of the full-size dX (convn.hip ophase). 9 taps in
+// all -- the forward's MACs, no zero-insertion, no zero-fill of dX (every pixel is in one class).
+// Optional mode-1 epilogue (the producing BN + ReLU's backward reduction, bx = its input at dX's
+// resolution): the four launches' partial rows are written one after another into part. Returns the
+// partial rows written (1 without part), 0 when the kernel declines (nothing launched).
+int64_t convn_dgrad_s2_(const at::Tensor& dy, const std::vector<at::Tensor>& wph, at::Tensor out, int64_t variant,
+                        c10::optional<at::Tensor> part, c10::optional<at::Tensor> bx, c10::optional<at::Tensor> bmean,
+                        c10::optional<at::Tensor> bss) {
+  TORCH_CHECK(dy.is_cuda() && dy.dim() == 4 && dy.scalar_type() == at::kBFloat16 &&
+                  dy.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "psd convn_dgrad_s2: dy must be a channels_last bf16 device tensor");
+  TORCH_CHECK(wph.size() == 4, "psd convn_dgrad_s2: four phase weights");
+  const int64_t Nb = dy.size(0), Co = dy.size(1), Ho = dy.size(2), Wo = dy.size(3);
+  const int64_t Ci = wph[0].size(0), M = Nb * Ho * Wo;
+  for (int k = 0; k < 4; ++k) {
+    const int64_t taps = (1 + (k >> 1)) * (1 + (k & 1));
+    TORCH_CHECK(wph[k].is_cuda() && wph[k].dim() == 2 && wph[k].scalar_type() == at::kBFloat16 &&
+                    wph[k].is_contiguous() && wph[k].size(0) == Ci && wph[k].size(1) == taps * Co &&
+                    wph[k].device() == dy.device(),
+                "psd convn_dgrad_s2: wph[k] must be a contiguous bf16 [Ci, taps * Co] tensor");
+  }
+  TORCH_CHECK(out.dim() == 2 && out.is_contiguous() && out.scalar_type() == at::kBFloat16 && out.size(0) == 4 * M &&
+                  out.size(1) == Ci && out.device() == dy.device(),
+              "psd convn_dgrad_s2: out must be a contiguous bf16 [Nb * 2Ho * 2Wo, Ci] tensor");
+  const bool fused = part.has_value() && part->defined();
+  int64_t per = 0;
+  if (fused) {
+    TORCH_CHECK(bx.has_value() && bx->defined() && bx->scalar_type() == at::kBFloat16 && bx->numel() == 4 * M * Ci &&
+                    bx->device() == dy.device() &&
+                    (bx->dim() == 4 ? bx->is_contiguous(at::MemoryFormat::ChannelsLast) : bx->is_contiguous()),
+                "psd convn_dgrad_s2: bx must be the BN input, bf16 like dX");
+    TORCH_CHECK(bmean.has_value() && bmean->defined() && bmean->scalar_type() == at::kFloat && bmean->numel() == Ci &&
+                    bmean->is_contiguous() && bss.has_value() && bss->defined() && bss->scalar_type() == at::kFloat &&
+                    bss->numel() == 2 * Ci && bss->is_contiguous(),
+                "psd convn_dgrad_s2: mode 1 needs the BN's fp32 mean [Ci] and scale/shift [2 Ci]");
+    per = std::max(convn_stats_rows((int)M), convn_part_rows_geo((int)M, (int)Ci, (int)std::max<int64_t>(variant, 0),
+                                                                  (int)Ho, (int)Wo, 2));
+    TORCH_CHECK(part->scalar_type() == at::kFloat && part->is_contiguous() && part->device() == dy.device() &&
+                    part->numel() >= 4 * per * 2 * Ci,
+                "psd convn_dgrad_s2: part must be fp32 [4 * convn_dgrad_s2_rows(...), 2, Ci]");
+  }
+  const int64_t xbytes = dy.numel() * 2;
+  if ((Co & (Co - 1)) != 0 || Co < 64 || xbytes > 0xFFFFFF00ll || convn_tile_n((int)Ci) == 0 || Ci % 8 != 0 ||
+      variant < 0 || variant >= convn_variants((int)Ci) || convn_variant_kind((int)Ci, (int)variant) != 0 ||
+      M >= (1 << 24))
+    return 0;
+  int logc = 0;
+  while ((1 << logc) < Co) ++logc;
+  const c10::DeviceGuard g(dy.device());
+  const hipStream_t st = c10::hip::getCurrentHIPStream(dy.device().index()).stream();
+  int64_t rows = 0;
+  for (int k = 0; k < 4; ++k) {
+    const int R = 1 + (k >> 1), S = 1 + (k & 1);
+    ConvnArgs a{};
+    a.K1 = R * S * (int)Co;
+    a.x = dy.data_ptr();
+    a.w = wph[k].data_ptr();
+    a.y = out.data_ptr();
+    a.xbytes = (uint32_t)xbytes;
+    a.wbytes = (uint32_t)(wph[k].numel() * 2);
+    a.M = (int)M;
+    a.N = (int)Ci;
+    a.K = a.K1;
+    a.H = (int)Ho;
+    a.W = (int)Wo;
+    a.logC = logc;
+    a.Ho = (int)Ho;
+    a.Wo = (int)Wo;
+    a.R = R;
+    a.S = S;
+    a.stride = 1;
+    a.pad = 0;
+    a.ldc = (int)Ci;
+    a.variant = (int)variant;
+    a.ophase = 1 + k;
+    if (fused) {
+      a.bwd = 1;
+      a.part = part->data_ptr<float>() + rows * 2 * Ci;
+      a.bx = reinterpret_cast<const uint16_t*>(bx->data_ptr());
+      a.bmean = bmean->data_ptr<float>();
+      a.bss = bss->data_ptr<float>();
+    }
+    const hipError_t e = launch_convn(a, st);
+    if (e == hipErrorNotSupported) {
+      TORCH_CHECK(k == 0, "psd convn_dgrad_s2: phase ", k, " declined after phase 0 ran");
+      return 0;
+    }
+    TORCH_CHECK(e == hipSuccess, "psd convn_dgrad_s2: ", hipGetErrorString(e));
+    if (fused) rows += convn_part_rows_geo((int)M, (int)Ci, (int)variant, (int)Ho, (int)Wo, R);
+  }
+  return fused ? rows : 1;
+}
+
+// partial rows to allocate for convn_dgrad_s2_ (all four phases) with this variant
+int64_t convn_dgrad_s2_rows(int64_t Nb, int64_t Ho, int64_t Wo, int64_t Ci, int64_t variant) {
+  const int M = (int)(Nb * Ho * Wo);
+  return 4 * (int64_t)std::max(convn_stats_rows(M), convn_part_rows_geo(M, (int)Ci, (int)std::max<int64_t>(variant, 0),
+                                                                         (int)Ho, (int)Wo, 2));
+}
+
 // bwd-data on the narrow kernel with the producing BN's backward reduction in the epilogue
 // (kernels/convn.hip bwd modes): out = g = mask (conv(dy, w2) [+ dr]); part gets the partials.
 // Returns the partial rows written, 0 when the kernel declines (nothing launched).

@@ -485,8 +485,21 @@ __global__ __launch_bounds__(512) void convn_kernel(ConvnArgs a) {
   const int tm = xcd_remap(blockIdx.x, tiles_m);
   const int m0 = tm * BM, n0 = blockIdx.y * BN;
   constexpr int SLOTB = G::SLOT;  // ring slot bytes
-  // output pixel of tile row p (-1: past M)
-  auto pix = [&](int p) -> int { return m0 + p < a.M ? m0 + p : -1; };
+  // output pixel of tile row p (-1: past M). A phase launch (ophase = 1 + (ph << 1 | pw): one of the
+  // four output-parity classes of a stride-2 bwd-data, ops/conv.py _dgrad_s2_phases) computes row
+  // m = (n, i, j) of the Ho x Wo phase grid and stores it at pixel (n, 2i + ph, 2j + pw) of the
+  // 2Ho x 2Wo output (every epilogue operand -- y, the BN input bx -- is addressed by that pixel)
+  const int oph = (a.ophase - 1) >> 1, opw = (a.ophase - 1) & 1;
+  const float inv_ohw = 1.f / (float)(a.Ho * a.Wo), inv_owo = 1.f / (float)a.Wo;
+  auto pix = [&](int p) -> int {
+    const int m = m0 + p;
+    if (m >= a.M) return -1;
+    if (a.ophase == 0) return m;
+    const int hw = a.Ho * a.Wo;
+    const int n = fdiv(m, hw, inv_ohw), rem = m - n * hw;
+    const int i = fdiv(rem, a.Wo, inv_owo), j = rem - i * a.Wo;
+    return ((n * 2 * a.Ho + 2 * i + oph) * 2 * a.Wo) + 2 * j + opw;
+  };
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wid / G::NWC, wc = wid % G::NWC;
@@ -1274,6 +1287,13 @@ hipError_t launch_convn(const ConvnArgs& a_in, hipStream_t st) {
                                                 (a.bwd != 3 || (a.bxd && a.bmean_d && a.part_d)) &&
                                                 (a.bwd != 5 || (a.Ho % 2 == 0 && a.Wo % 2 == 0))))));
   if (!ok) return hipErrorNotSupported;
+  // phase launches (stride-2 bwd-data): the gathered variants only, stride 1 / pad 0 over dY, no
+  // second operand, the plain or mode-1 epilogue; fdiv's exact range for the pixel map
+  if (a.ophase != 0 &&
+      (a.ophase > 4 || a.variant < 0 || a.variant >= plain_count(bn) || two || a.stride != 1 || a.pad != 0 ||
+       (a.bwd != 0 && a.bwd != 1) || a.M >= (1 << 24) || a.R > 2 || a.S > 2 ||
+       (int64_t)a.M * 4 * a.ldc * 2 > 0x7FFFFFFFll))
+    return hipErrorNotSupported;
   const int v = a.variant >= 0 ? a.variant : default_variant(a, bn);
   if (is_p1(bn, v)) return convp_launch(a, bn, st);
   if (is_persist(bn, v)) {

@@ -42,6 +42,9 @@ struct ConvnArgs {
   // never stored (ops/tail.py: statistics pass with y = nullptr, then this apply pass)
   const uint16_t* ares;
   uint8_t* amask;
+  // stride-2 bwd-data phase launch (gathered variants): 0 = none, else 1 + (ph << 1 | pw); the M rows
+  // of the Ho x Wo grid land at pixels (n, 2i + ph, 2j + pw) of a 2Ho x 2Wo output (convn.hip pix)
+  int ophase;
 };
 
 // output-channel tile of the kernel for N output channels (64, 128, 256 for N % 256 == 0), 0: unsupported

@@ -92,6 +92,10 @@ int64_t convn_(const at::Tensor& x, const at::Tensor& w2, at::Tensor out, int64_
                c10::optional<at::Tensor> apply_ss, c10::optional<at::Tensor> apply_res,
                c10::optional<at::Tensor> apply_mask);
 int64_t convn_stats_rows_(int64_t M);
+int64_t convn_dgrad_s2_(const at::Tensor& dy, const std::vector<at::Tensor>& wph, at::Tensor out, int64_t variant,
+                        c10::optional<at::Tensor> part, c10::optional<at::Tensor> bx, c10::optional<at::Tensor> bmean,
+                        c10::optional<at::Tensor> bss);
+int64_t convn_dgrad_s2_rows(int64_t Nb, int64_t Ho, int64_t Wo, int64_t Ci, int64_t variant);
 int64_t convn_bwd_(const at::Tensor& dy, const at::Tensor& w2, at::Tensor out, int64_t R, int64_t S, int64_t stride,
                    int64_t pad, at::Tensor part, int64_t variant, int64_t mode, c10::optional<at::Tensor> bx,
                    const at::Tensor& bmean, c10::optional<at::Tensor> bss, c10::optional<at::Tensor> bdr,

@@ -330,6 +330,58 @@ def _convn_bwd_variants(dy, w2, k: int, pad: int, fu: dict, dr) -> dict:
             if _variant_ok(cout, v, k, 1, pad, w, dy.shape[1], h)}
 
 
+def _s2_phase_weights(weight: torch.Tensor) -> list:
+    """The four output-parity phase weights of a stride-2 / pad-1 3x3 bwd-data (kernels/convn.hip
+    ophase): dX[2i + ph][2j + pw] = sum over dY rows i (+ i + 1 when ph = 1) and columns likewise, so
+    phase k = ph << 1 | pw takes taps r in (1,) / (2, 0) and s alike -- bf16 [Ci, R' S' Co] in
+    (dr, ds, co) order: W'[ci][dr][ds][co] = W[co][ci][r(dr)][s(ds)]."""
+    cin = weight.shape[1]
+    taps = ((1,), (2, 0))
+    out = []
+    for ph in (0, 1):
+        for pw in (0, 1):
+            wsel = weight[:, :, list(taps[ph])][:, :, :, list(taps[pw])]
+            out.append(wsel.permute(1, 2, 3, 0).reshape(cin, -1).contiguous())
+    return out
+
+
+def _dgrad_s2_phases(dy, weight, x, fu) -> dict:
+    """{"psdns<v>" / "psdnbs<v>": fn}: a stride-2 3x3 bwd-data on the narrow kernel as four phase
+    launches (no zero-insertion, no zero-filled dX; MIOpen's kernel runs a fill pass over dX first)
+    -- with ``fu`` (mode 1: the producing BN + ReLU) the fused candidates also reduce that BN's
+    backward in their epilogues and hand the partials over, as _convn_bwd_variants does."""
+    C = _native()
+    n, cin, h, w = x.shape
+    ho, wo = dy.shape[2], dy.shape[3]
+    wph = _Lazy(lambda: _s2_phase_weights(weight), (4,))
+
+    def make(v, fused):
+        def fn():
+            out = torch.empty(n * h * w, cin, device=dy.device, dtype=dy.dtype)
+            if fused:
+                part = torch.empty(C.convn_dgrad_s2_rows(n, ho, wo, cin, v) + 1, 2, cin, device=dy.device,
+                                   dtype=torch.float32)
+                rows = C.convn_dgrad_s2_(dy, wph(), out, v, part=part, bx=fu["bx"], bmean=fu["mean"], bss=fu["ss"])
+            else:
+                rows = C.convn_dgrad_s2_(dy, wph(), out, v)
+            if rows == 0:
+                raise RuntimeError("convn_dgrad_s2_ declined a shape it was offered for")
+            g = _from_2d(out, n, h, w)
+            if fused:
+                fu["bn"]._psd_bwd_pre = (g, part, rows)
+            return g
+        return fn
+
+    cands = {}
+    for v in range(C.convn_variants(cin)):
+        if C.convn_variant_kind(cin, v) != 0 or not C.convn_variant_ok(cin, v, 2, 2, 1, 0, wo, False):
+            continue
+        cands[f"psdns{v}"] = make(v, False)
+        if fu is not None:
+            cands[f"psdnbs{v}"] = make(v, True)
+    return cands
+
+
 def _dgrad_route(key: tuple, cands: dict, default: str, fu, dy_like) -> torch.Tensor:
     """bwd-data: the fastest candidate; with a BN backward fusion available the library and
     unfused candidates are timed with the reduction pass they leave to the BN. A non-fused choice
@@ -1021,6 +1073,21 @@ class _ConvFn(torch.autograd.Function):
                     if fu is not None:
                         fu["dr"] = fu["bn"]._psd_pending_dr.pop() if fu["mode"] >= 2 else None
                         cands.update(_convn_bwd_variants(dy, wf, k, pad, fu, fu["dr"]))
+                key = ("dgrad", n, cin, h, w, cout, k, stride)
+                dx = _dgrad_route(("conv",) + key, cands, "miopen", fu, x)
+            elif stride == 2 and k == 3 and pad == 1 and h == 2 * dy.shape[2] and w == 2 * dy.shape[3] \
+                    and _psdn_ok(cout, cin) and not ctx.fp8 and _feat("dgrad_s2_phase") \
+                    and x.is_contiguous(memory_format=torch.channels_last) \
+                    and dy.is_contiguous(memory_format=torch.channels_last):
+                # four output-parity phases of the narrow kernel vs MIOpen (its bwd-data zero-fills dX
+                # first), with bn1's backward reduction in the epilogue where that wins
+                fu = _bn_bwd_fusion(ctx.bn_in, x)
+                if fu is not None and fu["mode"] != 1:
+                    fu = None
+                if fu is not None:
+                    fu["dr"] = None
+                cands = {"miopen": miopen}
+                cands.update(_dgrad_s2_phases(dy, weight, x, fu))
                 key = ("dgrad", n, cin, h, w, cout, k, stride)
                 dx = _dgrad_route(("conv",) + key, cands, "miopen", fu, x)
             else:

@@ -64,6 +64,8 @@ FEATURES: dict[str, tuple[bool, str]] = {
     "convn_bwd": (True, "producing BN's backward reduction in the bwd-data epilogue (modes 1/2)"),
     "convn_bwd3": (True, "the dual-BN tail's reduction in the bwd-data epilogue (mode 3)"),
     "convn_bwd5": (True, "stride-2 downsample gradient added on the quarter grid (mode 5)"),
+    "dgrad_s2_phase": (True, "stride-2 3x3 bwd-data as four output-parity phase launches of the narrow kernel "
+                              "(with the producing BN's backward reduction in the epilogue) vs MIOpen"),
     "convw": (True, "narrow weight-gradient kernel (convw.hip) as a candidate"),
     "convw_persist": (True, "persistent layer-1 3x3 weight gradient (convhw)"),
     "gemm_stats": (True, "consumer-BN statistics in the 8-phase GEMM epilogue"),

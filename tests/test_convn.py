@@ -354,3 +354,90 @@ def test_convn_persistent_bwd_matches_gathered(gpu, Nb, H, mode):
     torch.testing.assert_close(p1, p0, rtol=0, atol=1e-6)
     raw = ref.permute(0, 2, 3, 1).reshape(M, 64)
     assert ((o0 == 0) | (o0 == raw) | (mode == 2)).all()  # mode 1: masked copy of dX
+
+
+S2_CASES = [  # Nb, Cin (= dX channels), H (= 2 Ho), Cout (= dY channels)
+    (2, 128, 56, 128),   # layer2's first conv2 (BN = 128)
+    (3, 256, 14, 256),   # layer3 family, ragged M (3 x 7 x 7 = 147 rows per phase)
+    (2, 512, 14, 512),   # layer4: two 256-wide column tiles
+    (2, 64, 28, 128),    # Cin 64 (BN = 64)
+]
+
+
+@pytest.mark.parametrize("nb,cin,H,cout", S2_CASES)
+def test_dgrad_s2_phases_exact(gpu, nb, cin, H, cout):
+    """Stride-2 3x3 bwd-data as four output-parity phase launches (convn_dgrad_s2_, kernels/convn.hip
+    ophase) == fp32 conv2d_input on small-integer operands (exact), every gathered variant; the
+    fused mode-1 epilogue: g = dX * relu'(bx * scale + shift) and the partials sum g, sum g (bx - mean)
+    vs fp32 references."""
+    from parameter_server_distributed_amd.ops.conv import _s2_phase_weights
+
+    C = native()
+    g = torch.Generator().manual_seed(0)
+    w = torch.randint(-2, 3, (cout, cin, 3, 3), generator=g).float()
+    dy = torch.randint(-2, 3, (nb, cout, H // 2, H // 2), generator=g).float()
+    ref = torch.nn.grad.conv2d_input((nb, cin, H, H), w, dy, stride=2, padding=1)
+    wb = w.to(gpu, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dyb = dy.to(gpu, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    wph = _s2_phase_weights(wb)
+    ref_cl = ref.permute(0, 2, 3, 1).reshape(-1, cin).to(gpu)
+    vs = [v for v in range(C.convn_variants(cin)) if C.convn_variant_kind(cin, v) == 0]
+    assert vs
+    bx = torch.randn(nb, cin, H, H, generator=g).to(gpu, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    mean = torch.randn(cin, generator=g).to(gpu)
+    ss = torch.cat([torch.rand(cin, generator=g) + 0.5, 0.3 * torch.randn(cin, generator=g)]).to(gpu)
+    bx2 = bx.permute(0, 2, 3, 1).reshape(-1, cin).float()
+    mask = (bx2 * ss[:cin] + ss[cin:]) > 0
+    g_ref = torch.where(mask, ref_cl, torch.zeros_like(ref_cl))
+    for v in vs:
+        out = torch.full((nb * H * H, cin), float("nan"), device=gpu, dtype=torch.bfloat16)
+        assert C.convn_dgrad_s2_(dyb, wph, out, v) == 1
+        # exact up to the bf16 rounding of the stored output (|dX| > 256 rounds; and every pixel written)
+        torch.testing.assert_close(out.float(), ref_cl, rtol=1 / 128, atol=0)
+        part = torch.empty(C.convn_dgrad_s2_rows(nb, H // 2, H // 2, cin, v), 2, cin, device=gpu)
+        out2 = torch.full_like(out, float("nan"))
+        rows = C.convn_dgrad_s2_(dyb, wph, out2, v, part=part, bx=bx, bmean=mean, bss=ss)
+        assert 0 < rows <= part.shape[0]
+        torch.testing.assert_close(out2.float(), g_ref, rtol=1 / 128, atol=0)
+        s1 = part[:rows, 0].double().sum(0)
+        s2 = part[:rows, 1].double().sum(0)
+        e1 = g_ref.double().sum(0)
+        # (the kernel sums the bf16-stored g)
+        gq = out2.float().double()
+        torch.testing.assert_close(s1, gq.sum(0), rtol=1e-5, atol=1e-2)
+        torch.testing.assert_close(s2, (gq * (bx2.double() - mean.double())).sum(0), rtol=1e-4, atol=1e-1)
+        torch.testing.assert_close(s1, e1, rtol=1e-2, atol=1.0)
+
+
+def test_dgrad_s2_in_resnet_block_matches_miopen(gpu, monkeypatch):
+    """A stride-2 bottleneck's conv2 bwd-data on the phase kernels (forced, plain and with bn1's
+    reduction fused) vs MIOpen: block input gradient and every parameter gradient."""
+    import torch.nn as nn
+
+    from parameter_server_distributed_amd.models.resnet import Bottleneck, _conv
+    from parameter_server_distributed_amd.ops import autotune
+    from parameter_server_distributed_amd.ops.bn import FusedBatchNorm2d
+
+    res = []
+    for force in ("psdnbs0", "psdns0", "miopen"):
+        monkeypatch.setenv("PSD_AUTOTUNE_FORCE", force)
+        monkeypatch.setenv("PSD_FEATURES", "tail_recompute=0")
+        autotune._DECISIONS.clear()
+        torch.manual_seed(0)
+        blk = Bottleneck(256, 128, 2, 64, nn.Sequential(_conv(256, 512, 1, 2), FusedBatchNorm2d(512)))
+        blk = blk.to(gpu).to(memory_format=torch.channels_last)
+        for p in blk.parameters():
+            p.data = p.data.to(torch.bfloat16)
+        x = torch.randn(4, 256, 28, 28, device=gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        x.requires_grad_(True)
+        y = blk(x)
+        y.float().pow(2).mean().backward()
+        picks = autotune.decisions()
+        got = [v for k, v in picks.items() if k[:2] == ("conv", "dgrad") and k[8] == 2]  # (stride 2)
+        assert got == [force], picks
+        res.append({"dx": x.grad.float(), **{n: p.grad.float() for n, p in blk.named_parameters()}})
+    autotune._DECISIONS.clear()
+    for r in res[:2]:
+        for n in res[2]:
+            a, b = r[n], res[2][n]
+            assert ((a - b).norm() / b.norm().clamp_min(1e-6)).item() < 2e-2, n
