@@ -1085,7 +1085,7 @@ static int convp_grid_x(int tiles_m, int tiles_n) {
 }
 
 template <int BN, bool STATS, int BWD>
-static hipError_t convp_launch_t(const ConvnArgs& a0, hipStream_t st) {
+static hipError_t convp_launch_t(const ConvnArgs& a0, hipStream_t st, int grid_mul = 1) {
   constexpr int WNT = P1Cfg<BN>::WNT;
   using G = Geo<128, BN, WNT, kP1Slots>;
   constexpr int LDS = p1_lds<BN>();
@@ -1100,8 +1100,10 @@ static hipError_t convp_launch_t(const ConvnArgs& a0, hipStream_t st) {
   ConvnArgs a = a0;
   a.nslot = kP1Slots;
   const int tiles_m = (a.M + 127) / 128, tiles_n = a.N / BN;
-  hipLaunchKernelGGL((convp_kernel<BN, WNT, kP1Slots, STATS, BWD>), dim3(convp_grid_x(tiles_m, tiles_n), tiles_n),
-                     dim3(G::NT), LDS, st, a, tiles_m);
+  int gx = convp_grid_x(tiles_m, tiles_n) * grid_mul;
+  if (gx > tiles_m) gx = tiles_m;
+  hipLaunchKernelGGL((convp_kernel<BN, WNT, kP1Slots, STATS, BWD>), dim3(gx, tiles_n), dim3(G::NT), LDS, st, a,
+                     tiles_m);
   return hipGetLastError();
 }
 
@@ -1117,7 +1119,7 @@ static int pr_slots(int K) {
 }
 
 template <int BN, bool STATS, int BWD>
-static hipError_t convpr_launch_t(const ConvnArgs& a0, int ns, hipStream_t st) {
+static hipError_t convpr_launch_t(const ConvnArgs& a0, int ns, hipStream_t st, int grid_mul = 1) {
   constexpr int WNT = P1Cfg<BN>::WNT;
   using G = Geo<128, BN, WNT, 3>;
   static bool attr = false;
@@ -1131,30 +1133,53 @@ static hipError_t convpr_launch_t(const ConvnArgs& a0, int ns, hipStream_t st) {
   a.nslot = ns;
   const int lds = (a.K / kBK) * BN * 128 + ns * 128 * 128 + G::NW * G::STG;
   const int tiles_m = (a.M + 127) / 128, tiles_n = a.N / BN;
-  hipLaunchKernelGGL((convpr_kernel<BN, WNT, STATS, BWD>), dim3(convp_grid_x(tiles_m, tiles_n), tiles_n),
-                     dim3(G::NT), lds, st, a, tiles_m);
+  int gx = convp_grid_x(tiles_m, tiles_n) * grid_mul;
+  if (gx > tiles_m) gx = tiles_m;
+  hipLaunchKernelGGL((convpr_kernel<BN, WNT, STATS, BWD>), dim3(gx, tiles_n), dim3(G::NT), lds, st, a, tiles_m);
   return hipGetLastError();
 }
 
 template <int BN>
-static hipError_t convpr_launch_s(const ConvnArgs& a, int ns, hipStream_t st) {
-  if (a.bwd == 1) return convpr_launch_t<BN, false, 1>(a, ns, st);
-  if (a.bwd == 2) return convpr_launch_t<BN, false, 2>(a, ns, st);
-  if (a.bwd == 3) return convpr_launch_t<BN, false, 3>(a, ns, st);
-  if (a.bwd == 5) return convpr_launch_t<BN, false, 5>(a, ns, st);
-  if (a.bwd == 8) return convpr_launch_t<BN, false, 8>(a, ns, st);
-  return a.part ? convpr_launch_t<BN, true, 0>(a, ns, st) : convpr_launch_t<BN, false, 0>(a, ns, st);
+static hipError_t convpr_launch_s(const ConvnArgs& a, int ns, hipStream_t st, int gm = 1) {
+  if (a.bwd == 1) return convpr_launch_t<BN, false, 1>(a, ns, st, gm);
+  if (a.bwd == 2) return convpr_launch_t<BN, false, 2>(a, ns, st, gm);
+  if (a.bwd == 3) return convpr_launch_t<BN, false, 3>(a, ns, st, gm);
+  if (a.bwd == 5) return convpr_launch_t<BN, false, 5>(a, ns, st, gm);
+  if (a.bwd == 8) return convpr_launch_t<BN, false, 8>(a, ns, st, gm);
+  return a.part ? convpr_launch_t<BN, true, 0>(a, ns, st, gm) : convpr_launch_t<BN, false, 0>(a, ns, st, gm);
 }
 
 template <int BN>
-static hipError_t convp_launch_s(const ConvnArgs& a, hipStream_t st) {
-  if (const int ns = pr_slots<BN>(a.K)) return convpr_launch_s<BN>(a, ns, st);
-  if (a.bwd == 1) return convp_launch_t<BN, false, 1>(a, st);
-  if (a.bwd == 2) return convp_launch_t<BN, false, 2>(a, st);
-  if (a.bwd == 3) return convp_launch_t<BN, false, 3>(a, st);
-  if (a.bwd == 5) return convp_launch_t<BN, false, 5>(a, st);
-  if (a.bwd == 8) return convp_launch_t<BN, false, 8>(a, st);
-  return a.part ? convp_launch_t<BN, true, 0>(a, st) : convp_launch_t<BN, false, 0>(a, st);
+static hipError_t convp_launch_s(const ConvnArgs& a, hipStream_t st, int gm = 1) {
+  if (const int ns = pr_slots<BN>(a.K)) return convpr_launch_s<BN>(a, ns, st, gm);
+  if (a.bwd == 1) return convp_launch_t<BN, false, 1>(a, st, gm);
+  if (a.bwd == 2) return convp_launch_t<BN, false, 2>(a, st, gm);
+  if (a.bwd == 3) return convp_launch_t<BN, false, 3>(a, st, gm);
+  if (a.bwd == 5) return convp_launch_t<BN, false, 5>(a, st, gm);
+  if (a.bwd == 8) return convp_launch_t<BN, false, 8>(a, st, gm);
+  return a.part ? convp_launch_t<BN, true, 0>(a, st, gm) : convp_launch_t<BN, false, 0>(a, st, gm);
+}
+
+// The two-workgroup form of the resident-B 1x1 kernel (variant kind 3, "p2"): a two-slot ring
+// (one A K-tile ahead) and twice the workgroups, two per CU when weights + ring + staging fit in
+// half the LDS. The epilogue-heavy passes (a bwd-data with the BN reduction: dr / mask reads and
+// the g stores per 128x256 tile against one 16 KiB A K-tile; the tail's apply pass) otherwise
+// expose each tile's epilogue load latency at one workgroup per CU; the second workgroup's
+// K-tile and epilogue run underneath. Shapes whose weights do not fit take the same grid on the
+// single-workgroup ring (the partial-row count depends only on the grid).
+template <int BN>
+static hipError_t convp2_launch_s(const ConvnArgs& a, hipStream_t st) {
+  using G = Geo<128, BN, P1Cfg<BN>::WNT, 3>;
+  const int lds2 = (a.K / kBK) * BN * 128 + 2 * 128 * 128 + G::NW * G::STG;
+  if (lds2 <= 80 * 1024) return convpr_launch_s<BN>(a, 2, st, 2);
+  return convp_launch_s<BN>(a, st, 2);
+}
+
+static hipError_t convp2_launch(const ConvnArgs& a, int bn, hipStream_t st) {
+  if (a.R != 1 || a.S != 1 || a.stride != 1 || a.pad != 0 || a.Ho != a.H || a.Wo != a.W) return hipErrorNotSupported;
+  if (bn == 256) return convp2_launch_s<256>(a, st);
+  if (bn == 128) return convp2_launch_s<128>(a, st);
+  return convp2_launch_s<64>(a, st);
 }
 
 static hipError_t convp_launch(const ConvnArgs& a, int bn, hipStream_t st) {
@@ -1206,19 +1231,20 @@ int convn_tile_n(int N) {
 
 // variants (tile geometry) per output width: the gathered ones (kind 0), then the persistent HALO
 // variant (convh_kernel, kind 2) for the 64-wide outputs, then the persistent 1x1 variant
-// (convp_kernel, kind 3). (The one-tile HALO variants -- kind 1 -- measured no faster than the
+// (convp_kernel, kind 3) and its two-workgroups-per-CU form (kind 4). (The one-tile HALO variants -- kind 1 -- measured no faster than the
 // gathered ones on the ResNet-50 shapes, profiles/convn_halo_r3.md, and were removed in round 5.)
 static int plain_count(int bn) { return bn == 256 ? 2 : 4; }
 static int persist_count(int bn) { return bn == 64 ? 1 : 0; }
-static int p1_count(int bn) { return bn ? 1 : 0; }
+static int p1_count(int bn) { return bn ? 2 : 0; }  // the persistent 1x1: one and two workgroups per CU
 static int convn_variant_count(int bn) { return plain_count(bn) + persist_count(bn) + p1_count(bn); }
 static bool is_persist(int bn, int v) { return v >= plain_count(bn) && v < plain_count(bn) + persist_count(bn); }
 static bool is_p1(int bn, int v) { return v == plain_count(bn) + persist_count(bn); }
+static bool is_p2(int bn, int v) { return v == plain_count(bn) + persist_count(bn) + 1; }
 
 int convn_variant_kind(int N, int v) {
   const int bn = convn_tile_n(N);
   if (!bn || v < 0 || v >= convn_variant_count(bn)) return -1;
-  return v < plain_count(bn) ? 0 : is_persist(bn, v) ? 2 : 3;
+  return v < plain_count(bn) ? 0 : is_persist(bn, v) ? 2 : is_p1(bn, v) ? 3 : 4;
 }
 
 int convn_variants(int N) {
@@ -1234,7 +1260,7 @@ static int default_variant(const ConvnArgs& a, int bn) {
 
 // BM of each variant (must match the dispatch in launch_convn)
 static int variant_bm(int bn, int v) {
-  if (is_persist(bn, v) || is_p1(bn, v)) return 128;
+  if (is_persist(bn, v) || is_p1(bn, v) || is_p2(bn, v)) return 128;
   if (bn == 64) return (v == 2 || v == 3) ? 256 : 128;
   if (bn == 128) return v == 2 ? 256 : 128;
   return 128;
@@ -1244,7 +1270,7 @@ bool convn_variant_ok(int N, int v, int R, int S, int stride, int pad, int Wo, b
   const int bn = convn_tile_n(N);
   if (!bn || v < 0 || v >= convn_variant_count(bn)) return false;
   if (v < plain_count(bn)) return true;
-  if (is_p1(bn, v)) return R == 1 && S == 1 && stride == 1 && pad == 0;
+  if (is_p1(bn, v) || is_p2(bn, v)) return R == 1 && S == 1 && stride == 1 && pad == 0;
   // persistent HALO (C = 64 and H = Ho are checked at launch: the predicate has no C)
   return !has_x2 && N == 64 && R == 3 && S == 3 && stride == 1 && pad == 1 && Wo + 2 <= 64;
 }
@@ -1260,6 +1286,10 @@ int convn_part_rows_geo(int M, int N, int variant, int Ho, int Wo, int R) {
     return 2 * convh_grid((M / (Ho * Wo)) * ((Ho + 1) / 2));
   }
   if (is_p1(bn, variant)) return 2 * convp_grid_x((M + 127) / 128, N / bn);
+  if (is_p2(bn, variant)) {
+    const int t = (M + 127) / 128, g = 2 * convp_grid_x(t, N / bn);
+    return 2 * (g < t ? g : t);
+  }
   return (bm / 64) * ((M + bm - 1) / bm);
 }
 
@@ -1296,6 +1326,7 @@ hipError_t launch_convn(const ConvnArgs& a_in, hipStream_t st) {
     return hipErrorNotSupported;
   const int v = a.variant >= 0 ? a.variant : default_variant(a, bn);
   if (is_p1(bn, v)) return convp_launch(a, bn, st);
+  if (is_p2(bn, v)) return convp2_launch(a, bn, st);
   if (is_persist(bn, v)) {
     if (!convh_ok(a) || a.bwd == 8 || !a.y) return hipErrorNotSupported;
     return convh_launch(a, st);

@@ -59,8 +59,9 @@ int convn_part_rows_geo(int M, int N, int variant, int Ho, int Wo, int R);
 // R / 2, Wo + R - 1 <= 64, no second operand)
 bool convn_variant_ok(int N, int v, int R, int S, int stride, int pad, int Wo, bool has_x2);
 int convn_variants(int N);
-// 0: gathered, 1: HALO, 2: persistent HALO (convh_kernel: C = N = 64, 3x3 / stride 1 / pad 1,
-// Wo <= 62, resident weights, double-buffered windows); -1: no such variant
+// 0: gathered, 2: persistent HALO (convh_kernel: C = N = 64, 3x3 / stride 1 / pad 1,
+// Wo <= 62, resident weights, double-buffered windows), 3: persistent 1x1 (convp / convpr),
+// 4: the persistent 1x1 at two workgroups per CU; -1: no such variant
 int convn_variant_kind(int N, int v);
 // hipErrorNotSupported outside the kernel's contract (nothing launched)
 hipError_t launch_convn(const ConvnArgs& a, hipStream_t stream);

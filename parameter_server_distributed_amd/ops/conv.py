@@ -245,7 +245,8 @@ def _variant_ok(cout: int, v: int, k: int, stride: int, pad: int, wo: int, cin: 
                 h: int | None = None) -> bool:
     """Variant v of the narrow kernel takes this shape: the gathered variants (kind 0), the
     persistent HALO variant (kind 2, C = N = 64 3x3 stride 1, H = Ho) and the persistent 1x1 variant
-    (kind 3) whenever their contract holds (features convn_persist / convn_p1)."""
+    (kind 3; kind 4 at two workgroups per CU) whenever their contract holds (features convn_persist /
+    convn_p1 / convn_p2)."""
     C = _native()
     if not C.convn_variant_ok(cout, v, k, k, stride, pad, wo):
         return False
@@ -254,6 +255,8 @@ def _variant_ok(cout: int, v: int, k: int, stride: int, pad: int, wo: int, cin: 
         return _feat("convn_persist") and cin == 64 and (h is None or h == wo)
     if kind == 3:  # persistent 1x1 (convp_kernel)
         return _feat("convn_p1")
+    if kind == 4:  # the same at two workgroups per CU
+        return _feat("convn_p1") and _feat("convn_p2")
     return kind == 0
 
 

@@ -70,6 +70,12 @@ def tail_ok(conv, bn, a2: torch.Tensor, idt: torch.Tensor) -> bool:
     return fold_ok(cin, cout) and C.convn_variants(cout) > 0 and (a2.shape[0] * a2.shape[2] * a2.shape[3]) % 8 == 0
 
 
+def _kind_ok(kind: int) -> bool:
+    """The narrow-kernel variant kinds the tail's 1x1 passes run on: gathered (0), persistent 1x1 (3)
+    and its two-workgroups-per-CU form (4, feature convn_p2)."""
+    return kind in (0, 3) or (kind == 4 and _feat("convn_p2"))
+
+
 def _variant(a2, w2, M: int, cin: int, cout: int, h: int, w: int, shift) -> int:
     """Narrow-kernel tile variant of the tail's apply pass (timed on scratch buffers with placeholder
     coefficients). Only the apply pass is timed: the statistics route is chosen on its own
@@ -97,7 +103,7 @@ def _variant(a2, w2, M: int, cin: int, cout: int, h: int, w: int, shift) -> int:
         return fn
 
     cands = {f"psdn{v}": make(v) for v in range(C.convn_variants(cout))
-             if C.convn_variant_kind(cout, v) in (0, 3) and C.convn_variant_ok(cout, v, 1, 1, 1, 0, w)}
+             if _kind_ok(C.convn_variant_kind(cout, v)) and C.convn_variant_ok(cout, v, 1, 1, 1, 0, w)}
     how = _at.choose(("tail", "apply", M, cin, cout), cands, next(iter(cands)))
     return int(how[4:])
 
@@ -309,7 +315,7 @@ def _ds_stride(convd):
 def _dual_variants(cout: int, w: int) -> list:
     C = _native()
     return [v for v in range(C.convn_variants(cout))
-            if C.convn_variant_kind(cout, v) in (0, 3) and C.convn_variant_ok(cout, v, 1, 1, 1, 0, w, True)]
+            if _kind_ok(C.convn_variant_kind(cout, v)) and C.convn_variant_ok(cout, v, 1, 1, 1, 0, w, True)]
 
 
 def _gram_moments(x, w2, shift, M: int) -> torch.Tensor:

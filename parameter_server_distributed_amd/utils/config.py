@@ -61,6 +61,7 @@ FEATURES: dict[str, tuple[bool, str]] = {
     "convn_stats": (True, "consumer-BN statistics in the narrow convolution's epilogue"),
     "convn_persist": (True, "persistent layer-1 3x3 kernel (convh)"),
     "convn_p1": (True, "persistent 1x1 kernels (convp / convpr)"),
+    "convn_p2": (True, "the persistent 1x1 kernel at two workgroups per CU (two-slot ring) as a candidate"),
     "convn_bwd": (True, "producing BN's backward reduction in the bwd-data epilogue (modes 1/2)"),
     "convn_bwd3": (True, "the dual-BN tail's reduction in the bwd-data epilogue (mode 3)"),
     "convn_bwd5": (True, "stride-2 downsample gradient added on the quarter grid (mode 5)"),

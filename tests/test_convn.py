@@ -411,33 +411,46 @@ def test_dgrad_s2_phases_exact(gpu, nb, cin, H, cout):
 
 def test_dgrad_s2_in_resnet_block_matches_miopen(gpu, monkeypatch):
     """A stride-2 bottleneck's conv2 bwd-data on the phase kernels (forced, plain and with bn1's
-    reduction fused) vs MIOpen: block input gradient and every parameter gradient."""
+    reduction fused) vs MIOpen, all three against an fp32 composite run of the same block: block
+    input gradient and every parameter gradient at MIOpen's bf16 error level (the BN weight
+    gradients are near-cancelling sums: two bf16 paths differ by several % on them, so each is
+    compared through fp32)."""
+    import copy
+
     import torch.nn as nn
 
     from parameter_server_distributed_amd.models.resnet import Bottleneck, _conv
     from parameter_server_distributed_amd.ops import autotune
     from parameter_server_distributed_amd.ops.bn import FusedBatchNorm2d
 
-    res = []
+    torch.manual_seed(0)
+    blk0 = Bottleneck(256, 128, 2, 64, nn.Sequential(_conv(256, 512, 1, 2), FusedBatchNorm2d(512)))
+    blk0 = blk0.to(gpu).to(memory_format=torch.channels_last)
+    for p in blk0.parameters():
+        p.data = p.data.to(torch.bfloat16)
+    x0 = torch.randn(4, 256, 28, 28, device=gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+
+    def run(blk, x):
+        x = x.clone().requires_grad_(True)
+        blk(x).float().pow(2).mean().backward()
+        return {"dx": x.grad.float(), **{n: p.grad.float() for n, p in blk.named_parameters()}}
+
+    monkeypatch.setenv("PSD_FEATURES", "tail_recompute=0")
+    res = {}
     for force in ("psdnbs0", "psdns0", "miopen"):
         monkeypatch.setenv("PSD_AUTOTUNE_FORCE", force)
-        monkeypatch.setenv("PSD_FEATURES", "tail_recompute=0")
         autotune._DECISIONS.clear()
-        torch.manual_seed(0)
-        blk = Bottleneck(256, 128, 2, 64, nn.Sequential(_conv(256, 512, 1, 2), FusedBatchNorm2d(512)))
-        blk = blk.to(gpu).to(memory_format=torch.channels_last)
-        for p in blk.parameters():
-            p.data = p.data.to(torch.bfloat16)
-        x = torch.randn(4, 256, 28, 28, device=gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        x.requires_grad_(True)
-        y = blk(x)
-        y.float().pow(2).mean().backward()
+        res[force] = run(copy.deepcopy(blk0), x0)
         picks = autotune.decisions()
         got = [v for k, v in picks.items() if k[:2] == ("conv", "dgrad") and k[8] == 2]  # (stride 2)
         assert got == [force], picks
-        res.append({"dx": x.grad.float(), **{n: p.grad.float() for n, p in blk.named_parameters()}})
     autotune._DECISIONS.clear()
-    for r in res[:2]:
-        for n in res[2]:
-            a, b = r[n], res[2][n]
-            assert ((a - b).norm() / b.norm().clamp_min(1e-6)).item() < 2e-2, n
+    ref = run(copy.deepcopy(blk0).float(), x0.float())
+
+    def err(g, n):
+        return ((g[n] - ref[n]).norm() / ref[n].norm().clamp_min(1e-6)).item()
+
+    for force in ("psdnbs0", "psdns0"):
+        for n in ref:
+            assert err(res[force], n) <= 1.5 * err(res["miopen"], n) + 1e-2, (force, n, err(res[force], n),
+                                                                              err(res["miopen"], n))

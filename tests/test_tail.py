@@ -38,7 +38,7 @@ def test_convn_stats_only_and_apply_epilogue_exact(gpu, Nb, H, cin, cout):
     shift = torch.zeros(cout, device=gpu)
     nv = 0
     for v in range(C.convn_variants(cout)):
-        if C.convn_variant_kind(cout, v) not in (0, 3) or not C.convn_variant_ok(cout, v, 1, 1, 1, 0, H):
+        if C.convn_variant_kind(cout, v) not in (0, 3, 4) or not C.convn_variant_ok(cout, v, 1, 1, 1, 0, H):
             continue
         nv += 1
         rows_alloc = max(C.convn_stats_rows(M), C.convn_part_rows(M, cout, v, H, H, 1))
@@ -86,7 +86,7 @@ def test_convn_bwd_epilogue_without_bn_input(gpu, mode):
     s1 = gref.sum(0)
     dyd = dy.to(gpu, torch.bfloat16).contiguous(memory_format=torch.channels_last)
     for v in range(C.convn_variants(N)):
-        if C.convn_variant_kind(N, v) not in (0, 3):
+        if C.convn_variant_kind(N, v) not in (0, 3, 4):
             continue
         out = torch.full((M, N), 7.0, device=gpu, dtype=torch.bfloat16)
         part = torch.full((max(C.convn_stats_rows(M), C.convn_part_rows(M, N, v, H, H, 1)), 2, N), float("nan"),
@@ -332,7 +332,7 @@ def test_tail_statistics_match_fp64(gpu, monkeypatch):
         C.bnfold_gram_stats(P, w2, shift, M, row)
         got["gram"] = row.double()
         for v in range(C.convn_variants(cout)):
-            if C.convn_variant_kind(cout, v) in (0, 3) and C.convn_variant_ok(cout, v, 1, 1, 1, 0, wd):
+            if C.convn_variant_kind(cout, v) in (0, 3, 4) and C.convn_variant_ok(cout, v, 1, 1, 1, 0, wd):
                 part = torch.empty(tail._part_rows(M, cout, v, h, wd, 1), 2, cout, device=gpu, dtype=torch.float32)
                 rows = C.convn_(a2, w2, part, 1, 1, 1, 0, part=part, shift=shift, variant=v, no_store=True)
                 assert rows > 0
