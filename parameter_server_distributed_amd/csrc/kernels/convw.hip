@@ -417,9 +417,9 @@ int pick_tkk(int tco, int KK, int v) {
 constexpr int nslot_of(int tco, int tkk) {
   return (tco + tkk) <= 128 ? 4 : std::min(5, (160 * 1024) / ((tco + tkk) / 64 * kSub));
 }
-int lds_of(int tco, int tkk) {
+int lds_of(int tco, int tkk, bool two = false) {
   if (tco == 384) return 4 * (256 + 64) / 64 * kSub;  // the single-tile fold: 4 dY + 1 x sub-images, 4 slots
-  return nslot_of(tco, tkk) * (tco + tkk) / 64 * kSub;
+  return (two ? 2 : nslot_of(tco, tkk)) * (tco + tkk) / 64 * kSub;
 }
 
 int cu_count() {
@@ -449,13 +449,18 @@ hipError_t launch_t(const ConvwArgs& a, int grid, hipStream_t st) {
 
 }  // namespace
 
-static int tiled_variants(int Cout, int KK) {
+// tile shapes (TCO x TKK) for this launch: the ring as deep as the LDS allows (one workgroup per
+// CU for the wider tiles), then (variant + count) the same shapes on a two-stage ring in half the
+// LDS at two workgroups per CU -- the HBM-bound large-M shapes stall every wave of a lone workgroup
+// at each stage's barrier; a second workgroup's stage runs underneath
+static int tile_shapes(int Cout, int KK) {
   const int tco = tile_co(Cout);  // plain launches (fold launches have one fixed tile)
   if (!tco || KK <= 0 || KK % 64 != 0) return 0;
   int n = 0;
   while (pick_tkk(tco, KK, n)) ++n;
   return n;
 }
+static int tiled_variants(int Cout, int KK) { return 2 * tile_shapes(Cout, KK); }
 
 // + the persistent HALO variant (convhw_kernel) for the 64 -> 64 3x3 shape (KK = 576)
 int convw_variants(int Cout, int KK) { return tiled_variants(Cout, KK) + (Cout == 64 && KK == 576 ? 1 : 0); }
@@ -490,7 +495,14 @@ static void tile_of(const ConvwArgs& a, int& tco, int& tkk) {
     }
     return;
   }
-  tkk = pick_tkk(tco, a.KK, a.variant < 0 ? 0 : a.variant);
+  const int v = a.variant < 0 ? 0 : a.variant, ns = tile_shapes(a.Cout, a.KK);
+  tkk = pick_tkk(tco, a.KK, ns > 0 ? v % ns : v);
+}
+
+// the two-stage-ring twin of a tile shape (plain launches only)
+static bool two_stage(const ConvwArgs& a) {
+  const int ns = tile_shapes(a.Cout, a.KK);
+  return !a.fold && ns > 0 && a.variant >= ns && a.variant < 2 * ns;
 }
 
 bool convw_fold_ok(int Cout, int KK, int Arows) {
@@ -577,7 +589,7 @@ ConvwPlan convw_plan(const ConvwArgs& a) {
   if (!tkk || a.M <= 0) return p;
   const int arows = a.fold ? a.Arows : a.Cout;
   const int ntile = (arows / tco) * (a.KK / tkk);
-  const int occ = std::max(1, std::min(2, (160 * 1024) / lds_of(tco, tkk)));
+  const int occ = std::max(1, std::min(2, (160 * 1024) / lds_of(tco, tkk, two_stage(a))));
   const int total = (a.M + kBP - 1) / kBP;
   // one round of workgroups over the chip, >= 4 stages per split
   int splits = std::max(1, (cu_count() * occ) / ntile);
@@ -631,7 +643,8 @@ hipError_t launch_convw(const ConvwArgs& a_in, hipStream_t st) {
   a.stages_per_split = (total + p.splits - 1) / p.splits;
   const int grid = p.splits * (a.Arows / tco) * (a.KK / tkk);
   hipError_t e = hipErrorNotSupported;
-#define PSD_CONVW(TCO_, TKK_, WR_) launch_t<TCO_, TKK_, WR_, nslot_of(TCO_, TKK_)>(a, grid, st)
+#define PSD_CONVW(TCO_, TKK_, WR_)                                                                \
+  (two_stage(a) ? launch_t<TCO_, TKK_, WR_, 2>(a, grid, st) : launch_t<TCO_, TKK_, WR_, nslot_of(TCO_, TKK_)>(a, grid, st))
   if (tco == 384) {
     e = launch_t<384, 64, 8, 4, 4>(a, grid, st);
   } else if (tco == 64) {

@@ -483,9 +483,10 @@ def _convw_cands(dy, x, k: int, stride: int, pad: int) -> dict:
         return fn
 
     nv = C.convw_variants(cout, kk)
-    if cout == 64 and kk == 576 and not _feat("convw_persist"):
-        nv -= 1  # the persistent HALO wgrad is the last variant of this shape (A/B switch)
-    return {f"psdw{v}": make(v) for v in range(nv)}
+    persist = 1 if (cout == 64 and kk == 576) else 0  # the persistent HALO wgrad: the last variant
+    shapes = (nv - persist) // 2  # tile shapes, then their two-stage-ring twins (kernels/convw.hip)
+    vs = [v for v in range(nv) if (v < shapes or _feat("convw_twostage")) and (v < 2 * shapes or _feat("convw_persist"))]
+    return {f"psdw{v}": make(v) for v in vs}
 
 
 class DelayedScale:

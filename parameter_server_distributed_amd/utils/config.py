@@ -69,6 +69,7 @@ FEATURES: dict[str, tuple[bool, str]] = {
                               "(with the producing BN's backward reduction in the epilogue) vs MIOpen"),
     "convw": (True, "narrow weight-gradient kernel (convw.hip) as a candidate"),
     "convw_persist": (True, "persistent layer-1 3x3 weight gradient (convhw)"),
+    "convw_twostage": (True, "narrow weight-gradient tiles also on a two-stage ring at two workgroups per CU"),
     "gemm_stats": (True, "consumer-BN statistics in the 8-phase GEMM epilogue"),
     # batch norm / bottleneck tail (ops/bn.py, ops/tail.py)
     "bn_fold": (True, "bn3's backward folded into conv3's bwd-data / weight-gradient GEMMs"),
