@@ -120,7 +120,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_elemt_coef", &bn_elemt_coef, py::arg("g"), py::arg("x"), py::arg("coef"));
   m.def("convw_fold_rows", &convw_fold_rows, py::arg("Cout"), py::arg("Cin"));
   m.def("convw_gram_rows", &convw_gram_rows_, py::arg("C"));
-  m.def("convw_gram_", &convw_gram_, py::arg("x"), py::arg("out"));
+  m.def("convw_gram_", &convw_gram_, py::arg("x"), py::arg("out"), py::arg("variant") = 0);
   m.def("bnfold_dgrad_weights", &bnfold_dgrad_weights, py::arg("w"), py::arg("coef"));
   m.def("bnfold_rowdot", &bnfold_rowdot, py::arg("P"), py::arg("w"), py::arg("row"));
   m.def("bnfold_gram_stats", &bnfold_gram_stats, py::arg("P"), py::arg("w"), py::arg("shift"), py::arg("M"),

@@ -591,7 +591,7 @@ at::Tensor stem_wgrad(const at::Tensor& x_in, const at::Tensor& dy_in) {
   const int64_t N = x.size(0), H = x.size(2), W = x.size(3), Ho = H / 2, Wo = W / 2;
   TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && dy.sizes() == at::IntArrayRef({N, 64, Ho, Wo}), "psd stem wgrad: dy shape");
   TORCH_CHECK(stem_wgrad_supported((int)H, (int)W, (int)Ho, (int)Wo), "psd stem wgrad: unsupported input ", x.sizes());
-  const int nblk = stem_wgrad_blocks((int)N, (int)Ho);
+  const int nblk = stem_wgrad_blocks((int)N, (int)Ho, (int)Wo);
   at::Tensor part = at::empty({(int64_t)nblk * 192 * 64}, x.options().dtype(at::kFloat));
   at::Tensor dw = at::empty({64, 3, 7, 7}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   hipError_t e = launch_stem_wgrad(reinterpret_cast<const uint16_t*>(x.data_ptr()),

@@ -824,7 +824,7 @@ int64_t convw_gram_rows_(int64_t C) { return convw_gram_rows((int)C); }
 // out = fp32 [convw_gram_rows(C), C]: rows [0, C) the Gram matrix x^T x of the [M, C] pixel rows of
 // x, row C their column sums -- one read of x (the BN statistics of y = x W^T without forming y:
 // ops/tail.py). False when the shape is unsupported.
-bool convw_gram_(const at::Tensor& x, at::Tensor out) {
+bool convw_gram_(const at::Tensor& x, at::Tensor out, int64_t variant) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.scalar_type() == at::kBFloat16 &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast),
               "psd convw_gram: x must be a channels_last bf16 tensor");
@@ -855,6 +855,7 @@ bool convw_gram_(const at::Tensor& x, at::Tensor out) {
   a.stride = 1;
   a.pad = 0;
   a.fold = 2;
+  a.variant = (int)variant;  // 1: the two-stage ring at two workgroups per CU
   a.Arows = (int)rows;
   const ConvwPlan p = convw_plan(a);
   if (p.splits <= 0) return false;

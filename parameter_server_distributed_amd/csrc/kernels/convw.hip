@@ -418,7 +418,7 @@ constexpr int nslot_of(int tco, int tkk) {
   return (tco + tkk) <= 128 ? 4 : std::min(5, (160 * 1024) / ((tco + tkk) / 64 * kSub));
 }
 int lds_of(int tco, int tkk, bool two = false) {
-  if (tco == 384) return 4 * (256 + 64) / 64 * kSub;  // the single-tile fold: 4 dY + 1 x sub-images, 4 slots
+  if (tco == 384) return (two ? 2 : 4) * (256 + 64) / 64 * kSub;  // the single-tile fold: 4 dY + 1 x sub-images
   return (two ? 2 : nslot_of(tco, tkk)) * (tco + tkk) / 64 * kSub;
 }
 
@@ -499,8 +499,9 @@ static void tile_of(const ConvwArgs& a, int& tco, int& tkk) {
   tkk = pick_tkk(tco, a.KK, ns > 0 ? v % ns : v);
 }
 
-// the two-stage-ring twin of a tile shape (plain launches only)
+// the two-stage-ring twin of a tile shape (fold / Gram launches: variant 1)
 static bool two_stage(const ConvwArgs& a) {
+  if (a.fold) return a.variant == 1;
   const int ns = tile_shapes(a.Cout, a.KK);
   return !a.fold && ns > 0 && a.variant >= ns && a.variant < 2 * ns;
 }
@@ -539,7 +540,7 @@ static ConvwPlan gram_plan(const ConvwArgs& a) {
   gram_tile(a.KK, tco, tkk, ns);
   if (!tco || a.M <= 0 || a.Arows != convw_gram_rows(a.KK)) return p;
   const int ntile = a.Arows / tco;
-  const int occ = std::max(1, std::min(2, (160 * 1024) / (ns * tkk / 64 * kSub)));
+  const int occ = std::max(1, std::min(2, (160 * 1024) / ((two_stage(a) ? 2 : ns) * tkk / 64 * kSub)));
   const int total = (a.M + kBP - 1) / kBP;
   int splits = std::max(1, (cu_count() * occ) / ntile);
   splits = std::min(splits, std::max(1, total / 4));
@@ -566,9 +567,10 @@ static hipError_t launch_gram(const ConvwArgs& a_in, hipStream_t st) {
   a.stages_per_split = (total + p.splits - 1) / p.splits;
   const int grid = p.splits * (a.Arows / tco);
   hipError_t e;
-  if (a.KK == 64) e = launch_t<128, 64, 4, 5, 0>(a, grid, st);
-  else if (a.KK == 128) e = launch_t<256, 128, 4, 5, 0>(a, grid, st);
-  else e = launch_t<128, 256, 2, 4, 0>(a, grid, st);
+  const bool two = two_stage(a);
+  if (a.KK == 64) e = two ? launch_t<128, 64, 4, 2, 0>(a, grid, st) : launch_t<128, 64, 4, 5, 0>(a, grid, st);
+  else if (a.KK == 128) e = two ? launch_t<256, 128, 4, 2, 0>(a, grid, st) : launch_t<256, 128, 4, 5, 0>(a, grid, st);
+  else e = two ? launch_t<128, 256, 2, 2, 0>(a, grid, st) : launch_t<128, 256, 2, 4, 0>(a, grid, st);
   if (e != hipSuccess) return e;
   const int64_t mn = (int64_t)a.Arows * a.KK;
   return launch_splitk_reduce(a.slab, a.splits, mn, a.out, 0, 0, 1.f, st, a.slab + (int64_t)a.splits * mn);
@@ -646,7 +648,7 @@ hipError_t launch_convw(const ConvwArgs& a_in, hipStream_t st) {
 #define PSD_CONVW(TCO_, TKK_, WR_)                                                                \
   (two_stage(a) ? launch_t<TCO_, TKK_, WR_, 2>(a, grid, st) : launch_t<TCO_, TKK_, WR_, nslot_of(TCO_, TKK_)>(a, grid, st))
   if (tco == 384) {
-    e = launch_t<384, 64, 8, 4, 4>(a, grid, st);
+    e = two_stage(a) ? launch_t<384, 64, 8, 2, 4>(a, grid, st) : launch_t<384, 64, 8, 4, 4>(a, grid, st);
   } else if (tco == 64) {
     if (tkk == 256) e = PSD_CONVW(64, 256, 2);
     else if (tkk == 192) e = PSD_CONVW(64, 192, 2);

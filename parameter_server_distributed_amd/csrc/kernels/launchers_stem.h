@@ -14,7 +14,7 @@ hipError_t launch_stem_conv(const uint16_t* x, const uint16_t* wk, uint16_t* y, 
 // from the image x and the conv-output gradient dy [N, Ho, Wo, 64]; part = stem_wgrad_blocks() x
 // 192 x 64 fp32 workspace.
 bool stem_wgrad_supported(int H, int W, int Ho, int Wo);
-int stem_wgrad_blocks(int N, int Ho);
+int stem_wgrad_blocks(int N, int Ho, int Wo);
 hipError_t launch_stem_wgrad(const uint16_t* x, const uint16_t* dy, float* part, uint16_t* dw, int N, int H, int W,
                              int Ho, int Wo, hipStream_t stream);
 }  // namespace psd

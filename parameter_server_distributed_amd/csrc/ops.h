@@ -117,7 +117,7 @@ bool convw_(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64_t R
             int64_t pad, int64_t variant, bool accumulate, bool fold);
 int64_t convw_fold_rows(int64_t Cout, int64_t Cin);
 int64_t convw_gram_rows_(int64_t C);
-bool convw_gram_(const at::Tensor& x, at::Tensor out);
+bool convw_gram_(const at::Tensor& x, at::Tensor out, int64_t variant);
 int64_t convw_variants_(int64_t Cout, int64_t KK);
 int64_t conv_fwd_fp8_(const at::Tensor& x, const at::Tensor& w2, const at::Tensor& x_scale, const at::Tensor& w_scale,
                       at::Tensor out, int64_t R, int64_t S, int64_t stride, int64_t pad, c10::optional<at::Tensor> part,

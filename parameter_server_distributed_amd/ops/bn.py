@@ -305,7 +305,7 @@ class _BNAddBNReluFn(torch.autograd.Function):
             for conv_, xin_ in ((c3, a2), (cd, xin)):
                 P = torch.empty(C.convw_fold_rows(conv_.weight.shape[0], conv_.weight.shape[1]), xin_.shape[1],
                                 device=g.device, dtype=torch.float32)
-                if not C.convw_(g, xin_, P, 1, 1, 1, 0, fold=True):
+                if not C.convw_(g, xin_, P, 1, 1, 1, 0, variant=int(_feat("convw_fold2")), fold=True):
                     raise RuntimeError("psd dual tail: convw_ declined the fold wgrad")
                 Ps.append(P)
             # the downsample BN's sums derive from bn3's sum g (same masked g) and its own sum g yd

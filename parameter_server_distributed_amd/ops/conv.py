@@ -525,6 +525,11 @@ def _sink_view(mod, weight):
     return sink(weight) if sink is not None else None
 
 
+def _fold_v() -> int:
+    """convw variant of the fold / Gram launches: 1 = the two-stage ring at two workgroups per CU."""
+    return 1 if _feat("convw_fold2") else 0
+
+
 def fold_ok(cin: int, cout: int) -> bool:
     """The BN-backward fold of a 1x1 convolution (cin -> cout) runs on our kernels for this shape:
     the K-concatenated dgrad on the narrow kernel and the fold wgrad (kernels/convw.hip)."""
@@ -570,7 +575,7 @@ def _fold_backward(ctx, fold, x, weight, need_x: bool, need_w: bool, P=None):
         Pw = P
         if Pw is None:
             Pw = torch.empty(frows, cin, device=g.device, dtype=torch.float32)
-            if not C.convw_(g, x, Pw, 1, 1, 1, 0, fold=True):
+            if not C.convw_(g, x, Pw, 1, 1, 1, 0, variant=_fold_v(), fold=True):
                 raise RuntimeError("convw_ declined a fold shape convw_fold_rows accepted")
         C.bnfold_combine(Pw, weight, coef, into)
 

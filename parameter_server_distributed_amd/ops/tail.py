@@ -39,7 +39,7 @@ import torch
 
 from ..utils.config import feature as _feat
 from . import autotune as _at
-from .conv import (Conv1x1, ConvNHWC, _fold_backward, _from_2d, _fwd_records, _native, _part_rows, _sink_view,
+from .conv import (Conv1x1, ConvNHWC, _fold_backward, _fold_v, _from_2d, _fwd_records, _native, _part_rows, _sink_view,
                    fold_ok)
 from .bn import FusedBatchNorm2d, StridedDr, take_dr
 
@@ -120,7 +120,7 @@ def _stats_route(a2, w2, M: int, cin: int, cout: int, v: int, h: int, w: int, sh
 
     def gram():
         P = torch.empty(C.convw_gram_rows(cin), cin, device=dev, dtype=torch.float32)
-        if not C.convw_gram_(a2, P):
+        if not C.convw_gram_(a2, P, variant=_fold_v()):
             raise _at.Declined("convw Gram launch")
         row = torch.empty(2, cout, device=dev, dtype=torch.float32)
         C.bnfold_gram_stats(P, w2, shift, M, row)
@@ -151,7 +151,7 @@ class _TailFn(torch.autograd.Function):
             # sum y = W s, sum y^2 = W^T G W from one read of a2 (G = a2^T a2, s = 1^T a2: the Gram
             # launch of the weight-gradient kernel) -- the GEMM is not recomputed for the statistics
             P = torch.empty(C.convw_gram_rows(cin), cin, device=a2.device, dtype=torch.float32)
-            if not C.convw_gram_(a2, P):
+            if not C.convw_gram_(a2, P, variant=_fold_v()):
                 raise RuntimeError("psd tail: convw declined the Gram launch")
             part = torch.empty(1, 2, cout, device=a2.device, dtype=torch.float32)
             C.bnfold_gram_stats(P, w2, bn.running_mean, M, part[0])
@@ -203,7 +203,7 @@ class _TailFn(torch.autograd.Function):
             if part.shape[0] <= rows:
                 raise RuntimeError("psd tail: the partials buffer has no row for sum g y")
             P = torch.empty(C.convw_fold_rows(cout, cin), cin, device=dy.device, dtype=torch.float32)
-            if not C.convw_(g, a2, P, 1, 1, 1, 0, fold=True):
+            if not C.convw_(g, a2, P, 1, 1, 1, 0, variant=_fold_v(), fold=True):
                 raise RuntimeError("psd tail: convw_ declined the fold wgrad")
             C.bnfold_rowdot(P, weight, part[rows])
             g, coef, dg, db = C.bn_bwd_coef(g, g, gamma, mean, invstd, part=part, rows=rows + 1, dgamma_out=dgo,
@@ -323,7 +323,7 @@ def _gram_moments(x, w2, shift, M: int) -> torch.Tensor:
     C = _native()
     cin = x.shape[1]
     P = torch.empty(C.convw_gram_rows(cin), cin, device=x.device, dtype=torch.float32)
-    if not C.convw_gram_(x, P):
+    if not C.convw_gram_(x, P, variant=_fold_v()):
         raise RuntimeError("psd dual tail: convw declined the Gram launch")
     part = torch.empty(1, 2, w2.shape[0], device=x.device, dtype=torch.float32)
     C.bnfold_gram_stats(P, w2, shift, M, part[0])
@@ -426,7 +426,7 @@ class _DualTailFn(torch.autograd.Function):
             Ps = []
             for inp, cin in ((a2, c3), (xin, cd)):
                 P = torch.empty(C.convw_fold_rows(cout, cin), cin, device=g.device, dtype=torch.float32)
-                if not C.convw_(g, inp, P, 1, 1, 1, 0, fold=True):
+                if not C.convw_(g, inp, P, 1, 1, 1, 0, variant=_fold_v(), fold=True):
                     raise RuntimeError("psd dual tail: convw_ declined the fold wgrad")
                 Ps.append(P)
             # the downsample BN's sums derive from bn3's sum g (same masked g) and its own sum g yd

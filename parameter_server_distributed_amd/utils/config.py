@@ -70,6 +70,7 @@ FEATURES: dict[str, tuple[bool, str]] = {
     "convw": (True, "narrow weight-gradient kernel (convw.hip) as a candidate"),
     "convw_persist": (True, "persistent layer-1 3x3 weight gradient (convhw)"),
     "convw_twostage": (True, "narrow weight-gradient tiles also on a two-stage ring at two workgroups per CU"),
+    "convw_fold2": (True, "the BN-fold and Gram weight-gradient launches on the two-stage ring (two workgroups per CU)"),
     "gemm_stats": (True, "consumer-BN statistics in the 8-phase GEMM epilogue"),
     # batch norm / bottleneck tail (ops/bn.py, ops/tail.py)
     "bn_fold": (True, "bn3's backward folded into conv3's bwd-data / weight-gradient GEMMs"),

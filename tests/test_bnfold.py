@@ -38,15 +38,18 @@ def test_convn_x2_bias_exact(gpu, cin, c2, cout):
         torch.testing.assert_close(out.float().cpu(), ref.bfloat16().float(), rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("variant", [0, 1])
 @pytest.mark.parametrize("cout,cin", [(256, 64), (512, 128), (1024, 256)])
-def test_convw_fold_exact(gpu, cout, cin):
-    """P = [g | x | 1]^T x (fp32, padded rows zero-free): g^T x, the Gram matrix and column sums."""
+def test_convw_fold_exact(gpu, cout, cin, variant):
+    """P = [g | x | 1]^T x (fp32, padded rows zero-free): g^T x, the Gram matrix and column sums
+    (variant 1: the two-stage ring at two workgroups per CU)."""
     gen = torch.Generator().manual_seed(9)
     g, x = _ints((2, cout, 13, 7), gen), _ints((2, cin, 13, 7), gen)
     rows = native().convw_fold_rows(cout, cin)
     P = torch.full((rows, cin), 7.0, device=gpu)
     assert native().convw_(g.to(gpu, torch.bfloat16).contiguous(memory_format=CL),
-                           x.to(gpu, torch.bfloat16).contiguous(memory_format=CL), P, 1, 1, 1, 0, fold=True)
+                           x.to(gpu, torch.bfloat16).contiguous(memory_format=CL), P, 1, 1, 1, 0, variant=variant,
+                           fold=True)
     g2, x2 = g.permute(0, 2, 3, 1).reshape(-1, cout), x.permute(0, 2, 3, 1).reshape(-1, cin)
     P = P.cpu()
     torch.testing.assert_close(P[:cout], g2.t() @ x2, rtol=0, atol=0)

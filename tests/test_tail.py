@@ -113,8 +113,9 @@ def test_bnfold_rowdot(gpu):
     torch.testing.assert_close(row[1].double().cpu(), want, rtol=1e-5, atol=1e-4)
 
 
+@pytest.mark.parametrize("variant", [0, 1])
 @pytest.mark.parametrize("Nb,H,cin,cout", [(2, 14, 64, 256), (3, 7, 128, 512), (1, 9, 256, 1024)])
-def test_bnfold_gram_stats_exact(gpu, Nb, H, cin, cout):
+def test_bnfold_gram_stats_exact(gpu, Nb, H, cin, cout, variant):
     """Gram statistics: the Gram launch gives G = x^T x and s = 1^T x from one read of x; then per
     channel (sum y - M k, sum y^2 - 2 k sum y + M k^2) = shifted sums of y = x W^T, never formed."""
     C = native()
@@ -128,7 +129,7 @@ def test_bnfold_gram_stats_exact(gpu, Nb, H, cin, cout):
     d = y - k.double()
     xd = x.to(gpu, torch.bfloat16).contiguous(memory_format=torch.channels_last)
     P = torch.full((C.convw_gram_rows(cin), cin), float("nan"), device=gpu)
-    assert C.convw_gram_(xd, P)
+    assert C.convw_gram_(xd, P, variant=variant)
     xm = x.permute(0, 2, 3, 1).reshape(M, cin).double()
     torch.testing.assert_close(P[:cin].double().cpu(), xm.t() @ xm, rtol=0, atol=0)
     torch.testing.assert_close(P[cin].double().cpu(), xm.sum(0), rtol=0, atol=0)
