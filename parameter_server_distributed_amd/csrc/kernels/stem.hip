@@ -352,27 +352,12 @@ bool stem_wgrad_supported(int H, int W, int Ho, int Wo) {
          kWgInRows * (6 * Wo + 24) / 8 <= 256 * kWgPatchIt && kWgRows * Wo * 8 <= 256 * kWgDyIt;
 }
 
-static int stem_cus() {
-  static int n = 0;
-  if (!n) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        n <= 0)
-      n = 256;
-  }
-  return n;
-}
-
-// one round of resident workgroups: the LDS (patch + transposed dY, 41 KiB at Wo = 112) allows 3 per
-// CU and the registers 4, so the former fixed 1024-workgroup grid ran as 768 + a 256-workgroup tail
-// round (the grid-stride item loop then gave a third of the CUs a second round)
+// (a grid capped at the resident workgroups -- 3 per CU by LDS -- measured slower: 1,013 vs 914 us,
+// profiles/r5/resnet50_b1024_r5e_kernels.md vs r5d)
 int stem_wgrad_blocks(int N, int Ho, int Wo) {
+  (void)Wo;
   const int items = N * (Ho / kWgRows);
-  const int lds = (kWgInRows * (6 * Wo + 24) + 64 * (kWgRows * Wo + 8)) * 2;
-  int per_cu = lds > 0 ? (160 * 1024) / lds : 4;
-  per_cu = per_cu < 1 ? 1 : (per_cu > 4 ? 4 : per_cu);
-  const int cap = per_cu * stem_cus();
-  return items < cap ? (items < 1 ? 1 : items) : cap;
+  return items < 1024 ? (items < 1 ? 1 : items) : 1024;
 }
 
 hipError_t launch_stem_wgrad(const uint16_t* x, const uint16_t* dy, float* part, uint16_t* dw, int N, int H, int W,
