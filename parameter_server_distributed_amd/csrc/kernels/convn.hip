@@ -235,15 +235,82 @@ __device__ __forceinline__ void convn_flush(const ConvnArgs& a, EpiSums<WNT / 16
   }
 }
 
+// The epilogue's per-row operands of one wave's 64 rows (the pixel index of each row this lane
+// stores, and for the BN-backward modes the BN input x / residual gradient dr / ReLU bits / the dual
+// tail's xd; for the apply mode the residual). epi_load issues the loads; a persistent kernel can
+// issue them for its NEXT tile before that tile's MFMA loop (convh_kernel), so the loads' latency
+// hides behind the taps instead of stalling the epilogue -- at one wave per SIMD nothing else does.
+template <int WNT>
+struct EpiOps {
+  static constexpr int CPR = WNT * 2 / 16;
+  static constexpr int PASSES = 16 * CPR / 64;
+  int mm[4][PASSES];
+  u32x4 exr[4][PASSES], rv4[4][PASSES], dv4[4][PASSES];
+  uint32_t bt[4][PASSES];
+};
+
+template <int WNT, int BWD, typename Pix>
+__device__ __forceinline__ void epi_load(const ConvnArgs& a, int wr, int wc, int lane, Pix pix, int n0, EpiOps<WNT>& o) {
+  constexpr bool BRED = BWD >= 1 && BWD <= 5;
+  constexpr bool APPLY = BWD == 8;
+  constexpr int CPR = EpiOps<WNT>::CPR, PASSES = EpiOps<WNT>::PASSES;
+  const int my_col = n0 + wc * WNT + (lane % CPR) * 8;
+  const bool has_bx = !BRED || a.bx != nullptr;
+  const bool fast_div = a.M < (1 << 24);
+  float inv_hw = 0.f, inv_wo = 0.f;
+  if constexpr (BWD == 5) {
+    inv_hw = 1.f / (float)(a.Ho * a.Wo);
+    inv_wo = 1.f / (float)a.Wo;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int ps = 0; ps < PASSES; ++ps) {
+      const int c = ps * 64 + lane;
+      const int rr = c / CPR;
+      const int m = pix(wr * 64 + i * 16 + rr);
+      o.mm[i][ps] = m;
+      if constexpr (APPLY) {
+        o.rv4[i][ps] = u32x4{0u, 0u, 0u, 0u};
+        if (m >= 0 && a.ares) o.rv4[i][ps] = *reinterpret_cast<const u32x4*>(a.ares + (int64_t)m * a.N + my_col);
+      }
+      if constexpr (BRED) {
+        o.exr[i][ps] = o.rv4[i][ps] = o.dv4[i][ps] = u32x4{0u, 0u, 0u, 0u};
+        o.bt[i][ps] = 0u;
+        if (m >= 0) {
+          if (has_bx) o.exr[i][ps] = *reinterpret_cast<const u32x4*>(a.bx + (int64_t)m * a.N + my_col);
+          if constexpr (BWD >= 2) {
+            if constexpr (BWD == 5) {
+              // residual-branch gradient of a stride-2 1x1 (downsample) convolution, on the quarter
+              // grid: non-zero only at even (h, w) of this (Ho x Wo) output grid
+              const int hw = a.Ho * a.Wo;
+              const int n = fast_div ? fdiv(m, hw, inv_hw) : m / hw, rem = m - n * hw;
+              const int h = fast_div ? fdiv(rem, a.Wo, inv_wo) : rem / a.Wo, w = rem - h * a.Wo;
+              if (((h | w) & 1) == 0) {
+                const int64_t q = ((int64_t)n * (a.Ho >> 1) + (h >> 1)) * (a.Wo >> 1) + (w >> 1);
+                o.rv4[i][ps] = *reinterpret_cast<const u32x4*>(a.bdr + q * a.N + my_col);
+              }
+            } else {
+              o.rv4[i][ps] = *reinterpret_cast<const u32x4*>(a.bdr + (int64_t)m * a.N + my_col);
+            }
+            o.bt[i][ps] = a.bmbits[((int64_t)m * a.N + my_col) >> 3];
+          }
+          if constexpr (BWD == 3) o.dv4[i][ps] = *reinterpret_cast<const u32x4*>(a.bxd + (int64_t)m * a.N + my_col);
+        }
+      }
+    }
+}
+
 // Epilogue of one wave's 64 x WNT accumulator block (shared by the gathered kernel, the persistent
 // HALO kernel and the persistent 1x1 kernel): per-wave, no barrier (``stg`` is this wave's own 2 KiB of LDS). C layout
 // of a 16x16 block: col = lane & 15, row = 4 * (lane >> 4) + r. ``pix(p)``: output pixel of tile row
 // p (-1: none). The reductions accumulate into ``es``; without DEFER they are flushed here to
 // partial row (tm * WM + wr).
-template <int BM, int BN, int WNT, bool STATS, int BWD, bool DEFER = false, typename Pix>
+template <int BM, int BN, int WNT, bool STATS, int BWD, bool DEFER = false, bool PRE = false, typename Pix>
 __device__ __forceinline__ void convn_epilogue(const ConvnArgs& a, f32x4 (&acc)[4][WNT / 16],
                                                const float (&kshift)[WNT / 16], int tm, int wr, int wc, int lane,
-                                               uint8_t* stg, Pix pix, int n0, EpiSums<WNT / 16>& es) {
+                                               uint8_t* stg, Pix pix, int n0, EpiSums<WNT / 16>& es,
+                                               const EpiOps<WNT>* pre = nullptr) {
   constexpr int JN = WNT / 16;
   constexpr int WM = BM / 64;
   const int cl = lane & 15, rq = (lane >> 4) * 4;
@@ -328,64 +395,26 @@ __device__ __forceinline__ void convn_epilogue(const ConvnArgs& a, f32x4 (&acc)[
   const int my_c16 = lane % CPR;
   const int my_col = n0 + wc * WNT + my_c16 * 8;
   float bmu[8], bsc[8], bsh[8], bmd[8];
-  float inv_hw = 0.f, inv_wo = 0.f;
-  const bool fast_div = a.M < (1 << 24);
-  if constexpr (BWD == 5) {
-    inv_hw = 1.f / (float)(a.Ho * a.Wo);
-    inv_wo = 1.f / (float)a.Wo;
-  }
   if constexpr (BWD == 3) load8_f32(a.bmean_d + my_col, bmd);
   if constexpr (BRED) load8_f32(a.bmean + my_col, bmu);
   if constexpr (BWD == 1) {
     load8_f32(a.bss + my_col, bsc);
     load8_f32(a.bss + a.N + my_col, bsh);
   }
-  // modes 2 / 3 / 5 without the BN input (bx null: a BN whose input was never stored, ops/tail.py):
-  // x is taken as 0, so the second partial is -mean * sum g (the caller adds sum g x itself)
-  const bool has_bx = !BRED || a.bx != nullptr;
-  // BWD: the epilogue operands of all this wave's rows (x, dr, mask bits, xd) are requested here,
-  // before the first is used -- the compiler cannot hoist them above the y stores (possible alias),
-  // and at one workgroup per CU (LDS) the per-row load -> use latency was the epilogue's cost
-  int mm[4][PASSES];
-  u32x4 exr[4][PASSES], rv4[4][PASSES], dv4[4][PASSES];
-  uint32_t bt[4][PASSES];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int ps = 0; ps < PASSES; ++ps) {
-      const int c = ps * 64 + lane;
-      const int rr = c / CPR;
-      const int m = pix(wr * 64 + i * 16 + rr);
-      mm[i][ps] = m;
-      if constexpr (APPLY) {
-        rv4[i][ps] = u32x4{0u, 0u, 0u, 0u};
-        if (m >= 0 && a.ares) rv4[i][ps] = *reinterpret_cast<const u32x4*>(a.ares + (int64_t)m * a.N + my_col);
-      }
-      if constexpr (BRED) {
-        exr[i][ps] = rv4[i][ps] = dv4[i][ps] = u32x4{0u, 0u, 0u, 0u};
-        bt[i][ps] = 0u;
-        if (m >= 0) {
-          if (has_bx) exr[i][ps] = *reinterpret_cast<const u32x4*>(a.bx + (int64_t)m * a.N + my_col);
-          if constexpr (BWD >= 2) {
-            if constexpr (BWD == 5) {
-              // residual-branch gradient of a stride-2 1x1 (downsample) convolution, on the quarter
-              // grid: non-zero only at even (h, w) of this (Ho x Wo) output grid
-              const int hw = a.Ho * a.Wo;
-              const int n = fast_div ? fdiv(m, hw, inv_hw) : m / hw, rem = m - n * hw;
-              const int h = fast_div ? fdiv(rem, a.Wo, inv_wo) : rem / a.Wo, w = rem - h * a.Wo;
-              if (((h | w) & 1) == 0) {
-                const int64_t q = ((int64_t)n * (a.Ho >> 1) + (h >> 1)) * (a.Wo >> 1) + (w >> 1);
-                rv4[i][ps] = *reinterpret_cast<const u32x4*>(a.bdr + q * a.N + my_col);
-              }
-            } else {
-              rv4[i][ps] = *reinterpret_cast<const u32x4*>(a.bdr + (int64_t)m * a.N + my_col);
-            }
-            bt[i][ps] = a.bmbits[((int64_t)m * a.N + my_col) >> 3];
-          }
-          if constexpr (BWD == 3) dv4[i][ps] = *reinterpret_cast<const u32x4*>(a.bxd + (int64_t)m * a.N + my_col);
-        }
-      }
-    }
+  // the epilogue operands of all this wave's rows (x, dr, mask bits, xd): issued here, before the
+  // first is used -- the compiler cannot hoist them above the y stores (possible alias), and at one
+  // workgroup per CU (LDS) the per-row load -> use latency was the epilogue's cost -- or (PRE) by
+  // the caller before this tile's MFMA loop. (modes 2 / 3 / 5 without the BN input -- bx null: a BN
+  // whose input was never stored, ops/tail.py -- take x as 0, so the second partial is -mean * sum g
+  // and the caller adds sum g x itself)
+  EpiOps<WNT> own;
+  if constexpr (!PRE) epi_load<WNT, BWD>(a, wr, wc, lane, pix, n0, own);
+  const EpiOps<WNT>& ops = PRE ? *pre : own;
+  const auto& mm = ops.mm;
+  const auto& exr = ops.exr;
+  const auto& rv4 = ops.rv4;
+  const auto& dv4 = ops.dv4;
+  const auto& bt = ops.bt;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int r = rq + L;  // this lane's row within the 16-row block after quad_t4
@@ -942,6 +971,14 @@ __global__ __launch_bounds__(256) void convh_kernel(ConvnArgs a, int ntiles) {
   uint8_t* stg = smem + kHxW + 2 * kHxWin + wid * 2048;
   EpiSums<2> es;  // this wave's reductions over all its tiles: one partial row per (workgroup, wave row)
   es.zero();
+  // output pixel of row p of tile tl (2 output rows x 64 slots; -1 outside the image)
+  auto pix_of = [&](int tl) {
+    const int n = tl / tpi, ho0 = (tl - n * tpi) * 2;
+    return [=](int p) -> int {
+      const int j = p >> 6, wo = p & 63;
+      return ((wo < a.Wo) & (ho0 + j < a.Ho)) ? (n * a.Ho + ho0 + j) * a.Wo + wo : -1;
+    };
+  };
   for (int tile = t_begin, it = 0; tile < t_end; ++tile, ++it) {
     const int b = it & 1;
     if (tile + 1 < t_end) stage(tile + 1, b ^ 1);  // lands under this tile's taps + epilogue
@@ -987,15 +1024,12 @@ __global__ __launch_bounds__(256) void convh_kernel(ConvnArgs a, int ntiles) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[cb][ks][i], fb[cb][ks][j], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     }
-    const int n = tile / tpi, ho0 = (tile - n * tpi) * 2;
-    auto pix = [&](int p) -> int {
-      const int j = p >> 6, wo = p & 63;
-      return ((wo < a.Wo) & (ho0 + j < a.Ho)) ? (n * a.Ho + ho0 + j) * a.Wo + wo : -1;
-    };
     // this wave's DMA of the next window landed (issued before the taps: nothing to wait for by
-    // now) -- BEFORE the epilogue, so the drain never waits on the epilogue's own stores
+    // now) -- BEFORE the epilogue, so the drain never waits on the epilogue's own stores. (Loading the
+    // epilogue operands one tile ahead, before the taps -- epi_load with PRE -- measured slower for
+    // the mode-1 dgrad: 0.470 vs 0.445 ms, profiles/r5/resnet50_b1024_r5g_autotune.txt)
     wait_vm<0>();
-    convn_epilogue<128, 64, 32, STATS, BWD, true>(a, acc, kshift, tile, wr, wc, lane, stg, pix, 0, es);
+    convn_epilogue<128, 64, 32, STATS, BWD, true>(a, acc, kshift, tile, wr, wc, lane, stg, pix_of(tile), 0, es);
     __syncthreads();  // every wave's: the next window is complete and this one no longer read
   }
   convn_flush<32, STATS, BWD>(a, es, (int64_t)blockIdx.x * 2 + wr, wc, lane, 0);
