@@ -1085,11 +1085,12 @@ class _ConvFn(torch.autograd.Function):
                 key = ("dgrad", n, cin, h, w, cout, k, stride)
                 dx = _dgrad_route(("conv",) + key, cands, "miopen", fu, x)
             elif stride == 2 and k == 3 and pad == 1 and h == 2 * dy.shape[2] and w == 2 * dy.shape[3] \
-                    and _psdn_ok(cout, cin) and not ctx.fp8 and _feat("dgrad_s2_phase") \
+                    and _psdn_ok(cout, cin) and _feat("dgrad_s2_phase") \
                     and x.is_contiguous(memory_format=torch.channels_last) \
                     and dy.is_contiguous(memory_format=torch.channels_last):
                 # four output-parity phases of the narrow kernel vs MIOpen (its bwd-data zero-fills dX
-                # first), with bn1's backward reduction in the epilogue where that wins
+                # first), with bn1's backward reduction in the epilogue where that wins (bf16, as the
+                # fp8 convolutions' strided bwd-data was: Wide-ResNet-101-2's layer 2-4 conv2)
                 fu = _bn_bwd_fusion(ctx.bn_in, x)
                 if fu is not None and fu["mode"] != 1:
                     fu = None
