@@ -315,11 +315,13 @@ def main():
     step_log = os.environ.get("PSD_STEP_LOG", "0") == "1"  # host time of each step() call (diagnosis)
     ts = []
     t0 = time.perf_counter()
+    c0 = time.thread_time()  # this (launching) thread's CPU time: how close the step is to host-bound
     loss = None
     for _ in range(a.steps):
         loss = tr.step()
         if step_log:
             ts.append(time.perf_counter())
+    host_cpu_ms = (time.thread_time() - c0) / max(a.steps, 1) * 1e3
     torch.cuda.synchronize(dev)
     barrier()
     el = time.perf_counter() - t0
@@ -410,6 +412,7 @@ def main():
             "staleness_p50": p50, "staleness_hist": hist, "final_loss": round(final_loss, 4),
             "params_finite": params_finite, "comm_probe_busbw_GBps": probe, "async_plane_bw": async_bw,
             "warmup_s": round(t_w, 2), "peak_mem_gb": round(mem_peak / 2**30, 2),
+            "host_cpu_ms_per_step": round(host_cpu_ms, 2),  # rank 0 launching thread (CPU time, not wall)
             "autotune": autotune_summary(),
             "autotune_source": at_src,
         }
