@@ -339,11 +339,14 @@ def _s2_phase_weights(weight: torch.Tensor) -> list:
     phase k = ph << 1 | pw takes taps r in (1,) / (2, 0) and s alike -- bf16 [Ci, R' S' Co] in
     (dr, ds, co) order: W'[ci][dr][ds][co] = W[co][ci][r(dr)][s(ds)]."""
     cin = weight.shape[1]
-    taps = ((1,), (2, 0))
+    # tap subsets by slicing only: r in (1,) = [1:2], r in (2, 0) = [0::2] reversed. (Indexing with a
+    # Python list uploads the index tensor host -> device on every call: 24 blocking copies per
+    # ResNet-50 step, each leaving the GPU idle ~25 us, profiles/r5/resnet50_b1024_r5g_kernels.md.)
+    sel = (lambda t, d: t.narrow(d, 1, 1), lambda t, d: t[(slice(None),) * d + (slice(None, None, 2),)].flip(d))
     out = []
     for ph in (0, 1):
         for pw in (0, 1):
-            wsel = weight[:, :, list(taps[ph])][:, :, :, list(taps[pw])]
+            wsel = sel[pw](sel[ph](weight, 2), 3)
             out.append(wsel.permute(1, 2, 3, 0).reshape(cin, -1).contiguous())
     return out
 
