@@ -64,9 +64,15 @@ def _dgrad_route(key: tuple, dy2: torch.Tensor, w: torch.Tensor, dx: torch.Tenso
     def blas():
         torch.mm(dy2, w, out=dx)
 
+    def sk():  # split-K (fp32 slabs + reduce): a long K over few output tiles (the MLM head's dgrad,
+        # K = 30,528 against 19 x 3 256-tiles, ran one K-loop per tile on 57 of 256 CUs)
+        C.gemm_splitk_(dy2, w, True, False, dx)
+
     if not _feat("linear_tune"):
         return nn_
     cands = {"mfma": nn_, "mfma_t": nt_, "blas": blas}
+    if dy2.shape[1] >= 4096 and dy2.shape[1] % 64 == 0:
+        cands["mfma_sk"] = sk
     return cands[_at.choose(("linear",) + key, cands, "mfma", lambda: dx)]
 
 
