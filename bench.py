@@ -333,6 +333,9 @@ def main():
     if step_log and rank == 0:
         prev = t0
         print("step host ms: " + " ".join(f"{(t - p) * 1e3:.1f}" for p, t in zip([t0] + ts[:-1], ts)), file=sys.stderr)
+        for ph in (getattr(tr, "host_phases", None) or [])[-a.steps:]:
+            print("host phases ms (begin forward backward finish): " + " ".join(f"{x * 1e3:.2f}" for x in ph),
+                  file=sys.stderr)
     if mode == "async":
         ps.drain()  # outside the timed region: every push of the run applied before reporting
     samples = a.batch * n_workers * a.steps

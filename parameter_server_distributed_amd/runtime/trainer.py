@@ -13,6 +13,7 @@ no polling.
 """
 from __future__ import annotations
 
+import os
 import time
 
 import torch
@@ -38,6 +39,8 @@ class Trainer:
         # src/parameter_main.cpp): device->host on a side stream, file write on a host thread
         self.checkpoint_prefix = checkpoint_prefix
         self.checkpoint_every = int(checkpoint_every)
+        # PSD_STEP_LOG=1: (begin, forward, backward, finish) host seconds of every eager step
+        self.host_phases = [] if os.environ.get("PSD_STEP_LOG", "0") == "1" else None
         self._ckpt_thread = None
         if tracer is not None:
             self.use_graph = False  # per-phase timing needs eager steps
@@ -50,6 +53,19 @@ class Trainer:
             self.ps.finish_step()
             return torch.zeros((), device=self.ps.device)
         tr = self.tracer
+        if tr is None and self.host_phases is not None:  # PSD_STEP_LOG=1: host time per phase (diagnosis)
+            t0 = time.perf_counter()
+            self.ps.begin_step()
+            t1 = time.perf_counter()
+            out = self.model(self.x)
+            loss = self.loss_fn(out, self.y)
+            t2 = time.perf_counter()
+            loss.backward()
+            t3 = time.perf_counter()
+            self.ps.finish_step()
+            t4 = time.perf_counter()
+            self.host_phases.append((t1 - t0, t2 - t1, t3 - t2, t4 - t3))
+            return loss
         if tr is None:
             self.ps.begin_step()
             out = self.model(self.x)
