@@ -293,11 +293,14 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(const uint16_t* __restr
         bfr[cb] = __builtin_bit_cast(
             bf16x8, *reinterpret_cast<const u32x4*>(dT + (cb * 16 + i16) * DLD + ((m0 + 8 * g) ^ dt_swz(cb * 16 + i16))));
       // A fragments: A[m][k] for 8 consecutive m (pixel p -> output row p / Wo, column p % Wo)
+      // (an item is kWgRows = 2 output rows: the row of pixel p is a compare, not a division -- the
+      // integer division by the runtime Wo made this loop VALU-bound, ~1,400 VALU per item per wave)
+      static_assert(kWgRows == 2, "pixel -> output row below assumes two rows per item");
       int pofs[8];
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
         const int p = m0 + 8 * g + t;
-        const int ohl = p / Wo, ow = p - ohl * Wo;
+        const int ohl = p >= Wo ? 1 : 0, ow = p - ohl * Wo;
         pofs[t] = 2 * ohl * RS + 6 * ow;
       }
 #pragma unroll
