@@ -138,6 +138,18 @@ __global__ __launch_bounds__(512) void convw_kernel(ConvwArgs a) {
   const int cmask = (1 << a.logC) - 1;
   const rsrc_t dyr = make_rsrc(a.dy, a.dybytes);
   const rsrc_t xr = make_rsrc(a.x, a.xbytes);
+  // the (r, s, ci0) of each K-block are fixed for this workgroup's column tile: resolved once here,
+  // not per stage (a runtime `/ S` per K-block and stage was a ~30-instruction VALU sequence)
+  int kb_r[G::NB], kb_s[G::NB], kb_ci[G::NB];
+#pragma unroll
+  for (int b = 0; b < G::NB; ++b) {
+    const int k0 = kk0 + b * 64;
+    const int rs = k0 >> a.logC;
+    kb_ci[b] = k0 & cmask;
+    kb_r[b] = rs / a.S;
+    kb_s[b] = rs - kb_r[b] * a.S;
+  }
+  const FastDiv dhw{(uint32_t)howo, a.howo_m, a.howo_s}, dwo{(uint32_t)a.Wo, a.wo_m, a.wo_s};
 
   const int total = (a.M + kBP - 1) / kBP;
   const int st0 = split * a.stages_per_split;
@@ -156,14 +168,15 @@ __global__ __launch_bounds__(512) void convw_kernel(ConvwArgs a) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(dyr, (__attribute__((address_space(3))) void*)(slot + j * kSub), 16,
                                                off, 0, 0, 0);
     }
-    const int n = m / howo, rem = m - n * howo;
-    const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
+    // (n, ho, wo) of the pixel by multiply-high (m < 2^31): the per-stage integer divisions by the
+    // runtime Ho*Wo and Wo were ~60 VALU per lane per stage
+    const int n = (int)fdiv_q((uint32_t)m, dhw), rem = m - n * howo;
+    const int ho = (int)fdiv_q((uint32_t)rem, dwo), wo = rem - ho * a.Wo;
     const int hb = ho * a.stride - a.pad, wb = wo * a.stride - a.pad;
 #pragma unroll
     for (int b = 0; b < G::NB; ++b) {
-      const int k0 = kk0 + b * 64;
-      const int rs = k0 >> a.logC, ci0 = k0 & cmask;
-      const int r = rs / a.S, s = rs - r * a.S;
+      const int ci0 = kb_ci[b];
+      const int r = kb_r[b], s = kb_s[b];
       const int hh = hb + r, ww = wb + s;
       const bool ok = mv && (unsigned)hh < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
       const uint32_t off =
@@ -534,6 +547,14 @@ int convw_gram_rows(int C) {
   return tco ? (C + 16 + tco - 1) / tco * tco : 0;
 }
 
+static void set_divs(ConvwArgs& a) {
+  const FastDiv hw = make_fastdiv((uint32_t)std::max(1, a.Ho * a.Wo)), wo = make_fastdiv((uint32_t)std::max(1, a.Wo));
+  a.howo_m = hw.m;
+  a.howo_s = hw.s;
+  a.wo_m = wo.m;
+  a.wo_s = wo.s;
+}
+
 static ConvwPlan gram_plan(const ConvwArgs& a) {
   ConvwPlan p{0, 0};
   int tco, tkk, ns;
@@ -560,6 +581,7 @@ static hipError_t launch_gram(const ConvwArgs& a_in, hipStream_t st) {
                   a_in.dybytes > 0 && (int64_t)a_in.M * a_in.KK * 2 <= (int64_t)a_in.xbytes && a_in.slab && a_in.out;
   if (!ok) return hipErrorNotSupported;
   ConvwArgs a = a_in;
+  set_divs(a);
   const ConvwPlan p = gram_plan(a);
   if (p.splits <= 0) return hipErrorNotSupported;
   const int total = (a.M + kBP - 1) / kBP;
@@ -639,6 +661,7 @@ hipError_t launch_convw(const ConvwArgs& a_in, hipStream_t st) {
                   (int64_t)a0.M * a0.Cout * 2 <= (int64_t)a0.dybytes;
   if (!ok) return hipErrorNotSupported;
   ConvwArgs a = a0;
+  set_divs(a);
   const ConvwPlan p = convw_plan(a);
   const int total = (a.M + kBP - 1) / kBP;
   a.splits = p.splits;

@@ -24,6 +24,7 @@ struct ConvwArgs {
   int Arows;
   // set by the launcher
   int splits, stages_per_split;
+  uint32_t howo_m, howo_s, wo_m, wo_s;  // round-up magic numbers of / (Ho*Wo) and / Wo (common.h FastDiv)
 };
 
 struct ConvwPlan {
