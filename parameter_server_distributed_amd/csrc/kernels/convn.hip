@@ -1267,7 +1267,7 @@ int convn_tile_n(int N) {
 // variant (convh_kernel, kind 2) for the 64-wide outputs, then the persistent 1x1 variant
 // (convp_kernel, kind 3) and its two-workgroups-per-CU form (kind 4). (The one-tile HALO variants -- kind 1 -- measured no faster than the
 // gathered ones on the ResNet-50 shapes, profiles/convn_halo_r3.md, and were removed in round 5.)
-static int plain_count(int bn) { return bn == 256 ? 2 : 4; }
+static int plain_count(int bn) { return bn == 256 ? 3 : 4; }
 static int persist_count(int bn) { return bn == 64 ? 1 : 0; }
 static int p1_count(int bn) { return bn ? 2 : 0; }  // the persistent 1x1: one and two workgroups per CU
 static int convn_variant_count(int bn) { return plain_count(bn) + persist_count(bn) + p1_count(bn); }
@@ -1376,9 +1376,11 @@ hipError_t launch_convn(const ConvnArgs& a_in, hipStream_t st) {
       if (v == 1) return convn_launch_s<128, 128, 64, 3>(a, st);
       if (v == 2) return convn_launch_s<256, 128, 64, 2>(a, st);
       return convn_launch_s<128, 128, 32, 2>(a, st);
-    default:  // 8 waves of 64x64, 3 or 2 slots
+    default:  // 8 waves of 64x64, 3 or 2 slots | 128-wide column tiles on a 2-slot ring (80 KiB: two
+              // workgroups per CU; the 256-wide tile's 2- and 3-slot rings hold the CU alone)
       if (v == 0) return convn_launch_s<128, 256, 64, 3>(a, st);
-      return convn_launch_s<128, 256, 64, 2>(a, st);
+      if (v == 1) return convn_launch_s<128, 256, 64, 2>(a, st);
+      return convn_launch_s<128, 128, 32, 2>(a, st);
   }
 }
 
