@@ -161,6 +161,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("dbeta_out") = py::none());
   m.def("gap_bwd", &gap_bwd);
   m.def("subsample2", &subsample2, py::arg("x"));
+  m.def("wprep_table", &wprep_table, py::arg("srcs"), py::arg("dsts"), py::arg("geo"));
+  m.def("wprep_run", &wprep_run, py::arg("table"), py::arg("tiles"));
   m.attr("OPT_SGD") = (int)OPT_SGD;
   m.attr("OPT_MOMENTUM") = (int)OPT_MOMENTUM;
   m.attr("OPT_ADAM") = (int)OPT_ADAM;

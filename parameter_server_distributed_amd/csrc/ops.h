@@ -1,5 +1,6 @@
 #pragma once
 #include <ATen/ATen.h>
+#include <tuple>
 #include <vector>
 
 namespace psd {
@@ -153,6 +154,11 @@ std::vector<at::Tensor> bn_pool_bwd(const at::Tensor& gpool, c10::optional<at::T
                                     c10::optional<at::Tensor> dgamma_out, c10::optional<at::Tensor> dbeta_out);
 at::Tensor gap_bwd(const at::Tensor& dy, int64_t H, int64_t W);
 at::Tensor subsample2(const at::Tensor& x);
+
+// batched bwd-data weight preparation (wprep_ops.cpp)
+std::tuple<at::Tensor, int64_t> wprep_table(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts,
+                                            const std::vector<int64_t>& geo);
+void wprep_run(const at::Tensor& table, int64_t tiles);
 
 // fused softmax cross-entropy on bf16 logits (xent_ops.cpp)
 void embed_bwd_(const at::Tensor& sorted, const at::Tensor& perm, const at::Tensor& dy, at::Tensor out);

@@ -38,6 +38,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..utils.config import feature as _feat
+from . import wprep as _wprep
 from . import autotune as _at
 from .bn import StridedDr, take_dr
 
@@ -196,9 +197,22 @@ class _Lazy:
         return self.t
 
 
-def _wt(w2: torch.Tensor) -> _Lazy:
-    """w2^T (contiguous), made on first use."""
-    return _Lazy(lambda: w2.t().contiguous(), (w2.shape[1], w2.shape[0]))
+def _wt(w2: torch.Tensor, mod=None, weight=None) -> _Lazy:
+    """w2^T (contiguous), made on first use: the step's batched operand (ops/wprep.py) when ``mod``'s
+    forward registered ``weight``, else a transpose copy."""
+    def make():
+        t = _wprep.get(mod, weight, "t") if weight is not None else None
+        return t if t is not None else w2.t().contiguous()
+    return _Lazy(make, (w2.shape[1], w2.shape[0]))
+
+
+def _wflip(mod, weight: torch.Tensor) -> torch.Tensor:
+    """The stride-1 bwd-data weight W'[ci][r][s][co] = W[co][ci][k-1-r][k-1-s] as [Ci, k k Co]."""
+    t = _wprep.get(mod, weight, "f")
+    if t is not None:
+        return t
+    cout, cin, k, _ = weight.shape
+    return weight.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, k * k * cout).contiguous()
 
 
 def _get(w):
@@ -351,7 +365,7 @@ def _s2_phase_weights(weight: torch.Tensor) -> list:
     return out
 
 
-def _dgrad_s2_phases(dy, weight, x, fu) -> dict:
+def _dgrad_s2_phases(dy, weight, x, fu, mod=None) -> dict:
     """{"psdns<v>" / "psdnbs<v>": fn}: a stride-2 3x3 bwd-data on the narrow kernel as four phase
     launches (no zero-insertion, no zero-filled dX; MIOpen's kernel runs a fill pass over dX first)
     -- with ``fu`` (mode 1: the producing BN + ReLU) the fused candidates also reduce that BN's
@@ -359,7 +373,11 @@ def _dgrad_s2_phases(dy, weight, x, fu) -> dict:
     C = _native()
     n, cin, h, w = x.shape
     ho, wo = dy.shape[2], dy.shape[3]
-    wph = _Lazy(lambda: _s2_phase_weights(weight), (4,))
+    def phases():
+        got = _wprep.get(mod, weight, "p")
+        return got if got is not None else _s2_phase_weights(weight)
+
+    wph = _Lazy(phases, (4,))
 
     def make(v, fused):
         def fn():
@@ -584,7 +602,7 @@ def _fold_backward(ctx, fold, x, weight, need_x: bool, need_w: bool, P=None):
 
     if need_x and foldable:
         w2, bvec = C.bnfold_dgrad_weights(weight, coef)
-        wt = _wt(weight.reshape(cout, cin))
+        wt = _wt(weight.reshape(cout, cin), ctx.mod, weight)
         fu = _bn_bwd_fusion(ctx.bn_in, x)
         if fu is not None:
             fu["dr"] = fu["bn"]._psd_pending_dr.pop() if fu["mode"] >= 2 else None
@@ -686,6 +704,8 @@ class _Conv1x1Fn(torch.autograd.Function):
         fp8 = f8 is not None
         ctx.mod = mod
         _fwd_records(ctx, mod)
+        if ctx.needs_input_grad[0]:
+            _wprep.note(mod, weight, "t")
         n, cin, h, w = x.shape
         cout = weight.shape[0]
         w2 = weight.reshape(cout, cin)
@@ -780,7 +800,7 @@ class _Conv1x1Fn(torch.autograd.Function):
                 dyq, sdy = got[0].permute(0, 2, 3, 1).reshape(n * h * w, cout), got[1]
             else:
                 dyq, sdy = _q_act(_as_2d(dy), e5m2=True, scaler=ctx.f8[1])
-            wtq, swt = _q_act(weight.reshape(cout, cin).t().contiguous())
+            wtq, swt = _q_act(_wt(weight.reshape(cout, cin), ctx.mod, weight)())
             out = torch.empty(n * h * w, cin, device=dy.device, dtype=dy.dtype)
             _native().gemm_fp8_(dyq, wtq, sdy, swt, out)
             FP8_CALLS["dgrad"] += 1
@@ -807,7 +827,7 @@ class _Conv1x1Fn(torch.autograd.Function):
                 cands["psd"] = psd
             fu = None
             if _psdn_ok(cout, cin):  # dX = dY . W as a 1x1 convolution of dY with W^T [cin, cout]
-                wt = _wt(w2)
+                wt = _wt(w2, ctx.mod, weight)
                 cands.update(_convn_variants(dy, wt, 1, 1, 0))
                 fu = _bn_bwd_fusion(ctx.bn_in, x)
                 if fu is not None:
@@ -970,7 +990,7 @@ def _strided_dgrad(mod, dy, weight, to, H: int, W: int):
     if _psd_ok(cout, cin):
         cands["psd"] = psd
     if _psdn_ok(cout, cin):
-        cands.update(_convn_variants(dy, _wt(w2), 1, 1, 0))
+        cands.update(_convn_variants(dy, _wt(w2, mod, weight), 1, 1, 0))
     t4 = cands[_choose(("dgrad_s2", M4, cin, cout), cands)]()
     if not t4.is_contiguous(memory_format=torch.channels_last):
         t4 = t4.contiguous(memory_format=torch.channels_last)
@@ -992,6 +1012,13 @@ class _ConvFn(torch.autograd.Function):
         n, _, h, w = x.shape
         ctx.stride, ctx.pad, ctx.fp8, ctx.f8 = stride, pad, fp8, f8
         ctx.save_for_backward(x, weight)
+        if ctx.needs_input_grad[0]:
+            if k == 1:
+                _wprep.note(mod, weight, "t")
+            elif stride == 1 and 2 * pad == k - 1:
+                _wprep.note(mod, weight, "f")
+            elif stride == 2 and k == 3 and pad == 1:
+                _wprep.note(mod, weight, "p")
 
         def miopen():
             return F.conv2d(x, weight, stride=stride, padding=pad)
@@ -1060,14 +1087,14 @@ class _ConvFn(torch.autograd.Function):
             if stride == 1 and _igemm_ok(cout, cin) and 2 * pad == k - 1 and ctx.fp8 and cout % 128 == 0 \
                     and _fp8_ok(k * k * cout, cin) and n * h * w >= 128 and _feat("fp8_dgrad"):
                 # fp8 bwd-data: e5m2 dY gathered by the implicit GEMM, e4m3 flipped weights
-                wf = weight.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, k * k * cout).contiguous()
+                wf = _wflip(ctx.mod, weight)
                 got = _take_dq8(ctx.mod, dy) if _mx_on() else None
                 dx = _igemm_fp8(dy, wf, k, 1, pad, e5m2=True, scaler=ctx.f8[1], pre=got)
                 if dx is None:
                     raise RuntimeError(f"conv_fwd_fp8_ (bwd-data) declined {tuple(dy.shape)} x {tuple(weight.shape)}")
             elif stride == 1 and (_igemm_ok(cout, cin) or _psdn_ok(cout, cin)) and 2 * pad == k - 1:
                 # dX = conv(dY, W'), W'[ci, r, s, co] = W[co, ci, k-1-r, k-1-s]: same kernel, same padding
-                wf = weight.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, k * k * cout).contiguous()
+                wf = _wflip(ctx.mod, weight)
 
                 def igemm():
                     y = _igemm(dy, wf, k, 1, pad)
@@ -1100,7 +1127,7 @@ class _ConvFn(torch.autograd.Function):
                 if fu is not None:
                     fu["dr"] = None
                 cands = {"miopen": miopen}
-                cands.update(_dgrad_s2_phases(dy, weight, x, fu))
+                cands.update(_dgrad_s2_phases(dy, weight, x, fu, ctx.mod))
                 key = ("dgrad", n, cin, h, w, cout, k, stride)
                 dx = _dgrad_route(("conv",) + key, cands, "miopen", fu, x)
             else:
