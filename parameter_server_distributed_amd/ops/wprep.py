@@ -79,6 +79,8 @@ class _Registry:
             return
         e = self.entries.get(key)
         if e is None or e.mod() is not mod or e.weight() is not weight or e.shape != tuple(weight.shape):
+            if torch.cuda.is_current_stream_capturing():
+                return  # no new persistent buffers inside a graph capture (its backward builds the operand)
             self.entries[key] = _Entry(mod, weight, kind)
             self.tables.pop(weight.device, None)
         else:
@@ -104,13 +106,15 @@ class _Registry:
         if w is None or w.data_ptr() != weight.data_ptr() or e.shape != tuple(weight.shape):
             return None
         dev = weight.device
-        if self.stale.get(dev, True):
-            self._refresh(dev)
+        if self.stale.get(dev, True) and not self._refresh(dev):
+            return None
         return e.dsts if kind == "p" else e.dsts[0]
 
-    def _refresh(self, dev) -> None:
+    def _refresh(self, dev) -> bool:
         """One launch over every registered operand of ``dev``, from the weights' current storage
-        (a job table per storage set: the PS's two alternating parameter buffers give two)."""
+        (a job table per storage set: the PS's two alternating parameter buffers give two). False
+        when a new table would be needed inside a graph capture (its host-to-device upload cannot be
+        captured): the callers then build their operands with torch ops."""
         from .. import native
 
         C = native()
@@ -129,6 +133,8 @@ class _Registry:
         sig = tuple(e.weight().data_ptr() for _, e in live)
         tab = cache.get(sig)
         if tab is None:
+            if torch.cuda.is_current_stream_capturing():
+                return False
             if len(cache) >= 4:
                 cache.clear()
             srcs, dsts, geo = [], [], []
@@ -143,6 +149,7 @@ class _Registry:
         if tab[0] is not None:
             C.wprep_run(tab[0], tab[1])
         self.stale[dev] = False
+        return True
 
 
 def _eligible(weight: torch.Tensor) -> bool:
