@@ -181,6 +181,11 @@ class AsyncPS:
         self.pbufs = [init.to(param_dtype)]
         if self.prefetch:
             self.pbufs.append(self.pbufs[0].clone())
+        # the model's parameters view ONE working buffer; each step copies its pulled buffer into it
+        # on the compute stream (_to_work: a ~70 us device copy for BERT-base) instead of re-pointing
+        # every parameter from Python (~200 `p.data =` per step: ~1 ms of host time at the step
+        # boundary, where the GPU waited for it -- profiles/r5/bert_base_b256_r5_kernels.md)
+        self.pwork = self.pbufs[0].clone() if self.prefetch else self.pbufs[0]
         self.cb = 0
         # MX pull targets (one per working buffer): e4m3 [total] + E8M0 scales [total / 32]
         self.q8s = [torch.zeros(total, dtype=torch.float8_e4m3fn, device=dev) for _ in self.pbufs] if self.pull_mx else []
@@ -223,9 +228,9 @@ class AsyncPS:
         self._layout = layout
         self._zero_plan = zero_plan([(o, p.numel()) for (_n, p, o, _k) in layout if id(p) not in self._direct], total)
         self._arrived: set = set()
-        self._pviews = [[_flat_view(b, o, p) for (_n, p, o, _k) in layout] for b in self.pbufs]
-        for (n, p, o, k), v in zip(layout, self._pviews[0]):
-            p.data = v
+        for (n, p, o, k) in layout:
+            p.data = _flat_view(self.pwork, o, p)
+        self._gview_cache = {}
         self._set_grad_views()
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for _, p, _o, _n in layout]
         self._next = 0
@@ -276,7 +281,7 @@ class AsyncPS:
         self.closed = False
         self._ckpt_seq = 0
         if self.pull_mx:  # the fp8 convolutions read the pulled e4m3 weights of the current buffer
-            install_fp8_weights(model, lambda: (self.q8s[self.cb], self.sc8s[self.cb], self.pbufs[self.cb]))
+            install_fp8_weights(model, lambda: (self.q8s[self.cb], self.sc8s[self.cb], self.pwork))
 
     def _connect(self, key, optim, log):
         """Exchange memory descriptors, map the peers, publish version 0, self-test, start."""
@@ -371,8 +376,8 @@ class AsyncPS:
     # ------------------------------------------------------------------ helpers
     @property
     def params_flat(self) -> torch.Tensor:
-        """The working weights of the current step."""
-        return self.pbufs[self.cb]
+        """The working weights of the current step (the buffer the model's parameters view)."""
+        return self.pwork
 
     def _barrier(self, tag: str):
         if self.world == 1:
@@ -394,12 +399,20 @@ class AsyncPS:
         return s.cuda_stream
 
     def _set_grad_views(self):
-        g = self.grads[self.gb]
-        self._grad_views = {}
+        views = self._gview_cache.get(self.gb)
+        if views is None:  # built once per gradient buffer (two alternate)
+            g = self.grads[self.gb]
+            views = {id(p): _flat_view(g, o, p) for (_n, p, o, _k) in self._layout}
+            self._gview_cache[self.gb] = views
+        self._grad_views = views
         for n, p, o, k in self._layout:
-            v = _flat_view(g, o, p)
-            self._grad_views[id(p)] = v
-            p.grad = None if id(p) in self._direct else v
+            p.grad = None if id(p) in self._direct else views[id(p)]
+
+    def _to_work(self):
+        """The pulled buffer of this step into the working weights (stream-ordered on the current
+        stream: after the previous step's kernels, before this step's)."""
+        if self.pwork is not self.pbufs[self.cb]:
+            self.pwork.copy_(self.pbufs[self.cb])
 
     def _sink(self, p):
         if id(p) not in self._direct:
@@ -409,7 +422,8 @@ class AsyncPS:
 
     def memory_bytes(self) -> dict:
         eb = lambda t: t.numel() * t.element_size()  # noqa: E731
-        return {"params": sum(eb(b) for b in self.pbufs), "grads": 2 * eb(self.grads[0]),
+        work = eb(self.pwork) if all(self.pwork is not b for b in self.pbufs) else 0
+        return {"params": sum(eb(b) for b in self.pbufs) + work, "grads": 2 * eb(self.grads[0]),
                 "master": sum(eb(t) for t in self.master.values()),
                 "state": sum(eb(t) for t in list(self.state1.values()) + list(self.state2.values()))}
 
@@ -430,14 +444,14 @@ class AsyncPS:
         self._next = 0
         if self.prefetch:
             self.cb = t % 2
-            for (_n, p, _o, _k), v in zip(self._layout, self._pviews[self.cb]):
-                p.data = v
             if self._prefetched is not None and self._prefetched[0] == t:
                 self.pulled = self._prefetched[1]
                 if self.is_cuda:
                     torch.cuda.current_stream(self.device).wait_event(self.pull_done[self.cb])
+                self._to_work()
                 return
         self.pulled = self._pull_into(t, self.cb, None)
+        self._to_work()
 
     def _pull_into(self, t: int, nb: int, stream) -> list:
         """Pull of step t into working buffer ``nb`` on ``stream`` (None: the current stream): the
@@ -535,6 +549,7 @@ class AsyncPS:
         snapshot. Workers otherwise hold the weights of their last pull, one round behind."""
         if self.is_worker and self.engine is not None:
             self.pulled = self._pull_into(0, self.cb, None)
+            self._to_work()
             if self.is_cuda:
                 torch.cuda.synchronize(self.device)
 
@@ -819,6 +834,7 @@ class AsyncPS:
         if self.is_worker:  # working weights = the restored snapshot (forward hooks, eval before a step);
             # with MX pulls the e4m3 copy the fp8 convolutions read (install_fp8_weights) is pulled too
             self.pulled = self._pull_into(0, self.cb, None)
+            self._to_work()
             if self.is_cuda:
                 torch.cuda.synchronize(self.device)
 
@@ -902,13 +918,15 @@ class AsyncPS:
             self.engine.publish_initial(k)
         self.engine.start()
         self.params_flat.copy_(full["master"].to(self.param_dtype))
-        for b in self.pbufs[1:]:
-            b.copy_(self.params_flat)
+        for b in self.pbufs:
+            if b is not self.pwork:
+                b.copy_(self.params_flat)
         for q, sc, b in zip(self.q8s, self.sc8s, self.pbufs):
             # MX pulls: the e4m3 weights the fp8 convolutions read, and the working bf16 copy as a
             # pull would leave it (dequantised)
             native().quant_mx_(full["master"], q, sc)
             native().dequant_mx_(q, sc, b)
+        self._to_work()
         self.step_idx = 0
         self._prefetched = None
         if self.is_cuda:
