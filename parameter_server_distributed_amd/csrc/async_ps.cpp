@@ -83,11 +83,15 @@ int64_t now_us() {
       .count();
 }
 
+// Spin-wait backoff of the engine's host waits (SSP pulls, commit events, inbox flags): yields,
+// then 20 us sleeps for the first ~1 s of a wait, 200 us after. (A wait the GPU ends -- a worker's
+// pull for the next step waiting on this step's commit -- typically lasts 10-20 ms: with 200 us
+// sleeps from ~20 ms on, it woke up to 200 us late, and the step boundary's GPU idle grew by that.)
 void backoff(int& spins) {
   if (++spins < 64) {
     std::this_thread::yield();
   } else {
-    std::this_thread::sleep_for(std::chrono::microseconds(spins < 1024 ? 20 : 200));
+    std::this_thread::sleep_for(std::chrono::microseconds(spins < 50000 ? 20 : 200));
   }
 }
 
