@@ -34,6 +34,8 @@ import time
 
 import torch
 
+from ..utils.config import feature as _feat
+
 _DECISIONS: dict[tuple, str] = {}
 _DECLINED_KEYS: set = set()  # keys where every candidate declined (decided once, for every rank)
 _DECLINED = "__declined__"
@@ -179,6 +181,11 @@ def choose(key: tuple, candidates: dict, default: str, probe=None) -> str:
     return best
 
 
+# candidate names that run a library kernel (MIOpen, hipBLASLt through torch.mm / F.linear)
+LIBRARY = frozenset({"miopen", "gemm", "blas"})
+OWN_MARGIN = 0.02
+
+
 def _time_and_pick(key: tuple, candidates: dict, default: str, probe) -> str:
     runs, declined = {}, []
     for name, fn in candidates.items():
@@ -202,6 +209,15 @@ def _time_and_pick(key: tuple, candidates: dict, default: str, probe) -> str:
     if bad:
         _REJECTED[key] = _REJECTED.get(key, []) + bad
     best = min(ok, key=ok.get)
+    if best in LIBRARY and _feat("prefer_own"):
+        # one of our kernels within OWN_MARGIN of a library winner takes the pick: closer than the
+        # run-to-run spread of one kernel's timing, such a decision flipped the library kernel in and
+        # out of the step from box to box (2-7 MIOpen weight gradients per ResNet-50 step)
+        own = {n: t for n, t in ok.items() if n not in LIBRARY}
+        if own:
+            o = min(own, key=own.get)
+            if own[o] <= ok[best] * (1.0 + OWN_MARGIN):
+                best = o
     _DECISIONS[key] = best
     _TIMES[key] = {n: round(r[0], 4) for n, r in runs.items()}
     if os.environ.get("PSD_AUTOTUNE_LOG"):

@@ -104,3 +104,32 @@ def test_autotune_all_declined_publishes_to_peers(tmp_path):
     for r in range(2):
         res = eval(open(tmp_path / f"d{r}.txt").read())
         assert res == ["declined", True, "declined", True, "error"], (r, res)
+
+
+def test_prefer_own_within_margin(monkeypatch):
+    """A library candidate ("miopen" / "gemm" / "blas") that wins by less than OWN_MARGIN yields to
+    the fastest of our kernels; a clear library win stands; the feature off restores the plain min."""
+    from parameter_server_distributed_amd.ops import autotune as at
+    from parameter_server_distributed_amd.utils.config import set_feature
+
+    out = torch.ones(4)
+    times = {}
+    monkeypatch.setattr(at, "_time_ms", lambda fn, probe=None: (times[fn()], [out, out]))
+    cands = {n: (lambda n=n: n) for n in ("miopen", "psdw0", "igemm")}
+
+    def pick(t, key):
+        times.clear()
+        times.update(t)
+        return at._time_and_pick(key, cands, "miopen", None)
+
+    try:
+        assert pick({"miopen": 1.00, "psdw0": 1.015, "igemm": 1.3}, ("t", 1)) == "psdw0"
+        assert pick({"miopen": 1.00, "psdw0": 1.05, "igemm": 1.3}, ("t", 2)) == "miopen"
+        assert pick({"miopen": 1.2, "psdw0": 1.05, "igemm": 1.0}, ("t", 3)) == "igemm"
+        set_feature("prefer_own", False)
+        assert pick({"miopen": 1.00, "psdw0": 1.015, "igemm": 1.3}, ("t", 4)) == "miopen"
+    finally:
+        set_feature("prefer_own", None)
+        for k in [("t", i) for i in range(1, 5)]:
+            at._DECISIONS.pop(k, None)
+            at._TIMES.pop(k, None)
