@@ -257,6 +257,14 @@ def main():
             ps.rebucket(a.bucket_mb)
         except Exception as e:  # noqa: BLE001 -- collective (every rank raises together): keep 16 MB
             bucket_probe = {"error": str(e)[:200]}
+    xfer_probe = None
+    if mode == "async" and world > 1:
+        # the scatter kernel's workgroup budget per owner segment: the smallest that keeps ~all of the
+        # link bandwidth (fewest CUs taken from the backward pass the pushes run beside)
+        try:
+            xfer_probe = ps.probe_xfer_blocks() or None
+        except Exception as e:  # noqa: BLE001 -- collective: every rank raises together; keep the default
+            xfer_probe = {"error": str(e)[:200]}
     if mode == "collective" and auto_bucket and world > 1 and a.backend == "nccl":
         from parameter_server_distributed_amd.parallel import bucketing
 
@@ -412,6 +420,7 @@ def main():
                                  if a.model in REF_BASELINE else None),
             "bucket_mb_chosen": a.bucket_mb, "bucket_probe_GBps": bucket_probe,
             "bucket_probe_transport": bucket_transport,
+            "async_xfer_blocks": xfer_probe,
             "staleness_p50": p50, "staleness_hist": hist, "final_loss": round(final_loss, 4),
             "params_finite": params_finite, "comm_probe_busbw_GBps": probe, "async_plane_bw": async_bw,
             "warmup_s": round(t_w, 2), "peak_mem_gb": round(mem_peak / 2**30, 2),

@@ -703,6 +703,19 @@ void AsyncEngine::set_xfer(bool kernel) {
   xfer_kernel_ = kernel;
 }
 
+void AsyncEngine::set_xfer_blocks(int cap) {
+  TORCH_CHECK(cap >= 1 && cap <= 1024, "psd async: xfer workgroups per segment in [1, 1024]");
+  xfer_cap_ = cap;
+}
+
+namespace {
+// the scatter / gather kernels move 16-byte vectors: a segment with an unaligned end takes the copy
+// path (hipMemcpyAsync accepts any alignment)
+inline bool aligned16(const void* a, const void* b) {
+  return ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0;
+}
+}  // namespace
+
 std::string AsyncEngine::xfer_mode() const {
   if (device_ < 0) return "host-memcpy";
   // "kernel": peer segments by the scatter / gather kernels, this rank's own by hipMemcpyAsync
@@ -776,7 +789,15 @@ std::vector<int64_t> AsyncEngine::pull_impl(int64_t step, char* dst, char* dst_s
   // the gather kernel pays where it drives several peers' links at once; a pull of only this
   // rank's own shards is a local copy, which the copy engine does without taking CUs from the
   // compute stream (N = 1: ResNet-50 / BERT-base 0.2 % / 0.1 % faster with the copies)
-  if (device_ >= 0 && xfer_kernel_ && remote) {
+  bool al = true;  // every segment 16-byte aligned (else the copy path)
+  for (int k = 0; k < P && al; ++k) {
+    if (dst_sc)
+      al = aligned16(publish_q_ptr(k, bufs[k]), dst + shard_off_[k]) && aligned16(dst_bf16 + shard_off_[k], nullptr) &&
+           shard_len_[k] % 32 == 0;
+    else
+      al = aligned16(publish_ptr(k, bufs[k]), dst + shard_off_[k] * esz_);
+  }
+  if (device_ >= 0 && xfer_kernel_ && remote && al) {
     // every shard's snapshot in one gather launch: all owners' links at once (kernels/xfer.hip)
     const c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device_));
     if (dst_sc) {
@@ -791,7 +812,7 @@ std::vector<int64_t> AsyncEngine::pull_impl(int64_t step, char* dst, char* dst_s
                                        dst_bf16 + shard_off_[k], shard_len_[k]};
           mx = std::max(mx, shard_len_[k]);
         }
-        L.blocks_per_seg = xfer_blocks(mx, 48);
+        L.blocks_per_seg = xfer_blocks(mx, xfer_cap_);
         hip_ok(launch_xfer_mx(L, static_cast<hipStream_t>(sp)), "launch_xfer_mx(pull)");
       }
     } else {
@@ -801,7 +822,7 @@ std::vector<int64_t> AsyncEngine::pull_impl(int64_t step, char* dst, char* dst_s
         L.seg[L.count++] = XferSeg{publish_ptr(k, bufs[k]), dst + shard_off_[k] * esz_, shard_len_[k] * esz_};
         mx = std::max(mx, shard_len_[k] * esz_);
       }
-      L.blocks_per_seg = xfer_blocks(mx, 48);
+      L.blocks_per_seg = xfer_blocks(mx, xfer_cap_);
       L.nt_load = 1;
       hip_ok(launch_xfer(L, static_cast<hipStream_t>(sp)), "launch_xfer(pull)");
     }
@@ -834,12 +855,13 @@ void AsyncEngine::push(int64_t step, const at::Tensor& grads_flat, int64_t lo, i
   check_error();
   const char* src = static_cast<const char*>(grads_flat.data_ptr());
   const int slot = (int)(step % (S_ + 1));
-  bool remote = false;
+  bool remote = false, al = true;
   for (size_t k = 0; k < owners_.size(); ++k) {
     const int64_t a = std::max(lo, shard_off_[k]), b = std::min(hi, shard_off_[k] + shard_len_[k]);
     remote = remote || (a < b && owners_[k] != rank_);
+    if (a < b) al = al && aligned16(src + a * esz_, inbox_ptr((int)k, my_wi_, slot) + (a - shard_off_[k]) * esz_);
   }
-  if (device_ >= 0 && xfer_kernel_ && remote) {
+  if (device_ >= 0 && xfer_kernel_ && remote && al) {
     // the bucket's slice for every owner it overlaps in one scatter launch (kernels/xfer.hip); a
     // push into this rank's own inbox only is a local copy (see pull_impl)
     XferList L{};
@@ -851,7 +873,7 @@ void AsyncEngine::push(int64_t step, const at::Tensor& grads_flat, int64_t lo, i
                                  (b - a) * esz_};
       mx = std::max(mx, (b - a) * esz_);
     }
-    L.blocks_per_seg = xfer_blocks(mx, 48);
+    L.blocks_per_seg = xfer_blocks(mx, xfer_cap_);
     L.nt_store = 1;
     const c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device_));
     hip_ok(launch_xfer(L, reinterpret_cast<hipStream_t>(stream)), "launch_xfer(push)");

@@ -91,6 +91,10 @@ class AsyncEngine {
   // every owner's peer memory at once (kernels/xfer.hip); false = one hipMemcpyAsync per shard
   void set_xfer(bool kernel);
   std::string xfer_mode() const;
+  // workgroups per segment of one scatter / gather launch (cap; default 48): the budget of CUs a
+  // push may take from the backward pass running beside it (bench.py probes it at N > 1)
+  void set_xfer_blocks(int cap);
+  int xfer_blocks_cap() const { return xfer_cap_; }
   void push(int64_t step, const at::Tensor& grads_flat, int64_t lo, int64_t hi, int64_t stream);
   void commit(int64_t step, std::vector<int64_t> pulled, int64_t stream);
   void wait_applied(int64_t nsteps);  // this worker's pushes 0..nsteps-1 applied at every shard
@@ -168,6 +172,7 @@ class AsyncEngine {
   int round_ = 1;
   bool fixed_ = false;
   bool xfer_kernel_ = false;  // set in the constructor: true on a GPU engine
+  int xfer_cap_ = 48;         // set_xfer_blocks
   double timeout_s_;
   double dead_after_s_ = 10.0;  // a peer's engine silent this long is presumed dead (PSD_ASYNC_DEAD_S)
   int esz_;

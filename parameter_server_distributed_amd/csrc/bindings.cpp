@@ -40,6 +40,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("optim_advance_", &optim_advance_, py::arg("dyn"), py::arg("beta1") = 0.9, py::arg("beta2") = 0.999);
   m.def("multi_reduce_", &multi_reduce_, py::arg("out"), py::arg("srcs"), py::arg("scale") = 1.0);
   m.def("pack_cast_", &pack_cast_, py::arg("srcs"), py::arg("dsts"));
+  m.def("xfer_", &xfer_, py::arg("srcs"), py::arg("dsts"), py::arg("blocks_per_seg"), py::arg("nt_store") = false);
   m.def("amax_", &amax_);
   m.def("quant_fp8_", &quant_fp8_);
   m.def("dequant_fp8_", &dequant_fp8_);
@@ -319,6 +320,8 @@ PYBIND11_MODULE(_C, m) {
       .def("memory_kind", &AsyncEngine::memory_kind)
       .def("set_xfer", &AsyncEngine::set_xfer)
       .def("xfer_mode", &AsyncEngine::xfer_mode)
+      .def("set_xfer_blocks", &AsyncEngine::set_xfer_blocks)
+      .def("xfer_blocks_cap", &AsyncEngine::xfer_blocks_cap)
       .def("error", &AsyncEngine::error)
       .def("inject_error", &AsyncEngine::inject_error)
       .def("counters", &AsyncEngine::counters)

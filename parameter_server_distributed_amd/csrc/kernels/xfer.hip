@@ -62,6 +62,15 @@ __global__ __launch_bounds__(256) void xfer_kernel(XferList L) {
     const int64_t o = n16 * 16 + threadIdx.x;
     static_cast<uint8_t*>(g.dst)[o] = static_cast<const uint8_t*>(g.src)[o];
   }
+  if constexpr (NTS) {
+    // Stores into a peer's memory (push): a system-scope release per wave before the kernel ends,
+    // so the commit event recorded behind this launch (async_ps.cpp defer -> post) can never be
+    // observed by the owner ahead of the bytes, whatever scope the runtime gives the end-of-kernel
+    // release (hipMemcpyAsync gave this ordering before). The counted wait is inline
+    // asm so the compiler cannot drop it after the release (MI355X_MICROARCH.md, compiler hazard).
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
 }
 
 template <int U>

@@ -14,6 +14,7 @@
 #include <cstring>
 
 #include "kernels/launchers.h"
+#include "kernels/launchers_xfer.h"
 
 namespace psd {
 
@@ -215,6 +216,24 @@ void multi_reduce_(at::Tensor out, const std::vector<at::Tensor>& srcs, double s
       else static_cast<float*>(out.data_ptr())[i] = acc;
     }
   });
+}
+
+void xfer_(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts, int64_t blocks_per_seg,
+           bool nt_store) {
+  TORCH_CHECK(srcs.size() == dsts.size() && !srcs.empty() && (int)srcs.size() <= kMaxXferSeg, "psd: xfer_ segments");
+  XferList L{};
+  for (size_t i = 0; i < srcs.size(); ++i) {
+    const at::Tensor &a = srcs[i], &b = dsts[i];
+    TORCH_CHECK(a.is_cuda() && b.is_cuda() && a.is_contiguous() && b.is_contiguous() && a.nbytes() == b.nbytes(),
+                "psd: xfer_ takes contiguous device tensors of equal byte size");
+    check_aligned(a, "xfer_ src");
+    check_aligned(b, "xfer_ dst");
+    L.seg[L.count++] = XferSeg{a.data_ptr(), b.data_ptr(), (int64_t)a.nbytes()};
+  }
+  L.blocks_per_seg = (int32_t)blocks_per_seg;
+  L.nt_store = nt_store ? 1 : 0;
+  const c10::DeviceGuard g(srcs[0].device());
+  hip_check(launch_xfer(L, cur_stream(srcs[0])), "launch_xfer");
 }
 
 void pack_cast_(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts) {

@@ -12,6 +12,10 @@ void fused_apply_(at::Tensor master, const std::vector<at::Tensor>& grads, c10::
 void optim_advance_(at::Tensor dyn, double beta1, double beta2);
 void multi_reduce_(at::Tensor out, const std::vector<at::Tensor>& srcs, double scale);
 void pack_cast_(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts);
+// the async plane's scatter kernel (kernels/xfer.hip) on explicit segments, on the current stream:
+// dsts[i] <- srcs[i] bytewise, blocks_per_seg workgroups per segment (transport measurements)
+void xfer_(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts, int64_t blocks_per_seg,
+           bool nt_store);
 void amax_(const at::Tensor& x, at::Tensor amax_out);
 void quant_fp8_(const at::Tensor& x, const at::Tensor& amax, double fp8_max, at::Tensor out, at::Tensor scale_inv);
 void quant_fp8_jit_(const at::Tensor& x, at::Tensor out, at::Tensor scale_inv);

@@ -309,28 +309,34 @@ class AsyncPS:
         if self.is_cuda:
             self.engine.set_xfer(self.xfer != "copy")
         try:
-            self.selftest()
+            self.selftest("kernel" if self.is_cuda and self.xfer != "copy" else "copy")
         except RuntimeError as e:  # collective: every rank sees the same failure
             if not (self.is_cuda and self.xfer == "auto"):
                 raise
             self.xfer_fallback = str(e)[:300]
             self.engine.set_xfer(False)
-            self.selftest()
+            self.selftest("copy")
         self.xfer_mode = self.engine.xfer_mode()
         self.engine.start()
 
-    def selftest(self):
+    def selftest(self, attempt: str = "copy"):
         """Collective start-up check of the peer-memory paths on this node (before any training):
         every worker DMA-writes a known pattern into its inbox on every shard owner, and every
         owner verifies what landed; every worker pulls the version-0 snapshots and compares each
         shard with its owner's published checksum (the ranks' weights need not agree yet: an elastic
         joiner's are replaced by load_canonical_state next). Raises on any mismatch on any rank (so a
-        caller can fall back to the collective plane instead of training on a broken path)."""
+        caller can fall back to the collective plane instead of training on a broken path).
+
+        ``attempt`` ("kernel" / "copy": the transport under test) tags every store key of this
+        attempt -- checksums, barrier, verdict -- so a retry after a failed kernel-path attempt never
+        meets the first attempt's counters (a reused barrier key is already at world size and would
+        let an owner check its inbox before the workers' second pushes landed)."""
         dev = self.device
+        tag = f"{attempt}"
         ok, why = True, ""
         for k in self.my_shards:  # the snapshot each owner published: bf16/fp32(master)
             v = self.master[k].to(self.param_dtype).double()
-            self.store.set(f"{self._key}/ck/{k}", f"{float(v.sum())!r} {float(v.abs().sum())!r}")
+            self.store.set(f"{self._key}/ck/{tag}/{k}", f"{float(v.sum())!r} {float(v.abs().sum())!r}")
         if self.is_worker:
             pat = (torch.arange(self.total, device=dev) % 251 + (self.rank + 1)).to(self.param_dtype)
             self.engine.push(0, pat, 0, self.total, self._stream_ptr())
@@ -339,15 +345,17 @@ class AsyncPS:
             if self.is_cuda:
                 torch.cuda.synchronize(dev)
             for k in range(self.P):
-                self.store.wait([f"{self._key}/ck/{k}"])
-                want_s, want_a = (float(x) for x in self.store.get(f"{self._key}/ck/{k}").decode().split())
+                self.store.wait([f"{self._key}/ck/{tag}/{k}"])
+                want_s, want_a = (float(x) for x in self.store.get(f"{self._key}/ck/{tag}/{k}").decode().split())
                 sl = got.narrow(0, self.shard_off[k], self.shard_len[k]).double()
                 if abs(float(sl.sum()) - want_s) > 1e-6 * max(want_a, 1.0) or \
                         abs(float(sl.abs().sum()) - want_a) > 1e-6 * max(want_a, 1.0):
                     ok, why = False, f"rank {self.rank}: pulled shard {k} != its owner's snapshot"
         if fault("selftest_fail_rank") == self.rank:  # fault injection (tests)
             ok, why = False, f"rank {self.rank}: injected self-test failure"
-        self._barrier("selftest-push")
+        if attempt == "kernel" and fault("selftest_fail_kernel") == self.rank:  # fails the kernel path only
+            ok, why = False, f"rank {self.rank}: injected kernel-transport self-test failure"
+        self._barrier(f"selftest-push/{tag}")
         for k in self.my_shards:
             for wi, w in enumerate(self.worker_ranks):
                 v = self.engine.inbox_view(k, wi, 0)
@@ -358,16 +366,18 @@ class AsyncPS:
                 v.zero_()
         if self.is_cuda:
             torch.cuda.synchronize(dev)
-        self._agree("selftest", "" if ok else why)
+        self._agree("selftest", "" if ok else why, attempt=tag)
         self.selftest_ok = True
 
-    def _agree(self, tag: str, err: str):
-        """Collective status exchange through the store: every rank raises if any rank failed."""
-        self.store.set(f"{self._key}/{tag}/{self.rank}", err or "ok")
+    def _agree(self, tag: str, err: str, attempt: str = ""):
+        """Collective status exchange through the store: every rank raises if any rank failed.
+        ``attempt`` keeps the keys of a retried exchange apart from the earlier ones."""
+        key = f"{self._key}/{tag}" + (f"/{attempt}" if attempt else "")
+        self.store.set(f"{key}/{self.rank}", err or "ok")
         errs = []
         for r in range(self.world):
-            self.store.wait([f"{self._key}/{tag}/{r}"])
-            v = self.store.get(f"{self._key}/{tag}/{r}").decode()
+            self.store.wait([f"{key}/{r}"])
+            v = self.store.get(f"{key}/{r}").decode()
             if v != "ok":
                 errs.append(v)
         if errs:
@@ -587,7 +597,7 @@ class AsyncPS:
         g = self.grads[0]
         elem = g.element_size()
         for mb in sizes_mb:
-            n = max(ALIGN, int(mb * (1 << 20)) // elem)
+            n = max(ALIGN, int(mb * (1 << 20)) // elem // ALIGN * ALIGN)  # chunk ends stay 16-B aligned
             el, err = 0.0, None
             if self.is_worker:
                 def run():
@@ -617,6 +627,61 @@ class AsyncPS:
             el = float(t[0])
             out[mb] = round(self.total * elem * self.P / max(el, 1e-9) / 1e9, 1) if el > 0 else None
         return out
+
+    def probe_xfer_blocks(self, caps=(8, 16, 24, 32, 48, 64, 96), reps: int = 3, keep: float = 0.9) -> dict:
+        """The scatter kernel's workgroup budget (collective, every rank; before training): each
+        worker pushes its whole gradient buffer into its inbox slot on every owner in one launch per
+        cap, timed (max over ranks). Returns {"GBps": {cap: GB/s}, "chosen": cap}: the SMALLEST cap
+        within ``keep`` of the best bandwidth -- the fewest CUs the push takes from the backward
+        pass running beside it for (nearly) the same link throughput -- and sets it on the engine.
+        Only meaningful where the kernel transport runs (a remote owner); otherwise returns {}."""
+        if not (self.is_cuda and self.xfer_mode == "kernel") or all(o == self.rank for o in self.owners):
+            remote = False
+        else:
+            remote = True
+        t = torch.tensor([1.0 if remote else 0.0], dtype=torch.float64)
+        if self.world > 1 and dist.is_initialized():
+            if dist.get_backend() == "nccl":
+                t = t.to(self.device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        if float(t[0]) == 0.0 or not self.is_cuda:
+            return {}
+        g = self.grads[0]
+        old = self.engine.xfer_blocks_cap()
+        res = {}
+        for cap in caps:
+            self.engine.set_xfer_blocks(int(cap))
+            el, err = 0.0, None
+            if self.is_worker:
+                try:
+                    st = self.comm_streams[0]
+                    self.engine.push(self.step_idx, g, 0, self.total, st.cuda_stream)
+                    st.synchronize()
+                    t0 = time.perf_counter()
+                    for _ in range(reps):
+                        self.engine.push(self.step_idx, g, 0, self.total, st.cuda_stream)
+                    st.synchronize()
+                    el = (time.perf_counter() - t0) / reps
+                except Exception as e:  # noqa: BLE001 -- reported collectively below
+                    err = e
+            t = torch.tensor([el, 1.0 if err is not None else 0.0], dtype=torch.float64)
+            if self.world > 1 and dist.is_initialized():
+                if dist.get_backend() == "nccl":
+                    t = t.to(self.device)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            if float(t[1]) > 0:
+                self.engine.set_xfer_blocks(old)
+                raise RuntimeError(f"xfer workgroup probe failed on a rank{f': {err}' if err is not None else ''}")
+            el = float(t[0])
+            res[int(cap)] = round(self.total * g.element_size() / max(el, 1e-9) / 1e9, 1) if el > 0 else None
+        ok = {c: v for c, v in res.items() if v}
+        if not ok:  # no worker timed anything (a pure-owner world): keep the default
+            self.engine.set_xfer_blocks(old)
+            return {"GBps": res, "chosen": old}
+        best = max(ok.values())
+        chosen = min(c for c, v in ok.items() if v >= keep * best)
+        self.engine.set_xfer_blocks(chosen)
+        return {"GBps": res, "chosen": chosen}
 
     def probe_bandwidth(self, reps: int = 3) -> dict:
         """After ``drain``: time this worker's full push (DMA of the whole gradient into its inbox slot

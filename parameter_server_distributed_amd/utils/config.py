@@ -148,6 +148,7 @@ FAULTS: dict[str, tuple[int, str]] = {
     "push_delay_ms": (0, "worker: sleep this long before every gradient push"),
     "exit_after_push": (-1, "worker: exit the process right after its k-th push"),
     "selftest_fail_rank": (-1, "async PS: this rank reports a failed start-up self-test"),
+    "selftest_fail_kernel": (-1, "async PS: this rank fails the kernel-transport self-test attempt only"),
 }
 
 

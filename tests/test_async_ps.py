@@ -67,7 +67,8 @@ def _worker(rank, world, port, shards, stale, steps, out_dir, slow_rank, delay_s
     torch.save({"rank": rank, "rec": rec, "log": ps.apply_log(), "init": init_master,
                 "master": {k: v.cpu() for k, v in ps.master.items()}, "mem": ps.engine.memory_kind(),
                 "hist": ps.staleness_histogram(), "shard_off": ps.shard_off, "shard_len": ps.shard_len,
-                "workers": ps.worker_ranks, "owners": ps.owners, "xfer": ps.xfer_mode},
+                "workers": ps.worker_ranks, "owners": ps.owners, "xfer": ps.xfer_mode,
+                "xfer_fallback": ps.xfer_fallback},
                os.path.join(out_dir, f"r{rank}.pt"))
     ps.close()
     dist.barrier()
@@ -246,6 +247,21 @@ def test_async_gpu_xfer_kernel_bitwise_equals_copies(tmp_path, gpu):
         for ea, eb in zip(a["rec"], b["rec"]):
             assert ea["pulled"] == eb["pulled"]
             assert torch.equal(ea["weights"], eb["weights"]) and torch.equal(ea["grad"], eb["grad"])
+
+
+@pytest.mark.gpu
+def test_async_gpu_kernel_selftest_failure_falls_back_on_every_rank(tmp_path, gpu, monkeypatch):
+    """with xfer="auto" a failed kernel-transport self-test on ONE rank retries the
+    self-test on the copy path under fresh store keys; every rank must end on hipMemcpyAsync (none
+    raises, none starts on the kernel path) and the run replays exactly."""
+    monkeypatch.setenv("PSD_FAULT", "selftest_fail_kernel=1")
+    mp.spawn(_worker, args=(3, _port(), 2, 0, 3, str(tmp_path), -1, 0.0, False, "cuda:0", "momentum", "bf16", "auto"),
+             nprocs=3, join=True)
+    _replay_and_check(str(tmp_path), 3, 0, bf16=True)
+    for r in range(3):
+        res = torch.load(os.path.join(str(tmp_path), f"r{r}.pt"), weights_only=False)
+        assert res["xfer"] == "hipMemcpyAsync", (r, res["xfer"])
+        assert "injected kernel-transport" in (res["xfer_fallback"] or ""), (r, res["xfer_fallback"])
 
 
 # World 8 on ONE MI355X (8 processes, real IPC mappings, the scatter / gather kernels): the BASELINE

@@ -133,3 +133,64 @@ def test_prefer_own_within_margin(monkeypatch):
         for k in [("t", i) for i in range(1, 5)]:
             at._DECISIONS.pop(k, None)
             at._TIMES.pop(k, None)
+
+
+def test_guard_rejects_zeros_on_small_magnitude_output():
+    """with an absolute 1e-2 floor a candidate returning zeros passed wherever the
+    reference's entries were all below 0.01 (a small weight gradient). The guard is now relative only."""
+    from parameter_server_distributed_amd.ops import autotune as at
+
+    g = torch.Generator().manual_seed(0)
+    ref = torch.randn(64, 32, generator=g) * 1e-3  # |entries| < 0.01
+    assert not at._agrees([torch.zeros_like(ref)], [ref])
+    assert not at._agrees([ref * 0.9], [ref])  # a 10 % scale error is wrong, whatever the magnitude
+    # bf16 rounding of the same values and a changed fp32 summation order are accepted
+    assert at._agrees([ref.to(torch.bfloat16).float()], [ref])
+    assert at._agrees([ref + 1e-4 * ref.abs().max() * torch.randn(64, 32, generator=g)], [ref])
+    # an all-zero reference takes only zeros; non-finite reference entries are skipped
+    z = torch.zeros(8)
+    assert at._agrees([z.clone()], [z]) and not at._agrees([z + 1e-12], [z])
+    r = torch.tensor([1.0, float("nan"), 2.0])
+    assert at._agrees([torch.tensor([1.0, 5.0, 2.0])], [r])
+    assert not at._agrees([torch.tensor([1.0, 5.0, float("inf")])], [r])
+
+
+def test_zeros_candidate_never_chosen(monkeypatch):
+    """End to end through _time_and_pick: the fastest candidate returns zeros on a small-magnitude
+    weight gradient and must be rejected, not chosen."""
+    from parameter_server_distributed_amd.ops import autotune as at
+
+    ref = torch.full((16, 16), 3e-3)
+    outs = {"mfma": ref, "fast_zero": torch.zeros(16, 16)}
+    times = {"mfma": 1.0, "fast_zero": 0.5}
+    monkeypatch.setattr(at, "_time_ms", lambda fn, probe=None: (times[fn()], [outs[fn()], outs[fn()]]))
+    key = ("t", "zeros")
+    try:
+        assert at._time_and_pick(key, {"mfma": lambda: "mfma", "fast_zero": lambda: "fast_zero"}, "mfma", None) == "mfma"
+        assert "fast_zero" in at.rejected()[key]
+    finally:
+        at._DECISIONS.pop(key, None)
+        at._TIMES.pop(key, None)
+        at._REJECTED.pop(key, None)
+
+
+def test_decision_file_schema(tmp_path):
+    """a decision file of another schema (older variant numbering) is refused."""
+    import json
+
+    import pytest
+
+    from parameter_server_distributed_amd.ops import autotune as at
+
+    old = tmp_path / "old.json"
+    old.write_text(json.dumps({"('conv1x1', 'wgrad', 1, 2, 3)": "psdw1"}))  # pre-schema format
+    with pytest.raises(ValueError, match="schema"):
+        at.load_decisions(str(old))
+    assert ("conv1x1", "wgrad", 1, 2, 3) not in at.decisions()
+    at.set_decision(("t", "schema"), "a")
+    try:
+        at.save_decisions(str(tmp_path / "new.json"))
+        assert json.loads((tmp_path / "new.json").read_text())["schema"] == at.SCHEMA
+        assert at.load_decisions(str(tmp_path / "new.json")) >= 1
+    finally:
+        at.set_decision(("t", "schema"), None)
