@@ -76,6 +76,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("aux") = py::none(), py::arg("part") = py::none(),
         py::arg("shift") = py::none());
   m.def("gemm_stats_rows", &gemm_stats_rows_, py::arg("M"));
+  m.def("gemm_ct_", &gemm_ct_, py::arg("A"), py::arg("B"), py::arg("out"), py::arg("bias") = py::none(),
+        py::arg("act") = 0, py::arg("aux") = py::none());
   m.def("gemm_gelu_bwd_", &gemm_gelu_bwd_, py::arg("A"), py::arg("B"), py::arg("a_kmajor"), py::arg("b_kmajor"),
         py::arg("pre"), py::arg("out"), py::arg("db"), py::arg("accumulate") = false);
   m.def("gemm_splitk_", &gemm_splitk_, py::arg("A"), py::arg("B"), py::arg("a_kmajor"), py::arg("b_kmajor"),

@@ -83,6 +83,45 @@ int64_t gemm_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool b_km
   return a.part ? rows : 1;
 }
 
+bool gemm_ct_(const at::Tensor& A, const at::Tensor& B, at::Tensor out, c10::optional<at::Tensor> bias, int64_t act,
+              c10::optional<at::Tensor> aux) {
+  chk2d(A, "A");
+  chk2d(B, "B");
+  const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
+  TORCH_CHECK(B.size(1) == K, "psd gemm_ct: K mismatch ", K, " vs ", B.size(1));
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == N && out.size(1) == M && out.stride(1) == 1 &&
+                  (out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat),
+              "psd gemm_ct: out must be [N, M] bf16 / fp32 with unit inner stride");
+  TORCH_CHECK(act >= 0 && act <= 2, "psd gemm_ct: act 0-2");
+  const bool has_aux = aux.has_value() && aux->defined();
+  if (has_aux)
+    TORCH_CHECK(aux->sizes() == out.sizes() && aux->strides() == out.strides() && aux->scalar_type() == at::kBFloat16,
+                "psd gemm_ct: aux like out (bf16)");
+  const bool has_bias = bias.has_value() && bias->defined();
+  if (has_bias) TORCH_CHECK(bias->numel() == M && bias->scalar_type() == at::kBFloat16, "psd gemm_ct: bias [M] bf16");
+  const c10::DeviceGuard g(A.device());
+  GemmArgs a{};
+  a.A = A.data_ptr();
+  a.B = B.data_ptr();
+  a.C = out.data_ptr();
+  a.bias = has_bias ? bias->data_ptr() : nullptr;
+  a.aux = has_aux ? aux->data_ptr() : nullptr;
+  a.M = (int)M;
+  a.N = (int)N;
+  a.K = (int)K;
+  a.lda = (int)A.stride(0);
+  a.ldb = (int)B.stride(0);
+  a.ldc = (int)out.stride(0);
+  a.a_kmajor = 1;
+  a.b_kmajor = 1;
+  a.act = (int)act;
+  a.c_f32 = out.scalar_type() == at::kFloat;
+  hipError_t e = launch_gemm_ct(a, stream_of(A));
+  if (e == hipErrorNotSupported) return false;
+  TORCH_CHECK(e == hipSuccess, "psd gemm_ct: ", hipGetErrorString(e));
+  return true;
+}
+
 // GELU-backward GEMM: out[M,N] = bf16(bf16(A op B) * gelu'(pre)) with the bias gradient
 // db[N] (+)= colsum(out) from the epilogue's per-tile partials (kernels/gemm.hip ACT 3): the
 // gradient of a GELU Linear's output computed by the next Linear's bwd-data GEMM goes straight to

@@ -325,8 +325,12 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 __device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
-// per-lane byte offsets of one operand's pieces (piece i of half h), loop-invariant
-template <bool KMAJ, int SEG, int ESZ, int PW>
+// per-lane byte offsets of one operand's pieces (piece i of half h), loop-invariant. VR: the valid
+// rows (K-major) / columns (M/N-major) of a half image (BM = 192: 96 of its 128; the rest of the
+// padded image is never read): the pieces / lanes past them get kMasked, an offset past every
+// descriptor's range (operands < 2 GiB there), so their DMA writes zeros and moves no bytes
+constexpr uint32_t kMasked = 0x80000000u;
+template <bool KMAJ, int SEG, int ESZ, int PW, int VR = 128>
 __device__ __forceinline__ void stage8_offsets(int ld, int wid, int lane, uint32_t (*vo)[PW]) {
 #pragma unroll
   for (int h = 0; h < 2; ++h)
@@ -336,12 +340,12 @@ __device__ __forceinline__ void stage8_offsets(int ld, int wid, int lane, uint32
       if (KMAJ) {  // [128 rows][128 B of k]: a piece is 8 rows x 128 B
         const int row = piece * 8 + (lane >> 3);
         const int c = (lane & 7) ^ ((row >> 1) & 7);
-        vo[h][i] = (uint32_t)half_to_tile<SEG>(row, h) * (uint32_t)ld * ESZ + c * 16;
+        vo[h][i] = row < VR ? (uint32_t)half_to_tile<SEG>(row, h) * (uint32_t)ld * ESZ + c * 16 : kMasked;
       } else {  // [64 k][128 cols] bf16: a piece is 4 k-rows x 256 B
         const int k = piece * 4 + (lane >> 4);
         const int f = (k & 3) | ((k >> 1) & 4);
         const int col = ((lane & 15) * 8) ^ (f << 4);
-        vo[h][i] = ((uint32_t)k * (uint32_t)ld + half_to_tile<SEG>(col, h)) * ESZ;
+        vo[h][i] = col < VR ? ((uint32_t)k * (uint32_t)ld + half_to_tile<SEG>(col, h)) * ESZ : kMasked;
       }
     }
 }
@@ -394,10 +398,9 @@ __device__ __forceinline__ void wait_vm() {
 }
 template <int N>
 __device__ __forceinline__ void wait_lgkm() {
-  if constexpr (N >= 15) asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");
-  else if constexpr (N == 8) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
-  else if constexpr (N == 4) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
-  else static_assert(N == 8 || N == 4, "lgkmcnt");
+  static_assert(N >= 0, "lgkmcnt");
+  if constexpr (N >= 15) asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");  // the counter saturates at 15
+  else asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
 }
 
 template <int CTRL>
@@ -476,11 +479,17 @@ __device__ __forceinline__ void tile_of(int wg, int tiles_m, int tiles_n, int& t
 // MX: the block-scaled fp8 form (per-32-K E8M0 scales of A rows and B columns): each K-tile's
 // scales (BM x 4 B of A, 256 x 4 B of B) ride in SC bytes at the end of its buffer, staged by one
 // extra 4-byte LDS-DMA per wave with the A-half0 pieces (so it is counted in VM like them).
+// BM = 192 (IM = 3, 48-row quadrants) keeps the 256-row LDS geometry: each A half image is padded
+// to 128 rows / columns (the last 32 masked at staging, never read), so the staging and the
+// fragment reads are the BM = 256 ones and the LDS is 160 KiB. With CT (C^T stored) it is the
+// 256 x 192 tile of Y = X W^T: 768-wide outputs make 4 x 128 = 512 tiles (2.0 rounds on 256 CUs)
+// instead of 384 256-tiles (1.5 rounds, the last half idle).
 template <int BM, bool MX = false>
 struct P8 {
   static constexpr int IM = BM / 64;         // 16-row blocks per quadrant
   static constexpr int QA = BM / 4;          // quadrant rows
-  static constexpr int HA = BM / 2 * 128;    // A half-tile bytes
+  static constexpr int VA = BM / 2;          // valid rows (K-major) / cols (M-major) of an A half image
+  static constexpr int HA = (BM == 192 ? 128 : BM / 2) * 128;  // A half-tile bytes (BM 192: padded)
   static constexpr int HB = 128 * 128;       // B half-tile bytes
   static constexpr int PWA = HA / 8192;      // A DMA pieces per wave per half-tile
   static constexpr int VM = 4 + PWA + (MX ? 1 : 0);  // DMA in flight after phase 3 (three half-tiles)
@@ -520,9 +529,16 @@ __device__ __forceinline__ float act_apply(float x) {
 // dW[cout][(r, s, ci)] = sum over output pixels p of dY[p][cout] * x[pixel(p) + (r, s)][ci], A = dY
 // M-major ([pixels][cout]), B = the gathered [pixels][R*S*C] N-major image (each lane's 16 bytes are
 // 8 channels of one shifted input pixel; pixels outside the image load zeros).
+// CT: the tile is stored transposed -- Y[n][m] = C[m][n], Y's row stride g.ldc -- with the bias per C
+// row (g.bias [M]) and ACT 0 / 1 / 2 (+ aux): Y = X W^T + b with A = W [out][in], B = X [tokens][in].
+// In the MFMA register layout a lane holds 4 consecutive C rows of one column = 4 contiguous Y
+// elements, so the store needs no transpose (8-byte bf16 / 16-byte fp32 per lane and block).
 template <int BM, bool AK, bool BKM, int MODE, bool F8 = false, int ACT = 0, bool GA = false, int F8A = 0,
-          bool GB = false, bool MX = false, bool ST = false>
+          bool GB = false, bool MX = false, bool ST = false, bool CT = false>
 __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
+  static_assert(!CT || (MODE == 0 && !ST && !GA && !GB && !F8 && ACT <= 2 && AK && BKM),
+                "transposed store: plain bf16 single-split GEMM of K-major operands");
+  static_assert(BM != 192 || (!MX && !GA && !F8 && !ST && MODE == 0), "192-row tiles: plain bf16 GEMM");
   static_assert(!ST || (MODE == 0 && !GB && ACT == 0 && AK),
                 "statistics epilogue: single split, bf16 out, no activation, K-major A (zero rows past M)");
   static_assert(!MX || (F8 && BM == 128 && MODE == 0), "MX: fp8, 128-row tiles (LDS), single split");
@@ -576,7 +592,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
   const uint32_t bytesA = AK ? ((uint32_t)(g.M - 1) * g.lda + g.K) * ESZ : ((uint32_t)(g.K - 1) * g.lda + g.M) * ESZ;
   const uint32_t bytesB = BKM ? ((uint32_t)(g.N - 1) * g.ldb + g.K) * ESZ : ((uint32_t)(g.K - 1) * g.ldb + g.N) * ESZ;
   uint32_t voA[2][P::PWA], voB[2][2];  // [half][piece]
-  stage8_offsets<AK, P::QA, ESZ, P::PWA>(g.lda, wid, lane, voA);
+  stage8_offsets<AK, P::QA, ESZ, P::PWA, P::VA>(g.lda, wid, lane, voA);
   stage8_offsets<BKM, 32, ESZ, 2>(g.ldb, wid, lane, voB);
   // GA: per (tile, half, piece) the window origin of the lane's output pixel: p0 = its top-left input
   // pixel index, hw = (h0 << 16) | (w0 & 0xffff) (h0 = -32768 for rows past M)
@@ -775,7 +791,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
 
   // VMEM stores of one tile's epilogue, per lane, in both output paths (exact: every store is
   // issued unconditionally, out-of-range rows/cols go to an offset outside the buffer descriptor)
-  constexpr int kEpiStores = 8 * IM + (ST ? 8 : 0);
+  constexpr int kEpiStores = 8 * IM + (ST ? 8 : 0) + (CT ? 8 * IM : 0);  // CT: C and aux per block
   // One K-tile of the 8-phase schedule at stream index u (= base + t); (am1, ak1) is the A source
   // of K-tile u+1, (am2, bn2, ak2) the A/B sources of K-tile u+2. first: the K-tile right after an
   // epilogue, whose phase-0 DMA was issued before the epilogue's stores; its phase-3 wait leaves
@@ -823,7 +839,8 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
   const bool f32out = MODE == 1 || g.c_f32;
   uint8_t* cbase = reinterpret_cast<uint8_t*>(g.C) + (MODE == 1 ? (int64_t)blockIdx.z * g.M * g.N * 4 : 0);
   const int ldo = MODE == 1 ? g.N : g.ldc;
-  const uint32_t cbytes = ((uint32_t)(g.M - 1) * ldo + g.N) * (f32out ? 4 : 2);
+  const uint32_t cbytes = CT ? ((uint32_t)(g.N - 1) * ldo + g.M) * (f32out ? 4 : 2)
+                              : ((uint32_t)(g.M - 1) * ldo + g.N) * (f32out ? 4 : 2);
   const bool want_aux = MODE == 0 && ACT == 2 && g.aux;
   uint8_t* stg = smem + 2 * P::BUF + wid * P::STG;  // this wave's epilogue staging slot
   float fmul = 1.f;
@@ -837,10 +854,16 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
     // (columns past N load zeros); retired by the K loop's own counted waits (older than its DMA,
     // nt >= 2) and read back at the epilogue. A register load would make the compiler wait for it,
     // and with it every older store and DMA, right here.
-    if (MODE == 0 && g.bias)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(make_rsrc(g.bias, (uint32_t)g.N * 2),
-                                               (__attribute__((address_space(3))) void*)stg, 4,
-                                               (uint32_t)(cn0 + wc * 64 + 2 * lane) * 2, 0, 0, 0);
+    if (MODE == 0 && g.bias) {
+      if constexpr (CT)  // the bias of the wave row's BM / 2 C rows (lanes past them: never read)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(make_rsrc(g.bias, (uint32_t)g.M * 2),
+                                                 (__attribute__((address_space(3))) void*)stg, 4,
+                                                 (uint32_t)(cm0 + wr * (BM / 2) + 2 * lane) * 2, 0, 0, 0);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(make_rsrc(g.bias, (uint32_t)g.N * 2),
+                                                 (__attribute__((address_space(3))) void*)stg, 4,
+                                                 (uint32_t)(cn0 + wc * 64 + 2 * lane) * 2, 0, 0, 0);
+    }
     if constexpr (ST)  // the statistics shift of the wave's 64 columns -> staging slot bytes 256..511
       __builtin_amdgcn_raw_ptr_buffer_load_lds(make_rsrc(g.shift, (uint32_t)g.N * 4),
                                                (__attribute__((address_space(3))) void*)(stg + 256), 4,
@@ -866,7 +889,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
 
     // ---- epilogue of tile jt (no barrier: the pipeline LDS already holds the next tile)
     float bv[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
-    if (MODE == 0 && g.bias) {
+    if (!CT && MODE == 0 && g.bias) {
 #pragma unroll
       for (int qn = 0; qn < 2; ++qn)
 #pragma unroll
@@ -877,7 +900,55 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
       for (int i = 0; i < 8 * IM; ++i) acc[i] *= fmul;
     }
     const rsrc_t rc = make_rsrc(cbase, cbytes);
-    if (f32out) {  // fp32: 16-byte row segments straight from registers
+    if constexpr (CT) {
+      // Y[n][m] = C[m][n]: per 16x16 block the lane's 4 accumulators are C rows rq..rq+3 of column
+      // cl = 4 contiguous Y elements (g.M % 4 == 0: all valid or none); every store is issued (the
+      // aux store against an empty descriptor when there is none), as the count kEpiStores assumes
+      const bool has_bias = g.bias != nullptr;
+      const rsrc_t ra = make_rsrc(want_aux ? g.aux : g.C, want_aux ? cbytes : 0u);
+      const uint16_t* bst = reinterpret_cast<const uint16_t*>(stg);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int i = 0; i < IM; ++i) {
+          const int mloc = (q >> 1) * P::QA + i * 16 + rq;  // within the wave row's BM / 2 rows
+          const int m = cm0 + wr * (BM / 2) + mloc;
+          float b4[4] = {0.f, 0.f, 0.f, 0.f};
+          if (has_bias) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) b4[r] = bf16_to_f32(bst[mloc + r]);
+          }
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int n = cn0 + wc * 64 + (q & 1) * 32 + j * 16 + cl;
+            const f32x4 a = acc[(q * IM + i) * 2 + j];
+            float w[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) w[r] = a[r] + b4[r];
+            const bool ok = m < g.M && n < g.N;
+            if (f32out) {
+              float o[4];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) o[r] = act_apply<ACT>(w[r]);
+              const uint32_t off = ok ? ((uint32_t)n * ldo + m) * 4 : kOOB;
+              __builtin_amdgcn_raw_buffer_store_b128(
+                  u32x4{__float_as_uint(o[0]), __float_as_uint(o[1]), __float_as_uint(o[2]), __float_as_uint(o[3])},
+                  rc, off, 0, 0);
+              __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, ra, kOOB, 0, 0);
+            } else {
+              const uint32_t off = ok ? ((uint32_t)n * ldo + m) * 2 : kOOB;
+              typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+              __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pack_bf16x2(w[0], w[1]), pack_bf16x2(w[2], w[3])}, ra,
+                                                    want_aux ? off : kOOB, 0, 0);
+              float o[4];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) o[r] = act_apply<ACT>(w[r]);
+              __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])}, rc, off,
+                                                    0, 0);
+            }
+          }
+        }
+    } else if (f32out) {  // fp32: 16-byte row segments straight from registers
 #pragma unroll
       for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -1251,14 +1322,14 @@ static int cu_count() {
 static int persistent_grid() { return cu_count(); }
 
 template <int BM, bool AK, bool BKM, int MODE, bool F8, int ACT, bool GA = false, int F8A = 0, bool GB = false,
-          bool MX = false, bool ST = false>
+          bool MX = false, bool ST = false, bool CT = false>
 static hipError_t launch_8p_act(const GemmArgs& g, int splits, hipStream_t st) {
   if constexpr (ACT == 3) {  // GELU backward + bias-gradient partials (g.aux = pre, g.part = [rows][N])
     if (!g.part || !g.aux || g.c_f32 || g.bias || splits != 1) return hipErrorNotSupported;
     if (g.rows_out) *g.rows_out = (g.M + BM - 1) / BM * 2;
   } else if constexpr (!ST) {
     if (g.part) {  // the consumer BN's statistics in the epilogue
-      if constexpr (MODE == 0 && !GB && ACT == 0 && AK) {
+      if constexpr (MODE == 0 && !GB && ACT == 0 && AK && !CT && BM != 192) {
         if (g.c_f32 || g.bias || !g.shift || splits != 1) return hipErrorNotSupported;
         if (g.rows_out) *g.rows_out = (g.M + BM - 1) / BM * 2;
         return launch_8p_act<BM, AK, BKM, MODE, F8, ACT, GA, F8A, GB, MX, true>(g, splits, st);
@@ -1270,7 +1341,7 @@ static hipError_t launch_8p_act(const GemmArgs& g, int splits, hipStream_t st) {
   constexpr int lds = P8<BM, MX>::LDS;
   static bool attr_set = false;  // per instantiation: set the >64 KiB LDS limit once
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT, GA, F8A, GB, MX, ST>,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT, GA, F8A, GB, MX, ST, CT>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     attr_set = true;
@@ -1281,8 +1352,8 @@ static hipError_t launch_8p_act(const GemmArgs& g, int splits, hipStream_t st) {
   constexpr int KT = F8 ? 128 : BK;
   int grid = nwg;
   if (MODE == 0 && splits == 1 && g.K / KT >= 2) grid = std::min(nwg, persistent_grid());
-  hipLaunchKernelGGL((gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT, GA, F8A, GB, MX, ST>), dim3(grid, 1, splits), dim3(512),
-                     lds, st, g);
+  hipLaunchKernelGGL((gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT, GA, F8A, GB, MX, ST, CT>), dim3(grid, 1, splits),
+                     dim3(512), lds, st, g);
   return hipGetLastError();
 }
 
@@ -1359,6 +1430,21 @@ hipError_t launch_gemm(const GemmArgs& g, hipStream_t st) {
   if (g.a_kmajor && !g.b_kmajor) return launch_layout<true, false, 0>(g, 1, st);
   if (!g.a_kmajor && !g.b_kmajor) return launch_layout<false, false, 0>(g, 1, st);
   return launch_layout<false, true, 0>(g, 1, st);
+}
+
+// Y[N][M] (row stride g.ldc) = (A . B^T)^T (+ bias[M])(act) on 192 x 256 tiles (A rows x B rows):
+// Y = X W^T + b with A = W [M = out][K], B = X [N = tokens][K], both K-major.
+hipError_t launch_gemm_ct(const GemmArgs& g, hipStream_t st) {
+  if (g.M <= 0 || g.N <= 0) return hipSuccess;
+  const int64_t ab = ((int64_t)(g.M - 1) * g.lda + g.K) * 2, bb = ((int64_t)(g.N - 1) * g.ldb + g.K) * 2;
+  const int64_t cb = ((int64_t)(g.N - 1) * g.ldc + g.M) * (g.c_f32 ? 4 : 2);
+  const bool ok = g.a_kmajor && g.b_kmajor && g.M % 8 == 0 && g.ldc % 8 == 0 && g.K % 64 == 0 && g.K >= 128 &&
+                  g.act >= 0 && g.act <= 2 && !g.part && !(g.aux && g.c_f32) && ab < ((int64_t)1 << 31) &&
+                  bb < ((int64_t)1 << 32) && cb < ((int64_t)1 << 32) && !(reinterpret_cast<uintptr_t>(g.bias) & 3);
+  if (!ok) return hipErrorNotSupported;
+  if (g.act == 1) return launch_8p_act<192, true, true, 0, false, 1, false, 0, false, false, false, true>(g, 1, st);
+  if (g.act == 2) return launch_8p_act<192, true, true, 0, false, 2, false, 0, false, false, false, true>(g, 1, st);
+  return launch_8p_act<192, true, true, 0, false, 0, false, 0, false, false, false, true>(g, 1, st);
 }
 
 hipError_t launch_conv_fwd(const GemmArgs& g, hipStream_t st) {

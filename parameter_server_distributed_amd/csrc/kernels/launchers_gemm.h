@@ -36,6 +36,9 @@ struct GemmArgs {
 };
 
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t stream);
+// transposed store on 192 x 256 tiles: C [N][ldc] = (A . B^T)^T (+ bias[M])(act 0-2, aux), A [M][K] and
+// B [N][K] K-major, M % 8 == 0, K % 64 == 0; hipErrorNotSupported outside that contract
+hipError_t launch_gemm_ct(const GemmArgs& g, hipStream_t stream);
 // C = (A_e4m3 . B_e4m3^T) * a_scale * b_scale (+bias)(act); A [M][K], B [N][K] fp8, K % 128 == 0
 hipError_t launch_gemm_fp8(const GemmArgs& g, hipStream_t stream);
 int gemm_splits(int M, int N, int K);

@@ -77,6 +77,11 @@ int64_t gemm_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool b_km
               c10::optional<at::Tensor> part, c10::optional<at::Tensor> shift);
 // statistics partial rows to allocate for a gemm_ / gemm_fp8_ / conv_fwd_ with part (any tile height)
 int64_t gemm_stats_rows_(int64_t M);
+// out[N, M] = B A^T (+bias[M])(act 0-2, aux = pre-activation) on 192 x 256 tiles stored transposed
+// (A [M, K], B [N, K] K-major: Y = X W^T + b with A = W, B = X); False when the shape is outside the
+// kernel's contract (nothing launched)
+bool gemm_ct_(const at::Tensor& A, const at::Tensor& B, at::Tensor out, c10::optional<at::Tensor> bias, int64_t act,
+              c10::optional<at::Tensor> aux);
 bool gemm_gelu_bwd_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool b_kmajor, const at::Tensor& pre,
                     at::Tensor out, at::Tensor db, bool accumulate);
 void gemm_splitk_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool b_kmajor, at::Tensor out,

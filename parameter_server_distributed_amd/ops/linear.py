@@ -40,13 +40,22 @@ def _ok(x: torch.Tensor, w: torch.Tensor) -> bool:
             and w.shape[1] % 8 == 0)
 
 
-def _route(key: tuple, mfma, blas, out: torch.Tensor | None = None):
-    """The faster of the MFMA kernel and hipBLASLt for this GEMM shape (ops/autotune.py); ``out``
-    is the buffer both candidates write (validated against each other on the first call)."""
+def _route(key: tuple, mfma, blas, out: torch.Tensor | None = None, extra: dict | None = None):
+    """The fastest of the MFMA kernel(s) and hipBLASLt for this GEMM shape (ops/autotune.py); ``out``
+    is the buffer every candidate writes (validated against each other on the first call);
+    ``extra``: more MFMA candidates by name (e.g. "mfma_ct", the 192 x 256 transposed-store tile)."""
     if not _feat("linear_tune"):
         return mfma
     probe = (lambda: out) if out is not None else None
-    return mfma if _at.choose(("linear",) + key, {"mfma": mfma, "blas": blas}, "mfma", probe) == "mfma" else blas
+    cands = {"mfma": mfma, **(extra or {}), "blas": blas}
+    return cands[_at.choose(("linear",) + key, cands, "mfma", probe)]
+
+
+def _ct(A, B, out, bias=None, act=0, aux=None):
+    """Y = B A^T (+bias)(act) on the 192 x 256 transposed-store tile (kernels/gemm.hip CT): for 768-wide
+    outputs 512 tiles = 2.0 rounds on 256 CUs where the 256 x 256 tile makes 384 = 1.5 rounds."""
+    if not native().gemm_ct_(A, B, out, bias, act, aux):
+        raise _at.Declined("192x256 transposed-store GEMM: shape outside the kernel's contract")
 
 
 def _dgrad_route(key: tuple, dy2: torch.Tensor, w: torch.Tensor, dx: torch.Tensor):
@@ -68,9 +77,12 @@ def _dgrad_route(key: tuple, dy2: torch.Tensor, w: torch.Tensor, dx: torch.Tenso
         # K = 30,528 against 19 x 3 256-tiles, ran one K-loop per tile on 57 of 256 CUs)
         C.gemm_splitk_(dy2, w, True, False, dx)
 
+    def ct():  # dX = dY W on the 192 x 256 transposed-store tile: A = W^T [in, out], B = dY [tokens, out]
+        _ct(w.t().contiguous(), dy2, dx)
+
     if not _feat("linear_tune"):
         return nn_
-    cands = {"mfma": nn_, "mfma_t": nt_, "blas": blas}
+    cands = {"mfma": nn_, "mfma_t": nt_, "mfma_ct": ct, "blas": blas}
     if dy2.shape[1] >= 4096 and dy2.shape[1] % 64 == 0:
         cands["mfma_sk"] = sk
     return cands[_at.choose(("linear",) + key, cands, "mfma", lambda: dx)]
@@ -139,7 +151,8 @@ class _LinearFn(torch.autograd.Function):
                 elif act == 2:
                     torch.ops.aten.gelu.out(aux, approximate="tanh", out=y)
 
-            _route(("fwd", M, x2.shape[1], N, act, bias is not None), mfma, blas, y)()
+            _route(("fwd", M, x2.shape[1], N, act, bias is not None), mfma, blas, y,
+                   {"mfma_ct": lambda: _ct(weight, x2, y, bias, act, aux)})()
         ctx.act = act
         ctx.mod = mod
         # per-forward token: a residual LayerNorm that hands this forward's input gradient over

@@ -214,7 +214,7 @@ def test_mfma_linear_fp8_forward_backward(gpu):
     assert relx < 0.08 and relw < 0.08, (relx, relw)
 
 
-@pytest.mark.parametrize("route", ["mfma", "blas"])
+@pytest.mark.parametrize("route", ["mfma", "mfma_ct", "blas"])
 @pytest.mark.parametrize("act", [None, "relu", "gelu"])
 def test_mfma_linear_routes_match_fp32(gpu, route, act):
     """Both per-shape routes of MfmaLinear (MFMA kernels / hipBLASLt + separate epilogue) against an
@@ -334,3 +334,52 @@ def test_ffn_gelu_handover_matches_unfused(gpu, monkeypatch):
     for a, b in zip(fused, (xr.grad, w1.grad, b1.grad, w2.grad, b2.grad)):
         rel = ((a.float() - b).norm() / b.norm()).item()
         assert rel < 2e-2, rel
+
+
+# ---------------------------------------------------------------- 192 x 256 tiles stored transposed
+# (gemm_ct_: Y[N, M] = B A^T + bias[M]; the 768-wide BERT GEMMs as 512 tiles instead of 384 256-tiles)
+CT_SHAPES = [(192, 256, 128), (200, 1000, 192), (768, 4096, 768), (2304, 2048, 256), (768, 520, 3072),
+             (392, 33000, 128)]
+
+
+@pytest.mark.parametrize("shape", CT_SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_gemm_ct_exact(gpu, shape):
+    """Small-integer operands: exact in fp32 out, every tile edge (M past 192-multiples, N past 256)."""
+    M, N, K = shape
+    g = torch.Generator().manual_seed(7)
+    a = torch.randint(-3, 4, (M, K), generator=g).float().to(torch.bfloat16)
+    b = torch.randint(-3, 4, (N, K), generator=g).float().to(torch.bfloat16)
+    ref = b.float() @ a.float().t()
+    out = torch.full((N, M), 7.0, dtype=torch.float32, device=gpu)
+    assert native().gemm_ct_(a.to(gpu), b.to(gpu), out)
+    torch.testing.assert_close(out.cpu(), ref, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("act", [0, 1, 2], ids=["none", "relu", "gelu"])
+@pytest.mark.parametrize("shape", [(768, 32768, 768), (2304, 4096, 768), (200, 1000, 192)], ids=str)
+def test_gemm_ct_bias_act_vs_fp32(gpu, act, shape):
+    """Random-normal operands: bias per output column of Y, ReLU / GELU and the GELU pre-activation,
+    bf16 out, against the fp32 reference of the same op (F.linear)."""
+    M, N, K = shape
+    g = torch.Generator().manual_seed(11)
+    w = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    x = torch.randn(N, K, generator=g).to(torch.bfloat16)
+    bias = torch.randn(M, generator=g).to(torch.bfloat16)
+    z = torch.nn.functional.linear(x.float(), w.float(), bias.float())
+    want = {0: z, 1: torch.relu(z), 2: torch.nn.functional.gelu(z, approximate="tanh")}[act]
+    out = torch.empty(N, M, dtype=torch.bfloat16, device=gpu)
+    aux = torch.empty(N, M, dtype=torch.bfloat16, device=gpu) if act == 2 else None
+    assert native().gemm_ct_(w.to(gpu), x.to(gpu), out, bias.to(gpu), act, aux)
+    torch.testing.assert_close(out.float().cpu(), want, rtol=2e-2, atol=2e-2)
+    if aux is not None:
+        torch.testing.assert_close(aux.float().cpu(), z, rtol=2e-2, atol=2e-2)
+
+
+def test_gemm_ct_declines_outside_contract(gpu):
+    C = native()
+    a = torch.zeros(100, 128, dtype=torch.bfloat16, device=gpu)  # M % 8 != 0
+    b = torch.zeros(256, 128, dtype=torch.bfloat16, device=gpu)
+    assert not C.gemm_ct_(a, b, torch.empty(256, 100, dtype=torch.bfloat16, device=gpu))
+    a = torch.zeros(192, 96, dtype=torch.bfloat16, device=gpu)  # K % 64 != 0
+    assert not C.gemm_ct_(a, torch.zeros(256, 96, dtype=torch.bfloat16, device=gpu),
+                          torch.empty(256, 192, dtype=torch.bfloat16, device=gpu))

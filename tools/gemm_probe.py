@@ -7,7 +7,8 @@
   python tools/gemm_probe.py --pmc NTxMxNxK                                 5 launches of one GEMM (rocprofv3 --pmc)
 
 Layouts: NT = X[M,K] . W[N,K]^T (forward), NN = dY[M,K] . W[K,N] (dgrad), TN = dY^T . X (wgrad,
-split-K into the fp32 slab + reduce, as ops/linear.py runs it).
+split-K into the fp32 slab + reduce, as ops/linear.py runs it), CT = the NT product on the 192 x 256
+transposed-store tile (gemm_ct_).
 """
 import argparse
 import os
@@ -22,7 +23,8 @@ SQUARE = [("NT", 4096, 4096, 4096), ("NT", 8192, 8192, 8192), ("NN", 4096, 4096,
 T = 256 * 128  # BERT-base tokens per step at the bench config
 BERT = [("NT", T, 2304, 768), ("NT", T, 3072, 768), ("NT", T, 768, 3072), ("NT", T, 768, 768),
         ("NN", T, 768, 2304), ("NN", T, 768, 3072), ("NN", T, 3072, 768),
-        ("TN", 2304, 768, T), ("TN", 3072, 768, T), ("TN", 768, 3072, T)]
+        ("TN", 2304, 768, T), ("TN", 3072, 768, T), ("TN", 768, 3072, T),
+        ("CT", T, 2304, 768), ("CT", T, 768, 768), ("CT", T, 768, 3072), ("CT", T, 3072, 768)]
 
 
 def rnd(*s):
@@ -39,6 +41,9 @@ def make(layout, M, N, K):
     if layout == "NN":
         a, b = rnd(M, K), rnd(K, N)
         return (lambda: C.gemm_(a, b, True, False, out)), (lambda: torch.mm(a, b, out=out)), out, (a, b)
+    if layout == "CT":  # C[M, N] = X W^T on the 192 x 256 transposed-store tile (A = W [N, K], B = X [M, K])
+        a, b = rnd(M, K), rnd(N, K)
+        return (lambda: C.gemm_ct_(b, a, out)), (lambda: torch.mm(a, b.t(), out=out)), out, (a, b)
     # TN: C[M, N] = A^T B with A [K, M], B [K, N] (wgrad: M = out features, K = tokens)
     a, b = rnd(K, M), rnd(K, N)
     return (lambda: C.gemm_splitk_(a, b, False, False, out, False, 1.0, 0)), \
