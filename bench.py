@@ -383,6 +383,10 @@ def main():
         dist.all_reduce(finite, op=dist.ReduceOp.MIN)
     params_finite = bool(finite.item() > 0)
     at_src = _autotune_source()  # (a collective at N > 1: every rank)
+    if rank == 0 and os.environ.get("PSD_AUTOTUNE_SAVE"):  # pin these choices in later runs (PSD_AUTOTUNE_FILE)
+        from parameter_server_distributed_amd.ops import autotune as _at_mod
+
+        _at_mod.save_decisions(os.environ["PSD_AUTOTUNE_SAVE"])
     if not params_finite and rank == 0:
         print("WARNING: non-finite weights or loss at the end of the timed steps", file=sys.stderr, flush=True)
     if rank == 0:
