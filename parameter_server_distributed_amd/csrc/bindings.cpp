@@ -56,7 +56,6 @@ PYBIND11_MODULE(_C, m) {
         py::arg("running_var"), py::arg("residual"), py::arg("relu"), py::arg("training"), py::arg("momentum"),
         py::arg("eps"), py::arg("counter"), py::arg("ss_eval"), py::arg("mask_out") = false,
         py::arg("residual_ss") = py::none(), py::arg("stats_only") = false, py::arg("q8_out") = py::none(),
-        py::arg("q8_hist") = py::none(), py::arg("q8_sinv") = py::none(), py::arg("q8_margin") = 1.0,
         py::arg("part_in") = py::none(), py::arg("part_rows") = 0, py::arg("q8_mx") = py::none());
   m.def("bn_reduce_", &bn_reduce_, py::arg("x"), py::arg("shift"));
   m.def("bn_bwd_reduce_", &bn_bwd_reduce_, py::arg("dy"), py::arg("x"), py::arg("save_mean"),

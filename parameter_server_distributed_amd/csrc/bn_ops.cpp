@@ -40,8 +40,7 @@ std::vector<at::Tensor> bn_fwd(const at::Tensor& x_in, c10::optional<at::Tensor>
                                c10::optional<at::Tensor> residual, bool relu, bool training, double momentum, double eps,
                                c10::optional<at::Tensor> counter, c10::optional<at::Tensor> ss_eval, bool mask_out,
                                c10::optional<at::Tensor> residual_ss, bool stats_only,
-                               c10::optional<at::Tensor> q8_out, c10::optional<at::Tensor> q8_hist,
-                               c10::optional<at::Tensor> q8_sinv, double q8_margin, c10::optional<at::Tensor> part_in,
+                               c10::optional<at::Tensor> q8_out, c10::optional<at::Tensor> part_in,
                                int64_t part_rows, c10::optional<at::Tensor> q8_mx) {
   TORCH_CHECK(x_in.is_cuda() && x_in.scalar_type() == at::kBFloat16, "psd bn: x must be a bf16 device tensor");
   const c10::DeviceGuard g(x_in.device());
@@ -120,19 +119,11 @@ std::vector<at::Tensor> bn_fwd(const at::Tensor& x_in, c10::optional<at::Tensor>
                     (reinterpret_cast<uintptr_t>(q.data_ptr()) & 7) == 0,
                 "psd bn: q8_out must be an e4m3fn tensor laid out like x (ReLU BNs)");
     a.q8 = reinterpret_cast<uint8_t*>(q.data_ptr());
-    if (q8_mx.has_value() && q8_mx->defined()) {  // MX: E8M0 per 32 channels, no history
-      TORCH_CHECK(q8_mx->scalar_type() == at::kByte && q8_mx->is_contiguous() && q8_mx->numel() * 32 == x.numel() &&
-                      C % 32 == 0 && q8_mx->device() == x.device(),
-                  "psd bn: q8_mx must be uint8 [numel / 32] (channels % 32 == 0)");
-      a.q8mx = q8_mx->data_ptr<uint8_t>();
-    } else {
-      TORCH_CHECK(q8_hist.has_value() && q8_hist->numel() >= 2 && q8_hist->scalar_type() == at::kFloat &&
-                      q8_sinv.has_value() && q8_sinv->numel() >= 1 && q8_sinv->scalar_type() == at::kFloat,
-                  "psd bn: q8_out needs q8_hist fp32[2] and q8_sinv fp32[1] (or MX scales)");
-      a.q8hist = q8_hist->data_ptr<float>();
-      a.q8sinv = q8_sinv->data_ptr<float>();
-      a.q8margin = (float)q8_margin;
-    }
+    // MX: E8M0 per 32 channels
+    TORCH_CHECK(q8_mx.has_value() && q8_mx->defined() && q8_mx->scalar_type() == at::kByte && q8_mx->is_contiguous() &&
+                    q8_mx->numel() * 32 == x.numel() && C % 32 == 0 && q8_mx->device() == x.device(),
+                "psd bn: q8_out needs q8_mx uint8 [numel / 32] (channels % 32 == 0)");
+    a.q8mx = q8_mx->data_ptr<uint8_t>();
   }
   hipError_t e = launch_bn_fwd(a, stream_of(x));
   TORCH_CHECK(e == hipSuccess, "psd bn fwd: ", hipGetErrorString(e));

@@ -219,26 +219,19 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const float* __res
 // RSS: the residual is itself a raw BN input (the downsample branch's convolution output) whose
 // scale/shift rss is applied here, so that BN's own apply pass (a full write + read of the
 // residual) never runs.
-// Q8: also write y as OCP e4m3 for an fp8 consumer convolution (delayed scaling: scale from the
-// consumer's amax history q8hist[0] * margin, this pass's amax max-reduced into q8hist[1]; the
-// roll kernel after the launch moves it to q8hist[0]) -- the consumer's own quantise pass (a full
-// read of y) never runs.
-// Q8 == 2: the e4m3 copy with MX block scales instead (one E8M0 byte per 32 channels into q8mx:
-// 4 lanes hold one block, the block maximum is a DPP quad reduction; no history, no roll).
+// Q8 == 2: also write y as OCP e4m3 with MX block scales for an fp8 consumer convolution (one E8M0
+// byte per 32 channels into q8mx: 4 lanes hold one block, the block maximum is a DPP quad
+// reduction) -- the consumer's own quantise pass (a full read of y) never runs. (The per-tensor
+// delayed-scaling form, Q8 == 1, measured no faster than the consumer quantising and was removed in
+// round 6.)
 template <bool RELU, bool RES, bool MASK_OUT, bool RSS = false, int Q8 = 0>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
                                                        const float* __restrict__ ss, uint16_t* __restrict__ y,
                                                        uint8_t* __restrict__ mbits, int pack4, int64_t nvec, int C,
                                                        const float* __restrict__ rss = nullptr,
-                                                       uint8_t* __restrict__ q8 = nullptr, float* q8hist = nullptr,
-                                                       float q8margin = 1.f, float* __restrict__ q8sinv = nullptr,
+                                                       uint8_t* __restrict__ q8 = nullptr,
                                                        uint8_t* __restrict__ q8mx = nullptr) {
-  float q8scale = 0.f, q8max = 0.f;
-  if (Q8 == 1) {
-    const float a = fmaxf(q8hist[0] * q8margin, 1e-12f);
-    q8scale = 448.f / a;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *q8sinv = a / 448.f;
-  }
+  static_assert(Q8 == 0 || Q8 == 2, "bn apply: fp8 side output is MX only");
   const int tpc = C >> 3;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;  // host guarantees stride % tpc == 0
   int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -270,18 +263,6 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
       const int eb = mx_quant8<false>(r, qb);
       *reinterpret_cast<uint2*>(q8 + v * 8) = qb;
       if ((v & 3) == 0) q8mx[v >> 2] = (uint8_t)eb;
-    }
-    if (Q8 == 1) {  // quantise the stored (bf16-rounded) values
-      uint32_t lo = 0, hi = 0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float r = bf16_to_f32(f32_to_bf16(t[j]));
-        q8max = fmaxf(q8max, fabsf(r));
-        const uint32_t b = (uint32_t)__hip_cvt_float_to_fp8(r * q8scale, __HIP_SATFINITE, __HIP_E4M3);
-        if (j < 4) lo |= b << (8 * j);
-        else hi |= b << (8 * (j - 4));
-      }
-      *reinterpret_cast<uint2*>(q8 + v * 8) = make_uint2(lo, hi);
     }
     if (MASK_OUT) {
       uint32_t bits = 0;
@@ -317,16 +298,6 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
     if (RES) load8_bf16(res + v * 8, rr);
     apply(v, t, rr);
   }
-  if (Q8 == 1) {
-    for (int off = 32; off > 0; off >>= 1) q8max = fmaxf(q8max, __shfl_xor(q8max, off, kWave));
-    if ((threadIdx.x & (kWave - 1)) == 0)
-      atomicMax(reinterpret_cast<unsigned int*>(q8hist + 1), __float_as_uint(q8max));  // one per wave
-  }
-}
-
-__global__ void bn_q8_roll_kernel(float* hist) {
-  hist[0] = hist[1];
-  hist[1] = 0.f;
 }
 
 // ------------------------------------------------------------------ backward
@@ -937,7 +908,7 @@ hipError_t launch_bn_fwd(const BnFwdArgs& a, hipStream_t st) {
     if (!a.relu || a.C % 32 != 0 || nvec % 4 != 0) return hipErrorInvalidValue;
 #define PSD_APM(S, B, RS)                                                                                      \
   hipLaunchKernelGGL((bn_apply_kernel<true, S, B, RS, 2>), dim3(g), dim3(256), 0, st, a.x, a.res, a.ss, a.y,    \
-                     a.mbits, 1, nvec, a.C, a.res_ss, a.q8, nullptr, 1.f, nullptr, a.q8mx)
+                     a.mbits, 1, nvec, a.C, a.res_ss, a.q8, a.q8mx)
     if (a.res_ss && a.res && a.mbits) PSD_APM(true, true, true);
     else if (a.res && a.mbits && !a.res_ss) PSD_APM(true, true, false);
     else if (!a.res && !a.mbits && !a.res_ss) PSD_APM(false, false, false);
@@ -945,20 +916,7 @@ hipError_t launch_bn_fwd(const BnFwdArgs& a, hipStream_t st) {
 #undef PSD_APM
     return hipGetLastError();
   }
-  if (a.q8) {  // fp8 side output for the consumer convolution (ReLU BNs: bn1 / bn2 / residual bn3)
-    if (!a.relu || !a.q8hist || !a.q8sinv) return hipErrorInvalidValue;
-    const int p4 = (int)(nvec % 4 == 0);
-#define PSD_APQ(S, B, RS)                                                                                      \
-  hipLaunchKernelGGL((bn_apply_kernel<true, S, B, RS, 1>), dim3(g), dim3(256), 0, st, a.x, a.res, a.ss, a.y, \
-                     a.mbits, p4, nvec, a.C, a.res_ss, a.q8, a.q8hist, a.q8margin, a.q8sinv)
-    if (a.res_ss && a.res && a.mbits) PSD_APQ(true, true, true);
-    else if (a.res && a.mbits && !a.res_ss) PSD_APQ(true, true, false);
-    else if (!a.res && !a.mbits && !a.res_ss) PSD_APQ(false, false, false);
-    else return hipErrorInvalidValue;
-#undef PSD_APQ
-    hipLaunchKernelGGL(bn_q8_roll_kernel, dim3(1), dim3(1), 0, st, a.q8hist);
-    return hipGetLastError();
-  }
+  if (a.q8) return hipErrorInvalidValue;  // the fp8 side output needs its MX scales
   if (a.res_ss) {  // residual = bn(res) applied on the fly (ReLU blocks only)
     if (!a.res || !a.relu) return hipErrorInvalidValue;
     if (a.mbits)

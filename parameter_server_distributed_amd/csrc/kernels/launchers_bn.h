@@ -24,9 +24,6 @@ struct BnFwdArgs {
   const float* res_ss;    // optional [2C]: res is a raw BN input, added as res*res_ss[c] + res_ss[C+c]
   int32_t stats_only;     // training: statistics / running stats / scale-shift only, no apply pass
   uint8_t* q8;            // optional [M, C] e4m3 copy of y for an fp8 consumer (delayed scaling)
-  float* q8hist;          // [2] the consumer's amax history (scale from [0]; this pass's amax -> [0])
-  float q8margin;
-  float* q8sinv;          // [1] out: the dequant factor of q8
   uint8_t* q8mx;          // MX instead of per-tensor: [M * C / 32] E8M0 block scales of q8 (no history)
   uint8_t* pool_arg;      // stem fusion: y = maxpool3x3s2(relu(bn(x))) [N, H/2, W/2, C] + argmax (optional)
   int32_t N, H, W;        // x as [N, H, W, C] (pool fusion only)

@@ -29,8 +29,7 @@ std::vector<at::Tensor> bn_fwd(const at::Tensor& x, c10::optional<at::Tensor> ga
                                c10::optional<at::Tensor> residual, bool relu, bool training, double momentum, double eps,
                                c10::optional<at::Tensor> counter, c10::optional<at::Tensor> ss_eval,
                                bool mask_out, c10::optional<at::Tensor> residual_ss, bool stats_only,
-                               c10::optional<at::Tensor> q8_out, c10::optional<at::Tensor> q8_hist,
-                               c10::optional<at::Tensor> q8_sinv, double q8_margin, c10::optional<at::Tensor> part_in,
+                               c10::optional<at::Tensor> q8_out, c10::optional<at::Tensor> part_in,
                                int64_t part_rows, c10::optional<at::Tensor> q8_mx);
 // statistics pass of the BN forward alone: shifted sums of x [M, C] into a fresh [rows, 2, C] fp32
 at::Tensor bn_reduce_(const at::Tensor& x, const at::Tensor& shift);

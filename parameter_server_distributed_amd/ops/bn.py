@@ -29,31 +29,19 @@ def _kernel_ok(x: torch.Tensor) -> bool:
 
 
 def _q8_args(mod, x: torch.Tensor) -> dict:
-    """If ``mod``'s output feeds an fp8 convolution (``_psd_q8_consumer``, wired by the model) whose
-    activation scaler already has an amax history, the apply pass also writes the e4m3 copy the
-    consumer would otherwise quantise in a pass of its own (ops/conv.py DelayedScale)."""
+    """If ``mod``'s output feeds an MX fp8 convolution (``_psd_q8_consumer``, wired by the model), the
+    apply pass also writes the e4m3 copy + one E8M0 scale per 32 channels (a lane quad's block
+    maximum, kernels/bn.hip Q8 == 2) -- the consumer's own quantise pass (a full read of y) never
+    runs. Per-tensor operands (feature fp8_mx off) are quantised by the consumer with its delayed
+    scale: a per-tensor hand-over from this pass measured no faster (WRN-101-2 b512 3,589 vs 3,606
+    img/s) and was removed in round 6. feature fp8_mx_handover off: the consumer quantises."""
     cons = getattr(mod, "_psd_q8_consumer", None)
     if cons is None or not mod.relu or x.dim() != 4 or not cons.psd_fp8_consumes(x.shape[1]):
         return {}
-    if _feat("fp8_mx"):
-        # MX operands: the apply pass writes e4m3 + one E8M0 scale per 32 channels (a lane quad's
-        # block maximum, kernels/bn.hip Q8 == 2) -- the consumer's own quantise pass (a full read of
-        # y) never runs. feature fp8_mx_handover off: the consumer quantises.
-        if x.shape[1] % 32 or not _feat("fp8_mx_handover"):
-            return {}
-        q = torch.empty_like(x, dtype=torch.float8_e4m3fn, memory_format=torch.channels_last)
-        return {"q8_out": q, "q8_mx": torch.empty(x.numel() // 32, dtype=torch.uint8, device=x.device)}
-    # measured on Wide-ResNet-101-2 b512: 3,589 / 3,584 img/s with the hand-over vs 3,606 without
-    # (same box, one call): the extra fp8 convert in the apply pass costs what the saved read of y
-    # gains, so it is opt-in (feature fp8_handover)
-    if not _feat("fp8_handover") or _feat("fp8_mx"):
-        return {}  # (the hand-over writes per-tensor e4m3; MX operands are quantised by the consumer)
-    sc = cons._f8[0]
-    if sc.hist is None or sc.hist.device != x.device:
+    if not _feat("fp8_mx") or x.shape[1] % 32 or not _feat("fp8_mx_handover"):
         return {}
     q = torch.empty_like(x, dtype=torch.float8_e4m3fn, memory_format=torch.channels_last)
-    return {"q8_out": q, "q8_hist": sc.hist, "q8_sinv": torch.empty(1, dtype=torch.float32, device=x.device),
-            "q8_margin": sc.margin}
+    return {"q8_out": q, "q8_mx": torch.empty(x.numel() // 32, dtype=torch.uint8, device=x.device)}
 
 
 def _stats_args(mod, x: torch.Tensor) -> dict:
@@ -88,8 +76,8 @@ def _dq8_hand_over(mod, dx: torch.Tensor, kw: dict) -> None:
 
 
 def _q8_hand_over(mod, y: torch.Tensor, kw: dict) -> None:
-    if kw:  # (y, e4m3 copy, its scale: fp32 [1] per-tensor or uint8 [numel / 32] MX)
-        mod._psd_q8_consumer._psd_q8_pending = (y, kw["q8_out"], kw["q8_mx"] if "q8_mx" in kw else kw["q8_sinv"])
+    if kw:  # (y, e4m3 copy, its MX scales uint8 [numel / 32])
+        mod._psd_q8_consumer._psd_q8_pending = (y, kw["q8_out"], kw["q8_mx"])
 
 
 class StridedDr:
@@ -191,10 +179,10 @@ class _FusedBNFn(torch.autograd.Function):
         mod._psd_bwd_pre = None
         if pre is not None and not (pre[0].data_ptr() == dy.data_ptr() and pre[0].shape == dy.shape):
             pre = None
-        # a residual BN (bn3) folds with its stored mask or pre-reduced partials; a plain ReLU BN (bn1,
-        # its mask recomputed from x) only with partials the consumer's bwd-data epilogue reduced
-        foldable = ctx.relu and w is not None and (
-            (ctx.has_res and mbits is not None) or (not ctx.has_res and pre is not None and _feat("bn1_fold")))
+        # a residual BN (bn3) folds into its producing 1x1 convolution (its stored mask or the partials
+        # the consumer's bwd-data epilogue pre-reduced). (bn1 folded into conv1 measured slower -- 70.9
+        # vs 68.0 ms/step, profiles/r5/ab_bn1_fold.md -- and was removed in round 6.)
+        foldable = ctx.relu and w is not None and ctx.has_res and mbits is not None
         conv = _fold_target(mod, x) if foldable else None
         if conv is not None:
             # BN-backward fold: reduction + finalize only; the producing 1x1 convolution's dgrad / wgrad

@@ -148,9 +148,8 @@ def _take_dq8(mod, dy: torch.Tensor):
 
 
 def _take_q8(mod, x: torch.Tensor):
-    """The e4m3 copy of ``x`` that the producing BN's apply pass wrote for this module (ops/bn.py,
-    delayed scaling with this module's activation scaler), as (q [N, C, H, W] channels_last,
-    scale_inv), or None. Consumed once."""
+    """The MX e4m3 copy of ``x`` that the producing BN's apply pass wrote for this module (ops/bn.py),
+    as (q [N, C, H, W] channels_last, E8M0 scales uint8 [numel / 32]), or None. Consumed once."""
     pend = getattr(mod, "_psd_q8_pending", None) if mod is not None else None
     if pend is None:
         return None

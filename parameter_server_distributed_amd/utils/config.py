@@ -77,9 +77,6 @@ FEATURES: dict[str, tuple[bool, str]] = {
     # batch norm / bottleneck tail (ops/bn.py, ops/tail.py)
     "bn_fold": (True, "bn3's backward folded into conv3's bwd-data / weight-gradient GEMMs"),
     "bn_fold_ds": (True, "the stride-1 downsample BN folded into its convolution's backward"),
-    "bn1_fold": (False, "bn1's backward folded into conv1's bwd-data / weight-gradient GEMMs (with the "
-                         "reduction pre-run in conv2's bwd-data epilogue); off: same-box ResNet-50 A/B "
-                         "70.9 vs 68.0 ms/step (profiles/r5/ab_bn1_fold.md)"),
     "dual_nobx": (True, "downsample blocks' dual tail without the BN inputs in the consumer epilogue"),
     "tail_recompute": (True, "identity blocks' conv3 output recomputed instead of stored"),
     "tail_gram": (True, "the recomputing tail's statistics from the Gram matrix of conv3's input"),
@@ -88,7 +85,6 @@ FEATURES: dict[str, tuple[bool, str]] = {
     "fp8_compute": (True, "fp8 convolutions where the model asks for them"),
     "fp8_mx": (True, "MX block scales for every fp8 operand; off: per-tensor scales"),
     "fp8_mx_handover": (True, "BN passes write the consumer's MX e4m3 input / producer's MX e5m2 dY"),
-    "fp8_handover": (False, "per-tensor (non-MX) fp8 hand-over from the BN passes"),
     "fp8_delayed": (True, "per-tensor fp8: delayed (previous-call amax) scaling"),
     "fp8_dgrad": (True, "fp8 e5m2-dY bwd-data of the fp8 convolutions"),
     # BERT (ops/linear.py, ops/attention.py)

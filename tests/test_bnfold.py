@@ -133,10 +133,9 @@ def _block_grads(gpu, monkeypatch, kind: str, mode: str):
     from parameter_server_distributed_amd.ops.bn import FusedBatchNorm2d
 
     # (the stored-output tails: the recomputing ones never take the unfolded path, ops/tail.py)
-    # mode 'fold1': conv2's bwd-data pre-reduces bn1 (psdnb), whose backward then folds into conv1
-    fold = mode in ("fold", "fold1")
-    monkeypatch.setenv("PSD_FEATURES", f"bn_fold={int(fold)},bn1_fold={int(mode == 'fold1')},tail_recompute=0")
-    monkeypatch.setenv("PSD_AUTOTUNE_FORCE", {"fold": "psdnf0,psdn0", "fold1": "psdnb0,psdnf0,psdn0"}.get(mode, "psdn0"))
+    fold = mode == "fold"
+    monkeypatch.setenv("PSD_FEATURES", f"bn_fold={int(fold)},tail_recompute=0")
+    monkeypatch.setenv("PSD_AUTOTUNE_FORCE", "psdnf0,psdn0" if fold else "psdn0")
     autotune._DECISIONS.clear()
     torch.manual_seed(2)
     if kind == "identity":
@@ -185,24 +184,6 @@ def test_block_fold_vs_fp32(gpu, monkeypatch, kind):
     for n in ef:
         assert ef[n] < 0.15, (n, ef[n], eu[n])
         assert ef[n] <= 1.1 * eu[n] + 2e-3, (n, ef[n], eu[n])
-
-
-@pytest.mark.parametrize("kind", ["identity", "down"])
-def test_bn1_fold_vs_fp32(gpu, monkeypatch, kind):
-    """bn1's backward folded into conv1 (its reduction pre-run in conv2's bwd-data epilogue, its
-    input gradient never formed: conv1's dgrad on [g | y1], its wgrad on the fold products) vs the
-    unfolded path, both against fp32: every gradient at the unfolded path's bf16 error level."""
-    gf, picks = _block_grads(gpu, monkeypatch, kind, "fold1")
-    cin = 256 if kind == "identity" else 64
-    assert any(k[:2] == ("conv1x1", "dgrad_fold") and k[3:5] == (cin, 64) and v != "unfold"
-               for k, v in picks.items()), picks
-    gu, _ = _block_grads(gpu, monkeypatch, kind, "unfold")
-    gr, _ = _block_grads(gpu, monkeypatch, kind, "fp32")
-    ef, eu = _rel(gf, gr), _rel(gu, gr)
-    print(kind, {n: (round(ef[n], 4), round(eu[n], 4)) for n in ef})
-    for n in ef:
-        assert ef[n] < 0.15, (n, ef[n], eu[n])
-        assert ef[n] <= 1.15 * eu[n] + 3e-3, (n, ef[n], eu[n])
 
 
 @pytest.mark.parametrize("force", ["psdnf0,psdn0", "psdnb0,psdnf0,psdn0"])

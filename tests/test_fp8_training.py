@@ -78,36 +78,6 @@ def test_fp8_wide_resnet_tracks_bf16(gpu, monkeypatch, mx):
 
 
 
-def test_bn_apply_writes_the_consumers_fp8_input(gpu, monkeypatch):
-    """A ReLU BN feeding an fp8 convolution writes the e4m3 copy of its output in the apply pass
-    with the consumer's delayed scale: bit-equal to the consumer quantising the output itself with
-    the same amax history, and the history then holds the output's amax."""
-    from parameter_server_distributed_amd.ops.bn import FusedBatchNorm2d
-    from parameter_server_distributed_amd.ops.conv import Conv1x1, DelayedScale
-
-    monkeypatch.setenv("PSD_FEATURES", "fp8_handover=1,fp8_mx=0")  # (the per-tensor delayed-scaling hand-over)
-    torch.manual_seed(2)
-    bn = FusedBatchNorm2d(256, relu=True).to(gpu)
-    bn.weight.data = bn.weight.data.to(torch.bfloat16)
-    bn.bias.data = bn.bias.data.to(torch.bfloat16)
-    conv = Conv1x1(256, 512, fp8=True).to(gpu, torch.bfloat16)
-    object.__setattr__(bn, "_psd_q8_consumer", conv)
-    conv._f8[0].hist = torch.tensor([3.0, 0.0], device=gpu)
-    x = torch.randn(4, 256, 14, 14, device=gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    y = bn(x.requires_grad_(True))
-    yb, q, sinv = conv._psd_q8_pending
-    assert yb.data_ptr() == y.data_ptr()
-    ref = DelayedScale(1.0)
-    ref.hist = torch.tensor([3.0, 0.0], device=gpu)
-    qr, sr = ref.quantize(y.detach().permute(0, 2, 3, 1), False)
-    torch.cuda.synchronize()
-    assert torch.equal(q.permute(0, 2, 3, 1).contiguous().view(torch.uint8), qr.view(torch.uint8))
-    assert torch.equal(sinv, sr)
-    amax = float(y.detach().float().abs().max())
-    assert float(conv._f8[0].hist[0]) == amax and float(conv._f8[0].hist[1]) == 0.0
-    out = conv(y)  # consumes the hand-over
-    assert conv._psd_q8_pending is None and out.shape == (4, 512, 14, 14)
-
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("e5m2", [False, True])
