@@ -6,6 +6,7 @@
 #include "checkpoint.h"
 #include "comm.h"
 #include "kernels/launchers.h"
+#include "kernels/launchers_gemm.h"
 #include "ops.h"
 #include "ps_core.h"
 #include "registry.h"
@@ -75,6 +76,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("aux") = py::none(), py::arg("part") = py::none(),
         py::arg("shift") = py::none());
   m.def("gemm_stats_rows", &gemm_stats_rows_, py::arg("M"));
+  m.def("gemm_set_bcontig", &gemm_set_bcontig, py::arg("on"));
   m.def("gemm_ct_", &gemm_ct_, py::arg("A"), py::arg("B"), py::arg("out"), py::arg("bias") = py::none(),
         py::arg("act") = 0, py::arg("aux") = py::none());
   m.def("gemm_gelu_bwd_", &gemm_gelu_bwd_, py::arg("A"), py::arg("B"), py::arg("a_kmajor"), py::arg("b_kmajor"),

@@ -330,7 +330,11 @@ __device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint32_t bytes) {
 // padded image is never read): the pieces / lanes past them get kMasked, an offset past every
 // descriptor's range (operands < 2 GiB there), so their DMA writes zeros and moves no bytes
 constexpr uint32_t kMasked = 0x80000000u;
-template <bool KMAJ, int SEG, int ESZ, int PW, int VR = 128>
+// CONTIG (N-major B of the split-K GEMMs): half h holds tile columns [128 h, 128 h + 128) instead of
+// quadrant column h of every wave column (four 32-column = 64-byte pieces per k-row), so each
+// 256-byte LDS row is two whole 128-byte lines of the operand; the wave -> column map of the
+// epilogue follows (ncol below)
+template <bool KMAJ, int SEG, int ESZ, int PW, int VR = 128, bool CONTIG = false>
 __device__ __forceinline__ void stage8_offsets(int ld, int wid, int lane, uint32_t (*vo)[PW]) {
 #pragma unroll
   for (int h = 0; h < 2; ++h)
@@ -345,7 +349,8 @@ __device__ __forceinline__ void stage8_offsets(int ld, int wid, int lane, uint32
         const int k = piece * 4 + (lane >> 4);
         const int f = (k & 3) | ((k >> 1) & 4);
         const int col = ((lane & 15) * 8) ^ (f << 4);
-        vo[h][i] = col < VR ? ((uint32_t)k * (uint32_t)ld + half_to_tile<SEG>(col, h)) * ESZ : kMasked;
+        const int tc = CONTIG ? h * 128 + col : half_to_tile<SEG>(col, h);
+        vo[h][i] = col < VR ? ((uint32_t)k * (uint32_t)ld + tc) * ESZ : kMasked;
       }
     }
 }
@@ -534,8 +539,9 @@ __device__ __forceinline__ float act_apply(float x) {
 // In the MFMA register layout a lane holds 4 consecutive C rows of one column = 4 contiguous Y
 // elements, so the store needs no transpose (8-byte bf16 / 16-byte fp32 per lane and block).
 template <int BM, bool AK, bool BKM, int MODE, bool F8 = false, int ACT = 0, bool GA = false, int F8A = 0,
-          bool GB = false, bool MX = false, bool ST = false, bool CT = false>
+          bool GB = false, bool MX = false, bool ST = false, bool CT = false, bool BC = false>
 __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
+  static_assert(!BC || (MODE == 1 && !BKM), "contiguous B halves: split-K (fp32 epilogue) with an N-major B");
   static_assert(!CT || (MODE == 0 && !ST && !GA && !GB && !F8 && ACT <= 2 && AK && BKM),
                 "transposed store: plain bf16 single-split GEMM of K-major operands");
   static_assert(BM != 192 || (!MX && !GA && !F8 && !ST && MODE == 0), "192-row tiles: plain bf16 GEMM");
@@ -593,7 +599,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
   const uint32_t bytesB = BKM ? ((uint32_t)(g.N - 1) * g.ldb + g.K) * ESZ : ((uint32_t)(g.K - 1) * g.ldb + g.N) * ESZ;
   uint32_t voA[2][P::PWA], voB[2][2];  // [half][piece]
   stage8_offsets<AK, P::QA, ESZ, P::PWA, P::VA>(g.lda, wid, lane, voA);
-  stage8_offsets<BKM, 32, ESZ, 2>(g.ldb, wid, lane, voB);
+  stage8_offsets<BKM, 32, ESZ, 2, 128, BC>(g.ldb, wid, lane, voB);
   // GA: per (tile, half, piece) the window origin of the lane's output pixel: p0 = its top-left input
   // pixel index, hw = (h0 << 16) | (w0 & 0xffff) (h0 = -32768 for rows past M)
   int cp0[2][P::PWA], chw[2][P::PWA], np0[2][P::PWA], nhw[2][P::PWA];
@@ -680,7 +686,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
         const int kk = (i * 8 + wid) * 4 + (lane >> 4);  // this lane's k-row (pixel) of the K-tile
         const int f = (kk & 3) | ((kk >> 1) & 4);
         const int col = ((lane & 15) * 8) ^ (f << 4);
-        const int n = n0 + half_to_tile<32>(col, h);      // (r, s, ci) column of dW
+        const int n = n0 + (BC ? h * 128 + col : half_to_tile<32>(col, h));  // (r, s, ci) column of dW
         const int rs = n >> g.cv_logC, ci = n & ((1 << g.cv_logC) - 1);
         const int r = rs / g.cv_S, sx = rs - r * g.cv_S;
         const int pix = k + kk;                           // output pixel
@@ -787,7 +793,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
   const int cl = lane & 15, rq = (lane >> 4) * 4;
   const int L = cl & 3;
   auto mrow = [&](int qm, int i) { return wr * (BM / 2) + qm * P::QA + i * 16 + rq + L; };
-  auto ncol = [&](int qn, int j) { return wc * 64 + qn * 32 + j * 16 + (cl & ~3); };
+  auto ncol = [&](int qn, int j) { return (BC ? qn * 128 + wc * 32 : wc * 64 + qn * 32) + j * 16 + (cl & ~3); };
 
   // VMEM stores of one tile's epilogue, per lane, in both output paths (exact: every store is
   // issued unconditionally, out-of-range rows/cols go to an offset outside the buffer descriptor)
@@ -1321,9 +1327,16 @@ static int cu_count() {
 // workgroups of the persistent 8-phase grid: one per CU (the kernel's LDS allows no second)
 static int persistent_grid() { return cu_count(); }
 
+// contiguous B halves for the split-K GEMMs with an N-major B (weight gradients); g_bc: off for A/Bs
+static bool g_bc = true;
+void gemm_set_bcontig(bool on) { g_bc = on; }
+
 template <int BM, bool AK, bool BKM, int MODE, bool F8, int ACT, bool GA = false, int F8A = 0, bool GB = false,
-          bool MX = false, bool ST = false, bool CT = false>
+          bool MX = false, bool ST = false, bool CT = false, bool BC = false>
 static hipError_t launch_8p_act(const GemmArgs& g, int splits, hipStream_t st) {
+  if constexpr (MODE == 1 && !BKM && !BC) {
+    if (g_bc) return launch_8p_act<BM, AK, BKM, MODE, F8, ACT, GA, F8A, GB, MX, ST, CT, true>(g, splits, st);
+  }
   if constexpr (ACT == 3) {  // GELU backward + bias-gradient partials (g.aux = pre, g.part = [rows][N])
     if (!g.part || !g.aux || g.c_f32 || g.bias || splits != 1) return hipErrorNotSupported;
     if (g.rows_out) *g.rows_out = (g.M + BM - 1) / BM * 2;
@@ -1341,7 +1354,7 @@ static hipError_t launch_8p_act(const GemmArgs& g, int splits, hipStream_t st) {
   constexpr int lds = P8<BM, MX>::LDS;
   static bool attr_set = false;  // per instantiation: set the >64 KiB LDS limit once
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT, GA, F8A, GB, MX, ST, CT>,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT, GA, F8A, GB, MX, ST, CT, BC>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     attr_set = true;
@@ -1352,7 +1365,7 @@ static hipError_t launch_8p_act(const GemmArgs& g, int splits, hipStream_t st) {
   constexpr int KT = F8 ? 128 : BK;
   int grid = nwg;
   if (MODE == 0 && splits == 1 && g.K / KT >= 2) grid = std::min(nwg, persistent_grid());
-  hipLaunchKernelGGL((gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT, GA, F8A, GB, MX, ST, CT>), dim3(grid, 1, splits),
+  hipLaunchKernelGGL((gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT, GA, F8A, GB, MX, ST, CT, BC>), dim3(grid, 1, splits),
                      dim3(512), lds, st, g);
   return hipGetLastError();
 }

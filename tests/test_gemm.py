@@ -383,3 +383,26 @@ def test_gemm_ct_declines_outside_contract(gpu):
     a = torch.zeros(192, 96, dtype=torch.bfloat16, device=gpu)  # K % 64 != 0
     assert not C.gemm_ct_(a, torch.zeros(256, 96, dtype=torch.bfloat16, device=gpu),
                           torch.empty(256, 192, dtype=torch.bfloat16, device=gpu))
+
+
+@pytest.mark.parametrize("shape", [(2304, 768, 8192), (768, 3072, 4096), (520, 1000, 2056)], ids=str)
+def test_gemm_splitk_bcontig_bitwise(gpu, shape):
+    """The split-K GEMM with an N-major B staged as contiguous 128-column halves (default) against the
+    quadrant-interleaved halves: the same K order per output, so bitwise equal; and exact against
+    fp32 on small integers."""
+    M, N, K = shape
+    C = native()
+    g = torch.Generator().manual_seed(13)
+    a = torch.randint(-3, 4, (K, M), generator=g).float().to(torch.bfloat16).to(gpu)
+    b = torch.randint(-3, 4, (K, N), generator=g).float().to(torch.bfloat16).to(gpu)
+    outs = []
+    for bc in (True, False):
+        out = torch.empty(M, N, dtype=torch.float32, device=gpu)
+        C.gemm_set_bcontig(bc)
+        try:
+            C.gemm_splitk_(a, b, False, False, out, False, 1.0, 0)
+        finally:
+            C.gemm_set_bcontig(True)
+        outs.append(out.cpu())
+    assert torch.equal(outs[0], outs[1])
+    torch.testing.assert_close(outs[0], a.float().cpu().t() @ b.float().cpu(), rtol=0, atol=0)

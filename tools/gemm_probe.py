@@ -23,7 +23,8 @@ SQUARE = [("NT", 4096, 4096, 4096), ("NT", 8192, 8192, 8192), ("NN", 4096, 4096,
 T = 256 * 128  # BERT-base tokens per step at the bench config
 BERT = [("NT", T, 2304, 768), ("NT", T, 3072, 768), ("NT", T, 768, 3072), ("NT", T, 768, 768),
         ("NN", T, 768, 2304), ("NN", T, 768, 3072), ("NN", T, 3072, 768),
-        ("TN", 2304, 768, T), ("TN", 3072, 768, T), ("TN", 768, 3072, T),
+        ("TN", 2304, 768, T), ("TN", 3072, 768, T), ("TN", 768, 3072, T), ("TN", 768, 768, T),
+        ("TN0", 2304, 768, T), ("TN0", 3072, 768, T), ("TN0", 768, 3072, T), ("TN0", 768, 768, T),
         ("CT", T, 2304, 768), ("CT", T, 768, 768), ("CT", T, 768, 3072), ("CT", T, 3072, 768)]
 
 
@@ -44,10 +45,17 @@ def make(layout, M, N, K):
     if layout == "CT":  # C[M, N] = X W^T on the 192 x 256 transposed-store tile (A = W [N, K], B = X [M, K])
         a, b = rnd(M, K), rnd(N, K)
         return (lambda: C.gemm_ct_(b, a, out)), (lambda: torch.mm(a, b.t(), out=out)), out, (a, b)
-    # TN: C[M, N] = A^T B with A [K, M], B [K, N] (wgrad: M = out features, K = tokens)
+    # TN: C[M, N] = A^T B with A [K, M], B [K, N] (wgrad: M = out features, K = tokens); TN0: the same
+    # with the quadrant-interleaved B halves (gemm_set_bcontig(False), the pre-round-6 staging)
     a, b = rnd(K, M), rnd(K, N)
-    return (lambda: C.gemm_splitk_(a, b, False, False, out, False, 1.0, 0)), \
-        (lambda: torch.mm(a.t(), b, out=out)), out, (a, b)
+    bc = layout != "TN0"
+
+    def ours():
+        C.gemm_set_bcontig(bc)
+        C.gemm_splitk_(a, b, False, False, out, False, 1.0, 0)
+        C.gemm_set_bcontig(True)
+
+    return ours, (lambda: torch.mm(a.t(), b, out=out)), out, (a, b)
 
 
 def t_us(fn, it):
