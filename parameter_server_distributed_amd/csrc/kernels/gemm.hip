@@ -1427,8 +1427,9 @@ static bool big_ok(const GemmArgs& g, int kseg) {
 
 template <bool AK, bool BKM, int MODE>
 static hipError_t launch_layout(const GemmArgs& g, int splits, hipStream_t st) {
-  if (big_ok(g, MODE == 1 ? g.k_per_split : g.K) && (MODE == 1 || g.K % 64 == 0))
-    return launch_big<AK, BKM, MODE>(g, splits, st);
+  // (the 8-phase K loop runs whole 64-k tiles: a K tail -- the last split's, in MODE 1 -- would be
+  // dropped, and a K-major operand reads the next row past K, so K % 64 != 0 takes the 128-tile kernel)
+  if (big_ok(g, MODE == 1 ? g.k_per_split : g.K) && g.K % 64 == 0) return launch_big<AK, BKM, MODE>(g, splits, st);
   if (g.part) return hipErrorNotSupported;  // statistics: the 8-phase epilogue only
   // tile choice: 128x128 by default, 128x64 / 64x128 for narrow operands (more tiles)
   if (g.N <= 64 && g.M > 64) return launch_t<2, 1, AK, BKM, MODE>(g, splits, st);

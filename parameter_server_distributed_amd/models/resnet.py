@@ -21,6 +21,7 @@ from ..ops.bn import FusedBatchNorm2d, bn_add_bn_relu
 from ..ops.conv import Conv1x1, ConvNHWC, stem_forward
 from ..ops.pool import MaxPool3x3s2, global_avg_pool
 from ..ops.tail import conv_bn_dual_tail, conv_bn_tail, dual_tail_ok, tail_ok
+from ..utils.config import feature as _feat
 
 
 class _Fork(torch.autograd.Function):
@@ -85,7 +86,11 @@ class Bottleneck(nn.Module):
         if isinstance(self.conv1, Conv1x1) and not fp8:
             # bn1's into conv1 (when conv2's bwd-data epilogue pre-reduced it: ops/bn.py)
             object.__setattr__(self.bn1, "_psd_fold_conv", self.conv1)
-        if isinstance(self.conv3, Conv1x1) and not fp8:
+        # fp8 identity blocks (feature tail_fp8): conv3 + bn3 run as the bf16 recomputing tail
+        # (ops/tail.py) -- bn3's input gradient folded into conv3's bf16 backward, conv3's output never
+        # stored -- so bn2 writes no e4m3 copy for conv3 and bn3 none of its input gradient
+        self._tail8 = bool(fp8 and downsample is None and isinstance(self.conv3, Conv1x1) and _feat("tail_fp8"))
+        if isinstance(self.conv3, Conv1x1) and (not fp8 or self._tail8):
             object.__setattr__(self.bn3, "_psd_fold_conv", self.conv3)
             # and a stride-1 downsample BN's into the downsample conv (layer 1's first block)
             if downsample is not None and len(downsample) == 2 and isinstance(downsample[0], Conv1x1):
@@ -93,9 +98,12 @@ class Bottleneck(nn.Module):
         if fp8:  # bn1 / bn2 quantise their outputs for the fp8 conv2 / conv3 in their apply pass
             # (plain attributes: object.__setattr__ keeps the consumer from becoming a submodule)
             object.__setattr__(self.bn1, "_psd_q8_consumer", self.conv2)
-            object.__setattr__(self.bn2, "_psd_q8_consumer", self.conv3)
+            if not self._tail8:
+                object.__setattr__(self.bn2, "_psd_q8_consumer", self.conv3)
             # and each BN's backward quantises its input gradient for the producing conv's fp8 bwd-data
             for conv, bn in ((self.conv1, self.bn1), (self.conv2, self.bn2), (self.conv3, self.bn3)):
+                if conv is self.conv3 and self._tail8:
+                    continue
                 if hasattr(conv, "psd_fp8_dgrad"):
                     object.__setattr__(bn, "_psd_dq8_producer", conv)
 

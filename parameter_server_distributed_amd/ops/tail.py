@@ -50,16 +50,21 @@ TAIL_CALLS = {"fwd": 0, "bwd_fused": 0, "bwd_recompute": 0, "dual_fwd": 0, "dual
 
 
 def tail_ok(conv, bn, a2: torch.Tensor, idt: torch.Tensor) -> bool:
-    """The recomputing tail applies: a bf16 Conv1x1 (no fp8) into a training ReLU FusedBatchNorm2d
-    with an identity residual, channels_last operands, a shape the narrow kernel and the fold take."""
-    if not (_feat("tail_recompute") and _feat("convn")) or not isinstance(conv, Conv1x1) \
-            or conv.fp8:
+    """The recomputing tail applies: a Conv1x1 into a training ReLU FusedBatchNorm2d with an identity
+    residual, channels_last operands, a shape the narrow kernel and the fold take. An fp8 Conv1x1
+    takes it only where the model wired its bn3 fold for it (feature ``tail_fp8``, models/resnet.py:
+    the block's conv3 then runs in bf16 inside the tail, its BN passes gone); the tail's output then
+    carries no e4m3 copy, so a next fp8 conv1 quantises it itself."""
+    if not (_feat("tail_recompute") and _feat("convn")) or not isinstance(conv, Conv1x1):
+        return False
+    tail8 = conv.fp8 and _feat("tail_fp8") and getattr(bn, "_psd_fold_conv", None) is conv
+    if conv.fp8 and not tail8:
         return False
     if not isinstance(bn, FusedBatchNorm2d) or not bn.relu or not bn.training or bn.weight is None:
         return False
     if not (a2.is_cuda and a2.dtype == torch.bfloat16 and idt.dtype == torch.bfloat16 and torch.is_grad_enabled()):
         return False
-    if conv.weight.dtype != torch.bfloat16 or getattr(bn, "_psd_q8_consumer", None) is not None:
+    if conv.weight.dtype != torch.bfloat16 or (getattr(bn, "_psd_q8_consumer", None) is not None and not tail8):
         return False
     cin, cout = conv.in_channels, conv.out_channels
     if idt.shape != (a2.shape[0], cout, a2.shape[2], a2.shape[3]):
