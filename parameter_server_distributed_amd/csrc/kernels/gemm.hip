@@ -1328,7 +1328,7 @@ static int cu_count() {
 static int persistent_grid() { return cu_count(); }
 
 // contiguous B halves for the split-K GEMMs with an N-major B (weight gradients); g_bc: off for A/Bs
-static bool g_bc = true;
+static bool g_bc = false;  // measured no faster on the BERT weight gradients (profiles/r6/gemm_probe_bert_r6b.md: TN vs TN0)
 void gemm_set_bcontig(bool on) { g_bc = on; }
 
 template <int BM, bool AK, bool BKM, int MODE, bool F8, int ACT, bool GA = false, int F8A = 0, bool GB = false,

@@ -42,8 +42,8 @@ hipError_t launch_gemm_ct(const GemmArgs& g, hipStream_t stream);
 // C = (A_e4m3 . B_e4m3^T) * a_scale * b_scale (+bias)(act); A [M][K], B [N][K] fp8, K % 128 == 0
 hipError_t launch_gemm_fp8(const GemmArgs& g, hipStream_t stream);
 int gemm_splits(int M, int N, int K);
-// split-K GEMMs with an N-major B stage each B half as contiguous 128-column rows (default on; off: the
-// quadrant-interleaved halves, for A/Bs)
+// split-K GEMMs with an N-major B: stage each B half as contiguous 128-column rows (whole 128-byte lines)
+// instead of the quadrant-interleaved halves. Default off: no faster on the BERT weight gradients.
 void gemm_set_bcontig(bool on);
 // out[M][Cout] = conv(x, w) (NHWC, no bias / activation), on the persistent 8-phase kernel with A
 // gathered from the input; hipErrorNotSupported when the shape is outside that kernel's contract

@@ -192,3 +192,60 @@ def test_fp8_wide_resnet_300_step_convergence(gpu, monkeypatch):
     assert abs(avg(l8, 0, 300) - avg(lb, 0, 300)) <= 0.10 * avg(lb, 0, 300)
     assert abs(half(l8) - half(lb)) <= max(3, 0.10 * half(lb))
     assert abs(avg(l8, 275, 300) - avg(lb, 275, 300)) <= 0.05 * avg(lb, 0, 8)
+
+
+def test_fp8_tail_on_vs_off_against_fp32(gpu, monkeypatch):
+    """the fp8 Wide-ResNet's identity blocks on the recomputing tail (feature
+    tail_fp8: conv3 + bn3 in bf16 inside the tail, bn3 folded into conv3's backward, conv3's output
+    never stored) vs the same model with the fp8 conv3 + separate BN passes, both against an fp32 run
+    of the same weights: the tail really ran, and its loss and first-step gradient are at least as
+    close to fp32 as the fp8-conv3 path's (the tail trades conv3's e4m3 rounding for bf16)."""
+    import copy
+
+    from parameter_server_distributed_amd.models import prepare
+    from parameter_server_distributed_amd.models.resnet import ResNet
+    from parameter_server_distributed_amd.ops import tail
+
+    def build(on):
+        monkeypatch.setenv("PSD_FEATURES", f"tail_fp8={int(on)}")  # read at model build
+        torch.manual_seed(0)
+        m = prepare(ResNet((2, 2, 2, 2), num_classes=100, width_per_group=128, fp8=True), gpu, torch.bfloat16,
+                    channels_last=True)
+        for p in m.parameters():
+            p.data = p.data.to(torch.bfloat16)
+        for mod in m.modules():  # non-zero bn3 scales: the tail's gradients are not trivially 0
+            if hasattr(mod, "bn3"):
+                torch.nn.init.uniform_(mod.bn3.weight, 0.1, 0.3)
+        return m.train()
+
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(32, 3, 64, 64, generator=g).to(gpu, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 100, (32,), generator=g).to(gpu)
+    runs = {}
+    for on in (True, False):
+        m = build(on)
+        if on:
+            ref = copy.deepcopy(m).float()  # fp32 reference: same weights, no fp8 / bf16 kernels
+        for k in tail.TAIL_CALLS:
+            tail.TAIL_CALLS[k] = 0
+        m.zero_grad(set_to_none=True)
+        loss = F.cross_entropy(m(x).float(), y)
+        loss.backward()
+        runs[on] = (float(loss), [p.grad.float().clone() for p in m.parameters()], dict(tail.TAIL_CALLS))
+    monkeypatch.setenv("PSD_FEATURES", "")
+    lr = F.cross_entropy(ref(x.float()), y)
+    lr.backward()
+    g32 = [p.grad.float().clone() for p in ref.parameters()]
+    assert runs[True][2]["fwd"] >= 3, runs[True][2]  # one identity block per stage; the fold takes stages 1-3
+    assert runs[False][2]["fwd"] == 0, runs[False][2]
+
+    def rel(gs):
+        num = sum(float((a - b).pow(2).sum()) for a, b in zip(gs, g32))
+        return num ** 0.5 / sum(float(b.pow(2).sum()) for b in g32) ** 0.5
+
+    e_on, e_off = rel(runs[True][1]), rel(runs[False][1])
+    l32 = float(lr)
+    print(f"loss fp32 {l32:.4f} tail {runs[True][0]:.4f} fp8-conv3 {runs[False][0]:.4f}; "
+          f"gradient rel-L2 vs fp32: tail {e_on:.4f} fp8-conv3 {e_off:.4f}")
+    assert abs(runs[True][0] - l32) <= abs(runs[False][0] - l32) + 0.01 * abs(l32)
+    assert e_on <= 1.1 * e_off + 0.02, (e_on, e_off)

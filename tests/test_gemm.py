@@ -387,9 +387,9 @@ def test_gemm_ct_declines_outside_contract(gpu):
 
 @pytest.mark.parametrize("shape", [(2304, 768, 8192), (768, 3072, 4096), (520, 1000, 2056)], ids=str)
 def test_gemm_splitk_bcontig_bitwise(gpu, shape):
-    """The split-K GEMM with an N-major B staged as contiguous 128-column halves (default) against the
-    quadrant-interleaved halves: the same K order per output, so bitwise equal; and exact against
-    fp32 on small integers."""
+    """The split-K GEMM with an N-major B staged as contiguous 128-column halves against the
+    quadrant-interleaved halves (default): the same K order per output, so bitwise equal; and exact
+    against fp32 on small integers."""
     M, N, K = shape
     C = native()
     g = torch.Generator().manual_seed(13)
@@ -402,7 +402,7 @@ def test_gemm_splitk_bcontig_bitwise(gpu, shape):
         try:
             C.gemm_splitk_(a, b, False, False, out, False, 1.0, 0)
         finally:
-            C.gemm_set_bcontig(True)
+            C.gemm_set_bcontig(False)
         outs.append(out.cpu())
     assert torch.equal(outs[0], outs[1])
     torch.testing.assert_close(outs[0], a.float().cpu().t() @ b.float().cpu(), rtol=0, atol=0)

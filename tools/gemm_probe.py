@@ -46,14 +46,14 @@ def make(layout, M, N, K):
         a, b = rnd(M, K), rnd(N, K)
         return (lambda: C.gemm_ct_(b, a, out)), (lambda: torch.mm(a, b.t(), out=out)), out, (a, b)
     # TN: C[M, N] = A^T B with A [K, M], B [K, N] (wgrad: M = out features, K = tokens); TN0: the same
-    # with the quadrant-interleaved B halves (gemm_set_bcontig(False), the pre-round-6 staging)
+    # with the B halves staged as contiguous 128-column rows (gemm_set_bcontig(True); default off)
     a, b = rnd(K, M), rnd(K, N)
-    bc = layout != "TN0"
+    bc = layout == "TN0"
 
     def ours():
         C.gemm_set_bcontig(bc)
         C.gemm_splitk_(a, b, False, False, out, False, 1.0, 0)
-        C.gemm_set_bcontig(True)
+        C.gemm_set_bcontig(False)
 
     return ours, (lambda: torch.mm(a.t(), b, out=out)), out, (a, b)
 
