@@ -147,6 +147,14 @@ def choose(key: tuple, candidates: dict, default: str, probe=None) -> str:
     """Name of the fastest *correct* candidate for ``key`` (timed and validated once, cached).
     ``probe``: returns the output tensor of a candidate that writes into a preallocated buffer
     instead of returning its result."""
+    if not _feat("library_candidates"):
+        # our kernels only: a library candidate (MIOpen / hipBLASLt) stays only where no kernel of
+        # ours takes the shape -- the reference of the correctness check is then our default kernel
+        own = {n: f for n, f in candidates.items() if n not in LIBRARY}
+        if own:
+            candidates = own
+            if default not in own:
+                default = next(iter(own))
     got = _DECISIONS.get(key)
     if got is not None and got in candidates:
         return got

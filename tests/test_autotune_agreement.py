@@ -194,3 +194,26 @@ def test_decision_file_schema(tmp_path):
         assert at.load_decisions(str(tmp_path / "new.json")) >= 1
     finally:
         at.set_decision(("t", "schema"), None)
+
+
+def test_library_candidates_off_keeps_only_own_kernels(monkeypatch):
+    """feature library_candidates off: MIOpen / hipBLASLt leave every candidate set in which one of
+    our kernels takes the shape (even when faster, and even as the default); they stay the fallback
+    where nothing of ours does."""
+    from parameter_server_distributed_amd.ops import autotune as at
+    from parameter_server_distributed_amd.utils.config import set_feature
+
+    out = torch.ones(4)
+    times = {"miopen": 0.5, "blas": 0.4, "psdw0": 1.0, "mfma": 0.9}
+    monkeypatch.setattr(at, "_time_ms", lambda fn, probe=None: (times[fn()], [out, out]))
+    set_feature("library_candidates", False)
+    keys = [("lib", 1), ("lib", 2), ("lib", 3)]
+    try:
+        assert at.choose(keys[0], {n: (lambda n=n: n) for n in ("miopen", "psdw0")}, "miopen") == "psdw0"
+        assert at.choose(keys[1], {n: (lambda n=n: n) for n in ("mfma", "blas", "psdw0")}, "mfma") == "mfma"
+        assert at.choose(keys[2], {"miopen": lambda: "miopen"}, "miopen") == "miopen"  # the only candidate
+    finally:
+        set_feature("library_candidates", None)
+        for k in keys:
+            at._DECISIONS.pop(k, None)
+            at._TIMES.pop(k, None)
