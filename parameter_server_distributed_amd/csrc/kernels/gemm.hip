@@ -802,38 +802,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
   // of K-tile u+1, (am2, bn2, ak2) the A/B sources of K-tile u+2. first: the K-tile right after an
   // epilogue, whose phase-0 DMA was issued before the epilogue's stores; its phase-3 wait leaves
   // those stores in flight (they are older than K-tile u+2's DMA only)
-  // L2 warm-up of a K-tile the LDS pipeline stages ~1.5 K-tiles later: the loop holds only ~0.75 of a
-  // K-tile of DMA in flight beyond the one being read (two LDS buffers), so at HBM / MALL latency the
-  // K-step waits on memory; a line already in L2 by then returns in a fraction of that. One 4-byte
-  // LDS-DMA per 128-byte line (waves 0-3: A, 4-7: B; 256 lines each) into bytes 512..767 of the
-  // wave's epilogue slot (never read; the bias / statistics shift use 0..511). Issued after phase
-  // 3's counted wait, so it is older than every DMA the next wait may leave in flight: the vmcnt
-  // constants are unchanged and it has landed before that wait retires (never issued in a tile's
-  // last K-step, so none lands during an epilogue).
-  constexpr bool kPF = !GA && !GB && !MX && BM != 192;
-  auto prefetch = [&](int m0, int n0, int k) {
-    if constexpr (kPF) {
-      const bool isA = wid < 4;
-      const int idx = (wid & 3) * 64 + lane;  // line index within the operand's K-tile
-      const bool km = isA ? AK : BKM;
-      const int rows = isA ? BM : kBig;
-      const int ld = isA ? g.lda : g.ldb;
-      const int r0 = isA ? m0 : n0;
-      uint32_t off;
-      const bool kin = k < g.K;  // (u+3 past this split / the operand: nothing to warm)
-      if (km) {  // [rows][ld]: one 128-byte line per tile row
-        off = (idx < rows && kin) ? ((uint32_t)(r0 + idx) * (uint32_t)ld + (uint32_t)k) * ESZ : kMasked;
-      } else {   // [k][ld]: rows / 64 lines per k-row (bf16: 2 bytes per column)
-        const int per = rows * ESZ / 128;
-        const int kr = idx / per, ch = idx - kr * per;
-        off = (kr < KT && kin) ? ((uint32_t)(k + kr) * (uint32_t)ld + (uint32_t)r0) * ESZ + ch * 128 : kMasked;
-      }
-      const rsrc_t src = isA ? make_rsrc(g.A, bytesA) : make_rsrc(g.B, bytesB);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          src, (__attribute__((address_space(3))) void*)(smem + 2 * P::BUF + wid * P::STG + 512), 4, off, 0, 0, 0);
-    }
-  };
-  auto kstep = [&](int u, int am1, int ak1, int am2, int bn2, int ak2, bool first, bool pfon) {
+  auto kstep = [&](int u, int am1, int ak1, int am2, int bn2, int ak2, bool first) {
     // ---- phase 0: q(0,0)
     readS(u);  // (before the B reads: retired by the same lgkmcnt wait)
     readB(half(u, 2), b0, fb0);
@@ -865,7 +834,6 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
       wait_vm<P::VM + kEpiStores>();  // K-tile u+1 complete; the epilogue stores may still drain
     else
       wait_vm<P::VM>();  // K-tile u+1 complete (its A-half1 was staged in phase 0)
-    if (pfon) prefetch(am2, bn2, ak2 + KT);  // K-tile u+3 (wave-uniform; past K: masked by the range check)
     __builtin_amdgcn_sched_barrier(0);
     PSD_SYNC_OPEN()
     quad(3, a1, b1, fa1, fb1);
@@ -918,7 +886,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g) {
       const int ak1 = d1 >= 0 ? sk0 : kbeg + (t + 1) * KT;
       const int am2 = d2 >= 0 ? sm0 : cm0, bn2 = d2 >= 0 ? sn0 : cn0;
       const int ak2 = d2 > 0 ? sk1 : (d2 == 0 ? sk0 : kbeg + (t + 2) * KT);
-      kstep(base + t, am1, ak1, am2, bn2, ak2, jt > 0 && t == 0, g.pf && t + 1 < nt);
+      kstep(base + t, am1, ak1, am2, bn2, ak2, jt > 0 && t == 0);
     }
     // the next tile's first K-tile issues its phase-0 DMA (A-half1 of its K-tile 1) here, BEFORE
     // the stores below, so that its phase-3 wait can leave the stores in flight (nt >= 2 whenever
@@ -1359,9 +1327,6 @@ static int cu_count() {
 // workgroups of the persistent 8-phase grid: one per CU (the kernel's LDS allows no second)
 static int persistent_grid() { return cu_count(); }
 
-static bool g_pf = true;
-void gemm_set_prefetch(bool on) { g_pf = on; }
-
 // contiguous B halves for the split-K GEMMs with an N-major B (weight gradients); g_bc: off for A/Bs
 static bool g_bc = false;  // measured no faster on the BERT weight gradients (profiles/r6/gemm_probe_bert_r6b.md: TN vs TN0)
 void gemm_set_bcontig(bool on) { g_bc = on; }
@@ -1400,10 +1365,8 @@ static hipError_t launch_8p_act(const GemmArgs& g, int splits, hipStream_t st) {
   constexpr int KT = F8 ? 128 : BK;
   int grid = nwg;
   if (MODE == 0 && splits == 1 && g.K / KT >= 2) grid = std::min(nwg, persistent_grid());
-  GemmArgs ga = g;
-  ga.pf = g_pf ? 1 : 0;
   hipLaunchKernelGGL((gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT, GA, F8A, GB, MX, ST, CT, BC>), dim3(grid, 1, splits),
-                     dim3(512), lds, st, ga);
+                     dim3(512), lds, st, g);
   return hipGetLastError();
 }
 

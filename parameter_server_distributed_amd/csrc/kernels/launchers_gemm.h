@@ -33,9 +33,6 @@ struct GemmArgs {
   float* part;
   const float* shift;
   int* rows_out;
-  // 8-phase kernels: warm L2 with K-tile t+3 (one 4-byte LDS-DMA per 128-byte line of both operand
-  // tiles, into an unread corner of the wave's epilogue slot) -- set by the launchers (gemm_set_prefetch)
-  int pf;
 };
 
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t stream);
@@ -48,8 +45,6 @@ int gemm_splits(int M, int N, int K);
 // split-K GEMMs with an N-major B: stage each B half as contiguous 128-column rows (whole 128-byte lines)
 // instead of the quadrant-interleaved halves. Default off: no faster on the BERT weight gradients.
 void gemm_set_bcontig(bool on);
-// L2 warm-up of K-tile t+3 in the 8-phase K loop (default on; off for A/Bs)
-void gemm_set_prefetch(bool on);
 // out[M][Cout] = conv(x, w) (NHWC, no bias / activation), on the persistent 8-phase kernel with A
 // gathered from the input; hipErrorNotSupported when the shape is outside that kernel's contract
 hipError_t launch_conv_fwd(const GemmArgs& g, hipStream_t stream);

@@ -406,38 +406,3 @@ def test_gemm_splitk_bcontig_bitwise(gpu, shape):
         outs.append(out.cpu())
     assert torch.equal(outs[0], outs[1])
     torch.testing.assert_close(outs[0], a.float().cpu().t() @ b.float().cpu(), rtol=0, atol=0)
-
-
-@pytest.mark.parametrize("layout", ["NT", "NN", "TN", "CT"])
-def test_gemm_l2_prefetch_bitwise(gpu, layout):
-    """The 8-phase K loop's L2 warm-up of K-tile t+3 (gemm_set_prefetch) moves no data the MFMAs read:
-    every layout's result is bitwise equal with it on and off (persistent multi-tile grids, split-K)."""
-    C = native()
-    g = torch.Generator().manual_seed(17)
-    M, N, K = (8192, 3072, 768) if layout != "TN" else (2304, 768, 16384)
-    a = torch.randn(M, K, generator=g).to(torch.bfloat16).to(gpu)
-    b = torch.randn(N, K, generator=g).to(torch.bfloat16).to(gpu)
-    at_, bt_ = (a.t().contiguous(), b.t().contiguous()) if layout == "TN" else (None, None)  # [K, M], [K, N]
-    outs = []
-    for pf in (True, False):
-        C.gemm_set_prefetch(pf)
-        try:
-            if layout == "NT":
-                out = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
-                C.gemm_(a, b, True, True, out)
-            elif layout == "NN":
-                out = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
-                C.gemm_(a, b.t().contiguous(), True, False, out)
-            elif layout == "TN":
-                out = torch.empty(M, N, dtype=torch.float32, device=gpu)
-                C.gemm_splitk_(at_, bt_, False, False, out)
-            else:
-                out = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
-                assert C.gemm_ct_(b, a, out)
-        finally:
-            C.gemm_set_prefetch(True)
-        outs.append(out.cpu())
-    assert torch.equal(outs[0], outs[1])
-    if layout in ("NT", "CT"):
-        ref = a.float().cpu() @ b.float().cpu().t()
-        assert ((outs[0].float() - ref).norm() / ref.norm()).item() < 1e-2

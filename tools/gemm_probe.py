@@ -82,8 +82,6 @@ def main():
     import torch.cuda.tunable as tn
 
     tn.enable(False)
-    # PSD_GEMM_PF=0: the 8-phase K loop without its L2 warm-up of K-tile t+3 (A/B)
-    native().gemm_set_prefetch(os.environ.get("PSD_GEMM_PF", "1") != "0")
     if a.pmc:
         lay, M, N, K = a.pmc.split("x")
         ours, lib, _, _ = make(lay, int(M), int(N), int(K))
