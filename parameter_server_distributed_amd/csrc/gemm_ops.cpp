@@ -183,6 +183,27 @@ void gemm_splitk_(const at::Tensor& A, const at::Tensor& B, bool a_kmajor, bool 
   TORCH_CHECK(b_kmajor || N % 8 == 0, "psd gemm_splitk: N % 8");
   const c10::DeviceGuard g(A.device());
   const int s = splits > 0 ? (int)splits : gemm_splits((int)M, (int)N, (int)K);
+  if (s == 1 && !accumulate && scale == 1.0) {
+    // one split (enough output tiles to fill the chip, e.g. the BERT MLM head's weight gradient:
+    // 120 x 3 256-tiles): the single-split GEMM writes the output itself -- no fp32 slab
+    // (94 MB written and read back there) and no reduce launch
+    GemmArgs a{};
+    a.A = A.data_ptr();
+    a.B = B.data_ptr();
+    a.C = out.data_ptr();
+    a.M = (int)M;
+    a.N = (int)N;
+    a.K = (int)K;
+    a.lda = (int)A.stride(0);
+    a.ldb = (int)B.stride(0);
+    a.ldc = (int)N;
+    a.a_kmajor = a_kmajor;
+    a.b_kmajor = b_kmajor;
+    a.c_f32 = out.scalar_type() == at::kFloat;
+    const hipError_t e = launch_gemm(a, stream_of(A));
+    TORCH_CHECK(e == hipSuccess, "psd gemm_splitk (single split): ", hipGetErrorString(e));
+    return;
+  }
   at::Tensor slab = at::empty({(int64_t)s * M * N}, A.options().dtype(at::kFloat));
   GemmArgs a{};
   a.A = A.data_ptr();

@@ -89,6 +89,8 @@ FEATURES: dict[str, tuple[bool, str]] = {
     "fp8_mx_handover": (True, "BN passes write the consumer's MX e4m3 input / producer's MX e5m2 dY"),
     "fp8_delayed": (True, "per-tensor fp8: delayed (previous-call amax) scaling"),
     "fp8_dgrad": (True, "fp8 e5m2-dY bwd-data of the fp8 convolutions"),
+    "xfer_local": (False, "async PS: own-shard pushes / pulls on the scatter / gather kernel (many workgroups, "
+                          "briefly) instead of HIP's device copy (a long-running blit kernel beside backward)"),
     "tail_fp8": (True, "fp8 models' identity blocks: conv3 + bn3 as the bf16 recomputing tail (bn3 folded "
                        "into conv3's bf16 backward, conv3's output never stored); read at model build"),
     # BERT (ops/linear.py, ops/attention.py)

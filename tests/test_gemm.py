@@ -406,3 +406,23 @@ def test_gemm_splitk_bcontig_bitwise(gpu, shape):
         outs.append(out.cpu())
     assert torch.equal(outs[0], outs[1])
     torch.testing.assert_close(outs[0], a.float().cpu().t() @ b.float().cpu(), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("out_f32", [True, False], ids=["f32", "bf16"])
+def test_gemm_splitk_single_split_direct(gpu, out_f32):
+    """A split-K GEMM whose shape gets one split (192 256-tiles: the chip is full without splitting)
+    runs as the single-split GEMM writing the output itself (no slab / reduce): exact on small
+    integers in TN layout, and the accumulate path (slab + reduce) still adds."""
+    M, N, K = 4096, 3072, 4096
+    C = native()
+    g = torch.Generator().manual_seed(23)
+    a = torch.randint(-2, 3, (K, M), generator=g).float()
+    b = torch.randint(-2, 3, (K, N), generator=g).float()
+    ref = a.t() @ b
+    dt = torch.float32 if out_f32 else torch.bfloat16
+    out = torch.empty(M, N, dtype=dt, device=gpu)
+    C.gemm_splitk_(a.to(torch.bfloat16).to(gpu), b.to(torch.bfloat16).to(gpu), False, False, out, False, 1.0, 0)
+    torch.testing.assert_close(out.float().cpu(), ref if out_f32 else ref.bfloat16().float(), rtol=0, atol=0)
+    acc = torch.full((M, N), 2.0, dtype=torch.float32, device=gpu)
+    C.gemm_splitk_(a.to(torch.bfloat16).to(gpu), b.to(torch.bfloat16).to(gpu), False, False, acc, True, 1.0, 0)
+    torch.testing.assert_close(acc.cpu(), ref + 2.0, rtol=0, atol=0)
