@@ -143,10 +143,13 @@ def _peer_decision(st, skey: str, candidates: dict) -> str | None:
     return name
 
 
-def choose(key: tuple, candidates: dict, default: str, probe=None) -> str:
+def choose(key: tuple, candidates: dict, default: str, probe=None, group=None) -> str:
     """Name of the fastest *correct* candidate for ``key`` (timed and validated once, cached).
     ``probe``: returns the output tensor of a candidate that writes into a preallocated buffer
-    instead of returning its result."""
+    instead of returning its result. ``group``: name -> family, for candidate sets whose families
+    return different (each internally consistent) tensors -- e.g. a fused bwd-data epilogue returns
+    the BN-masked gradient, the plain kernels dX: each candidate is validated against the first
+    candidate of its own family (the default's family against the default)."""
     if not _feat("library_candidates"):
         # our kernels only: a library candidate (MIOpen / hipBLASLt) stays only where no kernel of
         # ours takes the shape -- the reference of the correctness check is then our default kernel
@@ -182,7 +185,7 @@ def choose(key: tuple, candidates: dict, default: str, probe=None) -> str:
     # The claiming rank always publishes -- a decision, "every candidate declined", or its error --
     # so no peer waits on a key nobody will decide (and this rank never claims it again).
     try:
-        best = _time_and_pick(key, candidates, default, probe)
+        best = _time_and_pick(key, candidates, default, probe, group)
     except Declined:
         _DECLINED_KEYS.add(key)
         if st is not None:
@@ -205,7 +208,7 @@ LIBRARY = frozenset({"miopen", "gemm", "blas"})
 OWN_MARGIN = 0.02
 
 
-def _time_and_pick(key: tuple, candidates: dict, default: str, probe) -> str:
+def _time_and_pick(key: tuple, candidates: dict, default: str, probe, group=None) -> str:
     runs, declined = {}, []
     for name, fn in candidates.items():
         try:
@@ -223,7 +226,13 @@ def _time_and_pick(key: tuple, candidates: dict, default: str, probe) -> str:
         ref_name = next((n for n, r in runs.items() if all(o is None or bool(torch.isfinite(o).all())
                                                            for o in r[1])), ref_name)
         ref = runs[ref_name][1]
-    ok = {n: r[0] for n, r in runs.items() if n == ref_name or _agrees(r[1], ref)}
+    if group is None:
+        ok = {n: r[0] for n, r in runs.items() if n == ref_name or _agrees(r[1], ref)}
+    else:
+        refs = {group(ref_name): ref_name}  # per family: the default, else the family's first candidate
+        for n in runs:
+            refs.setdefault(group(n), n)
+        ok = {n: r[0] for n, r in runs.items() if n == refs[group(n)] or _agrees(r[1], runs[refs[group(n)]][1])}
     bad = [n for n in runs if n not in ok]
     if bad:
         _REJECTED[key] = _REJECTED.get(key, []) + bad

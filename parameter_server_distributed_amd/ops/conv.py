@@ -418,7 +418,8 @@ def _dgrad_route(key: tuple, cands: dict, default: str, fu, dy_like) -> torch.Te
             raise RuntimeError("psd: a BN without its stored input needs the fused bwd-data epilogue")
         key, default = key + ("nobx",), next(iter(cands))
     timed = {name: (fn if name.startswith("psdnb") else _with_bn_bwd_reduce(fn, fu)) for name, fn in cands.items()}
-    how = _at.choose(key + ("bnbwd",), timed, default)
+    # (the fused candidates return the BN-masked gradient g, the others dX: validated per family)
+    how = _at.choose(key + ("bnbwd",), timed, default, group=lambda n: n.startswith("psdnb"))
     out = cands[how]()
     if not how.startswith("psdnb"):
         fu["bn"]._psd_bwd_pre = None
@@ -665,7 +666,8 @@ def _fold_backward(ctx, fold, x, weight, need_x: bool, need_w: bool, P=None):
             how = _at.choose(key, cands, default)
         else:
             timed = {nm: (fn if nm.startswith("psdnb") else _with_bn_bwd_reduce(fn, fu)) for nm, fn in cands.items()}
-            how = _at.choose(key + ("bnbwd",), timed, default)
+            # (fused epilogues return the BN-masked gradient, the others dX: validated per family)
+            how = _at.choose(key + ("bnbwd",), timed, default, group=lambda nm: nm.startswith("psdnb"))
         timing["on"] = False
         if how != "unfold":
             dx = cands[how]()

@@ -72,8 +72,10 @@ FEATURES: dict[str, tuple[bool, str]] = {
     "convw_twostage": (True, "narrow weight-gradient tiles also on a two-stage ring at two workgroups per CU"),
     "convw_fold2": (True, "the BN-fold and Gram weight-gradient launches on the two-stage ring (two workgroups per CU)"),
     "gemm_stats": (True, "consumer-BN statistics in the 8-phase GEMM epilogue"),
-    "library_candidates": (True, "autotune times MIOpen / hipBLASLt candidates too; off: our kernels only wherever "
-                                 "one takes the shape (the library stays the fallback)"),
+    "library_candidates": (False, "autotune also times MIOpen / hipBLASLt candidates wherever one of our kernels "
+                                  "takes the shape; off (default): our kernels only there, the library only as the "
+                                  "fallback -- same-box ResNet-50 15,681 / 15,695 vs 15,557 / 15,591 img/s with them "
+                                  "(profiles/r6/ab_library_candidates.md)"),
     "prefer_own": (True, "autotune: our kernel takes a pick a library candidate wins by < 2 % (ops/autotune.py OWN_MARGIN)"),
     "wprep": (True, "every convolution's bwd-data weight operand (transpose / tap flip / stride-2 phases) in one batched launch per step (ops/wprep.py)"),
     # batch norm / bottleneck tail (ops/bn.py, ops/tail.py)

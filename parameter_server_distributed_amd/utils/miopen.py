@@ -1,10 +1,13 @@
-"""Ship MIOpen's tuned find-db and compiled-kernel cache with the repo.
+"""Ship MIOpen's tuned find-db with the repo (for the library fallback).
 
-A fresh MI355X box starts with an empty MIOpen user database, so the first training step of
-ResNet-50 spends minutes in convolution Find + kernel compilation. ``tuning/miopen`` holds the
-database and kernel cache produced on gfx950 by ``bench.py`` (MIOPEN_USER_DB_PATH /
-MIOPEN_CUSTOM_CACHE_DIR); ``install()`` copies it to a writable scratch directory and points
-MIOpen at it. Must run before the first convolution (ideally before ``import torch``).
+Since round 6 the benches run no MIOpen kernel: every ResNet-50 / WRN-101-2 convolution shape is
+taken by our kernels and the library is no longer an autotune candidate there (feature
+``library_candidates``, utils/config.py), so the prebuilt MIOpen kernel cache (a binary
+``.ukdb``) is no longer shipped. MIOpen stays the fallback for shapes none of our kernels takes
+(and the fp32 reference of tests); ``tuning/miopen/db`` holds its text find-db produced on gfx950,
+and ``install()`` copies it to a writable scratch directory and points MIOpen at it
+(MIOPEN_USER_DB_PATH / MIOPEN_CUSTOM_CACHE_DIR), so a fallback compiles only what it uses. Must run
+before the first convolution (ideally before ``import torch``).
 """
 from __future__ import annotations
 

@@ -4,7 +4,7 @@
 set -o pipefail
 F=$1; VALS=$2; shift 2
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
-OUT=$R/gpurun_out/ab_$F
+OUT=$R/gpurun_out/ab_${ABTAG:-$F}
 mkdir -p "$OUT"
 cd "$R"
 i=0

@@ -217,3 +217,26 @@ def test_library_candidates_off_keeps_only_own_kernels(monkeypatch):
         for k in keys:
             at._DECISIONS.pop(k, None)
             at._TIMES.pop(k, None)
+
+
+def test_groups_validate_within_family(monkeypatch):
+    """Candidate families returning different tensors (a fused bwd-data epilogue's BN-masked gradient
+    vs the plain kernels' dX) are each validated against their own family's reference: a correct
+    fused candidate is not rejected for differing from dX, and a wrong one still is."""
+    from parameter_server_distributed_amd.ops import autotune as at
+
+    dx = torch.linspace(-1, 1, 64)
+    g = dx * (dx > 0)  # the "masked" family
+    outs = {"plain0": dx, "plain1": dx * (1 + 1e-4), "psdnb0": g, "psdnb1": g * (1 - 1e-4), "psdnb2": torch.zeros(64)}
+    times = {"plain0": 1.0, "plain1": 0.9, "psdnb0": 0.8, "psdnb1": 0.7, "psdnb2": 0.1}
+    monkeypatch.setattr(at, "_time_ms", lambda fn, probe=None: (times[fn()], [outs[fn()], outs[fn()]]))
+    key = ("t", "groups")
+    try:
+        got = at._time_and_pick(key, {n: (lambda n=n: n) for n in outs}, "plain0", None,
+                                group=lambda n: n.startswith("psdnb"))
+        assert got == "psdnb1", got
+        assert at.rejected()[key] == ["psdnb2"], at.rejected()[key]
+    finally:
+        at._DECISIONS.pop(key, None)
+        at._TIMES.pop(key, None)
+        at._REJECTED.pop(key, None)
