@@ -236,7 +236,7 @@ def test_fp8_tail_on_vs_off_against_fp32(gpu, monkeypatch):
     lr = F.cross_entropy(ref(x.float()), y)
     lr.backward()
     g32 = [p.grad.float().clone() for p in ref.parameters()]
-    assert runs[True][2]["fwd"] >= 3, runs[True][2]  # one identity block per stage; the fold takes stages 1-3
+    assert runs[True][2]["fwd"] >= 2, runs[True][2]  # one identity block per stage; the fold takes stages 1-2 here
     assert runs[False][2]["fwd"] == 0, runs[False][2]
 
     def rel(gs):
