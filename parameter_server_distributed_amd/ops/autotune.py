@@ -150,7 +150,7 @@ def choose(key: tuple, candidates: dict, default: str, probe=None, group=None) -
     return different (each internally consistent) tensors -- e.g. a fused bwd-data epilogue returns
     the BN-masked gradient, the plain kernels dX: each candidate is validated against the first
     candidate of its own family (the default's family against the default)."""
-    if not _feat("library_candidates"):
+    if not _feat("library_linear" if key and key[0] == "linear" else "library_candidates"):
         # our kernels only: a library candidate (MIOpen / hipBLASLt) stays only where no kernel of
         # ours takes the shape -- the reference of the correctness check is then our default kernel
         own = {n: f for n, f in candidates.items() if n not in LIBRARY}

@@ -72,10 +72,13 @@ FEATURES: dict[str, tuple[bool, str]] = {
     "convw_twostage": (True, "narrow weight-gradient tiles also on a two-stage ring at two workgroups per CU"),
     "convw_fold2": (True, "the BN-fold and Gram weight-gradient launches on the two-stage ring (two workgroups per CU)"),
     "gemm_stats": (True, "consumer-BN statistics in the 8-phase GEMM epilogue"),
-    "library_candidates": (False, "autotune also times MIOpen / hipBLASLt candidates wherever one of our kernels "
-                                  "takes the shape; off (default): our kernels only there, the library only as the "
-                                  "fallback -- same-box ResNet-50 15,681 / 15,695 vs 15,557 / 15,591 img/s with them "
-                                  "(profiles/r6/ab_library_candidates.md)"),
+    "library_candidates": (False, "convolutions: autotune also times MIOpen / hipBLASLt candidates wherever one of "
+                                  "our kernels takes the shape; off (default): our kernels only there, the library "
+                                  "only as the fallback -- same-box ResNet-50 15,681 / 15,695 vs 15,557 / 15,591 "
+                                  "img/s with them (profiles/r6/ab_library_candidates.md)"),
+    "library_linear": (True, "Linear layers: hipBLASLt stays an autotune candidate (BERT-base same-box 9,576 / 9,505 "
+                             "vs 9,297 / 9,362 seq/s without it: it wins the QKV forward, the attention-output "
+                             "bwd-data and the MLM-head weight gradient in the step, profiles/r6/ab_library_candidates.md)"),
     "prefer_own": (True, "autotune: our kernel takes a pick a library candidate wins by < 2 % (ops/autotune.py OWN_MARGIN)"),
     "wprep": (True, "every convolution's bwd-data weight operand (transpose / tap flip / stride-2 phases) in one batched launch per step (ops/wprep.py)"),
     # batch norm / bottleneck tail (ops/bn.py, ops/tail.py)
@@ -93,8 +96,9 @@ FEATURES: dict[str, tuple[bool, str]] = {
     "fp8_dgrad": (True, "fp8 e5m2-dY bwd-data of the fp8 convolutions"),
     "xfer_local": (False, "async PS: own-shard pushes / pulls on the scatter / gather kernel (many workgroups, "
                           "briefly) instead of HIP's device copy (a long-running blit kernel beside backward)"),
-    "tail_fp8": (True, "fp8 models' identity blocks: conv3 + bn3 as the bf16 recomputing tail (bn3 folded "
-                       "into conv3's bf16 backward, conv3's output never stored); read at model build"),
+    "tail_fp8": (False, "fp8 models' identity blocks: conv3 + bn3 as the bf16 recomputing tail (bn3 folded "
+                       "into conv3's bf16 backward, conv3's output never stored); read at model build. Off: same-box "
+                       "WRN-101-2 4,136 vs 4,170 img/s (profiles/r6/ab_tail_fp8.md)"),
     # BERT (ops/linear.py, ops/attention.py)
     "linear_tune": (True, "per-shape MFMA / hipBLASLt choice for Linear layers; off: MFMA only"),
     "gelu_fuse": (True, "GELU backward in the consumer Linear's bwd-data GEMM epilogue"),
