@@ -48,8 +48,4 @@ def native():
                     "parameter_server_distributed_amd._C is not built; run "
                     "`python -m parameter_server_distributed_amd._build` (or __graft_entry__.build())"
                 ) from e
-        from .utils.config import feature
-
-        # kernel-launch features that live on the native side (read once, at load)
-        _NATIVE.gemm_set_persistent(feature("gemm_persistent"))
     return _NATIVE

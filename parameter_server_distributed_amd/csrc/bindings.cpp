@@ -77,7 +77,6 @@ PYBIND11_MODULE(_C, m) {
         py::arg("shift") = py::none());
   m.def("gemm_stats_rows", &gemm_stats_rows_, py::arg("M"));
   m.def("gemm_set_bcontig", &gemm_set_bcontig, py::arg("on"));
-  m.def("gemm_set_persistent", &gemm_set_persistent, py::arg("on"));
   m.def("gemm_ct_", &gemm_ct_, py::arg("A"), py::arg("B"), py::arg("out"), py::arg("bias") = py::none(),
         py::arg("act") = 0, py::arg("aux") = py::none());
   m.def("gemm_gelu_bwd_", &gemm_gelu_bwd_, py::arg("A"), py::arg("B"), py::arg("a_kmajor"), py::arg("b_kmajor"),

@@ -1327,12 +1327,6 @@ static int cu_count() {
 // workgroups of the persistent 8-phase grid: one per CU (the kernel's LDS allows no second)
 static int persistent_grid() { return cu_count(); }
 
-// single-split 8-phase GEMMs on the persistent grid (one workgroup per CU walking a fixed tile list;
-// default) or one workgroup per tile (the hardware dispatcher balances them: a workgroup that starts
-// late -- its CU held by a kernel of another stream, e.g. a push -- delays only its own tile)
-static bool g_persist = true;
-void gemm_set_persistent(bool on) { g_persist = on; }
-
 // contiguous B halves for the split-K GEMMs with an N-major B (weight gradients); g_bc: off for A/Bs
 static bool g_bc = false;  // measured no faster on the BERT weight gradients (profiles/r6/gemm_probe_bert_r6b.md: TN vs TN0)
 void gemm_set_bcontig(bool on) { g_bc = on; }
@@ -1370,7 +1364,7 @@ static hipError_t launch_8p_act(const GemmArgs& g, int splits, hipStream_t st) {
   // K-tiles per tile to run tiles back to back (big_ok guarantees K >= 256)
   constexpr int KT = F8 ? 128 : BK;
   int grid = nwg;
-  if (MODE == 0 && splits == 1 && g.K / KT >= 2 && g_persist) grid = std::min(nwg, persistent_grid());
+  if (MODE == 0 && splits == 1 && g.K / KT >= 2) grid = std::min(nwg, persistent_grid());
   hipLaunchKernelGGL((gemm8p_kernel<BM, AK, BKM, MODE, F8, ACT, GA, F8A, GB, MX, ST, CT, BC>), dim3(grid, 1, splits),
                      dim3(512), lds, st, g);
   return hipGetLastError();

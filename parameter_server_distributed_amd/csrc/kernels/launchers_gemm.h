@@ -45,8 +45,6 @@ int gemm_splits(int M, int N, int K);
 // split-K GEMMs with an N-major B: stage each B half as contiguous 128-column rows (whole 128-byte lines)
 // instead of the quadrant-interleaved halves. Default off: no faster on the BERT weight gradients.
 void gemm_set_bcontig(bool on);
-// single-split 8-phase GEMMs: persistent grid (default) or one workgroup per output tile
-void gemm_set_persistent(bool on);
 // out[M][Cout] = conv(x, w) (NHWC, no bias / activation), on the persistent 8-phase kernel with A
 // gathered from the input; hipErrorNotSupported when the shape is outside that kernel's contract
 hipError_t launch_conv_fwd(const GemmArgs& g, hipStream_t stream);

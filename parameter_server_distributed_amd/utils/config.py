@@ -71,8 +71,6 @@ FEATURES: dict[str, tuple[bool, str]] = {
     "convw_persist": (True, "persistent layer-1 3x3 weight gradient (convhw)"),
     "convw_twostage": (True, "narrow weight-gradient tiles also on a two-stage ring at two workgroups per CU"),
     "convw_fold2": (True, "the BN-fold and Gram weight-gradient launches on the two-stage ring (two workgroups per CU)"),
-    "gemm_persistent": (True, "single-split 8-phase GEMMs on the persistent grid (one workgroup per CU); off: one "
-                              "workgroup per output tile"),
     "gemm_stats": (True, "consumer-BN statistics in the 8-phase GEMM epilogue"),
     "library_candidates": (False, "convolutions: autotune also times MIOpen / hipBLASLt candidates wherever one of "
                                   "our kernels takes the shape; off (default): our kernels only there, the library "
