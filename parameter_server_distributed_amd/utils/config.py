@@ -94,6 +94,8 @@ FEATURES: dict[str, tuple[bool, str]] = {
     "fp8_mx_handover": (True, "BN passes write the consumer's MX e4m3 input / producer's MX e5m2 dY"),
     "fp8_delayed": (True, "per-tensor fp8: delayed (previous-call amax) scaling"),
     "fp8_dgrad": (True, "fp8 e5m2-dY bwd-data of the fp8 convolutions"),
+    "async_cached_local": (True, "async PS at world 1: inbox / publish buffers in plain (cached) device memory "
+                                 "instead of uncached IPC memory (read by the native engine)"),
     "xfer_local": (False, "async PS: own-shard pushes / pulls on the scatter / gather kernel (many workgroups, "
                           "briefly) instead of HIP's device copy (a long-running blit kernel beside backward)"),
     "tail_fp8": (False, "fp8 models' identity blocks: conv3 + bn3 as the bf16 recomputing tail (bn3 folded "
