@@ -150,16 +150,20 @@ def choose(key: tuple, candidates: dict, default: str, probe=None, group=None) -
     return different (each internally consistent) tensors -- e.g. a fused bwd-data epilogue returns
     the BN-masked gradient, the plain kernels dX: each candidate is validated against the first
     candidate of its own family (the default's family against the default)."""
+    full = candidates
+    lib_fallback = {}
     if not _feat("library_linear" if key and key[0] == "linear" else "library_candidates"):
         # our kernels only: a library candidate (MIOpen / hipBLASLt) stays only where no kernel of
-        # ours takes the shape -- the reference of the correctness check is then our default kernel
+        # ours takes the shape -- the reference of the correctness check is then our default kernel;
+        # if every one of ours declines at run time, the library candidates are timed after all
         own = {n: f for n, f in candidates.items() if n not in LIBRARY}
         if own:
+            lib_fallback = {n: f for n, f in candidates.items() if n in LIBRARY}
             candidates = own
             if default not in own:
                 default = next(iter(own))
     got = _DECISIONS.get(key)
-    if got is not None and got in candidates:
+    if got is not None and got in full:
         return got
     if key in _DECLINED_KEYS:
         raise Declined(f"autotune {key}: every candidate declined")
@@ -175,7 +179,7 @@ def choose(key: tuple, candidates: dict, default: str, probe=None, group=None) -
     skey = repr(key)
     if st is not None and int(st.add(f"psd/autotune/c/{skey}", 1)) > 1:
         try:
-            best = _peer_decision(st, skey, candidates)
+            best = _peer_decision(st, skey, full)
         except Declined:
             _DECLINED_KEYS.add(key)
             raise
@@ -185,7 +189,12 @@ def choose(key: tuple, candidates: dict, default: str, probe=None, group=None) -
     # The claiming rank always publishes -- a decision, "every candidate declined", or its error --
     # so no peer waits on a key nobody will decide (and this rank never claims it again).
     try:
-        best = _time_and_pick(key, candidates, default, probe, group)
+        try:
+            best = _time_and_pick(key, candidates, default, probe, group)
+        except Declined:
+            if not lib_fallback:
+                raise
+            best = _time_and_pick(key, lib_fallback, next(iter(lib_fallback)), probe, group)
     except Declined:
         _DECLINED_KEYS.add(key)
         if st is not None:

@@ -240,3 +240,33 @@ def test_groups_validate_within_family(monkeypatch):
         at._DECISIONS.pop(key, None)
         at._TIMES.pop(key, None)
         at._REJECTED.pop(key, None)
+
+
+def test_library_fallback_when_every_own_kernel_declines(monkeypatch):
+    """library_candidates off, but every one of our candidates declines the shape at run time (a
+    conv our implicit-GEMM kernels do not take): the library candidate is timed and chosen after
+    all -- never an 'every candidate declined' error -- and the decision is cached."""
+    from parameter_server_distributed_amd.ops import autotune as at
+    from parameter_server_distributed_amd.utils.config import set_feature
+
+    def nope():
+        raise at.Declined("shape not taken")
+
+    calls = []
+
+    def lib():
+        calls.append(1)
+        return torch.ones(4)
+
+    set_feature("library_candidates", False)
+    key = ("lib", "fallback")
+    try:
+        assert at.choose(key, {"igemm": nope, "psds_igemm": nope, "miopen": lib}, "miopen") == "miopen"
+        n = len(calls)
+        assert at.choose(key, {"igemm": nope, "psds_igemm": nope, "miopen": lib}, "miopen") == "miopen"
+        assert len(calls) == n  # cached: not re-timed
+    finally:
+        set_feature("library_candidates", None)
+        at._DECISIONS.pop(key, None)
+        at._TIMES.pop(key, None)
+        at._REJECTED.pop(key, None)
