@@ -41,10 +41,8 @@ __device__ __forceinline__ uint32_t amix32(uint32_t h) {  // murmur3 finalizer (
   h ^= h >> 16;
   return h;
 }
-__device__ __forceinline__ bool akeep(uint32_t key, uint64_t idx, uint32_t thresh) {
-  const uint32_t a = amix32(key ^ (uint32_t)idx * 0x9e3779b9u);
-  return amix32(a ^ (uint32_t)(idx >> 32) ^ 0x7f4a7c15u) >= thresh;
-}
+// (common.h drop_keep: one hash per element pair, 16 bits each; fwd and bwd index elements alike)
+__device__ __forceinline__ bool akeep(uint32_t key, uint64_t idx, uint32_t thresh) { return drop_keep(key, idx, thresh); }
 __device__ __forceinline__ uint32_t attn_key(uint32_t seed, const int64_t* step) {
   return amix32(seed * 0x27d4eb2fu ^ (uint32_t)(step ? *step : 0) * 0x165667b1u);
 }

@@ -80,4 +80,27 @@ inline int stream_grid(int64_t work_items, int block) {
   return (int)g;
 }
 
+// Counter-based dropout keep decision shared by the fused LayerNorm and attention kernels: one
+// murmur3 finalizer per PAIR of elements (idx >> 1), each element taking 16 bits of it against the
+// 16-bit threshold thresh32 >> 16 (keep probability resolution 2^-16). Forward and backward call it
+// with the same (key, idx), so the backward regenerates the forward's mask. (Two finalizers per
+// element before: the hash was ~a quarter of the LayerNorm passes' time.)
+__device__ __forceinline__ uint32_t drop_mix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85ebca6bu;
+  h ^= h >> 13;
+  h *= 0xc2b2ae35u;
+  h ^= h >> 16;
+  return h;
+}
+__device__ __forceinline__ uint32_t drop_pair_bits(uint32_t key, uint64_t idx) {
+  const uint64_t pr = idx >> 1;
+  return drop_mix32(key ^ (uint32_t)pr * 0x9e3779b9u ^ (uint32_t)(pr >> 32) * 0x7f4a7c15u);
+}
+__device__ __forceinline__ bool drop_keep(uint32_t key, uint64_t idx, uint32_t thresh32) {
+  const uint32_t h = drop_pair_bits(key, idx);
+  const uint32_t bits = (idx & 1) ? (h >> 16) : (h & 0xffffu);
+  return bits >= (thresh32 >> 16);
+}
+
 }  // namespace psd

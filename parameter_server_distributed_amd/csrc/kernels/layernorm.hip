@@ -32,9 +32,17 @@ __device__ __forceinline__ uint32_t mix32(uint32_t h) {  // murmur3 finalizer
   return h;
 }
 
-__device__ __forceinline__ bool keep_elem(uint32_t key, uint64_t idx, uint32_t thresh) {
-  const uint32_t a = mix32(key ^ (uint32_t)idx * 0x9e3779b9u);
-  return mix32(a ^ (uint32_t)(idx >> 32) ^ 0x7f4a7c15u) >= thresh;
+// the lane's E keep flags (common.h drop_keep's mask: 16 bits of one hash per element pair; off is
+// even -- a lane's E columns start at an even index -- so each pair's hash is computed once here)
+template <int E>
+__device__ __forceinline__ void keep_flags(uint32_t key, int64_t off, uint32_t thresh, bool (&kp)[E]) {
+  const uint32_t t16 = thresh >> 16;
+#pragma unroll
+  for (int j = 0; j < E / 2; ++j) {
+    const uint32_t hb = drop_pair_bits(key, (uint64_t)(off + 2 * j));
+    kp[2 * j] = (hb & 0xffffu) >= t16;
+    kp[2 * j + 1] = (hb >> 16) >= t16;
+  }
 }
 
 __device__ __forceinline__ float wave_sum(float v) {
@@ -85,15 +93,33 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const uint16_t* __restrict_
   load_e<E>(beta + c0, b);
   const uint32_t key = dropout_key(seed, step);
   const int64_t wstride = (int64_t)gridDim.x * (blockDim.x >> 6);
-  for (int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < rows; r += wstride) {
+  // software-pipelined as the backward: the next row's x / h loads are issued before this row's
+  // reductions (one row per wave in flight left the pass latency-bound)
+  int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  float nxv[E], nhv[E];
+  if (r < rows) {
+    load_e<E>(x + r * H + c0, nxv);
+    load_e<E>(h + r * H + c0, nhv);
+  }
+  for (; r < rows; r += wstride) {
     const int64_t off = r * H + c0;
     float xv[E], hv[E];
-    load_e<E>(x + off, xv);
-    load_e<E>(h + off, hv);
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      xv[i] = nxv[i];
+      hv[i] = nhv[i];
+    }
+    const int64_t rn = r + wstride;
+    if (rn < rows) {
+      load_e<E>(x + rn * H + c0, nxv);
+      load_e<E>(h + rn * H + c0, nhv);
+    }
+    bool kp[E];
+    if (thresh != 0u) keep_flags<E>(key, off, thresh, kp);
     float sum = 0.f;
 #pragma unroll
     for (int i = 0; i < E; ++i) {
-      const float d = (thresh == 0u || keep_elem(key, (uint64_t)(off + i), thresh)) ? hv[i] * scale : 0.f;
+      const float d = (thresh == 0u || kp[i]) ? hv[i] * scale : 0.f;
       xv[i] = bf16_to_f32(f32_to_bf16(xv[i] + d));  // s, rounded as stored (the LN input)
       sum += xv[i];
     }
@@ -176,9 +202,11 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
 #pragma unroll
     for (int i = 0; i < E; ++i) dv[i] = rstd * (dv[i] - a - sv[i] * bsum);  // d s
     store_e<E>(dx + off, dv);
+    bool kp[E];
+    if (thresh != 0u) keep_flags<E>(key, off, thresh, kp);
 #pragma unroll
     for (int i = 0; i < E; ++i) {
-      dv[i] = (thresh == 0u || keep_elem(key, (uint64_t)(off + i), thresh)) ? dv[i] * scale : 0.f;
+      dv[i] = (thresh == 0u || kp[i]) ? dv[i] * scale : 0.f;
       if constexpr (HS) ph[i] += dv[i];
     }
     store_e<E>(dh + off, dv);
