@@ -169,8 +169,8 @@ def choose(key: tuple, candidates: dict, default: str, probe=None, group=None) -
         raise Declined(f"autotune {key}: every candidate declined")
     # A/B runs: e.g. "mfma" / "blas" / "miopen" / "gemm", or a priority list "psdnb0,psdn0" (the
     # first name this op offers wins)
-    for forced in os.environ.get("PSD_AUTOTUNE_FORCE", "").split(","):
-        if forced and forced in candidates:
+    for forced in os.environ.get("PSD_AUTOTUNE_FORCE", "").split(","):  # (a forced library name overrides the filter)
+        if forced and forced in full:
             _DECISIONS[key] = forced
             return forced
     if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
