@@ -744,12 +744,6 @@ void AsyncEngine::set_xfer_blocks(int cap) {
   xfer_cap_ = cap;
 }
 
-void AsyncEngine::set_xfer_local(int blocks) {
-  TORCH_CHECK(blocks >= 0 && blocks <= 1024, "psd async: local xfer workgroups in [0, 1024]");
-  TORCH_CHECK(blocks == 0 || device_ >= 0, "psd async: the scatter / gather kernels need a GPU engine");
-  xfer_local_ = blocks;
-}
-
 namespace {
 // the scatter / gather kernels move 16-byte vectors: a segment with an unaligned end takes the copy
 // path (hipMemcpyAsync accepts any alignment)
@@ -839,9 +833,8 @@ std::vector<int64_t> AsyncEngine::pull_impl(int64_t step, char* dst, char* dst_s
     else
       al = aligned16(publish_ptr(k, bufs[k]), dst + shard_off_[k] * esz_);
   }
-  const bool local_k = !remote && xfer_local_ > 0;  // own shards only, on the kernel (set_xfer_local)
-  if (device_ >= 0 && ((xfer_kernel_ && remote) || local_k) && al) {
-    const int cap = remote ? xfer_cap_ : xfer_local_;
+  if (device_ >= 0 && xfer_kernel_ && remote && al) {
+    const int cap = xfer_cap_;
     // every shard's snapshot in one gather launch: all owners' links at once (kernels/xfer.hip)
     const c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device_));
     if (dst_sc) {
@@ -867,7 +860,7 @@ std::vector<int64_t> AsyncEngine::pull_impl(int64_t step, char* dst, char* dst_s
         mx = std::max(mx, shard_len_[k] * esz_);
       }
       L.blocks_per_seg = xfer_blocks(mx, cap);
-      L.nt_load = remote ? 1 : 0;
+      L.nt_load = 1;
       hip_ok(launch_xfer(L, static_cast<hipStream_t>(sp)), "launch_xfer(pull)");
     }
   } else {
@@ -905,10 +898,10 @@ void AsyncEngine::push(int64_t step, const at::Tensor& grads_flat, int64_t lo, i
     remote = remote || (a < b && owners_[k] != rank_);
     if (a < b) al = al && aligned16(src + a * esz_, inbox_ptr((int)k, my_wi_, slot) + (a - shard_off_[k]) * esz_);
   }
-  const bool local_k = !remote && xfer_local_ > 0;
-  if (device_ >= 0 && ((xfer_kernel_ && remote) || local_k) && al) {
+  if (device_ >= 0 && xfer_kernel_ && remote && al) {
     // the bucket's slice for every owner it overlaps in one scatter launch (kernels/xfer.hip); a
-    // push into this rank's own inbox only is a local copy unless set_xfer_local (see pull_impl)
+    // push into this rank's own inbox only is a local copy (see pull_impl; on the kernel it measured
+    // no faster at N = 1, profiles/r6/ab_xfer_local.md)
     XferList L{};
     int64_t mx = 0;
     for (size_t k = 0; k < owners_.size(); ++k) {
@@ -918,7 +911,7 @@ void AsyncEngine::push(int64_t step, const at::Tensor& grads_flat, int64_t lo, i
                                  (b - a) * esz_};
       mx = std::max(mx, (b - a) * esz_);
     }
-    L.blocks_per_seg = xfer_blocks(mx, remote ? xfer_cap_ : xfer_local_);
+    L.blocks_per_seg = xfer_blocks(mx, xfer_cap_);
     L.nt_store = 1;
     const c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device_));
     hip_ok(launch_xfer(L, reinterpret_cast<hipStream_t>(stream)), "launch_xfer(push)");

@@ -94,11 +94,6 @@ class AsyncEngine {
   // workgroups per segment of one scatter / gather launch (cap; default 48): the budget of CUs a
   // push may take from the backward pass running beside it (bench.py probes it at N > 1)
   void set_xfer_blocks(int cap);
-  // local (own-shard) pushes / pulls on the scatter / gather kernel too, with `blocks` workgroups per
-  // segment (0: the copy path). HIP's device-to-device copy is a blit kernel with few workgroups that
-  // runs long beside backward; a kernel that takes many CUs briefly finishes before the persistent
-  // GEMM / convolution launches queue behind it (tools/xfer_interference.py)
-  void set_xfer_local(int blocks);
   int xfer_blocks_cap() const { return xfer_cap_; }
   void push(int64_t step, const at::Tensor& grads_flat, int64_t lo, int64_t hi, int64_t stream);
   void commit(int64_t step, std::vector<int64_t> pulled, int64_t stream);
@@ -178,7 +173,6 @@ class AsyncEngine {
   bool fixed_ = false;
   bool xfer_kernel_ = false;  // set in the constructor: true on a GPU engine
   int xfer_cap_ = 48;         // set_xfer_blocks
-  int xfer_local_ = 0;        // set_xfer_local
   double timeout_s_;
   double dead_after_s_ = 10.0;  // a peer's engine silent this long is presumed dead (PSD_ASYNC_DEAD_S)
   int esz_;

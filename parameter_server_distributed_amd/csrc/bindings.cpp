@@ -325,7 +325,6 @@ PYBIND11_MODULE(_C, m) {
       .def("xfer_mode", &AsyncEngine::xfer_mode)
       .def("set_xfer_blocks", &AsyncEngine::set_xfer_blocks)
       .def("xfer_blocks_cap", &AsyncEngine::xfer_blocks_cap)
-      .def("set_xfer_local", &AsyncEngine::set_xfer_local)
       .def("error", &AsyncEngine::error)
       .def("inject_error", &AsyncEngine::inject_error)
       .def("counters", &AsyncEngine::counters)

@@ -59,12 +59,8 @@ import torch.nn as nn
 from .. import native
 from ..ops.optim import OptimConfig, OptimDyn
 from ..utils.config import fault
-from ..utils.config import feature as _feat
 from .collective_ps import ALIGN, _flat_view, _round, install_fp8_weights, zero_grads_, zero_plan
 
-# workgroups per segment of a local (own-shard) push / pull on the scatter / gather kernel: ~128 KiB
-# per workgroup up to this cap, so a 16 MB bucket is ~128 workgroups for ~10 us (feature xfer_local)
-XFER_LOCAL_BLOCKS = 256
 
 
 
@@ -313,8 +309,6 @@ class AsyncPS:
         self.xfer_fallback = None
         if self.is_cuda:
             self.engine.set_xfer(self.xfer != "copy")
-            # own-shard pushes / pulls on the scatter / gather kernel too (feature xfer_local)
-            self.engine.set_xfer_local(XFER_LOCAL_BLOCKS if (self.xfer != "copy" and _feat("xfer_local")) else 0)
         try:
             self.selftest("kernel" if self.is_cuda and self.xfer != "copy" else "copy")
         except RuntimeError as e:  # collective: every rank sees the same failure

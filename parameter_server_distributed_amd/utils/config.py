@@ -96,8 +96,6 @@ FEATURES: dict[str, tuple[bool, str]] = {
     "fp8_dgrad": (True, "fp8 e5m2-dY bwd-data of the fp8 convolutions"),
     "async_cached_local": (True, "async PS at world 1: inbox / publish buffers in plain (cached) device memory "
                                  "instead of uncached IPC memory (read by the native engine)"),
-    "xfer_local": (False, "async PS: own-shard pushes / pulls on the scatter / gather kernel (many workgroups, "
-                          "briefly) instead of HIP's device copy (a long-running blit kernel beside backward)"),
     "tail_fp8": (False, "fp8 models' identity blocks: conv3 + bn3 as the bf16 recomputing tail (bn3 folded "
                        "into conv3's bf16 backward, conv3's output never stored); read at model build. Off: same-box "
                        "WRN-101-2 4,136 vs 4,170 img/s (profiles/r6/ab_tail_fp8.md)"),
