@@ -117,10 +117,24 @@ def parse():
     ap.add_argument("--comm-probe", type=int, default=1,
                     help="N > 1 with RCCL: after the timed steps, measure all-reduce / reduce-scatter / all-gather "
                          "bus bandwidth vs bucket size over xGMI and report it (comm_probe in the JSON)")
+    ap.add_argument("--features", default="",
+                    help="kernel-path / engine feature overrides for this run, e.g. 'async_direct_pull=0,convn=1' "
+                         "(utils/config.py FEATURES; same syntax as PSD_FEATURES, which it replaces)")
     from parameter_server_distributed_amd.utils.config import apply_config
 
     apply_config(ap)
-    return ap.parse_args()
+    ap.add_argument("--step-log", action="store_true",
+                    help="diagnosis: print the host time of every timed step and of its begin / forward / backward "
+                         "/ finish phases (stderr)")
+    ap.add_argument("--prof-window", action="store_true",
+                    help="under rocprofv3 --selected-regions: trace / count only the timed steps (roctx pause at "
+                         "start-up, resume for the timed loop; utils/roctx.py)")
+    a = ap.parse_args()
+    if a.step_log:
+        os.environ["PSD_STEP_LOG"] = "1"
+    if a.features:  # before any kernel path or the native engine reads the registry
+        os.environ["PSD_FEATURES"] = a.features
+    return a
 
 
 def comm_probe(dev, world: int, sizes_mb=(1, 4, 16, 64, 256), iters: int = 5) -> dict:
@@ -187,6 +201,10 @@ def _autotune_source() -> dict:
 
 def main():
     a = parse()
+    if a.prof_window:
+        from parameter_server_distributed_amd.utils import roctx
+
+        roctx.pause()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -322,6 +340,8 @@ def main():
     barrier()
     step_log = os.environ.get("PSD_STEP_LOG", "0") == "1"  # host time of each step() call (diagnosis)
     ts = []
+    if a.prof_window:
+        roctx.resume()
     t0 = time.perf_counter()
     c0 = time.thread_time()  # this (launching) thread's CPU time: how close the step is to host-bound
     loss = None
@@ -332,6 +352,8 @@ def main():
     host_cpu_ms = (time.thread_time() - c0) / max(a.steps, 1) * 1e3
     torch.cuda.synchronize(dev)
     barrier()
+    if a.prof_window:
+        roctx.pause()
     el = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
@@ -342,8 +364,8 @@ def main():
         prev = t0
         print("step host ms: " + " ".join(f"{(t - p) * 1e3:.1f}" for p, t in zip([t0] + ts[:-1], ts)), file=sys.stderr)
         for ph in (getattr(tr, "host_phases", None) or [])[-a.steps:]:
-            print("host phases ms (begin forward backward finish): " + " ".join(f"{x * 1e3:.2f}" for x in ph),
-                  file=sys.stderr)
+            print("host phases ms (begin forward backward finish) + GPU drained before / after begin: " +
+                  " ".join(f"{x * 1e3:.2f}" for x in ph[:4]) + f" {ph[4]} {ph[5]}", file=sys.stderr)
     if mode == "async":
         ps.drain()  # outside the timed region: every push of the run applied before reporting
     samples = a.batch * n_workers * a.steps

@@ -238,7 +238,15 @@ AsyncEngine::AsyncEngine(int rank, int world, std::vector<int> owners, std::vect
     st.busy.assign(nbuf_, false);
   }
   if (device_ >= 0) {
-    ps_stream_ = c10::hip::getStreamFromPool(/*isHighPriority=*/true, (c10::DeviceIndex)device_).stream();
+    // With an SSP bound S >= 1 a round's apply has a whole worker step of slack (the pull that needs
+    // it comes one step later), so it runs in the background: a normal-priority stream and at most
+    // 2 workgroups per CU. A high-priority, 2048-workgroup apply took every CU slot for its ~0.85 ms
+    // and held back the compute stream's next kernels (BERT-base: ~0.9 ms per step boundary,
+    // profiles/r6/ab_apply_background.md). At S = 0 the apply is on the critical path: high priority,
+    // full grid.
+    const bool bg = S_ >= 1 && psd_feature_on("async_apply_background", true);
+    apply_cap_ = bg ? 512 : 0;
+    ps_stream_ = c10::hip::getStreamFromPool(/*isHighPriority=*/!bg, (c10::DeviceIndex)device_).stream();
     xfer_kernel_ = true;
   }
 }
@@ -640,7 +648,7 @@ void AsyncEngine::apply_into(ShardState& st, const std::vector<at::Tensor>& g_in
                st.s2.defined() ? c10::optional<at::Tensor>(st.s2) : c10::nullopt,
                bf16 ? c10::optional<at::Tensor>(st.publish[buf]) : c10::nullopt, st.dyn, st.hyper.kind,
                st.hyper.momentum, st.hyper.dampening, st.hyper.nesterov, st.hyper.weight_decay, st.hyper.beta1,
-               st.hyper.beta2, st.hyper.eps, false);
+               st.hyper.beta2, st.hyper.eps, false, apply_cap_);
   if (!bf16) st.publish[buf].copy_(st.master);
 }
 

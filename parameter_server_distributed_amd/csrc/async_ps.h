@@ -173,6 +173,7 @@ class AsyncEngine {
   bool fixed_ = false;
   bool xfer_kernel_ = false;  // set in the constructor: true on a GPU engine
   int xfer_cap_ = 48;         // set_xfer_blocks
+  int apply_cap_ = 0;         // fused-apply workgroups (0: the launcher's 2048); see the constructor
   double timeout_s_;
   double dead_after_s_ = 10.0;  // a peer's engine silent this long is presumed dead (PSD_ASYNC_DEAD_S)
   int esz_;

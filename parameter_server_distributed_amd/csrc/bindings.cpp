@@ -22,7 +22,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("fused_apply_", &fused_apply_, py::arg("master"), py::arg("grads"), py::arg("state1"), py::arg("state2"),
         py::arg("shadow"), py::arg("dyn"), py::arg("kind"), py::arg("momentum") = 0.0, py::arg("dampening") = 0.0,
         py::arg("nesterov") = false, py::arg("weight_decay") = 0.0, py::arg("beta1") = 0.9, py::arg("beta2") = 0.999,
-        py::arg("eps") = 1e-8, py::arg("maximize") = false);
+        py::arg("eps") = 1e-8, py::arg("maximize") = false,
+        py::arg("grid_cap") = 0);
   m.def(
       "async_hyper",
       [](int kind, int workers, double momentum, double beta1, double beta2, double weight_decay) {

@@ -65,7 +65,7 @@ struct SourceList {
 // shadow (bf16, optional) <- bf16(master[i]) in the same pass (the all-gather payload).
 hipError_t launch_fused_apply(const OptimHyper& hyper, const OptimDyn* dyn, float* master,
                               const SourceList& grads, float* state1, float* state2,
-                              uint16_t* shadow_bf16, int64_t n, hipStream_t stream);
+                              uint16_t* shadow_bf16, int64_t n, hipStream_t stream, int grid_cap = 0);
 
 // 1-thread kernel: dyn->step += 1; bias corrections for beta1/beta2.
 hipError_t launch_optim_advance(OptimDyn* dyn, float beta1, float beta2, hipStream_t stream);

@@ -128,9 +128,10 @@ __global__ void optim_advance_kernel(OptimDyn* dyn, float beta1, float beta2) {
 
 template <int KIND>
 static void dispatch_src(const OptimHyper& h, const OptimDyn* dyn, float* master, const SourceList& g,
-                         float* s1, float* s2, uint16_t* shadow, int64_t n, hipStream_t st) {
+                         float* s1, float* s2, uint16_t* shadow, int64_t n, hipStream_t st, int grid_cap) {
   const int block = 256;
-  const int grid = stream_grid((n >> 3) > 0 ? (n >> 3) : 1, block);
+  int grid = stream_grid((n >> 3) > 0 ? (n >> 3) : 1, block);
+  if (grid_cap > 0 && grid > grid_cap) grid = grid_cap;
   if (g.dtype == DT_BF16)
     hipLaunchKernelGGL((fused_apply_kernel<KIND, DT_BF16>), dim3(grid), dim3(block), 0, st, h, dyn, master, g,
                        s1, s2, shadow, n);
@@ -140,14 +141,14 @@ static void dispatch_src(const OptimHyper& h, const OptimDyn* dyn, float* master
 }
 
 hipError_t launch_fused_apply(const OptimHyper& h, const OptimDyn* dyn, float* master, const SourceList& g,
-                              float* s1, float* s2, uint16_t* shadow, int64_t n, hipStream_t st) {
+                              float* s1, float* s2, uint16_t* shadow, int64_t n, hipStream_t st, int grid_cap) {
   if (n <= 0) return hipSuccess;
   if (g.count < 1 || g.count > kMaxSources) return hipErrorInvalidValue;
   switch (h.kind) {
-    case OPT_SGD: dispatch_src<OPT_SGD>(h, dyn, master, g, s1, s2, shadow, n, st); break;
-    case OPT_MOMENTUM: dispatch_src<OPT_MOMENTUM>(h, dyn, master, g, s1, s2, shadow, n, st); break;
-    case OPT_ADAM: dispatch_src<OPT_ADAM>(h, dyn, master, g, s1, s2, shadow, n, st); break;
-    case OPT_ADAMW: dispatch_src<OPT_ADAMW>(h, dyn, master, g, s1, s2, shadow, n, st); break;
+    case OPT_SGD: dispatch_src<OPT_SGD>(h, dyn, master, g, s1, s2, shadow, n, st, grid_cap); break;
+    case OPT_MOMENTUM: dispatch_src<OPT_MOMENTUM>(h, dyn, master, g, s1, s2, shadow, n, st, grid_cap); break;
+    case OPT_ADAM: dispatch_src<OPT_ADAM>(h, dyn, master, g, s1, s2, shadow, n, st, grid_cap); break;
+    case OPT_ADAMW: dispatch_src<OPT_ADAMW>(h, dyn, master, g, s1, s2, shadow, n, st, grid_cap); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -111,7 +111,7 @@ SourceList make_sources(const std::vector<at::Tensor>& srcs, int64_t n, const at
 void fused_apply_(at::Tensor master, const std::vector<at::Tensor>& grads, c10::optional<at::Tensor> state1,
                   c10::optional<at::Tensor> state2, c10::optional<at::Tensor> shadow, at::Tensor dyn, int64_t kind,
                   double momentum, double dampening, bool nesterov, double weight_decay, double beta1, double beta2,
-                  double eps, bool maximize) {
+                  double eps, bool maximize, int64_t grid_cap) {
   TORCH_CHECK(master.scalar_type() == at::kFloat && master.is_contiguous(), "psd: master must be contiguous fp32");
   const int64_t n = master.numel();
   OptimHyper h{};
@@ -156,7 +156,8 @@ void fused_apply_(at::Tensor master, const std::vector<at::Tensor>& grads, c10::
     if (s2) check_aligned(*state2, "state2");
     if (sh) check_aligned(*shadow, "shadow");
     for (auto& t : grads) check_aligned(t, "grad");
-    hip_check(launch_fused_apply(h, dyn_ptr(dyn), master.data_ptr<float>(), src, s1, s2, sh, n, cur_stream(master)),
+    hip_check(launch_fused_apply(h, dyn_ptr(dyn), master.data_ptr<float>(), src, s1, s2, sh, n, cur_stream(master),
+                                 (int)grid_cap),
               "fused_apply");
     return;
   }

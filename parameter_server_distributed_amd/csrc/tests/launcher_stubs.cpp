@@ -6,7 +6,7 @@
 
 namespace psd {
 hipError_t launch_fused_apply(const OptimHyper&, const OptimDyn*, float*, const SourceList&, float*, float*, uint16_t*,
-                              int64_t, hipStream_t) {
+                              int64_t, hipStream_t, int) {
   return hipErrorNotSupported;
 }
 hipError_t launch_optim_advance(OptimDyn*, float, float, hipStream_t) { return hipErrorNotSupported; }

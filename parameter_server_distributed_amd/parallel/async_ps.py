@@ -58,7 +58,7 @@ import torch.nn as nn
 
 from .. import native
 from ..ops.optim import OptimConfig, OptimDyn
-from ..utils.config import fault
+from ..utils.config import fault, feature
 from .collective_ps import ALIGN, _flat_view, _round, install_fp8_weights, zero_grads_, zero_plan
 
 
@@ -178,7 +178,9 @@ class AsyncPS:
             _flat_view(init, o, p).copy_(p.detach().float())
         # working weights: with S >= 1 two buffers alternate per step, so the pull of step t+1 (DMA
         # from the owners' publish buffers) runs on a side stream while step t computes
-        self.prefetch = self.S >= 1
+        # (world 1: the pull is one local device copy, so pulling straight into the working weights at
+        # the step start costs less than the prefetch + working-buffer copy -- feature async_direct_pull)
+        self.prefetch = self.S >= 1 and not (self.world == 1 and feature("async_direct_pull"))
         self.pbufs = [init.to(param_dtype)]
         if self.prefetch:
             self.pbufs.append(self.pbufs[0].clone())

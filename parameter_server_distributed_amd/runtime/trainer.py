@@ -55,8 +55,15 @@ class Trainer:
         tr = self.tracer
         if tr is None and self.host_phases is not None:  # PSD_STEP_LOG=1: host time per phase (diagnosis)
             t0 = time.perf_counter()
+            # drained: the compute stream had already run out of queued work when the host got here
+            # (the GPU waits for the host at this step boundary)
+            drained = bool(self.ps.is_cuda and torch.cuda.current_stream(self.ps.device).query())
             self.ps.begin_step()
             t1 = time.perf_counter()
+            # ... or had finished the previous step's work by the time begin_step (its pull wait) let
+            # the host go on (the event was recorded after the previous step's last kernel)
+            ev = getattr(self, "_end_ev", None)
+            drained_after = bool(ev is not None and ev.query())
             out = self.model(self.x)
             loss = self.loss_fn(out, self.y)
             t2 = time.perf_counter()
@@ -64,7 +71,10 @@ class Trainer:
             t3 = time.perf_counter()
             self.ps.finish_step()
             t4 = time.perf_counter()
-            self.host_phases.append((t1 - t0, t2 - t1, t3 - t2, t4 - t3))
+            if self.ps.is_cuda:
+                self._end_ev = torch.cuda.Event()
+                self._end_ev.record(torch.cuda.current_stream(self.ps.device))
+            self.host_phases.append((t1 - t0, t2 - t1, t3 - t2, t4 - t3, drained, drained_after))
             return loss
         if tr is None:
             self.ps.begin_step()

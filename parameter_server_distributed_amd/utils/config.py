@@ -96,6 +96,12 @@ FEATURES: dict[str, tuple[bool, str]] = {
     "fp8_dgrad": (True, "fp8 e5m2-dY bwd-data of the fp8 convolutions"),
     "async_cached_local": (True, "async PS at world 1: inbox / publish buffers in plain (cached) device memory "
                                  "instead of uncached IPC memory (read by the native engine)"),
+    "async_apply_background": (True, "async PS with SSP bound >= 1: the owner's apply on a normal-priority stream "
+                                     "with at most 512 workgroups, beside the compute stream (read by the native "
+                                     "engine); off: high priority, full grid (the S = 0 setting)"),
+    "async_direct_pull": (True, "async PS at world 1: each step pulls straight into the model's working weights "
+                                "on the compute stream (one local copy) instead of prefetching into a second "
+                                "buffer and copying that into the working weights"),
     "tail_fp8": (False, "fp8 models' identity blocks: conv3 + bn3 as the bf16 recomputing tail (bn3 folded "
                        "into conv3's bf16 backward, conv3's output never stored); read at model build. Off: same-box "
                        "WRN-101-2 4,136 vs 4,170 img/s (profiles/r6/ab_tail_fp8.md)"),
