@@ -127,8 +127,8 @@ def parse():
                     help="diagnosis: print the host time of every timed step and of its begin / forward / backward "
                          "/ finish phases (stderr)")
     ap.add_argument("--prof-window", action="store_true",
-                    help="under rocprofv3 --selected-regions: trace / count only the timed steps (roctx pause at "
-                         "start-up, resume for the timed loop; utils/roctx.py)")
+                    help="under rocprofv3 --selected-regions: trace / count only the timed steps (roctx resume "
+                         "before the timed loop, pause after it; utils/roctx.py)")
     a = ap.parse_args()
     if a.step_log:
         os.environ["PSD_STEP_LOG"] = "1"
@@ -201,10 +201,8 @@ def _autotune_source() -> dict:
 
 def main():
     a = parse()
-    if a.prof_window:
+    if a.prof_window:  # (--selected-regions starts paused: a pause before the first resume aborts it)
         from parameter_server_distributed_amd.utils import roctx
-
-        roctx.pause()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -340,6 +338,17 @@ def main():
     barrier()
     step_log = os.environ.get("PSD_STEP_LOG", "0") == "1"  # host time of each step() call (diagnosis)
     ts = []
+    gc_log = []  # (generation, seconds) of every Python GC pass in the timed steps (step-log diagnosis)
+    if step_log:
+        import gc
+
+        def _gc_cb(phase, info, _t=[0.0]):
+            if phase == "start":
+                _t[0] = time.perf_counter()
+            else:
+                gc_log.append((info.get("generation"), time.perf_counter() - _t[0]))
+
+        gc.callbacks.append(_gc_cb)
     if a.prof_window:
         roctx.resume()
     t0 = time.perf_counter()
@@ -363,6 +372,13 @@ def main():
     if step_log and rank == 0:
         prev = t0
         print("step host ms: " + " ".join(f"{(t - p) * 1e3:.1f}" for p, t in zip([t0] + ts[:-1], ts)), file=sys.stderr)
+        bnd = [e0.elapsed_time(e1) for e0, e1 in getattr(tr, "boundary_evs", [])[-a.steps:] if e0 is not None]
+        if bnd:
+            print("GPU ms from each step's end to the next forward (begin_step on the compute stream): " +
+                  " ".join(f"{x:.3f}" for x in bnd), file=sys.stderr)
+        print(f"python gc in the timed steps: {len(gc_log)} passes, {sum(d for _, d in gc_log) * 1e3:.2f} ms, "
+              f"by generation {[sum(1 for g, _ in gc_log if g == k) for k in range(3)]}, "
+              f"longest {max((d for _, d in gc_log), default=0) * 1e3:.2f} ms", file=sys.stderr)
         for ph in (getattr(tr, "host_phases", None) or [])[-a.steps:]:
             print("host phases ms (begin forward backward finish) + GPU drained before / after begin: " +
                   " ".join(f"{x * 1e3:.2f}" for x in ph[:4]) + f" {ph[4]} {ph[5]}", file=sys.stderr)

@@ -241,9 +241,10 @@ AsyncEngine::AsyncEngine(int rank, int world, std::vector<int> owners, std::vect
     // With an SSP bound S >= 1 a round's apply has a whole worker step of slack (the pull that needs
     // it comes one step later), so it runs in the background: a normal-priority stream and at most
     // 2 workgroups per CU. A high-priority, 2048-workgroup apply took every CU slot for its ~0.85 ms
-    // and held back the compute stream's next kernels (BERT-base: ~0.9 ms per step boundary,
-    // profiles/r6/ab_apply_background.md). At S = 0 the apply is on the critical path: high priority,
-    // full grid.
+    // and held back the compute stream's next kernels (the gradient-zeroing fills waited up to
+    // 215 us for a slot in a BERT-base kernel trace; step time neutral within the box spread in
+    // plain runs, profiles/r6/boundary/README.md). At S = 0 the apply is on the critical path:
+    // high priority, full grid.
     const bool bg = S_ >= 1 && psd_feature_on("async_apply_background", true);
     apply_cap_ = bg ? 512 : 0;
     ps_stream_ = c10::hip::getStreamFromPool(/*isHighPriority=*/!bg, (c10::DeviceIndex)device_).stream();

@@ -41,6 +41,7 @@ class Trainer:
         self.checkpoint_every = int(checkpoint_every)
         # PSD_STEP_LOG=1: (begin, forward, backward, finish) host seconds of every eager step
         self.host_phases = [] if os.environ.get("PSD_STEP_LOG", "0") == "1" else None
+        self.boundary_evs = []  # (previous step's end, this step's forward start) events, with host_phases
         self._ckpt_thread = None
         if tracer is not None:
             self.use_graph = False  # per-phase timing needs eager steps
@@ -64,6 +65,9 @@ class Trainer:
             # the host go on (the event was recorded after the previous step's last kernel)
             ev = getattr(self, "_end_ev", None)
             drained_after = bool(ev is not None and ev.query())
+            if self.ps.is_cuda:  # GPU time of the step boundary: previous step's end -> this forward's start
+                self._fwd_ev = torch.cuda.Event(enable_timing=True)
+                self._fwd_ev.record(torch.cuda.current_stream(self.ps.device))
             out = self.model(self.x)
             loss = self.loss_fn(out, self.y)
             t2 = time.perf_counter()
@@ -72,8 +76,9 @@ class Trainer:
             self.ps.finish_step()
             t4 = time.perf_counter()
             if self.ps.is_cuda:
-                self._end_ev = torch.cuda.Event()
+                self._end_ev = torch.cuda.Event(enable_timing=True)
                 self._end_ev.record(torch.cuda.current_stream(self.ps.device))
+                self.boundary_evs.append((ev, self._fwd_ev))
             self.host_phases.append((t1 - t0, t2 - t1, t3 - t2, t4 - t3, drained, drained_after))
             return loss
         if tr is None:

@@ -1,7 +1,7 @@
 """rocprofv3 collection window from inside the program: ``roctxProfilerPause`` / ``Resume`` of the
 ROCm profiler SDK's roctx library, which ``rocprofv3 --selected-regions`` honours (only what runs
-between a resume and the next pause is traced). bench.py ``--prof-window`` pauses at start-up and
-resumes for the timed steps only, so a trace or counter pass holds the steps of interest and not
+between a resume and the next pause is traced; collection starts paused, and a pause before the
+first resume aborts the tool). bench.py ``--prof-window`` resumes for the timed steps only, so a trace or counter pass holds the steps of interest and not
 the start-up autotune (whose API calls alone overflow a 64 MiB result budget)."""
 from __future__ import annotations
 
