@@ -161,6 +161,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("ln_bwd", &ln_bwd, py::arg("dy"), py::arg("s"), py::arg("mean"), py::arg("rstd"), py::arg("gamma"), py::arg("p"),
         py::arg("seed"), py::arg("step") = py::none(), py::arg("dgamma_out") = py::none(),
         py::arg("dbeta_out") = py::none(), py::arg("dhsum_out") = py::none());
+  m.def("emb_ln_fwd", &emb_ln_fwd, py::arg("ids"), py::arg("types"), py::arg("W"), py::arg("P"), py::arg("T"),
+        py::arg("gamma"), py::arg("beta"), py::arg("S"), py::arg("eps"), py::arg("p"), py::arg("seed"),
+        py::arg("step") = py::none());
+  m.def("emb_ln_bwd", &emb_ln_bwd, py::arg("dy"), py::arg("ids"), py::arg("types"), py::arg("W"), py::arg("P"),
+        py::arg("T"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"), py::arg("S"), py::arg("p"), py::arg("seed"),
+        py::arg("step") = py::none(), py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none(),
+        py::arg("dT") = py::none());
   m.def("bn_pool_bwd", &bn_pool_bwd, py::arg("gpool"), py::arg("gpool2"), py::arg("arg"), py::arg("x"), py::arg("gamma"),
         py::arg("save_mean"), py::arg("save_invstd"), py::arg("ss"), py::arg("dgamma_out") = py::none(),
         py::arg("dbeta_out") = py::none());

@@ -253,7 +253,187 @@ __global__ __launch_bounds__(256) void ln_param_grad_kernel(const float* __restr
 #pragma unroll
   for (int r = 1; r < 8; ++r) s0 += red[r][cl];
   const int which = t / H, col = t - which * H;
-  (which == 0 ? dgamma : which == 1 ? dbeta : dhsum)[col] = f32_to_bf16(s0);
+  if (which == 0) dgamma[col] = f32_to_bf16(s0);
+  else if (which == 1) dbeta[col] = f32_to_bf16(s0);
+  else dhsum[(which - 2) * H + col] = f32_to_bf16(s0);  // the branch bias / the token-type rows
+}
+
+// ------------------------------------------------------------------ BERT embedding tail
+// y = dropout(LayerNorm(W[id] + P[r % S] + T[type])): PyTorch ran it as three gathers, two adds, a
+// layer_norm and a dropout forward (~0.22 ms of a BERT-base b256 step) and a dropout backward, the
+// layer_norm backward (three kernels), the position table's broadcast-sum backward and the token-type
+// one-hot GEMM backward (~0.26 ms; profiles/r6/bert_base_b256_r6d_kernels.md). Here one pass each way:
+// forward gathers the three rows of each token straight from the tables (one wave per token row, the
+// next row's gathers issued before this row's reductions) and writes y and the row statistics;
+// backward re-gathers the rows (nothing but the statistics is saved: the embedding sum is recomputed
+// exactly, in the same fp32 order), applies the dropout mask, runs the LN backward and writes the
+// gradient of the embedding sum (the word table's sorted deterministic scatter and the position
+// table's batch sum take it, ops/embedding.py) plus block partials of dgamma, dbeta and -- for the
+// usual <= 2 token types -- each type row's gradient, finalized by ln_param_grad_kernel.
+namespace {
+template <int E>
+struct EmbRows {
+  float w[E], p[E], t[E];
+  int ty;
+};
+
+template <int E>
+__device__ __forceinline__ void emb_fetch(const EmbLnArgs& a, int64_t r, int c0, EmbRows<E>& o) {
+  constexpr int H = 64 * E;
+  const int64_t id = a.ids[r];
+  const int64_t ty = a.types ? a.types[r] : 0;
+  const int64_t s = r % a.S;
+  o.ty = (ty >= 0 && ty < a.NT) ? (int)ty : -1;
+  if (id >= 0 && id < a.V) {
+    load_e<E>(a.W + id * H + c0, o.w);
+  } else {
+#pragma unroll
+    for (int i = 0; i < E; ++i) o.w[i] = 0.f;
+  }
+  load_e<E>(a.P + s * H + c0, o.p);
+  if (o.ty >= 0) {
+    load_e<E>(a.T + (int64_t)o.ty * H + c0, o.t);
+  } else {
+#pragma unroll
+    for (int i = 0; i < E; ++i) o.t[i] = 0.f;
+  }
+}
+}  // namespace
+
+template <int E>
+__global__ __launch_bounds__(256) void emb_ln_fwd_kernel(EmbLnArgs a, uint32_t thresh, float scale) {
+  constexpr int H = 64 * E;
+  const int lane = threadIdx.x & 63;
+  const int c0 = lane * E;
+  float g[E], b[E];
+  load_e<E>(a.gamma + c0, g);
+  load_e<E>(a.beta + c0, b);
+  const uint32_t key = dropout_key(a.seed, a.step);
+  const int64_t wstride = (int64_t)gridDim.x * (blockDim.x >> 6);
+  int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  EmbRows<E> nx;
+  if (r < a.rows) emb_fetch<E>(a, r, c0, nx);
+  for (; r < a.rows; r += wstride) {
+    const int64_t off = r * H + c0;
+    float xv[E];
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      xv[i] = (nx.w[i] + nx.p[i]) + nx.t[i];
+      sum += xv[i];
+    }
+    const int64_t rn = r + wstride;
+    if (rn < a.rows) emb_fetch<E>(a, rn, c0, nx);
+    const float mean = wave_sum(sum) * (1.f / H);
+    float sq = 0.f;
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      const float d = xv[i] - mean;
+      sq = fmaf(d, d, sq);
+    }
+    const float rstd = rsqrtf(wave_sum(sq) * (1.f / H) + a.eps);
+    bool kp[E];
+    if (thresh != 0u) keep_flags<E>(key, off, thresh, kp);
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      const float yv = fmaf((xv[i] - mean) * rstd, g[i], b[i]);
+      xv[i] = (thresh == 0u) ? yv : (kp[i] ? yv * scale : 0.f);
+    }
+    store_e<E>(a.y + off, xv);
+    if (lane == 0) {
+      a.mean[r] = mean;
+      a.rstd[r] = rstd;
+    }
+  }
+}
+
+template <int E, int NT>
+__global__ __launch_bounds__(256) void emb_ln_bwd_kernel(EmbLnArgs a, uint32_t thresh, float scale) {
+  constexpr int H = 64 * E;
+  constexpr int NPART = 2 + NT;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c0 = lane * E;
+  float g[E], pg[E], pb[E], pt[NT > 0 ? NT : 1][E];
+  load_e<E>(a.gamma + c0, g);
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    pg[i] = pb[i] = 0.f;
+#pragma unroll
+    for (int k = 0; k < (NT > 0 ? NT : 1); ++k) pt[k][i] = 0.f;
+  }
+  const uint32_t key = dropout_key(a.seed, a.step);
+  const int64_t wstride = (int64_t)gridDim.x * (blockDim.x >> 6);
+  int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+  EmbRows<E> nx;
+  float ndv[E], nmean = 0.f, nrstd = 0.f;
+  if (r < a.rows) {
+    emb_fetch<E>(a, r, c0, nx);
+    load_e<E>(a.dy + r * H + c0, ndv);
+    nmean = a.mean[r];
+    nrstd = a.rstd[r];
+  }
+  for (; r < a.rows; r += wstride) {
+    const int64_t off = r * H + c0;
+    float xh[E], dv[E];
+    const float mean = nmean, rstd = nrstd;
+    const int ty = nx.ty;
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      xh[i] = ((nx.w[i] + nx.p[i]) + nx.t[i] - mean) * rstd;  // the forward's sum, same order
+      dv[i] = ndv[i];
+    }
+    const int64_t rn = r + wstride;
+    if (rn < a.rows) {
+      emb_fetch<E>(a, rn, c0, nx);
+      load_e<E>(a.dy + rn * H + c0, ndv);
+      nmean = a.mean[rn];
+      nrstd = a.rstd[rn];
+    }
+    bool kp[E];
+    if (thresh != 0u) keep_flags<E>(key, off, thresh, kp);
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      if (thresh != 0u) dv[i] = kp[i] ? dv[i] * scale : 0.f;  // gradient at the LN output
+      pg[i] = fmaf(dv[i], xh[i], pg[i]);
+      pb[i] += dv[i];
+      dv[i] *= g[i];
+      s1 += dv[i];
+      s2 = fmaf(dv[i], xh[i], s2);
+    }
+    s1 = wave_sum(s1) * (1.f / H);
+    s2 = wave_sum(s2) * (1.f / H);
+#pragma unroll
+    for (int i = 0; i < E; ++i) dv[i] = rstd * (dv[i] - s1 - xh[i] * s2);
+    store_e<E>(a.dx + off, dv);
+    if constexpr (NT > 0) {
+#pragma unroll
+      for (int k = 0; k < NT; ++k)
+        if (ty == k) {
+#pragma unroll
+          for (int i = 0; i < E; ++i) pt[k][i] += dv[i];
+        }
+    }
+  }
+  __shared__ float red[4][NPART][H];
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    red[wv][0][c0 + i] = pg[i];
+    red[wv][1][c0 + i] = pb[i];
+#pragma unroll
+    for (int k = 0; k < NT; ++k) red[wv][2 + k][c0 + i] = pt[k][i];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < NPART * H; c += blockDim.x) {
+    const int which = c / H, col = c - which * H;
+    a.part[((int64_t)blockIdx.x * NPART + which) * H + col] =
+        (red[0][which][col] + red[1][which][col]) + (red[2][which][col] + red[3][which][col]);
+  }
+}
+
+int emb_ln_bwd_blocks(int64_t rows) {
+  const int64_t want = (rows + 4 * 8 - 1) / (4 * 8);
+  return (int)(want < 1 ? 1 : (want > 512 ? 512 : want));
 }
 
 int ln_bwd_blocks(int64_t rows) {
@@ -304,6 +484,34 @@ hipError_t launch_ln_bwd(const LnArgs& a, hipStream_t st) {
   const int np = hs ? 3 : 2;
   hipLaunchKernelGGL(ln_param_grad_kernel, dim3((np * a.H + 31) / 32), dim3(256), 0, st, a.part, blocks, a.H, np,
                      a.dgamma, a.dbeta, a.dhsum);
+  return hipGetLastError();
+}
+
+hipError_t launch_emb_ln_fwd(const EmbLnArgs& a, hipStream_t st) {
+  if (a.H != 768 || a.S <= 0 || a.NT < 0 || a.rows < 0) return hipErrorInvalidValue;
+  if (a.rows == 0) return hipSuccess;
+  const int64_t blocks64 = (a.rows + 3) / 4;
+  const int blocks = (int)(blocks64 > 2048 ? 2048 : blocks64);
+  const uint32_t th = keep_thresh(a.p);
+  const float sc = a.p > 0.f ? 1.f / (1.f - a.p) : 1.f;
+  hipLaunchKernelGGL(emb_ln_fwd_kernel<12>, dim3(blocks), dim3(256), 0, st, a, th, sc);
+  return hipGetLastError();
+}
+
+hipError_t launch_emb_ln_bwd(const EmbLnArgs& a, hipStream_t st) {
+  if (a.H != 768 || a.S <= 0 || a.NT < 0 || a.rows < 0) return hipErrorInvalidValue;
+  const int nt = a.dT ? a.NT : 0;  // type-row gradients fused for NT <= 2 only
+  if (nt > 2) return hipErrorInvalidValue;
+  if (a.rows == 0) return hipSuccess;
+  const int blocks = emb_ln_bwd_blocks(a.rows);
+  const uint32_t th = keep_thresh(a.p);
+  const float sc = a.p > 0.f ? 1.f / (1.f - a.p) : 1.f;
+  if (nt == 0) hipLaunchKernelGGL((emb_ln_bwd_kernel<12, 0>), dim3(blocks), dim3(256), 0, st, a, th, sc);
+  else if (nt == 1) hipLaunchKernelGGL((emb_ln_bwd_kernel<12, 1>), dim3(blocks), dim3(256), 0, st, a, th, sc);
+  else hipLaunchKernelGGL((emb_ln_bwd_kernel<12, 2>), dim3(blocks), dim3(256), 0, st, a, th, sc);
+  const int np = 2 + nt;
+  hipLaunchKernelGGL(ln_param_grad_kernel, dim3((np * a.H + 31) / 32), dim3(256), 0, st, a.part, blocks, a.H, np,
+                     a.dgamma, a.dbeta, a.dT);
   return hipGetLastError();
 }
 

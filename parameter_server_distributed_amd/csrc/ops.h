@@ -156,6 +156,16 @@ std::vector<at::Tensor> ln_bwd(const at::Tensor& dy, const at::Tensor& s, const 
                                const at::Tensor& gamma, double p, int64_t seed, c10::optional<at::Tensor> step,
                                c10::optional<at::Tensor> dgamma_out, c10::optional<at::Tensor> dbeta_out,
                                c10::optional<at::Tensor> dhsum_out);
+std::vector<at::Tensor> emb_ln_fwd(const at::Tensor& ids, const at::Tensor& types, const at::Tensor& W,
+                                   const at::Tensor& P, const at::Tensor& T, const at::Tensor& gamma,
+                                   const at::Tensor& beta, int64_t S, double eps, double p, int64_t seed,
+                                   c10::optional<at::Tensor> step);
+std::vector<at::Tensor> emb_ln_bwd(const at::Tensor& dy, const at::Tensor& ids, const at::Tensor& types,
+                                   const at::Tensor& W, const at::Tensor& P, const at::Tensor& T,
+                                   const at::Tensor& gamma, const at::Tensor& mean, const at::Tensor& rstd, int64_t S,
+                                   double p, int64_t seed, c10::optional<at::Tensor> step,
+                                   c10::optional<at::Tensor> dgamma_out, c10::optional<at::Tensor> dbeta_out,
+                                   c10::optional<at::Tensor> dT_out);
 std::vector<at::Tensor> bn_pool_bwd(const at::Tensor& gpool, c10::optional<at::Tensor> gpool2, const at::Tensor& arg,
                                     const at::Tensor& x, const at::Tensor& gamma, const at::Tensor& save_mean,
                                     const at::Tensor& save_invstd, const at::Tensor& ss,

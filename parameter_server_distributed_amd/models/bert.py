@@ -10,14 +10,12 @@ backward, which requires every weight to be consumed by exactly one autograd nod
 """
 from __future__ import annotations
 
-import math
 
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
 from ..ops.attention import FusedSelfAttention
-from ..ops.embedding import FusedEmbedding
+from ..ops.embedding import FusedBertEmbeddings
 from ..ops.layernorm import FusedAddLayerNorm, bump_step
 from ..ops.linear import MfmaLinear
 from ..ops.loss import cross_entropy
@@ -54,12 +52,9 @@ class BertForMLM(nn.Module):
     def __init__(self, layers=12, hidden=768, heads=12, vocab=VOCAB, max_pos=512, dropout=0.1):
         super().__init__()
         self.vocab = vocab
-        # deterministic gfx950 weight gradients (ops/embedding.py); the position table's gradient is
-        # first summed over the batch by autograd's broadcast, so it stays on nn.Embedding
-        self.word = FusedEmbedding(vocab, hidden)
-        self.pos = nn.Embedding(max_pos, hidden)
-        self.tok_type = FusedEmbedding(2, hidden)
-        self.ln = nn.LayerNorm(hidden, eps=1e-12)
+        # dropout(LayerNorm(word + position + token type)) on one fused kernel each way, with the
+        # word table's deterministic sorted-scatter gradient (ops/embedding.py)
+        self.emb = FusedBertEmbeddings(vocab, hidden, max_pos, 2, eps=1e-12, p=dropout, seed=4242)
         self.layers = nn.ModuleList([BertLayer(hidden, heads, 4 * hidden, dropout, i) for i in range(layers)])
         self.head = MfmaLinear(hidden, hidden, act="gelu")
         self.head_ln = nn.LayerNorm(hidden, eps=1e-12)
@@ -77,10 +72,7 @@ class BertForMLM(nn.Module):
     def forward(self, batch):
         ids, types, mlm_pos = batch
         bump_step(self)
-        S = ids.shape[1]
-        pos = torch.arange(S, device=ids.device)
-        x = self.word(ids) + self.pos(pos)[None] + self.tok_type(types)
-        x = F.dropout(self.ln(x), self.p, self.training)
+        x = self.emb(ids, types)
         for layer in self.layers:
             x = layer(x)
         # MLM head only on the masked positions (max_predictions_per_seq per sequence, as in the

@@ -96,14 +96,15 @@ class FusedAddLayerNorm(nn.LayerNorm):
 
 def bump_step(model: nn.Module) -> None:
     """Advance the model's dropout step counter (a non-persistent int64 buffer ``_psd_rng_step``,
-    moved with the model) and point every FusedAddLayerNorm / FusedSelfAttention at it. Called at the start of each
+    moved with the model) and point every FusedAddLayerNorm / FusedSelfAttention / FusedBertEmbeddings at it. Called at the start of each
     training forward; the increment runs on the device, so a captured hipGraph replays it."""
     step = getattr(model, "_psd_rng_step", None)
     if step is None or not model.training:
         return
     from .attention import FusedSelfAttention
+    from .embedding import FusedBertEmbeddings
 
     for m in model.modules():
-        if isinstance(m, (FusedAddLayerNorm, FusedSelfAttention)):
+        if isinstance(m, (FusedAddLayerNorm, FusedSelfAttention, FusedBertEmbeddings)):
             m.step = step
     step.add_(1)
