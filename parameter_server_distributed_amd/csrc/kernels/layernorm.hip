@@ -277,11 +277,25 @@ struct EmbRows {
   int ty;
 };
 
+// a row's ids, loaded one row ahead of its gathers (a gather right behind its own id load waits a
+// full memory round trip before it can issue)
+struct EmbIds {
+  int64_t id, ty;
+};
+__device__ __forceinline__ EmbIds emb_ids(const EmbLnArgs& a, int64_t r) {
+  EmbIds o{-1, -1};
+  if (r < a.rows) {
+    o.id = a.ids[r];
+    o.ty = a.types ? a.types[r] : 0;
+  }
+  return o;
+}
+
 template <int E>
-__device__ __forceinline__ void emb_fetch(const EmbLnArgs& a, int64_t r, int c0, EmbRows<E>& o) {
+__device__ __forceinline__ void emb_fetch(const EmbLnArgs& a, int64_t r, EmbIds ids, int c0, EmbRows<E>& o) {
   constexpr int H = 64 * E;
-  const int64_t id = a.ids[r];
-  const int64_t ty = a.types ? a.types[r] : 0;
+  const int64_t id = ids.id;
+  const int64_t ty = ids.ty;
   const int64_t s = r % a.S;
   o.ty = (ty >= 0 && ty < a.NT) ? (int)ty : -1;
   if (id >= 0 && id < a.V) {
@@ -312,7 +326,8 @@ __global__ __launch_bounds__(256) void emb_ln_fwd_kernel(EmbLnArgs a, uint32_t t
   const int64_t wstride = (int64_t)gridDim.x * (blockDim.x >> 6);
   int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   EmbRows<E> nx;
-  if (r < a.rows) emb_fetch<E>(a, r, c0, nx);
+  if (r < a.rows) emb_fetch<E>(a, r, emb_ids(a, r), c0, nx);
+  EmbIds nid = emb_ids(a, r + wstride);
   for (; r < a.rows; r += wstride) {
     const int64_t off = r * H + c0;
     float xv[E];
@@ -323,7 +338,10 @@ __global__ __launch_bounds__(256) void emb_ln_fwd_kernel(EmbLnArgs a, uint32_t t
       sum += xv[i];
     }
     const int64_t rn = r + wstride;
-    if (rn < a.rows) emb_fetch<E>(a, rn, c0, nx);
+    if (rn < a.rows) {
+      emb_fetch<E>(a, rn, nid, c0, nx);
+      nid = emb_ids(a, rn + wstride);
+    }
     const float mean = wave_sum(sum) * (1.f / H);
     float sq = 0.f;
 #pragma unroll
@@ -366,8 +384,9 @@ __global__ __launch_bounds__(256) void emb_ln_bwd_kernel(EmbLnArgs a, uint32_t t
   int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
   EmbRows<E> nx;
   float ndv[E], nmean = 0.f, nrstd = 0.f;
+  EmbIds nid = emb_ids(a, r + wstride);
   if (r < a.rows) {
-    emb_fetch<E>(a, r, c0, nx);
+    emb_fetch<E>(a, r, emb_ids(a, r), c0, nx);
     load_e<E>(a.dy + r * H + c0, ndv);
     nmean = a.mean[r];
     nrstd = a.rstd[r];
@@ -384,7 +403,8 @@ __global__ __launch_bounds__(256) void emb_ln_bwd_kernel(EmbLnArgs a, uint32_t t
     }
     const int64_t rn = r + wstride;
     if (rn < a.rows) {
-      emb_fetch<E>(a, rn, c0, nx);
+      emb_fetch<E>(a, rn, nid, c0, nx);
+      nid = emb_ids(a, rn + wstride);
       load_e<E>(a.dy + rn * H + c0, ndv);
       nmean = a.mean[rn];
       nrstd = a.rstd[rn];
@@ -490,8 +510,10 @@ hipError_t launch_ln_bwd(const LnArgs& a, hipStream_t st) {
 hipError_t launch_emb_ln_fwd(const EmbLnArgs& a, hipStream_t st) {
   if (a.H != 768 || a.S <= 0 || a.NT < 0 || a.rows < 0) return hipErrorInvalidValue;
   if (a.rows == 0) return hipSuccess;
+  // one row per wave up to 8192 workgroups: a gather waits on its id load, so the pass wants many
+  // rows in flight (at the LayerNorm kernels' 2048-workgroup cap it ran at ~1.6 TB/s)
   const int64_t blocks64 = (a.rows + 3) / 4;
-  const int blocks = (int)(blocks64 > 2048 ? 2048 : blocks64);
+  const int blocks = (int)(blocks64 > 8192 ? 8192 : blocks64);
   const uint32_t th = keep_thresh(a.p);
   const float sc = a.p > 0.f ? 1.f / (1.f - a.p) : 1.f;
   hipLaunchKernelGGL(emb_ln_fwd_kernel<12>, dim3(blocks), dim3(256), 0, st, a, th, sc);
