@@ -437,13 +437,22 @@ def test_dgrad_s2_in_resnet_block_matches_miopen(gpu, monkeypatch):
 
     monkeypatch.setenv("PSD_FEATURES", "tail_recompute=0")
     res = {}
-    for force in ("psdnbs0", "psdns0", "miopen"):
+    s2 = lambda k: k[:2] == ("conv", "dgrad") and k[8] == 2  # noqa: E731 (the stride-2 bwd-data key)
+    others = None
+    for force in ("miopen", "psdnbs0", "psdns0"):
         monkeypatch.setenv("PSD_AUTOTUNE_FORCE", force)
         autotune._DECISIONS.clear()
+        if others is not None:
+            # every other op of the block on the MIOpen run's picks: only the stride-2 bwd-data differs
+            # between the runs (per-run autotune picks elsewhere moved the near-cancelling BN weight
+            # gradients by up to ~9 % and made the comparison flaky)
+            autotune._DECISIONS.update(others)
         res[force] = run(copy.deepcopy(blk0), x0)
         picks = autotune.decisions()
-        got = [v for k, v in picks.items() if k[:2] == ("conv", "dgrad") and k[8] == 2]  # (stride 2)
+        got = [v for k, v in picks.items() if s2(k)]
         assert got == [force], picks
+        if others is None:
+            others = {k: v for k, v in picks.items() if not s2(k)}
     autotune._DECISIONS.clear()
     ref = run(copy.deepcopy(blk0).float(), x0.float())
 
