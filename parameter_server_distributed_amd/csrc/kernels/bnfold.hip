@@ -40,55 +40,68 @@ __global__ __launch_bounds__(256) void bnfold_prep_kernel(const uint16_t* __rest
 }
 
 // dW[c][i] = A_c P[c][i] + B_c sum_k W[c][k] G[k][i] + C_c s[i]  (G = P[Cout:Cout+Wd] = x^T x,
-// s = P[Cout+Wd] = 1^T x). The W G product is a small fp32 GEMM: 64 x 64 output tiles, k in chunks of
-// 32 staged through LDS (W transposed, so a thread's 4 rows are one float4), 4 x 4 outputs per lane
-// (16 FMAs per two LDS reads). The row-per-lane version streamed G once per 8 (later 32) output
-// rows from L2 and issued one LDS read per FMA: 67-111 us per call, 0.9-1.4 ms per ResNet-50 step
-// (profiles/resnet50_b1024_r4_kernels.md).
-constexpr int kCT = 64, kCK = 32;
+// s = P[Cout+Wd] = 1^T x). The W G product is a small fp32 GEMM on 32 x 32 output tiles, k in chunks
+// of 32 staged through LDS (W transposed: a thread's 2 rows are one float2), 2 x 2 outputs per lane.
+// The chunks are software-pipelined -- chunk k0 + 32's W and G loads are in registers before chunk
+// k0's FMAs run -- and the tiles are small enough for several workgroups per CU: the 64 x 64 tile
+// with a load -> sync -> compute chain per chunk ran 43 us per call on average, latency-bound (4 to
+// 256 workgroups per launch; 0.65 ms per ResNet-50 step, profiles/r6/resnet50_b1024_r6f_kernels.md).
+// The k order of every output's sum is unchanged (bitwise the same result).
+constexpr int kCT = 32, kCK = 32;
 __global__ __launch_bounds__(256) void bnfold_combine_kernel(const float* __restrict__ P, const uint16_t* __restrict__ W,
                                                              const float* __restrict__ coef, int Cout, int Wd,
                                                              uint16_t* __restrict__ out, int accumulate) {
-  __shared__ __attribute__((aligned(16))) float ws[kCK][kCT];  // W^T chunk: ws[k][r]
+  // W^T chunk ws[k][r], rows padded by 2 floats: the transposing stores (consecutive lanes =
+  // consecutive k) spread over the banks instead of all hitting one; float2 reads stay aligned
+  __shared__ __attribute__((aligned(16))) float ws[kCK][kCT + 2];
   __shared__ __attribute__((aligned(16))) float gs[kCK][kCT];  // G chunk: gs[k][i]
   const int r0 = blockIdx.x * kCT, i0 = blockIdx.y * kCT;
   const int tr = threadIdx.x >> 4, tc = threadIdx.x & 15;
   const float* G = P + (int64_t)Cout * Wd;
   const float* s = G + (int64_t)Wd * Wd;
-  float t[4][4];
+  constexpr int kPer = kCK * kCT / 256;  // elements of each operand a lane stages per chunk (4)
+  float wr[kPer], gr[kPer];
+  auto load = [&](int k0) {
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) t[a][b] = 0.f;
-  for (int k0 = 0; k0 < Wd; k0 += kCK) {
-    for (int e = threadIdx.x; e < kCK * kCT; e += 256) {
+    for (int q = 0; q < kPer; ++q) {
+      const int e = threadIdx.x + q * 256;
       const int r = e / kCK, k = e - r * kCK;  // consecutive lanes: consecutive k of one W row
-      ws[k][r] = (r0 + r < Cout && k0 + k < Wd) ? bf16_to_f32(W[(int64_t)(r0 + r) * Wd + k0 + k]) : 0.f;
+      wr[q] = (r0 + r < Cout && k0 + k < Wd) ? bf16_to_f32(W[(int64_t)(r0 + r) * Wd + k0 + k]) : 0.f;
+      const int kg = e / kCT, i = e - kg * kCT;
+      gr[q] = (k0 + kg < Wd && i0 + i < Wd) ? G[(int64_t)(k0 + kg) * Wd + i0 + i] : 0.f;
     }
-    for (int e = threadIdx.x; e < kCK * kCT; e += 256) {
-      const int k = e / kCT, i = e - k * kCT;
-      gs[k][i] = (k0 + k < Wd && i0 + i < Wd) ? G[(int64_t)(k0 + k) * Wd + i0 + i] : 0.f;
+  };
+  float t[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+  load(0);
+  for (int k0 = 0; k0 < Wd; k0 += kCK) {
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      const int e = threadIdx.x + q * 256;
+      const int r = e / kCK, k = e - r * kCK;
+      ws[k][r] = wr[q];
+      const int kg = e / kCT, i = e - kg * kCT;
+      gs[kg][i] = gr[q];
     }
     __syncthreads();
+    if (k0 + kCK < Wd) load(k0 + kCK);  // next chunk in flight during this chunk's FMAs
 #pragma unroll 8
     for (int k = 0; k < kCK; ++k) {
-      const float4 wa = *reinterpret_cast<const float4*>(&ws[k][tr * 4]);
-      const float4 gb = *reinterpret_cast<const float4*>(&gs[k][tc * 4]);
-      const float wv[4] = {wa.x, wa.y, wa.z, wa.w}, gv[4] = {gb.x, gb.y, gb.z, gb.w};
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) t[a][b] = fmaf(wv[a], gv[b], t[a][b]);
+      const float2 wa = *reinterpret_cast<const float2*>(&ws[k][tr * 2]);
+      const float2 gb = *reinterpret_cast<const float2*>(&gs[k][tc * 2]);
+      t[0][0] = fmaf(wa.x, gb.x, t[0][0]);
+      t[0][1] = fmaf(wa.x, gb.y, t[0][1]);
+      t[1][0] = fmaf(wa.y, gb.x, t[1][0]);
+      t[1][1] = fmaf(wa.y, gb.y, t[1][1]);
     }
     __syncthreads();
   }
 #pragma unroll
-  for (int a = 0; a < 4; ++a) {
-    const int c = r0 + tr * 4 + a;
+  for (int a = 0; a < 2; ++a) {
+    const int c = r0 + tr * 2 + a;
     if (c >= Cout) break;
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int i = i0 + tc * 4 + b;
+    for (int b = 0; b < 2; ++b) {
+      const int i = i0 + tc * 2 + b;
       if (i >= Wd) break;
       float v = coef[c] * P[(int64_t)c * Wd + i] + coef[Cout + c] * t[a][b] + coef[2 * Cout + c] * s[i];
       uint16_t* o = out + (int64_t)c * Wd + i;

@@ -57,7 +57,7 @@ def test_convw_fold_exact(gpu, cout, cin, variant):
     torch.testing.assert_close(P[cout + cin], x2.sum(0), rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("cout,cin", [(256, 64), (512, 128)])
+@pytest.mark.parametrize("cout,cin", [(256, 64), (512, 128), (1024, 256), (2048, 512), (96, 40)])
 def test_bnfold_weights_and_combine(gpu, cout, cin):
     """w2 = [(A o W)^T | W^T (B o W)], bvec = C^T W and dW = A o P1 + B o (W G) + C s vs fp32."""
     torch.manual_seed(1)
@@ -71,7 +71,7 @@ def test_bnfold_weights_and_combine(gpu, cout, cin):
     torch.testing.assert_close(w2[:, :cout].float().cpu(), ref_left, rtol=1e-2, atol=1e-3)
     torch.testing.assert_close(w2[:, cout:].float().cpu(), ref_m, rtol=2e-2, atol=2e-3)
     torch.testing.assert_close(bvec.cpu(), Cc @ Wf, rtol=1e-4, atol=1e-4)
-    rows = native().convw_fold_rows(cout, cin)
+    rows = native().convw_fold_rows(cout, cin) or cout + cin + 1  # (0: convw does not fold this shape)
     P = torch.randn(rows, cin)
     out = torch.zeros(cout, cin, device=gpu, dtype=torch.bfloat16)
     native().bnfold_combine(P.to(gpu), W.to(gpu), coef.to(gpu), out)
