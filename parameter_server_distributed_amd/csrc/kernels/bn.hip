@@ -102,8 +102,21 @@ __device__ __forceinline__ bool sum_partials(const float* __restrict__ part, int
   double a = 0.0, b = 0.0;
   if (c < C) {
     float fa[4] = {0.f, 0.f, 0.f, 0.f}, fb[4] = {0.f, 0.f, 0.f, 0.f};
-    int r = g, k = 0;
-    for (; r < nblk; r += 32, k = (k + 1) & 3) {  // 4 rotating fp32 accumulators, <= 64 rows each
+    int r = g;
+    for (; r + 96 < nblk; r += 128) {  // 4 fp32 accumulators, their 8 loads issued together
+      float va[4], vb[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        va[u] = part[(int64_t)(r + 32 * u) * 2 * C + c];
+        vb[u] = part[(int64_t)(r + 32 * u) * 2 * C + C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        fa[u] += va[u];
+        fb[u] += vb[u];
+      }
+    }
+    for (int k = 0; r < nblk; r += 32, k = (k + 1) & 3) {
       fa[k] += part[(int64_t)r * 2 * C + c];
       fb[k] += part[(int64_t)r * 2 * C + C + c];
     }
@@ -477,29 +490,40 @@ __global__ __launch_bounds__(256) void bn_fold_finalize_kernel(const float* __re
                                                                const float* __restrict__ r2) {
   const int C = BWD ? fb.C : ff.C;
   const int f = blockIdx.x, cg = blockIdx.y, F = gridDim.x;
-  const int col = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  const int c = cg * kFfCh + (col & 31);
-  const bool cok = c < C;
-  const int64_t coff = (int64_t)(col >> 5) * C + c;
+  // partial-row pass: 16 lanes x 16 bytes cover a row's 64 floats of this column group (32 sums,
+  // then 32 sums of squares: column col = 4 q4 + e), 16 row groups; 4 independent 16-byte loads in
+  // flight per lane (one float per lane per row left this fold at ~1 TB/s, 24 us per call)
+  const int q4 = threadIdx.x & 15, rg = threadIdx.x >> 4;
+  const int cq = cg * kFfCh + (q4 & 7) * 4;  // first of this lane's 4 channels (C % 8 == 0)
+  const bool qok = cq < C;
+  const int64_t qoff = (int64_t)(q4 >> 3) * C + cq;
   const int r0 = f * chunk, r1 = min(rows, r0 + chunk);
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-  if (cok) {
+  f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
+  if (qok) {
     int r = r0 + rg;
-    for (; r + 12 < r1; r += 16) {  // 4 independent loads in flight per lane
-      a0 += part[(int64_t)r * 2 * C + coff];
-      a1 += part[(int64_t)(r + 4) * 2 * C + coff];
-      a2 += part[(int64_t)(r + 8) * 2 * C + coff];
-      a3 += part[(int64_t)(r + 12) * 2 * C + coff];
+    for (; r + 48 < r1; r += 64) {
+      a0 += *reinterpret_cast<const f32x4*>(part + (int64_t)r * 2 * C + qoff);
+      a1 += *reinterpret_cast<const f32x4*>(part + (int64_t)(r + 16) * 2 * C + qoff);
+      a2 += *reinterpret_cast<const f32x4*>(part + (int64_t)(r + 32) * 2 * C + qoff);
+      a3 += *reinterpret_cast<const f32x4*>(part + (int64_t)(r + 48) * 2 * C + qoff);
     }
-    for (; r < r1; r += 4) a0 += part[(int64_t)r * 2 * C + coff];
+    for (; r < r1; r += 16) a0 += *reinterpret_cast<const f32x4*>(part + (int64_t)r * 2 * C + qoff);
   }
-  __shared__ float red[4][64];
+  __shared__ __attribute__((aligned(16))) float red[16][64];
   __shared__ double tot[4][64];
   __shared__ unsigned int ticket;
-  red[rg][col] = (a0 + a1) + (a2 + a3);
+  *reinterpret_cast<f32x4*>(&red[rg][q4 * 4]) = (a0 + a1) + (a2 + a3);
   __syncthreads();
+  const int col = threadIdx.x & 63, rq = threadIdx.x >> 6;
+  const int c = cg * kFfCh + (col & 31);
+  const bool cok = c < C;
   float* slab = ws + (int64_t)cg * kFfMaxF * 64;
-  if (rg == 0) slab[f * 64 + col] = ((red[0][col] + red[1][col]) + red[2][col]) + red[3][col];
+  if (rq == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][col];
+    slab[f * 64 + col] = t;
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -515,9 +539,19 @@ __global__ __launch_bounds__(256) void bn_fold_finalize_kernel(const float* __re
     __hip_atomic_store(&cnt[cg], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // reusable by the next launch
   }
   __syncthreads();
-  double t = 0.0;
-  for (int k = rg; k < F; k += 4) t += (double)slab[k * 64 + col];
-  tot[rg][col] = t;
+  // the reducing block: 8 independent slab loads in flight per lane (a one-load-per-iteration chain
+  // over the 256 slab rows was most of this kernel's ~20 us)
+  double t[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  int k = rq;
+  for (; k + 28 < F; k += 32) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = slab[(k + 4 * u) * 64 + col];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] += (double)v[u];
+  }
+  for (; k < F; k += 4) t[0] += (double)slab[k * 64 + col];
+  tot[rq][col] = ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
   __syncthreads();
   if (threadIdx.x < kFfCh && cok) {
     const int j = threadIdx.x;
@@ -558,8 +592,12 @@ template <bool BWD>
 static hipError_t fold_finalize(const float* part, int rows, float* ws, const FinFwd& ff, const FinBwd& fb,
                                 hipStream_t st, const FinBwd& fb2 = FinBwd{}, const float* r2 = nullptr) {
   const int C = BWD ? fb.C : ff.C;
+  if (C % 8 != 0 || (reinterpret_cast<uintptr_t>(part) & 15)) return hipErrorInvalidValue;  // 16-byte row loads
   const int ncg = (C + kFfCh - 1) / kFfCh;
-  int F = (rows + 63) / 64;  // >= 64 rows per block
+  // >= 256 rows per block: each block ends with an agent-scope release (its slab row must be visible
+  // to the reducing block on any XCD), and at one block per 64 rows those fences, not the loads, set
+  // the time (10-33 us per launch for 200-1600 blocks, profiles/r6/resnet50_b1024_r6i_kernels.md)
+  int F = (rows + 255) / 256;
   F = F < 1 ? 1 : (F > kFfMaxF ? kFfMaxF : F);
   const int chunk = (rows + F - 1) / F;
   F = (rows + chunk - 1) / chunk;
