@@ -129,9 +129,13 @@ def parse():
     ap.add_argument("--prof-window", action="store_true",
                     help="under rocprofv3 --selected-regions: trace / count only the timed steps (roctx resume "
                          "before the timed loop, pause after it; utils/roctx.py)")
+    ap.add_argument("--autotune-log", action="store_true",
+                    help="print every autotune decision with its candidates' timings (ops/autotune.py)")
     a = ap.parse_args()
     if a.step_log:
         os.environ["PSD_STEP_LOG"] = "1"
+    if a.autotune_log:
+        os.environ["PSD_AUTOTUNE_LOG"] = "1"
     if a.features:  # before any kernel path or the native engine reads the registry
         os.environ["PSD_FEATURES"] = a.features
     return a
