@@ -1616,6 +1616,74 @@ __global__ __launch_bounds__(256) void split_tree_kernel(const float* __restrict
   store8_f32(out + (int64_t)c * mn + v * 8, acc);
 }
 
+// 8 < splits <= 8 * GPV in ONE launch: a workgroup = VPB = 256 / GPV 8-element vectors x GPV split
+// groups; a lane sums its group's <= 8 slabs (independent loads, as a tree level), the groups'
+// partials meet in LDS and 8 lanes per vector (one element each) sum them in a fixed group order
+// (deterministic) and apply scale / accumulate / the output type. The tree of G = 8 levels plus the
+// final pass took 2-3 launches of ~6-8 us each per weight gradient (~150 launches, ~1.2 ms per
+// ResNet-50 step, profiles/r6/resnet50_b1024_r6j_kernels.md) for mostly small outputs.
+template <bool OUT_BF16, int GPV>
+__global__ __launch_bounds__(256) void split_reduce_lds_kernel(const float* __restrict__ slab, int splits, int64_t mn,
+                                                               void* __restrict__ out, int accumulate, float scale) {
+  constexpr int VPB = 256 / GPV;
+  __shared__ float part[GPV][VPB * 8];
+  const int v = threadIdx.x % VPB, gi = threadIdx.x / VPB;
+  const int64_t nvec = mn >> 3;
+  const int64_t vec = (int64_t)blockIdx.x * VPB + v;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (vec < nvec) {
+    const int s0 = gi * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (s0 + k < splits) {
+        float t[8];
+        load8_f32(slab + (int64_t)(s0 + k) * mn + vec * 8, t);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += t[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) part[gi][v * 8 + e] = acc[e];
+  __syncthreads();
+  for (int q = threadIdx.x; q < VPB * 8; q += 256) {  // (VPB * 8 > 256 lanes for GPV < 8)
+    const int vv = q >> 3, e = q & 7;
+    const int64_t ov = (int64_t)blockIdx.x * VPB + vv;
+    if (ov >= nvec) break;
+    float sum = 0.f;
+#pragma unroll 8
+    for (int g = 0; g < GPV; ++g) sum += part[g][vv * 8 + e];
+    sum *= scale;
+    const int64_t i = ov * 8 + e;
+    if (OUT_BF16) {
+      uint16_t* o = reinterpret_cast<uint16_t*>(out);
+      if (accumulate) sum += bf16_to_f32(o[i]);
+      o[i] = f32_to_bf16(sum);
+    } else {
+      float* o = reinterpret_cast<float*>(out);
+      if (accumulate) sum += o[i];
+      o[i] = sum;
+    }
+  }
+}
+
+template <bool OUT_BF16>
+static void launch_split_reduce_lds(const float* slab, int splits, int64_t mn, void* out, int accumulate, float scale,
+                                    hipStream_t st) {
+  const int groups = (splits + 7) / 8;  // 2 .. 64
+  const int64_t nvec = mn >> 3;
+#define PSD_SRL(G)                                                                                               \
+  hipLaunchKernelGGL((split_reduce_lds_kernel<OUT_BF16, G>), dim3((unsigned)((nvec + 256 / G - 1) / (256 / G))), \
+                     dim3(256), 0, st, slab, splits, mn, out, accumulate, scale)
+  if (groups <= 2) PSD_SRL(2);
+  else if (groups <= 4) PSD_SRL(4);
+  else if (groups <= 8) PSD_SRL(8);
+  else if (groups <= 16) PSD_SRL(16);
+  else if (groups <= 32) PSD_SRL(32);
+  else PSD_SRL(64);
+#undef PSD_SRL
+}
+
 int64_t splitk_tree_floats(int splits, int64_t mn) { return ((int64_t)(splits + 7) / 8 + 1) * mn; }
 
 // out (bf16 or fp32, [mn]) = (accumulate ? out : 0) + scale * sum over `splits` fp32 slabs of mn
@@ -1628,7 +1696,7 @@ hipError_t launch_splitk_reduce(float* slab, int splits, int64_t mn, void* out, 
   if (tree && mn % 8 == 0) {
     float* src = slab;
     float* dst = tree;
-    while (splits > 8) {
+    while (splits > 512) {  // tree levels only above what one LDS-reduce launch takes
       const int chunks = (splits + 7) / 8;
       const dim3 grid((unsigned)(((mn >> 3) + 255) / 256), (unsigned)chunks);
       hipLaunchKernelGGL(split_tree_kernel<8>, grid, dim3(256), 0, st, src, splits, mn, dst);
@@ -1638,6 +1706,11 @@ hipError_t launch_splitk_reduce(float* slab, int splits, int64_t mn, void* out, 
       dst = t;
     }
     slab = src;
+  }
+  if (mn % 8 == 0 && splits > 8 && splits <= 512) {
+    if (out_bf16) launch_split_reduce_lds<true>(slab, splits, mn, out, accumulate, scale, st);
+    else launch_split_reduce_lds<false>(slab, splits, mn, out, accumulate, scale, st);
+    return hipGetLastError();
   }
   const int grid = stream_grid((mn >> 3) > 0 ? (mn >> 3) : 1, 256);
   if (out_bf16)

@@ -122,15 +122,18 @@ class _Registry:
         for key, e in self.entries.items():
             if e.device != dev:
                 continue
-            if e.mod() is None or e.weight() is None:
+            # strong references for the rest of the refresh: a weak reference can die between two
+            # dereferences when a collection runs in between (a freed model's entries)
+            m, w = e.mod(), e.weight()
+            if m is None or w is None:
                 dead = True
                 continue
-            live.append((key, e))
+            live.append((key, e, w))
         if dead:
             self.entries = {k: e for k, e in self.entries.items() if e.mod() is not None and e.weight() is not None}
             self.tables.pop(dev, None)
         cache = self.tables.setdefault(dev, {})
-        sig = tuple(e.weight().data_ptr() for _, e in live)
+        sig = tuple(w.data_ptr() for _, _, w in live)
         tab = cache.get(sig)
         if tab is None:
             if torch.cuda.is_current_stream_capturing():
@@ -138,8 +141,7 @@ class _Registry:
             if len(cache) >= 4:
                 cache.clear()
             srcs, dsts, geo = [], [], []
-            for _, e in live:
-                w = e.weight()
+            for _, e, w in live:
                 for d, g in zip(e.dsts, e.geo):
                     srcs.append(w)
                     dsts.append(d)
