@@ -752,15 +752,8 @@ std::vector<at::Tensor> bnfold_dgrad_weights(const at::Tensor& w_in, const at::T
                                     (int)Cin, reinterpret_cast<uint16_t*>(w2.data_ptr()), (int)(Cout + Cin),
                                     reinterpret_cast<uint16_t*>(bw.data_ptr()), bvec.data_ptr<float>(), stream_of(w));
   TORCH_CHECK(e == hipSuccess, "psd bnfold prep: ", hipGetErrorString(e));
-  // M = (B o W)^T W (Cin x Cin, symmetric) into the right block of w2
-  if (Cin % 8 == 0) {
-    e = launch_bnfold_wgram(reinterpret_cast<const uint16_t*>(bw.data_ptr()), reinterpret_cast<const uint16_t*>(w.data_ptr()),
-                            (int)Cout, (int)Cin, reinterpret_cast<uint16_t*>(w2.data_ptr()) + Cout, (int)(Cout + Cin),
-                            stream_of(w));
-    TORCH_CHECK(e == hipSuccess, "psd bnfold wgram: ", hipGetErrorString(e));
-  } else {  // (the MFMA GEMM, TN layout)
-    gemm_(bw, w, false, false, w2.narrow(1, Cout, Cin), c10::nullopt, 0, c10::nullopt, c10::nullopt, c10::nullopt);
-  }
+  // M = (B o W)^T W (Cin x Cin, symmetric) into the right block of w2 (the MFMA GEMM, TN layout)
+  gemm_(bw, w, false, false, w2.narrow(1, Cout, Cin), c10::nullopt, 0, c10::nullopt, c10::nullopt, c10::nullopt);
   return {w2, bvec};
 }
 

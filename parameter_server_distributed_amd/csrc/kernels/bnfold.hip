@@ -111,52 +111,6 @@ __global__ __launch_bounds__(256) void bnfold_combine_kernel(const float* __rest
   }
 }
 
-// out[i][j] = sum_c A[c][i] B[c][j] (Wd x Wd, K = Cout up to 2048): 32 x 32 output tiles, the K range
-// split over the 4 waves of a workgroup (each lane a 4 x 4 block of the tile over its quarter of c,
-// two 8-byte loads per c, 8 c in flight), the quarters summed through LDS in a fixed order. The
-// generic GEMM ran this on 1-4 workgroups walking all of K (17-24 us per call, 11 calls per ResNet-50
-// step, profiles/r6/resnet50_b1024_r6m_kernels.md).
-__global__ __launch_bounds__(256) void bnfold_wgram_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
-                                                           int K, int Wd, uint16_t* __restrict__ out, int ldo) {
-  __shared__ float red[4][32][33];
-  const int i0 = blockIdx.x * 32, j0 = blockIdx.y * 32;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int ti = (lane >> 3) * 4, tj = (lane & 7) * 4;  // this lane's 4 x 4 block of the tile
-  const int kq = (K + 3) / 4, c0 = wv * kq, c1 = min(K, c0 + kq);
-  const bool iok = i0 + ti < Wd, jok = j0 + tj < Wd;  // (Wd % 8 == 0: a 4-block is whole or out)
-  float t[4][4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) t[a][b] = 0.f;
-  if (iok && jok) {
-#pragma unroll 8
-    for (int c = c0; c < c1; ++c) {
-      const uint2 av = *reinterpret_cast<const uint2*>(A + (int64_t)c * Wd + i0 + ti);
-      const uint2 bv = *reinterpret_cast<const uint2*>(B + (int64_t)c * Wd + j0 + tj);
-      const float a4[4] = {__uint_as_float(av.x << 16), __uint_as_float(av.x & 0xffff0000u),
-                           __uint_as_float(av.y << 16), __uint_as_float(av.y & 0xffff0000u)};
-      const float b4[4] = {__uint_as_float(bv.x << 16), __uint_as_float(bv.x & 0xffff0000u),
-                           __uint_as_float(bv.y << 16), __uint_as_float(bv.y & 0xffff0000u)};
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) t[a][b] = fmaf(a4[a], b4[b], t[a][b]);
-    }
-  }
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) red[wv][ti + a][tj + b] = t[a][b];
-  __syncthreads();
-  for (int q = threadIdx.x; q < 32 * 32; q += 256) {
-    const int r = q >> 5, cc = q & 31;
-    if (i0 + r >= Wd || j0 + cc >= Wd) continue;
-    const float v = (red[0][r][cc] + red[1][r][cc]) + (red[2][r][cc] + red[3][r][cc]);
-    out[(int64_t)(i0 + r) * ldo + j0 + cc] = f32_to_bf16(v);
-  }
-}
-
 // sum_m g[m][c] y[m][c] for y = x W^T that was never stored (ops/tail.py): with P[:Cout] = g^T x
 // from the fold wgrad, sum_m g y = sum_i W[c][i] P[c][i]. One wave per output channel, the row's
 // bf16 weights and fp32 P entries in 8-wide lane chunks; writes the partial row (0, that sum) that
@@ -300,14 +254,6 @@ hipError_t launch_bnfold_prep(const uint16_t* W, const float* coef, int Cout, in
                               uint16_t* bw, float* bvec, hipStream_t st) {
   if (Cout <= 0 || Wd <= 0 || ldw < Cout) return hipErrorInvalidValue;
   hipLaunchKernelGGL(bnfold_prep_kernel, dim3(Wd), dim3(256), 0, st, W, coef, Cout, Wd, w2, ldw, bw, bvec);
-  return hipGetLastError();
-}
-
-hipError_t launch_bnfold_wgram(const uint16_t* A, const uint16_t* B, int K, int Wd, uint16_t* out, int ldo,
-                               hipStream_t st) {
-  if (K <= 0 || Wd <= 0 || Wd % 8 != 0 || ldo < Wd) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(bnfold_wgram_kernel, dim3((Wd + 31) / 32, (Wd + 31) / 32), dim3(256), 0, st, A, B, K, Wd, out,
-                     ldo);
   return hipGetLastError();
 }
 

@@ -132,10 +132,6 @@ hipError_t launch_bnfold_dual_weights(const uint16_t* W3, const uint16_t* Wd, co
 hipError_t launch_bnfold_rowdot(const float* P, const uint16_t* W, int Cout, int Wd, float* row, hipStream_t st);
 hipError_t launch_bnfold_prep(const uint16_t* W, const float* coef, int Cout, int Wd, uint16_t* w2, int ldw,
                               uint16_t* bw, float* bvec, hipStream_t stream);
-// out[i][j] (bf16, row stride ldo) = sum_c A[c][i] B[c][j] for A, B bf16 [K][Wd] (the fold's symmetric
-// (B o W)^T W block of w2), fp32 accumulation
-hipError_t launch_bnfold_wgram(const uint16_t* A, const uint16_t* B, int K, int Wd, uint16_t* out, int ldo,
-                               hipStream_t st);
 hipError_t launch_bnfold_combine(const float* P, const uint16_t* W, const float* coef, int Cout, int Wd,
                                  uint16_t* out, int accumulate, hipStream_t stream);
 
