@@ -1076,10 +1076,13 @@ class _ConvFn(torch.autograd.Function):
         dx = dw = None
         to = ctx.strided_to
         if (ctx.needs_input_grad[0] and to is not None and k == 1 and stride == 2 and pad == 0 and h % 2 == 0
-                and w % 2 == 0 and _feat("convn_bwd5") and not ctx.fp8):
+                and w % 2 == 0 and _feat("convn_bwd5")):
             # downsample conv whose input gradient goes to the producing BN (the block's _Fork): dY . W
             # on the quarter grid only, handed over as a StridedDr (the consumer convolution's bwd-data
-            # adds it at even pixels, kernels/convn.hip mode 5); autograd gets a zero-stride marker
+            # adds it at even pixels, kernels/convn.hip mode 5, or the BN's own backward materialises
+            # it -- ops/bn.py take_dr -- where the consumer is an fp8 convolution); autograd gets a
+            # zero-stride marker. (fp8 downsample convolutions too: their bf16 bwd-data went to MIOpen's
+            # zero-fill + implicit GEMM, 3 launches / 0.6 ms per Wide-ResNet-101-2 step)
             dx = _strided_dgrad(ctx.mod, dy, weight, to, h, w)
         if ctx.needs_input_grad[0] and dx is None:
             def miopen():

@@ -249,3 +249,33 @@ def test_fp8_tail_on_vs_off_against_fp32(gpu, monkeypatch):
           f"gradient rel-L2 vs fp32: tail {e_on:.4f} fp8-conv3 {e_off:.4f}")
     assert abs(runs[True][0] - l32) <= abs(runs[False][0] - l32) + 0.01 * abs(l32)
     assert e_on <= 1.1 * e_off + 0.02, (e_on, e_off)
+
+
+@pytest.mark.gpu
+def test_fp8_downsample_quarter_grid_dgrad_matches_miopen(gpu, monkeypatch):
+    """The fp8 Wide-ResNet's stride-2 downsample convolutions hand their bwd-data over on the quarter
+    grid (ops/conv.py _strided_dgrad: dY . W on our GEMM / narrow kernels, added by the consumer or
+    materialised by the BN backward) instead of MIOpen's zero-filled full-size bwd-data: same weights,
+    same batch, every parameter gradient against the MIOpen path (feature convn_bwd5 off)."""
+    from parameter_server_distributed_amd.models import prepare
+    from parameter_server_distributed_amd.models.resnet import ResNet
+
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(32, 3, 64, 64, generator=g).to(gpu, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 100, (32,), generator=g).to(gpu)
+    grads = {}
+    for on in (True, False):
+        monkeypatch.setenv("PSD_FEATURES", f"convn_bwd5={int(on)}")
+        torch.manual_seed(0)
+        m = prepare(ResNet((2, 2, 2, 2), num_classes=100, width_per_group=128, fp8=True), gpu, torch.bfloat16,
+                    channels_last=True)
+        for p in m.parameters():
+            p.data = p.data.to(torch.bfloat16)
+        m.train()
+        F.cross_entropy(m(x).float(), y).backward()
+        grads[on] = [p.grad.float().clone() for p in m.parameters()]
+    num = sum(float((a - b).pow(2).sum()) for a, b in zip(grads[True], grads[False]))
+    den = sum(float(b.pow(2).sum()) for b in grads[False])
+    rel = (num / den) ** 0.5
+    print(f"fp8 downsample quarter-grid bwd-data vs MIOpen: gradient rel-L2 {rel:.5f}")
+    assert rel < 0.02, rel
