@@ -237,17 +237,20 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const float* __res
 // reduction) -- the consumer's own quantise pass (a full read of y) never runs. (The per-tensor
 // delayed-scaling form, Q8 == 1, measured no faster than the consumer quantising and was removed in
 // round 6.)
-template <bool RELU, bool RES, bool MASK_OUT, bool RSS = false, int Q8 = 0>
+// NT / span: streaming loads and stores, one-shot item ranges (common.h elem_range; host
+// elem_launch)
+template <bool RELU, bool RES, bool MASK_OUT, bool RSS = false, int Q8 = 0, bool NT = false>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
                                                        const float* __restrict__ ss, uint16_t* __restrict__ y,
                                                        uint8_t* __restrict__ mbits, int pack4, int64_t nvec, int C,
                                                        const float* __restrict__ rss = nullptr,
                                                        uint8_t* __restrict__ q8 = nullptr,
-                                                       uint8_t* __restrict__ q8mx = nullptr) {
+                                                       uint8_t* __restrict__ q8mx = nullptr, int span = 0) {
   static_assert(Q8 == 0 || Q8 == 2, "bn apply: fp8 side output is MX only");
   const int tpc = C >> 3;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;  // host guarantees stride % tpc == 0
-  int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const ElemRange er = elem_range(nvec, span);
+  const int64_t stride = er.stride, hi = er.hi;
+  int64_t v = er.v;
   const int cg = (int)(v % tpc);
   float sc[8], sh[8], rsc[8], rsh[8];
   load8_f32(ss + cg * 8, sc);
@@ -267,7 +270,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
       if (RELU) o = relu_nan(o);
       t[j] = o;
     }
-    store8_bf16(y + v * 8, t);
+    store8_bf16<NT>(y + v * 8, t);
     if (Q8 == 2) {  // MX: the stored (bf16-rounded) values, block scale from the lane quad
       float r[8];
 #pragma unroll
@@ -294,21 +297,21 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
       }
     }
   };
-  for (; v + stride < nvec; v += 2 * stride) {  // (lane quads stay together: nvec, stride % 4 == 0)
+  for (; v + stride < hi; v += 2 * stride) {  // (lane quads stay together: nvec, stride, span % 4 == 0)
     float t0[8], t1[8], r0[8], r1[8];
-    load8_bf16(x + v * 8, t0);
-    load8_bf16(x + (v + stride) * 8, t1);
+    load8_bf16<NT>(x + v * 8, t0);
+    load8_bf16<NT>(x + (v + stride) * 8, t1);
     if (RES) {
-      load8_bf16(res + v * 8, r0);
-      load8_bf16(res + (v + stride) * 8, r1);
+      load8_bf16<NT>(res + v * 8, r0);
+      load8_bf16<NT>(res + (v + stride) * 8, r1);
     }
     apply(v, t0, r0);
     apply(v + stride, t1, r1);
   }
-  for (; v < nvec; v += stride) {
+  for (; v < hi; v += stride) {
     float t[8], rr[8];
-    load8_bf16(x + v * 8, t);
-    if (RES) load8_bf16(res + v * 8, rr);
+    load8_bf16<NT>(x + v * 8, t);
+    if (RES) load8_bf16<NT>(res + v * 8, rr);
     apply(v, t, rr);
   }
 }
@@ -612,16 +615,17 @@ static hipError_t fold_finalize(const float* part, int rows, float* ws, const Fi
 // MODE 3: dy' = dy * (x*scale + shift > 0) (mask recomputed, kMaskX)
 // DQ: also write dx as MX e5m2 (one E8M0 byte per 32 channels) for the producing fp8 convolution's
 // bwd-data, whose own quantise pass (a full read of dx) then never runs (ops/bn.py _dq8_args)
-template <int MODE, bool DQ = false>
+template <int MODE, bool DQ = false, bool NT = false>
 __global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(const uint16_t* __restrict__ g, const uint16_t* __restrict__ g2,
                                                            const uint16_t* __restrict__ y, const float* __restrict__ ssf,
                                                            const uint16_t* __restrict__ x, const float* __restrict__ coef,
                                                            uint16_t* __restrict__ dx, int64_t nvec, int C,
                                                            uint8_t* __restrict__ dq = nullptr,
-                                                           uint8_t* __restrict__ dqmx = nullptr) {
+                                                           uint8_t* __restrict__ dqmx = nullptr, int span = 0) {
   const int tpc = C >> 3;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const ElemRange er = elem_range(nvec, span);
+  const int64_t stride = er.stride, hi = er.hi;
+  int64_t v = er.v;
   const int cg = (int)(v % tpc);
   float A[8], B[8], Cc[8], sc[8], sh[8];
   load8_f32(coef + cg * 8, A);
@@ -646,7 +650,7 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(const uint16_t* __res
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) gv[j] = fmaf(A[j], gv[j], fmaf(B[j], xv[j], Cc[j]));
-    store8_bf16(dx + v * 8, gv);
+    store8_bf16<NT>(dx + v * 8, gv);
     if constexpr (DQ) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) gv[j] = bf16_to_f32(f32_to_bf16(gv[j]));  // the stored values
@@ -657,29 +661,29 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(const uint16_t* __res
     }
   };
   // two items in flight per lane (all loads of both before either is used)
-  for (; v + stride < nvec; v += 2 * stride) {
+  for (; v + stride < hi; v += 2 * stride) {
     float g0[8], g1[8], x0[8], x1[8], h0[8], h1[8], y0[8], y1[8];
-    load8_bf16(g + v * 8, g0);
-    load8_bf16(g + (v + stride) * 8, g1);
-    load8_bf16(x + v * 8, x0);
-    load8_bf16(x + (v + stride) * 8, x1);
+    load8_bf16<NT>(g + v * 8, g0);
+    load8_bf16<NT>(g + (v + stride) * 8, g1);
+    load8_bf16<NT>(x + v * 8, x0);
+    load8_bf16<NT>(x + (v + stride) * 8, x1);
     if (MODE != 2 && g2) {
-      load8_bf16(g2 + v * 8, h0);
-      load8_bf16(g2 + (v + stride) * 8, h1);
+      load8_bf16<NT>(g2 + v * 8, h0);
+      load8_bf16<NT>(g2 + (v + stride) * 8, h1);
     }
     if (MODE == 1) {
-      load8_bf16(y + v * 8, y0);
-      load8_bf16(y + (v + stride) * 8, y1);
+      load8_bf16<NT>(y + v * 8, y0);
+      load8_bf16<NT>(y + (v + stride) * 8, y1);
     }
     elemt(v, g0, x0, h0, y0);
     elemt(v + stride, g1, x1, h1, y1);
   }
-  for (; v < nvec; v += stride) {
+  for (; v < hi; v += stride) {
     float gv[8], xv[8], h[8], yv[8];
-    load8_bf16(g + v * 8, gv);
-    load8_bf16(x + v * 8, xv);
-    if (MODE != 2 && g2) load8_bf16(g2 + v * 8, h);
-    if (MODE == 1) load8_bf16(y + v * 8, yv);
+    load8_bf16<NT>(g + v * 8, gv);
+    load8_bf16<NT>(x + v * 8, xv);
+    if (MODE != 2 && g2) load8_bf16<NT>(g2 + v * 8, h);
+    if (MODE == 1) load8_bf16<NT>(y + v * 8, yv);
     elemt(v, gv, xv, h, yv);
   }
 }
@@ -687,15 +691,17 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(const uint16_t* __res
 // dual elementwise pass: dx = A g + B x + C and dxd = Ad g + Bd xd + Cd from one read of g (= dr)
 // WDX false (the BN-backward fold of this BN's consumer convolution, ops/bn.py): only the downsample
 // BN's input gradient is written; this BN's own is folded into its producer's backward GEMMs
-template <bool WDX>
+template <bool WDX, bool NT = false>
 __global__ __launch_bounds__(256) void bn_bwd_elemt_dual_kernel(const uint16_t* __restrict__ g, const uint16_t* __restrict__ x,
                                                                 const float* __restrict__ coef, uint16_t* __restrict__ dx,
                                                                 const uint16_t* __restrict__ xd,
                                                                 const float* __restrict__ coef_d,
-                                                                uint16_t* __restrict__ dxd, int64_t nvec, int C) {
+                                                                uint16_t* __restrict__ dxd, int64_t nvec, int C,
+                                                                int span = 0) {
   const int tpc = C >> 3;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const ElemRange er = elem_range(nvec, span);
+  const int64_t stride = er.stride, hi = er.hi;
+  int64_t v = er.v;
   const int cg = (int)(v % tpc);
   float A[8], B[8], Cc[8], Ad[8], Bd[8], Cd[8];
   load8_f32(coef + cg * 8, A);
@@ -709,30 +715,30 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_dual_kernel(const uint16_t* 
     if constexpr (WDX) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = fmaf(A[j], gv[j], fmaf(B[j], xv[j], Cc[j]));
-      store8_bf16(dx + v * 8, o);
+      store8_bf16<NT>(dx + v * 8, o);
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = fmaf(Ad[j], gv[j], fmaf(Bd[j], dv[j], Cd[j]));
-    store8_bf16(dxd + v * 8, o);
+    store8_bf16<NT>(dxd + v * 8, o);
   };
-  for (; v + stride < nvec; v += 2 * stride) {  // two items in flight per lane
+  for (; v + stride < hi; v += 2 * stride) {  // two items in flight per lane
     float g0[8], g1[8], d0[8], d1[8], x0[8], x1[8];
-    load8_bf16(g + v * 8, g0);
-    load8_bf16(g + (v + stride) * 8, g1);
-    load8_bf16(xd + v * 8, d0);
-    load8_bf16(xd + (v + stride) * 8, d1);
+    load8_bf16<NT>(g + v * 8, g0);
+    load8_bf16<NT>(g + (v + stride) * 8, g1);
+    load8_bf16<NT>(xd + v * 8, d0);
+    load8_bf16<NT>(xd + (v + stride) * 8, d1);
     if constexpr (WDX) {
-      load8_bf16(x + v * 8, x0);
-      load8_bf16(x + (v + stride) * 8, x1);
+      load8_bf16<NT>(x + v * 8, x0);
+      load8_bf16<NT>(x + (v + stride) * 8, x1);
     }
     dual(v, g0, d0, x0);
     dual(v + stride, g1, d1, x1);
   }
-  for (; v < nvec; v += stride) {
+  for (; v < hi; v += stride) {
     float gv[8], dv[8], xv[8];
-    load8_bf16(g + v * 8, gv);
-    load8_bf16(xd + v * 8, dv);
-    if constexpr (WDX) load8_bf16(x + v * 8, xv);
+    load8_bf16<NT>(g + v * 8, gv);
+    load8_bf16<NT>(xd + v * 8, dv);
+    if constexpr (WDX) load8_bf16<NT>(x + v * 8, xv);
     dual(v, gv, dv, xv);
   }
 }
@@ -904,6 +910,55 @@ static int elem_grid(int64_t nvec, int C) {
   return g;
 }
 
+// Launch shape of the per-channel elementwise passes (apply, backward elementwise, dual): one-shot
+// 512-item blocks when C/8 divides 256 (common.h elem_range), else the grid-stride loop; streaming
+// loads / stores for tensors above 128 MB, which cannot stay in the 256 MB Infinity Cache for their
+// consumer anyway (below that the cached form measured faster: profiles/r6/elemt_variants.md).
+struct ElemLaunch {
+  int grid, span;
+  bool nt;
+};
+static ElemLaunch elem_launch(int64_t nvec, int C) {
+  const int tpc = C >> 3;
+  const bool nt = nvec * 16 > (128LL << 20);
+  if (tpc > 0 && 256 % tpc == 0) return {(int)((nvec + 511) / 512), 512, nt};
+  return {elem_grid(nvec, C), 0, nt};
+}
+
+template <bool R, bool S, bool B, bool RS, int Q8>
+static void apply_launch(const BnFwdArgs& a, const ElemLaunch& el, int64_t nvec, hipStream_t st) {
+  const int pack4 = (int)(nvec % 4 == 0);
+  if (el.nt)
+    hipLaunchKernelGGL((bn_apply_kernel<R, S, B, RS, Q8, true>), dim3(el.grid), dim3(256), 0, st, a.x, a.res, a.ss,
+                       a.y, a.mbits, pack4, nvec, a.C, a.res_ss, a.q8, a.q8mx, el.span);
+  else
+    hipLaunchKernelGGL((bn_apply_kernel<R, S, B, RS, Q8, false>), dim3(el.grid), dim3(256), 0, st, a.x, a.res, a.ss,
+                       a.y, a.mbits, pack4, nvec, a.C, a.res_ss, a.q8, a.q8mx, el.span);
+}
+
+template <int MODE, bool DQ>
+static void elemt_launch(const ElemLaunch& el, const uint16_t* g, const uint16_t* g2, const uint16_t* y,
+                         const float* ssf, const uint16_t* x, const float* coef, uint16_t* dx, int64_t nvec, int C,
+                         uint8_t* dq, uint8_t* dqmx, hipStream_t st) {
+  if (el.nt)
+    hipLaunchKernelGGL((bn_bwd_elemt_kernel<MODE, DQ, true>), dim3(el.grid), dim3(256), 0, st, g, g2, y, ssf, x, coef,
+                       dx, nvec, C, dq, dqmx, el.span);
+  else
+    hipLaunchKernelGGL((bn_bwd_elemt_kernel<MODE, DQ, false>), dim3(el.grid), dim3(256), 0, st, g, g2, y, ssf, x, coef,
+                       dx, nvec, C, dq, dqmx, el.span);
+}
+
+template <bool WDX>
+static void dual_launch(const ElemLaunch& el, const uint16_t* g, const uint16_t* x, const float* coef, uint16_t* dx,
+                        const uint16_t* xd, const float* coef_d, uint16_t* dxd, int64_t nvec, int C, hipStream_t st) {
+  if (el.nt)
+    hipLaunchKernelGGL((bn_bwd_elemt_dual_kernel<WDX, true>), dim3(el.grid), dim3(256), 0, st, g, x, coef, dx, xd,
+                       coef_d, dxd, nvec, C, el.span);
+  else
+    hipLaunchKernelGGL((bn_bwd_elemt_dual_kernel<WDX, false>), dim3(el.grid), dim3(256), 0, st, g, x, coef, dx, xd,
+                       coef_d, dxd, nvec, C, el.span);
+}
+
 hipError_t launch_bn_fwd(const BnFwdArgs& a, hipStream_t st) {
   if (a.M <= 0) return hipSuccess;
   if (a.C % 8 != 0) return hipErrorInvalidValue;
@@ -938,40 +993,28 @@ hipError_t launch_bn_fwd(const BnFwdArgs& a, hipStream_t st) {
     return hipGetLastError();
   }
   const int64_t nvec = a.M * (a.C / 8);
-  const int g = elem_grid(nvec, a.C);
-#define PSD_APPLY(R, S, B) \
-  hipLaunchKernelGGL((bn_apply_kernel<R, S, B>), dim3(g), dim3(256), 0, st, a.x, a.res, a.ss, a.y, a.mbits, \
-                     (int)(nvec % 4 == 0), nvec, a.C, nullptr)
+  const ElemLaunch el = elem_launch(nvec, a.C);
   if (a.q8 && a.q8mx) {  // MX fp8 side output (every lane quad = one 32-channel block)
     if (!a.relu || a.C % 32 != 0 || nvec % 4 != 0) return hipErrorInvalidValue;
-#define PSD_APM(S, B, RS)                                                                                      \
-  hipLaunchKernelGGL((bn_apply_kernel<true, S, B, RS, 2>), dim3(g), dim3(256), 0, st, a.x, a.res, a.ss, a.y,    \
-                     a.mbits, 1, nvec, a.C, a.res_ss, a.q8, a.q8mx)
-    if (a.res_ss && a.res && a.mbits) PSD_APM(true, true, true);
-    else if (a.res && a.mbits && !a.res_ss) PSD_APM(true, true, false);
-    else if (!a.res && !a.mbits && !a.res_ss) PSD_APM(false, false, false);
+    if (a.res_ss && a.res && a.mbits) apply_launch<true, true, true, true, 2>(a, el, nvec, st);
+    else if (a.res && a.mbits && !a.res_ss) apply_launch<true, true, true, false, 2>(a, el, nvec, st);
+    else if (!a.res && !a.mbits && !a.res_ss) apply_launch<true, false, false, false, 2>(a, el, nvec, st);
     else return hipErrorInvalidValue;
-#undef PSD_APM
     return hipGetLastError();
   }
   if (a.q8) return hipErrorInvalidValue;  // the fp8 side output needs its MX scales
   if (a.res_ss) {  // residual = bn(res) applied on the fly (ReLU blocks only)
     if (!a.res || !a.relu) return hipErrorInvalidValue;
-    if (a.mbits)
-      hipLaunchKernelGGL((bn_apply_kernel<true, true, true, true>), dim3(g), dim3(256), 0, st, a.x, a.res, a.ss, a.y,
-                         a.mbits, (int)(nvec % 4 == 0), nvec, a.C, a.res_ss);
-    else
-      hipLaunchKernelGGL((bn_apply_kernel<true, true, false, true>), dim3(g), dim3(256), 0, st, a.x, a.res, a.ss, a.y,
-                         a.mbits, (int)(nvec % 4 == 0), nvec, a.C, a.res_ss);
+    if (a.mbits) apply_launch<true, true, true, true, 0>(a, el, nvec, st);
+    else apply_launch<true, true, false, true, 0>(a, el, nvec, st);
     return hipGetLastError();
   }
-  if (a.relu && a.res && a.mbits) PSD_APPLY(true, true, true);
-  else if (a.relu && a.mbits) PSD_APPLY(true, false, true);
-  else if (a.relu && a.res) PSD_APPLY(true, true, false);
-  else if (a.relu) PSD_APPLY(true, false, false);
-  else if (a.res) PSD_APPLY(false, true, false);
-  else PSD_APPLY(false, false, false);
-#undef PSD_APPLY
+  if (a.relu && a.res && a.mbits) apply_launch<true, true, true, false, 0>(a, el, nvec, st);
+  else if (a.relu && a.mbits) apply_launch<true, false, true, false, 0>(a, el, nvec, st);
+  else if (a.relu && a.res) apply_launch<true, true, false, false, 0>(a, el, nvec, st);
+  else if (a.relu) apply_launch<true, false, false, false, 0>(a, el, nvec, st);
+  else if (a.res) apply_launch<false, true, false, false, 0>(a, el, nvec, st);
+  else apply_launch<false, false, false, false, 0>(a, el, nvec, st);
   return hipGetLastError();
 }
 
@@ -1037,11 +1080,10 @@ hipError_t launch_bn_bwd_pre(const uint16_t* g, const uint16_t* x, const uint16_
   const int64_t nvec = M * (C / 8);
   if (dq) {
     if (!dqmx || C % 32 != 0) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((bn_bwd_elemt_kernel<2, true>), dim3(elem_grid(nvec, C)), dim3(256), 0, st, g, nullptr, nullptr,
-                       nullptr, x, coef, dx, nvec, C, dq, dqmx);
+    elemt_launch<2, true>(elem_launch(nvec, C), g, nullptr, nullptr, nullptr, x, coef, dx, nvec, C, dq, dqmx, st);
   } else {
-    hipLaunchKernelGGL(bn_bwd_elemt_kernel<2>, dim3(elem_grid(nvec, C)), dim3(256), 0, st, g, nullptr, nullptr, nullptr,
-                       x, coef, dx, nvec, C);
+    elemt_launch<2, false>(elem_launch(nvec, C), g, nullptr, nullptr, nullptr, x, coef, dx, nvec, C, nullptr, nullptr,
+                           st);
   }
   return hipGetLastError();
 }
@@ -1053,8 +1095,7 @@ hipError_t launch_bn_elemt_coef(const uint16_t* g, const uint16_t* x, const floa
   if (M <= 0) return hipSuccess;
   if (C % 8 != 0) return hipErrorInvalidValue;
   const int64_t nvec = M * (C / 8);
-  hipLaunchKernelGGL(bn_bwd_elemt_kernel<2>, dim3(elem_grid(nvec, C)), dim3(256), 0, st, g, nullptr, nullptr, nullptr, x,
-                     coef, dx, nvec, C);
+  elemt_launch<2, false>(elem_launch(nvec, C), g, nullptr, nullptr, nullptr, x, coef, dx, nvec, C, nullptr, nullptr, st);
   return hipGetLastError();
 }
 
@@ -1082,12 +1123,8 @@ hipError_t launch_bn_bwd_dual_pre(const BnDualPreArgs& a, hipStream_t st) {
   if (!a.dx && !a.dxd) return hipSuccess;  // both BN input gradients folded into their convolutions
   if (!a.dxd) return hipErrorInvalidValue;
   const int64_t nvec = a.M * (a.C / 8);
-  if (a.dx)
-    hipLaunchKernelGGL(bn_bwd_elemt_dual_kernel<true>, dim3(elem_grid(nvec, a.C)), dim3(256), 0, st, a.g, a.x, a.coef,
-                       a.dx, a.xd, a.coef_d, a.dxd, nvec, a.C);
-  else
-    hipLaunchKernelGGL(bn_bwd_elemt_dual_kernel<false>, dim3(elem_grid(nvec, a.C)), dim3(256), 0, st, a.g, a.x,
-                       a.coef, a.dx, a.xd, a.coef_d, a.dxd, nvec, a.C);
+  if (a.dx) dual_launch<true>(elem_launch(nvec, a.C), a.g, a.x, a.coef, a.dx, a.xd, a.coef_d, a.dxd, nvec, a.C, st);
+  else dual_launch<false>(elem_launch(nvec, a.C), a.g, a.x, a.coef, a.dx, a.xd, a.coef_d, a.dxd, nvec, a.C, st);
   return hipGetLastError();
 }
 
@@ -1112,12 +1149,8 @@ hipError_t launch_bn_bwd(const BnBwdArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, fg, dim3(256), 0, st, a.part_d, gx,
                        FinBwd{a.M, a.C, a.gamma_d, a.mean_d, a.invstd_d, a.dgamma_d, a.dbeta_d, a.coef_d});
     const int64_t nvec = a.M * (a.C / 8);
-    if (a.dx)
-      hipLaunchKernelGGL(bn_bwd_elemt_dual_kernel<true>, dim3(elem_grid(nvec, a.C)), dim3(256), 0, st, a.dr, a.x, a.coef,
-                         a.dx, a.xd, a.coef_d, a.dxd, nvec, a.C);
-    else
-      hipLaunchKernelGGL(bn_bwd_elemt_dual_kernel<false>, dim3(elem_grid(nvec, a.C)), dim3(256), 0, st, a.dr, a.x,
-                         a.coef, a.dx, a.xd, a.coef_d, a.dxd, nvec, a.C);
+    if (a.dx) dual_launch<true>(elem_launch(nvec, a.C), a.dr, a.x, a.coef, a.dx, a.xd, a.coef_d, a.dxd, nvec, a.C, st);
+    else dual_launch<false>(elem_launch(nvec, a.C), a.dr, a.x, a.coef, a.dx, a.xd, a.coef_d, a.dxd, nvec, a.C, st);
     return hipGetLastError();
   }
 #define PSD_RED(K, O)                                                                                              \
@@ -1138,14 +1171,10 @@ hipError_t launch_bn_bwd(const BnBwdArgs& a, hipStream_t st) {
                      FinBwd{a.M, a.C, a.gamma, a.save_mean, a.save_invstd, a.dgamma, a.dbeta, a.coef});
   if (a.coef_only) return hipGetLastError();  // coefficients for the consumer's BN-backward fold
   const int64_t nvec = a.M * (a.C / 8);
-  const int g = elem_grid(nvec, a.C);
-#define PSD_EL(MODE, G, G2)                                                                                         \
-  if (a.dq)                                                                                                       \
-    hipLaunchKernelGGL((bn_bwd_elemt_kernel<MODE, true>), dim3(g), dim3(256), 0, st, G, G2, a.y, a.ss, a.x, a.coef, \
-                       a.dx, nvec, a.C, a.dq, a.dqmx);                                                              \
-  else                                                                                                            \
-    hipLaunchKernelGGL((bn_bwd_elemt_kernel<MODE>), dim3(g), dim3(256), 0, st, G, G2, a.y, a.ss, a.x, a.coef, a.dx, \
-                       nvec, a.C)
+  const ElemLaunch el = elem_launch(nvec, a.C);
+#define PSD_EL(MODE, G, G2)                                                                          \
+  if (a.dq) elemt_launch<MODE, true>(el, G, G2, a.y, a.ss, a.x, a.coef, a.dx, nvec, a.C, a.dq, a.dqmx, st); \
+  else elemt_launch<MODE, false>(el, G, G2, a.y, a.ss, a.x, a.coef, a.dx, nvec, a.C, nullptr, nullptr, st)
   if (a.dr) PSD_EL(2, a.dr, nullptr);
   else if (mask == kMaskY) PSD_EL(1, a.dy, a.dy2);
   else if (mask == kMaskX) PSD_EL(3, a.dy, a.dy2);

@@ -40,8 +40,14 @@ __device__ __forceinline__ void store8_f32(float* p, const float v[8]) {
   *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
   *reinterpret_cast<f32x4*>(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
 }
+// NT: nontemporal (streaming) load / store, for passes over tensors far larger than the 256 MB
+// Infinity Cache whose bytes are touched once (the BN elementwise passes: +35-45 % bandwidth on
+// 200-800 MB tensors, profiles/r6/elemt_variants.md)
+template <bool NT = false>
 __device__ __forceinline__ void load8_bf16(const uint16_t* p, float v[8]) {
-  u32x4 w = *reinterpret_cast<const u32x4*>(p);
+  u32x4 w;
+  if constexpr (NT) w = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  else w = *reinterpret_cast<const u32x4*>(p);
   uint32_t ws[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -49,11 +55,32 @@ __device__ __forceinline__ void load8_bf16(const uint16_t* p, float v[8]) {
     v[2 * i + 1] = __uint_as_float(ws[i] & 0xffff0000u);
   }
 }
+template <bool NT = false>
 __device__ __forceinline__ void store8_bf16(uint16_t* p, const float v[8]) {
   uint32_t ws[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) ws[i] = pack_bf16x2_rne(v[2 * i], v[2 * i + 1]);
-  *reinterpret_cast<u32x4*>(p) = u32x4{ws[0], ws[1], ws[2], ws[3]};
+  const u32x4 w{ws[0], ws[1], ws[2], ws[3]};
+  if constexpr (NT) __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));
+  else *reinterpret_cast<u32x4*>(p) = w;
+}
+
+// Item range of one lane in a per-channel elementwise pass over nvec 8-channel vectors (tpc = C/8
+// vectors per pixel). span > 0, one-shot: block b owns items [b*span, (b+1)*span) and its lanes step
+// by 256 (host: tpc | 256, so every item of a lane has channel group t % tpc). span == 0,
+// grid-stride: items b*256 + t + k*gridDim*256 (host: that stride % tpc == 0). One-shot grids of
+// 512-item blocks beat the 2048-block grid-stride loop by 30-45 % on large tensors
+// (profiles/r6/elemt_variants.md).
+struct ElemRange {
+  int64_t v, stride, hi;
+};
+__device__ __forceinline__ ElemRange elem_range(int64_t nvec, int span) {
+  if (span > 0) {
+    const int64_t lo = (int64_t)blockIdx.x * span;
+    const int64_t end = lo + span;
+    return {lo + threadIdx.x, (int64_t)blockDim.x, end < nvec ? end : nvec};
+  }
+  return {(int64_t)blockIdx.x * blockDim.x + threadIdx.x, (int64_t)gridDim.x * blockDim.x, nvec};
 }
 
 // Division by a run-time-invariant divisor d >= 1 for 0 <= x < 2^31 (Granlund-Montgomery

@@ -385,3 +385,45 @@ def test_downsample_bn_applied_inside_bn3_matches_unfused(gpu):
         e_f = ((f[n] - r[n]).norm() / r[n].norm().clamp_min(1e-6)).item()
         e_u = ((u[n] - r[n]).norm() / r[n].norm().clamp_min(1e-6)).item()
         assert e_f <= 1.5 * e_u + 1e-2, (n, e_f, e_u)
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(64, 128, 128, 128), (64, 24, 256, 256)], ids=lambda s: "x".join(map(str, s)))
+def test_fused_bn_streaming_launch_on_large_tensors(gpu, shape):
+    """Tensors above 128 MB take the streaming (nontemporal) one-shot elementwise launch (C/8 | 256)
+    or the streaming grid-stride one (C = 24): forward with residual + ReLU (bit-mask), backward,
+    and the coefficient-only elementwise pass, against fp32 on the GPU."""
+    from parameter_server_distributed_amd import native
+
+    torch.manual_seed(0)
+    N, C, H, W = shape
+    x = (torch.randn(shape, device=gpu) * 2 + 0.5).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    r = torch.randn(shape, device=gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(shape, device=gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    assert x.numel() * 2 > 128 << 20
+    m = FusedBatchNorm2d(C, relu=True).to(gpu)
+    with torch.no_grad():
+        m.weight.copy_(torch.rand(C) + 0.5)
+        m.bias.copy_(torch.randn(C) * 0.1)
+    m.weight.data = m.weight.data.to(torch.bfloat16)
+    m.bias.data = m.bias.data.to(torch.bfloat16)
+    xd, rd = x.clone().requires_grad_(True), r.clone().requires_grad_(True)
+    y = m(xd, rd)
+    y.backward(gy)
+
+    xr, rr = x.float().requires_grad_(True), r.float().requires_grad_(True)
+    wr = m.weight.detach().float().requires_grad_(True)
+    br = m.bias.detach().float().requires_grad_(True)
+    yr = F.relu(F.batch_norm(xr, None, None, wr, br, True, 0.1, 1e-5) + rr)
+    yr.backward(gy.float())
+    for name, a, b in (("y", y, yr), ("dx", xd.grad, xr.grad), ("dres", rd.grad, rr.grad)):
+        rel = ((a.float() - b).norm() / b.norm()).item()
+        assert rel < 1e-2, (name, rel)
+    del y, yr, xd, rd, xr, rr
+
+    g2 = gy.reshape(-1, C) if gy.is_contiguous() else gy.permute(0, 2, 3, 1).reshape(-1, C)
+    x2 = x.permute(0, 2, 3, 1).reshape(-1, C)
+    coef = torch.randn(3 * C, device=gpu)
+    got = native().bn_elemt_coef(g2, x2, coef)
+    want = coef[:C] * g2.float() + coef[C:2 * C] * x2.float() + coef[2 * C:]
+    rel = ((got.float() - want).norm() / want.norm()).item()
+    assert rel < 5e-3, rel
