@@ -856,13 +856,13 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_pool_kernel(const uint16_t* 
       const int h = 2 * k + (pq >> 1), w = 2 * j + (pq & 1);
       const int64_t off = (((int64_t)n * H + h) * W + w) * C + c8 * 8;
       float xv[8];
-      load8_bf16(x + off, xv);
+      load8_bf16<true>(x + off, xv);  // x and dx: touched once, streaming (1.6 GB at b1024)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float gm = fmaf(xv[e], sc[e], sh[e]) > 0.f ? g[pq][e] : 0.f;
         g[pq][e] = fmaf(A[e], gm, fmaf(B[e], xv[e], Cc[e]));
       }
-      store8_bf16(dx + off, g[pq]);
+      store8_bf16<true>(dx + off, g[pq]);
     }
   }
 }
