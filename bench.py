@@ -456,13 +456,16 @@ def main():
                        "staleness_bound": a.staleness, "optimizer": f"{opt_kind} fused gfx950", "bucket_mb": a.bucket_mb,
                        "pull_dtype": pull_dtype, "fp8_compute": fp8_compute, "tunableop": tunable_mode,
                        "transport": ps.t.name, "hipgraph": bool(tr.graphs), "graph_error": tr.graph_error},
-            "ps_semantics": (f"K-batch async SGD, K={ps.round} pushes per step (staleness bound {a.staleness}: "
-                             f"gradients may be up to {a.staleness + 1} steps stale; at bound 0 exactly synchronous)"
+            "ps_semantics": ((f"K-batch async SGD, K={ps.round} pushes per step (staleness bound {a.staleness}: "
+                              f"gradients may be up to {a.staleness + 1} steps stale)" if a.staleness else
+                              f"K-batch SGD at staleness bound 0, K={ps.round} pushes per step: exactly synchronous "
+                              "(every gradient is applied to the weights it was computed on)")
                              if mode == "async" else
                              (f"synchronous, fixed {a.staleness}-step gradient delay" if a.staleness else "synchronous")),
             "vs_baseline_note": ("vs the reference-semantics baseline (sync barrier, gRPC fp32 tensors, one host PS, "
-                                 "285.1 img/s x workers, tools/reference_baseline.py); this run's weights may be "
-                                 f"up to {a.staleness + 1} steps stale (SSP bound {a.staleness})"
+                                 "285.1 img/s x workers, tools/reference_baseline.py); "
+                                 + (f"this run's weights may be up to {a.staleness + 1} steps stale (SSP bound "
+                                    f"{a.staleness})" if a.staleness else "this run is synchronous (SSP bound 0)")
                                  if a.model in REF_BASELINE else None),
             "bucket_mb_chosen": a.bucket_mb, "bucket_probe_GBps": bucket_probe,
             "bucket_probe_transport": bucket_transport,
