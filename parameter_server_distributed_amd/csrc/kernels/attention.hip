@@ -42,7 +42,14 @@ __device__ __forceinline__ uint32_t amix32(uint32_t h) {  // murmur3 finalizer (
   return h;
 }
 // (common.h drop_keep: one hash per element pair, 16 bits each; fwd and bwd index elements alike)
-__device__ __forceinline__ bool akeep(uint32_t key, uint64_t idx, uint32_t thresh) { return drop_keep(key, idx, thresh); }
+// keep flags of the element pair (idx, idx + 1), idx even, from ONE hash -- drop_keep's mask bit for bit.
+// (Calling drop_keep per element hashed every pair twice: dropout cost the forward 57 % of its
+// time, 48.6 -> 76.2 us per BERT layer, tools/attn_bench.py.)
+__device__ __forceinline__ void akeep2(uint32_t key, uint64_t idx, uint32_t thresh, bool& k0, bool& k1) {
+  const uint32_t h = drop_pair_bits(key, idx);
+  k0 = (h & 0xffffu) >= (thresh >> 16);
+  k1 = (h >> 16) >= (thresh >> 16);
+}
 __device__ __forceinline__ uint32_t attn_key(uint32_t seed, const int64_t* step) {
   return amix32(seed * 0x27d4eb2fu ^ (uint32_t)(step ? *step : 0) * 0x165667b1u);
 }
@@ -199,12 +206,15 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
       for (int ks2 = 0; ks2 < 2; ++ks2) {
         float v[8];
+        bool kp[8];
+        if (drop) {  // elements e, e + 1 (e even) are keys kk, kk + 1 with kk even: one hash per pair
+#pragma unroll
+          for (int e = 0; e < 8; e += 2) akeep2(key, rowidx + 32 * j + acc_row(8 * ks2 + e, hh), a.thresh, kp[e], kp[e + 1]);
+        }
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const int i = 8 * ks2 + e;
-          const int kk = 32 * j + acc_row(i, hh);
-          v[e] = sc[j][i] * inv;
-          if (drop) v[e] = akeep(key, rowidx + kk, a.thresh) ? v[e] * a.rescale : 0.f;
+          v[e] = sc[j][8 * ks2 + e] * inv;
+          if (drop) v[e] = kp[e] ? v[e] * a.rescale : 0.f;
         }
         const abf16x8 pb = __builtin_bit_cast(
             abf16x8, u32x4{pack_bf16x2_rne(v[0], v[1]), pack_bf16x2_rne(v[2], v[3]), pack_bf16x2_rne(v[4], v[5]),
@@ -328,15 +338,19 @@ __global__ __launch_bounds__(128 * NW) void attn_bwd_kernel(AttnArgs a) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         float pv[4], dv[4];
+        bool kp[4];
+        if (drop) {  // keys k0 + 8g + 4hh + e: pairs (0, 1), (2, 3) share one hash
+          akeep2(key, rowidx + k0 + 8 * g + 4 * hh, a.thresh, kp[0], kp[1]);
+          akeep2(key, rowidx + k0 + 8 * g + 4 * hh + 2, a.thresh, kp[2], kp[3]);
+        }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int i = 4 * g + e;
           const float p = exp2f(st[i] * sl - lse2);
           float pd = p, dp = dpt[i];
           if (drop) {
-            const bool kp = akeep(key, rowidx + k0 + 8 * g + 4 * hh + e, a.thresh);
-            pd = kp ? p * a.rescale : 0.f;
-            dp = kp ? dp * a.rescale : 0.f;
+            pd = kp[e] ? p * a.rescale : 0.f;
+            dp = kp[e] ? dp * a.rescale : 0.f;
           }
           pv[e] = pd;
           dv[e] = p * (dp - Dq);

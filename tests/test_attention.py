@@ -125,3 +125,43 @@ def test_qkv_bias_grad_from_attention_matches_colsum(gpu):
     assert lin._psd_bias_hand is None
     for a, b in zip(got, ref):
         torch.testing.assert_close(a, b, rtol=1e-2, atol=1e-2 * float(b.abs().max()) + 1e-6)
+
+
+def _np_mix32(h):
+    import numpy as np
+
+    h = h.astype(np.uint64) & 0xFFFFFFFF
+    h ^= h >> 16
+    h = (h * 0x85EBCA6B) & 0xFFFFFFFF
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & 0xFFFFFFFF
+    h ^= h >> 16
+    return h
+
+
+@pytest.mark.gpu
+def test_attention_dropout_mask_is_the_documented_hash(gpu):
+    """The forward's keep-mask equals common.h drop_keep over idx = ((b*H + h)*S + q)*S + key with
+    the attention key (attention.hip attn_key), element for element: pins the one-hash-per-pair
+    form (akeep2) to the per-element definition."""
+    import numpy as np
+
+    from parameter_server_distributed_amd import native
+
+    C = native()
+    B, S, H, D, p, seed, stepv = 2, 64, 2, 64, 0.2, 11, 5
+    step = torch.tensor([stepv], device=gpu, dtype=torch.int64)
+    qkv = (torch.randn(B, S, 3, H, D, device=gpu) * 0.5).to(torch.bfloat16)
+    qkv[:, :, 2] = torch.eye(S, D, device=gpu, dtype=torch.bfloat16)[None, :, None, :].expand(B, S, H, D)
+    po, _ = C.attn_fwd(qkv.view(B, S, -1), H, p, seed, step)
+    got = (po.view(B, S, H, D).permute(0, 2, 1, 3) != 0).cpu().numpy()  # [B, H, q, key]
+
+    key = int(_np_mix32(np.array([((seed * 0x27D4EB2F) ^ (stepv * 0x165667B1)) & 0xFFFFFFFF]))[0])
+    idx = np.arange(B * H * S * S, dtype=np.uint64)
+    pr = idx >> 1
+    h = _np_mix32(np.uint64(key) ^ ((pr & 0xFFFFFFFF) * 0x9E3779B9 & 0xFFFFFFFF)
+                  ^ (((pr >> 32) * 0x7F4A7C15) & 0xFFFFFFFF))
+    bits = np.where(idx & 1, h >> 16, h & 0xFFFF)
+    thresh = min(4294967295, int(np.floor(p * 4294967296.0)))
+    want = (bits >= (thresh >> 16)).reshape(B, H, S, S)
+    assert (got == want).all(), int((got != want).sum())
