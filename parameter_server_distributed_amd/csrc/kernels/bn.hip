@@ -987,7 +987,9 @@ hipError_t launch_bn_fwd(const BnFwdArgs& a, hipStream_t st) {
     const int Ho = a.H / 2, Wo = a.W / 2;
     const int64_t total = (int64_t)a.N * Ho * Wo * (a.C / 8);
     if (total >= ((int64_t)1 << 31) - 2048 * 256) return hipErrorInvalidValue;  // 32-bit item indices
-    hipLaunchKernelGGL(bn_relu_maxpool_kernel, dim3(stream_grid(total, 256)), dim3(256), 0, st, a.x, a.ss, a.y,
+    // one item per lane (no grid-stride loop): like the elementwise passes, the one-shot grid
+    // streams faster than 2048 looping workgroups (profiles/r6/elemt_variants.md)
+    hipLaunchKernelGGL(bn_relu_maxpool_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, a.x, a.ss, a.y,
                        a.pool_arg, a.N, a.H, a.W, a.C, Ho, Wo, make_fastdiv((uint32_t)(a.C / 8)),
                        make_fastdiv((uint32_t)Wo), make_fastdiv((uint32_t)Ho));
     return hipGetLastError();
@@ -1044,7 +1046,7 @@ static hipError_t launch_bn_bwd_pool(const BnBwdArgs& a, hipStream_t st) {
                      a.save_mean, a.N, a.H, a.W, a.C, a.part, dwo, dho);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((a.C + kFinCh - 1) / kFinCh), dim3(256), 0, st, a.part, gx,
                      FinBwd{a.M, a.C, a.gamma, a.save_mean, a.save_invstd, a.dgamma, a.dbeta, a.coef});
-  const int g = elem_grid(total, a.C);
+  const int g = elem_grid(total, a.C);  // (a one-shot grid measured 4 % slower here, r6t)
   hipLaunchKernelGGL(bn_bwd_elemt_pool_kernel, dim3(g), dim3(256), 0, st, a.gpool, a.gpool2, a.pool_arg, a.ss, a.x,
                      a.coef, a.dx, a.N, a.H, a.W, a.C, dc8, dwo, dho);
   return hipGetLastError();
